@@ -1,0 +1,179 @@
+#!/usr/bin/env python3
+"""bench.py — links reconciled/sec of the MI355X reconcile engine (BASELINE.json metric).
+
+One step = one reconcile epoch over this rank's shard, inputs resident in HBM:
+  dictionary parse → pod-status table (+ RCCL all-gather across ranks) → lookup tables →
+  Reconcile gate + CalcDiff → batch compaction → addLink/delLink/UpdateLinks pure prefix
+  → MakeQdiscs; the host waits for each epoch (kdtn_epoch_sync).
+Workload (BASELINE configs[2]): per GPU a 1M-pod shard of a random
+10-regular topology — 10M Link records with heterogeneous netem/tbf properties — all
+AddLinks (realised status non-nil and empty). Weak scaling: every rank owns 1M pods of a
+(N × 1M)-pod graph; peers are spread over all shards, so each epoch all-gathers the
+pod-status table over RCCL/xGMI.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+For N > 1 launch with torch.distributed.run (one process per GPU).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch  # noqa: E402  (first: one HIP runtime per process, see kdtn/engine.py)
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "kube-dtn_amd"))
+
+from kdtn import Engine, abi, comm_unique_id, synth  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def emit_bytes(inp, n_add: int, n_upd: int, n_del: int) -> float:
+    """Algorithmic bytes of one k_emit launch: per AddLinks entry
+    1 (flag) + 12 (local_ip, local_mac, peer_pod ids) + 8 (uid) + 48 (12 prop ids) + 4 (gap)
+    read, 4 (index) + 16 (resolve record) + 72 (qdisc) written = 165 B; per topology
+    8 (offsets) + 1 (action) + 12 (ns, src_ip, net_ns) read + 12 (3 batch offsets) written
+    = 33 B; plus the 24 B parsed record of every property string, read once."""
+    T = inp.topos.n
+    per_add = 165.0
+    per_upd = 1 + 4 + 12 + 48 + 4 + 8 + 4 + 16 + 72   # flag, target, ids, props, gap, uid, out
+    per_del = 1 + 12 + 8 + 4 + 16
+    return per_add * n_add + per_upd * n_upd + per_del * n_del + 33.0 * T + 24.0 * inp.pdict.n
+
+
+def epoch_bytes(inp, n_add: int, n_upd: int, n_del: int) -> float:
+    """SURVEY §8(d) whole-epoch model: 92·M + 92·N + 16·T + 4·lists + 36·|add| + 72·|add∪upd|
+    + unique property-string bytes."""
+    M, N, T = inp.realised.n, inp.desired.n, inp.topos.n
+    return (92.0 * (M + N) + 16.0 * T + 4.0 * (n_add + n_upd + n_del) + 36.0 * n_add
+            + 72.0 * (n_add + n_upd) + float(inp.pdict.offs[-1]))
+
+
+def cpu_baseline(inp, budget_s: float):
+    """The CPU oracle (C restatement of the reference Go path) on a bounded sample of this
+    workload's topologies, single thread, loop time only (informer maps pre-built)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    T = inp.topos.n
+    t_end = min(T, 20_000)
+    timing = []
+    O.reconcile(inp, t_begin=0, t_end=t_end, timing=timing)    # warm + calibrate
+    rate = (inp.topos.des_off[t_end] - inp.topos.des_off[0]) / max(timing[-1], 1e-9)
+    want = int(min(T, max(t_end, budget_s * rate / max(inp.desired.n / T, 1.0))))
+    timing.clear()
+    O.reconcile(inp, t_begin=0, t_end=want, timing=timing)
+    links = int(inp.topos.des_off[want] - inp.topos.des_off[0])
+    return {"value": links / timing[-1], "unit": "links/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/kdtn_oracle.c on topologies [0,{want}) of rank 0's shard: "
+                      f"{links} links, {timing[-1]:.2f} s single-thread "
+                      f"(host nproc={os.cpu_count()})"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--pods", type=int, default=1_000_000, help="pods per GPU shard")
+    ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--cpu-budget-s", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    torch.cuda.set_device(local)
+
+    t0 = time.time()
+    inp = synth.make(args.config, pods_per_shard=args.pods, shard=rank, nshards=world)
+    gen_s = time.time() - t0
+    eng = Engine(device=local)
+    if world > 1:
+        uid = [comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        eng.comm_init(uid[0], world, rank)
+    eng.upload(inp)
+
+    for _ in range(args.warmup):
+        eng.run()
+        eng.sync()
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ksum: dict[str, float] = {}
+    t_start = time.perf_counter()
+    counts = None
+    for _ in range(args.steps):
+        eng.run()
+        counts = eng.sync()
+        for k, v in eng.kernel_times().items():
+            ksum[k] = ksum.get(k, 0.0) + v
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t[0])
+        n = torch.tensor([inp.desired.n], dtype=torch.float64)
+        dist.all_reduce(n, op=dist.ReduceOp.SUM)
+        links_total = float(n[0])
+    else:
+        links_total = float(inp.desired.n)
+
+    ms_step = elapsed / args.steps * 1e3
+    kavg = {k: v / args.steps for k, v in ksum.items()}
+    dom = max(kavg, key=kavg.get)
+    ebytes = emit_bytes(inp, counts.n_add, counts.n_upd, counts.n_del)
+    roof = {"kernel": "k_emit", "bound": "hbm", "achieved": ebytes / (kavg["emit"] * 1e-3) / 1e9,
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "traffic": None,
+            "bytes_per_launch": ebytes, "avg_ms": kavg["emit"], "dominant_stage": dom}
+    roof["frac"] = roof["achieved"] / roof["peak"]
+    pbytes = epoch_bytes(inp, counts.n_add, counts.n_upd, counts.n_del)
+    result = {
+        "metric": "links reconciled/sec (diff+qdisc) on 10M-link topology",
+        "value": links_total / (elapsed / args.steps),
+        "unit": "links/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (kdtn_synth config 2, seed 0x6b64746e)",
+        "config": {"workload": f"config{args.config}: {args.pods}-pod shard per GPU of a random "
+                               f"10-regular topology, {inp.desired.n} links/GPU, heterogeneous "
+                               f"netem/tbf props, all AddLinks (resolve + qdisc on every link)",
+                   "pods_per_gpu": inp.topos.n, "links_per_gpu": inp.desired.n,
+                   "global_links": int(links_total), "parallelism": f"shard{world}"},
+        "roofline": roof,
+        "epoch_roofline": {"bytes": pbytes, "achieved": pbytes / (ms_step * 1e-3) / 1e9,
+                           "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": pbytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS},
+        "kernels_ms": kavg,
+        "counts": {"add": counts.n_add, "upd": counts.n_upd, "del": counts.n_del},
+        "gen_s": round(gen_s, 2),
+    }
+    if rank == 0 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(inp, args.cpu_budget_s)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    eng.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,291 @@
+/*
+ * kdtn.h — C-ABI of the MI355X batch topology-reconcile engine (libkdtn.so).
+ *
+ * This is the drop-in boundary for kube-dtn's reconcile hot path. The reference
+ * (dtn-dslab/kube-dtn, Go) calls these pure functions directly; a Go build binds
+ * this header through cgo (stub in INTEGRATION.md). Every entry point below cites
+ * the reference function it replaces (paths relative to the reference root).
+ *
+ *   kdtn_reconcile_epoch  replaces, for every dirty Topology at once:
+ *     - the Reconcile gate   controllers/topology_controller.go:77-88
+ *     - CalcDiff             controllers/topology_controller.go:288-318
+ *     - EqualWithoutProperties controllers/topology_controller.go:342-351
+ *     - the pure prefix of the daemon batch handlers
+ *         AddLinks/addLink   daemon/kubedtn/handler.go:592-611, 316-459
+ *         DelLinks/delLink   daemon/kubedtn/handler.go:613-632, 461-492
+ *         UpdateLinks        daemon/kubedtn/handler.go:634-671
+ *     - MakeVeth parse       common/veth.go:13-41
+ *     - MakeQdiscs           common/qdisc.go:20-199, 361-370 (+ netlink.NewNetem)
+ *     - GetVniFromUid        common/utils.go:29-31
+ *     - VxlanManager.Get     daemon/vxlan/manager.go:65-71
+ *   kdtn_make_qdiscs      replaces common.MakeQdiscs (common/qdisc.go:20) for a batch
+ *
+ * Conventions
+ *   - No C++ or HIP types cross this ABI: plain pointers, sizes and PODs.
+ *   - Inputs are caller-owned HOST memory; the engine copies them to HBM and keeps
+ *     no caller pointer after a call returns (cgo rule).
+ *   - Return codes: 0 = OK, negative errno-style engine errors (kdtn_strerror).
+ *     Per-link semantic failures are DATA (kdtn_err in the output records), never
+ *     return codes — mirroring the reference where each link's error aborts only its
+ *     own batch (handler.go:604-605).
+ *   - A kdtn_ctx is not thread-safe; callers serialise (one per process/GPU).
+ *   - Strings are interned: a kdtn_strtab is a DEDUPLICATED dictionary (id equality
+ *     <=> byte equality) and id 0 MUST be the empty string "". kdtn_interner_*
+ *     builds such tables.
+ */
+#ifndef KDTN_H
+#define KDTN_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KDTN_ABI_VERSION 1
+
+/* ---- engine errors (return codes) ------------------------------------------------ */
+#define KDTN_OK          0
+#define KDTN_EINVAL    (-22)   /* malformed tables (offsets, ids out of range, ...)   */
+#define KDTN_ENOMEM    (-12)   /* device or host allocation failed                    */
+#define KDTN_EIO        (-5)   /* HIP / RCCL runtime failure                          */
+#define KDTN_ENOSPC    (-28)   /* an output capacity is smaller than the batch        */
+#define KDTN_ENODEV    (-19)   /* no usable gfx950 device                             */
+
+/* ---- per-link semantic errors: first failing step, reference order --------------- */
+typedef enum kdtn_err {
+    KDTN_E_NONE = 0,
+    KDTN_E_VETH_CIDR = 1,      /* MakeVeth local  net.ParseCIDR   common/veth.go:22          */
+    KDTN_E_VETH_MAC = 2,       /* MakeVeth local  net.ParseMAC    common/veth.go:33          */
+    KDTN_E_LATENCY = 3,        /* ParseDuration(latency)          common/qdisc.go:28         */
+    KDTN_E_LATENCY_CORR = 4,   /* ParseFloatPercentage            common/qdisc.go:34         */
+    KDTN_E_JITTER = 5,         /* common/qdisc.go:40 */
+    KDTN_E_LOSS = 6,           /* common/qdisc.go:46 */
+    KDTN_E_LOSS_CORR = 7,      /* common/qdisc.go:52 */
+    KDTN_E_DUPLICATE = 8,      /* common/qdisc.go:58 */
+    KDTN_E_DUPLICATE_CORR = 9, /* common/qdisc.go:64 */
+    KDTN_E_REORDER_PROB = 10,  /* common/qdisc.go:70 */
+    KDTN_E_REORDER_CORR = 11,  /* common/qdisc.go:76 */
+    KDTN_E_CORRUPT_PROB = 12,  /* common/qdisc.go:82 */
+    KDTN_E_CORRUPT_CORR = 13,  /* common/qdisc.go:88 */
+    KDTN_E_RATE = 14,          /* ParseRate                       common/qdisc.go:110        */
+    KDTN_E_PEER_LOOKUP = 15,   /* getPod miss                     daemon/kubedtn/handler.go:375-379 */
+    KDTN_E_PEER_NO_LINKS = 16, /* ToProtoPod: peer spec.links nil handler.go:65-69,380-384   */
+    KDTN_E_PEER_VETH_CIDR = 17,/* MakeVeth peer (same node)       handler.go:402             */
+    KDTN_E_PEER_VETH_MAC = 18
+} kdtn_err;
+
+/* Reconcile decision per Topology (controllers/topology_controller.go:77-88). */
+typedef enum kdtn_action {
+    KDTN_ACT_SKIP = 0,     /* reflect.DeepEqual(status.links, spec.links)          :77   */
+    KDTN_ACT_CREATED = 1,  /* status.links == nil: no batches, status := spec      :81   */
+    KDTN_ACT_DIFF = 2      /* CalcDiff → DelLinks, AddLinks, UpdateLinks           :88   */
+} kdtn_action;
+
+/* addLink classification (daemon/kubedtn/handler.go:316-459). */
+typedef enum kdtn_kind {
+    KDTN_KIND_NONE = 0,        /* not classified (error before classification, or not an add) */
+    KDTN_KIND_MACVLAN = 1,     /* peer_pod == "localhost"                 handler.go:333   */
+    KDTN_KIND_PHYSICAL = 2,    /* peer_pod has prefix "physical/"         handler.go:348   */
+    KDTN_KIND_PEER_DEAD = 3,   /* peer SrcIp or NetNs empty → skip, OK    handler.go:386-395 */
+    KDTN_KIND_SAME_NODE = 4,   /* peer.SrcIp == local.SrcIp → veth pair   handler.go:399   */
+    KDTN_KIND_CROSS_NODE = 5   /* VXLAN + RemotePod to peer daemon        handler.go:419   */
+} kdtn_kind;
+
+/* Link string columns (api/v1/topology_types.go:59-95), key of EqualWithoutProperties. */
+enum {
+    KDTN_K_LOCAL_INTF = 0, KDTN_K_LOCAL_IP, KDTN_K_LOCAL_MAC,
+    KDTN_K_PEER_INTF, KDTN_K_PEER_IP, KDTN_K_PEER_MAC, KDTN_K_PEER_POD,
+    KDTN_NKEY
+};
+/* LinkProperties string fields (api/v1/topology_types.go:119-176); Gap is separate. */
+enum {
+    KDTN_P_LATENCY = 0, KDTN_P_LATENCY_CORR, KDTN_P_JITTER, KDTN_P_LOSS, KDTN_P_LOSS_CORR,
+    KDTN_P_RATE, KDTN_P_DUPLICATE, KDTN_P_DUPLICATE_CORR, KDTN_P_REORDER_PROB,
+    KDTN_P_REORDER_CORR, KDTN_P_CORRUPT_PROB, KDTN_P_CORRUPT_CORR,
+    KDTN_NPROP
+};
+
+/* Topology flags */
+#define KDTN_TOPO_STATUS_NIL 0x1u   /* status.links == nil (JSON null/absent) */
+#define KDTN_TOPO_SPEC_NIL   0x2u   /* spec.links   == nil                    */
+
+/* ---- input tables ----------------------------------------------------------------- */
+typedef struct kdtn_strtab {
+    const uint8_t*  bytes;   /* arena                                          */
+    const uint32_t* offs;    /* n+1 byte offsets; string i = bytes[offs[i], offs[i+1]) */
+    uint32_t        n;       /* number of strings; id 0 must be ""             */
+} kdtn_strtab;
+
+/* A set of Link records, grouped by owning Topology (segments given by kdtn_topo_table). */
+typedef struct kdtn_link_table {
+    uint32_t        n;
+    const uint32_t* key[KDTN_NKEY];   /* kdict ids                                   */
+    const int64_t*  uid;              /* Link.UID (int on amd64 = int64)             */
+    const uint32_t* prop[KDTN_NPROP]; /* pdict ids                                   */
+    const uint32_t* gap;              /* LinkProperties.Gap                          */
+} kdtn_link_table;
+
+typedef struct kdtn_topo_table {
+    uint32_t        n;          /* T topologies in this shard                          */
+    const uint32_t* ns;         /* kdict id of metadata.namespace                      */
+    const uint32_t* name;       /* kdict id of metadata.name                           */
+    const uint32_t* src_ip;     /* kdict id of status.src_ip                           */
+    const uint32_t* net_ns;     /* kdict id of status.net_ns                           */
+    const uint8_t*  flags;      /* KDTN_TOPO_* bits                                    */
+    const uint32_t* real_off;   /* T+1 offsets into the realised table (status.links)  */
+    const uint32_t* des_off;    /* T+1 offsets into the desired table  (spec.links)    */
+} kdtn_topo_table;
+
+/* Snapshot of the daemons' VxlanManager maps (daemon/vxlan/manager.go:14-17):
+ * entry i says: on the node whose HOST_IP is kdict id node[i], VNI vni[i] is held
+ * by netns kdict id net_ns[i]. Keys (node, vni) must be unique (first wins). */
+typedef struct kdtn_vni_table {
+    uint32_t        n;
+    const uint32_t* node;
+    const int32_t*  vni;
+    const uint32_t* net_ns;
+} kdtn_vni_table;
+
+typedef struct kdtn_epoch_in {
+    kdtn_strtab     kdict;      /* key strings: names, namespaces, intfs, IPs, MACs, src_ip, net_ns */
+    kdtn_strtab     pdict;      /* LinkProperties strings                               */
+    kdtn_topo_table topos;
+    kdtn_link_table realised;   /* status.links of every topology, grouped             */
+    kdtn_link_table desired;    /* spec.links of every topology, grouped               */
+    kdtn_vni_table  vnis;
+    uint32_t        pod_slice;  /* multi-GPU: pod-table entries per rank (>= topos.n); 0 = topos.n */
+} kdtn_epoch_in;
+
+/* Property sets for the standalone kdtn_make_qdiscs (daemon UpdateLinks path). */
+typedef struct kdtn_props_table {
+    uint32_t        n;
+    const uint32_t* prop[KDTN_NPROP];
+    const uint32_t* gap;
+} kdtn_props_table;
+
+/* ---- outputs ---------------------------------------------------------------------- */
+/* MakeQdiscs result (common/qdisc.go:20-126 + netlink.NewNetem). 72 bytes.
+ * err != 0  ⇔ MakeQdiscs returned (nil, err): every other field is 0.
+ * has_netem == 0 && err == 0  ⇔ empty properties (proto.Size == 0): empty list. */
+typedef struct kdtn_qdisc {
+    uint32_t latency;        /* time2Tick(latency µs)                                  */
+    uint32_t delay_corr;     /* P2U(latency_corr) if latency µs > 0 && jitter µs > 0   */
+    uint32_t limit;          /* 1000                                                   */
+    uint32_t loss;           /* P2U(loss)                                              */
+    uint32_t loss_corr;      /* P2U(loss_corr) if loss > 0                             */
+    uint32_t gap;            /* Gap, or 1 if reorder_prob > 0 && Gap == 0              */
+    uint32_t duplicate;      /* P2U(duplicate)                                         */
+    uint32_t duplicate_corr; /* P2U(duplicate_corr) if duplicate > 0                   */
+    uint32_t jitter;         /* time2Tick(jitter µs) if latency ticks > 0 else µs      */
+    uint32_t reorder_prob;
+    uint32_t reorder_corr;
+    uint32_t corrupt_prob;
+    uint32_t corrupt_corr;
+    uint32_t tbf_buffer;     /* getTbfBurst(rate) common/qdisc.go:361-370              */
+    uint64_t tbf_rate;       /* ParseRate, bit/s                                       */
+    uint32_t tbf_minburst;   /* 1500                                                   */
+    uint8_t  has_netem;
+    uint8_t  has_tbf;        /* rate != 0                                              */
+    uint8_t  err;            /* kdtn_err (qdisc steps only)                            */
+    uint8_t  reserved;
+} kdtn_qdisc;
+
+/* Pure-prefix outcome of addLink / delLink / UpdateLinks for one batch entry. 16 bytes. */
+typedef struct kdtn_resolved {
+    uint32_t peer_topo;  /* global pod index of the peer Topology (lookup succeeded), else 0xFFFFFFFF */
+    int32_t  vni;        /* GetVniFromUid(uid) = int32(vxlan_base + uid)                   */
+    uint32_t vtep;       /* CROSS_NODE: kdict id of peer status.src_ip; PHYSICAL: kdict id of
+                            peer_pod (vtep = bytes[9:]); else 0                             */
+    uint8_t  kind;       /* kdtn_kind (add entries)                                        */
+    uint8_t  err;        /* kdtn_err: first failing step before the first syscall. For add
+                            SAME/CROSS/PHYSICAL the qdisc error is in kdtn_qdisc.err.  For
+                            update entries: MakeVeth error, else the MakeQdiscs error.        */
+    uint8_t  vni_hit;    /* del: VxlanManager.Get(vni) == local net_ns (handler.go:482-486);
+                            add PHYSICAL: local VNI map holds vni for another netns
+                            (handler.go:177-179); add CROSS_NODE: same check on the peer's node */
+    uint8_t  reserved;
+} kdtn_resolved;
+
+/* Epoch outputs, caller-owned host memory. Any pointer may be NULL (not returned).
+ * Batches are per Topology: entries of topology t are [off[t], off[t+1]) of each list,
+ * in the reference's order (del/upd: status order; add: spec order). */
+typedef struct kdtn_batches {
+    uint8_t*        action;          /* [T] kdtn_action                                  */
+    uint32_t*       del_off;         /* [T+1]                                            */
+    uint32_t*       add_off;         /* [T+1]                                            */
+    uint32_t*       upd_off;         /* [T+1]                                            */
+    uint32_t*       del_idx;         /* realised record index of each DelLinks entry     */
+    uint32_t*       add_idx;         /* desired record index of each AddLinks entry      */
+    uint32_t*       upd_idx;         /* desired record index of each UpdateLinks entry   */
+    kdtn_resolved*  del_res;
+    kdtn_resolved*  add_res;
+    kdtn_resolved*  upd_res;
+    kdtn_qdisc*     add_qdisc;
+    kdtn_qdisc*     upd_qdisc;
+    uint32_t        del_cap, add_cap, upd_cap;   /* in: entry capacities                */
+    uint32_t        n_del, n_add, n_upd;         /* out: entry counts                   */
+} kdtn_batches;
+
+typedef struct kdtn_counts { uint32_t n_del, n_add, n_upd, n_topos; } kdtn_counts;
+
+/* Epoch stages (bitmask for kdtn_epoch_run). */
+#define KDTN_STAGE_DIFF    0x1u   /* gate + CalcDiff + batch lists                     */
+#define KDTN_STAGE_RESOLVE 0x2u   /* MakeVeth + addLink classification + VNI           */
+#define KDTN_STAGE_QDISC   0x4u   /* MakeQdiscs for add ∪ update entries                */
+#define KDTN_STAGE_ALL     0x7u
+
+typedef struct kdtn_config {
+    int32_t  device;         /* HIP device ordinal; -1 = current device                */
+    int32_t  vxlan_base;     /* common/constants.go:8 VxlanBase (5000)                  */
+    double   tick_in_usec;   /* netlink initClock from /proc/net/psched (15.625 typical);
+                                0 reproduces an unreadable psched (time2Tick == 0)      */
+} kdtn_config;
+
+typedef struct kdtn_ctx kdtn_ctx;
+typedef struct kdtn_interner kdtn_interner;
+
+/* ---- lifecycle -------------------------------------------------------------------- */
+const char* kdtn_version(void);
+const char* kdtn_strerror(int code);
+const char* kdtn_err_name(int kdtn_err_code);
+int  kdtn_init(kdtn_ctx** out, const kdtn_config* cfg);
+void kdtn_destroy(kdtn_ctx* ctx);
+/* Run on a caller-provided hipStream_t (passed as void*); NULL restores the ctx stream. */
+int  kdtn_set_stream(kdtn_ctx* ctx, void* hip_stream);
+/* Reads /proc/net/psched like netlink initClock(); returns 0.0 if unreadable. */
+double kdtn_psched_tick_in_usec(void);
+
+/* ---- host string interning (deduplicated dictionaries, id 0 = "") ----------------- */
+int      kdtn_interner_new(kdtn_interner** out);
+void     kdtn_interner_free(kdtn_interner* it);
+uint32_t kdtn_intern(kdtn_interner* it, const char* s, uint32_t len);
+int      kdtn_intern_batch(kdtn_interner* it, const uint8_t* bytes, const uint64_t* offs,
+                           uint32_t n, uint32_t* ids_out);
+/* View of the dictionary; valid until the next kdtn_intern* call on it. */
+int      kdtn_interner_table(const kdtn_interner* it, kdtn_strtab* out);
+
+/* ---- reconcile epoch (CalcDiff + resolve + MakeQdiscs over all topologies) --------- */
+/* One synchronous call: upload, run KDTN_STAGE_ALL, download into `out`.               */
+int kdtn_reconcile_epoch(kdtn_ctx* ctx, const kdtn_epoch_in* in, kdtn_batches* out);
+/* Split form (device-resident inputs reused across epochs):                             */
+int kdtn_epoch_upload(kdtn_ctx* ctx, const kdtn_epoch_in* in);
+int kdtn_epoch_run(kdtn_ctx* ctx, uint32_t stages);          /* async on the ctx stream   */
+int kdtn_epoch_sync(kdtn_ctx* ctx, kdtn_counts* counts);     /* waits; counts may be NULL */
+int kdtn_epoch_download(kdtn_ctx* ctx, kdtn_batches* out);   /* after sync                */
+
+/* ---- standalone MakeQdiscs over a batch of property sets (UpdateLinks path) -------- */
+int kdtn_make_qdiscs(kdtn_ctx* ctx, const kdtn_strtab* pdict, const kdtn_props_table* props,
+                     kdtn_qdisc* out);
+
+/* ---- multi-GPU (one process per GPU): RCCL all-gather of the pod-status table ------ */
+int kdtn_comm_unique_id(uint8_t out[128]);
+int kdtn_comm_init(kdtn_ctx* ctx, const uint8_t unique_id[128], int nranks, int rank);
+
+/* ---- profiling hooks: per-kernel HIP-event times of the last epoch_run (ms) -------- */
+int kdtn_last_kernel_times(kdtn_ctx* ctx, const char** names, float* ms, int cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KDTN_H */

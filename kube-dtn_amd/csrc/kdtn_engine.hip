@@ -1,0 +1,691 @@
+// kdtn_engine.hip — host side of libkdtn.so: the C-ABI of include/kdtn.h over the
+// HIP kernels of kdtn_kernels.hip. One kdtn_ctx per process/GPU; device buffers are
+// owned by the context and reused across epochs (high-water-mark growth).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/kdtn.h"
+#include "kdtn_kernels.h"
+
+using namespace kdtn;
+
+namespace {
+
+constexpr int kMaxTimers = 16;
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+};
+
+#define HIP_TRY(expr)                                                                    \
+    do {                                                                                 \
+        hipError_t _e = (expr);                                                          \
+        if (_e != hipSuccess) {                                                          \
+            std::snprintf(g_last_error, sizeof(g_last_error), "%s: %s (%s:%d)", #expr,   \
+                          hipGetErrorString(_e), __FILE__, __LINE__);                    \
+            return KDTN_EIO;                                                             \
+        }                                                                                \
+    } while (0)
+
+thread_local char g_last_error[512] = "";
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+uint32_t next_pow2(uint64_t x) {
+    uint64_t p = 64;
+    while (p < x) p <<= 1;
+    return (uint32_t)p;
+}
+
+}  // namespace
+
+// Link table storage: all 21 columns carved from one allocation.
+struct DevLinkStore {
+    DevBuf buf;
+    uint32_t n = 0;
+    DevLinks view{};
+};
+
+struct kdtn_ctx {
+    int device = 0;
+    kdtn_config cfg{};
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    // dictionaries
+    DevBuf kd_bytes, kd_offs, kd_flags, pd_bytes, pd_offs, pd_parsed, pd_rate;
+    uint32_t D = 0, P = 0;
+    // topologies
+    DevBuf t_ns, t_name, t_src, t_netns, t_flags, t_roff, t_noff;
+    uint32_t T = 0;
+    // links
+    DevLinkStore real, des;
+    // vni table
+    DevBuf v_node, v_vni, v_netns, v_keys, v_vals;
+    uint32_t V = 0, vni_mask = 0;
+    // pods
+    DevBuf pods, pod_keys, pod_vals;
+    uint32_t slice = 0, pod_total = 0, pod_mask = 0;
+    // work
+    DevBuf oflag, otarget, nflag, wg_cnt, wg_base, misc, hscratch, fscratch;
+    // outputs
+    DevBuf action, del_off, add_off, upd_off, del_idx, add_idx, upd_idx;
+    DevBuf del_res, add_res, upd_res, add_qdisc, upd_qdisc;
+    // host-visible counters
+    uint32_t* h_misc = nullptr;   // pinned: [0]=default id, [1]=del, [2]=upd, [3]=add
+    bool uploaded = false;
+    bool ran = false;
+    uint32_t last_stages = 0;
+    // multi-GPU
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+    // timers
+    hipEvent_t ev[kMaxTimers + 1] = {};
+    const char* ev_name[kMaxTimers] = {};
+    int n_ev = 0;
+};
+
+namespace {
+
+int ensure(DevBuf& b, size_t bytes) {
+    bytes = std::max<size_t>(bytes, 256);
+    if (b.cap >= bytes) return KDTN_OK;
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+    hipError_t e = hipMalloc(&b.p, bytes);
+    if (e != hipSuccess) {
+        std::snprintf(g_last_error, sizeof(g_last_error), "hipMalloc(%zu): %s", bytes,
+                      hipGetErrorString(e));
+        b.p = nullptr;
+        return KDTN_ENOMEM;
+    }
+    b.cap = bytes;
+    return KDTN_OK;
+}
+void release(DevBuf& b) {
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+}
+
+#define TRY(expr)                   \
+    do {                            \
+        int _r = (expr);            \
+        if (_r != KDTN_OK) return _r; \
+    } while (0)
+
+int upload(kdtn_ctx* c, DevBuf& b, const void* src, size_t bytes) {
+    TRY(ensure(b, bytes));
+    if (bytes) HIP_TRY(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, c->stream));
+    return KDTN_OK;
+}
+
+template <typename T>
+T* dp(DevBuf& b) { return static_cast<T*>(b.p); }
+
+int check_strtab(const kdtn_strtab& t, const char* what) {
+    if (t.n == 0 || !t.offs || (!t.bytes && t.offs[t.n] != 0)) {
+        std::snprintf(g_last_error, sizeof(g_last_error), "%s: empty dictionary (id 0 must be \"\")", what);
+        return KDTN_EINVAL;
+    }
+    if (t.n >= 0x7FFFFFFFu) {
+        std::snprintf(g_last_error, sizeof(g_last_error), "%s: too many strings", what);
+        return KDTN_EINVAL;
+    }
+    if (t.offs[0] != 0 || t.offs[1] != 0) {
+        std::snprintf(g_last_error, sizeof(g_last_error), "%s: id 0 must be the empty string", what);
+        return KDTN_EINVAL;
+    }
+    for (uint32_t i = 0; i < t.n; ++i)
+        if (t.offs[i + 1] < t.offs[i]) {
+            std::snprintf(g_last_error, sizeof(g_last_error), "%s: offsets not monotone at %u", what, i);
+            return KDTN_EINVAL;
+        }
+    return KDTN_OK;
+}
+
+int check_ids(const uint32_t* col, uint32_t n, uint32_t lim, const char* what) {
+    if (n && !col) {
+        std::snprintf(g_last_error, sizeof(g_last_error), "%s: missing column", what);
+        return KDTN_EINVAL;
+    }
+    uint32_t mx = 0;
+    for (uint32_t i = 0; i < n; ++i) mx = std::max(mx, col[i]);
+    if (n && mx >= lim) {
+        std::snprintf(g_last_error, sizeof(g_last_error), "%s: id %u out of range (%u strings)", what, mx, lim);
+        return KDTN_EINVAL;
+    }
+    return KDTN_OK;
+}
+
+int check_offsets(const uint32_t* off, uint32_t T, uint32_t n, const char* what) {
+    if (!off) {
+        std::snprintf(g_last_error, sizeof(g_last_error), "%s: missing offsets", what);
+        return KDTN_EINVAL;
+    }
+    if (off[0] != 0 || off[T] != n) {
+        std::snprintf(g_last_error, sizeof(g_last_error), "%s: offsets must span [0,%u]", what, n);
+        return KDTN_EINVAL;
+    }
+    for (uint32_t t = 0; t < T; ++t)
+        if (off[t + 1] < off[t]) {
+            std::snprintf(g_last_error, sizeof(g_last_error), "%s: offsets not monotone at %u", what, t);
+            return KDTN_EINVAL;
+        }
+    return KDTN_OK;
+}
+
+int upload_links(kdtn_ctx* c, DevLinkStore& s, const kdtn_link_table& L, uint32_t D, uint32_t P,
+                 const char* what) {
+    const uint32_t n = L.n;
+    for (int k = 0; k < KDTN_NKEY; ++k) TRY(check_ids(L.key[k], n, D, what));
+    for (int k = 0; k < KDTN_NPROP; ++k) TRY(check_ids(L.prop[k], n, P, what));
+    if (n && (!L.uid || !L.gap)) {
+        std::snprintf(g_last_error, sizeof(g_last_error), "%s: missing uid/gap", what);
+        return KDTN_EINVAL;
+    }
+    const size_t col4 = align_up((size_t)std::max<uint32_t>(n, 1) * 4, 256);
+    const size_t col8 = align_up((size_t)std::max<uint32_t>(n, 1) * 8, 256);
+    const size_t total = col4 * (KDTN_NKEY + KDTN_NPROP + 1) + col8;
+    TRY(ensure(s.buf, total));
+    char* base = static_cast<char*>(s.buf.p);
+    size_t off = 0;
+    for (int k = 0; k < KDTN_NKEY; ++k) {
+        s.view.key[k] = reinterpret_cast<const uint32_t*>(base + off);
+        if (n) HIP_TRY(hipMemcpyAsync(base + off, L.key[k], (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+        off += col4;
+    }
+    s.view.uid = reinterpret_cast<const int64_t*>(base + off);
+    if (n) HIP_TRY(hipMemcpyAsync(base + off, L.uid, (size_t)n * 8, hipMemcpyHostToDevice, c->stream));
+    off += col8;
+    for (int k = 0; k < KDTN_NPROP; ++k) {
+        s.view.prop[k] = reinterpret_cast<const uint32_t*>(base + off);
+        if (n) HIP_TRY(hipMemcpyAsync(base + off, L.prop[k], (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+        off += col4;
+    }
+    s.view.gap = reinterpret_cast<const uint32_t*>(base + off);
+    if (n) HIP_TRY(hipMemcpyAsync(base + off, L.gap, (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+    s.view.n = n;
+    s.n = n;
+    return KDTN_OK;
+}
+
+uint32_t nblocks(uint64_t n, int block = BLOCK) { return (uint32_t)((n + block - 1) / block); }
+
+void timer_mark(kdtn_ctx* c, const char* name) {
+    if (c->n_ev >= kMaxTimers) return;
+    c->ev_name[c->n_ev] = name;
+    (void)hipEventRecord(c->ev[c->n_ev + 1], c->stream);
+    c->n_ev++;
+}
+
+DevTopos topo_view(kdtn_ctx* c) {
+    DevTopos t;
+    t.ns = dp<uint32_t>(c->t_ns);
+    t.name = dp<uint32_t>(c->t_name);
+    t.src_ip = dp<uint32_t>(c->t_src);
+    t.net_ns = dp<uint32_t>(c->t_netns);
+    t.flags = dp<uint8_t>(c->t_flags);
+    t.real_off = dp<uint32_t>(c->t_roff);
+    t.des_off = dp<uint32_t>(c->t_noff);
+    t.n = c->T;
+    return t;
+}
+
+}  // namespace
+
+// ======================================================================================
+// C-ABI
+// ======================================================================================
+extern "C" {
+
+const char* kdtn_version(void) { return "kdtn-mi355x 0.1 (abi 1, gfx950)"; }
+
+const char* kdtn_strerror(int code) {
+    switch (code) {
+    case KDTN_OK: return "ok";
+    case KDTN_EINVAL: return g_last_error[0] ? g_last_error : "invalid argument";
+    case KDTN_ENOMEM: return g_last_error[0] ? g_last_error : "out of memory";
+    case KDTN_EIO: return g_last_error[0] ? g_last_error : "HIP/RCCL runtime error";
+    case KDTN_ENOSPC: return "output capacity too small";
+    case KDTN_ENODEV: return g_last_error[0] ? g_last_error : "no usable gfx950 device";
+    default: return "unknown error";
+    }
+}
+
+const char* kdtn_err_name(int e) {
+    static const char* names[] = {"none", "veth_cidr", "veth_mac", "latency", "latency_corr",
+                                  "jitter", "loss", "loss_corr", "duplicate", "duplicate_corr",
+                                  "reorder_prob", "reorder_corr", "corrupt_prob", "corrupt_corr",
+                                  "rate", "peer_lookup", "peer_no_links", "peer_veth_cidr",
+                                  "peer_veth_mac"};
+    if (e < 0 || e >= (int)(sizeof(names) / sizeof(names[0]))) return "unknown";
+    return names[e];
+}
+
+double kdtn_psched_tick_in_usec(void) {
+    // netlink initClock(): /proc/net/psched "t2us us2t clock_res hz" in hex
+    FILE* f = std::fopen("/proc/net/psched", "r");
+    if (!f) return 0.0;
+    unsigned long long v[4];
+    int got = std::fscanf(f, "%llx %llx %llx %llx", &v[0], &v[1], &v[2], &v[3]);
+    std::fclose(f);
+    if (got != 4 || v[1] == 0) return 0.0;
+    if (v[2] == 1000000000ull) v[0] = v[1];
+    const double clock_factor = (double)v[2] / 1000000.0;
+    return (double)v[0] / (double)v[1] * clock_factor;
+}
+
+int kdtn_init(kdtn_ctx** out, const kdtn_config* cfg) {
+    if (!out || !cfg) return KDTN_EINVAL;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        std::snprintf(g_last_error, sizeof(g_last_error), "no HIP device visible");
+        return KDTN_ENODEV;
+    }
+    int dev = cfg->device;
+    if (dev < 0) HIP_TRY(hipGetDevice(&dev));
+    if (dev >= ndev) return KDTN_EINVAL;
+    HIP_TRY(hipSetDevice(dev));
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, dev));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        std::snprintf(g_last_error, sizeof(g_last_error), "device %d is %s, libkdtn is built for gfx950",
+                      dev, prop.gcnArchName);
+        return KDTN_ENODEV;
+    }
+    kdtn_ctx* c = new kdtn_ctx();
+    c->device = dev;
+    c->cfg = *cfg;
+    if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return KDTN_EIO;
+    }
+    c->stream = c->own_stream;
+    if (hipHostMalloc(reinterpret_cast<void**>(&c->h_misc), 64, hipHostMallocDefault) != hipSuccess) {
+        (void)hipStreamDestroy(c->own_stream);
+        delete c;
+        return KDTN_ENOMEM;
+    }
+    for (int i = 0; i <= kMaxTimers; ++i) (void)hipEventCreate(&c->ev[i]);
+    *out = c;
+    return KDTN_OK;
+}
+
+void kdtn_destroy(kdtn_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    DevBuf* bufs[] = {&c->kd_bytes, &c->kd_offs, &c->kd_flags, &c->pd_bytes, &c->pd_offs,
+                      &c->pd_parsed, &c->pd_rate, &c->t_ns, &c->t_name, &c->t_src, &c->t_netns,
+                      &c->t_flags, &c->t_roff, &c->t_noff, &c->real.buf, &c->des.buf, &c->v_node,
+                      &c->v_vni, &c->v_netns, &c->v_keys, &c->v_vals, &c->pods, &c->pod_keys,
+                      &c->pod_vals, &c->oflag, &c->otarget, &c->nflag, &c->wg_cnt, &c->wg_base,
+                      &c->misc, &c->hscratch, &c->fscratch, &c->action, &c->del_off, &c->add_off,
+                      &c->upd_off, &c->del_idx, &c->add_idx, &c->upd_idx, &c->del_res,
+                      &c->add_res, &c->upd_res, &c->add_qdisc, &c->upd_qdisc};
+    for (DevBuf* b : bufs) release(*b);
+    for (int i = 0; i <= kMaxTimers; ++i)
+        if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
+    if (c->comm) (void)ncclCommDestroy(c->comm);
+    if (c->h_misc) (void)hipHostFree(c->h_misc);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete c;
+}
+
+int kdtn_set_stream(kdtn_ctx* c, void* s) {
+    if (!c) return KDTN_EINVAL;
+    c->stream = s ? static_cast<hipStream_t>(s) : c->own_stream;
+    return KDTN_OK;
+}
+
+int kdtn_epoch_upload(kdtn_ctx* c, const kdtn_epoch_in* in) {
+    if (!c || !in) return KDTN_EINVAL;
+    HIP_TRY(hipSetDevice(c->device));
+    g_last_error[0] = 0;
+    TRY(check_strtab(in->kdict, "kdict"));
+    TRY(check_strtab(in->pdict, "pdict"));
+    const kdtn_topo_table& T = in->topos;
+    const uint32_t D = in->kdict.n, P = in->pdict.n;
+    TRY(check_offsets(T.real_off, T.n, in->realised.n, "topos.real_off"));
+    TRY(check_offsets(T.des_off, T.n, in->desired.n, "topos.des_off"));
+    if (T.n && (!T.flags)) return KDTN_EINVAL;
+    TRY(check_ids(T.ns, T.n, D, "topos.ns"));
+    TRY(check_ids(T.name, T.n, D, "topos.name"));
+    TRY(check_ids(T.src_ip, T.n, D, "topos.src_ip"));
+    TRY(check_ids(T.net_ns, T.n, D, "topos.net_ns"));
+    for (uint32_t t = 0; t < T.n; ++t) {
+        if ((T.flags[t] & KDTN_TOPO_STATUS_NIL) && T.real_off[t + 1] != T.real_off[t]) {
+            std::snprintf(g_last_error, sizeof(g_last_error), "topology %u: status.links nil but non-empty", t);
+            return KDTN_EINVAL;
+        }
+        if ((T.flags[t] & KDTN_TOPO_SPEC_NIL) && T.des_off[t + 1] != T.des_off[t]) {
+            std::snprintf(g_last_error, sizeof(g_last_error), "topology %u: spec.links nil but non-empty", t);
+            return KDTN_EINVAL;
+        }
+    }
+    TRY(check_ids(in->vnis.node, in->vnis.n, D, "vnis.node"));
+    TRY(check_ids(in->vnis.net_ns, in->vnis.n, D, "vnis.net_ns"));
+    const uint32_t slice = in->pod_slice ? in->pod_slice : T.n;
+    if (slice < T.n) return KDTN_EINVAL;
+
+    c->D = D;
+    c->P = P;
+    c->T = T.n;
+    TRY(upload(c, c->kd_bytes, in->kdict.bytes, in->kdict.offs[D]));
+    TRY(upload(c, c->kd_offs, in->kdict.offs, (size_t)(D + 1) * 4));
+    TRY(ensure(c->kd_flags, D));
+    TRY(upload(c, c->pd_bytes, in->pdict.bytes, in->pdict.offs[P]));
+    TRY(upload(c, c->pd_offs, in->pdict.offs, (size_t)(P + 1) * 4));
+    TRY(ensure(c->pd_parsed, (size_t)P * 16));
+    TRY(ensure(c->pd_rate, (size_t)P * 8));
+
+    TRY(upload(c, c->t_ns, T.ns, (size_t)T.n * 4));
+    TRY(upload(c, c->t_name, T.name, (size_t)T.n * 4));
+    TRY(upload(c, c->t_src, T.src_ip, (size_t)T.n * 4));
+    TRY(upload(c, c->t_netns, T.net_ns, (size_t)T.n * 4));
+    TRY(upload(c, c->t_flags, T.flags, (size_t)T.n));
+    TRY(upload(c, c->t_roff, T.real_off, (size_t)(T.n + 1) * 4));
+    TRY(upload(c, c->t_noff, T.des_off, (size_t)(T.n + 1) * 4));
+
+    TRY(upload_links(c, c->real, in->realised, D, P, "realised"));
+    TRY(upload_links(c, c->des, in->desired, D, P, "desired"));
+
+    const uint32_t V = in->vnis.n;
+    c->V = V;
+    TRY(upload(c, c->v_node, in->vnis.node, (size_t)V * 4));
+    TRY(upload(c, c->v_vni, in->vnis.vni, (size_t)V * 4));
+    TRY(upload(c, c->v_netns, in->vnis.net_ns, (size_t)V * 4));
+    c->vni_mask = V ? next_pow2((uint64_t)V * 2) - 1 : 0;
+    TRY(ensure(c->v_keys, (size_t)(c->vni_mask + 1) * 8));
+    TRY(ensure(c->v_vals, (size_t)(c->vni_mask + 1) * 4));
+
+    c->slice = slice;
+    c->pod_total = slice * (uint32_t)c->nranks;
+    c->pod_mask = next_pow2((uint64_t)c->pod_total * 2) - 1;
+    TRY(ensure(c->pods, (size_t)c->pod_total * 16));
+    TRY(ensure(c->pod_keys, (size_t)(c->pod_mask + 1) * 8));
+    TRY(ensure(c->pod_vals, (size_t)(c->pod_mask + 1) * 4));
+
+    const uint32_t M = in->realised.n, N = in->desired.n;
+    const uint32_t nwg = (T.n + TPW - 1) / TPW;
+    TRY(ensure(c->oflag, M));
+    TRY(ensure(c->otarget, (size_t)M * 4));
+    TRY(ensure(c->nflag, N));
+    TRY(ensure(c->wg_cnt, (size_t)nwg * 12));
+    TRY(ensure(c->wg_base, (size_t)nwg * 12));
+    TRY(ensure(c->misc, 64));
+    TRY(ensure(c->hscratch, ((size_t)M + N) * 4));
+    TRY(ensure(c->fscratch, (size_t)M + N));
+    TRY(ensure(c->action, T.n));
+    TRY(ensure(c->del_off, (size_t)(T.n + 1) * 4));
+    TRY(ensure(c->add_off, (size_t)(T.n + 1) * 4));
+    TRY(ensure(c->upd_off, (size_t)(T.n + 1) * 4));
+    TRY(ensure(c->del_idx, (size_t)M * 4));
+    TRY(ensure(c->upd_idx, (size_t)M * 4));
+    TRY(ensure(c->add_idx, (size_t)N * 4));
+    TRY(ensure(c->del_res, (size_t)M * 16));
+    TRY(ensure(c->upd_res, (size_t)M * 16));
+    TRY(ensure(c->add_res, (size_t)N * 16));
+    TRY(ensure(c->upd_qdisc, (size_t)M * 72));
+    TRY(ensure(c->add_qdisc, (size_t)N * 72));
+    HIP_TRY(hipStreamSynchronize(c->stream));   // host arrays may be released after return
+    c->uploaded = true;
+    c->ran = false;
+    return KDTN_OK;
+}
+
+int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
+    if (!c || !c->uploaded) return KDTN_EINVAL;
+    HIP_TRY(hipSetDevice(c->device));
+    stages |= KDTN_STAGE_DIFF;
+    c->last_stages = stages;
+    c->n_ev = 0;
+    hipStream_t s = c->stream;
+    (void)hipEventRecord(c->ev[0], s);
+    uint32_t* misc = dp<uint32_t>(c->misc);
+    HIP_TRY(hipMemsetAsync(misc, 0xFF, 64, s));   // default id = 0xFFFFFFFF
+
+    const DevTopos T = topo_view(c);
+    // dictionaries
+    if (c->D) k_kdict_flags<<<nblocks(c->D), BLOCK, 0, s>>>(dp<uint8_t>(c->kd_bytes), dp<uint32_t>(c->kd_offs),
+                                                         c->D, dp<uint8_t>(c->kd_flags), misc);
+    if (c->P) k_pdict_parse<<<nblocks(c->P), BLOCK, 0, s>>>(dp<uint8_t>(c->pd_bytes), dp<uint32_t>(c->pd_offs),
+                                                         c->P, c->cfg.tick_in_usec, dp<uint4>(c->pd_parsed),
+                                                         dp<uint64_t>(c->pd_rate));
+    timer_mark(c, "dict_parse");
+    const bool resolve = stages & KDTN_STAGE_RESOLVE;
+    if (resolve) {
+        // pod-status table (+ all-gather across ranks) and lookup tables
+        const uint32_t rank_base = c->slice * (uint32_t)c->rank;
+        if (c->slice) k_pods_fill<<<nblocks(c->slice), BLOCK, 0, s>>>(T, c->slice, rank_base, dp<uint4>(c->pods));
+        if (c->nranks > 1) {
+            uint4* pods = dp<uint4>(c->pods);
+            ncclResult_t r = ncclAllGather(pods + rank_base, pods, (size_t)c->slice * 4, ncclUint32, c->comm, s);
+            if (r != ncclSuccess) {
+                std::snprintf(g_last_error, sizeof(g_last_error), "ncclAllGather: %s", ncclGetErrorString(r));
+                return KDTN_EIO;
+            }
+        }
+        timer_mark(c, "pods_allgather");
+        HIP_TRY(hipMemsetAsync(c->pod_keys.p, 0xFF, (size_t)(c->pod_mask + 1) * 8, s));
+        HIP_TRY(hipMemsetAsync(c->pod_vals.p, 0xFF, (size_t)(c->pod_mask + 1) * 4, s));
+        if (c->pod_total)
+            k_pod_ht_build<<<nblocks(c->pod_total), BLOCK, 0, s>>>(dp<uint4>(c->pods), c->pod_total,
+                                                                  dp<uint64_t>(c->pod_keys),
+                                                                  dp<uint32_t>(c->pod_vals), c->pod_mask);
+        if (c->V) {
+            HIP_TRY(hipMemsetAsync(c->v_keys.p, 0xFF, (size_t)(c->vni_mask + 1) * 8, s));
+            HIP_TRY(hipMemsetAsync(c->v_vals.p, 0xFF, (size_t)(c->vni_mask + 1) * 4, s));
+            k_vni_ht_build<<<nblocks(c->V), BLOCK, 0, s>>>(dp<uint32_t>(c->v_node), dp<int32_t>(c->v_vni), c->V,
+                                                          dp<uint64_t>(c->v_keys), dp<uint32_t>(c->v_vals),
+                                                          c->vni_mask);
+        }
+        timer_mark(c, "hash_build");
+    }
+    const uint32_t nwg = (c->T + TPW - 1) / TPW;
+    if (c->T) {
+        DiffOut d;
+        d.oflag = dp<uint8_t>(c->oflag);
+        d.otarget = dp<uint32_t>(c->otarget);
+        d.nflag = dp<uint8_t>(c->nflag);
+        d.action = dp<uint8_t>(c->action);
+        d.wg_cnt = dp<uint32_t>(c->wg_cnt);
+        d.hscratch = dp<uint32_t>(c->hscratch);
+        d.fscratch = dp<uint8_t>(c->fscratch);
+        k_diff<<<nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, d);
+        timer_mark(c, "diff");
+    }
+    k_scan<<<1, 1024, 0, s>>>(dp<uint32_t>(c->wg_cnt), nwg, dp<uint32_t>(c->wg_base), misc + 1, c->T,
+                              dp<uint32_t>(c->del_off), dp<uint32_t>(c->add_off), dp<uint32_t>(c->upd_off));
+    timer_mark(c, "scan");
+    if (c->T) {
+        DevTables tb;
+        tb.kflags = dp<uint8_t>(c->kd_flags);
+        tb.pparsed = dp<uint4>(c->pd_parsed);
+        tb.prate = dp<uint64_t>(c->pd_rate);
+        tb.pods = dp<uint4>(c->pods);
+        tb.pod_keys = dp<uint64_t>(c->pod_keys);
+        tb.pod_vals = dp<uint32_t>(c->pod_vals);
+        tb.pod_mask = c->pod_mask;
+        tb.vni_keys = dp<uint64_t>(c->v_keys);
+        tb.vni_vals = dp<uint32_t>(c->v_vals);
+        tb.vni_netns = dp<uint32_t>(c->v_netns);
+        tb.vni_mask = c->V ? c->vni_mask : 0;
+        tb.default_id = misc;
+        tb.pod_base = c->slice * (uint32_t)c->rank;
+        tb.vxlan_base = c->cfg.vxlan_base;
+        EmitOut e;
+        e.del_off = dp<uint32_t>(c->del_off);
+        e.add_off = dp<uint32_t>(c->add_off);
+        e.upd_off = dp<uint32_t>(c->upd_off);
+        e.del_idx = dp<uint32_t>(c->del_idx);
+        e.add_idx = dp<uint32_t>(c->add_idx);
+        e.upd_idx = dp<uint32_t>(c->upd_idx);
+        e.del_res = dp<uint4>(c->del_res);
+        e.add_res = dp<uint4>(c->add_res);
+        e.upd_res = dp<uint4>(c->upd_res);
+        e.add_qdisc = dp<uint2>(c->add_qdisc);
+        e.upd_qdisc = dp<uint2>(c->upd_qdisc);
+        e.wg_base = dp<uint32_t>(c->wg_base);
+        e.stages = stages;
+        k_emit<<<nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, dp<uint8_t>(c->oflag),
+                                     dp<uint32_t>(c->otarget), dp<uint8_t>(c->nflag), dp<uint8_t>(c->action),
+                                     tb, e);
+        timer_mark(c, "emit");
+    }
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(c->h_misc, misc, 16, hipMemcpyDeviceToHost, s));
+    c->ran = true;
+    return KDTN_OK;
+}
+
+int kdtn_epoch_sync(kdtn_ctx* c, kdtn_counts* counts) {
+    if (!c || !c->ran) return KDTN_EINVAL;
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (counts) {
+        counts->n_del = c->h_misc[1];
+        counts->n_upd = c->h_misc[2];
+        counts->n_add = c->h_misc[3];
+        counts->n_topos = c->T;
+    }
+    return KDTN_OK;
+}
+
+int kdtn_epoch_download(kdtn_ctx* c, kdtn_batches* o) {
+    if (!c || !o || !c->ran) return KDTN_EINVAL;
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    const uint32_t nd = c->h_misc[1], nu = c->h_misc[2], na = c->h_misc[3];
+    o->n_del = nd;
+    o->n_upd = nu;
+    o->n_add = na;
+    if (nd > o->del_cap || nu > o->upd_cap || na > o->add_cap) return KDTN_ENOSPC;
+    hipStream_t s = c->stream;
+    auto d2h = [&](void* dst, DevBuf& b, size_t bytes) -> int {
+        if (dst && bytes) HIP_TRY(hipMemcpyAsync(dst, b.p, bytes, hipMemcpyDeviceToHost, s));
+        return KDTN_OK;
+    };
+    const bool res = c->last_stages & KDTN_STAGE_RESOLVE, q = c->last_stages & KDTN_STAGE_QDISC;
+    TRY(d2h(o->action, c->action, c->T));
+    TRY(d2h(o->del_off, c->del_off, (size_t)(c->T + 1) * 4));
+    TRY(d2h(o->add_off, c->add_off, (size_t)(c->T + 1) * 4));
+    TRY(d2h(o->upd_off, c->upd_off, (size_t)(c->T + 1) * 4));
+    TRY(d2h(o->del_idx, c->del_idx, (size_t)nd * 4));
+    TRY(d2h(o->add_idx, c->add_idx, (size_t)na * 4));
+    TRY(d2h(o->upd_idx, c->upd_idx, (size_t)nu * 4));
+    if (res) {
+        TRY(d2h(o->del_res, c->del_res, (size_t)nd * 16));
+        TRY(d2h(o->add_res, c->add_res, (size_t)na * 16));
+        TRY(d2h(o->upd_res, c->upd_res, (size_t)nu * 16));
+    }
+    if (q) {
+        TRY(d2h(o->add_qdisc, c->add_qdisc, (size_t)na * 72));
+        TRY(d2h(o->upd_qdisc, c->upd_qdisc, (size_t)nu * 72));
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    return KDTN_OK;
+}
+
+int kdtn_reconcile_epoch(kdtn_ctx* c, const kdtn_epoch_in* in, kdtn_batches* out) {
+    TRY(kdtn_epoch_upload(c, in));
+    TRY(kdtn_epoch_run(c, KDTN_STAGE_ALL));
+    TRY(kdtn_epoch_sync(c, nullptr));
+    return kdtn_epoch_download(c, out);
+}
+
+int kdtn_make_qdiscs(kdtn_ctx* c, const kdtn_strtab* pdict, const kdtn_props_table* props,
+                     kdtn_qdisc* out) {
+    if (!c || !pdict || !props || (!out && props->n)) return KDTN_EINVAL;
+    HIP_TRY(hipSetDevice(c->device));
+    g_last_error[0] = 0;
+    TRY(check_strtab(*pdict, "pdict"));
+    const uint32_t P = pdict->n, n = props->n;
+    for (int k = 0; k < KDTN_NPROP; ++k) TRY(check_ids(props->prop[k], n, P, "props"));
+    if (n && !props->gap) return KDTN_EINVAL;
+    TRY(upload(c, c->pd_bytes, pdict->bytes, pdict->offs[P]));
+    TRY(upload(c, c->pd_offs, pdict->offs, (size_t)(P + 1) * 4));
+    TRY(ensure(c->pd_parsed, (size_t)P * 16));
+    TRY(ensure(c->pd_rate, (size_t)P * 8));
+    // reuse the desired-link store for the property columns
+    kdtn_link_table L{};
+    L.n = n;
+    std::vector<uint32_t> zeros((size_t)std::max<uint32_t>(n, 1), 0u);
+    std::vector<int64_t> zuid((size_t)std::max<uint32_t>(n, 1), 0);
+    for (int k = 0; k < KDTN_NKEY; ++k) L.key[k] = zeros.data();
+    L.uid = zuid.data();
+    for (int k = 0; k < KDTN_NPROP; ++k) L.prop[k] = props->prop[k];
+    L.gap = props->gap;
+    TRY(upload_links(c, c->des, L, 1, P, "props"));
+    TRY(ensure(c->add_qdisc, (size_t)std::max<uint32_t>(n, 1) * 72));
+    hipStream_t s = c->stream;
+    k_pdict_parse<<<nblocks(P), BLOCK, 0, s>>>(dp<uint8_t>(c->pd_bytes), dp<uint32_t>(c->pd_offs), P,
+                                               c->cfg.tick_in_usec, dp<uint4>(c->pd_parsed),
+                                               dp<uint64_t>(c->pd_rate));
+    if (n)
+        k_qdisc_batch<<<nblocks(n), BLOCK, 0, s>>>(c->des.view, dp<uint4>(c->pd_parsed), dp<uint64_t>(c->pd_rate),
+                                                   dp<uint2>(c->add_qdisc));
+    HIP_TRY(hipGetLastError());
+    if (n) HIP_TRY(hipMemcpyAsync(out, c->add_qdisc.p, (size_t)n * 72, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    c->uploaded = false;   // the desired store was reused
+    return KDTN_OK;
+}
+
+int kdtn_comm_unique_id(uint8_t out[128]) {
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return KDTN_EIO;
+    static_assert(sizeof(id) == 128, "ncclUniqueId is 128 bytes");
+    std::memcpy(out, &id, 128);
+    return KDTN_OK;
+}
+
+int kdtn_comm_init(kdtn_ctx* c, const uint8_t uid[128], int nranks, int rank) {
+    if (!c || !uid || nranks < 1 || rank < 0 || rank >= nranks) return KDTN_EINVAL;
+    HIP_TRY(hipSetDevice(c->device));
+    if (c->comm) {
+        (void)ncclCommDestroy(c->comm);
+        c->comm = nullptr;
+    }
+    c->nranks = nranks;
+    c->rank = rank;
+    c->uploaded = false;
+    if (nranks == 1) return KDTN_OK;
+    ncclUniqueId id;
+    std::memcpy(&id, uid, 128);
+    ncclResult_t r = ncclCommInitRank(&c->comm, nranks, id, rank);
+    if (r != ncclSuccess) {
+        std::snprintf(g_last_error, sizeof(g_last_error), "ncclCommInitRank: %s", ncclGetErrorString(r));
+        c->comm = nullptr;
+        c->nranks = 1;
+        c->rank = 0;
+        return KDTN_EIO;
+    }
+    return KDTN_OK;
+}
+
+int kdtn_last_kernel_times(kdtn_ctx* c, const char** names, float* ms, int cap) {
+    if (!c) return KDTN_EINVAL;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    int n = std::min(cap, c->n_ev);
+    for (int i = 0; i < n; ++i) {
+        if (names) names[i] = c->ev_name[i];
+        float t = 0.f;
+        (void)hipEventElapsedTime(&t, c->ev[i], c->ev[i + 1]);
+        if (ms) ms[i] = t;
+    }
+    return n;
+}
+
+}  // extern "C"

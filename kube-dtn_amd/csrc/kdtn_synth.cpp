@@ -1,0 +1,563 @@
+// kdtn_synth.cpp — deterministic synthetic Topology workloads.
+// Bench/test infrastructure (host C++), not part of the engine: it emits exactly the
+// SoA tables + deduplicated dictionaries that the C-ABI (include/kdtn.h) consumes.
+//
+//   config 1  fat-tree: 1,000 spines + 9,000 leaves, 50,000 edges → 100,000 records,
+//             uniform props {latency:10ms, loss:0.1, rate:1Gbit}; realised = same keys
+//             with empty props → every record is an UpdateLinks entry.
+//   config 2  random 10-regular (multi)graph over T pods (pairing model: a keyed Feistel
+//             permutation of the 10·T stubs pairs stub π(2i) with π(2i+1); computable per
+//             shard), heterogeneous netem/tbf props seeded per uid, 64 nodes, 2 % dead
+//             pods; realised = empty non-nil status → every record is an AddLinks entry.
+//   config 3  churn on config 2: realised = config-2 desired; desired drops 1/60 of the
+//             edges, re-draws the props of 1/60, and adds n_edges/60 fresh edges (5 % churn).
+//   config 4  WAN twin: sites in namespaces of 100, power-law degrees (Chung-Lu inside a
+//             namespace, hubs ≈1000 links), 256 nodes, 1 % physical/ and 0.5 % localhost
+//             peers; realised empty → AddLinks, resolution-dominated.
+// Sharding: global pod p belongs to shard p / T_local (contiguous blocks, pod_slice =
+// T_local). Pod names, namespaces, node IPs and netns strings carry GLOBAL ids (a shared
+// dictionary prefix identical on every shard); per-link strings get shard-local ids.
+#include <cstdint>
+#include <cstdio>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace {
+
+uint64_t splitmix(uint64_t& x) {
+    uint64_t z = (x += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+uint64_t hmix(uint64_t a, uint64_t b) {
+    uint64_t x = a * 0x9E3779B97F4A7C15ull ^ (b + 0x632BE59BD9B4E019ull);
+    return splitmix(x);
+}
+
+struct Rng {
+    uint64_t s;
+    explicit Rng(uint64_t seed) : s(seed) {}
+    uint64_t next() { return splitmix(s); }
+    uint32_t below(uint32_t n) { return (uint32_t)((next() >> 11) % n); }
+    double unit() { return (double)(next() >> 11) * (1.0 / 9007199254740992.0); }
+};
+
+// Keyed bijection on [0, n) : Feistel network over the next power-of-two square, cycle walking.
+struct Perm {
+    uint64_t n, half_bits, mask, key;
+    Perm(uint64_t n_, uint64_t key_) : n(n_), key(key_) {
+        uint64_t bits = 2;
+        while ((1ull << bits) < n) ++bits;
+        if (bits & 1) ++bits;
+        half_bits = bits / 2;
+        mask = (1ull << half_bits) - 1;
+    }
+    uint64_t round_f(uint64_t r, int k) const { return hmix(key + (uint64_t)k, r) & mask; }
+    uint64_t fwd1(uint64_t x) const {
+        uint64_t l = x >> half_bits, r = x & mask;
+        for (int k = 0; k < 4; ++k) {
+            uint64_t nl = r, nr = l ^ round_f(r, k);
+            l = nl;
+            r = nr;
+        }
+        return (l << half_bits) | r;
+    }
+    uint64_t inv1(uint64_t y) const {
+        uint64_t l = y >> half_bits, r = y & mask;
+        for (int k = 3; k >= 0; --k) {
+            uint64_t pr = l, pl = r ^ round_f(l, k);
+            l = pl;
+            r = pr;
+        }
+        return (l << half_bits) | r;
+    }
+    uint64_t fwd(uint64_t x) const {
+        do { x = fwd1(x); } while (x >= n);
+        return x;
+    }
+    uint64_t inv(uint64_t y) const {
+        do { y = inv1(y); } while (y >= n);
+        return y;
+    }
+};
+
+struct Dict {
+    std::vector<uint8_t> bytes;
+    std::vector<uint32_t> offs{0};
+    std::unordered_map<std::string, uint32_t> map;
+    uint32_t fixed_end = 0;  // ids < fixed_end were appended without the map
+    Dict() { map.emplace(std::string(), 0u), push_raw("", 0); }
+    void push_raw(const char* s, size_t n) {
+        bytes.insert(bytes.end(), (const uint8_t*)s, (const uint8_t*)s + n);
+        offs.push_back((uint32_t)bytes.size());
+    }
+    uint32_t size() const { return (uint32_t)offs.size() - 1; }
+    uint32_t append_unique(const std::string& s) {  // caller guarantees uniqueness
+        uint32_t id = size();
+        push_raw(s.data(), s.size());
+        return id;
+    }
+    uint32_t intern(const std::string& s) {
+        auto it = map.find(s);
+        if (it != map.end()) return it->second;
+        uint32_t id = size();
+        push_raw(s.data(), s.size());
+        map.emplace(s, id);
+        return id;
+    }
+};
+
+struct Links {
+    std::vector<uint32_t> key[7];
+    std::vector<int64_t> uid;
+    std::vector<uint32_t> prop[12];
+    std::vector<uint32_t> gap;
+    size_t size() const { return uid.size(); }
+};
+
+struct Props {
+    std::string s[12];
+    uint32_t gap = 0;
+};
+
+struct Synth {
+    Dict kd, pd;
+    std::vector<uint32_t> t_ns, t_name, t_src, t_netns, t_roff{0}, t_noff{0};
+    std::vector<uint8_t> t_flags;
+    Links real, des;
+    std::vector<uint32_t> v_node, v_netns;
+    std::vector<int32_t> v_vni;
+    uint32_t pod_slice = 0, pod_base = 0, total_pods = 0;
+    // global-id bases of the shared dictionary prefix
+    uint32_t id_default = 0, id_node0 = 0, id_name0 = 0, id_netns0 = 0, id_ns0 = 0;
+    uint32_t n_nodes = 0;
+};
+
+std::string ip4(uint32_t a) {
+    char b[32];
+    std::snprintf(b, sizeof b, "10.%u.%u.%u/31", (a >> 16) & 255, (a >> 8) & 255, a & 255);
+    return b;
+}
+std::string node_ip(uint32_t n) {
+    char b[32];
+    std::snprintf(b, sizeof b, "192.168.%u.%u", n / 256, n % 256);
+    return b;
+}
+std::string num(const char* pre, uint64_t v, const char* suf = "") {
+    char b[64];
+    std::snprintf(b, sizeof b, "%s%llu%s", pre, (unsigned long long)v, suf);
+    return b;
+}
+
+// ---- heterogeneous LinkProperties ------------------------------
+std::string draw_duration(Rng& r) {
+    double u = r.unit();
+    if (u < 0.4) return num("", 1 + r.below(500), "ms");
+    if (u < 0.8) return num("", 1 + r.below(9999), "us");
+    if (u < 0.9) return "1.5s";
+    return "0.25ms";
+}
+std::string draw_pct(Rng& r) {
+    if (r.unit() < 0.01) return "100";
+    std::string s = num("", r.below(100));
+    if (r.unit() < 0.5) {
+        int nd = 1 + (int)r.below(4);
+        s += '.';
+        for (int k = 0; k < nd; ++k) s += (char)('0' + r.below(10));
+    }
+    return s;
+}
+std::string draw_rate(Rng& r) {
+    static const char* units[] = {"bit", "kbit", "Kibit", "Mbit", "Mibit", "Gbit", "bps", "Mbps", "Gibps"};
+    const char* u = units[r.below(9)];
+    if (r.unit() < 0.001) return num("", 1 + r.below(1000), "") + "." + num("", r.below(10)) + u;  // err=RATE
+    return num("", 1 + r.below(1000), u);
+}
+// props of a link are seeded by (seed, uid, version): both records of an edge agree.
+Props draw_props(uint64_t seed, uint64_t uid, uint32_t version) {
+    Rng r(hmix(hmix(seed, uid), version + 0x5151));
+    Props p;
+    if (r.unit() < 0.5) p.s[0] = draw_duration(r);   // latency
+    if (r.unit() < 0.5) p.s[1] = draw_pct(r);        // latency_corr
+    if (r.unit() < 0.3) p.s[2] = draw_duration(r);   // jitter
+    for (int k : {3, 4, 6, 7, 8, 9, 10, 11})          // loss … corrupt_corr
+        if (r.unit() < 0.5) p.s[k] = draw_pct(r);
+    if (r.unit() < 0.5) p.s[5] = draw_rate(r);       // rate
+    if (r.unit() < 0.2) p.gap = r.below(11);
+    return p;
+}
+
+void push_link(Synth& S, Links& L, const uint32_t key[7], int64_t uid, const Props& p) {
+    for (int k = 0; k < 7; ++k) L.key[k].push_back(key[k]);
+    L.uid.push_back(uid);
+    for (int k = 0; k < 12; ++k) L.prop[k].push_back(p.s[k].empty() ? 0u : S.pd.intern(p.s[k]));
+    L.gap.push_back(p.gap);
+}
+
+// shared dictionary prefix: "", "default", node IPs, then per pod: name, netns; namespaces
+void shared_prefix(Synth& S, uint32_t total_pods, uint32_t n_nodes, uint32_t n_ns,
+                   const char* name_fmt) {
+    S.id_default = S.kd.append_unique("default");
+    S.kd.map.emplace("default", S.id_default);
+    S.id_node0 = S.kd.size();
+    for (uint32_t n = 0; n < n_nodes; ++n) {
+        std::string s = node_ip(n);
+        S.kd.map.emplace(s, S.kd.append_unique(s));
+    }
+    S.id_ns0 = S.kd.size();
+    for (uint32_t q = 0; q < n_ns; ++q) {
+        std::string s = num("ns-", q);
+        S.kd.map.emplace(s, S.kd.append_unique(s));
+    }
+    S.id_name0 = S.kd.size();
+    char b[64];
+    for (uint32_t p = 0; p < total_pods; ++p) {
+        std::snprintf(b, sizeof b, name_fmt, p);
+        S.kd.push_raw(b, std::strlen(b));   // unique by construction; not looked up by string
+    }
+    S.id_netns0 = S.kd.size();
+    for (uint32_t p = 0; p < total_pods; ++p) {
+        std::snprintf(b, sizeof b, "/run/netns/cni-%08x", p);
+        S.kd.push_raw(b, std::strlen(b));
+    }
+    S.n_nodes = n_nodes;
+    S.total_pods = total_pods;
+}
+
+void push_topo(Synth& S, uint32_t p, uint32_t ns_id, bool dead, uint32_t node, uint8_t flags) {
+    S.t_ns.push_back(ns_id);
+    S.t_name.push_back(S.id_name0 + p);
+    S.t_src.push_back(dead ? 0u : S.id_node0 + node);
+    S.t_netns.push_back(dead ? 0u : S.id_netns0 + p);
+    S.t_flags.push_back(flags);
+}
+void close_topo(Synth& S) {
+    S.t_roff.push_back((uint32_t)S.real.size());
+    S.t_noff.push_back((uint32_t)S.des.size());
+}
+
+// ---- config 1 --------------------------------------------------------------------------
+void build_config1(Synth& S) {
+    const uint32_t SP = 1000, LF = 9000, T = SP + LF;
+    shared_prefix(S, T, 64, 0, "r%u");
+    // edges
+    struct E { uint32_t a, b; };
+    std::vector<E> edges;
+    for (uint32_t j = 0; j < LF; ++j)
+        for (uint32_t i = 0; i < 5; ++i) edges.push_back({SP + j, (5 * j + i) % SP});
+    for (uint32_t m = 0; m < LF / 2; ++m) edges.push_back({SP + 2 * m, SP + 2 * m + 1});
+    for (uint32_t m = 0; m < SP / 2; ++m) edges.push_back({2 * m, 2 * m + 1});
+    std::vector<std::vector<std::pair<uint32_t, uint32_t>>> adj(T);  // (edge, side)
+    for (uint32_t e = 0; e < edges.size(); ++e) {
+        adj[edges[e].a].push_back({e, 0});
+        adj[edges[e].b].push_back({e, 1});
+    }
+    // interface position of each (edge, side)
+    std::vector<uint32_t> pos(edges.size() * 2);
+    for (uint32_t p = 0; p < T; ++p)
+        for (uint32_t k = 0; k < adj[p].size(); ++k) pos[adj[p][k].first * 2 + adj[p][k].second] = k;
+    Props uni;
+    uni.s[0] = "10ms";
+    uni.s[3] = "0.1";
+    uni.s[5] = "1Gbit";
+    Props empty;
+    S.pod_slice = T;
+    S.pod_base = 0;
+    for (uint32_t p = 0; p < T; ++p) {
+        push_topo(S, p, S.id_default, false, p % 64, 0);
+        for (auto [e, side] : adj[p]) {
+            uint32_t peer = side ? edges[e].a : edges[e].b;
+            uint32_t key[7];
+            key[0] = S.kd.intern(num("eth", pos[e * 2 + side]));
+            key[1] = S.kd.intern(ip4(2 * e + side));
+            key[2] = 0;
+            key[3] = S.kd.intern(num("eth", pos[e * 2 + (side ^ 1)]));
+            key[4] = S.kd.intern(ip4(2 * e + (side ^ 1)));
+            key[5] = 0;
+            key[6] = S.id_name0 + peer;
+            push_link(S, S.real, key, e + 1, empty);
+            push_link(S, S.des, key, e + 1, uni);
+        }
+        close_topo(S);
+    }
+}
+
+// ---- config 2 / 3 ----------------------------------------------------------------------
+struct RegularGraph {
+    uint64_t stubs;
+    Perm perm;
+    uint32_t degree;
+    RegularGraph(uint64_t n_pods, uint32_t d, uint64_t seed)
+        : stubs(n_pods * d), perm(n_pods * d, seed), degree(d) {}
+    // stub s = pod*degree + position; returns partner stub and edge index
+    void partner(uint64_t s, uint64_t* other, uint64_t* edge, uint32_t* side) const {
+        uint64_t i = perm.inv(s);
+        *other = perm.fwd(i ^ 1ull);
+        *edge = i >> 1;
+        *side = (uint32_t)(i & 1ull);
+    }
+};
+
+void build_config23(Synth& S, int config, uint64_t seed, uint32_t pods_per_shard, uint32_t degree,
+                    uint32_t n_nodes, double dead_frac, uint32_t shard, uint32_t nshards) {
+    const uint64_t total = (uint64_t)pods_per_shard * nshards;
+    shared_prefix(S, (uint32_t)total, n_nodes, 0, "p%u");
+    RegularGraph G(total, degree, seed);
+    const uint64_t n_edges = G.stubs / 2;
+    S.pod_slice = pods_per_shard;
+    S.pod_base = shard * pods_per_shard;
+    auto is_dead = [&](uint64_t p) { return (double)(hmix(seed ^ 0xDEADull, p) >> 11) * (1.0 / 9007199254740992.0) < dead_frac; };
+    auto node_of = [&](uint64_t p) { return (uint32_t)(hmix(seed ^ 0x40DEull, p) % n_nodes); };
+    // churn decisions per edge (config 3): 0 keep, 1 delete, 2 re-draw props
+    auto churn = [&](uint64_t e) -> int {
+        double u = (double)(hmix(seed ^ 0xC4124ull, e) >> 11) * (1.0 / 9007199254740992.0);
+        return u < 1.0 / 60 ? 1 : (u < 2.0 / 60 ? 2 : 0);
+    };
+    // added edges (config 3): global list, each shard keeps those touching its pods
+    std::vector<std::vector<std::pair<uint64_t, uint32_t>>> added;  // per local pod: (new edge, side)
+    std::vector<std::pair<uint64_t, uint64_t>> new_edges;
+    if (config == 3) {
+        added.resize(pods_per_shard);
+        const uint64_t n_new = n_edges / 60;   // 1/60 of the edges added: 5 % churn split 3 ways
+        Rng r(seed ^ 0xADDull);
+        for (uint64_t q = 0; q < n_new; ++q) {
+            uint64_t a = r.next() % total, b = r.next() % total;
+            new_edges.push_back({a, b});
+            if (a / pods_per_shard == shard) added[a - S.pod_base].push_back({q, 0});
+            if (b / pods_per_shard == shard) added[b - S.pod_base].push_back({q, 1});
+        }
+    }
+    Props empty;
+    for (uint64_t lp = 0; lp < pods_per_shard; ++lp) {
+        const uint64_t p = S.pod_base + lp;
+        const bool dead = is_dead(p);
+        push_topo(S, (uint32_t)p, S.id_default, dead, node_of(p), 0);
+        uint32_t kept_pos = 0;
+        for (uint32_t k = 0; k < degree; ++k) {
+            uint64_t other, e;
+            uint32_t side;
+            G.partner(p * degree + k, &other, &e, &side);
+            const uint64_t peer = other / degree;
+            const uint32_t ppos = (uint32_t)(other % degree);
+            uint32_t key[7];
+            key[0] = S.kd.intern(num("eth", k));
+            key[1] = S.kd.intern(ip4((uint32_t)(2 * e + side)));
+            key[2] = 0;
+            key[3] = S.kd.intern(num("eth", ppos));
+            key[4] = S.kd.intern(ip4((uint32_t)(2 * e + (side ^ 1))));
+            key[5] = 0;
+            key[6] = S.id_name0 + (uint32_t)peer;
+            const Props pr = draw_props(seed, e + 1, 0);
+            if (config == 2) {
+                push_link(S, S.des, key, (int64_t)(e + 1), pr);
+            } else {
+                push_link(S, S.real, key, (int64_t)(e + 1), pr);
+                const int c = churn(e);
+                if (c == 1) continue;
+                push_link(S, S.des, key, (int64_t)(e + 1), c == 2 ? draw_props(seed, e + 1, 1) : pr);
+            }
+            ++kept_pos;
+        }
+        if (config == 3) {
+            uint32_t extra = 0;
+            for (auto [q, side] : added[lp]) {
+                const uint64_t a = new_edges[q].first, b = new_edges[q].second;
+                const uint64_t peer = side ? a : b;
+                const uint64_t e = n_edges + q;
+                uint32_t key[7];
+                key[0] = S.kd.intern(num("eth", degree + extra));
+                key[1] = S.kd.intern(ip4((uint32_t)(2 * e + side)));
+                key[2] = 0;
+                key[3] = S.kd.intern(num("nx", q));   // peer-side name of the new interface
+                key[4] = S.kd.intern(ip4((uint32_t)(2 * e + (side ^ 1))));
+                key[5] = 0;
+                key[6] = S.id_name0 + (uint32_t)peer;
+                push_link(S, S.des, key, (int64_t)(e + 1), draw_props(seed, e + 1, 0));
+                ++extra;
+            }
+        }
+        close_topo(S);
+    }
+}
+
+// ---- config 4: WAN digital twin --------------------------------------------------------
+void build_config4(Synth& S, uint64_t seed, uint32_t sites_per_shard, uint32_t shard, uint32_t nshards) {
+    const uint32_t per_ns = 100;
+    const uint64_t total = (uint64_t)sites_per_shard * nshards;
+    const uint32_t n_ns = (uint32_t)((total + per_ns - 1) / per_ns);
+    shared_prefix(S, (uint32_t)total, 256, n_ns, "site-%u");
+    S.pod_slice = sites_per_shard;
+    S.pod_base = shard * sites_per_shard;
+    // Chung-Lu inside each namespace: weight w_i ∝ (i+1)^-0.8 scaled to mean degree 20;
+    // the namespace's edge list is generated from (seed, ns) so every shard agrees.
+    std::vector<double> w(per_ns);
+    double ws = 0;
+    for (uint32_t i = 0; i < per_ns; ++i) ws += (w[i] = 1.0 / std::pow((double)(i + 1), 0.8));
+    const double mean_deg = 20.0;
+    const uint32_t edges_per_ns = (uint32_t)(per_ns * mean_deg / 2);
+    std::vector<double> cdf(per_ns);
+    double acc = 0;
+    for (uint32_t i = 0; i < per_ns; ++i) cdf[i] = (acc += w[i] / ws);
+    auto pick = [&](Rng& r) {
+        double u = r.unit();
+        uint32_t lo = 0, hi = per_ns - 1;
+        while (lo < hi) {
+            uint32_t mid = (lo + hi) / 2;
+            if (cdf[mid] < u) lo = mid + 1;
+            else hi = mid;
+        }
+        return lo;
+    };
+    auto is_dead = [&](uint64_t p) { return (hmix(seed ^ 0xDEADull, p) % 100) < 2; };
+    auto node_of = [&](uint64_t p) { return (uint32_t)(hmix(seed ^ 0x40DEull, p) % 256); };
+    Props empty;
+    const uint64_t p_first = S.pod_base, p_last = S.pod_base + sites_per_shard;
+    uint64_t ns_first = p_first / per_ns, ns_last = (p_last + per_ns - 1) / per_ns;
+    for (uint64_t q = ns_first; q < ns_last; ++q) {
+        Rng r(hmix(seed, q + 0x4000));
+        struct E { uint32_t a, b; uint8_t kind; };   // kind 0 pod-pod, 1 physical, 2 localhost
+        std::vector<E> edges(edges_per_ns);
+        for (auto& e : edges) {
+            e.a = pick(r);
+            e.b = pick(r);
+            while (e.b == e.a) e.b = pick(r);
+            double u = r.unit();
+            e.kind = u < 0.01 ? 1 : (u < 0.015 ? 2 : 0);
+        }
+        std::vector<std::vector<std::pair<uint32_t, uint32_t>>> adj(per_ns);
+        for (uint32_t k = 0; k < edges.size(); ++k) {
+            adj[edges[k].a].push_back({k, 0});
+            if (edges[k].kind == 0) adj[edges[k].b].push_back({k, 1});
+        }
+        std::vector<uint32_t> pos(edges.size() * 2, 0);
+        for (uint32_t i = 0; i < per_ns; ++i)
+            for (uint32_t k = 0; k < adj[i].size(); ++k) pos[adj[i][k].first * 2 + adj[i][k].second] = k;
+        for (uint32_t i = 0; i < per_ns; ++i) {
+            const uint64_t p = q * per_ns + i;
+            if (p < p_first || p >= p_last || p >= total) continue;
+            push_topo(S, (uint32_t)p, S.id_ns0 + (uint32_t)q, is_dead(p), node_of(p), 0);
+            for (auto [k, side] : adj[i]) {
+                const E& e = edges[k];
+                const uint64_t ge = q * edges_per_ns + k;
+                uint32_t key[7];
+                key[0] = S.kd.intern(num("ge-", pos[k * 2 + side]));
+                key[1] = S.kd.intern(ip4((uint32_t)(2 * ge + side)));
+                key[2] = 0;
+                key[5] = 0;
+                if (e.kind == 1) {
+                    key[3] = S.kd.intern("veth1");
+                    key[4] = S.kd.intern(ip4((uint32_t)(2 * ge + 1)));
+                    key[6] = S.kd.intern(std::string("physical/") + node_ip(200 + (uint32_t)(ge % 50)));
+                } else if (e.kind == 2) {
+                    key[3] = S.kd.intern("eth0");
+                    key[4] = 0;
+                    key[6] = S.kd.intern("localhost");
+                } else {
+                    const uint32_t peer_i = side ? e.a : e.b;
+                    key[3] = S.kd.intern(num("ge-", pos[k * 2 + (side ^ 1)]));
+                    key[4] = S.kd.intern(ip4((uint32_t)(2 * ge + (side ^ 1))));
+                    key[6] = S.id_name0 + (uint32_t)(q * per_ns + peer_i);
+                }
+                push_link(S, S.des, key, (int64_t)(ge + 1), draw_props(seed, ge + 1, 0));
+            }
+            close_topo(S);
+        }
+    }
+    // a VxlanManager snapshot: every 50th cross-node link already has a VNI on its node
+    for (size_t j = 0; j < S.des.size(); j += 50) {
+        S.v_node.push_back(S.id_node0 + (uint32_t)(j % 256));
+        S.v_vni.push_back((int32_t)(5000 + S.des.uid[j]));
+        S.v_netns.push_back(S.id_netns0 + (uint32_t)(hmix(seed, j) % total));
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+struct kdtn_synth_params {
+    uint64_t seed;
+    uint32_t pods_per_shard;
+    uint32_t degree;
+    uint32_t n_nodes;
+    double dead_frac;
+    uint32_t shard;
+    uint32_t nshards;
+};
+
+void* kdtn_synth_new(int config, const kdtn_synth_params* prm) {
+    Synth* S = new Synth();
+    switch (config) {
+    case 1: build_config1(*S); break;
+    case 2:
+    case 3:
+        build_config23(*S, config, prm->seed, prm->pods_per_shard, prm->degree, prm->n_nodes, prm->dead_frac,
+                       prm->shard, prm->nshards);
+        break;
+    case 4: build_config4(*S, prm->seed, prm->pods_per_shard, prm->shard, prm->nshards); break;
+    default: delete S; return nullptr;
+    }
+    if (config == 2 || config == 4) {
+        // realised = non-nil empty status: every spec link is added
+        S->t_roff.assign(S->t_ns.size() + 1, 0u);
+    }
+    S->kd.map.clear();
+    S->pd.map.clear();
+    return S;
+}
+
+void kdtn_synth_free(void* s) { delete static_cast<Synth*>(s); }
+
+// Named arrays: returns pointer, element count and element size.
+int kdtn_synth_get(void* sp, const char* name, void** ptr, uint64_t* n, uint32_t* elem) {
+    Synth& S = *static_cast<Synth*>(sp);
+    auto ret = [&](auto& v) {
+        *ptr = (void*)v.data();
+        *n = v.size();
+        *elem = (uint32_t)sizeof(v[0]);
+        return 0;
+    };
+    std::string nm(name);
+    if (nm == "kdict_bytes") return ret(S.kd.bytes);
+    if (nm == "kdict_offs") return ret(S.kd.offs);
+    if (nm == "pdict_bytes") return ret(S.pd.bytes);
+    if (nm == "pdict_offs") return ret(S.pd.offs);
+    if (nm == "t_ns") return ret(S.t_ns);
+    if (nm == "t_name") return ret(S.t_name);
+    if (nm == "t_src") return ret(S.t_src);
+    if (nm == "t_netns") return ret(S.t_netns);
+    if (nm == "t_flags") return ret(S.t_flags);
+    if (nm == "t_roff") return ret(S.t_roff);
+    if (nm == "t_noff") return ret(S.t_noff);
+    if (nm == "v_node") return ret(S.v_node);
+    if (nm == "v_vni") return ret(S.v_vni);
+    if (nm == "v_netns") return ret(S.v_netns);
+    for (int side = 0; side < 2; ++side) {
+        Links& L = side ? S.des : S.real;
+        const std::string pre = side ? "des_" : "real_";
+        for (int k = 0; k < 7; ++k)
+            if (nm == pre + "key" + std::to_string(k)) return ret(L.key[k]);
+        for (int k = 0; k < 12; ++k)
+            if (nm == pre + "prop" + std::to_string(k)) return ret(L.prop[k]);
+        if (nm == pre + "uid") return ret(L.uid);
+        if (nm == pre + "gap") return ret(L.gap);
+    }
+    if (nm == "meta") {
+        static thread_local uint32_t meta[4];
+        meta[0] = S.pod_slice;
+        meta[1] = S.pod_base;
+        meta[2] = S.total_pods;
+        meta[3] = S.id_default;
+        *ptr = meta;
+        *n = 4;
+        *elem = 4;
+        return 0;
+    }
+    return -1;
+}
+
+}  // extern "C"

@@ -1,0 +1,177 @@
+"""Python binding of libkdtn.so (the MI355X engine behind include/kdtn.h).
+
+The library is loaded from this package directory (built in-tree by `make -C kube-dtn_amd`).
+There is no fallback: if the HIP library is missing or no gfx950 device is visible the
+calls raise — the reconcile path only runs on the GPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import abi
+from .tables import BatchesOut, EpochInput, StrTab
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libkdtn.so")
+_lib = None
+
+
+class KdtnError(RuntimeError):
+    def __init__(self, code: int, what: str):
+        super().__init__(f"{what}: {code} ({lib().kdtn_strerror(code).decode()})")
+        self.code = code
+
+
+def lib() -> C.CDLL:
+    """Load libkdtn.so; raises ImportError when it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libkdtn.so not built ({LIB_PATH}); run `make -C kube-dtn_amd`")
+    # One HIP runtime per process: PyTorch-ROCm ships libamdhip64.so.7 / librccl.so.1 with the
+    # same SONAMEs libkdtn.so links against. Loading torch first makes libkdtn bind to those
+    # already-loaded copies instead of mapping a second runtime from /opt/rocm.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    L = C.CDLL(LIB_PATH)
+    vp = C.c_void_p
+    sig = {
+        "kdtn_version": (C.c_char_p, []),
+        "kdtn_strerror": (C.c_char_p, [C.c_int]),
+        "kdtn_err_name": (C.c_char_p, [C.c_int]),
+        "kdtn_init": (C.c_int, [C.POINTER(vp), C.POINTER(abi.Config)]),
+        "kdtn_destroy": (None, [vp]),
+        "kdtn_set_stream": (C.c_int, [vp, vp]),
+        "kdtn_psched_tick_in_usec": (C.c_double, []),
+        "kdtn_interner_new": (C.c_int, [C.POINTER(vp)]),
+        "kdtn_interner_free": (None, [vp]),
+        "kdtn_intern": (C.c_uint32, [vp, C.c_char_p, C.c_uint32]),
+        "kdtn_intern_batch": (C.c_int, [vp, abi.u8p, abi.u64p, C.c_uint32, abi.u32p]),
+        "kdtn_interner_table": (C.c_int, [vp, C.POINTER(abi.Strtab)]),
+        "kdtn_reconcile_epoch": (C.c_int, [vp, C.POINTER(abi.EpochIn), C.POINTER(abi.Batches)]),
+        "kdtn_epoch_upload": (C.c_int, [vp, C.POINTER(abi.EpochIn)]),
+        "kdtn_epoch_run": (C.c_int, [vp, C.c_uint32]),
+        "kdtn_epoch_sync": (C.c_int, [vp, C.POINTER(abi.Counts)]),
+        "kdtn_epoch_download": (C.c_int, [vp, C.POINTER(abi.Batches)]),
+        "kdtn_make_qdiscs": (C.c_int, [vp, C.POINTER(abi.Strtab), C.POINTER(abi.PropsTable), vp]),
+        "kdtn_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8 * 128)]),
+        "kdtn_comm_init": (C.c_int, [vp, C.POINTER(C.c_uint8 * 128), C.c_int, C.c_int]),
+        "kdtn_last_kernel_times": (C.c_int, [vp, C.POINTER(C.c_char_p), C.POINTER(C.c_float), C.c_int]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def _check(code: int, what: str) -> None:
+    if code != abi.OK:
+        raise KdtnError(code, what)
+
+
+def comm_unique_id() -> bytes:
+    buf = (C.c_uint8 * 128)()
+    _check(lib().kdtn_comm_unique_id(C.byref(buf)), "kdtn_comm_unique_id")
+    return bytes(buf)
+
+
+class Engine:
+    """One kdtn_ctx: a reconcile engine bound to one MI355X (gfx950) device."""
+
+    def __init__(self, device: int = 0, tick_in_usec: float | None = None, vxlan_base: int = 5000):
+        L = lib()
+        if tick_in_usec is None:
+            tick_in_usec = L.kdtn_psched_tick_in_usec()
+        self.tick_in_usec = float(tick_in_usec)
+        self.vxlan_base = int(vxlan_base)
+        cfg = abi.Config(device, vxlan_base, self.tick_in_usec)
+        ctx = C.c_void_p()
+        _check(L.kdtn_init(C.byref(ctx), C.byref(cfg)), "kdtn_init")
+        self._ctx = ctx
+        self._T = 0
+        self._caps = (0, 0, 0)
+
+    def close(self) -> None:
+        if self._ctx:
+            lib().kdtn_destroy(self._ctx)
+            self._ctx = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- multi-GPU -------------------------------------------------------------------
+    def comm_init(self, unique_id: bytes, nranks: int, rank: int) -> None:
+        buf = (C.c_uint8 * 128).from_buffer_copy(unique_id)
+        _check(lib().kdtn_comm_init(self._ctx, C.byref(buf), nranks, rank), "kdtn_comm_init")
+
+    def set_stream(self, stream_handle: int | None) -> None:
+        _check(lib().kdtn_set_stream(self._ctx, C.c_void_p(stream_handle or 0)), "kdtn_set_stream")
+
+    # ---- epoch -----------------------------------------------------------------------
+    def upload(self, inp: EpochInput) -> None:
+        cin = inp.to_c()
+        _check(lib().kdtn_epoch_upload(self._ctx, C.byref(cin)), "kdtn_epoch_upload")
+        self._T = inp.topos.n
+        self._caps = (inp.realised.n, inp.desired.n, inp.realised.n)
+
+    def run(self, stages: int = abi.STAGE_ALL) -> None:
+        _check(lib().kdtn_epoch_run(self._ctx, stages), "kdtn_epoch_run")
+
+    def sync(self) -> abi.Counts:
+        c = abi.Counts()
+        _check(lib().kdtn_epoch_sync(self._ctx, C.byref(c)), "kdtn_epoch_sync")
+        return c
+
+    def download(self) -> BatchesOut:
+        cd, ca, cu = self._caps
+        out = BatchesOut.alloc(self._T, cd, ca, cu)
+        b = out.to_c((max(cd, 1), max(ca, 1), max(cu, 1)))
+        _check(lib().kdtn_epoch_download(self._ctx, C.byref(b)), "kdtn_epoch_download")
+        return out.trim(b.n_del, b.n_add, b.n_upd)
+
+    def reconcile(self, inp: EpochInput, stages: int = abi.STAGE_ALL) -> BatchesOut:
+        """Reconcile gate + CalcDiff + resolve + MakeQdiscs over every topology of `inp`."""
+        self.upload(inp)
+        self.run(stages)
+        self.sync()
+        return self.download()
+
+    def kernel_times(self) -> dict[str, float]:
+        names = (C.c_char_p * 16)()
+        ms = (C.c_float * 16)()
+        n = lib().kdtn_last_kernel_times(self._ctx, names, ms, 16)
+        return {names[i].decode(): float(ms[i]) for i in range(max(n, 0))}
+
+    # ---- MakeQdiscs batch --------------------------------------------------------------
+    def make_qdiscs(self, pdict: StrTab, prop: np.ndarray, gap: np.ndarray) -> np.ndarray:
+        """common.MakeQdiscs for n property sets: prop (NPROP, n) pdict ids, gap (n,)."""
+        prop = np.ascontiguousarray(prop, dtype=np.uint32)
+        gap = np.ascontiguousarray(gap, dtype=np.uint32)
+        n = int(gap.shape[0])
+        t = abi.PropsTable()
+        t.n = n
+        for k in range(abi.NPROP):
+            t.prop[k] = abi.ptr(prop[k], abi.u32p)
+        t.gap = abi.ptr(gap, abi.u32p)
+        out = np.zeros(max(n, 1), abi.QDISC_DTYPE)
+        cp = pdict.to_c()
+        _check(lib().kdtn_make_qdiscs(self._ctx, C.byref(cp), C.byref(t), out.ctypes.data),
+               "kdtn_make_qdiscs")
+        return out[:n]

@@ -1,0 +1,207 @@
+"""Reference-shaped host types and the batched reconcile driver.
+
+Mirrors the reference's CRD types (api/v1/topology_types.go:28-206) and the call
+surface the engine replaces, so callers (and the parity tests) read like the reference:
+
+  TopologyReconciler.calc_diff(old, new)      ↔ controllers/topology_controller.go:288
+  TopologyReconciler.reconcile_all(topos)     ↔ Reconcile :61-156 for every dirty Topology
+  make_qdiscs(engine, props)                  ↔ common/qdisc.go:20 MakeQdiscs
+  KubeDTN.add_links / del_links / update_links↔ daemon/kubedtn/handler.go:592-671 (pure prefix)
+
+Everything here only packs/unpacks tables; the work happens in libkdtn.so on the GPU.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import abi
+from .engine import Engine
+from .tables import BatchesOut, EpochInput, Interner, Links, StrTab, Topos, Vnis
+
+PROP_FIELDS = abi.PROP_COLS
+
+
+@dataclass
+class LinkProperties:          # api/v1/topology_types.go:119-176
+    latency: str = ""
+    latency_corr: str = ""
+    jitter: str = ""
+    loss: str = ""
+    loss_corr: str = ""
+    rate: str = ""
+    gap: int = 0
+    duplicate: str = ""
+    duplicate_corr: str = ""
+    reorder_prob: str = ""
+    reorder_corr: str = ""
+    corrupt_prob: str = ""
+    corrupt_corr: str = ""
+
+    @classmethod
+    def from_dict(cls, d: dict | None) -> "LinkProperties":
+        d = d or {}
+        kw = {f: str(d.get(f, "")) for f in PROP_FIELDS if d.get(f) is not None}
+        return cls(gap=int(d.get("gap", 0) or 0), **kw)
+
+
+@dataclass
+class Link:                    # api/v1/topology_types.go:59-95
+    local_intf: str = ""
+    local_ip: str = ""
+    local_mac: str = ""
+    peer_intf: str = ""
+    peer_ip: str = ""
+    peer_mac: str = ""
+    peer_pod: str = ""
+    uid: int = 0
+    properties: LinkProperties = field(default_factory=LinkProperties)
+
+    @classmethod
+    def from_dict(cls, d: dict) -> "Link":
+        return cls(local_intf=str(d.get("local_intf", "")), local_ip=str(d.get("local_ip", "") or ""),
+                   local_mac=str(d.get("local_mac", "") or ""), peer_intf=str(d.get("peer_intf", "")),
+                   peer_ip=str(d.get("peer_ip", "") or ""), peer_mac=str(d.get("peer_mac", "") or ""),
+                   peer_pod=str(d.get("peer_pod", "")), uid=int(d.get("uid", 0)),
+                   properties=LinkProperties.from_dict(d.get("properties")))
+
+
+@dataclass
+class Topology:                # api/v1/topology_types.go:200-206 (Spec.Links, Status.*)
+    name: str
+    namespace: str = "default"
+    spec_links: list[Link] | None = None     # None = nil slice
+    status_links: list[Link] | None = None
+    src_ip: str = ""
+    net_ns: str = ""
+
+
+def topologies_from_manifest(docs) -> list[Topology]:
+    """Topology objects of a parsed K8s manifest (a List or single documents)."""
+    out = []
+    for doc in docs:
+        if not doc:
+            continue
+        items = doc.get("items", [doc]) if doc.get("kind") == "List" else [doc]
+        for it in items:
+            if it.get("kind") != "Topology":
+                continue
+            md = it.get("metadata", {})
+            spec = it.get("spec") or {}
+            links = spec.get("links")
+            status = it.get("status") or {}
+            slinks = status.get("links")
+            out.append(Topology(
+                name=md["name"], namespace=md.get("namespace", "default"),
+                spec_links=None if links is None else [Link.from_dict(l) for l in links],
+                status_links=None if slinks is None else [Link.from_dict(l) for l in slinks],
+                src_ip=status.get("src_ip", "") or "", net_ns=status.get("net_ns", "") or ""))
+    return out
+
+
+def pack(topos: list[Topology], vnis: list[tuple[str, int, str]] = (),
+         kdict: Interner | None = None, pdict: Interner | None = None) -> EpochInput:
+    """Intern and lay out topologies as the engine's SoA tables (status = realised side)."""
+    kd = kdict or Interner()
+    pd = pdict or Interner()
+    T = len(topos)
+    ns = np.zeros(T, np.uint32)
+    name = np.zeros(T, np.uint32)
+    src = np.zeros(T, np.uint32)
+    netns = np.zeros(T, np.uint32)
+    flags = np.zeros(T, np.uint8)
+    roff = np.zeros(T + 1, np.uint32)
+    noff = np.zeros(T + 1, np.uint32)
+    sides = ([], [])
+    for t, tp in enumerate(topos):
+        ns[t], name[t], src[t], netns[t] = kd(tp.namespace), kd(tp.name), kd(tp.src_ip), kd(tp.net_ns)
+        flags[t] = (abi.TOPO_STATUS_NIL if tp.status_links is None else 0) | \
+                   (abi.TOPO_SPEC_NIL if tp.spec_links is None else 0)
+        sides[0].extend(tp.status_links or [])
+        sides[1].extend(tp.spec_links or [])
+        roff[t + 1] = len(sides[0])
+        noff[t + 1] = len(sides[1])
+
+    def links(ls: list[Link]) -> Links:
+        L = Links.empty(len(ls))
+        for i, l in enumerate(ls):
+            for k, col in enumerate(abi.KEY_COLS):
+                L.key[k, i] = kd(getattr(l, col))
+            L.uid[i] = l.uid
+            for k, col in enumerate(PROP_FIELDS):
+                L.prop[k, i] = pd(getattr(l.properties, col))
+            L.gap[i] = l.properties.gap
+        return L
+
+    realised, desired = links(sides[0]), links(sides[1])
+    vn = Vnis(np.array([kd(n) for n, _, _ in vnis], np.uint32),
+              np.array([v for _, v, _ in vnis], np.int32),
+              np.array([kd(s) for _, _, s in vnis], np.uint32))
+    return EpochInput(kd.table(), pd.table(), Topos(ns, name, src, netns, flags, roff, noff),
+                      realised, desired, vn)
+
+
+@dataclass
+class TopologyBatches:
+    """What Reconcile sends for one Topology: action and the three LinksBatchQuery lists."""
+    action: int
+    add: list[Link]
+    delete: list[Link]
+    properties_changed: list[Link]
+    add_res: np.ndarray
+    del_res: np.ndarray
+    upd_res: np.ndarray
+    add_qdisc: np.ndarray
+    upd_qdisc: np.ndarray
+
+
+class TopologyReconciler:
+    """Batched counterpart of controllers/topology_controller.go's TopologyReconciler."""
+
+    def __init__(self, engine: Engine):
+        self.engine = engine
+
+    def calc_diff(self, old: list[Link], new: list[Link]):
+        """CalcDiff(old, new) → (add, del, propertiesChanged) (topology_controller.go:288-318)."""
+        tp = Topology("calc-diff", spec_links=list(new), status_links=list(old))
+        b = self.reconcile_all([tp])[0]
+        if b.action != abi.ACT_DIFF:   # CalcDiff itself is not gated: equal lists ⇒ nothing changed
+            return [], [], []
+        return b.add, b.delete, b.properties_changed
+
+    def reconcile_all(self, topos: list[Topology], vnis=()) -> list[TopologyBatches]:
+        inp = pack(topos, vnis)
+        out = self.engine.reconcile(inp)
+        return unpack(topos, out)
+
+
+def unpack(topos: list[Topology], out: BatchesOut) -> list[TopologyBatches]:
+    res = []
+    for t, tp in enumerate(topos):
+        st, sp = tp.status_links or [], tp.spec_links or []
+        r0 = sum(len(x.status_links or []) for x in topos[:t])
+        n0 = sum(len(x.spec_links or []) for x in topos[:t])
+        d0, d1 = out.del_off[t], out.del_off[t + 1]
+        a0, a1 = out.add_off[t], out.add_off[t + 1]
+        u0, u1 = out.upd_off[t], out.upd_off[t + 1]
+        res.append(TopologyBatches(
+            int(out.action[t]),
+            [sp[j - n0] for j in out.add_idx[a0:a1]],
+            [st[i - r0] for i in out.del_idx[d0:d1]],
+            [sp[j - n0] for j in out.upd_idx[u0:u1]],
+            out.add_res[a0:a1], out.del_res[d0:d1], out.upd_res[u0:u1],
+            out.add_qdisc[a0:a1], out.upd_qdisc[u0:u1]))
+    return res
+
+
+def make_qdiscs(engine: Engine, props: list[LinkProperties]) -> np.ndarray:
+    """common.MakeQdiscs for a batch of LinkProperties (common/qdisc.go:20-126)."""
+    pd = Interner()
+    prop = np.zeros((abi.NPROP, len(props)), np.uint32)
+    gap = np.zeros(len(props), np.uint32)
+    for i, p in enumerate(props):
+        for k, f in enumerate(PROP_FIELDS):
+            prop[k, i] = pd(getattr(p, f))
+        gap[i] = p.gap
+    return engine.make_qdiscs(pd.table(), prop, gap)

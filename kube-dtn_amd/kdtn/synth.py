@@ -1,0 +1,96 @@
+"""Synthetic workloads of SURVEY.md §8(d) (configs 1-4) from libkdtn_synth.so.
+
+Bench/test infrastructure: builds `EpochInput`s whose arrays alias the generator's memory
+(the generator object is kept alive by `EpochInput.owner`).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import abi
+from .tables import EpochInput, Links, StrTab, Topos, Vnis
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+SYNTH_PATH = os.path.join(_HERE, "libkdtn_synth.so")
+SEED = 0x6B64746E  # "kdtn"
+_lib = None
+
+
+class Params(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("pods_per_shard", C.c_uint32), ("degree", C.c_uint32),
+                ("n_nodes", C.c_uint32), ("dead_frac", C.c_double), ("shard", C.c_uint32),
+                ("nshards", C.c_uint32)]
+
+
+def _load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(SYNTH_PATH):
+            raise ImportError(f"{SYNTH_PATH} not built; run `make -C kube-dtn_amd`")
+        L = C.CDLL(SYNTH_PATH)
+        L.kdtn_synth_new.restype = C.c_void_p
+        L.kdtn_synth_new.argtypes = [C.c_int, C.POINTER(Params)]
+        L.kdtn_synth_free.argtypes = [C.c_void_p]
+        L.kdtn_synth_get.restype = C.c_int
+        L.kdtn_synth_get.argtypes = [C.c_void_p, C.c_char_p, C.POINTER(C.c_void_p),
+                                     C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]
+        _lib = L
+    return _lib
+
+
+class _Handle:
+    def __init__(self, ptr):
+        self.ptr = ptr
+
+    def __del__(self):
+        if self.ptr:
+            _load().kdtn_synth_free(self.ptr)
+            self.ptr = None
+
+
+_DT = {1: np.uint8, 4: np.uint32, 8: np.int64}
+
+
+def _arr(h: _Handle, name: str, dtype=None) -> np.ndarray:
+    p, n, e = C.c_void_p(), C.c_uint64(), C.c_uint32()
+    if _load().kdtn_synth_get(h.ptr, name.encode(), C.byref(p), C.byref(n), C.byref(e)) != 0:
+        raise KeyError(name)
+    dt = np.dtype(dtype or _DT[e.value])
+    if n.value == 0:
+        return np.zeros(0, dt)
+    buf = (C.c_uint8 * (n.value * e.value)).from_address(p.value)
+    return np.frombuffer(buf, dtype=dt)
+
+
+def _links(h: _Handle, pre: str) -> Links:
+    key = np.stack([_arr(h, f"{pre}key{k}") for k in range(abi.NKEY)]) if True else None
+    prop = np.stack([_arr(h, f"{pre}prop{k}") for k in range(abi.NPROP)])
+    uid = _arr(h, f"{pre}uid", np.int64)
+    gap = _arr(h, f"{pre}gap")
+    if uid.shape[0] == 0:
+        return Links.empty(0)
+    return Links(np.ascontiguousarray(key), uid, np.ascontiguousarray(prop), gap)
+
+
+def make(config: int, pods_per_shard: int = 1_000_000, degree: int = 10, n_nodes: int = 64,
+         dead_frac: float = 0.02, shard: int = 0, nshards: int = 1, seed: int = SEED) -> EpochInput:
+    """Build one shard of synthetic config `config` (1: fat-tree, 2: random-regular,
+    3: churn, 4: WAN twin). Config 1 ignores the size parameters."""
+    prm = Params(seed, pods_per_shard, degree, n_nodes, dead_frac, shard, nshards)
+    ptr = _load().kdtn_synth_new(config, C.byref(prm))
+    if not ptr:
+        raise ValueError(f"unknown synthetic config {config}")
+    h = _Handle(ptr)
+    kdict = StrTab(_arr(h, "kdict_bytes"), _arr(h, "kdict_offs"))
+    pdict = StrTab(_arr(h, "pdict_bytes"), _arr(h, "pdict_offs"))
+    topos = Topos(_arr(h, "t_ns"), _arr(h, "t_name"), _arr(h, "t_src"), _arr(h, "t_netns"),
+                  _arr(h, "t_flags"), _arr(h, "t_roff"), _arr(h, "t_noff"))
+    vn = Vnis(_arr(h, "v_node"), _arr(h, "v_vni", np.int32), _arr(h, "v_netns"))
+    meta = _arr(h, "meta")
+    inp = EpochInput(kdict, pdict, topos, _links(h, "real_"), _links(h, "des_"), vn,
+                     pod_slice=int(meta[0]), pod_base=int(meta[1]), owner=h)
+    inp.total_pods = int(meta[2])
+    return inp

@@ -1,0 +1,66 @@
+/*
+ * kdtn_oracle.h — TEST INFRASTRUCTURE ONLY (the checker, never the product).
+ *
+ * CPU restatement, in plain C, of the reference kube-dtn reconcile path
+ * (Go; dtn-dslab/kube-dtn) and of the third-party arithmetic it calls:
+ *   - Go 1.18 stdlib: time.ParseDuration, strconv.ParseFloat(s,32),
+ *     strconv.ParseUint, strings.ToLower/TrimSpace, net.ParseCIDR, net.ParseMAC
+ *   - github.com/vishvananda/netlink v1.1.1-0.20201029203352-d40f9887b852
+ *     (go.mod:20): NewNetem, Percentage2u32, time2Tick
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load
+ * this library. Parity status: the reference cannot be built here (no Go
+ * toolchain); the oracle is pinned by the hand-derived known-answer vectors of
+ * tests/golden/ (from config/samples and SURVEY Appendix B) — see DESIGN.md.
+ */
+#ifndef KDTN_ORACLE_H
+#define KDTN_ORACLE_H
+#include <stdint.h>
+#include "../include/kdtn.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Individual reference functions (0 = ok, nonzero = the reference returned err). */
+int      or_parse_duration(const char* s, uint32_t n, uint32_t* us);   /* common/qdisc.go:146-158 */
+int      or_parse_float32(const char* s, uint32_t n, float* out);      /* strconv.ParseFloat(s,32) */
+int      or_parse_pct(const char* s, uint32_t n, float* out);          /* common/qdisc.go:128-143 */
+int      or_parse_rate(const char* s, uint32_t n, uint64_t* out);      /* common/qdisc.go:162-199 */
+int      or_parse_cidr(const char* s, uint32_t n);                     /* 1 if net.ParseCIDR ok    */
+int      or_parse_mac(const char* s, uint32_t n);                      /* 1 if net.ParseMAC ok     */
+uint32_t or_p2u(float p);                                              /* netlink Percentage2u32   */
+uint32_t or_time2tick(uint32_t t, double tick_in_usec);                /* netlink time2Tick        */
+uint32_t or_tbf_burst(uint64_t rate);                                  /* common/qdisc.go:361-370  */
+int32_t  or_vni_from_uid(int64_t uid, int32_t base);                   /* common/utils.go:29-31    */
+
+/* MakeQdiscs on 12 property strings (KDTN_P_* order) + gap. */
+void or_make_qdisc(const char* const* strs, const uint32_t* lens, uint32_t gap,
+                   double tick_in_usec, kdtn_qdisc* out);
+
+/* Global pod table for peer lookups (multi-shard parity); NULL = the topology table. */
+typedef struct or_pods {
+    uint32_t        n;
+    const uint32_t* ns;
+    const uint32_t* name;
+    const uint32_t* src_ip;
+    const uint32_t* net_ns;
+    const uint8_t*  flags;
+    uint32_t        base;   /* global index of this shard's topology 0 */
+} or_pods;
+
+/* Full epoch over topologies [t_begin, t_end): Reconcile gate, literal O(k^2) CalcDiff,
+ * addLink/delLink/UpdateLinks pure prefix, MakeQdiscs. Offsets/lists are relative to
+ * t_begin. Returns 0, or KDTN_ENOSPC if a capacity is too small. */
+int or_reconcile_epoch(const kdtn_epoch_in* in, const or_pods* pods, double tick_in_usec,
+                       int32_t vxlan_base, uint32_t t_begin, uint32_t t_end,
+                       kdtn_batches* out);
+/* Same, also returning the wall time of the per-topology loop alone (the maps — the
+ * daemon's informer store and VxlanManager — already exist when Reconcile runs). */
+int or_reconcile_epoch_timed(const kdtn_epoch_in* in, const or_pods* pods, double tick_in_usec,
+                             int32_t vxlan_base, uint32_t t_begin, uint32_t t_end,
+                             kdtn_batches* out, double* loop_seconds);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,154 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes wrapper of the CPU oracle (libkdtn_oracle.so).
+
+The oracle is the plain-C restatement of the reference reconcile path (see
+kdtn_oracle.h). Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use
+it, as the checker / baseline; the product (libkdtn.so, kube-dtn_amd/kdtn) never does.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(_HERE), "kube-dtn_amd"))
+from kdtn import abi  # noqa: E402  (ABI struct layouts only)
+from kdtn.tables import BatchesOut, EpochInput  # noqa: E402
+
+LIB_PATH = os.path.join(_HERE, "libkdtn_oracle.so")
+_lib = None
+
+
+class Pods(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("ns", abi.u32p), ("name", abi.u32p), ("src_ip", abi.u32p),
+                ("net_ns", abi.u32p), ("flags", abi.u8p), ("base", C.c_uint32)]
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        cs, u32 = C.c_char_p, C.c_uint32
+        L.or_parse_duration.argtypes = [cs, u32, C.POINTER(C.c_uint32)]
+        L.or_parse_float32.argtypes = [cs, u32, C.POINTER(C.c_float)]
+        L.or_parse_pct.argtypes = [cs, u32, C.POINTER(C.c_float)]
+        L.or_parse_rate.argtypes = [cs, u32, C.POINTER(C.c_uint64)]
+        L.or_parse_cidr.argtypes = [cs, u32]
+        L.or_parse_mac.argtypes = [cs, u32]
+        L.or_p2u.argtypes = [C.c_float]
+        L.or_p2u.restype = C.c_uint32
+        L.or_time2tick.argtypes = [C.c_uint32, C.c_double]
+        L.or_time2tick.restype = C.c_uint32
+        L.or_tbf_burst.argtypes = [C.c_uint64]
+        L.or_tbf_burst.restype = C.c_uint32
+        L.or_vni_from_uid.argtypes = [C.c_int64, C.c_int32]
+        L.or_vni_from_uid.restype = C.c_int32
+        L.or_make_qdisc.argtypes = [C.POINTER(C.c_char_p), C.POINTER(C.c_uint32), C.c_uint32,
+                                    C.c_double, C.POINTER(abi.Qdisc)]
+        L.or_reconcile_epoch.argtypes = [C.POINTER(abi.EpochIn), C.POINTER(Pods), C.c_double,
+                                         C.c_int32, C.c_uint32, C.c_uint32, C.POINTER(abi.Batches)]
+        L.or_reconcile_epoch_timed.argtypes = L.or_reconcile_epoch.argtypes + [C.POINTER(C.c_double)]
+        _lib = L
+    return _lib
+
+
+def _b(s) -> bytes:
+    return s.encode() if isinstance(s, str) else bytes(s)
+
+
+def parse_duration(s):
+    """ParseDuration (common/qdisc.go:146): (ok, microseconds)."""
+    b = _b(s)
+    v = C.c_uint32()
+    return lib().or_parse_duration(b, len(b), C.byref(v)) == 0, v.value
+
+
+def parse_float32(s):
+    b = _b(s)
+    v = C.c_float()
+    return lib().or_parse_float32(b, len(b), C.byref(v)) == 0, v.value
+
+
+def parse_pct(s):
+    """ParseFloatPercentage (common/qdisc.go:128): (ok, float32 value)."""
+    b = _b(s)
+    v = C.c_float()
+    return lib().or_parse_pct(b, len(b), C.byref(v)) == 0, v.value
+
+
+def parse_rate(s):
+    """ParseRate (common/qdisc.go:162): (ok, bits/s)."""
+    b = _b(s)
+    v = C.c_uint64()
+    return lib().or_parse_rate(b, len(b), C.byref(v)) == 0, v.value
+
+
+def parse_cidr(s) -> bool:
+    b = _b(s)
+    return lib().or_parse_cidr(b, len(b)) == 1
+
+
+def parse_mac(s) -> bool:
+    b = _b(s)
+    return lib().or_parse_mac(b, len(b)) == 1
+
+
+def p2u(p: float) -> int:
+    return lib().or_p2u(p)
+
+
+def time2tick(t: int, tick: float) -> int:
+    return lib().or_time2tick(t, tick)
+
+
+def vni_from_uid(uid: int, base: int = 5000) -> int:
+    return lib().or_vni_from_uid(uid, base)
+
+
+def make_qdisc(props: dict, tick: float = 15.625) -> np.ndarray:
+    """MakeQdiscs (common/qdisc.go:20) of one LinkProperties given as a dict."""
+    strs = [_b(props.get(f, "")) for f in abi.PROP_COLS]
+    arr = (C.c_char_p * abi.NPROP)(*strs)
+    lens = (C.c_uint32 * abi.NPROP)(*[len(s) for s in strs])
+    q = abi.Qdisc()
+    lib().or_make_qdisc(arr, lens, int(props.get("gap", 0)), tick, C.byref(q))
+    return np.frombuffer(bytes(q), dtype=abi.QDISC_DTYPE)[0]
+
+
+def reconcile(inp: EpochInput, tick: float = 15.625, vxlan_base: int = 5000, pods=None,
+              t_begin: int = 0, t_end: int | None = None, timing: list | None = None) -> BatchesOut:
+    """Full reference epoch (gate + literal CalcDiff + daemon pure prefix + MakeQdiscs).
+
+    `pods`: optional global pod table (dict of numpy arrays ns/name/src_ip/net_ns/flags and
+    int `base`) for multi-shard parity; default = the shard's own topology table."""
+    T = inp.topos.n
+    if t_end is None:
+        t_end = T
+    cin = inp.to_c()
+    out = BatchesOut.alloc(t_end - t_begin, max(inp.realised.n, 1), max(inp.desired.n, 1),
+                           max(inp.realised.n, 1))
+    b = out.to_c((max(inp.realised.n, 1), max(inp.desired.n, 1), max(inp.realised.n, 1)))
+    pp = None
+    if pods is not None:
+        keep = {k: np.ascontiguousarray(v, dtype=np.uint8 if k == "flags" else np.uint32)
+                for k, v in pods.items() if k != "base"}
+        pp = Pods(len(keep["ns"]), abi.ptr(keep["ns"], abi.u32p), abi.ptr(keep["name"], abi.u32p),
+                  abi.ptr(keep["src_ip"], abi.u32p), abi.ptr(keep["net_ns"], abi.u32p),
+                  abi.ptr(keep["flags"], abi.u8p), int(pods.get("base", 0)))
+    secs = C.c_double(0.0)
+    rc = lib().or_reconcile_epoch_timed(C.byref(cin), C.byref(pp) if pp is not None else None, tick,
+                                        vxlan_base, t_begin, t_end, C.byref(b), C.byref(secs))
+    if timing is not None:
+        timing.append(secs.value)
+    if rc != 0:
+        raise RuntimeError(f"oracle reconcile failed: {rc}")
+    return out.trim(b.n_del, b.n_add, b.n_upd)

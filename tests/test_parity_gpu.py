@@ -1,0 +1,183 @@
+"""GPU parity: libkdtn.so (HIP, gfx950) vs the CPU oracle, bit for bit, through the C-ABI.
+
+Every output field of the epoch (actions, batch offsets and lists, resolve records,
+qdisc structs) is compared byte-for-byte. Sizes are small enough for the oracle to finish
+in seconds, except the full-size config-2 test which checks size-independent properties
+plus an oracle-checked window of topologies.
+"""
+import random
+
+import numpy as np
+import pytest
+
+import oracle as O
+from helpers import (ACTIONS, golden_epoch, midpoint_strings, random_epoch_input,
+                     random_float_strings, uids_by_topology, DURS, PCTS, RATES, IPS, MACS)
+from kdtn import abi, synth
+from kdtn.model import Link, LinkProperties, Topology, TopologyReconciler, make_qdiscs, pack
+from kdtn.tables import Interner
+
+pytestmark = pytest.mark.gpu
+TICK = 15.625
+
+
+def assert_same(eng_out, ora_out, ctx=""):
+    bad = eng_out.mismatches(ora_out)
+    if bad:
+        f = bad[0]
+        a, b = getattr(eng_out, f), getattr(ora_out, f)
+        n = min(len(a), len(b))
+        diff = [i for i in range(n) if a[i].tobytes() != b[i].tobytes()][:5]
+        raise AssertionError(f"{ctx}: fields {bad} differ; {f} len {len(a)} vs {len(b)}; "
+                             f"first idx {diff}: {[a[i] for i in diff]} vs {[b[i] for i in diff]}")
+
+
+@pytest.mark.parametrize("idx", range(5))
+def test_golden_transitions(engine, golden, idx):
+    tr = golden["transitions"][idx]
+    topos = golden_epoch(golden, tr)
+    inp = pack(topos)
+    out = engine.reconcile(inp)
+    got = uids_by_topology(topos, out)
+    for name, exp in tr["expect"].items():
+        assert got[name]["action"] == ACTIONS[exp["action"]], (tr["name"], name)
+        for k in ("del", "add", "upd"):
+            assert got[name][k] == exp[k], (tr["name"], name, k)
+    assert_same(out, O.reconcile(inp, tick=TICK), tr["name"])
+
+
+def test_golden_qdisc_known_answers(engine, golden):
+    props = [LinkProperties.from_dict(dict(c["props"])) for c in golden["qdisc"]]
+    got = make_qdiscs(engine, props)
+    for i, c in enumerate(golden["qdisc"]):
+        want = O.make_qdisc(c["props"], TICK)
+        assert got[i].tobytes() == want.tobytes(), c
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_random_epochs(engine, seed):
+    topos, inp = random_epoch_input(seed, T=150)
+    assert_same(engine.reconcile(inp), O.reconcile(inp, tick=TICK), f"seed {seed}")
+
+
+def test_topologies_larger_than_lds_window(engine):
+    # two hubs with > CAP (4096) records on both sides → global-scratch path of k_diff,
+    # plus a workgroup whose sum exceeds CAP through several mid-size topologies
+    topos, inp = random_epoch_input(1234, T=140, big=2, p_err=0.05)
+    assert max(inp.topos.real_off[1:] - inp.topos.real_off[:-1]) > 2000
+    assert_same(engine.reconcile(inp), O.reconcile(inp, tick=TICK), "hubs")
+
+
+def _props_batch(strings, field):
+    pd = Interner()
+    n = len(strings)
+    prop = np.zeros((abi.NPROP, n), np.uint32)
+    k = abi.PROP_COLS.index(field)
+    for i, s in enumerate(strings):
+        prop[k, i] = pd(s)
+    return pd.table(), prop, np.zeros(n, np.uint32)
+
+
+@pytest.mark.parametrize("field,pool", [("loss", "pct"), ("jitter", "dur"), ("rate", "rate"),
+                                        ("latency", "dur"), ("reorder_prob", "pct")])
+def test_parser_fuzz_vs_oracle(engine, field, pool):
+    rng = random.Random(hash((field, pool)) & 0xFFFF)
+    if pool == "pct":
+        strs = PCTS + midpoint_strings(rng, 300) + random_float_strings(rng, 3000)
+    elif pool == "dur":
+        strs = DURS + [f"{rng.randint(0, 10**rng.randint(1, 19))}.{rng.randint(0, 10**rng.randint(1, 22))}"
+                       f"{rng.choice(['ns', 'us', 'µs', 'ms', 's', 'm', 'h'])}" for _ in range(2000)]
+        strs += ["".join(rng.choice("0123456789.nsuµmh+-") for _ in range(rng.randint(1, 10)))
+                 for _ in range(2000)]
+    else:
+        strs = RATES + [f"{rng.choice([' ', '', chr(0xa0)])}{rng.randint(0, 10**rng.randint(1, 21))}"
+                        f"{rng.choice(['', 'k', 'K', 'm', 'G', 't', 'T'])}{rng.choice(['', 'i', 'I'])}"
+                        f"{rng.choice(['', 'bit', 'bps', 'BIT', 'Bps', 'b'])}{rng.choice(['', ' ', chr(0x3000)])}"
+                        for _ in range(3000)]
+    strs = list(dict.fromkeys(strs))
+    pd, prop, gap = _props_batch(strs, field)
+    got = engine.make_qdiscs(pd, prop, gap)
+    for i, s in enumerate(strs):
+        want = O.make_qdisc({field: s}, TICK)
+        assert got[i].tobytes() == want.tobytes(), (field, s, got[i], want)
+
+
+def test_cidr_mac_via_epoch(engine):
+    rng = random.Random(5)
+    ips = IPS + ["1.2.3.4/32", "255.255.255.255/0", "::/0", "::ffff:1.2.3.4/96", "1::2::3/64",
+                 "1:2:3:4:5:6:7:8/128", "1:2:3:4:5:6:7:8:9/128", "::1.2.3.4/128", "1.2.3/24",
+                 "01.2.3.4/8", "0.0.0.0/00", "1.2.3.4/", "/24", "1.2.3.4/3x"]
+    macs = MACS + ["00:00:5e:00:53:01:02:03:04:05:06:07:08:09:0a:0b:0c:0d:0e:0f", "0000.5e00.5301.0203",
+                   "00:00:5E:00:53:0G", "00:00:5e:00:53:01:", "000.05e00.5301"]
+    links = []
+    uid = 1
+    for ip in ips:
+        for mac in macs:
+            links.append(Link("eth0", ip, mac, "eth1", rng.choice(ips), rng.choice(macs), "b", uid))
+            uid += 1
+    topos = [Topology("a", "default", links, [], "10.0.0.1", "/ns/a"),
+             Topology("b", "default", [], [], "10.0.0.1", "/ns/b")]
+    inp = pack(topos)
+    out = engine.reconcile(inp)
+    assert_same(out, O.reconcile(inp, tick=TICK), "cidr/mac")
+    errs = set(out.add_res["err"].tolist())
+    assert {0, abi.E_VETH_CIDR, abi.E_VETH_MAC, abi.E_PEER_VETH_CIDR} <= errs
+
+
+@pytest.mark.parametrize("cfg,pods", [(1, 0), (2, 20000), (3, 20000), (4, 5000)])
+def test_synthetic_configs_small(engine, cfg, pods):
+    inp = synth.make(cfg, pods_per_shard=pods) if pods else synth.make(cfg)
+    out = engine.reconcile(inp)
+    assert_same(out, O.reconcile(inp, tick=TICK), f"config {cfg}")
+    if cfg == 1:
+        assert len(out.upd_idx) == 100_000 and len(out.add_idx) == 0
+    if cfg in (2, 4):
+        assert len(out.add_idx) == inp.desired.n
+
+
+def test_repeat_runs_are_identical(engine):
+    inp = synth.make(3, pods_per_shard=20000)
+    engine.upload(inp)
+    engine.run()
+    engine.sync()
+    a = engine.download()
+    engine.run()
+    engine.sync()
+    b = engine.download()
+    assert not a.mismatches(b)
+
+
+def test_reconciler_mirror_calc_diff(engine):
+    a = Link("eth1", "1.1.1.1/24", "", "eth1", "", "", "p", 1)
+    a2 = Link("eth1", "1.1.1.1/24", "", "eth1", "", "", "p", 1, LinkProperties(latency="5ms"))
+    b = Link("eth2", "", "", "eth2", "", "", "p", 2)
+    rec = TopologyReconciler(engine)
+    add, dele, chg = rec.calc_diff([a, a], [a2, a])
+    assert (add, dele, [l.uid for l in chg]) == ([], [], [1, 1])
+    add, dele, chg = rec.calc_diff([a], [b, b])
+    assert ([l.uid for l in add], [l.uid for l in dele], chg) == ([2, 2], [1], [])
+
+
+def test_config2_full_size_properties(engine):
+    """BASELINE config 2 at full size (1M pods, 10M links): size-independent properties
+    plus a bit-exact oracle check on a window of 20,000 topologies."""
+    inp = synth.make(2, pods_per_shard=1_000_000)
+    out = engine.reconcile(inp)
+    N, T = inp.desired.n, inp.topos.n
+    assert N == 10_000_000 and T == 1_000_000
+    assert len(out.add_idx) == N and len(out.del_idx) == 0 and len(out.upd_idx) == 0
+    assert np.array_equal(out.add_idx, np.arange(N, dtype=np.uint32))      # spec order kept
+    assert np.array_equal(out.add_off, inp.topos.des_off)
+    assert (out.action == abi.ACT_DIFF).all()
+    kinds = np.bincount(out.add_res["kind"], minlength=6)
+    assert kinds[abi.KIND_CROSS_NODE] > 0.9 * N and kinds[abi.KIND_SAME_NODE] > 0
+    assert (out.add_res["vni"] == (5000 + inp.desired.uid).astype(np.int32)).all()
+    rate_err = (out.add_qdisc["err"] == abi.E_RATE).mean()
+    assert 0.0002 < rate_err < 0.001
+    a, b = 400_000, 420_000
+    ora = O.reconcile(inp, tick=TICK, t_begin=a, t_end=b)
+    s, e = out.add_off[a], out.add_off[b]
+    assert (out.add_off[a:b + 1] - s).tobytes() == ora.add_off.tobytes()
+    assert out.add_idx[s:e].tobytes() == ora.add_idx.tobytes()
+    assert out.add_res[s:e].tobytes() == ora.add_res.tobytes()
+    assert out.add_qdisc[s:e].tobytes() == ora.add_qdisc.tobytes()
