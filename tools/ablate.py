@@ -1,0 +1,37 @@
+"""Per-stage ablation of one reconcile epoch (one process, data generated once).
+
+    python tools/ablate.py [--pods N] [--config C] [--reps R]
+Prints per-kernel HIP-event times for stage masks ALL, DIFF|RESOLVE, DIFF|QDISC, DIFF.
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch  # noqa: F401  (one HIP runtime)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "kube-dtn_amd"))
+from kdtn import Engine, abi, synth  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--pods", type=int, default=1_000_000)
+ap.add_argument("--config", type=int, default=2)
+ap.add_argument("--reps", type=int, default=10)
+a = ap.parse_args()
+inp = synth.make(a.config, pods_per_shard=a.pods)
+eng = Engine(device=0)
+eng.upload(inp)
+res = {}
+masks = {"ALL": abi.STAGE_ALL, "DIFF|RESOLVE": abi.STAGE_DIFF | abi.STAGE_RESOLVE,
+         "DIFF|QDISC": abi.STAGE_DIFF | abi.STAGE_QDISC, "DIFF": abi.STAGE_DIFF}
+for name, m in masks.items():
+    acc = {}
+    for r in range(a.reps + 2):
+        eng.run(m)
+        eng.sync()
+        if r >= 2:
+            for k, v in eng.kernel_times().items():
+                acc[k] = acc.get(k, 0.0) + v / a.reps
+    res[name] = {k: round(v, 4) for k, v in acc.items()}
+print(json.dumps({"config": a.config, "pods": a.pods, "links": inp.desired.n, "ms": res}, indent=1))
