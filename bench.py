@@ -33,8 +33,8 @@ from kdtn import Engine, abi, comm_unique_id, synth  # noqa: E402
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 
 
-def emit_bytes(inp, n_add: int, n_upd: int, n_del: int) -> float:
-    """Algorithmic bytes of one k_emit launch: per AddLinks entry
+def reconcile_bytes(inp, n_add: int, n_upd: int, n_del: int) -> float:
+    """Algorithmic bytes of one k_reconcile launch: per AddLinks entry
     1 (flag) + 12 (local_ip, local_mac, peer_pod ids) + 8 (uid) + 48 (12 prop ids) + 4 (gap)
     read, 4 (index) + 16 (resolve record) + 72 (qdisc) written = 165 B; per topology
     8 (offsets) + 1 (action) + 12 (ns, src_ip, net_ns) read + 12 (3 batch offsets) written
@@ -43,7 +43,11 @@ def emit_bytes(inp, n_add: int, n_upd: int, n_del: int) -> float:
     per_add = 165.0
     per_upd = 1 + 4 + 12 + 48 + 4 + 8 + 4 + 16 + 72   # flag, target, ids, props, gap, uid, out
     per_del = 1 + 12 + 8 + 4 + 16
-    return per_add * n_add + per_upd * n_upd + per_del * n_del + 33.0 * T + 24.0 * inp.pdict.n
+    # every realised record is compared (key + props) against the desired side when both
+    # lists are non-empty: 88 B per record per side (only when M > 0)
+    cmp = 88.0 * (inp.realised.n + (inp.desired.n if inp.realised.n else 0))
+    return (per_add * n_add + per_upd * n_upd + per_del * n_del + 33.0 * T + 24.0 * inp.pdict.n
+            + cmp)
 
 
 def epoch_bytes(inp, n_add: int, n_upd: int, n_del: int) -> float:
@@ -133,10 +137,11 @@ def main():
     ms_step = elapsed / args.steps * 1e3
     kavg = {k: v / args.steps for k, v in ksum.items()}
     dom = max(kavg, key=kavg.get)
-    ebytes = emit_bytes(inp, counts.n_add, counts.n_upd, counts.n_del)
-    roof = {"kernel": "k_emit", "bound": "hbm", "achieved": ebytes / (kavg["emit"] * 1e-3) / 1e9,
+    ebytes = reconcile_bytes(inp, counts.n_add, counts.n_upd, counts.n_del)
+    roof = {"kernel": "k_reconcile", "bound": "hbm",
+            "achieved": ebytes / (kavg["reconcile"] * 1e-3) / 1e9,
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "traffic": None,
-            "bytes_per_launch": ebytes, "avg_ms": kavg["emit"], "dominant_stage": dom}
+            "bytes_per_launch": ebytes, "avg_ms": kavg["reconcile"], "dominant_stage": dom}
     roof["frac"] = roof["achieved"] / roof["peak"]
     pbytes = epoch_bytes(inp, counts.n_add, counts.n_upd, counts.n_del)
     result = {

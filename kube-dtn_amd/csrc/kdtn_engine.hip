@@ -47,7 +47,8 @@ uint32_t next_pow2(uint64_t x) {
 
 }  // namespace
 
-// Link table storage: all 21 columns carved from one allocation.
+// Link table storage: 20 u32 columns + the i64 uid column carved from one allocation at a
+// fixed column stride, so kernels receive one base pointer per table.
 struct DevLinkStore {
     DevBuf buf;
     uint32_t n = 0;
@@ -60,7 +61,7 @@ struct kdtn_ctx {
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
     // dictionaries
-    DevBuf kd_bytes, kd_offs, kd_flags, pd_bytes, pd_offs, pd_parsed, pd_rate;
+    DevBuf kd_bytes, kd_offs, kd_flags, pd_bytes, pd_offs, pd_pct, pd_dur, pd_rate;
     uint32_t D = 0, P = 0;
     // topologies
     DevBuf t_ns, t_name, t_src, t_netns, t_flags, t_roff, t_noff;
@@ -71,15 +72,16 @@ struct kdtn_ctx {
     DevBuf v_node, v_vni, v_netns, v_keys, v_vals;
     uint32_t V = 0, vni_mask = 0;
     // pods
-    DevBuf pods, pod_keys, pod_vals;
+    DevBuf pods, pod_keys, pod_pay;
     uint32_t slice = 0, pod_total = 0, pod_mask = 0;
     // work
-    DevBuf oflag, otarget, nflag, wg_cnt, wg_base, misc, hscratch, fscratch;
+    DevBuf otarget, sync, misc, hscratch, fscratch;
+    uint32_t nwg = 0;
     // outputs
     DevBuf action, del_off, add_off, upd_off, del_idx, add_idx, upd_idx;
     DevBuf del_res, add_res, upd_res, add_qdisc, upd_qdisc;
     // host-visible counters
-    uint32_t* h_misc = nullptr;   // pinned: [0]=default id, [1]=del, [2]=upd, [3]=add
+    uint32_t* h_misc = nullptr;   // pinned: [0]=default id, [1]=del, [2]=upd, [3]=add, [4]=look-back error
     bool uploaded = false;
     bool ran = false;
     uint32_t last_stages = 0;
@@ -130,6 +132,17 @@ int upload(kdtn_ctx* c, DevBuf& b, const void* src, size_t bytes) {
 
 template <typename T>
 T* dp(DevBuf& b) { return static_cast<T*>(b.p); }
+
+// arenas get 64 B of slack: dictionary slices are staged with 16-B loads
+int upload_arena(kdtn_ctx* c, DevBuf& b, const void* src, size_t bytes) {
+    TRY(ensure(b, bytes + 64));
+    if (bytes) HIP_TRY(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, c->stream));
+    return KDTN_OK;
+}
+
+// k_reconcile sync block: 16 B (ticket, error word) + 3 look-back granules per workgroup,
+// padded to 16 B (memset size % 16 == 0, cdna_hip_programming.md G16)
+size_t sync_bytes(uint32_t nwg) { return align_up(16 + (size_t)nwg * 24, 16); }
 
 int check_strtab(const kdtn_strtab& t, const char* what) {
     if (t.n == 0 || !t.offs || (!t.bytes && t.offs[t.n] != 0)) {
@@ -192,27 +205,21 @@ int upload_links(kdtn_ctx* c, DevLinkStore& s, const kdtn_link_table& L, uint32_
         std::snprintf(g_last_error, sizeof(g_last_error), "%s: missing uid/gap", what);
         return KDTN_EINVAL;
     }
-    const size_t col4 = align_up((size_t)std::max<uint32_t>(n, 1) * 4, 256);
-    const size_t col8 = align_up((size_t)std::max<uint32_t>(n, 1) * 8, 256);
-    const size_t total = col4 * (KDTN_NKEY + KDTN_NPROP + 1) + col8;
+    const uint64_t stride = align_up((size_t)std::max<uint32_t>(n, 1), 64);   // u32 elements
+    const size_t total = (size_t)stride * 4 * (LINK_COLS32 + 2);
     TRY(ensure(s.buf, total));
-    char* base = static_cast<char*>(s.buf.p);
-    size_t off = 0;
-    for (int k = 0; k < KDTN_NKEY; ++k) {
-        s.view.key[k] = reinterpret_cast<const uint32_t*>(base + off);
-        if (n) HIP_TRY(hipMemcpyAsync(base + off, L.key[k], (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
-        off += col4;
+    uint32_t* base = static_cast<uint32_t*>(s.buf.p);
+    auto col = [&](int c) { return base + (size_t)c * stride; };
+    if (n) {
+        for (int k = 0; k < KDTN_NKEY; ++k)
+            HIP_TRY(hipMemcpyAsync(col(COL_KEY0 + k), L.key[k], (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+        for (int k = 0; k < KDTN_NPROP; ++k)
+            HIP_TRY(hipMemcpyAsync(col(COL_PROP0 + k), L.prop[k], (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(col(COL_GAP), L.gap, (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(col(COL_UID), L.uid, (size_t)n * 8, hipMemcpyHostToDevice, c->stream));
     }
-    s.view.uid = reinterpret_cast<const int64_t*>(base + off);
-    if (n) HIP_TRY(hipMemcpyAsync(base + off, L.uid, (size_t)n * 8, hipMemcpyHostToDevice, c->stream));
-    off += col8;
-    for (int k = 0; k < KDTN_NPROP; ++k) {
-        s.view.prop[k] = reinterpret_cast<const uint32_t*>(base + off);
-        if (n) HIP_TRY(hipMemcpyAsync(base + off, L.prop[k], (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
-        off += col4;
-    }
-    s.view.gap = reinterpret_cast<const uint32_t*>(base + off);
-    if (n) HIP_TRY(hipMemcpyAsync(base + off, L.gap, (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+    s.view.base = base;
+    s.view.stride = stride;
     s.view.n = n;
     s.n = n;
     return KDTN_OK;
@@ -326,13 +333,13 @@ void kdtn_destroy(kdtn_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     DevBuf* bufs[] = {&c->kd_bytes, &c->kd_offs, &c->kd_flags, &c->pd_bytes, &c->pd_offs,
-                      &c->pd_parsed, &c->pd_rate, &c->t_ns, &c->t_name, &c->t_src, &c->t_netns,
-                      &c->t_flags, &c->t_roff, &c->t_noff, &c->real.buf, &c->des.buf, &c->v_node,
-                      &c->v_vni, &c->v_netns, &c->v_keys, &c->v_vals, &c->pods, &c->pod_keys,
-                      &c->pod_vals, &c->oflag, &c->otarget, &c->nflag, &c->wg_cnt, &c->wg_base,
-                      &c->misc, &c->hscratch, &c->fscratch, &c->action, &c->del_off, &c->add_off,
-                      &c->upd_off, &c->del_idx, &c->add_idx, &c->upd_idx, &c->del_res,
-                      &c->add_res, &c->upd_res, &c->add_qdisc, &c->upd_qdisc};
+                      &c->pd_pct, &c->pd_dur, &c->pd_rate, &c->t_ns, &c->t_name, &c->t_src,
+                      &c->t_netns, &c->t_flags, &c->t_roff, &c->t_noff, &c->real.buf, &c->des.buf,
+                      &c->v_node, &c->v_vni, &c->v_netns, &c->v_keys, &c->v_vals, &c->pods,
+                      &c->pod_keys, &c->pod_pay, &c->otarget, &c->sync, &c->misc, &c->hscratch,
+                      &c->fscratch, &c->action, &c->del_off, &c->add_off, &c->upd_off, &c->del_idx,
+                      &c->add_idx, &c->upd_idx, &c->del_res, &c->add_res, &c->upd_res,
+                      &c->add_qdisc, &c->upd_qdisc};
     for (DevBuf* b : bufs) release(*b);
     for (int i = 0; i <= kMaxTimers; ++i)
         if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
@@ -381,13 +388,14 @@ int kdtn_epoch_upload(kdtn_ctx* c, const kdtn_epoch_in* in) {
     c->D = D;
     c->P = P;
     c->T = T.n;
-    TRY(upload(c, c->kd_bytes, in->kdict.bytes, in->kdict.offs[D]));
+    TRY(upload_arena(c, c->kd_bytes, in->kdict.bytes, in->kdict.offs[D]));
     TRY(upload(c, c->kd_offs, in->kdict.offs, (size_t)(D + 1) * 4));
     TRY(ensure(c->kd_flags, D));
-    TRY(upload(c, c->pd_bytes, in->pdict.bytes, in->pdict.offs[P]));
+    TRY(upload_arena(c, c->pd_bytes, in->pdict.bytes, in->pdict.offs[P]));
     TRY(upload(c, c->pd_offs, in->pdict.offs, (size_t)(P + 1) * 4));
-    TRY(ensure(c->pd_parsed, (size_t)P * 16));
-    TRY(ensure(c->pd_rate, (size_t)P * 8));
+    TRY(ensure(c->pd_pct, (size_t)P * 4));
+    TRY(ensure(c->pd_dur, (size_t)P * 16));
+    TRY(ensure(c->pd_rate, (size_t)P * 16));
 
     TRY(upload(c, c->t_ns, T.ns, (size_t)T.n * 4));
     TRY(upload(c, c->t_name, T.name, (size_t)T.n * 4));
@@ -414,15 +422,13 @@ int kdtn_epoch_upload(kdtn_ctx* c, const kdtn_epoch_in* in) {
     c->pod_mask = next_pow2((uint64_t)c->pod_total * 2) - 1;
     TRY(ensure(c->pods, (size_t)c->pod_total * 16));
     TRY(ensure(c->pod_keys, (size_t)(c->pod_mask + 1) * 8));
-    TRY(ensure(c->pod_vals, (size_t)(c->pod_mask + 1) * 4));
+    TRY(ensure(c->pod_pay, (size_t)(c->pod_mask + 1) * 16));
 
     const uint32_t M = in->realised.n, N = in->desired.n;
     const uint32_t nwg = (T.n + TPW - 1) / TPW;
-    TRY(ensure(c->oflag, M));
+    c->nwg = nwg;
     TRY(ensure(c->otarget, (size_t)M * 4));
-    TRY(ensure(c->nflag, N));
-    TRY(ensure(c->wg_cnt, (size_t)nwg * 12));
-    TRY(ensure(c->wg_base, (size_t)nwg * 12));
+    TRY(ensure(c->sync, sync_bytes(nwg)));
     TRY(ensure(c->misc, 64));
     TRY(ensure(c->hscratch, ((size_t)M + N) * 4));
     TRY(ensure(c->fscratch, (size_t)M + N));
@@ -453,15 +459,16 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
     hipStream_t s = c->stream;
     (void)hipEventRecord(c->ev[0], s);
     uint32_t* misc = dp<uint32_t>(c->misc);
-    HIP_TRY(hipMemsetAsync(misc, 0xFF, 64, s));   // default id = 0xFFFFFFFF
+    HIP_TRY(hipMemsetAsync(misc, 0xFF, 64, s));                       // default id = 0xFFFFFFFF
+    HIP_TRY(hipMemsetAsync(c->sync.p, 0, sync_bytes(c->nwg), s));    // ticket, error, look-back
 
     const DevTopos T = topo_view(c);
     // dictionaries
     if (c->D) k_kdict_flags<<<nblocks(c->D), BLOCK, 0, s>>>(dp<uint8_t>(c->kd_bytes), dp<uint32_t>(c->kd_offs),
                                                          c->D, dp<uint8_t>(c->kd_flags), misc);
     if (c->P) k_pdict_parse<<<nblocks(c->P), BLOCK, 0, s>>>(dp<uint8_t>(c->pd_bytes), dp<uint32_t>(c->pd_offs),
-                                                         c->P, c->cfg.tick_in_usec, dp<uint4>(c->pd_parsed),
-                                                         dp<uint64_t>(c->pd_rate));
+                                                         c->P, c->cfg.tick_in_usec, dp<uint32_t>(c->pd_pct),
+                                                         dp<uint4>(c->pd_dur), dp<uint4>(c->pd_rate));
     timer_mark(c, "dict_parse");
     const bool resolve = stages & KDTN_STAGE_RESOLVE;
     if (resolve) {
@@ -477,74 +484,75 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
             }
         }
         timer_mark(c, "pods_allgather");
-        HIP_TRY(hipMemsetAsync(c->pod_keys.p, 0xFF, (size_t)(c->pod_mask + 1) * 8, s));
-        HIP_TRY(hipMemsetAsync(c->pod_vals.p, 0xFF, (size_t)(c->pod_mask + 1) * 4, s));
-        if (c->pod_total)
-            k_pod_ht_build<<<nblocks(c->pod_total), BLOCK, 0, s>>>(dp<uint4>(c->pods), c->pod_total,
-                                                                  dp<uint64_t>(c->pod_keys),
-                                                                  dp<uint32_t>(c->pod_vals), c->pod_mask);
+        const size_t pcap = (size_t)c->pod_mask + 1;
+        HIP_TRY(hipMemsetAsync(c->pod_keys.p, 0xFF, pcap * 8, s));
+        HIP_TRY(hipMemsetAsync(c->pod_pay.p, 0xFF, pcap * 16, s));
+        unsigned long long* pkeys = dp<unsigned long long>(c->pod_keys);
+        if (c->pod_total) {
+            k_pod_ht_build<<<nblocks(c->pod_total), BLOCK, 0, s>>>(dp<uint4>(c->pods), c->pod_total, pkeys,
+                                                                  dp<uint4>(c->pod_pay), c->pod_mask);
+            k_pod_ht_finalize<<<nblocks(pcap), BLOCK, 0, s>>>(dp<uint4>(c->pods), pkeys, dp<uint4>(c->pod_pay),
+                                                             (uint32_t)pcap);
+        }
         if (c->V) {
-            HIP_TRY(hipMemsetAsync(c->v_keys.p, 0xFF, (size_t)(c->vni_mask + 1) * 8, s));
-            HIP_TRY(hipMemsetAsync(c->v_vals.p, 0xFF, (size_t)(c->vni_mask + 1) * 4, s));
+            const size_t vcap = (size_t)c->vni_mask + 1;
+            HIP_TRY(hipMemsetAsync(c->v_keys.p, 0xFF, vcap * 8, s));
+            HIP_TRY(hipMemsetAsync(c->v_vals.p, 0xFF, vcap * 4, s));
+            unsigned long long* vkeys = dp<unsigned long long>(c->v_keys);
             k_vni_ht_build<<<nblocks(c->V), BLOCK, 0, s>>>(dp<uint32_t>(c->v_node), dp<int32_t>(c->v_vni), c->V,
-                                                          dp<uint64_t>(c->v_keys), dp<uint32_t>(c->v_vals),
-                                                          c->vni_mask);
+                                                          vkeys, dp<uint32_t>(c->v_vals), c->vni_mask);
+            k_vni_ht_finalize<<<nblocks(vcap), BLOCK, 0, s>>>(vkeys, dp<uint32_t>(c->v_netns),
+                                                             dp<uint32_t>(c->v_vals), (uint32_t)vcap);
         }
         timer_mark(c, "hash_build");
     }
-    const uint32_t nwg = (c->T + TPW - 1) / TPW;
     if (c->T) {
-        DiffOut d;
-        d.oflag = dp<uint8_t>(c->oflag);
-        d.otarget = dp<uint32_t>(c->otarget);
-        d.nflag = dp<uint8_t>(c->nflag);
-        d.action = dp<uint8_t>(c->action);
-        d.wg_cnt = dp<uint32_t>(c->wg_cnt);
-        d.hscratch = dp<uint32_t>(c->hscratch);
-        d.fscratch = dp<uint8_t>(c->fscratch);
-        k_diff<<<nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, d);
-        timer_mark(c, "diff");
-    }
-    k_scan<<<1, 1024, 0, s>>>(dp<uint32_t>(c->wg_cnt), nwg, dp<uint32_t>(c->wg_base), misc + 1, c->T,
-                              dp<uint32_t>(c->del_off), dp<uint32_t>(c->add_off), dp<uint32_t>(c->upd_off));
-    timer_mark(c, "scan");
-    if (c->T) {
-        DevTables tb;
+        DevTables tb{};
         tb.kflags = dp<uint8_t>(c->kd_flags);
-        tb.pparsed = dp<uint4>(c->pd_parsed);
-        tb.prate = dp<uint64_t>(c->pd_rate);
-        tb.pods = dp<uint4>(c->pods);
+        tb.ppct = dp<uint32_t>(c->pd_pct);
+        tb.pdur = dp<uint4>(c->pd_dur);
+        tb.prate = dp<uint4>(c->pd_rate);
         tb.pod_keys = dp<uint64_t>(c->pod_keys);
-        tb.pod_vals = dp<uint32_t>(c->pod_vals);
+        tb.pod_pay = dp<uint4>(c->pod_pay);
         tb.pod_mask = c->pod_mask;
         tb.vni_keys = dp<uint64_t>(c->v_keys);
-        tb.vni_vals = dp<uint32_t>(c->v_vals);
-        tb.vni_netns = dp<uint32_t>(c->v_netns);
+        tb.vni_netns = dp<uint32_t>(c->v_vals);
         tb.vni_mask = c->V ? c->vni_mask : 0;
         tb.default_id = misc;
-        tb.pod_base = c->slice * (uint32_t)c->rank;
         tb.vxlan_base = c->cfg.vxlan_base;
-        EmitOut e;
-        e.del_off = dp<uint32_t>(c->del_off);
-        e.add_off = dp<uint32_t>(c->add_off);
-        e.upd_off = dp<uint32_t>(c->upd_off);
-        e.del_idx = dp<uint32_t>(c->del_idx);
-        e.add_idx = dp<uint32_t>(c->add_idx);
-        e.upd_idx = dp<uint32_t>(c->upd_idx);
-        e.del_res = dp<uint4>(c->del_res);
-        e.add_res = dp<uint4>(c->add_res);
-        e.upd_res = dp<uint4>(c->upd_res);
-        e.add_qdisc = dp<uint2>(c->add_qdisc);
-        e.upd_qdisc = dp<uint2>(c->upd_qdisc);
-        e.wg_base = dp<uint32_t>(c->wg_base);
-        e.stages = stages;
-        k_emit<<<nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, dp<uint8_t>(c->oflag),
-                                     dp<uint32_t>(c->otarget), dp<uint8_t>(c->nflag), dp<uint8_t>(c->action),
-                                     tb, e);
-        timer_mark(c, "emit");
+        RecOut o;
+        o.action = dp<uint8_t>(c->action);
+        o.del_off = dp<uint32_t>(c->del_off);
+        o.add_off = dp<uint32_t>(c->add_off);
+        o.upd_off = dp<uint32_t>(c->upd_off);
+        o.del_idx = dp<uint32_t>(c->del_idx);
+        o.add_idx = dp<uint32_t>(c->add_idx);
+        o.upd_idx = dp<uint32_t>(c->upd_idx);
+        o.del_res = dp<uint4>(c->del_res);
+        o.add_res = dp<uint4>(c->add_res);
+        o.upd_res = dp<uint4>(c->upd_res);
+        o.add_qdisc = dp<uint2>(c->add_qdisc);
+        o.upd_qdisc = dp<uint2>(c->upd_qdisc);
+        o.totals = misc + 1;
+        o.stages = stages;
+        RecWork w;
+        w.sync = dp<uint32_t>(c->sync);
+        w.status = reinterpret_cast<unsigned long long*>(static_cast<char*>(c->sync.p) + 16);
+        w.hscratch = dp<uint32_t>(c->hscratch);
+        w.fscratch = dp<uint8_t>(c->fscratch);
+        w.otarget = dp<uint32_t>(c->otarget);
+        w.nwg = c->nwg;
+        k_reconcile<<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w);
+        timer_mark(c, "reconcile");
+    } else {
+        HIP_TRY(hipMemsetAsync(misc + 1, 0, 12, s));
+        HIP_TRY(hipMemsetAsync(c->del_off.p, 0, 4, s));
+        HIP_TRY(hipMemsetAsync(c->add_off.p, 0, 4, s));
+        HIP_TRY(hipMemsetAsync(c->upd_off.p, 0, 4, s));
     }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(c->h_misc, misc, 16, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(c->h_misc + 4, dp<uint32_t>(c->sync) + 1, 4, hipMemcpyDeviceToHost, s));
     c->ran = true;
     return KDTN_OK;
 }
@@ -553,6 +561,10 @@ int kdtn_epoch_sync(kdtn_ctx* c, kdtn_counts* counts) {
     if (!c || !c->ran) return KDTN_EINVAL;
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->h_misc[4] != 0) {
+        std::snprintf(g_last_error, sizeof(g_last_error), "k_reconcile look-back timed out (0x%x)", c->h_misc[4]);
+        return KDTN_EIO;
+    }
     if (counts) {
         counts->n_del = c->h_misc[1];
         counts->n_upd = c->h_misc[2];
@@ -613,10 +625,11 @@ int kdtn_make_qdiscs(kdtn_ctx* c, const kdtn_strtab* pdict, const kdtn_props_tab
     const uint32_t P = pdict->n, n = props->n;
     for (int k = 0; k < KDTN_NPROP; ++k) TRY(check_ids(props->prop[k], n, P, "props"));
     if (n && !props->gap) return KDTN_EINVAL;
-    TRY(upload(c, c->pd_bytes, pdict->bytes, pdict->offs[P]));
+    TRY(upload_arena(c, c->pd_bytes, pdict->bytes, pdict->offs[P]));
     TRY(upload(c, c->pd_offs, pdict->offs, (size_t)(P + 1) * 4));
-    TRY(ensure(c->pd_parsed, (size_t)P * 16));
-    TRY(ensure(c->pd_rate, (size_t)P * 8));
+    TRY(ensure(c->pd_pct, (size_t)P * 4));
+    TRY(ensure(c->pd_dur, (size_t)P * 16));
+    TRY(ensure(c->pd_rate, (size_t)P * 16));
     // reuse the desired-link store for the property columns
     kdtn_link_table L{};
     L.n = n;
@@ -630,11 +643,13 @@ int kdtn_make_qdiscs(kdtn_ctx* c, const kdtn_strtab* pdict, const kdtn_props_tab
     TRY(ensure(c->add_qdisc, (size_t)std::max<uint32_t>(n, 1) * 72));
     hipStream_t s = c->stream;
     k_pdict_parse<<<nblocks(P), BLOCK, 0, s>>>(dp<uint8_t>(c->pd_bytes), dp<uint32_t>(c->pd_offs), P,
-                                               c->cfg.tick_in_usec, dp<uint4>(c->pd_parsed),
-                                               dp<uint64_t>(c->pd_rate));
-    if (n)
-        k_qdisc_batch<<<nblocks(n), BLOCK, 0, s>>>(c->des.view, dp<uint4>(c->pd_parsed), dp<uint64_t>(c->pd_rate),
-                                                   dp<uint2>(c->add_qdisc));
+                                               c->cfg.tick_in_usec, dp<uint32_t>(c->pd_pct),
+                                               dp<uint4>(c->pd_dur), dp<uint4>(c->pd_rate));
+    DevTables tb{};
+    tb.ppct = dp<uint32_t>(c->pd_pct);
+    tb.pdur = dp<uint4>(c->pd_dur);
+    tb.prate = dp<uint4>(c->pd_rate);
+    if (n) k_qdisc_batch<<<nblocks(n), BLOCK, 0, s>>>(c->des.view, tb, dp<uint2>(c->add_qdisc));
     HIP_TRY(hipGetLastError());
     if (n) HIP_TRY(hipMemcpyAsync(out, c->add_qdisc.p, (size_t)n * 72, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));

@@ -1,21 +1,26 @@
 // kdtn_kernels.h — HIP kernels of one reconcile epoch (gfx950 / CDNA4, wave64).
 //
-// Data layout in HBM (all SoA, one column per field, records grouped by Topology):
-//   link tables  : 7 × u32 key-string ids, i64 uid, 12 × u32 property ids, u32 gap
-//                  (88 B per record per side)
+// Data layout in HBM (struct-of-arrays, records grouped by Topology):
+//   link table   : ONE allocation per side, 21 columns at a fixed stride:
+//                  key[0..6] (u32 kdict ids) | prop[0..11] (u32 pdict ids) | gap (u32) | uid (i64)
+//                  → 88 B per record, one base pointer per table in the kernel arguments
 //   topologies   : u32 ns/name/src_ip/net_ns ids, u8 flags, u32 offsets (T+1) per side
-//   dictionaries : u8 arena + u32 offsets; parsed once per epoch into compact tables
-//                  kflags (u8 per key string) and pparsed (16 B per property string)
+//   dictionaries : u8 arena + u32 offsets, parsed once per epoch (one thread per string,
+//                  arena slices staged through LDS) into compact lookup tables:
+//                  kflags u8/key string; ppct u32 (Percentage2u32 or PCT_ERR);
+//                  pdur {us, ticks, err}; prate {lo, hi, err}
+//   pod table    : pods[g] = {ns, name, src_ip, net_ns|spec_nil<<31} per global pod index,
+//                  open-addressing keys (ns,name) + payload {g, src_ip, net_ns|flag}
+//                  probed together (one round trip per lookup).
 // Kernels (launch order):
-//   k_kdict_flags   MakeVeth/addLink predicates per key string         (D threads)
-//   k_pdict_parse   ParseDuration/ParseFloatPercentage/ParseRate       (P threads)
-//   k_pods_fill     pod-status slice of this rank (16 B per pod)       (slice threads)
+//   k_kdict_flags   MakeVeth / addLink predicates per key string          (D threads)
+//   k_pdict_parse   ParseDuration / ParseFloatPercentage / ParseRate      (P threads)
+//   k_pods_fill     this rank's pod-status slice                          (slice threads)
 //   [RCCL all-gather of the pod-status table when nranks > 1]
-//   k_pod_ht_build  (ns,name) → pod index open-addressing table        (pods threads)
-//   k_vni_ht_build  (node,vni) → VxlanManager entry                    (V threads)
-//   k_diff          gate + CalcDiff per workgroup of TPW topologies, LDS-staged hashes
-//   k_scan          exclusive scan of the per-workgroup batch counts   (1 workgroup)
-//   k_emit          order-preserving compaction into batch lists + resolve + MakeQdiscs
+//   k_pod_ht_build + k_pod_ht_finalize, k_vni_ht_build + k_vni_ht_finalize
+//   k_reconcile     ONE pass per workgroup of TPW topologies: Reconcile gate + CalcDiff in
+//                   LDS, decoupled look-back for the batch bases, then barrier-free emission
+//                   of the batch lists, addLink/delLink/UpdateLinks pure prefix, MakeQdiscs.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -26,8 +31,11 @@
 namespace kdtn {
 
 constexpr int BLOCK = 256;   // 4 waves of 64
-constexpr int TPW = 64;      // topologies per workgroup in k_diff / k_emit (= one wave of lanes)
-constexpr int CAP = 4096;    // LDS window capacity, records (old + new)
+constexpr int TPW = 64;      // topologies per workgroup in k_reconcile (one per lane of wave 0)
+constexpr int CAP = 2048;    // LDS window capacity, records (old + new) per workgroup
+constexpr int STAGE = 8192;  // LDS bytes for staged dictionary slices
+
+constexpr uint32_t PCT_ERR = 0xFFFFFFFEu;   // Percentage2u32 never yields this value
 
 // key-string flags
 enum : uint8_t {
@@ -36,18 +44,24 @@ enum : uint8_t {
     KF_LOCALHOST = 4,   // == "localhost"
     KF_PHYSICAL = 8,    // has prefix "physical/"
 };
-// property-string flags (pparsed.w)
-enum : uint32_t { PF_DUR_ERR = 1, PF_PCT_ERR = 2, PF_RATE_ERR = 4 };
 
-// record flags written by k_diff
-enum : uint8_t { RF_DEL = 1, RF_UPD = 2, RF_ADD = 1 };
+// record flags
+enum : uint8_t { RF_DEL = 1, RF_UPD = 2, RF_ADD = 4 };
+
+// column indices of the link store
+enum { COL_KEY0 = 0, COL_PROP0 = KDTN_NKEY, COL_GAP = KDTN_NKEY + KDTN_NPROP, COL_UID = COL_GAP + 1 };
+constexpr int LINK_COLS32 = COL_UID;   // u32 columns before the i64 uid column
 
 struct DevLinks {
-    const uint32_t* key[KDTN_NKEY];
-    const int64_t* uid;
-    const uint32_t* prop[KDTN_NPROP];
-    const uint32_t* gap;
+    const uint32_t* base;   // column c at base + c*stride; uid (i64) at base + COL_UID*stride
+    uint64_t stride;        // u32 elements per column (multiple of 64)
     uint32_t n;
+    __device__ __forceinline__ uint32_t key(int k, uint32_t i) const { return base[(uint64_t)k * stride + i]; }
+    __device__ __forceinline__ uint32_t prop(int k, uint32_t i) const { return base[(uint64_t)(COL_PROP0 + k) * stride + i]; }
+    __device__ __forceinline__ uint32_t gap(uint32_t i) const { return base[(uint64_t)COL_GAP * stride + i]; }
+    __device__ __forceinline__ int64_t uid(uint32_t i) const {
+        return reinterpret_cast<const int64_t*>(base + (uint64_t)COL_UID * stride)[i];
+    }
 };
 
 struct DevTopos {
@@ -61,65 +75,62 @@ struct DevTopos {
     uint32_t n;
 };
 
-struct DevTables {            // read-only lookup structures of the epoch
-    const uint8_t* kflags;    // [D]
-    const uint4* pparsed;     // [P] {p2u, dur_us, dur_ticks, flags}
-    const uint64_t* prate;    // [P]
-    const uint4* pods;        // [pod_total] {ns, name, src_ip, net_ns | spec_nil<<31}
-    const uint64_t* pod_keys; // [pod_mask+1]
-    const uint32_t* pod_vals;
+struct DevTables {             // read-only lookup structures of the epoch
+    const uint8_t* kflags;     // [D]
+    const uint32_t* ppct;      // [P]
+    const uint4* pdur;         // [P] {us, ticks, err, 0}
+    const uint4* prate;        // [P] {lo, hi, err, 0}
+    const uint64_t* pod_keys;  // [pod_mask+1]
+    const uint4* pod_pay;      // [pod_mask+1] {g, src_ip, net_ns|spec_nil<<31, 0}
     uint32_t pod_mask;
-    const uint64_t* vni_keys; // [vni_mask+1]
-    const uint32_t* vni_vals;
-    const uint32_t* vni_netns;
-    uint32_t vni_mask;
-    const uint32_t* default_id;  // kdict id of "default" (0xFFFFFFFF if absent)
-    uint32_t pod_base;        // global pod index of local topology 0
+    const uint64_t* vni_keys;  // [vni_mask+1]
+    const uint32_t* vni_netns; // [vni_mask+1] net_ns id of the first entry with that key
+    uint32_t vni_mask;         // 0 ⇒ empty table
+    const uint32_t* default_id;
     int32_t vxlan_base;
 };
 
-struct DiffOut {
-    uint8_t* oflag;           // [M]
-    uint32_t* otarget;        // [M] first matching desired index (valid when RF_UPD)
-    uint8_t* nflag;           // [N]
-    uint8_t* action;          // [T]
-    uint32_t* wg_cnt;         // [nwg*3] del, upd, add
-    uint32_t* hscratch;       // [M+N] window hashes for topologies larger than CAP
-    uint8_t* fscratch;        // [M+N] window flags for topologies larger than CAP
-};
-
-struct EmitOut {
+struct RecOut {
+    uint8_t* action;
     uint32_t* del_off;
     uint32_t* add_off;
     uint32_t* upd_off;
     uint32_t* del_idx;
     uint32_t* add_idx;
     uint32_t* upd_idx;
-    uint4* del_res;           // kdtn_resolved as 16 B
+    uint4* del_res;            // kdtn_resolved as 16 B
     uint4* add_res;
     uint4* upd_res;
-    uint2* add_qdisc;         // kdtn_qdisc as 9 × 8 B
+    uint2* add_qdisc;          // kdtn_qdisc as 9 × 8 B
     uint2* upd_qdisc;
-    const uint32_t* wg_base;  // [nwg*3]
+    uint32_t* totals;          // [3] del, upd, add
     uint32_t stages;
+};
+
+struct RecWork {
+    uint32_t* sync;            // [0] ticket, [1] error word, then (16 B aligned) status
+    unsigned long long* status;   // [nwg*3] look-back granules: state<<32 | count
+    uint32_t* hscratch;        // [M+N] window hashes of topologies larger than CAP
+    uint8_t* fscratch;         // [M+N] record flags when a workgroup exceeds CAP
+    uint32_t* otarget;         // [M]   first matching desired index (slow path)
+    uint32_t nwg;
 };
 
 __global__ void k_kdict_flags(const uint8_t* bytes, const uint32_t* offs, uint32_t n,
                               uint8_t* flags, uint32_t* default_id);
 __global__ void k_pdict_parse(const uint8_t* bytes, const uint32_t* offs, uint32_t n, double tick,
-                              uint4* parsed, uint64_t* rate);
+                              uint32_t* ppct, uint4* pdur, uint4* prate);
 __global__ void k_pods_fill(DevTopos T, uint32_t slice, uint32_t rank_base, uint4* pods);
-__global__ void k_pod_ht_build(const uint4* pods, uint32_t total, uint64_t* keys, uint32_t* vals,
-                               uint32_t mask);
-__global__ void k_vni_ht_build(const uint32_t* node, const int32_t* vni, uint32_t n, uint64_t* keys,
-                               uint32_t* vals, uint32_t mask);
-__global__ void k_diff(DevTopos T, DevLinks O, DevLinks N, DiffOut out);
-__global__ void k_scan(const uint32_t* wg_cnt, uint32_t nwg, uint32_t* wg_base, uint32_t* totals,
-                       uint32_t T, uint32_t* del_off, uint32_t* add_off, uint32_t* upd_off);
-__global__ void k_emit(DevTopos T, DevLinks O, DevLinks N, const uint8_t* oflag,
-                       const uint32_t* otarget, const uint8_t* nflag, const uint8_t* action,
-                       DevTables tb, EmitOut out);
-__global__ void k_qdisc_batch(DevLinks props, const uint4* pparsed, const uint64_t* prate,
-                              uint2* out);
+__global__ void k_pod_ht_build(const uint4* pods, uint32_t total, unsigned long long* keys,
+                               uint4* pay, uint32_t mask);
+__global__ void k_pod_ht_finalize(const uint4* pods, const unsigned long long* keys, uint4* pay,
+                                  uint32_t cap);
+__global__ void k_vni_ht_build(const uint32_t* node, const int32_t* vni, uint32_t n,
+                               unsigned long long* keys, uint32_t* vals, uint32_t mask);
+__global__ void k_vni_ht_finalize(const unsigned long long* keys, const uint32_t* net_ns,
+                                  uint32_t* vals, uint32_t cap);
+__global__ void k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out,
+                            RecWork wk);
+__global__ void k_qdisc_batch(DevLinks props, DevTables tb, uint2* out);
 
 }  // namespace kdtn

@@ -32,27 +32,27 @@ KD_INLINE uint64_t hash64(uint64_t x) {
 KD_INLINE uint32_t key_hash(const DevLinks& L, uint32_t i) {
     uint32_t h = 0x9E3779B9u;
 #pragma unroll
-    for (int k = 0; k < KDTN_NKEY; ++k) h = mix32(h, L.key[k][i]);
-    uint64_t u = (uint64_t)L.uid[i];
+    for (int k = 0; k < KDTN_NKEY; ++k) h = mix32(h, L.key(k, i));
+    const uint64_t u = (uint64_t)L.uid(i);
     h = mix32(h, (uint32_t)u);
     h = mix32(h, (uint32_t)(u >> 32));
     return fin32(h);
 }
 
-// EqualWithoutProperties (controllers/topology_controller.go:342-351). Interned ids:
+// EqualWithoutProperties (controllers/topology_controller.go:342-351); interned ids:
 // equal ids ⇔ equal strings.
 KD_INLINE bool key_eq(const DevLinks& A, uint32_t i, const DevLinks& B, uint32_t j) {
-    bool eq = A.uid[i] == B.uid[j];
+    bool eq = A.uid(i) == B.uid(j);
 #pragma unroll
-    for (int k = 0; k < KDTN_NKEY; ++k) eq = eq && (A.key[k][i] == B.key[k][j]);
+    for (int k = 0; k < KDTN_NKEY; ++k) eq = eq && (A.key(k, i) == B.key(k, j));
     return eq;
 }
 
 // reflect.DeepEqual(old.Properties, new.Properties) (:294): 12 strings + Gap.
 KD_INLINE bool props_eq(const DevLinks& A, uint32_t i, const DevLinks& B, uint32_t j) {
-    bool eq = A.gap[i] == B.gap[j];
+    bool eq = A.gap(i) == B.gap(j);
 #pragma unroll
-    for (int k = 0; k < KDTN_NPROP; ++k) eq = eq && (A.prop[k][i] == B.prop[k][j]);
+    for (int k = 0; k < KDTN_NPROP; ++k) eq = eq && (A.prop(k, i) == B.prop(k, j));
     return eq;
 }
 
@@ -71,16 +71,36 @@ KD_INLINE uint64_t lanemask_lt() {
     return lane == 0 ? 0ull : (~0ull >> (64 - lane));
 }
 
+// Stage the arena bytes of strings [s0, s1) into LDS with 16-B coalesced loads.
+// Returns the LDS image base (byte a0 of the arena maps to buf), or nullptr when the
+// slice does not fit (caller then reads the strings from global memory).
+KD_INLINE const uint8_t* stage_slice(const uint8_t* bytes, const uint32_t* offs, uint32_t s0,
+                                     uint32_t s1, uint4* buf, uint32_t* a0_out) {
+    const uint32_t b0 = offs[s0], b1 = offs[s1];
+    const uint32_t a0 = b0 & ~15u;
+    *a0_out = a0;
+    const uint32_t words = (b1 - a0 + 15) >> 4;
+    if (words * 16 > (uint32_t)STAGE) return nullptr;   // uniform across the block
+    const uint4* src = reinterpret_cast<const uint4*>(bytes + a0);
+    for (uint32_t w = threadIdx.x; w < words; w += BLOCK) buf[w] = src[w];
+    return reinterpret_cast<const uint8_t*>(buf);
+}
+
 // ======================================================================================
-// dictionary parsing
+// dictionary parsing (one thread per distinct string)
 // ======================================================================================
 __global__ void __launch_bounds__(BLOCK) k_kdict_flags(const uint8_t* bytes, const uint32_t* offs,
                                                        uint32_t n, uint8_t* flags,
                                                        uint32_t* default_id) {
-    uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    __shared__ uint4 buf[STAGE / 16];
+    const uint32_t s0 = blockIdx.x * BLOCK, s1 = min(s0 + BLOCK, n);
+    uint32_t a0;
+    const uint8_t* img = stage_slice(bytes, offs, s0, s1, buf, &a0);
+    __syncthreads();
+    const uint32_t i = s0 + threadIdx.x;
     if (i >= n) return;
     const uint32_t b = offs[i], len = offs[i + 1] - b;
-    const uint8_t* s = bytes + b;
+    const uint8_t* s = img ? img + (b - a0) : bytes + b;
     uint8_t f = 0;
     if (len) {
         if (!cidr_ok(s, len)) f |= KF_CIDR_BAD;   // common/veth.go:22
@@ -99,26 +119,29 @@ __global__ void __launch_bounds__(BLOCK) k_kdict_flags(const uint8_t* bytes, con
 }
 
 __global__ void __launch_bounds__(BLOCK) k_pdict_parse(const uint8_t* bytes, const uint32_t* offs,
-                                                       uint32_t n, double tick, uint4* parsed,
-                                                       uint64_t* rate) {
-    uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+                                                       uint32_t n, double tick, uint32_t* ppct,
+                                                       uint4* pdur, uint4* prate) {
+    __shared__ uint4 buf[STAGE / 16];
+    const uint32_t s0 = blockIdx.x * BLOCK, s1 = min(s0 + BLOCK, n);
+    uint32_t a0;
+    const uint8_t* img = stage_slice(bytes, offs, s0, s1, buf, &a0);
+    __syncthreads();
+    const uint32_t i = s0 + threadIdx.x;
     if (i >= n) return;
     const uint32_t b = offs[i], len = offs[i + 1] - b;
-    const uint8_t* s = bytes + b;
-    uint32_t fl = 0, dur = 0, ticks = 0, pu = 0;
-    uint64_t r = 0;
-    if (!parse_duration_us(s, len, &dur)) { fl |= PF_DUR_ERR; dur = 0; }
-    else ticks = time2tick(dur, tick);
+    const uint8_t* s = img ? img + (b - a0) : bytes + b;
+    uint32_t dur = 0;
+    const bool dok = parse_duration_us(s, len, &dur);
+    pdur[i] = dok ? make_uint4(dur, time2tick(dur, tick), 0u, 0u) : make_uint4(0u, 0u, 1u, 0u);
     float pct;
-    if (!parse_pct(s, len, &pct)) fl |= PF_PCT_ERR;
-    else pu = p2u(pct);
-    if (!parse_rate(s, len, &r)) { fl |= PF_RATE_ERR; r = 0; }
-    parsed[i] = make_uint4(pu, dur, ticks, fl);
-    rate[i] = r;
+    ppct[i] = parse_pct(s, len, &pct) ? p2u(pct) : PCT_ERR;
+    uint64_t r = 0;
+    const bool rok = parse_rate(s, len, &r);
+    prate[i] = rok ? make_uint4((uint32_t)r, (uint32_t)(r >> 32), 0u, 0u) : make_uint4(0u, 0u, 1u, 0u);
 }
 
 // ======================================================================================
-// pod-status table + hash tables
+// pod-status table + lookup tables
 // ======================================================================================
 __global__ void __launch_bounds__(BLOCK) k_pods_fill(DevTopos T, uint32_t slice, uint32_t rank_base,
                                                      uint4* pods) {
@@ -137,49 +160,70 @@ __global__ void __launch_bounds__(BLOCK) k_pods_fill(DevTopos T, uint32_t slice,
 }
 
 __global__ void __launch_bounds__(BLOCK) k_pod_ht_build(const uint4* pods, uint32_t total,
-                                                        uint64_t* keys, uint32_t* vals,
+                                                        unsigned long long* keys, uint4* pay,
                                                         uint32_t mask) {
-    uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
     if (g >= total) return;
     const uint4 e = pods[g];
     if (e.x == 0xFFFFFFFFu) return;
-    const uint64_t key = ((uint64_t)e.x << 32) | e.y;
+    const unsigned long long key = ((unsigned long long)e.x << 32) | e.y;
     uint32_t h = (uint32_t)hash64(key) & mask;
     for (;;) {
-        unsigned long long prev = atomicCAS((unsigned long long*)&keys[h], ~0ull, (unsigned long long)key);
+        const unsigned long long prev = atomicCAS(&keys[h], ~0ull, key);
         if (prev == ~0ull || prev == key) {
-            atomicMin(&vals[h], g);                 // informer store: first topology wins
+            atomicMin(&pay[h].x, g);                 // informer store: first topology wins
             return;
         }
         h = (h + 1) & mask;
     }
+}
+
+// payload of every occupied slot = the winning pod's status (one gather per pod, so that a
+// lookup needs a single round trip: key and payload are loaded together)
+__global__ void __launch_bounds__(BLOCK) k_pod_ht_finalize(const uint4* pods, const unsigned long long* keys,
+                                                           uint4* pay, uint32_t cap) {
+    const uint32_t h = blockIdx.x * BLOCK + threadIdx.x;
+    if (h >= cap || keys[h] == ~0ull) return;
+    const uint32_t g = pay[h].x;
+    const uint4 e = pods[g];
+    pay[h] = make_uint4(g, e.z, e.w, 0u);
 }
 
 __global__ void __launch_bounds__(BLOCK) k_vni_ht_build(const uint32_t* node, const int32_t* vni,
-                                                        uint32_t n, uint64_t* keys, uint32_t* vals,
-                                                        uint32_t mask) {
-    uint32_t v = blockIdx.x * BLOCK + threadIdx.x;
+                                                        uint32_t n, unsigned long long* keys,
+                                                        uint32_t* vals, uint32_t mask) {
+    const uint32_t v = blockIdx.x * BLOCK + threadIdx.x;
     if (v >= n) return;
-    const uint64_t key = ((uint64_t)node[v] << 32) | (uint32_t)vni[v];
+    const unsigned long long key = ((unsigned long long)node[v] << 32) | (uint32_t)vni[v];
     uint32_t h = (uint32_t)hash64(key) & mask;
     for (;;) {
-        unsigned long long prev = atomicCAS((unsigned long long*)&keys[h], ~0ull, (unsigned long long)key);
+        const unsigned long long prev = atomicCAS(&keys[h], ~0ull, key);
         if (prev == ~0ull || prev == key) {
-            atomicMin(&vals[h], v);
+            atomicMin(&vals[h], v);                  // first entry wins
             return;
         }
         h = (h + 1) & mask;
     }
 }
 
-KD_INLINE uint32_t pod_lookup(const DevTables& tb, uint32_t ns, uint32_t name) {
-    if (ns == 0xFFFFFFFFu) return 0xFFFFFFFFu;
+__global__ void __launch_bounds__(BLOCK) k_vni_ht_finalize(const unsigned long long* keys,
+                                                           const uint32_t* net_ns, uint32_t* vals,
+                                                           uint32_t cap) {
+    const uint32_t h = blockIdx.x * BLOCK + threadIdx.x;
+    if (h >= cap || keys[h] == ~0ull) return;
+    vals[h] = net_ns[vals[h]];
+}
+
+// getPod(name, ns) → {g, src_ip, net_ns|spec_nil} (handler.go:27-41); x = 0xFFFFFFFF on miss
+KD_INLINE uint4 pod_lookup(const DevTables& tb, uint32_t ns, uint32_t name) {
+    if (ns == 0xFFFFFFFFu) return make_uint4(0xFFFFFFFFu, 0, 0, 0);
     const uint64_t key = ((uint64_t)ns << 32) | name;
     uint32_t h = (uint32_t)hash64(key) & tb.pod_mask;
     for (;;) {
         const uint64_t k = tb.pod_keys[h];
-        if (k == key) return tb.pod_vals[h];
-        if (k == ~0ull) return 0xFFFFFFFFu;
+        const uint4 p = tb.pod_pay[h];
+        if (k == key) return p;
+        if (k == ~0ull) return make_uint4(0xFFFFFFFFu, 0, 0, 0);
         h = (h + 1) & tb.pod_mask;
     }
 }
@@ -191,326 +235,85 @@ KD_INLINE uint32_t vni_lookup(const DevTables& tb, uint32_t node, int32_t vni) {
     uint32_t h = (uint32_t)hash64(key) & tb.vni_mask;
     for (;;) {
         const uint64_t k = tb.vni_keys[h];
-        if (k == key) return tb.vni_netns[tb.vni_vals[h]];
+        const uint32_t v = tb.vni_netns[h];
+        if (k == key) return v;
         if (k == ~0ull) return 0xFFFFFFFFu;
         h = (h + 1) & tb.vni_mask;
     }
 }
 
 // ======================================================================================
-// k_diff: Reconcile gate + CalcDiff, one workgroup per TPW consecutive topologies.
+// per-entry outputs: MakeQdiscs, delLink / addLink / UpdateLinks pure prefix
 // ======================================================================================
-struct DiffShared {
-    uint32_t ooff[TPW + 1];
-    uint32_t noff[TPW + 1];
-    uint8_t tflag[TPW];
-    uint8_t dirty[TPW];
-    uint8_t act[TPW];
-    uint32_t cnt[3];
-    uint32_t hash[CAP];
-    uint8_t flag[CAP];
-    uint8_t lt[CAP];
-};
-
-// need element comparisons: both lists non-nil and non-empty
-KD_INLINE bool need_cmp(const DiffShared& sh, int tt) {
-    return (sh.tflag[tt] & (KDTN_TOPO_STATUS_NIL | KDTN_TOPO_SPEC_NIL)) == 0 &&
-           sh.ooff[tt + 1] > sh.ooff[tt] && sh.noff[tt + 1] > sh.noff[tt];
-}
-
-// Process the topologies [tb, te) of this workgroup as one window. hsh/flg hold the
-// window's records (old part first, then new part); lt == nullptr ⇒ single topology.
-__device__ void diff_window(DiffShared& sh, int tb, int te, const DevLinks& O, const DevLinks& N,
-                            uint32_t* hsh, uint8_t* flg, uint8_t* lt, const DiffOut& out,
-                            uint32_t t0) {
-    const uint32_t wo0 = sh.ooff[tb], wo1 = sh.ooff[te];
-    const uint32_t wn0 = sh.noff[tb], wn1 = sh.noff[te];
-    const uint32_t no = wo1 - wo0, nn = wn1 - wn0, tot = no + nn;
-    const int tid = threadIdx.x;
-
-    // A. segment of every record; key hashes where comparisons are needed
-    for (uint32_t r = tid; r < tot; r += BLOCK) {
-        const bool old = r < no;
-        const uint32_t idx = old ? wo0 + r : wn0 + (r - no);
-        int tt = tb;
-        if (lt) {
-            tt = find_seg(old ? sh.ooff : sh.noff, tb, te, idx);
-            lt[r] = (uint8_t)tt;
-        }
-        if (need_cmp(sh, tt)) hsh[r] = old ? key_hash(O, idx) : key_hash(N, idx);
-    }
-    __syncthreads();
-
-    // B. old side: first key-equal new record (CalcDiff :289-303) + positional DeepEqual (:77)
-    for (uint32_t r = tid; r < no; r += BLOCK) {
-        const int tt = lt ? lt[r] : tb;
-        if (!need_cmp(sh, tt)) continue;
-        const uint32_t i = wo0 + r;
-        const uint32_t h = hsh[r];
-        const uint32_t ns_ = sh.noff[tt], ne_ = sh.noff[tt + 1];
-        uint32_t first = 0xFFFFFFFFu;
-        for (uint32_t j = ns_; j < ne_; ++j) {
-            if (hsh[no + (j - wn0)] == h && key_eq(O, i, N, j)) { first = j; break; }
-        }
-        uint8_t f = 0;
-        if (first == 0xFFFFFFFFu) f = RF_DEL;
-        else if (!props_eq(O, i, N, first)) {
-            f = RF_UPD;
-            out.otarget[i] = first;
-        }
-        const uint32_t ko = sh.ooff[tt + 1] - sh.ooff[tt], kn = ne_ - ns_;
-        if (ko == kn) {
-            const uint32_t jp = ns_ + (i - sh.ooff[tt]);
-            bool eq;
-            if (first == jp) eq = (f == 0);
-            else eq = hsh[no + (jp - wn0)] == h && key_eq(O, i, N, jp) && props_eq(O, i, N, jp);
-            if (!eq) sh.dirty[tt] = 1;
-        }
-        flg[r] = f;
-    }
-    // C. new side: any key-equal old record (CalcDiff :305-316)
-    for (uint32_t r = tid; r < nn; r += BLOCK) {
-        const int tt = lt ? lt[no + r] : tb;
-        if (!need_cmp(sh, tt)) continue;
-        const uint32_t j = wn0 + r;
-        const uint32_t h = hsh[no + r];
-        bool found = false;
-        for (uint32_t i = sh.ooff[tt]; i < sh.ooff[tt + 1]; ++i) {
-            if (hsh[i - wo0] == h && key_eq(O, i, N, j)) { found = true; break; }
-        }
-        flg[no + r] = found ? 0 : RF_ADD;
-    }
-    __syncthreads();
-
-    // D. action per topology (topology_controller.go:77-88)
-    for (int tt = tb + tid; tt < te; tt += BLOCK) {
-        const uint8_t tf = sh.tflag[tt];
-        const bool st_nil = tf & KDTN_TOPO_STATUS_NIL, sp_nil = tf & KDTN_TOPO_SPEC_NIL;
-        const uint32_t ko = sh.ooff[tt + 1] - sh.ooff[tt], kn = sh.noff[tt + 1] - sh.noff[tt];
-        uint8_t a;
-        if (st_nil || sp_nil) a = (st_nil && sp_nil) ? KDTN_ACT_SKIP : (st_nil ? KDTN_ACT_CREATED : KDTN_ACT_DIFF);
-        else a = (ko == kn && !sh.dirty[tt]) ? KDTN_ACT_SKIP : KDTN_ACT_DIFF;
-        sh.act[tt] = a;
-        out.action[t0 + tt] = a;
-    }
-    __syncthreads();
-
-    // E. masked flags out + per-workgroup counts
-    uint32_t cd = 0, cu = 0, ca = 0;
-    for (uint32_t base = 0; base < tot; base += BLOCK) {
-        const uint32_t r = base + tid;
-        uint8_t f = 0;
-        bool old = false;
-        if (r < tot) {
-            old = r < no;
-            const int tt = lt ? lt[r] : tb;
-            if (sh.act[tt] == KDTN_ACT_DIFF) {
-                if (need_cmp(sh, tt)) f = flg[r];
-                else f = old ? RF_DEL : RF_ADD;   // the other list is empty
-            }
-            if (old) out.oflag[wo0 + r] = f;
-            else out.nflag[wn0 + (r - no)] = f;
-        }
-        cd += __popcll(__ballot(old && (f & RF_DEL)));
-        cu += __popcll(__ballot(old && (f & RF_UPD)));
-        ca += __popcll(__ballot(!old && r < tot && (f & RF_ADD)));
-    }
-    if ((tid & 63) == 0) {
-        atomicAdd(&sh.cnt[0], cd);
-        atomicAdd(&sh.cnt[1], cu);
-        atomicAdd(&sh.cnt[2], ca);
-    }
-    __syncthreads();
-}
-
-__global__ void __launch_bounds__(BLOCK) k_diff(DevTopos T, DevLinks O, DevLinks N, DiffOut out) {
-    __shared__ DiffShared sh;
-    const uint32_t wg = blockIdx.x;
-    const uint32_t t0 = wg * TPW;
-    const int nt = (int)min((uint32_t)TPW, T.n - t0);
-    const int tid = threadIdx.x;
-    if (tid <= nt) {
-        sh.ooff[tid] = T.real_off[t0 + tid];
-        sh.noff[tid] = T.des_off[t0 + tid];
-    }
-    if (tid < nt) {
-        sh.tflag[tid] = T.flags[t0 + tid];
-        sh.dirty[tid] = 0;
-    }
-    if (tid < 3) sh.cnt[tid] = 0;
-    __syncthreads();
-    const uint32_t total = (sh.ooff[nt] - sh.ooff[0]) + (sh.noff[nt] - sh.noff[0]);
-    if (total <= (uint32_t)CAP) {
-        diff_window(sh, 0, nt, O, N, sh.hash, sh.flag, sh.lt, out, t0);
-    } else {
-        for (int tt = 0; tt < nt; ++tt) {
-            const uint32_t k = (sh.ooff[tt + 1] - sh.ooff[tt]) + (sh.noff[tt + 1] - sh.noff[tt]);
-            if (k <= (uint32_t)CAP) {
-                diff_window(sh, tt, tt + 1, O, N, sh.hash, sh.flag, nullptr, out, t0);
-            } else {
-                const uint32_t gofs = sh.ooff[tt] + sh.noff[tt];
-                diff_window(sh, tt, tt + 1, O, N, out.hscratch + gofs, out.fscratch + gofs, nullptr,
-                            out, t0);
-            }
-        }
-    }
-    if (tid < 3) out.wg_cnt[wg * 3 + tid] = sh.cnt[tid];
-}
-
-// ======================================================================================
-// k_scan: exclusive scan of per-workgroup counts (3 lists), single workgroup of 1024.
-// ======================================================================================
-__global__ void __launch_bounds__(1024) k_scan(const uint32_t* wg_cnt, uint32_t nwg, uint32_t* wg_base,
-                                               uint32_t* totals, uint32_t T, uint32_t* del_off,
-                                               uint32_t* add_off, uint32_t* upd_off) {
-    __shared__ uint32_t s_w[16][3];
-    __shared__ uint32_t s_carry[3];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (tid < 3) s_carry[tid] = 0;
-    __syncthreads();
-    const uint32_t per = 16;                       // items per thread per tile
-    const uint32_t tile = 1024 * per;
-    for (uint32_t t0 = 0; t0 < nwg; t0 += tile) {
-        uint32_t loc[3] = {0, 0, 0};
-        const uint32_t b = t0 + tid * per;
-        for (uint32_t q = 0; q < per; ++q) {
-            const uint32_t w = b + q;
-            if (w < nwg) {
-                loc[0] += wg_cnt[w * 3 + 0];
-                loc[1] += wg_cnt[w * 3 + 1];
-                loc[2] += wg_cnt[w * 3 + 2];
-            }
-        }
-        uint32_t incl[3];
-        for (int c = 0; c < 3; ++c) {
-            uint32_t v = loc[c];
-            for (int d = 1; d < 64; d <<= 1) {
-                uint32_t o = __shfl_up(v, d, 64);
-                if (lane >= d) v += o;
-            }
-            incl[c] = v;
-            if (lane == 63) s_w[wave][c] = v;
-        }
-        __syncthreads();
-        uint32_t run[3];
-        for (int c = 0; c < 3; ++c) {
-            uint32_t pre = s_carry[c];
-            for (int w = 0; w < wave; ++w) pre += s_w[w][c];
-            run[c] = pre + incl[c] - loc[c];
-        }
-        for (uint32_t q = 0; q < per; ++q) {
-            const uint32_t w = b + q;
-            if (w < nwg) {
-                for (int c = 0; c < 3; ++c) {
-                    wg_base[w * 3 + c] = run[c];
-                    run[c] += wg_cnt[w * 3 + c];
-                }
-            }
-        }
-        __syncthreads();
-        if (tid < 3) {
-            uint32_t s = 0;
-            for (int w = 0; w < 16; ++w) s += s_w[w][tid];
-            s_carry[tid] += s;
-        }
-        __syncthreads();
-    }
-    if (tid == 0) {
-        totals[0] = s_carry[0];   // del
-        totals[1] = s_carry[1];   // upd
-        totals[2] = s_carry[2];   // add
-        del_off[T] = s_carry[0];
-        upd_off[T] = s_carry[1];
-        add_off[T] = s_carry[2];
-    }
-}
-
-// ======================================================================================
-// k_emit: batch lists + delLink/addLink/UpdateLinks pure prefix + MakeQdiscs
-// ======================================================================================
-struct EmitShared {
-    uint32_t ooff[TPW + 1];
-    uint32_t noff[TPW + 1];
-    uint8_t act[TPW];
-    uint32_t ns[TPW], src[TPW], netns[TPW];
-    uint32_t cnt[3][TPW];     // del, upd, add per topology
-    uint32_t wsum[BLOCK / 64][2];
-};
-
 // MakeQdiscs over parsed dictionary entries (common/qdisc.go:20-126 + netlink NewNetem)
-KD_INLINE void make_qdisc(const DevLinks& L, uint32_t j, const uint4* pp, const uint64_t* prate,
-                          uint32_t* q /* 18 words */) {
+KD_INLINE void make_qdisc(const DevLinks& L, uint32_t j, const DevTables& tb, uint32_t* q) {
 #pragma unroll
     for (int w = 0; w < 18; ++w) q[w] = 0;
     uint32_t id[KDTN_NPROP];
-    const uint32_t gap = L.gap[j];
+    const uint32_t gap = L.gap(j);
     bool empty = gap == 0;
 #pragma unroll
     for (int k = 0; k < KDTN_NPROP; ++k) {
-        id[k] = L.prop[k][j];
+        id[k] = L.prop(k, j);
         empty = empty && id[k] == 0;             // id 0 == "" (proto.Size == 0, :24)
     }
     if (empty) return;
-    const uint4 lat = pp[id[KDTN_P_LATENCY]];
-    const uint4 lco = pp[id[KDTN_P_LATENCY_CORR]];
-    const uint4 jit = pp[id[KDTN_P_JITTER]];
-    const uint4 los = pp[id[KDTN_P_LOSS]];
-    const uint4 lsc = pp[id[KDTN_P_LOSS_CORR]];
-    const uint4 dup = pp[id[KDTN_P_DUPLICATE]];
-    const uint4 dpc = pp[id[KDTN_P_DUPLICATE_CORR]];
-    const uint4 rop = pp[id[KDTN_P_REORDER_PROB]];
-    const uint4 roc = pp[id[KDTN_P_REORDER_CORR]];
-    const uint4 cop = pp[id[KDTN_P_CORRUPT_PROB]];
-    const uint4 coc = pp[id[KDTN_P_CORRUPT_CORR]];
-    const uint4 rt = pp[id[KDTN_P_RATE]];
+    const uint4 lat = tb.pdur[id[KDTN_P_LATENCY]];
+    const uint4 jit = tb.pdur[id[KDTN_P_JITTER]];
+    const uint4 rt = tb.prate[id[KDTN_P_RATE]];
+    const uint32_t lco = tb.ppct[id[KDTN_P_LATENCY_CORR]];
+    const uint32_t los = tb.ppct[id[KDTN_P_LOSS]];
+    const uint32_t lsc = tb.ppct[id[KDTN_P_LOSS_CORR]];
+    const uint32_t dup = tb.ppct[id[KDTN_P_DUPLICATE]];
+    const uint32_t dpc = tb.ppct[id[KDTN_P_DUPLICATE_CORR]];
+    const uint32_t rop = tb.ppct[id[KDTN_P_REORDER_PROB]];
+    const uint32_t roc = tb.ppct[id[KDTN_P_REORDER_CORR]];
+    const uint32_t cop = tb.ppct[id[KDTN_P_CORRUPT_PROB]];
+    const uint32_t coc = tb.ppct[id[KDTN_P_CORRUPT_CORR]];
     uint32_t err = 0;                            // first failing parse, reference order
-    if (lat.w & PF_DUR_ERR) err = KDTN_E_LATENCY;
-    else if (lco.w & PF_PCT_ERR) err = KDTN_E_LATENCY_CORR;
-    else if (jit.w & PF_DUR_ERR) err = KDTN_E_JITTER;
-    else if (los.w & PF_PCT_ERR) err = KDTN_E_LOSS;
-    else if (lsc.w & PF_PCT_ERR) err = KDTN_E_LOSS_CORR;
-    else if (dup.w & PF_PCT_ERR) err = KDTN_E_DUPLICATE;
-    else if (dpc.w & PF_PCT_ERR) err = KDTN_E_DUPLICATE_CORR;
-    else if (rop.w & PF_PCT_ERR) err = KDTN_E_REORDER_PROB;
-    else if (roc.w & PF_PCT_ERR) err = KDTN_E_REORDER_CORR;
-    else if (cop.w & PF_PCT_ERR) err = KDTN_E_CORRUPT_PROB;
-    else if (coc.w & PF_PCT_ERR) err = KDTN_E_CORRUPT_CORR;
-    else if (rt.w & PF_RATE_ERR) err = KDTN_E_RATE;
+    if (lat.z) err = KDTN_E_LATENCY;
+    else if (lco == PCT_ERR) err = KDTN_E_LATENCY_CORR;
+    else if (jit.z) err = KDTN_E_JITTER;
+    else if (los == PCT_ERR) err = KDTN_E_LOSS;
+    else if (lsc == PCT_ERR) err = KDTN_E_LOSS_CORR;
+    else if (dup == PCT_ERR) err = KDTN_E_DUPLICATE;
+    else if (dpc == PCT_ERR) err = KDTN_E_DUPLICATE_CORR;
+    else if (rop == PCT_ERR) err = KDTN_E_REORDER_PROB;
+    else if (roc == PCT_ERR) err = KDTN_E_REORDER_CORR;
+    else if (cop == PCT_ERR) err = KDTN_E_CORRUPT_PROB;
+    else if (coc == PCT_ERR) err = KDTN_E_CORRUPT_CORR;
+    else if (rt.z) err = KDTN_E_RATE;
     if (err) {
         q[17] = err << 16;                       // byte 70 = err
         return;
     }
     // NewNetem
-    const uint32_t lat_us = lat.y, jit_us = jit.y;
-    const uint32_t loss = los.x, dupl = dup.x;
-    const uint32_t lat_t = lat.z;                // time2Tick(latency)
+    const uint32_t lat_us = lat.x, jit_us = jit.x, lat_t = lat.y;
     q[0] = lat_t;                                                   // latency
-    q[1] = (lat_us > 0 && jit_us > 0) ? lco.x : 0u;                // delay_corr
+    q[1] = (lat_us > 0 && jit_us > 0) ? lco : 0u;                  // delay_corr
     q[2] = 1000u;                                                   // limit
-    q[3] = loss;                                                    // loss
-    q[4] = loss > 0 ? lsc.x : 0u;                                   // loss_corr
-    uint32_t g = gap;
-    if (rop.x > 0 && g == 0) g = 1;
-    q[5] = g;                                                       // gap
-    q[6] = dupl;                                                    // duplicate
-    q[7] = dupl > 0 ? dpc.x : 0u;                                   // duplicate_corr
-    q[8] = lat_t > 0 ? jit.z : jit_us;                              // jitter
-    q[9] = rop.x;
-    q[10] = roc.x;
-    q[11] = cop.x;
-    q[12] = coc.x;
-    const uint64_t rate = prate[id[KDTN_P_RATE]];
+    q[3] = los;                                                     // loss
+    q[4] = los > 0 ? lsc : 0u;                                      // loss_corr
+    q[5] = (rop > 0 && gap == 0) ? 1u : gap;                        // gap
+    q[6] = dup;                                                     // duplicate
+    q[7] = dup > 0 ? dpc : 0u;                                      // duplicate_corr
+    q[8] = lat_t > 0 ? jit.y : jit_us;                              // jitter
+    q[9] = rop;
+    q[10] = roc;
+    q[11] = cop;
+    q[12] = coc;
+    const uint64_t rate = ((uint64_t)rt.y << 32) | rt.x;
     uint32_t has_tbf = 0;
     if (rate != 0) {
         uint32_t burst = (uint32_t)(rate / 250ull);              // getTbfBurst
         if (burst < 5000u) burst = 5000u;
         q[13] = burst;
-        q[14] = (uint32_t)rate;
-        q[15] = (uint32_t)(rate >> 32);
+        q[14] = rt.x;
+        q[15] = rt.y;
         q[16] = 1500u;
         has_tbf = 1;
     }
-    q[17] = 1u | (has_tbf << 8);                 // has_netem, has_tbf, err=0
+    q[17] = 1u | (has_tbf << 8);                 // has_netem, has_tbf, err = 0
 }
 
 KD_INLINE void store_qdisc(uint2* dst, const uint32_t* q) {
@@ -535,206 +338,433 @@ KD_INLINE int32_t vni_of(int32_t base, int64_t uid) {   // common/utils.go:29-31
     return (int32_t)(uint32_t)((uint64_t)(int64_t)base + (uint64_t)uid);
 }
 
-// block-wide exclusive scan of two 0/1 flags; returns chunk totals
-KD_INLINE void block_scan2(EmitShared& sh, uint32_t a, uint32_t b, uint32_t* ea, uint32_t* eb,
-                           uint32_t* ta, uint32_t* tb) {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint64_t ba = __ballot(a), bb = __ballot(b);
-    const uint64_t lt = lanemask_lt();
-    if (lane == 0) {
-        sh.wsum[wave][0] = __popcll(ba);
-        sh.wsum[wave][1] = __popcll(bb);
+struct TopoCtx {       // the local pod of a batch (topology_controller.go:181-186)
+    uint32_t ns, src, netns;
+};
+
+// delLink (handler.go:461-492)
+KD_INLINE void emit_del(const DevLinks& O, uint32_t i, const TopoCtx& tc, const DevTables& tb,
+                        const RecOut& out, uint32_t e, bool res) {
+    out.del_idx[e] = i;
+    if (!res) return;
+    const int32_t vni = vni_of(tb.vxlan_base, O.uid(i));
+    const uint32_t err = veth_err(tb.kflags, O.key(KDTN_K_LOCAL_IP, i), O.key(KDTN_K_LOCAL_MAC, i),
+                                  KDTN_E_VETH_CIDR, KDTN_E_VETH_MAC);
+    uint32_t hit = 0;
+    if (!err) hit = vni_lookup(tb, tc.src, vni) == tc.netns;
+    out.del_res[e] = pack_res(0xFFFFFFFFu, vni, 0, 0, err, hit);
+}
+
+// UpdateLinks entry (handler.go:644-663): MakeVeth(local), then MakeQdiscs
+KD_INLINE void emit_upd(const DevLinks& N, uint32_t j, const DevTables& tb, const RecOut& out,
+                        uint32_t e, bool res, bool qd) {
+    out.upd_idx[e] = j;
+    if (!res && !qd) return;
+    uint32_t q[18];
+    make_qdisc(N, j, tb, q);
+    if (qd) store_qdisc(out.upd_qdisc + (size_t)e * 9, q);
+    if (res) {
+        const int32_t vni = vni_of(tb.vxlan_base, N.uid(j));
+        uint32_t err = veth_err(tb.kflags, N.key(KDTN_K_LOCAL_IP, j), N.key(KDTN_K_LOCAL_MAC, j),
+                                KDTN_E_VETH_CIDR, KDTN_E_VETH_MAC);
+        if (!err) err = (q[17] >> 16) & 0xFF;
+        out.upd_res[e] = pack_res(0xFFFFFFFFu, vni, 0, 0, err, 0);
+    }
+}
+
+// addLink pure prefix (handler.go:316-459) + MakeQdiscs
+KD_INLINE void emit_add(const DevLinks& N, uint32_t j, const TopoCtx& tc, const DevTables& tb,
+                        const RecOut& out, uint32_t e, bool res, bool qd) {
+    out.add_idx[e] = j;
+    if (qd) {
+        uint32_t q[18];
+        make_qdisc(N, j, tb, q);
+        store_qdisc(out.add_qdisc + (size_t)e * 9, q);
+    }
+    if (!res) return;
+    const int32_t vni = vni_of(tb.vxlan_base, N.uid(j));
+    uint32_t err = veth_err(tb.kflags, N.key(KDTN_K_LOCAL_IP, j), N.key(KDTN_K_LOCAL_MAC, j),
+                            KDTN_E_VETH_CIDR, KDTN_E_VETH_MAC);                          // :327
+    uint32_t kind = 0, peer = 0xFFFFFFFFu, vtep = 0, hit = 0;
+    if (!err) {
+        const uint32_t pp = N.key(KDTN_K_PEER_POD, j);
+        const uint8_t pf = tb.kflags[pp];
+        if (pf & KF_LOCALHOST) {
+            kind = KDTN_KIND_MACVLAN;                                                     // :333
+        } else if (pf & KF_PHYSICAL) {
+            kind = KDTN_KIND_PHYSICAL;                                                    // :348
+            vtep = pp;
+            const uint32_t nsx = vni_lookup(tb, tc.src, vni);                           // :177-179
+            hit = (nsx != 0xFFFFFFFFu && nsx != tc.netns);
+        } else {
+            const uint32_t lns = tc.ns == 0 ? *tb.default_id : tc.ns;                   // :29-31
+            const uint4 p = pod_lookup(tb, lns, pp);                                     // :375
+            if (p.x == 0xFFFFFFFFu) {
+                err = KDTN_E_PEER_LOOKUP;
+            } else {
+                peer = p.x;
+                const uint32_t p_src = p.y, p_ns = p.z & 0x7FFFFFFFu;
+                if (p.z & 0x80000000u) {
+                    err = KDTN_E_PEER_NO_LINKS;                                           // :380-384
+                } else if (p_src == 0 || p_ns == 0) {
+                    kind = KDTN_KIND_PEER_DEAD;                                           // :386-395
+                } else if (p_src == tc.src) {
+                    kind = KDTN_KIND_SAME_NODE;                                           // :399-418
+                    err = veth_err(tb.kflags, N.key(KDTN_K_PEER_IP, j), N.key(KDTN_K_PEER_MAC, j),
+                                   KDTN_E_PEER_VETH_CIDR, KDTN_E_PEER_VETH_MAC);
+                } else {
+                    kind = KDTN_KIND_CROSS_NODE;                                          // :419-453
+                    vtep = p_src;
+                    const uint32_t nsx = vni_lookup(tb, p_src, vni);
+                    hit = (nsx != 0xFFFFFFFFu && nsx != p_ns);
+                }
+            }
+        }
+    }
+    out.add_res[e] = pack_res(peer, vni, vtep, kind, err, hit);
+}
+
+// ======================================================================================
+// k_reconcile: one workgroup = TPW consecutive topologies (dynamic ticket order).
+// ======================================================================================
+struct RecShared {
+    uint32_t ooff[TPW + 1];
+    uint32_t noff[TPW + 1];
+    uint8_t tflag[TPW];
+    uint8_t dirty[TPW];
+    uint8_t act[TPW];
+    uint32_t ns[TPW], src[TPW], netns[TPW];
+    uint32_t tcnt[3][TPW];       // per-topology counts (del, upd, add) → exclusive offsets
+    uint32_t wsum[BLOCK / 64][3];
+    uint32_t wtot[3];
+    uint32_t base[3];
+    uint32_t ticket;
+    uint32_t hash[CAP];
+    uint16_t rank[CAP];          // entry position within the workgroup's list
+    uint16_t tgt[CAP];           // upd target, relative to the workgroup's first desired record
+    uint8_t flag[CAP];
+    uint8_t lt[CAP];
+};
+
+// need element comparisons: both lists non-nil and non-empty
+KD_INLINE bool need_cmp(const RecShared& s, int tt) {
+    return (s.tflag[tt] & (KDTN_TOPO_STATUS_NIL | KDTN_TOPO_SPEC_NIL)) == 0 &&
+           s.ooff[tt + 1] > s.ooff[tt] && s.noff[tt + 1] > s.noff[tt];
+}
+
+// Action of topology tt (topology_controller.go:77-88)
+KD_INLINE uint8_t topo_action(const RecShared& s, int tt) {
+    const uint8_t tf = s.tflag[tt];
+    const bool st_nil = tf & KDTN_TOPO_STATUS_NIL, sp_nil = tf & KDTN_TOPO_SPEC_NIL;
+    const uint32_t ko = s.ooff[tt + 1] - s.ooff[tt], kn = s.noff[tt + 1] - s.noff[tt];
+    if (st_nil || sp_nil) return (st_nil && sp_nil) ? KDTN_ACT_SKIP : (st_nil ? KDTN_ACT_CREATED : KDTN_ACT_DIFF);
+    return (ko == kn && !s.dirty[tt]) ? KDTN_ACT_SKIP : KDTN_ACT_DIFF;
+}
+
+// CalcDiff over the topologies [tb, te) of this workgroup as one window (records of the
+// window: old part [0, no) then new part [no, no+nn)). hsh/flg are LDS (lt != nullptr,
+// tgt16 valid) or global scratch (single topology; targets go to wk.otarget). Leaves the
+// MASKED flag of every window record in flg and accumulates per-topology counts.
+__device__ void diff_window(RecShared& s, int tb, int te, const DevLinks& O, const DevLinks& N,
+                            uint32_t* hsh, uint8_t* flg, uint8_t* lt, uint16_t* tgt16,
+                            uint32_t* otarget, uint32_t wn_base) {
+    const uint32_t wo0 = s.ooff[tb], wo1 = s.ooff[te];
+    const uint32_t wn0 = s.noff[tb], wn1 = s.noff[te];
+    const uint32_t no = wo1 - wo0, nn = wn1 - wn0, tot = no + nn;
+    const int tid = threadIdx.x;
+
+    // A. segment of every record; key hashes where comparisons are needed
+    for (uint32_t r = tid; r < tot; r += BLOCK) {
+        const bool old = r < no;
+        const uint32_t idx = old ? wo0 + r : wn0 + (r - no);
+        int tt = tb;
+        if (lt) {
+            tt = find_seg(old ? s.ooff : s.noff, tb, te, idx);
+            lt[r] = (uint8_t)tt;
+        }
+        if (need_cmp(s, tt)) hsh[r] = old ? key_hash(O, idx) : key_hash(N, idx);
     }
     __syncthreads();
-    uint32_t pa = 0, pb = 0, sa = 0, sb = 0;
-#pragma unroll
-    for (int w = 0; w < BLOCK / 64; ++w) {
-        const uint32_t xa = sh.wsum[w][0], xb = sh.wsum[w][1];
-        if (w < wave) { pa += xa; pb += xb; }
-        sa += xa;
-        sb += xb;
+
+    // B. old side: first key-equal new record (CalcDiff :289-303) + positional DeepEqual (:77)
+    for (uint32_t r = tid; r < no; r += BLOCK) {
+        const int tt = lt ? lt[r] : tb;
+        uint8_t f = RF_DEL;
+        if (need_cmp(s, tt)) {
+            const uint32_t i = wo0 + r;
+            const uint32_t h = hsh[r];
+            const uint32_t ns_ = s.noff[tt], ne_ = s.noff[tt + 1];
+            uint32_t first = 0xFFFFFFFFu;
+            for (uint32_t j = ns_; j < ne_; ++j) {
+                if (hsh[no + (j - wn0)] == h && key_eq(O, i, N, j)) { first = j; break; }
+            }
+            if (first != 0xFFFFFFFFu) {
+                if (!props_eq(O, i, N, first)) {
+                    f = RF_UPD;
+                    if (tgt16) tgt16[r] = (uint16_t)(first - wn_base);
+                    else otarget[i] = first;
+                } else {
+                    f = 0;
+                }
+            }
+            const uint32_t ko = s.ooff[tt + 1] - s.ooff[tt], kn = ne_ - ns_;
+            if (ko == kn) {
+                const uint32_t jp = ns_ + (i - s.ooff[tt]);
+                bool eq;
+                if (first == jp) eq = (f == 0);
+                else eq = hsh[no + (jp - wn0)] == h && key_eq(O, i, N, jp) && props_eq(O, i, N, jp);
+                if (!eq) s.dirty[tt] = 1;
+            }
+        }
+        flg[r] = f;
     }
-    *ea = pa + __popcll(ba & lt);
-    *eb = pb + __popcll(bb & lt);
-    *ta = sa;
-    *tb = sb;
+    // C. new side: any key-equal old record (CalcDiff :305-316)
+    for (uint32_t r = tid; r < nn; r += BLOCK) {
+        const int tt = lt ? lt[no + r] : tb;
+        uint8_t f = RF_ADD;
+        if (need_cmp(s, tt)) {
+            const uint32_t j = wn0 + r;
+            const uint32_t h = hsh[no + r];
+            for (uint32_t i = s.ooff[tt]; i < s.ooff[tt + 1]; ++i) {
+                if (hsh[i - wo0] == h && key_eq(O, i, N, j)) { f = 0; break; }
+            }
+        }
+        flg[no + r] = f;
+    }
+    __syncthreads();
+
+    // D. action per topology
+    for (int tt = tb + tid; tt < te; tt += BLOCK) s.act[tt] = topo_action(s, tt);
+    __syncthreads();
+
+    // E. mask by action; per-topology counts
+    for (uint32_t r = tid; r < tot; r += BLOCK) {
+        const int tt = lt ? lt[r] : tb;
+        uint8_t f = flg[r];
+        if (s.act[tt] != KDTN_ACT_DIFF) f = 0;
+        flg[r] = f;
+        if (f & RF_DEL) atomicAdd(&s.tcnt[0][tt], 1u);
+        if (f & RF_UPD) atomicAdd(&s.tcnt[1][tt], 1u);
+        if (f & RF_ADD) atomicAdd(&s.tcnt[2][tt], 1u);
+    }
     __syncthreads();
 }
 
-__global__ void __launch_bounds__(BLOCK) k_emit(DevTopos T, DevLinks O, DevLinks N,
-                                                const uint8_t* oflag, const uint32_t* otarget,
-                                                const uint8_t* nflag, const uint8_t* action,
-                                                DevTables tb, EmitOut out) {
-    __shared__ EmitShared sh;
-    const uint32_t wg = blockIdx.x;
+// Decoupled look-back over the workgroups' list counts (3 lists). Granules are 8-byte
+// {state:32 | count:32} words written and read at agent scope (sc1): the data is its own
+// flag, so no fences are needed (MI355X_MICROARCH.md, Valid forms / R2 granules).
+__device__ void lookback(RecShared& s, const RecWork& wk, uint32_t wg) {
+    const int tid = threadIdx.x;
+    if (tid < 3) {
+        const uint32_t agg = s.wtot[tid];
+        unsigned long long* mine = wk.status + (size_t)wg * 3 + tid;
+        uint32_t prefix = 0;
+        if (wg == 0) {
+            __hip_atomic_store(mine, (2ull << 32) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(mine, (1ull << 32) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            int64_t w = (int64_t)wg - 1;
+            uint32_t spins = 0;
+            while (w >= 0) {
+                const unsigned long long v =
+                    __hip_atomic_load(wk.status + (size_t)w * 3 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t st = (uint32_t)(v >> 32);
+                if (st == 0) {
+                    if (++spins > (1u << 26)) {           // bounded spin: report, never hang
+                        atomicOr(&wk.sync[1], 1u);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                prefix += (uint32_t)v;
+                if (st == 2) break;
+                --w;
+            }
+            __hip_atomic_store(mine, (2ull << 32) | (prefix + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s.base[tid] = prefix;
+    }
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(BLOCK) k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb,
+                                                     RecOut out, RecWork wk) {
+    __shared__ RecShared s;
+    const int tid = threadIdx.x;
+    if (tid == 0) s.ticket = atomicAdd(&wk.sync[0], 1u);    // dispatch order → look-back order
+    __syncthreads();
+    const uint32_t wg = s.ticket;
     const uint32_t t0 = wg * TPW;
     const int nt = (int)min((uint32_t)TPW, T.n - t0);
-    const int tid = threadIdx.x;
     if (tid <= nt) {
-        sh.ooff[tid] = T.real_off[t0 + tid];
-        sh.noff[tid] = T.des_off[t0 + tid];
+        s.ooff[tid] = T.real_off[t0 + tid];
+        s.noff[tid] = T.des_off[t0 + tid];
     }
     if (tid < nt) {
-        sh.act[tid] = action[t0 + tid];
-        sh.ns[tid] = T.ns[t0 + tid];
-        sh.src[tid] = T.src_ip[t0 + tid];
-        sh.netns[tid] = T.net_ns[t0 + tid];
+        s.tflag[tid] = T.flags[t0 + tid];
+        s.dirty[tid] = 0;
+        s.ns[tid] = T.ns[t0 + tid];
+        s.src[tid] = T.src_ip[t0 + tid];
+        s.netns[tid] = T.net_ns[t0 + tid];
     }
     if (tid < TPW) {
-        sh.cnt[0][tid] = 0;
-        sh.cnt[1][tid] = 0;
-        sh.cnt[2][tid] = 0;
+        s.tcnt[0][tid] = 0;
+        s.tcnt[1][tid] = 0;
+        s.tcnt[2][tid] = 0;
     }
     __syncthreads();
-    const uint32_t base_del = out.wg_base[wg * 3 + 0];
-    const uint32_t base_upd = out.wg_base[wg * 3 + 1];
-    const uint32_t base_add = out.wg_base[wg * 3 + 2];
+    const uint32_t o0 = s.ooff[0], o1 = s.ooff[nt], n0 = s.noff[0], n1 = s.noff[nt];
+    const uint32_t no = o1 - o0, nn = n1 - n0, tot = no + nn;
+    const bool fast = tot <= (uint32_t)CAP;
     const bool do_res = out.stages & KDTN_STAGE_RESOLVE;
     const bool do_q = out.stages & KDTN_STAGE_QDISC;
-    const uint32_t dflt = *tb.default_id;
 
-    // ---- old side: DelLinks / UpdateLinks entries, status order ------------------------
-    const uint32_t o0 = sh.ooff[0], o1 = sh.ooff[nt];
-    uint32_t carry_d = 0, carry_u = 0;
-    for (uint32_t c = o0; c < o1; c += BLOCK) {
-        const uint32_t i = c + tid;
-        const uint8_t f = i < o1 ? oflag[i] : 0;
-        const uint32_t isd = f & RF_DEL, isu = (f & RF_UPD) ? 1u : 0u;
-        uint32_t ed, eu, td, tu;
-        block_scan2(sh, isd, isu, &ed, &eu, &td, &tu);
-        if (isd | isu) {
-            const int tt = find_seg(sh.ooff, 0, nt, i);
-            if (isd) {
-                const uint32_t e = base_del + carry_d + ed;
-                out.del_idx[e] = i;
-                atomicAdd(&sh.cnt[0][tt], 1u);
-                if (do_res) {
-                    // delLink (handler.go:461-492)
-                    const int32_t vni = vni_of(tb.vxlan_base, O.uid[i]);
-                    const uint32_t err = veth_err(tb.kflags, O.key[KDTN_K_LOCAL_IP][i],
-                                                  O.key[KDTN_K_LOCAL_MAC][i], KDTN_E_VETH_CIDR,
-                                                  KDTN_E_VETH_MAC);
-                    uint32_t hit = 0;
-                    if (!err) hit = vni_lookup(tb, sh.src[tt], vni) == sh.netns[tt];
-                    out.del_res[e] = pack_res(0xFFFFFFFFu, vni, 0, 0, err, hit);
-                }
-            }
-            if (isu) {
-                const uint32_t e = base_upd + carry_u + eu;
-                const uint32_t j = otarget[i];
-                out.upd_idx[e] = j;
-                atomicAdd(&sh.cnt[1][tt], 1u);
-                uint32_t q[18];
-                if (do_q || do_res) make_qdisc(N, j, tb.pparsed, tb.prate, q);
-                if (do_q) store_qdisc(out.upd_qdisc + (size_t)e * 9, q);
-                if (do_res) {
-                    // UpdateLinks (handler.go:644-663): MakeVeth(local), then MakeQdiscs
-                    const int32_t vni = vni_of(tb.vxlan_base, N.uid[j]);
-                    uint32_t err = veth_err(tb.kflags, N.key[KDTN_K_LOCAL_IP][j],
-                                            N.key[KDTN_K_LOCAL_MAC][j], KDTN_E_VETH_CIDR,
-                                            KDTN_E_VETH_MAC);
-                    if (!err) err = (q[17] >> 16) & 0xFF;
-                    out.upd_res[e] = pack_res(0xFFFFFFFFu, vni, 0, 0, err, 0);
-                }
+    // ---- 1. Reconcile gate + CalcDiff ------------------------------------------------
+    if (fast) {
+        diff_window(s, 0, nt, O, N, s.hash, s.flag, s.lt, s.tgt, wk.otarget, n0);
+    } else {
+        for (int tt = 0; tt < nt; ++tt) {
+            const uint32_t k = (s.ooff[tt + 1] - s.ooff[tt]) + (s.noff[tt + 1] - s.noff[tt]);
+            const uint32_t gofs = s.ooff[tt] + s.noff[tt];
+            if (k <= (uint32_t)CAP) {
+                diff_window(s, tt, tt + 1, O, N, s.hash, s.flag, nullptr, nullptr, wk.otarget, 0);
+                // spill the window's masked flags to global scratch (slow-path emission reads them)
+                for (uint32_t r = tid; r < k; r += BLOCK) wk.fscratch[gofs + r] = s.flag[r];
+                __syncthreads();
+            } else {
+                diff_window(s, tt, tt + 1, O, N, wk.hscratch + gofs, wk.fscratch + gofs, nullptr,
+                            nullptr, wk.otarget, 0);
             }
         }
-        carry_d += td;
-        carry_u += tu;
     }
 
-    // ---- new side: AddLinks entries, spec order -----------------------------------------
-    const uint32_t n0 = sh.noff[0], n1 = sh.noff[nt];
-    uint32_t carry_a = 0;
-    for (uint32_t c = n0; c < n1; c += BLOCK) {
-        const uint32_t j = c + tid;
-        const uint32_t isa = (j < n1) ? (nflag[j] & RF_ADD) : 0u;
-        uint32_t ea, e2, ta, t2;
-        block_scan2(sh, isa, 0u, &ea, &e2, &ta, &t2);
-        if (isa) {
-            const int tt = find_seg(sh.noff, 0, nt, j);
-            const uint32_t e = base_add + carry_a + ea;
-            out.add_idx[e] = j;
-            atomicAdd(&sh.cnt[2][tt], 1u);
-            uint32_t q[18];
-            if (do_q) {
-                make_qdisc(N, j, tb.pparsed, tb.prate, q);
-                store_qdisc(out.add_qdisc + (size_t)e * 9, q);
-            }
-            if (do_res) {
-                // addLink pure prefix (handler.go:316-459)
-                const int32_t vni = vni_of(tb.vxlan_base, N.uid[j]);
-                uint32_t err = veth_err(tb.kflags, N.key[KDTN_K_LOCAL_IP][j],
-                                        N.key[KDTN_K_LOCAL_MAC][j], KDTN_E_VETH_CIDR,
-                                        KDTN_E_VETH_MAC);                       // :327
-                uint32_t kind = 0, peer = 0xFFFFFFFFu, vtep = 0, hit = 0;
-                if (!err) {
-                    const uint32_t pp = N.key[KDTN_K_PEER_POD][j];
-                    const uint8_t pf = tb.kflags[pp];
-                    if (pf & KF_LOCALHOST) {
-                        kind = KDTN_KIND_MACVLAN;                                  // :333
-                    } else if (pf & KF_PHYSICAL) {
-                        kind = KDTN_KIND_PHYSICAL;                                 // :348
-                        vtep = pp;
-                        const uint32_t nsx = vni_lookup(tb, sh.src[tt], vni);    // :177-179
-                        hit = (nsx != 0xFFFFFFFFu && nsx != sh.netns[tt]);
-                    } else {
-                        const uint32_t lns = sh.ns[tt] == 0 ? dflt : sh.ns[tt];  // :29-31
-                        const uint32_t g = pod_lookup(tb, lns, pp);               // :375
-                        if (g == 0xFFFFFFFFu) {
-                            err = KDTN_E_PEER_LOOKUP;
-                        } else {
-                            peer = g;
-                            const uint4 pe = tb.pods[g];
-                            const uint32_t p_src = pe.z, p_ns = pe.w & 0x7FFFFFFFu;
-                            if (pe.w & 0x80000000u) {
-                                err = KDTN_E_PEER_NO_LINKS;                        // :380-384
-                            } else if (p_src == 0 || p_ns == 0) {
-                                kind = KDTN_KIND_PEER_DEAD;                        // :386-395
-                            } else if (p_src == sh.src[tt]) {
-                                kind = KDTN_KIND_SAME_NODE;                        // :399-418
-                                err = veth_err(tb.kflags, N.key[KDTN_K_PEER_IP][j],
-                                               N.key[KDTN_K_PEER_MAC][j], KDTN_E_PEER_VETH_CIDR,
-                                               KDTN_E_PEER_VETH_MAC);
-                            } else {
-                                kind = KDTN_KIND_CROSS_NODE;                       // :419-453
-                                vtep = p_src;
-                                const uint32_t nsx = vni_lookup(tb, p_src, vni);
-                                hit = (nsx != 0xFFFFFFFFu && nsx != p_ns);
-                            }
-                        }
-                    }
-                }
-                out.add_res[e] = pack_res(peer, vni, vtep, kind, err, hit);
-            }
-        }
-        carry_a += ta;
-    }
-    __syncthreads();
-
-    // ---- per-topology batch offsets: wave 0, lane = topology --------------------------
+    // ---- 2. per-topology exclusive offsets within the workgroup, list totals -----------
     if (tid < 64) {
         const int tt = tid;
-        const uint32_t bases[3] = {base_del, base_upd, base_add};
-        uint32_t* offs[3] = {out.del_off, out.upd_off, out.add_off};
         for (int c = 0; c < 3; ++c) {
-            const uint32_t x = (tt < nt) ? sh.cnt[c][tt] : 0u;
+            const uint32_t x = (tt < nt) ? s.tcnt[c][tt] : 0u;
             uint32_t v = x;
             for (int d = 1; d < 64; d <<= 1) {
                 const uint32_t o = __shfl_up(v, d, 64);
                 if (tt >= d) v += o;
             }
-            if (tt < nt) offs[c][t0 + tt] = bases[c] + v - x;
+            s.tcnt[c][tt] = v - x;                   // exclusive
+            if (tt == 63) s.wtot[c] = v;
+        }
+    }
+    // ranks of flagged records within the workgroup's lists (fast path)
+    if (fast) {
+        const uint32_t per = (tot + BLOCK - 1) / BLOCK;
+        const uint32_t r0 = min(tot, tid * per), r1 = min(tot, r0 + per);
+        uint32_t c[3] = {0, 0, 0};
+        for (uint32_t r = r0; r < r1; ++r) {
+            const uint8_t f = s.flag[r];
+            c[0] += (f & RF_DEL) ? 1u : 0u;
+            c[1] += (f & RF_UPD) ? 1u : 0u;
+            c[2] += (f & RF_ADD) ? 1u : 0u;
+        }
+        const int lane = tid & 63, wave = tid >> 6;
+        uint32_t ex[3];
+        for (int k = 0; k < 3; ++k) {
+            uint32_t v = c[k];
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t o = __shfl_up(v, d, 64);
+                if (lane >= d) v += o;
+            }
+            ex[k] = v - c[k];
+            if (lane == 63) s.wsum[wave][k] = v;
+        }
+        __syncthreads();
+        for (int k = 0; k < 3; ++k)
+            for (int w = 0; w < wave; ++w) ex[k] += s.wsum[w][k];
+        for (uint32_t r = r0; r < r1; ++r) {
+            const uint8_t f = s.flag[r];
+            if (f & RF_DEL) s.rank[r] = (uint16_t)ex[0]++;
+            else if (f & RF_UPD) s.rank[r] = (uint16_t)ex[1]++;
+            else if (f & RF_ADD) s.rank[r] = (uint16_t)ex[2]++;
+        }
+    }
+    __syncthreads();
+
+    // ---- 3. batch bases: decoupled look-back -------------------------------------------
+    lookback(s, wk, wg);
+    const uint32_t bd = s.base[0], bu = s.base[1], ba = s.base[2];
+    if (wg == wk.nwg - 1 && tid < 3) {
+        const uint32_t total = s.base[tid] + s.wtot[tid];
+        out.totals[tid] = total;
+        (tid == 0 ? out.del_off : tid == 1 ? out.upd_off : out.add_off)[T.n] = total;
+    }
+    if (tid < nt) {
+        out.action[t0 + tid] = s.act[tid];
+        out.del_off[t0 + tid] = bd + s.tcnt[0][tid];
+        out.upd_off[t0 + tid] = bu + s.tcnt[1][tid];
+        out.add_off[t0 + tid] = ba + s.tcnt[2][tid];
+    }
+
+    // ---- 4. emission -------------------------------------------------------------------
+    if (fast) {
+        for (uint32_t r = tid; r < tot; r += BLOCK) {        // no barriers: full MLP
+            const uint8_t f = s.flag[r];
+            if (!f) continue;
+            const int tt = s.lt[r];
+            const TopoCtx tc{s.ns[tt], s.src[tt], s.netns[tt]};
+            if (f & RF_DEL) emit_del(O, o0 + r, tc, tb, out, bd + s.rank[r], do_res);
+            else if (f & RF_UPD) emit_upd(N, n0 + s.tgt[r], tb, out, bu + s.rank[r], do_res, do_q);
+            else emit_add(N, n0 + (r - no), tc, tb, out, ba + s.rank[r], do_res, do_q);
+        }
+        return;
+    }
+    // slow path: chunked, order-preserving compaction of the flags in global scratch
+    uint32_t cd = 0, cu = 0, ca = 0;
+    const int lane = tid & 63, wave = tid >> 6;
+    for (int side = 0; side < 2; ++side) {
+        const uint32_t lo = side ? n0 : o0, hi = side ? n1 : o1;
+        for (uint32_t c = lo; c < hi; c += BLOCK) {
+            const uint32_t x = c + tid;
+            uint8_t f = 0;
+            if (x < hi) {
+                const uint32_t tt_ = find_seg(side ? s.noff : s.ooff, 0, nt, x);
+                const uint32_t gofs = s.ooff[tt_] + s.noff[tt_];
+                const uint32_t pos = side ? (s.ooff[tt_ + 1] - s.ooff[tt_]) + (x - s.noff[tt_]) : (x - s.ooff[tt_]);
+                f = wk.fscratch[gofs + pos];
+            }
+            const uint64_t b0 = __ballot(f & RF_DEL), b1 = __ballot(f & RF_UPD), b2 = __ballot(f & RF_ADD);
+            if (lane == 0) {
+                s.wsum[wave][0] = __popcll(b0);
+                s.wsum[wave][1] = __popcll(b1);
+                s.wsum[wave][2] = __popcll(b2);
+            }
+            __syncthreads();
+            uint32_t p0 = 0, p1 = 0, p2 = 0, t0_ = 0, t1_ = 0, t2_ = 0;
+            for (int w = 0; w < BLOCK / 64; ++w) {
+                if (w < wave) { p0 += s.wsum[w][0]; p1 += s.wsum[w][1]; p2 += s.wsum[w][2]; }
+                t0_ += s.wsum[w][0];
+                t1_ += s.wsum[w][1];
+                t2_ += s.wsum[w][2];
+            }
+            const uint64_t lt = lanemask_lt();
+            if (f) {
+                const int tt = find_seg(side ? s.noff : s.ooff, 0, nt, x);
+                const TopoCtx tc{s.ns[tt], s.src[tt], s.netns[tt]};
+                if (f & RF_DEL) emit_del(O, x, tc, tb, out, bd + cd + p0 + __popcll(b0 & lt), do_res);
+                else if (f & RF_UPD) emit_upd(N, wk.otarget[x], tb, out, bu + cu + p1 + __popcll(b1 & lt), do_res, do_q);
+                else emit_add(N, x, tc, tb, out, ba + ca + p2 + __popcll(b2 & lt), do_res, do_q);
+            }
+            cd += t0_;
+            cu += t1_;
+            ca += t2_;
+            __syncthreads();
         }
     }
 }
 
 // Standalone MakeQdiscs over a batch of property sets (kdtn_make_qdiscs).
-__global__ void __launch_bounds__(BLOCK) k_qdisc_batch(DevLinks props, const uint4* pparsed,
-                                                       const uint64_t* prate, uint2* out) {
+__global__ void __launch_bounds__(BLOCK) k_qdisc_batch(DevLinks props, DevTables tb, uint2* out) {
     const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
     if (j >= props.n) return;
     uint32_t q[18];
-    make_qdisc(props, j, pparsed, prate, q);
+    make_qdisc(props, j, tb, q);
     store_qdisc(out + (size_t)j * 9, q);
 }
 
