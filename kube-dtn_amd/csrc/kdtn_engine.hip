@@ -69,10 +69,10 @@ struct kdtn_ctx {
     // links
     DevLinkStore real, des;
     // vni table
-    DevBuf v_node, v_vni, v_netns, v_keys, v_vals;
+    DevBuf v_node, v_vni, v_netns, v_ents, v_slots;
     uint32_t V = 0, vni_mask = 0;
     // pods
-    DevBuf pods, pod_keys, pod_pay;
+    DevBuf pods, pod_slots;
     uint32_t slice = 0, pod_total = 0, pod_mask = 0;
     // work
     DevBuf otarget, sync, misc, hscratch, fscratch;
@@ -335,8 +335,8 @@ void kdtn_destroy(kdtn_ctx* c) {
     DevBuf* bufs[] = {&c->kd_bytes, &c->kd_offs, &c->kd_flags, &c->pd_bytes, &c->pd_offs,
                       &c->pd_pct, &c->pd_dur, &c->pd_rate, &c->t_ns, &c->t_name, &c->t_src,
                       &c->t_netns, &c->t_flags, &c->t_roff, &c->t_noff, &c->real.buf, &c->des.buf,
-                      &c->v_node, &c->v_vni, &c->v_netns, &c->v_keys, &c->v_vals, &c->pods,
-                      &c->pod_keys, &c->pod_pay, &c->otarget, &c->sync, &c->misc, &c->hscratch,
+                      &c->v_node, &c->v_vni, &c->v_netns, &c->v_ents, &c->v_slots, &c->pods,
+                      &c->pod_slots, &c->otarget, &c->sync, &c->misc, &c->hscratch,
                       &c->fscratch, &c->action, &c->del_off, &c->add_off, &c->upd_off, &c->del_idx,
                       &c->add_idx, &c->upd_idx, &c->del_res, &c->add_res, &c->upd_res,
                       &c->add_qdisc, &c->upd_qdisc};
@@ -414,15 +414,14 @@ int kdtn_epoch_upload(kdtn_ctx* c, const kdtn_epoch_in* in) {
     TRY(upload(c, c->v_vni, in->vnis.vni, (size_t)V * 4));
     TRY(upload(c, c->v_netns, in->vnis.net_ns, (size_t)V * 4));
     c->vni_mask = V ? next_pow2((uint64_t)V * 2) - 1 : 0;
-    TRY(ensure(c->v_keys, (size_t)(c->vni_mask + 1) * 8));
-    TRY(ensure(c->v_vals, (size_t)(c->vni_mask + 1) * 4));
+    TRY(ensure(c->v_ents, (size_t)V * 16));
+    TRY(ensure(c->v_slots, (size_t)(c->vni_mask + 1) * 4));
 
     c->slice = slice;
     c->pod_total = slice * (uint32_t)c->nranks;
     c->pod_mask = next_pow2((uint64_t)c->pod_total * 2) - 1;
     TRY(ensure(c->pods, (size_t)c->pod_total * 16));
-    TRY(ensure(c->pod_keys, (size_t)(c->pod_mask + 1) * 8));
-    TRY(ensure(c->pod_pay, (size_t)(c->pod_mask + 1) * 16));
+    TRY(ensure(c->pod_slots, (size_t)(c->pod_mask + 1) * 4));
 
     const uint32_t M = in->realised.n, N = in->desired.n;
     const uint32_t nwg = (T.n + TPW - 1) / TPW;
@@ -485,24 +484,17 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         }
         timer_mark(c, "pods_allgather");
         const size_t pcap = (size_t)c->pod_mask + 1;
-        HIP_TRY(hipMemsetAsync(c->pod_keys.p, 0xFF, pcap * 8, s));
-        HIP_TRY(hipMemsetAsync(c->pod_pay.p, 0xFF, pcap * 16, s));
-        unsigned long long* pkeys = dp<unsigned long long>(c->pod_keys);
-        if (c->pod_total) {
-            k_pod_ht_build<<<nblocks(c->pod_total), BLOCK, 0, s>>>(dp<uint4>(c->pods), c->pod_total, pkeys,
-                                                                  dp<uint4>(c->pod_pay), c->pod_mask);
-            k_pod_ht_finalize<<<nblocks(pcap), BLOCK, 0, s>>>(dp<uint4>(c->pods), pkeys, dp<uint4>(c->pod_pay),
-                                                             (uint32_t)pcap);
-        }
+        HIP_TRY(hipMemsetAsync(c->pod_slots.p, 0xFF, pcap * 4, s));
+        if (c->pod_total)
+            k_pod_ht_build<<<nblocks(c->pod_total), BLOCK, 0, s>>>(dp<uint4>(c->pods), c->pod_total,
+                                                                  dp<uint32_t>(c->pod_slots), c->pod_mask);
         if (c->V) {
             const size_t vcap = (size_t)c->vni_mask + 1;
-            HIP_TRY(hipMemsetAsync(c->v_keys.p, 0xFF, vcap * 8, s));
-            HIP_TRY(hipMemsetAsync(c->v_vals.p, 0xFF, vcap * 4, s));
-            unsigned long long* vkeys = dp<unsigned long long>(c->v_keys);
-            k_vni_ht_build<<<nblocks(c->V), BLOCK, 0, s>>>(dp<uint32_t>(c->v_node), dp<int32_t>(c->v_vni), c->V,
-                                                          vkeys, dp<uint32_t>(c->v_vals), c->vni_mask);
-            k_vni_ht_finalize<<<nblocks(vcap), BLOCK, 0, s>>>(vkeys, dp<uint32_t>(c->v_netns),
-                                                             dp<uint32_t>(c->v_vals), (uint32_t)vcap);
+            HIP_TRY(hipMemsetAsync(c->v_slots.p, 0xFF, vcap * 4, s));
+            k_vni_pack<<<nblocks(c->V), BLOCK, 0, s>>>(dp<uint32_t>(c->v_node), dp<int32_t>(c->v_vni),
+                                                      dp<uint32_t>(c->v_netns), c->V, dp<uint4>(c->v_ents));
+            k_vni_ht_build<<<nblocks(c->V), BLOCK, 0, s>>>(dp<uint4>(c->v_ents), c->V, dp<uint32_t>(c->v_slots),
+                                                          c->vni_mask);
         }
         timer_mark(c, "hash_build");
     }
@@ -512,11 +504,11 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         tb.ppct = dp<uint32_t>(c->pd_pct);
         tb.pdur = dp<uint4>(c->pd_dur);
         tb.prate = dp<uint4>(c->pd_rate);
-        tb.pod_keys = dp<uint64_t>(c->pod_keys);
-        tb.pod_pay = dp<uint4>(c->pod_pay);
+        tb.pods = dp<uint4>(c->pods);
+        tb.pod_slots = dp<uint32_t>(c->pod_slots);
         tb.pod_mask = c->pod_mask;
-        tb.vni_keys = dp<uint64_t>(c->v_keys);
-        tb.vni_netns = dp<uint32_t>(c->v_vals);
+        tb.vnis = dp<uint4>(c->v_ents);
+        tb.vni_slots = dp<uint32_t>(c->v_slots);
         tb.vni_mask = c->V ? c->vni_mask : 0;
         tb.default_id = misc;
         tb.vxlan_base = c->cfg.vxlan_base;

@@ -10,14 +10,14 @@
 //                  kflags u8/key string; ppct u32 (Percentage2u32 or PCT_ERR);
 //                  pdur {us, ticks, err}; prate {lo, hi, err}
 //   pod table    : pods[g] = {ns, name, src_ip, net_ns|spec_nil<<31} per global pod index,
-//                  open-addressing keys (ns,name) + payload {g, src_ip, net_ns|flag}
-//                  probed together (one round trip per lookup).
+//                  open-addressing slots of pod indices keyed by (ns, name) (one CAS per
+//                  insert; a lookup = slot gather + pod-entry gather).
 // Kernels (launch order):
 //   k_kdict_flags   MakeVeth / addLink predicates per key string          (D threads)
 //   k_pdict_parse   ParseDuration / ParseFloatPercentage / ParseRate      (P threads)
 //   k_pods_fill     this rank's pod-status slice                          (slice threads)
 //   [RCCL all-gather of the pod-status table when nranks > 1]
-//   k_pod_ht_build + k_pod_ht_finalize, k_vni_ht_build + k_vni_ht_finalize
+//   k_pod_ht_build, k_vni_pack + k_vni_ht_build
 //   k_reconcile     ONE pass per workgroup of TPW topologies: Reconcile gate + CalcDiff in
 //                   LDS, decoupled look-back for the batch bases, then barrier-free emission
 //                   of the batch lists, addLink/delLink/UpdateLinks pure prefix, MakeQdiscs.
@@ -80,11 +80,11 @@ struct DevTables {             // read-only lookup structures of the epoch
     const uint32_t* ppct;      // [P]
     const uint4* pdur;         // [P] {us, ticks, err, 0}
     const uint4* prate;        // [P] {lo, hi, err, 0}
-    const uint64_t* pod_keys;  // [pod_mask+1]
-    const uint4* pod_pay;      // [pod_mask+1] {g, src_ip, net_ns|spec_nil<<31, 0}
+    const uint4* pods;         // [pod_total] {ns, name, src_ip, net_ns|spec_nil<<31}
+    const uint32_t* pod_slots; // [pod_mask+1] smallest pod index with the slot's key
     uint32_t pod_mask;
-    const uint64_t* vni_keys;  // [vni_mask+1]
-    const uint32_t* vni_netns; // [vni_mask+1] net_ns id of the first entry with that key
+    const uint4* vnis;         // [V] {node, vni, net_ns, 0}
+    const uint32_t* vni_slots; // [vni_mask+1]
     uint32_t vni_mask;         // 0 ⇒ empty table
     const uint32_t* default_id;
     int32_t vxlan_base;
@@ -121,14 +121,10 @@ __global__ void k_kdict_flags(const uint8_t* bytes, const uint32_t* offs, uint32
 __global__ void k_pdict_parse(const uint8_t* bytes, const uint32_t* offs, uint32_t n, double tick,
                               uint32_t* ppct, uint4* pdur, uint4* prate);
 __global__ void k_pods_fill(DevTopos T, uint32_t slice, uint32_t rank_base, uint4* pods);
-__global__ void k_pod_ht_build(const uint4* pods, uint32_t total, unsigned long long* keys,
-                               uint4* pay, uint32_t mask);
-__global__ void k_pod_ht_finalize(const uint4* pods, const unsigned long long* keys, uint4* pay,
-                                  uint32_t cap);
-__global__ void k_vni_ht_build(const uint32_t* node, const int32_t* vni, uint32_t n,
-                               unsigned long long* keys, uint32_t* vals, uint32_t mask);
-__global__ void k_vni_ht_finalize(const unsigned long long* keys, const uint32_t* net_ns,
-                                  uint32_t* vals, uint32_t cap);
+__global__ void k_pod_ht_build(const uint4* pods, uint32_t total, uint32_t* slots, uint32_t mask);
+__global__ void k_vni_ht_build(const uint4* ents, uint32_t n, uint32_t* slots, uint32_t mask);
+__global__ void k_vni_pack(const uint32_t* node, const int32_t* vni, const uint32_t* net_ns,
+                           uint32_t n, uint4* ents);
 __global__ void k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out,
                             RecWork wk);
 __global__ void k_qdisc_batch(DevLinks props, DevTables tb, uint2* out);

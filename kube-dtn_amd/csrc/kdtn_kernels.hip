@@ -89,18 +89,7 @@ KD_INLINE const uint8_t* stage_slice(const uint8_t* bytes, const uint32_t* offs,
 // ======================================================================================
 // dictionary parsing (one thread per distinct string)
 // ======================================================================================
-__global__ void __launch_bounds__(BLOCK) k_kdict_flags(const uint8_t* bytes, const uint32_t* offs,
-                                                       uint32_t n, uint8_t* flags,
-                                                       uint32_t* default_id) {
-    __shared__ uint4 buf[STAGE / 16];
-    const uint32_t s0 = blockIdx.x * BLOCK, s1 = min(s0 + BLOCK, n);
-    uint32_t a0;
-    const uint8_t* img = stage_slice(bytes, offs, s0, s1, buf, &a0);
-    __syncthreads();
-    const uint32_t i = s0 + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t b = offs[i], len = offs[i + 1] - b;
-    const uint8_t* s = img ? img + (b - a0) : bytes + b;
+KD_INLINE uint8_t kdict_flags_of(const uint8_t* s, uint32_t len, bool* is_default) {
     uint8_t f = 0;
     if (len) {
         if (!cidr_ok(s, len)) f |= KF_CIDR_BAD;   // common/veth.go:22
@@ -112,10 +101,40 @@ __global__ void __launch_bounds__(BLOCK) k_kdict_flags(const uint8_t* bytes, con
     if (len >= 9 && s[0] == 'p' && s[1] == 'h' && s[2] == 'y' && s[3] == 's' && s[4] == 'i' &&
         s[5] == 'c' && s[6] == 'a' && s[7] == 'l' && s[8] == '/')
         f |= KF_PHYSICAL;                         // handler.go:348
-    if (len == 7 && s[0] == 'd' && s[1] == 'e' && s[2] == 'f' && s[3] == 'a' && s[4] == 'u' &&
-        s[5] == 'l' && s[6] == 't')
-        atomicMin(default_id, i);                 // getPod: ns "" → "default" (handler.go:29-31)
+    *is_default = len == 7 && s[0] == 'd' && s[1] == 'e' && s[2] == 'f' && s[3] == 'a' &&
+                  s[4] == 'u' && s[5] == 'l' && s[6] == 't';
+    return f;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_kdict_flags(const uint8_t* bytes, const uint32_t* offs,
+                                                       uint32_t n, uint8_t* flags,
+                                                       uint32_t* default_id) {
+    __shared__ uint4 buf[STAGE / 16];
+    const uint32_t s0 = blockIdx.x * BLOCK, s1 = min(s0 + BLOCK, n);
+    uint32_t a0;
+    const bool staged = stage_slice(bytes, offs, s0, s1, buf, &a0) != nullptr;
+    __syncthreads();
+    const uint32_t i = s0 + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t b = offs[i], len = offs[i + 1] - b;
+    bool dflt;
+    uint8_t f;
+    if (staged) f = kdict_flags_of(reinterpret_cast<const uint8_t*>(buf) + (b - a0), len, &dflt);
+    else f = kdict_flags_of(bytes + b, len, &dflt);
+    if (dflt) atomicMin(default_id, i);          // getPod: ns "" → "default" (handler.go:29-31)
     flags[i] = f;
+}
+
+KD_INLINE void pdict_parse_one(const uint8_t* s, uint32_t len, double tick, uint32_t* pct_out,
+                               uint4* dur_out, uint4* rate_out) {
+    uint32_t dur = 0;
+    const bool dok = parse_duration_us(s, len, &dur);
+    *dur_out = dok ? make_uint4(dur, time2tick(dur, tick), 0u, 0u) : make_uint4(0u, 0u, 1u, 0u);
+    float pct;
+    *pct_out = parse_pct(s, len, &pct) ? p2u(pct) : PCT_ERR;
+    uint64_t r = 0;
+    const bool rok = parse_rate(s, len, &r);
+    *rate_out = rok ? make_uint4((uint32_t)r, (uint32_t)(r >> 32), 0u, 0u) : make_uint4(0u, 0u, 1u, 0u);
 }
 
 __global__ void __launch_bounds__(BLOCK) k_pdict_parse(const uint8_t* bytes, const uint32_t* offs,
@@ -124,20 +143,18 @@ __global__ void __launch_bounds__(BLOCK) k_pdict_parse(const uint8_t* bytes, con
     __shared__ uint4 buf[STAGE / 16];
     const uint32_t s0 = blockIdx.x * BLOCK, s1 = min(s0 + BLOCK, n);
     uint32_t a0;
-    const uint8_t* img = stage_slice(bytes, offs, s0, s1, buf, &a0);
+    const bool staged = stage_slice(bytes, offs, s0, s1, buf, &a0) != nullptr;
     __syncthreads();
     const uint32_t i = s0 + threadIdx.x;
     if (i >= n) return;
     const uint32_t b = offs[i], len = offs[i + 1] - b;
-    const uint8_t* s = img ? img + (b - a0) : bytes + b;
-    uint32_t dur = 0;
-    const bool dok = parse_duration_us(s, len, &dur);
-    pdur[i] = dok ? make_uint4(dur, time2tick(dur, tick), 0u, 0u) : make_uint4(0u, 0u, 1u, 0u);
-    float pct;
-    ppct[i] = parse_pct(s, len, &pct) ? p2u(pct) : PCT_ERR;
-    uint64_t r = 0;
-    const bool rok = parse_rate(s, len, &r);
-    prate[i] = rok ? make_uint4((uint32_t)r, (uint32_t)(r >> 32), 0u, 0u) : make_uint4(0u, 0u, 1u, 0u);
+    uint32_t pct;
+    uint4 dur, rate;
+    if (staged) pdict_parse_one(reinterpret_cast<const uint8_t*>(buf) + (b - a0), len, tick, &pct, &dur, &rate);
+    else pdict_parse_one(bytes + b, len, tick, &pct, &dur, &rate);
+    ppct[i] = pct;
+    pdur[i] = dur;
+    prate[i] = rate;
 }
 
 // ======================================================================================
@@ -159,71 +176,62 @@ __global__ void __launch_bounds__(BLOCK) k_pods_fill(DevTopos T, uint32_t slice,
     pods[rank_base + t] = e;
 }
 
+// Open addressing over pod indices: a slot holds the smallest index g of the pods with
+// its key (ns, name); the key itself is read from pods[g]. One CAS per insert; a lookup
+// reads the slot, then the pod entry (key check + payload) — 2 dependent 4/16-B gathers.
 __global__ void __launch_bounds__(BLOCK) k_pod_ht_build(const uint4* pods, uint32_t total,
-                                                        unsigned long long* keys, uint4* pay,
-                                                        uint32_t mask) {
+                                                        uint32_t* slots, uint32_t mask) {
     const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
     if (g >= total) return;
     const uint4 e = pods[g];
     if (e.x == 0xFFFFFFFFu) return;
-    const unsigned long long key = ((unsigned long long)e.x << 32) | e.y;
-    uint32_t h = (uint32_t)hash64(key) & mask;
+    uint32_t h = (uint32_t)hash64(((uint64_t)e.x << 32) | e.y) & mask;
     for (;;) {
-        const unsigned long long prev = atomicCAS(&keys[h], ~0ull, key);
-        if (prev == ~0ull || prev == key) {
-            atomicMin(&pay[h].x, g);                 // informer store: first topology wins
+        const uint32_t prev = atomicCAS(&slots[h], 0xFFFFFFFFu, g);
+        if (prev == 0xFFFFFFFFu) return;
+        const uint4 o = pods[prev];
+        if (o.x == e.x && o.y == e.y) {
+            atomicMin(&slots[h], g);                 // informer store: first topology wins
             return;
         }
         h = (h + 1) & mask;
     }
 }
 
-// payload of every occupied slot = the winning pod's status (one gather per pod, so that a
-// lookup needs a single round trip: key and payload are loaded together)
-__global__ void __launch_bounds__(BLOCK) k_pod_ht_finalize(const uint4* pods, const unsigned long long* keys,
-                                                           uint4* pay, uint32_t cap) {
-    const uint32_t h = blockIdx.x * BLOCK + threadIdx.x;
-    if (h >= cap || keys[h] == ~0ull) return;
-    const uint32_t g = pay[h].x;
-    const uint4 e = pods[g];
-    pay[h] = make_uint4(g, e.z, e.w, 0u);
+__global__ void __launch_bounds__(BLOCK) k_vni_pack(const uint32_t* node, const int32_t* vni,
+                                                    const uint32_t* net_ns, uint32_t n, uint4* ents) {
+    const uint32_t v = blockIdx.x * BLOCK + threadIdx.x;
+    if (v < n) ents[v] = make_uint4(node[v], (uint32_t)vni[v], net_ns[v], 0u);
 }
 
-__global__ void __launch_bounds__(BLOCK) k_vni_ht_build(const uint32_t* node, const int32_t* vni,
-                                                        uint32_t n, unsigned long long* keys,
-                                                        uint32_t* vals, uint32_t mask) {
+// VxlanManager snapshot: slots hold the smallest entry index with key (node, vni).
+__global__ void __launch_bounds__(BLOCK) k_vni_ht_build(const uint4* ents, uint32_t n, uint32_t* slots,
+                                                        uint32_t mask) {
     const uint32_t v = blockIdx.x * BLOCK + threadIdx.x;
     if (v >= n) return;
-    const unsigned long long key = ((unsigned long long)node[v] << 32) | (uint32_t)vni[v];
-    uint32_t h = (uint32_t)hash64(key) & mask;
+    const uint4 e = ents[v];
+    uint32_t h = (uint32_t)hash64(((uint64_t)e.x << 32) | e.y) & mask;
     for (;;) {
-        const unsigned long long prev = atomicCAS(&keys[h], ~0ull, key);
-        if (prev == ~0ull || prev == key) {
-            atomicMin(&vals[h], v);                  // first entry wins
+        const uint32_t prev = atomicCAS(&slots[h], 0xFFFFFFFFu, v);
+        if (prev == 0xFFFFFFFFu) return;
+        const uint4 o = ents[prev];
+        if (o.x == e.x && o.y == e.y) {
+            atomicMin(&slots[h], v);                 // first entry wins
             return;
         }
         h = (h + 1) & mask;
     }
-}
-
-__global__ void __launch_bounds__(BLOCK) k_vni_ht_finalize(const unsigned long long* keys,
-                                                           const uint32_t* net_ns, uint32_t* vals,
-                                                           uint32_t cap) {
-    const uint32_t h = blockIdx.x * BLOCK + threadIdx.x;
-    if (h >= cap || keys[h] == ~0ull) return;
-    vals[h] = net_ns[vals[h]];
 }
 
 // getPod(name, ns) → {g, src_ip, net_ns|spec_nil} (handler.go:27-41); x = 0xFFFFFFFF on miss
 KD_INLINE uint4 pod_lookup(const DevTables& tb, uint32_t ns, uint32_t name) {
     if (ns == 0xFFFFFFFFu) return make_uint4(0xFFFFFFFFu, 0, 0, 0);
-    const uint64_t key = ((uint64_t)ns << 32) | name;
-    uint32_t h = (uint32_t)hash64(key) & tb.pod_mask;
+    uint32_t h = (uint32_t)hash64(((uint64_t)ns << 32) | name) & tb.pod_mask;
     for (;;) {
-        const uint64_t k = tb.pod_keys[h];
-        const uint4 p = tb.pod_pay[h];
-        if (k == key) return p;
-        if (k == ~0ull) return make_uint4(0xFFFFFFFFu, 0, 0, 0);
+        const uint32_t g = tb.pod_slots[h];
+        if (g == 0xFFFFFFFFu) return make_uint4(0xFFFFFFFFu, 0, 0, 0);
+        const uint4 e = tb.pods[g];
+        if (e.x == ns && e.y == name) return make_uint4(g, e.z, e.w, 0u);
         h = (h + 1) & tb.pod_mask;
     }
 }
@@ -231,13 +239,12 @@ KD_INLINE uint4 pod_lookup(const DevTables& tb, uint32_t ns, uint32_t name) {
 // VxlanManager.Get(vni) on node `node`: net_ns id, or 0xFFFFFFFF when absent.
 KD_INLINE uint32_t vni_lookup(const DevTables& tb, uint32_t node, int32_t vni) {
     if (tb.vni_mask == 0) return 0xFFFFFFFFu;
-    const uint64_t key = ((uint64_t)node << 32) | (uint32_t)vni;
-    uint32_t h = (uint32_t)hash64(key) & tb.vni_mask;
+    uint32_t h = (uint32_t)hash64(((uint64_t)node << 32) | (uint32_t)vni) & tb.vni_mask;
     for (;;) {
-        const uint64_t k = tb.vni_keys[h];
-        const uint32_t v = tb.vni_netns[h];
-        if (k == key) return v;
-        if (k == ~0ull) return 0xFFFFFFFFu;
+        const uint32_t v = tb.vni_slots[h];
+        if (v == 0xFFFFFFFFu) return 0xFFFFFFFFu;
+        const uint4 e = tb.vnis[v];
+        if (e.x == node && e.y == (uint32_t)vni) return e.z;
         h = (h + 1) & tb.vni_mask;
     }
 }
@@ -550,40 +557,78 @@ __device__ void diff_window(RecShared& s, int tb, int te, const DevLinks& O, con
     __syncthreads();
 }
 
-// Decoupled look-back over the workgroups' list counts (3 lists). Granules are 8-byte
-// {state:32 | count:32} words written and read at agent scope (sc1): the data is its own
-// flag, so no fences are needed (MI355X_MICROARCH.md, Valid forms / R2 granules).
+// Decoupled look-back over the workgroups' list counts (3 lists), one wave, 64
+// predecessors per round trip. Granules are 8-byte {state:32 | count:32} words written and
+// read at agent scope (sc1); the data is its own flag, so no fences are needed
+// (MI355X_MICROARCH.md, Valid forms / R2 granules). state 1 = aggregate, 2 = inclusive.
+KD_INLINE uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
 __device__ void lookback(RecShared& s, const RecWork& wk, uint32_t wg) {
     const int tid = threadIdx.x;
-    if (tid < 3) {
-        const uint32_t agg = s.wtot[tid];
-        unsigned long long* mine = wk.status + (size_t)wg * 3 + tid;
-        uint32_t prefix = 0;
-        if (wg == 0) {
-            __hip_atomic_store(mine, (2ull << 32) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            __hip_atomic_store(mine, (1ull << 32) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            int64_t w = (int64_t)wg - 1;
+    if (tid < 64) {
+        const int lane = tid;
+        unsigned long long* st = wk.status;
+        if (lane < 3)
+            __hip_atomic_store(st + (size_t)wg * 3 + lane,
+                               ((wg == 0 ? 2ull : 1ull) << 32) | s.wtot[lane], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t pre[3] = {0u, 0u, 0u};
+        if (wg > 0) {
+            bool done[3] = {false, false, false};
+            int64_t whi = (int64_t)wg - 1;
             uint32_t spins = 0;
-            while (w >= 0) {
-                const unsigned long long v =
-                    __hip_atomic_load(wk.status + (size_t)w * 3 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const uint32_t st = (uint32_t)(v >> 32);
-                if (st == 0) {
-                    if (++spins > (1u << 26)) {           // bounded spin: report, never hang
-                        atomicOr(&wk.sync[1], 1u);
+            while (!(done[0] && done[1] && done[2])) {
+                const int64_t w = whi - lane;
+                uint64_t g[3] = {0, 0, 0};
+                if (w >= 0) {
+#pragma unroll
+                    for (int c = 0; c < 3; ++c)
+                        if (!done[c])
+                            g[c] = __hip_atomic_load(st + (size_t)w * 3 + c, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+                }
+                bool ready = true;
+                int fi[3];
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    fi[c] = 64;
+                    if (done[c]) continue;
+                    const uint32_t state = (uint32_t)(g[c] >> 32);
+                    const uint64_t inc = __ballot(w >= 0 && state == 2);
+                    const uint64_t nrd = __ballot(w >= 0 && state == 0);
+                    fi[c] = inc ? (__ffsll((long long)inc) - 1) : 64;
+                    const uint64_t upto = fi[c] >= 63 ? ~0ull : ((2ull << fi[c]) - 1);   // lanes 0..fi
+                    if (nrd & upto) ready = false;
+                }
+                if (!ready) {
+                    if (++spins > (1u << 24)) {              // bounded spin: report, never hang
+                        if (lane == 0) atomicOr(&wk.sync[1], 1u);
                         break;
                     }
-                    __builtin_amdgcn_s_sleep(1);
+                    __builtin_amdgcn_s_sleep(2);
                     continue;
                 }
-                prefix += (uint32_t)v;
-                if (st == 2) break;
-                --w;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    if (done[c]) continue;
+                    const uint32_t v = (w >= 0 && lane <= fi[c]) ? (uint32_t)g[c] : 0u;
+                    pre[c] += wave_sum(v);
+                    if (fi[c] < 64) done[c] = true;
+                }
+                whi -= 64;
             }
-            __hip_atomic_store(mine, (2ull << 32) | (prefix + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        s.base[tid] = prefix;
+        if (lane < 3) {
+            const uint32_t p = lane == 0 ? pre[0] : (lane == 1 ? pre[1] : pre[2]);
+            if (wg > 0)
+                __hip_atomic_store(st + (size_t)wg * 3 + lane, (2ull << 32) | (p + s.wtot[lane]),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s.base[lane] = p;
+        }
     }
     __syncthreads();
 }

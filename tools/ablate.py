@@ -18,6 +18,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--pods", type=int, default=1_000_000)
 ap.add_argument("--config", type=int, default=2)
 ap.add_argument("--reps", type=int, default=10)
+ap.add_argument("--masks", default="ALL,DIFF|RESOLVE,DIFF|QDISC,DIFF")
 a = ap.parse_args()
 inp = synth.make(a.config, pods_per_shard=a.pods)
 eng = Engine(device=0)
@@ -26,6 +27,8 @@ res = {}
 masks = {"ALL": abi.STAGE_ALL, "DIFF|RESOLVE": abi.STAGE_DIFF | abi.STAGE_RESOLVE,
          "DIFF|QDISC": abi.STAGE_DIFF | abi.STAGE_QDISC, "DIFF": abi.STAGE_DIFF}
 for name, m in masks.items():
+    if name not in a.masks.split(","):
+        continue
     acc = {}
     for r in range(a.reps + 2):
         eng.run(m)
