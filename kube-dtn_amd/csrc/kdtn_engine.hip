@@ -72,7 +72,7 @@ struct kdtn_ctx {
     DevBuf v_node, v_vni, v_netns, v_ents, v_slots;
     uint32_t V = 0, vni_mask = 0;
     // pods
-    DevBuf pods, pod_slots;
+    DevBuf pods, pod_slots, pod_wide;
     uint32_t slice = 0, pod_total = 0, pod_mask = 0;
     // work
     DevBuf otarget, sync, misc, hscratch, fscratch;
@@ -336,7 +336,7 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->pd_pct, &c->pd_dur, &c->pd_rate, &c->t_ns, &c->t_name, &c->t_src,
                       &c->t_netns, &c->t_flags, &c->t_roff, &c->t_noff, &c->real.buf, &c->des.buf,
                       &c->v_node, &c->v_vni, &c->v_netns, &c->v_ents, &c->v_slots, &c->pods,
-                      &c->pod_slots, &c->otarget, &c->sync, &c->misc, &c->hscratch,
+                      &c->pod_slots, &c->pod_wide, &c->otarget, &c->sync, &c->misc, &c->hscratch,
                       &c->fscratch, &c->action, &c->del_off, &c->add_off, &c->upd_off, &c->del_idx,
                       &c->add_idx, &c->upd_idx, &c->del_res, &c->add_res, &c->upd_res,
                       &c->add_qdisc, &c->upd_qdisc};
@@ -422,6 +422,7 @@ int kdtn_epoch_upload(kdtn_ctx* c, const kdtn_epoch_in* in) {
     c->pod_mask = next_pow2((uint64_t)c->pod_total * 2) - 1;
     TRY(ensure(c->pods, (size_t)c->pod_total * 16));
     TRY(ensure(c->pod_slots, (size_t)(c->pod_mask + 1) * 4));
+    TRY(ensure(c->pod_wide, (size_t)(c->pod_mask + 1) * 16));
 
     const uint32_t M = in->realised.n, N = in->desired.n;
     const uint32_t nwg = (T.n + TPW - 1) / TPW;
@@ -488,6 +489,8 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         if (c->pod_total)
             k_pod_ht_build<<<nblocks(c->pod_total), BLOCK, 0, s>>>(dp<uint4>(c->pods), c->pod_total,
                                                                   dp<uint32_t>(c->pod_slots), c->pod_mask);
+        k_pod_ht_expand<<<nblocks(pcap), BLOCK, 0, s>>>(dp<uint4>(c->pods), dp<uint32_t>(c->pod_slots),
+                                                       dp<uint4>(c->pod_wide), (uint32_t)pcap);
         if (c->V) {
             const size_t vcap = (size_t)c->vni_mask + 1;
             HIP_TRY(hipMemsetAsync(c->v_slots.p, 0xFF, vcap * 4, s));
@@ -505,7 +508,7 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         tb.pdur = dp<uint4>(c->pd_dur);
         tb.prate = dp<uint4>(c->pd_rate);
         tb.pods = dp<uint4>(c->pods);
-        tb.pod_slots = dp<uint32_t>(c->pod_slots);
+        tb.pod_wide = dp<uint4>(c->pod_wide);
         tb.pod_mask = c->pod_mask;
         tb.vnis = dp<uint4>(c->v_ents);
         tb.vni_slots = dp<uint32_t>(c->v_slots);
@@ -534,7 +537,16 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         w.fscratch = dp<uint8_t>(c->fscratch);
         w.otarget = dp<uint32_t>(c->otarget);
         w.nwg = c->nwg;
-        k_reconcile<<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w);
+        int variant = DEFAULT_VARIANT;
+        if (const char* ev = std::getenv("KDTN_VARIANT")) variant = std::atoi(ev);   // profiling A/B
+        switch (variant) {
+        case 0: k_reconcile<0><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
+        case 2: k_reconcile<2><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
+        case 3: k_reconcile<3><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
+        case 4: k_reconcile<4><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
+        case 5: k_reconcile<5><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
+        default: k_reconcile<1><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
+        }
         timer_mark(c, "reconcile");
     } else {
         HIP_TRY(hipMemsetAsync(misc + 1, 0, 12, s));

@@ -11,7 +11,7 @@
 //                  pdur {us, ticks, err}; prate {lo, hi, err}
 //   pod table    : pods[g] = {ns, name, src_ip, net_ns|spec_nil<<31} per global pod index,
 //                  open-addressing slots of pod indices keyed by (ns, name) (one CAS per
-//                  insert; a lookup = slot gather + pod-entry gather).
+//                  insert), expanded into 16-B self-contained slots: a lookup is ONE gather.
 // Kernels (launch order):
 //   k_kdict_flags   MakeVeth / addLink predicates per key string          (D threads)
 //   k_pdict_parse   ParseDuration / ParseFloatPercentage / ParseRate      (P threads)
@@ -62,7 +62,33 @@ struct DevLinks {
     __device__ __forceinline__ int64_t uid(uint32_t i) const {
         return reinterpret_cast<const int64_t*>(base + (uint64_t)COL_UID * stride)[i];
     }
+    // streaming (read-once) forms; NT = non-temporal, so they do not evict lookup tables
+    template <bool NT> __device__ __forceinline__ uint32_t ld32(uint64_t off) const {
+        if constexpr (NT) return __builtin_nontemporal_load(base + off);
+        else return base[off];
+    }
+    template <bool NT> __device__ __forceinline__ uint32_t key_s(int k, uint32_t i) const {
+        return ld32<NT>((uint64_t)k * stride + i);
+    }
+    template <bool NT> __device__ __forceinline__ uint32_t prop_s(int k, uint32_t i) const {
+        return ld32<NT>((uint64_t)(COL_PROP0 + k) * stride + i);
+    }
+    template <bool NT> __device__ __forceinline__ uint32_t gap_s(uint32_t i) const {
+        return ld32<NT>((uint64_t)COL_GAP * stride + i);
+    }
+    template <bool NT> __device__ __forceinline__ int64_t uid_s(uint32_t i) const {
+        const int64_t* p = reinterpret_cast<const int64_t*>(base + (uint64_t)COL_UID * stride) + i;
+        if constexpr (NT) return __builtin_nontemporal_load(p);
+        else return *p;
+    }
 };
+
+// Emission variants (A/B in one binary; kdtn_epoch_run picks KDTN_VARIANT or the default):
+//   bit 0: non-temporal streaming loads of link columns
+//   bit 1: non-temporal output stores
+//   bit 2: (profiling) compute MakeQdiscs but do not store it
+constexpr int VAR_NT_LOAD = 1, VAR_NT_STORE = 2, VAR_NO_QSTORE = 4;
+constexpr int DEFAULT_VARIANT = VAR_NT_LOAD;
 
 struct DevTopos {
     const uint32_t* ns;
@@ -81,7 +107,7 @@ struct DevTables {             // read-only lookup structures of the epoch
     const uint4* pdur;         // [P] {us, ticks, err, 0}
     const uint4* prate;        // [P] {lo, hi, err, 0}
     const uint4* pods;         // [pod_total] {ns, name, src_ip, net_ns|spec_nil<<31}
-    const uint32_t* pod_slots; // [pod_mask+1] smallest pod index with the slot's key
+    const uint4* pod_wide;     // [pod_mask+1] {ns, name, g|spec_nil<<31, src_ip|netns_empty<<31}
     uint32_t pod_mask;
     const uint4* vnis;         // [V] {node, vni, net_ns, 0}
     const uint32_t* vni_slots; // [vni_mask+1]
@@ -122,9 +148,11 @@ __global__ void k_pdict_parse(const uint8_t* bytes, const uint32_t* offs, uint32
                               uint32_t* ppct, uint4* pdur, uint4* prate);
 __global__ void k_pods_fill(DevTopos T, uint32_t slice, uint32_t rank_base, uint4* pods);
 __global__ void k_pod_ht_build(const uint4* pods, uint32_t total, uint32_t* slots, uint32_t mask);
+__global__ void k_pod_ht_expand(const uint4* pods, const uint32_t* slots, uint4* wide, uint32_t cap);
 __global__ void k_vni_ht_build(const uint4* ents, uint32_t n, uint32_t* slots, uint32_t mask);
 __global__ void k_vni_pack(const uint32_t* node, const int32_t* vni, const uint32_t* net_ns,
                            uint32_t n, uint4* ents);
+template <int V>
 __global__ void k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out,
                             RecWork wk);
 __global__ void k_qdisc_batch(DevLinks props, DevTables tb, uint2* out);

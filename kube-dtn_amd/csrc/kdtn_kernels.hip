@@ -204,6 +204,21 @@ __global__ void __launch_bounds__(BLOCK) k_vni_pack(const uint32_t* node, const 
     if (v < n) ents[v] = make_uint4(node[v], (uint32_t)vni[v], net_ns[v], 0u);
 }
 
+// Expand the slot table into 16-B self-contained slots {ns, name, g|spec_nil<<31,
+// src_ip|netns_empty<<31}: a lookup is then ONE random 16-B gather (key + payload).
+__global__ void __launch_bounds__(BLOCK) k_pod_ht_expand(const uint4* pods, const uint32_t* slots,
+                                                         uint4* wide, uint32_t cap) {
+    const uint32_t h = blockIdx.x * BLOCK + threadIdx.x;
+    if (h >= cap) return;
+    const uint32_t g = slots[h];
+    uint4 w = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+    if (g != 0xFFFFFFFFu) {
+        const uint4 e = pods[g];
+        w = make_uint4(e.x, e.y, g | (e.w & 0x80000000u), e.z | ((e.w & 0x7FFFFFFFu) == 0 ? 0x80000000u : 0u));
+    }
+    wide[h] = w;
+}
+
 // VxlanManager snapshot: slots hold the smallest entry index with key (node, vni).
 __global__ void __launch_bounds__(BLOCK) k_vni_ht_build(const uint4* ents, uint32_t n, uint32_t* slots,
                                                         uint32_t mask) {
@@ -223,15 +238,15 @@ __global__ void __launch_bounds__(BLOCK) k_vni_ht_build(const uint4* ents, uint3
     }
 }
 
-// getPod(name, ns) → {g, src_ip, net_ns|spec_nil} (handler.go:27-41); x = 0xFFFFFFFF on miss
-KD_INLINE uint4 pod_lookup(const DevTables& tb, uint32_t ns, uint32_t name) {
-    if (ns == 0xFFFFFFFFu) return make_uint4(0xFFFFFFFFu, 0, 0, 0);
+// getPod(name, ns) (handler.go:27-41) → {g|spec_nil<<31, src_ip|netns_empty<<31}; x = 0xFFFFFFFF
+// on a miss. Empty slots hold all-ones, which no (ns, name) key equals (ids < 2^31).
+KD_INLINE uint2 pod_lookup(const DevTables& tb, uint32_t ns, uint32_t name) {
+    if (ns == 0xFFFFFFFFu) return make_uint2(0xFFFFFFFFu, 0u);
     uint32_t h = (uint32_t)hash64(((uint64_t)ns << 32) | name) & tb.pod_mask;
     for (;;) {
-        const uint32_t g = tb.pod_slots[h];
-        if (g == 0xFFFFFFFFu) return make_uint4(0xFFFFFFFFu, 0, 0, 0);
-        const uint4 e = tb.pods[g];
-        if (e.x == ns && e.y == name) return make_uint4(g, e.z, e.w, 0u);
+        const uint4 w = tb.pod_wide[h];
+        if (w.x == ns && w.y == name) return make_uint2(w.z, w.w);
+        if (w.x == 0xFFFFFFFFu) return make_uint2(0xFFFFFFFFu, 0u);
         h = (h + 1) & tb.pod_mask;
     }
 }
@@ -253,15 +268,16 @@ KD_INLINE uint32_t vni_lookup(const DevTables& tb, uint32_t node, int32_t vni) {
 // per-entry outputs: MakeQdiscs, delLink / addLink / UpdateLinks pure prefix
 // ======================================================================================
 // MakeQdiscs over parsed dictionary entries (common/qdisc.go:20-126 + netlink NewNetem)
+template <bool NTL>
 KD_INLINE void make_qdisc(const DevLinks& L, uint32_t j, const DevTables& tb, uint32_t* q) {
 #pragma unroll
     for (int w = 0; w < 18; ++w) q[w] = 0;
     uint32_t id[KDTN_NPROP];
-    const uint32_t gap = L.gap(j);
+    const uint32_t gap = L.gap_s<NTL>(j);
     bool empty = gap == 0;
 #pragma unroll
     for (int k = 0; k < KDTN_NPROP; ++k) {
-        id[k] = L.prop(k, j);
+        id[k] = L.prop_s<NTL>(k, j);
         empty = empty && id[k] == 0;             // id 0 == "" (proto.Size == 0, :24)
     }
     if (empty) return;
@@ -323,9 +339,45 @@ KD_INLINE void make_qdisc(const DevLinks& L, uint32_t j, const DevTables& tb, ui
     q[17] = 1u | (has_tbf << 8);                 // has_netem, has_tbf, err = 0
 }
 
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <int V>
 KD_INLINE void store_qdisc(uint2* dst, const uint32_t* q) {
+    if constexpr ((V & VAR_NO_QSTORE) != 0) {
 #pragma unroll
-    for (int w = 0; w < 9; ++w) dst[w] = make_uint2(q[2 * w], q[2 * w + 1]);
+        for (int w = 0; w < 18; ++w) asm volatile("" ::"v"(q[w]));   // keep the work alive
+        return;
+    }
+    u32x2* d = reinterpret_cast<u32x2*>(dst);
+#pragma unroll
+    for (int w = 0; w < 9; ++w) {
+        u32x2 v;
+        v.x = q[2 * w];
+        v.y = q[2 * w + 1];
+        if constexpr ((V & VAR_NT_STORE) != 0) __builtin_nontemporal_store(v, d + w);
+        else d[w] = v;
+    }
+}
+
+template <int V>
+KD_INLINE void store_res(uint4* dst, uint4 r) {
+    if constexpr ((V & VAR_NT_STORE) != 0) {
+        u32x4 v;
+        v.x = r.x;
+        v.y = r.y;
+        v.z = r.z;
+        v.w = r.w;
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst));
+    } else {
+        *dst = r;
+    }
+}
+
+template <int V>
+KD_INLINE void store_idx(uint32_t* dst, uint32_t v) {
+    if constexpr ((V & VAR_NT_STORE) != 0) __builtin_nontemporal_store(v, dst);
+    else *dst = v;
 }
 
 KD_INLINE uint4 pack_res(uint32_t peer, int32_t vni, uint32_t vtep, uint32_t kind, uint32_t err,
@@ -350,51 +402,51 @@ struct TopoCtx {       // the local pod of a batch (topology_controller.go:181-1
 };
 
 // delLink (handler.go:461-492)
+template <int V>
 KD_INLINE void emit_del(const DevLinks& O, uint32_t i, const TopoCtx& tc, const DevTables& tb,
                         const RecOut& out, uint32_t e, bool res) {
-    out.del_idx[e] = i;
+    constexpr bool NTL = (V & VAR_NT_LOAD) != 0;
+    store_idx<V>(out.del_idx + e, i);
     if (!res) return;
-    const int32_t vni = vni_of(tb.vxlan_base, O.uid(i));
-    const uint32_t err = veth_err(tb.kflags, O.key(KDTN_K_LOCAL_IP, i), O.key(KDTN_K_LOCAL_MAC, i),
+    const int32_t vni = vni_of(tb.vxlan_base, O.uid_s<NTL>(i));
+    const uint32_t err = veth_err(tb.kflags, O.key_s<NTL>(KDTN_K_LOCAL_IP, i), O.key_s<NTL>(KDTN_K_LOCAL_MAC, i),
                                   KDTN_E_VETH_CIDR, KDTN_E_VETH_MAC);
     uint32_t hit = 0;
     if (!err) hit = vni_lookup(tb, tc.src, vni) == tc.netns;
-    out.del_res[e] = pack_res(0xFFFFFFFFu, vni, 0, 0, err, hit);
+    store_res<V>(out.del_res + e, pack_res(0xFFFFFFFFu, vni, 0, 0, err, hit));
 }
 
 // UpdateLinks entry (handler.go:644-663): MakeVeth(local), then MakeQdiscs
+template <int V>
 KD_INLINE void emit_upd(const DevLinks& N, uint32_t j, const DevTables& tb, const RecOut& out,
-                        uint32_t e, bool res, bool qd) {
-    out.upd_idx[e] = j;
+                        uint32_t e, bool res, bool qd, uint32_t* q) {
+    constexpr bool NTL = (V & VAR_NT_LOAD) != 0;
+    store_idx<V>(out.upd_idx + e, j);
     if (!res && !qd) return;
-    uint32_t q[18];
-    make_qdisc(N, j, tb, q);
-    if (qd) store_qdisc(out.upd_qdisc + (size_t)e * 9, q);
+    make_qdisc<NTL>(N, j, tb, q);
     if (res) {
-        const int32_t vni = vni_of(tb.vxlan_base, N.uid(j));
-        uint32_t err = veth_err(tb.kflags, N.key(KDTN_K_LOCAL_IP, j), N.key(KDTN_K_LOCAL_MAC, j),
+        const int32_t vni = vni_of(tb.vxlan_base, N.uid_s<NTL>(j));
+        uint32_t err = veth_err(tb.kflags, N.key_s<NTL>(KDTN_K_LOCAL_IP, j), N.key_s<NTL>(KDTN_K_LOCAL_MAC, j),
                                 KDTN_E_VETH_CIDR, KDTN_E_VETH_MAC);
         if (!err) err = (q[17] >> 16) & 0xFF;
-        out.upd_res[e] = pack_res(0xFFFFFFFFu, vni, 0, 0, err, 0);
+        store_res<V>(out.upd_res + e, pack_res(0xFFFFFFFFu, vni, 0, 0, err, 0));
     }
 }
 
 // addLink pure prefix (handler.go:316-459) + MakeQdiscs
+template <int V>
 KD_INLINE void emit_add(const DevLinks& N, uint32_t j, const TopoCtx& tc, const DevTables& tb,
-                        const RecOut& out, uint32_t e, bool res, bool qd) {
-    out.add_idx[e] = j;
-    if (qd) {
-        uint32_t q[18];
-        make_qdisc(N, j, tb, q);
-        store_qdisc(out.add_qdisc + (size_t)e * 9, q);
-    }
+                        const RecOut& out, uint32_t e, bool res, bool qd, uint32_t* q) {
+    constexpr bool NTL = (V & VAR_NT_LOAD) != 0;
+    store_idx<V>(out.add_idx + e, j);
+    if (qd) make_qdisc<NTL>(N, j, tb, q);
     if (!res) return;
-    const int32_t vni = vni_of(tb.vxlan_base, N.uid(j));
-    uint32_t err = veth_err(tb.kflags, N.key(KDTN_K_LOCAL_IP, j), N.key(KDTN_K_LOCAL_MAC, j),
+    const int32_t vni = vni_of(tb.vxlan_base, N.uid_s<NTL>(j));
+    uint32_t err = veth_err(tb.kflags, N.key_s<NTL>(KDTN_K_LOCAL_IP, j), N.key_s<NTL>(KDTN_K_LOCAL_MAC, j),
                             KDTN_E_VETH_CIDR, KDTN_E_VETH_MAC);                          // :327
     uint32_t kind = 0, peer = 0xFFFFFFFFu, vtep = 0, hit = 0;
     if (!err) {
-        const uint32_t pp = N.key(KDTN_K_PEER_POD, j);
+        const uint32_t pp = N.key_s<NTL>(KDTN_K_PEER_POD, j);
         const uint8_t pf = tb.kflags[pp];
         if (pf & KF_LOCALHOST) {
             kind = KDTN_KIND_MACVLAN;                                                     // :333
@@ -405,30 +457,72 @@ KD_INLINE void emit_add(const DevLinks& N, uint32_t j, const TopoCtx& tc, const 
             hit = (nsx != 0xFFFFFFFFu && nsx != tc.netns);
         } else {
             const uint32_t lns = tc.ns == 0 ? *tb.default_id : tc.ns;                   // :29-31
-            const uint4 p = pod_lookup(tb, lns, pp);                                     // :375
+            const uint2 p = pod_lookup(tb, lns, pp);                                     // :375
             if (p.x == 0xFFFFFFFFu) {
                 err = KDTN_E_PEER_LOOKUP;
             } else {
-                peer = p.x;
-                const uint32_t p_src = p.y, p_ns = p.z & 0x7FFFFFFFu;
-                if (p.z & 0x80000000u) {
+                peer = p.x & 0x7FFFFFFFu;
+                const uint32_t p_src = p.y & 0x7FFFFFFFu;
+                if (p.x & 0x80000000u) {
                     err = KDTN_E_PEER_NO_LINKS;                                           // :380-384
-                } else if (p_src == 0 || p_ns == 0) {
+                } else if (p_src == 0 || (p.y & 0x80000000u)) {
                     kind = KDTN_KIND_PEER_DEAD;                                           // :386-395
                 } else if (p_src == tc.src) {
                     kind = KDTN_KIND_SAME_NODE;                                           // :399-418
-                    err = veth_err(tb.kflags, N.key(KDTN_K_PEER_IP, j), N.key(KDTN_K_PEER_MAC, j),
+                    err = veth_err(tb.kflags, N.key_s<NTL>(KDTN_K_PEER_IP, j), N.key_s<NTL>(KDTN_K_PEER_MAC, j),
                                    KDTN_E_PEER_VETH_CIDR, KDTN_E_PEER_VETH_MAC);
                 } else {
                     kind = KDTN_KIND_CROSS_NODE;                                          // :419-453
                     vtep = p_src;
-                    const uint32_t nsx = vni_lookup(tb, p_src, vni);
-                    hit = (nsx != 0xFFFFFFFFu && nsx != p_ns);
+                    if (tb.vni_mask) {                                   // remote Update check
+                        const uint32_t nsx = vni_lookup(tb, p_src, vni);
+                        hit = (nsx != 0xFFFFFFFFu && nsx != (tb.pods[peer].w & 0x7FFFFFFFu));
+                    }
                 }
             }
         }
     }
-    out.add_res[e] = pack_res(peer, vni, vtep, kind, err, hit);
+    store_res<V>(out.add_res + e, pack_res(peer, vni, vtep, kind, err, hit));
+}
+
+// Store the 72-B qdisc structs of this wave's active lanes. Active lanes' output positions
+// are consecutive in lane order (every emission path assigns positions by an exclusive
+// count in record order), so the wave stages 32 structs at a time in LDS and writes them
+// as contiguous 512-B bursts instead of nine 8-B stores at a 72-B stride per lane.
+template <int V>
+__device__ __forceinline__ void wave_store_qdisc(uint2* outq, bool active, uint32_t e,
+                                                 const uint32_t* q, uint2* stage) {
+    const uint64_t m = __ballot(active);
+    if (m == 0) return;
+    if constexpr ((V & VAR_NO_QSTORE) != 0) {
+        if (active)
+#pragma unroll
+            for (int w = 0; w < 18; ++w) asm volatile("" ::"v"(q[w]));
+        return;
+    }
+    const int lane = threadIdx.x & 63;
+    const uint32_t p0 = __shfl(e, __ffsll((long long)m) - 1, 64);
+    const uint32_t rank = __popcll(m & lanemask_lt());
+    const uint32_t lo = __popcll(m & 0xFFFFFFFFull), all = __popcll(m);
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+        const uint32_t r0 = half ? lo : 0u, cnt = half ? all - lo : lo;
+        if (cnt == 0) continue;
+        if (active && ((lane >= 32) == (half == 1))) {
+            uint2* slot = stage + (rank - r0) * 9;
+#pragma unroll
+            for (int w = 0; w < 9; ++w) slot[w] = make_uint2(q[2 * w], q[2 * w + 1]);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        uint2* dst = outq + (size_t)(p0 + r0) * 9;
+        const uint32_t nq = cnt * 9;
+        for (uint32_t k = lane; k < nq; k += 64) dst[k] = stage[k];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
 }
 
 // ======================================================================================
@@ -446,6 +540,8 @@ struct RecShared {
     uint32_t wtot[3];
     uint32_t base[3];
     uint32_t ticket;
+    uint32_t any_cmp;
+    uint2 stage[BLOCK / 64][32 * 9];   // per-wave qdisc staging (wave_store_qdisc)
     uint32_t hash[CAP];
     uint16_t rank[CAP];          // entry position within the workgroup's list
     uint16_t tgt[CAP];           // upd target, relative to the workgroup's first desired record
@@ -633,6 +729,7 @@ __device__ void lookback(RecShared& s, const RecWork& wk, uint32_t wg) {
     __syncthreads();
 }
 
+template <int V>
 __global__ void __launch_bounds__(BLOCK) k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb,
                                                      RecOut out, RecWork wk) {
     __shared__ RecShared s;
@@ -664,9 +761,26 @@ __global__ void __launch_bounds__(BLOCK) k_reconcile(DevTopos T, DevLinks O, Dev
     const bool fast = tot <= (uint32_t)CAP;
     const bool do_res = out.stages & KDTN_STAGE_RESOLVE;
     const bool do_q = out.stages & KDTN_STAGE_QDISC;
+    if (tid < 64) {
+        const uint64_t b = __ballot(tid < nt && need_cmp(s, tid));
+        if (tid == 0) s.any_cmp = b != 0ull;
+    }
+    __syncthreads();
+    // bulk: no topology of this workgroup has both lists non-empty (new pods: status empty;
+    // deleted pods: spec nil) → every record of a DIFF topology is an entry, in order
+    const bool bulk = s.any_cmp == 0;
 
     // ---- 1. Reconcile gate + CalcDiff ------------------------------------------------
-    if (fast) {
+    if (bulk) {
+        if (tid < nt) {
+            const uint8_t a = topo_action(s, tid);
+            s.act[tid] = a;
+            const bool d = a == KDTN_ACT_DIFF;
+            s.tcnt[0][tid] = d ? s.ooff[tid + 1] - s.ooff[tid] : 0u;
+            s.tcnt[2][tid] = d ? s.noff[tid + 1] - s.noff[tid] : 0u;
+        }
+        __syncthreads();
+    } else if (fast) {
         diff_window(s, 0, nt, O, N, s.hash, s.flag, s.lt, s.tgt, wk.otarget, n0);
     } else {
         for (int tt = 0; tt < nt; ++tt) {
@@ -699,7 +813,7 @@ __global__ void __launch_bounds__(BLOCK) k_reconcile(DevTopos T, DevLinks O, Dev
         }
     }
     // ranks of flagged records within the workgroup's lists (fast path)
-    if (fast) {
+    if (fast && !bulk) {
         const uint32_t per = (tot + BLOCK - 1) / BLOCK;
         const uint32_t r0 = min(tot, tid * per), r1 = min(tot, r0 + per);
         uint32_t c[3] = {0, 0, 0};
@@ -748,15 +862,54 @@ __global__ void __launch_bounds__(BLOCK) k_reconcile(DevTopos T, DevLinks O, Dev
     }
 
     // ---- 4. emission -------------------------------------------------------------------
+    uint2* stage = s.stage[tid >> 6];
+    if (bulk) {
+        for (uint32_t b = 0; b < tot; b += BLOCK) {          // position = topology offset + index
+            const uint32_t r = b + tid;
+            bool qa = false;
+            uint32_t e = 0, q[18];
+            if (r < tot) {
+                const bool old = r < no;
+                const uint32_t x = old ? o0 + r : n0 + (r - no);
+                const int tt = find_seg(old ? s.ooff : s.noff, 0, nt, x);
+                if (s.act[tt] == KDTN_ACT_DIFF) {
+                    const TopoCtx tc{s.ns[tt], s.src[tt], s.netns[tt]};
+                    if (old) {
+                        emit_del<V>(O, x, tc, tb, out, bd + s.tcnt[0][tt] + (x - s.ooff[tt]), do_res);
+                    } else {
+                        e = ba + s.tcnt[2][tt] + (x - s.noff[tt]);
+                        emit_add<V>(N, x, tc, tb, out, e, do_res, do_q, q);
+                        qa = do_q;
+                    }
+                }
+            }
+            wave_store_qdisc<V>(out.add_qdisc, qa, e, q, stage);
+        }
+        return;
+    }
     if (fast) {
-        for (uint32_t r = tid; r < tot; r += BLOCK) {        // no barriers: full MLP
-            const uint8_t f = s.flag[r];
-            if (!f) continue;
-            const int tt = s.lt[r];
-            const TopoCtx tc{s.ns[tt], s.src[tt], s.netns[tt]};
-            if (f & RF_DEL) emit_del(O, o0 + r, tc, tb, out, bd + s.rank[r], do_res);
-            else if (f & RF_UPD) emit_upd(N, n0 + s.tgt[r], tb, out, bu + s.rank[r], do_res, do_q);
-            else emit_add(N, n0 + (r - no), tc, tb, out, ba + s.rank[r], do_res, do_q);
+        for (uint32_t b = 0; b < tot; b += BLOCK) {          // no workgroup barriers
+            const uint32_t r = b + tid;
+            bool qa = false, qu = false;
+            uint32_t e = 0, q[18];
+            const uint8_t f = r < tot ? s.flag[r] : 0;
+            if (f) {
+                const int tt = s.lt[r];
+                const TopoCtx tc{s.ns[tt], s.src[tt], s.netns[tt]};
+                if (f & RF_DEL) {
+                    emit_del<V>(O, o0 + r, tc, tb, out, bd + s.rank[r], do_res);
+                } else if (f & RF_UPD) {
+                    e = bu + s.rank[r];
+                    emit_upd<V>(N, n0 + s.tgt[r], tb, out, e, do_res, do_q, q);
+                    qu = do_q;
+                } else {
+                    e = ba + s.rank[r];
+                    emit_add<V>(N, n0 + (r - no), tc, tb, out, e, do_res, do_q, q);
+                    qa = do_q;
+                }
+            }
+            wave_store_qdisc<V>(out.add_qdisc, qa, e, q, stage);
+            wave_store_qdisc<V>(out.upd_qdisc, qu, e, q, stage);
         }
         return;
     }
@@ -792,9 +945,18 @@ __global__ void __launch_bounds__(BLOCK) k_reconcile(DevTopos T, DevLinks O, Dev
             if (f) {
                 const int tt = find_seg(side ? s.noff : s.ooff, 0, nt, x);
                 const TopoCtx tc{s.ns[tt], s.src[tt], s.netns[tt]};
-                if (f & RF_DEL) emit_del(O, x, tc, tb, out, bd + cd + p0 + __popcll(b0 & lt), do_res);
-                else if (f & RF_UPD) emit_upd(N, wk.otarget[x], tb, out, bu + cu + p1 + __popcll(b1 & lt), do_res, do_q);
-                else emit_add(N, x, tc, tb, out, ba + ca + p2 + __popcll(b2 & lt), do_res, do_q);
+                uint32_t q[18];
+                if (f & RF_DEL) {
+                    emit_del<V>(O, x, tc, tb, out, bd + cd + p0 + __popcll(b0 & lt), do_res);
+                } else if (f & RF_UPD) {
+                    const uint32_t e = bu + cu + p1 + __popcll(b1 & lt);
+                    emit_upd<V>(N, wk.otarget[x], tb, out, e, do_res, do_q, q);
+                    if (do_q) store_qdisc<V>(out.upd_qdisc + (size_t)e * 9, q);
+                } else {
+                    const uint32_t e = ba + ca + p2 + __popcll(b2 & lt);
+                    emit_add<V>(N, x, tc, tb, out, e, do_res, do_q, q);
+                    if (do_q) store_qdisc<V>(out.add_qdisc + (size_t)e * 9, q);
+                }
             }
             cd += t0_;
             cu += t1_;
@@ -809,8 +971,15 @@ __global__ void __launch_bounds__(BLOCK) k_qdisc_batch(DevLinks props, DevTables
     const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
     if (j >= props.n) return;
     uint32_t q[18];
-    make_qdisc(props, j, tb, q);
-    store_qdisc(out + (size_t)j * 9, q);
+    make_qdisc<false>(props, j, tb, q);
+    store_qdisc<0>(out + (size_t)j * 9, q);
 }
+
+template __global__ void k_reconcile<0>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
+template __global__ void k_reconcile<1>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
+template __global__ void k_reconcile<2>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
+template __global__ void k_reconcile<3>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
+template __global__ void k_reconcile<4>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
+template __global__ void k_reconcile<5>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
 
 }  // namespace kdtn

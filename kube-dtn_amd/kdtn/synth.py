@@ -44,10 +44,11 @@ def _load():
 class _Handle:
     def __init__(self, ptr):
         self.ptr = ptr
+        self.free = _load().kdtn_synth_free   # bound now: module globals may be gone at exit
 
     def __del__(self):
         if self.ptr:
-            _load().kdtn_synth_free(self.ptr)
+            self.free(self.ptr)
             self.ptr = None
 
 
@@ -75,10 +76,49 @@ def _links(h: _Handle, pre: str) -> Links:
     return Links(np.ascontiguousarray(key), uid, np.ascontiguousarray(prop), gap)
 
 
+def _cache_path(cache_dir, *key):
+    return os.path.join(cache_dir, "kdtn_synth_" + "_".join(str(k) for k in key) + ".npz")
+
+
+def _save(inp: EpochInput, path: str) -> None:
+    arrs = {"kb": inp.kdict.bytes_, "ko": inp.kdict.offs, "pb": inp.pdict.bytes_, "po": inp.pdict.offs,
+            "tns": inp.topos.ns, "tna": inp.topos.name, "tsr": inp.topos.src_ip, "tnn": inp.topos.net_ns,
+            "tfl": inp.topos.flags, "tro": inp.topos.real_off, "tdo": inp.topos.des_off,
+            "vno": inp.vnis.node, "vvn": inp.vnis.vni, "vnn": inp.vnis.net_ns,
+            "meta": np.array([inp.pod_slice, inp.pod_base, inp.total_pods], np.int64)}
+    for side, L in (("r", inp.realised), ("d", inp.desired)):
+        arrs[side + "k"], arrs[side + "u"], arrs[side + "p"], arrs[side + "g"] = L.key, L.uid, L.prop, L.gap
+    tmp = path + ".tmp.npz"
+    np.savez(tmp, **arrs)
+    os.replace(tmp, path)
+
+
+def _load_cached(path: str) -> EpochInput:
+    z = np.load(path)
+    m = z["meta"]
+    inp = EpochInput(StrTab(z["kb"], z["ko"]), StrTab(z["pb"], z["po"]),
+                     Topos(z["tns"], z["tna"], z["tsr"], z["tnn"], z["tfl"], z["tro"], z["tdo"]),
+                     Links(z["rk"], z["ru"], z["rp"], z["rg"]), Links(z["dk"], z["du"], z["dp"], z["dg"]),
+                     Vnis(z["vno"], z["vvn"], z["vnn"]), pod_slice=int(m[0]), pod_base=int(m[1]))
+    inp.total_pods = int(m[2])
+    return inp
+
+
 def make(config: int, pods_per_shard: int = 1_000_000, degree: int = 10, n_nodes: int = 64,
-         dead_frac: float = 0.02, shard: int = 0, nshards: int = 1, seed: int = SEED) -> EpochInput:
+         dead_frac: float = 0.02, shard: int = 0, nshards: int = 1, seed: int = SEED,
+         cache_dir: str | None = None) -> EpochInput:
     """Build one shard of synthetic config `config` (1: fat-tree, 2: random-regular,
-    3: churn, 4: WAN twin). Config 1 ignores the size parameters."""
+    3: churn, 4: WAN twin). Config 1 ignores the size parameters. With `cache_dir`, the
+    tables are memoised as an .npz there (profiling runs that start many processes)."""
+    if cache_dir:
+        path = _cache_path(cache_dir, config, pods_per_shard, degree, n_nodes, dead_frac, shard,
+                           nshards, seed)
+        if os.path.exists(path):
+            return _load_cached(path)
+        inp = make(config, pods_per_shard, degree, n_nodes, dead_frac, shard, nshards, seed)
+        os.makedirs(cache_dir, exist_ok=True)
+        _save(inp, path)
+        return inp
     prm = Params(seed, pods_per_shard, degree, n_nodes, dead_frac, shard, nshards)
     ptr = _load().kdtn_synth_new(config, C.byref(prm))
     if not ptr:

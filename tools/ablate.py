@@ -19,11 +19,27 @@ ap.add_argument("--pods", type=int, default=1_000_000)
 ap.add_argument("--config", type=int, default=2)
 ap.add_argument("--reps", type=int, default=10)
 ap.add_argument("--masks", default="ALL,DIFF|RESOLVE,DIFF|QDISC,DIFF")
+ap.add_argument("--cache", default="")
+ap.add_argument("--variants", default="", help="comma list of KDTN_VARIANT values, interleaved")
 a = ap.parse_args()
-inp = synth.make(a.config, pods_per_shard=a.pods)
+inp = synth.make(a.config, pods_per_shard=a.pods, cache_dir=a.cache or None)
 eng = Engine(device=0)
 eng.upload(inp)
 res = {}
+if a.variants:
+    vs = [v for v in a.variants.split(",")]
+    acc = {v: [] for v in vs}
+    for rep in range(a.reps + 2):
+        for v in vs:                      # interleaved rounds (cdna_hip_programming.md rule 24)
+            os.environ["KDTN_VARIANT"] = v
+            eng.run(abi.STAGE_ALL)
+            eng.sync()
+            if rep >= 2:
+                acc[v].append(eng.kernel_times()["reconcile"])
+    os.environ.pop("KDTN_VARIANT")
+    for v in vs:
+        x = sorted(acc[v])
+        res["variant_" + v] = {"median": round(x[len(x) // 2], 4), "min": round(x[0], 4)}
 masks = {"ALL": abi.STAGE_ALL, "DIFF|RESOLVE": abi.STAGE_DIFF | abi.STAGE_RESOLVE,
          "DIFF|QDISC": abi.STAGE_DIFF | abi.STAGE_QDISC, "DIFF": abi.STAGE_DIFF}
 for name, m in masks.items():
