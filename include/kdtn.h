@@ -284,6 +284,10 @@ int kdtn_comm_init(kdtn_ctx* ctx, const uint8_t unique_id[128], int nranks, int 
 
 /* ---- profiling hooks: per-kernel HIP-event times of the last epoch_run (ms) -------- */
 int kdtn_last_kernel_times(kdtn_ctx* ctx, const char** names, float* ms, int cap);
+/* Per-workgroup phase timestamps of k_reconcile (100 MHz clock; 6 words per workgroup:
+ * entry, topologies loaded, counts done, batch bases known, end, XCC_ID<<32|HW_ID) of the
+ * last epoch run with KDTN_VARIANT bit 16 set. Returns the number of words copied. */
+int kdtn_debug_wg_trace(kdtn_ctx* ctx, uint64_t* out, uint32_t cap);
 
 #ifdef __cplusplus
 }

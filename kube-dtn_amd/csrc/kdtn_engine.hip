@@ -61,7 +61,7 @@ struct kdtn_ctx {
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
     // dictionaries
-    DevBuf kd_bytes, kd_offs, kd_flags, pd_bytes, pd_offs, pd_pct, pd_dur, pd_rate;
+    DevBuf kd_bytes, kd_offs, kd_bits, pd_bytes, pd_offs, pd_pct, pd_dur, pd_rate;
     uint32_t D = 0, P = 0;
     // topologies
     DevBuf t_ns, t_name, t_src, t_netns, t_flags, t_roff, t_noff;
@@ -73,9 +73,10 @@ struct kdtn_ctx {
     uint32_t V = 0, vni_mask = 0;
     // pods
     DevBuf pods, pod_slots, pod_wide;
-    uint32_t slice = 0, pod_total = 0, pod_mask = 0;
+    uint32_t slice = 0, pod_total = 0, pod_mask = 0, kb_words = 0;
+    bool traced = false;
     // work
-    DevBuf otarget, sync, misc, hscratch, fscratch;
+    DevBuf otarget, sync, misc, hscratch, fscratch, trace;
     uint32_t nwg = 0;
     // outputs
     DevBuf action, del_off, add_off, upd_off, del_idx, add_idx, upd_idx;
@@ -332,7 +333,7 @@ void kdtn_destroy(kdtn_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    DevBuf* bufs[] = {&c->kd_bytes, &c->kd_offs, &c->kd_flags, &c->pd_bytes, &c->pd_offs,
+    DevBuf* bufs[] = {&c->kd_bytes, &c->kd_offs, &c->kd_bits, &c->pd_bytes, &c->pd_offs,
                       &c->pd_pct, &c->pd_dur, &c->pd_rate, &c->t_ns, &c->t_name, &c->t_src,
                       &c->t_netns, &c->t_flags, &c->t_roff, &c->t_noff, &c->real.buf, &c->des.buf,
                       &c->v_node, &c->v_vni, &c->v_netns, &c->v_ents, &c->v_slots, &c->pods,
@@ -390,7 +391,8 @@ int kdtn_epoch_upload(kdtn_ctx* c, const kdtn_epoch_in* in) {
     c->T = T.n;
     TRY(upload_arena(c, c->kd_bytes, in->kdict.bytes, in->kdict.offs[D]));
     TRY(upload(c, c->kd_offs, in->kdict.offs, (size_t)(D + 1) * 4));
-    TRY(ensure(c->kd_flags, D));
+    c->kb_words = (uint32_t)(((uint64_t)D + 63) / 64 * 2);
+    TRY(ensure(c->kd_bits, (size_t)KB_NSETS * c->kb_words * 4 + 4));
     TRY(upload_arena(c, c->pd_bytes, in->pdict.bytes, in->pdict.offs[P]));
     TRY(upload(c, c->pd_offs, in->pdict.offs, (size_t)(P + 1) * 4));
     TRY(ensure(c->pd_pct, (size_t)P * 4));
@@ -418,6 +420,11 @@ int kdtn_epoch_upload(kdtn_ctx* c, const kdtn_epoch_in* in) {
     TRY(ensure(c->v_slots, (size_t)(c->vni_mask + 1) * 4));
 
     c->slice = slice;
+    if ((uint64_t)slice * (uint64_t)c->nranks > POD_INDEX) {
+        std::snprintf(g_last_error, sizeof(g_last_error), "pod table of %llu entries exceeds 2^30",
+                      (unsigned long long)slice * (unsigned long long)c->nranks);
+        return KDTN_EINVAL;
+    }
     c->pod_total = slice * (uint32_t)c->nranks;
     c->pod_mask = next_pow2((uint64_t)c->pod_total * 2) - 1;
     TRY(ensure(c->pods, (size_t)c->pod_total * 16));
@@ -459,17 +466,18 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
     hipStream_t s = c->stream;
     (void)hipEventRecord(c->ev[0], s);
     uint32_t* misc = dp<uint32_t>(c->misc);
-    HIP_TRY(hipMemsetAsync(misc, 0xFF, 64, s));                       // default id = 0xFFFFFFFF
+    HIP_TRY(hipMemsetAsync(misc, 0xFF, 64, s));                       // special ids = 0xFFFFFFFF
     HIP_TRY(hipMemsetAsync(c->sync.p, 0, sync_bytes(c->nwg), s));    // ticket, error, look-back
 
     const DevTopos T = topo_view(c);
     // dictionaries
     if (c->D) k_kdict_flags<<<nblocks(c->D), BLOCK, 0, s>>>(dp<uint8_t>(c->kd_bytes), dp<uint32_t>(c->kd_offs),
-                                                         c->D, dp<uint8_t>(c->kd_flags), misc);
+                                                         c->D, dp<uint32_t>(c->kd_bits), c->kb_words, misc);
+    timer_mark(c, "kdict_parse");
     if (c->P) k_pdict_parse<<<nblocks(c->P), BLOCK, 0, s>>>(dp<uint8_t>(c->pd_bytes), dp<uint32_t>(c->pd_offs),
                                                          c->P, c->cfg.tick_in_usec, dp<uint32_t>(c->pd_pct),
                                                          dp<uint4>(c->pd_dur), dp<uint4>(c->pd_rate));
-    timer_mark(c, "dict_parse");
+    timer_mark(c, "pdict_parse");
     const bool resolve = stages & KDTN_STAGE_RESOLVE;
     if (resolve) {
         // pod-status table (+ all-gather across ranks) and lookup tables
@@ -490,6 +498,7 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
             k_pod_ht_build<<<nblocks(c->pod_total), BLOCK, 0, s>>>(dp<uint4>(c->pods), c->pod_total,
                                                                   dp<uint32_t>(c->pod_slots), c->pod_mask);
         k_pod_ht_expand<<<nblocks(pcap), BLOCK, 0, s>>>(dp<uint4>(c->pods), dp<uint32_t>(c->pod_slots),
+                                                       dp<uint32_t>(c->kd_bits) + (size_t)KB_PHYSICAL * c->kb_words,
                                                        dp<uint4>(c->pod_wide), (uint32_t)pcap);
         if (c->V) {
             const size_t vcap = (size_t)c->vni_mask + 1;
@@ -503,7 +512,8 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
     }
     if (c->T) {
         DevTables tb{};
-        tb.kflags = dp<uint8_t>(c->kd_flags);
+        tb.kbits = dp<uint32_t>(c->kd_bits);
+        tb.kb_words = c->kb_words;
         tb.ppct = dp<uint32_t>(c->pd_pct);
         tb.pdur = dp<uint4>(c->pd_dur);
         tb.prate = dp<uint4>(c->pd_rate);
@@ -513,7 +523,7 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         tb.vnis = dp<uint4>(c->v_ents);
         tb.vni_slots = dp<uint32_t>(c->v_slots);
         tb.vni_mask = c->V ? c->vni_mask : 0;
-        tb.default_id = misc;
+        tb.special = misc;
         tb.vxlan_base = c->cfg.vxlan_base;
         RecOut o;
         o.action = dp<uint8_t>(c->action);
@@ -537,14 +547,26 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         w.fscratch = dp<uint8_t>(c->fscratch);
         w.otarget = dp<uint32_t>(c->otarget);
         w.nwg = c->nwg;
+        w.trace = nullptr;
         int variant = DEFAULT_VARIANT;
         if (const char* ev = std::getenv("KDTN_VARIANT")) variant = std::atoi(ev);   // profiling A/B
+        if (variant & VAR_TRACE) {
+            TRY(ensure(c->trace, (size_t)c->nwg * TRACE_WORDS * 8));
+            w.trace = reinterpret_cast<unsigned long long*>(c->trace.p);
+            c->traced = true;
+        }
         switch (variant) {
         case 0: k_reconcile<0><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
         case 2: k_reconcile<2><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
         case 3: k_reconcile<3><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
         case 4: k_reconcile<4><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
         case 5: k_reconcile<5><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
+        case 9: k_reconcile<9><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
+        case 33: k_reconcile<33><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
+        case 65: k_reconcile<65><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
+        case 97: k_reconcile<97><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
+        case 17: k_reconcile<17><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
+        case 11: k_reconcile<11><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
         default: k_reconcile<1><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
         }
         timer_mark(c, "reconcile");
@@ -691,6 +713,15 @@ int kdtn_comm_init(kdtn_ctx* c, const uint8_t uid[128], int nranks, int rank) {
         return KDTN_EIO;
     }
     return KDTN_OK;
+}
+
+int kdtn_debug_wg_trace(kdtn_ctx* c, uint64_t* out, uint32_t cap) {
+    if (!c || !c->traced) return KDTN_EINVAL;
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    const uint32_t n = std::min<uint64_t>(cap, (uint64_t)c->nwg * TRACE_WORDS);
+    HIP_TRY(hipMemcpy(out, c->trace.p, (size_t)n * 8, hipMemcpyDeviceToHost));
+    return (int)n;
 }
 
 int kdtn_last_kernel_times(kdtn_ctx* c, const char** names, float* ms, int cap) {

@@ -7,11 +7,14 @@
 //   topologies   : u32 ns/name/src_ip/net_ns ids, u8 flags, u32 offsets (T+1) per side
 //   dictionaries : u8 arena + u32 offsets, parsed once per epoch (one thread per string,
 //                  arena slices staged through LDS) into compact lookup tables:
-//                  kflags u8/key string; ppct u32 (Percentage2u32 or PCT_ERR);
+//                  kbits: 3 bitsets over key strings (CIDR_BAD, MAC_BAD, PHYSICAL; 1.5 MB
+//                  per 12M strings, L2-resident); ppct u32 (Percentage2u32 or PCT_ERR);
 //                  pdur {us, ticks, err}; prate {lo, hi, err}
 //   pod table    : pods[g] = {ns, name, src_ip, net_ns|spec_nil<<31} per global pod index,
 //                  open-addressing slots of pod indices keyed by (ns, name) (one CAS per
-//                  insert), expanded into 16-B self-contained slots: a lookup is ONE gather.
+//                  insert), expanded into 16-B self-contained slots: a lookup is ONE gather
+//                  (the slot also carries the PHYSICAL bit of the pod's name, so a hit
+//                  needs no key-string flag read).
 // Kernels (launch order):
 //   k_kdict_flags   MakeVeth / addLink predicates per key string          (D threads)
 //   k_pdict_parse   ParseDuration / ParseFloatPercentage / ParseRate      (P threads)
@@ -37,13 +40,17 @@ constexpr int STAGE = 8192;  // LDS bytes for staged dictionary slices
 
 constexpr uint32_t PCT_ERR = 0xFFFFFFFEu;   // Percentage2u32 never yields this value
 
-// key-string flags
-enum : uint8_t {
-    KF_CIDR_BAD = 1,    // non-empty and net.ParseCIDR fails
-    KF_MAC_BAD = 2,     // non-empty and net.ParseMAC fails
-    KF_LOCALHOST = 4,   // == "localhost"
-    KF_PHYSICAL = 8,    // has prefix "physical/"
+// key-string predicates, one bitset each (bit i of word i/32 = string i)
+enum : int {
+    KB_CIDR_BAD = 0,    // non-empty and net.ParseCIDR fails
+    KB_MAC_BAD = 1,     // non-empty and net.ParseMAC fails
+    KB_PHYSICAL = 2,    // has prefix "physical/"
+    KB_NSETS = 3,
 };
+// special key-string ids found by k_kdict_flags (0xFFFFFFFF when absent)
+enum : int { SPECIAL_DEFAULT = 0, SPECIAL_LOCALHOST = 4 };   // word index in the misc buffer
+// pod slot flag bits (in the g word of a wide slot; pod indices < 2^30)
+constexpr uint32_t POD_SPEC_NIL = 0x80000000u, POD_PHYSICAL = 0x40000000u, POD_INDEX = 0x3FFFFFFFu;
 
 // record flags
 enum : uint8_t { RF_DEL = 1, RF_UPD = 2, RF_ADD = 4 };
@@ -87,7 +94,12 @@ struct DevLinks {
 //   bit 0: non-temporal streaming loads of link columns
 //   bit 1: non-temporal output stores
 //   bit 2: (profiling) compute MakeQdiscs but do not store it
-constexpr int VAR_NT_LOAD = 1, VAR_NT_STORE = 2, VAR_NO_QSTORE = 4;
+//   bit 3: non-temporal pod-slot gathers
+//   bit 4: (profiling) per-workgroup phase timestamps into RecWork::trace
+//   bits 5, 6: (profiling, wrong results) skip the pod-slot / percentage-table gathers
+constexpr int VAR_NT_LOAD = 1, VAR_NT_STORE = 2, VAR_NO_QSTORE = 4, VAR_NT_POD = 8, VAR_TRACE = 16,
+              VAR_SKIP_POD = 32, VAR_SKIP_PCT = 64;
+constexpr int TRACE_WORDS = 6;   // entry, topologies loaded, counts done, bases known, end, hw ids
 constexpr int DEFAULT_VARIANT = VAR_NT_LOAD;
 
 struct DevTopos {
@@ -102,17 +114,18 @@ struct DevTopos {
 };
 
 struct DevTables {             // read-only lookup structures of the epoch
-    const uint8_t* kflags;     // [D]
+    const uint32_t* kbits;     // [KB_NSETS][kb_words]
+    uint32_t kb_words;         // words per bitset (multiple of 2)
     const uint32_t* ppct;      // [P]
     const uint4* pdur;         // [P] {us, ticks, err, 0}
     const uint4* prate;        // [P] {lo, hi, err, 0}
     const uint4* pods;         // [pod_total] {ns, name, src_ip, net_ns|spec_nil<<31}
-    const uint4* pod_wide;     // [pod_mask+1] {ns, name, g|spec_nil<<31, src_ip|netns_empty<<31}
+    const uint4* pod_wide;     // [pod_mask+1] {ns, name, g|POD_* flags, src_ip|netns_empty<<31}
     uint32_t pod_mask;
     const uint4* vnis;         // [V] {node, vni, net_ns, 0}
     const uint32_t* vni_slots; // [vni_mask+1]
     uint32_t vni_mask;         // 0 ⇒ empty table
-    const uint32_t* default_id;
+    const uint32_t* special;   // [SPECIAL_DEFAULT] "default", [SPECIAL_LOCALHOST] "localhost"
     int32_t vxlan_base;
 };
 
@@ -139,16 +152,18 @@ struct RecWork {
     uint32_t* hscratch;        // [M+N] window hashes of topologies larger than CAP
     uint8_t* fscratch;         // [M+N] record flags when a workgroup exceeds CAP
     uint32_t* otarget;         // [M]   first matching desired index (slow path)
+    unsigned long long* trace; // [nwg][TRACE_WORDS] (VAR_TRACE only)
     uint32_t nwg;
 };
 
 __global__ void k_kdict_flags(const uint8_t* bytes, const uint32_t* offs, uint32_t n,
-                              uint8_t* flags, uint32_t* default_id);
+                              uint32_t* kbits, uint32_t kb_words, uint32_t* special);
 __global__ void k_pdict_parse(const uint8_t* bytes, const uint32_t* offs, uint32_t n, double tick,
                               uint32_t* ppct, uint4* pdur, uint4* prate);
 __global__ void k_pods_fill(DevTopos T, uint32_t slice, uint32_t rank_base, uint4* pods);
 __global__ void k_pod_ht_build(const uint4* pods, uint32_t total, uint32_t* slots, uint32_t mask);
-__global__ void k_pod_ht_expand(const uint4* pods, const uint32_t* slots, uint4* wide, uint32_t cap);
+__global__ void k_pod_ht_expand(const uint4* pods, const uint32_t* slots, const uint32_t* phys_bits,
+                                uint4* wide, uint32_t cap);
 __global__ void k_vni_ht_build(const uint4* ents, uint32_t n, uint32_t* slots, uint32_t mask);
 __global__ void k_vni_pack(const uint32_t* node, const int32_t* vni, const uint32_t* net_ns,
                            uint32_t n, uint4* ents);

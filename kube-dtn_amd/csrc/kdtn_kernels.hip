@@ -89,40 +89,88 @@ KD_INLINE const uint8_t* stage_slice(const uint8_t* bytes, const uint32_t* offs,
 // ======================================================================================
 // dictionary parsing (one thread per distinct string)
 // ======================================================================================
-KD_INLINE uint8_t kdict_flags_of(const uint8_t* s, uint32_t len, bool* is_default) {
-    uint8_t f = 0;
-    if (len) {
-        if (!cidr_ok(s, len)) f |= KF_CIDR_BAD;   // common/veth.go:22
-        if (!mac_ok(s, len)) f |= KF_MAC_BAD;     // common/veth.go:33
+// Word k of a string's first 24 bytes (bytes past the end are garbage; callers mask by len).
+KD_INLINE uint32_t wbyte(const uint32_t* w, int k) { return (w[k >> 2] >> (8 * (k & 3))) & 0xFFu; }
+
+// net.ParseCIDR validity for a string of <= 24 bytes without ':' (so not IPv6; common/veth.go:22),
+// branch-free over the register image: 4 dotted octets (1-3 digits, no leading zero, <= 255),
+// '/', then >= 1 digits with value <= 32 (dtoi accepts leading zeros).
+KD_INLINE bool cidr4_regs(const uint32_t* w, uint32_t len) {
+    uint32_t field = 0, nd = 0, val = 0, bad = 0;
+#pragma unroll
+    for (int k = 0; k < 24; ++k) {
+        const uint32_t c = wbyte(w, k);
+        const uint32_t act = (uint32_t)k < len;
+        const uint32_t d = c - '0';
+        const uint32_t isd = d < 10u;
+        const uint32_t oct = field < 4u;
+        // digit in an octet: no digit after a leading '0', at most 3 digits
+        const uint32_t zlead = (nd == 1u) & (val == 0u);
+        const uint32_t bad_d = oct & (zlead | (nd >= 3u));
+        // separator: '.' ends octets 0-2, '/' ends octet 3
+        const uint32_t sep_ok = (nd >= 1u) & (val <= 255u) &
+                                (((c == '.') & (field < 3u)) | ((c == '/') & (field == 3u)));
+        const uint32_t bad_c = isd ? bad_d : (oct ? (sep_ok ^ 1u) : 1u);
+        bad |= act & bad_c;
+        const uint32_t nval = isd ? min(val * 10u + d, 1000u) : 0u;
+        const uint32_t nnd = isd ? nd + 1u : 0u;
+        const uint32_t nfield = isd ? field : field + 1u;
+        val = act ? nval : val;
+        nd = act ? nnd : nd;
+        field = act ? nfield : field;
     }
-    if (len == 9 && s[0] == 'l' && s[1] == 'o' && s[2] == 'c' && s[3] == 'a' && s[4] == 'l' &&
-        s[5] == 'h' && s[6] == 'o' && s[7] == 's' && s[8] == 't')
-        f |= KF_LOCALHOST;                        // common.Localhost (handler.go:333)
-    if (len >= 9 && s[0] == 'p' && s[1] == 'h' && s[2] == 'y' && s[3] == 's' && s[4] == 'i' &&
-        s[5] == 'c' && s[6] == 'a' && s[7] == 'l' && s[8] == '/')
-        f |= KF_PHYSICAL;                         // handler.go:348
-    *is_default = len == 7 && s[0] == 'd' && s[1] == 'e' && s[2] == 'f' && s[3] == 'a' &&
-                  s[4] == 'u' && s[5] == 'l' && s[6] == 't';
-    return f;
+    return !bad && field == 4u && nd >= 1u && val <= 32u;
 }
 
+// One thread per key string, no LDS: the first 24 bytes are loaded as 7 aligned dwords and
+// funnel-shifted into registers; CIDR/MAC validity, "localhost", "physical/" and "default"
+// are decided there. Strings longer than 24 bytes, with ':' (IPv6) or shaped like a MAC
+// take the generic parsers (kdtn_parse.h) on global memory. Each wave packs its 64
+// predicate bits per set with a ballot (two u32 words per set, lanes 0 and 32).
 __global__ void __launch_bounds__(BLOCK) k_kdict_flags(const uint8_t* bytes, const uint32_t* offs,
-                                                       uint32_t n, uint8_t* flags,
-                                                       uint32_t* default_id) {
-    __shared__ uint4 buf[STAGE / 16];
-    const uint32_t s0 = blockIdx.x * BLOCK, s1 = min(s0 + BLOCK, n);
-    uint32_t a0;
-    const bool staged = stage_slice(bytes, offs, s0, s1, buf, &a0) != nullptr;
-    __syncthreads();
-    const uint32_t i = s0 + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t b = offs[i], len = offs[i + 1] - b;
-    bool dflt;
-    uint8_t f;
-    if (staged) f = kdict_flags_of(reinterpret_cast<const uint8_t*>(buf) + (b - a0), len, &dflt);
-    else f = kdict_flags_of(bytes + b, len, &dflt);
-    if (dflt) atomicMin(default_id, i);          // getPod: ns "" → "default" (handler.go:29-31)
-    flags[i] = f;
+                                                       uint32_t n, uint32_t* kbits, uint32_t kb_words,
+                                                       uint32_t* special) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    uint32_t f = 0;
+    if (i < n) {
+        const uint32_t b = offs[i], len = offs[i + 1] - b;
+        const uint32_t a = b & ~3u, sh = (b & 3u) * 8u;
+        const uint32_t* p = reinterpret_cast<const uint32_t*>(bytes + a);   // arena has 64 B slack
+        uint32_t d[7], w[6];
+#pragma unroll
+        for (int k = 0; k < 7; ++k) d[k] = p[k];
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+            w[k] = sh ? (d[k] >> sh) | (d[k + 1] << (32u - sh)) : d[k];
+        if (len) {
+            bool colon = false;
+#pragma unroll
+            for (int k = 0; k < 24; ++k) colon |= ((uint32_t)k < len) & (wbyte(w, k) == ':');
+            bool cok;
+            if (len <= 24 && !colon) cok = cidr4_regs(w, len);
+            else cok = cidr_ok(bytes + b, len);                            // common/veth.go:22
+            if (!cok) f |= 1u << KB_CIDR_BAD;
+            const uint32_t c2 = wbyte(w, 2), c4 = wbyte(w, 4);
+            bool mok = false;                                              // common/veth.go:33
+            if (len >= 14 && (c2 == ':' || c2 == '-' || c4 == '.')) mok = mac_ok(bytes + b, len);
+            if (!mok) f |= 1u << KB_MAC_BAD;
+        }
+        const uint32_t w2b = w[2] & 0xFFu;
+        if (len >= 9 && w[0] == 0x73796870u && w[1] == 0x6C616369u && w2b == '/')   // "phys" "ical" '/'
+            f |= 1u << KB_PHYSICAL;                                        // handler.go:348
+        if (len == 9 && w[0] == 0x61636F6Cu && w[1] == 0x736F686Cu && w2b == 't')   // "loca" "lhos" 't'
+            atomicMin(special + SPECIAL_LOCALHOST, i);                     // handler.go:333
+        if (len == 7 && w[0] == 0x61666564u && (w[1] & 0xFFFFFFu) == 0x746C75u)     // "defa" "ult"
+            atomicMin(special + SPECIAL_DEFAULT, i);                       // getPod ns "" (handler.go:29-31)
+    }
+    const int lane = threadIdx.x & 63;
+    const uint32_t w0 = (i - lane) >> 5;                       // first word of this wave
+#pragma unroll
+    for (int k = 0; k < KB_NSETS; ++k) {
+        const uint64_t m = __ballot((f >> k) & 1u);
+        if (w0 < kb_words && (lane == 0 || lane == 32))
+            kbits[(size_t)k * kb_words + w0 + (lane >> 5)] = lane ? (uint32_t)(m >> 32) : (uint32_t)m;
+    }
 }
 
 KD_INLINE void pdict_parse_one(const uint8_t* s, uint32_t len, double tick, uint32_t* pct_out,
@@ -204,17 +252,20 @@ __global__ void __launch_bounds__(BLOCK) k_vni_pack(const uint32_t* node, const 
     if (v < n) ents[v] = make_uint4(node[v], (uint32_t)vni[v], net_ns[v], 0u);
 }
 
-// Expand the slot table into 16-B self-contained slots {ns, name, g|spec_nil<<31,
+// Expand the slot table into 16-B self-contained slots {ns, name, g|spec_nil<<31|physical<<30,
 // src_ip|netns_empty<<31}: a lookup is then ONE random 16-B gather (key + payload).
 __global__ void __launch_bounds__(BLOCK) k_pod_ht_expand(const uint4* pods, const uint32_t* slots,
-                                                         uint4* wide, uint32_t cap) {
+                                                         const uint32_t* phys_bits, uint4* wide,
+                                                         uint32_t cap) {
     const uint32_t h = blockIdx.x * BLOCK + threadIdx.x;
     if (h >= cap) return;
     const uint32_t g = slots[h];
     uint4 w = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
     if (g != 0xFFFFFFFFu) {
         const uint4 e = pods[g];
-        w = make_uint4(e.x, e.y, g | (e.w & 0x80000000u), e.z | ((e.w & 0x7FFFFFFFu) == 0 ? 0x80000000u : 0u));
+        const uint32_t phys = (phys_bits[e.y >> 5] >> (e.y & 31)) & 1u;
+        w = make_uint4(e.x, e.y, g | (e.w & POD_SPEC_NIL) | (phys ? POD_PHYSICAL : 0u),
+                       e.z | ((e.w & 0x7FFFFFFFu) == 0 ? 0x80000000u : 0u));
     }
     wide[h] = w;
 }
@@ -238,13 +289,23 @@ __global__ void __launch_bounds__(BLOCK) k_vni_ht_build(const uint4* ents, uint3
     }
 }
 
-// getPod(name, ns) (handler.go:27-41) → {g|spec_nil<<31, src_ip|netns_empty<<31}; x = 0xFFFFFFFF
+// getPod(name, ns) (handler.go:27-41) → {g|POD_* flags, src_ip|netns_empty<<31}; x = 0xFFFFFFFF
 // on a miss. Empty slots hold all-ones, which no (ns, name) key equals (ids < 2^31).
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <bool NT = false>
 KD_INLINE uint2 pod_lookup(const DevTables& tb, uint32_t ns, uint32_t name) {
     if (ns == 0xFFFFFFFFu) return make_uint2(0xFFFFFFFFu, 0u);
     uint32_t h = (uint32_t)hash64(((uint64_t)ns << 32) | name) & tb.pod_mask;
     for (;;) {
-        const uint4 w = tb.pod_wide[h];
+        uint4 w;
+        if constexpr (NT) {       // no reuse to speak of: keep L2 for the parsed tables
+            const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(tb.pod_wide) + h);
+            w = make_uint4(v.x, v.y, v.z, v.w);
+        } else {
+            w = tb.pod_wide[h];
+        }
         if (w.x == ns && w.y == name) return make_uint2(w.z, w.w);
         if (w.x == 0xFFFFFFFFu) return make_uint2(0xFFFFFFFFu, 0u);
         h = (h + 1) & tb.pod_mask;
@@ -268,8 +329,9 @@ KD_INLINE uint32_t vni_lookup(const DevTables& tb, uint32_t node, int32_t vni) {
 // per-entry outputs: MakeQdiscs, delLink / addLink / UpdateLinks pure prefix
 // ======================================================================================
 // MakeQdiscs over parsed dictionary entries (common/qdisc.go:20-126 + netlink NewNetem)
-template <bool NTL>
+template <int V>
 KD_INLINE void make_qdisc(const DevLinks& L, uint32_t j, const DevTables& tb, uint32_t* q) {
+    constexpr bool NTL = (V & VAR_NT_LOAD) != 0;
 #pragma unroll
     for (int w = 0; w < 18; ++w) q[w] = 0;
     uint32_t id[KDTN_NPROP];
@@ -284,15 +346,20 @@ KD_INLINE void make_qdisc(const DevLinks& L, uint32_t j, const DevTables& tb, ui
     const uint4 lat = tb.pdur[id[KDTN_P_LATENCY]];
     const uint4 jit = tb.pdur[id[KDTN_P_JITTER]];
     const uint4 rt = tb.prate[id[KDTN_P_RATE]];
-    const uint32_t lco = tb.ppct[id[KDTN_P_LATENCY_CORR]];
-    const uint32_t los = tb.ppct[id[KDTN_P_LOSS]];
-    const uint32_t lsc = tb.ppct[id[KDTN_P_LOSS_CORR]];
-    const uint32_t dup = tb.ppct[id[KDTN_P_DUPLICATE]];
-    const uint32_t dpc = tb.ppct[id[KDTN_P_DUPLICATE_CORR]];
-    const uint32_t rop = tb.ppct[id[KDTN_P_REORDER_PROB]];
-    const uint32_t roc = tb.ppct[id[KDTN_P_REORDER_CORR]];
-    const uint32_t cop = tb.ppct[id[KDTN_P_CORRUPT_PROB]];
-    const uint32_t coc = tb.ppct[id[KDTN_P_CORRUPT_CORR]];
+    // (VAR_SKIP_PCT: profiling only, wrong results) the id stands in for the parsed value
+    auto pct = [&](int k) -> uint32_t {
+        if constexpr ((V & VAR_SKIP_PCT) != 0) return id[k];
+        else return tb.ppct[id[k]];
+    };
+    const uint32_t lco = pct(KDTN_P_LATENCY_CORR);
+    const uint32_t los = pct(KDTN_P_LOSS);
+    const uint32_t lsc = pct(KDTN_P_LOSS_CORR);
+    const uint32_t dup = pct(KDTN_P_DUPLICATE);
+    const uint32_t dpc = pct(KDTN_P_DUPLICATE_CORR);
+    const uint32_t rop = pct(KDTN_P_REORDER_PROB);
+    const uint32_t roc = pct(KDTN_P_REORDER_CORR);
+    const uint32_t cop = pct(KDTN_P_CORRUPT_PROB);
+    const uint32_t coc = pct(KDTN_P_CORRUPT_CORR);
     uint32_t err = 0;                            // first failing parse, reference order
     if (lat.z) err = KDTN_E_LATENCY;
     else if (lco == PCT_ERR) err = KDTN_E_LATENCY_CORR;
@@ -339,9 +406,6 @@ KD_INLINE void make_qdisc(const DevLinks& L, uint32_t j, const DevTables& tb, ui
     q[17] = 1u | (has_tbf << 8);                 // has_netem, has_tbf, err = 0
 }
 
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
 template <int V>
 KD_INLINE void store_qdisc(uint2* dst, const uint32_t* q) {
     if constexpr ((V & VAR_NO_QSTORE) != 0) {
@@ -385,11 +449,15 @@ KD_INLINE uint4 pack_res(uint32_t peer, int32_t vni, uint32_t vtep, uint32_t kin
     return make_uint4(peer, (uint32_t)vni, vtep, kind | (err << 8) | (hit << 16));
 }
 
-// MakeVeth(netns, intf, ip, mac) validity from key-string flags (common/veth.go:21-36)
-KD_INLINE uint32_t veth_err(const uint8_t* kf, uint32_t ip, uint32_t mac, uint32_t ecidr,
+KD_INLINE bool kbit(const DevTables& tb, int set, uint32_t id) {
+    return (tb.kbits[(size_t)set * tb.kb_words + (id >> 5)] >> (id & 31)) & 1u;
+}
+
+// MakeVeth(netns, intf, ip, mac) validity from key-string predicates (common/veth.go:21-36)
+KD_INLINE uint32_t veth_err(const DevTables& tb, uint32_t ip, uint32_t mac, uint32_t ecidr,
                             uint32_t emac) {
-    if (kf[ip] & KF_CIDR_BAD) return ecidr;
-    if (kf[mac] & KF_MAC_BAD) return emac;
+    if (kbit(tb, KB_CIDR_BAD, ip)) return ecidr;
+    if (kbit(tb, KB_MAC_BAD, mac)) return emac;
     return 0;
 }
 
@@ -409,7 +477,7 @@ KD_INLINE void emit_del(const DevLinks& O, uint32_t i, const TopoCtx& tc, const 
     store_idx<V>(out.del_idx + e, i);
     if (!res) return;
     const int32_t vni = vni_of(tb.vxlan_base, O.uid_s<NTL>(i));
-    const uint32_t err = veth_err(tb.kflags, O.key_s<NTL>(KDTN_K_LOCAL_IP, i), O.key_s<NTL>(KDTN_K_LOCAL_MAC, i),
+    const uint32_t err = veth_err(tb, O.key_s<NTL>(KDTN_K_LOCAL_IP, i), O.key_s<NTL>(KDTN_K_LOCAL_MAC, i),
                                   KDTN_E_VETH_CIDR, KDTN_E_VETH_MAC);
     uint32_t hit = 0;
     if (!err) hit = vni_lookup(tb, tc.src, vni) == tc.netns;
@@ -423,10 +491,10 @@ KD_INLINE void emit_upd(const DevLinks& N, uint32_t j, const DevTables& tb, cons
     constexpr bool NTL = (V & VAR_NT_LOAD) != 0;
     store_idx<V>(out.upd_idx + e, j);
     if (!res && !qd) return;
-    make_qdisc<NTL>(N, j, tb, q);
+    make_qdisc<V>(N, j, tb, q);
     if (res) {
         const int32_t vni = vni_of(tb.vxlan_base, N.uid_s<NTL>(j));
-        uint32_t err = veth_err(tb.kflags, N.key_s<NTL>(KDTN_K_LOCAL_IP, j), N.key_s<NTL>(KDTN_K_LOCAL_MAC, j),
+        uint32_t err = veth_err(tb, N.key_s<NTL>(KDTN_K_LOCAL_IP, j), N.key_s<NTL>(KDTN_K_LOCAL_MAC, j),
                                 KDTN_E_VETH_CIDR, KDTN_E_VETH_MAC);
         if (!err) err = (q[17] >> 16) & 0xFF;
         store_res<V>(out.upd_res + e, pack_res(0xFFFFFFFFu, vni, 0, 0, err, 0));
@@ -439,45 +507,51 @@ KD_INLINE void emit_add(const DevLinks& N, uint32_t j, const TopoCtx& tc, const 
                         const RecOut& out, uint32_t e, bool res, bool qd, uint32_t* q) {
     constexpr bool NTL = (V & VAR_NT_LOAD) != 0;
     store_idx<V>(out.add_idx + e, j);
-    if (qd) make_qdisc<NTL>(N, j, tb, q);
+    if (qd) make_qdisc<V>(N, j, tb, q);
     if (!res) return;
     const int32_t vni = vni_of(tb.vxlan_base, N.uid_s<NTL>(j));
-    uint32_t err = veth_err(tb.kflags, N.key_s<NTL>(KDTN_K_LOCAL_IP, j), N.key_s<NTL>(KDTN_K_LOCAL_MAC, j),
+    uint32_t err = veth_err(tb, N.key_s<NTL>(KDTN_K_LOCAL_IP, j), N.key_s<NTL>(KDTN_K_LOCAL_MAC, j),
                             KDTN_E_VETH_CIDR, KDTN_E_VETH_MAC);                          // :327
     uint32_t kind = 0, peer = 0xFFFFFFFFu, vtep = 0, hit = 0;
     if (!err) {
         const uint32_t pp = N.key_s<NTL>(KDTN_K_PEER_POD, j);
-        const uint8_t pf = tb.kflags[pp];
-        if (pf & KF_LOCALHOST) {
+        // Reference order: localhost (:333), "physical/" prefix (:348), getPod (:375). The
+        // lookup is pure, so it is done first: a hit carries the PHYSICAL bit of the pod's
+        // name, only a miss reads the key-string bitset.
+        uint2 p = make_uint2(0xFFFFFFFFu, 0u);
+        const bool lh = pp == tb.special[SPECIAL_LOCALHOST];
+        if (!lh) {
+            const uint32_t lns = tc.ns == 0 ? tb.special[SPECIAL_DEFAULT] : tc.ns;      // :29-31
+            if constexpr ((V & VAR_SKIP_POD) != 0) p = make_uint2(pp & POD_INDEX, lns);   // profiling only
+            else p = pod_lookup<(V & VAR_NT_POD) != 0>(tb, lns, pp);
+        }
+        const bool miss = p.x == 0xFFFFFFFFu;
+        if (lh) {
             kind = KDTN_KIND_MACVLAN;                                                     // :333
-        } else if (pf & KF_PHYSICAL) {
+        } else if (miss ? kbit(tb, KB_PHYSICAL, pp) : (p.x & POD_PHYSICAL) != 0) {
             kind = KDTN_KIND_PHYSICAL;                                                    // :348
             vtep = pp;
             const uint32_t nsx = vni_lookup(tb, tc.src, vni);                           // :177-179
             hit = (nsx != 0xFFFFFFFFu && nsx != tc.netns);
+        } else if (miss) {
+            err = KDTN_E_PEER_LOOKUP;                                                     // :375-379
         } else {
-            const uint32_t lns = tc.ns == 0 ? *tb.default_id : tc.ns;                   // :29-31
-            const uint2 p = pod_lookup(tb, lns, pp);                                     // :375
-            if (p.x == 0xFFFFFFFFu) {
-                err = KDTN_E_PEER_LOOKUP;
+            peer = p.x & POD_INDEX;
+            const uint32_t p_src = p.y & 0x7FFFFFFFu;
+            if (p.x & POD_SPEC_NIL) {
+                err = KDTN_E_PEER_NO_LINKS;                                               // :380-384
+            } else if (p_src == 0 || (p.y & 0x80000000u)) {
+                kind = KDTN_KIND_PEER_DEAD;                                               // :386-395
+            } else if (p_src == tc.src) {
+                kind = KDTN_KIND_SAME_NODE;                                               // :399-418
+                err = veth_err(tb, N.key_s<NTL>(KDTN_K_PEER_IP, j), N.key_s<NTL>(KDTN_K_PEER_MAC, j),
+                               KDTN_E_PEER_VETH_CIDR, KDTN_E_PEER_VETH_MAC);
             } else {
-                peer = p.x & 0x7FFFFFFFu;
-                const uint32_t p_src = p.y & 0x7FFFFFFFu;
-                if (p.x & 0x80000000u) {
-                    err = KDTN_E_PEER_NO_LINKS;                                           // :380-384
-                } else if (p_src == 0 || (p.y & 0x80000000u)) {
-                    kind = KDTN_KIND_PEER_DEAD;                                           // :386-395
-                } else if (p_src == tc.src) {
-                    kind = KDTN_KIND_SAME_NODE;                                           // :399-418
-                    err = veth_err(tb.kflags, N.key_s<NTL>(KDTN_K_PEER_IP, j), N.key_s<NTL>(KDTN_K_PEER_MAC, j),
-                                   KDTN_E_PEER_VETH_CIDR, KDTN_E_PEER_VETH_MAC);
-                } else {
-                    kind = KDTN_KIND_CROSS_NODE;                                          // :419-453
-                    vtep = p_src;
-                    if (tb.vni_mask) {                                   // remote Update check
-                        const uint32_t nsx = vni_lookup(tb, p_src, vni);
-                        hit = (nsx != 0xFFFFFFFFu && nsx != (tb.pods[peer].w & 0x7FFFFFFFu));
-                    }
+                kind = KDTN_KIND_CROSS_NODE;                                              // :419-453
+                vtep = p_src;
+                if (tb.vni_mask) {                                       // remote Update check
+                    const uint32_t nsx = vni_lookup(tb, p_src, vni);
+                    hit = (nsx != 0xFFFFFFFFu && nsx != (tb.pods[peer].w & 0x7FFFFFFFu));
                 }
             }
         }
@@ -729,14 +803,31 @@ __device__ void lookback(RecShared& s, const RecWork& wk, uint32_t wg) {
     __syncthreads();
 }
 
+// (VAR_TRACE) phase timestamp of this workgroup: 100 MHz chip-wide clock
+template <int V>
+KD_INLINE void trace_mark(const RecWork& wk, uint32_t wg, int k, unsigned long long t0 = 0) {
+    if constexpr ((V & VAR_TRACE) != 0) {
+        if (threadIdx.x == 0) wk.trace[(size_t)wg * TRACE_WORDS + k] = t0 ? t0 : __builtin_amdgcn_s_memrealtime();
+    }
+}
+
 template <int V>
 __global__ void __launch_bounds__(BLOCK) k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb,
                                                      RecOut out, RecWork wk) {
     __shared__ RecShared s;
     const int tid = threadIdx.x;
+    unsigned long long t_entry = 0;
+    if constexpr ((V & VAR_TRACE) != 0) t_entry = __builtin_amdgcn_s_memrealtime();
     if (tid == 0) s.ticket = atomicAdd(&wk.sync[0], 1u);    // dispatch order → look-back order
     __syncthreads();
     const uint32_t wg = s.ticket;
+    if constexpr ((V & VAR_TRACE) != 0) {
+        trace_mark<V>(wk, wg, 0, t_entry);
+        uint32_t xcc, hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        if (tid == 0) wk.trace[(size_t)wg * TRACE_WORDS + 5] = ((unsigned long long)xcc << 32) | hw;
+    }
     const uint32_t t0 = wg * TPW;
     const int nt = (int)min((uint32_t)TPW, T.n - t0);
     if (tid <= nt) {
@@ -756,6 +847,7 @@ __global__ void __launch_bounds__(BLOCK) k_reconcile(DevTopos T, DevLinks O, Dev
         s.tcnt[2][tid] = 0;
     }
     __syncthreads();
+    trace_mark<V>(wk, wg, 1);
     const uint32_t o0 = s.ooff[0], o1 = s.ooff[nt], n0 = s.noff[0], n1 = s.noff[nt];
     const uint32_t no = o1 - o0, nn = n1 - n0, tot = no + nn;
     const bool fast = tot <= (uint32_t)CAP;
@@ -847,7 +939,9 @@ __global__ void __launch_bounds__(BLOCK) k_reconcile(DevTopos T, DevLinks O, Dev
     __syncthreads();
 
     // ---- 3. batch bases: decoupled look-back -------------------------------------------
+    trace_mark<V>(wk, wg, 2);
     lookback(s, wk, wg);
+    trace_mark<V>(wk, wg, 3);
     const uint32_t bd = s.base[0], bu = s.base[1], ba = s.base[2];
     if (wg == wk.nwg - 1 && tid < 3) {
         const uint32_t total = s.base[tid] + s.wtot[tid];
@@ -885,6 +979,7 @@ __global__ void __launch_bounds__(BLOCK) k_reconcile(DevTopos T, DevLinks O, Dev
             }
             wave_store_qdisc<V>(out.add_qdisc, qa, e, q, stage);
         }
+        trace_mark<V>(wk, wg, 4);
         return;
     }
     if (fast) {
@@ -911,6 +1006,7 @@ __global__ void __launch_bounds__(BLOCK) k_reconcile(DevTopos T, DevLinks O, Dev
             wave_store_qdisc<V>(out.add_qdisc, qa, e, q, stage);
             wave_store_qdisc<V>(out.upd_qdisc, qu, e, q, stage);
         }
+        trace_mark<V>(wk, wg, 4);
         return;
     }
     // slow path: chunked, order-preserving compaction of the flags in global scratch
@@ -964,6 +1060,7 @@ __global__ void __launch_bounds__(BLOCK) k_reconcile(DevTopos T, DevLinks O, Dev
             __syncthreads();
         }
     }
+    trace_mark<V>(wk, wg, 4);
 }
 
 // Standalone MakeQdiscs over a batch of property sets (kdtn_make_qdiscs).
@@ -971,7 +1068,7 @@ __global__ void __launch_bounds__(BLOCK) k_qdisc_batch(DevLinks props, DevTables
     const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
     if (j >= props.n) return;
     uint32_t q[18];
-    make_qdisc<false>(props, j, tb, q);
+    make_qdisc<0>(props, j, tb, q);
     store_qdisc<0>(out + (size_t)j * 9, q);
 }
 
@@ -981,5 +1078,11 @@ template __global__ void k_reconcile<2>(DevTopos, DevLinks, DevLinks, DevTables,
 template __global__ void k_reconcile<3>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
 template __global__ void k_reconcile<4>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
 template __global__ void k_reconcile<5>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
+template __global__ void k_reconcile<9>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
+template __global__ void k_reconcile<11>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
+template __global__ void k_reconcile<17>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
+template __global__ void k_reconcile<33>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
+template __global__ void k_reconcile<65>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
+template __global__ void k_reconcile<97>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
 
 }  // namespace kdtn

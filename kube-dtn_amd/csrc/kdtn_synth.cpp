@@ -467,11 +467,13 @@ void build_config4(Synth& S, uint64_t seed, uint32_t sites_per_shard, uint32_t s
             close_topo(S);
         }
     }
-    // a VxlanManager snapshot: every 50th cross-node link already has a VNI on its node
-    for (size_t j = 0; j < S.des.size(); j += 50) {
-        S.v_node.push_back(S.id_node0 + (uint32_t)(j % 256));
-        S.v_vni.push_back((int32_t)(5000 + S.des.uid[j]));
-        S.v_netns.push_back(S.id_netns0 + (uint32_t)(hmix(seed, j) % total));
+    // a VxlanManager snapshot (node-global daemon state, identical on every shard): every
+    // 50th edge of the whole graph already has a VNI on some node
+    const uint64_t n_edges_all = (uint64_t)n_ns * edges_per_ns;
+    for (uint64_t ge = 0; ge < n_edges_all; ge += 50) {
+        S.v_node.push_back(S.id_node0 + (uint32_t)(ge % 256));
+        S.v_vni.push_back((int32_t)(5000 + ge + 1));
+        S.v_netns.push_back(S.id_netns0 + (uint32_t)(hmix(seed, ge) % total));
     }
 }
 

@@ -63,6 +63,7 @@ def lib() -> C.CDLL:
         "kdtn_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8 * 128)]),
         "kdtn_comm_init": (C.c_int, [vp, C.POINTER(C.c_uint8 * 128), C.c_int, C.c_int]),
         "kdtn_last_kernel_times": (C.c_int, [vp, C.POINTER(C.c_char_p), C.POINTER(C.c_float), C.c_int]),
+        "kdtn_debug_wg_trace": (C.c_int, [vp, C.POINTER(C.c_uint64), C.c_uint32]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -158,6 +159,15 @@ class Engine:
         ms = (C.c_float * 16)()
         n = lib().kdtn_last_kernel_times(self._ctx, names, ms, 16)
         return {names[i].decode(): float(ms[i]) for i in range(max(n, 0))}
+
+    def wg_trace(self) -> np.ndarray:
+        """(nwg, 6) uint64 phase timestamps of the last traced run (KDTN_VARIANT bit 16)."""
+        cap = 1 << 26
+        buf = np.zeros(cap, np.uint64)
+        n = lib().kdtn_debug_wg_trace(self._ctx, buf.ctypes.data_as(C.POINTER(C.c_uint64)), cap)
+        if n < 0:
+            raise KdtnError(n, "kdtn_debug_wg_trace")
+        return buf[:n].reshape(-1, 6)
 
     # ---- MakeQdiscs batch --------------------------------------------------------------
     def make_qdiscs(self, pdict: StrTab, prop: np.ndarray, gap: np.ndarray) -> np.ndarray:

@@ -124,6 +124,54 @@ def test_cidr_mac_via_epoch(engine):
     assert {0, abi.E_VETH_CIDR, abi.E_VETH_MAC, abi.E_PEER_VETH_CIDR} <= errs
 
 
+def _mutate(rng: random.Random, s: str, alphabet: str) -> str:
+    s = list(s)
+    for _ in range(rng.randint(0, 3)):
+        op = rng.randint(0, 2)
+        k = rng.randint(0, len(s))
+        if op == 0:
+            s.insert(k, rng.choice(alphabet))
+        elif op == 1 and s:
+            del s[min(k, len(s) - 1)]
+        elif s:
+            s[min(k, len(s) - 1)] = rng.choice(alphabet)
+    return "".join(s)
+
+
+def test_key_predicates_fuzz(engine):
+    """net.ParseCIDR / net.ParseMAC / localhost / physical/ predicates of key strings (the
+    register fast path of k_kdict_flags and its generic fallback) against the oracle."""
+    rng = random.Random(11)
+    ipa, maca = "0123456789./:", "0123456789abcdefABCDEFG:-."
+    ips = [f"{rng.randint(0, 300)}.{rng.randint(0, 300)}.{rng.randint(0, 300)}.{rng.randint(0, 300)}"
+           f"/{rng.choice(['', '0', '00', '032', '33', str(rng.randint(0, 40))])}" for _ in range(800)]
+    ips += [_mutate(rng, rng.choice(ips), ipa) for _ in range(1500)]
+    ips += ["".join(rng.choice(ipa) for _ in range(rng.randint(0, 30))) for _ in range(700)]
+    ips += ["0" * 30 + "1.2.3.4/8", "1.2.3.4/" + "0" * 25 + "8", "255.255.255.255/32", "1.2.3.4/32x"]
+    macs = [":".join(f"{rng.randint(0, 255):02x}" for _ in range(rng.choice([6, 8, 20])))
+            for _ in range(300)]
+    macs += [_mutate(rng, rng.choice(macs), maca) for _ in range(700)]
+    macs += ["".join(rng.choice(maca) for _ in range(rng.randint(10, 26))) for _ in range(300)]
+    peers = ["b", "localhost", "localhos", "localhostx", "physical/10.0.0.9", "physical/", "physical",
+             "Physical/1"]
+    links = []
+    uid = 1
+    for ip in ips:
+        links.append(Link("eth0", ip, "", "eth1", "", "", rng.choice(peers), uid))
+        uid += 1
+    for mac in macs:
+        links.append(Link("eth0", "10.0.0.1/24", mac, "eth1", "", "", rng.choice(peers), uid))
+        uid += 1
+    topos = [Topology("a", "default", links, [], "10.0.0.1", "/ns/a"),
+             Topology("b", "default", [], [], "10.0.0.2", "/ns/b")]
+    inp = pack(topos)
+    out = engine.reconcile(inp)
+    assert_same(out, O.reconcile(inp, tick=TICK), "key predicates")
+    errs = out.add_res["err"]
+    assert (errs == abi.E_VETH_CIDR).sum() > 100 and (errs == abi.E_VETH_MAC).sum() > 100
+    assert (errs == 0).sum() > 100
+
+
 @pytest.mark.parametrize("cfg,pods", [(1, 0), (2, 20000), (3, 20000), (4, 5000)])
 def test_synthetic_configs_small(engine, cfg, pods):
     inp = synth.make(cfg, pods_per_shard=pods) if pods else synth.make(cfg)
