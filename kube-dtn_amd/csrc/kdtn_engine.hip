@@ -47,8 +47,8 @@ uint32_t next_pow2(uint64_t x) {
 
 }  // namespace
 
-// Link table storage: 20 u32 columns + the i64 uid column carved from one allocation at a
-// fixed column stride, so kernels receive one base pointer per table.
+// Link table storage: one allocation in 64-record tiles (AoSoA, kdtn_kernels.h), so kernels
+// receive one base pointer per table.
 struct DevLinkStore {
     DevBuf buf;
     uint32_t n = 0;
@@ -61,7 +61,7 @@ struct kdtn_ctx {
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
     // dictionaries
-    DevBuf kd_bytes, kd_offs, kd_bits, pd_bytes, pd_offs, pd_pct, pd_dur, pd_rate;
+    DevBuf kd_bytes, kd_offs, kd_bits, pd_bytes, pd_offs, pd_pct, pd_dur, pd_rate, pd_rerr;
     uint32_t D = 0, P = 0;
     // topologies
     DevBuf t_ns, t_name, t_src, t_netns, t_flags, t_roff, t_noff;
@@ -206,21 +206,30 @@ int upload_links(kdtn_ctx* c, DevLinkStore& s, const kdtn_link_table& L, uint32_
         std::snprintf(g_last_error, sizeof(g_last_error), "%s: missing uid/gap", what);
         return KDTN_EINVAL;
     }
-    const uint64_t stride = align_up((size_t)std::max<uint32_t>(n, 1), 64);   // u32 elements
-    const size_t total = (size_t)stride * 4 * (LINK_COLS32 + 2);
-    TRY(ensure(s.buf, total));
-    uint32_t* base = static_cast<uint32_t*>(s.buf.p);
-    auto col = [&](int c) { return base + (size_t)c * stride; };
+    // tiles of 64 records (kdtn_kernels.h DevLinks): each column is a 2-D copy with a
+    // 256-B (uid: 512-B) run per tile
+    const size_t tiles = ((size_t)std::max<uint32_t>(n, 1) + TILE_RECS - 1) / TILE_RECS;
+    const size_t tile_bytes = (size_t)TILE_WORDS * 4;
+    TRY(ensure(s.buf, tiles * tile_bytes));
+    uint8_t* base = static_cast<uint8_t*>(s.buf.p);
+    auto put = [&](int col, const void* src, size_t esz) -> int {
+        const size_t full = n / TILE_RECS, tail = n % TILE_RECS;
+        const size_t run = TILE_RECS * esz;
+        uint8_t* dst = base + (size_t)col * TILE_RECS * 4;
+        if (full)
+            HIP_TRY(hipMemcpy2DAsync(dst, tile_bytes, src, run, run, full, hipMemcpyHostToDevice, c->stream));
+        if (tail)
+            HIP_TRY(hipMemcpyAsync(dst + full * tile_bytes, static_cast<const uint8_t*>(src) + full * run,
+                                   tail * esz, hipMemcpyHostToDevice, c->stream));
+        return KDTN_OK;
+    };
     if (n) {
-        for (int k = 0; k < KDTN_NKEY; ++k)
-            HIP_TRY(hipMemcpyAsync(col(COL_KEY0 + k), L.key[k], (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
-        for (int k = 0; k < KDTN_NPROP; ++k)
-            HIP_TRY(hipMemcpyAsync(col(COL_PROP0 + k), L.prop[k], (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
-        HIP_TRY(hipMemcpyAsync(col(COL_GAP), L.gap, (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
-        HIP_TRY(hipMemcpyAsync(col(COL_UID), L.uid, (size_t)n * 8, hipMemcpyHostToDevice, c->stream));
+        for (int k = 0; k < KDTN_NKEY; ++k) TRY(put(COL_KEY0 + k, L.key[k], 4));
+        for (int k = 0; k < KDTN_NPROP; ++k) TRY(put(COL_PROP0 + k, L.prop[k], 4));
+        TRY(put(COL_GAP, L.gap, 4));
+        TRY(put(COL_UID, L.uid, 8));
     }
-    s.view.base = base;
-    s.view.stride = stride;
+    s.view.base = reinterpret_cast<const uint32_t*>(base);
     s.view.n = n;
     s.n = n;
     return KDTN_OK;
@@ -334,7 +343,7 @@ void kdtn_destroy(kdtn_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     DevBuf* bufs[] = {&c->kd_bytes, &c->kd_offs, &c->kd_bits, &c->pd_bytes, &c->pd_offs,
-                      &c->pd_pct, &c->pd_dur, &c->pd_rate, &c->t_ns, &c->t_name, &c->t_src,
+                      &c->pd_pct, &c->pd_dur, &c->pd_rate, &c->pd_rerr, &c->t_ns, &c->t_name, &c->t_src,
                       &c->t_netns, &c->t_flags, &c->t_roff, &c->t_noff, &c->real.buf, &c->des.buf,
                       &c->v_node, &c->v_vni, &c->v_netns, &c->v_ents, &c->v_slots, &c->pods,
                       &c->pod_slots, &c->pod_wide, &c->otarget, &c->sync, &c->misc, &c->hscratch,
@@ -396,8 +405,9 @@ int kdtn_epoch_upload(kdtn_ctx* c, const kdtn_epoch_in* in) {
     TRY(upload_arena(c, c->pd_bytes, in->pdict.bytes, in->pdict.offs[P]));
     TRY(upload(c, c->pd_offs, in->pdict.offs, (size_t)(P + 1) * 4));
     TRY(ensure(c->pd_pct, (size_t)P * 4));
-    TRY(ensure(c->pd_dur, (size_t)P * 16));
-    TRY(ensure(c->pd_rate, (size_t)P * 16));
+    TRY(ensure(c->pd_dur, (size_t)P * 8));
+    TRY(ensure(c->pd_rate, (size_t)P * 8));
+    TRY(ensure(c->pd_rerr, (size_t)nblocks(P) * BLOCK / 8));
 
     TRY(upload(c, c->t_ns, T.ns, (size_t)T.n * 4));
     TRY(upload(c, c->t_name, T.name, (size_t)T.n * 4));
@@ -476,7 +486,7 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
     timer_mark(c, "kdict_parse");
     if (c->P) k_pdict_parse<<<nblocks(c->P), BLOCK, 0, s>>>(dp<uint8_t>(c->pd_bytes), dp<uint32_t>(c->pd_offs),
                                                          c->P, c->cfg.tick_in_usec, dp<uint32_t>(c->pd_pct),
-                                                         dp<uint4>(c->pd_dur), dp<uint4>(c->pd_rate));
+                                                         dp<uint2>(c->pd_dur), dp<uint2>(c->pd_rate), dp<uint32_t>(c->pd_rerr));
     timer_mark(c, "pdict_parse");
     const bool resolve = stages & KDTN_STAGE_RESOLVE;
     if (resolve) {
@@ -515,8 +525,9 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         tb.kbits = dp<uint32_t>(c->kd_bits);
         tb.kb_words = c->kb_words;
         tb.ppct = dp<uint32_t>(c->pd_pct);
-        tb.pdur = dp<uint4>(c->pd_dur);
-        tb.prate = dp<uint4>(c->pd_rate);
+        tb.pdur = dp<uint2>(c->pd_dur);
+        tb.prate = dp<uint2>(c->pd_rate);
+        tb.rate_err = dp<uint32_t>(c->pd_rerr);
         tb.pods = dp<uint4>(c->pods);
         tb.pod_wide = dp<uint4>(c->pod_wide);
         tb.pod_mask = c->pod_mask;
@@ -564,6 +575,8 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         case 9: k_reconcile<9><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
         case 33: k_reconcile<33><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
         case 65: k_reconcile<65><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
+        case 101: k_reconcile<101><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
+        case 113: k_reconcile<113><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
         case 97: k_reconcile<97><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
         case 17: k_reconcile<17><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
         case 11: k_reconcile<11><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
@@ -654,8 +667,9 @@ int kdtn_make_qdiscs(kdtn_ctx* c, const kdtn_strtab* pdict, const kdtn_props_tab
     TRY(upload_arena(c, c->pd_bytes, pdict->bytes, pdict->offs[P]));
     TRY(upload(c, c->pd_offs, pdict->offs, (size_t)(P + 1) * 4));
     TRY(ensure(c->pd_pct, (size_t)P * 4));
-    TRY(ensure(c->pd_dur, (size_t)P * 16));
-    TRY(ensure(c->pd_rate, (size_t)P * 16));
+    TRY(ensure(c->pd_dur, (size_t)P * 8));
+    TRY(ensure(c->pd_rate, (size_t)P * 8));
+    TRY(ensure(c->pd_rerr, (size_t)nblocks(P) * BLOCK / 8));
     // reuse the desired-link store for the property columns
     kdtn_link_table L{};
     L.n = n;
@@ -670,11 +684,12 @@ int kdtn_make_qdiscs(kdtn_ctx* c, const kdtn_strtab* pdict, const kdtn_props_tab
     hipStream_t s = c->stream;
     k_pdict_parse<<<nblocks(P), BLOCK, 0, s>>>(dp<uint8_t>(c->pd_bytes), dp<uint32_t>(c->pd_offs), P,
                                                c->cfg.tick_in_usec, dp<uint32_t>(c->pd_pct),
-                                               dp<uint4>(c->pd_dur), dp<uint4>(c->pd_rate));
+                                               dp<uint2>(c->pd_dur), dp<uint2>(c->pd_rate), dp<uint32_t>(c->pd_rerr));
     DevTables tb{};
     tb.ppct = dp<uint32_t>(c->pd_pct);
-    tb.pdur = dp<uint4>(c->pd_dur);
-    tb.prate = dp<uint4>(c->pd_rate);
+    tb.pdur = dp<uint2>(c->pd_dur);
+    tb.prate = dp<uint2>(c->pd_rate);
+    tb.rate_err = dp<uint32_t>(c->pd_rerr);
     if (n) k_qdisc_batch<<<nblocks(n), BLOCK, 0, s>>>(c->des.view, tb, dp<uint2>(c->add_qdisc));
     HIP_TRY(hipGetLastError());
     if (n) HIP_TRY(hipMemcpyAsync(out, c->add_qdisc.p, (size_t)n * 72, hipMemcpyDeviceToHost, s));

@@ -1,7 +1,7 @@
 // kdtn_kernels.h — HIP kernels of one reconcile epoch (gfx950 / CDNA4, wave64).
 //
 // Data layout in HBM (struct-of-arrays, records grouped by Topology):
-//   link table   : ONE allocation per side, 21 columns at a fixed stride:
+//   link table   : ONE allocation per side in tiles of 64 records (AoSoA, see DevLinks):
 //                  key[0..6] (u32 kdict ids) | prop[0..11] (u32 pdict ids) | gap (u32) | uid (i64)
 //                  → 88 B per record, one base pointer per table in the kernel arguments
 //   topologies   : u32 ns/name/src_ip/net_ns ids, u8 flags, u32 offsets (T+1) per side
@@ -55,38 +55,47 @@ constexpr uint32_t POD_SPEC_NIL = 0x80000000u, POD_PHYSICAL = 0x40000000u, POD_I
 // record flags
 enum : uint8_t { RF_DEL = 1, RF_UPD = 2, RF_ADD = 4 };
 
-// column indices of the link store
+// Link store: tiles of 64 records (AoSoA). A tile holds, for its 64 records, each u32 column
+// as 256 contiguous bytes (key[0..6], prop[0..11], gap) followed by the i64 uid column
+// (512 B): 5,632 B per tile. A wave's column load is one 256-B run, and every column of a
+// record is a fixed immediate offset from one per-record pointer (no per-column base
+// registers).
 enum { COL_KEY0 = 0, COL_PROP0 = KDTN_NKEY, COL_GAP = KDTN_NKEY + KDTN_NPROP, COL_UID = COL_GAP + 1 };
-constexpr int LINK_COLS32 = COL_UID;   // u32 columns before the i64 uid column
+constexpr int LINK_COLS32 = COL_UID;               // u32 columns before the i64 uid column
+constexpr int TILE_RECS = 64;
+constexpr int TILE_WORDS = (LINK_COLS32 + 2) * TILE_RECS;   // 1,408 u32 = 5,632 B
 
 struct DevLinks {
-    const uint32_t* base;   // column c at base + c*stride; uid (i64) at base + COL_UID*stride
-    uint64_t stride;        // u32 elements per column (multiple of 64)
+    const uint32_t* base;   // tile t at base + t*TILE_WORDS
     uint32_t n;
-    __device__ __forceinline__ uint32_t key(int k, uint32_t i) const { return base[(uint64_t)k * stride + i]; }
-    __device__ __forceinline__ uint32_t prop(int k, uint32_t i) const { return base[(uint64_t)(COL_PROP0 + k) * stride + i]; }
-    __device__ __forceinline__ uint32_t gap(uint32_t i) const { return base[(uint64_t)COL_GAP * stride + i]; }
-    __device__ __forceinline__ int64_t uid(uint32_t i) const {
-        return reinterpret_cast<const int64_t*>(base + (uint64_t)COL_UID * stride)[i];
+    // word 0 of record i's tile row: column c of record i at rec(i)[c*64]
+    __device__ __forceinline__ const uint32_t* rec(uint32_t i) const {
+        return base + (size_t)(i >> 6) * TILE_WORDS + (i & 63u);
     }
-    // streaming (read-once) forms; NT = non-temporal, so they do not evict lookup tables
-    template <bool NT> __device__ __forceinline__ uint32_t ld32(uint64_t off) const {
-        if constexpr (NT) return __builtin_nontemporal_load(base + off);
-        else return base[off];
+    template <bool NT> __device__ __forceinline__ uint32_t col(const uint32_t* r, int c) const {
+        if constexpr (NT) return __builtin_nontemporal_load(r + c * TILE_RECS);
+        else return r[c * TILE_RECS];
     }
-    template <bool NT> __device__ __forceinline__ uint32_t key_s(int k, uint32_t i) const {
-        return ld32<NT>((uint64_t)k * stride + i);
-    }
-    template <bool NT> __device__ __forceinline__ uint32_t prop_s(int k, uint32_t i) const {
-        return ld32<NT>((uint64_t)(COL_PROP0 + k) * stride + i);
-    }
-    template <bool NT> __device__ __forceinline__ uint32_t gap_s(uint32_t i) const {
-        return ld32<NT>((uint64_t)COL_GAP * stride + i);
-    }
-    template <bool NT> __device__ __forceinline__ int64_t uid_s(uint32_t i) const {
-        const int64_t* p = reinterpret_cast<const int64_t*>(base + (uint64_t)COL_UID * stride) + i;
+    template <bool NT> __device__ __forceinline__ int64_t uid_at(const uint32_t* r, uint32_t i) const {
+        const int64_t* p = reinterpret_cast<const int64_t*>(r - (i & 63u) + COL_UID * TILE_RECS) + (i & 63u);
         if constexpr (NT) return __builtin_nontemporal_load(p);
         else return *p;
+    }
+    __device__ __forceinline__ uint32_t key(int k, uint32_t i) const { return rec(i)[(COL_KEY0 + k) * TILE_RECS]; }
+    __device__ __forceinline__ uint32_t prop(int k, uint32_t i) const { return rec(i)[(COL_PROP0 + k) * TILE_RECS]; }
+    __device__ __forceinline__ uint32_t gap(uint32_t i) const { return rec(i)[COL_GAP * TILE_RECS]; }
+    __device__ __forceinline__ int64_t uid(uint32_t i) const { return uid_at<false>(rec(i), i); }
+    template <bool NT> __device__ __forceinline__ uint32_t key_s(int k, uint32_t i) const {
+        return col<NT>(rec(i), COL_KEY0 + k);
+    }
+    template <bool NT> __device__ __forceinline__ uint32_t prop_s(int k, uint32_t i) const {
+        return col<NT>(rec(i), COL_PROP0 + k);
+    }
+    template <bool NT> __device__ __forceinline__ uint32_t gap_s(uint32_t i) const {
+        return col<NT>(rec(i), COL_GAP);
+    }
+    template <bool NT> __device__ __forceinline__ int64_t uid_s(uint32_t i) const {
+        return uid_at<NT>(rec(i), i);
     }
 };
 
@@ -117,8 +126,9 @@ struct DevTables {             // read-only lookup structures of the epoch
     const uint32_t* kbits;     // [KB_NSETS][kb_words]
     uint32_t kb_words;         // words per bitset (multiple of 2)
     const uint32_t* ppct;      // [P]
-    const uint4* pdur;         // [P] {us, ticks, err, 0}
-    const uint4* prate;        // [P] {lo, hi, err, 0}
+    const uint2* pdur;         // [P] {us, ticks}; DUR_ERR = {0, 1} (time2Tick(0) == 0)
+    const uint2* prate;        // [P] {lo, hi}; all-ones = error or 2^64-1: see rate_err
+    const uint32_t* rate_err;  // [ceil(P/64)*2] bitset: ParseRate failed
     const uint4* pods;         // [pod_total] {ns, name, src_ip, net_ns|spec_nil<<31}
     const uint4* pod_wide;     // [pod_mask+1] {ns, name, g|POD_* flags, src_ip|netns_empty<<31}
     uint32_t pod_mask;
@@ -159,7 +169,7 @@ struct RecWork {
 __global__ void k_kdict_flags(const uint8_t* bytes, const uint32_t* offs, uint32_t n,
                               uint32_t* kbits, uint32_t kb_words, uint32_t* special);
 __global__ void k_pdict_parse(const uint8_t* bytes, const uint32_t* offs, uint32_t n, double tick,
-                              uint32_t* ppct, uint4* pdur, uint4* prate);
+                              uint32_t* ppct, uint2* pdur, uint2* prate, uint32_t* rate_err);
 __global__ void k_pods_fill(DevTopos T, uint32_t slice, uint32_t rank_base, uint4* pods);
 __global__ void k_pod_ht_build(const uint4* pods, uint32_t total, uint32_t* slots, uint32_t mask);
 __global__ void k_pod_ht_expand(const uint4* pods, const uint32_t* slots, const uint32_t* phys_bits,

@@ -92,40 +92,77 @@ KD_INLINE const uint8_t* stage_slice(const uint8_t* bytes, const uint32_t* offs,
 // Word k of a string's first 24 bytes (bytes past the end are garbage; callers mask by len).
 KD_INLINE uint32_t wbyte(const uint32_t* w, int k) { return (w[k >> 2] >> (8 * (k & 3))) & 0xFFu; }
 
-// net.ParseCIDR validity for a string of <= 24 bytes without ':' (so not IPv6; common/veth.go:22),
-// branch-free over the register image: 4 dotted octets (1-3 digits, no leading zero, <= 255),
-// '/', then >= 1 digits with value <= 32 (dtoi accepts leading zeros).
-KD_INLINE bool cidr4_regs(const uint32_t* w, uint32_t len) {
-    uint32_t field = 0, nd = 0, val = 0, bad = 0;
+// ---- SWAR character classes over 4 bytes (exact per byte, no compares: pure VALU) ----
+// high bit of each byte set where the byte is an ASCII digit
+KD_INLINE uint32_t swar_digit(uint32_t x) {
+    const uint32_t t = x ^ 0x30303030u;
+    return ~((t | 0x80808080u) - 0x0A0A0A0Au) & ~t & 0x80808080u;
+}
+// high bit of each byte set where the byte equals the byte replicated in `rep`
+KD_INLINE uint32_t swar_eq(uint32_t x, uint32_t rep) {
+    const uint32_t t = x ^ rep;
+    return ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
+}
+// gather the 4 byte-high bits into a nibble (byte k → bit k): the products never overlap
+KD_INLINE uint32_t swar_nib(uint32_t m) { return (((m >> 7) * 0x204081u) >> 21) & 0xFu; }
+// 4 bytes of the string starting at byte q (q <= 19) of the 24-byte register image
+KD_INLINE uint32_t window4(const uint32_t* w, uint32_t q) {
+    const uint32_t i = q >> 2;
+    const uint32_t lo = i == 0 ? w[0] : i == 1 ? w[1] : i == 2 ? w[2] : i == 3 ? w[3] : w[4];
+    const uint32_t hi = i == 0 ? w[1] : i == 1 ? w[2] : i == 2 ? w[3] : i == 3 ? w[4] : w[5];
+    return __builtin_amdgcn_alignbyte(hi, lo, q & 3u);
+}
+// one dotted-quad field of n digits starting with the 4-byte window c: dtoi, <= 255 and no
+// leading zero (net.parseIPv4, Go 1.18)
+KD_INLINE uint32_t octet_ok(uint32_t c, uint32_t n) {
+    const uint32_t d0 = (c & 0xFFu) - '0', d1 = ((c >> 8) & 0xFFu) - '0', d2 = ((c >> 16) & 0xFFu) - '0';
+    const uint32_t v = d0 * 100u + d1 * 10u + d2;
+    return (n >= 1u) & (n <= 3u) & ((n == 1u) | (d0 != 0u)) & ((n != 3u) | (v <= 255u));
+}
+
+// net.ParseCIDR validity from the register image of a string of <= 24 bytes
+// (common/veth.go:22). Decides every string without ':' whose prefix has <= 2 digits;
+// sets *slow for the rest (IPv6 candidates, long prefixes), which take cidr_ok().
+KD_INLINE bool cidr_swar(const uint32_t* w, uint32_t len, bool* slow) {
+    uint32_t D = 0, P = 0, S = 0, C = 0;
 #pragma unroll
-    for (int k = 0; k < 24; ++k) {
-        const uint32_t c = wbyte(w, k);
-        const uint32_t act = (uint32_t)k < len;
-        const uint32_t d = c - '0';
-        const uint32_t isd = d < 10u;
-        const uint32_t oct = field < 4u;
-        // digit in an octet: no digit after a leading '0', at most 3 digits
-        const uint32_t zlead = (nd == 1u) & (val == 0u);
-        const uint32_t bad_d = oct & (zlead | (nd >= 3u));
-        // separator: '.' ends octets 0-2, '/' ends octet 3
-        const uint32_t sep_ok = (nd >= 1u) & (val <= 255u) &
-                                (((c == '.') & (field < 3u)) | ((c == '/') & (field == 3u)));
-        const uint32_t bad_c = isd ? bad_d : (oct ? (sep_ok ^ 1u) : 1u);
-        bad |= act & bad_c;
-        const uint32_t nval = isd ? min(val * 10u + d, 1000u) : 0u;
-        const uint32_t nnd = isd ? nd + 1u : 0u;
-        const uint32_t nfield = isd ? field : field + 1u;
-        val = act ? nval : val;
-        nd = act ? nnd : nd;
-        field = act ? nfield : field;
+    for (int k = 0; k < 6; ++k) {
+        D |= swar_nib(swar_digit(w[k])) << (4 * k);
+        P |= swar_nib(swar_eq(w[k], 0x2E2E2E2Eu)) << (4 * k);   // '.'
+        S |= swar_nib(swar_eq(w[k], 0x2F2F2F2Fu)) << (4 * k);   // '/'
+        C |= swar_nib(swar_eq(w[k], 0x3A3A3A3Au)) << (4 * k);   // ':'
     }
-    return !bad && field == 4u && nd >= 1u && val <= 32u;
+    const uint32_t L = (1u << len) - 1u;
+    D &= L;
+    P &= L;
+    S &= L;
+    C &= L;
+    const uint32_t s = __builtin_ctz(S | 0x1000000u);           // first '/' (24 if none)
+    const uint32_t m = len - s - 1u;                             // prefix digits
+    *slow = (C != 0u) | (m > 2u && s < len);
+    const uint32_t sep = P | S;
+    uint32_t ok = ((D | sep) == L) & (__builtin_popcount(P) == 3) & (__builtin_popcount(S) == 1) &
+                  ((P >> s) == 0u) & ((sep & (sep << 1)) == 0u) & (D & 1u) & (s + 1u < len) & (s <= 15u);
+    const uint32_t p1 = __builtin_ctz(P | 0x1000000u);
+    const uint32_t P2 = P & (P - 1u);
+    const uint32_t p2 = __builtin_ctz(P2 | 0x1000000u);
+    const uint32_t p3 = __builtin_ctz((P2 & (P2 - 1u)) | 0x1000000u);
+    if (!ok) return false;                                       // positions below are in range
+    ok &= octet_ok(window4(w, 0), p1);
+    ok &= octet_ok(window4(w, p1 + 1u), p2 - p1 - 1u);
+    ok &= octet_ok(window4(w, p2 + 1u), p3 - p2 - 1u);
+    ok &= octet_ok(window4(w, p3 + 1u), s - p3 - 1u);
+    const uint32_t c = window4(w, s + 1u);                       // dtoi(prefix) <= 32
+    const uint32_t bits = m == 1u ? (c & 0xFFu) - '0' : ((c & 0xFFu) - '0') * 10u + (((c >> 8) & 0xFFu) - '0');
+    return ok && bits <= 32u;
 }
 
 // One thread per key string, no LDS: the first 24 bytes are loaded as 7 aligned dwords and
 // funnel-shifted into registers; CIDR/MAC validity, "localhost", "physical/" and "default"
-// are decided there. Strings longer than 24 bytes, with ':' (IPv6) or shaped like a MAC
-// take the generic parsers (kdtn_parse.h) on global memory. Each wave packs its 64
+// are decided there with SWAR class masks (no per-character control flow: the scalar unit,
+// which executes every lane-mask operation of a branchy parser, was this kernel's bound).
+// Strings longer than 24 bytes, with ':' (IPv6), long prefixes or shaped like a MAC take
+// the generic parsers (kdtn_parse.h) on global memory. Each wave packs its 64
 // predicate bits per set with a ballot (two u32 words per set, lanes 0 and 32).
 __global__ void __launch_bounds__(BLOCK) k_kdict_flags(const uint8_t* bytes, const uint32_t* offs,
                                                        uint32_t n, uint32_t* kbits, uint32_t kb_words,
@@ -143,12 +180,9 @@ __global__ void __launch_bounds__(BLOCK) k_kdict_flags(const uint8_t* bytes, con
         for (int k = 0; k < 6; ++k)
             w[k] = sh ? (d[k] >> sh) | (d[k + 1] << (32u - sh)) : d[k];
         if (len) {
-            bool colon = false;
-#pragma unroll
-            for (int k = 0; k < 24; ++k) colon |= ((uint32_t)k < len) & (wbyte(w, k) == ':');
-            bool cok;
-            if (len <= 24 && !colon) cok = cidr4_regs(w, len);
-            else cok = cidr_ok(bytes + b, len);                            // common/veth.go:22
+            bool slow = true, cok = false;
+            if (len <= 24) cok = cidr_swar(w, len, &slow);
+            if (slow) cok = cidr_ok(bytes + b, len);                       // common/veth.go:22
             if (!cok) f |= 1u << KB_CIDR_BAD;
             const uint32_t c2 = wbyte(w, 2), c4 = wbyte(w, 4);
             bool mok = false;                                              // common/veth.go:33
@@ -174,35 +208,41 @@ __global__ void __launch_bounds__(BLOCK) k_kdict_flags(const uint8_t* bytes, con
 }
 
 KD_INLINE void pdict_parse_one(const uint8_t* s, uint32_t len, double tick, uint32_t* pct_out,
-                               uint4* dur_out, uint4* rate_out) {
+                               uint2* dur_out, uint2* rate_out, bool* rate_bad) {
     uint32_t dur = 0;
     const bool dok = parse_duration_us(s, len, &dur);
-    *dur_out = dok ? make_uint4(dur, time2tick(dur, tick), 0u, 0u) : make_uint4(0u, 0u, 1u, 0u);
+    *dur_out = dok ? make_uint2(dur, time2tick(dur, tick)) : make_uint2(0u, 1u);   // DUR_ERR
     float pct;
     *pct_out = parse_pct(s, len, &pct) ? p2u(pct) : PCT_ERR;
     uint64_t r = 0;
     const bool rok = parse_rate(s, len, &r);
-    *rate_out = rok ? make_uint4((uint32_t)r, (uint32_t)(r >> 32), 0u, 0u) : make_uint4(0u, 0u, 1u, 0u);
+    *rate_out = rok ? make_uint2((uint32_t)r, (uint32_t)(r >> 32)) : make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+    *rate_bad = !rok;
 }
 
 __global__ void __launch_bounds__(BLOCK) k_pdict_parse(const uint8_t* bytes, const uint32_t* offs,
                                                        uint32_t n, double tick, uint32_t* ppct,
-                                                       uint4* pdur, uint4* prate) {
+                                                       uint2* pdur, uint2* prate, uint32_t* rate_err) {
     __shared__ uint4 buf[STAGE / 16];
     const uint32_t s0 = blockIdx.x * BLOCK, s1 = min(s0 + BLOCK, n);
     uint32_t a0;
     const bool staged = stage_slice(bytes, offs, s0, s1, buf, &a0) != nullptr;
     __syncthreads();
     const uint32_t i = s0 + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t b = offs[i], len = offs[i + 1] - b;
-    uint32_t pct;
-    uint4 dur, rate;
-    if (staged) pdict_parse_one(reinterpret_cast<const uint8_t*>(buf) + (b - a0), len, tick, &pct, &dur, &rate);
-    else pdict_parse_one(bytes + b, len, tick, &pct, &dur, &rate);
-    ppct[i] = pct;
-    pdur[i] = dur;
-    prate[i] = rate;
+    bool bad = false;
+    if (i < n) {
+        const uint32_t b = offs[i], len = offs[i + 1] - b;
+        uint32_t pct;
+        uint2 dur, rate;
+        if (staged) pdict_parse_one(reinterpret_cast<const uint8_t*>(buf) + (b - a0), len, tick, &pct, &dur, &rate, &bad);
+        else pdict_parse_one(bytes + b, len, tick, &pct, &dur, &rate, &bad);
+        ppct[i] = pct;
+        pdur[i] = dur;
+        prate[i] = rate;
+    }
+    const uint64_t m = __ballot(bad);
+    const int lane = threadIdx.x & 63;
+    if (lane == 0 || lane == 32) rate_err[((i - lane) >> 5) + (lane >> 5)] = lane ? (uint32_t)(m >> 32) : (uint32_t)m;
 }
 
 // ======================================================================================
@@ -294,22 +334,34 @@ __global__ void __launch_bounds__(BLOCK) k_vni_ht_build(const uint4* ents, uint3
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-template <bool NT = false>
-KD_INLINE uint2 pod_lookup(const DevTables& tb, uint32_t ns, uint32_t name) {
+template <bool NT>
+KD_INLINE uint4 pod_slot(const DevTables& tb, uint32_t h) {
+    if constexpr (NT) {           // little reuse: keep L2 for the parsed tables
+        const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(tb.pod_wide) + h);
+        return make_uint4(v.x, v.y, v.z, v.w);
+    } else {
+        return tb.pod_wide[h];
+    }
+}
+KD_INLINE uint32_t pod_home(const DevTables& tb, uint32_t ns, uint32_t name) {
+    return (uint32_t)hash64(((uint64_t)ns << 32) | name) & tb.pod_mask;
+}
+// Resolve a lookup whose home slot h already read as w (linear probing continues here).
+template <bool NT>
+KD_INLINE uint2 pod_probe(const DevTables& tb, uint32_t ns, uint32_t name, uint32_t h, uint4 w) {
     if (ns == 0xFFFFFFFFu) return make_uint2(0xFFFFFFFFu, 0u);
-    uint32_t h = (uint32_t)hash64(((uint64_t)ns << 32) | name) & tb.pod_mask;
     for (;;) {
-        uint4 w;
-        if constexpr (NT) {       // no reuse to speak of: keep L2 for the parsed tables
-            const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(tb.pod_wide) + h);
-            w = make_uint4(v.x, v.y, v.z, v.w);
-        } else {
-            w = tb.pod_wide[h];
-        }
         if (w.x == ns && w.y == name) return make_uint2(w.z, w.w);
         if (w.x == 0xFFFFFFFFu) return make_uint2(0xFFFFFFFFu, 0u);
         h = (h + 1) & tb.pod_mask;
+        w = pod_slot<NT>(tb, h);
     }
+}
+template <bool NT = false>
+KD_INLINE uint2 pod_lookup(const DevTables& tb, uint32_t ns, uint32_t name) {
+    if (ns == 0xFFFFFFFFu) return make_uint2(0xFFFFFFFFu, 0u);
+    const uint32_t h = pod_home(tb, ns, name);
+    return pod_probe<NT>(tb, ns, name, h, pod_slot<NT>(tb, h));
 }
 
 // VxlanManager.Get(vni) on node `node`: net_ns id, or 0xFFFFFFFF when absent.
@@ -328,42 +380,80 @@ KD_INLINE uint32_t vni_lookup(const DevTables& tb, uint32_t node, int32_t vni) {
 // ======================================================================================
 // per-entry outputs: MakeQdiscs, delLink / addLink / UpdateLinks pure prefix
 // ======================================================================================
-// MakeQdiscs over parsed dictionary entries (common/qdisc.go:20-126 + netlink NewNetem)
+// Columns of one link record that the outputs need, loaded together (one round trip).
+struct RecCols {
+    uint32_t lip, lmac, pp;           // local_ip, local_mac, peer_pod (kdict ids)
+    uint32_t prop[KDTN_NPROP];        // pdict ids
+    uint32_t gap;
+    int64_t uid;
+};
+
+template <bool NTL>
+KD_INLINE void load_cols(const DevLinks& L, uint32_t j, bool keys, bool props, RecCols& c) {
+    const uint32_t* r = L.rec(j);
+    if (keys) {
+        c.lip = L.col<NTL>(r, COL_KEY0 + KDTN_K_LOCAL_IP);
+        c.lmac = L.col<NTL>(r, COL_KEY0 + KDTN_K_LOCAL_MAC);
+        c.pp = L.col<NTL>(r, COL_KEY0 + KDTN_K_PEER_POD);
+        c.uid = L.uid_at<NTL>(r, j);
+    }
+    if (props) {
+#pragma unroll
+        for (int k = 0; k < KDTN_NPROP; ++k) c.prop[k] = L.col<NTL>(r, COL_PROP0 + k);
+        c.gap = L.col<NTL>(r, COL_GAP);
+    }
+}
+
+// Parsed-table values of one record's properties (12 independent gathers, issued together).
+// The property ids die once the gathers are issued: only `empty`, `gap` and the rate id
+// (for the rare all-ones rate) stay live.
+struct PropVals {
+    uint2 lat, jit, rt;
+    uint32_t pct[9];                  // latency_corr, loss, loss_corr, duplicate, duplicate_corr,
+                                      // reorder_prob, reorder_corr, corrupt_prob, corrupt_corr
+    uint32_t gap, rate_id;
+    bool empty;                       // all 12 strings "" and gap 0 (proto.Size == 0, :24)
+};
+constexpr int PCT_FIELDS[9] = {KDTN_P_LATENCY_CORR, KDTN_P_LOSS, KDTN_P_LOSS_CORR, KDTN_P_DUPLICATE,
+                               KDTN_P_DUPLICATE_CORR, KDTN_P_REORDER_PROB, KDTN_P_REORDER_CORR,
+                               KDTN_P_CORRUPT_PROB, KDTN_P_CORRUPT_CORR};
+
 template <int V>
-KD_INLINE void make_qdisc(const DevLinks& L, uint32_t j, const DevTables& tb, uint32_t* q) {
-    constexpr bool NTL = (V & VAR_NT_LOAD) != 0;
+KD_INLINE void gather_props(const RecCols& c, const DevTables& tb, PropVals& v) {
+    v.lat = tb.pdur[c.prop[KDTN_P_LATENCY]];
+    v.jit = tb.pdur[c.prop[KDTN_P_JITTER]];
+    v.rt = tb.prate[c.prop[KDTN_P_RATE]];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        // (VAR_SKIP_PCT: profiling only, wrong results) the id stands in for the parsed value
+        if constexpr ((V & VAR_SKIP_PCT) != 0) v.pct[k] = c.prop[PCT_FIELDS[k]];
+        else v.pct[k] = tb.ppct[c.prop[PCT_FIELDS[k]]];
+    }
+    uint32_t any = c.gap;
+#pragma unroll
+    for (int k = 0; k < KDTN_NPROP; ++k) any |= c.prop[k];   // id 0 == ""
+    v.empty = any == 0;
+    v.gap = c.gap;
+    v.rate_id = c.prop[KDTN_P_RATE];
+}
+
+KD_INLINE bool dur_err(uint2 d) { return d.x == 0u && d.y == 1u; }
+KD_INLINE bool rate_bad(const DevTables& tb, const PropVals& v) {
+    if ((v.rt.x & v.rt.y) != 0xFFFFFFFFu) return false;          // rare: error or 2^64-1
+    return (tb.rate_err[v.rate_id >> 5] >> (v.rate_id & 31)) & 1u;
+}
+
+// MakeQdiscs over parsed dictionary entries (common/qdisc.go:20-126 + netlink NewNetem)
+KD_INLINE void qdisc_from(const DevTables& tb, const PropVals& v, uint32_t* q) {
 #pragma unroll
     for (int w = 0; w < 18; ++w) q[w] = 0;
-    uint32_t id[KDTN_NPROP];
-    const uint32_t gap = L.gap_s<NTL>(j);
-    bool empty = gap == 0;
-#pragma unroll
-    for (int k = 0; k < KDTN_NPROP; ++k) {
-        id[k] = L.prop_s<NTL>(k, j);
-        empty = empty && id[k] == 0;             // id 0 == "" (proto.Size == 0, :24)
-    }
-    if (empty) return;
-    const uint4 lat = tb.pdur[id[KDTN_P_LATENCY]];
-    const uint4 jit = tb.pdur[id[KDTN_P_JITTER]];
-    const uint4 rt = tb.prate[id[KDTN_P_RATE]];
-    // (VAR_SKIP_PCT: profiling only, wrong results) the id stands in for the parsed value
-    auto pct = [&](int k) -> uint32_t {
-        if constexpr ((V & VAR_SKIP_PCT) != 0) return id[k];
-        else return tb.ppct[id[k]];
-    };
-    const uint32_t lco = pct(KDTN_P_LATENCY_CORR);
-    const uint32_t los = pct(KDTN_P_LOSS);
-    const uint32_t lsc = pct(KDTN_P_LOSS_CORR);
-    const uint32_t dup = pct(KDTN_P_DUPLICATE);
-    const uint32_t dpc = pct(KDTN_P_DUPLICATE_CORR);
-    const uint32_t rop = pct(KDTN_P_REORDER_PROB);
-    const uint32_t roc = pct(KDTN_P_REORDER_CORR);
-    const uint32_t cop = pct(KDTN_P_CORRUPT_PROB);
-    const uint32_t coc = pct(KDTN_P_CORRUPT_CORR);
+    if (v.empty) return;
+    const uint32_t lco = v.pct[0], los = v.pct[1], lsc = v.pct[2], dup = v.pct[3], dpc = v.pct[4],
+                   rop = v.pct[5], roc = v.pct[6], cop = v.pct[7], coc = v.pct[8];
     uint32_t err = 0;                            // first failing parse, reference order
-    if (lat.z) err = KDTN_E_LATENCY;
+    if (dur_err(v.lat)) err = KDTN_E_LATENCY;
     else if (lco == PCT_ERR) err = KDTN_E_LATENCY_CORR;
-    else if (jit.z) err = KDTN_E_JITTER;
+    else if (dur_err(v.jit)) err = KDTN_E_JITTER;
     else if (los == PCT_ERR) err = KDTN_E_LOSS;
     else if (lsc == PCT_ERR) err = KDTN_E_LOSS_CORR;
     else if (dup == PCT_ERR) err = KDTN_E_DUPLICATE;
@@ -372,34 +462,34 @@ KD_INLINE void make_qdisc(const DevLinks& L, uint32_t j, const DevTables& tb, ui
     else if (roc == PCT_ERR) err = KDTN_E_REORDER_CORR;
     else if (cop == PCT_ERR) err = KDTN_E_CORRUPT_PROB;
     else if (coc == PCT_ERR) err = KDTN_E_CORRUPT_CORR;
-    else if (rt.z) err = KDTN_E_RATE;
+    else if (rate_bad(tb, v)) err = KDTN_E_RATE;
     if (err) {
         q[17] = err << 16;                       // byte 70 = err
         return;
     }
     // NewNetem
-    const uint32_t lat_us = lat.x, jit_us = jit.x, lat_t = lat.y;
+    const uint32_t lat_us = v.lat.x, jit_us = v.jit.x, lat_t = v.lat.y;
     q[0] = lat_t;                                                   // latency
     q[1] = (lat_us > 0 && jit_us > 0) ? lco : 0u;                  // delay_corr
     q[2] = 1000u;                                                   // limit
     q[3] = los;                                                     // loss
     q[4] = los > 0 ? lsc : 0u;                                      // loss_corr
-    q[5] = (rop > 0 && gap == 0) ? 1u : gap;                        // gap
+    q[5] = (rop > 0 && v.gap == 0) ? 1u : v.gap;                    // gap
     q[6] = dup;                                                     // duplicate
     q[7] = dup > 0 ? dpc : 0u;                                      // duplicate_corr
-    q[8] = lat_t > 0 ? jit.y : jit_us;                              // jitter
+    q[8] = lat_t > 0 ? v.jit.y : jit_us;                            // jitter
     q[9] = rop;
     q[10] = roc;
     q[11] = cop;
     q[12] = coc;
-    const uint64_t rate = ((uint64_t)rt.y << 32) | rt.x;
+    const uint64_t rate = ((uint64_t)v.rt.y << 32) | v.rt.x;
     uint32_t has_tbf = 0;
     if (rate != 0) {
         uint32_t burst = (uint32_t)(rate / 250ull);              // getTbfBurst
         if (burst < 5000u) burst = 5000u;
         q[13] = burst;
-        q[14] = rt.x;
-        q[15] = rt.y;
+        q[14] = v.rt.x;
+        q[15] = v.rt.y;
         q[16] = 1500u;
         has_tbf = 1;
     }
@@ -469,16 +559,14 @@ struct TopoCtx {       // the local pod of a batch (topology_controller.go:181-1
     uint32_t ns, src, netns;
 };
 
-// delLink (handler.go:461-492)
+// delLink (handler.go:461-492) from loaded columns (keys)
 template <int V>
-KD_INLINE void emit_del(const DevLinks& O, uint32_t i, const TopoCtx& tc, const DevTables& tb,
+KD_INLINE void emit_del(const RecCols& c, uint32_t i, const TopoCtx& tc, const DevTables& tb,
                         const RecOut& out, uint32_t e, bool res) {
-    constexpr bool NTL = (V & VAR_NT_LOAD) != 0;
     store_idx<V>(out.del_idx + e, i);
     if (!res) return;
-    const int32_t vni = vni_of(tb.vxlan_base, O.uid_s<NTL>(i));
-    const uint32_t err = veth_err(tb, O.key_s<NTL>(KDTN_K_LOCAL_IP, i), O.key_s<NTL>(KDTN_K_LOCAL_MAC, i),
-                                  KDTN_E_VETH_CIDR, KDTN_E_VETH_MAC);
+    const int32_t vni = vni_of(tb.vxlan_base, c.uid);
+    const uint32_t err = veth_err(tb, c.lip, c.lmac, KDTN_E_VETH_CIDR, KDTN_E_VETH_MAC);
     uint32_t hit = 0;
     if (!err) hit = vni_lookup(tb, tc.src, vni) == tc.netns;
     store_res<V>(out.del_res + e, pack_res(0xFFFFFFFFu, vni, 0, 0, err, hit));
@@ -486,51 +574,72 @@ KD_INLINE void emit_del(const DevLinks& O, uint32_t i, const TopoCtx& tc, const 
 
 // UpdateLinks entry (handler.go:644-663): MakeVeth(local), then MakeQdiscs
 template <int V>
-KD_INLINE void emit_upd(const DevLinks& N, uint32_t j, const DevTables& tb, const RecOut& out,
+KD_INLINE void emit_upd(const RecCols& c, uint32_t j, const DevTables& tb, const RecOut& out,
                         uint32_t e, bool res, bool qd, uint32_t* q) {
-    constexpr bool NTL = (V & VAR_NT_LOAD) != 0;
     store_idx<V>(out.upd_idx + e, j);
     if (!res && !qd) return;
-    make_qdisc<V>(N, j, tb, q);
+    PropVals v;
+    gather_props<V>(c, tb, v);
+    uint32_t werr = 0;
+    if (res) werr = veth_err(tb, c.lip, c.lmac, KDTN_E_VETH_CIDR, KDTN_E_VETH_MAC);
+    qdisc_from(tb, v, q);
     if (res) {
-        const int32_t vni = vni_of(tb.vxlan_base, N.uid_s<NTL>(j));
-        uint32_t err = veth_err(tb, N.key_s<NTL>(KDTN_K_LOCAL_IP, j), N.key_s<NTL>(KDTN_K_LOCAL_MAC, j),
-                                KDTN_E_VETH_CIDR, KDTN_E_VETH_MAC);
-        if (!err) err = (q[17] >> 16) & 0xFF;
-        store_res<V>(out.upd_res + e, pack_res(0xFFFFFFFFu, vni, 0, 0, err, 0));
+        const uint32_t err = werr ? werr : (q[17] >> 16) & 0xFF;
+        store_res<V>(out.upd_res + e, pack_res(0xFFFFFFFFu, vni_of(tb.vxlan_base, c.uid), 0, 0, err, 0));
     }
 }
 
-// addLink pure prefix (handler.go:316-459) + MakeQdiscs
+// addLink pure prefix (handler.go:316-459) + MakeQdiscs, from loaded columns, in two steps:
+// add_gather issues every lookup the entry may need (parsed properties, key-string
+// predicate words, the home slot of the peer's pod) without using any, so an entry costs one
+// gather round trip and the caller can put the next records' column loads behind it;
+// add_finish combines them in the reference's step order and stores the outputs.
+struct AddGath {
+    PropVals v;
+    uint4 slot;                       // home slot of (ns, peer_pod)
+    uint32_t h, lns, kb_ip, kb_mac;
+};
+
 template <int V>
-KD_INLINE void emit_add(const DevLinks& N, uint32_t j, const TopoCtx& tc, const DevTables& tb,
-                        const RecOut& out, uint32_t e, bool res, bool qd, uint32_t* q) {
+KD_INLINE void add_gather(const RecCols& c, const TopoCtx& tc, const DevTables& tb, bool res, bool qd,
+                          AddGath& g) {
+    if (qd) gather_props<V>(c, tb, g.v);
+    if (!res) return;
+    g.lns = tc.ns == 0 ? tb.special[SPECIAL_DEFAULT] : tc.ns;                     // :29-31
+    g.kb_ip = tb.kbits[(size_t)KB_CIDR_BAD * tb.kb_words + (c.lip >> 5)];
+    g.kb_mac = tb.kbits[(size_t)KB_MAC_BAD * tb.kb_words + (c.lmac >> 5)];
+    if constexpr ((V & VAR_SKIP_POD) == 0) {
+        g.h = pod_home(tb, g.lns, c.pp);
+        g.slot = pod_slot<(V & VAR_NT_POD) != 0>(tb, g.h);
+    }
+}
+
+template <int V>
+KD_INLINE void add_finish(const RecCols& c, const AddGath& g, const DevLinks& N, uint32_t j,
+                          const TopoCtx& tc, const DevTables& tb, const RecOut& out, uint32_t e,
+                          bool res, bool qd, uint32_t* q) {
     constexpr bool NTL = (V & VAR_NT_LOAD) != 0;
     store_idx<V>(out.add_idx + e, j);
-    if (qd) make_qdisc<V>(N, j, tb, q);
+    if (qd) qdisc_from(tb, g.v, q);
     if (!res) return;
-    const int32_t vni = vni_of(tb.vxlan_base, N.uid_s<NTL>(j));
-    uint32_t err = veth_err(tb, N.key_s<NTL>(KDTN_K_LOCAL_IP, j), N.key_s<NTL>(KDTN_K_LOCAL_MAC, j),
-                            KDTN_E_VETH_CIDR, KDTN_E_VETH_MAC);                          // :327
+    const int32_t vni = vni_of(tb.vxlan_base, c.uid);
+    uint32_t err = ((g.kb_ip >> (c.lip & 31)) & 1u) ? (uint32_t)KDTN_E_VETH_CIDR
+                 : ((g.kb_mac >> (c.lmac & 31)) & 1u) ? (uint32_t)KDTN_E_VETH_MAC : 0u;   // :327
     uint32_t kind = 0, peer = 0xFFFFFFFFu, vtep = 0, hit = 0;
     if (!err) {
-        const uint32_t pp = N.key_s<NTL>(KDTN_K_PEER_POD, j);
         // Reference order: localhost (:333), "physical/" prefix (:348), getPod (:375). The
-        // lookup is pure, so it is done first: a hit carries the PHYSICAL bit of the pod's
-        // name, only a miss reads the key-string bitset.
+        // lookup is pure, so it was started first: a hit carries the PHYSICAL bit of the
+        // pod's name, only a miss reads the key-string bitset.
+        const bool lh = c.pp == tb.special[SPECIAL_LOCALHOST];
         uint2 p = make_uint2(0xFFFFFFFFu, 0u);
-        const bool lh = pp == tb.special[SPECIAL_LOCALHOST];
-        if (!lh) {
-            const uint32_t lns = tc.ns == 0 ? tb.special[SPECIAL_DEFAULT] : tc.ns;      // :29-31
-            if constexpr ((V & VAR_SKIP_POD) != 0) p = make_uint2(pp & POD_INDEX, lns);   // profiling only
-            else p = pod_lookup<(V & VAR_NT_POD) != 0>(tb, lns, pp);
-        }
+        if constexpr ((V & VAR_SKIP_POD) != 0) p = make_uint2(c.pp & POD_INDEX, g.lns);   // profiling only
+        else if (!lh) p = pod_probe<(V & VAR_NT_POD) != 0>(tb, g.lns, c.pp, g.h, g.slot);
         const bool miss = p.x == 0xFFFFFFFFu;
         if (lh) {
             kind = KDTN_KIND_MACVLAN;                                                     // :333
-        } else if (miss ? kbit(tb, KB_PHYSICAL, pp) : (p.x & POD_PHYSICAL) != 0) {
+        } else if (miss ? kbit(tb, KB_PHYSICAL, c.pp) : (p.x & POD_PHYSICAL) != 0) {
             kind = KDTN_KIND_PHYSICAL;                                                    // :348
-            vtep = pp;
+            vtep = c.pp;
             const uint32_t nsx = vni_lookup(tb, tc.src, vni);                           // :177-179
             hit = (nsx != 0xFFFFFFFFu && nsx != tc.netns);
         } else if (miss) {
@@ -557,6 +666,15 @@ KD_INLINE void emit_add(const DevLinks& N, uint32_t j, const TopoCtx& tc, const 
         }
     }
     store_res<V>(out.add_res + e, pack_res(peer, vni, vtep, kind, err, hit));
+}
+
+template <int V>
+KD_INLINE void emit_add(const RecCols& c, const DevLinks& N, uint32_t j, const TopoCtx& tc,
+                        const DevTables& tb, const RecOut& out, uint32_t e, bool res, bool qd,
+                        uint32_t* q) {
+    AddGath g;
+    add_gather<V>(c, tc, tb, res, qd, g);
+    add_finish<V>(c, g, N, j, tc, tb, out, e, res, qd, q);
 }
 
 // Store the 72-B qdisc structs of this wave's active lanes. Active lanes' output positions
@@ -957,27 +1075,53 @@ __global__ void __launch_bounds__(BLOCK) k_reconcile(DevTopos T, DevLinks O, Dev
 
     // ---- 4. emission -------------------------------------------------------------------
     uint2* stage = s.stage[tid >> 6];
+    constexpr bool NTL = (V & VAR_NT_LOAD) != 0;
     if (bulk) {
-        for (uint32_t b = 0; b < tot; b += BLOCK) {          // position = topology offset + index
-            const uint32_t r = b + tid;
+        // Every record of a DIFF topology is an entry at topology offset + index. Software
+        // pipelined: a thread's next record's columns are loaded right after this record's
+        // gathers are issued, so a wave has both in flight.
+        struct Slot { uint32_t x; int tt; bool old, on; };
+        auto decode = [&](uint32_t r) {
+            Slot sl{0u, 0, false, false};
+            if (r < tot) {
+                sl.old = r < no;
+                sl.x = sl.old ? o0 + r : n0 + (r - no);
+                sl.tt = find_seg(sl.old ? s.ooff : s.noff, 0, nt, sl.x);
+                sl.on = s.act[sl.tt] == KDTN_ACT_DIFF;
+            }
+            return sl;
+        };
+        auto fetch = [&](const Slot& sl, RecCols& c) {
+            if (sl.on) load_cols<NTL>(sl.old ? O : N, sl.x, do_res, !sl.old && do_q, c);
+        };
+        Slot cs = decode(tid);
+        RecCols cc;
+        fetch(cs, cc);
+        for (uint32_t b = 0; b < tot; b += BLOCK) {
+            const Slot nx = decode(b + BLOCK + tid);
+            RecCols nc;
             bool qa = false;
             uint32_t e = 0, q[18];
-            if (r < tot) {
-                const bool old = r < no;
-                const uint32_t x = old ? o0 + r : n0 + (r - no);
-                const int tt = find_seg(old ? s.ooff : s.noff, 0, nt, x);
-                if (s.act[tt] == KDTN_ACT_DIFF) {
-                    const TopoCtx tc{s.ns[tt], s.src[tt], s.netns[tt]};
-                    if (old) {
-                        emit_del<V>(O, x, tc, tb, out, bd + s.tcnt[0][tt] + (x - s.ooff[tt]), do_res);
-                    } else {
-                        e = ba + s.tcnt[2][tt] + (x - s.noff[tt]);
-                        emit_add<V>(N, x, tc, tb, out, e, do_res, do_q, q);
-                        qa = do_q;
-                    }
+            if (cs.on) {
+                const int tt = cs.tt;
+                const TopoCtx tc{s.ns[tt], s.src[tt], s.netns[tt]};
+                if (cs.old) {
+                    fetch(nx, nc);
+                    emit_del<V>(cc, cs.x, tc, tb, out, bd + s.tcnt[0][tt] + (cs.x - s.ooff[tt]), do_res);
+                } else {
+                    e = ba + s.tcnt[2][tt] + (cs.x - s.noff[tt]);
+                    AddGath g;
+                    add_gather<V>(cc, tc, tb, do_res, do_q, g);
+                    fetch(nx, nc);
+                    add_finish<V>(cc, g, N, cs.x, tc, tb, out, e, do_res, do_q, q);
+                    qa = do_q;
                 }
+            } else {
+                fetch(nx, nc);
             }
             wave_store_qdisc<V>(out.add_qdisc, qa, e, q, stage);
+            cs = nx;
+            cc = nc;
         }
         trace_mark<V>(wk, wg, 4);
         return;
@@ -991,15 +1135,21 @@ __global__ void __launch_bounds__(BLOCK) k_reconcile(DevTopos T, DevLinks O, Dev
             if (f) {
                 const int tt = s.lt[r];
                 const TopoCtx tc{s.ns[tt], s.src[tt], s.netns[tt]};
+                RecCols c;
                 if (f & RF_DEL) {
-                    emit_del<V>(O, o0 + r, tc, tb, out, bd + s.rank[r], do_res);
+                    load_cols<NTL>(O, o0 + r, do_res, false, c);
+                    emit_del<V>(c, o0 + r, tc, tb, out, bd + s.rank[r], do_res);
                 } else if (f & RF_UPD) {
                     e = bu + s.rank[r];
-                    emit_upd<V>(N, n0 + s.tgt[r], tb, out, e, do_res, do_q, q);
+                    const uint32_t j = n0 + s.tgt[r];
+                    load_cols<NTL>(N, j, do_res, do_q || do_res, c);
+                    emit_upd<V>(c, j, tb, out, e, do_res, do_q, q);
                     qu = do_q;
                 } else {
                     e = ba + s.rank[r];
-                    emit_add<V>(N, n0 + (r - no), tc, tb, out, e, do_res, do_q, q);
+                    const uint32_t j = n0 + (r - no);
+                    load_cols<NTL>(N, j, do_res, do_q, c);
+                    emit_add<V>(c, N, j, tc, tb, out, e, do_res, do_q, q);
                     qa = do_q;
                 }
             }
@@ -1042,15 +1192,20 @@ __global__ void __launch_bounds__(BLOCK) k_reconcile(DevTopos T, DevLinks O, Dev
                 const int tt = find_seg(side ? s.noff : s.ooff, 0, nt, x);
                 const TopoCtx tc{s.ns[tt], s.src[tt], s.netns[tt]};
                 uint32_t q[18];
+                RecCols c;
                 if (f & RF_DEL) {
-                    emit_del<V>(O, x, tc, tb, out, bd + cd + p0 + __popcll(b0 & lt), do_res);
+                    load_cols<NTL>(O, x, do_res, false, c);
+                    emit_del<V>(c, x, tc, tb, out, bd + cd + p0 + __popcll(b0 & lt), do_res);
                 } else if (f & RF_UPD) {
                     const uint32_t e = bu + cu + p1 + __popcll(b1 & lt);
-                    emit_upd<V>(N, wk.otarget[x], tb, out, e, do_res, do_q, q);
+                    const uint32_t j = wk.otarget[x];
+                    load_cols<NTL>(N, j, do_res, do_q || do_res, c);
+                    emit_upd<V>(c, j, tb, out, e, do_res, do_q, q);
                     if (do_q) store_qdisc<V>(out.upd_qdisc + (size_t)e * 9, q);
                 } else {
                     const uint32_t e = ba + ca + p2 + __popcll(b2 & lt);
-                    emit_add<V>(N, x, tc, tb, out, e, do_res, do_q, q);
+                    load_cols<NTL>(N, x, do_res, do_q, c);
+                    emit_add<V>(c, N, x, tc, tb, out, e, do_res, do_q, q);
                     if (do_q) store_qdisc<V>(out.add_qdisc + (size_t)e * 9, q);
                 }
             }
@@ -1068,7 +1223,11 @@ __global__ void __launch_bounds__(BLOCK) k_qdisc_batch(DevLinks props, DevTables
     const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
     if (j >= props.n) return;
     uint32_t q[18];
-    make_qdisc<0>(props, j, tb, q);
+    RecCols c;
+    load_cols<false>(props, j, false, true, c);
+    PropVals v;
+    gather_props<0>(c, tb, v);
+    qdisc_from(tb, v, q);
     store_qdisc<0>(out + (size_t)j * 9, q);
 }
 
@@ -1084,5 +1243,7 @@ template __global__ void k_reconcile<17>(DevTopos, DevLinks, DevLinks, DevTables
 template __global__ void k_reconcile<33>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
 template __global__ void k_reconcile<65>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
 template __global__ void k_reconcile<97>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
+template __global__ void k_reconcile<101>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
+template __global__ void k_reconcile<113>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
 
 }  // namespace kdtn
