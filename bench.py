@@ -58,9 +58,13 @@ def epoch_bytes(inp, n_add: int, n_upd: int, n_del: int) -> float:
             + 72.0 * (n_add + n_upd) + float(inp.pdict.offs[-1]))
 
 
-def cpu_baseline(inp, budget_s: float):
+def cpu_baseline(inp, budget_s: float, threads: int):
     """The CPU oracle (C restatement of the reference Go path) on a bounded sample of this
-    workload's topologies, single thread, loop time only (informer maps pre-built)."""
+    workload's topologies, loop time only (informer maps pre-built). Single thread, then
+    `threads` workers over disjoint topology ranges, mirroring the reference's
+    MaxConcurrentReconciles worker pool (controllers/topology_controller.go:335-337); the
+    ctypes call releases the GIL, so the workers run concurrently."""
+    from concurrent.futures import ThreadPoolExecutor
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     T = inp.topos.n
@@ -72,10 +76,40 @@ def cpu_baseline(inp, budget_s: float):
     timing.clear()
     O.reconcile(inp, t_begin=0, t_end=want, timing=timing)
     links = int(inp.topos.des_off[want] - inp.topos.des_off[0])
-    return {"value": links / timing[-1], "unit": "links/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/kdtn_oracle.c on topologies [0,{want}) of rank 0's shard: "
-                      f"{links} links, {timing[-1]:.2f} s single-thread "
-                      f"(host nproc={os.cpu_count()})"}
+    one = links / timing[-1]
+    # worker pool: each worker takes an equal slice of a sample `threads` times larger
+    n_par = int(min(T, want * threads))
+    bounds = [n_par * k // threads for k in range(threads + 1)]
+    ptim = [[] for _ in range(threads)]
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(lambda k: O.reconcile(inp, t_begin=bounds[k], t_end=bounds[k + 1],
+                                          timing=ptim[k]), range(threads)))
+    par_links = int(inp.topos.des_off[n_par] - inp.topos.des_off[0])
+    par_s = max(t[-1] for t in ptim)
+    return {"value": par_links / par_s, "unit": "links/s", "cores": threads, "kind": "port",
+            "value_1thread": one,
+            "sample": f"oracle/kdtn_oracle.c (literal CalcDiff loops, per-link MakeQdiscs, "
+                      f"map-based resolve) on rank 0's shard: {threads} threads over "
+                      f"topologies [0,{n_par}) = {par_links} links in {par_s:.2f} s (slowest "
+                      f"worker's loop); single thread: [0,{want}) = {links} links in "
+                      f"{timing[-1]:.2f} s (host nproc={os.cpu_count()})"}
+
+
+def pmc_traffic(links_per_gpu: int):
+    """HBM bytes per k_reconcile launch from the newest committed PMC summary of the same
+    workload (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from separate
+    FETCH_SIZE / WRITE_SIZE rocprofv3 passes, gfx950 correction applied), else None."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json"))):
+        with open(f) as fh:
+            d = json.load(fh)
+        if d.get("links_per_gpu") != links_per_gpu:
+            continue
+        for k, v in d["kernels"].items():
+            if k.startswith("k_reconcile") and "traffic_bytes" in v:
+                best = (v["traffic_bytes"], os.path.basename(f))
+    return best
 
 
 def main():
@@ -87,6 +121,8 @@ def main():
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--cpu-budget-s", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="CPU-baseline worker threads (the GPU box's CPU share is 16)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -143,6 +179,10 @@ def main():
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "traffic": None,
             "bytes_per_launch": ebytes, "avg_ms": kavg["reconcile"], "dominant_stage": dom}
     roof["frac"] = roof["achieved"] / roof["peak"]
+    tr = pmc_traffic(inp.desired.n)
+    if tr is not None:
+        roof["traffic"] = tr[0]
+        roof["traffic_source"] = f"profiles/{tr[1]} (2*FETCH_SIZE + WRITE_SIZE per launch)"
     pbytes = epoch_bytes(inp, counts.n_add, counts.n_upd, counts.n_del)
     result = {
         "metric": "links reconciled/sec (diff+qdisc) on 10M-link topology",
@@ -171,7 +211,7 @@ def main():
         "gen_s": round(gen_s, 2),
     }
     if rank == 0 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(inp, args.cpu_budget_s)
+        result["cpu_baseline"] = cpu_baseline(inp, args.cpu_budget_s, args.cpu_threads)
     if rank == 0:
         print(json.dumps(result), flush=True)
     eng.close()

@@ -1,0 +1,45 @@
+"""HBM traffic per k_reconcile launch from the FETCH_SIZE / WRITE_SIZE PMC passes.
+
+    python tools/pmc_traffic.py <gpurun_out/TAG> <profiles/OUT.json> [links_per_gpu]
+
+Reads the rocprofv3 counter CSVs of tools/gpu_round.sh's `pmc` step (one pass per counter:
+they cannot share a pass on gfx950) and applies MI355X_MICROARCH.md § HBM: FETCH_SIZE and
+WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE tallies 128-B read requests at 64 B, so it is
+doubled; WRITE_SIZE is taken as is. bench.py reports the result as roofline.traffic when
+the workload matches.
+"""
+import collections
+import csv
+import glob
+import json
+import sys
+
+
+def main():
+    root, dst = sys.argv[1], sys.argv[2]
+    links = int(sys.argv[3]) if len(sys.argv) > 3 else 10_000_000
+    vals = collections.defaultdict(list)
+    for f in sorted(glob.glob(f"{root}/pmc*/**/*counter_collection.csv", recursive=True)):
+        for r in csv.DictReader(open(f)):
+            k = r["Kernel_Name"].split("(")[0].replace("kdtn::", "").replace("void ", "")
+            vals[(k, r["Counter_Name"])].append(float(r["Counter_Value"]))
+    out = {"source": root, "links_per_gpu": links, "kernels": {}}
+    for (k, c), v in sorted(vals.items()):
+        if k.startswith("__amd"):
+            continue
+        out["kernels"].setdefault(k, {})[c + "_kib_mean"] = sum(v) / len(v)
+        out["kernels"][k][c + "_n"] = len(v)
+    for k, d in out["kernels"].items():
+        if "FETCH_SIZE_kib_mean" in d and "WRITE_SIZE_kib_mean" in d:
+            d["read_bytes"] = 2.0 * d["FETCH_SIZE_kib_mean"] * 1024.0
+            d["write_bytes"] = d["WRITE_SIZE_kib_mean"] * 1024.0
+            d["traffic_bytes"] = d["read_bytes"] + d["write_bytes"]
+    with open(dst, "w") as f:
+        json.dump(out, f, indent=1)
+    rec = [k for k in out["kernels"] if k.startswith("k_reconcile")]
+    for k in rec:
+        print(k, json.dumps(out["kernels"][k]))
+
+
+if __name__ == "__main__":
+    main()
