@@ -505,11 +505,11 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         const size_t pcap = (size_t)c->pod_mask + 1;
         HIP_TRY(hipMemsetAsync(c->pod_slots.p, 0xFF, pcap * 4, s));
         if (c->pod_total)
-            k_pod_ht_build<<<nblocks(c->pod_total), BLOCK, 0, s>>>(dp<uint4>(c->pods), c->pod_total,
-                                                                  dp<uint32_t>(c->pod_slots), c->pod_mask);
-        k_pod_ht_expand<<<nblocks(pcap), BLOCK, 0, s>>>(dp<uint4>(c->pods), dp<uint32_t>(c->pod_slots),
-                                                       dp<uint32_t>(c->kd_bits) + (size_t)KB_PHYSICAL * c->kb_words,
-                                                       dp<uint4>(c->pod_wide), (uint32_t)pcap);
+            k_pod_slots_build<<<nblocks(c->pod_total), BLOCK, 0, s>>>(dp<uint4>(c->pods), c->pod_total,
+                                                                     dp<uint32_t>(c->pod_slots), c->pod_mask);
+        k_pod_slots_expand<<<nblocks(pcap), BLOCK, 0, s>>>(dp<uint4>(c->pods), dp<uint32_t>(c->pod_slots),
+                                                          dp<uint32_t>(c->kd_bits) + (size_t)KB_PHYSICAL * c->kb_words,
+                                                          dp<uint4>(c->pod_wide), (uint32_t)pcap);
         if (c->V) {
             const size_t vcap = (size_t)c->vni_mask + 1;
             HIP_TRY(hipMemsetAsync(c->v_slots.p, 0xFF, vcap * 4, s));
@@ -559,6 +559,8 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         w.otarget = dp<uint32_t>(c->otarget);
         w.nwg = c->nwg;
         w.trace = nullptr;
+        w.first_partial = misc + MISC_FIRST_PARTIAL;                // 0xFFFFFFFF from the memset
+        k_full_prefix<<<nblocks(c->T), BLOCK, 0, s>>>(T, misc + MISC_FIRST_PARTIAL);
         int variant = DEFAULT_VARIANT;
         if (const char* ev = std::getenv("KDTN_VARIANT")) variant = std::atoi(ev);   // profiling A/B
         if (variant & VAR_TRACE) {
@@ -579,8 +581,17 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         case 113: k_reconcile<113><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
         case 97: k_reconcile<97><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
         case 17: k_reconcile<17><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
+        case 513: k_reconcile<513><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
+        case 1025: k_reconcile<1025><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
+        case 1537: k_reconcile<1537><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
+        case 529: k_reconcile<529><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
+        case 129: k_reconcile<129><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
+        case 257: k_reconcile<257><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
         case 11: k_reconcile<11><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
-        default: k_reconcile<1><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
+        case 1: k_reconcile<1><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
+        default:
+            k_reconcile<DEFAULT_VARIANT><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w);
+            break;
         }
         timer_mark(c, "reconcile");
     } else {

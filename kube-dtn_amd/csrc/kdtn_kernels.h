@@ -10,17 +10,16 @@
 //                  kbits: 3 bitsets over key strings (CIDR_BAD, MAC_BAD, PHYSICAL; 1.5 MB
 //                  per 12M strings, L2-resident); ppct u32 (Percentage2u32 or PCT_ERR);
 //                  pdur {us, ticks, err}; prate {lo, hi, err}
-//   pod table    : pods[g] = {ns, name, src_ip, net_ns|spec_nil<<31} per global pod index,
-//                  open-addressing slots of pod indices keyed by (ns, name) (one CAS per
-//                  insert), expanded into 16-B self-contained slots: a lookup is ONE gather
-//                  (the slot also carries the PHYSICAL bit of the pod's name, so a hit
-//                  needs no key-string flag read).
+//   pod table    : pods[g] = {ns, name, src_ip, net_ns|spec_nil<<31} per global pod index;
+//                  lookup table of 16-B self-contained slots keyed by (ns, name), probed in
+//                  128-B buckets: a lookup is ONE line (the slot also carries the PHYSICAL
+//                  bit of the pod's name, so a hit needs no key-string flag read).
 // Kernels (launch order):
 //   k_kdict_flags   MakeVeth / addLink predicates per key string          (D threads)
 //   k_pdict_parse   ParseDuration / ParseFloatPercentage / ParseRate      (P threads)
 //   k_pods_fill     this rank's pod-status slice                          (slice threads)
 //   [RCCL all-gather of the pod-status table when nranks > 1]
-//   k_pod_ht_build, k_vni_pack + k_vni_ht_build
+//   k_pod_slots_build + k_pod_slots_expand, k_vni_pack + k_vni_ht_build
 //   k_reconcile     ONE pass per workgroup of TPW topologies: Reconcile gate + CalcDiff in
 //                   LDS, decoupled look-back for the batch bases, then barrier-free emission
 //                   of the batch lists, addLink/delLink/UpdateLinks pure prefix, MakeQdiscs.
@@ -48,7 +47,7 @@ enum : int {
     KB_NSETS = 3,
 };
 // special key-string ids found by k_kdict_flags (0xFFFFFFFF when absent)
-enum : int { SPECIAL_DEFAULT = 0, SPECIAL_LOCALHOST = 4 };   // word index in the misc buffer
+enum : int { SPECIAL_DEFAULT = 0, SPECIAL_LOCALHOST = 4, MISC_FIRST_PARTIAL = 8 };   // misc words
 // pod slot flag bits (in the g word of a wide slot; pod indices < 2^30)
 constexpr uint32_t POD_SPEC_NIL = 0x80000000u, POD_PHYSICAL = 0x40000000u, POD_INDEX = 0x3FFFFFFFu;
 
@@ -106,10 +105,15 @@ struct DevLinks {
 //   bit 3: non-temporal pod-slot gathers
 //   bit 4: (profiling) per-workgroup phase timestamps into RecWork::trace
 //   bits 5, 6: (profiling, wrong results) skip the pod-slot / percentage-table gathers
+//   bits 7, 8: occupancy target of 5 / 6 waves per SIMD (register budget 96 / 80 VGPRs)
+//   bit 9: parsed-table gathers only for non-empty property ids (id 0 = "" parses to 0)
+//   bit 10: (A/B) always run the look-back, ignoring k_full_prefix
 constexpr int VAR_NT_LOAD = 1, VAR_NT_STORE = 2, VAR_NO_QSTORE = 4, VAR_NT_POD = 8, VAR_TRACE = 16,
-              VAR_SKIP_POD = 32, VAR_SKIP_PCT = 64;
+              VAR_SKIP_POD = 32, VAR_SKIP_PCT = 64, VAR_OCC5 = 128, VAR_OCC6 = 256,
+              VAR_MASK_EMPTY = 512, VAR_NO_PREFIX = 1024;
+constexpr int var_waves(int v) { return (v & VAR_OCC6) ? 6 : (v & VAR_OCC5) ? 5 : 1; }
 constexpr int TRACE_WORDS = 6;   // entry, topologies loaded, counts done, bases known, end, hw ids
-constexpr int DEFAULT_VARIANT = VAR_NT_LOAD;
+constexpr int DEFAULT_VARIANT = VAR_NT_LOAD | VAR_MASK_EMPTY;
 
 struct DevTopos {
     const uint32_t* ns;
@@ -130,7 +134,7 @@ struct DevTables {             // read-only lookup structures of the epoch
     const uint2* prate;        // [P] {lo, hi}; all-ones = error or 2^64-1: see rate_err
     const uint32_t* rate_err;  // [ceil(P/64)*2] bitset: ParseRate failed
     const uint4* pods;         // [pod_total] {ns, name, src_ip, net_ns|spec_nil<<31}
-    const uint4* pod_wide;     // [pod_mask+1] {ns, name, g|POD_* flags, src_ip|netns_empty<<31}
+    const uint4* pod_wide;     // [pod_mask+1] {ns, name, src_ip|netns_empty<<31, g<<2|phys<<1|spec_nil}
     uint32_t pod_mask;
     const uint4* vnis;         // [V] {node, vni, net_ns, 0}
     const uint32_t* vni_slots; // [vni_mask+1]
@@ -163,6 +167,7 @@ struct RecWork {
     uint8_t* fscratch;         // [M+N] record flags when a workgroup exceeds CAP
     uint32_t* otarget;         // [M]   first matching desired index (slow path)
     unsigned long long* trace; // [nwg][TRACE_WORDS] (VAR_TRACE only)
+    const uint32_t* first_partial;   // k_full_prefix: first chunk not known to emit all records
     uint32_t nwg;
 };
 
@@ -171,9 +176,9 @@ __global__ void k_kdict_flags(const uint8_t* bytes, const uint32_t* offs, uint32
 __global__ void k_pdict_parse(const uint8_t* bytes, const uint32_t* offs, uint32_t n, double tick,
                               uint32_t* ppct, uint2* pdur, uint2* prate, uint32_t* rate_err);
 __global__ void k_pods_fill(DevTopos T, uint32_t slice, uint32_t rank_base, uint4* pods);
-__global__ void k_pod_ht_build(const uint4* pods, uint32_t total, uint32_t* slots, uint32_t mask);
-__global__ void k_pod_ht_expand(const uint4* pods, const uint32_t* slots, const uint32_t* phys_bits,
-                                uint4* wide, uint32_t cap);
+__global__ void k_pod_slots_build(const uint4* pods, uint32_t total, uint32_t* slots, uint32_t mask);
+__global__ void k_pod_slots_expand(const uint4* pods, const uint32_t* slots, const uint32_t* phys_bits,
+                                   uint4* wide, uint32_t cap);
 __global__ void k_vni_ht_build(const uint4* ents, uint32_t n, uint32_t* slots, uint32_t mask);
 __global__ void k_vni_pack(const uint32_t* node, const int32_t* vni, const uint32_t* net_ns,
                            uint32_t n, uint4* ents);
@@ -181,5 +186,6 @@ template <int V>
 __global__ void k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out,
                             RecWork wk);
 __global__ void k_qdisc_batch(DevLinks props, DevTables tb, uint2* out);
+__global__ void k_full_prefix(DevTopos T, uint32_t* first_partial);
 
 }  // namespace kdtn

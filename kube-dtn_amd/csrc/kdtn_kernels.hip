@@ -167,15 +167,29 @@ KD_INLINE bool cidr_swar(const uint32_t* w, uint32_t len, bool* slow) {
 __global__ void __launch_bounds__(BLOCK) k_kdict_flags(const uint8_t* bytes, const uint32_t* offs,
                                                        uint32_t n, uint32_t* kbits, uint32_t kb_words,
                                                        uint32_t* special) {
+    // The block's arena slice is staged through LDS with 16-B coalesced loads; each lane then
+    // reads its string's first 28 bytes from LDS (7 aligned dwords) instead of issuing seven
+    // overlapping unaligned global loads.
+    __shared__ uint4 buf[STAGE / 16 + 2];                  // +32 B: reads past the slice end
+    const uint32_t s0 = blockIdx.x * BLOCK, s1 = min(s0 + BLOCK, n);
+    uint32_t a0 = 0;
+    const bool staged = s0 < n && stage_slice(bytes, offs, s0, s1, buf, &a0) != nullptr;
+    __syncthreads();
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     uint32_t f = 0;
     if (i < n) {
         const uint32_t b = offs[i], len = offs[i + 1] - b;
         const uint32_t a = b & ~3u, sh = (b & 3u) * 8u;
-        const uint32_t* p = reinterpret_cast<const uint32_t*>(bytes + a);   // arena has 64 B slack
         uint32_t d[7], w[6];
+        if (staged) {
+            const uint32_t* p = reinterpret_cast<const uint32_t*>(buf) + ((a - a0) >> 2);
 #pragma unroll
-        for (int k = 0; k < 7; ++k) d[k] = p[k];
+            for (int k = 0; k < 7; ++k) d[k] = p[k];
+        } else {
+            const uint32_t* p = reinterpret_cast<const uint32_t*>(bytes + a);   // arena has 64 B slack
+#pragma unroll
+            for (int k = 0; k < 7; ++k) d[k] = p[k];
+        }
 #pragma unroll
         for (int k = 0; k < 6; ++k)
             w[k] = sh ? (d[k] >> sh) | (d[k + 1] << (32u - sh)) : d[k];
@@ -264,39 +278,44 @@ __global__ void __launch_bounds__(BLOCK) k_pods_fill(DevTopos T, uint32_t slice,
     pods[rank_base + t] = e;
 }
 
-// Open addressing over pod indices: a slot holds the smallest index g of the pods with
-// its key (ns, name); the key itself is read from pods[g]. One CAS per insert; a lookup
-// reads the slot, then the pod entry (key check + payload) — 2 dependent 4/16-B gathers.
-__global__ void __launch_bounds__(BLOCK) k_pod_ht_build(const uint4* pods, uint32_t total,
-                                                        uint32_t* slots, uint32_t mask) {
+// Pod lookup table (informer store, handler.go:27-41): open addressing over 16-B
+// self-contained slots {ns, name, src_ip|netns_empty<<31, g<<2|physical<<1|spec_nil},
+// probed inside 128-B buckets of 8 slots (one L2 line) before moving to the next bucket,
+// so a lookup costs one line fetch at the table's load factor of 1/2.
+// Built in two passes: k_pod_slots_build claims u32 index slots with one 32-bit CAS per pod
+// (random device-scope atomics run at the memory side, so the build keeps them to one
+// per pod; atomicMin keeps the smallest pod index of duplicate keys, the informer's
+// first-wins), then k_pod_slots_expand writes the 16-B slots sequentially.
+KD_INLINE uint32_t pod_probe_slot(uint32_t home, uint32_t i, uint32_t mask) {
+    const uint32_t b = (home >> 3) + (i >> 3);
+    return ((b << 3) + ((home + i) & 7u)) & mask;
+}
+KD_INLINE uint32_t pod_home(uint32_t mask, uint32_t ns, uint32_t name) {
+    return (uint32_t)hash64(((uint64_t)ns << 32) | name) & mask;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_pod_slots_build(const uint4* pods, uint32_t total,
+                                                           uint32_t* slots, uint32_t mask) {
     const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
     if (g >= total) return;
     const uint4 e = pods[g];
-    if (e.x == 0xFFFFFFFFu) return;
-    uint32_t h = (uint32_t)hash64(((uint64_t)e.x << 32) | e.y) & mask;
-    for (;;) {
+    if (e.x == 0xFFFFFFFFu) return;                        // padding row
+    const uint32_t home = pod_home(mask, e.x, e.y);
+    for (uint32_t i = 0;; ++i) {
+        const uint32_t h = pod_probe_slot(home, i, mask);
         const uint32_t prev = atomicCAS(&slots[h], 0xFFFFFFFFu, g);
         if (prev == 0xFFFFFFFFu) return;
         const uint4 o = pods[prev];
         if (o.x == e.x && o.y == e.y) {
-            atomicMin(&slots[h], g);                 // informer store: first topology wins
+            atomicMin(&slots[h], g);                       // first topology wins
             return;
         }
-        h = (h + 1) & mask;
     }
 }
 
-__global__ void __launch_bounds__(BLOCK) k_vni_pack(const uint32_t* node, const int32_t* vni,
-                                                    const uint32_t* net_ns, uint32_t n, uint4* ents) {
-    const uint32_t v = blockIdx.x * BLOCK + threadIdx.x;
-    if (v < n) ents[v] = make_uint4(node[v], (uint32_t)vni[v], net_ns[v], 0u);
-}
-
-// Expand the slot table into 16-B self-contained slots {ns, name, g|spec_nil<<31|physical<<30,
-// src_ip|netns_empty<<31}: a lookup is then ONE random 16-B gather (key + payload).
-__global__ void __launch_bounds__(BLOCK) k_pod_ht_expand(const uint4* pods, const uint32_t* slots,
-                                                         const uint32_t* phys_bits, uint4* wide,
-                                                         uint32_t cap) {
+__global__ void __launch_bounds__(BLOCK) k_pod_slots_expand(const uint4* pods, const uint32_t* slots,
+                                                            const uint32_t* phys_bits, uint4* wide,
+                                                            uint32_t cap) {
     const uint32_t h = blockIdx.x * BLOCK + threadIdx.x;
     if (h >= cap) return;
     const uint32_t g = slots[h];
@@ -304,10 +323,16 @@ __global__ void __launch_bounds__(BLOCK) k_pod_ht_expand(const uint4* pods, cons
     if (g != 0xFFFFFFFFu) {
         const uint4 e = pods[g];
         const uint32_t phys = (phys_bits[e.y >> 5] >> (e.y & 31)) & 1u;
-        w = make_uint4(e.x, e.y, g | (e.w & POD_SPEC_NIL) | (phys ? POD_PHYSICAL : 0u),
-                       e.z | ((e.w & 0x7FFFFFFFu) == 0 ? 0x80000000u : 0u));
+        w = make_uint4(e.x, e.y, e.z | ((e.w & 0x7FFFFFFFu) == 0 ? 0x80000000u : 0u),
+                       (g << 2) | (phys << 1) | (e.w >> 31));
     }
     wide[h] = w;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_vni_pack(const uint32_t* node, const int32_t* vni,
+                                                    const uint32_t* net_ns, uint32_t n, uint4* ents) {
+    const uint32_t v = blockIdx.x * BLOCK + threadIdx.x;
+    if (v < n) ents[v] = make_uint4(node[v], (uint32_t)vni[v], net_ns[v], 0u);
 }
 
 // VxlanManager snapshot: slots hold the smallest entry index with key (node, vni).
@@ -343,24 +368,22 @@ KD_INLINE uint4 pod_slot(const DevTables& tb, uint32_t h) {
         return tb.pod_wide[h];
     }
 }
-KD_INLINE uint32_t pod_home(const DevTables& tb, uint32_t ns, uint32_t name) {
-    return (uint32_t)hash64(((uint64_t)ns << 32) | name) & tb.pod_mask;
-}
-// Resolve a lookup whose home slot h already read as w (linear probing continues here).
+// Resolve a lookup whose home slot h already read as w (probing continues in the bucket).
+// Returns {g | POD_SPEC_NIL | POD_PHYSICAL, src_ip | netns_empty<<31}; x = 0xFFFFFFFF on a miss.
 template <bool NT>
 KD_INLINE uint2 pod_probe(const DevTables& tb, uint32_t ns, uint32_t name, uint32_t h, uint4 w) {
     if (ns == 0xFFFFFFFFu) return make_uint2(0xFFFFFFFFu, 0u);
-    for (;;) {
-        if (w.x == ns && w.y == name) return make_uint2(w.z, w.w);
+    for (uint32_t i = 1;; ++i) {
+        if (w.x == ns && w.y == name)
+            return make_uint2((w.w >> 2) | ((w.w & 1u) << 31) | ((w.w & 2u) << 29), w.z);
         if (w.x == 0xFFFFFFFFu) return make_uint2(0xFFFFFFFFu, 0u);
-        h = (h + 1) & tb.pod_mask;
-        w = pod_slot<NT>(tb, h);
+        w = pod_slot<NT>(tb, pod_probe_slot(h, i, tb.pod_mask));
     }
 }
 template <bool NT = false>
 KD_INLINE uint2 pod_lookup(const DevTables& tb, uint32_t ns, uint32_t name) {
     if (ns == 0xFFFFFFFFu) return make_uint2(0xFFFFFFFFu, 0u);
-    const uint32_t h = pod_home(tb, ns, name);
+    const uint32_t h = pod_home(tb.pod_mask, ns, name);
     return pod_probe<NT>(tb, ns, name, h, pod_slot<NT>(tb, h));
 }
 
@@ -420,14 +443,24 @@ constexpr int PCT_FIELDS[9] = {KDTN_P_LATENCY_CORR, KDTN_P_LOSS, KDTN_P_LOSS_COR
 
 template <int V>
 KD_INLINE void gather_props(const RecCols& c, const DevTables& tb, PropVals& v) {
-    v.lat = tb.pdur[c.prop[KDTN_P_LATENCY]];
-    v.jit = tb.pdur[c.prop[KDTN_P_JITTER]];
-    v.rt = tb.prate[c.prop[KDTN_P_RATE]];
+    if constexpr ((V & VAR_MASK_EMPTY) != 0) {
+        // "" (id 0) parses to 0 in every table: only lanes with a string issue the gather
+        const uint32_t il = c.prop[KDTN_P_LATENCY], ij = c.prop[KDTN_P_JITTER], ir = c.prop[KDTN_P_RATE];
+        v.lat = il ? tb.pdur[il] : make_uint2(0u, 0u);
+        v.jit = ij ? tb.pdur[ij] : make_uint2(0u, 0u);
+        v.rt = ir ? tb.prate[ir] : make_uint2(0u, 0u);
+    } else {
+        v.lat = tb.pdur[c.prop[KDTN_P_LATENCY]];
+        v.jit = tb.pdur[c.prop[KDTN_P_JITTER]];
+        v.rt = tb.prate[c.prop[KDTN_P_RATE]];
+    }
 #pragma unroll
     for (int k = 0; k < 9; ++k) {
+        const uint32_t id = c.prop[PCT_FIELDS[k]];
         // (VAR_SKIP_PCT: profiling only, wrong results) the id stands in for the parsed value
-        if constexpr ((V & VAR_SKIP_PCT) != 0) v.pct[k] = c.prop[PCT_FIELDS[k]];
-        else v.pct[k] = tb.ppct[c.prop[PCT_FIELDS[k]]];
+        if constexpr ((V & VAR_SKIP_PCT) != 0) v.pct[k] = id;
+        else if constexpr ((V & VAR_MASK_EMPTY) != 0) v.pct[k] = id ? tb.ppct[id] : 0u;
+        else v.pct[k] = tb.ppct[id];
     }
     uint32_t any = c.gap;
 #pragma unroll
@@ -609,7 +642,7 @@ KD_INLINE void add_gather(const RecCols& c, const TopoCtx& tc, const DevTables& 
     g.kb_ip = tb.kbits[(size_t)KB_CIDR_BAD * tb.kb_words + (c.lip >> 5)];
     g.kb_mac = tb.kbits[(size_t)KB_MAC_BAD * tb.kb_words + (c.lmac >> 5)];
     if constexpr ((V & VAR_SKIP_POD) == 0) {
-        g.h = pod_home(tb, g.lns, c.pp);
+        g.h = pod_home(tb.pod_mask, g.lns, c.pp);
         g.slot = pod_slot<(V & VAR_NT_POD) != 0>(tb, g.h);
     }
 }
@@ -733,8 +766,10 @@ struct RecShared {
     uint32_t base[3];
     uint32_t ticket;
     uint32_t any_cmp;
-    uint2 stage[BLOCK / 64][32 * 9];   // per-wave qdisc staging (wave_store_qdisc)
-    uint32_t hash[CAP];
+    union {                       // CalcDiff hashes, then (emission) per-wave qdisc staging
+        uint32_t hash[CAP];
+        uint2 stage[BLOCK / 64][32 * 9];
+    };
     uint16_t rank[CAP];          // entry position within the workgroup's list
     uint16_t tgt[CAP];           // upd target, relative to the workgroup's first desired record
     uint8_t flag[CAP];
@@ -921,6 +956,32 @@ __device__ void lookback(RecShared& s, const RecWork& wk, uint32_t wg) {
     __syncthreads();
 }
 
+// First chunk (TPW topologies = one k_reconcile workgroup) holding a topology that does NOT
+// emit every one of its records as an entry. A topology without element comparisons
+// (a nil or empty side) emits all records when its action is DIFF (all old → DelLinks,
+// all new → AddLinks) and none otherwise, so it is "full" iff DIFF or both lists are
+// empty; a topology needing comparisons is conservatively not full. Chunks up to and
+// including the first partial one know their batch bases from the record offsets alone.
+__global__ void __launch_bounds__(BLOCK) k_full_prefix(DevTopos T, uint32_t* first_partial) {
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    bool partial = false;
+    if (t < T.n) {
+        const uint8_t tf = T.flags[t];
+        const uint32_t ko = T.real_off[t + 1] - T.real_off[t], kn = T.des_off[t + 1] - T.des_off[t];
+        const bool st_nil = tf & KDTN_TOPO_STATUS_NIL, sp_nil = tf & KDTN_TOPO_SPEC_NIL;
+        const bool cmp = !st_nil && !sp_nil && ko > 0 && kn > 0;
+        const bool empty = ko == 0 && kn == 0;
+        // action (topology_controller.go:77-88) of a topology without comparisons
+        const bool diff = (st_nil || sp_nil) ? (!st_nil && sp_nil) : !empty;
+        partial = cmp || !(diff || empty);
+    }
+    const uint64_t m = __ballot(partial);
+    if (m && (threadIdx.x & 63) == 0) {
+        const uint32_t t0 = blockIdx.x * BLOCK + (threadIdx.x & ~63u) + (uint32_t)(__ffsll((long long)m) - 1);
+        atomicMin(first_partial, t0 / TPW);
+    }
+}
+
 // (VAR_TRACE) phase timestamp of this workgroup: 100 MHz chip-wide clock
 template <int V>
 KD_INLINE void trace_mark(const RecWork& wk, uint32_t wg, int k, unsigned long long t0 = 0) {
@@ -930,8 +991,8 @@ KD_INLINE void trace_mark(const RecWork& wk, uint32_t wg, int k, unsigned long l
 }
 
 template <int V>
-__global__ void __launch_bounds__(BLOCK) k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb,
-                                                     RecOut out, RecWork wk) {
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(var_waves(V))))
+k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWork wk) {
     __shared__ RecShared s;
     const int tid = threadIdx.x;
     unsigned long long t_entry = 0;
@@ -1058,7 +1119,22 @@ __global__ void __launch_bounds__(BLOCK) k_reconcile(DevTopos T, DevLinks O, Dev
 
     // ---- 3. batch bases: decoupled look-back -------------------------------------------
     trace_mark<V>(wk, wg, 2);
-    lookback(s, wk, wg);
+    constexpr bool NTL = (V & VAR_NT_LOAD) != 0;
+    // Every topology before this workgroup's chunk emits all of its records (bulk DIFF:
+    // k_full_prefix found no earlier exception): the batch bases are the record offsets of
+    // the chunk, known without waiting on the predecessors. The inclusive prefix is
+    // published at once so that later workgroups' look-backs stop here.
+    if ((V & VAR_NO_PREFIX) == 0 && wg <= *wk.first_partial) {
+        if (tid < 3) {
+            const uint32_t p = tid == 0 ? s.ooff[0] : (tid == 1 ? 0u : s.noff[0]);
+            __hip_atomic_store(wk.status + (size_t)wg * 3 + tid, (2ull << 32) | (p + s.wtot[tid]),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s.base[tid] = p;
+        }
+        __syncthreads();
+    } else {
+        lookback(s, wk, wg);
+    }
     trace_mark<V>(wk, wg, 3);
     const uint32_t bd = s.base[0], bu = s.base[1], ba = s.base[2];
     if (wg == wk.nwg - 1 && tid < 3) {
@@ -1075,7 +1151,6 @@ __global__ void __launch_bounds__(BLOCK) k_reconcile(DevTopos T, DevLinks O, Dev
 
     // ---- 4. emission -------------------------------------------------------------------
     uint2* stage = s.stage[tid >> 6];
-    constexpr bool NTL = (V & VAR_NT_LOAD) != 0;
     if (bulk) {
         // Every record of a DIFF topology is an entry at topology offset + index. Software
         // pipelined: a thread's next record's columns are loaded right after this record's
@@ -1245,5 +1320,11 @@ template __global__ void k_reconcile<65>(DevTopos, DevLinks, DevLinks, DevTables
 template __global__ void k_reconcile<97>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
 template __global__ void k_reconcile<101>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
 template __global__ void k_reconcile<113>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
+template __global__ void k_reconcile<129>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
+template __global__ void k_reconcile<257>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
+template __global__ void k_reconcile<513>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
+template __global__ void k_reconcile<529>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
+template __global__ void k_reconcile<1025>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
+template __global__ void k_reconcile<1537>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
 
 }  // namespace kdtn

@@ -229,3 +229,30 @@ def test_config2_full_size_properties(engine):
     assert out.add_idx[s:e].tobytes() == ora.add_idx.tobytes()
     assert out.add_res[s:e].tobytes() == ora.add_res.tobytes()
     assert out.add_qdisc[s:e].tobytes() == ora.add_qdisc.tobytes()
+
+
+@pytest.mark.parametrize("variant", [513, 1025, 1537, 129, 0])
+def test_emission_variants_match_oracle(engine, variant, monkeypatch):
+    """Every non-profiling KDTN_VARIANT of k_reconcile (occupancy target, masked gathers,
+    early issue before the look-back) produces the oracle's bytes."""
+    monkeypatch.setenv("KDTN_VARIANT", str(variant))
+    for seed in (3, 17):
+        topos, inp = random_epoch_input(seed, T=150)
+        assert_same(engine.reconcile(inp), O.reconcile(inp, tick=TICK), f"v{variant} seed {seed}")
+    inp = synth.make(2, pods_per_shard=20000)
+    assert_same(engine.reconcile(inp), O.reconcile(inp, tick=TICK), f"v{variant} config 2")
+
+
+@pytest.mark.parametrize("variant", [1, 1025])
+def test_full_prefix_shortcut_boundaries(engine, variant, monkeypatch):
+    """k_full_prefix: chunks before the first partial topology take their batch bases from
+    the record offsets, later ones run the look-back. A CREATED topology (and one needing
+    comparisons) in the middle of an all-AddLinks epoch moves that boundary."""
+    monkeypatch.setenv("KDTN_VARIANT", str(variant))
+    inp = synth.make(2, pods_per_shard=20000)
+    inp.topos.flags = inp.topos.flags.copy()
+    inp.topos.flags[7001] |= abi.TOPO_STATUS_NIL            # CREATED: no entries
+    inp.topos.flags[13000] |= abi.TOPO_SPEC_NIL if inp.topos.des_off[13001] == inp.topos.des_off[13000] else 0
+    assert_same(engine.reconcile(inp), O.reconcile(inp, tick=TICK), f"v{variant} boundary")
+    inp3 = synth.make(3, pods_per_shard=20000)               # churn: comparisons everywhere
+    assert_same(engine.reconcile(inp3), O.reconcile(inp3, tick=TICK), f"v{variant} churn")
