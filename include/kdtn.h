@@ -278,6 +278,26 @@ int kdtn_epoch_download(kdtn_ctx* ctx, kdtn_batches* out);   /* after sync      
 int kdtn_make_qdiscs(kdtn_ctx* ctx, const kdtn_strtab* pdict, const kdtn_props_table* props,
                      kdtn_qdisc* out);
 
+/* ---- wire encoding of the batches (proto/v1 LinksBatchQuery) ------------------------ */
+/* The request bodies Reconcile sends after CalcDiff: for topology t and list l (0 DelLinks,
+ * 1 AddLinks, 2 UpdateLinks) the bytes of proto.Marshal(&pb.LinksBatchQuery{LocalPod:
+ * &pb.Pod{Name, SrcIp, NetNs, KubeNs}, Links: common.Map(links, Link.ToProto)})
+ * (controllers/topology_controller.go:180-188, 223-231, 266-274;
+ * api/v1/topology_types.go:97-109,178-194). Arena regions del | add | upd, topology order:
+ * batch (l, t) = bytes[off[l*T + t], off[l*T + t + 1]); empty when the list is empty (no
+ * RPC) or when Marshal fails on a string that is not valid UTF-8 (err[t] bit l).      */
+typedef struct kdtn_wire {
+    uint8_t*  bytes;        /* [cap] arena                                               */
+    uint64_t  cap;          /* in: arena capacity                                        */
+    uint64_t* off;          /* [3T+1] batch byte offsets                                 */
+    uint32_t* err;          /* [T] bit l: list l of the topology failed to marshal        */
+    uint64_t  n_bytes;      /* out: arena bytes used                                     */
+} kdtn_wire;
+/* After kdtn_epoch_run (any stages) + kdtn_epoch_sync: encode every batch on the GPU;
+ * returns the arena size through n_bytes. Synchronous. */
+int kdtn_epoch_encode(kdtn_ctx* ctx, uint64_t* n_bytes);
+int kdtn_epoch_download_wire(kdtn_ctx* ctx, kdtn_wire* out);
+
 /* ---- multi-GPU (one process per GPU): RCCL all-gather of the pod-status table ------ */
 int kdtn_comm_unique_id(uint8_t out[128]);
 int kdtn_comm_init(kdtn_ctx* ctx, const uint8_t unique_id[128], int nranks, int rank);

@@ -81,6 +81,10 @@ struct kdtn_ctx {
     // outputs
     DevBuf action, del_off, add_off, upd_off, del_idx, add_idx, upd_idx;
     DevBuf del_res, add_res, upd_res, add_qdisc, upd_qdisc;
+    // wire encoding
+    DevBuf kd_utf8, pd_utf8, w_rel, w_topo, w_size, w_err, w_off, w_part, w_arena;
+    uint64_t w_bytes = 0;
+    bool encoded = false;
     // host-visible counters
     uint32_t* h_misc = nullptr;   // pinned: [0]=default id, [1]=del, [2]=upd, [3]=add, [4]=look-back error
     bool uploaded = false;
@@ -349,7 +353,8 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->pod_slots, &c->pod_wide, &c->otarget, &c->sync, &c->misc, &c->hscratch,
                       &c->fscratch, &c->action, &c->del_off, &c->add_off, &c->upd_off, &c->del_idx,
                       &c->add_idx, &c->upd_idx, &c->del_res, &c->add_res, &c->upd_res,
-                      &c->add_qdisc, &c->upd_qdisc};
+                      &c->add_qdisc, &c->upd_qdisc, &c->kd_utf8, &c->pd_utf8, &c->w_rel,
+                      &c->w_topo, &c->w_size, &c->w_err, &c->w_off, &c->w_part, &c->w_arena};
     for (DevBuf* b : bufs) release(*b);
     for (int i = 0; i <= kMaxTimers; ++i)
         if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
@@ -584,6 +589,7 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         case 513: k_reconcile<513><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
         case 1025: k_reconcile<1025><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
         case 1537: k_reconcile<1537><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
+        case 641: k_reconcile<641><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
         case 529: k_reconcile<529><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
         case 129: k_reconcile<129><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
         case 257: k_reconcile<257><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
@@ -604,6 +610,7 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
     HIP_TRY(hipMemcpyAsync(c->h_misc, misc, 16, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipMemcpyAsync(c->h_misc + 4, dp<uint32_t>(c->sync) + 1, 4, hipMemcpyDeviceToHost, s));
     c->ran = true;
+    c->encoded = false;
     return KDTN_OK;
 }
 
@@ -706,6 +713,94 @@ int kdtn_make_qdiscs(kdtn_ctx* c, const kdtn_strtab* pdict, const kdtn_props_tab
     if (n) HIP_TRY(hipMemcpyAsync(out, c->add_qdisc.p, (size_t)n * 72, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     c->uploaded = false;   // the desired store was reused
+    return KDTN_OK;
+}
+
+int kdtn_epoch_encode(kdtn_ctx* c, uint64_t* n_bytes) {
+    if (!c || !c->ran) return KDTN_EINVAL;
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    hipStream_t s = c->stream;
+    const uint32_t nd = c->h_misc[1], nu = c->h_misc[2], na = c->h_misc[3];
+    const uint32_t T = c->T;
+    const uint64_t ne = (uint64_t)nd + na + nu;
+    if (ne > 0xFFFFFFFFull || 3ull * T + 1 > 0xFFFFFFFFull) return KDTN_EINVAL;
+    const uint32_t kw = (uint32_t)(((uint64_t)c->D + 63) / 64 * 2), pw = (uint32_t)(((uint64_t)c->P + 63) / 64 * 2);
+    TRY(ensure(c->kd_utf8, (size_t)kw * 4));
+    TRY(ensure(c->pd_utf8, (size_t)pw * 4));
+    TRY(ensure(c->w_rel, (size_t)ne * 4));
+    TRY(ensure(c->w_topo, (size_t)ne * 4));
+    TRY(ensure(c->w_size, (size_t)3 * T * 4));
+    TRY(ensure(c->w_err, align_up((size_t)T * 4, 16)));
+    TRY(ensure(c->w_off, ((size_t)3 * T + 1) * 8));
+    const uint32_t nb = nblocks((uint64_t)3 * T + 1, SCAN_CHUNK);
+    TRY(ensure(c->w_part, (size_t)nb * 8));
+    c->n_ev = 0;
+    (void)hipEventRecord(c->ev[0], s);
+    if (c->D) k_utf8_bits<<<nblocks(c->D), BLOCK, 0, s>>>(dp<uint8_t>(c->kd_bytes), dp<uint32_t>(c->kd_offs), c->D,
+                                                          dp<uint32_t>(c->kd_utf8));
+    if (c->P) k_utf8_bits<<<nblocks(c->P), BLOCK, 0, s>>>(dp<uint8_t>(c->pd_bytes), dp<uint32_t>(c->pd_offs), c->P,
+                                                          dp<uint32_t>(c->pd_utf8));
+    timer_mark(c, "wire_utf8");
+    HIP_TRY(hipMemsetAsync(c->w_err.p, 0, align_up((size_t)T * 4, 16), s));
+    WireIn w{};
+    w.kd_bytes = dp<uint8_t>(c->kd_bytes);
+    w.kd_offs = dp<uint32_t>(c->kd_offs);
+    w.kd_utf8 = dp<uint32_t>(c->kd_utf8);
+    w.pd_bytes = dp<uint8_t>(c->pd_bytes);
+    w.pd_offs = dp<uint32_t>(c->pd_offs);
+    w.pd_utf8 = dp<uint32_t>(c->pd_utf8);
+    w.t_name = dp<uint32_t>(c->t_name);
+    w.t_src = dp<uint32_t>(c->t_src);
+    w.t_netns = dp<uint32_t>(c->t_netns);
+    w.t_ns = dp<uint32_t>(c->t_ns);
+    w.list_off[0] = dp<uint32_t>(c->del_off);
+    w.list_off[1] = dp<uint32_t>(c->add_off);
+    w.list_off[2] = dp<uint32_t>(c->upd_off);
+    w.list_idx[0] = dp<uint32_t>(c->del_idx);
+    w.list_idx[1] = dp<uint32_t>(c->add_idx);
+    w.list_idx[2] = dp<uint32_t>(c->upd_idx);
+    w.list_base[0] = 0;
+    w.list_base[1] = nd;
+    w.list_base[2] = nd + na;
+    w.n_entries = (uint32_t)ne;
+    w.T = T;
+    WireWork wk{dp<uint32_t>(c->w_rel), dp<uint32_t>(c->w_topo), dp<uint32_t>(c->w_size), dp<uint32_t>(c->w_err),
+                dp<uint64_t>(c->w_off)};
+    if (T) k_wire_sizes<<<nblocks((uint64_t)3 * T), BLOCK, 0, s>>>(w, c->real.view, c->des.view, wk);
+    timer_mark(c, "wire_sizes");
+    const uint32_t n = 3 * T;
+    k_scan_partial<<<nb, BLOCK, 0, s>>>(dp<uint32_t>(c->w_size), n, dp<uint64_t>(c->w_part));
+    k_scan_top<<<1, BLOCK, 0, s>>>(dp<uint64_t>(c->w_part), nb);
+    k_scan_final<<<nb, BLOCK, 0, s>>>(dp<uint32_t>(c->w_size), n, dp<uint64_t>(c->w_part), dp<uint64_t>(c->w_off));
+    timer_mark(c, "wire_scan");
+    HIP_TRY(hipGetLastError());
+    uint64_t total = 0;
+    HIP_TRY(hipMemcpyAsync(&total, dp<uint64_t>(c->w_off) + n, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    TRY(ensure(c->w_arena, (size_t)total + 16));
+    timer_mark(c, "wire_host_sync");                // the arena size crosses to the host
+    if (ne) k_wire_write<<<nblocks(ne), BLOCK, 0, s>>>(w, c->real.view, c->des.view, wk, dp<uint8_t>(c->w_arena));
+    timer_mark(c, "wire_write");
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(s));
+    c->w_bytes = total;
+    c->encoded = true;
+    if (n_bytes) *n_bytes = total;
+    return KDTN_OK;
+}
+
+int kdtn_epoch_download_wire(kdtn_ctx* c, kdtn_wire* o) {
+    if (!c || !o || !c->encoded) return KDTN_EINVAL;
+    HIP_TRY(hipSetDevice(c->device));
+    o->n_bytes = c->w_bytes;
+    if (o->bytes && c->w_bytes > o->cap) return KDTN_ENOSPC;
+    hipStream_t s = c->stream;
+    if (o->bytes && c->w_bytes)
+        HIP_TRY(hipMemcpyAsync(o->bytes, c->w_arena.p, c->w_bytes, hipMemcpyDeviceToHost, s));
+    if (o->off) HIP_TRY(hipMemcpyAsync(o->off, c->w_off.p, ((size_t)3 * c->T + 1) * 8, hipMemcpyDeviceToHost, s));
+    if (o->err && c->T) HIP_TRY(hipMemcpyAsync(o->err, c->w_err.p, (size_t)c->T * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
     return KDTN_OK;
 }
 

@@ -185,6 +185,38 @@ __global__ void k_vni_pack(const uint32_t* node, const int32_t* vni, const uint3
 template <int V>
 __global__ void k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out,
                             RecWork wk);
+
+// ---- wire encoding of the batches (kdtn_wire.hip) --------------------------------------
+constexpr int SCAN_CHUNK = BLOCK * 4;   // values per block of the batch-offset scan
+struct WireIn {
+    const uint8_t* kd_bytes;
+    const uint32_t* kd_offs;
+    const uint32_t* kd_utf8;        // bitset: kdict string is not valid UTF-8
+    const uint8_t* pd_bytes;
+    const uint32_t* pd_offs;
+    const uint32_t* pd_utf8;
+    const uint32_t* t_name;
+    const uint32_t* t_src;
+    const uint32_t* t_netns;
+    const uint32_t* t_ns;
+    const uint32_t* list_off[3];    // del_off, add_off, upd_off
+    const uint32_t* list_idx[3];    // del_idx, add_idx, upd_idx
+    uint32_t list_base[3];          // global entry index of each list's first entry
+    uint32_t n_entries, T;
+};
+struct WireWork {
+    uint32_t* rel;                  // [entries] offset of the entry inside its batch
+    uint32_t* topo;                 // [entries] topology of the entry
+    uint32_t* size;                 // [3T] batch sizes (0: empty list or Marshal error)
+    uint32_t* err;                  // [T] bit l: list l failed to marshal
+    const uint64_t* off;            // [3T+1] batch byte offsets
+};
+__global__ void k_utf8_bits(const uint8_t* bytes, const uint32_t* offs, uint32_t n, uint32_t* bits);
+__global__ void k_wire_sizes(WireIn w, DevLinks O, DevLinks N, WireWork wk);
+__global__ void k_scan_partial(const uint32_t* size, uint32_t n, uint64_t* part);
+__global__ void k_scan_top(uint64_t* part, uint32_t nb);
+__global__ void k_scan_final(const uint32_t* size, uint32_t n, const uint64_t* part, uint64_t* off);
+__global__ void k_wire_write(WireIn w, DevLinks O, DevLinks N, WireWork wk, uint8_t* arena);
 __global__ void k_qdisc_batch(DevLinks props, DevTables tb, uint2* out);
 __global__ void k_full_prefix(DevTopos T, uint32_t* first_partial);
 

@@ -56,6 +56,20 @@ KD_INLINE bool props_eq(const DevLinks& A, uint32_t i, const DevLinks& B, uint32
     return eq;
 }
 
+// Table gather with a 32-bit byte offset from a uniform base: selects the global_load
+// "saddr" form (SGPR base + one offset VGPR) instead of a per-lane 64-bit address, which
+// saves a VGPR pair and the 64-bit address arithmetic per gather. Every gathered table is
+// well under 4 GiB (dictionaries, pod/VNI tables, bitsets).
+template <typename T>
+KD_INLINE T ldg(const T* base, uint32_t idx) {
+    return *reinterpret_cast<const T*>(reinterpret_cast<const uint8_t*>(base) + idx * (uint32_t)sizeof(T));
+}
+template <typename T>
+KD_INLINE T ldg_nt(const T* base, uint32_t idx) {
+    return __builtin_nontemporal_load(
+        reinterpret_cast<const T*>(reinterpret_cast<const uint8_t*>(base) + idx * (uint32_t)sizeof(T)));
+}
+
 // largest tt in [lo, hi) with off[tt] <= idx  (the segment containing idx)
 KD_INLINE int find_seg(const uint32_t* off, int lo, int hi, uint32_t idx) {
     while (hi - lo > 1) {
@@ -74,13 +88,14 @@ KD_INLINE uint64_t lanemask_lt() {
 // Stage the arena bytes of strings [s0, s1) into LDS with 16-B coalesced loads.
 // Returns the LDS image base (byte a0 of the arena maps to buf), or nullptr when the
 // slice does not fit (caller then reads the strings from global memory).
+template <int CAPB = STAGE>
 KD_INLINE const uint8_t* stage_slice(const uint8_t* bytes, const uint32_t* offs, uint32_t s0,
                                      uint32_t s1, uint4* buf, uint32_t* a0_out) {
     const uint32_t b0 = offs[s0], b1 = offs[s1];
     const uint32_t a0 = b0 & ~15u;
     *a0_out = a0;
     const uint32_t words = (b1 - a0 + 15) >> 4;
-    if (words * 16 > (uint32_t)STAGE) return nullptr;   // uniform across the block
+    if (words * 16 > (uint32_t)CAPB) return nullptr;    // uniform across the block
     const uint4* src = reinterpret_cast<const uint4*>(bytes + a0);
     for (uint32_t w = threadIdx.x; w < words; w += BLOCK) buf[w] = src[w];
     return reinterpret_cast<const uint8_t*>(buf);
@@ -167,29 +182,15 @@ KD_INLINE bool cidr_swar(const uint32_t* w, uint32_t len, bool* slow) {
 __global__ void __launch_bounds__(BLOCK) k_kdict_flags(const uint8_t* bytes, const uint32_t* offs,
                                                        uint32_t n, uint32_t* kbits, uint32_t kb_words,
                                                        uint32_t* special) {
-    // The block's arena slice is staged through LDS with 16-B coalesced loads; each lane then
-    // reads its string's first 28 bytes from LDS (7 aligned dwords) instead of issuing seven
-    // overlapping unaligned global loads.
-    __shared__ uint4 buf[STAGE / 16 + 2];                  // +32 B: reads past the slice end
-    const uint32_t s0 = blockIdx.x * BLOCK, s1 = min(s0 + BLOCK, n);
-    uint32_t a0 = 0;
-    const bool staged = s0 < n && stage_slice(bytes, offs, s0, s1, buf, &a0) != nullptr;
-    __syncthreads();
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     uint32_t f = 0;
     if (i < n) {
         const uint32_t b = offs[i], len = offs[i + 1] - b;
         const uint32_t a = b & ~3u, sh = (b & 3u) * 8u;
+        const uint32_t* p = reinterpret_cast<const uint32_t*>(bytes + a);   // arena has 64 B slack
         uint32_t d[7], w[6];
-        if (staged) {
-            const uint32_t* p = reinterpret_cast<const uint32_t*>(buf) + ((a - a0) >> 2);
 #pragma unroll
-            for (int k = 0; k < 7; ++k) d[k] = p[k];
-        } else {
-            const uint32_t* p = reinterpret_cast<const uint32_t*>(bytes + a);   // arena has 64 B slack
-#pragma unroll
-            for (int k = 0; k < 7; ++k) d[k] = p[k];
-        }
+        for (int k = 0; k < 7; ++k) d[k] = p[k];
 #pragma unroll
         for (int k = 0; k < 6; ++k)
             w[k] = sh ? (d[k] >> sh) | (d[k + 1] << (32u - sh)) : d[k];
@@ -362,10 +363,10 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 template <bool NT>
 KD_INLINE uint4 pod_slot(const DevTables& tb, uint32_t h) {
     if constexpr (NT) {           // little reuse: keep L2 for the parsed tables
-        const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(tb.pod_wide) + h);
+        const u32x4 v = ldg_nt(reinterpret_cast<const u32x4*>(tb.pod_wide), h);
         return make_uint4(v.x, v.y, v.z, v.w);
     } else {
-        return tb.pod_wide[h];
+        return ldg(tb.pod_wide, h);
     }
 }
 // Resolve a lookup whose home slot h already read as w (probing continues in the bucket).
@@ -392,9 +393,9 @@ KD_INLINE uint32_t vni_lookup(const DevTables& tb, uint32_t node, int32_t vni) {
     if (tb.vni_mask == 0) return 0xFFFFFFFFu;
     uint32_t h = (uint32_t)hash64(((uint64_t)node << 32) | (uint32_t)vni) & tb.vni_mask;
     for (;;) {
-        const uint32_t v = tb.vni_slots[h];
+        const uint32_t v = ldg(tb.vni_slots, h);
         if (v == 0xFFFFFFFFu) return 0xFFFFFFFFu;
-        const uint4 e = tb.vnis[v];
+        const uint4 e = ldg(tb.vnis, v);
         if (e.x == node && e.y == (uint32_t)vni) return e.z;
         h = (h + 1) & tb.vni_mask;
     }
@@ -446,21 +447,21 @@ KD_INLINE void gather_props(const RecCols& c, const DevTables& tb, PropVals& v) 
     if constexpr ((V & VAR_MASK_EMPTY) != 0) {
         // "" (id 0) parses to 0 in every table: only lanes with a string issue the gather
         const uint32_t il = c.prop[KDTN_P_LATENCY], ij = c.prop[KDTN_P_JITTER], ir = c.prop[KDTN_P_RATE];
-        v.lat = il ? tb.pdur[il] : make_uint2(0u, 0u);
-        v.jit = ij ? tb.pdur[ij] : make_uint2(0u, 0u);
-        v.rt = ir ? tb.prate[ir] : make_uint2(0u, 0u);
+        v.lat = il ? ldg(tb.pdur, il) : make_uint2(0u, 0u);
+        v.jit = ij ? ldg(tb.pdur, ij) : make_uint2(0u, 0u);
+        v.rt = ir ? ldg(tb.prate, ir) : make_uint2(0u, 0u);
     } else {
-        v.lat = tb.pdur[c.prop[KDTN_P_LATENCY]];
-        v.jit = tb.pdur[c.prop[KDTN_P_JITTER]];
-        v.rt = tb.prate[c.prop[KDTN_P_RATE]];
+        v.lat = ldg(tb.pdur, c.prop[KDTN_P_LATENCY]);
+        v.jit = ldg(tb.pdur, c.prop[KDTN_P_JITTER]);
+        v.rt = ldg(tb.prate, c.prop[KDTN_P_RATE]);
     }
 #pragma unroll
     for (int k = 0; k < 9; ++k) {
         const uint32_t id = c.prop[PCT_FIELDS[k]];
         // (VAR_SKIP_PCT: profiling only, wrong results) the id stands in for the parsed value
         if constexpr ((V & VAR_SKIP_PCT) != 0) v.pct[k] = id;
-        else if constexpr ((V & VAR_MASK_EMPTY) != 0) v.pct[k] = id ? tb.ppct[id] : 0u;
-        else v.pct[k] = tb.ppct[id];
+        else if constexpr ((V & VAR_MASK_EMPTY) != 0) v.pct[k] = id ? ldg(tb.ppct, id) : 0u;
+        else v.pct[k] = ldg(tb.ppct, id);
     }
     uint32_t any = c.gap;
 #pragma unroll
@@ -473,7 +474,7 @@ KD_INLINE void gather_props(const RecCols& c, const DevTables& tb, PropVals& v) 
 KD_INLINE bool dur_err(uint2 d) { return d.x == 0u && d.y == 1u; }
 KD_INLINE bool rate_bad(const DevTables& tb, const PropVals& v) {
     if ((v.rt.x & v.rt.y) != 0xFFFFFFFFu) return false;          // rare: error or 2^64-1
-    return (tb.rate_err[v.rate_id >> 5] >> (v.rate_id & 31)) & 1u;
+    return (ldg(tb.rate_err, v.rate_id >> 5) >> (v.rate_id & 31)) & 1u;
 }
 
 // MakeQdiscs over parsed dictionary entries (common/qdisc.go:20-126 + netlink NewNetem)
@@ -573,7 +574,7 @@ KD_INLINE uint4 pack_res(uint32_t peer, int32_t vni, uint32_t vtep, uint32_t kin
 }
 
 KD_INLINE bool kbit(const DevTables& tb, int set, uint32_t id) {
-    return (tb.kbits[(size_t)set * tb.kb_words + (id >> 5)] >> (id & 31)) & 1u;
+    return (ldg(tb.kbits + (size_t)set * tb.kb_words, id >> 5) >> (id & 31)) & 1u;
 }
 
 // MakeVeth(netns, intf, ip, mac) validity from key-string predicates (common/veth.go:21-36)
@@ -639,8 +640,8 @@ KD_INLINE void add_gather(const RecCols& c, const TopoCtx& tc, const DevTables& 
     if (qd) gather_props<V>(c, tb, g.v);
     if (!res) return;
     g.lns = tc.ns == 0 ? tb.special[SPECIAL_DEFAULT] : tc.ns;                     // :29-31
-    g.kb_ip = tb.kbits[(size_t)KB_CIDR_BAD * tb.kb_words + (c.lip >> 5)];
-    g.kb_mac = tb.kbits[(size_t)KB_MAC_BAD * tb.kb_words + (c.lmac >> 5)];
+    g.kb_ip = ldg(tb.kbits + (size_t)KB_CIDR_BAD * tb.kb_words, c.lip >> 5);
+    g.kb_mac = ldg(tb.kbits + (size_t)KB_MAC_BAD * tb.kb_words, c.lmac >> 5);
     if constexpr ((V & VAR_SKIP_POD) == 0) {
         g.h = pod_home(tb.pod_mask, g.lns, c.pp);
         g.slot = pod_slot<(V & VAR_NT_POD) != 0>(tb, g.h);
@@ -693,7 +694,7 @@ KD_INLINE void add_finish(const RecCols& c, const AddGath& g, const DevLinks& N,
                 vtep = p_src;
                 if (tb.vni_mask) {                                       // remote Update check
                     const uint32_t nsx = vni_lookup(tb, p_src, vni);
-                    hit = (nsx != 0xFFFFFFFFu && nsx != (tb.pods[peer].w & 0x7FFFFFFFu));
+                    hit = (nsx != 0xFFFFFFFFu && nsx != (ldg(tb.pods, peer).w & 0x7FFFFFFFu));
                 }
             }
         }
@@ -1324,6 +1325,7 @@ template __global__ void k_reconcile<129>(DevTopos, DevLinks, DevLinks, DevTable
 template __global__ void k_reconcile<257>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
 template __global__ void k_reconcile<513>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
 template __global__ void k_reconcile<529>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
+template __global__ void k_reconcile<641>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
 template __global__ void k_reconcile<1025>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
 template __global__ void k_reconcile<1537>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
 

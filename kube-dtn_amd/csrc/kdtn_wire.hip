@@ -1,0 +1,287 @@
+// kdtn_wire.hip — protobuf wire encoding of the epoch's batches on the GPU (SURVEY §8(f)
+// rank 1): for every Topology and list (DelLinks, AddLinks, UpdateLinks) the bytes of
+//
+//   proto.Marshal(&pb.LinksBatchQuery{LocalPod: &pb.Pod{Name, SrcIp, NetNs, KubeNs},
+//                                     Links: common.Map(links, v1.Link.ToProto)})
+//
+// that Reconcile sends (controllers/topology_controller.go:180-188, 223-231, 266-274;
+// api/v1/topology_types.go:97-109,178-194; proto/v1/kube_dtn.proto:8-53,65-68), so the Go
+// side can hand them to the gRPC stream without ToProto + Marshal per link.
+//
+// Layout: one byte arena, regions del | add | upd, each in topology order; batch (l, t)
+// occupies [off[l*T+t], off[l*T+t+1]) (empty when the list is empty — no RPC — or when a
+// string is not valid UTF-8, which makes Marshal fail; err[t] bit l marks the latter).
+//
+// Kernels (launch order, kdtn_epoch_encode):
+//   k_utf8_bits      unicode/utf8.ValidString per dictionary string → bitset (1 = invalid)
+//   k_wire_sizes     one thread per (list, topology): sizes of its Link messages, each
+//                    entry's offset inside the batch, batch size (0 on error)
+//   k_scan_*         exclusive scan of the 3T batch sizes → u64 offsets
+//   k_wire_write     one thread per entry: writes its Link (and, for the batch's first
+//                    entry, the LocalPod header) — string bytes copied from the arenas
+#include "kdtn_kernels.h"
+
+namespace kdtn {
+
+// ---- dictionary UTF-8 validity (Go unicode/utf8.ValidString) ---------------------------
+KD_INLINE bool utf8_ok(const uint8_t* s, uint32_t n) {
+    uint32_t i = 0;
+    while (i < n) {
+        const uint32_t c = s[i];
+        if (c < 0x80u) { ++i; continue; }
+        uint32_t need, lo = 0x80u, hi = 0xBFu;
+        if (c >= 0xC2u && c <= 0xDFu) need = 1;
+        else if (c == 0xE0u) { need = 2; lo = 0xA0u; }
+        else if (c >= 0xE1u && c <= 0xECu) need = 2;
+        else if (c == 0xEDu) { need = 2; hi = 0x9Fu; }
+        else if (c >= 0xEEu && c <= 0xEFu) need = 2;
+        else if (c == 0xF0u) { need = 3; lo = 0x90u; }
+        else if (c >= 0xF1u && c <= 0xF3u) need = 3;
+        else if (c == 0xF4u) { need = 3; hi = 0x8Fu; }
+        else return false;
+        if (i + need >= n) return false;
+        const uint32_t c1 = s[i + 1];
+        if (c1 < lo || c1 > hi) return false;
+        for (uint32_t k = 2; k <= need; ++k)
+            if (s[i + k] < 0x80u || s[i + k] > 0xBFu) return false;
+        i += need + 1;
+    }
+    return true;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_utf8_bits(const uint8_t* bytes, const uint32_t* offs,
+                                                     uint32_t n, uint32_t* bits) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    bool bad = false;
+    if (i < n) {
+        const uint32_t b = offs[i], len = offs[i + 1] - b;
+        bool ascii = true;
+        for (uint32_t k = 0; k < len && ascii; ++k) ascii = bytes[b + k] < 0x80u;
+        if (!ascii) bad = !utf8_ok(bytes + b, len);
+    }
+    const uint64_t m = __ballot(bad);
+    const int lane = threadIdx.x & 63;
+    if (lane == 0 || lane == 32) bits[((i - lane) >> 5) + (lane >> 5)] = lane ? (uint32_t)(m >> 32) : (uint32_t)m;
+}
+
+// ---- sizes ---------------------------------------------------------------------------------
+KD_INLINE uint32_t vlen(uint64_t v) {
+    uint32_t n = 1;
+    while (v >= 0x80u) { v >>= 7; ++n; }
+    return n;
+}
+KD_INLINE uint32_t str_field(uint32_t len) { return len ? 1u + vlen(len) + len : 0u; }
+KD_INLINE bool bit(const uint32_t* bits, uint32_t id) { return (bits[id >> 5] >> (id & 31)) & 1u; }
+KD_INLINE uint32_t slen(const uint32_t* offs, uint32_t id) { return offs[id + 1] - offs[id]; }
+
+// pb.LinkProperties / pb.Link sizes of record j; false if one of its strings is invalid UTF-8
+KD_INLINE bool link_sizes(const WireIn& w, const DevLinks& L, uint32_t j, uint32_t* psz, uint32_t* lsz) {
+    bool ok = true;
+    uint32_t p = 0;
+#pragma unroll
+    for (int k = 0; k < KDTN_NPROP; ++k) {
+        const uint32_t id = L.prop(k, j);
+        p += str_field(slen(w.pd_offs, id));
+        ok = ok && !bit(w.pd_utf8, id);
+    }
+    const uint32_t gap = L.gap(j);
+    if (gap) p += 1u + vlen(gap);
+    uint32_t l = 0;
+#pragma unroll
+    for (int k = 0; k < KDTN_NKEY; ++k) {
+        const uint32_t id = L.key(k, j);
+        l += str_field(slen(w.kd_offs, id));
+        ok = ok && !bit(w.kd_utf8, id);
+    }
+    const int64_t uid = L.uid(j);
+    if (uid) l += 1u + vlen((uint64_t)uid);
+    l += 1u + vlen(p) + p;
+    *psz = p;
+    *lsz = l;
+    return ok;
+}
+
+KD_INLINE uint32_t pod_size(const WireIn& w, uint32_t t, bool* ok) {
+    const uint32_t ids[4] = {w.t_name[t], w.t_src[t], w.t_netns[t], w.t_ns[t]};
+    uint32_t s = 0;
+    bool good = true;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        s += str_field(slen(w.kd_offs, ids[k]));
+        good = good && !bit(w.kd_utf8, ids[k]);
+    }
+    *ok = good;
+    return s;
+}
+
+// One thread per (list, topology): entry offsets inside the batch and the batch size.
+__global__ void __launch_bounds__(BLOCK) k_wire_sizes(WireIn w, DevLinks O, DevLinks N, WireWork wk) {
+    const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
+    if (g >= 3u * w.T) return;
+    const uint32_t lst = g / w.T, t = g - lst * w.T;
+    const uint32_t* off = w.list_off[lst];
+    const uint32_t* idx = w.list_idx[lst];
+    const DevLinks& L = lst == 0 ? O : N;
+    const uint32_t e0 = off[t], e1 = off[t + 1];
+    uint32_t size = 0;
+    if (e1 > e0) {
+        bool ok;
+        const uint32_t ps = pod_size(w, t, &ok);
+        uint64_t pos = 1u + vlen(ps) + ps;
+        for (uint32_t e = e0; e < e1; ++e) {
+            uint32_t psz, lsz;
+            ok = link_sizes(w, L, idx[e], &psz, &lsz) && ok;
+            wk.rel[w.list_base[lst] + e] = (uint32_t)pos;
+            wk.topo[w.list_base[lst] + e] = t;
+            pos += 1u + vlen(lsz) + lsz;
+        }
+        if (!ok || pos > 0xFFFFFFFFull) atomicOr(wk.err + t, 1u << lst);
+        else size = (uint32_t)pos;
+    }
+    wk.size[g] = size;
+}
+
+// ---- exclusive scan of the 3T batch sizes into u64 offsets -----------------------------
+KD_INLINE uint64_t block_exclusive(uint64_t v, uint64_t* sh, uint64_t* total) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint64_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t o = __shfl_up(x, d, 64);
+        if (lane >= d) x += o;
+    }
+    if (lane == 63) sh[wave] = x;
+    __syncthreads();
+    uint64_t base = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < BLOCK / 64; ++k) {
+        if (k < wave) base += sh[k];
+        tot += sh[k];
+    }
+    __syncthreads();
+    *total = tot;
+    return base + x - v;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_scan_partial(const uint32_t* size, uint32_t n, uint64_t* part) {
+    __shared__ uint64_t sh[BLOCK / 64];
+    const uint32_t b0 = blockIdx.x * SCAN_CHUNK + threadIdx.x * 4;
+    uint64_t v = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v += b0 + k < n ? size[b0 + k] : 0u;
+    uint64_t tot;
+    block_exclusive(v, sh, &tot);
+    if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+
+// single block: exclusive scan of the block totals in place
+__global__ void __launch_bounds__(BLOCK) k_scan_top(uint64_t* part, uint32_t nb) {
+    __shared__ uint64_t sh[BLOCK / 64];
+    uint64_t carry = 0;
+    for (uint32_t c = 0; c < nb; c += BLOCK) {
+        const uint32_t i = c + threadIdx.x;
+        const uint64_t v = i < nb ? part[i] : 0u;
+        uint64_t tot;
+        const uint64_t ex = block_exclusive(v, sh, &tot);
+        if (i < nb) part[i] = carry + ex;
+        carry += tot;
+    }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_scan_final(const uint32_t* size, uint32_t n, const uint64_t* part,
+                                                      uint64_t* off) {
+    __shared__ uint64_t sh[BLOCK / 64];
+    const uint32_t b0 = blockIdx.x * SCAN_CHUNK + threadIdx.x * 4;
+    uint32_t v[4];
+    uint64_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        v[k] = b0 + k < n ? size[b0 + k] : 0u;
+        sum += v[k];
+    }
+    uint64_t tot;
+    uint64_t x = part[blockIdx.x] + block_exclusive(sum, sh, &tot);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (b0 + k <= n) off[b0 + k] = x;     // off[n] = grand total
+        x += v[k];
+    }
+}
+
+// ---- writer --------------------------------------------------------------------------------
+KD_INLINE uint8_t* put_varint(uint8_t* p, uint64_t v) {
+    while (v >= 0x80u) {
+        *p++ = (uint8_t)(v | 0x80u);
+        v >>= 7;
+    }
+    *p++ = (uint8_t)v;
+    return p;
+}
+KD_INLINE uint8_t* put_str(uint8_t* p, uint32_t field, const uint8_t* arena, const uint32_t* offs, uint32_t id) {
+    const uint32_t b = offs[id], len = offs[id + 1] - b;
+    if (!len) return p;
+    *p++ = (uint8_t)(field << 3 | 2u);
+    p = put_varint(p, len);
+    for (uint32_t k = 0; k < len; ++k) p[k] = arena[b + k];
+    return p + len;
+}
+
+// One thread per entry of the three lists (global entry index g).
+__global__ void __launch_bounds__(BLOCK) k_wire_write(WireIn w, DevLinks O, DevLinks N, WireWork wk,
+                                                      uint8_t* arena) {
+    const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
+    if (g >= w.n_entries) return;
+    const uint32_t lst = g < w.list_base[1] ? 0u : (g < w.list_base[2] ? 1u : 2u);
+    const uint32_t e = g - w.list_base[lst];
+    const uint32_t t = wk.topo[g];
+    if ((wk.err[t] >> lst) & 1u) return;
+    const DevLinks& L = lst == 0 ? O : N;
+    const uint32_t j = w.list_idx[lst][e];
+    uint8_t* base = arena + wk.off[lst * w.T + t];
+    if (e == w.list_off[lst][t]) {                       // first entry: LocalPod header
+        bool ok;
+        const uint32_t ps = pod_size(w, t, &ok);
+        uint8_t* p = base;
+        *p++ = 1u << 3 | 2u;
+        p = put_varint(p, ps);
+        p = put_str(p, 1, w.kd_bytes, w.kd_offs, w.t_name[t]);
+        p = put_str(p, 2, w.kd_bytes, w.kd_offs, w.t_src[t]);
+        p = put_str(p, 3, w.kd_bytes, w.kd_offs, w.t_netns[t]);
+        p = put_str(p, 4, w.kd_bytes, w.kd_offs, w.t_ns[t]);
+    }
+    uint32_t psz, lsz;
+    link_sizes(w, L, j, &psz, &lsz);
+    uint8_t* p = base + wk.rel[g];
+    *p++ = 2u << 3 | 2u;
+    p = put_varint(p, lsz);
+    // pb.Link fields in number order: peer_pod 1, local_intf 2, peer_intf 3, local_ip 4,
+    // peer_ip 5, uid 6, properties 7, local_mac 8, peer_mac 9
+    p = put_str(p, 1, w.kd_bytes, w.kd_offs, L.key(KDTN_K_PEER_POD, j));
+    p = put_str(p, 2, w.kd_bytes, w.kd_offs, L.key(KDTN_K_LOCAL_INTF, j));
+    p = put_str(p, 3, w.kd_bytes, w.kd_offs, L.key(KDTN_K_PEER_INTF, j));
+    p = put_str(p, 4, w.kd_bytes, w.kd_offs, L.key(KDTN_K_LOCAL_IP, j));
+    p = put_str(p, 5, w.kd_bytes, w.kd_offs, L.key(KDTN_K_PEER_IP, j));
+    const int64_t uid = L.uid(j);
+    if (uid) {
+        *p++ = 6u << 3;
+        p = put_varint(p, (uint64_t)uid);
+    }
+    *p++ = 7u << 3 | 2u;
+    p = put_varint(p, psz);
+    // pb.LinkProperties: latency 1 .. rate 6, gap 7, duplicate 8 .. corrupt_corr 13 (KDTN_P_* order)
+#pragma unroll
+    for (int k = 0; k < KDTN_NPROP; ++k) {
+        if (k == KDTN_P_DUPLICATE) {
+            const uint32_t gap = L.gap(j);
+            if (gap) {
+                *p++ = 7u << 3;
+                p = put_varint(p, gap);
+            }
+        }
+        p = put_str(p, (uint32_t)(k < KDTN_P_DUPLICATE ? k + 1 : k + 2), w.pd_bytes, w.pd_offs, L.prop(k, j));
+    }
+    p = put_str(p, 8, w.kd_bytes, w.kd_offs, L.key(KDTN_K_LOCAL_MAC, j));
+    p = put_str(p, 9, w.kd_bytes, w.kd_offs, L.key(KDTN_K_PEER_MAC, j));
+}
+
+}  // namespace kdtn

@@ -104,6 +104,11 @@ class Counts(C.Structure):
                 ("n_topos", C.c_uint32)]
 
 
+class Wire(C.Structure):
+    _fields_ = [("bytes", C.c_void_p), ("cap", C.c_uint64), ("off", C.c_void_p), ("err", C.c_void_p),
+                ("n_bytes", C.c_uint64)]
+
+
 class Config(C.Structure):
     _fields_ = [("device", C.c_int32), ("vxlan_base", C.c_int32), ("tick_in_usec", C.c_double)]
 
@@ -125,7 +130,8 @@ EXPORTS = ["kdtn_version", "kdtn_strerror", "kdtn_err_name", "kdtn_init", "kdtn_
            "kdtn_interner_free", "kdtn_intern", "kdtn_intern_batch", "kdtn_interner_table",
            "kdtn_reconcile_epoch", "kdtn_epoch_upload", "kdtn_epoch_run", "kdtn_epoch_sync",
            "kdtn_epoch_download", "kdtn_make_qdiscs", "kdtn_comm_unique_id", "kdtn_comm_init",
-           "kdtn_last_kernel_times", "kdtn_debug_wg_trace"]
+           "kdtn_last_kernel_times", "kdtn_debug_wg_trace", "kdtn_epoch_encode",
+           "kdtn_epoch_download_wire"]
 
 
 def ptr(a: np.ndarray, t):

@@ -64,6 +64,8 @@ def lib() -> C.CDLL:
         "kdtn_comm_init": (C.c_int, [vp, C.POINTER(C.c_uint8 * 128), C.c_int, C.c_int]),
         "kdtn_last_kernel_times": (C.c_int, [vp, C.POINTER(C.c_char_p), C.POINTER(C.c_float), C.c_int]),
         "kdtn_debug_wg_trace": (C.c_int, [vp, C.POINTER(C.c_uint64), C.c_uint32]),
+        "kdtn_epoch_encode": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
+        "kdtn_epoch_download_wire": (C.c_int, [vp, C.POINTER(abi.Wire)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -153,6 +155,26 @@ class Engine:
         self.run(stages)
         self.sync()
         return self.download()
+
+    # ---- wire encoding of the batches (proto/v1 LinksBatchQuery) ------------------------
+    def encode(self) -> int:
+        """Encode every batch of the last epoch on the GPU (after run + sync); returns the
+        arena size in bytes."""
+        n = C.c_uint64()
+        _check(lib().kdtn_epoch_encode(self._ctx, C.byref(n)), "kdtn_epoch_encode")
+        return int(n.value)
+
+    def download_wire(self):
+        """(arena uint8, off uint64[3T+1], err uint32[T]) of the last kdtn_epoch_encode."""
+        w = abi.Wire()
+        _check(lib().kdtn_epoch_download_wire(self._ctx, C.byref(w)), "kdtn_epoch_download_wire")
+        n = int(w.n_bytes)
+        arena = np.zeros(max(n, 1), np.uint8)
+        off = np.zeros(3 * self._T + 1, np.uint64)
+        err = np.zeros(max(self._T, 1), np.uint32)
+        w.bytes, w.cap, w.off, w.err = arena.ctypes.data, arena.size, off.ctypes.data, err.ctypes.data
+        _check(lib().kdtn_epoch_download_wire(self._ctx, C.byref(w)), "kdtn_epoch_download_wire")
+        return arena[:n], off, err[:self._T]
 
     def kernel_times(self) -> dict[str, float]:
         names = (C.c_char_p * 16)()

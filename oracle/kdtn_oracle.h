@@ -60,6 +60,21 @@ int or_reconcile_epoch_timed(const kdtn_epoch_in* in, const or_pods* pods, doubl
                              int32_t vxlan_base, uint32_t t_begin, uint32_t t_end,
                              kdtn_batches* out, double* loop_seconds);
 
+/* ---- wire encoding of the batches (kdtn_oracle_wire.c) ---------------------------- */
+/* unicode/utf8.ValidString */
+int      or_utf8_valid(const uint8_t* s, uint32_t n);
+/* proto.Marshal(&pb.LinksBatchQuery{...}) of one batch of topology t: list 0 = DelLinks
+ * (realised records), 1 = AddLinks, 2 = UpdateLinks (desired records); idx = record
+ * indices. Returns the byte count (0 for an empty list: no RPC), or -1 when a string is
+ * not valid UTF-8 (Marshal error). out == NULL: size only. */
+int64_t  or_encode_batch(const kdtn_epoch_in* in, uint32_t t, int list, const uint32_t* idx,
+                         uint32_t n, uint8_t* out);
+/* Every batch of an epoch's outputs, regions del | add | upd in topology order:
+ * off[list*T + t] .. off[list*T + t + 1] (off has 3T+1 entries), err[t] bit list set when
+ * that batch failed to marshal (its range is empty). bytes == NULL: sizes only. */
+uint64_t or_encode_epoch(const kdtn_epoch_in* in, const kdtn_batches* b, uint32_t T,
+                         uint8_t* bytes, uint64_t* off, uint8_t* err);
+
 #ifdef __cplusplus
 }
 #endif

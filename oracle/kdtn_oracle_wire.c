@@ -1,0 +1,196 @@
+/*
+ * kdtn_oracle_wire.c — TEST INFRASTRUCTURE ONLY: CPU restatement of the gRPC request
+ * bodies the reference controller sends after CalcDiff, i.e. proto.Marshal of
+ *
+ *   &pb.LinksBatchQuery{LocalPod: &pb.Pod{Name, SrcIp, NetNs, KubeNs},
+ *                       Links: common.Map(links, v1.Link.ToProto)}
+ *
+ * for DelLinks / AddLinks / UpdateLinks (controllers/topology_controller.go:180-188,
+ * 223-231, 266-274; Link.ToProto / LinkProperties.ToProto api/v1/topology_types.go:97-109,
+ * 178-194; message schema proto/v1/kube_dtn.proto:8-53,65-68).
+ *
+ * Encoding rules restated from google.golang.org/protobuf (go.mod; proto3, no maps):
+ * fields in field-number order; scalars and strings omitted when zero / empty (implicit
+ * presence); a non-nil message field is always written, even when empty (ToProto always
+ * sets Properties, Reconcile always sets LocalPod); int64 as the varint of its two's
+ * complement (10 bytes when negative); a string field that is not valid UTF-8 makes
+ * Marshal fail ("string field contains invalid UTF-8"), so the RPC is never sent.
+ * tests/golden/make_wire_golden.py pins this file against the Python protobuf runtime.
+ */
+#include "kdtn_oracle.h"
+
+#include <string.h>
+
+typedef struct { const uint8_t* p; uint32_t n; } wstr;
+
+static wstr wget(const kdtn_strtab* t, uint32_t id) {
+    wstr s = {t->bytes + t->offs[id], t->offs[id + 1] - t->offs[id]};
+    return s;
+}
+
+/* unicode/utf8.ValidString (Go): no overlongs, no surrogates, max U+10FFFF */
+int or_utf8_valid(const uint8_t* s, uint32_t n) {
+    uint32_t i = 0;
+    while (i < n) {
+        uint8_t c = s[i];
+        if (c < 0x80) { i++; continue; }
+        uint32_t need, lo = 0x80, hi = 0xBF;
+        if (c >= 0xC2 && c <= 0xDF) need = 1;
+        else if (c == 0xE0) { need = 2; lo = 0xA0; }
+        else if (c >= 0xE1 && c <= 0xEC) need = 2;
+        else if (c == 0xED) { need = 2; hi = 0x9F; }
+        else if (c >= 0xEE && c <= 0xEF) need = 2;
+        else if (c == 0xF0) { need = 3; lo = 0x90; }
+        else if (c >= 0xF1 && c <= 0xF3) need = 3;
+        else if (c == 0xF4) { need = 3; hi = 0x8F; }
+        else return 0;
+        if (i + need >= n) return 0;                     /* truncated sequence */
+        uint8_t c1 = s[i + 1];
+        if (c1 < lo || c1 > hi) return 0;
+        for (uint32_t k = 2; k <= need; k++)
+            if (s[i + k] < 0x80 || s[i + k] > 0xBF) return 0;
+        i += need + 1;
+    }
+    return 1;
+}
+
+static uint32_t vlen(uint64_t v) {
+    uint32_t n = 1;
+    while (v >= 0x80) { v >>= 7; n++; }
+    return n;
+}
+static uint8_t* put_varint(uint8_t* p, uint64_t v) {
+    while (v >= 0x80) { *p++ = (uint8_t)(v | 0x80); v >>= 7; }
+    *p++ = (uint8_t)v;
+    return p;
+}
+/* string field: tag, length, bytes (omitted when empty) */
+static uint32_t str_size(wstr s) { return s.n ? 1 + vlen(s.n) + s.n : 0; }
+static uint8_t* put_str(uint8_t* p, uint32_t field, wstr s) {
+    if (!s.n) return p;
+    *p++ = (uint8_t)(field << 3 | 2);
+    p = put_varint(p, s.n);
+    memcpy(p, s.p, s.n);
+    return p + s.n;
+}
+
+/* pb.Link field numbers (kube_dtn.proto:17-27) for the key columns KDTN_K_* */
+static const uint32_t LINK_FIELD[KDTN_NKEY] = {2, 4, 8, 3, 5, 9, 1};   /* local_intf, local_ip, local_mac,
+                                                                           peer_intf, peer_ip, peer_mac, peer_pod */
+/* pb.LinkProperties field numbers (kube_dtn.proto:29-43) for KDTN_P_*; gap is field 7 */
+static const uint32_t PROP_FIELD[KDTN_NPROP] = {1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 13};
+
+typedef struct { const kdtn_epoch_in* in; const kdtn_link_table* L; uint32_t j; } wrec;
+
+static uint32_t props_size(wrec r) {
+    uint32_t n = 0;
+    for (int k = 0; k < KDTN_NPROP; k++) n += str_size(wget(&r.in->pdict, r.L->prop[k][r.j]));
+    if (r.L->gap[r.j]) n += 1 + vlen(r.L->gap[r.j]);
+    return n;
+}
+static uint32_t link_size(wrec r) {
+    uint32_t n = 0;
+    for (int k = 0; k < KDTN_NKEY; k++) n += str_size(wget(&r.in->kdict, r.L->key[k][r.j]));
+    if (r.L->uid[r.j]) n += 1 + vlen((uint64_t)r.L->uid[r.j]);
+    uint32_t ps = props_size(r);
+    n += 1 + vlen(ps) + ps;
+    return n;
+}
+static int link_utf8_ok(wrec r) {
+    for (int k = 0; k < KDTN_NKEY; k++) {
+        wstr s = wget(&r.in->kdict, r.L->key[k][r.j]);
+        if (!or_utf8_valid(s.p, s.n)) return 0;
+    }
+    for (int k = 0; k < KDTN_NPROP; k++) {
+        wstr s = wget(&r.in->pdict, r.L->prop[k][r.j]);
+        if (!or_utf8_valid(s.p, s.n)) return 0;
+    }
+    return 1;
+}
+static uint8_t* put_link(uint8_t* p, wrec r) {
+    /* fields in number order: peer_pod 1, local_intf 2, peer_intf 3, local_ip 4, peer_ip 5,
+       uid 6, properties 7, local_mac 8, peer_mac 9 */
+    static const int ORDER[KDTN_NKEY] = {KDTN_K_PEER_POD, KDTN_K_LOCAL_INTF, KDTN_K_PEER_INTF,
+                                         KDTN_K_LOCAL_IP, KDTN_K_PEER_IP, KDTN_K_LOCAL_MAC,
+                                         KDTN_K_PEER_MAC};
+    for (int q = 0; q < 5; q++)
+        p = put_str(p, LINK_FIELD[ORDER[q]], wget(&r.in->kdict, r.L->key[ORDER[q]][r.j]));
+    if (r.L->uid[r.j]) {
+        *p++ = 6 << 3 | 0;
+        p = put_varint(p, (uint64_t)r.L->uid[r.j]);
+    }
+    *p++ = 7 << 3 | 2;
+    p = put_varint(p, props_size(r));
+    for (int k = 0; k < KDTN_NPROP; k++) {
+        if (PROP_FIELD[k] == 8 && r.L->gap[r.j]) {           /* gap (7) precedes duplicate (8) */
+            *p++ = 7 << 3 | 0;
+            p = put_varint(p, r.L->gap[r.j]);
+        }
+        p = put_str(p, PROP_FIELD[k], wget(&r.in->pdict, r.L->prop[k][r.j]));
+    }
+    for (int q = 5; q < 7; q++)
+        p = put_str(p, LINK_FIELD[ORDER[q]], wget(&r.in->kdict, r.L->key[ORDER[q]][r.j]));
+    return p;
+}
+
+/* pb.Pod{Name 1, SrcIp 2, NetNs 3, KubeNs 4} of topology t */
+static void pod_strs(const kdtn_epoch_in* in, uint32_t t, wstr s[4]) {
+    s[0] = wget(&in->kdict, in->topos.name[t]);
+    s[1] = wget(&in->kdict, in->topos.src_ip[t]);
+    s[2] = wget(&in->kdict, in->topos.net_ns[t]);
+    s[3] = wget(&in->kdict, in->topos.ns[t]);
+}
+
+int64_t or_encode_batch(const kdtn_epoch_in* in, uint32_t t, int list, const uint32_t* idx,
+                        uint32_t n, uint8_t* out) {
+    const kdtn_link_table* L = list == 0 ? &in->realised : &in->desired;
+    wstr pod[4];
+    pod_strs(in, t, pod);
+    if (n == 0) return 0;                                     /* no RPC for an empty list */
+    for (int k = 0; k < 4; k++)
+        if (!or_utf8_valid(pod[k].p, pod[k].n)) return -1;
+    uint32_t psz = 0;
+    for (int k = 0; k < 4; k++) psz += str_size(pod[k]);
+    uint64_t total = 1 + vlen(psz) + psz;
+    for (uint32_t e = 0; e < n; e++) {
+        wrec r = {in, L, idx[e]};
+        if (!link_utf8_ok(r)) return -1;
+        uint32_t ls = link_size(r);
+        total += 1 + vlen(ls) + ls;
+    }
+    if (!out) return (int64_t)total;
+    uint8_t* p = out;
+    *p++ = 1 << 3 | 2;
+    p = put_varint(p, psz);
+    for (int k = 0; k < 4; k++) p = put_str(p, (uint32_t)k + 1, pod[k]);
+    for (uint32_t e = 0; e < n; e++) {
+        wrec r = {in, L, idx[e]};
+        *p++ = 2 << 3 | 2;
+        p = put_varint(p, link_size(r));
+        p = put_link(p, r);
+    }
+    return (int64_t)(p - out);
+}
+
+uint64_t or_encode_epoch(const kdtn_epoch_in* in, const kdtn_batches* b, uint32_t T, uint8_t* bytes,
+                         uint64_t* off, uint8_t* err) {
+    const uint32_t* lo[3] = {b->del_off, b->add_off, b->upd_off};
+    const uint32_t* li[3] = {b->del_idx, b->add_idx, b->upd_idx};
+    uint64_t pos = 0;
+    for (uint32_t t = 0; t < T; t++) err[t] = 0;
+    for (int list = 0; list < 3; list++) {
+        for (uint32_t t = 0; t < T; t++) {
+            off[(uint64_t)list * T + t] = pos;
+            const uint32_t e0 = lo[list][t], n = lo[list][t + 1] - e0;
+            int64_t sz = or_encode_batch(in, t, list, li[list] + e0, n, NULL);
+            if (sz < 0) {
+                err[t] |= (uint8_t)(1u << list);
+                continue;
+            }
+            if (bytes) or_encode_batch(in, t, list, li[list] + e0, n, bytes + pos);
+            pos += (uint64_t)sz;
+        }
+    }
+    off[3ull * T] = pos;
+    return pos;
+}

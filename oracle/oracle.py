@@ -152,3 +152,51 @@ def reconcile(inp: EpochInput, tick: float = 15.625, vxlan_base: int = 5000, pod
     if rc != 0:
         raise RuntimeError(f"oracle reconcile failed: {rc}")
     return out.trim(b.n_del, b.n_add, b.n_upd)
+
+
+def _wire_lib():
+    L = lib()
+    if not getattr(L, "_wire_bound", False):
+        L.or_utf8_valid.argtypes = [C.c_char_p, C.c_uint32]
+        L.or_encode_batch.argtypes = [C.POINTER(abi.EpochIn), C.c_uint32, C.c_int, abi.u32p, C.c_uint32,
+                                      C.c_void_p]
+        L.or_encode_batch.restype = C.c_int64
+        L.or_encode_epoch.argtypes = [C.POINTER(abi.EpochIn), C.POINTER(abi.Batches), C.c_uint32, C.c_void_p,
+                                      C.c_void_p, C.c_void_p]
+        L.or_encode_epoch.restype = C.c_uint64
+        L._wire_bound = True
+    return L
+
+
+def utf8_valid(s) -> bool:
+    b = _b(s)
+    return _wire_lib().or_utf8_valid(b, len(b)) == 1
+
+
+def encode_batch(inp: EpochInput, t: int, lst: int, idx) -> bytes | None:
+    """proto.Marshal of the LinksBatchQuery Reconcile sends for topology t's list `lst`
+    (0 DelLinks, 1 AddLinks, 2 UpdateLinks) of records `idx`; None = Marshal error."""
+    L = _wire_lib()
+    cin = inp.to_c()
+    idx = np.ascontiguousarray(idx, dtype=np.uint32)
+    ip = abi.ptr(idx if len(idx) else np.zeros(1, np.uint32), abi.u32p)
+    n = L.or_encode_batch(C.byref(cin), t, lst, ip, len(idx), None)
+    if n < 0:
+        return None
+    buf = (C.c_uint8 * max(n, 1))()
+    L.or_encode_batch(C.byref(cin), t, lst, ip, len(idx), C.cast(buf, C.c_void_p))
+    return bytes(buf)[:n]
+
+
+def encode_epoch(inp: EpochInput, out: BatchesOut):
+    """Wire bytes of every batch of an epoch: (arena uint8, off uint64[3T+1], err uint8[T])."""
+    L = _wire_lib()
+    T = inp.topos.n
+    cin = inp.to_c()
+    b = out.to_c((max(len(out.del_idx), 1), max(len(out.add_idx), 1), max(len(out.upd_idx), 1)))
+    off = np.zeros(3 * T + 1, np.uint64)
+    err = np.zeros(max(T, 1), np.uint8)
+    n = L.or_encode_epoch(C.byref(cin), C.byref(b), T, None, off.ctypes.data, err.ctypes.data)
+    arena = np.zeros(max(int(n), 1), np.uint8)
+    L.or_encode_epoch(C.byref(cin), C.byref(b), T, arena.ctypes.data, off.ctypes.data, err.ctypes.data)
+    return arena[:int(n)], off, err[:T]

@@ -198,3 +198,31 @@ def random_float_strings(rng: random.Random, n: int):
         else:
             out.append("".join(rng.choice("0123456789.eE+-_xXpPinfa") for _ in range(rng.randint(1, 8))))
     return out
+
+
+# ---- wire-encoding epochs: strings that stress proto.Marshal ---------------------------
+def wire_epoch_input(seed: int, T: int = 80):
+    """random_epoch plus strings and values that exercise the protobuf encoder: multi-byte
+    UTF-8, invalid UTF-8 (Marshal error), strings of 128+ bytes (2-byte length varints),
+    negative and large uids (10-byte varints), gaps >= 128."""
+    rng = random.Random(seed ^ 0x5A5A)
+    topos, vnis = random_epoch(seed, T=T, p_err=0.1)
+    uni = ["eth-µ", "veth–1", "日本", "x" * 130, "y" * 300, "🙂pod"]
+    bad = [b"\xff", b"ab\xc3", b"\xed\xa0\x80", b"\xc0\xaf", b"\xf4\x90\x80\x80"]
+    for t, tp in enumerate(topos):
+        if rng.random() < 0.05:
+            tp.name = tp.name + rng.choice(uni[:3])
+        for side in (tp.spec_links or [], tp.status_links or []):
+            for l in side:
+                r = rng.random()
+                if r < 0.05:
+                    l.peer_intf = rng.choice(uni)
+                elif r < 0.07:
+                    l.local_mac = rng.choice(bad)
+                elif r < 0.09:
+                    l.properties.rate = rng.choice(uni + [b"1\xffGbit"])
+                if rng.random() < 0.05:
+                    l.uid = rng.choice([-1, -5, -(2 ** 40), 2 ** 40, 2 ** 62, 127, 128, 16383, 16384])
+                if rng.random() < 0.05:
+                    l.properties.gap = rng.choice([127, 128, 300, 2 ** 31, 2 ** 32 - 1])
+    return topos, pack(topos, vnis)
