@@ -95,6 +95,25 @@ def cpu_baseline(inp, budget_s: float, threads: int):
                       f"{timing[-1]:.2f} s (host nproc={os.cpu_count()})"}
 
 
+def wire_stage(eng, reps: int = 5):
+    """Separate report (not part of `value`): the protobuf wire encoding of every batch of
+    the epoch (kdtn_epoch_encode: proto.Marshal of each LinksBatchQuery Reconcile sends).
+    GPU kernel time from HIP events, excluding the one host round trip that sizes the
+    arena; bytes = serialized output."""
+    eng.run()
+    eng.sync()
+    eng.encode()
+    acc: dict[str, float] = {}
+    n = 0
+    for _ in range(reps):
+        n = eng.encode()
+        for k, v in eng.kernel_times().items():
+            acc[k] = acc.get(k, 0.0) + v / reps
+    gpu_ms = sum(v for k, v in acc.items() if k != "wire_host_sync")
+    return {"bytes": n, "gpu_ms": gpu_ms, "out_GBps": n / (gpu_ms * 1e-3) / 1e9,
+            "kernels_ms": acc, "note": "not part of value; arena-size host round trip excluded"}
+
+
 def pmc_traffic(links_per_gpu: int):
     """HBM bytes per k_reconcile launch from the newest committed PMC summary of the same
     workload (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from separate
@@ -121,6 +140,7 @@ def main():
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--cpu-budget-s", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-wire", action="store_true", help="skip the wire-encoding stage report")
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="CPU-baseline worker threads (the GPU box's CPU share is 16)")
     args = ap.parse_args()
@@ -210,6 +230,8 @@ def main():
         "counts": {"add": counts.n_add, "upd": counts.n_upd, "del": counts.n_del},
         "gen_s": round(gen_s, 2),
     }
+    if not args.no_wire:
+        result["wire_stage"] = wire_stage(eng)
     if rank == 0 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(inp, args.cpu_budget_s, args.cpu_threads)
     if rank == 0:

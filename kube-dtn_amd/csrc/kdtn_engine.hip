@@ -556,6 +556,8 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         o.upd_qdisc = dp<uint2>(c->upd_qdisc);
         o.totals = misc + 1;
         o.stages = stages;
+        int variant = DEFAULT_VARIANT;
+        if (const char* ev = std::getenv("KDTN_VARIANT")) variant = std::atoi(ev);   // profiling A/B
         RecWork w;
         w.sync = dp<uint32_t>(c->sync);
         w.status = reinterpret_cast<unsigned long long*>(static_cast<char*>(c->sync.p) + 16);
@@ -566,8 +568,6 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         w.trace = nullptr;
         w.first_partial = misc + MISC_FIRST_PARTIAL;                // 0xFFFFFFFF from the memset
         k_full_prefix<<<nblocks(c->T), BLOCK, 0, s>>>(T, misc + MISC_FIRST_PARTIAL);
-        int variant = DEFAULT_VARIANT;
-        if (const char* ev = std::getenv("KDTN_VARIANT")) variant = std::atoi(ev);   // profiling A/B
         if (variant & VAR_TRACE) {
             TRY(ensure(c->trace, (size_t)c->nwg * TRACE_WORDS * 8));
             w.trace = reinterpret_cast<unsigned long long*>(c->trace.p);
@@ -767,6 +767,7 @@ int kdtn_epoch_encode(kdtn_ctx* c, uint64_t* n_bytes) {
     w.T = T;
     WireWork wk{dp<uint32_t>(c->w_rel), dp<uint32_t>(c->w_topo), dp<uint32_t>(c->w_size), dp<uint32_t>(c->w_err),
                 dp<uint64_t>(c->w_off)};
+    if (ne) k_wire_entry_sizes<<<nblocks(ne), BLOCK, 0, s>>>(w, c->real.view, c->des.view, wk);
     if (T) k_wire_sizes<<<nblocks((uint64_t)3 * T), BLOCK, 0, s>>>(w, c->real.view, c->des.view, wk);
     timer_mark(c, "wire_sizes");
     const uint32_t n = 3 * T;

@@ -188,6 +188,7 @@ __global__ void k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, Re
 
 // ---- wire encoding of the batches (kdtn_wire.hip) --------------------------------------
 constexpr int SCAN_CHUNK = BLOCK * 4;   // values per block of the batch-offset scan
+constexpr int WIRE_IMG = 12288;         // LDS bytes per wave for a wave's wire output
 struct WireIn {
     const uint8_t* kd_bytes;
     const uint32_t* kd_offs;
@@ -212,6 +213,7 @@ struct WireWork {
     const uint64_t* off;            // [3T+1] batch byte offsets
 };
 __global__ void k_utf8_bits(const uint8_t* bytes, const uint32_t* offs, uint32_t n, uint32_t* bits);
+__global__ void k_wire_entry_sizes(WireIn w, DevLinks O, DevLinks N, WireWork wk);
 __global__ void k_wire_sizes(WireIn w, DevLinks O, DevLinks N, WireWork wk);
 __global__ void k_scan_partial(const uint32_t* size, uint32_t n, uint64_t* part);
 __global__ void k_scan_top(uint64_t* part, uint32_t nb);

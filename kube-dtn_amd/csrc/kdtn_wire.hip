@@ -14,11 +14,13 @@
 //
 // Kernels (launch order, kdtn_epoch_encode):
 //   k_utf8_bits      unicode/utf8.ValidString per dictionary string → bitset (1 = invalid)
-//   k_wire_sizes     one thread per (list, topology): sizes of its Link messages, each
-//                    entry's offset inside the batch, batch size (0 on error)
+//   k_wire_entry_sizes  one thread per entry: encoded size of its Link (UTF-8 checked)
+//   k_wire_sizes     one thread per (list, topology): entry offsets inside the batch,
+//                    batch size (0 on error)
 //   k_scan_*         exclusive scan of the 3T batch sizes → u64 offsets
 //   k_wire_write     one thread per entry: writes its Link (and, for the batch's first
-//                    entry, the LocalPod header) — string bytes copied from the arenas
+//                    entry, the LocalPod header) into the wave's LDS image, which the wave
+//                    then stores with coalesced dword stores
 #include "kdtn_kernels.h"
 
 namespace kdtn {
@@ -114,26 +116,39 @@ KD_INLINE uint32_t pod_size(const WireIn& w, uint32_t t, bool* ok) {
     return s;
 }
 
-// One thread per (list, topology): entry offsets inside the batch and the batch size.
+// One thread per entry (all three lists): the encoded size of its Link field (tag +
+// length varint + message), or 0xFFFFFFFF if one of its strings is not valid UTF-8.
+__global__ void __launch_bounds__(BLOCK) k_wire_entry_sizes(WireIn w, DevLinks O, DevLinks N, WireWork wk) {
+    const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
+    if (g >= w.n_entries) return;
+    const uint32_t lst = g < w.list_base[1] ? 0u : (g < w.list_base[2] ? 1u : 2u);
+    const uint32_t j = w.list_idx[lst][g - w.list_base[lst]];
+    uint32_t psz, lsz;
+    const bool ok = link_sizes(w, lst == 0 ? O : N, j, &psz, &lsz);
+    wk.rel[g] = ok ? 1u + vlen(lsz) + lsz : 0xFFFFFFFFu;
+}
+
+// One thread per (list, topology): turns its entries' sizes into offsets inside the batch
+// (in place), records the entries' topology, and writes the batch size (0 on error).
 __global__ void __launch_bounds__(BLOCK) k_wire_sizes(WireIn w, DevLinks O, DevLinks N, WireWork wk) {
     const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
     if (g >= 3u * w.T) return;
     const uint32_t lst = g / w.T, t = g - lst * w.T;
     const uint32_t* off = w.list_off[lst];
-    const uint32_t* idx = w.list_idx[lst];
-    const DevLinks& L = lst == 0 ? O : N;
     const uint32_t e0 = off[t], e1 = off[t + 1];
     uint32_t size = 0;
     if (e1 > e0) {
         bool ok;
         const uint32_t ps = pod_size(w, t, &ok);
         uint64_t pos = 1u + vlen(ps) + ps;
+        uint32_t* rel = wk.rel + w.list_base[lst];
+        uint32_t* tp = wk.topo + w.list_base[lst];
         for (uint32_t e = e0; e < e1; ++e) {
-            uint32_t psz, lsz;
-            ok = link_sizes(w, L, idx[e], &psz, &lsz) && ok;
-            wk.rel[w.list_base[lst] + e] = (uint32_t)pos;
-            wk.topo[w.list_base[lst] + e] = t;
-            pos += 1u + vlen(lsz) + lsz;
+            const uint32_t sz = rel[e];
+            ok = ok && sz != 0xFFFFFFFFu;
+            rel[e] = (uint32_t)pos;
+            tp[e] = t;
+            pos += sz;
         }
         if (!ok || pos > 0xFFFFFFFFull) atomicOr(wk.err + t, 1u << lst);
         else size = (uint32_t)pos;
@@ -209,79 +224,152 @@ __global__ void __launch_bounds__(BLOCK) k_scan_final(const uint32_t* size, uint
 }
 
 // ---- writer --------------------------------------------------------------------------------
-KD_INLINE uint8_t* put_varint(uint8_t* p, uint64_t v) {
-    while (v >= 0x80u) {
-        *p++ = (uint8_t)(v | 0x80u);
-        v >>= 7;
+// Byte sink: the wave's LDS image (staged) or global memory (fallback), same code path.
+struct Sink {
+    uint8_t* p;
+    KD_INLINE void byte(uint8_t v) { *p++ = v; }
+    KD_INLINE void varint(uint64_t v) {
+        while (v >= 0x80u) {
+            *p++ = (uint8_t)(v | 0x80u);
+            v >>= 7;
+        }
+        *p++ = (uint8_t)v;
     }
-    *p++ = (uint8_t)v;
-    return p;
-}
-KD_INLINE uint8_t* put_str(uint8_t* p, uint32_t field, const uint8_t* arena, const uint32_t* offs, uint32_t id) {
-    const uint32_t b = offs[id], len = offs[id + 1] - b;
-    if (!len) return p;
-    *p++ = (uint8_t)(field << 3 | 2u);
-    p = put_varint(p, len);
-    for (uint32_t k = 0; k < len; ++k) p[k] = arena[b + k];
-    return p + len;
+    // string field: tag, length, bytes read from the arena as aligned dwords (arenas carry
+    // 64 B of slack, so reading past a string's end is safe)
+    KD_INLINE void str(uint32_t field, const uint8_t* arena, const uint32_t* offs, uint32_t id) {
+        const uint32_t b = offs[id], len = offs[id + 1] - b;
+        if (!len) return;
+        byte((uint8_t)(field << 3 | 2u));
+        varint(len);
+        const uint32_t* a32 = reinterpret_cast<const uint32_t*>(arena) + (b >> 2);
+        uint32_t sh = b & 3u, k = 0;
+        while (k < len) {
+            const uint32_t d = *a32++;
+            for (; sh < 4u && k < len; ++sh, ++k) *p++ = (uint8_t)(d >> (8u * sh));
+            sh = 0;
+        }
+    }
+};
+
+KD_INLINE uint32_t pod_header_size(const WireIn& w, uint32_t t) {
+    bool ok;
+    const uint32_t ps = pod_size(w, t, &ok);
+    return 1u + vlen(ps) + ps;
 }
 
-// One thread per entry of the three lists (global entry index g).
-__global__ void __launch_bounds__(BLOCK) k_wire_write(WireIn w, DevLinks O, DevLinks N, WireWork wk,
-                                                      uint8_t* arena) {
-    const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
-    if (g >= w.n_entries) return;
-    const uint32_t lst = g < w.list_base[1] ? 0u : (g < w.list_base[2] ? 1u : 2u);
-    const uint32_t e = g - w.list_base[lst];
-    const uint32_t t = wk.topo[g];
-    if ((wk.err[t] >> lst) & 1u) return;
-    const DevLinks& L = lst == 0 ? O : N;
-    const uint32_t j = w.list_idx[lst][e];
-    uint8_t* base = arena + wk.off[lst * w.T + t];
-    if (e == w.list_off[lst][t]) {                       // first entry: LocalPod header
+KD_INLINE void write_entry(Sink& o, const WireIn& w, const DevLinks& L, uint32_t j, bool header, uint32_t t) {
+    if (header) {                                         // LinksBatchQuery.local_pod
         bool ok;
-        const uint32_t ps = pod_size(w, t, &ok);
-        uint8_t* p = base;
-        *p++ = 1u << 3 | 2u;
-        p = put_varint(p, ps);
-        p = put_str(p, 1, w.kd_bytes, w.kd_offs, w.t_name[t]);
-        p = put_str(p, 2, w.kd_bytes, w.kd_offs, w.t_src[t]);
-        p = put_str(p, 3, w.kd_bytes, w.kd_offs, w.t_netns[t]);
-        p = put_str(p, 4, w.kd_bytes, w.kd_offs, w.t_ns[t]);
+        o.byte(1u << 3 | 2u);
+        o.varint(pod_size(w, t, &ok));
+        o.str(1, w.kd_bytes, w.kd_offs, w.t_name[t]);
+        o.str(2, w.kd_bytes, w.kd_offs, w.t_src[t]);
+        o.str(3, w.kd_bytes, w.kd_offs, w.t_netns[t]);
+        o.str(4, w.kd_bytes, w.kd_offs, w.t_ns[t]);
     }
     uint32_t psz, lsz;
     link_sizes(w, L, j, &psz, &lsz);
-    uint8_t* p = base + wk.rel[g];
-    *p++ = 2u << 3 | 2u;
-    p = put_varint(p, lsz);
+    o.byte(2u << 3 | 2u);                                 // LinksBatchQuery.links
+    o.varint(lsz);
     // pb.Link fields in number order: peer_pod 1, local_intf 2, peer_intf 3, local_ip 4,
     // peer_ip 5, uid 6, properties 7, local_mac 8, peer_mac 9
-    p = put_str(p, 1, w.kd_bytes, w.kd_offs, L.key(KDTN_K_PEER_POD, j));
-    p = put_str(p, 2, w.kd_bytes, w.kd_offs, L.key(KDTN_K_LOCAL_INTF, j));
-    p = put_str(p, 3, w.kd_bytes, w.kd_offs, L.key(KDTN_K_PEER_INTF, j));
-    p = put_str(p, 4, w.kd_bytes, w.kd_offs, L.key(KDTN_K_LOCAL_IP, j));
-    p = put_str(p, 5, w.kd_bytes, w.kd_offs, L.key(KDTN_K_PEER_IP, j));
+    o.str(1, w.kd_bytes, w.kd_offs, L.key(KDTN_K_PEER_POD, j));
+    o.str(2, w.kd_bytes, w.kd_offs, L.key(KDTN_K_LOCAL_INTF, j));
+    o.str(3, w.kd_bytes, w.kd_offs, L.key(KDTN_K_PEER_INTF, j));
+    o.str(4, w.kd_bytes, w.kd_offs, L.key(KDTN_K_LOCAL_IP, j));
+    o.str(5, w.kd_bytes, w.kd_offs, L.key(KDTN_K_PEER_IP, j));
     const int64_t uid = L.uid(j);
     if (uid) {
-        *p++ = 6u << 3;
-        p = put_varint(p, (uint64_t)uid);
+        o.byte(6u << 3);
+        o.varint((uint64_t)uid);
     }
-    *p++ = 7u << 3 | 2u;
-    p = put_varint(p, psz);
+    o.byte(7u << 3 | 2u);
+    o.varint(psz);
     // pb.LinkProperties: latency 1 .. rate 6, gap 7, duplicate 8 .. corrupt_corr 13 (KDTN_P_* order)
-#pragma unroll
     for (int k = 0; k < KDTN_NPROP; ++k) {
         if (k == KDTN_P_DUPLICATE) {
             const uint32_t gap = L.gap(j);
             if (gap) {
-                *p++ = 7u << 3;
-                p = put_varint(p, gap);
+                o.byte(7u << 3);
+                o.varint(gap);
             }
         }
-        p = put_str(p, (uint32_t)(k < KDTN_P_DUPLICATE ? k + 1 : k + 2), w.pd_bytes, w.pd_offs, L.prop(k, j));
+        o.str((uint32_t)(k < KDTN_P_DUPLICATE ? k + 1 : k + 2), w.pd_bytes, w.pd_offs, L.prop(k, j));
     }
-    p = put_str(p, 8, w.kd_bytes, w.kd_offs, L.key(KDTN_K_LOCAL_MAC, j));
-    p = put_str(p, 9, w.kd_bytes, w.kd_offs, L.key(KDTN_K_PEER_MAC, j));
+    o.str(8, w.kd_bytes, w.kd_offs, L.key(KDTN_K_LOCAL_MAC, j));
+    o.str(9, w.kd_bytes, w.kd_offs, L.key(KDTN_K_PEER_MAC, j));
+}
+
+// One thread per entry of the three lists (global entry index g). Consecutive entries
+// write consecutive arena bytes (empty and failed batches occupy none), so a wave's
+// output is one contiguous range: the lanes assemble it in the wave's LDS image with byte
+// writes, then the wave stores it with coalesced dword stores (byte stores only at the
+// two partial dwords shared with the neighbouring waves). A range larger than the image
+// is written straight to global memory.
+__global__ void __launch_bounds__(BLOCK) k_wire_write(WireIn w, DevLinks O, DevLinks N, WireWork wk,
+                                                      uint8_t* arena) {
+    __shared__ uint32_t img[BLOCK / 64][WIRE_IMG / 4];
+    const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    bool on = g < w.n_entries;
+    uint32_t lst = 0, t = 0, j = 0;
+    bool header = false;
+    uint64_t s0 = 0, s1 = 0;
+    if (on) {
+        lst = g < w.list_base[1] ? 0u : (g < w.list_base[2] ? 1u : 2u);
+        const uint32_t e = g - w.list_base[lst];
+        t = wk.topo[g];
+        on = ((wk.err[t] >> lst) & 1u) == 0;
+        if (on) {
+            j = w.list_idx[lst][e];
+            const uint64_t bo = wk.off[lst * w.T + t];
+            const uint32_t rel = wk.rel[g];
+            header = e == w.list_off[lst][t];
+            s0 = bo + (header ? 0u : rel);
+            const uint32_t nxt = e + 1 < w.list_off[lst][t + 1] ? wk.rel[g + 1] : (uint32_t)(wk.off[lst * w.T + t + 1] - bo);
+            s1 = bo + nxt;
+        }
+    }
+    // wave range
+    uint64_t r0 = on ? s0 : ~0ull, r1 = on ? s1 : 0ull;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint64_t a = __shfl_xor(r0, d, 64), b = __shfl_xor(r1, d, 64);
+        r0 = a < r0 ? a : r0;
+        r1 = b > r1 ? b : r1;
+    }
+    if (r1 <= r0) return;                                 // no active lane (wave-uniform)
+    const DevLinks& L = lst == 0 ? O : N;
+    const uint32_t lead = (uint32_t)(r0 & 3u);
+    if (r1 - r0 + lead > (uint64_t)WIRE_IMG) {            // too large: direct byte stores
+        if (on) {
+            Sink o{arena + s0};
+            write_entry(o, w, L, j, header, t);
+        }
+        return;
+    }
+    uint8_t* im = reinterpret_cast<uint8_t*>(img[threadIdx.x >> 6]);
+    if (on) {
+        Sink o{im + lead + (uint32_t)(s0 - r0)};
+        write_entry(o, w, L, j, header, t);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint64_t a0 = r0 - lead;                        // dword-aligned global start
+    const uint32_t nw = (uint32_t)((r1 - a0 + 3) >> 2);
+    const uint32_t* iw = img[threadIdx.x >> 6];
+    for (uint32_t q = lane; q < nw; q += 64) {
+        const uint64_t ga = a0 + 4ull * q;
+        const uint32_t v = iw[q];
+        if (ga >= r0 && ga + 4 <= r1) {
+            *reinterpret_cast<uint32_t*>(arena + ga) = v;
+        } else {
+            for (uint32_t k = 0; k < 4; ++k)
+                if (ga + k >= r0 && ga + k < r1) arena[ga + k] = (uint8_t)(v >> (8 * k));
+        }
+    }
 }
 
 }  // namespace kdtn

@@ -35,7 +35,8 @@ if a.variants:
             eng.run(abi.STAGE_ALL)
             eng.sync()
             if rep >= 2:
-                acc[v].append(eng.kernel_times()["reconcile"])
+                kt = eng.kernel_times()
+                acc[v].append(kt["reconcile"] + kt.get("qdisc", 0.0))   # split-qdisc variants
     os.environ.pop("KDTN_VARIANT")
     for v in vs:
         x = sorted(acc[v])
