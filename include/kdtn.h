@@ -19,6 +19,10 @@
  *     - GetVniFromUid        common/utils.go:29-31
  *     - VxlanManager.Get     daemon/vxlan/manager.go:65-71
  *   kdtn_make_qdiscs      replaces common.MakeQdiscs (common/qdisc.go:20) for a batch
+ *   kdtn_diff             replaces CalcDiff + the Reconcile gate alone
+ *   kdtn_resolve          replaces the pure prefix of the daemon's AddLinks / DelLinks for
+ *                         one LinksBatchQuery (handler.go:592-632)
+ *   kdtn_epoch_encode     replaces Link.ToProto + proto.Marshal of the batches
  *
  * Conventions
  *   - No C++ or HIP types cross this ABI: plain pointers, sizes and PODs.
@@ -273,6 +277,38 @@ int kdtn_epoch_upload(kdtn_ctx* ctx, const kdtn_epoch_in* in);
 int kdtn_epoch_run(kdtn_ctx* ctx, uint32_t stages);          /* async on the ctx stream   */
 int kdtn_epoch_sync(kdtn_ctx* ctx, kdtn_counts* counts);     /* waits; counts may be NULL */
 int kdtn_epoch_download(kdtn_ctx* ctx, kdtn_batches* out);   /* after sync                */
+
+/* Gate + CalcDiff only (KDTN_STAGE_DIFF): the Del/Add/Update index lists per Topology,
+ * without resolve or qdisc records (out->*_res / *_qdisc are not written). Replaces
+ * CalcDiff (controllers/topology_controller.go:288-318) and the gate (:77-88). */
+int kdtn_diff(kdtn_ctx* ctx, const kdtn_epoch_in* in, kdtn_batches* out);
+
+/* ---- daemon side: one LinksBatchQuery (daemon/kubedtn/handler.go:592-632) --------- */
+/* The informer's pods as the daemon sees them (getPod, handler.go:27-41; ToProtoPod
+ * :62-88): namespace, name, status src_ip / net_ns, KDTN_TOPO_SPEC_NIL when the pod's
+ * spec.links is nil (ToProtoPod's error). */
+typedef struct kdtn_pod_table {
+    uint32_t        n;
+    const uint32_t* ns;
+    const uint32_t* name;
+    const uint32_t* src_ip;
+    const uint32_t* net_ns;
+    const uint8_t*  flags;
+} kdtn_pod_table;
+#define KDTN_BATCH_ADD 0   /* AddLinks: addLink per link (handler.go:592-611, 316-459)   */
+#define KDTN_BATCH_DEL 1   /* DelLinks: delLink per link (handler.go:613-632, 461-492)   */
+/* Pure prefix of the daemon batch handler for the links of LocalPod = pods[local]:
+ * out[i] is link i's plan (kind, peer, VNI, VXLAN map check, first failing step) and,
+ * for AddLinks, qout[i] its MakeQdiscs result (qout may be NULL; ignored for DelLinks).
+ * The handler aborts at the first link whose err != 0 (kdtn_resolved.err or qout.err).
+ * A link whose peer is the local pod itself sees the local pod's spec as non-nil. */
+int kdtn_resolve(kdtn_ctx* ctx, const kdtn_strtab* kdict, const kdtn_strtab* pdict,
+                 const kdtn_pod_table* pods, uint32_t local, const kdtn_link_table* links,
+                 int batch_kind, const kdtn_vni_table* vnis, kdtn_resolved* out, kdtn_qdisc* qout);
+
+/* Pinned host memory for inputs/outputs (optional: faster H2D/D2H than pageable). */
+void* kdtn_host_alloc(uint64_t bytes);
+void  kdtn_host_free(void* p);
 
 /* ---- standalone MakeQdiscs over a batch of property sets (UpdateLinks path) -------- */
 int kdtn_make_qdiscs(kdtn_ctx* ctx, const kdtn_strtab* pdict, const kdtn_props_table* props,

@@ -486,8 +486,16 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
 
     const DevTopos T = topo_view(c);
     // dictionaries
-    if (c->D) k_kdict_flags<<<nblocks(c->D), BLOCK, 0, s>>>(dp<uint8_t>(c->kd_bytes), dp<uint32_t>(c->kd_offs),
-                                                         c->D, dp<uint32_t>(c->kd_bits), c->kb_words, misc);
+    if (c->D) {
+        int sub = 1;                                                   // strings per thread (2, 4: slower)
+        if (const char* ev = std::getenv("KDTN_KD_SUB")) sub = std::atoi(ev);   // profiling A/B
+        const uint8_t* kb = dp<uint8_t>(c->kd_bytes);
+        const uint32_t* ko = dp<uint32_t>(c->kd_offs);
+        uint32_t* bits = dp<uint32_t>(c->kd_bits);
+        if (sub == 4) k_kdict_flags<4><<<nblocks(c->D, BLOCK * 4), BLOCK, 0, s>>>(kb, ko, c->D, bits, c->kb_words, misc);
+        else if (sub == 1) k_kdict_flags<1><<<nblocks(c->D), BLOCK, 0, s>>>(kb, ko, c->D, bits, c->kb_words, misc);
+        else k_kdict_flags<2><<<nblocks(c->D, BLOCK * 2), BLOCK, 0, s>>>(kb, ko, c->D, bits, c->kb_words, misc);
+    }
     timer_mark(c, "kdict_parse");
     if (c->P) k_pdict_parse<<<nblocks(c->P), BLOCK, 0, s>>>(dp<uint8_t>(c->pd_bytes), dp<uint32_t>(c->pd_offs),
                                                          c->P, c->cfg.tick_in_usec, dp<uint32_t>(c->pd_pct),
@@ -671,6 +679,72 @@ int kdtn_reconcile_epoch(kdtn_ctx* c, const kdtn_epoch_in* in, kdtn_batches* out
     TRY(kdtn_epoch_run(c, KDTN_STAGE_ALL));
     TRY(kdtn_epoch_sync(c, nullptr));
     return kdtn_epoch_download(c, out);
+}
+
+int kdtn_diff(kdtn_ctx* c, const kdtn_epoch_in* in, kdtn_batches* out) {
+    TRY(kdtn_epoch_upload(c, in));
+    TRY(kdtn_epoch_run(c, KDTN_STAGE_DIFF));
+    TRY(kdtn_epoch_sync(c, nullptr));
+    return kdtn_epoch_download(c, out);
+}
+
+// One daemon batch as a one-topology epoch: the pods become the topology table (so peer
+// lookups see the informer's pods), the batch's links are the local pod's desired list
+// (AddLinks: realised non-nil and empty, so every link is an add in query order) or its
+// realised list (DelLinks: spec nil, so every link is a delete in query order).
+int kdtn_resolve(kdtn_ctx* c, const kdtn_strtab* kdict, const kdtn_strtab* pdict, const kdtn_pod_table* pods,
+                 uint32_t local, const kdtn_link_table* links, int batch_kind, const kdtn_vni_table* vnis,
+                 kdtn_resolved* out, kdtn_qdisc* qout) {
+    if (!c || !kdict || !pdict || !pods || !links || (links->n && !out)) return KDTN_EINVAL;
+    if (local >= pods->n || (batch_kind != KDTN_BATCH_ADD && batch_kind != KDTN_BATCH_DEL)) return KDTN_EINVAL;
+    if (!pods->ns || !pods->name || !pods->src_ip || !pods->net_ns || !pods->flags) return KDTN_EINVAL;
+    const uint32_t P = pods->n, n = links->n;
+    const bool add = batch_kind == KDTN_BATCH_ADD;
+    std::vector<uint8_t> flags(pods->flags, pods->flags + P);
+    std::vector<uint32_t> roff(P + 1, 0), noff(P + 1, 0);
+    for (uint32_t t = 0; t < P; ++t) {
+        if (t != local) flags[t] |= KDTN_TOPO_STATUS_NIL;             // no entries of their own
+        else flags[t] = add ? 0u : (uint8_t)KDTN_TOPO_SPEC_NIL;
+        roff[t + 1] = roff[t] + (!add && t == local ? n : 0);
+        noff[t + 1] = noff[t] + (add && t == local ? n : 0);
+    }
+    kdtn_epoch_in in{};
+    in.kdict = *kdict;
+    in.pdict = *pdict;
+    in.topos = kdtn_topo_table{P, pods->ns, pods->name, pods->src_ip, pods->net_ns, flags.data(), roff.data(),
+                               noff.data()};
+    kdtn_link_table empty{};
+    in.realised = add ? empty : *links;
+    in.desired = add ? *links : empty;
+    if (vnis) in.vnis = *vnis;
+    TRY(kdtn_epoch_upload(c, &in));
+    TRY(kdtn_epoch_run(c, add ? KDTN_STAGE_ALL : (KDTN_STAGE_DIFF | KDTN_STAGE_RESOLVE)));
+    kdtn_counts cnt{};
+    TRY(kdtn_epoch_sync(c, &cnt));
+    if ((add ? cnt.n_add : cnt.n_del) != n) {
+        std::snprintf(g_last_error, sizeof(g_last_error), "kdtn_resolve: %u of %u links planned",
+                      add ? cnt.n_add : cnt.n_del, n);
+        return KDTN_EIO;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    if (n) {
+        HIP_TRY(hipMemcpyAsync(out, add ? c->add_res.p : c->del_res.p, (size_t)n * 16, hipMemcpyDeviceToHost,
+                               c->stream));
+        if (add && qout)
+            HIP_TRY(hipMemcpyAsync(qout, c->add_qdisc.p, (size_t)n * 72, hipMemcpyDeviceToHost, c->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return KDTN_OK;
+}
+
+void* kdtn_host_alloc(uint64_t bytes) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+    return p;
+}
+
+void kdtn_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
 }
 
 int kdtn_make_qdiscs(kdtn_ctx* c, const kdtn_strtab* pdict, const kdtn_props_table* props,

@@ -171,6 +171,7 @@ struct RecWork {
     uint32_t nwg;
 };
 
+template <int SUB>
 __global__ void k_kdict_flags(const uint8_t* bytes, const uint32_t* offs, uint32_t n,
                               uint32_t* kbits, uint32_t kb_words, uint32_t* special);
 __global__ void k_pdict_parse(const uint8_t* bytes, const uint32_t* offs, uint32_t n, double tick,

@@ -179,48 +179,75 @@ KD_INLINE bool cidr_swar(const uint32_t* w, uint32_t len, bool* slow) {
 // Strings longer than 24 bytes, with ':' (IPv6), long prefixes or shaped like a MAC take
 // the generic parsers (kdtn_parse.h) on global memory. Each wave packs its 64
 // predicate bits per set with a ballot (two u32 words per set, lanes 0 and 32).
+// Predicate bits of one key string from its register image (first 24 bytes in w[]).
+KD_INLINE uint32_t kdict_bits(const uint8_t* bytes, uint32_t b, uint32_t len, const uint32_t* w, uint32_t i,
+                              uint32_t* special) {
+    uint32_t f = 0;
+    if (len) {
+        bool slow = true, cok = false;
+        if (len <= 24) cok = cidr_swar(w, len, &slow);
+        if (slow) cok = cidr_ok(bytes + b, len);                       // common/veth.go:22
+        if (!cok) f |= 1u << KB_CIDR_BAD;
+        const uint32_t c2 = wbyte(w, 2), c4 = wbyte(w, 4);
+        bool mok = false;                                              // common/veth.go:33
+        if (len >= 14 && (c2 == ':' || c2 == '-' || c4 == '.')) mok = mac_ok(bytes + b, len);
+        if (!mok) f |= 1u << KB_MAC_BAD;
+    }
+    const uint32_t w2b = w[2] & 0xFFu;
+    if (len >= 9 && w[0] == 0x73796870u && w[1] == 0x6C616369u && w2b == '/')   // "phys" "ical" '/'
+        f |= 1u << KB_PHYSICAL;                                        // handler.go:348
+    if (len == 9 && w[0] == 0x61636F6Cu && w[1] == 0x736F686Cu && w2b == 't')   // "loca" "lhos" 't'
+        atomicMin(special + SPECIAL_LOCALHOST, i);                     // handler.go:333
+    if (len == 7 && w[0] == 0x61666564u && (w[1] & 0xFFFFFFu) == 0x746C75u)     // "defa" "ult"
+        atomicMin(special + SPECIAL_DEFAULT, i);                       // getPod ns "" (handler.go:29-31)
+    return f;
+}
+
+// SUB strings per thread (block covers SUB*BLOCK consecutive strings): every offset load
+// of the thread's strings is issued, then every string's 7 dwords, then the parses run —
+// the kernel is latency-bound, so a wave keeps SUB strings' round trips in flight at once.
+template <int SUB>
 __global__ void __launch_bounds__(BLOCK) k_kdict_flags(const uint8_t* bytes, const uint32_t* offs,
                                                        uint32_t n, uint32_t* kbits, uint32_t kb_words,
                                                        uint32_t* special) {
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    uint32_t f = 0;
-    if (i < n) {
-        const uint32_t b = offs[i], len = offs[i + 1] - b;
-        const uint32_t a = b & ~3u, sh = (b & 3u) * 8u;
-        const uint32_t* p = reinterpret_cast<const uint32_t*>(bytes + a);   // arena has 64 B slack
-        uint32_t d[7], w[6];
+    const uint32_t i0 = blockIdx.x * BLOCK * SUB + threadIdx.x;
+    uint32_t b[SUB], len[SUB];
 #pragma unroll
-        for (int k = 0; k < 7; ++k) d[k] = p[k];
+    for (int s = 0; s < SUB; ++s) {
+        const uint32_t i = i0 + s * BLOCK;
+        const uint32_t ic = i < n ? i : n;                 // offs[n] exists
+        b[s] = offs[ic];
+        len[s] = (i < n ? offs[ic + 1] : b[s]) - b[s];
+    }
+    uint32_t d[SUB][7];
 #pragma unroll
-        for (int k = 0; k < 6; ++k)
-            w[k] = sh ? (d[k] >> sh) | (d[k + 1] << (32u - sh)) : d[k];
-        if (len) {
-            bool slow = true, cok = false;
-            if (len <= 24) cok = cidr_swar(w, len, &slow);
-            if (slow) cok = cidr_ok(bytes + b, len);                       // common/veth.go:22
-            if (!cok) f |= 1u << KB_CIDR_BAD;
-            const uint32_t c2 = wbyte(w, 2), c4 = wbyte(w, 4);
-            bool mok = false;                                              // common/veth.go:33
-            if (len >= 14 && (c2 == ':' || c2 == '-' || c4 == '.')) mok = mac_ok(bytes + b, len);
-            if (!mok) f |= 1u << KB_MAC_BAD;
-        }
-        const uint32_t w2b = w[2] & 0xFFu;
-        if (len >= 9 && w[0] == 0x73796870u && w[1] == 0x6C616369u && w2b == '/')   // "phys" "ical" '/'
-            f |= 1u << KB_PHYSICAL;                                        // handler.go:348
-        if (len == 9 && w[0] == 0x61636F6Cu && w[1] == 0x736F686Cu && w2b == 't')   // "loca" "lhos" 't'
-            atomicMin(special + SPECIAL_LOCALHOST, i);                     // handler.go:333
-        if (len == 7 && w[0] == 0x61666564u && (w[1] & 0xFFFFFFu) == 0x746C75u)     // "defa" "ult"
-            atomicMin(special + SPECIAL_DEFAULT, i);                       // getPod ns "" (handler.go:29-31)
+    for (int s = 0; s < SUB; ++s) {
+        const uint32_t* p = reinterpret_cast<const uint32_t*>(bytes + (b[s] & ~3u));   // arena has 64 B slack
+#pragma unroll
+        for (int k = 0; k < 7; ++k) d[s][k] = p[k];
     }
     const int lane = threadIdx.x & 63;
-    const uint32_t w0 = (i - lane) >> 5;                       // first word of this wave
 #pragma unroll
-    for (int k = 0; k < KB_NSETS; ++k) {
-        const uint64_t m = __ballot((f >> k) & 1u);
-        if (w0 < kb_words && (lane == 0 || lane == 32))
-            kbits[(size_t)k * kb_words + w0 + (lane >> 5)] = lane ? (uint32_t)(m >> 32) : (uint32_t)m;
+    for (int s = 0; s < SUB; ++s) {
+        const uint32_t i = i0 + s * BLOCK;
+        const uint32_t sh = (b[s] & 3u) * 8u;
+        uint32_t w[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+            w[k] = sh ? (d[s][k] >> sh) | (d[s][k + 1] << (32u - sh)) : d[s][k];
+        const uint32_t f = i < n ? kdict_bits(bytes, b[s], len[s], w, i, special) : 0u;
+        const uint32_t w0 = (i - lane) >> 5;                   // first word of this wave
+#pragma unroll
+        for (int k = 0; k < KB_NSETS; ++k) {
+            const uint64_t m = __ballot((f >> k) & 1u);
+            if (w0 < kb_words && (lane == 0 || lane == 32))
+                kbits[(size_t)k * kb_words + w0 + (lane >> 5)] = lane ? (uint32_t)(m >> 32) : (uint32_t)m;
+        }
     }
 }
+template __global__ void k_kdict_flags<1>(const uint8_t*, const uint32_t*, uint32_t, uint32_t*, uint32_t, uint32_t*);
+template __global__ void k_kdict_flags<2>(const uint8_t*, const uint32_t*, uint32_t, uint32_t*, uint32_t, uint32_t*);
+template __global__ void k_kdict_flags<4>(const uint8_t*, const uint32_t*, uint32_t, uint32_t*, uint32_t, uint32_t*);
 
 KD_INLINE void pdict_parse_one(const uint8_t* s, uint32_t len, double tick, uint32_t* pct_out,
                                uint2* dur_out, uint2* rate_out, bool* rate_bad) {

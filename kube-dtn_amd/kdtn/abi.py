@@ -109,6 +109,14 @@ class Wire(C.Structure):
                 ("n_bytes", C.c_uint64)]
 
 
+class PodTable(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("ns", u32p), ("name", u32p), ("src_ip", u32p), ("net_ns", u32p),
+                ("flags", u8p)]
+
+
+BATCH_ADD, BATCH_DEL = 0, 1
+
+
 class Config(C.Structure):
     _fields_ = [("device", C.c_int32), ("vxlan_base", C.c_int32), ("tick_in_usec", C.c_double)]
 
@@ -131,7 +139,8 @@ EXPORTS = ["kdtn_version", "kdtn_strerror", "kdtn_err_name", "kdtn_init", "kdtn_
            "kdtn_reconcile_epoch", "kdtn_epoch_upload", "kdtn_epoch_run", "kdtn_epoch_sync",
            "kdtn_epoch_download", "kdtn_make_qdiscs", "kdtn_comm_unique_id", "kdtn_comm_init",
            "kdtn_last_kernel_times", "kdtn_debug_wg_trace", "kdtn_epoch_encode",
-           "kdtn_epoch_download_wire"]
+           "kdtn_epoch_download_wire", "kdtn_diff", "kdtn_resolve", "kdtn_host_alloc",
+           "kdtn_host_free"]
 
 
 def ptr(a: np.ndarray, t):

@@ -65,6 +65,12 @@ def lib() -> C.CDLL:
         "kdtn_last_kernel_times": (C.c_int, [vp, C.POINTER(C.c_char_p), C.POINTER(C.c_float), C.c_int]),
         "kdtn_debug_wg_trace": (C.c_int, [vp, C.POINTER(C.c_uint64), C.c_uint32]),
         "kdtn_epoch_encode": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
+        "kdtn_diff": (C.c_int, [vp, C.POINTER(abi.EpochIn), C.POINTER(abi.Batches)]),
+        "kdtn_resolve": (C.c_int, [vp, C.POINTER(abi.Strtab), C.POINTER(abi.Strtab), C.POINTER(abi.PodTable),
+                                   C.c_uint32, C.POINTER(abi.LinkTable), C.c_int, C.POINTER(abi.VniTable),
+                                   vp, vp]),
+        "kdtn_host_alloc": (vp, [C.c_uint64]),
+        "kdtn_host_free": (None, [vp]),
         "kdtn_epoch_download_wire": (C.c_int, [vp, C.POINTER(abi.Wire)]),
     }
     for name, (res, args) in sig.items():
@@ -155,6 +161,38 @@ class Engine:
         self.run(stages)
         self.sync()
         return self.download()
+
+    def diff(self, inp: EpochInput) -> BatchesOut:
+        """Gate + CalcDiff only (kdtn_diff): index lists, no resolve / qdisc records."""
+        cin = inp.to_c()
+        out = BatchesOut.alloc(inp.topos.n, inp.realised.n, inp.desired.n, inp.realised.n)
+        b = out.to_c((max(inp.realised.n, 1), max(inp.desired.n, 1), max(inp.realised.n, 1)))
+        _check(lib().kdtn_diff(self._ctx, C.byref(cin), C.byref(b)), "kdtn_diff")
+        self._T = inp.topos.n
+        self._caps = (inp.realised.n, inp.desired.n, inp.realised.n)
+        return out.trim(b.n_del, b.n_add, b.n_upd)
+
+    # ---- daemon side: one LinksBatchQuery ------------------------------------------------
+    def resolve(self, kdict: StrTab, pdict: StrTab, pods: Topos, local: int, links, kind: int,
+                vnis=None):
+        """Pure prefix of AddLinks (kind=BATCH_ADD) / DelLinks (BATCH_DEL) for the links of
+        pods[local] (kdtn_resolve): (resolved records, qdisc records or None)."""
+        pt = abi.PodTable(pods.n, abi.ptr(np.ascontiguousarray(pods.ns, np.uint32), abi.u32p),
+                          abi.ptr(np.ascontiguousarray(pods.name, np.uint32), abi.u32p),
+                          abi.ptr(np.ascontiguousarray(pods.src_ip, np.uint32), abi.u32p),
+                          abi.ptr(np.ascontiguousarray(pods.net_ns, np.uint32), abi.u32p),
+                          abi.ptr(np.ascontiguousarray(pods.flags, np.uint8), abi.u8p))
+        lt = links.to_c()
+        n = links.n
+        res = np.zeros(max(n, 1), abi.RESOLVED_DTYPE)
+        q = np.zeros(max(n, 1), abi.QDISC_DTYPE) if kind == abi.BATCH_ADD else None
+        kd, pd = kdict.to_c(), pdict.to_c()
+        vt = vnis.to_c() if vnis is not None else abi.VniTable(0, None, None, None)
+        _check(lib().kdtn_resolve(self._ctx, C.byref(kd), C.byref(pd), C.byref(pt), local, C.byref(lt), kind,
+                                  C.byref(vt), res.ctypes.data, q.ctypes.data if q is not None else None),
+               "kdtn_resolve")
+        self._T = 0          # the context's epoch state now belongs to this call
+        return res[:n], (q[:n] if q is not None else None)
 
     # ---- wire encoding of the batches (proto/v1 LinksBatchQuery) ------------------------
     def encode(self) -> int:

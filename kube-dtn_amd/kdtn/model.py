@@ -195,6 +195,91 @@ def unpack(topos: list[Topology], out: BatchesOut) -> list[TopologyBatches]:
     return res
 
 
+@dataclass
+class BatchResult:
+    """What a daemon batch handler would return, and the per-link plans behind it:
+    `response` False with `first_failed` = the link whose step failed first (the handler
+    returns there: handler.go:604-605, 625-626, 650-662), `err` its kdtn_err."""
+    response: bool
+    first_failed: int
+    err: int
+    plans: np.ndarray            # kdtn_resolved per link
+    qdiscs: np.ndarray | None    # kdtn_qdisc per link (AddLinks / UpdateLinks)
+
+
+class KubeDTN:
+    """Daemon-side counterpart of daemon/kubedtn/handler.go's batch handlers (the pure
+    prefix before the first syscall), for one node: the informer's pods plus the node's
+    VxlanManager entries."""
+
+    def __init__(self, engine: Engine, pods: list[Topology], vxlan: list[tuple[str, int, str]] = ()):
+        self.engine = engine
+        self.kd, self.pd = Interner(), Interner()
+        self.pods = pods
+        self._index = {(p.namespace, p.name): i for i, p in reversed(list(enumerate(pods)))}
+        self._vxlan = list(vxlan)
+
+    def _tables(self):
+        kd = self.kd
+        P = len(self.pods)
+        t = Topos(np.array([kd(p.namespace) for p in self.pods], np.uint32),
+                  np.array([kd(p.name) for p in self.pods], np.uint32),
+                  np.array([kd(p.src_ip) for p in self.pods], np.uint32),
+                  np.array([kd(p.net_ns) for p in self.pods], np.uint32),
+                  np.array([abi.TOPO_SPEC_NIL if p.spec_links is None else 0 for p in self.pods], np.uint8),
+                  np.zeros(P + 1, np.uint32), np.zeros(P + 1, np.uint32))
+        v = Vnis(np.array([kd(n) for n, _, _ in self._vxlan], np.uint32),
+                 np.array([x for _, x, _ in self._vxlan], np.int32),
+                 np.array([kd(s) for _, _, s in self._vxlan], np.uint32))
+        return t, v
+
+    def _links(self, links: list[Link]) -> Links:
+        L = Links.empty(len(links))
+        for i, l in enumerate(links):
+            for k, col in enumerate(abi.KEY_COLS):
+                L.key[k, i] = self.kd(getattr(l, col))
+            L.uid[i] = l.uid
+            for k, col in enumerate(PROP_FIELDS):
+                L.prop[k, i] = self.pd(getattr(l.properties, col))
+            L.gap[i] = l.properties.gap
+        return L
+
+    def _batch(self, local_pod: str, kube_ns: str, links: list[Link], kind: int):
+        local = self._index[(kube_ns or "default", local_pod)]
+        L = self._links(links)
+        t, v = self._tables()
+        return self.engine.resolve(self.kd.table(), self.pd.table(), t, local, L, kind, v)
+
+    @staticmethod
+    def _outcome(plans, errs, qd):
+        bad = np.nonzero(errs)[0]
+        if len(bad) == 0:
+            return BatchResult(True, -1, 0, plans, qd)
+        return BatchResult(False, int(bad[0]), int(errs[bad[0]]), plans, qd)
+
+    def add_links(self, local_pod: str, kube_ns: str, links: list[Link]) -> BatchResult:
+        """AddLinks (handler.go:592-611): addLink per link, first error aborts."""
+        res, q = self._batch(local_pod, kube_ns, links, abi.BATCH_ADD)
+        # addLink's qdisc step runs inside SetupVeth / SetupVxLan (same-node, cross-node,
+        # physical), i.e. after a successful classification
+        qerr = np.where(np.isin(res["kind"], [abi.KIND_SAME_NODE, abi.KIND_CROSS_NODE, abi.KIND_PHYSICAL]),
+                        q["err"], 0)
+        errs = np.where(res["err"] != 0, res["err"], qerr)
+        return self._outcome(res, errs, q)
+
+    def del_links(self, local_pod: str, kube_ns: str, links: list[Link]) -> BatchResult:
+        """DelLinks (handler.go:613-632): delLink per link, first error aborts."""
+        res, _ = self._batch(local_pod, kube_ns, links, abi.BATCH_DEL)
+        return self._outcome(res, res["err"], None)
+
+    def update_links(self, local_pod: str, kube_ns: str, links: list[Link]) -> BatchResult:
+        """UpdateLinks (handler.go:634-671): MakeVeth(local) then MakeQdiscs per link."""
+        res, q = self._batch(local_pod, kube_ns, links, abi.BATCH_ADD)
+        veth = np.isin(res["err"], [abi.E_VETH_CIDR, abi.E_VETH_MAC])
+        errs = np.where(veth, res["err"], q["err"])
+        return self._outcome(res, errs, q)
+
+
 def make_qdiscs(engine: Engine, props: list[LinkProperties]) -> np.ndarray:
     """common.MakeQdiscs for a batch of LinkProperties (common/qdisc.go:20-126)."""
     pd = Interner()

@@ -293,3 +293,73 @@ def test_wire_encoding_golden_and_synthetic(engine, golden):
     for cfg, pods in ((1, 0), (2, 20000), (3, 20000), (4, 5000)):
         inp = synth.make(cfg, pods_per_shard=pods) if pods else synth.make(cfg)
         _wire_same(engine, inp, f"config {cfg}")
+
+
+def test_diff_only_entry_point(engine):
+    """kdtn_diff (gate + CalcDiff, no resolve/qdisc) gives the oracle's actions and lists."""
+    topos, inp = random_epoch_input(21, T=150)
+    got, want = engine.diff(inp), O.reconcile(inp, tick=TICK)
+    for f in ("action", "del_off", "add_off", "upd_off", "del_idx", "add_idx", "upd_idx"):
+        assert getattr(got, f).tobytes() == getattr(want, f).tobytes(), f
+
+
+@pytest.mark.parametrize("seed", [4, 9])
+def test_daemon_resolve_matches_epoch(engine, seed):
+    """kdtn_resolve (one LinksBatchQuery against the informer's pods) plans every link as
+    the full epoch does for a topology whose whole spec is added (status empty) or whose
+    whole status is deleted (spec nil)."""
+    from helpers import random_epoch
+    from kdtn.model import pack as pack_topos
+    topos, vnis = random_epoch(seed, T=120)
+    for i in range(0, len(topos), 5):                       # fresh pods: status [] → all adds
+        if topos[i].spec_links:
+            topos[i].status_links = []
+    for i in range(2, len(topos), 11):                      # deleted specs: all deletes
+        if topos[i].status_links:
+            topos[i].spec_links = None
+    inp = pack_topos(topos, vnis)
+    ref = O.reconcile(inp, tick=TICK)
+    T = inp.topos
+    checked = 0
+    for t in range(T.n):
+        if ref.action[t] != abi.ACT_DIFF:
+            continue
+        nr, nd = T.real_off[t + 1] - T.real_off[t], T.des_off[t + 1] - T.des_off[t]
+        if nr == 0 and nd > 0:
+            links = inp.desired.take(np.arange(T.des_off[t], T.des_off[t + 1]))
+            res, q = engine.resolve(inp.kdict, inp.pdict, T, t, links, abi.BATCH_ADD, inp.vnis)
+            a0, a1 = ref.add_off[t], ref.add_off[t + 1]
+            assert res.tobytes() == ref.add_res[a0:a1].tobytes(), t
+            assert q.tobytes() == ref.add_qdisc[a0:a1].tobytes(), t
+            checked += 1
+        elif nd == 0 and nr > 0 and T.flags[t] & abi.TOPO_SPEC_NIL:
+            links = inp.realised.take(np.arange(T.real_off[t], T.real_off[t + 1]))
+            res, _ = engine.resolve(inp.kdict, inp.pdict, T, t, links, abi.BATCH_DEL, inp.vnis)
+            d0, d1 = ref.del_off[t], ref.del_off[t + 1]
+            assert res.tobytes() == ref.del_res[d0:d1].tobytes(), t
+            checked += 1
+    assert checked >= 10
+
+
+def test_kubedtn_batch_handlers(engine, golden):
+    """KubeDTN.add_links / del_links / update_links on the sample triangle: kinds, VNIs and
+    the first-error abort of the daemon handlers (handler.go:592-671)."""
+    from kdtn.model import KubeDTN
+    tr = golden["transitions"][1]
+    topos = golden_epoch(golden, tr)
+    d = KubeDTN(engine, topos, vxlan=[(topos[0].src_ip, 5001, "/other/ns")])
+    r1 = topos[0]
+    ok = d.add_links(r1.name, r1.namespace, r1.spec_links)
+    assert ok.response and ok.first_failed == -1
+    assert set(ok.plans["kind"].tolist()) <= {abi.KIND_SAME_NODE, abi.KIND_CROSS_NODE}
+    assert (ok.plans["vni"] == [5000 + l.uid for l in r1.spec_links]).all()
+    bad = [Link(**{**r1.spec_links[0].__dict__})] + [Link("eth9", "1.2.3.4", "", "eth9", "", "", "r2", 77)]
+    res = d.add_links(r1.name, r1.namespace, bad)
+    assert not res.response and res.first_failed == 1 and res.err == abi.E_VETH_CIDR
+    ghost = [Link("eth8", "", "", "eth8", "", "", "nobody", 78)]
+    assert d.add_links(r1.name, r1.namespace, ghost).err == abi.E_PEER_LOOKUP
+    upd = d.update_links(r1.name, r1.namespace, [Link("eth1", "", "", "eth1", "", "", "r2", 1,
+                                                       LinkProperties(rate="1.5Gbit"))])
+    assert not upd.response and upd.err == abi.E_RATE
+    dl = d.del_links(r1.name, r1.namespace, r1.spec_links)
+    assert dl.response and dl.plans["vni_hit"].sum() == 0

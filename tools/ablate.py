@@ -21,6 +21,7 @@ ap.add_argument("--reps", type=int, default=10)
 ap.add_argument("--masks", default="ALL,DIFF|RESOLVE,DIFF|QDISC,DIFF")
 ap.add_argument("--cache", default="")
 ap.add_argument("--variants", default="", help="comma list of KDTN_VARIANT values, interleaved")
+ap.add_argument("--env", default="", help="NAME=v1,v2,...: interleaved A/B of an env knob, all stages timed")
 a = ap.parse_args()
 inp = synth.make(a.config, pods_per_shard=a.pods, cache_dir=a.cache or None)
 eng = Engine(device=0)
@@ -41,6 +42,20 @@ if a.variants:
     for v in vs:
         x = sorted(acc[v])
         res["variant_" + v] = {"median": round(x[len(x) // 2], 4), "min": round(x[0], 4)}
+if a.env:
+    name, vals = a.env.split("=")
+    acc = {v: {} for v in vals.split(",")}
+    for rep in range(a.reps + 2):
+        for v in acc:
+            os.environ[name] = v
+            eng.run(abi.STAGE_ALL)
+            eng.sync()
+            if rep >= 2:
+                for k, t in eng.kernel_times().items():
+                    acc[v].setdefault(k, []).append(t)
+    os.environ.pop(name)
+    for v, d in acc.items():
+        res[f"{name}={v}"] = {k: round(sorted(x)[len(x) // 2], 4) for k, x in d.items()}
 masks = {"ALL": abi.STAGE_ALL, "DIFF|RESOLVE": abi.STAGE_DIFF | abi.STAGE_RESOLVE,
          "DIFF|QDISC": abi.STAGE_DIFF | abi.STAGE_QDISC, "DIFF": abi.STAGE_DIFF}
 for name, m in masks.items():
