@@ -72,8 +72,8 @@ struct kdtn_ctx {
     DevBuf v_node, v_vni, v_netns, v_ents, v_slots;
     uint32_t V = 0, vni_mask = 0;
     // pods
-    DevBuf pods, pod_slots, pod_wide;
-    uint32_t slice = 0, pod_total = 0, pod_mask = 0, kb_words = 0;
+    DevBuf pods, pod_ovf, pod_direct;
+    uint32_t slice = 0, pod_total = 0, ovf_mask = 0, kb_words = 0, pod_stamp = 0;
     bool traced = false;
     // work
     DevBuf otarget, sync, misc, hscratch, fscratch, trace;
@@ -350,7 +350,7 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->pd_pct, &c->pd_dur, &c->pd_rate, &c->pd_rerr, &c->t_ns, &c->t_name, &c->t_src,
                       &c->t_netns, &c->t_flags, &c->t_roff, &c->t_noff, &c->real.buf, &c->des.buf,
                       &c->v_node, &c->v_vni, &c->v_netns, &c->v_ents, &c->v_slots, &c->pods,
-                      &c->pod_slots, &c->pod_wide, &c->otarget, &c->sync, &c->misc, &c->hscratch,
+                      &c->pod_ovf, &c->pod_direct, &c->otarget, &c->sync, &c->misc, &c->hscratch,
                       &c->fscratch, &c->action, &c->del_off, &c->add_off, &c->upd_off, &c->del_idx,
                       &c->add_idx, &c->upd_idx, &c->del_res, &c->add_res, &c->upd_res,
                       &c->add_qdisc, &c->upd_qdisc, &c->kd_utf8, &c->pd_utf8, &c->w_rel,
@@ -441,10 +441,14 @@ int kdtn_epoch_upload(kdtn_ctx* c, const kdtn_epoch_in* in) {
         return KDTN_EINVAL;
     }
     c->pod_total = slice * (uint32_t)c->nranks;
-    c->pod_mask = next_pow2((uint64_t)c->pod_total * 2) - 1;
+    c->ovf_mask = next_pow2((uint64_t)c->pod_total * 2) - 1;
     TRY(ensure(c->pods, (size_t)c->pod_total * 16));
-    TRY(ensure(c->pod_slots, (size_t)(c->pod_mask + 1) * 4));
-    TRY(ensure(c->pod_wide, (size_t)(c->pod_mask + 1) * 16));
+    TRY(ensure(c->pod_ovf, (size_t)(c->ovf_mask + 1) * 4));
+    if (c->pod_direct.cap < (size_t)D * 16) {                  // stamps start from a zeroed table
+        TRY(ensure(c->pod_direct, (size_t)D * 16));
+        HIP_TRY(hipMemsetAsync(c->pod_direct.p, 0, c->pod_direct.cap, c->stream));
+        c->pod_stamp = 0;
+    }
 
     const uint32_t M = in->realised.n, N = in->desired.n;
     const uint32_t nwg = (T.n + TPW - 1) / TPW;
@@ -515,14 +519,19 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
             }
         }
         timer_mark(c, "pods_allgather");
-        const size_t pcap = (size_t)c->pod_mask + 1;
-        HIP_TRY(hipMemsetAsync(c->pod_slots.p, 0xFF, pcap * 4, s));
-        if (c->pod_total)
-            k_pod_slots_build<<<nblocks(c->pod_total), BLOCK, 0, s>>>(dp<uint4>(c->pods), c->pod_total,
-                                                                     dp<uint32_t>(c->pod_slots), c->pod_mask);
-        k_pod_slots_expand<<<nblocks(pcap), BLOCK, 0, s>>>(dp<uint4>(c->pods), dp<uint32_t>(c->pod_slots),
-                                                          dp<uint32_t>(c->kd_bits) + (size_t)KB_PHYSICAL * c->kb_words,
-                                                          dp<uint4>(c->pod_wide), (uint32_t)pcap);
+        if (++c->pod_stamp >= 0x7FFFFFFFu) {                          // stamp wrap: clear once
+            HIP_TRY(hipMemsetAsync(c->pod_direct.p, 0, c->pod_direct.cap, s));
+            c->pod_stamp = 1;
+        }
+        HIP_TRY(hipMemsetAsync(c->pod_ovf.p, 0xFF, ((size_t)c->ovf_mask + 1) * 4, s));
+        if (c->pod_total) {
+            k_pod_direct_scatter<<<nblocks(c->pod_total), BLOCK, 0, s>>>(
+                dp<uint4>(c->pods), c->pod_total, dp<uint32_t>(c->kd_bits) + (size_t)KB_PHYSICAL * c->kb_words,
+                dp<uint4>(c->pod_direct), c->pod_stamp, c->D);
+            k_pod_direct_verify<<<nblocks(c->pod_total), BLOCK, 0, s>>>(dp<uint4>(c->pods), c->pod_total,
+                                                                       dp<uint4>(c->pod_direct), c->pod_stamp,
+                                                                       dp<uint32_t>(c->pod_ovf), c->ovf_mask, c->D);
+        }
         if (c->V) {
             const size_t vcap = (size_t)c->vni_mask + 1;
             HIP_TRY(hipMemsetAsync(c->v_slots.p, 0xFF, vcap * 4, s));
@@ -542,8 +551,10 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         tb.prate = dp<uint2>(c->pd_rate);
         tb.rate_err = dp<uint32_t>(c->pd_rerr);
         tb.pods = dp<uint4>(c->pods);
-        tb.pod_wide = dp<uint4>(c->pod_wide);
-        tb.pod_mask = c->pod_mask;
+        tb.pod_direct = dp<uint4>(c->pod_direct);
+        tb.pod_stamp = c->pod_stamp;
+        tb.pod_ovf = dp<uint32_t>(c->pod_ovf);
+        tb.ovf_mask = c->ovf_mask;
         tb.vnis = dp<uint4>(c->v_ents);
         tb.vni_slots = dp<uint32_t>(c->v_slots);
         tb.vni_mask = c->V ? c->vni_mask : 0;
@@ -597,6 +608,7 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         case 513: k_reconcile<513><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
         case 1025: k_reconcile<1025><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
         case 1537: k_reconcile<1537><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
+        case 545: k_reconcile<545><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
         case 641: k_reconcile<641><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
         case 529: k_reconcile<529><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
         case 129: k_reconcile<129><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;

@@ -11,15 +11,16 @@
 //                  per 12M strings, L2-resident); ppct u32 (Percentage2u32 or PCT_ERR);
 //                  pdur {us, ticks, err}; prate {lo, hi, err}
 //   pod table    : pods[g] = {ns, name, src_ip, net_ns|spec_nil<<31} per global pod index;
-//                  lookup table of 16-B self-contained slots keyed by (ns, name), probed in
-//                  128-B buckets: a lookup is ONE line (the slot also carries the PHYSICAL
-//                  bit of the pod's name, so a hit needs no key-string flag read).
+//                  lookup table of 16-B self-contained slots indexed by the name's kdict id
+//                  and stamped per epoch: a lookup is ONE gather with no probing (the slot
+//                  also carries the PHYSICAL bit of the name, so a hit needs no key-string
+//                  flag read); names shared by several pods go through an overflow table.
 // Kernels (launch order):
 //   k_kdict_flags   MakeVeth / addLink predicates per key string          (D threads)
 //   k_pdict_parse   ParseDuration / ParseFloatPercentage / ParseRate      (P threads)
 //   k_pods_fill     this rank's pod-status slice                          (slice threads)
 //   [RCCL all-gather of the pod-status table when nranks > 1]
-//   k_pod_slots_build + k_pod_slots_expand, k_vni_pack + k_vni_ht_build
+//   k_pod_direct_scatter + k_pod_direct_verify, k_vni_pack + k_vni_ht_build
 //   k_reconcile     ONE pass per workgroup of TPW topologies: Reconcile gate + CalcDiff in
 //                   LDS, decoupled look-back for the batch bases, then barrier-free emission
 //                   of the batch lists, addLink/delLink/UpdateLinks pure prefix, MakeQdiscs.
@@ -134,8 +135,10 @@ struct DevTables {             // read-only lookup structures of the epoch
     const uint2* prate;        // [P] {lo, hi}; all-ones = error or 2^64-1: see rate_err
     const uint32_t* rate_err;  // [ceil(P/64)*2] bitset: ParseRate failed
     const uint4* pods;         // [pod_total] {ns, name, src_ip, net_ns|spec_nil<<31}
-    const uint4* pod_wide;     // [pod_mask+1] {ns, name, src_ip|netns_empty<<31, g<<2|phys<<1|spec_nil}
-    uint32_t pod_mask;
+    const uint4* pod_direct;   // [D] by name id: {ns, g<<2|phys<<1|spec_nil, src_ip|netns_empty<<31, stamp<<1|multi}
+    uint32_t pod_stamp;        // this epoch's stamp
+    const uint32_t* pod_ovf;   // [ovf_mask+1] pod indices of shared names, keyed by (ns, name)
+    uint32_t ovf_mask;
     const uint4* vnis;         // [V] {node, vni, net_ns, 0}
     const uint32_t* vni_slots; // [vni_mask+1]
     uint32_t vni_mask;         // 0 ⇒ empty table
@@ -177,9 +180,10 @@ __global__ void k_kdict_flags(const uint8_t* bytes, const uint32_t* offs, uint32
 __global__ void k_pdict_parse(const uint8_t* bytes, const uint32_t* offs, uint32_t n, double tick,
                               uint32_t* ppct, uint2* pdur, uint2* prate, uint32_t* rate_err);
 __global__ void k_pods_fill(DevTopos T, uint32_t slice, uint32_t rank_base, uint4* pods);
-__global__ void k_pod_slots_build(const uint4* pods, uint32_t total, uint32_t* slots, uint32_t mask);
-__global__ void k_pod_slots_expand(const uint4* pods, const uint32_t* slots, const uint32_t* phys_bits,
-                                   uint4* wide, uint32_t cap);
+__global__ void k_pod_direct_scatter(const uint4* pods, uint32_t total, const uint32_t* phys_bits,
+                                     uint4* slots, uint32_t stamp, uint32_t nd);
+__global__ void k_pod_direct_verify(const uint4* pods, uint32_t total, uint4* slots, uint32_t stamp,
+                                    uint32_t* ovf, uint32_t mask, uint32_t nd);
 __global__ void k_vni_ht_build(const uint4* ents, uint32_t n, uint32_t* slots, uint32_t mask);
 __global__ void k_vni_pack(const uint32_t* node, const int32_t* vni, const uint32_t* net_ns,
                            uint32_t n, uint4* ents);

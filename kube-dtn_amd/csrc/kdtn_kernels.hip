@@ -306,14 +306,14 @@ __global__ void __launch_bounds__(BLOCK) k_pods_fill(DevTopos T, uint32_t slice,
     pods[rank_base + t] = e;
 }
 
-// Pod lookup table (informer store, handler.go:27-41): open addressing over 16-B
-// self-contained slots {ns, name, src_ip|netns_empty<<31, g<<2|physical<<1|spec_nil},
-// probed inside 128-B buckets of 8 slots (one L2 line) before moving to the next bucket,
-// so a lookup costs one line fetch at the table's load factor of 1/2.
-// Built in two passes: k_pod_slots_build claims u32 index slots with one 32-bit CAS per pod
-// (random device-scope atomics run at the memory side, so the build keeps them to one
-// per pod; atomicMin keeps the smallest pod index of duplicate keys, the informer's
-// first-wins), then k_pod_slots_expand writes the 16-B slots sequentially.
+// Pod lookup table (informer store, handler.go:27-41), direct-mapped by the kdict id of
+// the pod's name: slot[name] = {ns, g<<2|physical<<1|spec_nil, src_ip|netns_empty<<31,
+// stamp<<1|multi}. A peer lookup is ONE 16-B gather with no probing: the slot belongs to
+// this epoch when its stamp matches, and answers (ns, name) when ns matches. Names shared
+// by several pods (other namespaces, or duplicate keys) set `multi`; their lookups go to a
+// small overflow table of pod indices keyed by (ns, name), which keeps the informer's
+// first-wins (smallest index) with one CAS + atomicMin per colliding pod. The stamp (per
+// context, incremented each epoch) makes clearing the table unnecessary.
 KD_INLINE uint32_t pod_probe_slot(uint32_t home, uint32_t i, uint32_t mask) {
     const uint32_t b = (home >> 3) + (i >> 3);
     return ((b << 3) + ((home + i) & 7u)) & mask;
@@ -321,40 +321,48 @@ KD_INLINE uint32_t pod_probe_slot(uint32_t home, uint32_t i, uint32_t mask) {
 KD_INLINE uint32_t pod_home(uint32_t mask, uint32_t ns, uint32_t name) {
     return (uint32_t)hash64(((uint64_t)ns << 32) | name) & mask;
 }
-
-__global__ void __launch_bounds__(BLOCK) k_pod_slots_build(const uint4* pods, uint32_t total,
-                                                           uint32_t* slots, uint32_t mask) {
-    const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
-    if (g >= total) return;
-    const uint4 e = pods[g];
-    if (e.x == 0xFFFFFFFFu) return;                        // padding row
-    const uint32_t home = pod_home(mask, e.x, e.y);
+KD_INLINE void ovf_insert(const uint4* pods, uint32_t g, uint32_t ns, uint32_t name, uint32_t* ovf, uint32_t mask) {
+    const uint32_t home = pod_home(mask, ns, name);
     for (uint32_t i = 0;; ++i) {
         const uint32_t h = pod_probe_slot(home, i, mask);
-        const uint32_t prev = atomicCAS(&slots[h], 0xFFFFFFFFu, g);
-        if (prev == 0xFFFFFFFFu) return;
+        const uint32_t prev = atomicCAS(&ovf[h], 0xFFFFFFFFu, g);
+        if (prev == 0xFFFFFFFFu || prev == g) return;
         const uint4 o = pods[prev];
-        if (o.x == e.x && o.y == e.y) {
-            atomicMin(&slots[h], g);                       // first topology wins
+        if (o.x == ns && o.y == name) {
+            atomicMin(&ovf[h], g);                         // first topology wins
             return;
         }
     }
 }
 
-__global__ void __launch_bounds__(BLOCK) k_pod_slots_expand(const uint4* pods, const uint32_t* slots,
-                                                            const uint32_t* phys_bits, uint4* wide,
-                                                            uint32_t cap) {
-    const uint32_t h = blockIdx.x * BLOCK + threadIdx.x;
-    if (h >= cap) return;
-    const uint32_t g = slots[h];
-    uint4 w = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
-    if (g != 0xFFFFFFFFu) {
-        const uint4 e = pods[g];
-        const uint32_t phys = (phys_bits[e.y >> 5] >> (e.y & 31)) & 1u;
-        w = make_uint4(e.x, e.y, e.z | ((e.w & 0x7FFFFFFFu) == 0 ? 0x80000000u : 0u),
-                       (g << 2) | (phys << 1) | (e.w >> 31));
-    }
-    wide[h] = w;
+__global__ void __launch_bounds__(BLOCK) k_pod_direct_scatter(const uint4* pods, uint32_t total,
+                                                              const uint32_t* phys_bits, uint4* slots,
+                                                              uint32_t stamp, uint32_t nd) {
+    const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
+    if (g >= total) return;
+    const uint4 e = pods[g];
+    if (e.x == 0xFFFFFFFFu || e.y >= nd) return;           // padding row / name outside this dictionary
+    const uint32_t phys = (phys_bits[e.y >> 5] >> (e.y & 31)) & 1u;
+    slots[e.y] = make_uint4(e.x, (g << 2) | (phys << 1) | (e.w >> 31),
+                            e.z | ((e.w & 0x7FFFFFFFu) == 0 ? 0x80000000u : 0u), stamp << 1);
+}
+
+// Pods whose name slot was won by another pod: mark the name `multi` and put both pods
+// into the overflow table (duplicates are rare; the table then answers every lookup of
+// that name).
+__global__ void __launch_bounds__(BLOCK) k_pod_direct_verify(const uint4* pods, uint32_t total, uint4* slots,
+                                                             uint32_t stamp, uint32_t* ovf, uint32_t mask,
+                                                             uint32_t nd) {
+    const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
+    if (g >= total) return;
+    const uint4 e = pods[g];
+    if (e.x == 0xFFFFFFFFu || e.y >= nd) return;
+    const uint4 w = slots[e.y];
+    const uint32_t owner = w.y >> 2;
+    if (owner == g) return;
+    reinterpret_cast<uint32_t*>(slots + e.y)[3] = (stamp << 1) | 1u;
+    ovf_insert(pods, g, e.x, e.y, ovf, mask);
+    ovf_insert(pods, owner, pods[owner].x, e.y, ovf, mask);
 }
 
 __global__ void __launch_bounds__(BLOCK) k_vni_pack(const uint32_t* node, const int32_t* vni,
@@ -388,31 +396,34 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 template <bool NT>
-KD_INLINE uint4 pod_slot(const DevTables& tb, uint32_t h) {
+KD_INLINE uint4 pod_slot(const DevTables& tb, uint32_t name) {
     if constexpr (NT) {           // little reuse: keep L2 for the parsed tables
-        const u32x4 v = ldg_nt(reinterpret_cast<const u32x4*>(tb.pod_wide), h);
+        const u32x4 v = ldg_nt(reinterpret_cast<const u32x4*>(tb.pod_direct), name);
         return make_uint4(v.x, v.y, v.z, v.w);
     } else {
-        return ldg(tb.pod_wide, h);
+        return ldg(tb.pod_direct, name);
     }
 }
-// Resolve a lookup whose home slot h already read as w (probing continues in the bucket).
+// Resolve a lookup of (ns, name) whose direct slot already read as w.
 // Returns {g | POD_SPEC_NIL | POD_PHYSICAL, src_ip | netns_empty<<31}; x = 0xFFFFFFFF on a miss.
-template <bool NT>
-KD_INLINE uint2 pod_probe(const DevTables& tb, uint32_t ns, uint32_t name, uint32_t h, uint4 w) {
-    if (ns == 0xFFFFFFFFu) return make_uint2(0xFFFFFFFFu, 0u);
-    for (uint32_t i = 1;; ++i) {
-        if (w.x == ns && w.y == name)
-            return make_uint2((w.w >> 2) | ((w.w & 1u) << 31) | ((w.w & 2u) << 29), w.z);
-        if (w.x == 0xFFFFFFFFu) return make_uint2(0xFFFFFFFFu, 0u);
-        w = pod_slot<NT>(tb, pod_probe_slot(h, i, tb.pod_mask));
+KD_INLINE uint2 pod_resolve(const DevTables& tb, uint32_t ns, uint32_t name, uint4 w) {
+    if (ns == 0xFFFFFFFFu || (w.w >> 1) != tb.pod_stamp) return make_uint2(0xFFFFFFFFu, 0u);
+    if ((w.w & 1u) == 0) {
+        if (w.x != ns) return make_uint2(0xFFFFFFFFu, 0u);
+        return make_uint2((w.y >> 2) | ((w.y & 1u) << 31) | ((w.y & 2u) << 29), w.z);
     }
-}
-template <bool NT = false>
-KD_INLINE uint2 pod_lookup(const DevTables& tb, uint32_t ns, uint32_t name) {
-    if (ns == 0xFFFFFFFFu) return make_uint2(0xFFFFFFFFu, 0u);
-    const uint32_t h = pod_home(tb.pod_mask, ns, name);
-    return pod_probe<NT>(tb, ns, name, h, pod_slot<NT>(tb, h));
+    // name shared by several pods: overflow table of pod indices (rare)
+    const uint32_t home = pod_home(tb.ovf_mask, ns, name);
+    for (uint32_t i = 0;; ++i) {
+        const uint32_t g = ldg(tb.pod_ovf, pod_probe_slot(home, i, tb.ovf_mask));
+        if (g == 0xFFFFFFFFu) return make_uint2(0xFFFFFFFFu, 0u);
+        const uint4 e = ldg(tb.pods, g);
+        if (e.x == ns && e.y == name) {
+            const uint32_t phys = (w.y >> 1) & 1u;          // a property of the name string
+            return make_uint2(g | (e.w & POD_SPEC_NIL) | (phys ? POD_PHYSICAL : 0u),
+                              e.z | ((e.w & 0x7FFFFFFFu) == 0 ? 0x80000000u : 0u));
+        }
+    }
 }
 
 // VxlanManager.Get(vni) on node `node`: net_ns id, or 0xFFFFFFFF when absent.
@@ -657,8 +668,8 @@ KD_INLINE void emit_upd(const RecCols& c, uint32_t j, const DevTables& tb, const
 // add_finish combines them in the reference's step order and stores the outputs.
 struct AddGath {
     PropVals v;
-    uint4 slot;                       // home slot of (ns, peer_pod)
-    uint32_t h, lns, kb_ip, kb_mac;
+    uint4 slot;                       // direct slot of peer_pod
+    uint32_t lns, kb_ip, kb_mac;
 };
 
 template <int V>
@@ -669,10 +680,7 @@ KD_INLINE void add_gather(const RecCols& c, const TopoCtx& tc, const DevTables& 
     g.lns = tc.ns == 0 ? tb.special[SPECIAL_DEFAULT] : tc.ns;                     // :29-31
     g.kb_ip = ldg(tb.kbits + (size_t)KB_CIDR_BAD * tb.kb_words, c.lip >> 5);
     g.kb_mac = ldg(tb.kbits + (size_t)KB_MAC_BAD * tb.kb_words, c.lmac >> 5);
-    if constexpr ((V & VAR_SKIP_POD) == 0) {
-        g.h = pod_home(tb.pod_mask, g.lns, c.pp);
-        g.slot = pod_slot<(V & VAR_NT_POD) != 0>(tb, g.h);
-    }
+    if constexpr ((V & VAR_SKIP_POD) == 0) g.slot = pod_slot<(V & VAR_NT_POD) != 0>(tb, c.pp);
 }
 
 template <int V>
@@ -694,7 +702,7 @@ KD_INLINE void add_finish(const RecCols& c, const AddGath& g, const DevLinks& N,
         const bool lh = c.pp == tb.special[SPECIAL_LOCALHOST];
         uint2 p = make_uint2(0xFFFFFFFFu, 0u);
         if constexpr ((V & VAR_SKIP_POD) != 0) p = make_uint2(c.pp & POD_INDEX, g.lns);   // profiling only
-        else if (!lh) p = pod_probe<(V & VAR_NT_POD) != 0>(tb, g.lns, c.pp, g.h, g.slot);
+        else if (!lh) p = pod_resolve(tb, g.lns, c.pp, g.slot);
         const bool miss = p.x == 0xFFFFFFFFu;
         if (lh) {
             kind = KDTN_KIND_MACVLAN;                                                     // :333
@@ -1353,6 +1361,7 @@ template __global__ void k_reconcile<257>(DevTopos, DevLinks, DevLinks, DevTable
 template __global__ void k_reconcile<513>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
 template __global__ void k_reconcile<529>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
 template __global__ void k_reconcile<641>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
+template __global__ void k_reconcile<545>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
 template __global__ void k_reconcile<1025>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
 template __global__ void k_reconcile<1537>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
 

@@ -363,3 +363,31 @@ def test_kubedtn_batch_handlers(engine, golden):
     assert not upd.response and upd.err == abi.E_RATE
     dl = d.del_links(r1.name, r1.namespace, r1.spec_links)
     assert dl.response and dl.plans["vni_hit"].sum() == 0
+
+
+def test_pod_names_shared_across_namespaces(engine):
+    """getPod keys are (namespace, name) (handler.go:27-41): a name used in several
+    namespaces, and a duplicate key (the informer's first object wins), go through the
+    engine's overflow table; lookups from every namespace match the oracle."""
+    rng = random.Random(8)
+    nss = ["ns1", "ns2", "ns3", "default"]
+    topos = []
+    names = ["a", "b", "c"]
+    for i in range(40):
+        ns = nss[i % 4]
+        name = names[i % 3] if i < 30 else f"u{i}"
+        links = [Link(f"eth{k}", "", "", f"eth{k}", "", "", rng.choice(names + ["u31", "zz"]), 1000 * i + k,
+                      LinkProperties(latency="1ms"))
+                 for k in range(rng.randint(1, 4))]
+        topos.append(Topology(name, ns, links, [], rng.choice(["10.0.0.1", "10.0.0.2", ""]),
+                              rng.choice(["/run/ns/x", ""]) if i % 5 else "/run/ns/y"))
+    topos.append(Topology("a", "", [Link("eth0", "", "", "eth0", "", "", "a", 99)], [], "10.0.0.1", "/n"))
+    inp = pack(topos)
+    out = engine.reconcile(inp)
+    assert_same(out, O.reconcile(inp, tick=TICK), "shared names")
+    kinds = set(out.add_res["kind"].tolist())
+    assert abi.KIND_CROSS_NODE in kinds and (out.add_res["err"] == abi.E_PEER_LOOKUP).any()
+    # repeated epochs on the same context (stamped table, no clearing) stay exact
+    inp2 = pack(topos[5:])
+    assert_same(engine.reconcile(inp2), O.reconcile(inp2, tick=TICK), "second epoch")
+    assert_same(engine.reconcile(inp), O.reconcile(inp, tick=TICK), "third epoch")
