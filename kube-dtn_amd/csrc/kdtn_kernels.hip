@@ -154,7 +154,9 @@ KD_INLINE bool cidr_swar(const uint32_t* w, uint32_t len, bool* slow) {
     C &= L;
     const uint32_t s = __builtin_ctz(S | 0x1000000u);           // first '/' (24 if none)
     const uint32_t m = len - s - 1u;                             // prefix digits
-    *slow = (C != 0u) | (m > 2u && s < len);
+    // generic parser only for IPv6 candidates (any IPv6 text has a colon) and for IPv4-looking
+    // strings (first byte a digit) with a prefix of 3+ digits; anything else cannot parse
+    *slow = (C != 0u) | ((D & 1u) != 0u && m > 2u && s < len);
     const uint32_t sep = P | S;
     uint32_t ok = ((D | sep) == L) & (__builtin_popcount(P) == 3) & (__builtin_popcount(S) == 1) &
                   ((P >> s) == 0u) & ((sep & (sep << 1)) == 0u) & (D & 1u) & (s + 1u < len) & (s <= 15u);
