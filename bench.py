@@ -110,8 +110,19 @@ def wire_stage(eng, reps: int = 5):
         for k, v in eng.kernel_times().items():
             acc[k] = acc.get(k, 0.0) + v / reps
     gpu_ms = sum(v for k, v in acc.items() if k != "wire_host_sync")
-    return {"bytes": n, "gpu_ms": gpu_ms, "out_GBps": n / (gpu_ms * 1e-3) / 1e9,
-            "kernels_ms": acc, "note": "not part of value; arena-size host round trip excluded"}
+    res = {"bytes": n, "gpu_ms": gpu_ms, "out_GBps": n / (gpu_ms * 1e-3) / 1e9,
+           "kernels_ms": acc, "note": "not part of value; arena-size host round trip excluded"}
+    # RemotePod fan-out grouped per destination daemon (kdtn_epoch_fanout)
+    eng.fanout()
+    facc: dict[str, float] = {}
+    for _ in range(reps):
+        node, off, idx = eng.fanout()
+        for k, v in eng.kernel_times().items():
+            facc[k] = facc.get(k, 0.0) + v / reps
+    res["fanout"] = {"daemons": int(len(node)), "remote_rpcs": int(len(idx)),
+                     "gpu_ms": sum(v for k, v in facc.items() if k != "fanout_host_sync"),
+                     "kernels_ms": facc}
+    return res
 
 
 def pmc_traffic(links_per_gpu: int):

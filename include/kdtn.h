@@ -23,6 +23,8 @@
  *   kdtn_resolve          replaces the pure prefix of the daemon's AddLinks / DelLinks for
  *                         one LinksBatchQuery (handler.go:592-632)
  *   kdtn_epoch_encode     replaces Link.ToProto + proto.Marshal of the batches
+ *   kdtn_epoch_fanout     groups the daemons' UpdateRemote RPCs (common/utils.go:39-67)
+ *                         per destination daemon
  *
  * Conventions
  *   - No C++ or HIP types cross this ABI: plain pointers, sizes and PODs.
@@ -333,6 +335,23 @@ typedef struct kdtn_wire {
  * returns the arena size through n_bytes. Synchronous. */
 int kdtn_epoch_encode(kdtn_ctx* ctx, uint64_t* n_bytes);
 int kdtn_epoch_download_wire(kdtn_ctx* ctx, kdtn_wire* out);
+
+/* ---- RemotePod fan-out grouped per destination daemon ------------------------------ */
+/* The UpdateRemote RPCs the daemons would send for this epoch's AddLinks batches
+ * (daemon/kubedtn/handler.go:419-453, common/utils.go:39-67): an entry sends one when it is
+ * CROSS_NODE, its qdisc was built (SetupVxLan → MakeQdiscs fails first) and no earlier
+ * link of its batch failed (handler.go:601-607). The reference sends one RPC per link;
+ * here they are grouped per destination daemon (peer status.src_ip = kdtn_resolved.vtep):
+ * node[k] = kdict id of daemon k (ascending), its entries idx[off[k] .. off[k+1]) are
+ * add-list entry indices in add-list order. Requires a run with RESOLVE and QDISC. */
+typedef struct kdtn_fanout {
+    uint32_t* node;          /* [node_cap]                                            */
+    uint32_t* off;           /* [node_cap + 1]                                        */
+    uint32_t* idx;           /* [idx_cap]                                             */
+    uint32_t  node_cap, idx_cap;
+    uint32_t  n_nodes, n_send;   /* out                                               */
+} kdtn_fanout;
+int kdtn_epoch_fanout(kdtn_ctx* ctx, kdtn_fanout* out);
 
 /* ---- multi-GPU (one process per GPU): RCCL all-gather of the pod-status table ------ */
 int kdtn_comm_unique_id(uint8_t out[128]);

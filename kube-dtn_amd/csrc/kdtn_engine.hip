@@ -85,6 +85,9 @@ struct kdtn_ctx {
     DevBuf kd_utf8, pd_utf8, w_rel, w_topo, w_size, w_err, w_off, w_part, w_arena;
     uint64_t w_bytes = 0;
     bool encoded = false;
+    // RemotePod fan-out
+    DevBuf f_mark, f_send, f_node_idx, f_nodes, f_counts, f_base, f_part, f_idx;
+    uint32_t f_stamp = 0;
     // host-visible counters
     uint32_t* h_misc = nullptr;   // pinned: [0]=default id, [1]=del, [2]=upd, [3]=add, [4]=look-back error
     bool uploaded = false;
@@ -354,7 +357,9 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->fscratch, &c->action, &c->del_off, &c->add_off, &c->upd_off, &c->del_idx,
                       &c->add_idx, &c->upd_idx, &c->del_res, &c->add_res, &c->upd_res,
                       &c->add_qdisc, &c->upd_qdisc, &c->kd_utf8, &c->pd_utf8, &c->w_rel,
-                      &c->w_topo, &c->w_size, &c->w_err, &c->w_off, &c->w_part, &c->w_arena};
+                      &c->w_topo, &c->w_size, &c->w_err, &c->w_off, &c->w_part, &c->w_arena,
+                      &c->f_mark, &c->f_send, &c->f_node_idx, &c->f_nodes, &c->f_counts, &c->f_base,
+                      &c->f_part, &c->f_idx};
     for (DevBuf* b : bufs) release(*b);
     for (int i = 0; i <= kMaxTimers; ++i)
         if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
@@ -887,6 +892,90 @@ int kdtn_epoch_download_wire(kdtn_ctx* c, kdtn_wire* o) {
         HIP_TRY(hipMemcpyAsync(o->bytes, c->w_arena.p, c->w_bytes, hipMemcpyDeviceToHost, s));
     if (o->off) HIP_TRY(hipMemcpyAsync(o->off, c->w_off.p, ((size_t)3 * c->T + 1) * 8, hipMemcpyDeviceToHost, s));
     if (o->err && c->T) HIP_TRY(hipMemcpyAsync(o->err, c->w_err.p, (size_t)c->T * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return KDTN_OK;
+}
+
+int kdtn_epoch_fanout(kdtn_ctx* c, kdtn_fanout* o) {
+    if (!c || !o || !c->ran) return KDTN_EINVAL;
+    if ((c->last_stages & (KDTN_STAGE_RESOLVE | KDTN_STAGE_QDISC)) != (KDTN_STAGE_RESOLVE | KDTN_STAGE_QDISC))
+        return KDTN_EINVAL;
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    hipStream_t s = c->stream;
+    const uint32_t na = c->h_misc[3], T = c->T, D = c->D;
+    if (c->f_mark.cap < (size_t)D * 4) {                      // stamps start from a zeroed table
+        TRY(ensure(c->f_mark, (size_t)D * 4));
+        HIP_TRY(hipMemsetAsync(c->f_mark.p, 0, c->f_mark.cap, s));
+        c->f_stamp = 0;
+    }
+    if (++c->f_stamp == 0xFFFFFFFFu) {
+        HIP_TRY(hipMemsetAsync(c->f_mark.p, 0, c->f_mark.cap, s));
+        c->f_stamp = 1;
+    }
+    const uint32_t nchunks = nblocks(na, FAN_CHUNK);
+    const uint32_t nbd = nblocks(D, SCAN_CHUNK);
+    TRY(ensure(c->f_send, (size_t)na + 16));
+    TRY(ensure(c->f_node_idx, (size_t)D * 4));
+    TRY(ensure(c->f_nodes, (size_t)FAN_NODE_CAP * 4 + 16));
+    TRY(ensure(c->f_part, (size_t)nbd * 8 + 16));
+    TRY(ensure(c->f_counts, (size_t)FAN_NODE_CAP * nchunks * 4 + 16));
+    TRY(ensure(c->f_base, ((size_t)FAN_NODE_CAP * nchunks + 1) * 8 + 16));
+    TRY(ensure(c->f_idx, (size_t)na * 4 + 16));
+    uint32_t* misc = dp<uint32_t>(c->misc);
+    uint32_t* n_nodes = misc + MISC_FAN_NODES;
+    c->n_ev = 0;
+    (void)hipEventRecord(c->ev[0], s);
+    FanIn f{dp<uint32_t>(c->add_off), dp<uint4>(c->add_res), dp<uint2>(c->add_qdisc), T, na, c->f_stamp};
+    if (T) k_fan_mark<<<nblocks(T), BLOCK, 0, s>>>(f, dp<uint32_t>(c->f_mark), dp<uint8_t>(c->f_send));
+    k_fan_nodes_count<<<nbd, BLOCK, 0, s>>>(dp<uint32_t>(c->f_mark), D, c->f_stamp, dp<uint64_t>(c->f_part));
+    k_scan_top<<<1, BLOCK, 0, s>>>(dp<uint64_t>(c->f_part), nbd);
+    k_fan_nodes_write<<<nbd, BLOCK, 0, s>>>(dp<uint32_t>(c->f_mark), D, c->f_stamp, dp<uint64_t>(c->f_part),
+                                           dp<uint32_t>(c->f_node_idx), dp<uint32_t>(c->f_nodes), n_nodes);
+    timer_mark(c, "fanout_nodes");
+    uint32_t nn = 0;
+    HIP_TRY(hipMemcpyAsync(&nn, n_nodes, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (nn > (uint32_t)FAN_NODE_CAP) {
+        std::snprintf(g_last_error, sizeof(g_last_error), "fan-out over %u daemons (cap %d)", nn, FAN_NODE_CAP);
+        return KDTN_EINVAL;
+    }
+    timer_mark(c, "fanout_host_sync");
+    const uint32_t ncells = nn * nchunks;
+    uint32_t nsend = 0;
+    if (na && nn) {
+        k_fan_count<<<nchunks, 64, 0, s>>>(f, dp<uint8_t>(c->f_send), dp<uint32_t>(c->f_node_idx), n_nodes,
+                                           dp<uint32_t>(c->f_counts), nchunks);
+        const uint32_t nbc = nblocks((uint64_t)ncells + 1, SCAN_CHUNK);
+        TRY(ensure(c->w_part, (size_t)nbc * 8 + 16));
+        k_scan_partial<<<nbc, BLOCK, 0, s>>>(dp<uint32_t>(c->f_counts), ncells, dp<uint64_t>(c->w_part));
+        k_scan_top<<<1, BLOCK, 0, s>>>(dp<uint64_t>(c->w_part), nbc);
+        k_scan_final<<<nbc, BLOCK, 0, s>>>(dp<uint32_t>(c->f_counts), ncells, dp<uint64_t>(c->w_part),
+                                           dp<uint64_t>(c->f_base));
+        k_fan_scatter<<<nchunks, 64, 0, s>>>(f, dp<uint8_t>(c->f_send), dp<uint32_t>(c->f_node_idx), n_nodes,
+                                             dp<uint64_t>(c->f_base), nchunks, dp<uint32_t>(c->f_idx));
+        HIP_TRY(hipGetLastError());
+        uint64_t tot = 0;
+        HIP_TRY(hipMemcpyAsync(&tot, dp<uint64_t>(c->f_base) + ncells, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        nsend = (uint32_t)tot;
+    }
+    timer_mark(c, "fanout_group");
+    o->n_nodes = nn;
+    o->n_send = nsend;
+    if (nn > o->node_cap || nsend > o->idx_cap) return KDTN_ENOSPC;
+    if (o->node && nn) HIP_TRY(hipMemcpyAsync(o->node, c->f_nodes.p, (size_t)nn * 4, hipMemcpyDeviceToHost, s));
+    if (o->idx && nsend) HIP_TRY(hipMemcpyAsync(o->idx, c->f_idx.p, (size_t)nsend * 4, hipMemcpyDeviceToHost, s));
+    if (o->off) {
+        // off[k] = base of (node k, chunk 0): strided 8-B reads of the scanned (node, chunk) matrix
+        std::vector<uint64_t> b(nn ? nn : 1);
+        if (nn && na)
+            HIP_TRY(hipMemcpy2DAsync(b.data(), 8, dp<uint64_t>(c->f_base), (size_t)nchunks * 8, 8, nn,
+                                     hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        for (uint32_t k = 0; k < nn; ++k) o->off[k] = na ? (uint32_t)b[k] : 0u;
+        o->off[nn] = nsend;
+    }
     HIP_TRY(hipStreamSynchronize(s));
     return KDTN_OK;
 }

@@ -1,0 +1,139 @@
+// kdtn_fanout.hip — RemotePod fan-out grouping.
+//
+// For every AddLinks entry that makes the daemon call UpdateRemote — classified
+// CROSS_NODE (handler.go:419-453), its qdisc built (SetupVxLan → MakeQdiscs,
+// daemon/vxlan/vxlan.go:40, fails before the RPC) and its batch not aborted by an earlier
+// failing link (handler.go:601-607) — the RemotePod RPC goes to the peer's daemon at
+// peer status.src_ip (common/utils.go:39-67). The reference sends one RPC per link; this
+// stage groups them per destination daemon, so a caller can send one batch per node:
+// nodes in ascending kdict-id order of their src_ip, entries of a node in add-list order.
+//
+// Kernels: k_fan_mark (one thread per topology: first-error scan, marks senders and their
+// nodes in a stamped D-sized table), k_fan_nodes_* (compaction of marked node ids → dense
+// node index), k_fan_count / k_fan_scatter (single-wave workgroups over chunks of 4,096
+// entries: LDS histogram, node-major scan of the (node, chunk) counts, stable scatter).
+#include "kdtn_kernels.h"
+
+namespace kdtn {
+
+KD_INLINE bool sends_remote(uint4 r, uint32_t qerr) {
+    return (r.w & 0xFFu) == KDTN_KIND_CROSS_NODE && ((r.w >> 8) & 0xFFu) == 0 && qerr == 0;
+}
+// a link whose step fails aborts its batch (addLink's error chain; qdisc only where built)
+KD_INLINE bool add_fails(uint4 r, uint32_t qerr) {
+    const uint32_t kind = r.w & 0xFFu;
+    if ((r.w >> 8) & 0xFFu) return true;
+    return (kind == KDTN_KIND_SAME_NODE || kind == KDTN_KIND_CROSS_NODE || kind == KDTN_KIND_PHYSICAL) && qerr != 0;
+}
+KD_INLINE uint32_t qdisc_err(const uint2* q, uint32_t e) { return (q[(size_t)e * 9 + 8].y >> 16) & 0xFFu; }
+
+__global__ void __launch_bounds__(BLOCK) k_fan_mark(FanIn f, uint32_t* mark, uint8_t* send) {
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= f.T) return;
+    const uint32_t e0 = f.add_off[t], e1 = f.add_off[t + 1];
+    bool aborted = false;
+    for (uint32_t e = e0; e < e1; ++e) {
+        uint8_t s = 0;
+        if (!aborted) {
+            const uint4 r = f.add_res[e];
+            const uint32_t qe = qdisc_err(f.add_qdisc, e);
+            if (add_fails(r, qe)) aborted = true;
+            else if (sends_remote(r, qe)) {
+                s = 1;
+                mark[r.z] = f.stamp;
+            }
+        }
+        send[e] = s;
+    }
+}
+
+// marked node ids → dense node indices in id order (chunks of SCAN_CHUNK ids)
+__global__ void __launch_bounds__(BLOCK) k_fan_nodes_count(const uint32_t* mark, uint32_t nd, uint32_t stamp,
+                                                           uint64_t* part) {
+    __shared__ uint64_t sh[BLOCK / 64];
+    const uint32_t b0 = blockIdx.x * SCAN_CHUNK + threadIdx.x * 4;
+    uint64_t v = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v += (b0 + k < nd && mark[b0 + k] == stamp) ? 1u : 0u;
+    uint64_t tot;
+    block_exclusive(v, sh, &tot);
+    if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_fan_nodes_write(const uint32_t* mark, uint32_t nd, uint32_t stamp,
+                                                           const uint64_t* part, uint32_t* node_idx,
+                                                           uint32_t* nodes, uint32_t* n_nodes) {
+    __shared__ uint64_t sh[BLOCK / 64];
+    const uint32_t b0 = blockIdx.x * SCAN_CHUNK + threadIdx.x * 4;
+    bool m[4];
+    uint64_t v = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        m[k] = b0 + k < nd && mark[b0 + k] == stamp;
+        v += m[k] ? 1u : 0u;
+    }
+    uint64_t tot;
+    uint64_t x = part[blockIdx.x] + block_exclusive(v, sh, &tot);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (m[k]) {
+            node_idx[b0 + k] = (uint32_t)x;
+            nodes[x] = b0 + k;
+            ++x;
+        }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *n_nodes = (uint32_t)(part[blockIdx.x] + tot);
+}
+
+// (node, chunk) counts: one wave per chunk of FAN_CHUNK entries, LDS histogram
+__global__ void __launch_bounds__(64) k_fan_count(FanIn f, const uint8_t* send, const uint32_t* node_idx,
+                                                  const uint32_t* n_nodes, uint32_t* counts, uint32_t nchunks) {
+    __shared__ uint32_t h[FAN_NODE_CAP];
+    const uint32_t nn = *n_nodes;
+    if (nn > FAN_NODE_CAP) return;                          // reported by the host
+    for (uint32_t k = threadIdx.x; k < nn; k += 64) h[k] = 0;
+    __syncthreads();
+    const uint32_t c = blockIdx.x, e0 = c * FAN_CHUNK, e1 = min(e0 + FAN_CHUNK, f.n_add);
+    for (uint32_t e = e0 + threadIdx.x; e < e1; e += 64)
+        if (send[e]) atomicAdd(&h[node_idx[f.add_res[e].z]], 1u);
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < nn; k += 64) counts[(size_t)k * nchunks + c] = h[k];
+}
+
+// stable scatter: rounds of 64 entries in order; within a round, lanes with the same node
+// are ranked by lane (peeling one node per step); a running per-node counter in LDS
+// carries the order across rounds
+__global__ void __launch_bounds__(64) k_fan_scatter(FanIn f, const uint8_t* send, const uint32_t* node_idx,
+                                                    const uint32_t* n_nodes, const uint64_t* base, uint32_t nchunks,
+                                                    uint32_t* out_idx) {
+    __shared__ uint32_t run[FAN_NODE_CAP];
+    const uint32_t nn = *n_nodes;
+    if (nn > FAN_NODE_CAP) return;
+    const uint32_t c = blockIdx.x, e0 = c * FAN_CHUNK, e1 = min(e0 + FAN_CHUNK, f.n_add);
+    for (uint32_t k = threadIdx.x; k < nn; k += 64) run[k] = (uint32_t)base[(size_t)k * nchunks + c];
+    __syncthreads();
+    const int lane = threadIdx.x;
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    for (uint32_t r = e0; r < e1; r += 64) {
+        const uint32_t e = r + lane;
+        const bool on = e < e1 && send[e];
+        const uint32_t node = on ? node_idx[f.add_res[e].z] : 0u;
+        uint64_t pending = __ballot(on);
+        uint32_t pos = 0;
+        while (pending) {
+            const int leader = __ffsll((long long)pending) - 1;
+            const uint32_t ln = __shfl(node, leader, 64);
+            const uint64_t same = __ballot(on && node == ln) & pending;
+            const uint32_t b0 = run[ln];                    // uniform read
+            if ((same >> lane) & 1ull) pos = b0 + __popcll(same & lt);
+            __builtin_amdgcn_wave_barrier();
+            if (lane == leader) run[ln] = b0 + __popcll(same);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            pending &= ~same;
+        }
+        if (on) out_idx[pos] = e;
+    }
+}
+
+}  // namespace kdtn

@@ -48,7 +48,7 @@ enum : int {
     KB_NSETS = 3,
 };
 // special key-string ids found by k_kdict_flags (0xFFFFFFFF when absent)
-enum : int { SPECIAL_DEFAULT = 0, SPECIAL_LOCALHOST = 4, MISC_FIRST_PARTIAL = 8 };   // misc words
+enum : int { SPECIAL_DEFAULT = 0, SPECIAL_LOCALHOST = 4, MISC_FIRST_PARTIAL = 8, MISC_FAN_NODES = 12 };   // misc words
 // pod slot flag bits (in the g word of a wide slot; pod indices < 2^30)
 constexpr uint32_t POD_SPEC_NIL = 0x80000000u, POD_PHYSICAL = 0x40000000u, POD_INDEX = 0x3FFFFFFFu;
 
@@ -217,6 +217,44 @@ struct WireWork {
     uint32_t* err;                  // [T] bit l: list l failed to marshal
     const uint64_t* off;            // [3T+1] batch byte offsets
 };
+// ---- RemotePod fan-out grouping (kdtn_fanout.hip) ---------------------------------------
+constexpr int FAN_CHUNK = 4096;        // add entries per single-wave workgroup
+constexpr int FAN_NODE_CAP = 8192;     // destination daemons per epoch (LDS histogram)
+struct FanIn {
+    const uint32_t* add_off;
+    const uint4* add_res;
+    const uint2* add_qdisc;
+    uint32_t T, n_add, stamp;
+};
+__global__ void k_fan_mark(FanIn f, uint32_t* mark, uint8_t* send);
+__global__ void k_fan_nodes_count(const uint32_t* mark, uint32_t nd, uint32_t stamp, uint64_t* part);
+__global__ void k_fan_nodes_write(const uint32_t* mark, uint32_t nd, uint32_t stamp, const uint64_t* part,
+                                  uint32_t* node_idx, uint32_t* nodes, uint32_t* n_nodes);
+__global__ void k_fan_count(FanIn f, const uint8_t* send, const uint32_t* node_idx, const uint32_t* n_nodes,
+                            uint32_t* counts, uint32_t nchunks);
+__global__ void k_fan_scatter(FanIn f, const uint8_t* send, const uint32_t* node_idx, const uint32_t* n_nodes,
+                              const uint64_t* base, uint32_t nchunks, uint32_t* out_idx);
+KD_INLINE uint64_t block_exclusive(uint64_t v, uint64_t* sh, uint64_t* total) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint64_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t o = __shfl_up(x, d, 64);
+        if (lane >= d) x += o;
+    }
+    if (lane == 63) sh[wave] = x;
+    __syncthreads();
+    uint64_t base = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < BLOCK / 64; ++k) {
+        if (k < wave) base += sh[k];
+        tot += sh[k];
+    }
+    __syncthreads();
+    *total = tot;
+    return base + x - v;
+}
+
 __global__ void k_utf8_bits(const uint8_t* bytes, const uint32_t* offs, uint32_t n, uint32_t* bits);
 __global__ void k_wire_entry_sizes(WireIn w, DevLinks O, DevLinks N, WireWork wk);
 __global__ void k_wire_sizes(WireIn w, DevLinks O, DevLinks N, WireWork wk);

@@ -157,27 +157,6 @@ __global__ void __launch_bounds__(BLOCK) k_wire_sizes(WireIn w, DevLinks O, DevL
 }
 
 // ---- exclusive scan of the 3T batch sizes into u64 offsets -----------------------------
-KD_INLINE uint64_t block_exclusive(uint64_t v, uint64_t* sh, uint64_t* total) {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    uint64_t x = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint64_t o = __shfl_up(x, d, 64);
-        if (lane >= d) x += o;
-    }
-    if (lane == 63) sh[wave] = x;
-    __syncthreads();
-    uint64_t base = 0, tot = 0;
-#pragma unroll
-    for (int k = 0; k < BLOCK / 64; ++k) {
-        if (k < wave) base += sh[k];
-        tot += sh[k];
-    }
-    __syncthreads();
-    *total = tot;
-    return base + x - v;
-}
-
 __global__ void __launch_bounds__(BLOCK) k_scan_partial(const uint32_t* size, uint32_t n, uint64_t* part) {
     __shared__ uint64_t sh[BLOCK / 64];
     const uint32_t b0 = blockIdx.x * SCAN_CHUNK + threadIdx.x * 4;

@@ -70,6 +70,7 @@ def lib() -> C.CDLL:
                                    C.c_uint32, C.POINTER(abi.LinkTable), C.c_int, C.POINTER(abi.VniTable),
                                    vp, vp]),
         "kdtn_host_alloc": (vp, [C.c_uint64]),
+        "kdtn_epoch_fanout": (C.c_int, [vp, C.POINTER(abi.Fanout)]),
         "kdtn_host_free": (None, [vp]),
         "kdtn_epoch_download_wire": (C.c_int, [vp, C.POINTER(abi.Wire)]),
     }
@@ -213,6 +214,21 @@ class Engine:
         w.bytes, w.cap, w.off, w.err = arena.ctypes.data, arena.size, off.ctypes.data, err.ctypes.data
         _check(lib().kdtn_epoch_download_wire(self._ctx, C.byref(w)), "kdtn_epoch_download_wire")
         return arena[:n], off, err[:self._T]
+
+    def fanout(self):
+        """RemotePod RPCs of the last epoch grouped per destination daemon:
+        (node kdict ids, off[n_nodes+1], add-entry indices)."""
+        f = abi.Fanout()
+        rc = lib().kdtn_epoch_fanout(self._ctx, C.byref(f))          # sizes (no buffers yet)
+        if rc not in (abi.OK, abi.ENOSPC):
+            _check(rc, "kdtn_epoch_fanout")
+        node = np.zeros(max(f.n_nodes, 1), np.uint32)
+        off = np.zeros(f.n_nodes + 1, np.uint32)
+        idx = np.zeros(max(f.n_send, 1), np.uint32)
+        f.node, f.off, f.idx = node.ctypes.data, off.ctypes.data, idx.ctypes.data
+        f.node_cap, f.idx_cap = node.size, idx.size
+        _check(lib().kdtn_epoch_fanout(self._ctx, C.byref(f)), "kdtn_epoch_fanout")
+        return node[:f.n_nodes], off, idx[:f.n_send]
 
     def kernel_times(self) -> dict[str, float]:
         names = (C.c_char_p * 16)()

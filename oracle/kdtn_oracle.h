@@ -75,6 +75,12 @@ int64_t  or_encode_batch(const kdtn_epoch_in* in, uint32_t t, int list, const ui
 uint64_t or_encode_epoch(const kdtn_epoch_in* in, const kdtn_batches* b, uint32_t T,
                          uint8_t* bytes, uint64_t* off, uint8_t* err);
 
+/* RemotePod fan-out of an epoch's AddLinks outputs (needs add_res / add_qdisc): daemons
+ * node[0..n_nodes) ascending, entries idx[off[k]..off[k+1]) in add-list order. Capacities:
+ * node/off/idx >= n_add (+1 for off). Returns the number of senders. */
+uint32_t or_fanout(const kdtn_batches* b, uint32_t T, uint32_t* node, uint32_t* off, uint32_t* idx,
+                   uint32_t* n_nodes);
+
 #ifdef __cplusplus
 }
 #endif

@@ -19,6 +19,7 @@
  */
 #include "kdtn_oracle.h"
 
+#include <stdlib.h>
 #include <string.h>
 
 typedef struct { const uint8_t* p; uint32_t n; } wstr;
@@ -193,4 +194,52 @@ uint64_t or_encode_epoch(const kdtn_epoch_in* in, const kdtn_batches* b, uint32_
     }
     off[3ull * T] = pos;
     return pos;
+}
+
+/* ======================================================================================
+ * RemotePod fan-out (daemon/kubedtn/handler.go:419-453, 601-607; common/utils.go:39-67):
+ * the AddLinks entries that reach UpdateRemote, grouped by destination daemon
+ * (vtep = kdict id of the peer's status.src_ip), daemons in ascending id order, entries
+ * in add-list order.
+ * ==================================================================================== */
+static int fan_fails(const kdtn_resolved* r, const kdtn_qdisc* q) {
+    if (r->err) return 1;
+    return (r->kind == KDTN_KIND_SAME_NODE || r->kind == KDTN_KIND_CROSS_NODE ||
+            r->kind == KDTN_KIND_PHYSICAL) && q->err;
+}
+
+static int cmp_u64(const void* a, const void* b) {
+    uint64_t x = *(const uint64_t*)a, y = *(const uint64_t*)b;
+    return x < y ? -1 : x > y;
+}
+
+uint32_t or_fanout(const kdtn_batches* b, uint32_t T, uint32_t* node, uint32_t* off, uint32_t* idx,
+                   uint32_t* n_nodes) {
+    /* senders as (vtep << 32 | entry), sorted: stable by entry within a vtep */
+    uint32_t na = b->add_off[T];
+    uint64_t* keys = (uint64_t*)malloc(sizeof(uint64_t) * (na ? na : 1));
+    uint32_t ns = 0;
+    for (uint32_t t = 0; t < T; t++) {
+        for (uint32_t e = b->add_off[t]; e < b->add_off[t + 1]; e++) {
+            const kdtn_resolved* r = &b->add_res[e];
+            const kdtn_qdisc* q = &b->add_qdisc[e];
+            if (fan_fails(r, q)) break;                       /* the batch aborts here */
+            if (r->kind == KDTN_KIND_CROSS_NODE) keys[ns++] = ((uint64_t)r->vtep << 32) | e;
+        }
+    }
+    qsort(keys, ns, sizeof(uint64_t), cmp_u64);
+    uint32_t nn = 0;
+    for (uint32_t k = 0; k < ns; k++) {
+        uint32_t v = (uint32_t)(keys[k] >> 32);
+        if (k == 0 || v != (uint32_t)(keys[k - 1] >> 32)) {
+            node[nn] = v;
+            off[nn] = k;
+            nn++;
+        }
+        idx[k] = (uint32_t)keys[k];
+    }
+    off[nn] = ns;
+    *n_nodes = nn;
+    free(keys);
+    return ns;
 }

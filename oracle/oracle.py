@@ -200,3 +200,21 @@ def encode_epoch(inp: EpochInput, out: BatchesOut):
     arena = np.zeros(max(int(n), 1), np.uint8)
     L.or_encode_epoch(C.byref(cin), C.byref(b), T, arena.ctypes.data, off.ctypes.data, err.ctypes.data)
     return arena[:int(n)], off, err[:T]
+
+
+def fanout(out: BatchesOut, T: int):
+    """RemotePod fan-out per destination daemon: (node ids, off, entry idx)."""
+    L = _wire_lib()
+    if not getattr(L, "_fan_bound", False):
+        L.or_fanout.argtypes = [C.POINTER(abi.Batches), C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                C.POINTER(C.c_uint32)]
+        L.or_fanout.restype = C.c_uint32
+        L._fan_bound = True
+    b = out.to_c((max(len(out.del_idx), 1), max(len(out.add_idx), 1), max(len(out.upd_idx), 1)))
+    n = max(len(out.add_idx), 1)
+    node = np.zeros(n, np.uint32)
+    off = np.zeros(n + 1, np.uint32)
+    idx = np.zeros(n, np.uint32)
+    nn = C.c_uint32()
+    ns = L.or_fanout(C.byref(b), T, node.ctypes.data, off.ctypes.data, idx.ctypes.data, C.byref(nn))
+    return node[:nn.value], off[:nn.value + 1], idx[:ns]

@@ -391,3 +391,26 @@ def test_pod_names_shared_across_namespaces(engine):
     inp2 = pack(topos[5:])
     assert_same(engine.reconcile(inp2), O.reconcile(inp2, tick=TICK), "second epoch")
     assert_same(engine.reconcile(inp), O.reconcile(inp, tick=TICK), "third epoch")
+
+
+def _fanout_same(engine, inp, ctx):
+    out = engine.reconcile(inp)
+    node, off, idx = engine.fanout()
+    wn, wo, wi = O.fanout(O.reconcile(inp, tick=TICK), inp.topos.n)
+    assert np.array_equal(node, wn) and np.array_equal(off, wo) and np.array_equal(idx, wi), ctx
+    # every grouped entry is a CROSS_NODE add whose daemon is its peer's src_ip
+    for k in range(len(node)):
+        sel = idx[off[k]:off[k + 1]]
+        assert (out.add_res["vtep"][sel] == node[k]).all()
+        assert (out.add_res["kind"][sel] == abi.KIND_CROSS_NODE).all()
+    return len(idx)
+
+
+def test_remote_fanout_grouping(engine):
+    """RemotePod RPCs grouped per destination daemon (with the batch-abort rule) equal the
+    oracle's grouping on random epochs and the synthetic configs."""
+    for seed in (1, 2, 3):
+        topos, inp = random_epoch_input(seed, T=150, p_err=0.2)
+        _fanout_same(engine, inp, f"seed {seed}")
+    assert _fanout_same(engine, synth.make(2, pods_per_shard=20000), "config 2") > 100000
+    assert _fanout_same(engine, synth.make(4, pods_per_shard=5000), "config 4") > 1000
