@@ -25,6 +25,7 @@
  *   kdtn_epoch_encode     replaces Link.ToProto + proto.Marshal of the batches
  *   kdtn_epoch_fanout     groups the daemons' UpdateRemote RPCs (common/utils.go:39-67)
  *                         per destination daemon
+ *   kdtn_epoch_tc         synthesises SetVethQdiscs' `tc ... tbf` argv (common/qdisc.go:252-266)
  *
  * Conventions
  *   - No C++ or HIP types cross this ABI: plain pointers, sizes and PODs.
@@ -352,6 +353,23 @@ typedef struct kdtn_fanout {
     uint32_t  n_nodes, n_send;   /* out                                               */
 } kdtn_fanout;
 int kdtn_epoch_fanout(kdtn_ctx* ctx, kdtn_fanout* out);
+
+/* ---- tc argv of the TBF qdiscs -------------------------------------------------------- */
+/* SetVethQdiscs (common/qdisc.go:252-266) applies the TBF by exec'ing
+ *   tc qdisc add dev <LinkName> parent 1:1 handle 10:0 tbf rate <Rate> burst <Buffer>
+ *      latency 50ms minburst <Minburst>
+ * For every AddLinks / UpdateLinks entry whose MakeQdiscs produced a TBF (and whose
+ * plan has no error) this writes that argv (arguments NUL-terminated, without the
+ * leading "tc") for the entry's local interface (link.LocalIntf). Entries: add list, then
+ * update list; entry g = bytes[off[g], off[g+1]), empty = no tc command. */
+typedef struct kdtn_tc_argv {
+    uint8_t*  bytes;
+    uint64_t  cap;
+    uint64_t* off;           /* [n_add + n_upd + 1]                                    */
+    uint64_t  n_bytes;       /* out                                                    */
+} kdtn_tc_argv;
+int kdtn_epoch_tc(kdtn_ctx* ctx, uint64_t* n_bytes);   /* after run(QDISC|RESOLVE) + sync */
+int kdtn_epoch_download_tc(kdtn_ctx* ctx, kdtn_tc_argv* out);
 
 /* ---- multi-GPU (one process per GPU): RCCL all-gather of the pod-status table ------ */
 int kdtn_comm_unique_id(uint8_t out[128]);

@@ -88,6 +88,11 @@ struct kdtn_ctx {
     // RemotePod fan-out
     DevBuf f_mark, f_send, f_node_idx, f_nodes, f_counts, f_base, f_part, f_idx;
     uint32_t f_stamp = 0;
+    // tc argv
+    DevBuf tc_size, tc_off, tc_part, tc_arena;
+    uint64_t tc_bytes = 0;
+    uint32_t tc_n = 0;
+    bool tc_done = false;
     // host-visible counters
     uint32_t* h_misc = nullptr;   // pinned: [0]=default id, [1]=del, [2]=upd, [3]=add, [4]=look-back error
     bool uploaded = false;
@@ -359,7 +364,7 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->add_qdisc, &c->upd_qdisc, &c->kd_utf8, &c->pd_utf8, &c->w_rel,
                       &c->w_topo, &c->w_size, &c->w_err, &c->w_off, &c->w_part, &c->w_arena,
                       &c->f_mark, &c->f_send, &c->f_node_idx, &c->f_nodes, &c->f_counts, &c->f_base,
-                      &c->f_part, &c->f_idx};
+                      &c->f_part, &c->f_idx, &c->tc_size, &c->tc_off, &c->tc_part, &c->tc_arena};
     for (DevBuf* b : bufs) release(*b);
     for (int i = 0; i <= kMaxTimers; ++i)
         if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
@@ -636,6 +641,7 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
     HIP_TRY(hipMemcpyAsync(c->h_misc + 4, dp<uint32_t>(c->sync) + 1, 4, hipMemcpyDeviceToHost, s));
     c->ran = true;
     c->encoded = false;
+    c->tc_done = false;
     return KDTN_OK;
 }
 
@@ -977,6 +983,59 @@ int kdtn_epoch_fanout(kdtn_ctx* c, kdtn_fanout* o) {
         o->off[nn] = nsend;
     }
     HIP_TRY(hipStreamSynchronize(s));
+    return KDTN_OK;
+}
+
+int kdtn_epoch_tc(kdtn_ctx* c, uint64_t* n_bytes) {
+    if (!c || !c->ran) return KDTN_EINVAL;
+    if ((c->last_stages & (KDTN_STAGE_RESOLVE | KDTN_STAGE_QDISC)) != (KDTN_STAGE_RESOLVE | KDTN_STAGE_QDISC))
+        return KDTN_EINVAL;
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    hipStream_t s = c->stream;
+    const uint32_t nu = c->h_misc[2], na = c->h_misc[3];
+    const uint64_t n = (uint64_t)na + nu;
+    const uint32_t nb = nblocks(n + 1, SCAN_CHUNK);
+    TRY(ensure(c->tc_size, (size_t)n * 4 + 16));
+    TRY(ensure(c->tc_off, ((size_t)n + 1) * 8));
+    TRY(ensure(c->tc_part, (size_t)nb * 8 + 16));
+    TcIn w{c->des.view, dp<uint32_t>(c->add_idx), dp<uint32_t>(c->upd_idx), dp<uint4>(c->add_res),
+           dp<uint4>(c->upd_res), dp<uint2>(c->add_qdisc), dp<uint2>(c->upd_qdisc), dp<uint8_t>(c->kd_bytes),
+           dp<uint32_t>(c->kd_offs), na, nu};
+    c->n_ev = 0;
+    (void)hipEventRecord(c->ev[0], s);
+    if (n) k_tc_sizes<<<nblocks(n), BLOCK, 0, s>>>(w, dp<uint32_t>(c->tc_size));
+    k_scan_partial<<<nb, BLOCK, 0, s>>>(dp<uint32_t>(c->tc_size), (uint32_t)n, dp<uint64_t>(c->tc_part));
+    k_scan_top<<<1, BLOCK, 0, s>>>(dp<uint64_t>(c->tc_part), nb);
+    k_scan_final<<<nb, BLOCK, 0, s>>>(dp<uint32_t>(c->tc_size), (uint32_t)n, dp<uint64_t>(c->tc_part),
+                                      dp<uint64_t>(c->tc_off));
+    timer_mark(c, "tc_sizes");
+    HIP_TRY(hipGetLastError());
+    uint64_t total = 0;
+    HIP_TRY(hipMemcpyAsync(&total, dp<uint64_t>(c->tc_off) + n, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    TRY(ensure(c->tc_arena, (size_t)total + 16));
+    timer_mark(c, "tc_host_sync");
+    if (n) k_tc_write<<<nblocks(n), BLOCK, 0, s>>>(w, dp<uint64_t>(c->tc_off), dp<uint8_t>(c->tc_arena));
+    timer_mark(c, "tc_write");
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(s));
+    c->tc_bytes = total;
+    c->tc_n = (uint32_t)n;
+    c->tc_done = true;
+    if (n_bytes) *n_bytes = total;
+    return KDTN_OK;
+}
+
+int kdtn_epoch_download_tc(kdtn_ctx* c, kdtn_tc_argv* o) {
+    if (!c || !o || !c->tc_done) return KDTN_EINVAL;
+    HIP_TRY(hipSetDevice(c->device));
+    o->n_bytes = c->tc_bytes;
+    if (o->bytes && c->tc_bytes > o->cap) return KDTN_ENOSPC;
+    if (o->bytes && c->tc_bytes)
+        HIP_TRY(hipMemcpyAsync(o->bytes, c->tc_arena.p, c->tc_bytes, hipMemcpyDeviceToHost, c->stream));
+    if (o->off) HIP_TRY(hipMemcpyAsync(o->off, c->tc_off.p, ((size_t)c->tc_n + 1) * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
     return KDTN_OK;
 }
 

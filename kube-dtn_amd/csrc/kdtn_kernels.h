@@ -217,6 +217,22 @@ struct WireWork {
     uint32_t* err;                  // [T] bit l: list l failed to marshal
     const uint64_t* off;            // [3T+1] batch byte offsets
 };
+// ---- tc argv synthesis (kdtn_tc.hip) ---------------------------------------------------
+struct TcIn {
+    DevLinks N;
+    const uint32_t* add_idx;
+    const uint32_t* upd_idx;
+    const uint4* add_res;
+    const uint4* upd_res;
+    const uint2* add_qdisc;
+    const uint2* upd_qdisc;
+    const uint8_t* kd_bytes;
+    const uint32_t* kd_offs;
+    uint32_t n_add, n_upd;
+};
+__global__ void k_tc_sizes(TcIn w, uint32_t* size);
+__global__ void k_tc_write(TcIn w, const uint64_t* off, uint8_t* arena);
+
 // ---- RemotePod fan-out grouping (kdtn_fanout.hip) ---------------------------------------
 constexpr int FAN_CHUNK = 4096;        // add entries per single-wave workgroup
 constexpr int FAN_NODE_CAP = 8192;     // destination daemons per epoch (LDS histogram)

@@ -1,0 +1,107 @@
+// kdtn_tc.hip — `tc` argv synthesis for the TBF qdiscs.
+//
+// SetVethQdiscs (common/qdisc.go:201-290) adds netem over netlink and the TBF with
+//   exec("tc", "qdisc", "add", "dev", <veth LinkName>, "parent", "1:1", "handle", "10:0",
+//        "tbf", "rate", fmt.Sprint(Rate), "burst", fmt.Sprint(Buffer), "latency", "50ms",
+//        "minburst", fmt.Sprint(Minburst))                                   (:252-266)
+// ("parent 1:1 handle 10:0" because MakeQdiscs always puts the netem first). For every
+// AddLinks / UpdateLinks entry whose MakeQdiscs produced a TBF and no error, this stage
+// writes that argv (NUL-terminated arguments) for the entry's local interface
+// (link.LocalIntf: the veth of UpdateLinks (handler.go:649-658), the local end of a
+// same-node veth pair or VXLAN interface). Layout: add entries then update entries;
+// entry g's argv = bytes[off[g], off[g+1]) (empty when it runs no tc command).
+#include "kdtn_kernels.h"
+
+namespace kdtn {
+
+KD_INLINE uint32_t ndigits(uint64_t v) {
+    uint32_t n = 1;
+    while (v >= 10u) { v /= 10u; ++n; }
+    return n;
+}
+// fixed argument bytes: "qdisc add dev " + " parent 1:1 handle 10:0 tbf rate " + " burst " +
+// " latency 50ms minburst " + final NUL (every separator is a NUL)
+constexpr uint32_t TC_FIXED = 14 + 1 + 32 + 1 + 6 + 1 + 22 + 1;
+
+struct TcEntry {
+    uint32_t intf;      // kdict id of LocalIntf
+    uint64_t rate;
+    uint32_t buffer, minburst;
+    bool on;
+};
+
+KD_INLINE TcEntry tc_entry(const TcIn& w, uint32_t g) {
+    TcEntry t{0, 0, 0, 0, false};
+    const bool upd = g >= w.n_add;
+    const uint32_t e = upd ? g - w.n_add : g;
+    const uint2* q = (upd ? w.upd_qdisc : w.add_qdisc) + (size_t)e * 9;
+    const uint4 r = (upd ? w.upd_res : w.add_res)[e];
+    const uint32_t flags = q[8].y;                         // has_netem | has_tbf<<8 | err<<16
+    if (((flags >> 8) & 0xFFu) == 0 || ((flags >> 16) & 0xFFu) != 0 || ((r.w >> 8) & 0xFFu) != 0) return t;
+    if (!upd) {                        // addLink sets qdiscs only on veth / VXLAN interfaces
+        const uint32_t kind = r.w & 0xFFu;
+        if (kind != KDTN_KIND_SAME_NODE && kind != KDTN_KIND_CROSS_NODE && kind != KDTN_KIND_PHYSICAL) return t;
+    }
+    const uint32_t j = (upd ? w.upd_idx : w.add_idx)[e];
+    t.intf = w.N.key(KDTN_K_LOCAL_INTF, j);
+    t.buffer = q[6].y;                                     // kdtn_qdisc word 13
+    t.rate = ((uint64_t)q[7].y << 32) | q[7].x;            // words 14, 15
+    t.minburst = q[8].x;                                   // word 16
+    t.on = true;
+    return t;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_tc_sizes(TcIn w, uint32_t* size) {
+    const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
+    if (g >= w.n_add + w.n_upd) return;
+    const TcEntry t = tc_entry(w, g);
+    size[g] = t.on ? TC_FIXED + (w.kd_offs[t.intf + 1] - w.kd_offs[t.intf]) + ndigits(t.rate) +
+                         ndigits(t.buffer) + ndigits(t.minburst)
+                   : 0u;
+}
+
+struct Out {
+    uint8_t* p;
+    KD_INLINE void lit(const char* s) {
+        while (*s) *p++ = (uint8_t)*s++;
+        *p++ = 0;
+    }
+    KD_INLINE void num(uint64_t v) {
+        const uint32_t n = ndigits(v);
+        for (uint32_t k = n; k-- > 0;) {
+            p[k] = (uint8_t)('0' + v % 10u);
+            v /= 10u;
+        }
+        p += n;
+        *p++ = 0;
+    }
+};
+
+__global__ void __launch_bounds__(BLOCK) k_tc_write(TcIn w, const uint64_t* off, uint8_t* arena) {
+    const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
+    if (g >= w.n_add + w.n_upd) return;
+    const TcEntry t = tc_entry(w, g);
+    if (!t.on) return;
+    Out o{arena + off[g]};
+    o.lit("qdisc");
+    o.lit("add");
+    o.lit("dev");
+    const uint32_t b = w.kd_offs[t.intf], len = w.kd_offs[t.intf + 1] - b;
+    for (uint32_t k = 0; k < len; ++k) *o.p++ = w.kd_bytes[b + k];
+    *o.p++ = 0;
+    o.lit("parent");
+    o.lit("1:1");
+    o.lit("handle");
+    o.lit("10:0");
+    o.lit("tbf");
+    o.lit("rate");
+    o.num(t.rate);
+    o.lit("burst");
+    o.num(t.buffer);
+    o.lit("latency");
+    o.lit("50ms");
+    o.lit("minburst");
+    o.num(t.minburst);
+}
+
+}  // namespace kdtn

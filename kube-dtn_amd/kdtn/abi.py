@@ -114,6 +114,10 @@ class Fanout(C.Structure):
                 ("idx_cap", C.c_uint32), ("n_nodes", C.c_uint32), ("n_send", C.c_uint32)]
 
 
+class TcArgv(C.Structure):
+    _fields_ = [("bytes", C.c_void_p), ("cap", C.c_uint64), ("off", C.c_void_p), ("n_bytes", C.c_uint64)]
+
+
 class PodTable(C.Structure):
     _fields_ = [("n", C.c_uint32), ("ns", u32p), ("name", u32p), ("src_ip", u32p), ("net_ns", u32p),
                 ("flags", u8p)]
@@ -145,7 +149,7 @@ EXPORTS = ["kdtn_version", "kdtn_strerror", "kdtn_err_name", "kdtn_init", "kdtn_
            "kdtn_epoch_download", "kdtn_make_qdiscs", "kdtn_comm_unique_id", "kdtn_comm_init",
            "kdtn_last_kernel_times", "kdtn_debug_wg_trace", "kdtn_epoch_encode",
            "kdtn_epoch_download_wire", "kdtn_diff", "kdtn_resolve", "kdtn_host_alloc",
-           "kdtn_host_free", "kdtn_epoch_fanout"]
+           "kdtn_host_free", "kdtn_epoch_fanout", "kdtn_epoch_tc", "kdtn_epoch_download_tc"]
 
 
 def ptr(a: np.ndarray, t):

@@ -71,6 +71,8 @@ def lib() -> C.CDLL:
                                    vp, vp]),
         "kdtn_host_alloc": (vp, [C.c_uint64]),
         "kdtn_epoch_fanout": (C.c_int, [vp, C.POINTER(abi.Fanout)]),
+        "kdtn_epoch_tc": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
+        "kdtn_epoch_download_tc": (C.c_int, [vp, C.POINTER(abi.TcArgv)]),
         "kdtn_host_free": (None, [vp]),
         "kdtn_epoch_download_wire": (C.c_int, [vp, C.POINTER(abi.Wire)]),
     }
@@ -214,6 +216,17 @@ class Engine:
         w.bytes, w.cap, w.off, w.err = arena.ctypes.data, arena.size, off.ctypes.data, err.ctypes.data
         _check(lib().kdtn_epoch_download_wire(self._ctx, C.byref(w)), "kdtn_epoch_download_wire")
         return arena[:n], off, err[:self._T]
+
+    def tc_argv(self, n_entries: int):
+        """SetVethQdiscs' `tc ... tbf` argv per add-then-update entry of the last epoch:
+        (arena uint8 of NUL-terminated arguments, off uint64[n_entries + 1])."""
+        n = C.c_uint64()
+        _check(lib().kdtn_epoch_tc(self._ctx, C.byref(n)), "kdtn_epoch_tc")
+        arena = np.zeros(max(int(n.value), 1), np.uint8)
+        off = np.zeros(n_entries + 1, np.uint64)
+        t = abi.TcArgv(arena.ctypes.data, arena.size, off.ctypes.data, 0)
+        _check(lib().kdtn_epoch_download_tc(self._ctx, C.byref(t)), "kdtn_epoch_download_tc")
+        return arena[:int(n.value)], off
 
     def fanout(self):
         """RemotePod RPCs of the last epoch grouped per destination daemon:

@@ -81,6 +81,10 @@ uint64_t or_encode_epoch(const kdtn_epoch_in* in, const kdtn_batches* b, uint32_
 uint32_t or_fanout(const kdtn_batches* b, uint32_t T, uint32_t* node, uint32_t* off, uint32_t* idx,
                    uint32_t* n_nodes);
 
+/* SetVethQdiscs' tc argv per add (veth/VXLAN kinds) then update entry with a TBF and no
+ * error (common/qdisc.go:252-266); off has n_add + n_upd + 1 entries. */
+uint64_t or_tc_epoch(const kdtn_epoch_in* in, const kdtn_batches* b, uint8_t* bytes, uint64_t* off);
+
 #ifdef __cplusplus
 }
 #endif

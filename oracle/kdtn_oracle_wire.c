@@ -19,6 +19,7 @@
  */
 #include "kdtn_oracle.h"
 
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -242,4 +243,47 @@ uint32_t or_fanout(const kdtn_batches* b, uint32_t T, uint32_t* node, uint32_t* 
     *n_nodes = nn;
     free(keys);
     return ns;
+}
+
+/* ======================================================================================
+ * tc argv of SetVethQdiscs' TBF (common/qdisc.go:252-266): "qdisc add dev <intf> parent
+ * 1:1 handle 10:0 tbf rate <Rate> burst <Buffer> latency 50ms minburst <Minburst>", each
+ * argument NUL-terminated, for every add entry that reaches SetVethQdiscs (veth / VXLAN
+ * kinds) and every update entry, with a TBF and no error. Add entries then update entries.
+ * ==================================================================================== */
+static uint64_t tc_one(const kdtn_epoch_in* in, uint32_t j, const kdtn_qdisc* q, uint8_t* out) {
+    char tmp[256];
+    wstr intf = wget(&in->kdict, in->desired.key[KDTN_K_LOCAL_INTF][j]);
+    int n1 = snprintf(tmp, sizeof tmp, "qdisc%cadd%cdev%c", 0, 0, 0);
+    uint64_t pos = 0;
+    if (out) memcpy(out, tmp, (size_t)n1);
+    pos += (uint64_t)n1;
+    if (out) memcpy(out + pos, intf.p, intf.n);
+    pos += intf.n;
+    int n2 = snprintf(tmp, sizeof tmp, "%cparent%c1:1%chandle%c10:0%ctbf%crate%c%llu%cburst%c%u%clatency%c50ms%cminburst%c%u%c",
+                      0, 0, 0, 0, 0, 0, 0, (unsigned long long)q->tbf_rate, 0, 0, q->tbf_buffer, 0, 0, 0, 0,
+                      q->tbf_minburst, 0);
+    if (out) memcpy(out + pos, tmp, (size_t)n2);
+    return pos + (uint64_t)n2;
+}
+
+uint64_t or_tc_epoch(const kdtn_epoch_in* in, const kdtn_batches* b, uint8_t* bytes, uint64_t* off) {
+    uint64_t pos = 0;
+    uint32_t g = 0;
+    for (int upd = 0; upd < 2; upd++) {
+        uint32_t n = upd ? b->n_upd : b->n_add;
+        for (uint32_t e = 0; e < n; e++, g++) {
+            off[g] = pos;
+            const kdtn_resolved* r = upd ? &b->upd_res[e] : &b->add_res[e];
+            const kdtn_qdisc* q = upd ? &b->upd_qdisc[e] : &b->add_qdisc[e];
+            if (!q->has_tbf || q->err || r->err) continue;
+            if (!upd && r->kind != KDTN_KIND_SAME_NODE && r->kind != KDTN_KIND_CROSS_NODE &&
+                r->kind != KDTN_KIND_PHYSICAL)
+                continue;
+            uint32_t j = upd ? b->upd_idx[e] : b->add_idx[e];
+            pos += tc_one(in, j, q, bytes ? bytes + pos : NULL);
+        }
+    }
+    off[g] = pos;
+    return pos;
 }

@@ -414,3 +414,16 @@ def test_remote_fanout_grouping(engine):
         _fanout_same(engine, inp, f"seed {seed}")
     assert _fanout_same(engine, synth.make(2, pods_per_shard=20000), "config 2") > 100000
     assert _fanout_same(engine, synth.make(4, pods_per_shard=5000), "config 4") > 1000
+
+
+def test_tc_argv_synthesis(engine):
+    """`tc qdisc add ... tbf` argv per AddLinks / UpdateLinks entry (common/qdisc.go:252-266)
+    equals the oracle's on random epochs and the synthetic configs."""
+    cases = [random_epoch_input(s, T=150)[1] for s in (5, 6)]
+    cases += [synth.make(1), synth.make(2, pods_per_shard=20000), synth.make(3, pods_per_shard=20000)]
+    for k, inp in enumerate(cases):
+        out = engine.reconcile(inp)
+        arena, off = engine.tc_argv(len(out.add_idx) + len(out.upd_idx))
+        wa, wo = O.tc_epoch(inp, O.reconcile(inp, tick=TICK))
+        assert np.array_equal(off, wo), k
+        assert arena.tobytes() == wa.tobytes(), k

@@ -58,3 +58,21 @@ def test_utf8_validity_edges():
            b"\xf5\x80\x80\x80", b"\xe2\x82", b"a\xff"]
     assert all(O.utf8_valid(s) for s in ok)
     assert not any(O.utf8_valid(s) for s in bad)
+
+
+def test_tc_argv_known_answer(golden):
+    """SetVethQdiscs' TBF command (common/qdisc.go:252-266) for the bandwidth sample
+    (config/samples/tc/bandwidth.yaml: rate "1Gbit" → Rate 1e9, getTbfBurst 4e6)."""
+    tr = next(t for t in golden["transitions"] if t["name"] == "S1->S2")
+    topos = golden_epoch(golden, tr)
+    inp = pack(topos)
+    out = O.reconcile(inp)
+    arena, off = O.tc_epoch(inp, out)
+    cmds = [arena[int(off[i]):int(off[i + 1])].tobytes() for i in range(len(off) - 1)]
+    cmds = [c.split(b"\0")[:-1] for c in cmds if c]
+    assert cmds, "the bandwidth transition updates links with a TBF"
+    by_rate = {c[10]: c for c in cmds}
+    want = [b"qdisc", b"add", b"dev", cmds[0][3], b"parent", b"1:1", b"handle", b"10:0", b"tbf", b"rate",
+            b"1000000000", b"burst", b"4000000", b"latency", b"50ms", b"minburst", b"1500"]
+    assert by_rate[b"1000000000"][:3] == want[:3] and by_rate[b"1000000000"][4:] == want[4:]
+    assert all(len(c) == 17 for c in cmds)
