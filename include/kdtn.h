@@ -371,6 +371,67 @@ typedef struct kdtn_tc_argv {
 int kdtn_epoch_tc(kdtn_ctx* ctx, uint64_t* n_bytes);   /* after run(QDISC|RESOLVE) + sync */
 int kdtn_epoch_download_tc(kdtn_ctx* ctx, kdtn_tc_argv* out);
 
+/* ---- CR ingest: TopologyList JSON → device-resident epoch tables ---------------------- */
+/* The step before the diff: the controller's informer lists the
+ * Topology CRs as a Kubernetes `TopologyList` JSON document and decodes it with
+ * sigs.k8s.io/json (apimachinery v0.24, case-sensitive keys) into the typed structs of
+ * api/v1/topology_types.go:28-56,59-95,119-176. kdtn_json_ingest performs that decode on
+ * the GPU and leaves the result where kdtn_epoch_upload would: interned dictionaries
+ * (ids in first-occurrence document order, id 0 = ""), the topology table (items order;
+ * metadata.namespace/name, status.src_ip/net_ns, KDTN_TOPO_*_NIL when a links list is
+ * absent or null) and both link stores (spec.links = desired, status.links = realised),
+ * so kdtn_epoch_run follows with no host SoA build or table upload.
+ * Decoding follows Go's encoding/json: full syntax validation first (checkValid,
+ * nesting ≤ 10000), string escapes and \u surrogate pairs, invalid UTF-8 coerced to
+ * U+FFFD, null leaves a field unchanged (a links list nil), null array elements decode
+ * to zero values, uid via ParseInt(·,10,64), gap via ParseUint into uint32, unknown
+ * fields skipped. Documented deviations: a schema field repeated inside one object
+ * (Go: last wins) is reported as KDTN_JSON_DUPKEY (decode such a document on the host),
+ * and fields outside the path (metadata other than name/namespace, status.skipped,
+ * apiVersion, kind) are skipped without type checks. */
+typedef enum kdtn_json_err {
+    KDTN_JSON_OK = 0,
+    KDTN_JSON_SYNTAX = 1,   /* not valid JSON (json.SyntaxError)                                */
+    KDTN_JSON_DEPTH = 2,    /* nesting deeper than 10000 (scanner maxNestingDepth)              */
+    KDTN_JSON_TYPE = 3,     /* json.UnmarshalTypeError on a schema field (wrong JSON type,
+                               uid not an int64 literal, gap not a uint32 literal)              */
+    KDTN_JSON_DUPKEY = 4    /* a schema field repeated in one object (host fallback)            */
+} kdtn_json_err;
+
+typedef struct kdtn_ingest_info {
+    uint32_t n_topos, n_desired, n_realised;   /* T, N (spec.links), M (status.links)     */
+    uint32_t n_kdict, n_pdict;                 /* dictionary sizes (including id 0 = "")  */
+    int32_t  json_err;                         /* kdtn_json_err                           */
+    uint64_t err_offset;                       /* byte offset of an error (best effort)   */
+    uint64_t n_tokens;                         /* JSON tokens in the document             */
+    uint64_t kdict_bytes, pdict_bytes;         /* dictionary arena sizes                  */
+} kdtn_ingest_info;
+
+/* Host copies of the decoded tables (caller-owned, sized from kdtn_ingest_info; any NULL
+ * pointer is skipped). Link columns are SoA: key column k of record i at key[k*n + i]. */
+typedef struct kdtn_ingest_tables {
+    uint8_t*  kd_bytes;  uint32_t* kd_offs;    /* [kdict_bytes], [n_kdict + 1]            */
+    uint8_t*  pd_bytes;  uint32_t* pd_offs;
+    uint32_t* ns; uint32_t* name; uint32_t* src_ip; uint32_t* net_ns;   /* [T]            */
+    uint8_t*  flags;                            /* [T]                                      */
+    uint32_t* real_off; uint32_t* des_off;      /* [T + 1]                                  */
+    uint32_t* des_key; uint32_t* des_prop; uint32_t* des_gap; int64_t* des_uid;
+    uint32_t* real_key; uint32_t* real_prop; uint32_t* real_gap; int64_t* real_uid;
+} kdtn_ingest_tables;
+
+#define KDTN_EBADMSG (-74)   /* the JSON document was rejected: kdtn_ingest_info.json_err */
+
+/* H2D of the document (< 4 GiB) into the context's HBM. */
+int kdtn_json_upload(kdtn_ctx* ctx, const uint8_t* doc, uint64_t n);
+/* Decode the uploaded document on the GPU into the epoch inputs (synchronous). vnis:
+ * VxlanManager snapshot (NULL = empty), with ids in the document's kdict: strings not in
+ * the document cannot be referenced, so a snapshot is given as kdict ids of the result of
+ * a previous ingest of the same document shape. Single-shard contexts only (nranks == 1).
+ * Returns KDTN_OK, KDTN_EBADMSG (info->json_err says why) or an engine error. */
+int kdtn_json_ingest(kdtn_ctx* ctx, const kdtn_vni_table* vnis, kdtn_ingest_info* info);
+/* D2H of the decoded tables of the last successful ingest. */
+int kdtn_ingest_download(kdtn_ctx* ctx, kdtn_ingest_tables* out);
+
 /* ---- multi-GPU (one process per GPU): RCCL all-gather of the pod-status table ------ */
 int kdtn_comm_unique_id(uint8_t out[128]);
 int kdtn_comm_init(kdtn_ctx* ctx, const uint8_t unique_id[128], int nranks, int rank);

@@ -85,6 +85,22 @@ uint32_t or_fanout(const kdtn_batches* b, uint32_t T, uint32_t* node, uint32_t* 
  * error (common/qdisc.go:252-266); off has n_add + n_upd + 1 entries. */
 uint64_t or_tc_epoch(const kdtn_epoch_in* in, const kdtn_batches* b, uint8_t* bytes, uint64_t* off);
 
+/* ---- CR ingest (kdtn_oracle_json.c): TopologyList JSON → epoch tables ------------- */
+typedef struct or_json_tables {
+    int32_t   json_err;       /* kdtn_json_err                                   */
+    uint64_t  err_offset;
+    uint32_t  T, N, M, n_kdict, n_pdict;
+    uint64_t  kdict_bytes, pdict_bytes;
+    uint8_t*  kd_bytes; uint32_t* kd_offs; uint8_t* pd_bytes; uint32_t* pd_offs;
+    uint32_t *ns, *name, *src_ip, *net_ns; uint8_t* flags; uint32_t *real_off, *des_off;
+    uint32_t *des_key, *des_prop, *des_gap; int64_t* des_uid;     /* key[k*N + i]  */
+    uint32_t *real_key, *real_prop, *real_gap; int64_t* real_uid;
+} or_json_tables;
+/* Decode (Go json.Unmarshal into a TopologyList); 0 = done (json_err says whether the
+ * document was accepted), -1 = out of memory. Free with or_json_free. */
+int  or_json_ingest(const uint8_t* doc, uint64_t n, or_json_tables* out);
+void or_json_free(or_json_tables* t);
+
 #ifdef __cplusplus
 }
 #endif

@@ -235,3 +235,58 @@ def tc_epoch(inp: EpochInput, out: BatchesOut):
     arena = np.zeros(max(int(n), 1), np.uint8)
     L.or_tc_epoch(C.byref(cin), C.byref(b), arena.ctypes.data, off.ctypes.data)
     return arena[:int(n)], off
+
+
+# ---- CR ingest (kdtn_oracle_json.c) ------------------------------------------------------
+class JsonTables(C.Structure):
+    _fields_ = [("json_err", C.c_int32), ("err_offset", C.c_uint64),
+                ("T", C.c_uint32), ("N", C.c_uint32), ("M", C.c_uint32),
+                ("n_kdict", C.c_uint32), ("n_pdict", C.c_uint32),
+                ("kdict_bytes", C.c_uint64), ("pdict_bytes", C.c_uint64)] + [
+        (f, C.c_void_p) for f in ("kd_bytes", "kd_offs", "pd_bytes", "pd_offs", "ns", "name",
+                                  "src_ip", "net_ns", "flags", "real_off", "des_off",
+                                  "des_key", "des_prop", "des_gap", "des_uid",
+                                  "real_key", "real_prop", "real_gap", "real_uid")]
+
+
+def _np(ptr, n, dtype):
+    dtype = np.dtype(dtype)
+    if n == 0 or not ptr:
+        return np.zeros(n, dtype)
+    buf = (C.c_uint8 * (n * dtype.itemsize)).from_address(ptr)
+    return np.frombuffer(buf, dtype=dtype, count=n).copy()
+
+
+def json_ingest(doc: bytes):
+    """Go json.Unmarshal of a TopologyList document into the epoch tables.
+    Returns (json_err, err_offset, EpochInput | None)."""
+    from kdtn.tables import Links, StrTab, Topos
+    L = lib()
+    if not getattr(L, "_json_bound", False):
+        L.or_json_ingest.argtypes = [C.c_char_p, C.c_uint64, C.POINTER(JsonTables)]
+        L.or_json_free.argtypes = [C.POINTER(JsonTables)]
+        L._json_bound = True
+    t = JsonTables()
+    if L.or_json_ingest(doc, len(doc), C.byref(t)) != 0:
+        raise MemoryError("oracle json ingest")
+    try:
+        if t.json_err:
+            return int(t.json_err), int(t.err_offset), None
+        T, N, M = t.T, t.N, t.M
+
+        def links(key, prop, gap, uid, n):
+            return Links(_np(key, 7 * n, np.uint32).reshape(7, n),
+                         _np(uid, n, np.int64),
+                         _np(prop, 12 * n, np.uint32).reshape(12, n),
+                         _np(gap, n, np.uint32))
+        inp = EpochInput(
+            StrTab(_np(t.kd_bytes, t.kdict_bytes, np.uint8), _np(t.kd_offs, t.n_kdict + 1, np.uint32)),
+            StrTab(_np(t.pd_bytes, t.pdict_bytes, np.uint8), _np(t.pd_offs, t.n_pdict + 1, np.uint32)),
+            Topos(_np(t.ns, T, np.uint32), _np(t.name, T, np.uint32), _np(t.src_ip, T, np.uint32),
+                  _np(t.net_ns, T, np.uint32), _np(t.flags, T, np.uint8),
+                  _np(t.real_off, T + 1, np.uint32), _np(t.des_off, T + 1, np.uint32)),
+            links(t.real_key, t.real_prop, t.real_gap, t.real_uid, M),
+            links(t.des_key, t.des_prop, t.des_gap, t.des_uid, N))
+        return 0, 0, inp
+    finally:
+        L.or_json_free(C.byref(t))
