@@ -93,6 +93,15 @@ struct kdtn_ctx {
     uint64_t tc_bytes = 0;
     uint32_t tc_n = 0;
     bool tc_done = false;
+    // CR ingest (kdtn_ingest.hip): document, block masks, token stream, decode scratch
+    DevBuf j_doc, j_q, j_bs, j_hb, j_qcnt, j_qoff, j_tok, j_open, j_close, j_tcnt, j_dcnt, j_toff, j_doff;
+    DevBuf j_toks, j_par, j_role, j_ord, j_tagg, j_gagg, j_cnt3, j_coff3, j_small, j_part;
+    DevBuf j_tflags, j_tseen, j_dseen, j_rseen, j_kslots, j_krep, j_pslots, j_prep, j_heap;
+    DevBuf j_bits, j_bcnt, j_wrank, j_kslot_id, j_pslot_id, j_len, j_off64;
+    uint64_t j_n = 0;
+    uint32_t j_nb = 0;
+    bool j_loaded = false, j_done = false;
+    kdtn_ingest_info j_info{};
     // host-visible counters
     uint32_t* h_misc = nullptr;   // pinned: [0]=default id, [1]=del, [2]=upd, [3]=add, [4]=look-back error
     bool uploaded = false;
@@ -269,6 +278,69 @@ DevTopos topo_view(kdtn_ctx* c) {
     return t;
 }
 
+// per-string parse tables of both dictionaries (c->D, c->P set)
+int prepare_dicts(kdtn_ctx* c) {
+    const uint32_t D = c->D, P = c->P;
+    c->kb_words = (uint32_t)(((uint64_t)D + 63) / 64 * 2);
+    TRY(ensure(c->kd_bits, (size_t)KB_NSETS * c->kb_words * 4 + 4));
+    TRY(ensure(c->pd_pct, (size_t)P * 4));
+    TRY(ensure(c->pd_dur, (size_t)P * 8));
+    TRY(ensure(c->pd_rate, (size_t)P * 8));
+    TRY(ensure(c->pd_rerr, (size_t)nblocks(P) * BLOCK / 8));
+    return KDTN_OK;
+}
+
+// everything an epoch needs besides its input tables: VNI snapshot, pod tables, work and
+// output buffers (c->D, c->T set; shared by kdtn_epoch_upload and kdtn_json_ingest)
+int prepare_epoch(kdtn_ctx* c, const kdtn_vni_table& vn, uint32_t slice, uint32_t M, uint32_t N) {
+    const uint32_t D = c->D;
+    const uint32_t V = vn.n;
+    c->V = V;
+    TRY(upload(c, c->v_node, vn.node, (size_t)V * 4));
+    TRY(upload(c, c->v_vni, vn.vni, (size_t)V * 4));
+    TRY(upload(c, c->v_netns, vn.net_ns, (size_t)V * 4));
+    c->vni_mask = V ? next_pow2((uint64_t)V * 2) - 1 : 0;
+    TRY(ensure(c->v_ents, (size_t)V * 16));
+    TRY(ensure(c->v_slots, (size_t)(c->vni_mask + 1) * 4));
+
+    c->slice = slice;
+    if ((uint64_t)slice * (uint64_t)c->nranks > POD_INDEX) {
+        std::snprintf(g_last_error, sizeof(g_last_error), "pod table of %llu entries exceeds 2^30",
+                      (unsigned long long)slice * (unsigned long long)c->nranks);
+        return KDTN_EINVAL;
+    }
+    c->pod_total = slice * (uint32_t)c->nranks;
+    c->ovf_mask = next_pow2((uint64_t)c->pod_total * 2) - 1;
+    TRY(ensure(c->pods, (size_t)c->pod_total * 16));
+    TRY(ensure(c->pod_ovf, (size_t)(c->ovf_mask + 1) * 4));
+    if (c->pod_direct.cap < (size_t)D * 16) {                  // stamps start from a zeroed table
+        TRY(ensure(c->pod_direct, (size_t)D * 16));
+        HIP_TRY(hipMemsetAsync(c->pod_direct.p, 0, c->pod_direct.cap, c->stream));
+        c->pod_stamp = 0;
+    }
+
+    const uint32_t nwg = (c->T + TPW - 1) / TPW;
+    c->nwg = nwg;
+    TRY(ensure(c->otarget, (size_t)M * 4));
+    TRY(ensure(c->sync, sync_bytes(nwg)));
+    TRY(ensure(c->misc, 64));
+    TRY(ensure(c->hscratch, ((size_t)M + N) * 4));
+    TRY(ensure(c->fscratch, (size_t)M + N));
+    TRY(ensure(c->action, c->T));
+    TRY(ensure(c->del_off, (size_t)(c->T + 1) * 4));
+    TRY(ensure(c->add_off, (size_t)(c->T + 1) * 4));
+    TRY(ensure(c->upd_off, (size_t)(c->T + 1) * 4));
+    TRY(ensure(c->del_idx, (size_t)M * 4));
+    TRY(ensure(c->upd_idx, (size_t)M * 4));
+    TRY(ensure(c->add_idx, (size_t)N * 4));
+    TRY(ensure(c->del_res, (size_t)M * 16));
+    TRY(ensure(c->upd_res, (size_t)M * 16));
+    TRY(ensure(c->add_res, (size_t)N * 16));
+    TRY(ensure(c->upd_qdisc, (size_t)M * 72));
+    TRY(ensure(c->add_qdisc, (size_t)N * 72));
+    return KDTN_OK;
+}
+
 }  // namespace
 
 // ======================================================================================
@@ -364,7 +436,13 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->add_qdisc, &c->upd_qdisc, &c->kd_utf8, &c->pd_utf8, &c->w_rel,
                       &c->w_topo, &c->w_size, &c->w_err, &c->w_off, &c->w_part, &c->w_arena,
                       &c->f_mark, &c->f_send, &c->f_node_idx, &c->f_nodes, &c->f_counts, &c->f_base,
-                      &c->f_part, &c->f_idx, &c->tc_size, &c->tc_off, &c->tc_part, &c->tc_arena};
+                      &c->f_part, &c->f_idx, &c->tc_size, &c->tc_off, &c->tc_part, &c->tc_arena,
+                      &c->j_doc, &c->j_q, &c->j_bs, &c->j_hb, &c->j_qcnt, &c->j_qoff, &c->j_tok, &c->j_open,
+                      &c->j_close, &c->j_tcnt, &c->j_dcnt, &c->j_toff, &c->j_doff, &c->j_toks, &c->j_par,
+                      &c->j_role, &c->j_ord, &c->j_tagg, &c->j_gagg, &c->j_cnt3, &c->j_coff3, &c->j_small,
+                      &c->j_part, &c->j_tflags, &c->j_tseen, &c->j_dseen, &c->j_rseen, &c->j_kslots, &c->j_krep,
+                      &c->j_pslots, &c->j_prep, &c->j_heap, &c->j_bits, &c->j_bcnt, &c->j_wrank,
+                      &c->j_kslot_id, &c->j_pslot_id, &c->j_len, &c->j_off64};
     for (DevBuf* b : bufs) release(*b);
     for (int i = 0; i <= kMaxTimers; ++i)
         if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
@@ -415,14 +493,9 @@ int kdtn_epoch_upload(kdtn_ctx* c, const kdtn_epoch_in* in) {
     c->T = T.n;
     TRY(upload_arena(c, c->kd_bytes, in->kdict.bytes, in->kdict.offs[D]));
     TRY(upload(c, c->kd_offs, in->kdict.offs, (size_t)(D + 1) * 4));
-    c->kb_words = (uint32_t)(((uint64_t)D + 63) / 64 * 2);
-    TRY(ensure(c->kd_bits, (size_t)KB_NSETS * c->kb_words * 4 + 4));
     TRY(upload_arena(c, c->pd_bytes, in->pdict.bytes, in->pdict.offs[P]));
     TRY(upload(c, c->pd_offs, in->pdict.offs, (size_t)(P + 1) * 4));
-    TRY(ensure(c->pd_pct, (size_t)P * 4));
-    TRY(ensure(c->pd_dur, (size_t)P * 8));
-    TRY(ensure(c->pd_rate, (size_t)P * 8));
-    TRY(ensure(c->pd_rerr, (size_t)nblocks(P) * BLOCK / 8));
+    TRY(prepare_dicts(c));
 
     TRY(upload(c, c->t_ns, T.ns, (size_t)T.n * 4));
     TRY(upload(c, c->t_name, T.name, (size_t)T.n * 4));
@@ -435,51 +508,7 @@ int kdtn_epoch_upload(kdtn_ctx* c, const kdtn_epoch_in* in) {
     TRY(upload_links(c, c->real, in->realised, D, P, "realised"));
     TRY(upload_links(c, c->des, in->desired, D, P, "desired"));
 
-    const uint32_t V = in->vnis.n;
-    c->V = V;
-    TRY(upload(c, c->v_node, in->vnis.node, (size_t)V * 4));
-    TRY(upload(c, c->v_vni, in->vnis.vni, (size_t)V * 4));
-    TRY(upload(c, c->v_netns, in->vnis.net_ns, (size_t)V * 4));
-    c->vni_mask = V ? next_pow2((uint64_t)V * 2) - 1 : 0;
-    TRY(ensure(c->v_ents, (size_t)V * 16));
-    TRY(ensure(c->v_slots, (size_t)(c->vni_mask + 1) * 4));
-
-    c->slice = slice;
-    if ((uint64_t)slice * (uint64_t)c->nranks > POD_INDEX) {
-        std::snprintf(g_last_error, sizeof(g_last_error), "pod table of %llu entries exceeds 2^30",
-                      (unsigned long long)slice * (unsigned long long)c->nranks);
-        return KDTN_EINVAL;
-    }
-    c->pod_total = slice * (uint32_t)c->nranks;
-    c->ovf_mask = next_pow2((uint64_t)c->pod_total * 2) - 1;
-    TRY(ensure(c->pods, (size_t)c->pod_total * 16));
-    TRY(ensure(c->pod_ovf, (size_t)(c->ovf_mask + 1) * 4));
-    if (c->pod_direct.cap < (size_t)D * 16) {                  // stamps start from a zeroed table
-        TRY(ensure(c->pod_direct, (size_t)D * 16));
-        HIP_TRY(hipMemsetAsync(c->pod_direct.p, 0, c->pod_direct.cap, c->stream));
-        c->pod_stamp = 0;
-    }
-
-    const uint32_t M = in->realised.n, N = in->desired.n;
-    const uint32_t nwg = (T.n + TPW - 1) / TPW;
-    c->nwg = nwg;
-    TRY(ensure(c->otarget, (size_t)M * 4));
-    TRY(ensure(c->sync, sync_bytes(nwg)));
-    TRY(ensure(c->misc, 64));
-    TRY(ensure(c->hscratch, ((size_t)M + N) * 4));
-    TRY(ensure(c->fscratch, (size_t)M + N));
-    TRY(ensure(c->action, T.n));
-    TRY(ensure(c->del_off, (size_t)(T.n + 1) * 4));
-    TRY(ensure(c->add_off, (size_t)(T.n + 1) * 4));
-    TRY(ensure(c->upd_off, (size_t)(T.n + 1) * 4));
-    TRY(ensure(c->del_idx, (size_t)M * 4));
-    TRY(ensure(c->upd_idx, (size_t)M * 4));
-    TRY(ensure(c->add_idx, (size_t)N * 4));
-    TRY(ensure(c->del_res, (size_t)M * 16));
-    TRY(ensure(c->upd_res, (size_t)M * 16));
-    TRY(ensure(c->add_res, (size_t)N * 16));
-    TRY(ensure(c->upd_qdisc, (size_t)M * 72));
-    TRY(ensure(c->add_qdisc, (size_t)N * 72));
+    TRY(prepare_epoch(c, in->vnis, slice, in->realised.n, in->desired.n));
     HIP_TRY(hipStreamSynchronize(c->stream));   // host arrays may be released after return
     c->uploaded = true;
     c->ran = false;
@@ -1038,6 +1067,384 @@ int kdtn_epoch_download_tc(kdtn_ctx* c, kdtn_tc_argv* o) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     return KDTN_OK;
 }
+
+}  // extern "C"
+
+// ======================================================================================
+// CR ingest: TopologyList JSON → device-resident epoch tables (kdtn_ingest.hip)
+// ======================================================================================
+namespace {
+
+// exclusive scan of n u32 values into n+1 u64 offsets (out[n] = total)
+int scan_u32(kdtn_ctx* c, const uint32_t* in, uint32_t n, uint64_t* out) {
+    const uint32_t nb = nblocks((uint64_t)n + 1, SCAN_CHUNK);
+    TRY(ensure(c->j_part, (size_t)nb * 8));
+    hipStream_t s = c->stream;
+    k_scan_partial<<<nb, BLOCK, 0, s>>>(in, n, dp<uint64_t>(c->j_part));
+    k_scan_top<<<1, BLOCK, 0, s>>>(dp<uint64_t>(c->j_part), nb);
+    k_scan_final<<<nb, BLOCK, 0, s>>>(in, n, dp<uint64_t>(c->j_part), out);
+    return KDTN_OK;
+}
+
+template <typename T>
+int d2h(kdtn_ctx* c, T* host, const void* dev, size_t count = 1) {
+    HIP_TRY(hipMemcpyAsync(host, dev, sizeof(T) * count, hipMemcpyDeviceToHost, c->stream));
+    return KDTN_OK;
+}
+
+// small control block: [0] syntax error, [1] decode error (pos << 8 | code, ~0 = none),
+// [2] heap bytes used, [3] status | seen_root << 32, [4] kd fill | pd fill << 32
+constexpr size_t J_SMALL = 64;
+
+int json_reject(kdtn_ctx* c, kdtn_ingest_info* info, unsigned long long word) {
+    c->j_info.json_err = (int32_t)(word & 0xFF);
+    c->j_info.err_offset = word >> 8;
+    if (info) *info = c->j_info;
+    c->j_done = false;
+    c->uploaded = false;
+    std::snprintf(g_last_error, sizeof(g_last_error), "TopologyList rejected: json error %d at byte %llu",
+                  c->j_info.json_err, (unsigned long long)c->j_info.err_offset);
+    return KDTN_EBADMSG;
+}
+
+// ids of one dictionary in first-occurrence order, its arena and offsets
+int json_dict(kdtn_ctx* c, const JsDict& dt, const JsIntern& in, uint32_t ntok, DevBuf& slot_id, DevBuf& bytes,
+              DevBuf& offs, uint32_t* n_out, uint64_t* bytes_out) {
+    hipStream_t s = c->stream;
+    const uint32_t nw = (ntok + 31) / 32, cap = dt.mask + 1;
+    TRY(ensure(c->j_bits, (size_t)nw * 4));
+    TRY(ensure(c->j_bcnt, (size_t)nw * 4));
+    TRY(ensure(c->j_wrank, ((size_t)nw + 1) * 8));
+    HIP_TRY(hipMemsetAsync(c->j_bits.p, 0, (size_t)nw * 4, s));
+    k_js_rep_mark<<<nblocks(cap), BLOCK, 0, s>>>(dt, dp<uint32_t>(c->j_bits));
+    k_js_popc<<<nblocks(nw), BLOCK, 0, s>>>(dp<uint32_t>(c->j_bits), nw, dp<uint32_t>(c->j_bcnt));
+    TRY(scan_u32(c, dp<uint32_t>(c->j_bcnt), nw, dp<uint64_t>(c->j_wrank)));
+    uint64_t uniq = 0;
+    TRY(d2h(c, &uniq, dp<uint64_t>(c->j_wrank) + nw));
+    HIP_TRY(hipStreamSynchronize(s));
+    const uint32_t n = (uint32_t)uniq + 1;                    // + id 0 = ""
+    TRY(ensure(slot_id, (size_t)cap * 4));
+    TRY(ensure(c->j_len, (size_t)n * 4));
+    TRY(ensure(c->j_off64, ((size_t)n + 1) * 8));
+    HIP_TRY(hipMemsetAsync(c->j_len.p, 0, (size_t)n * 4, s));
+    k_js_ids<<<nblocks(cap), BLOCK, 0, s>>>(dt, dp<uint32_t>(c->j_bits), dp<uint64_t>(c->j_wrank),
+                                            dp<uint32_t>(slot_id), dp<uint32_t>(c->j_len));
+    TRY(scan_u32(c, dp<uint32_t>(c->j_len), n, dp<uint64_t>(c->j_off64)));
+    uint64_t total = 0;
+    TRY(d2h(c, &total, dp<uint64_t>(c->j_off64) + n));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (total > 0xFFFFFF00ull) {
+        std::snprintf(g_last_error, sizeof(g_last_error), "dictionary arena of %llu bytes exceeds 4 GiB",
+                      (unsigned long long)total);
+        return KDTN_EINVAL;
+    }
+    TRY(ensure(bytes, (size_t)total + 64));
+    TRY(ensure(offs, ((size_t)n + 1) * 4));
+    HIP_TRY(hipMemsetAsync(offs.p, 0, 4, s));
+    HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(dp<uint32_t>(offs) + n), (int)(uint32_t)total, 1, s));
+    k_js_dict_copy<<<nblocks(cap), BLOCK, 0, s>>>(dt, in, dp<uint32_t>(slot_id), dp<uint64_t>(c->j_off64),
+                                                  dp<uint32_t>(offs), dp<uint8_t>(bytes));
+    *n_out = n;
+    *bytes_out = total;
+    return KDTN_OK;
+}
+
+int link_store_alloc(kdtn_ctx* c, DevLinkStore& st, uint32_t n) {
+    const size_t tiles = ((size_t)std::max<uint32_t>(n, 1) + TILE_RECS - 1) / TILE_RECS;
+    TRY(ensure(st.buf, tiles * TILE_WORDS * 4));
+    st.view.base = dp<uint32_t>(st.buf);
+    st.view.n = n;
+    st.n = n;
+    return KDTN_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int kdtn_json_upload(kdtn_ctx* c, const uint8_t* doc, uint64_t n) {
+    if (!c || (n && !doc)) return KDTN_EINVAL;
+    if (n >= 0xFFFFFF00ull) {
+        std::snprintf(g_last_error, sizeof(g_last_error), "document of %llu bytes: the GPU ingest takes < 4 GiB",
+                      (unsigned long long)n);
+        return KDTN_EINVAL;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    const uint32_t nb = (uint32_t)((n + 63) / 64);
+    const size_t padded = (size_t)nb * 64 + 128;             // whitespace tail: blocks and look-ahead
+    TRY(ensure(c->j_doc, padded));
+    if (n) HIP_TRY(hipMemcpyAsync(c->j_doc.p, doc, n, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemsetAsync(dp<uint8_t>(c->j_doc) + n, ' ', padded - n, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->j_n = n;
+    c->j_nb = nb;
+    c->j_loaded = true;
+    c->j_done = false;
+    return KDTN_OK;
+}
+
+int kdtn_json_ingest(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest_info* info) {
+    if (!c || !c->j_loaded) return KDTN_EINVAL;
+    if (c->nranks > 1) {
+        std::snprintf(g_last_error, sizeof(g_last_error), "kdtn_json_ingest: single-shard contexts only");
+        return KDTN_EINVAL;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    g_last_error[0] = 0;
+    hipStream_t s = c->stream;
+    c->j_info = kdtn_ingest_info{};
+    c->uploaded = false;
+    c->ran = false;
+    c->n_ev = 0;
+    (void)hipEventRecord(c->ev[0], s);
+    const uint32_t nb = c->j_nb;
+    if (nb == 0) return json_reject(c, info, (0ull << 8) | KDTN_JSON_SYNTAX);   // empty document
+
+    TRY(ensure(c->j_small, J_SMALL));
+    unsigned long long* small = dp<unsigned long long>(c->j_small);
+    HIP_TRY(hipMemsetAsync(small, 0xFF, 16, s));
+    HIP_TRY(hipMemsetAsync(small + 2, 0, J_SMALL - 16, s));
+    for (DevBuf* b : {&c->j_q, &c->j_bs, &c->j_hb, &c->j_tok, &c->j_open, &c->j_close}) TRY(ensure(*b, (size_t)nb * 8));
+    for (DevBuf* b : {&c->j_qcnt, &c->j_tcnt, &c->j_dcnt}) TRY(ensure(*b, (size_t)nb * 4));
+    for (DevBuf* b : {&c->j_qoff, &c->j_toff, &c->j_doff}) TRY(ensure(*b, ((size_t)nb + 1) * 8));
+    JsDoc j{dp<uint8_t>(c->j_doc), (uint32_t)c->j_n, nb, dp<uint64_t>(c->j_q), dp<uint64_t>(c->j_bs),
+            dp<uint64_t>(c->j_hb)};
+    JsMasks m{dp<uint64_t>(c->j_tok), dp<uint64_t>(c->j_open), dp<uint64_t>(c->j_close), dp<uint32_t>(c->j_tcnt),
+              dp<uint32_t>(c->j_dcnt)};
+
+    // 1. block masks, string state, token counts, depth
+    k_js_quotes<<<nblocks(nb), BLOCK, 0, s>>>(j, dp<uint64_t>(c->j_q), dp<uint64_t>(c->j_bs), dp<uint64_t>(c->j_hb),
+                                             dp<uint32_t>(c->j_qcnt));
+    TRY(scan_u32(c, dp<uint32_t>(c->j_qcnt), nb, dp<uint64_t>(c->j_qoff)));
+    k_js_classify<<<nblocks(nb), BLOCK, 0, s>>>(j, dp<uint64_t>(c->j_qoff), m, small);
+    TRY(scan_u32(c, dp<uint32_t>(c->j_tcnt), nb, dp<uint64_t>(c->j_toff)));
+    TRY(scan_u32(c, dp<uint32_t>(c->j_dcnt), nb, dp<uint64_t>(c->j_doff)));
+    timer_mark(c, "js_blocks");
+    uint64_t quotes = 0, ntok64 = 0;
+    unsigned long long serr = 0;
+    TRY(d2h(c, &quotes, dp<uint64_t>(c->j_qoff) + nb));
+    TRY(d2h(c, &ntok64, dp<uint64_t>(c->j_toff) + nb));
+    TRY(d2h(c, &serr, small));
+    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(hipGetLastError());
+    if (quotes & 1) serr = std::min<unsigned long long>(serr, (c->j_n << 8) | KDTN_JSON_SYNTAX);   // unterminated
+    if (ntok64 == 0) serr = std::min<unsigned long long>(serr, KDTN_JSON_SYNTAX);
+    if (serr != ~0ull) return json_reject(c, info, serr);
+    const uint32_t ntok = (uint32_t)ntok64;
+    c->j_info.n_tokens = ntok64;
+
+    // 2. token stream, parents, checkValid
+    TRY(ensure(c->j_toks, (size_t)ntok * 8));
+    TRY(ensure(c->j_par, (size_t)ntok * 4));
+    TRY(ensure(c->j_role, (size_t)ntok));
+    TRY(ensure(c->j_ord, (size_t)ntok * 4));
+    const uint2* toks = dp<uint2>(c->j_toks);
+    uint32_t* par = dp<uint32_t>(c->j_par);
+    k_js_tokens<<<nblocks(nb), BLOCK, 0, s>>>(j, m, dp<uint64_t>(c->j_toff), dp<uint64_t>(c->j_doff),
+                                             dp<uint2>(c->j_toks), small);
+    timer_mark(c, "js_tokens");
+    const uint32_t ntiles = (ntok + JS_TILE - 1) / JS_TILE, ng = (ntiles + BLOCK - 1) / BLOCK;
+    TRY(ensure(c->j_tagg, (size_t)ntiles * JS_PD * 4));
+    TRY(ensure(c->j_gagg, (size_t)ng * JS_PD * 4));
+    k_js_par_agg<<<ntiles, BLOCK, 0, s>>>(toks, ntok, dp<uint32_t>(c->j_tagg));
+    k_js_par_group<<<ng, BLOCK, 0, s>>>(dp<uint32_t>(c->j_tagg), ntiles, dp<uint32_t>(c->j_gagg));
+    k_js_par_top<<<1, BLOCK, 0, s>>>(dp<uint32_t>(c->j_gagg), ng);
+    k_js_par_tiles<<<ng, BLOCK, 0, s>>>(dp<uint32_t>(c->j_tagg), ntiles, dp<uint32_t>(c->j_gagg));
+    k_js_par_apply<<<ntiles, BLOCK, 0, s>>>(toks, ntok, dp<uint32_t>(c->j_tagg), par);
+    k_js_deep<<<nblocks(ntok), BLOCK, 0, s>>>(toks, ntok, par);
+    timer_mark(c, "js_parents");
+    k_js_validate<<<nblocks(ntok), BLOCK, 0, s>>>(j, toks, ntok, par, small);
+    timer_mark(c, "js_validate");
+    TRY(d2h(c, &serr, small));
+    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(hipGetLastError());
+    if (serr != ~0ull) return json_reject(c, info, serr);
+
+    // 3. schema roles, items / links ordinals
+    uint8_t* role = dp<uint8_t>(c->j_role);
+    uint32_t* ord = dp<uint32_t>(c->j_ord);
+    k_js_roles<<<nblocks(ntok), BLOCK, 0, s>>>(j, toks, ntok, par, role);
+    TRY(ensure(c->j_cnt3, (size_t)3 * ntiles * 4));
+    TRY(ensure(c->j_coff3, (size_t)3 * (ntiles + 1) * 8));
+    k_js_elems_count<<<ntiles, BLOCK, 0, s>>>(j, toks, ntok, par, role, dp<uint32_t>(c->j_cnt3), small + 1);
+    for (int q = 0; q < 3; ++q)
+        TRY(scan_u32(c, dp<uint32_t>(c->j_cnt3) + (size_t)q * ntiles, ntiles,
+                     dp<uint64_t>(c->j_coff3) + (size_t)q * (ntiles + 1)));
+    uint64_t tot[3];
+    for (int q = 0; q < 3; ++q) TRY(d2h(c, tot + q, dp<uint64_t>(c->j_coff3) + (size_t)q * (ntiles + 1) + ntiles));
+    unsigned long long derr = 0;
+    TRY(d2h(c, &derr, small + 1));
+    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(hipGetLastError());
+    if (derr != ~0ull) return json_reject(c, info, derr);
+    const uint32_t T = (uint32_t)tot[0], N = (uint32_t)tot[1], M = (uint32_t)tot[2];
+    timer_mark(c, "js_elements");
+
+    // 4. output tables
+    c->T = T;
+    for (DevBuf* b : {&c->t_ns, &c->t_name, &c->t_src, &c->t_netns, &c->j_tflags, &c->j_tseen})
+        TRY(ensure(*b, (size_t)T * 4));
+    TRY(ensure(c->t_flags, (size_t)T));
+    TRY(ensure(c->t_roff, ((size_t)T + 1) * 4));
+    TRY(ensure(c->t_noff, ((size_t)T + 1) * 4));
+    TRY(link_store_alloc(c, c->des, N));
+    TRY(link_store_alloc(c, c->real, M));
+    TRY(ensure(c->j_dseen, (size_t)N * 4));
+    TRY(ensure(c->j_rseen, (size_t)M * 4));
+    JsTopoOut to{dp<uint32_t>(c->t_ns), dp<uint32_t>(c->t_name), dp<uint32_t>(c->t_src), dp<uint32_t>(c->t_netns),
+                 dp<uint32_t>(c->j_tflags), dp<uint32_t>(c->t_roff), dp<uint32_t>(c->t_noff), dp<uint32_t>(c->j_tseen)};
+    k_js_elems_write<<<ntiles, BLOCK, 0, s>>>(toks, ntok, par, role, dp<uint64_t>(c->j_coff3), ntiles, ord, to);
+    HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(to.real_off + T), (int)M, 1, s));
+    HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(to.des_off + T), (int)N, 1, s));
+    JsStore des{dp<uint32_t>(c->des.buf), dp<uint32_t>(c->j_dseen)};
+    JsStore real{dp<uint32_t>(c->real.buf), dp<uint32_t>(c->j_rseen)};
+
+    // 5. schema values + interning; a table or heap that fills up is grown and the pass rerun
+    uint32_t kcap = next_pow2(std::max<uint64_t>(1024, 2ull * ((uint64_t)N + M) + 4ull * T));
+    uint32_t pcap = next_pow2(std::max<uint64_t>(1024, ((uint64_t)N + M) / 2 + 64));
+    uint64_t hcap = std::max<uint64_t>(1 << 20, c->j_n / 16);
+    JsIntern in{};
+    for (int attempt = 0;; ++attempt) {
+        TRY(ensure(c->j_kslots, (size_t)kcap * 8));
+        TRY(ensure(c->j_krep, (size_t)kcap * 4));
+        TRY(ensure(c->j_pslots, (size_t)pcap * 8));
+        TRY(ensure(c->j_prep, (size_t)pcap * 4));
+        TRY(ensure(c->j_heap, (size_t)hcap + 64));
+        HIP_TRY(hipMemsetAsync(c->j_kslots.p, 0, (size_t)kcap * 8, s));
+        HIP_TRY(hipMemsetAsync(c->j_krep.p, 0xFF, (size_t)kcap * 4, s));
+        HIP_TRY(hipMemsetAsync(c->j_pslots.p, 0, (size_t)pcap * 8, s));
+        HIP_TRY(hipMemsetAsync(c->j_prep.p, 0xFF, (size_t)pcap * 4, s));
+        HIP_TRY(hipMemsetAsync(small + 2, 0, J_SMALL - 16, s));
+        HIP_TRY(hipMemsetAsync(small + 1, 0xFF, 8, s));
+        for (DevBuf* b : {&c->t_ns, &c->t_name, &c->t_src, &c->t_netns, &c->j_tseen})
+            HIP_TRY(hipMemsetAsync(b->p, 0, (size_t)T * 4, s));
+        HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(to.flags), (int)(KDTN_TOPO_SPEC_NIL | KDTN_TOPO_STATUS_NIL),
+                                  T, s));
+        HIP_TRY(hipMemsetAsync(c->des.buf.p, 0, c->des.buf.cap, s));
+        HIP_TRY(hipMemsetAsync(c->real.buf.p, 0, c->real.buf.cap, s));
+        HIP_TRY(hipMemsetAsync(c->j_dseen.p, 0, (size_t)N * 4, s));
+        HIP_TRY(hipMemsetAsync(c->j_rseen.p, 0, (size_t)M * 4, s));
+        in.doc = j.doc;
+        in.heap = dp<uint8_t>(c->j_heap);
+        in.heap_used = small + 2;
+        in.heap_cap = hcap;
+        in.status = reinterpret_cast<uint32_t*>(small + 3);
+        in.seen_root = reinterpret_cast<uint32_t*>(small + 3) + 1;
+        in.kd = JsDict{dp<unsigned long long>(c->j_kslots), dp<uint32_t>(c->j_krep),
+                       reinterpret_cast<uint32_t*>(small + 4), kcap - 1, kcap / 4 * 3};
+        in.pd = JsDict{dp<unsigned long long>(c->j_pslots), dp<uint32_t>(c->j_prep),
+                       reinterpret_cast<uint32_t*>(small + 4) + 1, pcap - 1, pcap / 4 * 3};
+        k_js_values<<<nblocks(ntok), BLOCK, 0, s>>>(j, toks, ntok, par, role, ord, to, des, real, in, small + 1);
+        unsigned long long ctl[3];
+        TRY(d2h(c, ctl, small + 1, 3));
+        uint32_t fills[2];
+        TRY(d2h(c, fills, small + 4, 2));
+        HIP_TRY(hipStreamSynchronize(s));
+        HIP_TRY(hipGetLastError());
+        const uint32_t status = (uint32_t)ctl[2];
+        if (status & JS_ST_LONG) {
+            std::snprintf(g_last_error, sizeof(g_last_error), "a schema string is longer than 16 MiB");
+            return KDTN_EINVAL;
+        }
+        if (status & JS_ST_OVERFLOW) {
+            if (attempt >= 6) return KDTN_ENOMEM;
+            if (fills[0] >= in.kd.limit) kcap *= 4;
+            if (fills[1] >= in.pd.limit) pcap *= 4;
+            if (ctl[1] > hcap) hcap = std::max<uint64_t>(hcap * 4, ctl[1] + (1 << 20));
+            if (fills[0] < in.kd.limit && fills[1] < in.pd.limit && ctl[1] <= hcap) { kcap *= 2; pcap *= 2; }
+            continue;
+        }
+        if (ctl[0] != ~0ull) return json_reject(c, info, ctl[0]);
+        break;
+    }
+    timer_mark(c, "js_values");
+
+    // 6. ids in first-occurrence order, dictionaries, id columns
+    uint64_t kbytes = 0, pbytes = 0;
+    TRY(json_dict(c, in.kd, in, ntok, c->j_kslot_id, c->kd_bytes, c->kd_offs, &c->D, &kbytes));
+    TRY(json_dict(c, in.pd, in, ntok, c->j_pslot_id, c->pd_bytes, c->pd_offs, &c->P, &pbytes));
+    constexpr uint32_t IDW = (KDTN_NKEY + KDTN_NPROP) * TILE_RECS;
+    if (N) k_js_finalize_links<<<nblocks((uint64_t)(N + TILE_RECS - 1) / TILE_RECS * IDW), BLOCK, 0, s>>>(
+        des, N, dp<uint32_t>(c->j_kslot_id), dp<uint32_t>(c->j_pslot_id));
+    if (M) k_js_finalize_links<<<nblocks((uint64_t)(M + TILE_RECS - 1) / TILE_RECS * IDW), BLOCK, 0, s>>>(
+        real, M, dp<uint32_t>(c->j_kslot_id), dp<uint32_t>(c->j_pslot_id));
+    if (T) k_js_finalize_topos<<<nblocks(T), BLOCK, 0, s>>>(to, T, dp<uint32_t>(c->j_kslot_id), dp<uint8_t>(c->t_flags));
+    timer_mark(c, "js_intern");
+    HIP_TRY(hipGetLastError());
+
+    // 7. the epoch inputs are in place: finish what kdtn_epoch_upload would set up
+    TRY(prepare_dicts(c));
+    const kdtn_vni_table none{0, nullptr, nullptr, nullptr};
+    const kdtn_vni_table& vn = vnis ? *vnis : none;
+    TRY(check_ids(vn.node, vn.n, c->D, "vnis.node"));
+    TRY(check_ids(vn.net_ns, vn.n, c->D, "vnis.net_ns"));
+    TRY(prepare_epoch(c, vn, T, M, N));
+    HIP_TRY(hipStreamSynchronize(s));
+    c->j_info.n_topos = T;
+    c->j_info.n_desired = N;
+    c->j_info.n_realised = M;
+    c->j_info.n_kdict = c->D;
+    c->j_info.n_pdict = c->P;
+    c->j_info.kdict_bytes = kbytes;
+    c->j_info.pdict_bytes = pbytes;
+    if (info) *info = c->j_info;
+    c->j_done = true;
+    c->uploaded = true;
+    return KDTN_OK;
+}
+
+int kdtn_ingest_download(kdtn_ctx* c, kdtn_ingest_tables* o) {
+    if (!c || !o || !c->j_done) return KDTN_EINVAL;
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const kdtn_ingest_info& I = c->j_info;
+    auto get = [&](void* dst, const DevBuf& b, size_t bytes) -> int {
+        if (dst && bytes) HIP_TRY(hipMemcpyAsync(dst, b.p, bytes, hipMemcpyDeviceToHost, s));
+        return KDTN_OK;
+    };
+    TRY(get(o->kd_bytes, c->kd_bytes, I.kdict_bytes));
+    TRY(get(o->kd_offs, c->kd_offs, ((size_t)I.n_kdict + 1) * 4));
+    TRY(get(o->pd_bytes, c->pd_bytes, I.pdict_bytes));
+    TRY(get(o->pd_offs, c->pd_offs, ((size_t)I.n_pdict + 1) * 4));
+    const size_t T = I.n_topos;
+    TRY(get(o->ns, c->t_ns, T * 4));
+    TRY(get(o->name, c->t_name, T * 4));
+    TRY(get(o->src_ip, c->t_src, T * 4));
+    TRY(get(o->net_ns, c->t_netns, T * 4));
+    TRY(get(o->flags, c->t_flags, T));
+    TRY(get(o->real_off, c->t_roff, (T + 1) * 4));
+    TRY(get(o->des_off, c->t_noff, (T + 1) * 4));
+    // AoSoA tiles → SoA columns
+    auto cols = [&](const DevLinkStore& st, uint32_t* key, uint32_t* prop, uint32_t* gap, int64_t* uid) -> int {
+        const uint32_t n = st.n;
+        if (!n) return KDTN_OK;
+        const size_t full = n / TILE_RECS, tail = n % TILE_RECS, tile_bytes = (size_t)TILE_WORDS * 4;
+        const uint8_t* base = static_cast<const uint8_t*>(st.buf.p);
+        auto col = [&](int cidx, void* dst, size_t esz) -> int {
+            if (!dst) return KDTN_OK;
+            const size_t run = TILE_RECS * esz;
+            const uint8_t* src = base + (size_t)cidx * TILE_RECS * 4;
+            if (full) HIP_TRY(hipMemcpy2DAsync(dst, run, src, tile_bytes, run, full, hipMemcpyDeviceToHost, s));
+            if (tail)
+                HIP_TRY(hipMemcpyAsync(static_cast<uint8_t*>(dst) + full * run, src + full * tile_bytes, tail * esz,
+                                       hipMemcpyDeviceToHost, s));
+            return KDTN_OK;
+        };
+        for (int k = 0; k < KDTN_NKEY; ++k) TRY(col(COL_KEY0 + k, key ? key + (size_t)k * n : nullptr, 4));
+        for (int k = 0; k < KDTN_NPROP; ++k) TRY(col(COL_PROP0 + k, prop ? prop + (size_t)k * n : nullptr, 4));
+        TRY(col(COL_GAP, gap, 4));
+        TRY(col(COL_UID, uid, 8));
+        return KDTN_OK;
+    };
+    TRY(cols(c->des, o->des_key, o->des_prop, o->des_gap, o->des_uid));
+    TRY(cols(c->real, o->real_key, o->real_prop, o->real_gap, o->real_uid));
+    HIP_TRY(hipStreamSynchronize(s));
+    return KDTN_OK;
+}
+
+}  // extern "C"
+
+extern "C" {
 
 int kdtn_comm_unique_id(uint8_t out[128]) {
     ncclUniqueId id;

@@ -1,0 +1,1051 @@
+// kdtn_ingest.hip — CR ingest on the GPU: a Kubernetes TopologyList
+// JSON document in HBM → the epoch tables kdtn_epoch_run consumes (interned dictionaries,
+// topology table, both AoSoA link stores), following Go's encoding/json as forked by
+// sigs.k8s.io/json (see include/kdtn.h kdtn_json_ingest; CPU restatement and parity oracle:
+// oracle/kdtn_oracle_json.c).
+//
+// The document is processed as 64-byte blocks (one lane each, bit k of a block mask =
+// byte k) and then as a token stream, bit-parallel in the style of structural indexing:
+//   k_js_quotes     backslash / quote / high-bit masks; unescaped quotes (escape runs)
+//   [scan]          quote counts → in-string state at every block start (parity)
+//   k_js_classify   in-string mask (prefix XOR), structural / string-open / scalar-start
+//                   token bits, opens / closes, control bytes
+//   [scan x2]       token offsets, nesting depth at every block start
+//   k_js_tokens     token stream: {byte offset, pre-depth | kind << 24}
+//   k_js_par_*      parent (enclosing container) of every token: per depth level d ≤ 16 the
+//                   last open bracket with post-depth d before the token, an element-wise
+//                   max-scan over 4096-token tiles; deeper tokens walk back (k_js_deep)
+//   k_js_validate   checkValid as local rules on (previous token, token, container kind),
+//                   string escapes and number / literal grammar, bracket matching
+//   k_js_roles      schema role of every container (items, metadata, spec, links, ...)
+//   k_js_elems_*    ordinals of items and links elements (tile counts + scans) → topology
+//                   index, record index and the per-topology record offsets
+//   k_js_values     every schema field: type check, duplicate check, uid / gap parse, and
+//                   string interning into a lock-free open-addressing table (64-bit CAS of
+//                   a self-describing key {tag, heap, len, off}); atomicMin keeps each
+//                   string's first occurrence
+//   k_js_rep_mark / k_js_ids / k_js_dict_copy / k_js_finalize
+//                   ids = rank of the first occurrence in document order (bitmap popcount
+//                   scan), dictionary arenas in id order, table slots → ids
+#include "kdtn_kernels.h"
+
+namespace kdtn {
+
+// ---------------------------------------------------------------- byte-class SWAR helpers
+KD_INLINE uint32_t mm4(uint32_t z) { return ((z >> 7) * 0x10204080u) >> 28; }   // bits 7,15,23,31 → 4 bits
+KD_INLINE uint32_t eqb(uint32_t w, uint32_t c) {                                 // byte == c
+    const uint32_t t = w ^ (c * 0x01010101u);
+    return ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
+}
+KD_INLINE uint32_t ltb(uint32_t w, uint32_t n) {                                 // byte < n (n ≤ 128)
+    return ~(((w & 0x7F7F7F7Fu) + (128u - n) * 0x01010101u) | w) & 0x80808080u;
+}
+KD_INLINE uint64_t prefix_xor(uint64_t x) {
+    x ^= x << 1; x ^= x << 2; x ^= x << 4; x ^= x << 8; x ^= x << 16; x ^= x << 32;
+    return x;
+}
+KD_INLINE void load_block(const uint8_t* doc, uint32_t b, uint32_t w[16]) {
+    const uint4* p = reinterpret_cast<const uint4*>(doc + (size_t)b * 64);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint4 v = p[k];
+        w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+    }
+}
+KD_INLINE void js_fail(unsigned long long* err, uint32_t pos, uint32_t code) {
+    atomicMin(err, ((unsigned long long)pos << 8) | code);
+}
+KD_INLINE bool is_struct_byte(uint32_t c) {
+    return c == '{' || c == '}' || c == '[' || c == ']' || c == ':' || c == ',';
+}
+
+KD_INLINE uint32_t esc_byte(uint32_t x) {          // \b \f \n \r \t; \" \\ \/ stand for themselves
+    switch (x) {
+    case 'b': return 0x08u;
+    case 'f': return 0x0Cu;
+    case 'n': return 0x0Au;
+    case 'r': return 0x0Du;
+    case 't': return 0x09u;
+    default: return x;
+    }
+}
+// ---------------------------------------------------------------- k_js_quotes
+__global__ void __launch_bounds__(BLOCK) k_js_quotes(JsDoc j, uint64_t* qmask, uint64_t* bsmask,
+                                                     uint64_t* hbmask, uint32_t* qcnt) {
+    const uint32_t b = blockIdx.x * BLOCK + threadIdx.x;
+    if (b >= j.nb) return;
+    uint32_t w[16];
+    load_block(j.doc, b, w);
+    uint64_t bs = 0, q = 0, hb = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        bs |= (uint64_t)mm4(eqb(w[k], '\\')) << (4 * k);
+        q |= (uint64_t)mm4(eqb(w[k], '"')) << (4 * k);
+        hb |= (uint64_t)mm4(w[k] & 0x80808080u) << (4 * k);
+    }
+    // is byte 0 escaped? an odd run of backslashes ends right before the block
+    bool pe = false;
+    if (b > 0 && j.doc[(size_t)b * 64 - 1] == '\\') {
+        uint64_t i = (uint64_t)b * 64 - 1, run = 0;
+        for (;;) {
+            if (j.doc[i] != '\\') break;
+            ++run;
+            if (i == 0) break;
+            --i;
+        }
+        pe = run & 1;
+    }
+    uint64_t esc = 0;
+    if (bs | (uint64_t)pe) {                  // escaped byte = one after an odd backslash run
+        bool e = pe;
+        for (int k = 0; k < 64; ++k) {
+            if (e) { esc |= 1ull << k; e = false; }
+            else if ((bs >> k) & 1) e = true;
+        }
+    }
+    const uint64_t quote = q & ~esc;
+    qmask[b] = quote;
+    bsmask[b] = bs;
+    hbmask[b] = hb;
+    qcnt[b] = __popcll(quote);
+}
+
+// ---------------------------------------------------------------- k_js_classify
+__global__ void __launch_bounds__(BLOCK) k_js_classify(JsDoc j, const uint64_t* qoff, JsMasks m,
+                                                       unsigned long long* err) {
+    const uint32_t b = blockIdx.x * BLOCK + threadIdx.x;
+    if (b >= j.nb) return;
+    uint32_t w[16];
+    load_block(j.doc, b, w);
+    uint64_t op = 0, cl = 0, pun = 0, ctl = 0, wsc = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const uint32_t lw = w[k] | 0x20202020u;            // '[' → '{', ']' → '}'
+        const uint32_t o = mm4(eqb(lw, '{')), c = mm4(eqb(lw, '}'));
+        op |= (uint64_t)o << (4 * k);
+        cl |= (uint64_t)c << (4 * k);
+        pun |= (uint64_t)(mm4(eqb(w[k], ':')) | mm4(eqb(w[k], ','))) << (4 * k);
+        ctl |= (uint64_t)mm4(ltb(w[k], 0x20)) << (4 * k);
+        wsc |= (uint64_t)mm4(ltb(w[k], 0x21)) << (4 * k);
+    }
+    const uint64_t quote = j.qmask[b];
+    const bool S = qoff[b] & 1;                            // inside a string at byte 0
+    const uint64_t instr = prefix_xor(quote) ^ (S ? ~0ull : 0ull);
+    const uint64_t out = ~instr;
+    const uint64_t structural = (op | cl | pun) & out;
+    const uint64_t str_open = quote & instr;
+    const uint64_t scalar = out & ~quote & ~wsc & ~(op | cl | pun);
+    bool prev_scalar = false;
+    if (b > 0 && !S) {
+        const uint32_t c = j.doc[(size_t)b * 64 - 1];
+        prev_scalar = !(c <= 0x20 || c == '"' || is_struct_byte(c));
+    }
+    const uint64_t scalar_start = scalar & ~((scalar << 1) | (uint64_t)prev_scalar);
+    const uint64_t tok = structural | str_open | scalar_start;
+    // control bytes: never inside a string; outside only \t \n \r
+    if (ctl) {
+        uint64_t bad = ctl & instr;
+        uint64_t octl = ctl & out;
+        while (octl) {
+            const int k = __ffsll((long long)octl) - 1;
+            octl &= octl - 1;
+            const uint32_t c = j.doc[(size_t)b * 64 + k];
+            if (c != '\t' && c != '\n' && c != '\r') bad |= 1ull << k;
+        }
+        if (bad) js_fail(err, b * 64 + (__ffsll((long long)bad) - 1), KDTN_JSON_SYNTAX);
+    }
+    m.tok[b] = tok;
+    m.open[b] = op & out;
+    m.close[b] = cl & out;
+    m.tcnt[b] = __popcll(tok);
+    m.dcnt[b] = 64u + __popcll(op & out) - __popcll(cl & out);
+}
+
+// ---------------------------------------------------------------- k_js_tokens
+KD_INLINE uint32_t kind_of(uint32_t c) {
+    switch (c) {
+    case '{': return TK_OBJ;
+    case '}': return TK_OBJ_END;
+    case '[': return TK_ARR;
+    case ']': return TK_ARR_END;
+    case ':': return TK_COLON;
+    case ',': return TK_COMMA;
+    case '"': return TK_STR;
+    default: return TK_SCALAR;
+    }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_js_tokens(JsDoc j, JsMasks m, const uint64_t* toff, const uint64_t* doff,
+                                                     uint2* toks, unsigned long long* err) {
+    const uint32_t b = blockIdx.x * BLOCK + threadIdx.x;
+    if (b >= j.nb) return;
+    uint64_t tok = m.tok[b];
+    if (!tok) return;
+    const uint64_t op = m.open[b], cl = m.close[b];
+    uint32_t idx = (uint32_t)toff[b];
+    const int64_t d0 = (int64_t)doff[b] - 64ll * b;
+    while (tok) {
+        const int k = __ffsll((long long)tok) - 1;
+        tok &= tok - 1;
+        const uint64_t below = (1ull << k) - 1;
+        int64_t d = d0 + __popcll(op & below) - __popcll(cl & below);
+        const uint32_t pos = b * 64 + k;
+        const uint32_t kind = kind_of(j.doc[pos]);
+        if (d < 0 || ((kind == TK_OBJ_END || kind == TK_ARR_END) && d < 1)) {
+            js_fail(err, pos, KDTN_JSON_SYNTAX);      // a close with nothing open
+            d = d < 0 ? 0 : d;
+        }
+        if ((kind == TK_OBJ || kind == TK_ARR) && d >= 10000) js_fail(err, pos, KDTN_JSON_DEPTH);
+        if (d > (int64_t)TK_DEPTH_MASK) d = TK_DEPTH_MASK;
+        toks[idx++] = make_uint2(pos, (uint32_t)d | (kind << 24));
+    }
+}
+
+// ---------------------------------------------------------------- parents
+// Per tile of JS_TILE tokens: lane d (0..JS_PD-1) = 1 + index of the last open bracket whose
+// post-depth is d + 1 (pre-depth d), 0 = none; combining is an element-wise max.
+KD_INLINE bool tk_open(uint32_t meta) {
+    const uint32_t k = meta >> 24;
+    return k == TK_OBJ || k == TK_ARR;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_js_par_agg(const uint2* toks, uint32_t ntok, uint32_t* tagg) {
+    __shared__ uint32_t sh[BLOCK * (JS_PD + 1)];
+    uint32_t* row = sh + threadIdx.x * (JS_PD + 1);
+#pragma unroll
+    for (int d = 0; d < JS_PD; ++d) row[d] = 0;
+    const uint32_t base = blockIdx.x * JS_TILE + threadIdx.x * JS_PER;
+    for (int k = 0; k < JS_PER; ++k) {
+        const uint32_t i = base + k;
+        if (i >= ntok) break;
+        const uint32_t meta = toks[i].y;
+        const uint32_t d = meta & TK_DEPTH_MASK;
+        if (tk_open(meta) && d < JS_PD) row[d] = i + 1;
+    }
+    __syncthreads();
+    if (threadIdx.x < JS_PD) {
+        uint32_t v = 0;
+        for (int t = 0; t < BLOCK; ++t) v = max(v, sh[t * (JS_PD + 1) + threadIdx.x]);
+        tagg[(size_t)blockIdx.x * JS_PD + threadIdx.x] = v;
+    }
+}
+
+// groups of BLOCK tiles: per-group max per lane
+__global__ void __launch_bounds__(BLOCK) k_js_par_group(const uint32_t* tagg, uint32_t ntiles, uint32_t* gagg) {
+    __shared__ uint32_t sh[BLOCK];
+    const int lane = threadIdx.x & (JS_PD - 1), part = threadIdx.x / JS_PD;   // 16 parts of 16 tiles
+    uint32_t v = 0;
+    for (int k = 0; k < BLOCK / (BLOCK / JS_PD); ++k) {
+        const uint32_t t = blockIdx.x * BLOCK + part * (BLOCK / (BLOCK / JS_PD)) + k;
+        if (t < ntiles) v = max(v, tagg[(size_t)t * JS_PD + lane]);
+    }
+    sh[threadIdx.x] = v;
+    __syncthreads();
+    if (threadIdx.x < JS_PD) {
+        uint32_t r = 0;
+        for (int p = 0; p < BLOCK / JS_PD; ++p) r = max(r, sh[p * JS_PD + threadIdx.x]);
+        gagg[(size_t)blockIdx.x * JS_PD + threadIdx.x] = r;
+    }
+}
+
+// single block: exclusive max-scan over the groups, in place
+__global__ void __launch_bounds__(BLOCK) k_js_par_top(uint32_t* gagg, uint32_t ng) {
+    __shared__ uint32_t sh[BLOCK];
+    const int lane = threadIdx.x & (JS_PD - 1), part = threadIdx.x / JS_PD;
+    constexpr int NP = BLOCK / JS_PD;
+    const uint32_t per = (ng + NP - 1) / NP;
+    const uint32_t g0 = part * per, g1 = min(ng, g0 + per);
+    uint32_t v = 0;
+    for (uint32_t g = g0; g < g1; ++g) v = max(v, gagg[(size_t)g * JS_PD + lane]);
+    sh[threadIdx.x] = v;
+    __syncthreads();
+    uint32_t run = 0;
+    for (int p = 0; p < part; ++p) run = max(run, sh[p * JS_PD + lane]);
+    for (uint32_t g = g0; g < g1; ++g) {
+        const uint32_t x = gagg[(size_t)g * JS_PD + lane];
+        gagg[(size_t)g * JS_PD + lane] = run;
+        run = max(run, x);
+    }
+}
+
+// within each group: exclusive max-scan over its tiles → texcl (in place over tagg)
+__global__ void __launch_bounds__(BLOCK) k_js_par_tiles(uint32_t* tagg, uint32_t ntiles, const uint32_t* gagg) {
+    __shared__ uint32_t sh[2][BLOCK * JS_PD];
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    uint32_t* cur = sh[0];
+    uint32_t* nxt = sh[1];
+#pragma unroll
+    for (int d = 0; d < JS_PD; ++d) cur[threadIdx.x * JS_PD + d] = t < ntiles ? tagg[(size_t)t * JS_PD + d] : 0u;
+    __syncthreads();
+    for (int off = 1; off < BLOCK; off <<= 1) {                  // inclusive Hillis-Steele
+#pragma unroll
+        for (int d = 0; d < JS_PD; ++d) {
+            uint32_t v = cur[threadIdx.x * JS_PD + d];
+            if ((int)threadIdx.x >= off) v = max(v, cur[(threadIdx.x - off) * JS_PD + d]);
+            nxt[threadIdx.x * JS_PD + d] = v;
+        }
+        __syncthreads();
+        uint32_t* tmp = cur; cur = nxt; nxt = tmp;
+    }
+    if (t < ntiles) {
+#pragma unroll
+        for (int d = 0; d < JS_PD; ++d) {
+            const uint32_t ex = threadIdx.x ? cur[(threadIdx.x - 1) * JS_PD + d] : 0u;
+            tagg[(size_t)t * JS_PD + d] = max(ex, gagg[(size_t)blockIdx.x * JS_PD + d]);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_js_par_apply(const uint2* toks, uint32_t ntok, const uint32_t* texcl,
+                                                        uint32_t* par) {
+    __shared__ uint32_t sh[2][BLOCK * JS_PD];
+    __shared__ uint32_t st[BLOCK * (JS_PD + 1)];
+    uint32_t* row = st + threadIdx.x * (JS_PD + 1);
+#pragma unroll
+    for (int d = 0; d < JS_PD; ++d) row[d] = 0;
+    const uint32_t base = blockIdx.x * JS_TILE + threadIdx.x * JS_PER;
+    for (int k = 0; k < JS_PER; ++k) {
+        const uint32_t i = base + k;
+        if (i >= ntok) break;
+        const uint32_t meta = toks[i].y;
+        const uint32_t d = meta & TK_DEPTH_MASK;
+        if (tk_open(meta) && d < JS_PD) row[d] = i + 1;
+    }
+    uint32_t* cur = sh[0];
+    uint32_t* nxt = sh[1];
+#pragma unroll
+    for (int d = 0; d < JS_PD; ++d) cur[threadIdx.x * JS_PD + d] = row[d];
+    __syncthreads();
+    for (int off = 1; off < BLOCK; off <<= 1) {
+#pragma unroll
+        for (int d = 0; d < JS_PD; ++d) {
+            uint32_t v = cur[threadIdx.x * JS_PD + d];
+            if ((int)threadIdx.x >= off) v = max(v, cur[(threadIdx.x - off) * JS_PD + d]);
+            nxt[threadIdx.x * JS_PD + d] = v;
+        }
+        __syncthreads();
+        uint32_t* tmp = cur; cur = nxt; nxt = tmp;
+    }
+#pragma unroll
+    for (int d = 0; d < JS_PD; ++d) {
+        const uint32_t ex = threadIdx.x ? cur[(threadIdx.x - 1) * JS_PD + d] : 0u;
+        row[d] = max(ex, texcl[(size_t)blockIdx.x * JS_PD + d]);
+    }
+    for (int k = 0; k < JS_PER; ++k) {
+        const uint32_t i = base + k;
+        if (i >= ntok) break;
+        const uint32_t meta = toks[i].y;
+        const uint32_t d = meta & TK_DEPTH_MASK;
+        uint32_t p = JS_NONE;
+        if (d >= 1 && d <= JS_PD) p = row[d - 1] - 1;          // 0 - 1 = JS_NONE (malformed)
+        else if (d > JS_PD) p = JS_DEEP;
+        par[i] = p;
+        if (tk_open(meta) && d < JS_PD) row[d] = i + 1;
+    }
+}
+
+// tokens nested deeper than JS_PD: nearest earlier token with a smaller pre-depth
+__global__ void __launch_bounds__(BLOCK) k_js_deep(const uint2* toks, uint32_t ntok, uint32_t* par) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= ntok || par[i] != JS_DEEP) return;
+    const uint32_t d = toks[i].y & TK_DEPTH_MASK;
+    uint32_t k = i;
+    while (k > 0) {
+        --k;
+        if ((toks[k].y & TK_DEPTH_MASK) < d) break;
+    }
+    par[i] = k;
+}
+
+// ---------------------------------------------------------------- validation
+KD_INLINE uint32_t tkind(uint2 t) { return t.y >> 24; }
+KD_INLINE uint32_t tdepth(uint2 t) { return t.y & TK_DEPTH_MASK; }
+KD_INLINE bool value_start(uint32_t k) { return k == TK_OBJ || k == TK_ARR || k == TK_STR || k == TK_SCALAR; }
+KD_INLINE bool is_hexc(uint32_t c) { return (c >= '0' && c <= '9') || ((c | 32) >= 'a' && (c | 32) <= 'f'); }
+
+// closing quote of the string literal whose opening quote is at pos
+KD_INLINE uint32_t str_end(const JsDoc& j, uint32_t pos) {
+    uint32_t b = (pos + 1) >> 6;
+    uint64_t w = j.qmask[b] & (~0ull << ((pos + 1) & 63));
+    while (!w) w = j.qmask[++b];
+    return b * 64 + (__ffsll((long long)w) - 1);
+}
+// any bit of mask[] in byte range [a, e)
+KD_INLINE bool any_in(const uint64_t* mask, uint32_t a, uint32_t e) {
+    if (a >= e) return false;
+    uint32_t b = a >> 6;
+    const uint32_t be = (e - 1) >> 6;
+    uint64_t w = mask[b] & (~0ull << (a & 63));
+    for (;;) {
+        if (b == be) {
+            const uint32_t hi = e - b * 64;                        // 1..64
+            if (hi < 64) w &= (1ull << hi) - 1;
+            return w != 0;
+        }
+        if (w) return true;
+        w = mask[++b];
+    }
+}
+KD_INLINE bool tk_key(const uint2* toks, const uint32_t* par, uint32_t i) {   // an object member name
+    if (i == 0 || tkind(toks[i]) != TK_STR) return false;
+    const uint32_t pk = tkind(toks[i - 1]);
+    if (pk != TK_OBJ && pk != TK_COMMA) return false;
+    const uint32_t p = par[i];
+    return p < JS_DEEP && tkind(toks[p]) == TK_OBJ;
+}
+
+KD_INLINE bool valid_scalar(const JsDoc& j, uint32_t pos) {
+    const uint8_t* s = j.doc;
+    const uint32_t n = j.n;
+    uint32_t i = pos;
+    auto term = [&](uint32_t k) {
+        if (k >= n) return true;
+        const uint32_t c = s[k];
+        return c <= 0x20 || c == '"' || is_struct_byte(c);
+    };
+    const uint32_t c0 = s[i];
+    if (c0 == 't') return i + 4 <= n && s[i + 1] == 'r' && s[i + 2] == 'u' && s[i + 3] == 'e' && term(i + 4);
+    if (c0 == 'f') return i + 5 <= n && s[i + 1] == 'a' && s[i + 2] == 'l' && s[i + 3] == 's' && s[i + 4] == 'e' && term(i + 5);
+    if (c0 == 'n') return i + 4 <= n && s[i + 1] == 'u' && s[i + 2] == 'l' && s[i + 3] == 'l' && term(i + 4);
+    if (i < n && s[i] == '-') ++i;
+    if (i >= n || !is_digit(s[i])) return false;
+    if (s[i] == '0') ++i;
+    else while (i < n && is_digit(s[i])) ++i;
+    if (i < n && s[i] == '.') {
+        ++i;
+        if (i >= n || !is_digit(s[i])) return false;
+        while (i < n && is_digit(s[i])) ++i;
+    }
+    if (i < n && (s[i] == 'e' || s[i] == 'E')) {
+        ++i;
+        if (i < n && (s[i] == '+' || s[i] == '-')) ++i;
+        if (i >= n || !is_digit(s[i])) return false;
+        while (i < n && is_digit(s[i])) ++i;
+    }
+    return term(i);
+}
+
+__global__ void __launch_bounds__(BLOCK) k_js_validate(JsDoc j, const uint2* toks, uint32_t ntok, const uint32_t* par,
+                                                       unsigned long long* err) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= ntok) return;
+    const uint2 t = toks[i];
+    const uint32_t kind = tkind(t), d = tdepth(t), pos = t.x;
+    const uint32_t p = par[i];
+    const uint32_t ck = d == 0 ? 0xFFu : (p < JS_DEEP ? tkind(toks[p]) : 0xFEu);   // container kind
+    bool ok;
+    if (i == 0) {
+        ok = value_start(kind) && d == 0;
+    } else {
+        if (d == 0) ok = false;                                   // a second top-level value
+        else {
+            const uint32_t pk = tkind(toks[i - 1]);
+            switch (pk) {
+            case TK_OBJ: ok = kind == TK_STR || kind == TK_OBJ_END; break;
+            case TK_ARR: ok = value_start(kind) || kind == TK_ARR_END; break;
+            case TK_COLON: ok = value_start(kind); break;
+            case TK_COMMA: ok = ck == TK_OBJ ? kind == TK_STR : (ck == TK_ARR && value_start(kind)); break;
+            case TK_STR:
+                if (tk_key(toks, par, i - 1)) { ok = kind == TK_COLON; break; }
+                [[fallthrough]];
+            default:                                              // after a value
+                ok = kind == TK_COMMA || kind == TK_OBJ_END || kind == TK_ARR_END;
+            }
+        }
+        if (ok && kind == TK_OBJ_END) ok = ck == TK_OBJ;
+        if (ok && kind == TK_ARR_END) ok = ck == TK_ARR;
+    }
+    if (ok && i == ntok - 1) {                                    // the document ends here
+        ok = (kind == TK_STR || kind == TK_SCALAR) ? d == 0 : ((kind == TK_OBJ_END || kind == TK_ARR_END) && d == 1);
+    }
+    if (ok && kind == TK_SCALAR) ok = valid_scalar(j, pos);
+    if (ok && kind == TK_STR) {
+        const uint32_t e = str_end(j, pos);
+        if (any_in(j.bsmask, pos + 1, e)) {                       // escapes: \" \\ \/ \b \f \n \r \t \uXXXX
+            for (uint32_t k = pos + 1; k < e && ok; ++k) {
+                if (j.doc[k] != '\\') continue;
+                const uint32_t c = j.doc[k + 1];
+                if (c == 'u') {
+                    ok = k + 5 < e && is_hexc(j.doc[k + 2]) && is_hexc(j.doc[k + 3]) && is_hexc(j.doc[k + 4]) &&
+                         is_hexc(j.doc[k + 5]);
+                    k += 5;
+                } else {
+                    ok = c == '"' || c == '\\' || c == '/' || c == 'b' || c == 'f' || c == 'n' || c == 'r' || c == 't';
+                    k += 1;
+                }
+            }
+        }
+    }
+    if (!ok) js_fail(err, pos, KDTN_JSON_SYNTAX);
+}
+
+// ---------------------------------------------------------------- key matching
+// Decodes the member name at string token pos (escapes included) and returns the index of
+// the equal name in names[0..n), or -1. Names are ASCII and at most 15 bytes.
+KD_INLINE int match_key(const JsDoc& j, uint32_t pos, const char (*names)[16], int n) {
+    char buf[16];
+    int len = 0;
+    const uint32_t e = str_end(j, pos);
+    if (e - pos - 1 > 6 * 16) return -1;
+    for (uint32_t k = pos + 1; k < e; ++k) {
+        uint32_t c = j.doc[k];
+        if (c == '\\') {
+            const uint32_t x = j.doc[k + 1];
+            if (x == 'u') {
+                uint32_t r = 0;
+                for (int q = 2; q < 6; ++q) {
+                    const uint32_t h = j.doc[k + q];
+                    r = r * 16 + (h <= '9' ? h - '0' : (h | 32) - 'a' + 10);
+                }
+                if (r >= 0x80) return -1;
+                c = r;
+                k += 5;
+            } else {
+                c = esc_byte(x);
+                k += 1;
+            }
+        } else if (c >= 0x80) {
+            return -1;
+        }
+        if (len >= 15) return -1;
+        buf[len++] = (char)c;
+    }
+    for (int f = 0; f < n; ++f) {
+        const char* s = names[f];
+        int q = 0;
+        while (q < len && s[q] == buf[q]) ++q;
+        if (q == len && s[q] == 0) return f;
+    }
+    return -1;
+}
+
+__constant__ char kItems[1][16] = {"items"};
+__constant__ char kItem[3][16] = {"metadata", "spec", "status"};
+__constant__ char kMeta[2][16] = {"name", "namespace"};
+__constant__ char kLinks[1][16] = {"links"};
+__constant__ char kStatus[3][16] = {"links", "src_ip", "net_ns"};
+__constant__ char kLink[KDTN_NKEY + 2][16] = {"local_intf", "local_ip", "local_mac", "peer_intf", "peer_ip",
+                                              "peer_mac", "peer_pod", "uid", "properties"};
+__constant__ char kProps[KDTN_NPROP + 1][16] = {"latency", "latency_corr", "jitter", "loss", "loss_corr", "rate",
+                                                "duplicate", "duplicate_corr", "reorder_prob", "reorder_corr",
+                                                "corrupt_prob", "corrupt_corr", "gap"};
+
+// ---------------------------------------------------------------- roles
+// role of the container c whose enclosing container has role r (c is the child token)
+KD_INLINE uint32_t child_role(const JsDoc& j, const uint2* toks, uint32_t r, uint32_t c) {
+    const uint32_t kind = tkind(toks[c]);
+    const bool member = tkind(toks[c - 1]) == TK_COLON;
+    if (!member) {                                                // array element
+        if (kind != TK_OBJ) return R_NONE;
+        return r == R_ITEMS ? R_ITEM : r == R_SPEC_LINKS ? R_LINK_S : r == R_STATUS_LINKS ? R_LINK_R : R_NONE;
+    }
+    const uint32_t kpos = toks[c - 2].x;
+    switch (r) {
+    case R_ROOT:
+        return (kind == TK_ARR && match_key(j, kpos, kItems, 1) == 0) ? R_ITEMS : R_NONE;
+    case R_ITEM: {
+        if (kind != TK_OBJ) return R_NONE;
+        const int f = match_key(j, kpos, kItem, 3);
+        return f == 0 ? R_META : f == 1 ? R_SPEC : f == 2 ? R_STATUS : R_NONE;
+    }
+    case R_SPEC:
+        return (kind == TK_ARR && match_key(j, kpos, kLinks, 1) == 0) ? R_SPEC_LINKS : R_NONE;
+    case R_STATUS:
+        return (kind == TK_ARR && match_key(j, kpos, kLinks, 1) == 0) ? R_STATUS_LINKS : R_NONE;
+    case R_LINK_S:
+    case R_LINK_R:
+        return (kind == TK_OBJ && match_key(j, kpos, kLink, KDTN_NKEY + 2) == KDTN_NKEY + 1)
+                   ? (r == R_LINK_S ? R_PROPS_S : R_PROPS_R) : R_NONE;
+    default:
+        return R_NONE;
+    }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_js_roles(JsDoc j, const uint2* toks, uint32_t ntok, const uint32_t* par,
+                                                    uint8_t* role) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= ntok) return;
+    const uint2 t = toks[i];
+    if (!tk_open(t.y)) return;
+    const uint32_t d = tdepth(t);
+    uint32_t r = R_NONE;
+    if (d <= 6) {
+        uint32_t chain[7];
+        uint32_t c = i;
+        for (int k = (int)d; k >= 0; --k) {                       // chain[k] = ancestor at depth k
+            chain[k] = c;
+            if (k) c = par[c];
+        }
+        r = tkind(toks[chain[0]]) == TK_OBJ ? R_ROOT : R_NONE;
+        for (uint32_t k = 1; k <= d && r != R_NONE; ++k) r = child_role(j, toks, r, chain[k]);
+    }
+    role[i] = (uint8_t)r;
+}
+
+// ---------------------------------------------------------------- element ordinals
+// class of token i: 1 + {0 items element, 1 spec.links element, 2 status.links element}, or 0
+KD_INLINE uint32_t elem_class(const uint2* toks, const uint32_t* par, const uint8_t* role, uint32_t i) {
+    if (i == 0) return 0;
+    const uint32_t pk = tkind(toks[i - 1]);
+    if (pk != TK_ARR && pk != TK_COMMA) return 0;
+    if (!value_start(tkind(toks[i]))) return 0;
+    const uint32_t p = par[i];
+    if (p >= JS_DEEP || tkind(toks[p]) != TK_ARR) return 0;
+    const uint32_t r = role[p];
+    return r == R_ITEMS ? 1 : r == R_SPEC_LINKS ? 2 : r == R_STATUS_LINKS ? 3 : 0;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_js_elems_count(JsDoc j, const uint2* toks, uint32_t ntok, const uint32_t* par,
+                                                          const uint8_t* role, uint32_t* cnt3,
+                                                          unsigned long long* derr) {
+    __shared__ uint32_t sh[3];
+    if (threadIdx.x < 3) sh[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t c[3] = {0, 0, 0};
+    const uint32_t base = blockIdx.x * JS_TILE + threadIdx.x * JS_PER;
+    if (base == 0 && ntok) {                                      // the document must be an object or null
+        const uint2 t = toks[0];
+        if (!(tkind(t) == TK_OBJ || (tkind(t) == TK_SCALAR && j.doc[t.x] == 'n'))) js_fail(derr, t.x, KDTN_JSON_TYPE);
+    }
+    for (int k = 0; k < JS_PER; ++k) {
+        const uint32_t i = base + k;
+        if (i >= ntok) break;
+        const uint32_t cls = elem_class(toks, par, role, i);
+        if (!cls) continue;
+        const uint2 t = toks[i];
+        const uint32_t kind = tkind(t);
+        if (!(kind == TK_OBJ || (kind == TK_SCALAR && j.doc[t.x] == 'n'))) js_fail(derr, t.x, KDTN_JSON_TYPE);
+        c[cls - 1]++;
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+        if (c[q]) atomicAdd(&sh[q], c[q]);
+    __syncthreads();
+    if (threadIdx.x < 3) cnt3[(size_t)threadIdx.x * gridDim.x + blockIdx.x] = sh[threadIdx.x];
+}
+
+__global__ void __launch_bounds__(BLOCK) k_js_elems_write(const uint2* toks, uint32_t ntok, const uint32_t* par,
+                                                          const uint8_t* role, const uint64_t* coff3, uint32_t ntiles,
+                                                          uint32_t* ord, JsTopoOut to) {
+    __shared__ uint64_t sh[BLOCK / 64];
+    uint32_t c[3] = {0, 0, 0};
+    const uint32_t base = blockIdx.x * JS_TILE + threadIdx.x * JS_PER;
+    for (int k = 0; k < JS_PER; ++k) {
+        const uint32_t i = base + k;
+        if (i >= ntok) break;
+        const uint32_t cls = elem_class(toks, par, role, i);
+        if (cls) c[cls - 1]++;
+    }
+    uint32_t run[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        uint64_t tot;
+        run[q] = (uint32_t)(coff3[(size_t)q * (ntiles + 1) + blockIdx.x] + block_exclusive(c[q], sh, &tot));
+    }
+    for (int k = 0; k < JS_PER; ++k) {
+        const uint32_t i = base + k;
+        if (i >= ntok) break;
+        const uint32_t cls = elem_class(toks, par, role, i);
+        if (!cls) continue;
+        const uint32_t o = run[cls - 1]++;
+        ord[i] = o;
+        if (cls == 1) {                                            // a Topology: its record offsets
+            to.des_off[o] = run[1];
+            to.real_off[o] = run[2];
+        }
+    }
+}
+
+// ---------------------------------------------------------------- schema values
+KD_INLINE uint64_t fnv_step(uint64_t h, uint32_t c) { return (h ^ c) * 1099511628211ull; }
+
+// utf8.DecodeRune length of a valid sequence at s (bounded by e), 0 = invalid
+KD_INLINE uint32_t utf8_len(const uint8_t* s, const uint8_t* e) {
+    const uint32_t c = s[0];
+    uint32_t need, lo = 0x80, hi = 0xBF;
+    if (c >= 0xC2 && c <= 0xDF) need = 1;
+    else if (c == 0xE0) { need = 2; lo = 0xA0; }
+    else if (c >= 0xE1 && c <= 0xEC) need = 2;
+    else if (c == 0xED) { need = 2; hi = 0x9F; }
+    else if (c >= 0xEE && c <= 0xEF) need = 2;
+    else if (c == 0xF0) { need = 3; lo = 0x90; }
+    else if (c >= 0xF1 && c <= 0xF3) need = 3;
+    else if (c == 0xF4) { need = 3; hi = 0x8F; }
+    else return 0;
+    if ((uint32_t)(e - s) < need + 1) return 0;
+    if (s[1] < lo || s[1] > hi) return 0;
+    for (uint32_t k = 2; k <= need; ++k)
+        if (s[k] < 0x80 || s[k] > 0xBF) return 0;
+    return need + 1;
+}
+KD_INLINE int hex4(const uint8_t* p, const uint8_t* e) {         // getu4
+    if (e - p < 6 || p[0] != '\\' || p[1] != 'u') return -1;
+    int r = 0;
+    for (int k = 2; k < 6; ++k) {
+        const uint32_t h = p[k];
+        if (!is_hexc(h)) return -1;
+        r = r * 16 + (int)(h <= '9' ? h - '0' : (h | 32) - 'a' + 10);
+    }
+    return r;
+}
+KD_INLINE uint32_t rune_len(uint32_t r) { return r < 0x80 ? 1 : r < 0x800 ? 2 : r < 0x10000 ? 3 : 4; }
+KD_INLINE uint32_t put_rune(uint8_t* o, uint32_t r) {
+    if (r < 0x80) { o[0] = (uint8_t)r; return 1; }
+    if (r < 0x800) { o[0] = (uint8_t)(0xC0 | (r >> 6)); o[1] = (uint8_t)(0x80 | (r & 63)); return 2; }
+    if (r < 0x10000) {
+        o[0] = (uint8_t)(0xE0 | (r >> 12)); o[1] = (uint8_t)(0x80 | ((r >> 6) & 63)); o[2] = (uint8_t)(0x80 | (r & 63));
+        return 3;
+    }
+    o[0] = (uint8_t)(0xF0 | (r >> 18)); o[1] = (uint8_t)(0x80 | ((r >> 12) & 63));
+    o[2] = (uint8_t)(0x80 | ((r >> 6) & 63)); o[3] = (uint8_t)(0x80 | (r & 63));
+    return 4;
+}
+// \uXXXX at d[r] (with a following low surrogate when it pairs): the rune, r advanced past it;
+// lone or unpaired surrogates become U+FFFD (utf16.DecodeRune, encoding/json unquote)
+KD_INLINE uint32_t u_escape(const uint8_t* d, uint32_t& r, uint32_t e) {
+    int rr = hex4(d + r, d + e);
+    r += 6;
+    if (rr >= 0xD800 && rr < 0xE000) {
+        const int r1 = hex4(d + r, d + e);
+        if (rr < 0xDC00 && r1 >= 0xDC00 && r1 < 0xE000) {
+            r += 6;
+            return (uint32_t)((((rr - 0xD800) << 10) | (r1 - 0xDC00)) + 0x10000);
+        }
+        return 0xFFFDu;
+    }
+    return (uint32_t)rr;
+}
+// encoding/json unquote of the literal content d[a, e): decoded length (pass 1) and bytes
+// (pass 2). Invalid UTF-8 bytes become U+FFFD (3 bytes each).
+KD_INLINE uint32_t unquote_len(const uint8_t* d, uint32_t a, uint32_t e) {
+    uint32_t w = 0, r = a;
+    while (r < e) {
+        const uint32_t c = d[r];
+        if (c == '\\') {
+            if (d[r + 1] == 'u') w += rune_len(u_escape(d, r, e));
+            else { w += 1; r += 2; }
+        } else if (c < 0x80) {
+            w += 1;
+            r += 1;
+        } else {
+            const uint32_t k = utf8_len(d + r, d + e);
+            w += k ? k : 3u;
+            r += k ? k : 1u;
+        }
+    }
+    return w;
+}
+KD_INLINE void unquote_write(const uint8_t* d, uint32_t a, uint32_t e, uint8_t* out) {
+    uint32_t w = 0, r = a;
+    while (r < e) {
+        const uint32_t c = d[r];
+        if (c == '\\') {
+            if (d[r + 1] == 'u') w += put_rune(out + w, u_escape(d, r, e));
+            else { out[w++] = (uint8_t)esc_byte(d[r + 1]); r += 2; }
+        } else if (c < 0x80) {
+            out[w++] = (uint8_t)c;
+            r += 1;
+        } else {
+            const uint32_t k = utf8_len(d + r, d + e);
+            if (k) {
+                for (uint32_t q = 0; q < k; ++q) out[w + q] = d[r + q];
+                w += k;
+                r += k;
+            } else {
+                w += put_rune(out + w, 0xFFFDu);
+                r += 1;
+            }
+        }
+    }
+}
+
+// intern table key word: [63:57] hash tag | [56] heap | [55:32] length | [31:0] offset
+KD_INLINE const uint8_t* key_bytes(const JsIntern& in, uint64_t kw) {
+    return ((kw >> 56) & 1 ? in.heap : in.doc) + (uint32_t)kw;
+}
+
+// returns the table slot of the string [p, p+len) (len ≥ 1), or JS_NONE on overflow
+KD_INLINE uint32_t intern(const JsIntern& in, const JsDict& dt, const uint8_t* p, uint32_t len, uint64_t kw_self,
+                          uint64_t h, uint32_t occ) {
+    const uint64_t tag = h >> 57;
+    const uint64_t kw = (tag << 57) | kw_self;
+    uint32_t s = (uint32_t)h & dt.mask;
+    for (uint32_t probe = 0; probe <= dt.mask; ++probe) {
+        unsigned long long cur = __hip_atomic_load(dt.slots + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == 0) {
+            if ((kw >> 56) & 1) __threadfence();       // heap bytes visible before the key
+            cur = atomicCAS(dt.slots + s, 0ull, (unsigned long long)kw);
+            if (cur == 0) {
+                if (atomicAdd(dt.fill, 1u) >= dt.limit) atomicOr(in.status, JS_ST_OVERFLOW);
+                atomicMin(dt.rep + s, occ);
+                return s;
+            }
+        }
+        if ((cur >> 57) == tag && ((cur >> 32) & 0xFFFFFFu) == len) {
+            uint32_t k = 0;
+            if ((cur >> 56) & 1) {                    // heap bytes of another thread: coherent loads
+                const uint32_t off = (uint32_t)cur;
+                while (k < len) {
+                    const uint32_t wd = __hip_atomic_load(reinterpret_cast<const uint32_t*>(in.heap) + ((off + k) >> 2),
+                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (((wd >> (8 * ((off + k) & 3))) & 0xFFu) != p[k]) break;
+                    ++k;
+                }
+            } else {
+                const uint8_t* q = in.doc + (uint32_t)cur;
+                while (k < len && q[k] == p[k]) ++k;
+            }
+            if (k == len) {
+                atomicMin(dt.rep + s, occ);
+                return s;
+            }
+        }
+        s = (s + 1) & dt.mask;
+    }
+    atomicOr(in.status, JS_ST_OVERFLOW);
+    return JS_NONE;
+}
+
+// string value at token i → 1 + table slot (0 = empty string); JS_NONE on overflow
+KD_INLINE uint32_t string_slot(const JsDoc& j, const JsIntern& in, const JsDict& dt, uint32_t i, uint32_t pos) {
+    const uint32_t e = str_end(j, pos);
+    const uint32_t a = pos + 1;
+    if (e == a) return 0;
+    if (!any_in(j.bsmask, a, e) && !any_in(j.hbmask, a, e)) {     // plain ASCII: the bytes themselves
+        const uint32_t len = e - a;
+        if (len > 0xFFFFFFu) { atomicOr(in.status, JS_ST_LONG); return JS_NONE; }
+        uint64_t h = 1469598103934665603ull;
+        for (uint32_t k = a; k < e; ++k) h = fnv_step(h, j.doc[k]);
+        h ^= h >> 29;
+        const uint32_t s = intern(in, dt, j.doc + a, len, ((uint64_t)len << 32) | a, h, i);
+        return s == JS_NONE ? JS_NONE : s + 1;
+    }
+    const uint32_t len = unquote_len(j.doc, a, e);
+    if (len == 0) return 0;
+    if (len > 0xFFFFFFu) { atomicOr(in.status, JS_ST_LONG); return JS_NONE; }
+    const unsigned long long at = atomicAdd(in.heap_used, (unsigned long long)((len + 3) & ~3u));
+    if (at + len > in.heap_cap) { atomicOr(in.status, JS_ST_OVERFLOW); return JS_NONE; }
+    uint8_t* out = in.heap + at;
+    unquote_write(j.doc, a, e, out);
+    uint64_t h = 1469598103934665603ull;
+    for (uint32_t k = 0; k < len; ++k) h = fnv_step(h, out[k]);
+    h ^= h >> 29;
+    const uint32_t s = intern(in, dt, out, len, (1ull << 56) | ((uint64_t)len << 32) | (uint32_t)at, h, i);
+    return s == JS_NONE ? JS_NONE : s + 1;
+}
+
+// strconv.ParseInt(s, 10, 64) / ParseUint + uint32 overflow on the scalar at pos
+KD_INLINE bool parse_int64(const JsDoc& j, uint32_t pos, int64_t* out) {
+    uint32_t i = pos;
+    const bool neg = j.doc[i] == '-';
+    if (neg) ++i;
+    uint64_t v = 0;
+    uint32_t nd = 0;
+    for (; i < j.n; ++i) {
+        const uint32_t c = j.doc[i];
+        if (c <= 0x20 || c == ',' || c == '}' || c == ']') break;
+        if (!is_digit(c)) return false;
+        if (v > (~0ull - 9) / 10) return false;
+        v = v * 10 + (c - '0');
+        if (v > (1ull << 63)) return false;
+        ++nd;
+    }
+    if (!nd || (!neg && v > 0x7FFFFFFFFFFFFFFFull)) return false;
+    *out = neg ? (int64_t)(0ull - v) : (int64_t)v;
+    return true;
+}
+KD_INLINE bool parse_uint32(const JsDoc& j, uint32_t pos, uint32_t* out) {
+    uint64_t v = 0;
+    uint32_t nd = 0;
+    for (uint32_t i = pos; i < j.n; ++i) {
+        const uint32_t c = j.doc[i];
+        if (c <= 0x20 || c == ',' || c == '}' || c == ']') break;
+        if (!is_digit(c)) return false;
+        v = v * 10 + (c - '0');
+        if (v > 0xFFFFFFFFull) return false;
+        ++nd;
+    }
+    if (!nd) return false;
+    *out = (uint32_t)v;
+    return true;
+}
+
+KD_INLINE uint32_t* store_word(const JsStore& st, uint32_t rec, int col) {
+    return st.base + (size_t)(rec >> 6) * TILE_WORDS + col * TILE_RECS + (rec & 63u);
+}
+
+__global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, const uint2* toks, uint32_t ntok, const uint32_t* par,
+                                                     const uint8_t* role, const uint32_t* ord, JsTopoOut to,
+                                                     JsStore des, JsStore real, JsIntern in, unsigned long long* derr) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i < 2 || i >= ntok) return;
+    if (tkind(toks[i - 1]) != TK_COLON) return;
+    const uint32_t o = par[i];
+    if (o >= JS_DEEP) return;
+    const uint32_t r = role[o];
+    if (r == R_NONE || r == R_ITEMS || r == R_SPEC_LINKS || r == R_STATUS_LINKS) return;
+    const uint2 t = toks[i];
+    const uint32_t kind = tkind(t), kpos = toks[i - 2].x;
+    const bool null = kind == TK_SCALAR && j.doc[t.x] == 'n';
+    uint32_t* seen;
+    int f, bit;
+    uint32_t topo = 0, rec = 0;
+    const JsStore* st = nullptr;
+    switch (r) {
+    case R_ROOT:
+        f = match_key(j, kpos, kItems, 1);
+        seen = in.seen_root; bit = f;
+        break;
+    case R_ITEM:
+        f = match_key(j, kpos, kItem, 3);
+        topo = ord[o]; seen = to.seen + topo; bit = f;
+        break;
+    case R_META:
+        f = match_key(j, kpos, kMeta, 2);
+        topo = ord[par[o]]; seen = to.seen + topo; bit = 3 + f;
+        break;
+    case R_SPEC:
+        f = match_key(j, kpos, kLinks, 1);
+        topo = ord[par[o]]; seen = to.seen + topo; bit = 5 + f;
+        break;
+    case R_STATUS:
+        f = match_key(j, kpos, kStatus, 3);
+        topo = ord[par[o]]; seen = to.seen + topo; bit = 6 + f;
+        break;
+    case R_LINK_S:
+    case R_LINK_R:
+        f = match_key(j, kpos, kLink, KDTN_NKEY + 2);
+        st = r == R_LINK_S ? &des : &real;
+        rec = ord[o]; seen = st->seen + rec; bit = f;
+        break;
+    default: {                                                    // R_PROPS_S / R_PROPS_R
+        f = match_key(j, kpos, kProps, KDTN_NPROP + 1);
+        st = r == R_PROPS_S ? &des : &real;
+        rec = ord[par[o]]; seen = st->seen + rec; bit = 9 + f;
+        break;
+    }
+    }
+    if (f < 0) return;
+    if (atomicOr(seen, 1u << bit) & (1u << bit)) {
+        js_fail(derr, kpos, KDTN_JSON_DUPKEY);
+        return;
+    }
+    bool ok = true;
+    switch (r) {
+    case R_ROOT: ok = null || kind == TK_ARR; break;
+    case R_ITEM: ok = null || kind == TK_OBJ; break;
+    case R_SPEC:
+    case R_STATUS:
+        if (r == R_SPEC || f == 0) {                              // links
+            ok = null || kind == TK_ARR;
+            if (kind == TK_ARR) atomicAnd(to.flags + topo, r == R_SPEC ? ~(uint32_t)KDTN_TOPO_SPEC_NIL : ~(uint32_t)KDTN_TOPO_STATUS_NIL);
+            break;
+        }
+        [[fallthrough]];
+    case R_META: {
+        if (null) break;
+        if (kind != TK_STR) { ok = false; break; }
+        const uint32_t v = string_slot(j, in, in.kd, i, t.x);
+        if (v == JS_NONE) return;
+        uint32_t* dst = r == R_META ? (f == 0 ? to.name : to.ns) : (f == 1 ? to.src_ip : to.net_ns);
+        dst[topo] = v;
+        break;
+    }
+    default: {                                                    // link / properties fields
+        const bool props = r == R_PROPS_S || r == R_PROPS_R;
+        if (!props && f == KDTN_NKEY + 1) { ok = null || kind == TK_OBJ; break; }   // properties
+        if (!props && f == KDTN_NKEY) {                                           // uid
+            if (null) break;
+            int64_t v;
+            ok = kind == TK_SCALAR && parse_int64(j, t.x, &v);
+            if (ok) {
+                uint32_t* w = store_word(*st, rec, COL_UID) - (rec & 63u);        // i64 column of the tile
+                reinterpret_cast<int64_t*>(w)[rec & 63u] = v;
+            }
+            break;
+        }
+        if (props && f == KDTN_NPROP) {                                           // gap
+            if (null) break;
+            uint32_t v;
+            ok = kind == TK_SCALAR && parse_uint32(j, t.x, &v);
+            if (ok) *store_word(*st, rec, COL_GAP) = v;
+            break;
+        }
+        if (null) break;
+        if (kind != TK_STR) { ok = false; break; }
+        const uint32_t v = string_slot(j, in, props ? in.pd : in.kd, i, t.x);
+        if (v == JS_NONE) return;
+        *store_word(*st, rec, props ? COL_PROP0 + f : COL_KEY0 + f) = v;
+        break;
+    }
+    }
+    if (!ok) js_fail(derr, t.x, KDTN_JSON_TYPE);
+}
+
+// ---------------------------------------------------------------- ids in first-occurrence order
+__global__ void __launch_bounds__(BLOCK) k_js_rep_mark(JsDict dt, uint32_t* bits) {
+    const uint32_t s = blockIdx.x * BLOCK + threadIdx.x;
+    if (s > dt.mask || dt.slots[s] == 0) return;
+    const uint32_t occ = dt.rep[s];
+    atomicOr(bits + (occ >> 5), 1u << (occ & 31));
+}
+
+__global__ void __launch_bounds__(BLOCK) k_js_popc(const uint32_t* bits, uint32_t nw, uint32_t* cnt) {
+    const uint32_t w = blockIdx.x * BLOCK + threadIdx.x;
+    if (w < nw) cnt[w] = __popc(bits[w]);
+}
+
+// per slot: id = 1 + rank of its first occurrence; length by id
+__global__ void __launch_bounds__(BLOCK) k_js_ids(JsDict dt, const uint32_t* bits, const uint64_t* wrank,
+                                                  uint32_t* slot_id, uint32_t* len_by_id) {
+    const uint32_t s = blockIdx.x * BLOCK + threadIdx.x;
+    if (s > dt.mask) return;
+    const unsigned long long kw = dt.slots[s];
+    if (kw == 0) return;
+    const uint32_t occ = dt.rep[s];
+    const uint32_t id = 1u + (uint32_t)wrank[occ >> 5] + __popc(bits[occ >> 5] & ((1u << (occ & 31)) - 1u));
+    slot_id[s] = id;
+    len_by_id[id] = (uint32_t)(kw >> 32) & 0xFFFFFFu;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_js_dict_copy(JsDict dt, JsIntern in, const uint32_t* slot_id,
+                                                        const uint64_t* off64, uint32_t* offs, uint8_t* arena) {
+    const uint32_t s = blockIdx.x * BLOCK + threadIdx.x;
+    if (s > dt.mask) return;
+    const unsigned long long kw = dt.slots[s];
+    if (kw == 0) return;
+    const uint32_t id = slot_id[s];
+    const uint32_t len = (uint32_t)(kw >> 32) & 0xFFFFFFu;
+    const uint64_t at = off64[id];
+    offs[id] = (uint32_t)at;
+    const uint8_t* src = key_bytes(in, kw);
+    for (uint32_t k = 0; k < len; ++k) arena[at + k] = src[k];
+}
+
+// slot + 1 → id in every id column; topology flags to bytes
+__global__ void __launch_bounds__(BLOCK) k_js_finalize_links(JsStore st, uint32_t n, const uint32_t* kslot_id,
+                                                             const uint32_t* pslot_id) {
+    constexpr uint32_t IDW = (KDTN_NKEY + KDTN_NPROP) * TILE_RECS;   // id words per tile
+    const uint64_t g = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    const uint64_t tile = g / IDW;
+    const uint32_t r = (uint32_t)(g % IDW), col = r / TILE_RECS, lane = r % TILE_RECS;
+    if (tile * TILE_RECS + lane >= n) return;
+    uint32_t* w = st.base + tile * TILE_WORDS + r;
+    const uint32_t v = *w;
+    if (v) *w = (col < KDTN_NKEY ? kslot_id : pslot_id)[v - 1];
+}
+
+__global__ void __launch_bounds__(BLOCK) k_js_finalize_topos(JsTopoOut to, uint32_t T, const uint32_t* kslot_id,
+                                                             uint8_t* flags8) {
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= T) return;
+    uint32_t* cols[4] = {to.ns, to.name, to.src_ip, to.net_ns};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t v = cols[k][t];
+        if (v) cols[k][t] = kslot_id[v - 1];
+    }
+    flags8[t] = (uint8_t)to.flags[t];
+}
+
+}  // namespace kdtn

@@ -281,4 +281,89 @@ __global__ void k_wire_write(WireIn w, DevLinks O, DevLinks N, WireWork wk, uint
 __global__ void k_qdisc_batch(DevLinks props, DevTables tb, uint2* out);
 __global__ void k_full_prefix(DevTopos T, uint32_t* first_partial);
 
+// ---- CR ingest: TopologyList JSON → epoch tables (kdtn_ingest.hip) ------------------------
+// token word: {byte offset, pre-depth | kind << 24}
+enum : uint32_t { TK_OBJ = 0, TK_OBJ_END = 1, TK_ARR = 2, TK_ARR_END = 3, TK_COLON = 4, TK_COMMA = 5,
+                  TK_STR = 6, TK_SCALAR = 7 };
+constexpr uint32_t TK_DEPTH_MASK = 0xFFFFFFu;
+constexpr int JS_PD = 16;                    // depth levels resolved by the parent max-scan
+constexpr int JS_PER = 16;                   // tokens per thread in tile kernels
+constexpr int JS_TILE = BLOCK * JS_PER;      // tokens per tile
+constexpr uint32_t JS_NONE = 0xFFFFFFFFu, JS_DEEP = 0xFFFFFFFEu;
+// container roles on the TopologyList schema
+enum : uint32_t { R_NONE = 0, R_ROOT, R_ITEMS, R_ITEM, R_META, R_SPEC, R_STATUS, R_SPEC_LINKS, R_STATUS_LINKS,
+                  R_LINK_S, R_LINK_R, R_PROPS_S, R_PROPS_R };
+constexpr uint32_t JS_ST_OVERFLOW = 1, JS_ST_LONG = 2;   // intern status bits
+
+struct JsDoc {
+    const uint8_t* doc;        // padded with spaces to nb*64 (+64 B)
+    uint32_t n;                // document bytes
+    uint32_t nb;               // 64-byte blocks
+    const uint64_t* qmask;     // unescaped quotes
+    const uint64_t* bsmask;    // backslashes
+    const uint64_t* hbmask;    // bytes >= 0x80
+};
+struct JsMasks {
+    uint64_t* tok;             // token starts
+    uint64_t* open;            // { [ outside strings
+    uint64_t* close;           // } ] outside strings
+    uint32_t* tcnt;            // tokens per block
+    uint32_t* dcnt;            // 64 + opens - closes per block
+};
+struct JsTopoOut {
+    uint32_t* ns;
+    uint32_t* name;
+    uint32_t* src_ip;
+    uint32_t* net_ns;
+    uint32_t* flags;           // u32 KDTN_TOPO_* bits during the decode
+    uint32_t* real_off;
+    uint32_t* des_off;
+    uint32_t* seen;            // schema fields met per topology (duplicate check)
+};
+struct JsStore {
+    uint32_t* base;            // AoSoA link store (DevLinks layout)
+    uint32_t* seen;            // schema fields met per record
+};
+struct JsDict {
+    unsigned long long* slots; // key words, 0 = empty
+    uint32_t* rep;             // first occurrence (token index) per slot
+    uint32_t* fill;
+    uint32_t mask, limit;
+};
+struct JsIntern {
+    const uint8_t* doc;
+    uint8_t* heap;             // decoded strings that differ from their raw bytes
+    unsigned long long* heap_used;
+    uint64_t heap_cap;
+    uint32_t* status;          // JS_ST_* bits
+    uint32_t* seen_root;
+    JsDict kd, pd;
+};
+__global__ void k_js_quotes(JsDoc j, uint64_t* qmask, uint64_t* bsmask, uint64_t* hbmask, uint32_t* qcnt);
+__global__ void k_js_classify(JsDoc j, const uint64_t* qoff, JsMasks m, unsigned long long* err);
+__global__ void k_js_tokens(JsDoc j, JsMasks m, const uint64_t* toff, const uint64_t* doff, uint2* toks,
+                            unsigned long long* err);
+__global__ void k_js_par_agg(const uint2* toks, uint32_t ntok, uint32_t* tagg);
+__global__ void k_js_par_group(const uint32_t* tagg, uint32_t ntiles, uint32_t* gagg);
+__global__ void k_js_par_top(uint32_t* gagg, uint32_t ng);
+__global__ void k_js_par_tiles(uint32_t* tagg, uint32_t ntiles, const uint32_t* gagg);
+__global__ void k_js_par_apply(const uint2* toks, uint32_t ntok, const uint32_t* texcl, uint32_t* par);
+__global__ void k_js_deep(const uint2* toks, uint32_t ntok, uint32_t* par);
+__global__ void k_js_validate(JsDoc j, const uint2* toks, uint32_t ntok, const uint32_t* par, unsigned long long* err);
+__global__ void k_js_roles(JsDoc j, const uint2* toks, uint32_t ntok, const uint32_t* par, uint8_t* role);
+__global__ void k_js_elems_count(JsDoc j, const uint2* toks, uint32_t ntok, const uint32_t* par, const uint8_t* role,
+                                 uint32_t* cnt3, unsigned long long* derr);
+__global__ void k_js_elems_write(const uint2* toks, uint32_t ntok, const uint32_t* par, const uint8_t* role,
+                                 const uint64_t* coff3, uint32_t ntiles, uint32_t* ord, JsTopoOut to);
+__global__ void k_js_values(JsDoc j, const uint2* toks, uint32_t ntok, const uint32_t* par, const uint8_t* role,
+                            const uint32_t* ord, JsTopoOut to, JsStore des, JsStore real, JsIntern in,
+                            unsigned long long* derr);
+__global__ void k_js_rep_mark(JsDict dt, uint32_t* bits);
+__global__ void k_js_popc(const uint32_t* bits, uint32_t nw, uint32_t* cnt);
+__global__ void k_js_ids(JsDict dt, const uint32_t* bits, const uint64_t* wrank, uint32_t* slot_id, uint32_t* len_by_id);
+__global__ void k_js_dict_copy(JsDict dt, JsIntern in, const uint32_t* slot_id, const uint64_t* off64, uint32_t* offs,
+                               uint8_t* arena);
+__global__ void k_js_finalize_links(JsStore st, uint32_t n, const uint32_t* kslot_id, const uint32_t* pslot_id);
+__global__ void k_js_finalize_topos(JsTopoOut to, uint32_t T, const uint32_t* kslot_id, uint8_t* flags8);
+
 }  // namespace kdtn

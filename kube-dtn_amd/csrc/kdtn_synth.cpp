@@ -22,8 +22,11 @@
 #include <cmath>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
+
+#include "../../include/kdtn.h"
 
 namespace {
 
@@ -561,5 +564,141 @@ int kdtn_synth_get(void* sp, const char* name, void** ptr, uint64_t* n, uint32_t
     }
     return -1;
 }
+
+// ---- TopologyList JSON writer (CR-ingest workloads) ------------------------------------------
+// Writes the tables as the API server serves Topology CRs: keys sorted, spec link strings only
+// when set (as written in a user's YAML), status links with every key (the controller's typed
+// json.Marshal), properties always present with its non-empty fields, strings escaped like
+// encoding/json's Marshal (\", \\, control bytes, HTML-safe \u003c \u003e \u0026,
+// U+2028/2029). flags bit 0: one newline + two-space indent per item (kubectl-style).
+namespace {
+struct JsonW {
+    std::string o;
+    const kdtn_epoch_in* in;
+    void raw(const char* s) { o += s; }
+    void str(const kdtn_strtab& t, uint32_t id) {
+        const uint8_t* p = t.bytes + t.offs[id];
+        const uint32_t n = t.offs[id + 1] - t.offs[id];
+        o += '"';
+        static const char* hex = "0123456789abcdef";
+        for (uint32_t i = 0; i < n; ++i) {
+            const uint8_t c = p[i];
+            if (c == '"' || c == '\\') { o += '\\'; o += (char)c; }
+            else if (c == '\n') o += "\\n";
+            else if (c == '\r') o += "\\r";
+            else if (c == '\t') o += "\\t";
+            else if (c < 0x20 || c == '<' || c == '>' || c == '&') {
+                o += "\\u00"; o += hex[c >> 4]; o += hex[c & 15];
+            } else if (c == 0xE2 && i + 2 < n && p[i + 1] == 0x80 && (p[i + 2] == 0xA8 || p[i + 2] == 0xA9)) {
+                o += p[i + 2] == 0xA8 ? "\\u2028" : "\\u2029";
+                i += 2;
+            } else o += (char)c;
+        }
+        o += '"';
+    }
+    void kv(const char* k, const kdtn_strtab& t, uint32_t id, bool& first, bool always) {
+        if (!id && !always) return;
+        if (!first) o += ',';
+        first = false;
+        o += '"'; o += k; o += "\":";
+        str(t, id);
+    }
+    void link(const kdtn_link_table& L, uint32_t i, bool all) {
+        static const char* const KEY[7] = {"local_intf", "local_ip", "local_mac", "peer_intf", "peer_ip",
+                                           "peer_mac", "peer_pod"};
+        static const char* const PROP[12] = {"latency", "latency_corr", "jitter", "loss", "loss_corr", "rate",
+                                             "duplicate", "duplicate_corr", "reorder_prob", "reorder_corr",
+                                             "corrupt_prob", "corrupt_corr"};
+        // sorted: corrupt_corr corrupt_prob duplicate duplicate_corr [gap] jitter latency latency_corr
+        //         loss loss_corr rate reorder_corr reorder_prob
+        static const int ORD[12] = {11, 10, 6, 7, 2, 0, 1, 3, 4, 5, 9, 8};
+        o += '{';
+        bool first = true;
+        for (int k = 0; k < 7; ++k) kv(KEY[k], in->kdict, L.key[k][i], first, all);
+        if (!first) o += ',';
+        o += "\"properties\":{";
+        bool pf = true;
+        for (int q = 0; q < 12; ++q) {
+            if (q == 4 && L.gap[i]) {
+                if (!pf) o += ',';
+                pf = false;
+                o += "\"gap\":" + std::to_string(L.gap[i]);
+            }
+            kv(PROP[ORD[q]], in->pdict, L.prop[ORD[q]][i], pf, false);
+        }
+        o += "},\"uid\":" + std::to_string((long long)L.uid[i]) + "}";
+    }
+};
+
+std::string json_range(const kdtn_epoch_in* in, uint32_t t0, uint32_t t1, uint32_t flags) {
+    JsonW w;
+    w.in = in;
+    const kdtn_topo_table& T = in->topos;
+    for (uint32_t t = t0; t < t1; ++t) {
+        if (t) w.o += ',';
+        if (flags & 1) w.o += "\n  ";
+        w.raw("{\"apiVersion\":\"y-young.github.io/v1\",\"kind\":\"Topology\",\"metadata\":{");
+        bool f = true;
+        w.kv("name", in->kdict, T.name[t], f, true);
+        w.kv("namespace", in->kdict, T.ns[t], f, true);
+        w.raw("},\"spec\":{\"links\":");
+        if (T.flags[t] & KDTN_TOPO_SPEC_NIL) w.raw("null");
+        else {
+            w.o += '[';
+            for (uint32_t i = T.des_off[t]; i < T.des_off[t + 1]; ++i) {
+                if (i != T.des_off[t]) w.o += ',';
+                w.link(in->desired, i, false);
+            }
+            w.o += ']';
+        }
+        w.raw("},\"status\":{\"links\":");
+        if (T.flags[t] & KDTN_TOPO_STATUS_NIL) w.raw("null");
+        else {
+            w.o += '[';
+            for (uint32_t i = T.real_off[t]; i < T.real_off[t + 1]; ++i) {
+                if (i != T.real_off[t]) w.o += ',';
+                w.link(in->realised, i, true);
+            }
+            w.o += ']';
+        }
+        f = false;
+        w.kv("net_ns", in->kdict, T.net_ns[t], f, true);
+        w.raw(",\"skipped\":null");
+        f = false;
+        w.kv("src_ip", in->kdict, T.src_ip[t], f, true);
+        w.raw("}}");
+    }
+    return w.o;
+}
+}  // namespace
+
+// Builds the document (threads over topology ranges); kdtn_synth_json_copy / _free.
+void* kdtn_synth_json_new(const kdtn_epoch_in* in, uint32_t flags, uint64_t* size) {
+    auto* parts = new std::vector<std::string>();
+    const uint32_t T = in->topos.n;
+    const uint32_t P = T > 4096 ? std::min(16u, std::max(1u, std::thread::hardware_concurrency())) : 1;
+    parts->assign(P + 2, std::string());
+    (*parts)[0] = "{\"apiVersion\":\"y-young.github.io/v1\",\"items\":[";
+    std::vector<std::thread> th;
+    for (uint32_t p = 0; p < P; ++p) {
+        const uint32_t t0 = (uint32_t)((uint64_t)T * p / P), t1 = (uint32_t)((uint64_t)T * (p + 1) / P);
+        th.emplace_back([=] { (*parts)[p + 1] = json_range(in, t0, t1, flags); });
+    }
+    for (auto& x : th) x.join();
+    (*parts)[P + 1] = std::string(flags & 1 ? "\n" : "") +
+                      "],\"kind\":\"TopologyList\",\"metadata\":{\"resourceVersion\":\"1\"}}";
+    uint64_t n = 0;
+    for (auto& x : *parts) n += x.size();
+    *size = n;
+    return parts;
+}
+void kdtn_synth_json_copy(void* h, uint8_t* out) {
+    uint64_t at = 0;
+    for (auto& x : *static_cast<std::vector<std::string>*>(h)) {
+        std::memcpy(out + at, x.data(), x.size());
+        at += x.size();
+    }
+}
+void kdtn_synth_json_free(void* h) { delete static_cast<std::vector<std::string>*>(h); }
 
 }  // extern "C"

@@ -126,6 +126,24 @@ class PodTable(C.Structure):
 BATCH_ADD, BATCH_DEL = 0, 1
 
 
+class IngestInfo(C.Structure):
+    _fields_ = [("n_topos", C.c_uint32), ("n_desired", C.c_uint32), ("n_realised", C.c_uint32),
+                ("n_kdict", C.c_uint32), ("n_pdict", C.c_uint32), ("json_err", C.c_int32),
+                ("err_offset", C.c_uint64), ("n_tokens", C.c_uint64), ("kdict_bytes", C.c_uint64),
+                ("pdict_bytes", C.c_uint64)]
+
+
+class IngestTables(C.Structure):
+    _fields_ = [(f, C.c_void_p) for f in (
+        "kd_bytes", "kd_offs", "pd_bytes", "pd_offs", "ns", "name", "src_ip", "net_ns", "flags",
+        "real_off", "des_off", "des_key", "des_prop", "des_gap", "des_uid",
+        "real_key", "real_prop", "real_gap", "real_uid")]
+
+
+EBADMSG = -74
+JSON_OK, JSON_SYNTAX, JSON_DEPTH, JSON_TYPE, JSON_DUPKEY = 0, 1, 2, 3, 4
+
+
 class Config(C.Structure):
     _fields_ = [("device", C.c_int32), ("vxlan_base", C.c_int32), ("tick_in_usec", C.c_double)]
 
@@ -149,7 +167,8 @@ EXPORTS = ["kdtn_version", "kdtn_strerror", "kdtn_err_name", "kdtn_init", "kdtn_
            "kdtn_epoch_download", "kdtn_make_qdiscs", "kdtn_comm_unique_id", "kdtn_comm_init",
            "kdtn_last_kernel_times", "kdtn_debug_wg_trace", "kdtn_epoch_encode",
            "kdtn_epoch_download_wire", "kdtn_diff", "kdtn_resolve", "kdtn_host_alloc",
-           "kdtn_host_free", "kdtn_epoch_fanout", "kdtn_epoch_tc", "kdtn_epoch_download_tc"]
+           "kdtn_host_free", "kdtn_epoch_fanout", "kdtn_epoch_tc", "kdtn_epoch_download_tc",
+           "kdtn_json_upload", "kdtn_json_ingest", "kdtn_ingest_download"]
 
 
 def ptr(a: np.ndarray, t):

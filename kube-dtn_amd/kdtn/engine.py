@@ -75,6 +75,9 @@ def lib() -> C.CDLL:
         "kdtn_epoch_download_tc": (C.c_int, [vp, C.POINTER(abi.TcArgv)]),
         "kdtn_host_free": (None, [vp]),
         "kdtn_epoch_download_wire": (C.c_int, [vp, C.POINTER(abi.Wire)]),
+        "kdtn_json_upload": (C.c_int, [vp, C.c_char_p, C.c_uint64]),
+        "kdtn_json_ingest": (C.c_int, [vp, C.POINTER(abi.VniTable), C.POINTER(abi.IngestInfo)]),
+        "kdtn_ingest_download": (C.c_int, [vp, C.POINTER(abi.IngestTables)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -142,6 +145,57 @@ class Engine:
         _check(lib().kdtn_epoch_upload(self._ctx, C.byref(cin)), "kdtn_epoch_upload")
         self._T = inp.topos.n
         self._caps = (inp.realised.n, inp.desired.n, inp.realised.n)
+
+    def json_upload(self, doc: bytes) -> None:
+        """H2D of a TopologyList JSON document (kdtn_json_upload)."""
+        _check(lib().kdtn_json_upload(self._ctx, doc, len(doc)), "kdtn_json_upload")
+
+    def json_ingest(self, vnis=None) -> abi.IngestInfo:
+        """Decode the uploaded document on the GPU into device-resident epoch inputs
+        (kdtn_json_ingest). A rejected document raises KdtnError(EBADMSG) whose .info holds
+        json_err / err_offset."""
+        info = abi.IngestInfo()
+        cv = vnis.to_c() if vnis is not None else None
+        rc = lib().kdtn_json_ingest(self._ctx, C.byref(cv) if cv is not None else None, C.byref(info))
+        if rc == abi.EBADMSG:
+            e = KdtnError(rc, "kdtn_json_ingest")
+            e.info = info
+            raise e
+        _check(rc, "kdtn_json_ingest")
+        self._T = info.n_topos
+        self._caps = (info.n_realised, info.n_desired, info.n_realised)
+        self._ingest = info
+        return info
+
+    def ingest(self, doc: bytes, vnis=None) -> abi.IngestInfo:
+        self.json_upload(doc)
+        return self.json_ingest(vnis)
+
+    def ingest_tables(self) -> EpochInput:
+        """D2H of the tables the last json_ingest decoded (kdtn_ingest_download)."""
+        from .tables import Links, StrTab, Topos
+        I = self._ingest
+        T, N, M = I.n_topos, I.n_desired, I.n_realised
+        z = np.zeros
+        kd, kdo = z(max(I.kdict_bytes, 1), np.uint8), z(I.n_kdict + 1, np.uint32)
+        pd, pdo = z(max(I.pdict_bytes, 1), np.uint8), z(I.n_pdict + 1, np.uint32)
+        tp = [z(T, np.uint32) for _ in range(4)] + [z(T, np.uint8), z(T + 1, np.uint32), z(T + 1, np.uint32)]
+
+        def links(n):
+            return Links(z((abi.NKEY, n), np.uint32), z(n, np.int64), z((abi.NPROP, n), np.uint32),
+                         z(n, np.uint32))
+        des, real = links(N), links(M)
+        t = abi.IngestTables()
+        for f, a in (("kd_bytes", kd), ("kd_offs", kdo), ("pd_bytes", pd), ("pd_offs", pdo),
+                     ("ns", tp[0]), ("name", tp[1]), ("src_ip", tp[2]), ("net_ns", tp[3]),
+                     ("flags", tp[4]), ("real_off", tp[5]), ("des_off", tp[6]),
+                     ("des_key", des.key), ("des_prop", des.prop), ("des_gap", des.gap), ("des_uid", des.uid),
+                     ("real_key", real.key), ("real_prop", real.prop), ("real_gap", real.gap),
+                     ("real_uid", real.uid)):
+            setattr(t, f, a.ctypes.data if a.size else None)
+        _check(lib().kdtn_ingest_download(self._ctx, C.byref(t)), "kdtn_ingest_download")
+        return EpochInput(StrTab(kd[:I.kdict_bytes], kdo), StrTab(pd[:I.pdict_bytes], pdo),
+                          Topos(*tp), real, des)
 
     def run(self, stages: int = abi.STAGE_ALL) -> None:
         _check(lib().kdtn_epoch_run(self._ctx, stages), "kdtn_epoch_run")

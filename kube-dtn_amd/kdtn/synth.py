@@ -134,3 +134,25 @@ def make(config: int, pods_per_shard: int = 1_000_000, degree: int = 10, n_nodes
                      pod_slice=int(meta[0]), pod_base=int(meta[1]), owner=h)
     inp.total_pods = int(meta[2])
     return inp
+
+
+def topology_list_json(inp: EpochInput, pretty: bool = False) -> bytes:
+    """The epoch's Topology CRs as a Kubernetes TopologyList JSON document, the way the API
+    server serves them (sorted keys, encoding/json escaping) — the CR-ingest workload."""
+    L = _load()
+    if not getattr(L, "_json_bound", False):
+        from . import abi
+        L.kdtn_synth_json_new.restype = C.c_void_p
+        L.kdtn_synth_json_new.argtypes = [C.POINTER(abi.EpochIn), C.c_uint32, C.POINTER(C.c_uint64)]
+        L.kdtn_synth_json_copy.argtypes = [C.c_void_p, C.c_void_p]
+        L.kdtn_synth_json_free.argtypes = [C.c_void_p]
+        L._json_bound = True
+    cin = inp.to_c()
+    n = C.c_uint64()
+    h = L.kdtn_synth_json_new(C.byref(cin), 1 if pretty else 0, C.byref(n))
+    try:
+        buf = C.create_string_buffer(n.value)
+        L.kdtn_synth_json_copy(h, buf)
+        return buf.raw[:n.value]
+    finally:
+        L.kdtn_synth_json_free(h)

@@ -1,0 +1,168 @@
+"""GPU parity of the CR ingest (kdtn_json_ingest, kdtn_ingest.hip) against the C oracle's
+decode of the same TopologyList documents (oracle/kdtn_oracle_json.c, itself pinned by
+tests/test_ingest_cpu.py): every table bit for bit (dictionaries in first-occurrence
+order, topology columns and offsets, both link stores), the rejection class of malformed
+documents, and JSON → ingest → epoch → batches against the oracle chain.
+"""
+from __future__ import annotations
+
+import random
+
+import numpy as np
+import pytest
+
+import json_ref as jr
+import oracle as O
+from kdtn import abi, synth
+from kdtn.engine import KdtnError
+from test_ingest_cpu import (BAD_SYNTAX, DUPS, GO_STRINGS, TYPE_ERRORS, GOLDEN, rand_topos, s0p,
+                             sample_doc)
+
+pytestmark = pytest.mark.gpu
+TICK = 15.625
+
+
+def tables_equal(a, b, ctx=""):
+    """EpochInput equality, array by array"""
+    pairs = [("kdict.bytes", a.kdict.bytes_, b.kdict.bytes_), ("kdict.offs", a.kdict.offs, b.kdict.offs),
+             ("pdict.bytes", a.pdict.bytes_, b.pdict.bytes_), ("pdict.offs", a.pdict.offs, b.pdict.offs)]
+    for f in ("ns", "name", "src_ip", "net_ns", "flags", "real_off", "des_off"):
+        pairs.append(("topos." + f, getattr(a.topos, f), getattr(b.topos, f)))
+    for side in ("desired", "realised"):
+        for f in ("key", "prop", "gap", "uid"):
+            pairs.append((f"{side}.{f}", getattr(getattr(a, side), f), getattr(getattr(b, side), f)))
+    for name, x, y in pairs:
+        x, y = np.asarray(x), np.asarray(y)
+        if x.shape != y.shape or x.tobytes() != y.tobytes():
+            raise AssertionError(f"{ctx}: {name} differs: shape {x.shape} vs {y.shape}; "
+                                 f"{x.ravel()[:8]} vs {y.ravel()[:8]}")
+
+
+def gpu_ingest(engine, doc):
+    """(json_err, tables | None) from the GPU"""
+    try:
+        engine.ingest(doc)
+    except KdtnError as e:
+        if e.code != abi.EBADMSG:
+            raise
+        return e.info.json_err, None
+    return 0, engine.ingest_tables()
+
+
+def check_doc(engine, doc, ctx=""):
+    e0, _, want = O.json_ingest(doc)
+    e1, got = gpu_ingest(engine, doc)
+    assert e1 == e0, f"{ctx}: GPU json_err {e1}, oracle {e0}"
+    if want is not None:
+        tables_equal(got, want, ctx)
+    return want
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_random_documents(engine, seed):
+    rng = random.Random(seed)
+    root = jr.topology_list(rand_topos(rng, 60 + 20 * seed), rng)
+    doc = jr.dumps(root, rng, ws=0.3 if seed % 2 else 0.0, esc=0.08 if seed % 3 == 0 else 0.0).encode()
+    check_doc(engine, doc, f"seed {seed}")
+
+
+@pytest.mark.parametrize("doc", BAD_SYNTAX + TYPE_ERRORS + DUPS)
+def test_rejections(engine, doc):
+    check_doc(engine, doc, repr(doc[:60]))
+
+
+def test_depth(engine):
+    for d in (15, 16, 17, 40, 9999, 10000, 10001):
+        for wrap in (False, True):
+            inner = b"[" * d + b"]" * d
+            doc = (b'{"items":[{"metadata":{"name":"a","x":' + inner + b'}}]}') if wrap else inner
+            check_doc(engine, doc, f"depth {d} wrap {wrap}")
+    # deep non-schema structure between links: parents of deep tokens, then schema again
+    deep = b'{"k":' + b'{"a":[' * 30 + b'1' + b']}' * 30 + b'}'
+    doc = (b'{"items":[{"metadata":{"name":"p","annotations":' + deep + b'},"spec":{"links":[{"uid":1,'
+           b'"x":' + deep + b',"peer_pod":"q"},{"uid":2}]}}]}')
+    check_doc(engine, doc, "deep")
+
+
+@pytest.mark.parametrize("lit,want", GO_STRINGS)
+def test_go_strings(engine, lit, want):
+    doc = b'{"items":[{"metadata":{"name":' + lit + b'}}]}'
+    got = check_doc(engine, doc, repr(lit))
+    assert got.kdict.get(int(got.topos.name[0])) == want
+
+
+def test_block_boundaries(engine):
+    """quotes, backslash runs, scalars and multi-byte runes straddling 64-byte blocks"""
+    rng = random.Random(7)
+    for trial in range(40):
+        pad = rng.randrange(0, 130)
+        s = rng.choice(["a\\\\\\\"b", "\\\\\\\\", "x\\\"y\\\\", "é中😀", "\\u00e9\\ud83d\\ude00", "q" * 70])
+        doc = (b'{"items":[{"metadata":{"name":"' + b" " * 0 + b'n' * pad + b'","namespace":"' + s.encode() +
+               b'"},"spec":{"links":[{"uid":' + str(rng.randrange(-10**18, 10**18)).encode() +
+               b',"properties":{"gap":' + str(rng.randrange(0, 2**32)).encode() + b'}}]}}]}')
+        doc = doc.replace(b",", b"," + b" " * rng.randrange(0, 70), rng.randrange(0, 4))
+        check_doc(engine, doc, f"trial {trial}")
+
+
+def test_many_tiles(engine):
+    """a document with > 2 groups of 4096-token tiles (parent scan across groups)"""
+    rng = random.Random(11)
+    topos = rand_topos(rng, 2500)
+    doc = jr.dumps(jr.topology_list(topos, rng, extra=True), rng).encode()
+    want = check_doc(engine, doc, "many tiles")
+    assert engine._ingest.n_tokens > 2 * 256 * 4096 or want.desired.n > 1000
+
+
+@pytest.mark.parametrize("tr", range(len(GOLDEN["transitions"])))
+def test_samples_chain(engine, tr):
+    """config/samples CRs as JSON → GPU ingest → GPU epoch == oracle ingest → oracle epoch"""
+    t = GOLDEN["transitions"][tr]
+    GOLDEN["sets"].setdefault("S0p", s0p())
+    doc = sample_doc(t["status"], t["spec"])
+    want = check_doc(engine, doc, t["name"])
+    engine.ingest(doc)
+    engine.run()
+    engine.sync()
+    out = engine.download()
+    ref = O.reconcile(want, tick=TICK)
+    assert not out.mismatches(ref), out.mismatches(ref)
+
+
+@pytest.mark.parametrize("config", [1, 3, 4])
+def test_synthetic_configs(engine, config):
+    """synthetic workloads serialised as the API server would, then ingested"""
+    kw = dict(pods_per_shard=3000) if config in (3, 4) else {}
+    inp = synth.make(config, **kw)
+    doc = synth.topology_list_json(inp, pretty=config == 4)
+    want = check_doc(engine, doc, f"config {config}")
+    # round trip: the strings behind every id equal the generator's
+    for k in range(abi.NKEY):
+        a = want.desired.key[k][:500]
+        assert [want.kdict.get(int(i)) for i in a] == [inp.kdict.get(int(i)) for i in inp.desired.key[k][:500]]
+    engine.ingest(doc)
+    engine.run()
+    engine.sync()
+    out = engine.download()
+    assert not out.mismatches(O.reconcile(want, tick=TICK))
+
+
+def test_config2_full_size_properties(engine):
+    """config 2 (1M pods, 10M links, ≈2 GB of JSON): counts, offsets and a sampled string
+    round trip at full size; the oracle decodes a 20k-pod slice of the same generator."""
+    inp = synth.make(2, pods_per_shard=1_000_000)
+    doc = synth.topology_list_json(inp)
+    info = engine.ingest(doc)
+    assert (info.n_topos, info.n_desired, info.n_realised) == (inp.topos.n, inp.desired.n, 0)
+    got = engine.ingest_tables()
+    assert (got.topos.des_off == inp.topos.des_off).all()
+    assert (got.desired.uid == inp.desired.uid).all()
+    assert (got.topos.flags == inp.topos.flags).all()
+    rng = np.random.default_rng(5)
+    for i in rng.integers(0, inp.desired.n, 2000):
+        for k in range(abi.NKEY):
+            assert got.kdict.get(int(got.desired.key[k][i])) == inp.kdict.get(int(inp.desired.key[k][i]))
+        for k in range(abi.NPROP):
+            assert got.pdict.get(int(got.desired.prop[k][i])) == inp.pdict.get(int(inp.desired.prop[k][i]))
+    # ids are first-occurrence ranks: every id appears first after all smaller ids
+    small = synth.make(2, pods_per_shard=20_000)
+    check_doc(engine, synth.topology_list_json(small), "config 2 slice")
