@@ -125,6 +125,60 @@ def wire_stage(eng, reps: int = 5):
     return res
 
 
+def ingest_stage(eng, inp, reps: int = 5, cpu_sample_pods: int = 20_000):
+    """Separate report (not part of `value`): CR ingest of this shard's Topology CRs as a
+    TopologyList JSON document (kdtn_json_ingest: json.Unmarshal + SoA + interning on the
+    GPU, document resident in HBM). Wall time per ingest includes its three host round
+    trips (token / element counts, intern table fill); roofline bytes = document read once
+    + the decoded tables written once (88 B per link record, 25 B per topology, dictionary
+    arenas + offsets). CPU baseline: the oracle's decode (oracle/kdtn_oracle_json.c, the
+    reference's json.Unmarshal restated) single-threaded on a bounded slice of the workload."""
+    doc = synth.topology_list_json(inp)
+    t = time.perf_counter()
+    eng.json_upload(doc)
+    h2d_s = time.perf_counter() - t
+    info = eng.json_ingest()
+    acc: dict[str, float] = {}
+    walls = []
+    for _ in range(reps):
+        t = time.perf_counter()
+        info = eng.json_ingest()
+        walls.append(time.perf_counter() - t)
+        for k, v in eng.kernel_times().items():
+            acc[k] = acc.get(k, 0.0) + v / reps
+    wall = sorted(walls)[len(walls) // 2]
+    gpu_ms = sum(v for k, v in acc.items() if k != "js_sync")
+    out_bytes = (88.0 * (info.n_desired + info.n_realised) + 25.0 * info.n_topos + info.kdict_bytes
+                 + info.pdict_bytes + 4.0 * (info.n_kdict + info.n_pdict + 2))
+    alg = len(doc) + out_bytes
+    res = {"doc_bytes": len(doc), "links": int(info.n_desired + info.n_realised), "topologies": int(info.n_topos),
+           "tokens": int(info.n_tokens), "wall_ms": wall * 1e3, "gpu_ms": gpu_ms,
+           "links_per_s": (info.n_desired + info.n_realised) / wall, "json_GBps": len(doc) / wall / 1e9,
+           "roofline": {"bound": "hbm", "bytes": alg, "achieved": alg / (gpu_ms * 1e-3) / 1e9,
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": alg / (gpu_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
+           "kernels_ms": acc, "h2d_GBps": len(doc) / h2d_s / 1e9,
+           "note": "not part of value; the document is resident in HBM (h2d_GBps is the PCIe "
+                   "upload measured separately)"}
+    del doc
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        small = synth.make(2, pods_per_shard=cpu_sample_pods)
+        sdoc = synth.topology_list_json(small)
+        t = time.perf_counter()
+        O.json_ingest(sdoc)
+        cs = time.perf_counter() - t
+        res["cpu_baseline"] = {"links_per_s": small.desired.n / cs, "json_GBps": len(sdoc) / cs / 1e9,
+                               "cores": 1, "kind": "port",
+                               "sample": f"oracle/kdtn_oracle_json.c on a {cpu_sample_pods}-pod config-2 "
+                                         f"TopologyList ({len(sdoc)} bytes, {small.desired.n} links) in "
+                                         f"{cs:.2f} s"}
+    except Exception as e:   # the oracle is optional for the stage report
+        res["cpu_baseline"] = {"error": str(e)}
+    return res
+
+
 def pmc_traffic(links_per_gpu: int):
     """HBM bytes per k_reconcile launch from the newest committed PMC summary of the same
     workload (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from separate
@@ -152,6 +206,7 @@ def main():
     ap.add_argument("--cpu-budget-s", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-wire", action="store_true", help="skip the wire-encoding stage report")
+    ap.add_argument("--no-ingest", action="store_true", help="skip the CR-ingest stage report")
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="CPU-baseline worker threads (the GPU box's CPU share is 16)")
     args = ap.parse_args()
@@ -245,6 +300,8 @@ def main():
         result["wire_stage"] = wire_stage(eng)
     if rank == 0 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(inp, args.cpu_budget_s, args.cpu_threads)
+    if not args.no_ingest and world == 1:
+        result["ingest_stage"] = ingest_stage(eng, inp)
     if rank == 0:
         print(json.dumps(result), flush=True)
     eng.close()

@@ -18,7 +18,7 @@ using namespace kdtn;
 
 namespace {
 
-constexpr int kMaxTimers = 16;
+constexpr int kMaxTimers = 32;
 
 struct DevBuf {
     void* p = nullptr;
@@ -95,6 +95,8 @@ struct kdtn_ctx {
     bool tc_done = false;
     // CR ingest (kdtn_ingest.hip): document, block masks, token stream, decode scratch
     DevBuf j_doc, j_q, j_bs, j_hb, j_qcnt, j_qoff, j_tok, j_open, j_close, j_tcnt, j_dcnt, j_toff, j_doff;
+    DevBuf j_ocnt, j_ooff, j_olist;
+    uint32_t j_kcap = 0, j_pcap = 0;   // intern table sizes that fit the last document
     DevBuf j_toks, j_par, j_role, j_ord, j_tagg, j_gagg, j_cnt3, j_coff3, j_small, j_part;
     DevBuf j_tflags, j_tseen, j_dseen, j_rseen, j_kslots, j_krep, j_pslots, j_prep, j_heap;
     DevBuf j_bits, j_bcnt, j_wrank, j_kslot_id, j_pslot_id, j_len, j_off64;
@@ -442,7 +444,8 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->j_role, &c->j_ord, &c->j_tagg, &c->j_gagg, &c->j_cnt3, &c->j_coff3, &c->j_small,
                       &c->j_part, &c->j_tflags, &c->j_tseen, &c->j_dseen, &c->j_rseen, &c->j_kslots, &c->j_krep,
                       &c->j_pslots, &c->j_prep, &c->j_heap, &c->j_bits, &c->j_bcnt, &c->j_wrank,
-                      &c->j_kslot_id, &c->j_pslot_id, &c->j_len, &c->j_off64};
+                      &c->j_kslot_id, &c->j_pslot_id, &c->j_len, &c->j_off64, &c->j_ocnt, &c->j_ooff,
+                      &c->j_olist};
     for (DevBuf* b : bufs) release(*b);
     for (int i = 0; i <= kMaxTimers; ++i)
         if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
@@ -1119,9 +1122,11 @@ int json_dict(kdtn_ctx* c, const JsDict& dt, const JsIntern& in, uint32_t ntok, 
     k_js_rep_mark<<<nblocks(cap), BLOCK, 0, s>>>(dt, dp<uint32_t>(c->j_bits));
     k_js_popc<<<nblocks(nw), BLOCK, 0, s>>>(dp<uint32_t>(c->j_bits), nw, dp<uint32_t>(c->j_bcnt));
     TRY(scan_u32(c, dp<uint32_t>(c->j_bcnt), nw, dp<uint64_t>(c->j_wrank)));
+    timer_mark(c, "js_intern");
     uint64_t uniq = 0;
     TRY(d2h(c, &uniq, dp<uint64_t>(c->j_wrank) + nw));
     HIP_TRY(hipStreamSynchronize(s));
+    timer_mark(c, "js_sync");
     const uint32_t n = (uint32_t)uniq + 1;                    // + id 0 = ""
     TRY(ensure(slot_id, (size_t)cap * 4));
     TRY(ensure(c->j_len, (size_t)n * 4));
@@ -1130,9 +1135,11 @@ int json_dict(kdtn_ctx* c, const JsDict& dt, const JsIntern& in, uint32_t ntok, 
     k_js_ids<<<nblocks(cap), BLOCK, 0, s>>>(dt, dp<uint32_t>(c->j_bits), dp<uint64_t>(c->j_wrank),
                                             dp<uint32_t>(slot_id), dp<uint32_t>(c->j_len));
     TRY(scan_u32(c, dp<uint32_t>(c->j_len), n, dp<uint64_t>(c->j_off64)));
+    timer_mark(c, "js_intern");
     uint64_t total = 0;
     TRY(d2h(c, &total, dp<uint64_t>(c->j_off64) + n));
     HIP_TRY(hipStreamSynchronize(s));
+    timer_mark(c, "js_sync");
     if (total > 0xFFFFFF00ull) {
         std::snprintf(g_last_error, sizeof(g_last_error), "dictionary arena of %llu bytes exceeds 4 GiB",
                       (unsigned long long)total);
@@ -1205,12 +1212,12 @@ int kdtn_json_ingest(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest_info* 
     HIP_TRY(hipMemsetAsync(small, 0xFF, 16, s));
     HIP_TRY(hipMemsetAsync(small + 2, 0, J_SMALL - 16, s));
     for (DevBuf* b : {&c->j_q, &c->j_bs, &c->j_hb, &c->j_tok, &c->j_open, &c->j_close}) TRY(ensure(*b, (size_t)nb * 8));
-    for (DevBuf* b : {&c->j_qcnt, &c->j_tcnt, &c->j_dcnt}) TRY(ensure(*b, (size_t)nb * 4));
-    for (DevBuf* b : {&c->j_qoff, &c->j_toff, &c->j_doff}) TRY(ensure(*b, ((size_t)nb + 1) * 8));
+    for (DevBuf* b : {&c->j_qcnt, &c->j_tcnt, &c->j_dcnt, &c->j_ocnt}) TRY(ensure(*b, (size_t)nb * 4));
+    for (DevBuf* b : {&c->j_qoff, &c->j_toff, &c->j_doff, &c->j_ooff}) TRY(ensure(*b, ((size_t)nb + 1) * 8));
     JsDoc j{dp<uint8_t>(c->j_doc), (uint32_t)c->j_n, nb, dp<uint64_t>(c->j_q), dp<uint64_t>(c->j_bs),
             dp<uint64_t>(c->j_hb)};
     JsMasks m{dp<uint64_t>(c->j_tok), dp<uint64_t>(c->j_open), dp<uint64_t>(c->j_close), dp<uint32_t>(c->j_tcnt),
-              dp<uint32_t>(c->j_dcnt)};
+              dp<uint32_t>(c->j_dcnt), dp<uint32_t>(c->j_ocnt)};
 
     // 1. block masks, string state, token counts, depth
     k_js_quotes<<<nblocks(nb), BLOCK, 0, s>>>(j, dp<uint64_t>(c->j_q), dp<uint64_t>(c->j_bs), dp<uint64_t>(c->j_hb),
@@ -1219,13 +1226,16 @@ int kdtn_json_ingest(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest_info* 
     k_js_classify<<<nblocks(nb), BLOCK, 0, s>>>(j, dp<uint64_t>(c->j_qoff), m, small);
     TRY(scan_u32(c, dp<uint32_t>(c->j_tcnt), nb, dp<uint64_t>(c->j_toff)));
     TRY(scan_u32(c, dp<uint32_t>(c->j_dcnt), nb, dp<uint64_t>(c->j_doff)));
+    TRY(scan_u32(c, dp<uint32_t>(c->j_ocnt), nb, dp<uint64_t>(c->j_ooff)));
     timer_mark(c, "js_blocks");
-    uint64_t quotes = 0, ntok64 = 0;
+    uint64_t quotes = 0, ntok64 = 0, nopen64 = 0;
+    TRY(d2h(c, &nopen64, dp<uint64_t>(c->j_ooff) + nb));
     unsigned long long serr = 0;
     TRY(d2h(c, &quotes, dp<uint64_t>(c->j_qoff) + nb));
     TRY(d2h(c, &ntok64, dp<uint64_t>(c->j_toff) + nb));
     TRY(d2h(c, &serr, small));
     HIP_TRY(hipStreamSynchronize(s));
+    timer_mark(c, "js_sync");                       // host round trips are timed apart
     HIP_TRY(hipGetLastError());
     if (quotes & 1) serr = std::min<unsigned long long>(serr, (c->j_n << 8) | KDTN_JSON_SYNTAX);   // unterminated
     if (ntok64 == 0) serr = std::min<unsigned long long>(serr, KDTN_JSON_SYNTAX);
@@ -1238,10 +1248,13 @@ int kdtn_json_ingest(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest_info* 
     TRY(ensure(c->j_par, (size_t)ntok * 4));
     TRY(ensure(c->j_role, (size_t)ntok));
     TRY(ensure(c->j_ord, (size_t)ntok * 4));
+    const uint32_t nopen = (uint32_t)nopen64;
+    TRY(ensure(c->j_olist, (size_t)nopen * 4));
     const uint2* toks = dp<uint2>(c->j_toks);
     uint32_t* par = dp<uint32_t>(c->j_par);
     k_js_tokens<<<nblocks(nb), BLOCK, 0, s>>>(j, m, dp<uint64_t>(c->j_toff), dp<uint64_t>(c->j_doff),
-                                             dp<uint2>(c->j_toks), small);
+                                             dp<uint64_t>(c->j_ooff), dp<uint2>(c->j_toks), dp<uint32_t>(c->j_olist),
+                                             small);
     timer_mark(c, "js_tokens");
     const uint32_t ntiles = (ntok + JS_TILE - 1) / JS_TILE, ng = (ntiles + BLOCK - 1) / BLOCK;
     TRY(ensure(c->j_tagg, (size_t)ntiles * JS_PD * 4));
@@ -1257,28 +1270,32 @@ int kdtn_json_ingest(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest_info* 
     timer_mark(c, "js_validate");
     TRY(d2h(c, &serr, small));
     HIP_TRY(hipStreamSynchronize(s));
+    timer_mark(c, "js_sync");
     HIP_TRY(hipGetLastError());
     if (serr != ~0ull) return json_reject(c, info, serr);
 
     // 3. schema roles, items / links ordinals
     uint8_t* role = dp<uint8_t>(c->j_role);
     uint32_t* ord = dp<uint32_t>(c->j_ord);
-    k_js_roles<<<nblocks(ntok), BLOCK, 0, s>>>(j, toks, ntok, par, role);
+    HIP_TRY(hipMemsetAsync(role, 0, ntok, s));                  // R_NONE below the schema levels
+    for (uint32_t level = 0; level <= 6 && nopen; ++level)
+        k_js_roles<<<nblocks(nopen), BLOCK, 0, s>>>(j, toks, dp<uint32_t>(c->j_olist), nopen, par, role, level);
     TRY(ensure(c->j_cnt3, (size_t)3 * ntiles * 4));
     TRY(ensure(c->j_coff3, (size_t)3 * (ntiles + 1) * 8));
     k_js_elems_count<<<ntiles, BLOCK, 0, s>>>(j, toks, ntok, par, role, dp<uint32_t>(c->j_cnt3), small + 1);
     for (int q = 0; q < 3; ++q)
         TRY(scan_u32(c, dp<uint32_t>(c->j_cnt3) + (size_t)q * ntiles, ntiles,
                      dp<uint64_t>(c->j_coff3) + (size_t)q * (ntiles + 1)));
+    timer_mark(c, "js_elements");
     uint64_t tot[3];
     for (int q = 0; q < 3; ++q) TRY(d2h(c, tot + q, dp<uint64_t>(c->j_coff3) + (size_t)q * (ntiles + 1) + ntiles));
     unsigned long long derr = 0;
     TRY(d2h(c, &derr, small + 1));
     HIP_TRY(hipStreamSynchronize(s));
+    timer_mark(c, "js_sync");
     HIP_TRY(hipGetLastError());
     if (derr != ~0ull) return json_reject(c, info, derr);
     const uint32_t T = (uint32_t)tot[0], N = (uint32_t)tot[1], M = (uint32_t)tot[2];
-    timer_mark(c, "js_elements");
 
     // 4. output tables
     c->T = T;
@@ -1300,8 +1317,8 @@ int kdtn_json_ingest(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest_info* 
     JsStore real{dp<uint32_t>(c->real.buf), dp<uint32_t>(c->j_rseen)};
 
     // 5. schema values + interning; a table or heap that fills up is grown and the pass rerun
-    uint32_t kcap = next_pow2(std::max<uint64_t>(1024, 2ull * ((uint64_t)N + M) + 4ull * T));
-    uint32_t pcap = next_pow2(std::max<uint64_t>(1024, ((uint64_t)N + M) / 2 + 64));
+    uint32_t kcap = std::max(c->j_kcap, next_pow2(std::max<uint64_t>(1024, 2ull * ((uint64_t)N + M) + 4ull * T)));
+    uint32_t pcap = std::max(c->j_pcap, next_pow2(std::max<uint64_t>(1024, ((uint64_t)N + M) / 2 + 64)));
     uint64_t hcap = std::max<uint64_t>(1 << 20, c->j_n / 16);
     JsIntern in{};
     for (int attempt = 0;; ++attempt) {
@@ -1330,39 +1347,37 @@ int kdtn_json_ingest(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest_info* 
         in.heap_cap = hcap;
         in.status = reinterpret_cast<uint32_t*>(small + 3);
         in.seen_root = reinterpret_cast<uint32_t*>(small + 3) + 1;
-        in.kd = JsDict{dp<unsigned long long>(c->j_kslots), dp<uint32_t>(c->j_krep),
-                       reinterpret_cast<uint32_t*>(small + 4), kcap - 1, kcap / 4 * 3};
-        in.pd = JsDict{dp<unsigned long long>(c->j_pslots), dp<uint32_t>(c->j_prep),
-                       reinterpret_cast<uint32_t*>(small + 4) + 1, pcap - 1, pcap / 4 * 3};
+        in.kd = JsDict{dp<unsigned long long>(c->j_kslots), dp<uint32_t>(c->j_krep), kcap - 1};
+        in.pd = JsDict{dp<unsigned long long>(c->j_pslots), dp<uint32_t>(c->j_prep), pcap - 1};
         k_js_values<<<nblocks(ntok), BLOCK, 0, s>>>(j, toks, ntok, par, role, ord, to, des, real, in, small + 1);
+        timer_mark(c, "js_values");
         unsigned long long ctl[3];
         TRY(d2h(c, ctl, small + 1, 3));
-        uint32_t fills[2];
-        TRY(d2h(c, fills, small + 4, 2));
         HIP_TRY(hipStreamSynchronize(s));
+        timer_mark(c, "js_sync");
         HIP_TRY(hipGetLastError());
         const uint32_t status = (uint32_t)ctl[2];
         if (status & JS_ST_LONG) {
             std::snprintf(g_last_error, sizeof(g_last_error), "a schema string is longer than 16 MiB");
             return KDTN_EINVAL;
         }
-        if (status & JS_ST_OVERFLOW) {
+        if (status & JS_ST_OVERFLOW) {                  // a table filled up or the heap ran out
             if (attempt >= 6) return KDTN_ENOMEM;
-            if (fills[0] >= in.kd.limit) kcap *= 4;
-            if (fills[1] >= in.pd.limit) pcap *= 4;
             if (ctl[1] > hcap) hcap = std::max<uint64_t>(hcap * 4, ctl[1] + (1 << 20));
-            if (fills[0] < in.kd.limit && fills[1] < in.pd.limit && ctl[1] <= hcap) { kcap *= 2; pcap *= 2; }
+            else { kcap = std::min<uint64_t>((uint64_t)kcap * 4, 1u << 31); pcap = std::min<uint64_t>((uint64_t)pcap * 4, 1u << 31); }
             continue;
         }
         if (ctl[0] != ~0ull) return json_reject(c, info, ctl[0]);
         break;
     }
-    timer_mark(c, "js_values");
 
     // 6. ids in first-occurrence order, dictionaries, id columns
     uint64_t kbytes = 0, pbytes = 0;
     TRY(json_dict(c, in.kd, in, ntok, c->j_kslot_id, c->kd_bytes, c->kd_offs, &c->D, &kbytes));
     TRY(json_dict(c, in.pd, in, ntok, c->j_pslot_id, c->pd_bytes, c->pd_offs, &c->P, &pbytes));
+    // keep the intern tables at most half full for the next document of this shape
+    c->j_kcap = std::max(kcap, next_pow2(2ull * c->D));
+    c->j_pcap = std::max(pcap, next_pow2(2ull * c->P));
     constexpr uint32_t IDW = (KDTN_NKEY + KDTN_NPROP) * TILE_RECS;
     if (N) k_js_finalize_links<<<nblocks((uint64_t)(N + TILE_RECS - 1) / TILE_RECS * IDW), BLOCK, 0, s>>>(
         des, N, dp<uint32_t>(c->j_kslot_id), dp<uint32_t>(c->j_pslot_id));

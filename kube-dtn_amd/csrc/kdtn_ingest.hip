@@ -159,6 +159,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_classify(JsDoc j, const uint64_t* 
     m.close[b] = cl & out;
     m.tcnt[b] = __popcll(tok);
     m.dcnt[b] = 64u + __popcll(op & out) - __popcll(cl & out);
+    m.ocnt[b] = __popcll(op & out);
 }
 
 // ---------------------------------------------------------------- k_js_tokens
@@ -176,13 +177,15 @@ KD_INLINE uint32_t kind_of(uint32_t c) {
 }
 
 __global__ void __launch_bounds__(BLOCK) k_js_tokens(JsDoc j, JsMasks m, const uint64_t* toff, const uint64_t* doff,
-                                                     uint2* toks, unsigned long long* err) {
+                                                     const uint64_t* ooff, uint2* toks, uint32_t* olist,
+                                                     unsigned long long* err) {
     const uint32_t b = blockIdx.x * BLOCK + threadIdx.x;
     if (b >= j.nb) return;
     uint64_t tok = m.tok[b];
     if (!tok) return;
     const uint64_t op = m.open[b], cl = m.close[b];
     uint32_t idx = (uint32_t)toff[b];
+    uint32_t oi = (uint32_t)ooff[b];
     const int64_t d0 = (int64_t)doff[b] - 64ll * b;
     while (tok) {
         const int k = __ffsll((long long)tok) - 1;
@@ -195,7 +198,10 @@ __global__ void __launch_bounds__(BLOCK) k_js_tokens(JsDoc j, JsMasks m, const u
             js_fail(err, pos, KDTN_JSON_SYNTAX);      // a close with nothing open
             d = d < 0 ? 0 : d;
         }
-        if ((kind == TK_OBJ || kind == TK_ARR) && d >= 10000) js_fail(err, pos, KDTN_JSON_DEPTH);
+        if (kind == TK_OBJ || kind == TK_ARR) {
+            if (d >= 10000) js_fail(err, pos, KDTN_JSON_DEPTH);
+            olist[oi++] = idx;
+        }
         if (d > (int64_t)TK_DEPTH_MASK) d = TK_DEPTH_MASK;
         toks[idx++] = make_uint2(pos, (uint32_t)d | (kind << 24));
     }
@@ -275,14 +281,14 @@ __global__ void __launch_bounds__(BLOCK) k_js_par_tiles(uint32_t* tagg, uint32_t
     uint32_t* cur = sh[0];
     uint32_t* nxt = sh[1];
 #pragma unroll
-    for (int d = 0; d < JS_PD; ++d) cur[threadIdx.x * JS_PD + d] = t < ntiles ? tagg[(size_t)t * JS_PD + d] : 0u;
+    for (int d = 0; d < JS_PD; ++d) cur[d * BLOCK + threadIdx.x] = t < ntiles ? tagg[(size_t)t * JS_PD + d] : 0u;
     __syncthreads();
-    for (int off = 1; off < BLOCK; off <<= 1) {                  // inclusive Hillis-Steele
+    for (int off = 1; off < BLOCK; off <<= 1) {                  // inclusive Hillis-Steele, [lane][thread]
 #pragma unroll
         for (int d = 0; d < JS_PD; ++d) {
-            uint32_t v = cur[threadIdx.x * JS_PD + d];
-            if ((int)threadIdx.x >= off) v = max(v, cur[(threadIdx.x - off) * JS_PD + d]);
-            nxt[threadIdx.x * JS_PD + d] = v;
+            uint32_t v = cur[d * BLOCK + threadIdx.x];
+            if ((int)threadIdx.x >= off) v = max(v, cur[d * BLOCK + threadIdx.x - off]);
+            nxt[d * BLOCK + threadIdx.x] = v;
         }
         __syncthreads();
         uint32_t* tmp = cur; cur = nxt; nxt = tmp;
@@ -290,7 +296,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_par_tiles(uint32_t* tagg, uint32_t
     if (t < ntiles) {
 #pragma unroll
         for (int d = 0; d < JS_PD; ++d) {
-            const uint32_t ex = threadIdx.x ? cur[(threadIdx.x - 1) * JS_PD + d] : 0u;
+            const uint32_t ex = threadIdx.x ? cur[d * BLOCK + threadIdx.x - 1] : 0u;
             tagg[(size_t)t * JS_PD + d] = max(ex, gagg[(size_t)blockIdx.x * JS_PD + d]);
         }
     }
@@ -314,21 +320,21 @@ __global__ void __launch_bounds__(BLOCK) k_js_par_apply(const uint2* toks, uint3
     uint32_t* cur = sh[0];
     uint32_t* nxt = sh[1];
 #pragma unroll
-    for (int d = 0; d < JS_PD; ++d) cur[threadIdx.x * JS_PD + d] = row[d];
+    for (int d = 0; d < JS_PD; ++d) cur[d * BLOCK + threadIdx.x] = row[d];
     __syncthreads();
     for (int off = 1; off < BLOCK; off <<= 1) {
 #pragma unroll
         for (int d = 0; d < JS_PD; ++d) {
-            uint32_t v = cur[threadIdx.x * JS_PD + d];
-            if ((int)threadIdx.x >= off) v = max(v, cur[(threadIdx.x - off) * JS_PD + d]);
-            nxt[threadIdx.x * JS_PD + d] = v;
+            uint32_t v = cur[d * BLOCK + threadIdx.x];
+            if ((int)threadIdx.x >= off) v = max(v, cur[d * BLOCK + threadIdx.x - off]);
+            nxt[d * BLOCK + threadIdx.x] = v;
         }
         __syncthreads();
         uint32_t* tmp = cur; cur = nxt; nxt = tmp;
     }
 #pragma unroll
     for (int d = 0; d < JS_PD; ++d) {
-        const uint32_t ex = threadIdx.x ? cur[(threadIdx.x - 1) * JS_PD + d] : 0u;
+        const uint32_t ex = threadIdx.x ? cur[d * BLOCK + threadIdx.x - 1] : 0u;
         row[d] = max(ex, texcl[(size_t)blockIdx.x * JS_PD + d]);
     }
     for (int k = 0; k < JS_PER; ++k) {
@@ -483,8 +489,8 @@ __global__ void __launch_bounds__(BLOCK) k_js_validate(JsDoc j, const uint2* tok
 // Decodes the member name at string token pos (escapes included) and returns the index of
 // the equal name in names[0..n), or -1. Names are ASCII and at most 15 bytes.
 KD_INLINE int match_key(const JsDoc& j, uint32_t pos, const char (*names)[16], int n) {
-    char buf[16];
-    int len = 0;
+    uint64_t lo = 0, hi = 0;
+    uint32_t len = 0;
     const uint32_t e = str_end(j, pos);
     if (e - pos - 1 > 6 * 16) return -1;
     for (uint32_t k = pos + 1; k < e; ++k) {
@@ -507,32 +513,33 @@ KD_INLINE int match_key(const JsDoc& j, uint32_t pos, const char (*names)[16], i
         } else if (c >= 0x80) {
             return -1;
         }
-        if (len >= 15) return -1;
-        buf[len++] = (char)c;
+        if (len >= 15 || c == 0) return -1;
+        if (len < 8) lo |= (uint64_t)c << (8 * len);
+        else hi |= (uint64_t)c << (8 * (len - 8));
+        ++len;
     }
     for (int f = 0; f < n; ++f) {
-        const char* s = names[f];
-        int q = 0;
-        while (q < len && s[q] == buf[q]) ++q;
-        if (q == len && s[q] == 0) return f;
+        const uint64_t* w = reinterpret_cast<const uint64_t*>(names[f]);
+        if (w[0] == lo && w[1] == hi) return f;
     }
     return -1;
 }
 
-__constant__ char kItems[1][16] = {"items"};
-__constant__ char kItem[3][16] = {"metadata", "spec", "status"};
-__constant__ char kMeta[2][16] = {"name", "namespace"};
-__constant__ char kLinks[1][16] = {"links"};
-__constant__ char kStatus[3][16] = {"links", "src_ip", "net_ns"};
-__constant__ char kLink[KDTN_NKEY + 2][16] = {"local_intf", "local_ip", "local_mac", "peer_intf", "peer_ip",
+__constant__ __attribute__((aligned(16))) char kItems[1][16] = {"items"};
+__constant__ __attribute__((aligned(16))) char kItem[3][16] = {"metadata", "spec", "status"};
+__constant__ __attribute__((aligned(16))) char kMeta[2][16] = {"name", "namespace"};
+__constant__ __attribute__((aligned(16))) char kLinks[1][16] = {"links"};
+__constant__ __attribute__((aligned(16))) char kStatus[3][16] = {"links", "src_ip", "net_ns"};
+__constant__ __attribute__((aligned(16))) char kLink[KDTN_NKEY + 2][16] = {"local_intf", "local_ip", "local_mac", "peer_intf", "peer_ip",
                                               "peer_mac", "peer_pod", "uid", "properties"};
-__constant__ char kProps[KDTN_NPROP + 1][16] = {"latency", "latency_corr", "jitter", "loss", "loss_corr", "rate",
+__constant__ __attribute__((aligned(16))) char kProps[KDTN_NPROP + 1][16] = {"latency", "latency_corr", "jitter", "loss", "loss_corr", "rate",
                                                 "duplicate", "duplicate_corr", "reorder_prob", "reorder_corr",
                                                 "corrupt_prob", "corrupt_corr", "gap"};
 
 // ---------------------------------------------------------------- roles
 // role of the container c whose enclosing container has role r (c is the child token)
 KD_INLINE uint32_t child_role(const JsDoc& j, const uint2* toks, uint32_t r, uint32_t c) {
+    if (r == R_NONE || r == R_META || r >= R_PROPS_S) return R_NONE;
     const uint32_t kind = tkind(toks[c]);
     const bool member = tkind(toks[c - 1]) == TK_COLON;
     if (!member) {                                                // array element
@@ -561,24 +568,17 @@ KD_INLINE uint32_t child_role(const JsDoc& j, const uint2* toks, uint32_t r, uin
     }
 }
 
-__global__ void __launch_bounds__(BLOCK) k_js_roles(JsDoc j, const uint2* toks, uint32_t ntok, const uint32_t* par,
-                                                    uint8_t* role) {
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= ntok) return;
+// one nesting level at a time over the open brackets: a container's role follows from its
+// parent's (already set by the previous level), its kind and its member name
+__global__ void __launch_bounds__(BLOCK) k_js_roles(JsDoc j, const uint2* toks, const uint32_t* olist, uint32_t nopen,
+                                                    const uint32_t* par, uint8_t* role, uint32_t level) {
+    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+    if (k >= nopen) return;
+    const uint32_t i = olist[k];
     const uint2 t = toks[i];
-    if (!tk_open(t.y)) return;
-    const uint32_t d = tdepth(t);
-    uint32_t r = R_NONE;
-    if (d <= 6) {
-        uint32_t chain[7];
-        uint32_t c = i;
-        for (int k = (int)d; k >= 0; --k) {                       // chain[k] = ancestor at depth k
-            chain[k] = c;
-            if (k) c = par[c];
-        }
-        r = tkind(toks[chain[0]]) == TK_OBJ ? R_ROOT : R_NONE;
-        for (uint32_t k = 1; k <= d && r != R_NONE; ++k) r = child_role(j, toks, r, chain[k]);
-    }
+    if (tdepth(t) != level) return;
+    const uint32_t r = level == 0 ? (tkind(t) == TK_OBJ ? R_ROOT : R_NONE)
+                                  : child_role(j, toks, role[par[i]], i);
     role[i] = (uint8_t)r;
 }
 
@@ -586,6 +586,8 @@ __global__ void __launch_bounds__(BLOCK) k_js_roles(JsDoc j, const uint2* toks, 
 // class of token i: 1 + {0 items element, 1 spec.links element, 2 status.links element}, or 0
 KD_INLINE uint32_t elem_class(const uint2* toks, const uint32_t* par, const uint8_t* role, uint32_t i) {
     if (i == 0) return 0;
+    const uint32_t d = tdepth(toks[i]);
+    if (d != 2 && d != 5) return 0;                 // items elements: depth 2; links elements: 5
     const uint32_t pk = tkind(toks[i - 1]);
     if (pk != TK_ARR && pk != TK_COMMA) return 0;
     if (!value_start(tkind(toks[i]))) return 0;
@@ -776,7 +778,6 @@ KD_INLINE uint32_t intern(const JsIntern& in, const JsDict& dt, const uint8_t* p
             if ((kw >> 56) & 1) __threadfence();       // heap bytes visible before the key
             cur = atomicCAS(dt.slots + s, 0ull, (unsigned long long)kw);
             if (cur == 0) {
-                if (atomicAdd(dt.fill, 1u) >= dt.limit) atomicOr(in.status, JS_ST_OVERFLOW);
                 atomicMin(dt.rep + s, occ);
                 return s;
             }
@@ -795,8 +796,9 @@ KD_INLINE uint32_t intern(const JsIntern& in, const JsDict& dt, const uint8_t* p
                 const uint8_t* q = in.doc + (uint32_t)cur;
                 while (k < len && q[k] == p[k]) ++k;
             }
-            if (k == len) {
-                atomicMin(dt.rep + s, occ);
+            if (k == len) {                           // hot strings: skip the atomic when it cannot lower
+                if (occ < __hip_atomic_load(dt.rep + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                    atomicMin(dt.rep + s, occ);
                 return s;
             }
         }
@@ -879,6 +881,8 @@ __global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, const uint2* toks,
                                                      JsStore des, JsStore real, JsIntern in, unsigned long long* derr) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i < 2 || i >= ntok) return;
+    const uint32_t dv = tdepth(toks[i]);             // members of root 1, item 3, meta/spec/status 4,
+    if (dv != 1 && dv != 3 && dv != 4 && dv != 6 && dv != 7) return;   // link 6, properties 7
     if (tkind(toks[i - 1]) != TK_COLON) return;
     const uint32_t o = par[i];
     if (o >= JS_DEEP) return;

@@ -309,6 +309,7 @@ struct JsMasks {
     uint64_t* close;           // } ] outside strings
     uint32_t* tcnt;            // tokens per block
     uint32_t* dcnt;            // 64 + opens - closes per block
+    uint32_t* ocnt;            // opens per block
 };
 struct JsTopoOut {
     uint32_t* ns;
@@ -327,8 +328,7 @@ struct JsStore {
 struct JsDict {
     unsigned long long* slots; // key words, 0 = empty
     uint32_t* rep;             // first occurrence (token index) per slot
-    uint32_t* fill;
-    uint32_t mask, limit;
+    uint32_t mask;
 };
 struct JsIntern {
     const uint8_t* doc;
@@ -341,8 +341,8 @@ struct JsIntern {
 };
 __global__ void k_js_quotes(JsDoc j, uint64_t* qmask, uint64_t* bsmask, uint64_t* hbmask, uint32_t* qcnt);
 __global__ void k_js_classify(JsDoc j, const uint64_t* qoff, JsMasks m, unsigned long long* err);
-__global__ void k_js_tokens(JsDoc j, JsMasks m, const uint64_t* toff, const uint64_t* doff, uint2* toks,
-                            unsigned long long* err);
+__global__ void k_js_tokens(JsDoc j, JsMasks m, const uint64_t* toff, const uint64_t* doff, const uint64_t* ooff,
+                            uint2* toks, uint32_t* olist, unsigned long long* err);
 __global__ void k_js_par_agg(const uint2* toks, uint32_t ntok, uint32_t* tagg);
 __global__ void k_js_par_group(const uint32_t* tagg, uint32_t ntiles, uint32_t* gagg);
 __global__ void k_js_par_top(uint32_t* gagg, uint32_t ng);
@@ -350,7 +350,8 @@ __global__ void k_js_par_tiles(uint32_t* tagg, uint32_t ntiles, const uint32_t* 
 __global__ void k_js_par_apply(const uint2* toks, uint32_t ntok, const uint32_t* texcl, uint32_t* par);
 __global__ void k_js_deep(const uint2* toks, uint32_t ntok, uint32_t* par);
 __global__ void k_js_validate(JsDoc j, const uint2* toks, uint32_t ntok, const uint32_t* par, unsigned long long* err);
-__global__ void k_js_roles(JsDoc j, const uint2* toks, uint32_t ntok, const uint32_t* par, uint8_t* role);
+__global__ void k_js_roles(JsDoc j, const uint2* toks, const uint32_t* olist, uint32_t nopen, const uint32_t* par,
+                           uint8_t* role, uint32_t level);
 __global__ void k_js_elems_count(JsDoc j, const uint2* toks, uint32_t ntok, const uint32_t* par, const uint8_t* role,
                                  uint32_t* cnt3, unsigned long long* derr);
 __global__ void k_js_elems_write(const uint2* toks, uint32_t ntok, const uint32_t* par, const uint8_t* role,

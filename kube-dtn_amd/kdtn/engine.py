@@ -298,10 +298,14 @@ class Engine:
         return node[:f.n_nodes], off, idx[:f.n_send]
 
     def kernel_times(self) -> dict[str, float]:
-        names = (C.c_char_p * 16)()
-        ms = (C.c_float * 16)()
-        n = lib().kdtn_last_kernel_times(self._ctx, names, ms, 16)
-        return {names[i].decode(): float(ms[i]) for i in range(max(n, 0))}
+        names = (C.c_char_p * 32)()
+        ms = (C.c_float * 32)()
+        n = lib().kdtn_last_kernel_times(self._ctx, names, ms, 32)
+        out: dict[str, float] = {}
+        for i in range(max(n, 0)):               # a stage timed in several pieces is summed
+            k = names[i].decode()
+            out[k] = out.get(k, 0.0) + float(ms[i])
+        return out
 
     def wg_trace(self) -> np.ndarray:
         """(nwg, 6) uint64 phase timestamps of the last traced run (KDTN_VARIANT bit 16)."""
