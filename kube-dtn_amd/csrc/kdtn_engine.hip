@@ -95,7 +95,7 @@ struct kdtn_ctx {
     bool tc_done = false;
     // CR ingest (kdtn_ingest.hip): document, block masks, token stream, decode scratch
     DevBuf j_doc, j_q, j_bs, j_hb, j_qcnt, j_qoff, j_tok, j_open, j_close, j_tcnt, j_dcnt, j_toff, j_doff;
-    DevBuf j_ocnt, j_ooff, j_olist;
+    DevBuf j_ocnt, j_ooff, j_olist, j_ccnt, j_coff, j_vlist;
     uint32_t j_kcap = 0, j_pcap = 0;   // intern table sizes that fit the last document
     DevBuf j_toks, j_par, j_role, j_ord, j_tagg, j_gagg, j_cnt3, j_coff3, j_small, j_part;
     DevBuf j_tflags, j_tseen, j_dseen, j_rseen, j_kslots, j_krep, j_pslots, j_prep, j_heap;
@@ -445,7 +445,7 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->j_part, &c->j_tflags, &c->j_tseen, &c->j_dseen, &c->j_rseen, &c->j_kslots, &c->j_krep,
                       &c->j_pslots, &c->j_prep, &c->j_heap, &c->j_bits, &c->j_bcnt, &c->j_wrank,
                       &c->j_kslot_id, &c->j_pslot_id, &c->j_len, &c->j_off64, &c->j_ocnt, &c->j_ooff,
-                      &c->j_olist};
+                      &c->j_olist, &c->j_ccnt, &c->j_coff, &c->j_vlist};
     for (DevBuf* b : bufs) release(*b);
     for (int i = 0; i <= kMaxTimers; ++i)
         if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
@@ -1212,12 +1212,13 @@ int kdtn_json_ingest(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest_info* 
     HIP_TRY(hipMemsetAsync(small, 0xFF, 16, s));
     HIP_TRY(hipMemsetAsync(small + 2, 0, J_SMALL - 16, s));
     for (DevBuf* b : {&c->j_q, &c->j_bs, &c->j_hb, &c->j_tok, &c->j_open, &c->j_close}) TRY(ensure(*b, (size_t)nb * 8));
-    for (DevBuf* b : {&c->j_qcnt, &c->j_tcnt, &c->j_dcnt, &c->j_ocnt}) TRY(ensure(*b, (size_t)nb * 4));
-    for (DevBuf* b : {&c->j_qoff, &c->j_toff, &c->j_doff, &c->j_ooff}) TRY(ensure(*b, ((size_t)nb + 1) * 8));
+    for (DevBuf* b : {&c->j_qcnt, &c->j_tcnt, &c->j_dcnt, &c->j_ocnt, &c->j_ccnt}) TRY(ensure(*b, (size_t)nb * 4));
+    for (DevBuf* b : {&c->j_qoff, &c->j_toff, &c->j_doff, &c->j_ooff, &c->j_coff})
+        TRY(ensure(*b, ((size_t)nb + 1) * 8));
     JsDoc j{dp<uint8_t>(c->j_doc), (uint32_t)c->j_n, nb, dp<uint64_t>(c->j_q), dp<uint64_t>(c->j_bs),
             dp<uint64_t>(c->j_hb)};
     JsMasks m{dp<uint64_t>(c->j_tok), dp<uint64_t>(c->j_open), dp<uint64_t>(c->j_close), dp<uint32_t>(c->j_tcnt),
-              dp<uint32_t>(c->j_dcnt), dp<uint32_t>(c->j_ocnt)};
+              dp<uint32_t>(c->j_dcnt), dp<uint32_t>(c->j_ocnt), dp<uint32_t>(c->j_ccnt)};
 
     // 1. block masks, string state, token counts, depth
     k_js_quotes<<<nblocks(nb), BLOCK, 0, s>>>(j, dp<uint64_t>(c->j_q), dp<uint64_t>(c->j_bs), dp<uint64_t>(c->j_hb),
@@ -1227,9 +1228,12 @@ int kdtn_json_ingest(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest_info* 
     TRY(scan_u32(c, dp<uint32_t>(c->j_tcnt), nb, dp<uint64_t>(c->j_toff)));
     TRY(scan_u32(c, dp<uint32_t>(c->j_dcnt), nb, dp<uint64_t>(c->j_doff)));
     TRY(scan_u32(c, dp<uint32_t>(c->j_ocnt), nb, dp<uint64_t>(c->j_ooff)));
+    TRY(scan_u32(c, dp<uint32_t>(c->j_ccnt), nb, dp<uint64_t>(c->j_coff)));
     timer_mark(c, "js_blocks");
     uint64_t quotes = 0, ntok64 = 0, nopen64 = 0;
     TRY(d2h(c, &nopen64, dp<uint64_t>(c->j_ooff) + nb));
+    uint64_t nval64 = 0;
+    TRY(d2h(c, &nval64, dp<uint64_t>(c->j_coff) + nb));
     unsigned long long serr = 0;
     TRY(d2h(c, &quotes, dp<uint64_t>(c->j_qoff) + nb));
     TRY(d2h(c, &ntok64, dp<uint64_t>(c->j_toff) + nb));
@@ -1250,11 +1254,13 @@ int kdtn_json_ingest(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest_info* 
     TRY(ensure(c->j_ord, (size_t)ntok * 4));
     const uint32_t nopen = (uint32_t)nopen64;
     TRY(ensure(c->j_olist, (size_t)nopen * 4));
+    const uint32_t nval = (uint32_t)nval64;
+    TRY(ensure(c->j_vlist, (size_t)nval * 4));
     const uint2* toks = dp<uint2>(c->j_toks);
     uint32_t* par = dp<uint32_t>(c->j_par);
     k_js_tokens<<<nblocks(nb), BLOCK, 0, s>>>(j, m, dp<uint64_t>(c->j_toff), dp<uint64_t>(c->j_doff),
-                                             dp<uint64_t>(c->j_ooff), dp<uint2>(c->j_toks), dp<uint32_t>(c->j_olist),
-                                             small);
+                                             dp<uint64_t>(c->j_ooff), dp<uint64_t>(c->j_coff), dp<uint2>(c->j_toks),
+                                             dp<uint32_t>(c->j_olist), dp<uint32_t>(c->j_vlist), small);
     timer_mark(c, "js_tokens");
     const uint32_t ntiles = (ntok + JS_TILE - 1) / JS_TILE, ng = (ntiles + BLOCK - 1) / BLOCK;
     TRY(ensure(c->j_tagg, (size_t)ntiles * JS_PD * 4));
@@ -1347,9 +1353,13 @@ int kdtn_json_ingest(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest_info* 
         in.heap_cap = hcap;
         in.status = reinterpret_cast<uint32_t*>(small + 3);
         in.seen_root = reinterpret_cast<uint32_t*>(small + 3) + 1;
+        in.variant = (uint32_t)std::strtoul(std::getenv("KDTN_JS_VARIANT") ? std::getenv("KDTN_JS_VARIANT") : "0",
+                                            nullptr, 0);
         in.kd = JsDict{dp<unsigned long long>(c->j_kslots), dp<uint32_t>(c->j_krep), kcap - 1};
         in.pd = JsDict{dp<unsigned long long>(c->j_pslots), dp<uint32_t>(c->j_prep), pcap - 1};
-        k_js_values<<<nblocks(ntok), BLOCK, 0, s>>>(j, toks, ntok, par, role, ord, to, des, real, in, small + 1);
+        if (nval)
+            k_js_values<<<nblocks(nval), BLOCK, 0, s>>>(j, toks, dp<uint32_t>(c->j_vlist), nval, par, role, ord, to,
+                                                        des, real, in, small + 1);
         timer_mark(c, "js_values");
         unsigned long long ctl[3];
         TRY(d2h(c, ctl, small + 1, 3));

@@ -117,14 +117,16 @@ __global__ void __launch_bounds__(BLOCK) k_js_classify(JsDoc j, const uint64_t* 
     if (b >= j.nb) return;
     uint32_t w[16];
     load_block(j.doc, b, w);
-    uint64_t op = 0, cl = 0, pun = 0, ctl = 0, wsc = 0;
+    uint64_t op = 0, cl = 0, pun = 0, ctl = 0, wsc = 0, colon = 0;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
         const uint32_t lw = w[k] | 0x20202020u;            // '[' → '{', ']' → '}'
         const uint32_t o = mm4(eqb(lw, '{')), c = mm4(eqb(lw, '}'));
         op |= (uint64_t)o << (4 * k);
         cl |= (uint64_t)c << (4 * k);
-        pun |= (uint64_t)(mm4(eqb(w[k], ':')) | mm4(eqb(w[k], ','))) << (4 * k);
+        const uint32_t cn = mm4(eqb(w[k], ':'));
+        colon |= (uint64_t)cn << (4 * k);
+        pun |= (uint64_t)(cn | mm4(eqb(w[k], ','))) << (4 * k);
         ctl |= (uint64_t)mm4(ltb(w[k], 0x20)) << (4 * k);
         wsc |= (uint64_t)mm4(ltb(w[k], 0x21)) << (4 * k);
     }
@@ -160,6 +162,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_classify(JsDoc j, const uint64_t* 
     m.tcnt[b] = __popcll(tok);
     m.dcnt[b] = 64u + __popcll(op & out) - __popcll(cl & out);
     m.ocnt[b] = __popcll(op & out);
+    m.ccnt[b] = __popcll(colon & out);
 }
 
 // ---------------------------------------------------------------- k_js_tokens
@@ -177,15 +180,15 @@ KD_INLINE uint32_t kind_of(uint32_t c) {
 }
 
 __global__ void __launch_bounds__(BLOCK) k_js_tokens(JsDoc j, JsMasks m, const uint64_t* toff, const uint64_t* doff,
-                                                     const uint64_t* ooff, uint2* toks, uint32_t* olist,
-                                                     unsigned long long* err) {
+                                                     const uint64_t* ooff, const uint64_t* coff, uint2* toks,
+                                                     uint32_t* olist, uint32_t* vlist, unsigned long long* err) {
     const uint32_t b = blockIdx.x * BLOCK + threadIdx.x;
     if (b >= j.nb) return;
     uint64_t tok = m.tok[b];
     if (!tok) return;
     const uint64_t op = m.open[b], cl = m.close[b];
     uint32_t idx = (uint32_t)toff[b];
-    uint32_t oi = (uint32_t)ooff[b];
+    uint32_t oi = (uint32_t)ooff[b], vi = (uint32_t)coff[b];
     const int64_t d0 = (int64_t)doff[b] - 64ll * b;
     while (tok) {
         const int k = __ffsll((long long)tok) - 1;
@@ -201,6 +204,8 @@ __global__ void __launch_bounds__(BLOCK) k_js_tokens(JsDoc j, JsMasks m, const u
         if (kind == TK_OBJ || kind == TK_ARR) {
             if (d >= 10000) js_fail(err, pos, KDTN_JSON_DEPTH);
             olist[oi++] = idx;
+        } else if (kind == TK_COLON) {
+            vlist[vi++] = idx + 1;                    // the member value follows its colon
         }
         if (d > (int64_t)TK_DEPTH_MASK) d = TK_DEPTH_MASK;
         toks[idx++] = make_uint2(pos, (uint32_t)d | (kind << 24));
@@ -773,7 +778,11 @@ KD_INLINE uint32_t intern(const JsIntern& in, const JsDict& dt, const uint8_t* p
     const uint64_t kw = (tag << 57) | kw_self;
     uint32_t s = (uint32_t)h & dt.mask;
     for (uint32_t probe = 0; probe <= dt.mask; ++probe) {
-        unsigned long long cur = __hip_atomic_load(dt.slots + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // slots are written once (CAS from 0): a plain load is either that final key or a stale 0,
+        // and a stale 0 only sends us to the CAS, which returns the real key
+        unsigned long long cur = (in.variant & JSV_COHERENT) ? __hip_atomic_load(dt.slots + s, __ATOMIC_RELAXED,
+                                                                                 __HIP_MEMORY_SCOPE_AGENT)
+                                                             : dt.slots[s];
         if (cur == 0) {
             if ((kw >> 56) & 1) __threadfence();       // heap bytes visible before the key
             cur = atomicCAS(dt.slots + s, 0ull, (unsigned long long)kw);
@@ -797,8 +806,7 @@ KD_INLINE uint32_t intern(const JsIntern& in, const JsDict& dt, const uint8_t* p
                 while (k < len && q[k] == p[k]) ++k;
             }
             if (k == len) {                           // hot strings: skip the atomic when it cannot lower
-                if (occ < __hip_atomic_load(dt.rep + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                    atomicMin(dt.rep + s, occ);
+                if (!(in.variant & JSV_NO_REP) && occ < dt.rep[s]) atomicMin(dt.rep + s, occ);
                 return s;
             }
         }
@@ -876,14 +884,15 @@ KD_INLINE uint32_t* store_word(const JsStore& st, uint32_t rec, int col) {
     return st.base + (size_t)(rec >> 6) * TILE_WORDS + col * TILE_RECS + (rec & 63u);
 }
 
-__global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, const uint2* toks, uint32_t ntok, const uint32_t* par,
-                                                     const uint8_t* role, const uint32_t* ord, JsTopoOut to,
-                                                     JsStore des, JsStore real, JsIntern in, unsigned long long* derr) {
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i < 2 || i >= ntok) return;
+__global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, const uint2* toks, const uint32_t* vlist, uint32_t nval,
+                                                     const uint32_t* par, const uint8_t* role, const uint32_t* ord,
+                                                     JsTopoOut to, JsStore des, JsStore real, JsIntern in,
+                                                     unsigned long long* derr) {
+    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+    if (k >= nval) return;
+    const uint32_t i = vlist[k];                       // object member values, document order
     const uint32_t dv = tdepth(toks[i]);             // members of root 1, item 3, meta/spec/status 4,
     if (dv != 1 && dv != 3 && dv != 4 && dv != 6 && dv != 7) return;   // link 6, properties 7
-    if (tkind(toks[i - 1]) != TK_COLON) return;
     const uint32_t o = par[i];
     if (o >= JS_DEEP) return;
     const uint32_t r = role[o];
@@ -930,7 +939,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, const uint2* toks,
     }
     }
     if (f < 0) return;
-    if (atomicOr(seen, 1u << bit) & (1u << bit)) {
+    if (!(in.variant & JSV_NO_SEEN) && (atomicOr(seen, 1u << bit) & (1u << bit))) {
         js_fail(derr, kpos, KDTN_JSON_DUPKEY);
         return;
     }
@@ -949,7 +958,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, const uint2* toks,
     case R_META: {
         if (null) break;
         if (kind != TK_STR) { ok = false; break; }
-        const uint32_t v = string_slot(j, in, in.kd, i, t.x);
+        const uint32_t v = (in.variant & JSV_NO_INTERN) ? 1u : string_slot(j, in, in.kd, i, t.x);
         if (v == JS_NONE) return;
         uint32_t* dst = r == R_META ? (f == 0 ? to.name : to.ns) : (f == 1 ? to.src_ip : to.net_ns);
         dst[topo] = v;
@@ -977,7 +986,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, const uint2* toks,
         }
         if (null) break;
         if (kind != TK_STR) { ok = false; break; }
-        const uint32_t v = string_slot(j, in, props ? in.pd : in.kd, i, t.x);
+        const uint32_t v = (in.variant & JSV_NO_INTERN) ? 1u : string_slot(j, in, props ? in.pd : in.kd, i, t.x);
         if (v == JS_NONE) return;
         *store_word(*st, rec, props ? COL_PROP0 + f : COL_KEY0 + f) = v;
         break;

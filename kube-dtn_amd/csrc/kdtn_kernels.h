@@ -294,6 +294,8 @@ constexpr uint32_t JS_NONE = 0xFFFFFFFFu, JS_DEEP = 0xFFFFFFFEu;
 enum : uint32_t { R_NONE = 0, R_ROOT, R_ITEMS, R_ITEM, R_META, R_SPEC, R_STATUS, R_SPEC_LINKS, R_STATUS_LINKS,
                   R_LINK_S, R_LINK_R, R_PROPS_S, R_PROPS_R };
 constexpr uint32_t JS_ST_OVERFLOW = 1, JS_ST_LONG = 2;   // intern status bits
+// ingest variants (KDTN_JS_VARIANT, profiling only; bits 1-3 give wrong tables)
+constexpr uint32_t JSV_COHERENT = 1, JSV_NO_SEEN = 2, JSV_NO_REP = 4, JSV_NO_INTERN = 8;
 
 struct JsDoc {
     const uint8_t* doc;        // padded with spaces to nb*64 (+64 B)
@@ -310,6 +312,7 @@ struct JsMasks {
     uint32_t* tcnt;            // tokens per block
     uint32_t* dcnt;            // 64 + opens - closes per block
     uint32_t* ocnt;            // opens per block
+    uint32_t* ccnt;            // colons per block
 };
 struct JsTopoOut {
     uint32_t* ns;
@@ -338,11 +341,13 @@ struct JsIntern {
     uint32_t* status;          // JS_ST_* bits
     uint32_t* seen_root;
     JsDict kd, pd;
+    uint32_t variant;
 };
 __global__ void k_js_quotes(JsDoc j, uint64_t* qmask, uint64_t* bsmask, uint64_t* hbmask, uint32_t* qcnt);
 __global__ void k_js_classify(JsDoc j, const uint64_t* qoff, JsMasks m, unsigned long long* err);
 __global__ void k_js_tokens(JsDoc j, JsMasks m, const uint64_t* toff, const uint64_t* doff, const uint64_t* ooff,
-                            uint2* toks, uint32_t* olist, unsigned long long* err);
+                            const uint64_t* coff, uint2* toks, uint32_t* olist, uint32_t* vlist,
+                            unsigned long long* err);
 __global__ void k_js_par_agg(const uint2* toks, uint32_t ntok, uint32_t* tagg);
 __global__ void k_js_par_group(const uint32_t* tagg, uint32_t ntiles, uint32_t* gagg);
 __global__ void k_js_par_top(uint32_t* gagg, uint32_t ng);
@@ -356,9 +361,9 @@ __global__ void k_js_elems_count(JsDoc j, const uint2* toks, uint32_t ntok, cons
                                  uint32_t* cnt3, unsigned long long* derr);
 __global__ void k_js_elems_write(const uint2* toks, uint32_t ntok, const uint32_t* par, const uint8_t* role,
                                  const uint64_t* coff3, uint32_t ntiles, uint32_t* ord, JsTopoOut to);
-__global__ void k_js_values(JsDoc j, const uint2* toks, uint32_t ntok, const uint32_t* par, const uint8_t* role,
-                            const uint32_t* ord, JsTopoOut to, JsStore des, JsStore real, JsIntern in,
-                            unsigned long long* derr);
+__global__ void k_js_values(JsDoc j, const uint2* toks, const uint32_t* vlist, uint32_t nval, const uint32_t* par,
+                            const uint8_t* role, const uint32_t* ord, JsTopoOut to, JsStore des, JsStore real,
+                            JsIntern in, unsigned long long* derr);
 __global__ void k_js_rep_mark(JsDict dt, uint32_t* bits);
 __global__ void k_js_popc(const uint32_t* bits, uint32_t nw, uint32_t* cnt);
 __global__ void k_js_ids(JsDict dt, const uint32_t* bits, const uint64_t* wrank, uint32_t* slot_id, uint32_t* len_by_id);
