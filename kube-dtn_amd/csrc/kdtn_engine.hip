@@ -98,7 +98,7 @@ struct kdtn_ctx {
     DevBuf j_ocnt, j_ooff, j_olist, j_ccnt, j_coff, j_vlist;
     uint32_t j_kcap = 0, j_pcap = 0;   // intern table sizes that fit the last document
     DevBuf j_toks, j_par, j_role, j_ord, j_tagg, j_gagg, j_cnt3, j_coff3, j_small, j_part;
-    DevBuf j_tflags, j_tseen, j_dseen, j_rseen, j_kslots, j_krep, j_pslots, j_prep, j_heap;
+    DevBuf j_tflags, j_owner, j_vown, j_kslots, j_krep, j_pslots, j_prep, j_heap;
     DevBuf j_bits, j_bcnt, j_wrank, j_kslot_id, j_pslot_id, j_len, j_off64;
     uint64_t j_n = 0;
     uint32_t j_nb = 0;
@@ -442,7 +442,7 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->j_doc, &c->j_q, &c->j_bs, &c->j_hb, &c->j_qcnt, &c->j_qoff, &c->j_tok, &c->j_open,
                       &c->j_close, &c->j_tcnt, &c->j_dcnt, &c->j_toff, &c->j_doff, &c->j_toks, &c->j_par,
                       &c->j_role, &c->j_ord, &c->j_tagg, &c->j_gagg, &c->j_cnt3, &c->j_coff3, &c->j_small,
-                      &c->j_part, &c->j_tflags, &c->j_tseen, &c->j_dseen, &c->j_rseen, &c->j_kslots, &c->j_krep,
+                      &c->j_part, &c->j_tflags, &c->j_owner, &c->j_vown, &c->j_kslots, &c->j_krep,
                       &c->j_pslots, &c->j_prep, &c->j_heap, &c->j_bits, &c->j_bcnt, &c->j_wrank,
                       &c->j_kslot_id, &c->j_pslot_id, &c->j_len, &c->j_off64, &c->j_ocnt, &c->j_ooff,
                       &c->j_olist, &c->j_ccnt, &c->j_coff, &c->j_vlist};
@@ -1305,22 +1305,27 @@ int kdtn_json_ingest(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest_info* 
 
     // 4. output tables
     c->T = T;
-    for (DevBuf* b : {&c->t_ns, &c->t_name, &c->t_src, &c->t_netns, &c->j_tflags, &c->j_tseen})
+    for (DevBuf* b : {&c->t_ns, &c->t_name, &c->t_src, &c->t_netns, &c->j_tflags})
         TRY(ensure(*b, (size_t)T * 4));
     TRY(ensure(c->t_flags, (size_t)T));
     TRY(ensure(c->t_roff, ((size_t)T + 1) * 4));
     TRY(ensure(c->t_noff, ((size_t)T + 1) * 4));
     TRY(link_store_alloc(c, c->des, N));
     TRY(link_store_alloc(c, c->real, M));
-    TRY(ensure(c->j_dseen, (size_t)N * 4));
-    TRY(ensure(c->j_rseen, (size_t)M * 4));
+    const uint64_t owners = 1 + 9ull * T + 22ull * ((uint64_t)N + M);
+    if (owners >= JS_NONE) {
+        std::snprintf(g_last_error, sizeof(g_last_error), "ingest: too many records for one document");
+        return KDTN_EINVAL;
+    }
+    TRY(ensure(c->j_owner, (size_t)owners * 4));
+    TRY(ensure(c->j_vown, (size_t)nval * 4));
     JsTopoOut to{dp<uint32_t>(c->t_ns), dp<uint32_t>(c->t_name), dp<uint32_t>(c->t_src), dp<uint32_t>(c->t_netns),
-                 dp<uint32_t>(c->j_tflags), dp<uint32_t>(c->t_roff), dp<uint32_t>(c->t_noff), dp<uint32_t>(c->j_tseen)};
+                 dp<uint32_t>(c->j_tflags), dp<uint32_t>(c->t_roff), dp<uint32_t>(c->t_noff)};
     k_js_elems_write<<<ntiles, BLOCK, 0, s>>>(toks, ntok, par, role, dp<uint64_t>(c->j_coff3), ntiles, ord, to);
     HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(to.real_off + T), (int)M, 1, s));
     HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(to.des_off + T), (int)N, 1, s));
-    JsStore des{dp<uint32_t>(c->des.buf), dp<uint32_t>(c->j_dseen)};
-    JsStore real{dp<uint32_t>(c->real.buf), dp<uint32_t>(c->j_rseen)};
+    JsStore des{dp<uint32_t>(c->des.buf)};
+    JsStore real{dp<uint32_t>(c->real.buf)};
 
     // 5. schema values + interning; a table or heap that fills up is grown and the pass rerun
     uint32_t kcap = std::max(c->j_kcap, next_pow2(std::max<uint64_t>(1024, 2ull * ((uint64_t)N + M) + 4ull * T)));
@@ -1339,20 +1344,22 @@ int kdtn_json_ingest(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest_info* 
         HIP_TRY(hipMemsetAsync(c->j_prep.p, 0xFF, (size_t)pcap * 4, s));
         HIP_TRY(hipMemsetAsync(small + 2, 0, J_SMALL - 16, s));
         HIP_TRY(hipMemsetAsync(small + 1, 0xFF, 8, s));
-        for (DevBuf* b : {&c->t_ns, &c->t_name, &c->t_src, &c->t_netns, &c->j_tseen})
+        for (DevBuf* b : {&c->t_ns, &c->t_name, &c->t_src, &c->t_netns})
             HIP_TRY(hipMemsetAsync(b->p, 0, (size_t)T * 4, s));
         HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(to.flags), (int)(KDTN_TOPO_SPEC_NIL | KDTN_TOPO_STATUS_NIL),
                                   T, s));
         HIP_TRY(hipMemsetAsync(c->des.buf.p, 0, c->des.buf.cap, s));
         HIP_TRY(hipMemsetAsync(c->real.buf.p, 0, c->real.buf.cap, s));
-        HIP_TRY(hipMemsetAsync(c->j_dseen.p, 0, (size_t)N * 4, s));
-        HIP_TRY(hipMemsetAsync(c->j_rseen.p, 0, (size_t)M * 4, s));
+        if (nval) HIP_TRY(hipMemsetAsync(c->j_vown.p, 0xFF, (size_t)nval * 4, s));
         in.doc = j.doc;
         in.heap = dp<uint8_t>(c->j_heap);
         in.heap_used = small + 2;
         in.heap_cap = hcap;
         in.status = reinterpret_cast<uint32_t*>(small + 3);
-        in.seen_root = reinterpret_cast<uint32_t*>(small + 3) + 1;
+        in.owner = dp<uint32_t>(c->j_owner);
+        in.vown = dp<uint32_t>(c->j_vown);
+        in.own_des = 1 + 9 * T;
+        in.own_real = in.own_des + 22 * N;
         in.variant = (uint32_t)std::strtoul(std::getenv("KDTN_JS_VARIANT") ? std::getenv("KDTN_JS_VARIANT") : "0",
                                             nullptr, 0);
         in.kd = JsDict{dp<unsigned long long>(c->j_kslots), dp<uint32_t>(c->j_krep), kcap - 1};
@@ -1360,6 +1367,9 @@ int kdtn_json_ingest(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest_info* 
         if (nval)
             k_js_values<<<nblocks(nval), BLOCK, 0, s>>>(j, toks, dp<uint32_t>(c->j_vlist), nval, par, role, ord, to,
                                                         des, real, in, small + 1);
+        if (nval && !(in.variant & JSV_NO_SEEN))
+            k_js_dups<<<nblocks(nval), BLOCK, 0, s>>>(toks, dp<uint32_t>(c->j_vlist), nval, dp<uint32_t>(c->j_vown),
+                                                      dp<uint32_t>(c->j_owner), small + 1);
         timer_mark(c, "js_values");
         unsigned long long ctl[3];
         TRY(d2h(c, ctl, small + 1, 3));

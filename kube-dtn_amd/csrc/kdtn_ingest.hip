@@ -498,6 +498,21 @@ KD_INLINE int match_key(const JsDoc& j, uint32_t pos, const char (*names)[16], i
     uint32_t len = 0;
     const uint32_t e = str_end(j, pos);
     if (e - pos - 1 > 6 * 16) return -1;
+    if (e - pos - 1 <= 15 && !any_in(j.bsmask, pos + 1, e)) {     // plain name: three aligned words
+        const uint32_t a = pos + 1, L = e - a;
+        const uint64_t* w = reinterpret_cast<const uint64_t*>(j.doc + (a & ~7u));
+        const uint32_t sh = (a & 7u) * 8;
+        const uint64_t w0 = w[0], w1 = w[1], w2 = w[2];
+        lo = sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;
+        hi = sh ? (w1 >> sh) | (w2 << (64 - sh)) : w1;
+        if (L < 8) { lo &= (1ull << (8 * L)) - 1; hi = 0; }
+        else hi &= L == 8 ? 0ull : (1ull << (8 * (L - 8))) - 1;
+        for (int f = 0; f < n; ++f) {
+            const uint64_t* nm = reinterpret_cast<const uint64_t*>(names[f]);
+            if (nm[0] == lo && nm[1] == hi) return f;
+        }
+        return -1;
+    }
     for (uint32_t k = pos + 1; k < e; ++k) {
         uint32_t c = j.doc[k];
         if (c == '\\') {
@@ -900,49 +915,50 @@ __global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, const uint2* toks,
     const uint2 t = toks[i];
     const uint32_t kind = tkind(t), kpos = toks[i - 2].x;
     const bool null = kind == TK_SCALAR && j.doc[t.x] == 'n';
-    uint32_t* seen;
     int f, bit;
+    uint32_t own;                                      // owner slot of (object, field): duplicate check
     uint32_t topo = 0, rec = 0;
     const JsStore* st = nullptr;
     switch (r) {
     case R_ROOT:
         f = match_key(j, kpos, kItems, 1);
-        seen = in.seen_root; bit = f;
+        bit = f; own = 0;
         break;
     case R_ITEM:
         f = match_key(j, kpos, kItem, 3);
-        topo = ord[o]; seen = to.seen + topo; bit = f;
+        topo = ord[o]; bit = f; own = 1 + topo * 9;
         break;
     case R_META:
         f = match_key(j, kpos, kMeta, 2);
-        topo = ord[par[o]]; seen = to.seen + topo; bit = 3 + f;
+        topo = ord[par[o]]; bit = 3 + f; own = 1 + topo * 9;
         break;
     case R_SPEC:
         f = match_key(j, kpos, kLinks, 1);
-        topo = ord[par[o]]; seen = to.seen + topo; bit = 5 + f;
+        topo = ord[par[o]]; bit = 5 + f; own = 1 + topo * 9;
         break;
     case R_STATUS:
         f = match_key(j, kpos, kStatus, 3);
-        topo = ord[par[o]]; seen = to.seen + topo; bit = 6 + f;
+        topo = ord[par[o]]; bit = 6 + f; own = 1 + topo * 9;
         break;
     case R_LINK_S:
     case R_LINK_R:
         f = match_key(j, kpos, kLink, KDTN_NKEY + 2);
         st = r == R_LINK_S ? &des : &real;
-        rec = ord[o]; seen = st->seen + rec; bit = f;
+        rec = ord[o]; bit = f; own = (r == R_LINK_S ? in.own_des : in.own_real) + rec * 22;
         break;
     default: {                                                    // R_PROPS_S / R_PROPS_R
         f = match_key(j, kpos, kProps, KDTN_NPROP + 1);
         st = r == R_PROPS_S ? &des : &real;
-        rec = ord[par[o]]; seen = st->seen + rec; bit = 9 + f;
+        rec = ord[par[o]]; bit = 9 + f; own = (r == R_PROPS_S ? in.own_des : in.own_real) + rec * 22;
         break;
     }
     }
     if (f < 0) return;
-    if (!(in.variant & JSV_NO_SEEN) && (atomicOr(seen, 1u << bit) & (1u << bit))) {
-        js_fail(derr, kpos, KDTN_JSON_DUPKEY);
-        return;
-    }
+    // a plain store of this member's token index; k_js_dups then flags every member whose
+    // (object, field) slot another member overwrote (no atomics on the hot path)
+    own += bit;
+    in.owner[own] = i;
+    in.vown[k] = own;
     bool ok = true;
     switch (r) {
     case R_ROOT: ok = null || kind == TK_ARR; break;
@@ -993,6 +1009,19 @@ __global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, const uint2* toks,
     }
     }
     if (!ok) js_fail(derr, t.x, KDTN_JSON_TYPE);
+}
+
+// a schema field repeated in one object: both members stored into the same owner slot and
+// only one of them can find itself there
+__global__ void __launch_bounds__(BLOCK) k_js_dups(const uint2* toks, const uint32_t* vlist, uint32_t nval,
+                                                   const uint32_t* vown, const uint32_t* owner,
+                                                   unsigned long long* derr) {
+    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+    if (k >= nval) return;
+    const uint32_t own = vown[k];
+    if (own == JS_NONE) return;
+    const uint32_t i = vlist[k];
+    if (owner[own] != i) js_fail(derr, toks[i - 2].x, KDTN_JSON_DUPKEY);
 }
 
 // ---------------------------------------------------------------- ids in first-occurrence order

@@ -322,11 +322,9 @@ struct JsTopoOut {
     uint32_t* flags;           // u32 KDTN_TOPO_* bits during the decode
     uint32_t* real_off;
     uint32_t* des_off;
-    uint32_t* seen;            // schema fields met per topology (duplicate check)
 };
 struct JsStore {
     uint32_t* base;            // AoSoA link store (DevLinks layout)
-    uint32_t* seen;            // schema fields met per record
 };
 struct JsDict {
     unsigned long long* slots; // key words, 0 = empty
@@ -339,7 +337,9 @@ struct JsIntern {
     unsigned long long* heap_used;
     uint64_t heap_cap;
     uint32_t* status;          // JS_ST_* bits
-    uint32_t* seen_root;
+    uint32_t* owner;           // token index per (object, schema field): root 1, topology 9, record 22
+    uint32_t* vown;            // per member value: its owner slot, JS_NONE = not a schema field
+    uint32_t own_des, own_real;   // first record slot of each side
     JsDict kd, pd;
     uint32_t variant;
 };
@@ -364,6 +364,8 @@ __global__ void k_js_elems_write(const uint2* toks, uint32_t ntok, const uint32_
 __global__ void k_js_values(JsDoc j, const uint2* toks, const uint32_t* vlist, uint32_t nval, const uint32_t* par,
                             const uint8_t* role, const uint32_t* ord, JsTopoOut to, JsStore des, JsStore real,
                             JsIntern in, unsigned long long* derr);
+__global__ void k_js_dups(const uint2* toks, const uint32_t* vlist, uint32_t nval, const uint32_t* vown,
+                          const uint32_t* owner, unsigned long long* derr);
 __global__ void k_js_rep_mark(JsDict dt, uint32_t* bits);
 __global__ void k_js_popc(const uint32_t* bits, uint32_t nw, uint32_t* cnt);
 __global__ void k_js_ids(JsDict dt, const uint32_t* bits, const uint64_t* wrank, uint32_t* slot_id, uint32_t* len_by_id);
