@@ -127,6 +127,7 @@ KD_INLINE uint32_t window4(const uint32_t* w, uint32_t q) {
     const uint32_t hi = i == 0 ? w[1] : i == 1 ? w[2] : i == 2 ? w[3] : i == 3 ? w[4] : w[5];
     return __builtin_amdgcn_alignbyte(hi, lo, q & 3u);
 }
+KD_INLINE bool hexb(uint32_t c) { return (c - '0' < 10u) | ((c | 0x20u) - 'a' < 6u); }
 // one dotted-quad field of n digits starting with the 4-byte window c: dtoi, <= 255 and no
 // leading zero (net.parseIPv4, Go 1.18)
 KD_INLINE uint32_t octet_ok(uint32_t c, uint32_t n) {
@@ -185,14 +186,27 @@ KD_INLINE bool cidr_swar(const uint32_t* w, uint32_t len, bool* slow) {
 KD_INLINE uint32_t kdict_bits(const uint8_t* bytes, uint32_t b, uint32_t len, const uint32_t* w, uint32_t i,
                               uint32_t* special) {
     uint32_t f = 0;
-    if (len) {
+    const uint32_t c0 = w[0] & 0xFFu;
+    if (len && !hexb(c0) && c0 != ':') {
+        // neither an IP (digit, hex digit or ':' first: parseIPv4 / parseIPv6) nor a MAC (hex
+        // digit first): both predicates fail without classifying the bytes
+        f = (1u << KB_CIDR_BAD) | (1u << KB_MAC_BAD);
+    } else if (len) {
         bool slow = true, cok = false;
         if (len <= 24) cok = cidr_swar(w, len, &slow);
         if (slow) cok = cidr_ok(bytes + b, len);                       // common/veth.go:22
         if (!cok) f |= 1u << KB_CIDR_BAD;
         const uint32_t c2 = wbyte(w, 2), c4 = wbyte(w, 4);
         bool mok = false;                                              // common/veth.go:33
-        if (len >= 14 && (c2 == ':' || c2 == '-' || c4 == '.')) mok = mac_ok(bytes + b, len);
+        // net.ParseMAC's necessary conditions, decided in registers: the length of one of its
+        // six layouts and hex digits in the first group (s[0..1] for ':'/'-', s[0..3] for '.').
+        // Only candidates run the byte-wise parser (an IPv4 CIDR like "10.5.123.45/31" has
+        // s[4] == '.' and len 14, and used to take it in most waves).
+        bool cand = false;
+        if (c2 == ':' || c2 == '-') cand = (len == 17 || len == 23 || len == 59) && hexb(wbyte(w, 0)) && hexb(wbyte(w, 1));
+        else if (c4 == '.') cand = (len == 14 || len == 19 || len == 49) && hexb(wbyte(w, 0)) && hexb(wbyte(w, 1)) &&
+                                   hexb(c2) && hexb(wbyte(w, 3));
+        if (cand) mok = mac_ok(bytes + b, len);
         if (!mok) f |= 1u << KB_MAC_BAD;
     }
     const uint32_t w2b = w[2] & 0xFFu;

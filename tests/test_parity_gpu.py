@@ -102,7 +102,9 @@ def test_parser_fuzz_vs_oracle(engine, field, pool):
         assert got[i].tobytes() == want.tobytes(), (field, s, got[i], want)
 
 
-def test_cidr_mac_via_epoch(engine):
+@pytest.mark.parametrize("kd_sub", ["1", "2"])
+def test_cidr_mac_via_epoch(engine, kd_sub, monkeypatch):
+    monkeypatch.setenv("KDTN_KD_SUB", kd_sub)      # 1 or 2 strings per thread in k_kdict_flags
     rng = random.Random(5)
     ips = IPS + ["1.2.3.4/32", "255.255.255.255/0", "::/0", "::ffff:1.2.3.4/96", "1::2::3/64",
                  "1:2:3:4:5:6:7:8/128", "1:2:3:4:5:6:7:8:9/128", "::1.2.3.4/128", "1.2.3/24",
@@ -138,9 +140,12 @@ def _mutate(rng: random.Random, s: str, alphabet: str) -> str:
     return "".join(s)
 
 
-def test_key_predicates_fuzz(engine):
+@pytest.mark.parametrize("kd_sub", ["1", "2", "4"])
+def test_key_predicates_fuzz(engine, kd_sub, monkeypatch):
     """net.ParseCIDR / net.ParseMAC / localhost / physical/ predicates of key strings (the
-    register fast path of k_kdict_flags and its generic fallback) against the oracle."""
+    register fast path of k_kdict_flags and its generic fallback) against the oracle, for
+    1, 2 and 4 strings per thread; long strings take the generic parsers."""
+    monkeypatch.setenv("KDTN_KD_SUB", kd_sub)
     rng = random.Random(11)
     ipa, maca = "0123456789./:", "0123456789abcdefABCDEFG:-."
     ips = [f"{rng.randint(0, 300)}.{rng.randint(0, 300)}.{rng.randint(0, 300)}.{rng.randint(0, 300)}"
@@ -148,6 +153,8 @@ def test_key_predicates_fuzz(engine):
     ips += [_mutate(rng, rng.choice(ips), ipa) for _ in range(1500)]
     ips += ["".join(rng.choice(ipa) for _ in range(rng.randint(0, 30))) for _ in range(700)]
     ips += ["0" * 30 + "1.2.3.4/8", "1.2.3.4/" + "0" * 25 + "8", "255.255.255.255/32", "1.2.3.4/32x"]
+    ips += ["1" * k + ".2.3.4/8" for k in (1500, 1800, 2100, 2400, 2700, 3000, 3300, 3600)]
+    ips += ["localhost", "default", "physical/1.2.3.4"] + [f"10.{k}.0.1/24" for k in range(40)]
     macs = [":".join(f"{rng.randint(0, 255):02x}" for _ in range(rng.choice([6, 8, 20])))
             for _ in range(300)]
     macs += [_mutate(rng, rng.choice(macs), maca) for _ in range(700)]
