@@ -114,7 +114,7 @@ constexpr int VAR_NT_LOAD = 1, VAR_NT_STORE = 2, VAR_NO_QSTORE = 4, VAR_NT_POD =
               VAR_MASK_EMPTY = 512, VAR_NO_PREFIX = 1024;
 constexpr int var_waves(int v) { return (v & VAR_OCC6) ? 6 : (v & VAR_OCC5) ? 5 : 1; }
 constexpr int TRACE_WORDS = 6;   // entry, topologies loaded, counts done, bases known, end, hw ids
-constexpr int DEFAULT_VARIANT = VAR_NT_LOAD | VAR_MASK_EMPTY;
+constexpr int DEFAULT_VARIANT = VAR_NT_LOAD | VAR_NT_STORE | VAR_MASK_EMPTY;   // 515
 
 struct DevTopos {
     const uint32_t* ns;

@@ -795,7 +795,16 @@ __device__ __forceinline__ void wave_store_qdisc(uint2* outq, bool active, uint3
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         uint2* dst = outq + (size_t)(p0 + r0) * 9;
         const uint32_t nq = cnt * 9;
-        for (uint32_t k = lane; k < nq; k += 64) dst[k] = stage[k];
+        for (uint32_t k = lane; k < nq; k += 64) {
+            if constexpr ((V & VAR_NT_STORE) != 0) {
+                u32x2 v;
+                v.x = stage[k].x;
+                v.y = stage[k].y;
+                __builtin_nontemporal_store(v, reinterpret_cast<u32x2*>(dst + k));
+            } else {
+                dst[k] = stage[k];
+            }
+        }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1380,5 +1389,8 @@ template __global__ void k_reconcile<641>(DevTopos, DevLinks, DevLinks, DevTable
 template __global__ void k_reconcile<545>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
 template __global__ void k_reconcile<1025>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
 template __global__ void k_reconcile<1537>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
+template __global__ void k_reconcile<515>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
+template __global__ void k_reconcile<521>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
+template __global__ void k_reconcile<523>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
 
 }  // namespace kdtn

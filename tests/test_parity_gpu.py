@@ -238,7 +238,7 @@ def test_config2_full_size_properties(engine):
     assert out.add_qdisc[s:e].tobytes() == ora.add_qdisc.tobytes()
 
 
-@pytest.mark.parametrize("variant", [1, 1025, 1537, 641, 0])
+@pytest.mark.parametrize("variant", [1, 1025, 1537, 641, 0, 513, 523])
 def test_emission_variants_match_oracle(engine, variant, monkeypatch):
     """Every non-profiling KDTN_VARIANT of k_reconcile (occupancy target, masked gathers,
     early issue before the look-back) produces the oracle's bytes."""
