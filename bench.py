@@ -296,9 +296,9 @@ def main():
         "counts": {"add": counts.n_add, "upd": counts.n_upd, "del": counts.n_del},
         "gen_s": round(gen_s, 2),
     }
-    if not args.no_wire:
+    if not args.no_wire and world == 1:
         result["wire_stage"] = wire_stage(eng)
-    if rank == 0 and not args.no_cpu_baseline:
+    if world == 1 and not args.no_cpu_baseline:            # CPU baseline: rank 0 at N=1 only
         result["cpu_baseline"] = cpu_baseline(inp, args.cpu_budget_s, args.cpu_threads)
     if not args.no_ingest and world == 1:
         result["ingest_stage"] = ingest_stage(eng, inp)

@@ -60,6 +60,8 @@ struct kdtn_ctx {
     kdtn_config cfg{};
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
+    hipStream_t comm_stream = nullptr;          // RCCL pod-status exchange (nranks > 1)
+    hipEvent_t ev_fill = nullptr, ev_ag = nullptr;
     // dictionaries
     DevBuf kd_bytes, kd_offs, kd_bits, pd_bytes, pd_offs, pd_pct, pd_dur, pd_rate, pd_rerr;
     uint32_t D = 0, P = 0;
@@ -428,6 +430,7 @@ void kdtn_destroy(kdtn_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
+    if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
     DevBuf* bufs[] = {&c->kd_bytes, &c->kd_offs, &c->kd_bits, &c->pd_bytes, &c->pd_offs,
                       &c->pd_pct, &c->pd_dur, &c->pd_rate, &c->pd_rerr, &c->t_ns, &c->t_name, &c->t_src,
                       &c->t_netns, &c->t_flags, &c->t_roff, &c->t_noff, &c->real.buf, &c->des.buf,
@@ -450,6 +453,9 @@ void kdtn_destroy(kdtn_ctx* c) {
     for (int i = 0; i <= kMaxTimers; ++i)
         if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
     if (c->comm) (void)ncclCommDestroy(c->comm);
+    if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
+    if (c->ev_fill) (void)hipEventDestroy(c->ev_fill);
+    if (c->ev_ag) (void)hipEventDestroy(c->ev_ag);
     if (c->h_misc) (void)hipHostFree(c->h_misc);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
@@ -531,6 +537,27 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
     HIP_TRY(hipMemsetAsync(c->sync.p, 0, sync_bytes(c->nwg), s));    // ticket, error, look-back
 
     const DevTopos T = topo_view(c);
+    const bool resolve = stages & KDTN_STAGE_RESOLVE;
+    const bool exchange = resolve && c->nranks > 1;
+    if (resolve) {
+        // pod-status rows first: across ranks they are all-gathered over RCCL on the comm
+        // stream while this stream parses the dictionaries (the exchange needs neither)
+        const uint32_t rank_base = c->slice * (uint32_t)c->rank;
+        if (c->slice) k_pods_fill<<<nblocks(c->slice), BLOCK, 0, s>>>(T, c->slice, rank_base, dp<uint4>(c->pods));
+        if (exchange) {
+            HIP_TRY(hipEventRecord(c->ev_fill, s));
+            HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_fill, 0));
+            uint4* pods = dp<uint4>(c->pods);
+            ncclResult_t r = ncclAllGather(pods + rank_base, pods, (size_t)c->slice * 4, ncclUint32, c->comm,
+                                           c->comm_stream);
+            if (r != ncclSuccess) {
+                std::snprintf(g_last_error, sizeof(g_last_error), "ncclAllGather: %s", ncclGetErrorString(r));
+                return KDTN_EIO;
+            }
+            HIP_TRY(hipEventRecord(c->ev_ag, c->comm_stream));
+        }
+        timer_mark(c, "pods_fill");
+    }
     // dictionaries
     if (c->D) {
         int sub = 1;                                                   // strings per thread (2, 4: slower)
@@ -547,19 +574,8 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
                                                          c->P, c->cfg.tick_in_usec, dp<uint32_t>(c->pd_pct),
                                                          dp<uint2>(c->pd_dur), dp<uint2>(c->pd_rate), dp<uint32_t>(c->pd_rerr));
     timer_mark(c, "pdict_parse");
-    const bool resolve = stages & KDTN_STAGE_RESOLVE;
     if (resolve) {
-        // pod-status table (+ all-gather across ranks) and lookup tables
-        const uint32_t rank_base = c->slice * (uint32_t)c->rank;
-        if (c->slice) k_pods_fill<<<nblocks(c->slice), BLOCK, 0, s>>>(T, c->slice, rank_base, dp<uint4>(c->pods));
-        if (c->nranks > 1) {
-            uint4* pods = dp<uint4>(c->pods);
-            ncclResult_t r = ncclAllGather(pods + rank_base, pods, (size_t)c->slice * 4, ncclUint32, c->comm, s);
-            if (r != ncclSuccess) {
-                std::snprintf(g_last_error, sizeof(g_last_error), "ncclAllGather: %s", ncclGetErrorString(r));
-                return KDTN_EIO;
-            }
-        }
+        if (exchange) HIP_TRY(hipStreamWaitEvent(s, c->ev_ag, 0));   // exchange not hidden by the parses
         timer_mark(c, "pods_allgather");
         if (++c->pod_stamp >= 0x7FFFFFFFu) {                          // stamp wrap: clear once
             HIP_TRY(hipMemsetAsync(c->pod_direct.p, 0, c->pod_direct.cap, s));
@@ -1503,6 +1519,11 @@ int kdtn_comm_init(kdtn_ctx* c, const uint8_t uid[128], int nranks, int rank) {
     c->rank = rank;
     c->uploaded = false;
     if (nranks == 1) return KDTN_OK;
+    if (!c->comm_stream) {
+        HIP_TRY(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&c->ev_fill, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&c->ev_ag, hipEventDisableTiming));
+    }
     ncclUniqueId id;
     std::memcpy(&id, uid, 128);
     ncclResult_t r = ncclCommInitRank(&c->comm, nranks, id, rank);
