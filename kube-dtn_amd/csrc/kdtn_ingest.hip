@@ -681,6 +681,40 @@ __global__ void __launch_bounds__(BLOCK) k_js_elems_write(const uint2* toks, uin
 // ---------------------------------------------------------------- schema values
 KD_INLINE uint64_t fnv_step(uint64_t h, uint32_t c) { return (h ^ c) * 1099511628211ull; }
 
+// The 32 document bytes starting at byte a, as 8 words aligned to a: nine aligned dword
+// loads issued together (the document has >= 128 bytes of padding), so a short string costs
+// one memory round trip instead of one per byte.
+constexpr uint32_t WIN = 32;
+KD_INLINE void load_window(const uint8_t* doc, uint32_t a, uint32_t u[8]) {
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(doc + (a & ~3u));
+    uint32_t w[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) w[k] = p[k];
+    const uint32_t sh = a & 3u;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) u[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+}
+KD_INLINE uint32_t win_byte(const uint32_t u[8], int k) { return (u[k >> 2] >> (8 * (k & 3))) & 0xFFu; }
+// FNV-1a over the first len (<= WIN) bytes of a window: the same value as the byte loop
+KD_INLINE uint64_t fnv_window(const uint32_t u[8], uint32_t len) {
+    uint64_t h = 1469598103934665603ull;
+#pragma unroll
+    for (int k = 0; k < (int)WIN; ++k)
+        if ((uint32_t)k < len) h = fnv_step(h, win_byte(u, k));
+    return h;
+}
+// first len (<= WIN) bytes of two windows equal
+KD_INLINE bool window_eq(const uint32_t a[8], const uint32_t b[8], uint32_t len) {
+    bool eq = true;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint32_t lo = 4u * k;
+        const uint32_t m = len >= lo + 4 ? 0xFFFFFFFFu : len <= lo ? 0u : (1u << (8 * (len - lo))) - 1u;
+        eq &= ((a[k] ^ b[k]) & m) == 0;
+    }
+    return eq;
+}
+
 // utf8.DecodeRune length of a valid sequence at s (bounded by e), 0 = invalid
 KD_INLINE uint32_t utf8_len(const uint8_t* s, const uint8_t* e) {
     const uint32_t c = s[0];
@@ -788,7 +822,7 @@ KD_INLINE const uint8_t* key_bytes(const JsIntern& in, uint64_t kw) {
 
 // returns the table slot of the string [p, p+len) (len ≥ 1), or JS_NONE on overflow
 KD_INLINE uint32_t intern(const JsIntern& in, const JsDict& dt, const uint8_t* p, uint32_t len, uint64_t kw_self,
-                          uint64_t h, uint32_t occ) {
+                          uint64_t h, uint32_t occ, const uint32_t* pw = nullptr) {
     const uint64_t tag = h >> 57;
     const uint64_t kw = (tag << 57) | kw_self;
     uint32_t s = (uint32_t)h & dt.mask;
@@ -816,6 +850,10 @@ KD_INLINE uint32_t intern(const JsIntern& in, const JsDict& dt, const uint8_t* p
                     if (((wd >> (8 * ((off + k) & 3))) & 0xFFu) != p[k]) break;
                     ++k;
                 }
+            } else if (pw && len <= WIN) {            // both in the document: compare windows
+                uint32_t qw[8];
+                load_window(in.doc, (uint32_t)cur, qw);
+                k = window_eq(pw, qw, len) ? len : 0u;
             } else {
                 const uint8_t* q = in.doc + (uint32_t)cur;
                 while (k < len && q[k] == p[k]) ++k;
@@ -839,10 +877,18 @@ KD_INLINE uint32_t string_slot(const JsDoc& j, const JsIntern& in, const JsDict&
     if (!any_in(j.bsmask, a, e) && !any_in(j.hbmask, a, e)) {     // plain ASCII: the bytes themselves
         const uint32_t len = e - a;
         if (len > 0xFFFFFFu) { atomicOr(in.status, JS_ST_LONG); return JS_NONE; }
-        uint64_t h = 1469598103934665603ull;
-        for (uint32_t k = a; k < e; ++k) h = fnv_step(h, j.doc[k]);
+        uint64_t h;
+        uint32_t pw[8];
+        const bool win = len <= WIN;
+        if (win) {
+            load_window(j.doc, a, pw);
+            h = fnv_window(pw, len);
+        } else {
+            h = 1469598103934665603ull;
+            for (uint32_t k = a; k < e; ++k) h = fnv_step(h, j.doc[k]);
+        }
         h ^= h >> 29;
-        const uint32_t s = intern(in, dt, j.doc + a, len, ((uint64_t)len << 32) | a, h, i);
+        const uint32_t s = intern(in, dt, j.doc + a, len, ((uint64_t)len << 32) | a, h, i, win ? pw : nullptr);
         return s == JS_NONE ? JS_NONE : s + 1;
     }
     const uint32_t len = unquote_len(j.doc, a, e);
@@ -860,7 +906,42 @@ KD_INLINE uint32_t string_slot(const JsDoc& j, const JsIntern& in, const JsDict&
 }
 
 // strconv.ParseInt(s, 10, 64) / ParseUint + uint32 overflow on the scalar at pos
+// The scalar's bytes up to its terminator from one window: v = the digits (at most 20) as a
+// u64 with overflow beyond 2^64 flagged, nd = their count, neg = a leading '-'; returns false
+// when the window holds no terminator (long scalars take the byte loops below).
+KD_INLINE bool scalar_window(const JsDoc& j, uint32_t pos, uint64_t* v, uint32_t* nd, bool* neg, bool* bad) {
+    uint32_t u[8];
+    load_window(j.doc, pos, u);
+    *neg = (u[0] & 0xFFu) == '-';
+    uint64_t x = 0;
+    uint32_t n = 0;
+    bool done = false, b = false;
+#pragma unroll
+    for (int k = 0; k < (int)WIN; ++k) {
+        const uint32_t c = win_byte(u, k);
+        if (done || (k == 0 && *neg)) continue;
+        if (c <= 0x20 || c == ',' || c == '}' || c == ']') { done = true; continue; }
+        if (c - '0' >= 10u) b = true;
+        if (x > (~0ull - 9) / 10) b = true;
+        x = x * 10 + (c - '0');
+        ++n;
+    }
+    *v = x;
+    *nd = n;
+    *bad = b;
+    return done;
+}
 KD_INLINE bool parse_int64(const JsDoc& j, uint32_t pos, int64_t* out) {
+    {
+        uint64_t v;
+        uint32_t nd;
+        bool neg, bad;
+        if (scalar_window(j, pos, &v, &nd, &neg, &bad)) {
+            if (bad || !nd || v > (1ull << 63) || (!neg && v > 0x7FFFFFFFFFFFFFFFull)) return false;
+            *out = neg ? (int64_t)(0ull - v) : (int64_t)v;
+            return true;
+        }
+    }
     uint32_t i = pos;
     const bool neg = j.doc[i] == '-';
     if (neg) ++i;
@@ -880,6 +961,16 @@ KD_INLINE bool parse_int64(const JsDoc& j, uint32_t pos, int64_t* out) {
     return true;
 }
 KD_INLINE bool parse_uint32(const JsDoc& j, uint32_t pos, uint32_t* out) {
+    {
+        uint64_t v;
+        uint32_t nd;
+        bool neg, bad;
+        if (scalar_window(j, pos, &v, &nd, &neg, &bad)) {
+            if (neg || bad || !nd || v > 0xFFFFFFFFull) return false;
+            *out = (uint32_t)v;
+            return true;
+        }
+    }
     uint64_t v = 0;
     uint32_t nd = 0;
     for (uint32_t i = pos; i < j.n; ++i) {

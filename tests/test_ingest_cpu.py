@@ -48,7 +48,11 @@ def both(doc: bytes):
 
 WORDS = ["eth0", "eth1", "r1", "r2", "default", "kube-system", "10.0.0.1/24", "12.12.12.2/24",
          "00:00:5e:00:53:01", "physical/10.1.1.1", "localhost", "é", "中文", "😀x", "a\"b", "a\\b",
-         "tab\there", "/run/netns/r1", "", "10ms", "0.5", "1Gbit", "100Mibps", "1.5s", "99.9"]
+         "tab\there", "/run/netns/r1", "", "10ms", "0.5", "1Gbit", "100Mibps", "1.5s", "99.9",
+         # around the GPU's 32-byte string window: equal prefixes, last-byte differences
+         "x" * 31, "x" * 32, "x" * 33, "x" * 31 + "y", "x" * 32 + "y", "x" * 64,
+         "/run/netns/cni-0123456789abcdef0", "/run/netns/cni-0123456789abcdef1",
+         "/run/netns/cni-0123456789abcde", "/run/netns/cni-0123456789abcdf"]
 
 
 def rand_link(rng):
@@ -152,6 +156,11 @@ TYPE_ERRORS = [
     b'{"items":[{"spec":{"links":[{"properties":{"gap":4294967296}}]}}]}',
     b'{"items":[{"spec":{"links":[{"properties":{"gap":1.0}}]}}]}',
     b'{"items":[{"spec":{"links":[{"properties":{"rate":100}}]}}]}',
+    b'{"items":[{"spec":{"links":[{"uid":12345678901234567890123456789012345}]}}]}',
+    b'{"items":[{"spec":{"links":[{"uid":-1234567890123456789012345678901234}]}}]}',
+    b'{"items":[{"spec":{"links":[{"properties":{"gap":123456789012345678901234567890123}}]}}]}',
+    b'{"items":[{"spec":{"links":[{"uid":18446744073709551616}]}}]}',
+    b'{"items":[{"spec":{"links":[{"properties":{"gap":18446744073709551615}}]}}]}',
 ]
 
 
