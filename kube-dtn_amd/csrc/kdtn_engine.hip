@@ -1230,7 +1230,8 @@ int kdtn_json_ingest(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest_info* 
     unsigned long long* small = dp<unsigned long long>(c->j_small);
     HIP_TRY(hipMemsetAsync(small, 0xFF, 16, s));
     HIP_TRY(hipMemsetAsync(small + 2, 0, J_SMALL - 16, s));
-    for (DevBuf* b : {&c->j_q, &c->j_bs, &c->j_hb, &c->j_tok, &c->j_open, &c->j_close}) TRY(ensure(*b, (size_t)nb * 8));
+    // one word past the end: any_in reads the word after a string's first (its bits are masked)
+    for (DevBuf* b : {&c->j_q, &c->j_bs, &c->j_hb, &c->j_tok, &c->j_open, &c->j_close}) TRY(ensure(*b, ((size_t)nb + 1) * 8));
     for (DevBuf* b : {&c->j_qcnt, &c->j_tcnt, &c->j_dcnt, &c->j_ocnt, &c->j_ccnt}) TRY(ensure(*b, (size_t)nb * 4));
     for (DevBuf* b : {&c->j_qoff, &c->j_toff, &c->j_doff, &c->j_ooff, &c->j_coff})
         TRY(ensure(*b, ((size_t)nb + 1) * 8));

@@ -182,7 +182,16 @@ KD_INLINE uint32_t kind_of(uint32_t c) {
 __global__ void __launch_bounds__(BLOCK) k_js_tokens(JsDoc j, JsMasks m, const uint64_t* toff, const uint64_t* doff,
                                                      const uint64_t* ooff, const uint64_t* coff, uint2* toks,
                                                      uint32_t* olist, uint32_t* vlist, unsigned long long* err) {
+    // each lane's 64-byte block goes to LDS first, so the per-token kind lookups below are LDS
+    // reads instead of one dependent global byte load per token
+    __shared__ uint4 blk[BLOCK * 4];
     const uint32_t b = blockIdx.x * BLOCK + threadIdx.x;
+    if (b < j.nb) {
+        const uint4* p = reinterpret_cast<const uint4*>(j.doc + (size_t)b * 64);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) blk[threadIdx.x * 4 + q] = p[q];
+    }
+    const uint8_t* mine = reinterpret_cast<const uint8_t*>(blk + threadIdx.x * 4);
     if (b >= j.nb) return;
     uint64_t tok = m.tok[b];
     if (!tok) return;
@@ -196,7 +205,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_tokens(JsDoc j, JsMasks m, const u
         const uint64_t below = (1ull << k) - 1;
         int64_t d = d0 + __popcll(op & below) - __popcll(cl & below);
         const uint32_t pos = b * 64 + k;
-        const uint32_t kind = kind_of(j.doc[pos]);
+        const uint32_t kind = kind_of(mine[k]);
         if (d < 0 || ((kind == TK_OBJ_END || kind == TK_ARR_END) && d < 1)) {
             js_fail(err, pos, KDTN_JSON_SYNTAX);      // a close with nothing open
             d = d < 0 ? 0 : d;
@@ -384,6 +393,14 @@ KD_INLINE uint32_t str_end(const JsDoc& j, uint32_t pos) {
 // any bit of mask[] in byte range [a, e)
 KD_INLINE bool any_in(const uint64_t* mask, uint32_t a, uint32_t e) {
     if (a >= e) return false;
+    if (e - a <= 64) {                                 // two words, no loop (masks have nb + 1 words)
+        const uint32_t b = a >> 6, sh = a & 63u, L = e - a;
+        uint64_t w = mask[b] >> sh;
+        const uint64_t nx = mask[b + 1];
+        w |= sh ? nx << (64 - sh) : 0ull;
+        if (L < 64) w &= (1ull << L) - 1;
+        return w != 0;
+    }
     uint32_t b = a >> 6;
     const uint32_t be = (e - 1) >> 6;
     uint64_t w = mask[b] & (~0ull << (a & 63));
@@ -507,11 +524,12 @@ KD_INLINE int match_key(const JsDoc& j, uint32_t pos, const char (*names)[16], i
         hi = sh ? (w1 >> sh) | (w2 << (64 - sh)) : w1;
         if (L < 8) { lo &= (1ull << (8 * L)) - 1; hi = 0; }
         else hi &= L == 8 ? 0ull : (1ull << (8 * (L - 8))) - 1;
+        int hit = -1;                                              // names are distinct
         for (int f = 0; f < n; ++f) {
             const uint64_t* nm = reinterpret_cast<const uint64_t*>(names[f]);
-            if (nm[0] == lo && nm[1] == hi) return f;
+            hit = (nm[0] == lo && nm[1] == hi) ? f : hit;
         }
-        return -1;
+        return hit;
     }
     for (uint32_t k = pos + 1; k < e; ++k) {
         uint32_t c = j.doc[k];
@@ -695,12 +713,22 @@ KD_INLINE void load_window(const uint8_t* doc, uint32_t a, uint32_t u[8]) {
     for (int k = 0; k < 8; ++k) u[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
 }
 KD_INLINE uint32_t win_byte(const uint32_t u[8], int k) { return (u[k >> 2] >> (8 * (k & 3))) & 0xFFu; }
-// FNV-1a over the first len (<= WIN) bytes of a window: the same value as the byte loop
-KD_INLINE uint64_t fnv_window(const uint32_t u[8], uint32_t len) {
-    uint64_t h = 1469598103934665603ull;
+// Hash of a string of len (<= WIN) bytes held in a window: one 64-bit FNV-style step per
+// 4-byte word (bytes past len masked off, len folded into the seed). Every string of at most
+// WIN bytes is hashed this way, from the document or the decode heap alike, and longer
+// strings by the byte loop, so equal strings always hash equally. Words past the longest
+// string of the wave are skipped (wave-uniform test), the rest predicated without branches.
+KD_INLINE uint64_t word_hash(const uint32_t u[8], uint32_t len) {
+    uint64_t h = 1469598103934665603ull ^ len;
 #pragma unroll
-    for (int k = 0; k < (int)WIN; ++k)
-        if ((uint32_t)k < len) h = fnv_step(h, win_byte(u, k));
+    for (int k = 0; k < 8; ++k) {
+        const uint32_t lo = 4u * k;
+        if (__ballot(lo < len)) {
+            const uint32_t m = len >= lo + 4 ? 0xFFFFFFFFu : len <= lo ? 0u : (1u << (8 * (len - lo))) - 1u;
+            const uint64_t hn = fnv_step(h, u[k] & m);
+            h = lo < len ? hn : h;
+        }
+    }
     return h;
 }
 // first len (<= WIN) bytes of two windows equal
@@ -882,7 +910,7 @@ KD_INLINE uint32_t string_slot(const JsDoc& j, const JsIntern& in, const JsDict&
         const bool win = len <= WIN;
         if (win) {
             load_window(j.doc, a, pw);
-            h = fnv_window(pw, len);
+            h = word_hash(pw, len);
         } else {
             h = 1469598103934665603ull;
             for (uint32_t k = a; k < e; ++k) h = fnv_step(h, j.doc[k]);
@@ -899,7 +927,13 @@ KD_INLINE uint32_t string_slot(const JsDoc& j, const JsIntern& in, const JsDict&
     uint8_t* out = in.heap + at;
     unquote_write(j.doc, a, e, out);
     uint64_t h = 1469598103934665603ull;
-    for (uint32_t k = 0; k < len; ++k) h = fnv_step(h, out[k]);
+    if (len <= WIN) {                                  // the heap has 64 B of slack past heap_cap
+        uint32_t hw[8];
+        load_window(in.heap, (uint32_t)at, hw);
+        h = word_hash(hw, len);
+    } else {
+        for (uint32_t k = 0; k < len; ++k) h = fnv_step(h, out[k]);
+    }
     h ^= h >> 29;
     const uint32_t s = intern(in, dt, out, len, (1ull << 56) | ((uint64_t)len << 32) | (uint32_t)at, h, i);
     return s == JS_NONE ? JS_NONE : s + 1;
