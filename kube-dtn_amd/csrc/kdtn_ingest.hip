@@ -234,9 +234,10 @@ __global__ void __launch_bounds__(BLOCK) k_js_par_agg(const uint2* toks, uint32_
     uint32_t* row = sh + threadIdx.x * (JS_PD + 1);
 #pragma unroll
     for (int d = 0; d < JS_PD; ++d) row[d] = 0;
-    const uint32_t base = blockIdx.x * JS_TILE + threadIdx.x * JS_PER;
-    for (int k = 0; k < JS_PER; ++k) {
-        const uint32_t i = base + k;
+    // a tile's aggregate is a max, so the tokens are read coalesced (token t0 + q*BLOCK + tid)
+    const uint32_t t0 = blockIdx.x * JS_TILE;
+    for (int q = 0; q < JS_PER; ++q) {
+        const uint32_t i = t0 + q * BLOCK + threadIdx.x;
         if (i >= ntok) break;
         const uint32_t meta = toks[i].y;
         const uint32_t d = meta & TK_DEPTH_MASK;
@@ -316,18 +317,31 @@ __global__ void __launch_bounds__(BLOCK) k_js_par_tiles(uint32_t* tagg, uint32_t
     }
 }
 
+// tile-local token l of thread l / JS_PER lives at tpad(l): rows of JS_PER + 1 words, so the
+// threads' sequential walks over their JS_PER tokens hit distinct LDS banks
+KD_INLINE uint32_t tpad(uint32_t l) { return l + l / JS_PER; }
+constexpr int JS_TPAD = JS_TILE + JS_TILE / JS_PER;
+
 __global__ void __launch_bounds__(BLOCK) k_js_par_apply(const uint2* toks, uint32_t ntok, const uint32_t* texcl,
                                                         uint32_t* par) {
     __shared__ uint32_t sh[2][BLOCK * JS_PD];
     __shared__ uint32_t st[BLOCK * (JS_PD + 1)];
+    __shared__ uint32_t tm[JS_TPAD];              // token metas in, parents out
+    const uint32_t t0 = blockIdx.x * JS_TILE;
+    for (int q = 0; q < JS_PER; ++q) {            // coalesced staging of the tile
+        const uint32_t l = q * BLOCK + threadIdx.x;
+        tm[tpad(l)] = t0 + l < ntok ? toks[t0 + l].y : 0u;
+    }
     uint32_t* row = st + threadIdx.x * (JS_PD + 1);
 #pragma unroll
     for (int d = 0; d < JS_PD; ++d) row[d] = 0;
-    const uint32_t base = blockIdx.x * JS_TILE + threadIdx.x * JS_PER;
+    __syncthreads();
+    const uint32_t base = t0 + threadIdx.x * JS_PER;
+    uint32_t* mine = tm + threadIdx.x * (JS_PER + 1);
     for (int k = 0; k < JS_PER; ++k) {
         const uint32_t i = base + k;
         if (i >= ntok) break;
-        const uint32_t meta = toks[i].y;
+        const uint32_t meta = mine[k];
         const uint32_t d = meta & TK_DEPTH_MASK;
         if (tk_open(meta) && d < JS_PD) row[d] = i + 1;
     }
@@ -354,13 +368,18 @@ __global__ void __launch_bounds__(BLOCK) k_js_par_apply(const uint2* toks, uint3
     for (int k = 0; k < JS_PER; ++k) {
         const uint32_t i = base + k;
         if (i >= ntok) break;
-        const uint32_t meta = toks[i].y;
+        const uint32_t meta = mine[k];
         const uint32_t d = meta & TK_DEPTH_MASK;
         uint32_t p = JS_NONE;
         if (d >= 1 && d <= JS_PD) p = row[d - 1] - 1;          // 0 - 1 = JS_NONE (malformed)
         else if (d > JS_PD) p = JS_DEEP;
-        par[i] = p;
+        mine[k] = p;
         if (tk_open(meta) && d < JS_PD) row[d] = i + 1;
+    }
+    __syncthreads();
+    for (int q = 0; q < JS_PER; ++q) {            // coalesced write-out
+        const uint32_t l = q * BLOCK + threadIdx.x;
+        if (t0 + l < ntok) par[t0 + l] = tm[tpad(l)];
     }
 }
 
@@ -642,13 +661,13 @@ __global__ void __launch_bounds__(BLOCK) k_js_elems_count(JsDoc j, const uint2* 
     if (threadIdx.x < 3) sh[threadIdx.x] = 0;
     __syncthreads();
     uint32_t c[3] = {0, 0, 0};
-    const uint32_t base = blockIdx.x * JS_TILE + threadIdx.x * JS_PER;
-    if (base == 0 && ntok) {                                      // the document must be an object or null
+    const uint32_t t0 = blockIdx.x * JS_TILE;
+    if (t0 + threadIdx.x == 0 && ntok) {                          // the document must be an object or null
         const uint2 t = toks[0];
         if (!(tkind(t) == TK_OBJ || (tkind(t) == TK_SCALAR && j.doc[t.x] == 'n'))) js_fail(derr, t.x, KDTN_JSON_TYPE);
     }
-    for (int k = 0; k < JS_PER; ++k) {
-        const uint32_t i = base + k;
+    for (int q = 0; q < JS_PER; ++q) {                            // counts: coalesced order
+        const uint32_t i = t0 + q * BLOCK + threadIdx.x;
         if (i >= ntok) break;
         const uint32_t cls = elem_class(toks, par, role, i);
         if (!cls) continue;
@@ -668,12 +687,18 @@ __global__ void __launch_bounds__(BLOCK) k_js_elems_write(const uint2* toks, uin
                                                           const uint8_t* role, const uint64_t* coff3, uint32_t ntiles,
                                                           uint32_t* ord, JsTopoOut to) {
     __shared__ uint64_t sh[BLOCK / 64];
+    __shared__ uint8_t tc[JS_TPAD];                // element class per tile token
+    const uint32_t t0 = blockIdx.x * JS_TILE;
+    for (int q = 0; q < JS_PER; ++q) {            // classes: coalesced order
+        const uint32_t l = q * BLOCK + threadIdx.x;
+        tc[tpad(l)] = t0 + l < ntok ? (uint8_t)elem_class(toks, par, role, t0 + l) : (uint8_t)0;
+    }
+    __syncthreads();
+    const uint8_t* mine = tc + threadIdx.x * (JS_PER + 1);
     uint32_t c[3] = {0, 0, 0};
-    const uint32_t base = blockIdx.x * JS_TILE + threadIdx.x * JS_PER;
+    const uint32_t base = t0 + threadIdx.x * JS_PER;
     for (int k = 0; k < JS_PER; ++k) {
-        const uint32_t i = base + k;
-        if (i >= ntok) break;
-        const uint32_t cls = elem_class(toks, par, role, i);
+        const uint32_t cls = mine[k];
         if (cls) c[cls - 1]++;
     }
     uint32_t run[3];
@@ -685,7 +710,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_elems_write(const uint2* toks, uin
     for (int k = 0; k < JS_PER; ++k) {
         const uint32_t i = base + k;
         if (i >= ntok) break;
-        const uint32_t cls = elem_class(toks, par, role, i);
+        const uint32_t cls = mine[k];
         if (!cls) continue;
         const uint32_t o = run[cls - 1]++;
         ord[i] = o;
