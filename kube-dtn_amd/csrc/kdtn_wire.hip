@@ -216,6 +216,27 @@ struct Sink {
     }
     // string field: tag, length, bytes read from the arena as aligned dwords (arenas carry
     // 64 B of slack, so reading past a string's end is safe)
+    // string field whose arena range [b, b + len) is already known: the first 32 bytes come
+    // from nine aligned dword loads issued together (one round trip), the rest dword by dword
+    KD_INLINE void strb(uint32_t field, const uint8_t* arena, uint32_t b, uint32_t len) {
+        if (!len) return;
+        byte((uint8_t)(field << 3 | 2u));
+        varint(len);
+        const uint32_t* a32 = reinterpret_cast<const uint32_t*>(arena) + (b >> 2);
+        const uint32_t sh = b & 3u;
+        uint32_t w[9];
+#pragma unroll
+        for (int q = 0; q < 9; ++q) w[q] = a32[q];
+        const uint32_t head = len < 32u ? len : 32u;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const uint32_t d = __builtin_amdgcn_alignbyte(w[q + 1], w[q], sh);   // string bytes 4q..4q+3
+#pragma unroll
+            for (uint32_t c = 0; c < 4; ++c)
+                if (4u * q + c < head) *p++ = (uint8_t)(d >> (8u * c));
+        }
+        for (uint32_t k = 32; k < len; ++k) *p++ = arena[b + k];
+    }
     KD_INLINE void str(uint32_t field, const uint8_t* arena, const uint32_t* offs, uint32_t id) {
         const uint32_t b = offs[id], len = offs[id + 1] - b;
         if (!len) return;
@@ -251,13 +272,31 @@ KD_INLINE void write_entry(Sink& o, const WireIn& w, const DevLinks& L, uint32_t
     link_sizes(w, L, j, &psz, &lsz);
     o.byte(2u << 3 | 2u);                                 // LinksBatchQuery.links
     o.varint(lsz);
+    // every string's arena range first (independent gathers, one round trip)
+    uint32_t kb[KDTN_NKEY], kl[KDTN_NKEY], pb[KDTN_NPROP], pl[KDTN_NPROP];
+#pragma unroll
+    for (int k = 0; k < KDTN_NKEY; ++k) {
+        const uint32_t id = L.key(k, j);
+        kb[k] = w.kd_offs[id];
+        kl[k] = w.kd_offs[id + 1];
+    }
+#pragma unroll
+    for (int k = 0; k < KDTN_NPROP; ++k) {
+        const uint32_t id = L.prop(k, j);
+        pb[k] = id ? w.pd_offs[id] : 0u;              // id 0 = "" (empty: no field)
+        pl[k] = id ? w.pd_offs[id + 1] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < KDTN_NKEY; ++k) kl[k] -= kb[k];
+#pragma unroll
+    for (int k = 0; k < KDTN_NPROP; ++k) pl[k] -= pb[k];
     // pb.Link fields in number order: peer_pod 1, local_intf 2, peer_intf 3, local_ip 4,
     // peer_ip 5, uid 6, properties 7, local_mac 8, peer_mac 9
-    o.str(1, w.kd_bytes, w.kd_offs, L.key(KDTN_K_PEER_POD, j));
-    o.str(2, w.kd_bytes, w.kd_offs, L.key(KDTN_K_LOCAL_INTF, j));
-    o.str(3, w.kd_bytes, w.kd_offs, L.key(KDTN_K_PEER_INTF, j));
-    o.str(4, w.kd_bytes, w.kd_offs, L.key(KDTN_K_LOCAL_IP, j));
-    o.str(5, w.kd_bytes, w.kd_offs, L.key(KDTN_K_PEER_IP, j));
+    o.strb(1, w.kd_bytes, kb[KDTN_K_PEER_POD], kl[KDTN_K_PEER_POD]);
+    o.strb(2, w.kd_bytes, kb[KDTN_K_LOCAL_INTF], kl[KDTN_K_LOCAL_INTF]);
+    o.strb(3, w.kd_bytes, kb[KDTN_K_PEER_INTF], kl[KDTN_K_PEER_INTF]);
+    o.strb(4, w.kd_bytes, kb[KDTN_K_LOCAL_IP], kl[KDTN_K_LOCAL_IP]);
+    o.strb(5, w.kd_bytes, kb[KDTN_K_PEER_IP], kl[KDTN_K_PEER_IP]);
     const int64_t uid = L.uid(j);
     if (uid) {
         o.byte(6u << 3);
@@ -274,10 +313,10 @@ KD_INLINE void write_entry(Sink& o, const WireIn& w, const DevLinks& L, uint32_t
                 o.varint(gap);
             }
         }
-        o.str((uint32_t)(k < KDTN_P_DUPLICATE ? k + 1 : k + 2), w.pd_bytes, w.pd_offs, L.prop(k, j));
+        o.strb((uint32_t)(k < KDTN_P_DUPLICATE ? k + 1 : k + 2), w.pd_bytes, pb[k], pl[k]);
     }
-    o.str(8, w.kd_bytes, w.kd_offs, L.key(KDTN_K_LOCAL_MAC, j));
-    o.str(9, w.kd_bytes, w.kd_offs, L.key(KDTN_K_PEER_MAC, j));
+    o.strb(8, w.kd_bytes, kb[KDTN_K_LOCAL_MAC], kl[KDTN_K_LOCAL_MAC]);
+    o.strb(9, w.kd_bytes, kb[KDTN_K_PEER_MAC], kl[KDTN_K_PEER_MAC]);
 }
 
 // One thread per entry of the three lists (global entry index g). Consecutive entries
