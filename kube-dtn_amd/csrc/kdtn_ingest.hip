@@ -472,6 +472,69 @@ KD_INLINE bool valid_scalar(const JsDoc& j, uint32_t pos) {
     return term(i);
 }
 
+// valid_scalar from one window of registers (load_window, below): the literal / number
+// grammar as a byte DFA over the 32 bytes at pos. 1 = valid, 0 = invalid, -1 = the window
+// holds no decision (a number longer than the window, or the window reaches past the
+// document end) and the byte loop above decides.
+KD_INLINE void load_window(const uint8_t* doc, uint32_t a, uint32_t u[8]);
+KD_INLINE int valid_scalar_window(const JsDoc& j, uint32_t pos) {
+    if (pos + 32 > j.n) return -1;
+    uint32_t u[8];
+    load_window(j.doc, pos, u);
+    auto term = [](uint32_t c) { return c <= 0x20 || c == '"' || is_struct_byte(c); };
+    const uint32_t c0 = u[0] & 0xFFu, b4 = u[1] & 0xFFu, b5 = (u[1] >> 8) & 0xFFu;
+    if (c0 == 't') return u[0] == 0x65757274u && term(b4);            // "true"
+    if (c0 == 'f') return u[0] == 0x736c6166u && b4 == 'e' && term(b5); // "fals" "e"
+    if (c0 == 'n') return u[0] == 0x6c6c756eu && term(b4);            // "null"
+    // 0 start, 1 after '-', 2 leading 0, 3 integer digits, 4 after '.', 5 fraction digits,
+    // 6 after e/E, 7 after the exponent sign, 8 exponent digits
+    uint32_t st = 0;
+    int res = -1;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+        const uint32_t c = (u[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+        if (res >= 0) continue;
+        const bool dig = c - '0' < 10u, ee = (c | 32u) == 'e';
+        switch (st) {
+        case 0: st = c == '-' ? 1u : c == '0' ? 2u : dig ? 3u : 9u; break;
+        case 1: st = c == '0' ? 2u : dig ? 3u : 9u; break;
+        case 2: st = c == '.' ? 4u : ee ? 6u : 10u; break;
+        case 3: st = dig ? 3u : c == '.' ? 4u : ee ? 6u : 10u; break;
+        case 4: st = dig ? 5u : 9u; break;
+        case 5: st = dig ? 5u : ee ? 6u : 10u; break;
+        case 6: st = (c == '+' || c == '-') ? 7u : dig ? 8u : 9u; break;
+        case 7: st = dig ? 8u : 9u; break;
+        default: st = dig ? 8u : 10u; break;                            // 8
+        }
+        if (st == 9u) res = 0;                                          // grammar violated
+        else if (st == 10u) res = term(c) ? 1 : 0;                      // the number ended at c
+    }
+    return res;
+}
+
+// The string token at pos: its closing quote e and whether a backslash lies in (pos, e).
+// The quote and backslash words of the opening block and the next one are loaded together,
+// so a string ending within them costs one memory round trip (masks have nb + 1 words).
+KD_INLINE uint32_t str_end_bs(const JsDoc& j, uint32_t pos, bool* bs) {
+    const uint32_t a = pos + 1, b = a >> 6, sh = a & 63u;
+    const uint64_t q0 = j.qmask[b], q1 = j.qmask[b + 1], s0 = j.bsmask[b], s1 = j.bsmask[b + 1];
+    const uint64_t qa = q0 & (~0ull << sh);
+    uint32_t e;
+    if (qa) e = b * 64 + (__ffsll((long long)qa) - 1);
+    else if (q1) e = (b + 1) * 64 + (__ffsll((long long)q1) - 1);
+    else {
+        e = str_end(j, pos);
+        *bs = any_in(j.bsmask, a, e);
+        return e;
+    }
+    // backslashes in [a, e): e - a <= 127 here, within words b and b + 1
+    const uint32_t eb = e - b * 64;                                     // 0..127
+    const uint64_t m0 = (~0ull << sh) & (eb >= 64 ? ~0ull : ((1ull << eb) - 1));
+    const uint64_t m1 = eb > 64 ? ((eb - 64 >= 64) ? ~0ull : ((1ull << (eb - 64)) - 1)) : 0ull;
+    *bs = ((s0 & m0) | (s1 & m1)) != 0;
+    return e;
+}
+
 __global__ void __launch_bounds__(BLOCK) k_js_validate(JsDoc j, const uint2* toks, uint32_t ntok, const uint32_t* par,
                                                        unsigned long long* err) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
@@ -505,10 +568,14 @@ __global__ void __launch_bounds__(BLOCK) k_js_validate(JsDoc j, const uint2* tok
     if (ok && i == ntok - 1) {                                    // the document ends here
         ok = (kind == TK_STR || kind == TK_SCALAR) ? d == 0 : ((kind == TK_OBJ_END || kind == TK_ARR_END) && d == 1);
     }
-    if (ok && kind == TK_SCALAR) ok = valid_scalar(j, pos);
+    if (ok && kind == TK_SCALAR) {
+        const int w = valid_scalar_window(j, pos);
+        ok = w >= 0 ? w != 0 : valid_scalar(j, pos);
+    }
     if (ok && kind == TK_STR) {
-        const uint32_t e = str_end(j, pos);
-        if (any_in(j.bsmask, pos + 1, e)) {                       // escapes: \" \\ \/ \b \f \n \r \t \uXXXX
+        bool bs;
+        const uint32_t e = str_end_bs(j, pos, &bs);
+        if (bs) {                                                 // escapes: \" \\ \/ \b \f \n \r \t \uXXXX
             for (uint32_t k = pos + 1; k < e && ok; ++k) {
                 if (j.doc[k] != '\\') continue;
                 const uint32_t c = j.doc[k + 1];

@@ -262,3 +262,17 @@ def test_samples_ingest_then_reconcile(tr):
                             ("upd", inp.desired, out.upd_off)):
             idx = getattr(out, lst + "_idx")[off[ti]:off[ti + 1]]
             assert [int(L.uid[i]) for i in idx] == exp[lst], (name, lst)
+
+
+def test_window_scalars_oracle_pinned():
+    """the oracle's checkValid on the GPU window cases agrees with Python's json"""
+    import test_ingest_gpu as g
+    for s in g.WIN_SCALARS:
+        doc = b'{"p":[' + s + b'],"q":"' + b"z" * 40 + b'"}'
+        e1, _, _ = oracle.json_ingest(doc)
+        try:
+            json.loads(doc, parse_constant=lambda c: (_ for _ in ()).throw(ValueError(c)))
+            std_ok = True
+        except ValueError:
+            std_ok = False
+        assert (e1 != jr.SYNTAX) == std_ok, (s, e1)

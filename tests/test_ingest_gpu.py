@@ -166,3 +166,41 @@ def test_config2_full_size_properties(engine):
     # ids are first-occurrence ranks: every id appears first after all smaller ids
     small = synth.make(2, pods_per_shard=20_000)
     check_doc(engine, synth.topology_list_json(small), "config 2 slice")
+
+
+# Scalars and strings far enough from the document end that k_js_validate decides them from
+# one 32-byte register window (valid_scalar_window) and one pair of quote/backslash mask
+# words (str_end_bs); BAD_SYNTAX's short documents only reach the byte loops.
+WIN_SCALARS = [b"0", b"-0", b"7", b"-12", b"0.5", b"-0.25e+3", b"1E9", b"1e-7", b"12345678901234567890",
+               b"1.25E+10", b"true", b"false", b"null", b"01", b"-", b"1.", b"1e", b"1e+", b".5", b"+1",
+               b"-a", b"1.e3", b"1x", b"0x1", b"truex", b"fals", b"nul", b"nulll", b"tru", b"falsee",
+               b"1" * 31, b"1" * 32, b"1" * 40, b"1." + b"5" * 35, b"1e" + b"9" * 33, b"-" + b"0" * 2,
+               b"00", b"1.5.2", b"1e5e5", b"1-2", b"NaN", b"Infinity"]
+
+
+@pytest.mark.parametrize("sep", [b"", b" ", b"\t\n"])
+def test_window_scalars(engine, sep):
+    for s in WIN_SCALARS:
+        for pad in (0, 1, 3, 29, 61):
+            doc = (b'{"' + b"p" * pad + b'":[' + s + sep + b"]," + b'"q":"' + b"z" * 40 + b'",'
+                   b'"items":[{"metadata":{"name":"a"},"spec":{"links":[{"uid":' + s + sep + b"}]}}]}")
+            check_doc(engine, doc, f"scalar {s!r} pad {pad}")
+
+
+def test_window_strings(engine):
+    rng = random.Random(7)
+    for L in list(range(0, 70)) + [126, 127, 128, 129, 191, 300]:
+        for pad in (0, 1, 62, 63):
+            body = bytes(rng.choice(b"abcXYZ019 -") for _ in range(L))
+            variants = [body]
+            if L >= 2:
+                k = rng.randrange(L - 1)
+                variants.append(body[:k] + b"\\n" + body[k + 1:])
+                variants.append(body[:k] + b"\\q" + body[k + 1:])           # invalid escape
+                variants.append(body[:-1] + b"\\\\")                          # escaped backslash at the end
+                variants.append(body[:k] + b"\\u00e9" + body[k:])
+                variants.append(body[:k] + b'\\"' + body[k:])
+            for v in variants:
+                doc = (b'{"' + b"p" * pad + b'":"' + v + b'","items":[{"metadata":{"name":"' + v + b'",'
+                       b'"namespace":"n"}}], "t":"' + b"w" * 40 + b'"}')
+                check_doc(engine, doc, f"string len {L} pad {pad} {v[:20]!r}")
