@@ -537,26 +537,50 @@ KD_INLINE uint32_t str_end_bs(const JsDoc& j, uint32_t pos, bool* bs) {
 
 __global__ void __launch_bounds__(BLOCK) k_js_validate(JsDoc j, const uint2* toks, uint32_t ntok, const uint32_t* par,
                                                        unsigned long long* err) {
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    // the block's tokens (with the two before) and parents (with the one before) staged in
+    // LDS with coalesced loads: a token's neighbours, and parents inside the block, come from
+    // LDS instead of further global loads
+    __shared__ uint2 st[BLOCK + 2];
+    __shared__ uint32_t sp[BLOCK + 1];
+    const uint32_t b0 = blockIdx.x * BLOCK, i = b0 + threadIdx.x;
+    if (i < ntok) {
+        st[threadIdx.x + 2] = toks[i];
+        sp[threadIdx.x + 1] = par[i];
+    }
+    if (threadIdx.x < 2) {
+        const uint32_t k = b0 + threadIdx.x;                      // token b0 - 2 + threadIdx.x
+        st[threadIdx.x] = k >= 2 ? toks[k - 2] : make_uint2(0u, 0u);
+        if (threadIdx.x == 1) sp[0] = b0 >= 1 ? par[b0 - 1] : JS_DEEP;
+    }
+    __syncthreads();
     if (i >= ntok) return;
-    const uint2 t = toks[i];
+    auto kind_of = [&](uint32_t q) {                              // tkind(toks[q]), q < JS_DEEP
+        return q + 2 >= b0 && q < b0 + BLOCK ? tkind(st[q + 2 - b0]) : tkind(toks[q]);
+    };
+    const uint2 t = st[threadIdx.x + 2];
     const uint32_t kind = tkind(t), d = tdepth(t), pos = t.x;
-    const uint32_t p = par[i];
-    const uint32_t ck = d == 0 ? 0xFFu : (p < JS_DEEP ? tkind(toks[p]) : 0xFEu);   // container kind
+    const uint32_t p = sp[threadIdx.x + 1];
+    const uint32_t pkind = p < JS_DEEP ? kind_of(p) : 0xFEu;
+    const uint32_t ck = d == 0 ? 0xFFu : pkind;                   // container kind
     bool ok;
     if (i == 0) {
         ok = value_start(kind) && d == 0;
     } else {
         if (d == 0) ok = false;                                   // a second top-level value
         else {
-            const uint32_t pk = tkind(toks[i - 1]);
+            const uint32_t pk = tkind(st[threadIdx.x + 1]);
             switch (pk) {
             case TK_OBJ: ok = kind == TK_STR || kind == TK_OBJ_END; break;
             case TK_ARR: ok = value_start(kind) || kind == TK_ARR_END; break;
             case TK_COLON: ok = value_start(kind); break;
             case TK_COMMA: ok = ck == TK_OBJ ? kind == TK_STR : (ck == TK_ARR && value_start(kind)); break;
-            case TK_STR:
-                if (tk_key(toks, par, i - 1)) { ok = kind == TK_COLON; break; }
+            case TK_STR: {
+                // tk_key(toks, par, i - 1) from the staged neighbours
+                const uint32_t ppk = i >= 2 ? tkind(st[threadIdx.x]) : 0xFFu, pp = sp[threadIdx.x];
+                const bool key = i >= 2 && (ppk == TK_OBJ || ppk == TK_COMMA) && pp < JS_DEEP &&
+                                 (pp == p ? pkind : kind_of(pp)) == TK_OBJ;
+                if (key) { ok = kind == TK_COLON; break; }
+            }
                 [[fallthrough]];
             default:                                              // after a value
                 ok = kind == TK_COMMA || kind == TK_OBJ_END || kind == TK_ARR_END;
