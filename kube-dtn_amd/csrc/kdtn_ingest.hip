@@ -512,12 +512,15 @@ KD_INLINE int valid_scalar_window(const JsDoc& j, uint32_t pos) {
     return res;
 }
 
-// The string token at pos: its closing quote e and whether a backslash lies in (pos, e).
-// The quote and backslash words of the opening block and the next one are loaded together,
-// so a string ending within them costs one memory round trip (masks have nb + 1 words).
-KD_INLINE uint32_t str_end_bs(const JsDoc& j, uint32_t pos, bool* bs) {
+// The string token at pos: its closing quote e and whether a backslash (and, when hb is
+// given, a byte >= 0x80) lies in (pos, e). The mask words of the opening block and the next
+// one are loaded together, so a string ending within them costs one memory round trip
+// (masks have nb + 1 words).
+KD_INLINE uint32_t str_end_bs(const JsDoc& j, uint32_t pos, bool* bs, bool* hb = nullptr) {
     const uint32_t a = pos + 1, b = a >> 6, sh = a & 63u;
     const uint64_t q0 = j.qmask[b], q1 = j.qmask[b + 1], s0 = j.bsmask[b], s1 = j.bsmask[b + 1];
+    uint64_t h0 = 0, h1 = 0;
+    if (hb) { h0 = j.hbmask[b]; h1 = j.hbmask[b + 1]; }
     const uint64_t qa = q0 & (~0ull << sh);
     uint32_t e;
     if (qa) e = b * 64 + (__ffsll((long long)qa) - 1);
@@ -525,13 +528,15 @@ KD_INLINE uint32_t str_end_bs(const JsDoc& j, uint32_t pos, bool* bs) {
     else {
         e = str_end(j, pos);
         *bs = any_in(j.bsmask, a, e);
+        if (hb) *hb = any_in(j.hbmask, a, e);
         return e;
     }
-    // backslashes in [a, e): e - a <= 127 here, within words b and b + 1
-    const uint32_t eb = e - b * 64;                                     // 0..127
+    // [a, e) lies within words b and b + 1 here (e - b * 64 <= 127)
+    const uint32_t eb = e - b * 64;
     const uint64_t m0 = (~0ull << sh) & (eb >= 64 ? ~0ull : ((1ull << eb) - 1));
-    const uint64_t m1 = eb > 64 ? ((eb - 64 >= 64) ? ~0ull : ((1ull << (eb - 64)) - 1)) : 0ull;
+    const uint64_t m1 = eb > 64 ? ((1ull << (eb - 64)) - 1) : 0ull;
     *bs = ((s0 & m0) | (s1 & m1)) != 0;
+    if (hb) *hb = ((h0 & m0) | (h1 & m1)) != 0;
     return e;
 }
 
@@ -623,13 +628,15 @@ __global__ void __launch_bounds__(BLOCK) k_js_validate(JsDoc j, const uint2* tok
 KD_INLINE int match_key(const JsDoc& j, uint32_t pos, const char (*names)[16], int n) {
     uint64_t lo = 0, hi = 0;
     uint32_t len = 0;
-    const uint32_t e = str_end(j, pos);
+    // the three aligned words a plain name needs are loaded with the mask words (one round trip)
+    const uint64_t* w = reinterpret_cast<const uint64_t*>(j.doc + ((pos + 1) & ~7u));
+    const uint64_t w0 = w[0], w1 = w[1], w2 = w[2];
+    bool bs;
+    const uint32_t e = str_end_bs(j, pos, &bs);
     if (e - pos - 1 > 6 * 16) return -1;
-    if (e - pos - 1 <= 15 && !any_in(j.bsmask, pos + 1, e)) {     // plain name: three aligned words
+    if (e - pos - 1 <= 15 && !bs) {                               // plain name: three aligned words
         const uint32_t a = pos + 1, L = e - a;
-        const uint64_t* w = reinterpret_cast<const uint64_t*>(j.doc + (a & ~7u));
         const uint32_t sh = (a & 7u) * 8;
-        const uint64_t w0 = w[0], w1 = w[1], w2 = w[2];
         lo = sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;
         hi = sh ? (w1 >> sh) | (w2 << (64 - sh)) : w1;
         if (L < 8) { lo &= (1ull << (8 * L)) - 1; hi = 0; }
@@ -1015,17 +1022,18 @@ KD_INLINE uint32_t intern(const JsIntern& in, const JsDict& dt, const uint8_t* p
 
 // string value at token i → 1 + table slot (0 = empty string); JS_NONE on overflow
 KD_INLINE uint32_t string_slot(const JsDoc& j, const JsIntern& in, const JsDict& dt, uint32_t i, uint32_t pos) {
-    const uint32_t e = str_end(j, pos);
     const uint32_t a = pos + 1;
+    uint32_t pw[8];
+    load_window(j.doc, a, pw);                         // issued with the mask loads (one round trip)
+    bool bs, hb;
+    const uint32_t e = str_end_bs(j, pos, &bs, &hb);
     if (e == a) return 0;
-    if (!any_in(j.bsmask, a, e) && !any_in(j.hbmask, a, e)) {     // plain ASCII: the bytes themselves
+    if (!bs && !hb) {                                  // plain ASCII: the bytes themselves
         const uint32_t len = e - a;
         if (len > 0xFFFFFFu) { atomicOr(in.status, JS_ST_LONG); return JS_NONE; }
         uint64_t h;
-        uint32_t pw[8];
         const bool win = len <= WIN;
         if (win) {
-            load_window(j.doc, a, pw);
             h = word_hash(pw, len);
         } else {
             h = 1469598103934665603ull;
