@@ -623,9 +623,10 @@ __global__ void __launch_bounds__(BLOCK) k_js_validate(JsDoc j, const uint2* tok
 }
 
 // ---------------------------------------------------------------- key matching
-// Decodes the member name at string token pos (escapes included) and returns the index of
-// the equal name in names[0..n), or -1. Names are ASCII and at most 15 bytes.
-KD_INLINE int match_key(const JsDoc& j, uint32_t pos, const char (*names)[16], int n) {
+// Decodes the member name at string token pos (escapes included) into two little-endian
+// words; ok = false when it cannot equal a schema name (names are ASCII, at most 15 bytes).
+struct KeyName { uint64_t lo, hi; bool ok; };
+KD_INLINE KeyName key_name(const JsDoc& j, uint32_t pos) {
     uint64_t lo = 0, hi = 0;
     uint32_t len = 0;
     // the three aligned words a plain name needs are loaded with the mask words (one round trip)
@@ -633,7 +634,7 @@ KD_INLINE int match_key(const JsDoc& j, uint32_t pos, const char (*names)[16], i
     const uint64_t w0 = w[0], w1 = w[1], w2 = w[2];
     bool bs;
     const uint32_t e = str_end_bs(j, pos, &bs);
-    if (e - pos - 1 > 6 * 16) return -1;
+    if (e - pos - 1 > 6 * 16) return {0, 0, false};
     if (e - pos - 1 <= 15 && !bs) {                               // plain name: three aligned words
         const uint32_t a = pos + 1, L = e - a;
         const uint32_t sh = (a & 7u) * 8;
@@ -641,12 +642,7 @@ KD_INLINE int match_key(const JsDoc& j, uint32_t pos, const char (*names)[16], i
         hi = sh ? (w1 >> sh) | (w2 << (64 - sh)) : w1;
         if (L < 8) { lo &= (1ull << (8 * L)) - 1; hi = 0; }
         else hi &= L == 8 ? 0ull : (1ull << (8 * (L - 8))) - 1;
-        int hit = -1;                                              // names are distinct
-        for (int f = 0; f < n; ++f) {
-            const uint64_t* nm = reinterpret_cast<const uint64_t*>(names[f]);
-            hit = (nm[0] == lo && nm[1] == hi) ? f : hit;
-        }
-        return hit;
+        return {lo, hi, true};
     }
     for (uint32_t k = pos + 1; k < e; ++k) {
         uint32_t c = j.doc[k];
@@ -658,7 +654,7 @@ KD_INLINE int match_key(const JsDoc& j, uint32_t pos, const char (*names)[16], i
                     const uint32_t h = j.doc[k + q];
                     r = r * 16 + (h <= '9' ? h - '0' : (h | 32) - 'a' + 10);
                 }
-                if (r >= 0x80) return -1;
+                if (r >= 0x80) return {0, 0, false};
                 c = r;
                 k += 5;
             } else {
@@ -666,18 +662,26 @@ KD_INLINE int match_key(const JsDoc& j, uint32_t pos, const char (*names)[16], i
                 k += 1;
             }
         } else if (c >= 0x80) {
-            return -1;
+            return {0, 0, false};
         }
-        if (len >= 15 || c == 0) return -1;
+        if (len >= 15 || c == 0) return {0, 0, false};
         if (len < 8) lo |= (uint64_t)c << (8 * len);
         else hi |= (uint64_t)c << (8 * (len - 8));
         ++len;
     }
+    return {lo, hi, true};
+}
+// index of the decoded name in names[0..n) (distinct), or -1
+KD_INLINE int key_match(const KeyName& k, const char (*names)[16], int n) {
+    int hit = -1;
     for (int f = 0; f < n; ++f) {
-        const uint64_t* w = reinterpret_cast<const uint64_t*>(names[f]);
-        if (w[0] == lo && w[1] == hi) return f;
+        const uint64_t* nm = reinterpret_cast<const uint64_t*>(names[f]);
+        hit = (k.ok && nm[0] == k.lo && nm[1] == k.hi) ? f : hit;
     }
-    return -1;
+    return hit;
+}
+KD_INLINE int match_key(const JsDoc& j, uint32_t pos, const char (*names)[16], int n) {
+    return key_match(key_name(j, pos), names, n);
 }
 
 __constant__ __attribute__((aligned(16))) char kItems[1][16] = {"items"};
@@ -1155,14 +1159,16 @@ __global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, const uint2* toks,
     const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
     if (k >= nval) return;
     const uint32_t i = vlist[k];                       // object member values, document order
-    const uint32_t dv = tdepth(toks[i]);             // members of root 1, item 3, meta/spec/status 4,
+    const uint2 t = toks[i];
+    const uint32_t kpos = toks[i - 2].x;
+    const uint32_t dv = tdepth(t);                     // members of root 1, item 3, meta/spec/status 4,
     if (dv != 1 && dv != 3 && dv != 4 && dv != 6 && dv != 7) return;   // link 6, properties 7
     const uint32_t o = par[i];
     if (o >= JS_DEEP) return;
     const uint32_t r = role[o];
+    const KeyName kn = key_name(j, kpos);              // decoded while role[o] is in flight
     if (r == R_NONE || r == R_ITEMS || r == R_SPEC_LINKS || r == R_STATUS_LINKS) return;
-    const uint2 t = toks[i];
-    const uint32_t kind = tkind(t), kpos = toks[i - 2].x;
+    const uint32_t kind = tkind(t);
     const bool null = kind == TK_SCALAR && j.doc[t.x] == 'n';
     int f, bit;
     uint32_t own;                                      // owner slot of (object, field): duplicate check
@@ -1170,33 +1176,33 @@ __global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, const uint2* toks,
     const JsStore* st = nullptr;
     switch (r) {
     case R_ROOT:
-        f = match_key(j, kpos, kItems, 1);
+        f = key_match(kn, kItems, 1);
         bit = f; own = 0;
         break;
     case R_ITEM:
-        f = match_key(j, kpos, kItem, 3);
+        f = key_match(kn, kItem, 3);
         topo = ord[o]; bit = f; own = 1 + topo * 9;
         break;
     case R_META:
-        f = match_key(j, kpos, kMeta, 2);
+        f = key_match(kn, kMeta, 2);
         topo = ord[par[o]]; bit = 3 + f; own = 1 + topo * 9;
         break;
     case R_SPEC:
-        f = match_key(j, kpos, kLinks, 1);
+        f = key_match(kn, kLinks, 1);
         topo = ord[par[o]]; bit = 5 + f; own = 1 + topo * 9;
         break;
     case R_STATUS:
-        f = match_key(j, kpos, kStatus, 3);
+        f = key_match(kn, kStatus, 3);
         topo = ord[par[o]]; bit = 6 + f; own = 1 + topo * 9;
         break;
     case R_LINK_S:
     case R_LINK_R:
-        f = match_key(j, kpos, kLink, KDTN_NKEY + 2);
+        f = key_match(kn, kLink, KDTN_NKEY + 2);
         st = r == R_LINK_S ? &des : &real;
         rec = ord[o]; bit = f; own = (r == R_LINK_S ? in.own_des : in.own_real) + rec * 22;
         break;
     default: {                                                    // R_PROPS_S / R_PROPS_R
-        f = match_key(j, kpos, kProps, KDTN_NPROP + 1);
+        f = key_match(kn, kProps, KDTN_NPROP + 1);
         st = r == R_PROPS_S ? &des : &real;
         rec = ord[par[o]]; bit = 9 + f; own = (r == R_PROPS_S ? in.own_des : in.own_real) + rec * 22;
         break;
