@@ -179,45 +179,91 @@ KD_INLINE uint32_t kind_of(uint32_t c) {
     }
 }
 
+// position of the r-th (0-based) set bit of m (r < popcount(m))
+KD_INLINE uint32_t select_bit(uint64_t m, uint32_t r) {
+    uint32_t pos = 0;
+#pragma unroll
+    for (int w = 32; w >= 1; w >>= 1) {
+        const uint32_t c = __popcll(m & ((1ull << w) - 1));
+        if (r >= c) { r -= c; m >>= w; pos += w; }
+    }
+    return pos;
+}
+
+// Token writer. Each lane owns one 64-byte block (its bytes go to LDS, its masks and offsets
+// to per-lane LDS slots); the wave's tokens are contiguous in toks[], so the wave writes them
+// round by round, lane l taking the wave's token r = round * 64 + l (owner block by binary
+// search over the wave's token prefix, bit by select): coalesced 8-byte stores instead of
+// every lane walking its own block's tokens into its own region.
 __global__ void __launch_bounds__(BLOCK) k_js_tokens(JsDoc j, JsMasks m, const uint64_t* toff, const uint64_t* doff,
                                                      const uint64_t* ooff, const uint64_t* coff, uint2* toks,
                                                      uint32_t* olist, uint32_t* vlist, unsigned long long* err) {
-    // each lane's 64-byte block goes to LDS first, so the per-token kind lookups below are LDS
-    // reads instead of one dependent global byte load per token
     __shared__ uint4 blk[BLOCK * 4];
+    __shared__ uint64_t stok[BLOCK], sop[BLOCK], scl[BLOCK], scol[BLOCK];
+    __shared__ int64_t sd0[BLOCK];
+    __shared__ uint32_t sex[BLOCK], soo[BLOCK], sco[BLOCK];
+    const uint32_t lane = threadIdx.x & 63u, w0 = threadIdx.x & ~63u;
     const uint32_t b = blockIdx.x * BLOCK + threadIdx.x;
+    uint64_t tok = 0, ti = 0;
     if (b < j.nb) {
         const uint4* p = reinterpret_cast<const uint4*>(j.doc + (size_t)b * 64);
+        uint4 v[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) blk[threadIdx.x * 4 + q] = p[q];
+        for (int q = 0; q < 4; ++q) v[q] = p[q];
+        tok = m.tok[b];
+        ti = toff[b];
+        sop[threadIdx.x] = m.open[b];
+        scl[threadIdx.x] = m.close[b];
+        sd0[threadIdx.x] = (int64_t)doff[b] - 64ll * b;
+        soo[threadIdx.x] = (uint32_t)ooff[b];
+        sco[threadIdx.x] = (uint32_t)coff[b];
+        uint64_t col = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            blk[threadIdx.x * 4 + q] = v[q];
+            const uint32_t wd[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+            for (int h = 0; h < 4; ++h) col |= (uint64_t)mm4(eqb(wd[h], ':')) << (4 * (q * 4 + h));
+        }
+        scol[threadIdx.x] = col & tok;                 // structural colons
     }
-    const uint8_t* mine = reinterpret_cast<const uint8_t*>(blk + threadIdx.x * 4);
-    if (b >= j.nb) return;
-    uint64_t tok = m.tok[b];
-    if (!tok) return;
-    const uint64_t op = m.open[b], cl = m.close[b];
-    uint32_t idx = (uint32_t)toff[b];
-    uint32_t oi = (uint32_t)ooff[b], vi = (uint32_t)coff[b];
-    const int64_t d0 = (int64_t)doff[b] - 64ll * b;
-    while (tok) {
-        const int k = __ffsll((long long)tok) - 1;
-        tok &= tok - 1;
+    stok[threadIdx.x] = tok;
+    const uint32_t cnt = __popcll(tok);
+    uint32_t inc = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(inc, d, 64);
+        if (lane >= (uint32_t)d) inc += o;
+    }
+    sex[threadIdx.x] = inc - cnt;
+    const uint32_t wtot = __shfl(inc, 63, 64);
+    const uint32_t base = (uint32_t)__shfl(ti, 0, 64);  // toff of the wave's first block
+    __syncthreads();
+    for (uint32_t r = lane; r < wtot; r += 64) {
+        uint32_t L = 0;                                    // last lane with sex <= r
+#pragma unroll
+        for (uint32_t st = 32; st >= 1; st >>= 1)
+            if (sex[w0 + L + st] <= r) L += st;
+        const uint32_t o = w0 + L;
+        const uint32_t k = select_bit(stok[o], r - sex[o]);
         const uint64_t below = (1ull << k) - 1;
-        int64_t d = d0 + __popcll(op & below) - __popcll(cl & below);
-        const uint32_t pos = b * 64 + k;
-        const uint32_t kind = kind_of(mine[k]);
+        int64_t d = sd0[o] + __popcll(sop[o] & below) - __popcll(scl[o] & below);
+        const uint32_t bb = blockIdx.x * BLOCK + o;
+        const uint32_t pos = bb * 64 + k;
+        const uint32_t kind = kind_of(reinterpret_cast<const uint8_t*>(blk + o * 4)[k]);
         if (d < 0 || ((kind == TK_OBJ_END || kind == TK_ARR_END) && d < 1)) {
             js_fail(err, pos, KDTN_JSON_SYNTAX);      // a close with nothing open
             d = d < 0 ? 0 : d;
         }
+        const uint32_t idx = base + r;
         if (kind == TK_OBJ || kind == TK_ARR) {
             if (d >= 10000) js_fail(err, pos, KDTN_JSON_DEPTH);
-            olist[oi++] = idx;
+            olist[soo[o] + __popcll(sop[o] & below)] = idx;
         } else if (kind == TK_COLON) {
-            vlist[vi++] = idx + 1;                    // the member value follows its colon
+            vlist[sco[o] + __popcll(scol[o] & below)] = idx + 1;   // the member value follows its colon
         }
         if (d > (int64_t)TK_DEPTH_MASK) d = TK_DEPTH_MASK;
-        toks[idx++] = make_uint2(pos, (uint32_t)d | (kind << 24));
+        toks[idx] = make_uint2(pos, (uint32_t)d | (kind << 24));
     }
 }
 
