@@ -370,7 +370,7 @@ constexpr int JS_TPAD = JS_TILE + JS_TILE / JS_PER;
 
 __global__ void __launch_bounds__(BLOCK) k_js_par_apply(const uint2* toks, uint32_t ntok, const uint32_t* texcl,
                                                         uint32_t* par) {
-    __shared__ uint32_t sh[2][BLOCK * JS_PD];
+    __shared__ uint32_t wt[BLOCK / 64][JS_PD];
     __shared__ uint32_t st[BLOCK * (JS_PD + 1)];
     __shared__ uint32_t tm[JS_TPAD];              // token metas in, parents out
     const uint32_t t0 = blockIdx.x * JS_TILE;
@@ -391,24 +391,27 @@ __global__ void __launch_bounds__(BLOCK) k_js_par_apply(const uint2* toks, uint3
         const uint32_t d = meta & TK_DEPTH_MASK;
         if (tk_open(meta) && d < JS_PD) row[d] = i + 1;
     }
-    uint32_t* cur = sh[0];
-    uint32_t* nxt = sh[1];
-#pragma unroll
-    for (int d = 0; d < JS_PD; ++d) cur[d * BLOCK + threadIdx.x] = row[d];
-    __syncthreads();
-    for (int off = 1; off < BLOCK; off <<= 1) {
-#pragma unroll
-        for (int d = 0; d < JS_PD; ++d) {
-            uint32_t v = cur[d * BLOCK + threadIdx.x];
-            if ((int)threadIdx.x >= off) v = max(v, cur[d * BLOCK + threadIdx.x - off]);
-            nxt[d * BLOCK + threadIdx.x] = v;
-        }
-        __syncthreads();
-        uint32_t* tmp = cur; cur = nxt; nxt = tmp;
-    }
+    // exclusive max-scan of the rows over the workgroup: wave shuffles, then the earlier
+    // waves' totals through LDS (no LDS ping-pong buffers, so more workgroups fit per CU)
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    uint32_t incl[JS_PD];
 #pragma unroll
     for (int d = 0; d < JS_PD; ++d) {
-        const uint32_t ex = threadIdx.x ? cur[d * BLOCK + threadIdx.x - 1] : 0u;
+        uint32_t v = row[d];
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t o = __shfl_up(v, off, 64);
+            if (lane >= (uint32_t)off) v = max(v, o);
+        }
+        incl[d] = v;
+        if (lane == 63) wt[wave][d] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int d = 0; d < JS_PD; ++d) {
+        uint32_t ex = __shfl_up(incl[d], 1, 64);
+        if (lane == 0) ex = 0;
+        for (uint32_t w = 0; w < wave; ++w) ex = max(ex, wt[w][d]);
         row[d] = max(ex, texcl[(size_t)blockIdx.x * JS_PD + d]);
     }
     for (int k = 0; k < JS_PER; ++k) {
