@@ -806,7 +806,7 @@ KD_INLINE uint32_t elem_class(const uint2* toks, const uint32_t* par, const uint
 }
 
 __global__ void __launch_bounds__(BLOCK) k_js_elems_count(JsDoc j, const uint2* toks, uint32_t ntok, const uint32_t* par,
-                                                          const uint8_t* role, uint32_t* cnt3,
+                                                          const uint8_t* role, uint32_t* cnt3, uint8_t* ecls,
                                                           unsigned long long* derr) {
     __shared__ uint32_t sh[3];
     if (threadIdx.x < 3) sh[threadIdx.x] = 0;
@@ -821,6 +821,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_elems_count(JsDoc j, const uint2* 
         const uint32_t i = t0 + q * BLOCK + threadIdx.x;
         if (i >= ntok) break;
         const uint32_t cls = elem_class(toks, par, role, i);
+        ecls[i] = (uint8_t)cls;                                   // kept for k_js_elems_write
         if (!cls) continue;
         const uint2 t = toks[i];
         const uint32_t kind = tkind(t);
@@ -834,15 +835,14 @@ __global__ void __launch_bounds__(BLOCK) k_js_elems_count(JsDoc j, const uint2* 
     if (threadIdx.x < 3) cnt3[(size_t)threadIdx.x * gridDim.x + blockIdx.x] = sh[threadIdx.x];
 }
 
-__global__ void __launch_bounds__(BLOCK) k_js_elems_write(const uint2* toks, uint32_t ntok, const uint32_t* par,
-                                                          const uint8_t* role, const uint64_t* coff3, uint32_t ntiles,
-                                                          uint32_t* ord, JsTopoOut to) {
+__global__ void __launch_bounds__(BLOCK) k_js_elems_write(const uint8_t* ecls, uint32_t ntok, const uint64_t* coff3,
+                                                          uint32_t ntiles, uint32_t* ord, JsTopoOut to) {
     __shared__ uint64_t sh[BLOCK / 64];
     __shared__ uint8_t tc[JS_TPAD];                // element class per tile token
     const uint32_t t0 = blockIdx.x * JS_TILE;
     for (int q = 0; q < JS_PER; ++q) {            // classes: coalesced order
         const uint32_t l = q * BLOCK + threadIdx.x;
-        tc[tpad(l)] = t0 + l < ntok ? (uint8_t)elem_class(toks, par, role, t0 + l) : (uint8_t)0;
+        tc[tpad(l)] = t0 + l < ntok ? ecls[t0 + l] : (uint8_t)0;
     }
     __syncthreads();
     const uint8_t* mine = tc + threadIdx.x * (JS_PER + 1);

@@ -358,9 +358,9 @@ __global__ void k_js_validate(JsDoc j, const uint2* toks, uint32_t ntok, const u
 __global__ void k_js_roles(JsDoc j, const uint2* toks, const uint32_t* olist, uint32_t nopen, const uint32_t* par,
                            uint8_t* role, uint32_t level);
 __global__ void k_js_elems_count(JsDoc j, const uint2* toks, uint32_t ntok, const uint32_t* par, const uint8_t* role,
-                                 uint32_t* cnt3, unsigned long long* derr);
-__global__ void k_js_elems_write(const uint2* toks, uint32_t ntok, const uint32_t* par, const uint8_t* role,
-                                 const uint64_t* coff3, uint32_t ntiles, uint32_t* ord, JsTopoOut to);
+                                 uint32_t* cnt3, uint8_t* ecls, unsigned long long* derr);
+__global__ void k_js_elems_write(const uint8_t* ecls, uint32_t ntok, const uint64_t* coff3, uint32_t ntiles,
+                                 uint32_t* ord, JsTopoOut to);
 __global__ void k_js_values(JsDoc j, const uint2* toks, const uint32_t* vlist, uint32_t nval, const uint32_t* par,
                             const uint8_t* role, const uint32_t* ord, JsTopoOut to, JsStore des, JsStore real,
                             JsIntern in, unsigned long long* derr);
