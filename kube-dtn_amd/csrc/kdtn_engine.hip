@@ -99,7 +99,7 @@ struct kdtn_ctx {
     DevBuf j_doc, j_q, j_bs, j_hb, j_qcnt, j_qoff, j_tok, j_open, j_close, j_tcnt, j_dcnt, j_toff, j_doff;
     DevBuf j_ocnt, j_ooff, j_olist, j_ccnt, j_coff, j_vlist;
     uint32_t j_kcap = 0, j_pcap = 0;   // intern table sizes that fit the last document
-    DevBuf j_toks, j_par, j_role, j_ecls, j_ord, j_tagg, j_gagg, j_cnt3, j_coff3, j_small, j_part;
+    DevBuf j_toks, j_par, j_role, j_ecls, j_odep, j_ord, j_tagg, j_gagg, j_cnt3, j_coff3, j_small, j_part;
     DevBuf j_tflags, j_owner, j_vown, j_kslots, j_krep, j_pslots, j_prep, j_heap;
     DevBuf j_bits, j_bcnt, j_wrank, j_kslot_id, j_pslot_id, j_len, j_off64;
     uint64_t j_n = 0;
@@ -444,7 +444,7 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->f_part, &c->f_idx, &c->tc_size, &c->tc_off, &c->tc_part, &c->tc_arena,
                       &c->j_doc, &c->j_q, &c->j_bs, &c->j_hb, &c->j_qcnt, &c->j_qoff, &c->j_tok, &c->j_open,
                       &c->j_close, &c->j_tcnt, &c->j_dcnt, &c->j_toff, &c->j_doff, &c->j_toks, &c->j_par,
-                      &c->j_role, &c->j_ecls, &c->j_ord, &c->j_tagg, &c->j_gagg, &c->j_cnt3, &c->j_coff3, &c->j_small,
+                      &c->j_role, &c->j_ecls, &c->j_odep, &c->j_ord, &c->j_tagg, &c->j_gagg, &c->j_cnt3, &c->j_coff3, &c->j_small,
                       &c->j_part, &c->j_tflags, &c->j_owner, &c->j_vown, &c->j_kslots, &c->j_krep,
                       &c->j_pslots, &c->j_prep, &c->j_heap, &c->j_bits, &c->j_bcnt, &c->j_wrank,
                       &c->j_kslot_id, &c->j_pslot_id, &c->j_len, &c->j_off64, &c->j_ocnt, &c->j_ooff,
@@ -1275,6 +1275,7 @@ int kdtn_json_ingest(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest_info* 
     TRY(ensure(c->j_ord, (size_t)ntok * 4));
     const uint32_t nopen = (uint32_t)nopen64;
     TRY(ensure(c->j_olist, (size_t)nopen * 4));
+    TRY(ensure(c->j_odep, (size_t)nopen));
     const uint32_t nval = (uint32_t)nval64;
     TRY(ensure(c->j_vlist, (size_t)nval * 4));
     const uint2* toks = dp<uint2>(c->j_toks);
@@ -1306,7 +1307,8 @@ int kdtn_json_ingest(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest_info* 
     uint32_t* ord = dp<uint32_t>(c->j_ord);
     HIP_TRY(hipMemsetAsync(role, 0, ntok, s));                  // R_NONE below the schema levels
     for (uint32_t level = 0; level <= 6 && nopen; ++level)
-        k_js_roles<<<nblocks(nopen), BLOCK, 0, s>>>(j, toks, dp<uint32_t>(c->j_olist), nopen, par, role, level);
+        k_js_roles<<<nblocks(nopen), BLOCK, 0, s>>>(j, toks, dp<uint32_t>(c->j_olist), nopen, par, role,
+                                                    dp<uint8_t>(c->j_odep), level);
     TRY(ensure(c->j_cnt3, (size_t)3 * ntiles * 4));
     TRY(ensure(c->j_coff3, (size_t)3 * (ntiles + 1) * 8));
     k_js_elems_count<<<ntiles, BLOCK, 0, s>>>(j, toks, ntok, par, role, dp<uint32_t>(c->j_cnt3),

@@ -779,12 +779,20 @@ KD_INLINE uint32_t child_role(const JsDoc& j, const uint2* toks, uint32_t r, uin
 // one nesting level at a time over the open brackets: a container's role follows from its
 // parent's (already set by the previous level), its kind and its member name
 __global__ void __launch_bounds__(BLOCK) k_js_roles(JsDoc j, const uint2* toks, const uint32_t* olist, uint32_t nopen,
-                                                    const uint32_t* par, uint8_t* role, uint32_t level) {
+                                                    const uint32_t* par, uint8_t* role, uint8_t* odep,
+                                                    uint32_t level) {
     const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
     if (k >= nopen) return;
+    // level 0 records every open bracket's depth (one byte, saturated); later levels read
+    // that byte coalesced and touch the token only at their own level
+    if (level != 0 && odep[k] != level) return;
     const uint32_t i = olist[k];
     const uint2 t = toks[i];
-    if (tdepth(t) != level) return;
+    if (level == 0) {
+        const uint32_t d = tdepth(t);
+        odep[k] = (uint8_t)(d > 254u ? 255u : d);
+        if (d != 0) return;
+    }
     const uint32_t r = level == 0 ? (tkind(t) == TK_OBJ ? R_ROOT : R_NONE)
                                   : child_role(j, toks, role[par[i]], i);
     role[i] = (uint8_t)r;

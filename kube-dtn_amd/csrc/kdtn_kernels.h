@@ -356,7 +356,7 @@ __global__ void k_js_par_apply(const uint2* toks, uint32_t ntok, const uint32_t*
 __global__ void k_js_deep(const uint2* toks, uint32_t ntok, uint32_t* par);
 __global__ void k_js_validate(JsDoc j, const uint2* toks, uint32_t ntok, const uint32_t* par, unsigned long long* err);
 __global__ void k_js_roles(JsDoc j, const uint2* toks, const uint32_t* olist, uint32_t nopen, const uint32_t* par,
-                           uint8_t* role, uint32_t level);
+                           uint8_t* role, uint8_t* odep, uint32_t level);
 __global__ void k_js_elems_count(JsDoc j, const uint2* toks, uint32_t ntok, const uint32_t* par, const uint8_t* role,
                                  uint32_t* cnt3, uint8_t* ecls, unsigned long long* derr);
 __global__ void k_js_elems_write(const uint8_t* ecls, uint32_t ntok, const uint64_t* coff3, uint32_t ntiles,
