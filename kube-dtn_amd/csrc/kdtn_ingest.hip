@@ -1372,6 +1372,14 @@ __global__ void __launch_bounds__(BLOCK) k_js_dict_copy(JsDict dt, JsIntern in, 
     const uint32_t len = (uint32_t)(kw >> 32) & 0xFFFFFFu;
     const uint64_t at = off64[id];
     offs[id] = (uint32_t)at;
+    if (len <= WIN) {                   // one batch of aligned loads (doc and heap are padded)
+        uint32_t u[8];
+        load_window((kw >> 56) & 1 ? in.heap : in.doc, (uint32_t)kw, u);
+#pragma unroll
+        for (uint32_t k = 0; k < WIN; ++k)
+            if (k < len) arena[at + k] = (uint8_t)win_byte(u, (int)k);
+        return;
+    }
     const uint8_t* src = key_bytes(in, kw);
     for (uint32_t k = 0; k < len; ++k) arena[at + k] = src[k];
 }
