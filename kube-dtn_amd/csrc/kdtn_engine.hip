@@ -1271,7 +1271,7 @@ int kdtn_json_ingest(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest_info* 
     TRY(ensure(c->j_toks, (size_t)ntok * 8));
     TRY(ensure(c->j_par, (size_t)ntok * 4));
     TRY(ensure(c->j_role, (size_t)ntok));
-    TRY(ensure(c->j_ecls, (size_t)ntok));
+    TRY(ensure(c->j_ecls, ((size_t)ntok + JS_TILE - 1) / JS_TILE * JS_TILE));   // whole tiles (uint4 reads)
     TRY(ensure(c->j_ord, (size_t)ntok * 4));
     const uint32_t nopen = (uint32_t)nopen64;
     TRY(ensure(c->j_olist, (size_t)nopen * 4));
@@ -1294,7 +1294,7 @@ int kdtn_json_ingest(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest_info* 
     k_js_par_apply<<<ntiles, BLOCK, 0, s>>>(toks, ntok, dp<uint32_t>(c->j_tagg), par);
     k_js_deep<<<nblocks(ntok), BLOCK, 0, s>>>(toks, ntok, par);
     timer_mark(c, "js_parents");
-    k_js_validate<<<nblocks(ntok), BLOCK, 0, s>>>(j, toks, ntok, par, small);
+    k_js_validate<<<nblocks(ntok), BLOCK, 0, s>>>(j, toks, ntok, par, dp<uint8_t>(c->j_ecls), small);
     timer_mark(c, "js_validate");
     TRY(d2h(c, &serr, small));
     HIP_TRY(hipStreamSynchronize(s));

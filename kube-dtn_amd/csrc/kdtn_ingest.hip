@@ -590,7 +590,7 @@ KD_INLINE uint32_t str_end_bs(const JsDoc& j, uint32_t pos, bool* bs, bool* hb =
 }
 
 __global__ void __launch_bounds__(BLOCK) k_js_validate(JsDoc j, const uint2* toks, uint32_t ntok, const uint32_t* par,
-                                                       unsigned long long* err) {
+                                                       uint8_t* ecand, unsigned long long* err) {
     // the block's tokens (with the two before) and parents (with the one before) staged in
     // LDS with coalesced loads: a token's neighbours, and parents inside the block, come from
     // LDS instead of further global loads
@@ -617,6 +617,13 @@ __global__ void __launch_bounds__(BLOCK) k_js_validate(JsDoc j, const uint2* tok
     const uint32_t pkind = p < JS_DEEP ? kind_of(p) : 0xFEu;
     const uint32_t ck = d == 0 ? 0xFFu : pkind;                   // container kind
     bool ok;
+    {
+        // element candidate (see k_js_elems_count), from the staged neighbours:
+        // k_js_elems_count then reads one byte per token instead of the token stream
+        const uint32_t pk = i ? tkind(st[threadIdx.x + 1]) : 0xFFu;
+        ecand[i] = (uint8_t)(i != 0 && (d == 2 || d == 5) && (pk == TK_ARR || pk == TK_COMMA) && value_start(kind) &&
+                             p < JS_DEEP && pkind == TK_ARR);
+    }
     if (i == 0) {
         ok = value_start(kind) && d == 0;
     } else {
@@ -799,20 +806,9 @@ __global__ void __launch_bounds__(BLOCK) k_js_roles(JsDoc j, const uint2* toks, 
 }
 
 // ---------------------------------------------------------------- element ordinals
-// class of token i: 1 + {0 items element, 1 spec.links element, 2 status.links element}, or 0
-KD_INLINE uint32_t elem_class(const uint2* toks, const uint32_t* par, const uint8_t* role, uint32_t i) {
-    if (i == 0) return 0;
-    const uint32_t d = tdepth(toks[i]);
-    if (d != 2 && d != 5) return 0;                 // items elements: depth 2; links elements: 5
-    const uint32_t pk = tkind(toks[i - 1]);
-    if (pk != TK_ARR && pk != TK_COMMA) return 0;
-    if (!value_start(tkind(toks[i]))) return 0;
-    const uint32_t p = par[i];
-    if (p >= JS_DEEP || tkind(toks[p]) != TK_ARR) return 0;
-    const uint32_t r = role[p];
-    return r == R_ITEMS ? 1 : r == R_SPEC_LINKS ? 2 : r == R_STATUS_LINKS ? 3 : 0;
-}
-
+// Element class of token i: 1 + {0 items element, 1 spec.links element, 2 status.links
+// element}, or 0. k_js_validate marks the candidates (depth 2 for items elements, 5 for links
+// elements; after '[' or ','; a value; parent an array); the parent array's role decides.
 __global__ void __launch_bounds__(BLOCK) k_js_elems_count(JsDoc j, const uint2* toks, uint32_t ntok, const uint32_t* par,
                                                           const uint8_t* role, uint32_t* cnt3, uint8_t* ecls,
                                                           unsigned long long* derr) {
@@ -825,17 +821,33 @@ __global__ void __launch_bounds__(BLOCK) k_js_elems_count(JsDoc j, const uint2* 
         const uint2 t = toks[0];
         if (!(tkind(t) == TK_OBJ || (tkind(t) == TK_SCALAR && j.doc[t.x] == 'n'))) js_fail(derr, t.x, KDTN_JSON_TYPE);
     }
-    for (int q = 0; q < JS_PER; ++q) {                            // counts: coalesced order
-        const uint32_t i = t0 + q * BLOCK + threadIdx.x;
-        if (i >= ntok) break;
-        const uint32_t cls = elem_class(toks, par, role, i);
-        ecls[i] = (uint8_t)cls;                                   // kept for k_js_elems_write
-        if (!cls) continue;
-        const uint2 t = toks[i];
-        const uint32_t kind = tkind(t);
-        if (!(kind == TK_OBJ || (kind == TK_SCALAR && j.doc[t.x] == 'n'))) js_fail(derr, t.x, KDTN_JSON_TYPE);
-        c[cls - 1]++;
+    // counts: the thread's 16 candidate bytes (JS_PER == 16) as one coalesced 16-byte load;
+    // the buffer is padded to whole tiles, bytes past ntok are ignored
+    static_assert(JS_PER == 16, "one uint4 of candidate bytes per thread");
+    const uint32_t base = t0 + threadIdx.x * JS_PER;
+    uint4* cp = reinterpret_cast<uint4*>(ecls + base);
+    uint4 cv = *cp;
+    uint32_t w[4] = {cv.x, cv.y, cv.z, cv.w};
+    bool changed = false;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        if (!w[q]) continue;
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+            const uint32_t i = base + q * 4 + h;
+            if (i >= ntok || !((w[q] >> (8 * h)) & 0xFFu)) continue;
+            const uint32_t r = role[par[i]];
+            const uint32_t cls = r == R_ITEMS ? 1 : r == R_SPEC_LINKS ? 2 : r == R_STATUS_LINKS ? 3 : 0;
+            w[q] = (w[q] & ~(0xFFu << (8 * h))) | (cls << (8 * h));   // the class, for k_js_elems_write
+            changed = true;
+            if (!cls) continue;
+            const uint2 t = toks[i];
+            const uint32_t kind = tkind(t);
+            if (!(kind == TK_OBJ || (kind == TK_SCALAR && j.doc[t.x] == 'n'))) js_fail(derr, t.x, KDTN_JSON_TYPE);
+            c[cls - 1]++;
+        }
     }
+    if (changed) *cp = make_uint4(w[0], w[1], w[2], w[3]);
 #pragma unroll
     for (int q = 0; q < 3; ++q)
         if (c[q]) atomicAdd(&sh[q], c[q]);

@@ -354,7 +354,8 @@ __global__ void k_js_par_top(uint32_t* gagg, uint32_t ng);
 __global__ void k_js_par_tiles(uint32_t* tagg, uint32_t ntiles, const uint32_t* gagg);
 __global__ void k_js_par_apply(const uint2* toks, uint32_t ntok, const uint32_t* texcl, uint32_t* par);
 __global__ void k_js_deep(const uint2* toks, uint32_t ntok, uint32_t* par);
-__global__ void k_js_validate(JsDoc j, const uint2* toks, uint32_t ntok, const uint32_t* par, unsigned long long* err);
+__global__ void k_js_validate(JsDoc j, const uint2* toks, uint32_t ntok, const uint32_t* par, uint8_t* ecand,
+                              unsigned long long* err);
 __global__ void k_js_roles(JsDoc j, const uint2* toks, const uint32_t* olist, uint32_t nopen, const uint32_t* par,
                            uint8_t* role, uint8_t* odep, uint32_t level);
 __global__ void k_js_elems_count(JsDoc j, const uint2* toks, uint32_t ntok, const uint32_t* par, const uint8_t* role,
