@@ -1235,6 +1235,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, const uint2* toks,
     const uint32_t o = par[i];
     if (o >= JS_DEEP) return;
     const uint32_t r = role[o];
+    const uint32_t po = par[o];                        // the grandparent, loaded with the role
     const KeyName kn = key_name(j, kpos);              // decoded while role[o] is in flight
     if (r == R_NONE || r == R_ITEMS || r == R_SPEC_LINKS || r == R_STATUS_LINKS) return;
     const uint32_t kind = tkind(t);
@@ -1254,15 +1255,15 @@ __global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, const uint2* toks,
         break;
     case R_META:
         f = key_match(kn, kMeta, 2);
-        topo = ord[par[o]]; bit = 3 + f; own = 1 + topo * 9;
+        topo = ord[po]; bit = 3 + f; own = 1 + topo * 9;
         break;
     case R_SPEC:
         f = key_match(kn, kLinks, 1);
-        topo = ord[par[o]]; bit = 5 + f; own = 1 + topo * 9;
+        topo = ord[po]; bit = 5 + f; own = 1 + topo * 9;
         break;
     case R_STATUS:
         f = key_match(kn, kStatus, 3);
-        topo = ord[par[o]]; bit = 6 + f; own = 1 + topo * 9;
+        topo = ord[po]; bit = 6 + f; own = 1 + topo * 9;
         break;
     case R_LINK_S:
     case R_LINK_R:
@@ -1273,7 +1274,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, const uint2* toks,
     default: {                                                    // R_PROPS_S / R_PROPS_R
         f = key_match(kn, kProps, KDTN_NPROP + 1);
         st = r == R_PROPS_S ? &des : &real;
-        rec = ord[par[o]]; bit = 9 + f; own = (r == R_PROPS_S ? in.own_des : in.own_real) + rec * 22;
+        rec = ord[po]; bit = 9 + f; own = (r == R_PROPS_S ? in.own_des : in.own_real) + rec * 22;
         break;
     }
     }
