@@ -560,14 +560,17 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
     }
     // dictionaries
     if (c->D) {
-        int sub = 1;                                                   // strings per thread (2, 4: slower)
-        if (const char* ev = std::getenv("KDTN_KD_SUB")) sub = std::atoi(ev);   // profiling A/B
         const uint8_t* kb = dp<uint8_t>(c->kd_bytes);
         const uint32_t* ko = dp<uint32_t>(c->kd_offs);
         uint32_t* bits = dp<uint32_t>(c->kd_bits);
+#if KDTN_PROFILING
+        int sub = 1;                                                   // strings per thread (2, 4: slower)
+        if (const char* ev = std::getenv("KDTN_KD_SUB")) sub = std::atoi(ev);
         if (sub == 4) k_kdict_flags<4><<<nblocks(c->D, BLOCK * 4), BLOCK, 0, s>>>(kb, ko, c->D, bits, c->kb_words, misc);
-        else if (sub == 1) k_kdict_flags<1><<<nblocks(c->D), BLOCK, 0, s>>>(kb, ko, c->D, bits, c->kb_words, misc);
-        else k_kdict_flags<2><<<nblocks(c->D, BLOCK * 2), BLOCK, 0, s>>>(kb, ko, c->D, bits, c->kb_words, misc);
+        else if (sub == 2) k_kdict_flags<2><<<nblocks(c->D, BLOCK * 2), BLOCK, 0, s>>>(kb, ko, c->D, bits, c->kb_words, misc);
+        else
+#endif
+        k_kdict_flags<1><<<nblocks(c->D), BLOCK, 0, s>>>(kb, ko, c->D, bits, c->kb_words, misc);
     }
     timer_mark(c, "kdict_parse");
     if (c->P) k_pdict_parse<<<nblocks(c->P), BLOCK, 0, s>>>(dp<uint8_t>(c->pd_bytes), dp<uint32_t>(c->pd_offs),
@@ -633,8 +636,6 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         o.upd_qdisc = dp<uint2>(c->upd_qdisc);
         o.totals = misc + 1;
         o.stages = stages;
-        int variant = DEFAULT_VARIANT;
-        if (const char* ev = std::getenv("KDTN_VARIANT")) variant = std::atoi(ev);   // profiling A/B
         RecWork w;
         w.sync = dp<uint32_t>(c->sync);
         w.status = reinterpret_cast<unsigned long long*>(static_cast<char*>(c->sync.p) + 16);
@@ -645,6 +646,9 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         w.trace = nullptr;
         w.first_partial = misc + MISC_FIRST_PARTIAL;                // 0xFFFFFFFF from the memset
         k_full_prefix<<<nblocks(c->T), BLOCK, 0, s>>>(T, misc + MISC_FIRST_PARTIAL);
+#if KDTN_PROFILING
+        int variant = DEFAULT_VARIANT;
+        if (const char* ev = std::getenv("KDTN_VARIANT")) variant = std::atoi(ev);
         if (variant & VAR_TRACE) {
             TRY(ensure(c->trace, (size_t)c->nwg * TRACE_WORDS * 8));
             w.trace = reinterpret_cast<unsigned long long*>(c->trace.p);
@@ -680,6 +684,9 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
             k_reconcile<DEFAULT_VARIANT><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w);
             break;
         }
+#else
+        k_reconcile<DEFAULT_VARIANT><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w);
+#endif
         timer_mark(c, "reconcile");
     } else {
         HIP_TRY(hipMemsetAsync(misc + 1, 0, 12, s));
@@ -1384,14 +1391,18 @@ int kdtn_json_ingest(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest_info* 
         in.vown = dp<uint32_t>(c->j_vown);
         in.own_des = 1 + 9 * T;
         in.own_real = in.own_des + 22 * N;
+#if KDTN_PROFILING
         in.variant = (uint32_t)std::strtoul(std::getenv("KDTN_JS_VARIANT") ? std::getenv("KDTN_JS_VARIANT") : "0",
                                             nullptr, 0);
+#else
+        in.variant = 0;
+#endif
         in.kd = JsDict{dp<unsigned long long>(c->j_kslots), dp<uint32_t>(c->j_krep), kcap - 1};
         in.pd = JsDict{dp<unsigned long long>(c->j_pslots), dp<uint32_t>(c->j_prep), pcap - 1};
         if (nval)
             k_js_values<<<nblocks(nval), BLOCK, 0, s>>>(j, toks, dp<uint32_t>(c->j_vlist), nval, par, role, ord, to,
                                                         des, real, in, small + 1);
-        if (nval && !(in.variant & JSV_NO_SEEN))
+        if (nval && !(KDTN_PROFILING && (in.variant & JSV_NO_SEEN)))
             k_js_dups<<<nblocks(nval), BLOCK, 0, s>>>(toks, dp<uint32_t>(c->j_vlist), nval, dp<uint32_t>(c->j_vown),
                                                       dp<uint32_t>(c->j_owner), small + 1);
         timer_mark(c, "js_values");

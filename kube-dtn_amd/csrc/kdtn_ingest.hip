@@ -1053,7 +1053,7 @@ KD_INLINE uint32_t intern(const JsIntern& in, const JsDict& dt, const uint8_t* p
     for (uint32_t probe = 0; probe <= dt.mask; ++probe) {
         // slots are written once (CAS from 0): a plain load is either that final key or a stale 0,
         // and a stale 0 only sends us to the CAS, which returns the real key
-        unsigned long long cur = (in.variant & JSV_COHERENT) ? __hip_atomic_load(dt.slots + s, __ATOMIC_RELAXED,
+        unsigned long long cur = (KDTN_PROFILING && (in.variant & JSV_COHERENT)) ? __hip_atomic_load(dt.slots + s, __ATOMIC_RELAXED,
                                                                                  __HIP_MEMORY_SCOPE_AGENT)
                                                              : dt.slots[s];
         if (cur == 0) {
@@ -1083,7 +1083,7 @@ KD_INLINE uint32_t intern(const JsIntern& in, const JsDict& dt, const uint8_t* p
                 while (k < len && q[k] == p[k]) ++k;
             }
             if (k == len) {                           // hot strings: skip the atomic when it cannot lower
-                if (!(in.variant & JSV_NO_REP) && occ < dt.rep[s]) atomicMin(dt.rep + s, occ);
+                if (!(KDTN_PROFILING && (in.variant & JSV_NO_REP)) && occ < dt.rep[s]) atomicMin(dt.rep + s, occ);
                 return s;
             }
         }
@@ -1299,7 +1299,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, const uint2* toks,
     case R_META: {
         if (null) break;
         if (kind != TK_STR) { ok = false; break; }
-        const uint32_t v = (in.variant & JSV_NO_INTERN) ? 1u : string_slot(j, in, in.kd, i, t.x);
+        const uint32_t v = (KDTN_PROFILING && (in.variant & JSV_NO_INTERN)) ? 1u : string_slot(j, in, in.kd, i, t.x);
         if (v == JS_NONE) return;
         uint32_t* dst = r == R_META ? (f == 0 ? to.name : to.ns) : (f == 1 ? to.src_ip : to.net_ns);
         dst[topo] = v;
@@ -1327,7 +1327,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, const uint2* toks,
         }
         if (null) break;
         if (kind != TK_STR) { ok = false; break; }
-        const uint32_t v = (in.variant & JSV_NO_INTERN) ? 1u : string_slot(j, in, props ? in.pd : in.kd, i, t.x);
+        const uint32_t v = (KDTN_PROFILING && (in.variant & JSV_NO_INTERN)) ? 1u : string_slot(j, in, props ? in.pd : in.kd, i, t.x);
         if (v == JS_NONE) return;
         *store_word(*st, rec, props ? COL_PROP0 + f : COL_KEY0 + f) = v;
         break;

@@ -99,7 +99,14 @@ struct DevLinks {
     }
 };
 
-// Emission variants (A/B in one binary; kdtn_epoch_run picks KDTN_VARIANT or the default):
+// Profiling build (make -C kube-dtn_amd prof → prof/libkdtn_prof.so, -DKDTN_PROFILING=1):
+// the A/B variants below are instantiated and selected from KDTN_VARIANT / KDTN_KD_SUB /
+// KDTN_JS_VARIANT. The product library (kdtn/libkdtn.so) compiles only DEFAULT_VARIANT and
+// the parity-tested paths, and reads no environment variable.
+#ifndef KDTN_PROFILING
+#define KDTN_PROFILING 0
+#endif
+// Emission variants (A/B in the profiling build; the product runs DEFAULT_VARIANT):
 //   bit 0: non-temporal streaming loads of link columns
 //   bit 1: non-temporal output stores
 //   bit 2: (profiling) compute MakeQdiscs but do not store it
@@ -294,7 +301,7 @@ constexpr uint32_t JS_NONE = 0xFFFFFFFFu, JS_DEEP = 0xFFFFFFFEu;
 enum : uint32_t { R_NONE = 0, R_ROOT, R_ITEMS, R_ITEM, R_META, R_SPEC, R_STATUS, R_SPEC_LINKS, R_STATUS_LINKS,
                   R_LINK_S, R_LINK_R, R_PROPS_S, R_PROPS_R };
 constexpr uint32_t JS_ST_OVERFLOW = 1, JS_ST_LONG = 2;   // intern status bits
-// ingest variants (KDTN_JS_VARIANT, profiling only; bits 1-3 give wrong tables)
+// ingest variants (KDTN_JS_VARIANT, profiling build only; bits 1-3 give wrong tables)
 constexpr uint32_t JSV_COHERENT = 1, JSV_NO_SEEN = 2, JSV_NO_REP = 4, JSV_NO_INTERN = 8;
 
 struct JsDoc {

@@ -262,8 +262,10 @@ __global__ void __launch_bounds__(BLOCK) k_kdict_flags(const uint8_t* bytes, con
     }
 }
 template __global__ void k_kdict_flags<1>(const uint8_t*, const uint32_t*, uint32_t, uint32_t*, uint32_t, uint32_t*);
+#if KDTN_PROFILING
 template __global__ void k_kdict_flags<2>(const uint8_t*, const uint32_t*, uint32_t, uint32_t*, uint32_t, uint32_t*);
 template __global__ void k_kdict_flags<4>(const uint8_t*, const uint32_t*, uint32_t, uint32_t*, uint32_t, uint32_t*);
+#endif
 
 KD_INLINE void pdict_parse_one(const uint8_t* s, uint32_t len, double tick, uint32_t* pct_out,
                                uint2* dur_out, uint2* rate_out, bool* rate_bad) {
@@ -1367,6 +1369,8 @@ __global__ void __launch_bounds__(BLOCK) k_qdisc_batch(DevLinks props, DevTables
     store_qdisc<0>(out + (size_t)j * 9, q);
 }
 
+template __global__ void k_reconcile<515>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
+#if KDTN_PROFILING
 template __global__ void k_reconcile<0>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
 template __global__ void k_reconcile<1>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
 template __global__ void k_reconcile<2>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
@@ -1389,8 +1393,8 @@ template __global__ void k_reconcile<641>(DevTopos, DevLinks, DevLinks, DevTable
 template __global__ void k_reconcile<545>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
 template __global__ void k_reconcile<1025>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
 template __global__ void k_reconcile<1537>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
-template __global__ void k_reconcile<515>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
 template __global__ void k_reconcile<521>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
 template __global__ void k_reconcile<523>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
+#endif
 
 }  // namespace kdtn

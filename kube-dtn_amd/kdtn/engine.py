@@ -17,6 +17,17 @@ from .tables import BatchesOut, EpochInput, StrTab
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libkdtn.so")
 _lib = None
+PROF_LIB_PATH = os.path.join(os.path.dirname(_HERE), "prof", "libkdtn_prof.so")
+
+
+def use_profiling_library() -> None:
+    """tools/ only: bind the profiling build (make -C kube-dtn_amd prof), whose A/B kernel
+    variants are selected from KDTN_VARIANT / KDTN_KD_SUB / KDTN_JS_VARIANT. The product
+    library kdtn/libkdtn.so reads no environment variable. Call before the first Engine."""
+    global LIB_PATH
+    if _lib is not None and LIB_PATH != PROF_LIB_PATH:
+        raise RuntimeError("libkdtn.so is already loaded in this process")
+    LIB_PATH = PROF_LIB_PATH
 
 
 class KdtnError(RuntimeError):

@@ -63,3 +63,15 @@ def test_error_names():
     L = engine.lib()
     assert [L.kdtn_err_name(i).decode() for i in range(len(abi.ERR_NAMES))] == abi.ERR_NAMES
     assert abs(L.kdtn_psched_tick_in_usec() - 15.625) < 1e-12 or L.kdtn_psched_tick_in_usec() >= 0
+
+
+def test_product_library_reads_no_environment():
+    """The product library compiles only the parity-tested kernel paths: no A/B switch
+    (KDTN_VARIANT / KDTN_KD_SUB / KDTN_JS_VARIANT) is read from the environment, and only
+    the default k_reconcile instantiation is present (the variants live in the profiling
+    build, kube-dtn_amd/prof/libkdtn_prof.so)."""
+    data = open(engine.LIB_PATH, "rb").read()
+    for knob in (b"KDTN_VARIANT", b"KDTN_KD_SUB", b"KDTN_JS_VARIANT"):
+        assert knob not in data, knob
+    names = set(re.findall(rb"_ZN4kdtn11k_reconcileILi(\d+)E", data))
+    assert len(names) == 1, names

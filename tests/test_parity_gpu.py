@@ -102,9 +102,7 @@ def test_parser_fuzz_vs_oracle(engine, field, pool):
         assert got[i].tobytes() == want.tobytes(), (field, s, got[i], want)
 
 
-@pytest.mark.parametrize("kd_sub", ["1", "2"])
-def test_cidr_mac_via_epoch(engine, kd_sub, monkeypatch):
-    monkeypatch.setenv("KDTN_KD_SUB", kd_sub)      # 1 or 2 strings per thread in k_kdict_flags
+def test_cidr_mac_via_epoch(engine):
     rng = random.Random(5)
     ips = IPS + ["1.2.3.4/32", "255.255.255.255/0", "::/0", "::ffff:1.2.3.4/96", "1::2::3/64",
                  "1:2:3:4:5:6:7:8/128", "1:2:3:4:5:6:7:8:9/128", "::1.2.3.4/128", "1.2.3/24",
@@ -140,12 +138,10 @@ def _mutate(rng: random.Random, s: str, alphabet: str) -> str:
     return "".join(s)
 
 
-@pytest.mark.parametrize("kd_sub", ["1", "2", "4"])
-def test_key_predicates_fuzz(engine, kd_sub, monkeypatch):
+def test_key_predicates_fuzz(engine):
     """net.ParseCIDR / net.ParseMAC / localhost / physical/ predicates of key strings (the
-    register fast path of k_kdict_flags and its generic fallback) against the oracle, for
-    1, 2 and 4 strings per thread; long strings take the generic parsers."""
-    monkeypatch.setenv("KDTN_KD_SUB", kd_sub)
+    register fast path of k_kdict_flags and its generic fallback) against the oracle; long
+    strings take the generic parsers."""
     rng = random.Random(11)
     ipa, maca = "0123456789./:", "0123456789abcdefABCDEFG:-."
     ips = [f"{rng.randint(0, 300)}.{rng.randint(0, 300)}.{rng.randint(0, 300)}.{rng.randint(0, 300)}"
@@ -238,31 +234,17 @@ def test_config2_full_size_properties(engine):
     assert out.add_qdisc[s:e].tobytes() == ora.add_qdisc.tobytes()
 
 
-@pytest.mark.parametrize("variant", [1, 1025, 1537, 641, 0, 513, 523])
-def test_emission_variants_match_oracle(engine, variant, monkeypatch):
-    """Every non-profiling KDTN_VARIANT of k_reconcile (occupancy target, masked gathers,
-    early issue before the look-back) produces the oracle's bytes."""
-    monkeypatch.setenv("KDTN_VARIANT", str(variant))
-    for seed in (3, 17):
-        topos, inp = random_epoch_input(seed, T=150)
-        assert_same(engine.reconcile(inp), O.reconcile(inp, tick=TICK), f"v{variant} seed {seed}")
-    inp = synth.make(2, pods_per_shard=20000)
-    assert_same(engine.reconcile(inp), O.reconcile(inp, tick=TICK), f"v{variant} config 2")
-
-
-@pytest.mark.parametrize("variant", [1, 1025])
-def test_full_prefix_shortcut_boundaries(engine, variant, monkeypatch):
+def test_full_prefix_shortcut_boundaries(engine):
     """k_full_prefix: chunks before the first partial topology take their batch bases from
     the record offsets, later ones run the look-back. A CREATED topology (and one needing
     comparisons) in the middle of an all-AddLinks epoch moves that boundary."""
-    monkeypatch.setenv("KDTN_VARIANT", str(variant))
     inp = synth.make(2, pods_per_shard=20000)
     inp.topos.flags = inp.topos.flags.copy()
     inp.topos.flags[7001] |= abi.TOPO_STATUS_NIL            # CREATED: no entries
     inp.topos.flags[13000] |= abi.TOPO_SPEC_NIL if inp.topos.des_off[13001] == inp.topos.des_off[13000] else 0
-    assert_same(engine.reconcile(inp), O.reconcile(inp, tick=TICK), f"v{variant} boundary")
+    assert_same(engine.reconcile(inp), O.reconcile(inp, tick=TICK), "boundary")
     inp3 = synth.make(3, pods_per_shard=20000)               # churn: comparisons everywhere
-    assert_same(engine.reconcile(inp3), O.reconcile(inp3, tick=TICK), f"v{variant} churn")
+    assert_same(engine.reconcile(inp3), O.reconcile(inp3, tick=TICK), "churn")
 
 
 def _wire_same(engine, inp, ctx):

@@ -1,6 +1,7 @@
 """Per-stage ablation of one reconcile epoch (one process, data generated once).
 
     python tools/ablate.py [--pods N] [--config C] [--reps R]
+(--variants / --env A/B runs load the profiling library: make -C kube-dtn_amd prof)
 Prints per-kernel HIP-event times for stage masks ALL, DIFF|RESOLVE, DIFF|QDISC, DIFF.
 """
 import argparse
@@ -23,6 +24,9 @@ ap.add_argument("--cache", default="")
 ap.add_argument("--variants", default="", help="comma list of KDTN_VARIANT values, interleaved")
 ap.add_argument("--env", default="", help="NAME=v1,v2,...: interleaved A/B of an env knob, all stages timed")
 a = ap.parse_args()
+if a.variants or a.env:                 # A/B variants live in the profiling build
+    from kdtn import engine as _kdtn_engine
+    _kdtn_engine.use_profiling_library()
 inp = synth.make(a.config, pods_per_shard=a.pods, cache_dir=a.cache or None)
 eng = Engine(device=0)
 eng.upload(inp)

@@ -4,6 +4,8 @@ bits (1 coherent slot loads, 2 no duplicate-check atomics, 4 no first-occurrence
 import json, os, sys, time
 import torch  # noqa: F401
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "kube-dtn_amd"))
+from kdtn import engine as _kdtn_engine  # noqa: E402
+_kdtn_engine.use_profiling_library()   # A/B variants live in the profiling build
 from kdtn import Engine, synth
 inp = synth.make(2, pods_per_shard=int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000)
 doc = synth.topology_list_json(inp)

@@ -14,6 +14,8 @@ import torch  # noqa: F401  (one HIP runtime)
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "kube-dtn_amd"))
+from kdtn import engine as _kdtn_engine  # noqa: E402
+_kdtn_engine.use_profiling_library()   # A/B variants live in the profiling build
 from kdtn import Engine, abi, synth  # noqa: E402
 
 ap = argparse.ArgumentParser()
