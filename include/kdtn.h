@@ -79,7 +79,11 @@ typedef enum kdtn_err {
     KDTN_E_PEER_LOOKUP = 15,   /* getPod miss                     daemon/kubedtn/handler.go:375-379 */
     KDTN_E_PEER_NO_LINKS = 16, /* ToProtoPod: peer spec.links nil handler.go:65-69,380-384   */
     KDTN_E_PEER_VETH_CIDR = 17,/* MakeVeth peer (same node)       handler.go:402             */
-    KDTN_E_PEER_VETH_MAC = 18
+    KDTN_E_PEER_VETH_MAC = 18,
+    KDTN_E_REMOTE_CIDR = 19    /* peer daemon's Update: net.ParseCIDR(IntfIp = link.PeerIp) in
+                                  vxlan.CreateOrUpdate (daemon/vxlan/vxlan.go:80-83) fails, so
+                                  UpdateRemote (common/utils.go:62-65) and addLink (handler.go:448-451)
+                                  return it after the local VXLAN + qdiscs were set up */
 } kdtn_err;
 
 /* Reconcile decision per Topology (controllers/topology_controller.go:77-88). */
@@ -211,7 +215,10 @@ typedef struct kdtn_resolved {
     uint8_t  vni_hit;    /* del: VxlanManager.Get(vni) == local net_ns (handler.go:482-486);
                             add PHYSICAL: local VNI map holds vni for another netns
                             (handler.go:177-179); add CROSS_NODE: same check on the peer's node */
-    uint8_t  reserved;
+    uint8_t  remote_err; /* add CROSS_NODE: KDTN_E_REMOTE_CIDR when the RemotePod this link sends
+                            is rejected by the peer daemon (link.PeerIp set and not a CIDR). The
+                            link's local steps run (VXLAN, qdiscs, RPC sent), then addLink returns
+                            the error and the batch aborts after this link.                    */
 } kdtn_resolved;
 
 /* Epoch outputs, caller-owned host memory. Any pointer may be NULL (not returned).
@@ -337,11 +344,21 @@ typedef struct kdtn_wire {
 int kdtn_epoch_encode(kdtn_ctx* ctx, uint64_t* n_bytes);
 int kdtn_epoch_download_wire(kdtn_ctx* ctx, kdtn_wire* out);
 
+/* ---- which batch entries the daemons reach ------------------------------------------- */
+/* Reconcile sends a topology's batches in the order DelLinks, AddLinks, UpdateLinks and
+ * stops at the first RPC that fails (controllers/topology_controller.go:93-116); each daemon
+ * handler stops at its first failing link (daemon/kubedtn/handler.go:601-607, 622-628,
+ * 644-662). An entry is REACHED when no earlier entry of its list and no entry of an
+ * earlier list of its topology failed. A link fails when: del — kdtn_resolved.err; add —
+ * kdtn_resolved.err, or its qdisc err for the kinds that build qdiscs (SAME_NODE,
+ * CROSS_NODE, PHYSICAL), or kdtn_resolved.remote_err (after its own local steps); update —
+ * kdtn_resolved.err. kdtn_epoch_fanout and kdtn_epoch_tc apply this rule.             */
+
 /* ---- RemotePod fan-out grouped per destination daemon ------------------------------ */
 /* The UpdateRemote RPCs the daemons would send for this epoch's AddLinks batches
  * (daemon/kubedtn/handler.go:419-453, common/utils.go:39-67): an entry sends one when it is
- * CROSS_NODE, its qdisc was built (SetupVxLan → MakeQdiscs fails first) and no earlier
- * link of its batch failed (handler.go:601-607). The reference sends one RPC per link;
+ * REACHED, CROSS_NODE and its qdisc was built (SetupVxLan → MakeQdiscs fails first). The
+ * reference sends one RPC per link;
  * here they are grouped per destination daemon (peer status.src_ip = kdtn_resolved.vtep):
  * node[k] = kdict id of daemon k (ascending), its entries idx[off[k] .. off[k+1]) are
  * add-list entry indices in add-list order. Requires a run with RESOLVE and QDISC. */
@@ -358,14 +375,17 @@ int kdtn_epoch_fanout(kdtn_ctx* ctx, kdtn_fanout* out);
 /* SetVethQdiscs (common/qdisc.go:252-266) applies the TBF by exec'ing
  *   tc qdisc add dev <LinkName> parent 1:1 handle 10:0 tbf rate <Rate> burst <Buffer>
  *      latency 50ms minburst <Minburst>
- * For every AddLinks / UpdateLinks entry whose MakeQdiscs produced a TBF (and whose
- * plan has no error) this writes that argv (arguments NUL-terminated, without the
- * leading "tc") for the entry's local interface (link.LocalIntf). Entries: add list, then
- * update list; entry g = bytes[off[g], off[g+1]), empty = no tc command. */
+ * inside the interface's netns. For every REACHED AddLinks / UpdateLinks entry whose plan
+ * has no error and whose MakeQdiscs produced a TBF this writes that argv (arguments
+ * NUL-terminated, without the leading "tc"). Command slots: add entry e has two, 2e for
+ * link.LocalIntf (UpdateLinks' veth, the local VXLAN, or the local end of a veth pair) and
+ * 2e+1 for link.PeerIntf in the peer pod's netns (SAME_NODE only: CreateVeth sets the
+ * qdiscs on both ends, common/veth.go:53-60); update entry u has one, slot 2*n_add + u, for
+ * link.LocalIntf. Slot g = bytes[off[g], off[g+1]), empty = no tc command. */
 typedef struct kdtn_tc_argv {
     uint8_t*  bytes;
     uint64_t  cap;
-    uint64_t* off;           /* [n_add + n_upd + 1]                                    */
+    uint64_t* off;           /* [2*n_add + n_upd + 1] command slots                   */
     uint64_t  n_bytes;       /* out                                                    */
 } kdtn_tc_argv;
 int kdtn_epoch_tc(kdtn_ctx* ctx, uint64_t* n_bytes);   /* after run(QDISC|RESOLVE) + sync */

@@ -88,7 +88,7 @@ struct kdtn_ctx {
     uint64_t w_bytes = 0;
     bool encoded = false;
     // RemotePod fan-out
-    DevBuf f_mark, f_send, f_node_idx, f_nodes, f_counts, f_base, f_part, f_idx;
+    DevBuf f_mark, f_send, f_node_idx, f_nodes, f_counts, f_base, f_part, f_idx, f_reach_upd;
     uint32_t f_stamp = 0;
     // tc argv
     DevBuf tc_size, tc_off, tc_part, tc_arena;
@@ -345,6 +345,18 @@ int prepare_epoch(kdtn_ctx* c, const kdtn_vni_table& vn, uint32_t slice, uint32_
     return KDTN_OK;
 }
 
+// Which batch entries the daemons reach (k_reach; include/kdtn.h): c->f_send (add) and
+// c->f_reach_upd (update) flags of the last run; stamps destination daemons into `mark`.
+int run_reach(kdtn_ctx* c, uint32_t* mark, uint32_t stamp) {
+    const uint32_t nu = c->h_misc[2], na = c->h_misc[3];
+    TRY(ensure(c->f_send, (size_t)na + 16));
+    TRY(ensure(c->f_reach_upd, (size_t)nu + 16));
+    ReachIn r{dp<uint32_t>(c->del_off), dp<uint4>(c->del_res), dp<uint32_t>(c->add_off), dp<uint4>(c->add_res),
+              dp<uint2>(c->add_qdisc), dp<uint32_t>(c->upd_off), dp<uint4>(c->upd_res), c->T, stamp};
+    if (c->T) k_reach<<<nblocks(c->T), BLOCK, 0, c->stream>>>(r, mark, dp<uint8_t>(c->f_send), dp<uint8_t>(c->f_reach_upd));
+    return KDTN_OK;
+}
+
 }  // namespace
 
 // ======================================================================================
@@ -371,7 +383,7 @@ const char* kdtn_err_name(int e) {
                                   "jitter", "loss", "loss_corr", "duplicate", "duplicate_corr",
                                   "reorder_prob", "reorder_corr", "corrupt_prob", "corrupt_corr",
                                   "rate", "peer_lookup", "peer_no_links", "peer_veth_cidr",
-                                  "peer_veth_mac"};
+                                  "peer_veth_mac", "remote_cidr"};
     if (e < 0 || e >= (int)(sizeof(names) / sizeof(names[0]))) return "unknown";
     return names[e];
 }
@@ -441,7 +453,7 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->add_qdisc, &c->upd_qdisc, &c->kd_utf8, &c->pd_utf8, &c->w_rel,
                       &c->w_topo, &c->w_size, &c->w_err, &c->w_off, &c->w_part, &c->w_arena,
                       &c->f_mark, &c->f_send, &c->f_node_idx, &c->f_nodes, &c->f_counts, &c->f_base,
-                      &c->f_part, &c->f_idx, &c->tc_size, &c->tc_off, &c->tc_part, &c->tc_arena,
+                      &c->f_part, &c->f_idx, &c->f_reach_upd, &c->tc_size, &c->tc_off, &c->tc_part, &c->tc_arena,
                       &c->j_doc, &c->j_q, &c->j_bs, &c->j_hb, &c->j_qcnt, &c->j_qoff, &c->j_tok, &c->j_open,
                       &c->j_close, &c->j_tcnt, &c->j_dcnt, &c->j_toff, &c->j_doff, &c->j_toks, &c->j_par,
                       &c->j_role, &c->j_ecls, &c->j_odep, &c->j_ord, &c->j_tagg, &c->j_gagg, &c->j_cnt3, &c->j_coff3, &c->j_small,
@@ -979,7 +991,6 @@ int kdtn_epoch_fanout(kdtn_ctx* c, kdtn_fanout* o) {
     }
     const uint32_t nchunks = nblocks(na, FAN_CHUNK);
     const uint32_t nbd = nblocks(D, SCAN_CHUNK);
-    TRY(ensure(c->f_send, (size_t)na + 16));
     TRY(ensure(c->f_node_idx, (size_t)D * 4));
     TRY(ensure(c->f_nodes, (size_t)FAN_NODE_CAP * 4 + 16));
     TRY(ensure(c->f_part, (size_t)nbd * 8 + 16));
@@ -991,7 +1002,7 @@ int kdtn_epoch_fanout(kdtn_ctx* c, kdtn_fanout* o) {
     c->n_ev = 0;
     (void)hipEventRecord(c->ev[0], s);
     FanIn f{dp<uint32_t>(c->add_off), dp<uint4>(c->add_res), dp<uint2>(c->add_qdisc), T, na, c->f_stamp};
-    if (T) k_fan_mark<<<nblocks(T), BLOCK, 0, s>>>(f, dp<uint32_t>(c->f_mark), dp<uint8_t>(c->f_send));
+    TRY(run_reach(c, dp<uint32_t>(c->f_mark), c->f_stamp));
     k_fan_nodes_count<<<nbd, BLOCK, 0, s>>>(dp<uint32_t>(c->f_mark), D, c->f_stamp, dp<uint64_t>(c->f_part));
     k_scan_top<<<1, BLOCK, 0, s>>>(dp<uint64_t>(c->f_part), nbd);
     k_fan_nodes_write<<<nbd, BLOCK, 0, s>>>(dp<uint32_t>(c->f_mark), D, c->f_stamp, dp<uint64_t>(c->f_part),
@@ -1052,16 +1063,20 @@ int kdtn_epoch_tc(kdtn_ctx* c, uint64_t* n_bytes) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     hipStream_t s = c->stream;
     const uint32_t nu = c->h_misc[2], na = c->h_misc[3];
-    const uint64_t n = (uint64_t)na + nu;
+    const uint64_t n = 2ull * na + nu;                    // command slots: 2 per add entry, 1 per update
+    if (n >= 0xFFFFFFFFull) return KDTN_EINVAL;
     const uint32_t nb = nblocks(n + 1, SCAN_CHUNK);
     TRY(ensure(c->tc_size, (size_t)n * 4 + 16));
     TRY(ensure(c->tc_off, ((size_t)n + 1) * 8));
     TRY(ensure(c->tc_part, (size_t)nb * 8 + 16));
-    TcIn w{c->des.view, dp<uint32_t>(c->add_idx), dp<uint32_t>(c->upd_idx), dp<uint4>(c->add_res),
-           dp<uint4>(c->upd_res), dp<uint2>(c->add_qdisc), dp<uint2>(c->upd_qdisc), dp<uint8_t>(c->kd_bytes),
-           dp<uint32_t>(c->kd_offs), na, nu};
     c->n_ev = 0;
     (void)hipEventRecord(c->ev[0], s);
+    TRY(run_reach(c, nullptr, 0));
+    timer_mark(c, "tc_reach");
+    TcIn w{c->des.view, dp<uint8_t>(c->f_send), dp<uint8_t>(c->f_reach_upd), dp<uint32_t>(c->add_idx),
+           dp<uint32_t>(c->upd_idx), dp<uint4>(c->add_res),
+           dp<uint4>(c->upd_res), dp<uint2>(c->add_qdisc), dp<uint2>(c->upd_qdisc), dp<uint8_t>(c->kd_bytes),
+           dp<uint32_t>(c->kd_offs), na, nu};
     if (n) k_tc_sizes<<<nblocks(n), BLOCK, 0, s>>>(w, dp<uint32_t>(c->tc_size));
     k_scan_partial<<<nb, BLOCK, 0, s>>>(dp<uint32_t>(c->tc_size), (uint32_t)n, dp<uint64_t>(c->tc_part));
     k_scan_top<<<1, BLOCK, 0, s>>>(dp<uint64_t>(c->tc_part), nb);

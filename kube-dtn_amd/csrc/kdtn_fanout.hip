@@ -2,14 +2,15 @@
 //
 // For every AddLinks entry that makes the daemon call UpdateRemote — classified
 // CROSS_NODE (handler.go:419-453), its qdisc built (SetupVxLan → MakeQdiscs,
-// daemon/vxlan/vxlan.go:40, fails before the RPC) and its batch not aborted by an earlier
-// failing link (handler.go:601-607) — the RemotePod RPC goes to the peer's daemon at
+// daemon/vxlan/vxlan.go:40, fails before the RPC) and REACHED: no earlier link of its batch,
+// and no DelLinks entry of its topology, failed (handler.go:601-607,
+// topology_controller.go:93-106) — the RemotePod RPC goes to the peer's daemon at
 // peer status.src_ip (common/utils.go:39-67). The reference sends one RPC per link; this
 // stage groups them per destination daemon, so a caller can send one batch per node:
 // nodes in ascending kdict-id order of their src_ip, entries of a node in add-list order.
 //
-// Kernels: k_fan_mark (one thread per topology: first-error scan, marks senders and their
-// nodes in a stamped D-sized table), k_fan_nodes_* (compaction of marked node ids → dense
+// Kernels: k_reach (one thread per topology: RPC-order first-error scan, marks senders and
+// their nodes in a stamped D-sized table), k_fan_nodes_* (compaction of marked node ids → dense
 // node index), k_fan_count / k_fan_scatter (single-wave workgroups over chunks of 4,096
 // entries: LDS histogram, node-major scan of the (node, chunk) counts, stable scatter).
 #include "kdtn_kernels.h"
@@ -19,7 +20,8 @@ namespace kdtn {
 KD_INLINE bool sends_remote(uint4 r, uint32_t qerr) {
     return (r.w & 0xFFu) == KDTN_KIND_CROSS_NODE && ((r.w >> 8) & 0xFFu) == 0 && qerr == 0;
 }
-// a link whose step fails aborts its batch (addLink's error chain; qdisc only where built)
+// a link whose step fails before its RPC aborts its batch (addLink's error chain; qdisc only
+// where built)
 KD_INLINE bool add_fails(uint4 r, uint32_t qerr) {
     const uint32_t kind = r.w & 0xFFu;
     if ((r.w >> 8) & 0xFFu) return true;
@@ -27,23 +29,42 @@ KD_INLINE bool add_fails(uint4 r, uint32_t qerr) {
 }
 KD_INLINE uint32_t qdisc_err(const uint2* q, uint32_t e) { return (q[(size_t)e * 9 + 8].y >> 16) & 0xFFu; }
 
-__global__ void __launch_bounds__(BLOCK) k_fan_mark(FanIn f, uint32_t* mark, uint8_t* send) {
+// Which entries the daemons reach (include/kdtn.h): one thread per topology walks its
+// DelLinks, AddLinks, UpdateLinks entries in RPC order (topology_controller.go:93-116) and
+// stops at the first failing link (handler.go:601-607, 622-628, 644-662). Writes per add
+// entry REACH_ON | REACH_SEND, per update entry REACH_ON, and (mark != nullptr) stamps the
+// destination daemon of every RemotePod sent.
+__global__ void __launch_bounds__(BLOCK) k_reach(ReachIn f, uint32_t* mark, uint8_t* reach_add, uint8_t* reach_upd) {
     const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
     if (t >= f.T) return;
-    const uint32_t e0 = f.add_off[t], e1 = f.add_off[t + 1];
-    bool aborted = false;
-    for (uint32_t e = e0; e < e1; ++e) {
-        uint8_t s = 0;
-        if (!aborted) {
+    bool ok = true;
+    for (uint32_t e = f.del_off[t], e1 = f.del_off[t + 1]; e < e1 && ok; ++e)
+        if ((f.del_res[e].w >> 8) & 0xFFu) ok = false;                      // delLink error
+    for (uint32_t e = f.add_off[t], e1 = f.add_off[t + 1]; e < e1; ++e) {
+        uint8_t a = 0;
+        if (ok) {
+            a = REACH_ON;
             const uint4 r = f.add_res[e];
             const uint32_t qe = qdisc_err(f.add_qdisc, e);
-            if (add_fails(r, qe)) aborted = true;
-            else if (sends_remote(r, qe)) {
-                s = 1;
-                mark[r.z] = f.stamp;
+            if (add_fails(r, qe)) {
+                ok = false;
+            } else {
+                if (sends_remote(r, qe)) {
+                    a |= REACH_SEND;
+                    if (mark) mark[r.z] = f.stamp;
+                }
+                if (r.w >> 24) ok = false;                                  // remote Update failed
             }
         }
-        send[e] = s;
+        reach_add[e] = a;
+    }
+    for (uint32_t e = f.upd_off[t], e1 = f.upd_off[t + 1]; e < e1; ++e) {
+        uint8_t a = 0;
+        if (ok) {
+            a = REACH_ON;
+            if ((f.upd_res[e].w >> 8) & 0xFFu) ok = false;                  // MakeVeth / MakeQdiscs error
+        }
+        reach_upd[e] = a;
     }
 }
 
@@ -94,7 +115,7 @@ __global__ void __launch_bounds__(64) k_fan_count(FanIn f, const uint8_t* send, 
     __syncthreads();
     const uint32_t c = blockIdx.x, e0 = c * FAN_CHUNK, e1 = min(e0 + FAN_CHUNK, f.n_add);
     for (uint32_t e = e0 + threadIdx.x; e < e1; e += 64)
-        if (send[e]) atomicAdd(&h[node_idx[f.add_res[e].z]], 1u);
+        if (send[e] & REACH_SEND) atomicAdd(&h[node_idx[f.add_res[e].z]], 1u);
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < nn; k += 64) counts[(size_t)k * nchunks + c] = h[k];
 }
@@ -115,7 +136,7 @@ __global__ void __launch_bounds__(64) k_fan_scatter(FanIn f, const uint8_t* send
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     for (uint32_t r = e0; r < e1; r += 64) {
         const uint32_t e = r + lane;
-        const bool on = e < e1 && send[e];
+        const bool on = e < e1 && (send[e] & REACH_SEND);
         const uint32_t node = on ? node_idx[f.add_res[e].z] : 0u;
         uint64_t pending = __ballot(on);
         uint32_t pos = 0;

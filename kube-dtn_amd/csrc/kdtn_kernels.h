@@ -227,6 +227,8 @@ struct WireWork {
 // ---- tc argv synthesis (kdtn_tc.hip) ---------------------------------------------------
 struct TcIn {
     DevLinks N;
+    const uint8_t* reach_add;       // k_reach flags
+    const uint8_t* reach_upd;
     const uint32_t* add_idx;
     const uint32_t* upd_idx;
     const uint4* add_res;
@@ -249,7 +251,19 @@ struct FanIn {
     const uint2* add_qdisc;
     uint32_t T, n_add, stamp;
 };
-__global__ void k_fan_mark(FanIn f, uint32_t* mark, uint8_t* send);
+// which entries the daemons reach (kdtn_fanout.hip k_reach; include/kdtn.h)
+enum : uint8_t { REACH_ON = 1, REACH_SEND = 2 };
+struct ReachIn {
+    const uint32_t* del_off;
+    const uint4* del_res;
+    const uint32_t* add_off;
+    const uint4* add_res;
+    const uint2* add_qdisc;
+    const uint32_t* upd_off;
+    const uint4* upd_res;
+    uint32_t T, stamp;
+};
+__global__ void k_reach(ReachIn f, uint32_t* mark, uint8_t* reach_add, uint8_t* reach_upd);
 __global__ void k_fan_nodes_count(const uint32_t* mark, uint32_t nd, uint32_t stamp, uint64_t* part);
 __global__ void k_fan_nodes_write(const uint32_t* mark, uint32_t nd, uint32_t stamp, const uint64_t* part,
                                   uint32_t* node_idx, uint32_t* nodes, uint32_t* n_nodes);

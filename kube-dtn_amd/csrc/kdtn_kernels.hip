@@ -462,7 +462,7 @@ KD_INLINE uint32_t vni_lookup(const DevTables& tb, uint32_t node, int32_t vni) {
 // ======================================================================================
 // Columns of one link record that the outputs need, loaded together (one round trip).
 struct RecCols {
-    uint32_t lip, lmac, pp;           // local_ip, local_mac, peer_pod (kdict ids)
+    uint32_t lip, lmac, pp, pip;      // local_ip, local_mac, peer_pod, peer_ip (kdict ids)
     uint32_t prop[KDTN_NPROP];        // pdict ids
     uint32_t gap;
     int64_t uid;
@@ -475,6 +475,7 @@ KD_INLINE void load_cols(const DevLinks& L, uint32_t j, bool keys, bool props, R
         c.lip = L.col<NTL>(r, COL_KEY0 + KDTN_K_LOCAL_IP);
         c.lmac = L.col<NTL>(r, COL_KEY0 + KDTN_K_LOCAL_MAC);
         c.pp = L.col<NTL>(r, COL_KEY0 + KDTN_K_PEER_POD);
+        c.pip = L.col<NTL>(r, COL_KEY0 + KDTN_K_PEER_IP);
         c.uid = L.uid_at<NTL>(r, j);
     }
     if (props) {
@@ -625,8 +626,8 @@ KD_INLINE void store_idx(uint32_t* dst, uint32_t v) {
 }
 
 KD_INLINE uint4 pack_res(uint32_t peer, int32_t vni, uint32_t vtep, uint32_t kind, uint32_t err,
-                         uint32_t hit) {
-    return make_uint4(peer, (uint32_t)vni, vtep, kind | (err << 8) | (hit << 16));
+                         uint32_t hit, uint32_t remote_err = 0) {
+    return make_uint4(peer, (uint32_t)vni, vtep, kind | (err << 8) | (hit << 16) | (remote_err << 24));
 }
 
 KD_INLINE bool kbit(const DevTables& tb, int set, uint32_t id) {
@@ -687,7 +688,7 @@ KD_INLINE void emit_upd(const RecCols& c, uint32_t j, const DevTables& tb, const
 struct AddGath {
     PropVals v;
     uint4 slot;                       // direct slot of peer_pod
-    uint32_t lns, kb_ip, kb_mac;
+    uint32_t lns, kb_ip, kb_mac, kb_pip;
 };
 
 template <int V>
@@ -698,6 +699,7 @@ KD_INLINE void add_gather(const RecCols& c, const TopoCtx& tc, const DevTables& 
     g.lns = tc.ns == 0 ? tb.special[SPECIAL_DEFAULT] : tc.ns;                     // :29-31
     g.kb_ip = ldg(tb.kbits + (size_t)KB_CIDR_BAD * tb.kb_words, c.lip >> 5);
     g.kb_mac = ldg(tb.kbits + (size_t)KB_MAC_BAD * tb.kb_words, c.lmac >> 5);
+    g.kb_pip = ldg(tb.kbits + (size_t)KB_CIDR_BAD * tb.kb_words, c.pip >> 5);    // peer end (same / cross node)
     if constexpr ((V & VAR_SKIP_POD) == 0) g.slot = pod_slot<(V & VAR_NT_POD) != 0>(tb, c.pp);
 }
 
@@ -712,7 +714,8 @@ KD_INLINE void add_finish(const RecCols& c, const AddGath& g, const DevLinks& N,
     const int32_t vni = vni_of(tb.vxlan_base, c.uid);
     uint32_t err = ((g.kb_ip >> (c.lip & 31)) & 1u) ? (uint32_t)KDTN_E_VETH_CIDR
                  : ((g.kb_mac >> (c.lmac & 31)) & 1u) ? (uint32_t)KDTN_E_VETH_MAC : 0u;   // :327
-    uint32_t kind = 0, peer = 0xFFFFFFFFu, vtep = 0, hit = 0;
+    uint32_t kind = 0, peer = 0xFFFFFFFFu, vtep = 0, hit = 0, rerr = 0;
+    const bool pip_bad = (g.kb_pip >> (c.pip & 31)) & 1u;
     if (!err) {
         // Reference order: localhost (:333), "physical/" prefix (:348), getPod (:375). The
         // lookup is pure, so it was started first: a hit carries the PHYSICAL bit of the
@@ -740,11 +743,13 @@ KD_INLINE void add_finish(const RecCols& c, const AddGath& g, const DevLinks& N,
                 kind = KDTN_KIND_PEER_DEAD;                                               // :386-395
             } else if (p_src == tc.src) {
                 kind = KDTN_KIND_SAME_NODE;                                               // :399-418
-                err = veth_err(tb, N.key_s<NTL>(KDTN_K_PEER_IP, j), N.key_s<NTL>(KDTN_K_PEER_MAC, j),
-                               KDTN_E_PEER_VETH_CIDR, KDTN_E_PEER_VETH_MAC);
+                err = pip_bad ? (uint32_t)KDTN_E_PEER_VETH_CIDR                         // MakeVeth(peer) :402
+                    : kbit(tb, KB_MAC_BAD, N.key_s<NTL>(KDTN_K_PEER_MAC, j)) ? (uint32_t)KDTN_E_PEER_VETH_MAC : 0u;
             } else {
                 kind = KDTN_KIND_CROSS_NODE;                                              // :419-453
                 vtep = p_src;
+                // the peer daemon's Update parses IntfIp = link.PeerIp (vxlan.go:80-83, utils.go:45)
+                if (pip_bad) rerr = KDTN_E_REMOTE_CIDR;
                 if (tb.vni_mask) {                                       // remote Update check
                     const uint32_t nsx = vni_lookup(tb, p_src, vni);
                     hit = (nsx != 0xFFFFFFFFu && nsx != (ldg(tb.pods, peer).w & 0x7FFFFFFFu));
@@ -752,7 +757,7 @@ KD_INLINE void add_finish(const RecCols& c, const AddGath& g, const DevLinks& N,
             }
         }
     }
-    store_res<V>(out.add_res + e, pack_res(peer, vni, vtep, kind, err, hit));
+    store_res<V>(out.add_res + e, pack_res(peer, vni, vtep, kind, err, hit, rerr));
 }
 
 template <int V>

@@ -8,8 +8,11 @@
 // AddLinks / UpdateLinks entry whose MakeQdiscs produced a TBF and no error, this stage
 // writes that argv (NUL-terminated arguments) for the entry's local interface
 // (link.LocalIntf: the veth of UpdateLinks (handler.go:649-658), the local end of a
-// same-node veth pair or VXLAN interface). Layout: add entries then update entries;
-// entry g's argv = bytes[off[g], off[g+1]) (empty when it runs no tc command).
+// same-node veth pair or VXLAN interface) and, for a same-node veth pair, for the peer end
+// (link.PeerIntf, common/veth.go:53-60). Only entries the daemon reaches (k_reach: no
+// earlier failing link in the topology's Del/Add/Update RPC sequence) run tc. Layout: two
+// command slots per add entry, then one per update entry; slot g's argv =
+// bytes[off[g], off[g+1]) (empty when it runs no tc command).
 #include "kdtn_kernels.h"
 
 namespace kdtn {
@@ -30,10 +33,14 @@ struct TcEntry {
     bool on;
 };
 
+// command slot g: add entry g/2 (even: LocalIntf, odd: PeerIntf of a same-node veth pair),
+// then update entry g - 2*n_add (LocalIntf)
 KD_INLINE TcEntry tc_entry(const TcIn& w, uint32_t g) {
     TcEntry t{0, 0, 0, 0, false};
-    const bool upd = g >= w.n_add;
-    const uint32_t e = upd ? g - w.n_add : g;
+    const bool upd = g >= 2u * w.n_add;
+    const uint32_t e = upd ? g - 2u * w.n_add : g >> 1;
+    const bool peer_end = !upd && (g & 1u);
+    if (((upd ? w.reach_upd : w.reach_add)[e] & REACH_ON) == 0) return t;   // batch aborted earlier
     const uint2* q = (upd ? w.upd_qdisc : w.add_qdisc) + (size_t)e * 9;
     const uint4 r = (upd ? w.upd_res : w.add_res)[e];
     const uint32_t flags = q[8].y;                         // has_netem | has_tbf<<8 | err<<16
@@ -41,9 +48,10 @@ KD_INLINE TcEntry tc_entry(const TcIn& w, uint32_t g) {
     if (!upd) {                        // addLink sets qdiscs only on veth / VXLAN interfaces
         const uint32_t kind = r.w & 0xFFu;
         if (kind != KDTN_KIND_SAME_NODE && kind != KDTN_KIND_CROSS_NODE && kind != KDTN_KIND_PHYSICAL) return t;
+        if (peer_end && kind != KDTN_KIND_SAME_NODE) return t;   // CreateVeth: both ends (veth.go:53-60)
     }
     const uint32_t j = (upd ? w.upd_idx : w.add_idx)[e];
-    t.intf = w.N.key(KDTN_K_LOCAL_INTF, j);
+    t.intf = w.N.key(peer_end ? KDTN_K_PEER_INTF : KDTN_K_LOCAL_INTF, j);
     t.buffer = q[6].y;                                     // kdtn_qdisc word 13
     t.rate = ((uint64_t)q[7].y << 32) | q[7].x;            // words 14, 15
     t.minburst = q[8].x;                                   // word 16
@@ -53,7 +61,7 @@ KD_INLINE TcEntry tc_entry(const TcIn& w, uint32_t g) {
 
 __global__ void __launch_bounds__(BLOCK) k_tc_sizes(TcIn w, uint32_t* size) {
     const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
-    if (g >= w.n_add + w.n_upd) return;
+    if (g >= 2u * w.n_add + w.n_upd) return;
     const TcEntry t = tc_entry(w, g);
     size[g] = t.on ? TC_FIXED + (w.kd_offs[t.intf + 1] - w.kd_offs[t.intf]) + ndigits(t.rate) +
                          ndigits(t.buffer) + ndigits(t.minburst)
@@ -79,7 +87,7 @@ struct Out {
 
 __global__ void __launch_bounds__(BLOCK) k_tc_write(TcIn w, const uint64_t* off, uint8_t* arena) {
     const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
-    if (g >= w.n_add + w.n_upd) return;
+    if (g >= 2u * w.n_add + w.n_upd) return;
     const TcEntry t = tc_entry(w, g);
     if (!t.on) return;
     Out o{arena + off[g]};

@@ -19,10 +19,11 @@ E_LATENCY, E_LATENCY_CORR, E_JITTER, E_LOSS, E_LOSS_CORR = 3, 4, 5, 6, 7
 E_DUPLICATE, E_DUPLICATE_CORR, E_REORDER_PROB, E_REORDER_CORR = 8, 9, 10, 11
 E_CORRUPT_PROB, E_CORRUPT_CORR, E_RATE = 12, 13, 14
 E_PEER_LOOKUP, E_PEER_NO_LINKS, E_PEER_VETH_CIDR, E_PEER_VETH_MAC = 15, 16, 17, 18
+E_REMOTE_CIDR = 19
 ERR_NAMES = ["none", "veth_cidr", "veth_mac", "latency", "latency_corr", "jitter", "loss",
              "loss_corr", "duplicate", "duplicate_corr", "reorder_prob", "reorder_corr",
              "corrupt_prob", "corrupt_corr", "rate", "peer_lookup", "peer_no_links",
-             "peer_veth_cidr", "peer_veth_mac"]
+             "peer_veth_cidr", "peer_veth_mac", "remote_cidr"]
 
 ACT_SKIP, ACT_CREATED, ACT_DIFF = 0, 1, 2
 KIND_NONE, KIND_MACVLAN, KIND_PHYSICAL, KIND_PEER_DEAD, KIND_SAME_NODE, KIND_CROSS_NODE = range(6)
@@ -87,7 +88,7 @@ class Qdisc(C.Structure):
 class Resolved(C.Structure):
     _fields_ = [("peer_topo", C.c_uint32), ("vni", C.c_int32), ("vtep", C.c_uint32),
                 ("kind", C.c_uint8), ("err", C.c_uint8), ("vni_hit", C.c_uint8),
-                ("reserved", C.c_uint8)]
+                ("remote_err", C.c_uint8)]
 
 
 class Batches(C.Structure):
@@ -156,7 +157,7 @@ QDISC_DTYPE = np.dtype([(n, np.uint64 if n == "tbf_rate" else (np.uint8 if n in 
     align=True)
 RESOLVED_DTYPE = np.dtype([("peer_topo", np.uint32), ("vni", np.int32), ("vtep", np.uint32),
                            ("kind", np.uint8), ("err", np.uint8), ("vni_hit", np.uint8),
-                           ("reserved", np.uint8)], align=True)
+                           ("remote_err", np.uint8)], align=True)
 assert QDISC_DTYPE.itemsize == 72 and RESOLVED_DTYPE.itemsize == 16
 
 # symbols include/kdtn.h declares (checked by the CPU test suite)

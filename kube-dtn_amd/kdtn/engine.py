@@ -282,13 +282,15 @@ class Engine:
         _check(lib().kdtn_epoch_download_wire(self._ctx, C.byref(w)), "kdtn_epoch_download_wire")
         return arena[:n], off, err[:self._T]
 
-    def tc_argv(self, n_entries: int):
-        """SetVethQdiscs' `tc ... tbf` argv per add-then-update entry of the last epoch:
-        (arena uint8 of NUL-terminated arguments, off uint64[n_entries + 1])."""
+    def tc_argv(self, n_add: int, n_upd: int):
+        """SetVethQdiscs' `tc ... tbf` argv of the last epoch's reached entries: (arena uint8
+        of NUL-terminated arguments, off uint64[2*n_add + n_upd + 1]); add entry e owns
+        command slots 2e (LocalIntf) and 2e+1 (PeerIntf of a same-node veth pair), update
+        entry u slot 2*n_add + u."""
         n = C.c_uint64()
         _check(lib().kdtn_epoch_tc(self._ctx, C.byref(n)), "kdtn_epoch_tc")
         arena = np.zeros(max(int(n.value), 1), np.uint8)
-        off = np.zeros(n_entries + 1, np.uint64)
+        off = np.zeros(2 * n_add + n_upd + 1, np.uint64)
         t = abi.TcArgv(arena.ctypes.data, arena.size, off.ctypes.data, 0)
         _check(lib().kdtn_epoch_download_tc(self._ctx, C.byref(t)), "kdtn_epoch_download_tc")
         return arena[:int(n.value)], off

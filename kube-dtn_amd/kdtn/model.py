@@ -265,6 +265,9 @@ class KubeDTN:
         qerr = np.where(np.isin(res["kind"], [abi.KIND_SAME_NODE, abi.KIND_CROSS_NODE, abi.KIND_PHYSICAL]),
                         q["err"], 0)
         errs = np.where(res["err"] != 0, res["err"], qerr)
+        # a cross-node link whose RemotePod the peer daemon rejects fails after its local
+        # steps (UpdateRemote's error, handler.go:448-451)
+        errs = np.where(errs != 0, errs, res["remote_err"])
         return self._outcome(res, errs, q)
 
     def del_links(self, local_pod: str, kube_ns: str, links: list[Link]) -> BatchResult:

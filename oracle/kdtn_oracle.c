@@ -863,6 +863,12 @@ int or_reconcile_epoch_timed(const kdtn_epoch_in* in, const or_pods* pods_in, do
                             } else {
                                 r.kind = KDTN_KIND_CROSS_NODE;                       /* :419-453 */
                                 r.vtep = P->src_ip[p];
+                                /* UpdateRemote → peer's Update → SetupVxLan → CreateOrUpdate:
+                                 * net.ParseCIDR(IntfIp = link.PeerIp) (common/utils.go:45,
+                                 * daemon/vxlan/vxlan.go:80-83); its error returns from addLink
+                                 * (handler.go:448-451) after the local steps */
+                                ostr pip = tab_get(KD, N->key[KDTN_K_PEER_IP][j]);
+                                if (pip.n != 0 && !or_parse_cidr(pip.p, pip.n)) r.remote_err = KDTN_E_REMOTE_CIDR;
                                 /* remote Update on the peer's node (:177-179) */
                                 uint32_t kl2 = p_srcip.n + 5, val;
                                 char* k2 = (char*)malloc(kl2);

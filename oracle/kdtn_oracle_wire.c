@@ -198,10 +198,10 @@ uint64_t or_encode_epoch(const kdtn_epoch_in* in, const kdtn_batches* b, uint32_
 }
 
 /* ======================================================================================
- * RemotePod fan-out (daemon/kubedtn/handler.go:419-453, 601-607; common/utils.go:39-67):
- * the AddLinks entries that reach UpdateRemote, grouped by destination daemon
- * (vtep = kdict id of the peer's status.src_ip), daemons in ascending id order, entries
- * in add-list order.
+ * Which entries the daemons reach: Reconcile sends DelLinks, AddLinks, UpdateLinks in that
+ * order and returns at the first failed RPC (controllers/topology_controller.go:93-116);
+ * each handler returns at its first failing link (daemon/kubedtn/handler.go:601-607,
+ * 622-628, 644-662). ra[e] / ru[e]: bit 0 reached, bit 1 (add) sends a RemotePod.
  * ==================================================================================== */
 static int fan_fails(const kdtn_resolved* r, const kdtn_qdisc* q) {
     if (r->err) return 1;
@@ -209,6 +209,41 @@ static int fan_fails(const kdtn_resolved* r, const kdtn_qdisc* q) {
             r->kind == KDTN_KIND_PHYSICAL) && q->err;
 }
 
+static void or_reach(const kdtn_batches* b, uint32_t T, uint8_t* ra, uint8_t* ru) {
+    for (uint32_t t = 0; t < T; t++) {
+        int ok = 1;
+        for (uint32_t e = b->del_off[t]; e < b->del_off[t + 1] && ok; e++)
+            if (b->del_res[e].err) ok = 0;                                  /* delLink :470-474 */
+        for (uint32_t e = b->add_off[t]; e < b->add_off[t + 1]; e++) {
+            uint8_t a = 0;
+            if (ok) {
+                const kdtn_resolved* r = &b->add_res[e];
+                a = 1;
+                if (fan_fails(r, &b->add_qdisc[e])) ok = 0;
+                else {
+                    if (r->kind == KDTN_KIND_CROSS_NODE) a |= 2;               /* UpdateRemote :448 */
+                    if (r->remote_err) ok = 0;                                  /* :449-451 */
+                }
+            }
+            ra[e] = a;
+        }
+        for (uint32_t e = b->upd_off[t]; e < b->upd_off[t + 1]; e++) {
+            uint8_t a = 0;
+            if (ok) {
+                a = 1;
+                if (b->upd_res[e].err) ok = 0;                                  /* :649-657 */
+            }
+            ru[e] = a;
+        }
+    }
+}
+
+/* ======================================================================================
+ * RemotePod fan-out (daemon/kubedtn/handler.go:419-453, 601-607; common/utils.go:39-67):
+ * the AddLinks entries that reach UpdateRemote, grouped by destination daemon
+ * (vtep = kdict id of the peer's status.src_ip), daemons in ascending id order, entries
+ * in add-list order.
+ * ==================================================================================== */
 static int cmp_u64(const void* a, const void* b) {
     uint64_t x = *(const uint64_t*)a, y = *(const uint64_t*)b;
     return x < y ? -1 : x > y;
@@ -217,17 +252,16 @@ static int cmp_u64(const void* a, const void* b) {
 uint32_t or_fanout(const kdtn_batches* b, uint32_t T, uint32_t* node, uint32_t* off, uint32_t* idx,
                    uint32_t* n_nodes) {
     /* senders as (vtep << 32 | entry), sorted: stable by entry within a vtep */
-    uint32_t na = b->add_off[T];
+    uint32_t na = b->add_off[T], nu = b->upd_off[T];
     uint64_t* keys = (uint64_t*)malloc(sizeof(uint64_t) * (na ? na : 1));
+    uint8_t* ra = (uint8_t*)malloc(na + 1);
+    uint8_t* ru = (uint8_t*)malloc(nu + 1);
+    or_reach(b, T, ra, ru);
     uint32_t ns = 0;
-    for (uint32_t t = 0; t < T; t++) {
-        for (uint32_t e = b->add_off[t]; e < b->add_off[t + 1]; e++) {
-            const kdtn_resolved* r = &b->add_res[e];
-            const kdtn_qdisc* q = &b->add_qdisc[e];
-            if (fan_fails(r, q)) break;                       /* the batch aborts here */
-            if (r->kind == KDTN_KIND_CROSS_NODE) keys[ns++] = ((uint64_t)r->vtep << 32) | e;
-        }
-    }
+    for (uint32_t e = 0; e < na; e++)
+        if (ra[e] & 2) keys[ns++] = ((uint64_t)b->add_res[e].vtep << 32) | e;
+    free(ra);
+    free(ru);
     qsort(keys, ns, sizeof(uint64_t), cmp_u64);
     uint32_t nn = 0;
     for (uint32_t k = 0; k < ns; k++) {
@@ -248,12 +282,13 @@ uint32_t or_fanout(const kdtn_batches* b, uint32_t T, uint32_t* node, uint32_t* 
 /* ======================================================================================
  * tc argv of SetVethQdiscs' TBF (common/qdisc.go:252-266): "qdisc add dev <intf> parent
  * 1:1 handle 10:0 tbf rate <Rate> burst <Buffer> latency 50ms minburst <Minburst>", each
- * argument NUL-terminated, for every add entry that reaches SetVethQdiscs (veth / VXLAN
- * kinds) and every update entry, with a TBF and no error. Add entries then update entries.
+ * argument NUL-terminated, for every REACHED add entry that calls SetVethQdiscs (veth /
+ * VXLAN kinds; both ends of a same-node veth pair) and every REACHED update entry, with a
+ * TBF and no error.
  * ==================================================================================== */
-static uint64_t tc_one(const kdtn_epoch_in* in, uint32_t j, const kdtn_qdisc* q, uint8_t* out) {
+static uint64_t tc_one(const kdtn_epoch_in* in, uint32_t j, int col, const kdtn_qdisc* q, uint8_t* out) {
     char tmp[256];
-    wstr intf = wget(&in->kdict, in->desired.key[KDTN_K_LOCAL_INTF][j]);
+    wstr intf = wget(&in->kdict, in->desired.key[col][j]);
     int n1 = snprintf(tmp, sizeof tmp, "qdisc%cadd%cdev%c", 0, 0, 0);
     uint64_t pos = 0;
     if (out) memcpy(out, tmp, (size_t)n1);
@@ -268,22 +303,35 @@ static uint64_t tc_one(const kdtn_epoch_in* in, uint32_t j, const kdtn_qdisc* q,
 }
 
 uint64_t or_tc_epoch(const kdtn_epoch_in* in, const kdtn_batches* b, uint8_t* bytes, uint64_t* off) {
+    /* command slots: add entry e → 2e (LocalIntf), 2e+1 (PeerIntf of a same-node veth pair,
+     * common/veth.go:53-60); update entry u → 2*n_add + u (LocalIntf) */
+    const uint32_t T = in->topos.n;
+    uint8_t* ra = (uint8_t*)malloc(b->n_add + 1);
+    uint8_t* ru = (uint8_t*)malloc(b->n_upd + 1);
+    or_reach(b, T, ra, ru);
     uint64_t pos = 0;
     uint32_t g = 0;
-    for (int upd = 0; upd < 2; upd++) {
-        uint32_t n = upd ? b->n_upd : b->n_add;
-        for (uint32_t e = 0; e < n; e++, g++) {
-            off[g] = pos;
-            const kdtn_resolved* r = upd ? &b->upd_res[e] : &b->add_res[e];
-            const kdtn_qdisc* q = upd ? &b->upd_qdisc[e] : &b->add_qdisc[e];
-            if (!q->has_tbf || q->err || r->err) continue;
-            if (!upd && r->kind != KDTN_KIND_SAME_NODE && r->kind != KDTN_KIND_CROSS_NODE &&
-                r->kind != KDTN_KIND_PHYSICAL)
-                continue;
-            uint32_t j = upd ? b->upd_idx[e] : b->add_idx[e];
-            pos += tc_one(in, j, q, bytes ? bytes + pos : NULL);
-        }
+    for (uint32_t e = 0; e < b->n_add; e++) {
+        const kdtn_resolved* r = &b->add_res[e];
+        const kdtn_qdisc* q = &b->add_qdisc[e];
+        const int on = (ra[e] & 1) && q->has_tbf && !q->err && !r->err &&
+                       (r->kind == KDTN_KIND_SAME_NODE || r->kind == KDTN_KIND_CROSS_NODE ||
+                        r->kind == KDTN_KIND_PHYSICAL);
+        off[g++] = pos;
+        if (on) pos += tc_one(in, b->add_idx[e], KDTN_K_LOCAL_INTF, q, bytes ? bytes + pos : NULL);
+        off[g++] = pos;
+        if (on && r->kind == KDTN_KIND_SAME_NODE)
+            pos += tc_one(in, b->add_idx[e], KDTN_K_PEER_INTF, q, bytes ? bytes + pos : NULL);
+    }
+    for (uint32_t e = 0; e < b->n_upd; e++) {
+        const kdtn_resolved* r = &b->upd_res[e];
+        const kdtn_qdisc* q = &b->upd_qdisc[e];
+        off[g++] = pos;
+        if ((ru[e] & 1) && q->has_tbf && !q->err && !r->err)
+            pos += tc_one(in, b->upd_idx[e], KDTN_K_LOCAL_INTF, q, bytes ? bytes + pos : NULL);
     }
     off[g] = pos;
+    free(ra);
+    free(ru);
     return pos;
 }

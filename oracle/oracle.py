@@ -221,7 +221,8 @@ def fanout(out: BatchesOut, T: int):
 
 
 def tc_epoch(inp: EpochInput, out: BatchesOut):
-    """tc argv arena (uint8) and per-entry offsets (uint64, add then update entries)."""
+    """tc argv arena (uint8) and command-slot offsets (uint64): two slots per add entry
+    (LocalIntf, PeerIntf of a same-node veth pair), then one per update entry."""
     L = _wire_lib()
     if not getattr(L, "_tc_bound", False):
         L.or_tc_epoch.argtypes = [C.POINTER(abi.EpochIn), C.POINTER(abi.Batches), C.c_void_p, C.c_void_p]
@@ -230,7 +231,7 @@ def tc_epoch(inp: EpochInput, out: BatchesOut):
     cin = inp.to_c()
     b = out.to_c((max(len(out.del_idx), 1), max(len(out.add_idx), 1), max(len(out.upd_idx), 1)))
     b.n_del, b.n_add, b.n_upd = len(out.del_idx), len(out.add_idx), len(out.upd_idx)
-    off = np.zeros(len(out.add_idx) + len(out.upd_idx) + 1, np.uint64)
+    off = np.zeros(2 * len(out.add_idx) + len(out.upd_idx) + 1, np.uint64)
     n = L.or_tc_epoch(C.byref(cin), C.byref(b), None, off.ctypes.data)
     arena = np.zeros(max(int(n), 1), np.uint8)
     L.or_tc_epoch(C.byref(cin), C.byref(b), arena.ctypes.data, off.ctypes.data)

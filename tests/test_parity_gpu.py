@@ -412,7 +412,27 @@ def test_tc_argv_synthesis(engine):
     cases += [synth.make(1), synth.make(2, pods_per_shard=20000), synth.make(3, pods_per_shard=20000)]
     for k, inp in enumerate(cases):
         out = engine.reconcile(inp)
-        arena, off = engine.tc_argv(len(out.add_idx) + len(out.upd_idx))
+        arena, off = engine.tc_argv(len(out.add_idx), len(out.upd_idx))
         wa, wo = O.tc_epoch(inp, O.reconcile(inp, tick=TICK))
         assert np.array_equal(off, wo), k
         assert arena.tobytes() == wa.tobytes(), k
+
+
+def test_reach_rule_scenario_and_error_heavy_epochs(engine):
+    """Batch-abort rule across the DelLinks → AddLinks → UpdateLinks RPC sequence, remote
+    rejection of a RemotePod (peer_ip without a mask) and both veth ends of a same-node pair:
+    fan-out and tc argv equal the oracle on a hand-built scenario and on error-heavy random
+    epochs; resolve records carry remote_err exactly as the oracle."""
+    from test_reach_cpu import scenario
+    cases = [pack(scenario())] + [random_epoch_input(s, T=150, p_err=0.4)[1] for s in (31, 32, 33)]
+    for k, inp in enumerate(cases):
+        ora = O.reconcile(inp, tick=TICK)
+        out = engine.reconcile(inp)
+        assert_same(out, ora, f"case {k}")
+        node, off, idx = engine.fanout()
+        wn, wo, wi = O.fanout(ora, inp.topos.n)
+        assert np.array_equal(node, wn) and np.array_equal(off, wo) and np.array_equal(idx, wi), k
+        arena, toff = engine.tc_argv(len(out.add_idx), len(out.upd_idx))
+        wa, wto = O.tc_epoch(inp, ora)
+        assert np.array_equal(toff, wto) and arena.tobytes() == wa.tobytes(), k
+    assert (ora.add_res["remote_err"] == abi.E_REMOTE_CIDR).any()
