@@ -452,9 +452,36 @@ int kdtn_json_ingest(kdtn_ctx* ctx, const kdtn_vni_table* vnis, kdtn_ingest_info
 /* D2H of the decoded tables of the last successful ingest. */
 int kdtn_ingest_download(kdtn_ctx* ctx, kdtn_ingest_tables* out);
 
-/* ---- multi-GPU (one process per GPU): RCCL all-gather of the pod-status table ------ */
+/* ---- multi-GPU (one process per GPU) ---------------------------------------------------- */
+/* Owner shard of a Topology: hash64(namespace ‖ "/" ‖ name) mod nshards (SURVEY.md §8(e);
+ * the key is the informer's object key, cache.MetaNamespaceKeyFunc). A controller routes
+ * each Topology (both its spec and status links) to the context of rank
+ * kdtn_topology_shard(...), keeping informer order within a shard, so CalcDiff, resolve and
+ * MakeQdiscs are shard-local; the batches of the shards are disjoint sets of Topologies.
+ * Host-only: no GPU call. */
+uint32_t kdtn_topology_shard(const uint8_t* ns, uint32_t ns_len, const uint8_t* name, uint32_t name_len,
+                             uint32_t nshards);
+
+/* The one exchange: peer resolution (getPod + ToProtoPod, daemon/kubedtn/handler.go:375-399)
+ * needs the pod-status row of every Topology of every shard. Rank r's topologies occupy the
+ * global pod indices [r*pod_slice, r*pod_slice + T_r) — kdtn_resolved.peer_topo is such an
+ * index — so every rank uploads the same kdtn_epoch_in.pod_slice (>= its T) and uses the
+ * same kdict ids for pod names, namespaces, src_ip and net_ns strings (one shared
+ * interner prefix). Transports:
+ *   RCCL (production): kdtn_comm_init; kdtn_epoch_run all-gathers the rows over xGMI on a
+ *     comm stream, overlapped with the dictionary parses.
+ *   host (any collective library, e.g. gloo): kdtn_comm_set_ranks; per epoch, after
+ *     kdtn_epoch_upload: kdtn_pods_export → all-gather of pod_slice rows per rank in rank
+ *     order → kdtn_pods_import → kdtn_epoch_run (KDTN_EINVAL if the import is missing). */
+typedef struct kdtn_pod_row {
+    uint32_t ns, name, src_ip;  /* kdict ids; padding rows (T_r <= i < pod_slice) have ns = name = ~0 */
+    uint32_t net_ns_nil;        /* kdict id of status.net_ns | KDTN_TOPO_SPEC_NIL-derived bit 31   */
+} kdtn_pod_row;
 int kdtn_comm_unique_id(uint8_t out[128]);
 int kdtn_comm_init(kdtn_ctx* ctx, const uint8_t unique_id[128], int nranks, int rank);
+int kdtn_comm_set_ranks(kdtn_ctx* ctx, int nranks, int rank);          /* host transport */
+int kdtn_pods_export(kdtn_ctx* ctx, kdtn_pod_row* rows);                /* [pod_slice] rows */
+int kdtn_pods_import(kdtn_ctx* ctx, const kdtn_pod_row* rows, uint64_t n);   /* n = pod_slice*nranks */
 
 /* ---- profiling hooks: per-kernel HIP-event times of the last epoch_run (ms) -------- */
 int kdtn_last_kernel_times(kdtn_ctx* ctx, const char** names, float* ms, int cap);

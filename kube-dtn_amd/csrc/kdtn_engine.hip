@@ -114,6 +114,7 @@ struct kdtn_ctx {
     // multi-GPU
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
+    bool pods_imported = false;   // host transport: this epoch's global pod table is in place
     // timers
     hipEvent_t ev[kMaxTimers + 1] = {};
     const char* ev_name[kMaxTimers] = {};
@@ -533,6 +534,7 @@ int kdtn_epoch_upload(kdtn_ctx* c, const kdtn_epoch_in* in) {
     HIP_TRY(hipStreamSynchronize(c->stream));   // host arrays may be released after return
     c->uploaded = true;
     c->ran = false;
+    c->pods_imported = false;
     return KDTN_OK;
 }
 
@@ -550,8 +552,14 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
 
     const DevTopos T = topo_view(c);
     const bool resolve = stages & KDTN_STAGE_RESOLVE;
-    const bool exchange = resolve && c->nranks > 1;
-    if (resolve) {
+    const bool host_xchg = resolve && c->nranks > 1 && !c->comm;      // rows imported by the caller
+    const bool exchange = resolve && c->nranks > 1 && c->comm;
+    if (host_xchg && !c->pods_imported) {
+        std::snprintf(g_last_error, sizeof(g_last_error),
+                      "host transport: kdtn_pods_import the gathered pod table before kdtn_epoch_run");
+        return KDTN_EINVAL;
+    }
+    if (resolve && !host_xchg) {
         // pod-status rows first: across ranks they are all-gathered over RCCL on the comm
         // stream while this stream parses the dictionaries (the exchange needs neither)
         const uint32_t rank_base = c->slice * (uint32_t)c->rank;
@@ -568,6 +576,8 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
             }
             HIP_TRY(hipEventRecord(c->ev_ag, c->comm_stream));
         }
+        timer_mark(c, "pods_fill");
+    } else if (resolve) {
         timer_mark(c, "pods_fill");
     }
     // dictionaries
@@ -1565,6 +1575,47 @@ int kdtn_comm_init(kdtn_ctx* c, const uint8_t uid[128], int nranks, int rank) {
         c->rank = 0;
         return KDTN_EIO;
     }
+    return KDTN_OK;
+}
+
+int kdtn_comm_set_ranks(kdtn_ctx* c, int nranks, int rank) {
+    if (!c || nranks < 1 || rank < 0 || rank >= nranks) return KDTN_EINVAL;
+    HIP_TRY(hipSetDevice(c->device));
+    if (c->comm) {
+        (void)ncclCommDestroy(c->comm);
+        c->comm = nullptr;
+    }
+    c->nranks = nranks;
+    c->rank = rank;
+    c->uploaded = false;
+    c->pods_imported = false;
+    return KDTN_OK;
+}
+
+int kdtn_pods_export(kdtn_ctx* c, kdtn_pod_row* rows) {
+    if (!c || !c->uploaded || (c->slice && !rows)) return KDTN_EINVAL;
+    HIP_TRY(hipSetDevice(c->device));
+    const uint32_t rank_base = c->slice * (uint32_t)c->rank;
+    uint4* pods = dp<uint4>(c->pods);
+    if (c->slice) {
+        k_pods_fill<<<nblocks(c->slice), BLOCK, 0, c->stream>>>(topo_view(c), c->slice, rank_base, pods);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(rows, pods + rank_base, (size_t)c->slice * 16, hipMemcpyDeviceToHost, c->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return KDTN_OK;
+}
+
+int kdtn_pods_import(kdtn_ctx* c, const kdtn_pod_row* rows, uint64_t n) {
+    if (!c || !c->uploaded || n != c->pod_total || (n && !rows)) {
+        if (c) std::snprintf(g_last_error, sizeof(g_last_error), "kdtn_pods_import: %llu rows, expected pod_slice*nranks = %u",
+                             (unsigned long long)n, c->pod_total);
+        return KDTN_EINVAL;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    if (n) HIP_TRY(hipMemcpyAsync(c->pods.p, rows, (size_t)n * 16, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->pods_imported = true;
     return KDTN_OK;
 }
 

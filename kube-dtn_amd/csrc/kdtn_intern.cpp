@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "../../include/kdtn.h"
+#include "kdtn_shard.h"
 
 namespace {
 uint64_t fnv(const uint8_t* p, size_t n) {
@@ -97,3 +98,8 @@ int kdtn_interner_table(const kdtn_interner* it, kdtn_strtab* out) {
 }
 
 }  // extern "C"
+
+extern "C" uint32_t kdtn_topology_shard(const uint8_t* ns, uint32_t ns_len, const uint8_t* name,
+                                        uint32_t name_len, uint32_t nshards) {
+    return kdtn::topology_shard(ns, ns_len, name, name_len, nshards);
+}

@@ -14,19 +14,27 @@
 //   config 4  WAN twin: sites in namespaces of 100, power-law degrees (Chung-Lu inside a
 //             namespace, hubs ≈1000 links), 256 nodes, 1 % physical/ and 0.5 % localhost
 //             peers; realised empty → AddLinks, resolution-dominated.
-// Sharding: global pod p belongs to shard p / T_local (contiguous blocks, pod_slice =
-// T_local). Pod names, namespaces, node IPs and netns strings carry GLOBAL ids (a shared
-// dictionary prefix identical on every shard); per-link strings get shard-local ids.
+// Sharding (configs 2-4): "hash" (the engine's) gives pod p to shard
+// kdtn_topology_shard(namespace, name, G) = hash64(namespace/name) mod G, the shard's pods in
+// ascending p; pod_slice = the largest shard's pod count (every rank uses the same) and
+// pod_base = shard * pod_slice, so the engine's global pod index of the shard's t-th pod is
+// pod_base + t ("t_gid" maps it back to p). "block" (legacy) gives shard k the contiguous
+// pods [k*pods_per_shard, (k+1)*pods_per_shard). Pod names, namespaces, node IPs and netns
+// strings carry GLOBAL ids (a shared dictionary prefix identical on every shard); per-link
+// strings get shard-local ids.
 #include <cstdint>
 #include <cstdio>
 #include <cmath>
 #include <cstring>
+#include <algorithm>
+#include <array>
 #include <string>
 #include <thread>
 #include <unordered_map>
 #include <vector>
 
 #include "../../include/kdtn.h"
+#include "kdtn_shard.h"
 
 namespace {
 
@@ -135,6 +143,17 @@ struct Synth {
     std::vector<uint32_t> v_node, v_netns;
     std::vector<int32_t> v_vni;
     uint32_t pod_slice = 0, pod_base = 0, total_pods = 0;
+    std::vector<uint32_t> owned;      // global pod ids of this shard, ascending ("t_gid")
+    std::vector<uint32_t> local_of;   // global pod id → local topology index (~0: other shard)
+    // config 3 churn sequence: per desired record its global edge id, side and props version
+    struct Churn {
+        bool on = false;
+        uint64_t seed = 0, total = 0, n_edges = 0, q_next = 0;
+        uint32_t epoch = 0;
+        std::vector<uint64_t> edge;
+        std::vector<uint8_t> side;
+        std::vector<uint32_t> ver;
+    } ch;
     // global-id bases of the shared dictionary prefix
     uint32_t id_default = 0, id_node0 = 0, id_name0 = 0, id_netns0 = 0, id_ns0 = 0;
     uint32_t n_nodes = 0;
@@ -231,6 +250,33 @@ void shared_prefix(Synth& S, uint32_t total_pods, uint32_t n_nodes, uint32_t n_n
     S.total_pods = total_pods;
 }
 
+// Which pods this shard owns (see the header comment). ns_id(p) is the kdict id of pod p's
+// namespace; names are the shared-prefix strings id_name0 + p.
+template <typename NsOf>
+void assign_shard(Synth& S, uint64_t total, uint32_t pods_per_shard, uint32_t shard, uint32_t nshards,
+                  bool hash, NsOf ns_id) {
+    S.local_of.assign(total, 0xFFFFFFFFu);
+    if (!hash) {
+        S.pod_slice = pods_per_shard;
+        S.pod_base = shard * pods_per_shard;
+        for (uint64_t p = S.pod_base; p < S.pod_base + (uint64_t)pods_per_shard && p < total; ++p) S.owned.push_back((uint32_t)p);
+    } else {
+        std::vector<uint32_t> cnt(nshards, 0);
+        for (uint64_t p = 0; p < total; ++p) {
+            const uint32_t ns = ns_id(p), nm = S.id_name0 + (uint32_t)p;
+            const uint32_t r = kdtn::topology_shard(S.kd.bytes.data() + S.kd.offs[ns], S.kd.offs[ns + 1] - S.kd.offs[ns],
+                                                    S.kd.bytes.data() + S.kd.offs[nm], S.kd.offs[nm + 1] - S.kd.offs[nm],
+                                                    nshards);
+            ++cnt[r];
+            if (r == shard) S.owned.push_back((uint32_t)p);
+        }
+        S.pod_slice = 0;
+        for (uint32_t c : cnt) S.pod_slice = std::max(S.pod_slice, c);
+        S.pod_base = shard * S.pod_slice;
+    }
+    for (uint32_t t = 0; t < S.owned.size(); ++t) S.local_of[S.owned[t]] = t;
+}
+
 void push_topo(Synth& S, uint32_t p, uint32_t ns_id, bool dead, uint32_t node, uint8_t flags) {
     S.t_ns.push_back(ns_id);
     S.t_name.push_back(S.id_name0 + p);
@@ -270,6 +316,7 @@ void build_config1(Synth& S) {
     Props empty;
     S.pod_slice = T;
     S.pod_base = 0;
+    for (uint32_t p = 0; p < T; ++p) S.owned.push_back(p);
     for (uint32_t p = 0; p < T; ++p) {
         push_topo(S, p, S.id_default, false, p % 64, 0);
         for (auto [e, side] : adj[p]) {
@@ -305,41 +352,117 @@ struct RegularGraph {
     }
 };
 
-void build_config23(Synth& S, int config, uint64_t seed, uint32_t pods_per_shard, uint32_t degree,
-                    uint32_t n_nodes, double dead_frac, uint32_t shard, uint32_t nshards) {
-    const uint64_t total = (uint64_t)pods_per_shard * nshards;
-    shared_prefix(S, (uint32_t)total, n_nodes, 0, "p%u");
-    RegularGraph G(total, degree, seed);
-    const uint64_t n_edges = G.stubs / 2;
-    S.pod_slice = pods_per_shard;
-    S.pod_base = shard * pods_per_shard;
-    auto is_dead = [&](uint64_t p) { return (double)(hmix(seed ^ 0xDEADull, p) >> 11) * (1.0 / 9007199254740992.0) < dead_frac; };
-    auto node_of = [&](uint64_t p) { return (uint32_t)(hmix(seed ^ 0x40DEull, p) % n_nodes); };
-    // churn decisions per edge (config 3): 0 keep, 1 delete, 2 re-draw props
-    auto churn = [&](uint64_t e) -> int {
-        double u = (double)(hmix(seed ^ 0xC4124ull, e) >> 11) * (1.0 / 9007199254740992.0);
+// ---- config 3: churn epochs ---------------------------------------------------------------
+// One reconcile epoch of SURVEY §8(d) config 3: realised := the previous desired; each
+// alive edge is deleted (both records) with p = 1/60 or gets new props (both records) with
+// p = 1/60, decided by hash(seed, epoch, edge) so every shard agrees; n_edges/60 fresh edges
+// (new uid, random endpoints, both records appended to their pods' lists) are added. About
+// 5 % of the edges churn per epoch: ≈ 167k del, 167k upd and 167k add records at 10M links.
+// Status order = the previous spec order; kept records keep their positions. New strings
+// (a fresh edge's IPs and interface names) are unique, so they are appended to the key
+// dictionary without a lookup: every epoch's kdict extends the previous one.
+void churn_advance(Synth& S) {
+    auto& C = S.ch;
+    C.epoch++;
+    const uint64_t seed = C.seed, total = C.total;
+    auto decide = [&](uint64_t e) -> int {
+        const double u = (double)(hmix(hmix(seed ^ 0xC4124ull, C.epoch), e) >> 11) * (1.0 / 9007199254740992.0);
         return u < 1.0 / 60 ? 1 : (u < 2.0 / 60 ? 2 : 0);
     };
-    // added edges (config 3): global list, each shard keeps those touching its pods
-    std::vector<std::vector<std::pair<uint64_t, uint32_t>>> added;  // per local pod: (new edge, side)
-    std::vector<std::pair<uint64_t, uint64_t>> new_edges;
-    if (config == 3) {
-        added.resize(pods_per_shard);
-        const uint64_t n_new = n_edges / 60;   // 1/60 of the edges added: 5 % churn split 3 ways
-        Rng r(seed ^ 0xADDull);
-        for (uint64_t q = 0; q < n_new; ++q) {
-            uint64_t a = r.next() % total, b = r.next() % total;
-            new_edges.push_back({a, b});
-            if (a / pods_per_shard == shard) added[a - S.pod_base].push_back({q, 0});
-            if (b / pods_per_shard == shard) added[b - S.pod_base].push_back({q, 1});
-        }
+    S.real = std::move(S.des);
+    S.des = Links();
+    std::vector<uint64_t> r_edge = std::move(C.edge);
+    std::vector<uint8_t> r_side = std::move(C.side);
+    std::vector<uint32_t> r_ver = std::move(C.ver);
+    C.edge.clear();
+    C.side.clear();
+    C.ver.clear();
+    S.t_roff = S.t_noff;
+    S.t_noff.assign(1, 0u);
+    const uint64_t n_new = C.n_edges / 60;
+    std::vector<std::vector<std::pair<uint64_t, uint32_t>>> added(S.owned.size());   // (q, side)
+    std::vector<uint64_t> peer_of(n_new * 2);
+    Rng r(hmix(seed ^ 0xADDull, C.epoch));
+    for (uint64_t k = 0; k < n_new; ++k) {
+        const uint64_t a = r.next() % total;
+        uint64_t b = r.next() % total;
+        if (b == a) b = (b + 1) % total;
+        peer_of[2 * k] = b;
+        peer_of[2 * k + 1] = a;
+        if (S.local_of[a] != 0xFFFFFFFFu) added[S.local_of[a]].push_back({k, 0});
+        if (S.local_of[b] != 0xFFFFFFFFu) added[S.local_of[b]].push_back({k, 1});
     }
+    auto copy_rec = [&](uint32_t i, const Props* np) {
+        for (int k = 0; k < 7; ++k) S.des.key[k].push_back(S.real.key[k][i]);
+        S.des.uid.push_back(S.real.uid[i]);
+        if (np) {
+            for (int k = 0; k < 12; ++k) S.des.prop[k].push_back(np->s[k].empty() ? 0u : S.pd.intern(np->s[k]));
+            S.des.gap.push_back(np->gap);
+        } else {
+            for (int k = 0; k < 12; ++k) S.des.prop[k].push_back(S.real.prop[k][i]);
+            S.des.gap.push_back(S.real.gap[i]);
+        }
+    };
+    // a fresh edge's strings, interned once per shard (both of its records may be local)
+    std::unordered_map<uint64_t, std::array<uint32_t, 4>> fresh;
+    auto fresh_ids = [&](uint64_t q, uint64_t e) -> const std::array<uint32_t, 4>& {
+        auto it = fresh.find(q);
+        if (it != fresh.end()) return it->second;
+        std::array<uint32_t, 4> v{S.kd.append_unique(num("nx", q, "-a")), S.kd.append_unique(num("nx", q, "-b")),
+                                  S.kd.append_unique(ip4((uint32_t)(2 * e))), S.kd.append_unique(ip4((uint32_t)(2 * e + 1)))};
+        return fresh.emplace(q, v).first->second;
+    };
+    for (uint32_t t = 0; t < S.owned.size(); ++t) {
+        for (uint32_t i = S.t_roff[t]; i < S.t_roff[t + 1]; ++i) {
+            const uint64_t e = r_edge[i];
+            const int c = decide(e);
+            if (c == 1) continue;                                       // deleted edge
+            uint32_t ver = r_ver[i];
+            if (c == 2) {
+                ++ver;
+                const Props np = draw_props(seed, e + 1, ver);
+                copy_rec(i, &np);
+            } else {
+                copy_rec(i, nullptr);
+            }
+            C.edge.push_back(e);
+            C.side.push_back(r_side[i]);
+            C.ver.push_back(ver);
+        }
+        for (auto [k, side] : added[t]) {
+            const uint64_t q = C.q_next + k, e = C.n_edges + q;
+            const auto& f = fresh_ids(q, e);
+            uint32_t key[7];
+            key[0] = f[side];
+            key[1] = f[2 + side];
+            key[2] = 0;
+            key[3] = f[side ^ 1];
+            key[4] = f[2 + (side ^ 1)];
+            key[5] = 0;
+            key[6] = S.id_name0 + (uint32_t)peer_of[2 * k + side];
+            push_link(S, S.des, key, (int64_t)(e + 1), draw_props(seed, e + 1, 0));
+            C.edge.push_back(e);
+            C.side.push_back((uint8_t)side);
+            C.ver.push_back(0);
+        }
+        S.t_noff.push_back((uint32_t)S.des.size());
+    }
+    C.q_next += n_new;
+}
+
+void build_config23(Synth& S, int config, uint64_t seed, uint64_t total, uint32_t pods_per_shard, uint32_t degree,
+                    uint32_t n_nodes, double dead_frac, uint32_t shard, uint32_t nshards, bool hash) {
+    shared_prefix(S, (uint32_t)total, n_nodes, 0, "p%u");
+    assign_shard(S, total, pods_per_shard, shard, nshards, hash, [&](uint64_t) { return S.id_default; });
+    RegularGraph G(total, degree, seed);
+    const uint64_t n_edges = G.stubs / 2;
+    auto is_dead = [&](uint64_t p) { return (double)(hmix(seed ^ 0xDEADull, p) >> 11) * (1.0 / 9007199254740992.0) < dead_frac; };
+    auto node_of = [&](uint64_t p) { return (uint32_t)(hmix(seed ^ 0x40DEull, p) % n_nodes); };
     Props empty;
-    for (uint64_t lp = 0; lp < pods_per_shard; ++lp) {
-        const uint64_t p = S.pod_base + lp;
+    for (uint64_t lp = 0; lp < S.owned.size(); ++lp) {
+        const uint64_t p = S.owned[lp];
         const bool dead = is_dead(p);
         push_topo(S, (uint32_t)p, S.id_default, dead, node_of(p), 0);
-        uint32_t kept_pos = 0;
         for (uint32_t k = 0; k < degree; ++k) {
             uint64_t other, e;
             uint32_t side;
@@ -354,47 +477,32 @@ void build_config23(Synth& S, int config, uint64_t seed, uint32_t pods_per_shard
             key[4] = S.kd.intern(ip4((uint32_t)(2 * e + (side ^ 1))));
             key[5] = 0;
             key[6] = S.id_name0 + (uint32_t)peer;
-            const Props pr = draw_props(seed, e + 1, 0);
-            if (config == 2) {
-                push_link(S, S.des, key, (int64_t)(e + 1), pr);
-            } else {
-                push_link(S, S.real, key, (int64_t)(e + 1), pr);
-                const int c = churn(e);
-                if (c == 1) continue;
-                push_link(S, S.des, key, (int64_t)(e + 1), c == 2 ? draw_props(seed, e + 1, 1) : pr);
-            }
-            ++kept_pos;
-        }
-        if (config == 3) {
-            uint32_t extra = 0;
-            for (auto [q, side] : added[lp]) {
-                const uint64_t a = new_edges[q].first, b = new_edges[q].second;
-                const uint64_t peer = side ? a : b;
-                const uint64_t e = n_edges + q;
-                uint32_t key[7];
-                key[0] = S.kd.intern(num("eth", degree + extra));
-                key[1] = S.kd.intern(ip4((uint32_t)(2 * e + side)));
-                key[2] = 0;
-                key[3] = S.kd.intern(num("nx", q));   // peer-side name of the new interface
-                key[4] = S.kd.intern(ip4((uint32_t)(2 * e + (side ^ 1))));
-                key[5] = 0;
-                key[6] = S.id_name0 + (uint32_t)peer;
-                push_link(S, S.des, key, (int64_t)(e + 1), draw_props(seed, e + 1, 0));
-                ++extra;
+            push_link(S, S.des, key, (int64_t)(e + 1), draw_props(seed, e + 1, 0));
+            if (config == 3) {
+                S.ch.edge.push_back(e);
+                S.ch.side.push_back((uint8_t)side);
+                S.ch.ver.push_back(0);
             }
         }
         close_topo(S);
     }
+    if (config == 3) {                        // realised = config 2's desired, desired = epoch 1
+        S.ch.on = true;
+        S.ch.seed = seed;
+        S.ch.total = total;
+        S.ch.n_edges = n_edges;
+        churn_advance(S);
+    }
 }
 
 // ---- config 4: WAN digital twin --------------------------------------------------------
-void build_config4(Synth& S, uint64_t seed, uint32_t sites_per_shard, uint32_t shard, uint32_t nshards) {
+void build_config4(Synth& S, uint64_t seed, uint64_t total, uint32_t sites_per_shard, uint32_t shard,
+                   uint32_t nshards, bool hash) {
     const uint32_t per_ns = 100;
-    const uint64_t total = (uint64_t)sites_per_shard * nshards;
     const uint32_t n_ns = (uint32_t)((total + per_ns - 1) / per_ns);
     shared_prefix(S, (uint32_t)total, 256, n_ns, "site-%u");
-    S.pod_slice = sites_per_shard;
-    S.pod_base = shard * sites_per_shard;
+    assign_shard(S, total, sites_per_shard, shard, nshards, hash,
+                 [&](uint64_t p) { return S.id_ns0 + (uint32_t)(p / per_ns); });
     // Chung-Lu inside each namespace: weight w_i ∝ (i+1)^-0.8 scaled to mean degree 20;
     // the namespace's edge list is generated from (seed, ns) so every shard agrees.
     std::vector<double> w(per_ns);
@@ -418,9 +526,10 @@ void build_config4(Synth& S, uint64_t seed, uint32_t sites_per_shard, uint32_t s
     auto is_dead = [&](uint64_t p) { return (hmix(seed ^ 0xDEADull, p) % 100) < 2; };
     auto node_of = [&](uint64_t p) { return (uint32_t)(hmix(seed ^ 0x40DEull, p) % 256); };
     Props empty;
-    const uint64_t p_first = S.pod_base, p_last = S.pod_base + sites_per_shard;
-    uint64_t ns_first = p_first / per_ns, ns_last = (p_last + per_ns - 1) / per_ns;
-    for (uint64_t q = ns_first; q < ns_last; ++q) {
+    std::vector<uint8_t> ns_has(n_ns, 0);                  // namespaces holding a pod of this shard
+    for (uint32_t p : S.owned) ns_has[p / per_ns] = 1;
+    for (uint64_t q = 0; q < n_ns; ++q) {
+        if (!ns_has[q]) continue;
         Rng r(hmix(seed, q + 0x4000));
         struct E { uint32_t a, b; uint8_t kind; };   // kind 0 pod-pod, 1 physical, 2 localhost
         std::vector<E> edges(edges_per_ns);
@@ -441,7 +550,7 @@ void build_config4(Synth& S, uint64_t seed, uint32_t sites_per_shard, uint32_t s
             for (uint32_t k = 0; k < adj[i].size(); ++k) pos[adj[i][k].first * 2 + adj[i][k].second] = k;
         for (uint32_t i = 0; i < per_ns; ++i) {
             const uint64_t p = q * per_ns + i;
-            if (p < p_first || p >= p_last || p >= total) continue;
+            if (p >= total || S.local_of[p] == 0xFFFFFFFFu) continue;
             push_topo(S, (uint32_t)p, S.id_ns0 + (uint32_t)q, is_dead(p), node_of(p), 0);
             for (auto [k, side] : adj[i]) {
                 const E& e = edges[k];
@@ -486,12 +595,14 @@ extern "C" {
 
 struct kdtn_synth_params {
     uint64_t seed;
-    uint32_t pods_per_shard;
+    uint32_t pods_per_shard;   // block sharding: pods per shard
     uint32_t degree;
     uint32_t n_nodes;
     double dead_frac;
     uint32_t shard;
     uint32_t nshards;
+    uint32_t hash_sharding;    // 1: shard = kdtn_topology_shard(namespace, name, nshards)
+    uint32_t total_pods;       // hash sharding: pods of the whole topology
 };
 
 void* kdtn_synth_new(int config, const kdtn_synth_params* prm) {
@@ -500,10 +611,14 @@ void* kdtn_synth_new(int config, const kdtn_synth_params* prm) {
     case 1: build_config1(*S); break;
     case 2:
     case 3:
-        build_config23(*S, config, prm->seed, prm->pods_per_shard, prm->degree, prm->n_nodes, prm->dead_frac,
-                       prm->shard, prm->nshards);
+    case 4: {
+        const bool hash = prm->hash_sharding != 0;
+        const uint64_t total = hash ? (uint64_t)prm->total_pods : (uint64_t)prm->pods_per_shard * prm->nshards;
+        if (config == 4) build_config4(*S, prm->seed, total, prm->pods_per_shard, prm->shard, prm->nshards, hash);
+        else build_config23(*S, config, prm->seed, total, prm->pods_per_shard, prm->degree, prm->n_nodes,
+                            prm->dead_frac, prm->shard, prm->nshards, hash);
         break;
-    case 4: build_config4(*S, prm->seed, prm->pods_per_shard, prm->shard, prm->nshards); break;
+    }
     default: delete S; return nullptr;
     }
     if (config == 2 || config == 4) {
@@ -511,8 +626,17 @@ void* kdtn_synth_new(int config, const kdtn_synth_params* prm) {
         S->t_roff.assign(S->t_ns.size() + 1, 0u);
     }
     S->kd.map.clear();
-    S->pd.map.clear();
+    if (!S->ch.on) S->pd.map.clear();          // churn epochs intern re-drawn props
     return S;
+}
+
+// config 3: advance to the next churn epoch (realised := desired, new desired). Arrays
+// returned by kdtn_synth_get before the call are invalidated. -1 if not a churn workload.
+int kdtn_synth_advance(void* sp) {
+    Synth& S = *static_cast<Synth*>(sp);
+    if (!S.ch.on) return -1;
+    churn_advance(S);
+    return (int)S.ch.epoch;
 }
 
 void kdtn_synth_free(void* s) { delete static_cast<Synth*>(s); }
@@ -541,6 +665,7 @@ int kdtn_synth_get(void* sp, const char* name, void** ptr, uint64_t* n, uint32_t
     if (nm == "v_node") return ret(S.v_node);
     if (nm == "v_vni") return ret(S.v_vni);
     if (nm == "v_netns") return ret(S.v_netns);
+    if (nm == "t_gid") return ret(S.owned);
     for (int side = 0; side < 2; ++side) {
         Links& L = side ? S.des : S.real;
         const std::string pre = side ? "des_" : "real_";

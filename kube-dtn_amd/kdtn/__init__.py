@@ -5,7 +5,7 @@ MakeQdiscs) runs as HIP kernels on gfx950 behind the C-ABI in include/kdtn.h; th
 package packs tables, calls the ABI and unpacks the batches.
 """
 from . import abi
-from .engine import Engine, KdtnError, comm_unique_id, lib
+from .engine import Engine, KdtnError, comm_unique_id, lib, topology_shard
 from .tables import BatchesOut, EpochInput, Interner, Links, StrTab, Topos, Vnis
 
 __all__ = ["abi", "Engine", "KdtnError", "comm_unique_id", "lib", "BatchesOut", "EpochInput",

@@ -89,6 +89,10 @@ def lib() -> C.CDLL:
         "kdtn_json_upload": (C.c_int, [vp, C.c_char_p, C.c_uint64]),
         "kdtn_json_ingest": (C.c_int, [vp, C.POINTER(abi.VniTable), C.POINTER(abi.IngestInfo)]),
         "kdtn_ingest_download": (C.c_int, [vp, C.POINTER(abi.IngestTables)]),
+        "kdtn_topology_shard": (C.c_uint32, [C.c_char_p, C.c_uint32, C.c_char_p, C.c_uint32, C.c_uint32]),
+        "kdtn_comm_set_ranks": (C.c_int, [vp, C.c_int, C.c_int]),
+        "kdtn_pods_export": (C.c_int, [vp, vp]),
+        "kdtn_pods_import": (C.c_int, [vp, vp, C.c_uint64]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -101,6 +105,13 @@ def lib() -> C.CDLL:
 def _check(code: int, what: str) -> None:
     if code != abi.OK:
         raise KdtnError(code, what)
+
+
+def topology_shard(namespace, name, nshards: int) -> int:
+    """Owner shard of a Topology: hash64(namespace/name) mod nshards (kdtn_topology_shard)."""
+    ns = namespace.encode() if isinstance(namespace, str) else bytes(namespace)
+    nm = name.encode() if isinstance(name, str) else bytes(name)
+    return int(lib().kdtn_topology_shard(ns, len(ns), nm, len(nm), nshards))
 
 
 def comm_unique_id() -> bytes:
@@ -146,6 +157,22 @@ class Engine:
     def comm_init(self, unique_id: bytes, nranks: int, rank: int) -> None:
         buf = (C.c_uint8 * 128).from_buffer_copy(unique_id)
         _check(lib().kdtn_comm_init(self._ctx, C.byref(buf), nranks, rank), "kdtn_comm_init")
+
+    def set_ranks(self, nranks: int, rank: int) -> None:
+        """Host transport for the pod-status exchange (kdtn_comm_set_ranks): per epoch,
+        pods_export → all-gather by the caller → pods_import → run."""
+        _check(lib().kdtn_comm_set_ranks(self._ctx, nranks, rank), "kdtn_comm_set_ranks")
+
+    def pods_export(self, pod_slice: int) -> np.ndarray:
+        """This rank's pod-status rows (pod_slice × 4 u32: ns, name, src_ip, net_ns|nil<<31)."""
+        rows = np.zeros((max(pod_slice, 1), 4), np.uint32)
+        _check(lib().kdtn_pods_export(self._ctx, rows.ctypes.data), "kdtn_pods_export")
+        return rows[:pod_slice]
+
+    def pods_import(self, rows: np.ndarray) -> None:
+        """The gathered table of every rank's rows, rank order ((pod_slice*nranks) × 4 u32)."""
+        rows = np.ascontiguousarray(rows, dtype=np.uint32)
+        _check(lib().kdtn_pods_import(self._ctx, rows.ctypes.data, rows.shape[0]), "kdtn_pods_import")
 
     def set_stream(self, stream_handle: int | None) -> None:
         _check(lib().kdtn_set_stream(self._ctx, C.c_void_p(stream_handle or 0)), "kdtn_set_stream")

@@ -22,7 +22,7 @@ _lib = None
 class Params(C.Structure):
     _fields_ = [("seed", C.c_uint64), ("pods_per_shard", C.c_uint32), ("degree", C.c_uint32),
                 ("n_nodes", C.c_uint32), ("dead_frac", C.c_double), ("shard", C.c_uint32),
-                ("nshards", C.c_uint32)]
+                ("nshards", C.c_uint32), ("hash_sharding", C.c_uint32), ("total_pods", C.c_uint32)]
 
 
 def _load():
@@ -37,6 +37,8 @@ def _load():
         L.kdtn_synth_get.restype = C.c_int
         L.kdtn_synth_get.argtypes = [C.c_void_p, C.c_char_p, C.POINTER(C.c_void_p),
                                      C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]
+        L.kdtn_synth_advance.restype = C.c_int
+        L.kdtn_synth_advance.argtypes = [C.c_void_p]
         _lib = L
     return _lib
 
@@ -85,7 +87,7 @@ def _save(inp: EpochInput, path: str) -> None:
             "tns": inp.topos.ns, "tna": inp.topos.name, "tsr": inp.topos.src_ip, "tnn": inp.topos.net_ns,
             "tfl": inp.topos.flags, "tro": inp.topos.real_off, "tdo": inp.topos.des_off,
             "vno": inp.vnis.node, "vvn": inp.vnis.vni, "vnn": inp.vnis.net_ns,
-            "meta": np.array([inp.pod_slice, inp.pod_base, inp.total_pods], np.int64)}
+            "meta": np.array([inp.pod_slice, inp.pod_base, inp.total_pods], np.int64), "gid": inp.gid}
     for side, L in (("r", inp.realised), ("d", inp.desired)):
         arrs[side + "k"], arrs[side + "u"], arrs[side + "p"], arrs[side + "g"] = L.key, L.uid, L.prop, L.gap
     tmp = path + ".tmp.npz"
@@ -101,29 +103,42 @@ def _load_cached(path: str) -> EpochInput:
                      Links(z["rk"], z["ru"], z["rp"], z["rg"]), Links(z["dk"], z["du"], z["dp"], z["dg"]),
                      Vnis(z["vno"], z["vvn"], z["vnn"]), pod_slice=int(m[0]), pod_base=int(m[1]))
     inp.total_pods = int(m[2])
+    inp.gid = z["gid"]
     return inp
 
 
 def make(config: int, pods_per_shard: int = 1_000_000, degree: int = 10, n_nodes: int = 64,
          dead_frac: float = 0.02, shard: int = 0, nshards: int = 1, seed: int = SEED,
-         cache_dir: str | None = None) -> EpochInput:
+         cache_dir: str | None = None, total_pods: int | None = None) -> EpochInput:
     """Build one shard of synthetic config `config` (1: fat-tree, 2: random-regular,
-    3: churn, 4: WAN twin). Config 1 ignores the size parameters. With `cache_dir`, the
-    tables are memoised as an .npz there (profiling runs that start many processes)."""
+    3: churn, 4: WAN twin). Config 1 ignores the size parameters.
+
+    Sharding: with `total_pods`, the topology has total_pods pods and this shard owns those
+    with kdtn_topology_shard(namespace, name, nshards) == shard (the engine's hash sharding,
+    strong scaling); `inp.gid` maps local topologies to global pod ids and the engine's
+    global pod index of local topology t is inp.pod_base + t. Without it, shard k owns the
+    contiguous pods [k*pods_per_shard, (k+1)*pods_per_shard) (legacy block sharding). With
+    `cache_dir`, the tables are memoised as an .npz there."""
+    hash_sh = total_pods is not None
     if cache_dir:
         path = _cache_path(cache_dir, config, pods_per_shard, degree, n_nodes, dead_frac, shard,
-                           nshards, seed)
+                           nshards, seed, *(["h", total_pods] if hash_sh else []))
         if os.path.exists(path):
             return _load_cached(path)
-        inp = make(config, pods_per_shard, degree, n_nodes, dead_frac, shard, nshards, seed)
+        inp = make(config, pods_per_shard, degree, n_nodes, dead_frac, shard, nshards, seed,
+                   total_pods=total_pods)
         os.makedirs(cache_dir, exist_ok=True)
         _save(inp, path)
         return inp
-    prm = Params(seed, pods_per_shard, degree, n_nodes, dead_frac, shard, nshards)
+    prm = Params(seed, pods_per_shard, degree, n_nodes, dead_frac, shard, nshards, int(hash_sh),
+                 int(total_pods or 0))
     ptr = _load().kdtn_synth_new(config, C.byref(prm))
     if not ptr:
         raise ValueError(f"unknown synthetic config {config}")
-    h = _Handle(ptr)
+    return _input(_Handle(ptr))
+
+
+def _input(h: _Handle) -> EpochInput:
     kdict = StrTab(_arr(h, "kdict_bytes"), _arr(h, "kdict_offs"))
     pdict = StrTab(_arr(h, "pdict_bytes"), _arr(h, "pdict_offs"))
     topos = Topos(_arr(h, "t_ns"), _arr(h, "t_name"), _arr(h, "t_src"), _arr(h, "t_netns"),
@@ -133,7 +148,45 @@ def make(config: int, pods_per_shard: int = 1_000_000, degree: int = 10, n_nodes
     inp = EpochInput(kdict, pdict, topos, _links(h, "real_"), _links(h, "des_"), vn,
                      pod_slice=int(meta[0]), pod_base=int(meta[1]), owner=h)
     inp.total_pods = int(meta[2])
+    inp.gid = _arr(h, "t_gid").astype(np.int64)
     return inp
+
+
+class ChurnSequence:
+    """SURVEY §8(d) config 3 as a sequence of reconcile epochs: epoch 1 has config 2's
+    desired links as realised; each advance() makes the current desired the realised side
+    and churns 5 % of the edges (1/60 deleted, 1/60 re-drawn props, n_edges/60 added). The
+    key / property dictionaries only grow (append-only interning), so each epoch's kdict
+    and pdict extend the previous epoch's. Arguments as make(config=3, ...)."""
+
+    def __init__(self, pods_per_shard: int = 1_000_000, shard: int = 0, nshards: int = 1,
+                 total_pods: int | None = None, seed: int = SEED, degree: int = 10, n_nodes: int = 64,
+                 dead_frac: float = 0.02):
+        prm = Params(seed, pods_per_shard, degree, n_nodes, dead_frac, shard, nshards,
+                     int(total_pods is not None), int(total_pods or 0))
+        ptr = _load().kdtn_synth_new(3, C.byref(prm))
+        self._h = _Handle(ptr)
+        self.epoch = 1
+
+    def epoch_input(self, copy: bool = False) -> EpochInput:
+        """This epoch's tables; without `copy` the arrays alias the generator and are only
+        valid until the next advance()."""
+        inp = _input(self._h)
+        if not copy:
+            return inp
+        c = lambda a: np.array(a, copy=True)
+        out = EpochInput(StrTab(c(inp.kdict.bytes_), c(inp.kdict.offs)), StrTab(c(inp.pdict.bytes_), c(inp.pdict.offs)),
+                         Topos(*[c(getattr(inp.topos, f)) for f in ("ns", "name", "src_ip", "net_ns", "flags",
+                                                                     "real_off", "des_off")]),
+                         Links(c(inp.realised.key), c(inp.realised.uid), c(inp.realised.prop), c(inp.realised.gap)),
+                         Links(c(inp.desired.key), c(inp.desired.uid), c(inp.desired.prop), c(inp.desired.gap)),
+                         Vnis(c(inp.vnis.node), c(inp.vnis.vni), c(inp.vnis.net_ns)),
+                         pod_slice=inp.pod_slice, pod_base=inp.pod_base)
+        out.total_pods, out.gid = inp.total_pods, c(inp.gid)
+        return out
+
+    def advance(self) -> None:
+        self.epoch = _load().kdtn_synth_advance(self._h.ptr)
 
 
 def topology_list_json(inp: EpochInput, pretty: bool = False) -> bytes:

@@ -157,6 +157,7 @@ class EpochInput:
     pod_slice: int = 0
     pod_base: int = 0            # global pod index of topology 0 (multi-shard)
     owner: object = None         # keeps a generator's memory alive
+    gid: np.ndarray | None = None    # synthetic workloads: global pod id of each local topology
 
     def to_c(self) -> abi.EpochIn:
         c = abi.EpochIn(self.kdict.to_c(), self.pdict.to_c(), self.topos.to_c(),
