@@ -5,19 +5,27 @@ One step = one reconcile epoch over this rank's shard, inputs resident in HBM:
   dictionary parse → pod-status table (+ RCCL all-gather across ranks) → lookup tables →
   Reconcile gate + CalcDiff → batch compaction → addLink/delLink/UpdateLinks pure prefix
   → MakeQdiscs; the host waits for each epoch (kdtn_epoch_sync).
-Workload (BASELINE configs[2]): per GPU a 1M-pod shard of a random
-10-regular topology — 10M Link records with heterogeneous netem/tbf properties — all
-AddLinks (realised status non-nil and empty). Weak scaling: every rank owns 1M pods of a
-(N × 1M)-pod graph; peers are spread over all shards, so each epoch all-gathers the
-pod-status table over RCCL/xGMI.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+Workloads; topologies are sharded across ranks as the engine shards them,
+hash64(namespace/name) mod N (kdtn_topology_shard), one process per GPU:
+  --config 2 (default, BASELINE configs[2], the metric's 10M-link topology): a 1M-pod random
+      10-regular topology, 10M Link records with heterogeneous netem/tbf props, all AddLinks
+      (realised status non-nil and empty). Strong scaling by default: the same 10M links are
+      split over N GPUs; --scaling weak gives every GPU --pods pods instead.
+  --config 3 (churn): the same topology as an epoch sequence; each epoch realised := the
+      previous desired and 5 % of the edges churn (1/60 deleted, 1/60 new props, 1/60 new);
+      --warmup epochs, then the mean over --steps epochs (default 10). Uploads happen between
+      the timed epochs.
+  --config 4 (WAN twin): 100k sites in namespaces of 100, power-law degrees, 256 nodes.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C] [--scaling strong|weak]
 For N > 1 launch with torch.distributed.run (one process per GPU).
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -28,23 +36,34 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "kube-dtn_amd"))
 
+import numpy as np  # noqa: E402
+
 from kdtn import Engine, abi, comm_unique_id, synth  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+DEFAULT_PODS = {2: 1_000_000, 3: 1_000_000, 4: 100_000}
+WORKLOAD = {
+    2: "config2: random 10-regular topology of {pods} pods ({links} Link records), heterogeneous "
+       "netem/tbf props, all AddLinks (resolve + qdisc on every link)",
+    3: "config3: churn epochs on a random 10-regular topology of {pods} pods (~{links} Link records): "
+       "per epoch 5% of the edges churn (1/60 deleted, 1/60 re-drawn props, 1/60 added), diff-dominated; "
+       "mean of {steps} epochs",
+    4: "config4: WAN twin of {pods} sites in namespaces of 100 (power-law degrees, 256 nodes, 1% "
+       "physical/ and 0.5% localhost peers), {links} Link records, all AddLinks (resolve-dominated)",
+}
 
 
 def reconcile_bytes(inp, n_add: int, n_upd: int, n_del: int) -> float:
-    """Algorithmic bytes of one k_reconcile launch (DESIGN.md §Roofline): per AddLinks entry
-    1 (flag) + 12 (local_ip, local_mac, peer_pod ids) + 8 (uid) + 48 (12 prop ids) + 4 (gap)
-    read, 4 (index) + 16 (resolve record) + 72 (qdisc) written = 165 B; per topology
-    8 (offsets) + 1 (action) + 12 (ns, src_ip, net_ns) read + 12 (3 batch offsets) written
-    = 33 B; plus the 24 B parsed record of every property string, read once."""
+    """Algorithmic bytes of one k_reconcile launch (DESIGN.md §3): per AddLinks entry
+    1 (flag) + 16 (local_ip, local_mac, peer_pod, peer_ip ids) + 8 (uid) + 48 (12 prop ids)
+    + 4 (gap) read, 4 (index) + 16 (resolve record) + 72 (qdisc) written = 169 B; per
+    topology 8 (offsets) + 1 (action) + 12 (ns, src_ip, net_ns) read + 12 (3 batch offsets)
+    written = 33 B; plus the 24 B parsed record of every property string, read once; when
+    realised lists are non-empty, 88 B per record of both sides (read once to compare)."""
     T = inp.topos.n
-    per_add = 165.0
+    per_add = 1 + 16 + 8 + 48 + 4 + 4 + 16 + 72
     per_upd = 1 + 4 + 12 + 48 + 4 + 8 + 4 + 16 + 72   # flag, target, ids, props, gap, uid, out
     per_del = 1 + 12 + 8 + 4 + 16
-    # every realised record is compared (key + props) against the desired side when both
-    # lists are non-empty: 88 B per record per side (only when M > 0)
     cmp = 88.0 * (inp.realised.n + (inp.desired.n if inp.realised.n else 0))
     return (per_add * n_add + per_upd * n_upd + per_del * n_del + 33.0 * T + 24.0 * inp.pdict.n
             + cmp)
@@ -58,12 +77,28 @@ def epoch_bytes(inp, n_add: int, n_upd: int, n_del: int) -> float:
             + 72.0 * (n_add + n_upd) + float(inp.pdict.offs[-1]))
 
 
-def cpu_baseline(inp, budget_s: float, threads: int):
+def cpu_share():
+    """CPUs this process may use: the affinity mask, capped by a cgroup v2 cpu.max quota."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = int(q) / int(p)
+    except (OSError, ValueError):
+        pass
+    share = aff if quota is None else max(1, min(aff, int(math.ceil(quota))))
+    return share, {"nproc": os.cpu_count(), "affinity": aff, "cgroup_quota_cpus": quota,
+                   "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
+def cpu_baseline(inp, budget_s: float, threads: int, share_info: dict):
     """The CPU oracle (C restatement of the reference Go path) on a bounded sample of this
     workload's topologies, loop time only (informer maps pre-built). Single thread, then
     `threads` workers over disjoint topology ranges, mirroring the reference's
-    MaxConcurrentReconciles worker pool (controllers/topology_controller.go:335-337); the
-    ctypes call releases the GIL, so the workers run concurrently."""
+    MaxConcurrentReconciles: 32 worker pool (controllers/topology_controller.go:335-337),
+    capped by the CPUs this process may use; the ctypes call releases the GIL, so the
+    workers run concurrently."""
     from concurrent.futures import ThreadPoolExecutor
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
@@ -77,7 +112,6 @@ def cpu_baseline(inp, budget_s: float, threads: int):
     O.reconcile(inp, t_begin=0, t_end=want, timing=timing)
     links = int(inp.topos.des_off[want] - inp.topos.des_off[0])
     one = links / timing[-1]
-    # worker pool: each worker takes an equal slice of a sample `threads` times larger
     n_par = int(min(T, want * threads))
     bounds = [n_par * k // threads for k in range(threads + 1)]
     ptim = [[] for _ in range(threads)]
@@ -87,12 +121,12 @@ def cpu_baseline(inp, budget_s: float, threads: int):
     par_links = int(inp.topos.des_off[n_par] - inp.topos.des_off[0])
     par_s = max(t[-1] for t in ptim)
     return {"value": par_links / par_s, "unit": "links/s", "cores": threads, "kind": "port",
-            "value_1thread": one,
+            "value_1thread": one, "host": share_info,
             "sample": f"oracle/kdtn_oracle.c (literal CalcDiff loops, per-link MakeQdiscs, "
-                      f"map-based resolve) on rank 0's shard: {threads} threads over "
-                      f"topologies [0,{n_par}) = {par_links} links in {par_s:.2f} s (slowest "
-                      f"worker's loop); single thread: [0,{want}) = {links} links in "
-                      f"{timing[-1]:.2f} s (host nproc={os.cpu_count()})"}
+                      f"map-based resolve) on rank 0's shard: {threads} threads (min(32, CPUs this "
+                      f"process may use)) over topologies [0,{n_par}) = {par_links} links in "
+                      f"{par_s:.2f} s (slowest worker's loop); single thread: [0,{want}) = {links} "
+                      f"links in {timing[-1]:.2f} s"}
 
 
 def wire_stage(eng, reps: int = 5):
@@ -112,7 +146,6 @@ def wire_stage(eng, reps: int = 5):
     gpu_ms = sum(v for k, v in acc.items() if k != "wire_host_sync")
     res = {"bytes": n, "gpu_ms": gpu_ms, "out_GBps": n / (gpu_ms * 1e-3) / 1e9,
            "kernels_ms": acc, "note": "not part of value; arena-size host round trip excluded"}
-    # RemotePod fan-out grouped per destination daemon (kdtn_epoch_fanout)
     eng.fanout()
     facc: dict[str, float] = {}
     for _ in range(reps):
@@ -125,14 +158,40 @@ def wire_stage(eng, reps: int = 5):
     return res
 
 
-def ingest_stage(eng, inp, reps: int = 5, cpu_sample_pods: int = 20_000):
+def e2e_stage(eng, inp, reps: int = 3):
+    """PCIe-inclusive epoch (separate report, never `value`): kdtn_reconcile_epoch's pieces —
+    upload of the host tables (pageable numpy arrays), run + sync, download of every output
+    — timed separately, median of `reps`."""
+    ups, runs, downs = [], [], []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        eng.upload(inp)
+        t1 = time.perf_counter()
+        eng.run()
+        eng.sync()
+        t2 = time.perf_counter()
+        out = eng.download()
+        t3 = time.perf_counter()
+        ups.append(t1 - t0)
+        runs.append(t2 - t1)
+        downs.append(t3 - t2)
+    med = lambda x: sorted(x)[len(x) // 2]
+    up_b = (88 * (inp.realised.n + inp.desired.n) + 25 * inp.topos.n + len(inp.kdict.bytes_)
+            + 4 * inp.kdict.n + len(inp.pdict.bytes_) + 4 * inp.pdict.n)
+    down_b = sum(getattr(out, f).nbytes for f in out.FIELDS)
+    tot = med(ups) + med(runs) + med(downs)
+    return {"links_per_s": inp.desired.n / tot, "ms": tot * 1e3, "upload_ms": med(ups) * 1e3,
+            "run_ms": med(runs) * 1e3, "download_ms": med(downs) * 1e3, "upload_bytes": up_b,
+            "download_bytes": down_b, "host_link_GBps": (up_b + down_b) / (med(ups) + med(downs)) / 1e9,
+            "note": "not part of value: upload + epoch + download of caller-owned pageable host "
+                    "memory, as one kdtn_reconcile_epoch call would do"}
+
+
+def ingest_stage(eng, inp, steps: int, reps: int = 5, cpu_sample_pods: int = 20_000):
     """Separate report (not part of `value`): CR ingest of this shard's Topology CRs as a
     TopologyList JSON document (kdtn_json_ingest: json.Unmarshal + SoA + interning on the
-    GPU, document resident in HBM). Wall time per ingest includes its three host round
-    trips (token / element counts, intern table fill); roofline bytes = document read once
-    + the decoded tables written once (88 B per link record, 25 B per topology, dictionary
-    arenas + offsets). CPU baseline: the oracle's decode (oracle/kdtn_oracle_json.c, the
-    reference's json.Unmarshal restated) single-threaded on a bounded slice of the workload."""
+    GPU, document resident in HBM), then the epoch run on the ingest-produced tables (ids in
+    the ingest's own interning order) next to the synthetic tables of `value`."""
     doc = synth.topology_list_json(inp)
     t = time.perf_counter()
     eng.json_upload(doc)
@@ -161,6 +220,21 @@ def ingest_stage(eng, inp, reps: int = 5, cpu_sample_pods: int = 20_000):
            "note": "not part of value; the document is resident in HBM (h2d_GBps is the PCIe "
                    "upload measured separately)"}
     del doc
+    # the epoch on the ingest-produced tables (first-occurrence kdict ids)
+    for _ in range(2):
+        eng.run()
+        eng.sync()
+    ksum: dict[str, float] = {}
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(steps):
+        eng.run()
+        eng.sync()
+        for k, v in eng.kernel_times().items():
+            ksum[k] = ksum.get(k, 0.0) + v / steps
+    el = (time.perf_counter() - t) / steps
+    res["epoch_on_ingest_tables"] = {"ms_per_step": el * 1e3, "links_per_s": info.n_desired / el,
+                                     "kernels_ms": ksum, "n_kdict": int(info.n_kdict)}
     try:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as O
@@ -179,7 +253,7 @@ def ingest_stage(eng, inp, reps: int = 5, cpu_sample_pods: int = 20_000):
     return res
 
 
-def pmc_traffic(links_per_gpu: int):
+def pmc_traffic(config: int, links: int):
     """HBM bytes per k_reconcile launch from the newest committed PMC summary of the same
     workload (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from separate
     FETCH_SIZE / WRITE_SIZE rocprofv3 passes, gfx950 correction applied), else None."""
@@ -188,7 +262,7 @@ def pmc_traffic(links_per_gpu: int):
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json"))):
         with open(f) as fh:
             d = json.load(fh)
-        if d.get("links_per_gpu") != links_per_gpu:
+        if d.get("links_per_gpu") != links or d.get("config", 2) != config:
             continue
         for k, v in d["kernels"].items():
             if k.startswith("k_reconcile") and "traffic_bytes" in v:
@@ -196,20 +270,65 @@ def pmc_traffic(links_per_gpu: int):
     return best
 
 
+def path_stats(inp) -> dict:
+    """How k_reconcile's workgroups (64 topologies each) split between its paths: bulk (no
+    topology needs element comparisons), fast (CalcDiff window in LDS, <= CAP records) and
+    slow (global-scratch window)."""
+    T = inp.topos
+    nt = T.n
+    ro, no = T.real_off.astype(np.int64), T.des_off.astype(np.int64)
+    ko, kn = ro[1:] - ro[:-1], no[1:] - no[:-1]
+    cmp = ((T.flags & 3) == 0) & (ko > 0) & (kn > 0)
+    nwg = (nt + 63) // 64
+    idx = np.arange(nwg) * 64
+    anyc = np.logical_or.reduceat(cmp, idx) if nt else np.zeros(0, bool)
+    tot = (ro[np.minimum(idx + 64, nt)] - ro[idx]) + (no[np.minimum(idx + 64, nt)] - no[idx])
+    return {"workgroups": int(nwg), "bulk": int((~anyc).sum()), "fast": int((anyc & (tot <= 2048)).sum()),
+            "slow": int((anyc & (tot > 2048)).sum())}
+
+
+def allmax(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t[0])
+
+
+def allsum(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t[0])
+
+
+def barrier(world: int) -> None:
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--pods", type=int, default=1_000_000, help="pods per GPU shard")
-    ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=None, help="timed epochs (default 20; config 3: 10)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed epochs (default 3; config 3: 1)")
+    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4))
+    ap.add_argument("--pods", type=int, default=None,
+                    help="pods of the whole topology (strong) or per GPU (weak)")
+    ap.add_argument("--scaling", default="strong", choices=("strong", "weak"))
     ap.add_argument("--cpu-budget-s", type=float, default=12.0)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(32, CPUs this process may use)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-wire", action="store_true", help="skip the wire-encoding stage report")
     ap.add_argument("--no-ingest", action="store_true", help="skip the CR-ingest stage report")
-    ap.add_argument("--cpu-threads", type=int, default=16,
-                    help="CPU-baseline worker threads (the GPU box's CPU share is 16)")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive epoch report")
     args = ap.parse_args()
+    churn = args.config == 3
+    steps = args.steps if args.steps is not None else (10 if churn else 20)
+    warmup = args.warmup if args.warmup is not None else (1 if churn else 3)
+    pods = args.pods or DEFAULT_PODS[args.config]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -217,9 +336,15 @@ def main():
     if world > 1:
         dist.init_process_group("gloo")
     torch.cuda.set_device(local)
+    total_pods = pods if args.scaling == "strong" else pods * world
 
     t0 = time.time()
-    inp = synth.make(args.config, pods_per_shard=args.pods, shard=rank, nshards=world)
+    cs = None
+    if churn:
+        cs = synth.ChurnSequence(total_pods=total_pods, shard=rank, nshards=world)
+        inp = cs.epoch_input()
+    else:
+        inp = synth.make(args.config, total_pods=total_pods, shard=rank, nshards=world)
     gen_s = time.time() - t0
     eng = Engine(device=local)
     if world > 1:
@@ -228,80 +353,122 @@ def main():
         eng.comm_init(uid[0], world, rank)
     eng.upload(inp)
 
-    for _ in range(args.warmup):
-        eng.run()
-        eng.sync()
-
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
     ksum: dict[str, float] = {}
-    t_start = time.perf_counter()
-    counts = None
-    for _ in range(args.steps):
-        eng.run()
-        counts = eng.sync()
-        for k, v in eng.kernel_times().items():
-            ksum[k] = ksum.get(k, 0.0) + v
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t_start
-    if world > 1:
-        dist.barrier()
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t[0])
-        n = torch.tensor([inp.desired.n], dtype=torch.float64)
-        dist.all_reduce(n, op=dist.ReduceOp.SUM)
-        links_total = float(n[0])
+    counts_acc = np.zeros(3)
+    bytes_acc = epoch_acc = 0.0
+    links_local = 0
+    elapsed = 0.0
+    diff_ms = []
+    pstats = None
+    if not churn:
+        for _ in range(warmup):
+            eng.run()
+            eng.sync()
+        barrier(world)
+        t_start = time.perf_counter()
+        counts = None
+        for _ in range(steps):
+            eng.run()
+            counts = eng.sync()
+            for k, v in eng.kernel_times().items():
+                ksum[k] = ksum.get(k, 0.0) + v
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t_start
+        barrier(world)
+        elapsed = allmax(elapsed, world)
+        links_local = inp.desired.n * steps
+        counts_acc += np.array([counts.n_add, counts.n_upd, counts.n_del]) * steps
+        bytes_acc = reconcile_bytes(inp, counts.n_add, counts.n_upd, counts.n_del) * steps
+        epoch_acc = epoch_bytes(inp, counts.n_add, counts.n_upd, counts.n_del) * steps
+        pstats = path_stats(inp)
     else:
-        links_total = float(inp.desired.n)
-
-    ms_step = elapsed / args.steps * 1e3
-    kavg = {k: v / args.steps for k, v in ksum.items()}
+        # one upload per epoch (untimed), each epoch timed between barriers; sum over epochs
+        for ep in range(warmup + steps):
+            if ep:
+                cs.advance()
+                inp = cs.epoch_input()
+                eng.upload(inp)
+            timed = ep >= warmup
+            barrier(world)
+            t = time.perf_counter()
+            eng.run()
+            counts = eng.sync()
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t
+            kt = eng.kernel_times()
+            barrier(world)
+            dt = allmax(dt, world)
+            if not timed:
+                continue
+            elapsed += dt
+            for k, v in kt.items():
+                ksum[k] = ksum.get(k, 0.0) + v
+            links_local += inp.desired.n
+            counts_acc += np.array([counts.n_add, counts.n_upd, counts.n_del])
+            bytes_acc += reconcile_bytes(inp, counts.n_add, counts.n_upd, counts.n_del)
+            epoch_acc += epoch_bytes(inp, counts.n_add, counts.n_upd, counts.n_del)
+            eng.run(abi.STAGE_DIFF)                      # gate + CalcDiff + lists alone (report)
+            eng.sync()
+            diff_ms.append(eng.kernel_times()["reconcile"])
+            if pstats is None:
+                pstats = path_stats(inp)
+    links_total = allsum(links_local, world)
+    nsteps = steps
+    ms_step = elapsed / nsteps * 1e3
+    kavg = {k: v / nsteps for k, v in ksum.items()}
+    bytes_launch = bytes_acc / nsteps
     dom = max(kavg, key=kavg.get)
-    ebytes = reconcile_bytes(inp, counts.n_add, counts.n_upd, counts.n_del)
     roof = {"kernel": "k_reconcile", "bound": "hbm",
-            "achieved": ebytes / (kavg["reconcile"] * 1e-3) / 1e9,
+            "achieved": bytes_launch / (kavg["reconcile"] * 1e-3) / 1e9,
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "traffic": None,
-            "bytes_per_launch": ebytes, "avg_ms": kavg["reconcile"], "dominant_stage": dom}
+            "bytes_per_launch": bytes_launch, "avg_ms": kavg["reconcile"], "dominant_stage": dom}
     roof["frac"] = roof["achieved"] / roof["peak"]
-    tr = pmc_traffic(inp.desired.n)
+    tr = pmc_traffic(args.config, inp.desired.n) if world == 1 else None
     if tr is not None:
         roof["traffic"] = tr[0]
         roof["traffic_source"] = f"profiles/{tr[1]} (2*FETCH_SIZE + WRITE_SIZE per launch)"
-    pbytes = epoch_bytes(inp, counts.n_add, counts.n_upd, counts.n_del)
+    eb = epoch_acc / nsteps
+    links_per_epoch = links_total / nsteps
     result = {
         "metric": "links reconciled/sec (diff+qdisc) on 10M-link topology",
-        "value": links_total / (elapsed / args.steps),
+        "value": links_total / elapsed,
         "unit": "links/s",
         "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
+        "steps": nsteps,
+        "warmup": warmup,
         "ms_per_step": ms_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "u32",
-        "data": "synthetic (kdtn_synth config 2, seed 0x6b64746e)",
-        "config": {"workload": f"config{args.config}: {args.pods}-pod shard per GPU of a random "
-                               f"10-regular topology, {inp.desired.n} links/GPU, heterogeneous "
-                               f"netem/tbf props, all AddLinks (resolve + qdisc on every link)",
-                   "pods_per_gpu": inp.topos.n, "links_per_gpu": inp.desired.n,
-                   "global_links": int(links_total), "parallelism": f"shard{world}"},
+        "data": f"synthetic (kdtn_synth config {args.config}, seed 0x6b64746e), hash-sharded by namespace/name",
+        "config": {"workload": WORKLOAD[args.config].format(pods=total_pods, links=int(links_per_epoch),
+                                                            steps=nsteps),
+                   "config": args.config, "pods_total": total_pods, "links_per_epoch": int(links_per_epoch),
+                   "links_rank0": int(links_local / nsteps), "pods_rank0": inp.topos.n,
+                   "parallelism": f"shard{world} (hash64(ns/name) mod {world})"},
         "roofline": roof,
-        "epoch_roofline": {"bytes": pbytes, "achieved": pbytes / (ms_step * 1e-3) / 1e9,
+        "epoch_roofline": {"bytes": eb, "achieved": eb / (ms_step * 1e-3) / 1e9,
                            "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                           "frac": pbytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS},
+                           "frac": eb / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS},
         "kernels_ms": kavg,
-        "counts": {"add": counts.n_add, "upd": counts.n_upd, "del": counts.n_del},
+        "counts_per_epoch_rank0": dict(zip(("add", "upd", "del"), (counts_acc / nsteps).tolist())),
+        "k_reconcile_paths_rank0": pstats,
         "gen_s": round(gen_s, 2),
     }
-    if not args.no_wire and world == 1:
+    if diff_ms:
+        result["diff_only_reconcile_ms"] = float(np.mean(diff_ms))
+        result["diff_share_of_reconcile"] = float(np.mean(diff_ms)) / kavg["reconcile"]
+    if world == 1 and not args.no_e2e and not churn:
+        result["e2e_pcie"] = e2e_stage(eng, inp)
+    if world == 1 and not args.no_wire and args.config == 2:
         result["wire_stage"] = wire_stage(eng)
     if world == 1 and not args.no_cpu_baseline:            # CPU baseline: rank 0 at N=1 only
-        result["cpu_baseline"] = cpu_baseline(inp, args.cpu_budget_s, args.cpu_threads)
-    if not args.no_ingest and world == 1:
-        result["ingest_stage"] = ingest_stage(eng, inp)
+        share, info = cpu_share()
+        threads = args.cpu_threads or min(32, share)
+        result["cpu_baseline"] = cpu_baseline(inp, args.cpu_budget_s, threads, info)
+    if world == 1 and not args.no_ingest and args.config == 2:
+        result["ingest_stage"] = ingest_stage(eng, inp, steps)
     if rank == 0:
         print(json.dumps(result), flush=True)
     eng.close()

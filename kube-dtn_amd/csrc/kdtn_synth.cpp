@@ -503,11 +503,12 @@ void build_config4(Synth& S, uint64_t seed, uint64_t total, uint32_t sites_per_s
     shared_prefix(S, (uint32_t)total, 256, n_ns, "site-%u");
     assign_shard(S, total, sites_per_shard, shard, nshards, hash,
                  [&](uint64_t p) { return S.id_ns0 + (uint32_t)(p / per_ns); });
-    // Chung-Lu inside each namespace: weight w_i ∝ (i+1)^-0.8 scaled to mean degree 20;
+    // Chung-Lu inside each namespace: weight w_i ∝ (i+1)^-1.7 (the hub of a namespace draws
+    // about half of its 2,000 link ends: hubs of ~1,000 links), mean degree 20;
     // the namespace's edge list is generated from (seed, ns) so every shard agrees.
     std::vector<double> w(per_ns);
     double ws = 0;
-    for (uint32_t i = 0; i < per_ns; ++i) ws += (w[i] = 1.0 / std::pow((double)(i + 1), 0.8));
+    for (uint32_t i = 0; i < per_ns; ++i) ws += (w[i] = 1.0 / std::pow((double)(i + 1), 1.7));
     const double mean_deg = 20.0;
     const uint32_t edges_per_ns = (uint32_t)(per_ns * mean_deg / 2);
     std::vector<double> cdf(per_ns);

@@ -1,0 +1,102 @@
+"""BASELINE configs 3 and 4 at their stated sizes on the GPU.
+
+Config 3 (churn, diff-dominated): 10M-link topology, 5 % of the edges churn per epoch; three
+consecutive epochs through one context. Checked at full size by an exact set-algebra restatement of
+CalcDiff over (topology, uid) keys — every key is unique in this workload, so del / add /
+upd are exactly the key differences and the key intersection with changed properties, each
+in list order — plus bit-exact oracle windows of 20,000 topologies (every output field).
+Config 4 (WAN twin, resolve-dominated): 100k sites, ~2M links, checked bit-exact against
+the oracle in full."""
+import numpy as np
+import pytest
+
+import oracle as O
+from kdtn import abi, synth
+
+pytestmark = pytest.mark.gpu
+TICK = 15.625
+
+
+def _seg(off, n):
+    return np.repeat(np.arange(len(off) - 1, dtype=np.int64), np.diff(off.astype(np.int64)))[:n]
+
+
+def _keys(links, topo):
+    return (topo << 40) | links.uid.astype(np.int64)
+
+
+def _window_same(inp, out, a, b):
+    ora = O.reconcile(inp, tick=TICK, t_begin=a, t_end=b)
+    for lst, res, q in (("del", "del_res", None), ("add", "add_res", "add_qdisc"), ("upd", "upd_res", "upd_qdisc")):
+        off = getattr(out, lst + "_off")
+        s, e = off[a], off[b]
+        assert (off[a:b + 1] - s).tobytes() == getattr(ora, lst + "_off").tobytes(), lst
+        assert getattr(out, lst + "_idx")[s:e].tobytes() == getattr(ora, lst + "_idx").tobytes(), lst
+        assert getattr(out, res)[s:e].tobytes() == getattr(ora, res).tobytes(), lst
+        if q:
+            assert getattr(out, q)[s:e].tobytes() == getattr(ora, q).tobytes(), lst
+    assert out.action[a:b].tobytes() == ora.action.tobytes()
+
+
+def check_config3_lists(inp, out, to, tn):
+    """CalcDiff as set algebra over (topology, uid) keys. A self-loop edge of the pairing
+    model puts two records with one uid into one topology; those few topologies are checked
+    against the oracle instead."""
+    T = inp.topos
+    ko, kn = _keys(inp.realised, to), _keys(inp.desired, tn)
+    uo, co = np.unique(ko, return_counts=True)
+    un, cn = np.unique(kn, return_counts=True)
+    dup_t = np.unique(np.concatenate([uo[co > 1] >> 40, un[cn > 1] >> 40]))
+    for t in dup_t.tolist():
+        _window_same(inp, out, t, t + 1)
+    okr, okn = ~np.isin(to, dup_t), ~np.isin(tn, dup_t)
+    in_new = np.isin(ko, kn)
+    in_old = np.isin(kn, ko)
+    want_del = np.nonzero(~in_new & okr)[0]
+    want_add = np.nonzero(~in_old & okn)[0]
+    order_n = np.argsort(kn, kind="stable")
+    i = np.nonzero(in_new & okr)[0]
+    j = order_n[np.searchsorted(kn[order_n], ko[i])]
+    pdiff = (inp.realised.prop[:, i] != inp.desired.prop[:, j]).any(axis=0) | (inp.realised.gap[i] != inp.desired.gap[j])
+    want_upd = j[pdiff]
+    keep = lambda idx, seg: idx[~np.isin(seg[idx], dup_t)]
+    assert np.array_equal(keep(out.del_idx, to), want_del.astype(np.uint32))
+    assert np.array_equal(keep(out.add_idx, tn), want_add.astype(np.uint32))
+    assert np.array_equal(keep(out.upd_idx, tn), want_upd.astype(np.uint32))
+    for lst, idx, seg in (("del", out.del_idx, to), ("add", out.add_idx, tn), ("upd", out.upd_idx, tn)):
+        cnt = np.bincount(seg[idx], minlength=T.n)
+        assert np.array_equal(np.diff(getattr(out, lst + "_off").astype(np.int64)), cnt), lst
+
+
+def test_config3_churn_epochs_full_size(engine):
+    cs = synth.ChurnSequence(pods_per_shard=1_000_000)
+    for ep in range(3):
+        if ep:
+            cs.advance()
+        inp = cs.epoch_input()
+        T = inp.topos
+        M, N = inp.realised.n, inp.desired.n
+        assert 9_800_000 < N < 10_200_000 and T.n == 1_000_000
+        out = engine.reconcile(inp)
+        to, tn = _seg(T.real_off, M), _seg(T.des_off, N)
+        check_config3_lists(inp, out, to, tn)
+        for n in (len(out.del_idx), len(out.add_idx), len(out.upd_idx)):
+            assert 150_000 < n < 185_000
+        assert (out.action == abi.ACT_DIFF).sum() > 0.25 * T.n
+        assert (out.add_res["vni"] == (5000 + inp.desired.uid[out.add_idx]).astype(np.int32)).all()
+        assert (out.upd_qdisc["has_netem"] | (out.upd_qdisc["err"] > 0)).any()
+        _window_same(inp, out, 300_000 + 100_000 * ep, 320_000 + 100_000 * ep)
+
+
+def test_config4_wan_full_size(engine):
+    inp = synth.make(4, pods_per_shard=100_000)
+    assert inp.topos.n == 100_000 and 1_500_000 < inp.desired.n < 2_500_000
+    out = engine.reconcile(inp)
+    ora = O.reconcile(inp, tick=TICK)
+    bad = out.mismatches(ora)
+    assert not bad, bad
+    kinds = np.bincount(out.add_res["kind"], minlength=6)
+    assert kinds[abi.KIND_CROSS_NODE] > 0.9 * inp.desired.n
+    assert kinds[abi.KIND_PHYSICAL] > 0 and kinds[abi.KIND_MACVLAN] > 0
+    hub = np.diff(inp.topos.des_off.astype(np.int64)).max()
+    assert hub >= 500                                           # power-law hubs
