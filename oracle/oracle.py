@@ -18,7 +18,8 @@ sys.path.insert(0, os.path.join(os.path.dirname(_HERE), "kube-dtn_amd"))
 from kdtn import abi  # noqa: E402  (ABI struct layouts only)
 from kdtn.tables import BatchesOut, EpochInput  # noqa: E402
 
-LIB_PATH = os.path.join(_HERE, "libkdtn_oracle.so")
+# KDTN_ORACLE_LIB: the ASan/UBSan build (make -C oracle sanitize) for tests/test_oracle_sanitizers.py
+LIB_PATH = os.environ.get("KDTN_ORACLE_LIB") or os.path.join(_HERE, "libkdtn_oracle.so")
 _lib = None
 
 

@@ -63,3 +63,22 @@ def test_kubedtn_add_links_stops_at_remote_rejection():
     errs = np.where(errs != 0, errs, res["remote_err"])
     out = KubeDTN._outcome(res, errs, q)
     assert not out.response and out.first_failed == 1 and out.err == abi.E_REMOTE_CIDR
+
+
+def test_oracle_adversarial_epochs_run_clean():
+    """The oracle over adversarial random epochs (duplicates, nil vs empty, invalid strings,
+    >CAP hubs): reconcile, fan-out, tc argv and wire encoding complete with consistent sizes
+    (this file also runs under ASan/UBSan, tests/test_oracle_sanitizers.py)."""
+    from helpers import random_epoch_input, wire_epoch_input
+    for seed in range(4):
+        _, inp = random_epoch_input(seed, T=60, big=1 if seed == 3 else 0, p_err=0.3)
+        out = O.reconcile(inp, tick=15.625)
+        assert out.add_off[-1] == len(out.add_idx) and out.del_off[-1] == len(out.del_idx)
+        node, off, idx = O.fanout(out, inp.topos.n)
+        assert off[-1] == len(idx)
+        arena, toff = O.tc_epoch(inp, out)
+        assert toff[-1] == len(arena) and len(toff) == 2 * len(out.add_idx) + len(out.upd_idx) + 1
+        _, winp = wire_epoch_input(seed, T=40)
+        wout = O.reconcile(winp)
+        a, woff, err = O.encode_epoch(winp, wout)
+        assert int(woff[-1]) == len(a)

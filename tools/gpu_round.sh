@@ -2,7 +2,7 @@
 # One GPU-box pass: parity tests, smoke, bench, rocprofv3 kernel-trace stats of the bench
 # command, and the two HBM PMC passes (FETCH_SIZE / WRITE_SIZE in separate runs).
 # Usage (on the GPU box, from the repo root): bash tools/gpu_round.sh <tag> [what]
-#   what: comma list of tests,smoke,bench,stats,pmc (default: all)
+#   what: comma list of tests,smoke,bench,bench3,bench4,stats,pmc (default: tests,smoke,bench,stats,pmc)
 # Every GPU step has its own time limit and the script stops at the first failure.
 set -euo pipefail
 TAG=${1:-r01}
@@ -13,7 +13,7 @@ mkdir -p $OUT
 has() { [[ ",$WHAT," == *",$1,"* ]]; }
 
 if has tests; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+  timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
       > $OUT/pytest_gpu.log 2>&1
   tail -3 $OUT/pytest_gpu.log
 fi
@@ -24,6 +24,14 @@ fi
 if has bench; then
   timeout -k 10 400 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err
   cat $OUT/bench.json
+fi
+if has bench3; then
+  timeout -k 10 500 python -u bench.py --config 3 > $OUT/bench3.json 2> $OUT/bench3.err
+  cat $OUT/bench3.json
+fi
+if has bench4; then
+  timeout -k 10 300 python -u bench.py --config 4 > $OUT/bench4.json 2> $OUT/bench4.err
+  cat $OUT/bench4.json
 fi
 cd /tmp && export TMPDIR=/tmp
 if has stats; then
