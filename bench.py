@@ -15,7 +15,8 @@ hash64(namespace/name) mod N (kdtn_topology_shard), one process per GPU:
   --config 3 (churn): the same topology as an epoch sequence; each epoch realised := the
       previous desired and 5 % of the edges churn (1/60 deleted, 1/60 new props, 1/60 new);
       --warmup epochs, then the mean over --steps epochs (default 10). Uploads happen between
-      the timed epochs.
+      the timed epochs; the dictionaries are append-only (kdict_keep / pdict_keep), so each
+      epoch parses only its new strings.
   --config 4 (WAN twin): 100k sites in namespaces of 100, power-law degrees, 256 nodes.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C] [--scaling strong|weak]
@@ -385,9 +386,10 @@ def main():
         # one upload per epoch (untimed), each epoch timed between barriers; sum over epochs
         for ep in range(warmup + steps):
             if ep:
+                keep = (inp.kdict.n, inp.pdict.n)          # the churn interner only appends
                 cs.advance()
                 inp = cs.epoch_input()
-                eng.upload(inp)
+                eng.upload(inp, *keep)
             timed = ep >= warmup
             barrier(world)
             t = time.perf_counter()
@@ -456,6 +458,27 @@ def main():
         "k_reconcile_paths_rank0": pstats,
         "gen_s": round(gen_s, 2),
     }
+    if not churn:
+        # the next epoch over the same CR set: dictionaries resident and already parsed
+        # (kdict_keep / pdict_keep = everything); a separate report, not `value`
+        eng.upload(inp, inp.kdict.n, inp.pdict.n)
+        for _ in range(2):
+            eng.run()
+            eng.sync()
+        barrier(world)
+        t = time.perf_counter()
+        rsum: dict[str, float] = {}
+        for _ in range(steps):
+            eng.run()
+            eng.sync()
+            for k, v in eng.kernel_times().items():
+                rsum[k] = rsum.get(k, 0.0) + v / steps
+        torch.cuda.synchronize()
+        el = allmax(time.perf_counter() - t, world)
+        result["epoch_dicts_parsed"] = {"ms_per_step": el / steps * 1e3, "links_per_s": links_total / el,
+                                        "kernels_ms": rsum,
+                                        "note": "same epoch re-run with kdict_keep/pdict_keep = all strings "
+                                                "(append-only interner, nothing new to parse)"}
     if diff_ms:
         result["diff_only_reconcile_ms"] = float(np.mean(diff_ms))
         result["diff_share_of_reconcile"] = float(np.mean(diff_ms)) / kavg["reconcile"]

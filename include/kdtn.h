@@ -166,6 +166,14 @@ typedef struct kdtn_epoch_in {
     kdtn_link_table desired;    /* spec.links of every topology, grouped               */
     kdtn_vni_table  vnis;
     uint32_t        pod_slice;  /* multi-GPU: pod-table entries per rank (>= topos.n); 0 = topos.n */
+    /* Append-only interning across epochs: the first kdict_keep (pdict_keep) strings are
+     * byte-identical to the previous upload's on this context, whose parsed tables (MakeVeth /
+     * addLink predicates, ParseDuration / ParseFloatPercentage / ParseRate results) are kept:
+     * only the new suffix is uploaded and each kdtn_epoch_run parses only the strings this
+     * upload added. 0 = upload and parse the whole dictionary. KDTN_EINVAL when the prefix was
+     * not parsed on this context (no run since an upload that kept fewer strings, or the
+     * arena offsets disagree). */
+    uint32_t        kdict_keep, pdict_keep;
 } kdtn_epoch_in;
 
 /* Property sets for the standalone kdtn_make_qdiscs (daemon UpdateLinks path). */

@@ -62,9 +62,13 @@ struct kdtn_ctx {
     hipStream_t stream = nullptr;
     hipStream_t comm_stream = nullptr;          // RCCL pod-status exchange (nranks > 1)
     hipEvent_t ev_fill = nullptr, ev_ag = nullptr;
-    // dictionaries
-    DevBuf kd_bytes, kd_offs, kd_bits, pd_bytes, pd_offs, pd_pct, pd_dur, pd_rate, pd_rerr;
+    // dictionaries; parsed tables persist across uploads for an append-only interner
+    // (kdtn_epoch_in.kdict_keep / pdict_keep): *_valid strings have valid parsed tables, a run
+    // parses [*_from, n) — the strings its upload added
+    DevBuf kd_bytes, kd_offs, kd_bits, pd_bytes, pd_offs, pd_pct, pd_dur, pd_rate, pd_rerr, kd_special;
     uint32_t D = 0, P = 0;
+    uint32_t kd_from = 0, pd_from = 0, kd_valid = 0, pd_valid = 0, kb_cap = 0;
+
     // topologies
     DevBuf t_ns, t_name, t_src, t_netns, t_flags, t_roff, t_noff;
     uint32_t T = 0;
@@ -139,6 +143,26 @@ int ensure(DevBuf& b, size_t bytes) {
     b.cap = bytes;
     return KDTN_OK;
 }
+// Grow b to at least `bytes`, keeping its first `keep` bytes (stream-ordered copy).
+int ensure_keep(DevBuf& b, size_t bytes, size_t keep, hipStream_t s) {
+    bytes = std::max<size_t>(bytes, 256);
+    if (b.cap >= bytes) return KDTN_OK;
+    if (!keep || !b.p) return ensure(b, bytes);
+    const size_t cap = std::max(bytes, b.cap + b.cap / 2);
+    void* np = nullptr;
+    hipError_t e = hipMalloc(&np, cap);
+    if (e != hipSuccess) {
+        std::snprintf(g_last_error, sizeof(g_last_error), "hipMalloc(%zu): %s", cap, hipGetErrorString(e));
+        return KDTN_ENOMEM;
+    }
+    HIP_TRY(hipMemcpyAsync(np, b.p, std::min(keep, b.cap), hipMemcpyDeviceToDevice, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    (void)hipFree(b.p);
+    b.p = np;
+    b.cap = cap;
+    return KDTN_OK;
+}
+
 void release(DevBuf& b) {
     if (b.p) (void)hipFree(b.p);
     b.p = nullptr;
@@ -164,6 +188,18 @@ T* dp(DevBuf& b) { return static_cast<T*>(b.p); }
 int upload_arena(kdtn_ctx* c, DevBuf& b, const void* src, size_t bytes) {
     TRY(ensure(b, bytes + 64));
     if (bytes) HIP_TRY(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, c->stream));
+    return KDTN_OK;
+}
+
+// Dictionary arena + offsets, uploading only what follows the first `keep` strings.
+int upload_dict(kdtn_ctx* c, DevBuf& bytes, DevBuf& offs, const kdtn_strtab& t, uint32_t keep) {
+    const size_t b0 = t.offs[keep], b1 = t.offs[t.n];
+    TRY(ensure_keep(bytes, b1 + 64, keep ? b0 : 0, c->stream));
+    TRY(ensure_keep(offs, ((size_t)t.n + 1) * 4, keep ? ((size_t)keep + 1) * 4 : 0, c->stream));
+    if (b1 > b0) HIP_TRY(hipMemcpyAsync(static_cast<uint8_t*>(bytes.p) + b0, t.bytes + b0, b1 - b0,
+                                        hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(static_cast<uint32_t*>(offs.p) + keep, t.offs + keep, ((size_t)t.n - keep + 1) * 4,
+                           hipMemcpyHostToDevice, c->stream));
     return KDTN_OK;
 }
 
@@ -283,15 +319,33 @@ DevTopos topo_view(kdtn_ctx* c) {
     return t;
 }
 
-// per-string parse tables of both dictionaries (c->D, c->P set)
+// per-string parse tables of both dictionaries (c->D, c->P set), keeping the parsed
+// tables of the first c->kd_valid / c->pd_valid strings. kbits holds KB_NSETS bitsets at a
+// stride of kb_cap words; growing the stride moves each set.
 int prepare_dicts(kdtn_ctx* c) {
     const uint32_t D = c->D, P = c->P;
-    c->kb_words = (uint32_t)(((uint64_t)D + 63) / 64 * 2);
-    TRY(ensure(c->kd_bits, (size_t)KB_NSETS * c->kb_words * 4 + 4));
-    TRY(ensure(c->pd_pct, (size_t)P * 4));
-    TRY(ensure(c->pd_dur, (size_t)P * 8));
-    TRY(ensure(c->pd_rate, (size_t)P * 8));
-    TRY(ensure(c->pd_rerr, (size_t)nblocks(P) * BLOCK / 8));
+    hipStream_t s = c->stream;
+    const uint32_t need = (uint32_t)(((uint64_t)D + 63) / 64 * 2);
+    if (need > c->kb_cap || !c->kd_bits.p) {
+        const uint32_t cap = std::max<uint32_t>(need, c->kd_valid ? c->kb_cap + c->kb_cap / 2 : 0);
+        DevBuf nb;
+        TRY(ensure(nb, (size_t)KB_NSETS * cap * 4 + 4));
+        const uint32_t keepw = (uint32_t)(((uint64_t)c->kd_valid + 63) / 64 * 2);
+        if (keepw && c->kd_bits.p)
+            HIP_TRY(hipMemcpy2DAsync(nb.p, (size_t)cap * 4, c->kd_bits.p, (size_t)c->kb_cap * 4, (size_t)keepw * 4,
+                                     KB_NSETS, hipMemcpyDeviceToDevice, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        release(c->kd_bits);
+        c->kd_bits = nb;
+        c->kb_cap = cap;
+    }
+    c->kb_words = c->kb_cap;
+    const size_t pv = c->pd_valid;
+    TRY(ensure_keep(c->pd_pct, (size_t)P * 4, pv * 4, s));
+    TRY(ensure_keep(c->pd_dur, (size_t)P * 8, pv * 8, s));
+    TRY(ensure_keep(c->pd_rate, (size_t)P * 8, pv * 8, s));
+    TRY(ensure_keep(c->pd_rerr, (size_t)nblocks(P) * BLOCK / 8, (pv + 63) / 64 * 8, s));
+    TRY(ensure(c->kd_special, 64));
     return KDTN_OK;
 }
 
@@ -510,13 +564,31 @@ int kdtn_epoch_upload(kdtn_ctx* c, const kdtn_epoch_in* in) {
     const uint32_t slice = in->pod_slice ? in->pod_slice : T.n;
     if (slice < T.n) return KDTN_EINVAL;
 
+    // append-only dictionaries: the first *_keep strings equal the previous upload's (the
+    // arena offset of the kept prefix is checked against the device copy)
+    const uint32_t kk = in->kdict_keep, pk = in->pdict_keep;
+    uint32_t dev_off[2] = {0, 0};
+    if (kk <= c->kd_valid && kk && kk <= D)
+        HIP_TRY(hipMemcpyAsync(dev_off, dp<uint32_t>(c->kd_offs) + kk, 4, hipMemcpyDeviceToHost, c->stream));
+    if (pk <= c->pd_valid && pk && pk <= P)
+        HIP_TRY(hipMemcpyAsync(dev_off + 1, dp<uint32_t>(c->pd_offs) + pk, 4, hipMemcpyDeviceToHost, c->stream));
+    if (kk || pk) HIP_TRY(hipStreamSynchronize(c->stream));
+    if (kk > D || pk > P || kk > c->kd_valid || pk > c->pd_valid || (kk && in->kdict.offs[kk] != dev_off[0]) ||
+        (pk && in->pdict.offs[pk] != dev_off[1])) {
+        std::snprintf(g_last_error, sizeof(g_last_error),
+                      "kdict_keep %u / pdict_keep %u: not a prefix of the previous upload's parsed dictionaries "
+                      "(%u / %u strings)", kk, pk, c->kd_valid, c->pd_valid);
+        return KDTN_EINVAL;
+    }
     c->D = D;
     c->P = P;
     c->T = T.n;
-    TRY(upload_arena(c, c->kd_bytes, in->kdict.bytes, in->kdict.offs[D]));
-    TRY(upload(c, c->kd_offs, in->kdict.offs, (size_t)(D + 1) * 4));
-    TRY(upload_arena(c, c->pd_bytes, in->pdict.bytes, in->pdict.offs[P]));
-    TRY(upload(c, c->pd_offs, in->pdict.offs, (size_t)(P + 1) * 4));
+    c->kd_valid = kk;
+    c->pd_valid = pk;
+    c->kd_from = kk;
+    c->pd_from = pk;
+    TRY(upload_dict(c, c->kd_bytes, c->kd_offs, in->kdict, kk));
+    TRY(upload_dict(c, c->pd_bytes, c->pd_offs, in->pdict, pk));
     TRY(prepare_dicts(c));
 
     TRY(upload(c, c->t_ns, T.ns, (size_t)T.n * 4));
@@ -547,7 +619,7 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
     hipStream_t s = c->stream;
     (void)hipEventRecord(c->ev[0], s);
     uint32_t* misc = dp<uint32_t>(c->misc);
-    HIP_TRY(hipMemsetAsync(misc, 0xFF, 64, s));                       // special ids = 0xFFFFFFFF
+    HIP_TRY(hipMemsetAsync(misc, 0xFF, 64, s));                       // first_partial etc. = 0xFFFFFFFF
     HIP_TRY(hipMemsetAsync(c->sync.p, 0, sync_bytes(c->nwg), s));    // ticket, error, look-back
 
     const DevTopos T = topo_view(c);
@@ -580,24 +652,38 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
     } else if (resolve) {
         timer_mark(c, "pods_fill");
     }
-    // dictionaries
-    if (c->D) {
-        const uint8_t* kb = dp<uint8_t>(c->kd_bytes);
-        const uint32_t* ko = dp<uint32_t>(c->kd_offs);
-        uint32_t* bits = dp<uint32_t>(c->kd_bits);
+    // dictionaries: the strings this upload added (all of them unless kdict_keep /
+    // pdict_keep), from a multiple of 64 so every wave writes whole predicate words
+    uint32_t* special = dp<uint32_t>(c->kd_special);
+    {
+        const uint32_t k0 = c->kd_from & ~63u;
+        k_special_clip<<<1, 64, 0, s>>>(special, k0);                 // ids >= k0 are recomputed
+        if (c->D > k0) {
+            const uint8_t* kb = dp<uint8_t>(c->kd_bytes);
+            const uint32_t* ko = dp<uint32_t>(c->kd_offs);
+            uint32_t* bits = dp<uint32_t>(c->kd_bits);
+            const uint32_t nk = c->D - k0;
 #if KDTN_PROFILING
-        int sub = 1;                                                   // strings per thread (2, 4: slower)
-        if (const char* ev = std::getenv("KDTN_KD_SUB")) sub = std::atoi(ev);
-        if (sub == 4) k_kdict_flags<4><<<nblocks(c->D, BLOCK * 4), BLOCK, 0, s>>>(kb, ko, c->D, bits, c->kb_words, misc);
-        else if (sub == 2) k_kdict_flags<2><<<nblocks(c->D, BLOCK * 2), BLOCK, 0, s>>>(kb, ko, c->D, bits, c->kb_words, misc);
-        else
+            int sub = 1;                                               // strings per thread (2, 4: slower)
+            if (const char* ev = std::getenv("KDTN_KD_SUB")) sub = std::atoi(ev);
+            if (sub == 4) k_kdict_flags<4><<<nblocks(nk, BLOCK * 4), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
+            else if (sub == 2) k_kdict_flags<2><<<nblocks(nk, BLOCK * 2), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
+            else
 #endif
-        k_kdict_flags<1><<<nblocks(c->D), BLOCK, 0, s>>>(kb, ko, c->D, bits, c->kb_words, misc);
+            k_kdict_flags<1><<<nblocks(nk), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
+        }
     }
     timer_mark(c, "kdict_parse");
-    if (c->P) k_pdict_parse<<<nblocks(c->P), BLOCK, 0, s>>>(dp<uint8_t>(c->pd_bytes), dp<uint32_t>(c->pd_offs),
-                                                         c->P, c->cfg.tick_in_usec, dp<uint32_t>(c->pd_pct),
-                                                         dp<uint2>(c->pd_dur), dp<uint2>(c->pd_rate), dp<uint32_t>(c->pd_rerr));
+    {
+        const uint32_t p0 = c->pd_from & ~63u;
+        if (c->P > p0)
+            k_pdict_parse<<<nblocks(c->P - p0), BLOCK, 0, s>>>(dp<uint8_t>(c->pd_bytes), dp<uint32_t>(c->pd_offs), p0,
+                                                               c->P, c->cfg.tick_in_usec, dp<uint32_t>(c->pd_pct),
+                                                               dp<uint2>(c->pd_dur), dp<uint2>(c->pd_rate),
+                                                               dp<uint32_t>(c->pd_rerr));
+    }
+    c->kd_valid = c->D;
+    c->pd_valid = c->P;
     timer_mark(c, "pdict_parse");
     if (resolve) {
         if (exchange) HIP_TRY(hipStreamWaitEvent(s, c->ev_ag, 0));   // exchange not hidden by the parses
@@ -641,7 +727,7 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         tb.vnis = dp<uint4>(c->v_ents);
         tb.vni_slots = dp<uint32_t>(c->v_slots);
         tb.vni_mask = c->V ? c->vni_mask : 0;
-        tb.special = misc;
+        tb.special = special;
         tb.vxlan_base = c->cfg.vxlan_base;
         RecOut o;
         o.action = dp<uint8_t>(c->action);
@@ -859,6 +945,8 @@ int kdtn_make_qdiscs(kdtn_ctx* c, const kdtn_strtab* pdict, const kdtn_props_tab
     const uint32_t P = pdict->n, n = props->n;
     for (int k = 0; k < KDTN_NPROP; ++k) TRY(check_ids(props->prop[k], n, P, "props"));
     if (n && !props->gap) return KDTN_EINVAL;
+    c->pd_valid = c->pd_from = 0;                          // this call owns the property tables now
+    c->uploaded = false;
     TRY(upload_arena(c, c->pd_bytes, pdict->bytes, pdict->offs[P]));
     TRY(upload(c, c->pd_offs, pdict->offs, (size_t)(P + 1) * 4));
     TRY(ensure(c->pd_pct, (size_t)P * 4));
@@ -877,7 +965,7 @@ int kdtn_make_qdiscs(kdtn_ctx* c, const kdtn_strtab* pdict, const kdtn_props_tab
     TRY(upload_links(c, c->des, L, 1, P, "props"));
     TRY(ensure(c->add_qdisc, (size_t)std::max<uint32_t>(n, 1) * 72));
     hipStream_t s = c->stream;
-    k_pdict_parse<<<nblocks(P), BLOCK, 0, s>>>(dp<uint8_t>(c->pd_bytes), dp<uint32_t>(c->pd_offs), P,
+    k_pdict_parse<<<nblocks(P), BLOCK, 0, s>>>(dp<uint8_t>(c->pd_bytes), dp<uint32_t>(c->pd_offs), 0u, P,
                                                c->cfg.tick_in_usec, dp<uint32_t>(c->pd_pct),
                                                dp<uint2>(c->pd_dur), dp<uint2>(c->pd_rate), dp<uint32_t>(c->pd_rerr));
     DevTables tb{};
@@ -1253,6 +1341,7 @@ int kdtn_json_ingest(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest_info* 
     c->j_info = kdtn_ingest_info{};
     c->uploaded = false;
     c->ran = false;
+    c->kd_valid = c->pd_valid = c->kd_from = c->pd_from = 0;   // the document's dictionaries are new
     c->n_ev = 0;
     (void)hipEventRecord(c->ev[0], s);
     const uint32_t nb = c->j_nb;

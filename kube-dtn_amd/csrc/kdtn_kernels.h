@@ -53,7 +53,7 @@ enum : int { SPECIAL_DEFAULT = 0, SPECIAL_LOCALHOST = 4, MISC_FIRST_PARTIAL = 8,
 constexpr uint32_t POD_SPEC_NIL = 0x80000000u, POD_PHYSICAL = 0x40000000u, POD_INDEX = 0x3FFFFFFFu;
 
 // record flags
-enum : uint8_t { RF_DEL = 1, RF_UPD = 2, RF_ADD = 4 };
+enum : uint8_t { RF_DEL = 1, RF_UPD = 2, RF_ADD = 4, RF_MATCHED = 0x80 };   // MATCHED: CalcDiff scratch
 
 // Link store: tiles of 64 records (AoSoA). A tile holds, for its 64 records, each u32 column
 // as 256 contiguous bytes (key[0..6], prop[0..11], gap) followed by the i64 uid column
@@ -181,10 +181,11 @@ struct RecWork {
     uint32_t nwg;
 };
 
+__global__ void k_special_clip(uint32_t* special, uint32_t k0);
 template <int SUB>
-__global__ void k_kdict_flags(const uint8_t* bytes, const uint32_t* offs, uint32_t n,
+__global__ void k_kdict_flags(const uint8_t* bytes, const uint32_t* offs, uint32_t first, uint32_t n,
                               uint32_t* kbits, uint32_t kb_words, uint32_t* special);
-__global__ void k_pdict_parse(const uint8_t* bytes, const uint32_t* offs, uint32_t n, double tick,
+__global__ void k_pdict_parse(const uint8_t* bytes, const uint32_t* offs, uint32_t first, uint32_t n, double tick,
                               uint32_t* ppct, uint2* pdur, uint2* prate, uint32_t* rate_err);
 __global__ void k_pods_fill(DevTopos T, uint32_t slice, uint32_t rank_base, uint4* pods);
 __global__ void k_pod_direct_scatter(const uint4* pods, uint32_t total, const uint32_t* phys_bits,

@@ -28,32 +28,38 @@ KD_INLINE uint64_t hash64(uint64_t x) {
     return x;
 }
 
-// 32-bit hash of the EqualWithoutProperties key (7 string ids + uid).
-KD_INLINE uint32_t key_hash(const DevLinks& L, uint32_t i) {
+// EqualWithoutProperties key (7 string ids + uid as two words) and the DeepEqual'd
+// properties (12 ids + Gap) of one record, loaded with independent loads (no short-circuit
+// chains: every load of a comparison is in flight at once).
+constexpr int KEYW = KDTN_NKEY + 2, PROPW = KDTN_NPROP + 1;
+KD_INLINE void load_key(const DevLinks& L, uint32_t i, uint32_t* k) {
+    const uint32_t* r = L.rec(i);
+#pragma unroll
+    for (int c = 0; c < KDTN_NKEY; ++c) k[c] = r[(COL_KEY0 + c) * TILE_RECS];
+    const uint64_t u = (uint64_t)L.uid_at<false>(r, i);
+    k[KDTN_NKEY] = (uint32_t)u;
+    k[KDTN_NKEY + 1] = (uint32_t)(u >> 32);
+}
+KD_INLINE void load_props(const DevLinks& L, uint32_t i, uint32_t* p) {
+    const uint32_t* r = L.rec(i);
+#pragma unroll
+    for (int c = 0; c < KDTN_NPROP; ++c) p[c] = r[(COL_PROP0 + c) * TILE_RECS];
+    p[KDTN_NPROP] = r[COL_GAP * TILE_RECS];
+}
+template <int W>
+KD_INLINE bool words_eq(const uint32_t* a, const uint32_t* b) {
+    uint32_t d = 0;
+#pragma unroll
+    for (int c = 0; c < W; ++c) d |= a[c] ^ b[c];
+    return d == 0;
+}
+// 32-bit hash of the EqualWithoutProperties key (controllers/topology_controller.go:342-351);
+// interned ids: equal ids ⇔ equal strings.
+KD_INLINE uint32_t key_hash_w(const uint32_t* k) {
     uint32_t h = 0x9E3779B9u;
 #pragma unroll
-    for (int k = 0; k < KDTN_NKEY; ++k) h = mix32(h, L.key(k, i));
-    const uint64_t u = (uint64_t)L.uid(i);
-    h = mix32(h, (uint32_t)u);
-    h = mix32(h, (uint32_t)(u >> 32));
+    for (int c = 0; c < KEYW; ++c) h = mix32(h, k[c]);
     return fin32(h);
-}
-
-// EqualWithoutProperties (controllers/topology_controller.go:342-351); interned ids:
-// equal ids ⇔ equal strings.
-KD_INLINE bool key_eq(const DevLinks& A, uint32_t i, const DevLinks& B, uint32_t j) {
-    bool eq = A.uid(i) == B.uid(j);
-#pragma unroll
-    for (int k = 0; k < KDTN_NKEY; ++k) eq = eq && (A.key(k, i) == B.key(k, j));
-    return eq;
-}
-
-// reflect.DeepEqual(old.Properties, new.Properties) (:294): 12 strings + Gap.
-KD_INLINE bool props_eq(const DevLinks& A, uint32_t i, const DevLinks& B, uint32_t j) {
-    bool eq = A.gap(i) == B.gap(j);
-#pragma unroll
-    for (int k = 0; k < KDTN_NPROP; ++k) eq = eq && (A.prop(k, i) == B.prop(k, j));
-    return eq;
 }
 
 // Table gather with a 32-bit byte offset from a uniform base: selects the global_load
@@ -219,14 +225,22 @@ KD_INLINE uint32_t kdict_bits(const uint8_t* bytes, uint32_t b, uint32_t len, co
     return f;
 }
 
+// Special key-string ids (SPECIAL_DEFAULT, SPECIAL_LOCALHOST) persist across uploads of an
+// append-only dictionary; before a parse from string k0 the ids >= k0 are forgotten.
+__global__ void k_special_clip(uint32_t* special, uint32_t k0) {
+    const int t = threadIdx.x;
+    if ((t == SPECIAL_DEFAULT || t == SPECIAL_LOCALHOST) && special[t] >= k0) special[t] = 0xFFFFFFFFu;
+}
+
 // SUB strings per thread (block covers SUB*BLOCK consecutive strings): every offset load
 // of the thread's strings is issued, then every string's 7 dwords, then the parses run —
 // the kernel is latency-bound, so a wave keeps SUB strings' round trips in flight at once.
+// Strings [first, n) (first a multiple of 64: every wave writes whole predicate words).
 template <int SUB>
 __global__ void __launch_bounds__(BLOCK) k_kdict_flags(const uint8_t* bytes, const uint32_t* offs,
-                                                       uint32_t n, uint32_t* kbits, uint32_t kb_words,
-                                                       uint32_t* special) {
-    const uint32_t i0 = blockIdx.x * BLOCK * SUB + threadIdx.x;
+                                                       uint32_t first, uint32_t n, uint32_t* kbits,
+                                                       uint32_t kb_words, uint32_t* special) {
+    const uint32_t i0 = first + blockIdx.x * BLOCK * SUB + threadIdx.x;
     uint32_t b[SUB], len[SUB];
 #pragma unroll
     for (int s = 0; s < SUB; ++s) {
@@ -261,10 +275,10 @@ __global__ void __launch_bounds__(BLOCK) k_kdict_flags(const uint8_t* bytes, con
         }
     }
 }
-template __global__ void k_kdict_flags<1>(const uint8_t*, const uint32_t*, uint32_t, uint32_t*, uint32_t, uint32_t*);
+template __global__ void k_kdict_flags<1>(const uint8_t*, const uint32_t*, uint32_t, uint32_t, uint32_t*, uint32_t, uint32_t*);
 #if KDTN_PROFILING
-template __global__ void k_kdict_flags<2>(const uint8_t*, const uint32_t*, uint32_t, uint32_t*, uint32_t, uint32_t*);
-template __global__ void k_kdict_flags<4>(const uint8_t*, const uint32_t*, uint32_t, uint32_t*, uint32_t, uint32_t*);
+template __global__ void k_kdict_flags<2>(const uint8_t*, const uint32_t*, uint32_t, uint32_t, uint32_t*, uint32_t, uint32_t*);
+template __global__ void k_kdict_flags<4>(const uint8_t*, const uint32_t*, uint32_t, uint32_t, uint32_t*, uint32_t, uint32_t*);
 #endif
 
 KD_INLINE void pdict_parse_one(const uint8_t* s, uint32_t len, double tick, uint32_t* pct_out,
@@ -280,11 +294,12 @@ KD_INLINE void pdict_parse_one(const uint8_t* s, uint32_t len, double tick, uint
     *rate_bad = !rok;
 }
 
+// Strings [first, n) (first a multiple of 64: every wave writes whole rate_err words).
 __global__ void __launch_bounds__(BLOCK) k_pdict_parse(const uint8_t* bytes, const uint32_t* offs,
-                                                       uint32_t n, double tick, uint32_t* ppct,
+                                                       uint32_t first, uint32_t n, double tick, uint32_t* ppct,
                                                        uint2* pdur, uint2* prate, uint32_t* rate_err) {
     __shared__ uint4 buf[STAGE / 16];
-    const uint32_t s0 = blockIdx.x * BLOCK, s1 = min(s0 + BLOCK, n);
+    const uint32_t s0 = first + blockIdx.x * BLOCK, s1 = min(s0 + BLOCK, n);
     uint32_t a0;
     const bool staged = stage_slice(bytes, offs, s0, s1, buf, &a0) != nullptr;
     __syncthreads();
@@ -871,7 +886,8 @@ __device__ void diff_window(RecShared& s, int tb, int te, const DevLinks& O, con
     const uint32_t no = wo1 - wo0, nn = wn1 - wn0, tot = no + nn;
     const int tid = threadIdx.x;
 
-    // A. segment of every record; key hashes where comparisons are needed
+    // A. segment of every record; key hashes of the new records where comparisons are
+    //    needed (an old record hashes its own key in B); new records' marks cleared
     for (uint32_t r = tid; r < tot; r += BLOCK) {
         const bool old = r < no;
         const uint32_t idx = old ? wo0 + r : wn0 + (r - no);
@@ -880,26 +896,44 @@ __device__ void diff_window(RecShared& s, int tb, int te, const DevLinks& O, con
             tt = find_seg(old ? s.ooff : s.noff, tb, te, idx);
             lt[r] = (uint8_t)tt;
         }
-        if (need_cmp(s, tt)) hsh[r] = old ? key_hash(O, idx) : key_hash(N, idx);
+        if (!old) {
+            if (need_cmp(s, tt)) {
+                uint32_t k[KEYW];
+                load_key(N, idx, k);
+                hsh[r] = key_hash_w(k);
+            }
+            flg[r] = 0;
+        }
     }
     __syncthreads();
 
-    // B. old side: first key-equal new record (CalcDiff :289-303) + positional DeepEqual (:77)
+    // B. old side: first key-equal new record (CalcDiff :289-303) + positional DeepEqual (:77).
+    //    The old record's key and properties are loaded once (coalesced: consecutive threads,
+    //    consecutive records); a candidate is verified with all its loads in flight together.
     for (uint32_t r = tid; r < no; r += BLOCK) {
         const int tt = lt ? lt[r] : tb;
         uint8_t f = RF_DEL;
         if (need_cmp(s, tt)) {
             const uint32_t i = wo0 + r;
-            const uint32_t h = hsh[r];
+            uint32_t ki[KEYW], pi[PROPW];
+            load_key(O, i, ki);
+            load_props(O, i, pi);
+            const uint32_t h = key_hash_w(ki);
             const uint32_t ns_ = s.noff[tt], ne_ = s.noff[tt + 1];
             uint32_t first = 0xFFFFFFFFu;
             for (uint32_t j = ns_; j < ne_; ++j) {
-                if (hsh[no + (j - wn0)] == h && key_eq(O, i, N, j)) { first = j; break; }
+                if (hsh[no + (j - wn0)] != h) continue;
+                uint32_t kj[KEYW];
+                load_key(N, j, kj);
+                if (words_eq<KEYW>(ki, kj)) { first = j; break; }
             }
             if (first != 0xFFFFFFFFu) {
-                if (!props_eq(O, i, N, first)) {
+                flg[no + (first - wn0)] = RF_MATCHED;        // j is some old record's first match
+                uint32_t pj[PROPW];
+                load_props(N, first, pj);
+                if (!words_eq<PROPW>(pi, pj)) {
                     f = RF_UPD;
-                    if (tgt16) tgt16[r] = (uint16_t)(first - wn_base);
+                    if (tgt16) tgt16[r] = (uint16_t)(first - wn0);
                     else otarget[i] = first;
                 } else {
                     f = 0;
@@ -909,25 +943,47 @@ __device__ void diff_window(RecShared& s, int tb, int te, const DevLinks& O, con
             if (ko == kn) {
                 const uint32_t jp = ns_ + (i - s.ooff[tt]);
                 bool eq;
-                if (first == jp) eq = (f == 0);
-                else eq = hsh[no + (jp - wn0)] == h && key_eq(O, i, N, jp) && props_eq(O, i, N, jp);
+                if (first == jp) {
+                    eq = (f == 0);
+                } else if (hsh[no + (jp - wn0)] != h) {
+                    eq = false;
+                } else {
+                    uint32_t kj[KEYW], pj[PROPW];
+                    load_key(N, jp, kj);
+                    load_props(N, jp, pj);
+                    eq = words_eq<KEYW>(ki, kj) && words_eq<PROPW>(pi, pj);
+                }
                 if (!eq) s.dirty[tt] = 1;
             }
         }
         flg[r] = f;
     }
-    // C. new side: any key-equal old record (CalcDiff :305-316)
+    __syncthreads();
+
+    // C. new side: any key-equal old record (CalcDiff :305-316). Key equality is an
+    //    equivalence: j has one iff it is some old record's first match (marked in B) or
+    //    equals an earlier marked new record of its topology (a duplicate key in spec).
     for (uint32_t r = tid; r < nn; r += BLOCK) {
         const int tt = lt ? lt[no + r] : tb;
         uint8_t f = RF_ADD;
         if (need_cmp(s, tt)) {
-            const uint32_t j = wn0 + r;
-            const uint32_t h = hsh[no + r];
-            for (uint32_t i = s.ooff[tt]; i < s.ooff[tt + 1]; ++i) {
-                if (hsh[i - wo0] == h && key_eq(O, i, N, j)) { f = 0; break; }
+            if (flg[no + r] & RF_MATCHED) {
+                f = 0;
+            } else {
+                const uint32_t j = wn0 + r;
+                const uint32_t h = hsh[no + r];
+                bool have = false;
+                for (uint32_t j2 = s.noff[tt]; j2 < j && !have; ++j2) {
+                    if (hsh[no + (j2 - wn0)] != h || !(flg[no + (j2 - wn0)] & RF_MATCHED)) continue;
+                    uint32_t ka[KEYW], kb[KEYW];
+                    load_key(N, j, ka);
+                    load_key(N, j2, kb);
+                    have = words_eq<KEYW>(ka, kb);
+                }
+                if (have) f = 0;
             }
         }
-        flg[no + r] = f;
+        flg[no + r] = f | (flg[no + r] & RF_MATCHED);    // other threads still read the mark
     }
     __syncthreads();
 
@@ -938,7 +994,7 @@ __device__ void diff_window(RecShared& s, int tb, int te, const DevLinks& O, con
     // E. mask by action; per-topology counts
     for (uint32_t r = tid; r < tot; r += BLOCK) {
         const int tt = lt ? lt[r] : tb;
-        uint8_t f = flg[r];
+        uint8_t f = flg[r] & (RF_DEL | RF_UPD | RF_ADD);
         if (s.act[tt] != KDTN_ACT_DIFF) f = 0;
         flg[r] = f;
         if (f & RF_DEL) atomicAdd(&s.tcnt[0][tt], 1u);

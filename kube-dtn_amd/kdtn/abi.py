@@ -66,7 +66,7 @@ class VniTable(C.Structure):
 class EpochIn(C.Structure):
     _fields_ = [("kdict", Strtab), ("pdict", Strtab), ("topos", TopoTable),
                 ("realised", LinkTable), ("desired", LinkTable), ("vnis", VniTable),
-                ("pod_slice", C.c_uint32)]
+                ("pod_slice", C.c_uint32), ("kdict_keep", C.c_uint32), ("pdict_keep", C.c_uint32)]
 
 
 class PropsTable(C.Structure):

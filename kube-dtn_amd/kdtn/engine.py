@@ -178,8 +178,12 @@ class Engine:
         _check(lib().kdtn_set_stream(self._ctx, C.c_void_p(stream_handle or 0)), "kdtn_set_stream")
 
     # ---- epoch -----------------------------------------------------------------------
-    def upload(self, inp: EpochInput) -> None:
+    def upload(self, inp: EpochInput, kdict_keep: int = 0, pdict_keep: int = 0) -> None:
+        """kdtn_epoch_upload. kdict_keep / pdict_keep: the dictionaries extend the previous
+        upload's first that many strings (append-only interning): only the suffix is
+        uploaded and parsed."""
         cin = inp.to_c()
+        cin.kdict_keep, cin.pdict_keep = kdict_keep, pdict_keep
         _check(lib().kdtn_epoch_upload(self._ctx, C.byref(cin)), "kdtn_epoch_upload")
         self._T = inp.topos.n
         self._caps = (inp.realised.n, inp.desired.n, inp.realised.n)

@@ -436,3 +436,40 @@ def test_reach_rule_scenario_and_error_heavy_epochs(engine):
         wa, wto = O.tc_epoch(inp, ora)
         assert np.array_equal(toff, wto) and arena.tobytes() == wa.tobytes(), k
     assert (ora.add_res["remote_err"] == abi.E_REMOTE_CIDR).any()
+
+
+def test_append_only_dictionaries_keep_parsed_tables(engine):
+    """kdtn_epoch_in.kdict_keep / pdict_keep: consecutive epochs whose interners only grow
+    upload and parse only the new strings; the outputs equal a fresh full upload's and the
+    oracle's. A later upload that keeps a shorter prefix (strings after it replaced,
+    "localhost" / "default" moved) recomputes them; keeping more than was parsed fails."""
+    from kdtn.abi import EINVAL
+    from kdtn.engine import KdtnError
+    kd, pd = Interner(), Interner()
+    prev = None
+    for seed in (41, 42, 43):
+        topos, vnis = __import__("helpers").random_epoch(seed, T=120)
+        inp = pack(topos, vnis, kdict=kd, pdict=pd)
+        keep = (prev.kdict.n, prev.pdict.n) if prev is not None else (0, 0)
+        engine.upload(inp, *keep)
+        engine.run()
+        engine.sync()
+        got = engine.download()
+        assert_same(got, O.reconcile(inp, tick=TICK), f"keep seed {seed}")
+        prev = inp
+    with pytest.raises(KdtnError) as e:                      # more than the parsed prefix
+        engine.upload(prev, prev.kdict.n + 1, 0)
+    assert e.value.code == EINVAL
+    # a shorter kept prefix, then strings that differ from the previous suffix
+    topos, vnis = __import__("helpers").random_epoch(44, T=80)
+    kd2, pd2 = Interner(), Interner()
+    for i in range(min(40, len(kd) - 1)):
+        kd2(prev.kdict.get(i + 1))
+    for i in range(min(10, len(pd) - 1)):
+        pd2(prev.pdict.get(i + 1))
+    kd2("zz-new"), kd2("localhost"), kd2("default")
+    inp = pack(topos, vnis, kdict=kd2, pdict=pd2)
+    engine.upload(inp, 41, 11)
+    engine.run()
+    engine.sync()
+    assert_same(engine.download(), O.reconcile(inp, tick=TICK), "shorter prefix")
