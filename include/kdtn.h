@@ -493,8 +493,9 @@ int kdtn_pods_import(kdtn_ctx* ctx, const kdtn_pod_row* rows, uint64_t n);   /* 
 
 /* ---- profiling hooks: per-kernel HIP-event times of the last epoch_run (ms) -------- */
 int kdtn_last_kernel_times(kdtn_ctx* ctx, const char** names, float* ms, int cap);
-/* Per-workgroup phase timestamps of k_reconcile (100 MHz clock; 6 words per workgroup:
- * entry, topologies loaded, counts done, batch bases known, end, XCC_ID<<32|HW_ID) of the
+/* Per-workgroup phase timestamps of k_reconcile (100 MHz clock; 8 words per workgroup:
+ * entry, topologies loaded, counts done, batch bases known, end, XCC_ID<<32|HW_ID, CalcDiff
+ * window phase A done, phase B done) of the
  * last epoch run with KDTN_VARIANT bit 16 set. Returns the number of words copied. */
 int kdtn_debug_wg_trace(kdtn_ctx* ctx, uint64_t* out, uint32_t cap);
 

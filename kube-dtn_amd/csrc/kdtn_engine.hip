@@ -763,37 +763,19 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
             c->traced = true;
         }
         switch (variant) {
-        case 0: k_reconcile<0><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
-        case 515: k_reconcile<515><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
-        case 521: k_reconcile<521><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
-        case 523: k_reconcile<523><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
-        case 2: k_reconcile<2><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
-        case 3: k_reconcile<3><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
-        case 4: k_reconcile<4><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
-        case 5: k_reconcile<5><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
-        case 9: k_reconcile<9><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
-        case 33: k_reconcile<33><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
-        case 65: k_reconcile<65><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
-        case 101: k_reconcile<101><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
-        case 113: k_reconcile<113><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
-        case 97: k_reconcile<97><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
-        case 17: k_reconcile<17><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
-        case 513: k_reconcile<513><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
-        case 1025: k_reconcile<1025><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
-        case 1537: k_reconcile<1537><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
-        case 545: k_reconcile<545><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
-        case 641: k_reconcile<641><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
-        case 529: k_reconcile<529><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
-        case 129: k_reconcile<129><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
-        case 257: k_reconcile<257><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
-        case 11: k_reconcile<11><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
-        case 1: k_reconcile<1><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
+#define KDTN_VARIANT_CASE(V) \
+        case V: k_reconcile<V><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
+        KDTN_PROFILING_VARIANTS(KDTN_VARIANT_CASE)
+#undef KDTN_VARIANT_CASE
         default:
             k_reconcile<DEFAULT_VARIANT><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w);
             break;
         }
 #else
-        k_reconcile<DEFAULT_VARIANT><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w);
+        if (c->real.n && c->des.n)               // CalcDiff windows: the comparison-heavy build
+            k_reconcile<DEFAULT_VARIANT | VAR_DIFF><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w);
+        else
+            k_reconcile<DEFAULT_VARIANT><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w);
 #endif
         timer_mark(c, "reconcile");
     } else {

@@ -878,9 +878,11 @@ KD_INLINE uint8_t topo_action(const RecShared& s, int tt) {
 // window: old part [0, no) then new part [no, no+nn)). hsh/flg are LDS (lt != nullptr,
 // tgt16 valid) or global scratch (single topology; targets go to wk.otarget). Leaves the
 // MASKED flag of every window record in flg and accumulates per-topology counts.
+// TR (profiling trace build): phase timestamps into tr[6] (A done) and tr[7] (B done).
+template <bool TR>
 __device__ void diff_window(RecShared& s, int tb, int te, const DevLinks& O, const DevLinks& N,
                             uint32_t* hsh, uint8_t* flg, uint8_t* lt, uint16_t* tgt16,
-                            uint32_t* otarget, uint32_t wn_base) {
+                            uint32_t* otarget, uint32_t wn_base, unsigned long long* tr = nullptr) {
     const uint32_t wo0 = s.ooff[tb], wo1 = s.ooff[te];
     const uint32_t wn0 = s.noff[tb], wn1 = s.noff[te];
     const uint32_t no = wo1 - wo0, nn = wn1 - wn0, tot = no + nn;
@@ -898,14 +900,20 @@ __device__ void diff_window(RecShared& s, int tb, int te, const DevLinks& O, con
         }
         if (!old) {
             if (need_cmp(s, tt)) {
-                uint32_t k[KEYW];
+                uint32_t k[KEYW], p[PROPW];
                 load_key(N, idx, k);
+                load_props(N, idx, p);               // warms L2 for B's candidate loads
+#pragma unroll
+                for (int c = 0; c < PROPW; ++c) asm volatile("" ::"v"(p[c]));
                 hsh[r] = key_hash_w(k);
             }
             flg[r] = 0;
         }
     }
     __syncthreads();
+    if constexpr (TR) {
+        if (tid == 0) tr[6] = __builtin_amdgcn_s_memrealtime();
+    }
 
     // B. old side: first key-equal new record (CalcDiff :289-303) + positional DeepEqual (:77).
     //    The old record's key and properties are loaded once (coalesced: consecutive threads,
@@ -921,16 +929,16 @@ __device__ void diff_window(RecShared& s, int tb, int te, const DevLinks& O, con
             const uint32_t h = key_hash_w(ki);
             const uint32_t ns_ = s.noff[tt], ne_ = s.noff[tt + 1];
             uint32_t first = 0xFFFFFFFFu;
+            uint32_t pj[PROPW];
             for (uint32_t j = ns_; j < ne_; ++j) {
                 if (hsh[no + (j - wn0)] != h) continue;
                 uint32_t kj[KEYW];
                 load_key(N, j, kj);
+                load_props(N, j, pj);                        // L2-warm: key and props in one trip
                 if (words_eq<KEYW>(ki, kj)) { first = j; break; }
             }
             if (first != 0xFFFFFFFFu) {
                 flg[no + (first - wn0)] = RF_MATCHED;        // j is some old record's first match
-                uint32_t pj[PROPW];
-                load_props(N, first, pj);
                 if (!words_eq<PROPW>(pi, pj)) {
                     f = RF_UPD;
                     if (tgt16) tgt16[r] = (uint16_t)(first - wn0);
@@ -959,6 +967,9 @@ __device__ void diff_window(RecShared& s, int tb, int te, const DevLinks& O, con
         flg[r] = f;
     }
     __syncthreads();
+    if constexpr (TR) {
+        if (tid == 0) tr[7] = __builtin_amdgcn_s_memrealtime();
+    }
 
     // C. new side: any key-equal old record (CalcDiff :305-316). Key equality is an
     //    equivalence: j has one iff it is some old record's first match (marked in B) or
@@ -1121,7 +1132,21 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
     const int tid = threadIdx.x;
     unsigned long long t_entry = 0;
     if constexpr ((V & VAR_TRACE) != 0) t_entry = __builtin_amdgcn_s_memrealtime();
-    if (tid == 0) s.ticket = atomicAdd(&wk.sync[0], 1u);    // dispatch order → look-back order
+    if (tid == 0) {
+        if constexpr ((V & VAR_XCD) != 0) {
+            // every chunk emits all of its records (no look-back anywhere): a static map that
+            // gives XCD x (= blockIdx % 8) the contiguous chunks [start(x), start(x) + count(x)),
+            // so an XCD's L2 sees the dictionary ids of its own range of links
+            if (*wk.first_partial >= wk.nwg) {
+                const uint32_t x = blockIdx.x & 7u, k = blockIdx.x >> 3, q = wk.nwg >> 3, r = wk.nwg & 7u;
+                s.ticket = x * q + min(x, r) + k;
+            } else {
+                s.ticket = atomicAdd(&wk.sync[0], 1u);
+            }
+        } else {
+            s.ticket = atomicAdd(&wk.sync[0], 1u);      // dispatch order → look-back order
+        }
+    }
     __syncthreads();
     const uint32_t wg = s.ticket;
     if constexpr ((V & VAR_TRACE) != 0) {
@@ -1176,18 +1201,21 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
         }
         __syncthreads();
     } else if (fast) {
-        diff_window(s, 0, nt, O, N, s.hash, s.flag, s.lt, s.tgt, wk.otarget, n0);
+        if constexpr ((V & VAR_TRACE) != 0)
+            diff_window<true>(s, 0, nt, O, N, s.hash, s.flag, s.lt, s.tgt, wk.otarget, n0, wk.trace + (size_t)wg * TRACE_WORDS);
+        else
+            diff_window<false>(s, 0, nt, O, N, s.hash, s.flag, s.lt, s.tgt, wk.otarget, n0);
     } else {
         for (int tt = 0; tt < nt; ++tt) {
             const uint32_t k = (s.ooff[tt + 1] - s.ooff[tt]) + (s.noff[tt + 1] - s.noff[tt]);
             const uint32_t gofs = s.ooff[tt] + s.noff[tt];
             if (k <= (uint32_t)CAP) {
-                diff_window(s, tt, tt + 1, O, N, s.hash, s.flag, nullptr, nullptr, wk.otarget, 0);
+                diff_window<false>(s, tt, tt + 1, O, N, s.hash, s.flag, nullptr, nullptr, wk.otarget, 0);
                 // spill the window's masked flags to global scratch (slow-path emission reads them)
                 for (uint32_t r = tid; r < k; r += BLOCK) wk.fscratch[gofs + r] = s.flag[r];
                 __syncthreads();
             } else {
-                diff_window(s, tt, tt + 1, O, N, wk.hscratch + gofs, wk.fscratch + gofs, nullptr,
+                diff_window<false>(s, tt, tt + 1, O, N, wk.hscratch + gofs, wk.fscratch + gofs, nullptr,
                             nullptr, wk.otarget, 0);
             }
         }
@@ -1293,6 +1321,30 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
         auto fetch = [&](const Slot& sl, RecCols& c) {
             if (sl.on) load_cols<NTL>(sl.old ? O : N, sl.x, do_res, !sl.old && do_q, c);
         };
+        if constexpr ((V & VAR_DIFF) != 0) {
+            // comparison-heavy build: one record at a time (fewer registers, more waves)
+            for (uint32_t b = 0; b < tot; b += BLOCK) {
+                const Slot cs = decode(b + tid);
+                bool qa = false;
+                uint32_t e = 0, q[18];
+                if (cs.on) {
+                    const int tt = cs.tt;
+                    const TopoCtx tc{s.ns[tt], s.src[tt], s.netns[tt]};
+                    RecCols cc;
+                    fetch(cs, cc);
+                    if (cs.old) {
+                        emit_del<V>(cc, cs.x, tc, tb, out, bd + s.tcnt[0][tt] + (cs.x - s.ooff[tt]), do_res);
+                    } else {
+                        e = ba + s.tcnt[2][tt] + (cs.x - s.noff[tt]);
+                        emit_add<V>(cc, N, cs.x, tc, tb, out, e, do_res, do_q, q);
+                        qa = do_q;
+                    }
+                }
+                wave_store_qdisc<V>(out.add_qdisc, qa, e, q, stage);
+            }
+            trace_mark<V>(wk, wg, 4);
+            return;
+        }
         Slot cs = decode(tid);
         RecCols cc;
         fetch(cs, cc);
@@ -1430,32 +1482,12 @@ __global__ void __launch_bounds__(BLOCK) k_qdisc_batch(DevLinks props, DevTables
     store_qdisc<0>(out + (size_t)j * 9, q);
 }
 
-template __global__ void k_reconcile<515>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
+template __global__ void k_reconcile<DEFAULT_VARIANT>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
+template __global__ void k_reconcile<DEFAULT_VARIANT | VAR_DIFF>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
 #if KDTN_PROFILING
-template __global__ void k_reconcile<0>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
-template __global__ void k_reconcile<1>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
-template __global__ void k_reconcile<2>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
-template __global__ void k_reconcile<3>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
-template __global__ void k_reconcile<4>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
-template __global__ void k_reconcile<5>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
-template __global__ void k_reconcile<9>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
-template __global__ void k_reconcile<11>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
-template __global__ void k_reconcile<17>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
-template __global__ void k_reconcile<33>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
-template __global__ void k_reconcile<65>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
-template __global__ void k_reconcile<97>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
-template __global__ void k_reconcile<101>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
-template __global__ void k_reconcile<113>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
-template __global__ void k_reconcile<129>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
-template __global__ void k_reconcile<257>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
-template __global__ void k_reconcile<513>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
-template __global__ void k_reconcile<529>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
-template __global__ void k_reconcile<641>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
-template __global__ void k_reconcile<545>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
-template __global__ void k_reconcile<1025>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
-template __global__ void k_reconcile<1537>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
-template __global__ void k_reconcile<521>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
-template __global__ void k_reconcile<523>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
+#define KDTN_VARIANT_INST(V) template __global__ void k_reconcile<V>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
+KDTN_PROFILING_VARIANTS(KDTN_VARIANT_INST)
+#undef KDTN_VARIANT_INST
 #endif
 
 }  // namespace kdtn

@@ -352,13 +352,13 @@ class Engine:
         return out
 
     def wg_trace(self) -> np.ndarray:
-        """(nwg, 6) uint64 phase timestamps of the last traced run (KDTN_VARIANT bit 16)."""
+        """(nwg, 8) uint64 phase timestamps of the last traced run (KDTN_VARIANT bit 16)."""
         cap = 1 << 26
         buf = np.zeros(cap, np.uint64)
         n = lib().kdtn_debug_wg_trace(self._ctx, buf.ctypes.data_as(C.POINTER(C.c_uint64)), cap)
         if n < 0:
             raise KdtnError(n, "kdtn_debug_wg_trace")
-        return buf[:n].reshape(-1, 6)
+        return buf[:n].reshape(-1, 8)
 
     # ---- MakeQdiscs batch --------------------------------------------------------------
     def make_qdiscs(self, pdict: StrTab, prop: np.ndarray, gap: np.ndarray) -> np.ndarray:

@@ -74,4 +74,4 @@ def test_product_library_reads_no_environment():
     for knob in (b"KDTN_VARIANT", b"KDTN_KD_SUB", b"KDTN_JS_VARIANT"):
         assert knob not in data, knob
     names = set(re.findall(rb"_ZN4kdtn11k_reconcileILi(\d+)E", data))
-    assert len(names) == 1, names
+    assert names == {b"515", b"2563"}, names      # default and comparison-heavy builds

@@ -27,9 +27,23 @@ ap.add_argument("--cache", default="")
 ap.add_argument("--out", default="")
 a = ap.parse_args()
 assert a.variant & 16, "trace bit (16) required"
-inp = synth.make(a.config, pods_per_shard=a.pods, cache_dir=a.cache or None)
+if a.config == 3:                       # the second churn epoch (dictionaries append-only)
+    cs = synth.ChurnSequence(pods_per_shard=a.pods)
+    inp0 = cs.epoch_input()
+    keep = (inp0.kdict.n, inp0.pdict.n)
+    eng0 = None
+else:
+    inp = synth.make(a.config, pods_per_shard=a.pods, cache_dir=a.cache or None)
 eng = Engine(device=0)
-eng.upload(inp)
+if a.config == 3:
+    eng.upload(inp0)
+    eng.run()
+    eng.sync()
+    cs.advance()
+    inp = cs.epoch_input()
+    eng.upload(inp, *keep)
+else:
+    eng.upload(inp)
 os.environ["KDTN_VARIANT"] = str(a.variant)
 for _ in range(a.reps):
     eng.run(abi.STAGE_ALL)
@@ -53,5 +67,11 @@ res = {"config": a.config, "pods": a.pods, "nwg": int(tr.shape[0]), "kernel_ms_e
        "start_spread_us": pct(us[:, 0]),
        "wgs_per_xcc": np.bincount(xcc, minlength=8).tolist()}
 # look-back wait vs ticket order: how far back does a typical workgroup wait
+tw = tr.shape[1]
+if tw >= 8 and (tr[:, 6] > 0).any():           # fast-path CalcDiff window phases
+    m = tr[:, 6] > 0
+    res["diff_phaseA_us"] = pct((tr[m, 6] - tr[m, 1]) * 0.01)
+    res["diff_phaseB_us"] = pct((tr[m, 7] - tr[m, 6]) * 0.01)
+    res["diff_rest_to_counts_us"] = pct((tr[m, 2] - tr[m, 7]) * 0.01)
 res["lookback_by_decile_us"] = [round(float(np.median(dur["p2->3"][i::10])), 2) for i in range(10)]
 print(json.dumps(res, indent=1))
