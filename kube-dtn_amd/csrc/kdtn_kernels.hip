@@ -844,7 +844,7 @@ struct RecShared {
     uint8_t act[TPW];
     uint32_t ns[TPW], src[TPW], netns[TPW];
     uint32_t tcnt[3][TPW];       // per-topology counts (del, upd, add) → exclusive offsets
-    uint32_t wsum[BLOCK / 64][3];
+    uint32_t wsum[BLOCK / 64][4];
     uint32_t wtot[3];
     uint32_t base[3];
     uint32_t ticket;
@@ -854,6 +854,8 @@ struct RecShared {
         uint2 stage[BLOCK / 64][32 * 9];
     };
     uint16_t rank[CAP];          // entry position within the workgroup's list
+    uint16_t dense[CAP];         // fast path: the flagged records, in record order
+    uint32_t n_dense;
     uint16_t tgt[CAP];           // upd target, relative to the workgroup's first desired record
     uint8_t flag[CAP];
     uint8_t lt[CAP];
@@ -900,11 +902,8 @@ __device__ void diff_window(RecShared& s, int tb, int te, const DevLinks& O, con
         }
         if (!old) {
             if (need_cmp(s, tt)) {
-                uint32_t k[KEYW], p[PROPW];
+                uint32_t k[KEYW];
                 load_key(N, idx, k);
-                load_props(N, idx, p);               // warms L2 for B's candidate loads
-#pragma unroll
-                for (int c = 0; c < PROPW; ++c) asm volatile("" ::"v"(p[c]));
                 hsh[r] = key_hash_w(k);
             }
             flg[r] = 0;
@@ -916,30 +915,49 @@ __device__ void diff_window(RecShared& s, int tb, int te, const DevLinks& O, con
     }
 
     // B. old side: first key-equal new record (CalcDiff :289-303) + positional DeepEqual (:77).
-    //    The old record's key and properties are loaded once (coalesced: consecutive threads,
-    //    consecutive records); a candidate is verified with all its loads in flight together.
+    //    The old record and the new record at the same position (the common first match of
+    //    an unchanged or edited link) are loaded together in one round trip (both coalesced:
+    //    consecutive threads, consecutive records); the LDS key hashes find the first match
+    //    when the positional record is not it, and any earlier duplicate key when it is.
     for (uint32_t r = tid; r < no; r += BLOCK) {
         const int tt = lt ? lt[r] : tb;
         uint8_t f = RF_DEL;
         if (need_cmp(s, tt)) {
             const uint32_t i = wo0 + r;
-            uint32_t ki[KEYW], pi[PROPW];
+            const uint32_t os_ = s.ooff[tt], ns_ = s.noff[tt], ne_ = s.noff[tt + 1];
+            const uint32_t jp = ns_ + (i - os_);
+            const bool have_p = jp < ne_;
+            uint32_t ki[KEYW], pi[PROPW], kj[KEYW], pj[PROPW];
             load_key(O, i, ki);
             load_props(O, i, pi);
+            if (have_p) {
+                load_key(N, jp, kj);
+                load_props(N, jp, pj);
+            }
             const uint32_t h = key_hash_w(ki);
-            const uint32_t ns_ = s.noff[tt], ne_ = s.noff[tt + 1];
+            const bool pos_key = have_p && words_eq<KEYW>(ki, kj);
+            const bool pos_eq = pos_key && words_eq<PROPW>(pi, pj);
             uint32_t first = 0xFFFFFFFFu;
-            uint32_t pj[PROPW];
-            for (uint32_t j = ns_; j < ne_; ++j) {
-                if (hsh[no + (j - wn0)] != h) continue;
-                uint32_t kj[KEYW];
-                load_key(N, j, kj);
-                load_props(N, j, pj);                        // L2-warm: key and props in one trip
-                if (words_eq<KEYW>(ki, kj)) { first = j; break; }
+            bool same_props = false;
+            const uint32_t jend = pos_key ? jp : ne_;       // before jp: an earlier duplicate only
+            for (uint32_t j = ns_; j < jend; ++j) {
+                if (j == jp || hsh[no + (j - wn0)] != h) continue;
+                uint32_t kx[KEYW], px[PROPW];
+                load_key(N, j, kx);
+                load_props(N, j, px);
+                if (words_eq<KEYW>(ki, kx)) {
+                    first = j;
+                    same_props = words_eq<PROPW>(pi, px);
+                    break;
+                }
+            }
+            if (first == 0xFFFFFFFFu && pos_key) {
+                first = jp;
+                same_props = pos_eq;
             }
             if (first != 0xFFFFFFFFu) {
                 flg[no + (first - wn0)] = RF_MATCHED;        // j is some old record's first match
-                if (!words_eq<PROPW>(pi, pj)) {
+                if (!same_props) {
                     f = RF_UPD;
                     if (tgt16) tgt16[r] = (uint16_t)(first - wn0);
                     else otarget[i] = first;
@@ -947,22 +965,7 @@ __device__ void diff_window(RecShared& s, int tb, int te, const DevLinks& O, con
                     f = 0;
                 }
             }
-            const uint32_t ko = s.ooff[tt + 1] - s.ooff[tt], kn = ne_ - ns_;
-            if (ko == kn) {
-                const uint32_t jp = ns_ + (i - s.ooff[tt]);
-                bool eq;
-                if (first == jp) {
-                    eq = (f == 0);
-                } else if (hsh[no + (jp - wn0)] != h) {
-                    eq = false;
-                } else {
-                    uint32_t kj[KEYW], pj[PROPW];
-                    load_key(N, jp, kj);
-                    load_props(N, jp, pj);
-                    eq = words_eq<KEYW>(ki, kj) && words_eq<PROPW>(pi, pj);
-                }
-                if (!eq) s.dirty[tt] = 1;
-            }
+            if (s.ooff[tt + 1] - os_ == ne_ - ns_ && !pos_eq) s.dirty[tt] = 1;
         }
         flg[r] = f;
     }
@@ -1239,16 +1242,17 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
     if (fast && !bulk) {
         const uint32_t per = (tot + BLOCK - 1) / BLOCK;
         const uint32_t r0 = min(tot, tid * per), r1 = min(tot, r0 + per);
-        uint32_t c[3] = {0, 0, 0};
+        uint32_t c[4] = {0, 0, 0, 0};                 // del, upd, add, any (dense list)
         for (uint32_t r = r0; r < r1; ++r) {
             const uint8_t f = s.flag[r];
             c[0] += (f & RF_DEL) ? 1u : 0u;
             c[1] += (f & RF_UPD) ? 1u : 0u;
             c[2] += (f & RF_ADD) ? 1u : 0u;
+            c[3] += f ? 1u : 0u;
         }
         const int lane = tid & 63, wave = tid >> 6;
-        uint32_t ex[3];
-        for (int k = 0; k < 3; ++k) {
+        uint32_t ex[4];
+        for (int k = 0; k < 4; ++k) {
             uint32_t v = c[k];
             for (int d = 1; d < 64; d <<= 1) {
                 const uint32_t o = __shfl_up(v, d, 64);
@@ -1258,10 +1262,12 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
             if (lane == 63) s.wsum[wave][k] = v;
         }
         __syncthreads();
-        for (int k = 0; k < 3; ++k)
+        for (int k = 0; k < 4; ++k)
             for (int w = 0; w < wave; ++w) ex[k] += s.wsum[w][k];
+        if (tid == BLOCK - 1) s.n_dense = ex[3] + c[3];
         for (uint32_t r = r0; r < r1; ++r) {
             const uint8_t f = s.flag[r];
+            if (f) s.dense[ex[3]++] = (uint16_t)r;
             if (f & RF_DEL) s.rank[r] = (uint16_t)ex[0]++;
             else if (f & RF_UPD) s.rank[r] = (uint16_t)ex[1]++;
             else if (f & RF_ADD) s.rank[r] = (uint16_t)ex[2]++;
@@ -1378,11 +1384,14 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
         return;
     }
     if (fast) {
-        for (uint32_t b = 0; b < tot; b += BLOCK) {          // no workgroup barriers
-            const uint32_t r = b + tid;
+        // only the flagged records, densely (a churn epoch flags a few % of them): one pass
+        // of dependent loads per BLOCK flagged records instead of per BLOCK records
+        const uint32_t nd = s.n_dense;
+        for (uint32_t b = 0; b < nd; b += BLOCK) {           // no workgroup barriers
+            const uint32_t r = b + tid < nd ? s.dense[b + tid] : 0u;
             bool qa = false, qu = false;
             uint32_t e = 0, q[18];
-            const uint8_t f = r < tot ? s.flag[r] : 0;
+            const uint8_t f = b + tid < nd ? s.flag[r] : 0;
             if (f) {
                 const int tt = s.lt[r];
                 const TopoCtx tc{s.ns[tt], s.src[tt], s.netns[tt]};
