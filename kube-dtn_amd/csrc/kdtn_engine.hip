@@ -75,7 +75,7 @@ struct kdtn_ctx {
     // links
     DevLinkStore real, des;
     // vni table
-    DevBuf v_node, v_vni, v_netns, v_ents, v_slots;
+    DevBuf v_node, v_vni, v_netns, v_ents, v_slots, v_table;
     uint32_t V = 0, vni_mask = 0;
     // pods
     DevBuf pods, pod_ovf, pod_direct;
@@ -205,7 +205,10 @@ int upload_dict(kdtn_ctx* c, DevBuf& bytes, DevBuf& offs, const kdtn_strtab& t, 
 
 // k_reconcile sync block: 16 B (ticket, error word) + 3 look-back granules per workgroup,
 // padded to 16 B (memset size % 16 == 0, cdna_hip_programming.md G16)
-size_t sync_bytes(uint32_t nwg) { return align_up(16 + (size_t)nwg * 24, 16); }
+// ticket + error word, look-back granules [nwg*3] u64, then VAR_DIFF counts and bases [nwg*3] u32 each
+// (16-B aligned: k_place_scan reads and writes them as uint4)
+size_t sync_counts_at(uint32_t nwg) { return align_up(16 + (size_t)nwg * 24, 16); }
+size_t sync_bytes(uint32_t nwg) { return sync_counts_at(nwg) + 2 * align_up((size_t)nwg * 12, 16); }
 
 int check_strtab(const kdtn_strtab& t, const char* what) {
     if (t.n == 0 || !t.offs || (!t.bytes && t.offs[t.n] != 0)) {
@@ -361,6 +364,7 @@ int prepare_epoch(kdtn_ctx* c, const kdtn_vni_table& vn, uint32_t slice, uint32_
     c->vni_mask = V ? next_pow2((uint64_t)V * 2) - 1 : 0;
     TRY(ensure(c->v_ents, (size_t)V * 16));
     TRY(ensure(c->v_slots, (size_t)(c->vni_mask + 1) * 4));
+    TRY(ensure(c->v_table, (size_t)(c->vni_mask + 1) * 16));
 
     c->slice = slice;
     if ((uint64_t)slice * (uint64_t)c->nranks > POD_INDEX) {
@@ -371,11 +375,13 @@ int prepare_epoch(kdtn_ctx* c, const kdtn_vni_table& vn, uint32_t slice, uint32_
     c->pod_total = slice * (uint32_t)c->nranks;
     c->ovf_mask = next_pow2((uint64_t)c->pod_total * 2) - 1;
     TRY(ensure(c->pods, (size_t)c->pod_total * 16));
-    TRY(ensure(c->pod_ovf, (size_t)(c->ovf_mask + 1) * 4));
+    if (c->pod_ovf.cap < (size_t)(c->ovf_mask + 1) * 8) {       // stamped slots start zeroed
+        TRY(ensure(c->pod_ovf, (size_t)(c->ovf_mask + 1) * 8));
+        HIP_TRY(hipMemsetAsync(c->pod_ovf.p, 0, c->pod_ovf.cap, c->stream));
+    }
     if (c->pod_direct.cap < (size_t)D * 16) {                  // stamps start from a zeroed table
         TRY(ensure(c->pod_direct, (size_t)D * 16));
-        HIP_TRY(hipMemsetAsync(c->pod_direct.p, 0, c->pod_direct.cap, c->stream));
-        c->pod_stamp = 0;
+        HIP_TRY(hipMemsetAsync(c->pod_direct.p, 0, c->pod_direct.cap, c->stream));   // stamp 0 = empty
     }
 
     const uint32_t nwg = (c->T + TPW - 1) / TPW;
@@ -389,14 +395,16 @@ int prepare_epoch(kdtn_ctx* c, const kdtn_vni_table& vn, uint32_t slice, uint32_
     TRY(ensure(c->del_off, (size_t)(c->T + 1) * 4));
     TRY(ensure(c->add_off, (size_t)(c->T + 1) * 4));
     TRY(ensure(c->upd_off, (size_t)(c->T + 1) * 4));
-    TRY(ensure(c->del_idx, (size_t)M * 4));
-    TRY(ensure(c->upd_idx, (size_t)M * 4));
-    TRY(ensure(c->add_idx, (size_t)N * 4));
-    TRY(ensure(c->del_res, (size_t)M * 16));
-    TRY(ensure(c->upd_res, (size_t)M * 16));
-    TRY(ensure(c->add_res, (size_t)N * 16));
-    TRY(ensure(c->upd_qdisc, (size_t)M * 72));
-    TRY(ensure(c->add_qdisc, (size_t)N * 72));
+    // the comparison build (both lists non-empty) emits deferred chunks into upper halves
+    const size_t h = (M && N) ? 2 : 1;
+    TRY(ensure(c->del_idx, h * M * 4));
+    TRY(ensure(c->upd_idx, h * M * 4));
+    TRY(ensure(c->add_idx, h * N * 4));
+    TRY(ensure(c->del_res, h * M * 16));
+    TRY(ensure(c->upd_res, h * M * 16));
+    TRY(ensure(c->add_res, h * N * 16));
+    TRY(ensure(c->upd_qdisc, h * M * 72));
+    TRY(ensure(c->add_qdisc, h * N * 72));
     return KDTN_OK;
 }
 
@@ -501,7 +509,7 @@ void kdtn_destroy(kdtn_ctx* c) {
     DevBuf* bufs[] = {&c->kd_bytes, &c->kd_offs, &c->kd_bits, &c->pd_bytes, &c->pd_offs,
                       &c->pd_pct, &c->pd_dur, &c->pd_rate, &c->pd_rerr, &c->t_ns, &c->t_name, &c->t_src,
                       &c->t_netns, &c->t_flags, &c->t_roff, &c->t_noff, &c->real.buf, &c->des.buf,
-                      &c->v_node, &c->v_vni, &c->v_netns, &c->v_ents, &c->v_slots, &c->pods,
+                      &c->v_node, &c->v_vni, &c->v_netns, &c->v_ents, &c->v_slots, &c->v_table, &c->pods,
                       &c->pod_ovf, &c->pod_direct, &c->otarget, &c->sync, &c->misc, &c->hscratch,
                       &c->fscratch, &c->action, &c->del_off, &c->add_off, &c->upd_off, &c->del_idx,
                       &c->add_idx, &c->upd_idx, &c->del_res, &c->add_res, &c->upd_res,
@@ -690,16 +698,16 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         timer_mark(c, "pods_allgather");
         if (++c->pod_stamp >= 0x7FFFFFFFu) {                          // stamp wrap: clear once
             HIP_TRY(hipMemsetAsync(c->pod_direct.p, 0, c->pod_direct.cap, s));
+            HIP_TRY(hipMemsetAsync(c->pod_ovf.p, 0, c->pod_ovf.cap, s));
             c->pod_stamp = 1;
         }
-        HIP_TRY(hipMemsetAsync(c->pod_ovf.p, 0xFF, ((size_t)c->ovf_mask + 1) * 4, s));
         if (c->pod_total) {
             k_pod_direct_scatter<<<nblocks(c->pod_total), BLOCK, 0, s>>>(
                 dp<uint4>(c->pods), c->pod_total, dp<uint32_t>(c->kd_bits) + (size_t)KB_PHYSICAL * c->kb_words,
                 dp<uint4>(c->pod_direct), c->pod_stamp, c->D);
             k_pod_direct_verify<<<nblocks(c->pod_total), BLOCK, 0, s>>>(dp<uint4>(c->pods), c->pod_total,
                                                                        dp<uint4>(c->pod_direct), c->pod_stamp,
-                                                                       dp<uint32_t>(c->pod_ovf), c->ovf_mask, c->D);
+                                                                       dp<unsigned long long>(c->pod_ovf), c->ovf_mask, c->D);
         }
         if (c->V) {
             const size_t vcap = (size_t)c->vni_mask + 1;
@@ -708,6 +716,8 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
                                                       dp<uint32_t>(c->v_netns), c->V, dp<uint4>(c->v_ents));
             k_vni_ht_build<<<nblocks(c->V), BLOCK, 0, s>>>(dp<uint4>(c->v_ents), c->V, dp<uint32_t>(c->v_slots),
                                                           c->vni_mask);
+            k_vni_fill<<<nblocks(vcap), BLOCK, 0, s>>>(dp<uint4>(c->v_ents), dp<uint32_t>(c->v_slots), (uint32_t)vcap,
+                                                       dp<uint4>(c->v_table));
         }
         timer_mark(c, "hash_build");
     }
@@ -722,9 +732,9 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         tb.pods = dp<uint4>(c->pods);
         tb.pod_direct = dp<uint4>(c->pod_direct);
         tb.pod_stamp = c->pod_stamp;
-        tb.pod_ovf = dp<uint32_t>(c->pod_ovf);
+        tb.pod_ovf = dp<unsigned long long>(c->pod_ovf);
         tb.ovf_mask = c->ovf_mask;
-        tb.vnis = dp<uint4>(c->v_ents);
+        tb.vnis = dp<uint4>(c->v_table);
         tb.vni_slots = dp<uint32_t>(c->v_slots);
         tb.vni_mask = c->V ? c->vni_mask : 0;
         tb.special = special;
@@ -753,7 +763,14 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         w.nwg = c->nwg;
         w.trace = nullptr;
         w.first_partial = misc + MISC_FIRST_PARTIAL;                // 0xFFFFFFFF from the memset
-        k_full_prefix<<<nblocks(c->T), BLOCK, 0, s>>>(T, misc + MISC_FIRST_PARTIAL);
+        w.wcount = reinterpret_cast<uint32_t*>(static_cast<char*>(c->sync.p) + sync_counts_at(c->nwg));
+        w.m_cap = c->real.n;
+        w.n_cap = c->des.n;
+        uint32_t* wbase = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(w.wcount) + align_up((size_t)c->nwg * 12, 16));
+        bool placed = false;                                        // VAR_DIFF: k_place_scan + k_place
+        k_full_prefix<<<(unsigned)std::min<uint64_t>(FP_GRID, (c->T + 4 * FP_BLOCK - 1) / (4 * FP_BLOCK)), FP_BLOCK, 0, s>>>(
+            T, misc + MISC_FIRST_PARTIAL);
+        timer_mark(c, "full_prefix");
 #if KDTN_PROFILING
         int variant = DEFAULT_VARIANT;
         if (const char* ev = std::getenv("KDTN_VARIANT")) variant = std::atoi(ev);
@@ -764,7 +781,7 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         }
         switch (variant) {
 #define KDTN_VARIANT_CASE(V) \
-        case V: k_reconcile<V><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); break;
+        case V: k_reconcile<V><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); placed = (V & VAR_DIFF) != 0; break;
         KDTN_PROFILING_VARIANTS(KDTN_VARIANT_CASE)
 #undef KDTN_VARIANT_CASE
         default:
@@ -772,12 +789,25 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
             break;
         }
 #else
-        if (c->real.n && c->des.n)               // CalcDiff windows: the comparison-heavy build
+        if (c->real.n && c->des.n) {             // CalcDiff windows: the comparison-heavy build
             k_reconcile<DEFAULT_VARIANT | VAR_DIFF><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w);
-        else
+            placed = true;
+        } else {
             k_reconcile<DEFAULT_VARIANT><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w);
+        }
 #endif
         timer_mark(c, "reconcile");
+        if (placed) {
+            if ((size_t)c->real.n * 2 > c->del_idx.cap / 4 || (size_t)c->des.n * 2 > c->add_idx.cap / 4) {
+                std::snprintf(g_last_error, sizeof(g_last_error), "deferred placement without upper halves");
+                return KDTN_EINVAL;
+            }
+            k_place_scan<<<1, PLACE_SCAN_BLOCK, 0, s>>>(w.wcount, c->nwg, wbase, o, c->T);
+            timer_mark(c, "place_scan");
+            k_place<<<(c->nwg + BLOCK / 64 - 1) / (BLOCK / 64), BLOCK, 0, s>>>(T, w.wcount, wbase, w.first_partial, o,
+                                                                              w.m_cap, w.n_cap, c->nwg);
+            timer_mark(c, "place");
+        }
     } else {
         HIP_TRY(hipMemsetAsync(misc + 1, 0, 12, s));
         HIP_TRY(hipMemsetAsync(c->del_off.p, 0, 4, s));

@@ -158,10 +158,10 @@ struct DevTables {             // read-only lookup structures of the epoch
     const uint4* pods;         // [pod_total] {ns, name, src_ip, net_ns|spec_nil<<31}
     const uint4* pod_direct;   // [D] by name id: {ns, g<<2|phys<<1|spec_nil, src_ip|netns_empty<<31, stamp<<1|multi}
     uint32_t pod_stamp;        // this epoch's stamp
-    const uint32_t* pod_ovf;   // [ovf_mask+1] pod indices of shared names, keyed by (ns, name)
+    const unsigned long long* pod_ovf;   // [ovf_mask+1] {stamp, pod index} of shared names, keyed by (ns, name)
     uint32_t ovf_mask;
-    const uint4* vnis;         // [V] {node, vni, net_ns, 0}
-    const uint32_t* vni_slots; // [vni_mask+1]
+    const uint4* vnis;         // [vni_mask+1] open-addressing slots {node, vni, net_ns, 0}, node ~0 = empty
+    const uint32_t* vni_slots; // (build scratch: entry index per slot)
     uint32_t vni_mask;         // 0 ⇒ empty table
     const uint32_t* special;   // [SPECIAL_DEFAULT] "default", [SPECIAL_LOCALHOST] "localhost"
     int32_t vxlan_base;
@@ -192,8 +192,17 @@ struct RecWork {
     uint32_t* otarget;         // [M]   first matching desired index (slow path)
     unsigned long long* trace; // [nwg][TRACE_WORDS] (VAR_TRACE only)
     const uint32_t* first_partial;   // k_full_prefix: first chunk not known to emit all records
+    uint32_t* wcount;          // [nwg*3] list counts per workgroup (VAR_DIFF: k_place_scan input)
+    uint32_t m_cap, n_cap;     // VAR_DIFF: deferred chunks emit at m_cap + o0 / n_cap + n0
     uint32_t nwg;
 };
+
+// VAR_DIFF placement (after k_reconcile): exclusive bases per workgroup and list totals, then
+// the deferred chunks' entries moved from the upper halves of the output arrays.
+__global__ void k_place_scan(const uint32_t* wcount, uint32_t nwg, uint32_t* wbase, RecOut out, uint32_t T);
+__global__ void k_place(DevTopos T, const uint32_t* wcount, const uint32_t* wbase, const uint32_t* first_partial,
+                        RecOut out, uint32_t m_cap, uint32_t n_cap, uint32_t nwg);
+constexpr int PLACE_SCAN_BLOCK = 1024, PLACE_PER = 8;    // k_place_scan: workgroups per thread per tile
 
 __global__ void k_special_clip(uint32_t* special, uint32_t k0);
 template <int SUB>
@@ -205,8 +214,9 @@ __global__ void k_pods_fill(DevTopos T, uint32_t slice, uint32_t rank_base, uint
 __global__ void k_pod_direct_scatter(const uint4* pods, uint32_t total, const uint32_t* phys_bits,
                                      uint4* slots, uint32_t stamp, uint32_t nd);
 __global__ void k_pod_direct_verify(const uint4* pods, uint32_t total, uint4* slots, uint32_t stamp,
-                                    uint32_t* ovf, uint32_t mask, uint32_t nd);
+                                    unsigned long long* ovf, uint32_t mask, uint32_t nd);
 __global__ void k_vni_ht_build(const uint4* ents, uint32_t n, uint32_t* slots, uint32_t mask);
+__global__ void k_vni_fill(const uint4* ents, const uint32_t* slots, uint32_t nslots, uint4* out);
 __global__ void k_vni_pack(const uint32_t* node, const int32_t* vni, const uint32_t* net_ns,
                            uint32_t n, uint4* ents);
 template <int V>
@@ -315,6 +325,7 @@ __global__ void k_scan_top(uint64_t* part, uint32_t nb);
 __global__ void k_scan_final(const uint32_t* size, uint32_t n, const uint64_t* part, uint64_t* off);
 __global__ void k_wire_write(WireIn w, DevLinks O, DevLinks N, WireWork wk, uint8_t* arena);
 __global__ void k_qdisc_batch(DevLinks props, DevTables tb, uint2* out);
+constexpr int FP_BLOCK = 1024, FP_GRID = 256;       // k_full_prefix launch shape
 __global__ void k_full_prefix(DevTopos T, uint32_t* first_partial);
 
 // ---- CR ingest: TopologyList JSON → epoch tables (kdtn_ingest.hip) ------------------------

@@ -354,15 +354,25 @@ KD_INLINE uint32_t pod_probe_slot(uint32_t home, uint32_t i, uint32_t mask) {
 KD_INLINE uint32_t pod_home(uint32_t mask, uint32_t ns, uint32_t name) {
     return (uint32_t)hash64(((uint64_t)ns << 32) | name) & mask;
 }
-KD_INLINE void ovf_insert(const uint4* pods, uint32_t g, uint32_t ns, uint32_t name, uint32_t* ovf, uint32_t mask) {
+// Overflow slots are {stamp:32 | g:32} words: a slot of an older epoch reads as empty, so
+// the table needs no clearing between epochs (the stamp is the direct table's).
+KD_INLINE void ovf_insert(const uint4* pods, uint32_t g, uint32_t ns, uint32_t name, unsigned long long* ovf,
+                          uint32_t mask, uint32_t stamp) {
     const uint32_t home = pod_home(mask, ns, name);
+    const unsigned long long mine = ((unsigned long long)stamp << 32) | g;
     for (uint32_t i = 0;; ++i) {
         const uint32_t h = pod_probe_slot(home, i, mask);
-        const uint32_t prev = atomicCAS(&ovf[h], 0xFFFFFFFFu, g);
-        if (prev == 0xFFFFFFFFu || prev == g) return;
-        const uint4 o = pods[prev];
+        unsigned long long cur = __hip_atomic_load(ovf + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while ((uint32_t)(cur >> 32) != stamp) {                 // stale: claim it
+            const unsigned long long prev = atomicCAS(ovf + h, cur, mine);
+            if (prev == cur) return;
+            cur = prev;
+        }
+        const uint32_t og = (uint32_t)cur;
+        if (og == g) return;
+        const uint4 o = pods[og];
         if (o.x == ns && o.y == name) {
-            atomicMin(&ovf[h], g);                         // first topology wins
+            atomicMin(ovf + h, mine);                           // first topology wins (same stamp)
             return;
         }
     }
@@ -384,7 +394,7 @@ __global__ void __launch_bounds__(BLOCK) k_pod_direct_scatter(const uint4* pods,
 // into the overflow table (duplicates are rare; the table then answers every lookup of
 // that name).
 __global__ void __launch_bounds__(BLOCK) k_pod_direct_verify(const uint4* pods, uint32_t total, uint4* slots,
-                                                             uint32_t stamp, uint32_t* ovf, uint32_t mask,
+                                                             uint32_t stamp, unsigned long long* ovf, uint32_t mask,
                                                              uint32_t nd) {
     const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
     if (g >= total) return;
@@ -394,14 +404,23 @@ __global__ void __launch_bounds__(BLOCK) k_pod_direct_verify(const uint4* pods, 
     const uint32_t owner = w.y >> 2;
     if (owner == g) return;
     reinterpret_cast<uint32_t*>(slots + e.y)[3] = (stamp << 1) | 1u;
-    ovf_insert(pods, g, e.x, e.y, ovf, mask);
-    ovf_insert(pods, owner, pods[owner].x, e.y, ovf, mask);
+    ovf_insert(pods, g, e.x, e.y, ovf, mask, stamp);
+    ovf_insert(pods, owner, pods[owner].x, e.y, ovf, mask, stamp);
 }
 
 __global__ void __launch_bounds__(BLOCK) k_vni_pack(const uint32_t* node, const int32_t* vni,
                                                     const uint32_t* net_ns, uint32_t n, uint4* ents) {
     const uint32_t v = blockIdx.x * BLOCK + threadIdx.x;
     if (v < n) ents[v] = make_uint4(node[v], (uint32_t)vni[v], net_ns[v], 0u);
+}
+
+// Slot contents after the build: the entry itself (first wins), or node = ~0 (empty).
+__global__ void __launch_bounds__(BLOCK) k_vni_fill(const uint4* ents, const uint32_t* slots, uint32_t nslots,
+                                                    uint4* out) {
+    const uint32_t h = blockIdx.x * BLOCK + threadIdx.x;
+    if (h >= nslots) return;
+    const uint32_t v = slots[h];
+    out[h] = v == 0xFFFFFFFFu ? make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u) : ents[v];
 }
 
 // VxlanManager snapshot: slots hold the smallest entry index with key (node, vni).
@@ -448,8 +467,9 @@ KD_INLINE uint2 pod_resolve(const DevTables& tb, uint32_t ns, uint32_t name, uin
     // name shared by several pods: overflow table of pod indices (rare)
     const uint32_t home = pod_home(tb.ovf_mask, ns, name);
     for (uint32_t i = 0;; ++i) {
-        const uint32_t g = ldg(tb.pod_ovf, pod_probe_slot(home, i, tb.ovf_mask));
-        if (g == 0xFFFFFFFFu) return make_uint2(0xFFFFFFFFu, 0u);
+        const unsigned long long w8 = ldg(tb.pod_ovf, pod_probe_slot(home, i, tb.ovf_mask));
+        if ((uint32_t)(w8 >> 32) != tb.pod_stamp) return make_uint2(0xFFFFFFFFu, 0u);   // empty this epoch
+        const uint32_t g = (uint32_t)w8;
         const uint4 e = ldg(tb.pods, g);
         if (e.x == ns && e.y == name) {
             const uint32_t phys = (w.y >> 1) & 1u;          // a property of the name string
@@ -459,14 +479,14 @@ KD_INLINE uint2 pod_resolve(const DevTables& tb, uint32_t ns, uint32_t name, uin
     }
 }
 
-// VxlanManager.Get(vni) on node `node`: net_ns id, or 0xFFFFFFFF when absent.
+// VxlanManager.Get(vni) on node `node`: net_ns id, or 0xFFFFFFFF when absent. The slots hold
+// the entries themselves ({node, vni, net_ns}, node = ~0 when empty): one gather per probe.
 KD_INLINE uint32_t vni_lookup(const DevTables& tb, uint32_t node, int32_t vni) {
     if (tb.vni_mask == 0) return 0xFFFFFFFFu;
     uint32_t h = (uint32_t)hash64(((uint64_t)node << 32) | (uint32_t)vni) & tb.vni_mask;
     for (;;) {
-        const uint32_t v = ldg(tb.vni_slots, h);
-        if (v == 0xFFFFFFFFu) return 0xFFFFFFFFu;
-        const uint4 e = ldg(tb.vnis, v);
+        const uint4 e = ldg(tb.vnis, h);
+        if (e.x == 0xFFFFFFFFu) return 0xFFFFFFFFu;
         if (e.x == node && e.y == (uint32_t)vni) return e.z;
         h = (h + 1) & tb.vni_mask;
     }
@@ -621,6 +641,18 @@ KD_INLINE void store_qdisc(uint2* dst, const uint32_t* q) {
 }
 
 template <int V>
+KD_INLINE void store_q8(uint2* dst, uint2 v) {
+    if constexpr ((V & VAR_NT_STORE) != 0) {
+        u32x2 x;
+        x.x = v.x;
+        x.y = v.y;
+        __builtin_nontemporal_store(x, reinterpret_cast<u32x2*>(dst));
+    } else {
+        *dst = v;
+    }
+}
+
+template <int V>
 KD_INLINE void store_res(uint4* dst, uint4 r) {
     if constexpr ((V & VAR_NT_STORE) != 0) {
         u32x4 v;
@@ -665,34 +697,42 @@ struct TopoCtx {       // the local pod of a batch (topology_controller.go:181-1
     uint32_t ns, src, netns;
 };
 
-// delLink (handler.go:461-492) from loaded columns (keys)
-template <int V>
-KD_INLINE void emit_del(const RecCols& c, uint32_t i, const TopoCtx& tc, const DevTables& tb,
-                        const RecOut& out, uint32_t e, bool res) {
-    store_idx<V>(out.del_idx + e, i);
-    if (!res) return;
+// delLink (handler.go:461-492) from loaded columns (keys). The *_calc forms compute an
+// entry's outputs without storing them (the caller may not know its position yet).
+KD_INLINE uint4 del_calc(const RecCols& c, const TopoCtx& tc, const DevTables& tb) {
     const int32_t vni = vni_of(tb.vxlan_base, c.uid);
     const uint32_t err = veth_err(tb, c.lip, c.lmac, KDTN_E_VETH_CIDR, KDTN_E_VETH_MAC);
     uint32_t hit = 0;
     if (!err) hit = vni_lookup(tb, tc.src, vni) == tc.netns;
-    store_res<V>(out.del_res + e, pack_res(0xFFFFFFFFu, vni, 0, 0, err, hit));
+    return pack_res(0xFFFFFFFFu, vni, 0, 0, err, hit);
+}
+
+template <int V>
+KD_INLINE void emit_del(const RecCols& c, uint32_t i, const TopoCtx& tc, const DevTables& tb,
+                        const RecOut& out, uint32_t e, bool res) {
+    store_idx<V>(out.del_idx + e, i);
+    if (res) store_res<V>(out.del_res + e, del_calc(c, tc, tb));
 }
 
 // UpdateLinks entry (handler.go:644-663): MakeVeth(local), then MakeQdiscs
 template <int V>
-KD_INLINE void emit_upd(const RecCols& c, uint32_t j, const DevTables& tb, const RecOut& out,
-                        uint32_t e, bool res, bool qd, uint32_t* q) {
-    store_idx<V>(out.upd_idx + e, j);
-    if (!res && !qd) return;
+KD_INLINE uint4 upd_calc(const RecCols& c, const DevTables& tb, bool res, uint32_t* q) {
     PropVals v;
     gather_props<V>(c, tb, v);
     uint32_t werr = 0;
     if (res) werr = veth_err(tb, c.lip, c.lmac, KDTN_E_VETH_CIDR, KDTN_E_VETH_MAC);
     qdisc_from(tb, v, q);
-    if (res) {
-        const uint32_t err = werr ? werr : (q[17] >> 16) & 0xFF;
-        store_res<V>(out.upd_res + e, pack_res(0xFFFFFFFFu, vni_of(tb.vxlan_base, c.uid), 0, 0, err, 0));
-    }
+    const uint32_t err = werr ? werr : (q[17] >> 16) & 0xFF;
+    return pack_res(0xFFFFFFFFu, vni_of(tb.vxlan_base, c.uid), 0, 0, err, 0);
+}
+
+template <int V>
+KD_INLINE void emit_upd(const RecCols& c, uint32_t j, const DevTables& tb, const RecOut& out,
+                        uint32_t e, bool res, bool qd, uint32_t* q) {
+    store_idx<V>(out.upd_idx + e, j);
+    if (!res && !qd) return;
+    const uint4 r = upd_calc<V>(c, tb, res, q);
+    if (res) store_res<V>(out.upd_res + e, r);
 }
 
 // addLink pure prefix (handler.go:316-459) + MakeQdiscs, from loaded columns, in two steps:
@@ -719,13 +759,11 @@ KD_INLINE void add_gather(const RecCols& c, const TopoCtx& tc, const DevTables& 
 }
 
 template <int V>
-KD_INLINE void add_finish(const RecCols& c, const AddGath& g, const DevLinks& N, uint32_t j,
-                          const TopoCtx& tc, const DevTables& tb, const RecOut& out, uint32_t e,
-                          bool res, bool qd, uint32_t* q) {
+KD_INLINE uint4 add_calc(const RecCols& c, const AddGath& g, const DevLinks& N, uint32_t j,
+                         const TopoCtx& tc, const DevTables& tb, bool res, bool qd, uint32_t* q) {
     constexpr bool NTL = (V & VAR_NT_LOAD) != 0;
-    store_idx<V>(out.add_idx + e, j);
     if (qd) qdisc_from(tb, g.v, q);
-    if (!res) return;
+    if (!res) return make_uint4(0u, 0u, 0u, 0u);
     const int32_t vni = vni_of(tb.vxlan_base, c.uid);
     uint32_t err = ((g.kb_ip >> (c.lip & 31)) & 1u) ? (uint32_t)KDTN_E_VETH_CIDR
                  : ((g.kb_mac >> (c.lmac & 31)) & 1u) ? (uint32_t)KDTN_E_VETH_MAC : 0u;   // :327
@@ -772,7 +810,16 @@ KD_INLINE void add_finish(const RecCols& c, const AddGath& g, const DevLinks& N,
             }
         }
     }
-    store_res<V>(out.add_res + e, pack_res(peer, vni, vtep, kind, err, hit, rerr));
+    return pack_res(peer, vni, vtep, kind, err, hit, rerr);
+}
+
+template <int V>
+KD_INLINE void add_finish(const RecCols& c, const AddGath& g, const DevLinks& N, uint32_t j,
+                          const TopoCtx& tc, const DevTables& tb, const RecOut& out, uint32_t e,
+                          bool res, bool qd, uint32_t* q) {
+    store_idx<V>(out.add_idx + e, j);
+    const uint4 r = add_calc<V>(c, g, N, j, tc, tb, res, qd, q);
+    if (res) store_res<V>(out.add_res + e, r);
 }
 
 template <int V>
@@ -1028,15 +1075,17 @@ KD_INLINE uint32_t wave_sum(uint32_t v) {
     return v;
 }
 
+KD_INLINE void publish_aggregate(const RecShared& s, const RecWork& wk, uint32_t wg, int lane) {
+    __hip_atomic_store(wk.status + (size_t)wg * 3 + lane, ((wg == 0 ? 2ull : 1ull) << 32) | s.wtot[lane],
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ void lookback(RecShared& s, const RecWork& wk, uint32_t wg) {
     const int tid = threadIdx.x;
     if (tid < 64) {
         const int lane = tid;
         unsigned long long* st = wk.status;
-        if (lane < 3)
-            __hip_atomic_store(st + (size_t)wg * 3 + lane,
-                               ((wg == 0 ? 2ull : 1ull) << 32) | s.wtot[lane], __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+        if (lane < 3) publish_aggregate(s, wk, wg, lane);
         uint32_t pre[3] = {0u, 0u, 0u};
         if (wg > 0) {
             bool done[3] = {false, false, false};
@@ -1100,24 +1149,48 @@ __device__ void lookback(RecShared& s, const RecWork& wk, uint32_t wg) {
 // all new → AddLinks) and none otherwise, so it is "full" iff DIFF or both lists are
 // empty; a topology needing comparisons is conservatively not full. Chunks up to and
 // including the first partial one know their batch bases from the record offsets alone.
-__global__ void __launch_bounds__(BLOCK) k_full_prefix(DevTopos T, uint32_t* first_partial) {
-    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
-    bool partial = false;
-    if (t < T.n) {
-        const uint8_t tf = T.flags[t];
-        const uint32_t ko = T.real_off[t + 1] - T.real_off[t], kn = T.des_off[t + 1] - T.des_off[t];
-        const bool st_nil = tf & KDTN_TOPO_STATUS_NIL, sp_nil = tf & KDTN_TOPO_SPEC_NIL;
-        const bool cmp = !st_nil && !sp_nil && ko > 0 && kn > 0;
-        const bool empty = ko == 0 && kn == 0;
-        // action (topology_controller.go:77-88) of a topology without comparisons
-        const bool diff = (st_nil || sp_nil) ? (!st_nil && sp_nil) : !empty;
-        partial = cmp || !(diff || empty);
+KD_INLINE bool topo_partial(uint8_t tf, uint32_t ko, uint32_t kn) {
+    const bool st_nil = tf & KDTN_TOPO_STATUS_NIL, sp_nil = tf & KDTN_TOPO_SPEC_NIL;
+    const bool cmp = !st_nil && !sp_nil && ko > 0 && kn > 0;
+    const bool empty = ko == 0 && kn == 0;
+    // action (topology_controller.go:77-88) of a topology without comparisons
+    const bool diff = (st_nil || sp_nil) ? (!st_nil && sp_nil) : !empty;
+    return cmp || !(diff || empty);
+}
+
+// Four topologies per thread (16-B offset loads), grid-stride over FP_GRID blocks, one
+// global atomicMin per block: an epoch of partial topologies (config 3) sent every wave's
+// atomic to one address (133 µs).
+__global__ void __launch_bounds__(FP_BLOCK) k_full_prefix(DevTopos T, uint32_t* first_partial) {
+    __shared__ uint32_t bmin;
+    if (threadIdx.x == 0) bmin = 0xFFFFFFFFu;
+    __syncthreads();
+    const uint32_t stride = gridDim.x * FP_BLOCK * 4;
+    for (uint32_t base = blockIdx.x * FP_BLOCK * 4; base < T.n; base += stride) {
+        const uint32_t t0 = base + threadIdx.x * 4;
+        uint32_t first = 0xFFFFFFFFu;                  // first partial topology of the four
+        if (t0 + 4 <= T.n) {
+            const uint4 ro = *reinterpret_cast<const uint4*>(T.real_off + t0);
+            const uint4 dn = *reinterpret_cast<const uint4*>(T.des_off + t0);
+            const uint32_t ro4 = T.real_off[t0 + 4], dn4 = T.des_off[t0 + 4];
+            const uint32_t fl = *reinterpret_cast<const uint32_t*>(T.flags + t0);
+            if (topo_partial(fl >> 24, ro4 - ro.w, dn4 - dn.w)) first = t0 + 3;
+            if (topo_partial((fl >> 16) & 0xFF, ro.w - ro.z, dn.w - dn.z)) first = t0 + 2;
+            if (topo_partial((fl >> 8) & 0xFF, ro.z - ro.y, dn.z - dn.y)) first = t0 + 1;
+            if (topo_partial(fl & 0xFF, ro.y - ro.x, dn.y - dn.x)) first = t0;
+        } else {
+            for (uint32_t t = t0 + 3; t + 1 > t0; --t)
+                if (t < T.n && topo_partial(T.flags[t], T.real_off[t + 1] - T.real_off[t],
+                                            T.des_off[t + 1] - T.des_off[t]))
+                    first = t;
+        }
+        const bool partial = first != 0xFFFFFFFFu;
+        const uint64_t m = __ballot(partial);
+        if (partial && (threadIdx.x & 63) == (uint32_t)(__ffsll((long long)m) - 1))
+            atomicMin(&bmin, first / TPW);              // lanes hold increasing topologies
+        if (__syncthreads_or(m != 0)) break;         // later iterations only hold later chunks
     }
-    const uint64_t m = __ballot(partial);
-    if (m && (threadIdx.x & 63) == 0) {
-        const uint32_t t0 = blockIdx.x * BLOCK + (threadIdx.x & ~63u) + (uint32_t)(__ffsll((long long)m) - 1);
-        atomicMin(first_partial, t0 / TPW);
-    }
+    if (threadIdx.x == 0 && bmin != 0xFFFFFFFFu) atomicMin(first_partial, bmin);
 }
 
 // (VAR_TRACE) phase timestamp of this workgroup: 100 MHz chip-wide clock
@@ -1282,7 +1355,17 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
     // k_full_prefix found no earlier exception): the batch bases are the record offsets of
     // the chunk, known without waiting on the predecessors. The inclusive prefix is
     // published at once so that later workgroups' look-backs stop here.
-    if ((V & VAR_NO_PREFIX) == 0 && wg <= *wk.first_partial) {
+    const bool prefix = (V & VAR_NO_PREFIX) == 0 && wg <= *wk.first_partial;
+    // Comparison build: a chunk behind the full prefix does not wait for its predecessors'
+    // windows. It emits at record-offset bases into the upper halves of the output arrays
+    // (every list of a chunk holds at most as many entries as its records), and k_place moves
+    // the entries down once k_place_scan has summed the workgroup counts.
+    constexpr bool kDefer = (V & VAR_DIFF) != 0;
+    const bool deferred = kDefer && !prefix;
+    if constexpr (kDefer) {
+        if (tid < 3) wk.wcount[(size_t)wg * 3 + tid] = s.wtot[tid];
+    }
+    if (prefix) {
         if (tid < 3) {
             const uint32_t p = tid == 0 ? s.ooff[0] : (tid == 1 ? 0u : s.noff[0]);
             __hip_atomic_store(wk.status + (size_t)wg * 3 + tid, (2ull << 32) | (p + s.wtot[tid]),
@@ -1290,21 +1373,24 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
             s.base[tid] = p;
         }
         __syncthreads();
+    } else if (deferred) {
+        if (tid < 3) s.base[tid] = tid == 2 ? wk.n_cap + s.noff[0] : wk.m_cap + s.ooff[0];
+        __syncthreads();
     } else {
         lookback(s, wk, wg);
     }
     trace_mark<V>(wk, wg, 3);
     const uint32_t bd = s.base[0], bu = s.base[1], ba = s.base[2];
-    if (wg == wk.nwg - 1 && tid < 3) {
+    if (!kDefer && wg == wk.nwg - 1 && tid < 3) {             // comparison build: k_place_scan
         const uint32_t total = s.base[tid] + s.wtot[tid];
         out.totals[tid] = total;
         (tid == 0 ? out.del_off : tid == 1 ? out.upd_off : out.add_off)[T.n] = total;
     }
     if (tid < nt) {
         out.action[t0 + tid] = s.act[tid];
-        out.del_off[t0 + tid] = bd + s.tcnt[0][tid];
-        out.upd_off[t0 + tid] = bu + s.tcnt[1][tid];
-        out.add_off[t0 + tid] = ba + s.tcnt[2][tid];
+        out.del_off[t0 + tid] = (deferred ? 0u : bd) + s.tcnt[0][tid];   // k_place adds the base
+        out.upd_off[t0 + tid] = (deferred ? 0u : bu) + s.tcnt[1][tid];
+        out.add_off[t0 + tid] = (deferred ? 0u : ba) + s.tcnt[2][tid];
     }
 
     // ---- 4. emission -------------------------------------------------------------------
@@ -1476,6 +1562,126 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
         }
     }
     trace_mark<V>(wk, wg, 4);
+}
+
+// ---- VAR_DIFF placement -------------------------------------------------------------
+// Exclusive bases of every workgroup's three lists (one block; nwg × 3 counts), the list
+// totals and the closing offsets [T]. Tiles of PLACE_SCAN_BLOCK × PLACE_PER workgroups:
+// each thread loads its PLACE_PER consecutive count triples with independent 16-B loads
+// (one memory round trip per tile), scans them in registers, block-scans the thread sums.
+__global__ void __launch_bounds__(PLACE_SCAN_BLOCK) k_place_scan(const uint32_t* wcount, uint32_t nwg,
+                                                                 uint32_t* wbase, RecOut out, uint32_t T) {
+    __shared__ uint32_t wsum[PLACE_SCAN_BLOCK / 64][3];
+    __shared__ uint32_t carry[3];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid < 3) carry[tid] = 0;
+    constexpr uint32_t TILE = PLACE_SCAN_BLOCK * PLACE_PER;
+    for (uint32_t t0 = 0; t0 < nwg; t0 += TILE) {
+        const uint32_t w0 = t0 + tid * PLACE_PER;
+        uint32_t v[PLACE_PER * 3];
+        if (w0 + PLACE_PER <= nwg) {
+            const uint4* src = reinterpret_cast<const uint4*>(wcount + (size_t)w0 * 3);
+#pragma unroll
+            for (int k = 0; k < PLACE_PER * 3 / 4; ++k) {
+                const uint4 x = src[k];
+                v[4 * k] = x.x;
+                v[4 * k + 1] = x.y;
+                v[4 * k + 2] = x.z;
+                v[4 * k + 3] = x.w;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < PLACE_PER * 3; ++k)
+                v[k] = w0 + k / 3 < nwg ? wcount[(size_t)w0 * 3 + k] : 0u;
+        }
+        uint32_t ex[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            uint32_t x = 0;
+#pragma unroll
+            for (int k = 0; k < PLACE_PER; ++k) x += v[3 * k + c];
+            uint32_t sc = x;
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t o = __shfl_up(sc, d, 64);
+                if (lane >= (uint32_t)d) sc += o;
+            }
+            ex[c] = sc - x;
+            if (lane == 63) wsum[wave][c] = sc;
+        }
+        __syncthreads();
+        uint32_t tot[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            uint32_t add = carry[c], all = 0;
+            for (uint32_t w = 0; w < PLACE_SCAN_BLOCK / 64; ++w) {
+                if (w < wave) add += wsum[w][c];
+                all += wsum[w][c];
+            }
+            tot[c] = all;
+            uint32_t run = ex[c] + add;
+#pragma unroll
+            for (int k = 0; k < PLACE_PER; ++k) {
+                const uint32_t x = v[3 * k + c];
+                v[3 * k + c] = run;                       // exclusive base, in place
+                run += x;
+            }
+        }
+        if (w0 + PLACE_PER <= nwg) {
+            uint4* dst = reinterpret_cast<uint4*>(wbase + (size_t)w0 * 3);
+#pragma unroll
+            for (int k = 0; k < PLACE_PER * 3 / 4; ++k) dst[k] = make_uint4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+        } else {
+#pragma unroll
+            for (int k = 0; k < PLACE_PER * 3; ++k)
+                if (w0 + k / 3 < nwg) wbase[(size_t)w0 * 3 + k] = v[k];
+        }
+        __syncthreads();                                  // wsum / carry reads done
+        if (tid < 3) carry[tid] += tot[tid];
+        __syncthreads();
+    }
+    if (tid < 3) {
+        out.totals[tid] = carry[tid];
+        (tid == 0 ? out.del_off : tid == 1 ? out.upd_off : out.add_off)[T] = carry[tid];
+    }
+}
+
+// One wave per deferred chunk: per-topology offsets += the chunk's bases, entries moved
+// from [cap + record offset, +count) to [base, +count) of the same arrays (never overlapping).
+__global__ void __launch_bounds__(BLOCK) k_place(DevTopos T, const uint32_t* wcount, const uint32_t* wbase,
+                                                 const uint32_t* first_partial, RecOut out, uint32_t m_cap,
+                                                 uint32_t n_cap, uint32_t nwg) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wg = blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
+    if (wg >= nwg || wg <= *first_partial) return;          // prefix chunks wrote final positions
+    const uint32_t t0 = wg * TPW, nt = min((uint32_t)TPW, T.n - t0);
+    const uint32_t cd = wcount[(size_t)wg * 3], cu = wcount[(size_t)wg * 3 + 1], ca = wcount[(size_t)wg * 3 + 2];
+    const uint32_t bd = wbase[(size_t)wg * 3], bu = wbase[(size_t)wg * 3 + 1], ba = wbase[(size_t)wg * 3 + 2];
+    if (lane < nt) {
+        out.del_off[t0 + lane] += bd;
+        out.upd_off[t0 + lane] += bu;
+        out.add_off[t0 + lane] += ba;
+    }
+    const uint32_t sd = m_cap + T.real_off[t0], sa = n_cap + T.des_off[t0];
+    const bool res = out.stages & KDTN_STAGE_RESOLVE, qd = out.stages & KDTN_STAGE_QDISC;
+    constexpr int V = DEFAULT_VARIANT;
+    for (uint32_t k = lane; k < cd; k += 64) {
+        store_idx<V>(out.del_idx + bd + k, out.del_idx[sd + k]);
+        if (res) store_res<V>(out.del_res + bd + k, out.del_res[sd + k]);
+    }
+    for (uint32_t k = lane; k < cu; k += 64) {
+        store_idx<V>(out.upd_idx + bu + k, out.upd_idx[sd + k]);
+        if (res) store_res<V>(out.upd_res + bu + k, out.upd_res[sd + k]);
+    }
+    for (uint32_t k = lane; k < ca; k += 64) {
+        store_idx<V>(out.add_idx + ba + k, out.add_idx[sa + k]);
+        if (res) store_res<V>(out.add_res + ba + k, out.add_res[sa + k]);
+    }
+    if (qd) {
+        for (uint32_t k = lane; k < cu * 9; k += 64)
+            store_q8<V>(out.upd_qdisc + (size_t)bu * 9 + k, out.upd_qdisc[(size_t)sd * 9 + k]);
+        for (uint32_t k = lane; k < ca * 9; k += 64)
+            store_q8<V>(out.add_qdisc + (size_t)ba * 9 + k, out.add_qdisc[(size_t)sa * 9 + k]);
+    }
 }
 
 // Standalone MakeQdiscs over a batch of property sets (kdtn_make_qdiscs).

@@ -1,6 +1,6 @@
 """HBM traffic per k_reconcile launch from the FETCH_SIZE / WRITE_SIZE PMC passes.
 
-    python tools/pmc_traffic.py <gpurun_out/TAG> <profiles/OUT.json> [links_per_gpu]
+    python tools/pmc_traffic.py <gpurun_out/TAG> <profiles/OUT.json> [links_per_gpu] [config] [glob]
 
 Reads the rocprofv3 counter CSVs of tools/gpu_round.sh's `pmc` step (one pass per counter:
 they cannot share a pass on gfx950) and applies MI355X_MICROARCH.md § HBM: FETCH_SIZE and
@@ -18,12 +18,14 @@ import sys
 def main():
     root, dst = sys.argv[1], sys.argv[2]
     links = int(sys.argv[3]) if len(sys.argv) > 3 else 10_000_000
+    config = int(sys.argv[4]) if len(sys.argv) > 4 else 2
+    pat = sys.argv[5] if len(sys.argv) > 5 else "pmc*"
     vals = collections.defaultdict(list)
-    for f in sorted(glob.glob(f"{root}/pmc*/**/*counter_collection.csv", recursive=True)):
+    for f in sorted(glob.glob(f"{root}/{pat}/**/*counter_collection.csv", recursive=True)):
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"].split("(")[0].replace("kdtn::", "").replace("void ", "")
             vals[(k, r["Counter_Name"])].append(float(r["Counter_Value"]))
-    out = {"source": root, "links_per_gpu": links, "kernels": {}}
+    out = {"source": root, "links_per_gpu": links, "config": config, "kernels": {}}
     for (k, c), v in sorted(vals.items()):
         if k.startswith("__amd"):
             continue
