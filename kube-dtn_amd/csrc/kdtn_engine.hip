@@ -57,6 +57,7 @@ struct DevLinkStore {
 
 struct kdtn_ctx {
     int device = 0;
+    uint32_t n_cus = 256;
     kdtn_config cfg{};
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
@@ -486,6 +487,7 @@ int kdtn_init(kdtn_ctx** out, const kdtn_config* cfg) {
     kdtn_ctx* c = new kdtn_ctx();
     c->device = dev;
     c->cfg = *cfg;
+    c->n_cus = (uint32_t)std::max(1, prop.multiProcessorCount);
     if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return KDTN_EIO;
@@ -768,6 +770,9 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         w.n_cap = c->des.n;
         uint32_t* wbase = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(w.wcount) + align_up((size_t)c->nwg * 12, 16));
         bool placed = false;                                        // VAR_DIFF: k_place_scan + k_place
+        // several workgroups per chunk when the chunks would not fill the chip about four times
+        // over (4 resident k_reconcile workgroups per CU): they share a bulk chunk's records
+        w.split = std::max<uint32_t>(1, std::min<uint32_t>(4, (4 * 4 * c->n_cus + c->nwg - 1) / c->nwg));
         k_full_prefix<<<(unsigned)std::min<uint64_t>(FP_GRID, (c->T + 4 * FP_BLOCK - 1) / (4 * FP_BLOCK)), FP_BLOCK, 0, s>>>(
             T, misc + MISC_FIRST_PARTIAL);
         timer_mark(c, "full_prefix");
@@ -775,25 +780,26 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         int variant = DEFAULT_VARIANT;
         if (const char* ev = std::getenv("KDTN_VARIANT")) variant = std::atoi(ev);
         if (variant & VAR_TRACE) {
+            w.split = 1;                                           // trace slots per chunk
             TRY(ensure(c->trace, (size_t)c->nwg * TRACE_WORDS * 8));
             w.trace = reinterpret_cast<unsigned long long*>(c->trace.p);
             c->traced = true;
         }
         switch (variant) {
 #define KDTN_VARIANT_CASE(V) \
-        case V: k_reconcile<V><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); placed = (V & VAR_DIFF) != 0; break;
+        case V: k_reconcile<V><<<c->nwg * w.split, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); placed = (V & VAR_DIFF) != 0; break;
         KDTN_PROFILING_VARIANTS(KDTN_VARIANT_CASE)
 #undef KDTN_VARIANT_CASE
         default:
-            k_reconcile<DEFAULT_VARIANT><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w);
+            k_reconcile<DEFAULT_VARIANT><<<c->nwg * w.split, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w);
             break;
         }
 #else
         if (c->real.n && c->des.n) {             // CalcDiff windows: the comparison-heavy build
-            k_reconcile<DEFAULT_VARIANT | VAR_DIFF><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w);
+            k_reconcile<DEFAULT_VARIANT | VAR_DIFF><<<c->nwg * w.split, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w);
             placed = true;
         } else {
-            k_reconcile<DEFAULT_VARIANT><<<c->nwg, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w);
+            k_reconcile<DEFAULT_VARIANT><<<c->nwg * w.split, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w);
         }
 #endif
         timer_mark(c, "reconcile");

@@ -1208,23 +1208,12 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
     const int tid = threadIdx.x;
     unsigned long long t_entry = 0;
     if constexpr ((V & VAR_TRACE) != 0) t_entry = __builtin_amdgcn_s_memrealtime();
-    if (tid == 0) {
-        if constexpr ((V & VAR_XCD) != 0) {
-            // every chunk emits all of its records (no look-back anywhere): a static map that
-            // gives XCD x (= blockIdx % 8) the contiguous chunks [start(x), start(x) + count(x)),
-            // so an XCD's L2 sees the dictionary ids of its own range of links
-            if (*wk.first_partial >= wk.nwg) {
-                const uint32_t x = blockIdx.x & 7u, k = blockIdx.x >> 3, q = wk.nwg >> 3, r = wk.nwg & 7u;
-                s.ticket = x * q + min(x, r) + k;
-            } else {
-                s.ticket = atomicAdd(&wk.sync[0], 1u);
-            }
-        } else {
-            s.ticket = atomicAdd(&wk.sync[0], 1u);      // dispatch order → look-back order
-        }
-    }
+    if (tid == 0) s.ticket = atomicAdd(&wk.sync[0], 1u);   // dispatch order → look-back order
     __syncthreads();
-    const uint32_t wg = s.ticket;
+    // wk.split workgroups per chunk: part 0 does the chunk's work; in a bulk chunk of the full
+    // prefix (bases known without predecessors) the parts share its records, so a small epoch
+    // whose chunks hold many records does not leave most of the chip idle in a second round
+    const uint32_t wg = s.ticket / wk.split, part = s.ticket - wg * wk.split;
     if constexpr ((V & VAR_TRACE) != 0) {
         trace_mark<V>(wk, wg, 0, t_entry);
         uint32_t xcc, hw;
@@ -1265,6 +1254,12 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
     // bulk: no topology of this workgroup has both lists non-empty (new pods: status empty;
     // deleted pods: spec nil) → every record of a DIFF topology is an entry, in order
     const bool bulk = s.any_cmp == 0;
+    const bool prefix = (V & VAR_NO_PREFIX) == 0 && wg <= *wk.first_partial;
+    const bool shared = bulk && prefix;                  // the parts split the records
+    if (part != 0 && !shared) return;                    // (block-uniform)
+    const bool lead = part == 0;
+    const uint32_t per = shared ? (tot + wk.split - 1) / wk.split : tot;
+    const uint32_t rlo = min(tot, part * per), rhi = min(tot, rlo + per);
 
     // ---- 1. Reconcile gate + CalcDiff ------------------------------------------------
     if (bulk) {
@@ -1355,7 +1350,6 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
     // k_full_prefix found no earlier exception): the batch bases are the record offsets of
     // the chunk, known without waiting on the predecessors. The inclusive prefix is
     // published at once so that later workgroups' look-backs stop here.
-    const bool prefix = (V & VAR_NO_PREFIX) == 0 && wg <= *wk.first_partial;
     // Comparison build: a chunk behind the full prefix does not wait for its predecessors'
     // windows. It emits at record-offset bases into the upper halves of the output arrays
     // (every list of a chunk holds at most as many entries as its records), and k_place moves
@@ -1363,15 +1357,15 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
     constexpr bool kDefer = (V & VAR_DIFF) != 0;
     const bool deferred = kDefer && !prefix;
     if constexpr (kDefer) {
-        if (tid < 3) wk.wcount[(size_t)wg * 3 + tid] = s.wtot[tid];
+        if (lead && tid < 3) wk.wcount[(size_t)wg * 3 + tid] = s.wtot[tid];
     }
     if (prefix) {
-        if (tid < 3) {
+        if (lead && tid < 3) {
             const uint32_t p = tid == 0 ? s.ooff[0] : (tid == 1 ? 0u : s.noff[0]);
             __hip_atomic_store(wk.status + (size_t)wg * 3 + tid, (2ull << 32) | (p + s.wtot[tid]),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s.base[tid] = p;
         }
+        if (tid < 3) s.base[tid] = tid == 0 ? s.ooff[0] : (tid == 1 ? 0u : s.noff[0]);
         __syncthreads();
     } else if (deferred) {
         if (tid < 3) s.base[tid] = tid == 2 ? wk.n_cap + s.noff[0] : wk.m_cap + s.ooff[0];
@@ -1381,12 +1375,12 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
     }
     trace_mark<V>(wk, wg, 3);
     const uint32_t bd = s.base[0], bu = s.base[1], ba = s.base[2];
-    if (!kDefer && wg == wk.nwg - 1 && tid < 3) {             // comparison build: k_place_scan
+    if (!kDefer && lead && wg == wk.nwg - 1 && tid < 3) {             // comparison build: k_place_scan
         const uint32_t total = s.base[tid] + s.wtot[tid];
         out.totals[tid] = total;
         (tid == 0 ? out.del_off : tid == 1 ? out.upd_off : out.add_off)[T.n] = total;
     }
-    if (tid < nt) {
+    if (lead && tid < nt) {
         out.action[t0 + tid] = s.act[tid];
         out.del_off[t0 + tid] = (deferred ? 0u : bd) + s.tcnt[0][tid];   // k_place adds the base
         out.upd_off[t0 + tid] = (deferred ? 0u : bu) + s.tcnt[1][tid];
@@ -1402,7 +1396,7 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
         struct Slot { uint32_t x; int tt; bool old, on; };
         auto decode = [&](uint32_t r) {
             Slot sl{0u, 0, false, false};
-            if (r < tot) {
+            if (r < rhi) {
                 sl.old = r < no;
                 sl.x = sl.old ? o0 + r : n0 + (r - no);
                 sl.tt = find_seg(sl.old ? s.ooff : s.noff, 0, nt, sl.x);
@@ -1415,7 +1409,7 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
         };
         if constexpr ((V & VAR_DIFF) != 0) {
             // comparison-heavy build: one record at a time (fewer registers, more waves)
-            for (uint32_t b = 0; b < tot; b += BLOCK) {
+            for (uint32_t b = rlo; b < rhi; b += BLOCK) {
                 const Slot cs = decode(b + tid);
                 bool qa = false;
                 uint32_t e = 0, q[18];
@@ -1437,10 +1431,10 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
             trace_mark<V>(wk, wg, 4);
             return;
         }
-        Slot cs = decode(tid);
+        Slot cs = decode(rlo + tid);
         RecCols cc;
         fetch(cs, cc);
-        for (uint32_t b = 0; b < tot; b += BLOCK) {
+        for (uint32_t b = rlo; b < rhi; b += BLOCK) {
             const Slot nx = decode(b + BLOCK + tid);
             RecCols nc;
             bool qa = false;
