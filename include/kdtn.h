@@ -454,11 +454,30 @@ int kdtn_json_upload(kdtn_ctx* ctx, const uint8_t* doc, uint64_t n);
 /* Decode the uploaded document on the GPU into the epoch inputs (synchronous). vnis:
  * VxlanManager snapshot (NULL = empty), with ids in the document's kdict: strings not in
  * the document cannot be referenced, so a snapshot is given as kdict ids of the result of
- * a previous ingest of the same document shape. Single-shard contexts only (nranks == 1).
+ * a previous ingest of the same document shape. Single-shard contexts only (nranks == 1;
+ * a rank of several uses kdtn_json_ingest_shard).
  * Returns KDTN_OK, KDTN_EBADMSG (info->json_err says why) or an engine error. */
 int kdtn_json_ingest(kdtn_ctx* ctx, const kdtn_vni_table* vnis, kdtn_ingest_info* info);
 /* D2H of the decoded tables of the last successful ingest. */
 int kdtn_ingest_download(kdtn_ctx* ctx, kdtn_ingest_tables* out);
+
+/* Sharded ingest for one rank of nshards (SURVEY §8(e) with §8(f) rank 2). Every controller
+ * replica's informer holds the whole Topology store (the controller watches all Topologies,
+ * controllers/topology_controller.go:332-339), so every rank decodes the WHOLE TopologyList:
+ * dictionary ids are then identical on every rank (first occurrence in one document) and
+ * each rank fills the pod-status row of every Topology itself — no exchange. The epoch is
+ * cut down on the GPU to the Topologies this rank owns (kdtn_topology_shard(namespace,
+ * name, nshards) == shard, document order kept; topology table and both link stores
+ * compacted), and peers are reported as document indices (kdtn_resolved.peer_topo = the
+ * unsharded topology index). Leaves the context as rank `shard` of `nshards` with its pod
+ * table in place, so kdtn_epoch_run follows directly. info: the shard's n_topos /
+ * n_desired / n_realised and the document's dictionaries; kdtn_ingest_download returns the
+ * shard's tables. A context with an RCCL communicator is refused. */
+int kdtn_json_ingest_shard(kdtn_ctx* ctx, const kdtn_vni_table* vnis, uint32_t nshards, uint32_t shard,
+                           kdtn_ingest_info* info);
+/* Document index of each of the last ingest's topologies ([info.n_topos]; the identity
+ * after an unsharded ingest). */
+int kdtn_ingest_shard_topos(kdtn_ctx* ctx, uint32_t* doc_index);
 
 /* ---- multi-GPU (one process per GPU) ---------------------------------------------------- */
 /* Owner shard of a Topology: hash64(namespace ‖ "/" ‖ name) mod nshards (SURVEY.md §8(e);

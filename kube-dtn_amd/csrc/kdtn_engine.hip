@@ -72,9 +72,14 @@ struct kdtn_ctx {
 
     // topologies
     DevBuf t_ns, t_name, t_src, t_netns, t_flags, t_roff, t_noff;
+    // sharded ingest: selection, scans, the shard's tables before they are swapped in
+    DevBuf sh_keep, sh_kreal, sh_kdes, sh_tidx, sh_roff64, sh_noff64, sh_doc;
+    DevBuf sh_ns, sh_name, sh_src, sh_netns, sh_flags, sh_roff, sh_noff;
     uint32_t T = 0;
     // links
     DevLinkStore real, des;
+    DevLinkStore sh_real, sh_des;              // sharded ingest: the shard's link stores (swapped in)
+    uint32_t sh_T = 0;                         // sharded ingest: topologies of the shard (doc index table)
     // vni table
     DevBuf v_node, v_vni, v_netns, v_ents, v_slots, v_table;
     uint32_t V = 0, vni_mask = 0;
@@ -525,7 +530,10 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->j_part, &c->j_tflags, &c->j_owner, &c->j_vown, &c->j_kslots, &c->j_krep,
                       &c->j_pslots, &c->j_prep, &c->j_heap, &c->j_bits, &c->j_bcnt, &c->j_wrank,
                       &c->j_kslot_id, &c->j_pslot_id, &c->j_len, &c->j_off64, &c->j_ocnt, &c->j_ooff,
-                      &c->j_olist, &c->j_ccnt, &c->j_coff, &c->j_vlist};
+                      &c->j_olist, &c->j_ccnt, &c->j_coff, &c->j_vlist, &c->sh_keep, &c->sh_kreal,
+                      &c->sh_kdes, &c->sh_tidx, &c->sh_roff64, &c->sh_noff64, &c->sh_doc, &c->sh_ns,
+                      &c->sh_name, &c->sh_src, &c->sh_netns, &c->sh_flags, &c->sh_roff, &c->sh_noff,
+                      &c->sh_des.buf, &c->sh_real.buf};
     for (DevBuf* b : bufs) release(*b);
     for (int i = 0; i <= kMaxTimers; ++i)
         if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
@@ -1347,13 +1355,10 @@ int kdtn_json_upload(kdtn_ctx* c, const uint8_t* doc, uint64_t n) {
     return KDTN_OK;
 }
 
-int kdtn_json_ingest(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest_info* info) {
+static int json_ingest_full(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest_info* info) {
     if (!c || !c->j_loaded) return KDTN_EINVAL;
-    if (c->nranks > 1) {
-        std::snprintf(g_last_error, sizeof(g_last_error), "kdtn_json_ingest: single-shard contexts only");
-        return KDTN_EINVAL;
-    }
     HIP_TRY(hipSetDevice(c->device));
+    c->sh_T = 0;
     g_last_error[0] = 0;
     hipStream_t s = c->stream;
     c->j_info = kdtn_ingest_info{};
@@ -1592,6 +1597,115 @@ int kdtn_json_ingest(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest_info* 
     if (info) *info = c->j_info;
     c->j_done = true;
     c->uploaded = true;
+    return KDTN_OK;
+}
+
+int kdtn_json_ingest(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest_info* info) {
+    if (c && c->nranks > 1) {
+        std::snprintf(g_last_error, sizeof(g_last_error),
+                      "kdtn_json_ingest: single-shard contexts (kdtn_json_ingest_shard for a rank of several)");
+        return KDTN_EINVAL;
+    }
+    return json_ingest_full(c, vnis, info);
+}
+
+// The whole document decoded as for one GPU, then the epoch cut down to this shard's
+// Topologies on the GPU: the full table fills the pod-status rows of every Topology (pod
+// index = document index), the shard's topology rows and records are compacted into fresh
+// tables that are swapped in, and the context is left as a rank whose pod table is in place.
+int kdtn_json_ingest_shard(kdtn_ctx* c, const kdtn_vni_table* vnis, uint32_t nshards, uint32_t shard,
+                           kdtn_ingest_info* info) {
+    if (!c || nshards < 1 || shard >= nshards || nshards > 0x7FFFFFFFu) return KDTN_EINVAL;
+    if (c->comm) {
+        std::snprintf(g_last_error, sizeof(g_last_error),
+                      "kdtn_json_ingest_shard: the context has an RCCL communicator (no exchange is needed)");
+        return KDTN_EINVAL;
+    }
+    c->nranks = 1;
+    c->rank = 0;
+    TRY(json_ingest_full(c, vnis, info));
+    if (nshards == 1) return KDTN_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const uint32_t Tf = c->T, Mf = c->real.n, Nf = c->des.n;
+    const DevTopos full = topo_view(c);
+    // 1. selection and the shard's offsets
+    for (DevBuf* b : {&c->sh_keep, &c->sh_kreal, &c->sh_kdes}) TRY(ensure(*b, ((size_t)Tf + 1) * 4));
+    for (DevBuf* b : {&c->sh_tidx, &c->sh_roff64, &c->sh_noff64}) TRY(ensure(*b, ((size_t)Tf + 1) * 8));
+    if (Tf)
+        k_shard_mark<<<nblocks(Tf), BLOCK, 0, s>>>(full, dp<uint8_t>(c->kd_bytes), dp<uint32_t>(c->kd_offs), nshards,
+                                                   shard, dp<uint32_t>(c->sh_keep), dp<uint32_t>(c->sh_kreal),
+                                                   dp<uint32_t>(c->sh_kdes));
+    TRY(scan_u32(c, dp<uint32_t>(c->sh_keep), Tf, dp<uint64_t>(c->sh_tidx)));
+    TRY(scan_u32(c, dp<uint32_t>(c->sh_kreal), Tf, dp<uint64_t>(c->sh_roff64)));
+    TRY(scan_u32(c, dp<uint32_t>(c->sh_kdes), Tf, dp<uint64_t>(c->sh_noff64)));
+    uint64_t cnt[3] = {0, 0, 0};
+    TRY(d2h(c, cnt, dp<uint64_t>(c->sh_tidx) + Tf));
+    TRY(d2h(c, cnt + 1, dp<uint64_t>(c->sh_roff64) + Tf));
+    TRY(d2h(c, cnt + 2, dp<uint64_t>(c->sh_noff64) + Tf));
+    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(hipGetLastError());
+    const uint32_t Ts = (uint32_t)cnt[0], Ms = (uint32_t)cnt[1], Ns = (uint32_t)cnt[2];
+    // 2. the shard's tables
+    for (DevBuf* b : {&c->sh_ns, &c->sh_name, &c->sh_src, &c->sh_netns, &c->sh_doc}) TRY(ensure(*b, ((size_t)Ts + 1) * 4));
+    TRY(ensure(c->sh_flags, (size_t)Ts + 1));
+    TRY(ensure(c->sh_roff, ((size_t)Ts + 1) * 4));
+    TRY(ensure(c->sh_noff, ((size_t)Ts + 1) * 4));
+    TRY(link_store_alloc(c, c->sh_real, Ms));
+    TRY(link_store_alloc(c, c->sh_des, Ns));
+    HIP_TRY(hipMemsetAsync(c->sh_real.buf.p, 0, c->sh_real.buf.cap, s));   // tile padding as an upload leaves it
+    HIP_TRY(hipMemsetAsync(c->sh_des.buf.p, 0, c->sh_des.buf.cap, s));
+    DevTopos out{dp<uint32_t>(c->sh_ns), dp<uint32_t>(c->sh_name), dp<uint32_t>(c->sh_src), dp<uint32_t>(c->sh_netns),
+                 dp<uint8_t>(c->sh_flags), dp<uint32_t>(c->sh_roff), dp<uint32_t>(c->sh_noff), Ts};
+    k_shard_topos<<<nblocks((uint64_t)Tf + 1), BLOCK, 0, s>>>(full, dp<uint32_t>(c->sh_keep), dp<uint64_t>(c->sh_tidx),
+                                                              dp<uint64_t>(c->sh_roff64), dp<uint64_t>(c->sh_noff64), out,
+                                                              dp<uint32_t>(c->sh_doc));
+    if (Mf)
+        k_shard_links<<<nblocks(Mf), BLOCK, 0, s>>>(c->real.view, full.real_off, Tf, dp<uint32_t>(c->sh_keep),
+                                                    dp<uint64_t>(c->sh_roff64), dp<uint32_t>(c->sh_real.buf));
+    if (Nf)
+        k_shard_links<<<nblocks(Nf), BLOCK, 0, s>>>(c->des.view, full.des_off, Tf, dp<uint32_t>(c->sh_keep),
+                                                    dp<uint64_t>(c->sh_noff64), dp<uint32_t>(c->sh_des.buf));
+    HIP_TRY(hipGetLastError());
+    // 3. a rank of nshards with every Topology's pod-status row: pod index = document index
+    const uint32_t slice = (Tf + nshards - 1) / nshards;
+    c->nranks = (int)nshards;
+    c->rank = (int)shard;
+    c->T = Ts;
+    const kdtn_vni_table none{0, nullptr, nullptr, nullptr};
+    TRY(prepare_epoch(c, vnis ? *vnis : none, slice, Ms, Ns));
+    if (c->pod_total)
+        k_pods_fill<<<nblocks(c->pod_total), BLOCK, 0, s>>>(full, c->pod_total, 0u, dp<uint4>(c->pods));
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(s));                // the full tables are read until here
+    std::swap(c->t_ns, c->sh_ns);
+    std::swap(c->t_name, c->sh_name);
+    std::swap(c->t_src, c->sh_src);
+    std::swap(c->t_netns, c->sh_netns);
+    std::swap(c->t_flags, c->sh_flags);
+    std::swap(c->t_roff, c->sh_roff);
+    std::swap(c->t_noff, c->sh_noff);
+    std::swap(c->real, c->sh_real);
+    std::swap(c->des, c->sh_des);
+    c->sh_T = Ts;
+    c->pods_imported = true;
+    c->j_info.n_topos = Ts;
+    c->j_info.n_desired = Ns;
+    c->j_info.n_realised = Ms;
+    if (info) *info = c->j_info;
+    return KDTN_OK;
+}
+
+int kdtn_ingest_shard_topos(kdtn_ctx* c, uint32_t* doc_index) {
+    if (!c || !c->j_done || (c->sh_T && !doc_index)) return KDTN_EINVAL;
+    HIP_TRY(hipSetDevice(c->device));
+    if (c->nranks == 1) {                            // unsharded: the identity
+        for (uint32_t t = 0; t < c->T; ++t) doc_index[t] = t;
+        return KDTN_OK;
+    }
+    if (c->sh_T)
+        HIP_TRY(hipMemcpyAsync(doc_index, c->sh_doc.p, (size_t)c->sh_T * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
     return KDTN_OK;
 }
 

@@ -28,6 +28,7 @@
 //                   ids = rank of the first occurrence in document order (bitmap popcount
 //                   scan), dictionary arenas in id order, table slots → ids
 #include "kdtn_kernels.h"
+#include "kdtn_shard.h"
 
 namespace kdtn {
 
@@ -1421,6 +1422,70 @@ __global__ void __launch_bounds__(BLOCK) k_js_finalize_topos(JsTopoOut to, uint3
         if (v) cols[k][t] = kslot_id[v - 1];
     }
     flags8[t] = (uint8_t)to.flags[t];
+}
+
+// ---------------------------------------------------------------- sharded ingest
+// Topology t belongs to this shard when kdtn_topology_shard(namespace, name) says so
+// (kdtn_shard.h, the host function itself); kreal / kdes are its record counts when kept.
+__global__ void __launch_bounds__(BLOCK) k_shard_mark(DevTopos T, const uint8_t* kd_bytes, const uint32_t* kd_offs,
+                                                      uint32_t nshards, uint32_t shard, uint32_t* keep,
+                                                      uint32_t* kreal, uint32_t* kdes) {
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= T.n) return;
+    const uint32_t a = T.ns[t], b = T.name[t];
+    const uint32_t a0 = kd_offs[a], a1 = kd_offs[a + 1], b0 = kd_offs[b], b1 = kd_offs[b + 1];
+    const bool k = topology_shard(kd_bytes + a0, a1 - a0, kd_bytes + b0, b1 - b0, nshards) == shard;
+    keep[t] = k ? 1u : 0u;
+    kreal[t] = k ? T.real_off[t + 1] - T.real_off[t] : 0u;
+    kdes[t] = k ? T.des_off[t + 1] - T.des_off[t] : 0u;
+}
+
+// kept topology t → row tidx[t] of the shard's table (offsets from the kept counts' scans)
+__global__ void __launch_bounds__(BLOCK) k_shard_topos(DevTopos T, const uint32_t* keep, const uint64_t* tidx,
+                                                       const uint64_t* roff, const uint64_t* noff, DevTopos out,
+                                                       uint32_t* doc_index) {
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t > T.n) return;
+    if (t == T.n) {                                                 // closing offsets
+        const uint32_t n = (uint32_t)tidx[t];
+        const_cast<uint32_t*>(out.real_off)[n] = (uint32_t)roff[t];
+        const_cast<uint32_t*>(out.des_off)[n] = (uint32_t)noff[t];
+        return;
+    }
+    if (!keep[t]) return;
+    const uint32_t r = (uint32_t)tidx[t];
+    const_cast<uint32_t*>(out.ns)[r] = T.ns[t];
+    const_cast<uint32_t*>(out.name)[r] = T.name[t];
+    const_cast<uint32_t*>(out.src_ip)[r] = T.src_ip[t];
+    const_cast<uint32_t*>(out.net_ns)[r] = T.net_ns[t];
+    const_cast<uint8_t*>(out.flags)[r] = T.flags[t];
+    const_cast<uint32_t*>(out.real_off)[r] = (uint32_t)roff[t];
+    const_cast<uint32_t*>(out.des_off)[r] = (uint32_t)noff[t];
+    doc_index[r] = t;
+}
+
+// one thread per record of one side: its topology by binary search over the document's
+// offsets (the largest t with off[t] <= j), copied with its 22 words when the topology is kept
+__global__ void __launch_bounds__(BLOCK) k_shard_links(DevLinks in, const uint32_t* off, uint32_t nt,
+                                                       const uint32_t* keep, const uint64_t* noff,
+                                                       uint32_t* out_base) {
+    const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= in.n) return;
+    uint32_t lo = 0, hi = nt;                                       // off[lo] <= j < off[hi]
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (off[mid] <= j) lo = mid;
+        else hi = mid;
+    }
+    if (!keep[lo]) return;
+    const uint32_t d = (uint32_t)noff[lo] + (j - off[lo]);
+    const uint32_t* src = in.base + (size_t)(j >> 6) * TILE_WORDS + (j & 63u);
+    uint32_t* dst = out_base + (size_t)(d >> 6) * TILE_WORDS + (d & 63u);
+#pragma unroll
+    for (int c = 0; c < LINK_COLS32; ++c) dst[c * TILE_RECS] = src[c * TILE_RECS];
+    const int64_t* su = reinterpret_cast<const int64_t*>(in.base + (size_t)(j >> 6) * TILE_WORDS + LINK_COLS32 * TILE_RECS);
+    int64_t* du = reinterpret_cast<int64_t*>(out_base + (size_t)(d >> 6) * TILE_WORDS + LINK_COLS32 * TILE_RECS);
+    du[d & 63u] = su[j & 63u];
 }
 
 }  // namespace kdtn

@@ -422,4 +422,13 @@ __global__ void k_js_dict_copy(JsDict dt, JsIntern in, const uint32_t* slot_id, 
 __global__ void k_js_finalize_links(JsStore st, uint32_t n, const uint32_t* kslot_id, const uint32_t* pslot_id);
 __global__ void k_js_finalize_topos(JsTopoOut to, uint32_t T, const uint32_t* kslot_id, uint8_t* flags8);
 
+// sharded ingest (kdtn_json_ingest_shard): keep[t] = this shard owns topology t; then the
+// kept topologies' columns and records compacted into fresh tables (document order kept)
+__global__ void k_shard_mark(DevTopos T, const uint8_t* kd_bytes, const uint32_t* kd_offs, uint32_t nshards,
+                             uint32_t shard, uint32_t* keep, uint32_t* kreal, uint32_t* kdes);
+__global__ void k_shard_topos(DevTopos T, const uint32_t* keep, const uint64_t* tidx, const uint64_t* roff,
+                              const uint64_t* noff, DevTopos out, uint32_t* doc_index);
+__global__ void k_shard_links(DevLinks in, const uint32_t* off, uint32_t nt, const uint32_t* keep,
+                              const uint64_t* noff, uint32_t* out_base);
+
 }  // namespace kdtn

@@ -6,11 +6,19 @@
 #pragma once
 #include <stdint.h>
 
+// callable from host code and, in HIP translation units, from kernels (the sharded ingest
+// picks a rank's Topologies on the GPU with the same function)
+#if defined(__HIPCC__)
+#define KDTN_SHARD_FN __host__ __device__ inline
+#else
+#define KDTN_SHARD_FN inline
+#endif
+
 namespace kdtn {
 
 // FNV-1a 64 over the key bytes, then the murmur3 fmix64 finalizer (FNV's low bits alone are
 // weak for short, similar keys like "default/p123").
-inline uint64_t topology_key_hash(const uint8_t* ns, uint32_t ns_len, const uint8_t* name, uint32_t name_len) {
+KDTN_SHARD_FN uint64_t topology_key_hash(const uint8_t* ns, uint32_t ns_len, const uint8_t* name, uint32_t name_len) {
     uint64_t h = 1469598103934665603ull;
     for (uint32_t i = 0; i < ns_len; ++i) h = (h ^ ns[i]) * 1099511628211ull;
     h = (h ^ (uint8_t)'/') * 1099511628211ull;
@@ -23,7 +31,7 @@ inline uint64_t topology_key_hash(const uint8_t* ns, uint32_t ns_len, const uint
     return h;
 }
 
-inline uint32_t topology_shard(const uint8_t* ns, uint32_t ns_len, const uint8_t* name, uint32_t name_len,
+KDTN_SHARD_FN uint32_t topology_shard(const uint8_t* ns, uint32_t ns_len, const uint8_t* name, uint32_t name_len,
                                uint32_t nshards) {
     return nshards <= 1 ? 0u : (uint32_t)(topology_key_hash(ns, ns_len, name, name_len) % nshards);
 }

@@ -170,7 +170,8 @@ EXPORTS = ["kdtn_version", "kdtn_strerror", "kdtn_err_name", "kdtn_init", "kdtn_
            "kdtn_epoch_download_wire", "kdtn_diff", "kdtn_resolve", "kdtn_host_alloc",
            "kdtn_host_free", "kdtn_epoch_fanout", "kdtn_epoch_tc", "kdtn_epoch_download_tc",
            "kdtn_json_upload", "kdtn_json_ingest", "kdtn_ingest_download", "kdtn_topology_shard",
-           "kdtn_comm_set_ranks", "kdtn_pods_export", "kdtn_pods_import"]
+           "kdtn_comm_set_ranks", "kdtn_pods_export", "kdtn_pods_import", "kdtn_json_ingest_shard",
+           "kdtn_ingest_shard_topos"]
 
 
 def ptr(a: np.ndarray, t):

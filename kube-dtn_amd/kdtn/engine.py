@@ -89,6 +89,9 @@ def lib() -> C.CDLL:
         "kdtn_json_upload": (C.c_int, [vp, C.c_char_p, C.c_uint64]),
         "kdtn_json_ingest": (C.c_int, [vp, C.POINTER(abi.VniTable), C.POINTER(abi.IngestInfo)]),
         "kdtn_ingest_download": (C.c_int, [vp, C.POINTER(abi.IngestTables)]),
+        "kdtn_json_ingest_shard": (C.c_int, [vp, C.POINTER(abi.VniTable), C.c_uint32, C.c_uint32,
+                                             C.POINTER(abi.IngestInfo)]),
+        "kdtn_ingest_shard_topos": (C.c_int, [vp, vp]),
         "kdtn_topology_shard": (C.c_uint32, [C.c_char_p, C.c_uint32, C.c_char_p, C.c_uint32, C.c_uint32]),
         "kdtn_comm_set_ranks": (C.c_int, [vp, C.c_int, C.c_int]),
         "kdtn_pods_export": (C.c_int, [vp, vp]),
@@ -192,26 +195,38 @@ class Engine:
         """H2D of a TopologyList JSON document (kdtn_json_upload)."""
         _check(lib().kdtn_json_upload(self._ctx, doc, len(doc)), "kdtn_json_upload")
 
-    def json_ingest(self, vnis=None) -> abi.IngestInfo:
+    def json_ingest(self, vnis=None, shard=None) -> abi.IngestInfo:
         """Decode the uploaded document on the GPU into device-resident epoch inputs
         (kdtn_json_ingest). A rejected document raises KdtnError(EBADMSG) whose .info holds
-        json_err / err_offset."""
+        json_err / err_offset. shard=(nshards, rank): the whole document decoded, the epoch
+        cut down to that rank's Topologies (kdtn_json_ingest_shard)."""
         info = abi.IngestInfo()
         cv = vnis.to_c() if vnis is not None else None
-        rc = lib().kdtn_json_ingest(self._ctx, C.byref(cv) if cv is not None else None, C.byref(info))
+        pv = C.byref(cv) if cv is not None else None
+        if shard is None:
+            name, rc = "kdtn_json_ingest", lib().kdtn_json_ingest(self._ctx, pv, C.byref(info))
+        else:
+            name = "kdtn_json_ingest_shard"
+            rc = lib().kdtn_json_ingest_shard(self._ctx, pv, int(shard[0]), int(shard[1]), C.byref(info))
         if rc == abi.EBADMSG:
-            e = KdtnError(rc, "kdtn_json_ingest")
+            e = KdtnError(rc, name)
             e.info = info
             raise e
-        _check(rc, "kdtn_json_ingest")
+        _check(rc, name)
         self._T = info.n_topos
         self._caps = (info.n_realised, info.n_desired, info.n_realised)
         self._ingest = info
         return info
 
-    def ingest(self, doc: bytes, vnis=None) -> abi.IngestInfo:
+    def ingest(self, doc: bytes, vnis=None, shard=None) -> abi.IngestInfo:
         self.json_upload(doc)
-        return self.json_ingest(vnis)
+        return self.json_ingest(vnis, shard)
+
+    def ingest_doc_index(self) -> np.ndarray:
+        """Document index of each topology of the last ingest (kdtn_ingest_shard_topos)."""
+        out = np.zeros(max(self._T, 1), np.uint32)
+        _check(lib().kdtn_ingest_shard_topos(self._ctx, out.ctypes.data), "kdtn_ingest_shard_topos")
+        return out[:self._T]
 
     def ingest_tables(self) -> EpochInput:
         """D2H of the tables the last json_ingest decoded (kdtn_ingest_download)."""
