@@ -496,7 +496,8 @@ uint32_t kdtn_topology_shard(const uint8_t* ns, uint32_t ns_len, const uint8_t* 
  * same kdict ids for pod names, namespaces, src_ip and net_ns strings (one shared
  * interner prefix). Transports:
  *   RCCL (production): kdtn_comm_init; kdtn_epoch_run all-gathers the rows over xGMI on a
- *     comm stream, overlapped with the dictionary parses.
+ *     comm stream, overlapped with the dictionary parses (nranks == 1 also builds a
+ *     one-rank communicator, so the RCCL path runs on a single GPU).
  *   host (any collective library, e.g. gloo): kdtn_comm_set_ranks; per epoch, after
  *     kdtn_epoch_upload: kdtn_pods_export → all-gather of pod_slice rows per rank in rank
  *     order → kdtn_pods_import → kdtn_epoch_run (KDTN_EINVAL if the import is missing). */
@@ -511,6 +512,9 @@ int kdtn_pods_export(kdtn_ctx* ctx, kdtn_pod_row* rows);                /* [pod_
 int kdtn_pods_import(kdtn_ctx* ctx, const kdtn_pod_row* rows, uint64_t n);   /* n = pod_slice*nranks */
 
 /* ---- profiling hooks: per-kernel HIP-event times of the last epoch_run (ms) -------- */
+/* Timing level of kdtn_epoch_run's HIP events (each costs ≈5 µs of stream time): 0 none,
+ * 1 k_reconcile and the placement kernels only, 2 every stage (default). */
+int kdtn_set_timing(kdtn_ctx* ctx, int level);
 int kdtn_last_kernel_times(kdtn_ctx* ctx, const char** names, float* ms, int cap);
 /* Per-workgroup phase timestamps of k_reconcile (100 MHz clock; 8 words per workgroup:
  * entry, topologies loaded, counts done, batch bases known, end, XCC_ID<<32|HW_ID, CalcDiff

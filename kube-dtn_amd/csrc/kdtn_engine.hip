@@ -117,7 +117,7 @@ struct kdtn_ctx {
     bool j_loaded = false, j_done = false;
     kdtn_ingest_info j_info{};
     // host-visible counters
-    uint32_t* h_misc = nullptr;   // pinned: [0]=default id, [1]=del, [2]=upd, [3]=add, [4]=look-back error
+    uint32_t* h_misc = nullptr;   // pinned: [1]=del, [2]=upd, [3]=add, [4]=look-back error (sync header words)
     bool uploaded = false;
     bool ran = false;
     uint32_t last_stages = 0;
@@ -125,7 +125,8 @@ struct kdtn_ctx {
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
     bool pods_imported = false;   // host transport: this epoch's global pod table is in place
-    // timers
+    // timers: 0 none, 1 k_reconcile (+ placement) only, 2 every stage (kdtn_set_timing)
+    int timing = 2;
     hipEvent_t ev[kMaxTimers + 1] = {};
     const char* ev_name[kMaxTimers] = {};
     int n_ev = 0;
@@ -213,7 +214,7 @@ int upload_dict(kdtn_ctx* c, DevBuf& bytes, DevBuf& offs, const kdtn_strtab& t, 
 // padded to 16 B (memset size % 16 == 0, cdna_hip_programming.md G16)
 // ticket + error word, look-back granules [nwg*3] u64, then VAR_DIFF counts and bases [nwg*3] u32 each
 // (16-B aligned: k_place_scan reads and writes them as uint4)
-size_t sync_counts_at(uint32_t nwg) { return align_up(16 + (size_t)nwg * 24, 16); }
+size_t sync_counts_at(uint32_t nwg) { return align_up(SYNC_HEADER_BYTES + (size_t)nwg * 24, 16); }
 size_t sync_bytes(uint32_t nwg) { return sync_counts_at(nwg) + 2 * align_up((size_t)nwg * 12, 16); }
 
 int check_strtab(const kdtn_strtab& t, const char* what) {
@@ -308,8 +309,10 @@ int upload_links(kdtn_ctx* c, DevLinkStore& s, const kdtn_link_table& L, uint32_
 
 uint32_t nblocks(uint64_t n, int block = BLOCK) { return (uint32_t)((n + block - 1) / block); }
 
-void timer_mark(kdtn_ctx* c, const char* name) {
-    if (c->n_ev >= kMaxTimers) return;
+// Each timing event costs ≈5 µs of stream time on MI355X (measured: two consecutive marks
+// with nothing between them read 5.4 µs), so epoch stages are marked at a level.
+void timer_mark(kdtn_ctx* c, const char* name, int level = 0) {
+    if (c->n_ev >= kMaxTimers || c->timing < level) return;
     c->ev_name[c->n_ev] = name;
     (void)hipEventRecord(c->ev[c->n_ev + 1], c->stream);
     c->n_ev++;
@@ -326,6 +329,12 @@ DevTopos topo_view(kdtn_ctx* c) {
     t.des_off = dp<uint32_t>(c->t_noff);
     t.n = c->T;
     return t;
+}
+
+// Special key-string ids (SPECIAL_DEFAULT / SPECIAL_LOCALHOST) at or past the parse start
+// are forgotten when an upload sets it; every run's k_kdict_flags re-finds them there.
+void clip_specials(kdtn_ctx* c) {
+    if (c->kd_special.p) k_special_clip<<<1, 64, 0, c->stream>>>(dp<uint32_t>(c->kd_special), c->kd_from & ~63u);
 }
 
 // per-string parse tables of both dictionaries (c->D, c->P set), keeping the parsed
@@ -355,6 +364,7 @@ int prepare_dicts(kdtn_ctx* c) {
     TRY(ensure_keep(c->pd_rate, (size_t)P * 8, pv * 8, s));
     TRY(ensure_keep(c->pd_rerr, (size_t)nblocks(P) * BLOCK / 8, (pv + 63) / 64 * 8, s));
     TRY(ensure(c->kd_special, 64));
+    clip_specials(c);
     return KDTN_OK;
 }
 
@@ -635,15 +645,14 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
     c->last_stages = stages;
     c->n_ev = 0;
     hipStream_t s = c->stream;
-    (void)hipEventRecord(c->ev[0], s);
-    uint32_t* misc = dp<uint32_t>(c->misc);
-    HIP_TRY(hipMemsetAsync(misc, 0xFF, 64, s));                       // first_partial etc. = 0xFFFFFFFF
-    HIP_TRY(hipMemsetAsync(c->sync.p, 0, sync_bytes(c->nwg), s));    // ticket, error, look-back
+    if (c->timing >= 2) (void)hipEventRecord(c->ev[0], s);
+    uint32_t* sync = dp<uint32_t>(c->sync);
+    HIP_TRY(hipMemsetAsync(sync, 0, sync_bytes(c->nwg), s));          // header (SYNC_*), look-back
 
     const DevTopos T = topo_view(c);
     const bool resolve = stages & KDTN_STAGE_RESOLVE;
     const bool host_xchg = resolve && c->nranks > 1 && !c->comm;      // rows imported by the caller
-    const bool exchange = resolve && c->nranks > 1 && c->comm;
+    const bool exchange = resolve && c->comm;                          // RCCL (a 1-rank comm too)
     if (host_xchg && !c->pods_imported) {
         std::snprintf(g_last_error, sizeof(g_last_error),
                       "host transport: kdtn_pods_import the gathered pod table before kdtn_epoch_run");
@@ -666,16 +675,15 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
             }
             HIP_TRY(hipEventRecord(c->ev_ag, c->comm_stream));
         }
-        timer_mark(c, "pods_fill");
+        timer_mark(c, "pods_fill", 2);
     } else if (resolve) {
-        timer_mark(c, "pods_fill");
+        timer_mark(c, "pods_fill", 2);
     }
     // dictionaries: the strings this upload added (all of them unless kdict_keep /
     // pdict_keep), from a multiple of 64 so every wave writes whole predicate words
     uint32_t* special = dp<uint32_t>(c->kd_special);
     {
-        const uint32_t k0 = c->kd_from & ~63u;
-        k_special_clip<<<1, 64, 0, s>>>(special, k0);                 // ids >= k0 are recomputed
+        const uint32_t k0 = c->kd_from & ~63u;                        // (clip_specials ran at upload)
         if (c->D > k0) {
             const uint8_t* kb = dp<uint8_t>(c->kd_bytes);
             const uint32_t* ko = dp<uint32_t>(c->kd_offs);
@@ -691,7 +699,7 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
             k_kdict_flags<1><<<nblocks(nk), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
         }
     }
-    timer_mark(c, "kdict_parse");
+    timer_mark(c, "kdict_parse", 2);
     {
         const uint32_t p0 = c->pd_from & ~63u;
         if (c->P > p0)
@@ -702,10 +710,10 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
     }
     c->kd_valid = c->D;
     c->pd_valid = c->P;
-    timer_mark(c, "pdict_parse");
+    timer_mark(c, "pdict_parse", 2);
     if (resolve) {
         if (exchange) HIP_TRY(hipStreamWaitEvent(s, c->ev_ag, 0));   // exchange not hidden by the parses
-        timer_mark(c, "pods_allgather");
+        timer_mark(c, "pods_allgather", 2);
         if (++c->pod_stamp >= 0x7FFFFFFFu) {                          // stamp wrap: clear once
             HIP_TRY(hipMemsetAsync(c->pod_direct.p, 0, c->pod_direct.cap, s));
             HIP_TRY(hipMemsetAsync(c->pod_ovf.p, 0, c->pod_ovf.cap, s));
@@ -729,7 +737,7 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
             k_vni_fill<<<nblocks(vcap), BLOCK, 0, s>>>(dp<uint4>(c->v_ents), dp<uint32_t>(c->v_slots), (uint32_t)vcap,
                                                        dp<uint4>(c->v_table));
         }
-        timer_mark(c, "hash_build");
+        timer_mark(c, "hash_build", 2);
     }
     if (c->T) {
         DevTables tb{};
@@ -762,17 +770,17 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         o.upd_res = dp<uint4>(c->upd_res);
         o.add_qdisc = dp<uint2>(c->add_qdisc);
         o.upd_qdisc = dp<uint2>(c->upd_qdisc);
-        o.totals = misc + 1;
+        o.totals = sync + SYNC_TOTALS;
         o.stages = stages;
         RecWork w;
-        w.sync = dp<uint32_t>(c->sync);
-        w.status = reinterpret_cast<unsigned long long*>(static_cast<char*>(c->sync.p) + 16);
+        w.sync = sync;
+        w.status = reinterpret_cast<unsigned long long*>(static_cast<char*>(c->sync.p) + SYNC_HEADER_BYTES);
         w.hscratch = dp<uint32_t>(c->hscratch);
         w.fscratch = dp<uint8_t>(c->fscratch);
         w.otarget = dp<uint32_t>(c->otarget);
         w.nwg = c->nwg;
         w.trace = nullptr;
-        w.first_partial = misc + MISC_FIRST_PARTIAL;                // 0xFFFFFFFF from the memset
+        w.first_partial_inv = sync + SYNC_FIRST_PARTIAL_INV;         // 0 (none) from the memset
         w.wcount = reinterpret_cast<uint32_t*>(static_cast<char*>(c->sync.p) + sync_counts_at(c->nwg));
         w.m_cap = c->real.n;
         w.n_cap = c->des.n;
@@ -782,8 +790,9 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         // over (4 resident k_reconcile workgroups per CU): they share a bulk chunk's records
         w.split = std::max<uint32_t>(1, std::min<uint32_t>(4, (4 * 4 * c->n_cus + c->nwg - 1) / c->nwg));
         k_full_prefix<<<(unsigned)std::min<uint64_t>(FP_GRID, (c->T + 4 * FP_BLOCK - 1) / (4 * FP_BLOCK)), FP_BLOCK, 0, s>>>(
-            T, misc + MISC_FIRST_PARTIAL);
-        timer_mark(c, "full_prefix");
+            T, sync + SYNC_FIRST_PARTIAL_INV);
+        timer_mark(c, "full_prefix", 2);
+        if (c->timing == 1) (void)hipEventRecord(c->ev[0], s);
 #if KDTN_PROFILING
         int variant = DEFAULT_VARIANT;
         if (const char* ev = std::getenv("KDTN_VARIANT")) variant = std::atoi(ev);
@@ -810,27 +819,25 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
             k_reconcile<DEFAULT_VARIANT><<<c->nwg * w.split, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w);
         }
 #endif
-        timer_mark(c, "reconcile");
+        timer_mark(c, "reconcile", 1);
         if (placed) {
             if ((size_t)c->real.n * 2 > c->del_idx.cap / 4 || (size_t)c->des.n * 2 > c->add_idx.cap / 4) {
                 std::snprintf(g_last_error, sizeof(g_last_error), "deferred placement without upper halves");
                 return KDTN_EINVAL;
             }
             k_place_scan<<<1, PLACE_SCAN_BLOCK, 0, s>>>(w.wcount, c->nwg, wbase, o, c->T);
-            timer_mark(c, "place_scan");
-            k_place<<<(c->nwg + BLOCK / 64 - 1) / (BLOCK / 64), BLOCK, 0, s>>>(T, w.wcount, wbase, w.first_partial, o,
+            timer_mark(c, "place_scan", 1);
+            k_place<<<(c->nwg + BLOCK / 64 - 1) / (BLOCK / 64), BLOCK, 0, s>>>(T, w.wcount, wbase, w.first_partial_inv, o,
                                                                               w.m_cap, w.n_cap, c->nwg);
-            timer_mark(c, "place");
+            timer_mark(c, "place", 1);
         }
     } else {
-        HIP_TRY(hipMemsetAsync(misc + 1, 0, 12, s));
         HIP_TRY(hipMemsetAsync(c->del_off.p, 0, 4, s));
         HIP_TRY(hipMemsetAsync(c->add_off.p, 0, 4, s));
         HIP_TRY(hipMemsetAsync(c->upd_off.p, 0, 4, s));
     }
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(c->h_misc, misc, 16, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(c->h_misc + 4, dp<uint32_t>(c->sync) + 1, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(c->h_misc + 1, sync + SYNC_TOTALS, 16, hipMemcpyDeviceToHost, s));   // totals, look-back error
     c->ran = true;
     c->encoded = false;
     c->tc_done = false;
@@ -1780,7 +1787,6 @@ int kdtn_comm_init(kdtn_ctx* c, const uint8_t uid[128], int nranks, int rank) {
     c->nranks = nranks;
     c->rank = rank;
     c->uploaded = false;
-    if (nranks == 1) return KDTN_OK;
     if (!c->comm_stream) {
         HIP_TRY(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
         HIP_TRY(hipEventCreateWithFlags(&c->ev_fill, hipEventDisableTiming));
@@ -1847,6 +1853,12 @@ int kdtn_debug_wg_trace(kdtn_ctx* c, uint64_t* out, uint32_t cap) {
     const uint32_t n = std::min<uint64_t>(cap, (uint64_t)c->nwg * TRACE_WORDS);
     HIP_TRY(hipMemcpy(out, c->trace.p, (size_t)n * 8, hipMemcpyDeviceToHost));
     return (int)n;
+}
+
+int kdtn_set_timing(kdtn_ctx* c, int level) {
+    if (!c || level < 0 || level > 2) return KDTN_EINVAL;
+    c->timing = level;
+    return KDTN_OK;
 }
 
 int kdtn_last_kernel_times(kdtn_ctx* c, const char** names, float* ms, int cap) {

@@ -48,7 +48,13 @@ enum : int {
     KB_NSETS = 3,
 };
 // special key-string ids found by k_kdict_flags (0xFFFFFFFF when absent)
-enum : int { SPECIAL_DEFAULT = 0, SPECIAL_LOCALHOST = 4, MISC_FIRST_PARTIAL = 8, MISC_FAN_NODES = 12 };   // misc words
+enum : int { SPECIAL_DEFAULT = 0, SPECIAL_LOCALHOST = 4, MISC_FAN_NODES = 12 };   // misc words
+// epoch sync header (u32 words; zeroed by the epoch's only memset, the look-back status
+// follows at SYNC_HEADER_BYTES). The ticket counter, which every k_reconcile workgroup
+// increments, has a 128-B line to itself; the host reads words [SYNC_TOTALS, SYNC_TOTALS + 4)
+// (totals, look-back error) back with one copy.
+enum : int { SYNC_TICKET = 0, SYNC_TOTALS = 32 /* [3] del, upd, add */, SYNC_ERR = 35,
+             SYNC_FIRST_PARTIAL_INV = 36 /* ~first partial chunk: 0 = none */, SYNC_HEADER_BYTES = 256 };
 // pod slot flag bits (in the g word of a wide slot; pod indices < 2^30)
 constexpr uint32_t POD_SPEC_NIL = 0x80000000u, POD_PHYSICAL = 0x40000000u, POD_INDEX = 0x3FFFFFFFu;
 
@@ -184,13 +190,13 @@ struct RecOut {
 };
 
 struct RecWork {
-    uint32_t* sync;            // [0] ticket, [1] error word, then (16 B aligned) status
+    uint32_t* sync;            // header (SYNC_*), then status at SYNC_HEADER_BYTES
     unsigned long long* status;   // [nwg*3] look-back granules: state<<32 | count
     uint32_t* hscratch;        // [M+N] window hashes of topologies larger than CAP
     uint8_t* fscratch;         // [M+N] record flags when a workgroup exceeds CAP
     uint32_t* otarget;         // [M]   first matching desired index (slow path)
     unsigned long long* trace; // [nwg][TRACE_WORDS] (VAR_TRACE only)
-    const uint32_t* first_partial;   // k_full_prefix: first chunk not known to emit all records
+    const uint32_t* first_partial_inv;   // k_full_prefix: ~(first chunk not known to emit all records)
     uint32_t* wcount;          // [nwg*3] list counts per workgroup (VAR_DIFF: k_place_scan input)
     uint32_t m_cap, n_cap;     // VAR_DIFF: deferred chunks emit at m_cap + o0 / n_cap + n0
     uint32_t nwg;
@@ -200,7 +206,7 @@ struct RecWork {
 // VAR_DIFF placement (after k_reconcile): exclusive bases per workgroup and list totals, then
 // the deferred chunks' entries moved from the upper halves of the output arrays.
 __global__ void k_place_scan(const uint32_t* wcount, uint32_t nwg, uint32_t* wbase, RecOut out, uint32_t T);
-__global__ void k_place(DevTopos T, const uint32_t* wcount, const uint32_t* wbase, const uint32_t* first_partial,
+__global__ void k_place(DevTopos T, const uint32_t* wcount, const uint32_t* wbase, const uint32_t* first_partial_inv,
                         RecOut out, uint32_t m_cap, uint32_t n_cap, uint32_t nwg);
 constexpr int PLACE_SCAN_BLOCK = 1024, PLACE_PER = 8;    // k_place_scan: workgroups per thread per tile
 
@@ -326,7 +332,7 @@ __global__ void k_scan_final(const uint32_t* size, uint32_t n, const uint64_t* p
 __global__ void k_wire_write(WireIn w, DevLinks O, DevLinks N, WireWork wk, uint8_t* arena);
 __global__ void k_qdisc_batch(DevLinks props, DevTables tb, uint2* out);
 constexpr int FP_BLOCK = 1024, FP_GRID = 256;       // k_full_prefix launch shape
-__global__ void k_full_prefix(DevTopos T, uint32_t* first_partial);
+__global__ void k_full_prefix(DevTopos T, uint32_t* first_partial_inv);
 
 // ---- CR ingest: TopologyList JSON → epoch tables (kdtn_ingest.hip) ------------------------
 // token word: {byte offset, pre-depth | kind << 24}

@@ -1116,7 +1116,7 @@ __device__ void lookback(RecShared& s, const RecWork& wk, uint32_t wg) {
                 }
                 if (!ready) {
                     if (++spins > (1u << 24)) {              // bounded spin: report, never hang
-                        if (lane == 0) atomicOr(&wk.sync[1], 1u);
+                        if (lane == 0) atomicOr(&wk.sync[SYNC_ERR], 1u);
                         break;
                     }
                     __builtin_amdgcn_s_sleep(2);
@@ -1161,7 +1161,8 @@ KD_INLINE bool topo_partial(uint8_t tf, uint32_t ko, uint32_t kn) {
 // Four topologies per thread (16-B offset loads), grid-stride over FP_GRID blocks, one
 // global atomicMin per block: an epoch of partial topologies (config 3) sent every wave's
 // atomic to one address (133 µs).
-__global__ void __launch_bounds__(FP_BLOCK) k_full_prefix(DevTopos T, uint32_t* first_partial) {
+// The result is stored inverted (atomicMax of ~chunk) so the zeroed sync header means "none".
+__global__ void __launch_bounds__(FP_BLOCK) k_full_prefix(DevTopos T, uint32_t* first_partial_inv) {
     __shared__ uint32_t bmin;
     if (threadIdx.x == 0) bmin = 0xFFFFFFFFu;
     __syncthreads();
@@ -1190,7 +1191,7 @@ __global__ void __launch_bounds__(FP_BLOCK) k_full_prefix(DevTopos T, uint32_t* 
             atomicMin(&bmin, first / TPW);              // lanes hold increasing topologies
         if (__syncthreads_or(m != 0)) break;         // later iterations only hold later chunks
     }
-    if (threadIdx.x == 0 && bmin != 0xFFFFFFFFu) atomicMin(first_partial, bmin);
+    if (threadIdx.x == 0 && bmin != 0xFFFFFFFFu) atomicMax(first_partial_inv, ~bmin);
 }
 
 // (VAR_TRACE) phase timestamp of this workgroup: 100 MHz chip-wide clock
@@ -1208,7 +1209,7 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
     const int tid = threadIdx.x;
     unsigned long long t_entry = 0;
     if constexpr ((V & VAR_TRACE) != 0) t_entry = __builtin_amdgcn_s_memrealtime();
-    if (tid == 0) s.ticket = atomicAdd(&wk.sync[0], 1u);   // dispatch order → look-back order
+    if (tid == 0) s.ticket = atomicAdd(&wk.sync[SYNC_TICKET], 1u);   // dispatch order → look-back order
     __syncthreads();
     // wk.split workgroups per chunk: part 0 does the chunk's work; in a bulk chunk of the full
     // prefix (bases known without predecessors) the parts share its records, so a small epoch
@@ -1254,7 +1255,7 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
     // bulk: no topology of this workgroup has both lists non-empty (new pods: status empty;
     // deleted pods: spec nil) → every record of a DIFF topology is an entry, in order
     const bool bulk = s.any_cmp == 0;
-    const bool prefix = (V & VAR_NO_PREFIX) == 0 && wg <= *wk.first_partial;
+    const bool prefix = (V & VAR_NO_PREFIX) == 0 && wg <= ~*wk.first_partial_inv;
     const bool shared = bulk && prefix;                  // the parts split the records
     if (part != 0 && !shared) return;                    // (block-uniform)
     const bool lead = part == 0;
@@ -1642,11 +1643,11 @@ __global__ void __launch_bounds__(PLACE_SCAN_BLOCK) k_place_scan(const uint32_t*
 // One wave per deferred chunk: per-topology offsets += the chunk's bases, entries moved
 // from [cap + record offset, +count) to [base, +count) of the same arrays (never overlapping).
 __global__ void __launch_bounds__(BLOCK) k_place(DevTopos T, const uint32_t* wcount, const uint32_t* wbase,
-                                                 const uint32_t* first_partial, RecOut out, uint32_t m_cap,
+                                                 const uint32_t* first_partial_inv, RecOut out, uint32_t m_cap,
                                                  uint32_t n_cap, uint32_t nwg) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wg = blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
-    if (wg >= nwg || wg <= *first_partial) return;          // prefix chunks wrote final positions
+    if (wg >= nwg || wg <= ~*first_partial_inv) return;          // prefix chunks wrote final positions
     const uint32_t t0 = wg * TPW, nt = min((uint32_t)TPW, T.n - t0);
     const uint32_t cd = wcount[(size_t)wg * 3], cu = wcount[(size_t)wg * 3 + 1], ca = wcount[(size_t)wg * 3 + 2];
     const uint32_t bd = wbase[(size_t)wg * 3], bu = wbase[(size_t)wg * 3 + 1], ba = wbase[(size_t)wg * 3 + 2];

@@ -73,6 +73,7 @@ def lib() -> C.CDLL:
         "kdtn_make_qdiscs": (C.c_int, [vp, C.POINTER(abi.Strtab), C.POINTER(abi.PropsTable), vp]),
         "kdtn_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8 * 128)]),
         "kdtn_comm_init": (C.c_int, [vp, C.POINTER(C.c_uint8 * 128), C.c_int, C.c_int]),
+        "kdtn_set_timing": (C.c_int, [vp, C.c_int]),
         "kdtn_last_kernel_times": (C.c_int, [vp, C.POINTER(C.c_char_p), C.POINTER(C.c_float), C.c_int]),
         "kdtn_debug_wg_trace": (C.c_int, [vp, C.POINTER(C.c_uint64), C.c_uint32]),
         "kdtn_epoch_encode": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
@@ -355,6 +356,10 @@ class Engine:
         f.node_cap, f.idx_cap = node.size, idx.size
         _check(lib().kdtn_epoch_fanout(self._ctx, C.byref(f)), "kdtn_epoch_fanout")
         return node[:f.n_nodes], off, idx[:f.n_send]
+
+    def set_timing(self, level: int) -> None:
+        """HIP-event timing of kdtn_epoch_run: 0 none, 1 k_reconcile (+ placement), 2 every stage."""
+        _check(lib().kdtn_set_timing(self._ctx, level), "kdtn_set_timing")
 
     def kernel_times(self) -> dict[str, float]:
         names = (C.c_char_p * 32)()

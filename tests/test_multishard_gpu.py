@@ -95,3 +95,23 @@ def test_engine_shards_equal_unsharded_oracle(config, world):
     want_fan = _fan_rows(full, ref, wn, wo, wi, np.arange(full.topos.n))
     key = lambda a: a[np.lexsort(a.T[::-1])]
     assert np.array_equal(key(fan), key(want_fan))
+
+
+def test_rccl_one_rank_communicator_equals_local_epoch():
+    """The production transport on one GPU: kdtn_comm_init with a one-rank RCCL communicator
+    makes kdtn_epoch_run all-gather the pod-status rows with ncclAllGather on the comm
+    stream (in place, slice = every pod). The epoch equals the oracle's bit for bit."""
+    import oracle as O
+    from kdtn import Engine, comm_unique_id, synth
+    inp = synth.make(4, total_pods=5000)
+    want = O.reconcile(inp, tick=15.625)
+    with Engine(device=0, tick_in_usec=15.625) as eng:
+        eng.comm_init(comm_unique_id(), 1, 0)
+        eng.upload(inp)
+        for _ in range(2):                       # the second epoch reuses the communicator
+            eng.run()
+            eng.sync()
+            got = eng.download()
+            assert "pods_allgather" in eng.kernel_times()
+            bad = got.mismatches(want)
+            assert not bad, f"RCCL one-rank epoch differs from the oracle in {bad}"
