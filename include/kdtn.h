@@ -158,6 +158,11 @@ typedef struct kdtn_vni_table {
     const uint32_t* net_ns;
 } kdtn_vni_table;
 
+/* kdtn_epoch_in.vnis.n = KDTN_VNI_RESIDENT: use the context's resident map (the last uploaded
+ * snapshot, or the state kdtn_epoch_vni_apply left) instead of uploading one; its ids must
+ * still name the same strings (append-only kdict). */
+#define KDTN_VNI_RESIDENT 0xFFFFFFFFu
+
 typedef struct kdtn_epoch_in {
     kdtn_strtab     kdict;      /* key strings: names, namespaces, intfs, IPs, MACs, src_ip, net_ns */
     kdtn_strtab     pdict;      /* LinkProperties strings                               */
@@ -510,6 +515,32 @@ int kdtn_comm_init(kdtn_ctx* ctx, const uint8_t unique_id[128], int nranks, int 
 int kdtn_comm_set_ranks(kdtn_ctx* ctx, int nranks, int rank);          /* host transport */
 int kdtn_pods_export(kdtn_ctx* ctx, kdtn_pod_row* rows);                /* [pod_slice] rows */
 int kdtn_pods_import(kdtn_ctx* ctx, const kdtn_pod_row* rows, uint64_t n);   /* n = pod_slice*nranks */
+
+/* ---- VxlanManager state after the epoch ---------------------------------------------
+ * Replaces the daemons' map mutations (daemon/vxlan/manager.go:57-63 Add / Delete, called at
+ * daemon/kubedtn/handler.go:192 remote/physical Update, :440 cross-node addLink, :484-487
+ * delLink) for the entries the daemons reach (as kdtn_epoch_fanout defines them): a delete
+ * for each reached DelLinks entry whose vni_hit is set (before its first MakeVeth error);
+ * for each reached AddLinks entry without error, Store(vni, local netns) on the local node
+ * (cross-node and physical peers) and, for cross-node ones whose remote Update succeeds
+ * (remote_err == 0), Store(vni, peer netns) on the peer's node. The reference applies them
+ * in goroutine order; here every delete comes first, then the adds, and the first add of a
+ * key (node, vni) in (topology, add-list, local-before-remote) order wins. The result
+ * becomes the context's resident map (KDTN_VNI_RESIDENT) and, with out->node / vni / net_ns
+ * (capacity out->cap entries; NULL = count only), is downloaded: entries of the epoch's adds
+ * first, then the surviving snapshot entries, keys unique. Needs a single-shard run with
+ * the resolve and qdisc stages; KDTN_ENOSPC when cap < n (the map is applied anyway). */
+typedef struct kdtn_vni_state {
+    uint64_t  cap;
+    uint32_t  n;                /* out: entries of the map after the epoch */
+    uint32_t* node;
+    int32_t*  vni;
+    uint32_t* net_ns;
+} kdtn_vni_state;
+int kdtn_epoch_vni_apply(kdtn_ctx* ctx, kdtn_vni_state* out);
+/* The resident map (the last uploaded snapshot or applied state): out->n, and the arrays
+ * when given (KDTN_ENOSPC when out->cap < n). */
+int kdtn_vni_download(kdtn_ctx* ctx, kdtn_vni_state* out);
 
 /* ---- profiling hooks: per-kernel HIP-event times of the last epoch_run (ms) -------- */
 /* Timing level of kdtn_epoch_run's HIP events (each costs ≈5 µs of stream time): 0 none,

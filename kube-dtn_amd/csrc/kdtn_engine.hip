@@ -83,6 +83,10 @@ struct kdtn_ctx {
     // vni table
     DevBuf v_node, v_vni, v_netns, v_ents, v_slots, v_table;
     uint32_t V = 0, vni_mask = 0;
+    // kdtn_epoch_vni_apply: ops, snapshot marks, the new map's table, arrays and scan partials
+    DevBuf vx_ops, vx_dead, vx_slots, vx_node, vx_vni, vx_netns, vx_part;
+    bool vres_ok = false;          // v_node/v_vni/v_netns hold a map usable as KDTN_VNI_RESIDENT
+    uint32_t vres_n = 0, vres_D = 0;
     // pods
     DevBuf pods, pod_ovf, pod_direct;
     uint32_t slice = 0, pod_total = 0, ovf_mask = 0, kb_words = 0, pod_stamp = 0;
@@ -331,6 +335,23 @@ DevTopos topo_view(kdtn_ctx* c) {
     return t;
 }
 
+// Parse the property strings [p0, n): one thread per (string, interpretation) when split
+// (three launches' worth of waves in one grid), else one thread per string.
+void launch_pdict(kdtn_ctx* c, uint32_t p0, uint32_t n) {
+    bool split = KDTN_PD_SPLIT_DEFAULT;
+#if KDTN_PROFILING
+    if (const char* ev = std::getenv("KDTN_PD_SPLIT")) split = std::atoi(ev) != 0;
+#endif
+    const dim3 grid(nblocks(n - p0), split ? 3 : 1);
+    auto go = [&](auto kern) {
+        kern<<<grid, BLOCK, 0, c->stream>>>(dp<uint8_t>(c->pd_bytes), dp<uint32_t>(c->pd_offs), p0, n,
+                                            c->cfg.tick_in_usec, dp<uint32_t>(c->pd_pct), dp<uint2>(c->pd_dur),
+                                            dp<uint2>(c->pd_rate), dp<uint32_t>(c->pd_rerr));
+    };
+    if (split) go(k_pdict_parse<true>);
+    else go(k_pdict_parse<false>);
+}
+
 // Special key-string ids (SPECIAL_DEFAULT / SPECIAL_LOCALHOST) at or past the parse start
 // are forgotten when an upload sets it; every run's k_kdict_flags re-finds them there.
 void clip_specials(kdtn_ctx* c) {
@@ -368,15 +389,35 @@ int prepare_dicts(kdtn_ctx* c) {
     return KDTN_OK;
 }
 
+// VxlanManager snapshot ids valid for a dictionary of D strings; KDTN_VNI_RESIDENT needs a
+// resident map whose ids all exist (the dictionary only grew since it was made)
+int check_vnis(kdtn_ctx* c, const kdtn_vni_table& vn, uint32_t D) {
+    if (vn.n == KDTN_VNI_RESIDENT) {
+        if (!c->vres_ok || D < c->vres_D) {
+            std::snprintf(g_last_error, sizeof(g_last_error), "KDTN_VNI_RESIDENT: no resident VXLAN map for this dictionary");
+            return KDTN_EINVAL;
+        }
+        return KDTN_OK;
+    }
+    TRY(check_ids(vn.node, vn.n, D, "vnis.node"));
+    return check_ids(vn.net_ns, vn.n, D, "vnis.net_ns");
+}
+
 // everything an epoch needs besides its input tables: VNI snapshot, pod tables, work and
 // output buffers (c->D, c->T set; shared by kdtn_epoch_upload and kdtn_json_ingest)
 int prepare_epoch(kdtn_ctx* c, const kdtn_vni_table& vn, uint32_t slice, uint32_t M, uint32_t N) {
     const uint32_t D = c->D;
-    const uint32_t V = vn.n;
+    const bool resident = vn.n == KDTN_VNI_RESIDENT;
+    const uint32_t V = resident ? c->vres_n : vn.n;
     c->V = V;
-    TRY(upload(c, c->v_node, vn.node, (size_t)V * 4));
-    TRY(upload(c, c->v_vni, vn.vni, (size_t)V * 4));
-    TRY(upload(c, c->v_netns, vn.net_ns, (size_t)V * 4));
+    if (!resident) {
+        TRY(upload(c, c->v_node, vn.node, (size_t)V * 4));
+        TRY(upload(c, c->v_vni, vn.vni, (size_t)V * 4));
+        TRY(upload(c, c->v_netns, vn.net_ns, (size_t)V * 4));
+        c->vres_ok = true;                      // the uploaded map stays resident
+        c->vres_n = V;
+        c->vres_D = D;
+    }
     c->vni_mask = V ? next_pow2((uint64_t)V * 2) - 1 : 0;
     TRY(ensure(c->v_ents, (size_t)V * 16));
     TRY(ensure(c->v_slots, (size_t)(c->vni_mask + 1) * 4));
@@ -587,8 +628,7 @@ int kdtn_epoch_upload(kdtn_ctx* c, const kdtn_epoch_in* in) {
             return KDTN_EINVAL;
         }
     }
-    TRY(check_ids(in->vnis.node, in->vnis.n, D, "vnis.node"));
-    TRY(check_ids(in->vnis.net_ns, in->vnis.n, D, "vnis.net_ns"));
+    TRY(check_vnis(c, in->vnis, D));
     const uint32_t slice = in->pod_slice ? in->pod_slice : T.n;
     if (slice < T.n) return KDTN_EINVAL;
 
@@ -702,11 +742,7 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
     timer_mark(c, "kdict_parse", 2);
     {
         const uint32_t p0 = c->pd_from & ~63u;
-        if (c->P > p0)
-            k_pdict_parse<<<nblocks(c->P - p0), BLOCK, 0, s>>>(dp<uint8_t>(c->pd_bytes), dp<uint32_t>(c->pd_offs), p0,
-                                                               c->P, c->cfg.tick_in_usec, dp<uint32_t>(c->pd_pct),
-                                                               dp<uint2>(c->pd_dur), dp<uint2>(c->pd_rate),
-                                                               dp<uint32_t>(c->pd_rerr));
+        if (c->P > p0) launch_pdict(c, p0, c->P);
     }
     c->kd_valid = c->D;
     c->pd_valid = c->P;
@@ -787,8 +823,15 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         uint32_t* wbase = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(w.wcount) + align_up((size_t)c->nwg * 12, 16));
         bool placed = false;                                        // VAR_DIFF: k_place_scan + k_place
         // several workgroups per chunk when the chunks would not fill the chip about four times
-        // over (4 resident k_reconcile workgroups per CU): they share a bulk chunk's records
-        w.split = std::max<uint32_t>(1, std::min<uint32_t>(4, (4 * 4 * c->n_cus + c->nwg - 1) / c->nwg));
+        // over (4 resident k_reconcile workgroups per CU): they share a bulk chunk's records,
+        // at least ~320 records per part (measured: 125k-pod config 2, 640 records per chunk:
+        // split 2 0.097 ms, 3 0.106, 4 0.115; 12.5k-site config 4, 1266 per chunk: 4 best)
+        const uint64_t per_chunk = ((uint64_t)c->real.n + c->des.n) / std::max<uint32_t>(c->nwg, 1);
+        w.split = std::max<uint32_t>(1, std::min<uint32_t>({4u, (4 * 4 * c->n_cus + c->nwg - 1) / c->nwg,
+                                                            (uint32_t)std::max<uint64_t>(1, per_chunk / 320)}));
+#if KDTN_PROFILING
+        if (const char* ev = std::getenv("KDTN_SPLIT")) if (std::atoi(ev) > 0) w.split = (uint32_t)std::atoi(ev);
+#endif
         k_full_prefix<<<(unsigned)std::min<uint64_t>(FP_GRID, (c->T + 4 * FP_BLOCK - 1) / (4 * FP_BLOCK)), FP_BLOCK, 0, s>>>(
             T, sync + SYNC_FIRST_PARTIAL_INV);
         timer_mark(c, "full_prefix", 2);
@@ -998,9 +1041,7 @@ int kdtn_make_qdiscs(kdtn_ctx* c, const kdtn_strtab* pdict, const kdtn_props_tab
     TRY(upload_links(c, c->des, L, 1, P, "props"));
     TRY(ensure(c->add_qdisc, (size_t)std::max<uint32_t>(n, 1) * 72));
     hipStream_t s = c->stream;
-    k_pdict_parse<<<nblocks(P), BLOCK, 0, s>>>(dp<uint8_t>(c->pd_bytes), dp<uint32_t>(c->pd_offs), 0u, P,
-                                               c->cfg.tick_in_usec, dp<uint32_t>(c->pd_pct),
-                                               dp<uint2>(c->pd_dur), dp<uint2>(c->pd_rate), dp<uint32_t>(c->pd_rerr));
+    if (P) launch_pdict(c, 0u, P);
     DevTables tb{};
     tb.ppct = dp<uint32_t>(c->pd_pct);
     tb.pdur = dp<uint2>(c->pd_dur);
@@ -1590,8 +1631,7 @@ static int json_ingest_full(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest
     TRY(prepare_dicts(c));
     const kdtn_vni_table none{0, nullptr, nullptr, nullptr};
     const kdtn_vni_table& vn = vnis ? *vnis : none;
-    TRY(check_ids(vn.node, vn.n, c->D, "vnis.node"));
-    TRY(check_ids(vn.net_ns, vn.n, c->D, "vnis.net_ns"));
+    TRY(check_vnis(c, vn, c->D));
     TRY(prepare_epoch(c, vn, T, M, N));
     HIP_TRY(hipStreamSynchronize(s));
     c->j_info.n_topos = T;
@@ -1853,6 +1893,90 @@ int kdtn_debug_wg_trace(kdtn_ctx* c, uint64_t* out, uint32_t cap) {
     const uint32_t n = std::min<uint64_t>(cap, (uint64_t)c->nwg * TRACE_WORDS);
     HIP_TRY(hipMemcpy(out, c->trace.p, (size_t)n * 8, hipMemcpyDeviceToHost));
     return (int)n;
+}
+
+int kdtn_epoch_vni_apply(kdtn_ctx* c, kdtn_vni_state* out) {
+    if (!c || !c->ran) return KDTN_EINVAL;
+    const uint32_t need = KDTN_STAGE_RESOLVE | KDTN_STAGE_QDISC;
+    if ((c->last_stages & need) != need || c->nranks != 1) {
+        std::snprintf(g_last_error, sizeof(g_last_error),
+                      "kdtn_epoch_vni_apply: needs a single-shard epoch run with resolve and qdisc stages");
+        return KDTN_EINVAL;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    HIP_TRY(hipStreamSynchronize(s));                 // counts of the run (h_misc)
+    const uint32_t nd = c->h_misc[1], na = c->h_misc[3], V = c->V;
+    const uint64_t n_ops = 2ull * na, n_ext = n_ops + V;
+    if (n_ext >= 0x7FFFFFFFull) return KDTN_EINVAL;
+    c->n_ev = 0;
+    (void)hipEventRecord(c->ev[0], s);
+    TRY(ensure(c->vx_ops, ((size_t)nd + n_ops) * 16));
+    TRY(ensure(c->vx_dead, (size_t)V + 16));
+    uint4* ops = dp<uint4>(c->vx_ops);
+    VniOpsIn f{ReachIn{dp<uint32_t>(c->del_off), dp<uint4>(c->del_res), dp<uint32_t>(c->add_off), dp<uint4>(c->add_res),
+                       dp<uint2>(c->add_qdisc), dp<uint32_t>(c->upd_off), dp<uint4>(c->upd_res), c->T, 0u},
+               dp<uint32_t>(c->t_src), dp<uint32_t>(c->t_netns), dp<uint4>(c->pods), nd, na};
+    if (c->T) k_vni_ops<<<nblocks(c->T), BLOCK, 0, s>>>(f, ops);
+    const uint4* ents = dp<uint4>(c->v_ents);
+    uint8_t* dead = dp<uint8_t>(c->vx_dead);
+    if (V) {                                          // the run built the snapshot table
+        k_vni_shadow<<<nblocks(V), BLOCK, 0, s>>>(ents, V, dp<uint32_t>(c->v_slots), c->vni_mask, dead);
+        if (nd) k_vni_del<<<nblocks(nd), BLOCK, 0, s>>>(ops, nd, ents, dp<uint32_t>(c->v_slots), c->vni_mask, dead);
+    }
+    timer_mark(c, "vni_ops");
+    const uint32_t mask = next_pow2(n_ext * 2) - 1;
+    TRY(ensure(c->vx_slots, ((size_t)mask + 1) * 4));
+    HIP_TRY(hipMemsetAsync(c->vx_slots.p, 0xFF, ((size_t)mask + 1) * 4, s));
+    uint32_t* slots = dp<uint32_t>(c->vx_slots);
+    const uint4* aops = ops + nd;
+    const uint32_t nb = nblocks(n_ext, SCAN_CHUNK);
+    TRY(ensure(c->vx_part, (size_t)nb * 8 + 8));
+    TRY(ensure(c->vx_node, (size_t)n_ext * 4));
+    TRY(ensure(c->vx_vni, (size_t)n_ext * 4));
+    TRY(ensure(c->vx_netns, (size_t)n_ext * 4));
+    uint32_t* n_out = dp<uint32_t>(c->misc) + MISC_VNI_N;
+    HIP_TRY(hipMemsetAsync(n_out, 0, 4, s));
+    if (n_ext) {
+        k_vni_insert<<<nblocks(n_ext), BLOCK, 0, s>>>(aops, (uint32_t)n_ops, ents, dead, V, slots, mask);
+        k_vni_vis_count<<<nb, BLOCK, 0, s>>>(aops, (uint32_t)n_ops, ents, dead, V, slots, mask, dp<uint64_t>(c->vx_part));
+        k_scan_top<<<1, BLOCK, 0, s>>>(dp<uint64_t>(c->vx_part), nb);
+        k_vni_vis_write<<<nb, BLOCK, 0, s>>>(aops, (uint32_t)n_ops, ents, dead, V, slots, mask, dp<uint64_t>(c->vx_part),
+                                            dp<uint32_t>(c->vx_node), dp<int32_t>(c->vx_vni), dp<uint32_t>(c->vx_netns),
+                                            n_out);
+    }
+    HIP_TRY(hipGetLastError());
+    timer_mark(c, "vni_map");
+    HIP_TRY(hipMemcpyAsync(c->h_misc + 5, n_out, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const uint32_t n = c->h_misc[5];
+    // the new map becomes the resident one (the next upload's KDTN_VNI_RESIDENT)
+    std::swap(c->v_node, c->vx_node);
+    std::swap(c->v_vni, c->vx_vni);
+    std::swap(c->v_netns, c->vx_netns);
+    c->vres_ok = true;
+    c->vres_n = n;
+    c->vres_D = c->D;
+    return out ? kdtn_vni_download(c, out) : KDTN_OK;
+}
+
+int kdtn_vni_download(kdtn_ctx* c, kdtn_vni_state* out) {
+    if (!c || !out) return KDTN_EINVAL;
+    if (!c->vres_ok) {
+        out->n = 0;
+        return KDTN_OK;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    const uint32_t n = c->vres_n;
+    out->n = n;
+    if (!out->node && !out->vni && !out->net_ns) return KDTN_OK;
+    if (n > out->cap) return KDTN_ENOSPC;
+    hipStream_t s = c->stream;
+    if (n && out->node) HIP_TRY(hipMemcpyAsync(out->node, c->v_node.p, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    if (n && out->vni) HIP_TRY(hipMemcpyAsync(out->vni, c->v_vni.p, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    if (n && out->net_ns) HIP_TRY(hipMemcpyAsync(out->net_ns, c->v_netns.p, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return KDTN_OK;
 }
 
 int kdtn_set_timing(kdtn_ctx* c, int level) {

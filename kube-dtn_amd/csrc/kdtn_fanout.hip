@@ -17,18 +17,6 @@
 
 namespace kdtn {
 
-KD_INLINE bool sends_remote(uint4 r, uint32_t qerr) {
-    return (r.w & 0xFFu) == KDTN_KIND_CROSS_NODE && ((r.w >> 8) & 0xFFu) == 0 && qerr == 0;
-}
-// a link whose step fails before its RPC aborts its batch (addLink's error chain; qdisc only
-// where built)
-KD_INLINE bool add_fails(uint4 r, uint32_t qerr) {
-    const uint32_t kind = r.w & 0xFFu;
-    if ((r.w >> 8) & 0xFFu) return true;
-    return (kind == KDTN_KIND_SAME_NODE || kind == KDTN_KIND_CROSS_NODE || kind == KDTN_KIND_PHYSICAL) && qerr != 0;
-}
-KD_INLINE uint32_t qdisc_err(const uint2* q, uint32_t e) { return (q[(size_t)e * 9 + 8].y >> 16) & 0xFFu; }
-
 // Which entries the daemons reach (include/kdtn.h): one thread per topology walks its
 // DelLinks, AddLinks, UpdateLinks entries in RPC order (topology_controller.go:93-116) and
 // stops at the first failing link (handler.go:601-607, 622-628, 644-662). Writes per add

@@ -48,7 +48,7 @@ enum : int {
     KB_NSETS = 3,
 };
 // special key-string ids found by k_kdict_flags (0xFFFFFFFF when absent)
-enum : int { SPECIAL_DEFAULT = 0, SPECIAL_LOCALHOST = 4, MISC_FAN_NODES = 12 };   // misc words
+enum : int { SPECIAL_DEFAULT = 0, SPECIAL_LOCALHOST = 4, MISC_FAN_NODES = 12, MISC_VNI_N = 13 };   // misc words
 // epoch sync header (u32 words; zeroed by the epoch's only memset, the look-back status
 // follows at SYNC_HEADER_BYTES). The ticket counter, which every k_reconcile workgroup
 // increments, has a 128-B line to itself; the host reads words [SYNC_TOTALS, SYNC_TOTALS + 4)
@@ -111,6 +111,10 @@ struct DevLinks {
 // the parity-tested paths, and reads no environment variable.
 #ifndef KDTN_PROFILING
 #define KDTN_PROFILING 0
+#endif
+// k_pdict_parse: one thread per (string, interpretation) instead of one per string
+#ifndef KDTN_PD_SPLIT_DEFAULT
+#define KDTN_PD_SPLIT_DEFAULT true    // 125k-pod config 2: 0.0374 -> 0.0341 ms; 1M: equal
 #endif
 // Emission variants (A/B in the profiling build; the product runs DEFAULT_VARIANT):
 //   bit 0: non-temporal streaming loads of link columns
@@ -214,6 +218,7 @@ __global__ void k_special_clip(uint32_t* special, uint32_t k0);
 template <int SUB>
 __global__ void k_kdict_flags(const uint8_t* bytes, const uint32_t* offs, uint32_t first, uint32_t n,
                               uint32_t* kbits, uint32_t kb_words, uint32_t* special);
+template <bool SPLIT>
 __global__ void k_pdict_parse(const uint8_t* bytes, const uint32_t* offs, uint32_t first, uint32_t n, double tick,
                               uint32_t* ppct, uint2* pdur, uint2* prate, uint32_t* rate_err);
 __global__ void k_pods_fill(DevTopos T, uint32_t slice, uint32_t rank_base, uint4* pods);
@@ -282,7 +287,32 @@ struct FanIn {
     const uint2* add_qdisc;
     uint32_t T, n_add, stamp;
 };
+// murmur3 finalizer (hash tables keyed by packed ids)
+KD_INLINE uint64_t hash64(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xFF51AFD7ED558CCDull;
+    x ^= x >> 33;
+    x *= 0xC4CEB9FE1A85EC53ull;
+    x ^= x >> 33;
+    return x;
+}
+// home slot of a VxlanManager key (node, vni)
+KD_INLINE uint32_t vni_home(uint32_t node, uint32_t vni, uint32_t mask) {
+    return (uint32_t)hash64(((uint64_t)node << 32) | vni) & mask;
+}
+
 // which entries the daemons reach (kdtn_fanout.hip k_reach; include/kdtn.h)
+KD_INLINE bool sends_remote(uint4 r, uint32_t qerr) {
+    return (r.w & 0xFFu) == KDTN_KIND_CROSS_NODE && ((r.w >> 8) & 0xFFu) == 0 && qerr == 0;
+}
+// a link whose step fails before its RPC aborts its batch (addLink's error chain; qdisc only
+// where built)
+KD_INLINE bool add_fails(uint4 r, uint32_t qerr) {
+    const uint32_t kind = r.w & 0xFFu;
+    if ((r.w >> 8) & 0xFFu) return true;
+    return (kind == KDTN_KIND_SAME_NODE || kind == KDTN_KIND_CROSS_NODE || kind == KDTN_KIND_PHYSICAL) && qerr != 0;
+}
+KD_INLINE uint32_t qdisc_err(const uint2* q, uint32_t e) { return (q[(size_t)e * 9 + 8].y >> 16) & 0xFFu; }
 enum : uint8_t { REACH_ON = 1, REACH_SEND = 2 };
 struct ReachIn {
     const uint32_t* del_off;
@@ -295,6 +325,29 @@ struct ReachIn {
     uint32_t T, stamp;
 };
 __global__ void k_reach(ReachIn f, uint32_t* mark, uint8_t* reach_add, uint8_t* reach_upd);
+
+// VxlanManager state after the epoch (kdtn_vni.hip; include/kdtn.h kdtn_epoch_vni_apply)
+struct VniOpsIn {
+    ReachIn r;                      // the epoch's batches (r.stamp unused)
+    const uint32_t* t_src;          // topology status.src_ip / status.net_ns (kdict ids)
+    const uint32_t* t_netns;
+    const uint4* pods;              // global pod-status rows (peer netns of a remote Update)
+    uint32_t n_del, n_add;
+};
+// one op per del entry (slot e) and two per add entry (slots n_del + 2e, + 1):
+// {node, vni, net_ns, kind} with kind VOP_NONE / VOP_DEL / VOP_ADD
+enum : uint32_t { VOP_NONE = 0, VOP_DEL = 1, VOP_ADD = 2 };
+__global__ void k_vni_ops(VniOpsIn f, uint4* ops);
+__global__ void k_vni_shadow(const uint4* ents, uint32_t n_ents, const uint32_t* slots, uint32_t mask, uint8_t* dead);
+__global__ void k_vni_del(const uint4* ops, uint32_t n_del, const uint4* ents, const uint32_t* slots, uint32_t mask,
+                          uint8_t* dead);
+__global__ void k_vni_insert(const uint4* add_ops, uint32_t n_ops, const uint4* ents, const uint8_t* dead, uint32_t n_ents,
+                             uint32_t* slots, uint32_t mask);
+__global__ void k_vni_vis_count(const uint4* add_ops, uint32_t n_ops, const uint4* ents, const uint8_t* dead,
+                                uint32_t n_ents, const uint32_t* slots, uint32_t mask, uint64_t* part);
+__global__ void k_vni_vis_write(const uint4* add_ops, uint32_t n_ops, const uint4* ents, const uint8_t* dead,
+                                uint32_t n_ents, const uint32_t* slots, uint32_t mask, const uint64_t* part,
+                                uint32_t* node, int32_t* vni, uint32_t* net_ns, uint32_t* n_out);
 __global__ void k_fan_nodes_count(const uint32_t* mark, uint32_t nd, uint32_t stamp, uint64_t* part);
 __global__ void k_fan_nodes_write(const uint32_t* mark, uint32_t nd, uint32_t stamp, const uint64_t* part,
                                   uint32_t* node_idx, uint32_t* nodes, uint32_t* n_nodes);

@@ -19,14 +19,6 @@ KD_INLINE uint32_t fin32(uint32_t h) {
     h ^= h >> 16;
     return h;
 }
-KD_INLINE uint64_t hash64(uint64_t x) {
-    x ^= x >> 33;
-    x *= 0xFF51AFD7ED558CCDull;
-    x ^= x >> 33;
-    x *= 0xC4CEB9FE1A85EC53ull;
-    x ^= x >> 33;
-    return x;
-}
 
 // EqualWithoutProperties key (7 string ids + uid as two words) and the DeepEqual'd
 // properties (12 ids + Gap) of one record, loaded with independent loads (no short-circuit
@@ -281,25 +273,34 @@ template __global__ void k_kdict_flags<2>(const uint8_t*, const uint32_t*, uint3
 template __global__ void k_kdict_flags<4>(const uint8_t*, const uint32_t*, uint32_t, uint32_t, uint32_t*, uint32_t, uint32_t*);
 #endif
 
+// One property string's interpretations: WHICH = 7 all three, else one of PD_DUR / PD_PCT /
+// PD_RATE (the split launch gives each interpretation its own threads: more waves in flight
+// for a latency-bound parse, and each parse path alone needs fewer registers).
+enum : int { PD_DUR = 1, PD_PCT = 2, PD_RATE = 4 };
+template <int WHICH>
 KD_INLINE void pdict_parse_one(const uint8_t* s, uint32_t len, double tick, uint32_t* pct_out,
                                uint2* dur_out, uint2* rate_out, bool* rate_bad) {
-    uint32_t dur = 0;
-    const bool dok = parse_duration_us(s, len, &dur);
-    *dur_out = dok ? make_uint2(dur, time2tick(dur, tick)) : make_uint2(0u, 1u);   // DUR_ERR
-    float pct;
-    *pct_out = parse_pct(s, len, &pct) ? p2u(pct) : PCT_ERR;
-    uint64_t r = 0;
-    const bool rok = parse_rate(s, len, &r);
-    *rate_out = rok ? make_uint2((uint32_t)r, (uint32_t)(r >> 32)) : make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
-    *rate_bad = !rok;
+    if constexpr ((WHICH & PD_DUR) != 0) {
+        uint32_t dur = 0;
+        const bool dok = parse_duration_us(s, len, &dur);
+        *dur_out = dok ? make_uint2(dur, time2tick(dur, tick)) : make_uint2(0u, 1u);   // DUR_ERR
+    }
+    if constexpr ((WHICH & PD_PCT) != 0) {
+        float pct;
+        *pct_out = parse_pct(s, len, &pct) ? p2u(pct) : PCT_ERR;
+    }
+    if constexpr ((WHICH & PD_RATE) != 0) {
+        uint64_t r = 0;
+        const bool rok = parse_rate(s, len, &r);
+        *rate_out = rok ? make_uint2((uint32_t)r, (uint32_t)(r >> 32)) : make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+        *rate_bad = !rok;
+    }
 }
 
-// Strings [first, n) (first a multiple of 64: every wave writes whole rate_err words).
-__global__ void __launch_bounds__(BLOCK) k_pdict_parse(const uint8_t* bytes, const uint32_t* offs,
-                                                       uint32_t first, uint32_t n, double tick, uint32_t* ppct,
-                                                       uint2* pdur, uint2* prate, uint32_t* rate_err) {
-    __shared__ uint4 buf[STAGE / 16];
-    const uint32_t s0 = first + blockIdx.x * BLOCK, s1 = min(s0 + BLOCK, n);
+template <int WHICH>
+KD_INLINE void pdict_parse_block(const uint8_t* bytes, const uint32_t* offs, uint32_t s0, uint32_t n, double tick,
+                                 uint32_t* ppct, uint2* pdur, uint2* prate, uint32_t* rate_err, uint4* buf) {
+    const uint32_t s1 = min(s0 + BLOCK, n);
     uint32_t a0;
     const bool staged = stage_slice(bytes, offs, s0, s1, buf, &a0) != nullptr;
     __syncthreads();
@@ -309,16 +310,39 @@ __global__ void __launch_bounds__(BLOCK) k_pdict_parse(const uint8_t* bytes, con
         const uint32_t b = offs[i], len = offs[i + 1] - b;
         uint32_t pct;
         uint2 dur, rate;
-        if (staged) pdict_parse_one(reinterpret_cast<const uint8_t*>(buf) + (b - a0), len, tick, &pct, &dur, &rate, &bad);
-        else pdict_parse_one(bytes + b, len, tick, &pct, &dur, &rate, &bad);
-        ppct[i] = pct;
-        pdur[i] = dur;
-        prate[i] = rate;
+        const uint8_t* str = staged ? reinterpret_cast<const uint8_t*>(buf) + (b - a0) : bytes + b;
+        pdict_parse_one<WHICH>(str, len, tick, &pct, &dur, &rate, &bad);
+        if constexpr ((WHICH & PD_PCT) != 0) ppct[i] = pct;
+        if constexpr ((WHICH & PD_DUR) != 0) pdur[i] = dur;
+        if constexpr ((WHICH & PD_RATE) != 0) prate[i] = rate;
     }
-    const uint64_t m = __ballot(bad);
-    const int lane = threadIdx.x & 63;
-    if (lane == 0 || lane == 32) rate_err[((i - lane) >> 5) + (lane >> 5)] = lane ? (uint32_t)(m >> 32) : (uint32_t)m;
+    if constexpr ((WHICH & PD_RATE) != 0) {
+        const uint64_t m = __ballot(bad);
+        const int lane = threadIdx.x & 63;
+        if (lane == 0 || lane == 32) rate_err[((i - lane) >> 5) + (lane >> 5)] = lane ? (uint32_t)(m >> 32) : (uint32_t)m;
+    }
 }
+
+// Strings [first, n) (first a multiple of 64: every wave writes whole rate_err words).
+// SPLIT: gridDim.y = 3, blockIdx.y picks the interpretation.
+template <bool SPLIT>
+__global__ void __launch_bounds__(BLOCK) k_pdict_parse(const uint8_t* bytes, const uint32_t* offs,
+                                                       uint32_t first, uint32_t n, double tick, uint32_t* ppct,
+                                                       uint2* pdur, uint2* prate, uint32_t* rate_err) {
+    __shared__ uint4 buf[STAGE / 16];
+    const uint32_t s0 = first + blockIdx.x * BLOCK;
+    if constexpr (SPLIT) {
+        if (blockIdx.y == 0) pdict_parse_block<PD_PCT>(bytes, offs, s0, n, tick, ppct, pdur, prate, rate_err, buf);
+        else if (blockIdx.y == 1) pdict_parse_block<PD_DUR>(bytes, offs, s0, n, tick, ppct, pdur, prate, rate_err, buf);
+        else pdict_parse_block<PD_RATE>(bytes, offs, s0, n, tick, ppct, pdur, prate, rate_err, buf);
+    } else {
+        pdict_parse_block<PD_DUR | PD_PCT | PD_RATE>(bytes, offs, s0, n, tick, ppct, pdur, prate, rate_err, buf);
+    }
+}
+template __global__ void k_pdict_parse<false>(const uint8_t*, const uint32_t*, uint32_t, uint32_t, double, uint32_t*,
+                                              uint2*, uint2*, uint32_t*);
+template __global__ void k_pdict_parse<true>(const uint8_t*, const uint32_t*, uint32_t, uint32_t, double, uint32_t*,
+                                             uint2*, uint2*, uint32_t*);
 
 // ======================================================================================
 // pod-status table + lookup tables

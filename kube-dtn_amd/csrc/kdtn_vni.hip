@@ -1,0 +1,175 @@
+// kdtn_vni.hip — VxlanManager state after the epoch (include/kdtn.h kdtn_epoch_vni_apply).
+//
+// The daemons' maps change as the reached entries run: delLink deletes VNI 5000+uid on the
+// local node when the map holds the local pod's netns there (handler.go:484-487); a
+// cross-node addLink stores (vni, local netns) on the local node after SetupVxLan
+// (:440) and the peer daemon's Update stores (vni, peer netns) on the peer's node
+// (:192, reached unless remote_err); a physical peer's local Update stores (vni, local netns)
+// (:355-371 → :192). Map ops are sync.Map Store / Delete (daemon/vxlan/manager.go:57-63).
+// Deterministic order (the reference's is goroutine order): every delete first, then every
+// add; per key the first add in (topology, add-list, local-before-remote) order wins.
+//
+// Kernels: k_vni_ops (one thread per topology: RPC-order reach as k_reach, one op slot per
+// del entry and two per add entry), k_vni_shadow / k_vni_del (snapshot entries that are not,
+// or no longer, in the map: shadowed duplicates, deleted keys), then the
+// new map as a first-wins table over [add ops, surviving snapshot entries] (k_vni_insert)
+// and its visible entries compacted in that order (k_vni_vis_count / k_scan_top /
+// k_vni_vis_write).
+#include "kdtn_kernels.h"
+
+namespace kdtn {
+
+__global__ void __launch_bounds__(BLOCK) k_vni_ops(VniOpsIn f, uint4* ops) {
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= f.r.T) return;
+    const uint32_t src = f.t_src[t], netns = f.t_netns[t];
+    const uint4 none = make_uint4(0u, 0u, 0u, VOP_NONE);
+    bool ok = true;
+    for (uint32_t e = f.r.del_off[t], e1 = f.r.del_off[t + 1]; e < e1; ++e) {
+        uint4 op = none;
+        if (ok) {
+            const uint4 r = f.r.del_res[e];
+            if ((r.w >> 8) & 0xFFu) ok = false;                              // MakeVeth error :470-474
+            else if ((r.w >> 16) & 0xFFu) op = make_uint4(src, r.y, 0u, VOP_DEL);   // vni_hit :484-487
+        }
+        ops[e] = op;
+    }
+    uint4* aops = ops + f.n_del;
+    for (uint32_t e = f.r.add_off[t], e1 = f.r.add_off[t + 1]; e < e1; ++e) {
+        uint4 lo = none, rm = none;
+        if (ok) {
+            const uint4 r = f.r.add_res[e];
+            const uint32_t qe = qdisc_err(f.r.add_qdisc, e);
+            if (add_fails(r, qe)) {
+                ok = false;
+            } else {
+                const uint32_t kind = r.w & 0xFFu;
+                if (kind == KDTN_KIND_CROSS_NODE || kind == KDTN_KIND_PHYSICAL)
+                    lo = make_uint4(src, r.y, netns, VOP_ADD);                // :440 / :192
+                if (kind == KDTN_KIND_CROSS_NODE) {
+                    if (r.w >> 24) ok = false;                                 // remote Update failed
+                    else rm = make_uint4(r.z, r.y, f.pods[r.x].w & 0x7FFFFFFFu, VOP_ADD);   // peer node :192
+                }
+            }
+        }
+        aops[2 * (size_t)e] = lo;
+        aops[2 * (size_t)e + 1] = rm;
+    }
+}
+
+// slot of key (node, vni) in the snapshot table (entries ents[slots[h]]), or 0xFFFFFFFF
+KD_INLINE uint32_t vni_find(const uint4* ents, const uint32_t* slots, uint32_t mask, uint32_t node, uint32_t vni) {
+    for (uint32_t h = vni_home(node, vni, mask);; h = (h + 1) & mask) {
+        const uint32_t s = slots[h];
+        if (s == 0xFFFFFFFFu) return s;
+        const uint4 e = ents[s];
+        if (e.x == node && e.y == vni) return s;
+    }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_vni_del(const uint4* ops, uint32_t n_del, const uint4* ents,
+                                                   const uint32_t* slots, uint32_t mask, uint8_t* dead) {
+    const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= n_del) return;
+    const uint4 op = ops[j];
+    if (op.w != VOP_DEL || mask == 0) return;
+    const uint32_t i = vni_find(ents, slots, mask, op.x, op.y);
+    if (i != 0xFFFFFFFFu) dead[i] = 1;
+}
+
+// snapshot entries shadowed by an earlier entry of the same key (first wins) are not in the map
+__global__ void __launch_bounds__(BLOCK) k_vni_shadow(const uint4* ents, uint32_t n_ents, const uint32_t* slots,
+                                                      uint32_t mask, uint8_t* dead) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n_ents) return;
+    const uint4 e = ents[i];
+    dead[i] = vni_find(ents, slots, mask, e.x, e.y) != i;
+}
+
+// Extended entry x: add op x (x < n_ops) or snapshot entry x - n_ops; present = an add op,
+// or a snapshot entry that is the visible one of its key (the snapshot's own first wins)
+// and was not deleted.
+KD_INLINE bool ext_entry(const uint4* add_ops, uint32_t n_ops, const uint4* ents, const uint8_t* dead, uint32_t x,
+                         uint4* e) {
+    if (x < n_ops) {
+        *e = add_ops[x];
+        return e->w == VOP_ADD;
+    }
+    const uint32_t i = x - n_ops;
+    *e = ents[i];
+    return !dead[i];
+}
+
+__global__ void __launch_bounds__(BLOCK) k_vni_insert(const uint4* add_ops, uint32_t n_ops, const uint4* ents,
+                                                      const uint8_t* dead, uint32_t n_ents, uint32_t* slots,
+                                                      uint32_t mask) {
+    const uint32_t x = blockIdx.x * BLOCK + threadIdx.x;
+    if (x >= n_ops + n_ents) return;
+    uint4 e;
+    if (!ext_entry(add_ops, n_ops, ents, dead, x, &e)) return;
+    for (uint32_t h = vni_home(e.x, e.y, mask);; h = (h + 1) & mask) {
+        const uint32_t prev = atomicCAS(&slots[h], 0xFFFFFFFFu, x);
+        if (prev == 0xFFFFFFFFu) return;
+        uint4 o;
+        ext_entry(add_ops, n_ops, ents, dead, prev, &o);
+        if (o.x == e.x && o.y == e.y) {
+            atomicMin(&slots[h], x);                  // first in extended order wins
+            return;
+        }
+    }
+}
+
+KD_INLINE bool ext_visible(const uint4* add_ops, uint32_t n_ops, const uint4* ents, const uint8_t* dead, uint32_t n_ents,
+                           const uint32_t* slots, uint32_t mask, uint32_t x, uint4* e) {
+    if (x >= n_ops + n_ents || !ext_entry(add_ops, n_ops, ents, dead, x, e)) return false;
+    for (uint32_t h = vni_home(e->x, e->y, mask);; h = (h + 1) & mask) {
+        const uint32_t s = slots[h];
+        if (s == 0xFFFFFFFFu) return false;
+        uint4 o;
+        ext_entry(add_ops, n_ops, ents, dead, s, &o);
+        if (o.x == e->x && o.y == e->y) return s == x;
+    }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_vni_vis_count(const uint4* add_ops, uint32_t n_ops, const uint4* ents,
+                                                         const uint8_t* dead, uint32_t n_ents, const uint32_t* slots,
+                                                         uint32_t mask, uint64_t* part) {
+    __shared__ uint64_t sh[BLOCK / 64];
+    const uint32_t b0 = blockIdx.x * SCAN_CHUNK + threadIdx.x * 4;
+    uint64_t v = 0;
+    uint4 e;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v += ext_visible(add_ops, n_ops, ents, dead, n_ents, slots, mask, b0 + k, &e) ? 1u : 0u;
+    uint64_t tot;
+    block_exclusive(v, sh, &tot);
+    if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_vni_vis_write(const uint4* add_ops, uint32_t n_ops, const uint4* ents,
+                                                         const uint8_t* dead, uint32_t n_ents, const uint32_t* slots,
+                                                         uint32_t mask, const uint64_t* part, uint32_t* node,
+                                                         int32_t* vni, uint32_t* net_ns, uint32_t* n_out) {
+    __shared__ uint64_t sh[BLOCK / 64];
+    const uint32_t b0 = blockIdx.x * SCAN_CHUNK + threadIdx.x * 4;
+    bool m[4];
+    uint4 e[4];
+    uint64_t v = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        m[k] = ext_visible(add_ops, n_ops, ents, dead, n_ents, slots, mask, b0 + k, &e[k]);
+        v += m[k] ? 1u : 0u;
+    }
+    uint64_t tot;
+    uint64_t x = part[blockIdx.x] + block_exclusive(v, sh, &tot);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (m[k]) {
+            node[x] = e[k].x;
+            vni[x] = (int32_t)e[k].y;
+            net_ns[x] = e[k].z;
+            ++x;
+        }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *n_out = (uint32_t)(part[blockIdx.x] + tot);
+}
+
+}  // namespace kdtn

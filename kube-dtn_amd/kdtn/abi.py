@@ -63,6 +63,13 @@ class VniTable(C.Structure):
     _fields_ = [("n", C.c_uint32), ("node", u32p), ("vni", i32p), ("net_ns", u32p)]
 
 
+VNI_RESIDENT = 0xFFFFFFFF   # kdtn_epoch_in.vnis.n: use the context's resident VXLAN map
+
+
+class VniState(C.Structure):
+    _fields_ = [("cap", C.c_uint64), ("n", C.c_uint32), ("node", u32p), ("vni", i32p), ("net_ns", u32p)]
+
+
 class EpochIn(C.Structure):
     _fields_ = [("kdict", Strtab), ("pdict", Strtab), ("topos", TopoTable),
                 ("realised", LinkTable), ("desired", LinkTable), ("vnis", VniTable),
@@ -166,7 +173,7 @@ EXPORTS = ["kdtn_version", "kdtn_strerror", "kdtn_err_name", "kdtn_init", "kdtn_
            "kdtn_interner_free", "kdtn_intern", "kdtn_intern_batch", "kdtn_interner_table",
            "kdtn_reconcile_epoch", "kdtn_epoch_upload", "kdtn_epoch_run", "kdtn_epoch_sync",
            "kdtn_epoch_download", "kdtn_make_qdiscs", "kdtn_comm_unique_id", "kdtn_comm_init",
-           "kdtn_set_timing", "kdtn_last_kernel_times", "kdtn_debug_wg_trace", "kdtn_epoch_encode",
+           "kdtn_set_timing", "kdtn_epoch_vni_apply", "kdtn_vni_download", "kdtn_last_kernel_times", "kdtn_debug_wg_trace", "kdtn_epoch_encode",
            "kdtn_epoch_download_wire", "kdtn_diff", "kdtn_resolve", "kdtn_host_alloc",
            "kdtn_host_free", "kdtn_epoch_fanout", "kdtn_epoch_tc", "kdtn_epoch_download_tc",
            "kdtn_json_upload", "kdtn_json_ingest", "kdtn_ingest_download", "kdtn_topology_shard",

@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 from . import abi
-from .tables import BatchesOut, EpochInput, StrTab
+from .tables import BatchesOut, EpochInput, StrTab, Vnis
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libkdtn.so")
@@ -74,6 +74,8 @@ def lib() -> C.CDLL:
         "kdtn_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8 * 128)]),
         "kdtn_comm_init": (C.c_int, [vp, C.POINTER(C.c_uint8 * 128), C.c_int, C.c_int]),
         "kdtn_set_timing": (C.c_int, [vp, C.c_int]),
+        "kdtn_epoch_vni_apply": (C.c_int, [vp, C.POINTER(abi.VniState)]),
+        "kdtn_vni_download": (C.c_int, [vp, C.POINTER(abi.VniState)]),
         "kdtn_last_kernel_times": (C.c_int, [vp, C.POINTER(C.c_char_p), C.POINTER(C.c_float), C.c_int]),
         "kdtn_debug_wg_trace": (C.c_int, [vp, C.POINTER(C.c_uint64), C.c_uint32]),
         "kdtn_epoch_encode": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
@@ -356,6 +358,22 @@ class Engine:
         f.node_cap, f.idx_cap = node.size, idx.size
         _check(lib().kdtn_epoch_fanout(self._ctx, C.byref(f)), "kdtn_epoch_fanout")
         return node[:f.n_nodes], off, idx[:f.n_send]
+
+    def vni_apply(self) -> Vnis:
+        """kdtn_epoch_vni_apply: the daemons' VxlanManager maps after the last epoch's reached
+        entries; the result also becomes the engine's resident map (Vnis.keep_resident())."""
+        _check(lib().kdtn_epoch_vni_apply(self._ctx, None), "kdtn_epoch_vni_apply")
+        return self.vni_download()
+
+    def vni_download(self) -> Vnis:
+        """kdtn_vni_download: the engine's resident VXLAN map."""
+        st = abi.VniState(0, 0, None, None, None)
+        _check(lib().kdtn_vni_download(self._ctx, C.byref(st)), "kdtn_vni_download")
+        n = st.n
+        node, vni, ns = np.zeros(max(n, 1), np.uint32), np.zeros(max(n, 1), np.int32), np.zeros(max(n, 1), np.uint32)
+        st = abi.VniState(max(n, 1), 0, abi.ptr(node, abi.u32p), abi.ptr(vni, abi.i32p), abi.ptr(ns, abi.u32p))
+        _check(lib().kdtn_vni_download(self._ctx, C.byref(st)), "kdtn_vni_download")
+        return Vnis(node[:n], vni[:n], ns[:n])
 
     def set_timing(self, level: int) -> None:
         """HIP-event timing of kdtn_epoch_run: 0 none, 1 k_reconcile (+ placement), 2 every stage."""

@@ -131,12 +131,19 @@ class Vnis:
     node: np.ndarray = field(default_factory=lambda: np.zeros(0, np.uint32))
     vni: np.ndarray = field(default_factory=lambda: np.zeros(0, np.int32))
     net_ns: np.ndarray = field(default_factory=lambda: np.zeros(0, np.uint32))
+    resident: bool = False      # KDTN_VNI_RESIDENT: the engine keeps its own map (no upload)
+
+    @classmethod
+    def keep_resident(cls) -> "Vnis":
+        return cls(resident=True)
 
     @property
     def n(self) -> int:
         return int(self.node.shape[0])
 
     def to_c(self) -> abi.VniTable:
+        if self.resident:
+            return abi.VniTable(abi.VNI_RESIDENT, None, None, None)
         self.node = np.ascontiguousarray(self.node, dtype=np.uint32)
         self.vni = np.ascontiguousarray(self.vni, dtype=np.int32)
         self.net_ns = np.ascontiguousarray(self.net_ns, dtype=np.uint32)

@@ -84,6 +84,11 @@ uint32_t or_fanout(const kdtn_batches* b, uint32_t T, uint32_t* node, uint32_t* 
 /* SetVethQdiscs' tc argv per add (veth/VXLAN kinds) then update entry with a TBF and no
  * error (common/qdisc.go:252-266); off has n_add + n_upd + 1 entries. */
 uint64_t or_tc_epoch(const kdtn_epoch_in* in, const kdtn_batches* b, uint8_t* bytes, uint64_t* off);
+/* VxlanManager maps after the epoch's reached entries (deletes, then first-wins adds);
+ * returns the entry count (out_* may be NULL to count). pod_netns: net_ns id per global pod. */
+uint32_t or_vni_apply(const kdtn_batches* b, uint32_t T, const uint32_t* t_src, const uint32_t* t_netns,
+                      const uint32_t* pod_netns, const kdtn_vni_table* snap, uint32_t* out_node,
+                      int32_t* out_vni, uint32_t* out_netns);
 
 /* ---- CR ingest (kdtn_oracle_json.c): TopologyList JSON → epoch tables ------------- */
 typedef struct or_json_tables {

@@ -335,3 +335,100 @@ uint64_t or_tc_epoch(const kdtn_epoch_in* in, const kdtn_batches* b, uint8_t* by
     free(ru);
     return pos;
 }
+
+/* ======================================================================================
+ * VxlanManager state after the epoch (daemon/vxlan/manager.go:57-63 Add / Delete as
+ * sync.Map Store / Delete): delLink deletes VNI 5000+uid on the local node when Get(vni) is
+ * the local pod's netns (daemon/kubedtn/handler.go:480-487); a cross-node addLink stores
+ * (vni, local netns) after SetupVxLan (:426-440) and the peer daemon's Update stores
+ * (vni, peer netns) (common/utils.go:39-48 payload NetNs = peerPod.NetNs; handler.go:192);
+ * a physical peer's local Update stores (vni, local netns) (:348-371). Entries reached as in
+ * or_reach. The reference runs them in goroutine order; this restatement fixes one:
+ * every delete first, then every add, the first add of a (node, vni) key in (topology,
+ * add-list, local-before-remote) order winning. Output: the winning adds in that order,
+ * then the snapshot's surviving entries (first occurrence of each key) in snapshot order.
+ * ==================================================================================== */
+typedef struct { uint64_t* key; uint32_t* val; uint32_t mask; } vmap;
+static uint64_t vkey(uint32_t node, int32_t vni) { return ((uint64_t)node << 32) | (uint32_t)vni; }
+static uint32_t* vslot(vmap* m, uint64_t k) {      /* value slot of k (UINT32_MAX = absent) */
+    uint64_t h = k * 0x9E3779B97F4A7C15ull;
+    for (uint32_t i = (uint32_t)(h >> 32) & m->mask;; i = (i + 1) & m->mask) {
+        if (m->val[i] == UINT32_MAX || m->key[i] == k) {
+            m->key[i] = k;
+            return &m->val[i];
+        }
+    }
+}
+
+uint32_t or_vni_apply(const kdtn_batches* b, uint32_t T, const uint32_t* t_src, const uint32_t* t_netns,
+                      const uint32_t* pod_netns, const kdtn_vni_table* snap, uint32_t* out_node,
+                      int32_t* out_vni, uint32_t* out_netns) {
+    const uint32_t nd = b->del_off[T], na = b->add_off[T], V = snap->n;
+    uint64_t cap = 64;
+    while (cap < 2ull * (V + 2ull * na + 1)) cap <<= 1;
+    vmap snapm = {calloc(cap, 8), malloc(cap * 4), (uint32_t)cap - 1};   /* key → first snapshot entry */
+    vmap addm = {calloc(cap, 8), malloc(cap * 4), (uint32_t)cap - 1};    /* key → winning add (order) */
+    memset(snapm.val, 0xFF, cap * 4);
+    memset(addm.val, 0xFF, cap * 4);
+    uint8_t* gone = calloc(V + 1, 1);
+    for (uint32_t i = 0; i < V; i++) {
+        uint32_t* v = vslot(&snapm, vkey(snap->node[i], snap->vni[i]));
+        if (*v == UINT32_MAX) *v = i;
+        else gone[i] = 1;                                            /* shadowed duplicate */
+    }
+    uint32_t* an = malloc(sizeof(uint32_t) * (2 * na + 1));
+    int32_t* av = malloc(sizeof(int32_t) * (2 * na + 1));
+    uint32_t* as = malloc(sizeof(uint32_t) * (2 * na + 1));
+    uint32_t nadd = 0;
+    (void)nd;
+    for (int pass = 0; pass < 2; pass++) {                           /* 0: deletes, 1: adds */
+        for (uint32_t t = 0; t < T; t++) {
+            int ok = 1;
+            for (uint32_t e = b->del_off[t]; e < b->del_off[t + 1] && ok; e++) {
+                const kdtn_resolved* r = &b->del_res[e];
+                if (r->err) { ok = 0; break; }
+                if (pass == 0 && r->vni_hit) {
+                    uint32_t* v = vslot(&snapm, vkey(t_src[t], r->vni));
+                    if (*v != UINT32_MAX) gone[*v] = 1;
+                }
+            }
+            for (uint32_t e = b->add_off[t]; e < b->add_off[t + 1] && ok; e++) {
+                const kdtn_resolved* r = &b->add_res[e];
+                if (fan_fails(r, &b->add_qdisc[e])) { ok = 0; break; }
+                if (pass == 0) { if (r->kind == KDTN_KIND_CROSS_NODE && r->remote_err) ok = 0; continue; }
+                uint32_t node[2], netns[2], k = 0;
+                if (r->kind == KDTN_KIND_CROSS_NODE || r->kind == KDTN_KIND_PHYSICAL) {
+                    node[k] = t_src[t];
+                    netns[k++] = t_netns[t];
+                }
+                if (r->kind == KDTN_KIND_CROSS_NODE) {
+                    if (r->remote_err) ok = 0;
+                    else {
+                        node[k] = r->vtep;
+                        netns[k++] = pod_netns[r->peer_topo];
+                    }
+                }
+                for (uint32_t q = 0; q < k; q++) {
+                    uint32_t* v = vslot(&addm, vkey(node[q], r->vni));
+                    if (*v != UINT32_MAX) continue;                      /* an earlier add won */
+                    *v = nadd;
+                    an[nadd] = node[q];
+                    av[nadd] = r->vni;
+                    as[nadd++] = netns[q];
+                }
+            }
+        }
+    }
+    uint32_t n = 0;
+    for (uint32_t q = 0; q < nadd; q++, n++) {
+        if (out_node) { out_node[n] = an[q]; out_vni[n] = av[q]; out_netns[n] = as[q]; }
+    }
+    for (uint32_t i = 0; i < V; i++) {
+        if (gone[i]) continue;
+        if (*vslot(&addm, vkey(snap->node[i], snap->vni[i])) != UINT32_MAX) continue;   /* overridden */
+        if (out_node) { out_node[n] = snap->node[i]; out_vni[n] = snap->vni[i]; out_netns[n] = snap->net_ns[i]; }
+        n++;
+    }
+    free(snapm.key); free(snapm.val); free(addm.key); free(addm.val); free(gone); free(an); free(av); free(as);
+    return n;
+}

@@ -292,3 +292,27 @@ def json_ingest(doc: bytes):
         return 0, 0, inp
     finally:
         L.or_json_free(C.byref(t))
+
+
+def vni_apply(inp: EpochInput, out: BatchesOut, pod_netns=None):
+    """VxlanManager maps after the epoch's reached entries (or_vni_apply): (node, vni, net_ns)
+    arrays — the winning adds in (topology, add-list, local-before-remote) order, then the
+    snapshot's surviving entries. pod_netns: net_ns id per global pod (default: this
+    epoch's topologies)."""
+    L = _wire_lib()
+    if not getattr(L, "_vni_bound", False):
+        L.or_vni_apply.argtypes = [C.POINTER(abi.Batches), C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                   C.POINTER(abi.VniTable), C.c_void_p, C.c_void_p, C.c_void_p]
+        L.or_vni_apply.restype = C.c_uint32
+        L._vni_bound = True
+    T = inp.topos.n
+    b = out.to_c((max(len(out.del_idx), 1), max(len(out.add_idx), 1), max(len(out.upd_idx), 1)))
+    src = np.ascontiguousarray(inp.topos.src_ip, np.uint32)
+    ns = np.ascontiguousarray(inp.topos.net_ns, np.uint32)
+    pn = np.ascontiguousarray(ns if pod_netns is None else pod_netns, np.uint32)
+    vt = inp.vnis.to_c()
+    n = L.or_vni_apply(C.byref(b), T, src.ctypes.data, ns.ctypes.data, pn.ctypes.data, C.byref(vt), None, None, None)
+    node, vni, net = np.zeros(max(n, 1), np.uint32), np.zeros(max(n, 1), np.int32), np.zeros(max(n, 1), np.uint32)
+    L.or_vni_apply(C.byref(b), T, src.ctypes.data, ns.ctypes.data, pn.ctypes.data, C.byref(vt), node.ctypes.data,
+                   vni.ctypes.data, net.ctypes.data)
+    return node[:n], vni[:n], net[:n]
