@@ -1233,12 +1233,22 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
     const int tid = threadIdx.x;
     unsigned long long t_entry = 0;
     if constexpr ((V & VAR_TRACE) != 0) t_entry = __builtin_amdgcn_s_memrealtime();
-    if (tid == 0) s.ticket = atomicAdd(&wk.sync[SYNC_TICKET], 1u);   // dispatch order → look-back order
-    __syncthreads();
+    constexpr bool kDefer = (V & VAR_DIFF) != 0;
+    const uint32_t fpi = *wk.first_partial_inv;          // ~first partial chunk (0: none)
+    // A dynamic ticket (dispatch order) orders look-backs after scheduled predecessors. Without
+    // look-backs — every chunk in the full prefix, or the comparison build, whose chunks past
+    // it are deferred — the workgroup index serves and the single-address atomic (one per
+    // workgroup) stays off every workgroup's critical path.
+    const bool need_ticket = (V & VAR_NO_PREFIX) != 0 || (!kDefer && fpi != 0u);
+    if (need_ticket) {
+        if (tid == 0) s.ticket = atomicAdd(&wk.sync[SYNC_TICKET], 1u);
+        __syncthreads();
+    }
+    const uint32_t tk = need_ticket ? s.ticket : blockIdx.x;
     // wk.split workgroups per chunk: part 0 does the chunk's work; in a bulk chunk of the full
     // prefix (bases known without predecessors) the parts share its records, so a small epoch
     // whose chunks hold many records does not leave most of the chip idle in a second round
-    const uint32_t wg = s.ticket / wk.split, part = s.ticket - wg * wk.split;
+    const uint32_t wg = tk / wk.split, part = tk - wg * wk.split;
     if constexpr ((V & VAR_TRACE) != 0) {
         trace_mark<V>(wk, wg, 0, t_entry);
         uint32_t xcc, hw;
@@ -1279,7 +1289,7 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
     // bulk: no topology of this workgroup has both lists non-empty (new pods: status empty;
     // deleted pods: spec nil) → every record of a DIFF topology is an entry, in order
     const bool bulk = s.any_cmp == 0;
-    const bool prefix = (V & VAR_NO_PREFIX) == 0 && wg <= ~*wk.first_partial_inv;
+    const bool prefix = (V & VAR_NO_PREFIX) == 0 && wg <= ~fpi;
     const bool shared = bulk && prefix;                  // the parts split the records
     if (part != 0 && !shared) return;                    // (block-uniform)
     const bool lead = part == 0;
@@ -1379,7 +1389,6 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
     // windows. It emits at record-offset bases into the upper halves of the output arrays
     // (every list of a chunk holds at most as many entries as its records), and k_place moves
     // the entries down once k_place_scan has summed the workgroup counts.
-    constexpr bool kDefer = (V & VAR_DIFF) != 0;
     const bool deferred = kDefer && !prefix;
     if constexpr (kDefer) {
         if (lead && tid < 3) wk.wcount[(size_t)wg * 3 + tid] = s.wtot[tid];
