@@ -1235,6 +1235,25 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
     if constexpr ((V & VAR_TRACE) != 0) t_entry = __builtin_amdgcn_s_memrealtime();
     constexpr bool kDefer = (V & VAR_DIFF) != 0;
     const uint32_t fpi = *wk.first_partial_inv;          // ~first partial chunk (0: none)
+    // The chunk's topology rows, loaded for chunk blockIdx.x / split while fpi is in flight
+    // (reloaded below in the rare ticket case).
+    struct TopoRow { uint32_t ro, no, ns, src, netns; uint8_t fl; };
+    auto load_rows = [&](uint32_t w, TopoRow& r) {
+        const uint32_t t0_ = w * TPW;
+        const int nt_ = (int)min((uint32_t)TPW, T.n - t0_);
+        if (tid <= nt_) {
+            r.ro = T.real_off[t0_ + tid];
+            r.no = T.des_off[t0_ + tid];
+        }
+        if (tid < nt_) {
+            r.fl = T.flags[t0_ + tid];
+            r.ns = T.ns[t0_ + tid];
+            r.src = T.src_ip[t0_ + tid];
+            r.netns = T.net_ns[t0_ + tid];
+        }
+    };
+    TopoRow row{};
+    load_rows(blockIdx.x / wk.split, row);
     // A dynamic ticket (dispatch order) orders look-backs after scheduled predecessors. Without
     // look-backs — every chunk in the full prefix, or the comparison build, whose chunks past
     // it are deferred — the workgroup index serves and the single-address atomic (one per
@@ -1249,6 +1268,7 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
     // prefix (bases known without predecessors) the parts share its records, so a small epoch
     // whose chunks hold many records does not leave most of the chip idle in a second round
     const uint32_t wg = tk / wk.split, part = tk - wg * wk.split;
+    if (need_ticket && wg != blockIdx.x / wk.split) load_rows(wg, row);
     if constexpr ((V & VAR_TRACE) != 0) {
         trace_mark<V>(wk, wg, 0, t_entry);
         uint32_t xcc, hw;
@@ -1259,15 +1279,15 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
     const uint32_t t0 = wg * TPW;
     const int nt = (int)min((uint32_t)TPW, T.n - t0);
     if (tid <= nt) {
-        s.ooff[tid] = T.real_off[t0 + tid];
-        s.noff[tid] = T.des_off[t0 + tid];
+        s.ooff[tid] = row.ro;
+        s.noff[tid] = row.no;
     }
     if (tid < nt) {
-        s.tflag[tid] = T.flags[t0 + tid];
+        s.tflag[tid] = row.fl;
         s.dirty[tid] = 0;
-        s.ns[tid] = T.ns[t0 + tid];
-        s.src[tid] = T.src_ip[t0 + tid];
-        s.netns[tid] = T.net_ns[t0 + tid];
+        s.ns[tid] = row.ns;
+        s.src[tid] = row.src;
+        s.netns[tid] = row.netns;
     }
     if (tid < TPW) {
         s.tcnt[0][tid] = 0;
@@ -1469,7 +1489,12 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
         RecCols cc;
         fetch(cs, cc);
         for (uint32_t b = rlo; b < rhi; b += BLOCK) {
-            const Slot nx = decode(b + BLOCK + tid);
+            // the next record's segment search (LDS) runs after this record's gathers issue
+            Slot nx;
+            if constexpr ((V & VAR_DECODE_FIRST) != 0) nx = decode(b + BLOCK + tid);
+            auto next = [&]() {
+                if constexpr ((V & VAR_DECODE_FIRST) == 0) nx = decode(b + BLOCK + tid);
+            };
             RecCols nc;
             bool qa = false;
             uint32_t e = 0, q[18];
@@ -1477,17 +1502,20 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
                 const int tt = cs.tt;
                 const TopoCtx tc{s.ns[tt], s.src[tt], s.netns[tt]};
                 if (cs.old) {
+                    next();
                     fetch(nx, nc);
                     emit_del<V>(cc, cs.x, tc, tb, out, bd + s.tcnt[0][tt] + (cs.x - s.ooff[tt]), do_res);
                 } else {
                     e = ba + s.tcnt[2][tt] + (cs.x - s.noff[tt]);
                     AddGath g;
                     add_gather<V>(cc, tc, tb, do_res, do_q, g);
+                    next();
                     fetch(nx, nc);
                     add_finish<V>(cc, g, N, cs.x, tc, tb, out, e, do_res, do_q, q);
                     qa = do_q;
                 }
             } else {
+                next();
                 fetch(nx, nc);
             }
             wave_store_qdisc<V>(out.add_qdisc, qa, e, q, stage);
