@@ -341,6 +341,19 @@ void launch_pdict(kdtn_ctx* c, uint32_t p0, uint32_t n) {
     bool split = KDTN_PD_SPLIT_DEFAULT;
 #if KDTN_PROFILING
     if (const char* ev = std::getenv("KDTN_PD_SPLIT")) split = std::atoi(ev) != 0;
+    if (const char* ev = std::getenv("KDTN_PD_ONLY")) {           // one interpretation alone (A/B)
+        const int w = std::atoi(ev);
+        auto one = [&](auto kern) {
+            kern<<<nblocks(n - p0), BLOCK, 0, c->stream>>>(dp<uint8_t>(c->pd_bytes), dp<uint32_t>(c->pd_offs), p0, n,
+                                                          c->cfg.tick_in_usec, dp<uint32_t>(c->pd_pct),
+                                                          dp<uint2>(c->pd_dur), dp<uint2>(c->pd_rate),
+                                                          dp<uint32_t>(c->pd_rerr));
+        };
+        if (w == PD_DUR) { one(k_pdict_only<PD_DUR>); return; }
+        if (w == PD_PCT) { one(k_pdict_only<PD_PCT>); return; }
+        if (w == PD_RATE) { one(k_pdict_only<PD_RATE>); return; }
+        if (w == (PD_RATE | PD_RATE_GENERIC)) { one(k_pdict_only<PD_RATE | PD_RATE_GENERIC>); return; }
+    }
 #endif
     const dim3 grid(nblocks(n - p0), split ? 3 : 1);
     auto go = [&](auto kern) {
@@ -732,11 +745,12 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
 #if KDTN_PROFILING
             int sub = 1;                                               // strings per thread (2, 4: slower)
             if (const char* ev = std::getenv("KDTN_KD_SUB")) sub = std::atoi(ev);
-            if (sub == 4) k_kdict_flags<4><<<nblocks(nk, BLOCK * 4), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
-            else if (sub == 2) k_kdict_flags<2><<<nblocks(nk, BLOCK * 2), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
+            if (sub == 4) k_kdict_flags<4, false><<<nblocks(nk, BLOCK * 4), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
+            else if (sub == 2) k_kdict_flags<2, false><<<nblocks(nk, BLOCK * 2), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
+            else if (sub == 8) k_kdict_flags<1, true><<<nblocks(nk), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
             else
 #endif
-            k_kdict_flags<1><<<nblocks(nk), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
+            k_kdict_flags<1, false><<<nblocks(nk), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
         }
     }
     timer_mark(c, "kdict_parse", 2);

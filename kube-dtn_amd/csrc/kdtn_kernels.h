@@ -216,9 +216,13 @@ __global__ void k_place(DevTopos T, const uint32_t* wcount, const uint32_t* wbas
 constexpr int PLACE_SCAN_BLOCK = 1024, PLACE_PER = 8;    // k_place_scan: workgroups per thread per tile
 
 __global__ void k_special_clip(uint32_t* special, uint32_t k0);
-template <int SUB>
+template <int SUB, bool X4>
 __global__ void k_kdict_flags(const uint8_t* bytes, const uint32_t* offs, uint32_t first, uint32_t n,
                               uint32_t* kbits, uint32_t kb_words, uint32_t* special);
+template <int WHICH>
+__global__ void k_pdict_only(const uint8_t* bytes, const uint32_t* offs, uint32_t first, uint32_t n, double tick,
+                             uint32_t* ppct, uint2* pdur, uint2* prate, uint32_t* rate_err);
+enum : int { PD_DUR = 1, PD_PCT = 2, PD_RATE = 4, PD_RATE_GENERIC = 8 /* (A/B) no ASCII fast path */ };
 template <bool SPLIT>
 __global__ void k_pdict_parse(const uint8_t* bytes, const uint32_t* offs, uint32_t first, uint32_t n, double tick,
                               uint32_t* ppct, uint2* pdur, uint2* prate, uint32_t* rate_err);

@@ -228,7 +228,8 @@ __global__ void k_special_clip(uint32_t* special, uint32_t k0) {
 // of the thread's strings is issued, then every string's 7 dwords, then the parses run —
 // the kernel is latency-bound, so a wave keeps SUB strings' round trips in flight at once.
 // Strings [first, n) (first a multiple of 64: every wave writes whole predicate words).
-template <int SUB>
+// X4: the window comes from three 16-B aligned loads (48 bytes) instead of seven dwords.
+template <int SUB, bool X4>
 __global__ void __launch_bounds__(BLOCK) k_kdict_flags(const uint8_t* bytes, const uint32_t* offs,
                                                        uint32_t first, uint32_t n, uint32_t* kbits,
                                                        uint32_t kb_words, uint32_t* special) {
@@ -244,9 +245,19 @@ __global__ void __launch_bounds__(BLOCK) k_kdict_flags(const uint8_t* bytes, con
     uint32_t d[SUB][7];
 #pragma unroll
     for (int s = 0; s < SUB; ++s) {
-        const uint32_t* p = reinterpret_cast<const uint32_t*>(bytes + (b[s] & ~3u));   // arena has 64 B slack
+        if constexpr (X4) {
+            const uint4* p = reinterpret_cast<const uint4*>(bytes + (b[s] & ~15u));    // arena has 64 B slack
+            const uint4 q0 = p[0], q1 = p[1], q2 = p[2];
+            const uint32_t D[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
+            const uint32_t o = (b[s] >> 2) & 3u;
 #pragma unroll
-        for (int k = 0; k < 7; ++k) d[s][k] = p[k];
+            for (int k = 0; k < 7; ++k)
+                d[s][k] = o == 0 ? D[k] : o == 1 ? D[k + 1] : o == 2 ? D[k + 2] : D[k + 3];
+        } else {
+            const uint32_t* p = reinterpret_cast<const uint32_t*>(bytes + (b[s] & ~3u));   // arena has 64 B slack
+#pragma unroll
+            for (int k = 0; k < 7; ++k) d[s][k] = p[k];
+        }
     }
     const int lane = threadIdx.x & 63;
 #pragma unroll
@@ -267,16 +278,16 @@ __global__ void __launch_bounds__(BLOCK) k_kdict_flags(const uint8_t* bytes, con
         }
     }
 }
-template __global__ void k_kdict_flags<1>(const uint8_t*, const uint32_t*, uint32_t, uint32_t, uint32_t*, uint32_t, uint32_t*);
+template __global__ void k_kdict_flags<1, false>(const uint8_t*, const uint32_t*, uint32_t, uint32_t, uint32_t*, uint32_t, uint32_t*);
 #if KDTN_PROFILING
-template __global__ void k_kdict_flags<2>(const uint8_t*, const uint32_t*, uint32_t, uint32_t, uint32_t*, uint32_t, uint32_t*);
-template __global__ void k_kdict_flags<4>(const uint8_t*, const uint32_t*, uint32_t, uint32_t, uint32_t*, uint32_t, uint32_t*);
+template __global__ void k_kdict_flags<1, true>(const uint8_t*, const uint32_t*, uint32_t, uint32_t, uint32_t*, uint32_t, uint32_t*);
+template __global__ void k_kdict_flags<2, false>(const uint8_t*, const uint32_t*, uint32_t, uint32_t, uint32_t*, uint32_t, uint32_t*);
+template __global__ void k_kdict_flags<4, false>(const uint8_t*, const uint32_t*, uint32_t, uint32_t, uint32_t*, uint32_t, uint32_t*);
 #endif
 
 // One property string's interpretations: WHICH = 7 all three, else one of PD_DUR / PD_PCT /
 // PD_RATE (the split launch gives each interpretation its own threads: more waves in flight
 // for a latency-bound parse, and each parse path alone needs fewer registers).
-enum : int { PD_DUR = 1, PD_PCT = 2, PD_RATE = 4 };
 template <int WHICH>
 KD_INLINE void pdict_parse_one(const uint8_t* s, uint32_t len, double tick, uint32_t* pct_out,
                                uint2* dur_out, uint2* rate_out, bool* rate_bad) {
@@ -291,7 +302,7 @@ KD_INLINE void pdict_parse_one(const uint8_t* s, uint32_t len, double tick, uint
     }
     if constexpr ((WHICH & PD_RATE) != 0) {
         uint64_t r = 0;
-        const bool rok = parse_rate(s, len, &r);
+        const bool rok = (WHICH & PD_RATE_GENERIC) ? parse_rate_generic(s, len, &r) : parse_rate(s, len, &r);
         *rate_out = rok ? make_uint2((uint32_t)r, (uint32_t)(r >> 32)) : make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
         *rate_bad = !rok;
     }
@@ -339,6 +350,24 @@ __global__ void __launch_bounds__(BLOCK) k_pdict_parse(const uint8_t* bytes, con
         pdict_parse_block<PD_DUR | PD_PCT | PD_RATE>(bytes, offs, s0, n, tick, ppct, pdur, prate, rate_err, buf);
     }
 }
+#if KDTN_PROFILING
+// (profiling) one interpretation alone: WHICH = PD_DUR / PD_PCT / PD_RATE
+template <int WHICH>
+__global__ void __launch_bounds__(BLOCK) k_pdict_only(const uint8_t* bytes, const uint32_t* offs, uint32_t first,
+                                                      uint32_t n, double tick, uint32_t* ppct, uint2* pdur,
+                                                      uint2* prate, uint32_t* rate_err) {
+    __shared__ uint4 buf[STAGE / 16];
+    pdict_parse_block<WHICH>(bytes, offs, first + blockIdx.x * BLOCK, n, tick, ppct, pdur, prate, rate_err, buf);
+}
+template __global__ void k_pdict_only<PD_DUR>(const uint8_t*, const uint32_t*, uint32_t, uint32_t, double, uint32_t*,
+                                              uint2*, uint2*, uint32_t*);
+template __global__ void k_pdict_only<PD_PCT>(const uint8_t*, const uint32_t*, uint32_t, uint32_t, double, uint32_t*,
+                                              uint2*, uint2*, uint32_t*);
+template __global__ void k_pdict_only<PD_RATE>(const uint8_t*, const uint32_t*, uint32_t, uint32_t, double, uint32_t*,
+                                               uint2*, uint2*, uint32_t*);
+template __global__ void k_pdict_only<PD_RATE | PD_RATE_GENERIC>(const uint8_t*, const uint32_t*, uint32_t, uint32_t,
+                                                                 double, uint32_t*, uint2*, uint2*, uint32_t*);
+#endif
 template __global__ void k_pdict_parse<false>(const uint8_t*, const uint32_t*, uint32_t, uint32_t, double, uint32_t*,
                                               uint2*, uint2*, uint32_t*);
 template __global__ void k_pdict_parse<true>(const uint8_t*, const uint32_t*, uint32_t, uint32_t, double, uint32_t*,

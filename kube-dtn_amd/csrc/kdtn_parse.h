@@ -436,7 +436,7 @@ KD_INLINE int rate_char(uint32_t r) {
     return 0x80;
 }
 
-KD_INLINE bool parse_rate(const uint8_t* s, uint32_t n, uint64_t* out) {
+KD_INLINE bool parse_rate_generic(const uint8_t* s, uint32_t n, uint64_t* out) {
     *out = 0;
     // pass 1: trimmed rune range and the last 5 mapped chars
     uint32_t a = 0;
@@ -504,6 +504,47 @@ KD_INLINE bool parse_rate(const uint8_t* s, uint32_t n, uint64_t* out) {
         if (v >= cutoff) return false;
         v *= 10;
         uint64_t v1 = v + (uint64_t)(c - '0');
+        if (v1 < v) return false;
+        v = v1;
+    }
+    *out = v * mult;
+    return true;
+}
+
+// ParseRate of a string of printable ASCII without spaces (every synthetic and nearly every
+// real rate string): TrimSpace is the identity, each byte is one rune and ToLower is ASCII,
+// so the suffix test reads the last bytes and ParseUint the first ones directly — the same
+// result as parse_rate_generic without its rune decoding and ring buffer per character.
+KD_INLINE bool parse_rate(const uint8_t* s, uint32_t n, uint64_t* out) {
+    bool simple = n > 0;
+    for (uint32_t i = 0; i < n; ++i) simple &= s[i] >= 0x21 && s[i] <= 0x7E;
+    if (!simple) return parse_rate_generic(s, n, out);
+    *out = 0;
+    auto tc = [&](uint32_t k) -> int { return k < n ? lower_ascii(s[n - 1 - k]) : -1; };   // k-th from end
+    uint32_t strip = 0;
+    uint64_t mult = 1;
+    if (n >= 3 && tc(2) == 'b' && tc(1) == 'i' && tc(0) == 't') strip = 3;
+    else if (n >= 3 && tc(2) == 'b' && tc(1) == 'p' && tc(0) == 's') { strip = 3; mult = 8; }
+    uint64_t base = 1000;
+    if (n - strip >= 1 && tc(strip) == 'i') { ++strip; base = 1024; }
+    if (n - strip >= 1) {
+        const int u = tc(strip);
+        const int idx = u == 'k' ? 0 : u == 'm' ? 1 : u == 'g' ? 2 : u == 't' ? 3 : -1;
+        if (idx >= 0) {
+            ++strip;
+            for (int j = 0; j <= idx; ++j) mult *= base;
+        }
+    }
+    const uint32_t keep = n - strip;
+    if (keep == 0) return false;                    // ParseUint("") → syntax error
+    uint64_t v = 0;
+    const uint64_t cutoff = 0xFFFFFFFFFFFFFFFFull / 10 + 1;
+    for (uint32_t k = 0; k < keep; ++k) {
+        const int c = s[k];
+        if (!is_digit(c)) return false;
+        if (v >= cutoff) return false;
+        v *= 10;
+        const uint64_t v1 = v + (uint64_t)(c - '0');
         if (v1 < v) return false;
         v = v1;
     }
