@@ -698,10 +698,6 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
     c->last_stages = stages;
     c->n_ev = 0;
     hipStream_t s = c->stream;
-    if (c->timing >= 2) (void)hipEventRecord(c->ev[0], s);
-    uint32_t* sync = dp<uint32_t>(c->sync);
-    HIP_TRY(hipMemsetAsync(sync, 0, sync_bytes(c->nwg), s));          // header (SYNC_*), look-back
-
     const DevTopos T = topo_view(c);
     const bool resolve = stages & KDTN_STAGE_RESOLVE;
     const bool host_xchg = resolve && c->nranks > 1 && !c->comm;      // rows imported by the caller
@@ -711,11 +707,18 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
                       "host transport: kdtn_pods_import the gathered pod table before kdtn_epoch_run");
         return KDTN_EINVAL;
     }
-    if (resolve && !host_xchg) {
-        // pod-status rows first: across ranks they are all-gathered over RCCL on the comm
-        // stream while this stream parses the dictionaries (the exchange needs neither)
+    if (c->timing >= 2) (void)hipEventRecord(c->ev[0], s);
+    uint32_t* sync = dp<uint32_t>(c->sync);
+    {
+        // one launch zeroes the sync header (SYNC_*) and look-back area and fills this rank's
+        // pod-status rows: across ranks they are all-gathered over RCCL on the comm stream
+        // while this stream parses the dictionaries (the exchange needs neither)
+        const uint32_t n16 = (uint32_t)(sync_bytes(c->nwg) / 16);
+        const uint32_t nbz = std::min<uint32_t>(nblocks(n16), 256);
+        const uint32_t fill = (resolve && !host_xchg) ? c->slice : 0u;
         const uint32_t rank_base = c->slice * (uint32_t)c->rank;
-        if (c->slice) k_pods_fill<<<nblocks(c->slice), BLOCK, 0, s>>>(T, c->slice, rank_base, dp<uint4>(c->pods));
+        k_epoch_begin<<<nbz + nblocks(fill), BLOCK, 0, s>>>(reinterpret_cast<uint4*>(sync), n16, nbz, T, fill,
+                                                            rank_base, dp<uint4>(c->pods));
         if (exchange) {
             HIP_TRY(hipEventRecord(c->ev_fill, s));
             HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_fill, 0));
@@ -728,8 +731,6 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
             }
             HIP_TRY(hipEventRecord(c->ev_ag, c->comm_stream));
         }
-        timer_mark(c, "pods_fill", 2);
-    } else if (resolve) {
         timer_mark(c, "pods_fill", 2);
     }
     // dictionaries: the strings this upload added (all of them unless kdict_keep /
@@ -773,9 +774,6 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
             k_pod_direct_scatter<<<nblocks(c->pod_total), BLOCK, 0, s>>>(
                 dp<uint4>(c->pods), c->pod_total, dp<uint32_t>(c->kd_bits) + (size_t)KB_PHYSICAL * c->kb_words,
                 dp<uint4>(c->pod_direct), c->pod_stamp, c->D);
-            k_pod_direct_verify<<<nblocks(c->pod_total), BLOCK, 0, s>>>(dp<uint4>(c->pods), c->pod_total,
-                                                                       dp<uint4>(c->pod_direct), c->pod_stamp,
-                                                                       dp<unsigned long long>(c->pod_ovf), c->ovf_mask, c->D);
         }
         if (c->V) {
             const size_t vcap = (size_t)c->vni_mask + 1;
@@ -846,9 +844,18 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
 #if KDTN_PROFILING
         if (const char* ev = std::getenv("KDTN_SPLIT")) if (std::atoi(ev) > 0) w.split = (uint32_t)std::atoi(ev);
 #endif
-        k_full_prefix<<<(unsigned)std::min<uint64_t>(FP_GRID, (c->T + 4 * FP_BLOCK - 1) / (4 * FP_BLOCK)), FP_BLOCK, 0, s>>>(
-            T, sync + SYNC_FIRST_PARTIAL_INV);
-        timer_mark(c, "full_prefix", 2);
+        if (resolve && c->pod_total) {                  // the pod-table verify with the full-prefix scan
+            const uint32_t nbv = nblocks(c->pod_total);
+            const uint32_t nbp = (uint32_t)std::min<uint64_t>(4 * FP_GRID, (c->T + 4 * BLOCK - 1) / (4 * BLOCK));
+            k_pod_verify_prefix<<<nbv + std::max<uint32_t>(nbp, 1), BLOCK, 0, s>>>(
+                dp<uint4>(c->pods), c->pod_total, dp<uint4>(c->pod_direct), c->pod_stamp,
+                dp<unsigned long long>(c->pod_ovf), c->ovf_mask, c->D, T, sync + SYNC_FIRST_PARTIAL_INV, nbv);
+            timer_mark(c, "verify_prefix", 2);
+        } else {
+            k_full_prefix<<<(unsigned)std::min<uint64_t>(FP_GRID, (c->T + 4 * FP_BLOCK - 1) / (4 * FP_BLOCK)), FP_BLOCK, 0, s>>>(
+                T, sync + SYNC_FIRST_PARTIAL_INV);
+            timer_mark(c, "full_prefix", 2);
+        }
         if (c->timing == 1) (void)hipEventRecord(c->ev[0], s);
 #if KDTN_PROFILING
         int variant = DEFAULT_VARIANT;

@@ -227,6 +227,8 @@ template <bool SPLIT>
 __global__ void k_pdict_parse(const uint8_t* bytes, const uint32_t* offs, uint32_t first, uint32_t n, double tick,
                               uint32_t* ppct, uint2* pdur, uint2* prate, uint32_t* rate_err);
 __global__ void k_pods_fill(DevTopos T, uint32_t slice, uint32_t rank_base, uint4* pods);
+__global__ void k_epoch_begin(uint4* sync, uint32_t n16, uint32_t nbz, DevTopos T, uint32_t slice, uint32_t rank_base,
+                              uint4* pods);
 __global__ void k_pod_direct_scatter(const uint4* pods, uint32_t total, const uint32_t* phys_bits,
                                      uint4* slots, uint32_t stamp, uint32_t nd);
 __global__ void k_pod_direct_verify(const uint4* pods, uint32_t total, uint4* slots, uint32_t stamp,
@@ -391,6 +393,9 @@ __global__ void k_wire_write(WireIn w, DevLinks O, DevLinks N, WireWork wk, uint
 __global__ void k_qdisc_batch(DevLinks props, DevTables tb, uint2* out);
 constexpr int FP_BLOCK = 1024, FP_GRID = 256;       // k_full_prefix launch shape
 __global__ void k_full_prefix(DevTopos T, uint32_t* first_partial_inv);
+__global__ void k_pod_verify_prefix(const uint4* pods, uint32_t total, uint4* slots, uint32_t stamp,
+                                    unsigned long long* ovf, uint32_t mask, uint32_t nd, DevTopos T,
+                                    uint32_t* first_partial_inv, uint32_t nbv);
 
 // ---- CR ingest: TopologyList JSON → epoch tables (kdtn_ingest.hip) ------------------------
 // token word: {byte offset, pre-depth | kind << 24}

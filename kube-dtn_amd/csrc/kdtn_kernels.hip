@@ -376,9 +376,25 @@ template __global__ void k_pdict_parse<true>(const uint8_t*, const uint32_t*, ui
 // ======================================================================================
 // pod-status table + lookup tables
 // ======================================================================================
+KD_INLINE void pods_fill_one(const DevTopos& T, uint32_t slice, uint32_t rank_base, uint4* pods, uint32_t t);
+
 __global__ void __launch_bounds__(BLOCK) k_pods_fill(DevTopos T, uint32_t slice, uint32_t rank_base,
                                                      uint4* pods) {
-    uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    pods_fill_one(T, slice, rank_base, pods, blockIdx.x * BLOCK + threadIdx.x);
+}
+
+// The epoch's first launch: zero the sync header and look-back area (n16 16-B words, blocks
+// [0, nbz)) and fill this rank's pod-status rows (the other blocks; slice 0 = none).
+__global__ void __launch_bounds__(BLOCK) k_epoch_begin(uint4* sync, uint32_t n16, uint32_t nbz, DevTopos T,
+                                                       uint32_t slice, uint32_t rank_base, uint4* pods) {
+    if (blockIdx.x < nbz) {
+        for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n16; i += nbz * BLOCK) sync[i] = make_uint4(0u, 0u, 0u, 0u);
+        return;
+    }
+    pods_fill_one(T, slice, rank_base, pods, (blockIdx.x - nbz) * BLOCK + threadIdx.x);
+}
+
+KD_INLINE void pods_fill_one(const DevTopos& T, uint32_t slice, uint32_t rank_base, uint4* pods, uint32_t t) {
     if (t >= slice) return;
     uint4 e;
     if (t < T.n) {
@@ -446,10 +462,8 @@ __global__ void __launch_bounds__(BLOCK) k_pod_direct_scatter(const uint4* pods,
 // Pods whose name slot was won by another pod: mark the name `multi` and put both pods
 // into the overflow table (duplicates are rare; the table then answers every lookup of
 // that name).
-__global__ void __launch_bounds__(BLOCK) k_pod_direct_verify(const uint4* pods, uint32_t total, uint4* slots,
-                                                             uint32_t stamp, unsigned long long* ovf, uint32_t mask,
-                                                             uint32_t nd) {
-    const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
+KD_INLINE void pod_verify_one(const uint4* pods, uint32_t total, uint4* slots, uint32_t stamp,
+                               unsigned long long* ovf, uint32_t mask, uint32_t nd, uint32_t g) {
     if (g >= total) return;
     const uint4 e = pods[g];
     if (e.x == 0xFFFFFFFFu || e.y >= nd) return;
@@ -459,6 +473,12 @@ __global__ void __launch_bounds__(BLOCK) k_pod_direct_verify(const uint4* pods, 
     reinterpret_cast<uint32_t*>(slots + e.y)[3] = (stamp << 1) | 1u;
     ovf_insert(pods, g, e.x, e.y, ovf, mask, stamp);
     ovf_insert(pods, owner, pods[owner].x, e.y, ovf, mask, stamp);
+}
+
+__global__ void __launch_bounds__(BLOCK) k_pod_direct_verify(const uint4* pods, uint32_t total, uint4* slots,
+                                                             uint32_t stamp, unsigned long long* ovf, uint32_t mask,
+                                                             uint32_t nd) {
+    pod_verify_one(pods, total, slots, stamp, ovf, mask, nd, blockIdx.x * BLOCK + threadIdx.x);
 }
 
 __global__ void __launch_bounds__(BLOCK) k_vni_pack(const uint32_t* node, const int32_t* vni,
@@ -1211,16 +1231,17 @@ KD_INLINE bool topo_partial(uint8_t tf, uint32_t ko, uint32_t kn) {
     return cmp || !(diff || empty);
 }
 
-// Four topologies per thread (16-B offset loads), grid-stride over FP_GRID blocks, one
-// global atomicMin per block: an epoch of partial topologies (config 3) sent every wave's
-// atomic to one address (133 µs).
-// The result is stored inverted (atomicMax of ~chunk) so the zeroed sync header means "none".
-__global__ void __launch_bounds__(FP_BLOCK) k_full_prefix(DevTopos T, uint32_t* first_partial_inv) {
-    __shared__ uint32_t bmin;
-    if (threadIdx.x == 0) bmin = 0xFFFFFFFFu;
+// Four topologies per thread (16-B offset loads), grid-stride over the role's nb blocks of
+// NT threads, one global atomicMax per block: an epoch of partial topologies (config 3) sent
+// every wave's atomic to one address (133 µs). The result is stored inverted (atomicMax of
+// ~chunk) so the zeroed sync header means "none".
+template <int NT>
+KD_INLINE void full_prefix_blocks(const DevTopos& T, uint32_t* first_partial_inv, uint32_t bid, uint32_t nb,
+                                  uint32_t* bmin) {
+    if (threadIdx.x == 0) *bmin = 0xFFFFFFFFu;
     __syncthreads();
-    const uint32_t stride = gridDim.x * FP_BLOCK * 4;
-    for (uint32_t base = blockIdx.x * FP_BLOCK * 4; base < T.n; base += stride) {
+    const uint32_t stride = nb * NT * 4;
+    for (uint32_t base = bid * NT * 4; base < T.n; base += stride) {
         const uint32_t t0 = base + threadIdx.x * 4;
         uint32_t first = 0xFFFFFFFFu;                  // first partial topology of the four
         if (t0 + 4 <= T.n) {
@@ -1241,10 +1262,29 @@ __global__ void __launch_bounds__(FP_BLOCK) k_full_prefix(DevTopos T, uint32_t* 
         const bool partial = first != 0xFFFFFFFFu;
         const uint64_t m = __ballot(partial);
         if (partial && (threadIdx.x & 63) == (uint32_t)(__ffsll((long long)m) - 1))
-            atomicMin(&bmin, first / TPW);              // lanes hold increasing topologies
+            atomicMin(bmin, first / TPW);               // lanes hold increasing topologies
         if (__syncthreads_or(m != 0)) break;         // later iterations only hold later chunks
     }
-    if (threadIdx.x == 0 && bmin != 0xFFFFFFFFu) atomicMax(first_partial_inv, ~bmin);
+    if (threadIdx.x == 0 && *bmin != 0xFFFFFFFFu) atomicMax(first_partial_inv, ~*bmin);
+}
+
+__global__ void __launch_bounds__(FP_BLOCK) k_full_prefix(DevTopos T, uint32_t* first_partial_inv) {
+    __shared__ uint32_t bmin;
+    full_prefix_blocks<FP_BLOCK>(T, first_partial_inv, blockIdx.x, gridDim.x, &bmin);
+}
+
+// k_pod_direct_verify and k_full_prefix in one launch (independent work; one kernel boundary
+// less per epoch): blocks [0, nbv) verify pods, the rest scan topologies.
+__global__ void __launch_bounds__(BLOCK) k_pod_verify_prefix(const uint4* pods, uint32_t total, uint4* slots,
+                                                             uint32_t stamp, unsigned long long* ovf, uint32_t mask,
+                                                             uint32_t nd, DevTopos T, uint32_t* first_partial_inv,
+                                                             uint32_t nbv) {
+    __shared__ uint32_t bmin;
+    if (blockIdx.x < nbv) {
+        pod_verify_one(pods, total, slots, stamp, ovf, mask, nd, blockIdx.x * BLOCK + threadIdx.x);
+        return;
+    }
+    full_prefix_blocks<BLOCK>(T, first_partial_inv, blockIdx.x - nbv, gridDim.x - nbv, &bmin);
 }
 
 // (VAR_TRACE) phase timestamp of this workgroup: 100 MHz chip-wide clock

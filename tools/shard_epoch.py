@@ -1,0 +1,73 @@
+"""One rank of the N-GPU strong-scaling run, measured on one GPU: rank R of N owns the
+topologies with kdtn_topology_shard(ns, name, N) == R of the config-2 topology; the
+all-gathered pod-status table (every rank's rows, rank-major, pod_slice rows per rank) is
+built on the host from the unsharded topology (same shared kdict prefix) and imported with
+the host transport (kdtn_pods_import), so each epoch runs exactly the rank's kernels minus
+the RCCL all-gather's wait. Checks that the rank's own rows equal kdtn_pods_export.
+
+    python tools/shard_epoch.py [--pods 1000000] [--nshards 8] [--rank 0] [--reps 30]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch  # noqa: F401  (one HIP runtime)
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "kube-dtn_amd"))
+import numpy as np  # noqa: E402
+
+from kdtn import Engine, abi, synth, topology_shard  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--pods", type=int, default=1_000_000)
+ap.add_argument("--nshards", type=int, default=8)
+ap.add_argument("--rank", type=int, default=0)
+ap.add_argument("--reps", type=int, default=30)
+a = ap.parse_args()
+t0 = time.time()
+full = synth.make(2, total_pods=a.pods)
+sh = synth.make(2, total_pods=a.pods, shard=a.rank, nshards=a.nshards)
+gen_s = time.time() - t0
+kb, ko = full.kdict.bytes_, full.kdict.offs
+s = lambda i: bytes(kb[ko[i]:ko[i + 1]])
+T = full.topos
+owner = np.array([topology_shard(s(T.ns[t]), s(T.name[t]), a.nshards) for t in range(T.n)], np.int64)
+slice_ = sh.pod_slice
+rows = np.zeros((a.nshards * slice_, 4), np.uint32)
+rows[:, 0] = rows[:, 1] = 0xFFFFFFFF
+nil = ((T.flags & abi.TOPO_SPEC_NIL) != 0).astype(np.uint32) << 31
+for k in range(a.nshards):
+    g = np.nonzero(owner == k)[0]
+    assert len(g) <= slice_
+    rows[k * slice_:k * slice_ + len(g)] = np.stack([T.ns[g], T.name[g], T.src_ip[g], T.net_ns[g] | nil[g]]).T
+    if k == a.rank:
+        assert np.array_equal(g, sh.gid), "rank's topologies differ from the generator's shard"
+
+res = {"config": 2, "pods_total": a.pods, "nshards": a.nshards, "rank": a.rank, "links_rank": int(sh.desired.n),
+       "topos_rank": int(sh.topos.n), "pod_slice": int(slice_), "kdict": int(sh.kdict.n), "pdict": int(sh.pdict.n),
+       "gen_s": round(gen_s, 1)}
+with Engine(device=0) as eng:
+    eng.set_ranks(a.nshards, a.rank)
+    eng.upload(sh)
+    mine = eng.pods_export(slice_)
+    assert np.array_equal(mine, rows[a.rank * slice_:(a.rank + 1) * slice_]), "own rows differ from the host table"
+    eng.pods_import(rows)
+    for level in (2, 1, 0):
+        eng.set_timing(level)
+        for _ in range(3):
+            eng.run()
+            eng.sync()
+        tot = []
+        for _ in range(a.reps):
+            t = time.perf_counter()
+            eng.run()
+            eng.sync()
+            tot.append(time.perf_counter() - t)
+        res[f"L{level}"] = {"ms_epoch": sorted(tot)[len(tot) // 2] * 1e3, "kernels_ms": eng.kernel_times() if level else {}}
+    ms = res["L0"]["ms_epoch"]
+    res["projected_links_per_s_at_N"] = a.pods * 10 / (ms * 1e-3)
+    res["note"] = ("rank epoch without the RCCL all-gather wait (rows imported once); links_per_s projected as "
+                   "10 links per pod over the rank's epoch")
+print(json.dumps(res), flush=True)
