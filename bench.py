@@ -529,6 +529,17 @@ def main():
         share, info = cpu_share()
         threads = args.cpu_threads or min(32, share)
         result["cpu_baseline"] = cpu_baseline(inp, args.cpu_budget_s, threads, info)
+    if world == 1 and args.config == 4:                    # VxlanManager maps after the epoch
+        eng.run()
+        eng.sync()
+        t = time.perf_counter()
+        vm = eng.vni_apply()
+        wall = time.perf_counter() - t
+        kt = eng.kernel_times()
+        result["vni_apply_stage"] = {"entries_before": int(inp.vnis.n), "entries_after": int(vm.n),
+                                     "gpu_ms": sum(kt.values()), "kernels_ms": kt, "wall_ms": wall * 1e3,
+                                     "note": "not part of value: kdtn_epoch_vni_apply (deletes, then first-wins "
+                                             "adds of the reached entries) + download of the map"}
     if world == 1 and not args.no_ingest and args.config == 2:
         result["ingest_stage"] = ingest_stage(eng, inp, steps)
     if rank == 0:

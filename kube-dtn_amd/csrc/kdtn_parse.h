@@ -204,21 +204,90 @@ KD_INLINE int cmp_decimal_vs_dyadic(const uint8_t* s, uint32_t beg, uint32_t end
     return 0;
 }
 
-// pow10 as doubles (exact for 0..22)
-KD_INLINE double pow10_exact(int e) {
-    double r = 1.0;
-    double b = 10.0;
-    // exact repeated squaring for e <= 22 (all intermediates exact)
-    while (e) {
-        if (e & 1) r = __dmul_rn(r, b);
-        b = __dmul_rn(b, b);
-        e >>= 1;
+// pow10 as doubles (exact for 0..22): a table lookup (every power up to 1e22 is exact)
+static __constant__ double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                                         1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+KD_INLINE double pow10_exact(int e) { return kPow10[e]; }
+
+// The value of a syntactically valid float string from its readFloat state (mantissa,
+// significant digits, decimal point, digit range for the exact compare): the rounding to
+// float32 and the percentage range check.
+KD_INLINE bool pct_finish(const uint8_t* s, bool neg, bool hex, bool trunc, uint64_t mant, int ndmant, long dp,
+                          uint32_t dig_beg, uint32_t dig_end, float* out) {
+    if (mant == 0) { *out = 0.0f; return true; }   // ±0 → 0 (−0 is not < 0)
+
+    // Only |V| <= 100 matters. Values below 1e-30 (float32 normal range starts at
+    // ~1.18e-38) need just one fact: whether they round to zero, i.e. |V| <= 2^-150
+    // (the tie at exactly 2^-150 goes to the even value 0). Positive tiny values are
+    // accepted either way and Percentage2u32 maps them to 0; negative ones are an
+    // error unless they round to -0. This keeps all float32 arithmetic normal.
+    float v;
+    const double TWO_M150 = 7.006492321624085354618647916449580656401309709382578858785341e-46;
+    if (hex) {
+        // value = mant × 2^(dp - 4*ndmant), plus a sticky bit when digits were cut
+        long e2 = dp - 4L * ndmant;
+        int lz = __clzll(mant);
+        uint64_t m = mant << lz;                 // top bit at 63
+        long E = e2 + 63 - lz;                   // value in [2^E, 2^(E+1))
+        if (E >= 7) return false;                // >= 128: > 100 or < 0
+        if (E < -100) {
+            if (!neg) { *out = 0.0f; return true; }
+            bool nonzero = E > -150 || (E == -150 && ((m << 1) != 0 || trunc));
+            if (nonzero) return false;
+            *out = 0.0f;
+            return true;
+        }
+        uint64_t kept = m >> 40;                 // 24 significant bits
+        uint64_t rest = m << 24;
+        bool half = (rest >> 63) & 1ull;
+        bool low = ((rest << 1) != 0) || trunc;
+        if (half && (low || (kept & 1ull))) ++kept;
+        v = (float)ldexp((double)kept, (int)(E - 23));   // exact
+    } else {
+        // decimal: V = 0.<digits> × 10^dp
+        if (dp >= 4) return false;               // |V| >= 100.0 × 10: > 100 or < 0
+        if (dp <= -46) { *out = 0.0f; return true; }  // |V| < 1e-46 < 2^-150 → ±0
+        int e10 = (int)(dp - ndmant);            // V ≈ mant × 10^e10
+        double approx = (double)mant;
+        if (e10 >= 0) approx = __dmul_rn(approx, pow10_exact(e10));
+        else if (e10 >= -22) approx = __ddiv_rn(approx, pow10_exact(-e10));
+        else {
+            approx = __ddiv_rn(approx, 1e22);
+            int r = -e10 - 22;
+            while (r > 22) { approx = __ddiv_rn(approx, 1e22); r -= 22; }
+            approx = __ddiv_rn(approx, pow10_exact(r));
+        }
+        if (approx < 1e-30) {
+            if (!neg) { *out = 0.0f; return true; }
+            int r = cmp_decimal_vs_dyadic(s, dig_beg, dig_end, dp, TWO_M150);
+            if (r > 0) return false;
+            *out = 0.0f;
+            return true;
+        }
+        float c = (float)approx;
+        float cd = nextafterf(c, 0.0f);
+        float cu = nextafterf(c, 3.4e38f);
+        double mlo = ((double)cd + (double)c) * 0.5;
+        double mhi = ((double)c + (double)cu) * 0.5;
+        double tol = approx * 1e-13;
+        v = c;
+        if (fabs(approx - mhi) <= tol) {
+            int r = cmp_decimal_vs_dyadic(s, dig_beg, dig_end, dp, mhi);
+            if (r > 0) v = cu;
+            else if (r == 0) v = (__float_as_uint(c) & 1u) ? cu : c;
+        } else if (fabs(approx - mlo) <= tol) {
+            int r = cmp_decimal_vs_dyadic(s, dig_beg, dig_end, dp, mlo);
+            if (r < 0) v = cd;
+            else if (r == 0) v = (__float_as_uint(c) & 1u) ? cd : c;
+        }
     }
-    return r;
+    if (neg) v = -v;
+    if (v < 0.0f || v > 100.0f) return false;
+    *out = v;
+    return true;
 }
 
-// ParseFloatPercentage(s): "" → 0; any Go syntax/range error, NaN, <0 or >100 → error.
-KD_INLINE bool parse_pct(const uint8_t* s, uint32_t n, float* out) {
+KD_INLINE bool parse_pct_generic(const uint8_t* s, uint32_t n, float* out) {
     *out = 0.0f;
     if (n == 0) return true;
     // special(): inf/infinity/nan forms are all errors for a percentage (NaN → error,
@@ -309,77 +378,48 @@ KD_INLINE bool parse_pct(const uint8_t* s, uint32_t n, float* out) {
         if (saw == '_') return false;
     }
     if (i != n) return false;
-    if (mant == 0) { *out = 0.0f; return true; }   // ±0 → 0 (−0 is not < 0)
+    return pct_finish(s, neg, hex, trunc, mant, ndmant, dp, dig_beg, dig_end, out);
+}
 
-    // Only |V| <= 100 matters. Values below 1e-30 (float32 normal range starts at
-    // ~1.18e-38) need just one fact: whether they round to zero, i.e. |V| <= 2^-150
-    // (the tie at exactly 2^-150 goes to the even value 0). Positive tiny values are
-    // accepted either way and Percentage2u32 maps them to 0; negative ones are an
-    // error unless they round to -0. This keeps all float32 arithmetic normal.
-    float v;
-    const double TWO_M150 = 7.006492321624085354618647916449580656401309709382578858785341e-46;
-    if (hex) {
-        // value = mant × 2^(dp - 4*ndmant), plus a sticky bit when digits were cut
-        long e2 = dp - 4L * ndmant;
-        int lz = __clzll(mant);
-        uint64_t m = mant << lz;                 // top bit at 63
-        long E = e2 + 63 - lz;                   // value in [2^E, 2^(E+1))
-        if (E >= 7) return false;                // >= 128: > 100 or < 0
-        if (E < -100) {
-            if (!neg) { *out = 0.0f; return true; }
-            bool nonzero = E > -150 || (E == -150 && ((m << 1) != 0 || trunc));
-            if (nonzero) return false;
-            *out = 0.0f;
-            return true;
-        }
-        uint64_t kept = m >> 40;                 // 24 significant bits
-        uint64_t rest = m << 24;
-        bool half = (rest >> 63) & 1ull;
-        bool low = ((rest << 1) != 0) || trunc;
-        if (half && (low || (kept & 1ull))) ++kept;
-        v = (float)ldexp((double)kept, (int)(E - 23));   // exact
-    } else {
-        // decimal: V = 0.<digits> × 10^dp
-        if (dp >= 4) return false;               // |V| >= 100.0 × 10: > 100 or < 0
-        if (dp <= -46) { *out = 0.0f; return true; }  // |V| < 1e-46 < 2^-150 → ±0
-        int e10 = (int)(dp - ndmant);            // V ≈ mant × 10^e10
-        double approx = (double)mant;
-        if (e10 >= 0) approx = __dmul_rn(approx, pow10_exact(e10));
-        else if (e10 >= -22) approx = __ddiv_rn(approx, pow10_exact(-e10));
-        else {
-            approx = __ddiv_rn(approx, 1e22);
-            int r = -e10 - 22;
-            while (r > 22) { approx = __ddiv_rn(approx, 1e22); r -= 22; }
-            approx = __ddiv_rn(approx, pow10_exact(r));
-        }
-        if (approx < 1e-30) {
-            if (!neg) { *out = 0.0f; return true; }
-            int r = cmp_decimal_vs_dyadic(s, dig_beg, dig_end, dp, TWO_M150);
-            if (r > 0) return false;
-            *out = 0.0f;
-            return true;
-        }
-        float c = (float)approx;
-        float cd = nextafterf(c, 0.0f);
-        float cu = nextafterf(c, 3.4e38f);
-        double mlo = ((double)cd + (double)c) * 0.5;
-        double mhi = ((double)c + (double)cu) * 0.5;
-        double tol = approx * 1e-13;
-        v = c;
-        if (fabs(approx - mhi) <= tol) {
-            int r = cmp_decimal_vs_dyadic(s, dig_beg, dig_end, dp, mhi);
-            if (r > 0) v = cu;
-            else if (r == 0) v = (__float_as_uint(c) & 1u) ? cu : c;
-        } else if (fabs(approx - mlo) <= tol) {
-            int r = cmp_decimal_vs_dyadic(s, dig_beg, dig_end, dp, mlo);
-            if (r < 0) v = cd;
-            else if (r == 0) v = (__float_as_uint(c) & 1u) ? cd : c;
+// ParseFloatPercentage of a plain decimal of at most 16 bytes (digits and at most one '.',
+// starting with a digit or '.'): its bytes are loaded at once and scanned by a fully
+// unrolled, predicated readFloat (no sign, base prefix, underscore or exponent can occur, and
+// 16 digits never reach the 19-digit mantissa limit); anything else takes the generic parser.
+KD_INLINE bool parse_pct(const uint8_t* s, uint32_t n, float* out) {
+    if (n == 0 || n > 16) return parse_pct_generic(s, n, out);
+    uint32_t c[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) c[k] = (uint32_t)k < n ? s[k] : 0u;
+    bool ok = true, sawdot = false, sawdigits = false;
+    long nd = 0, dp = 0;
+    uint64_t mant = 0;
+    int ndmant = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        if ((uint32_t)k < n) {
+            const uint32_t ch = c[k];
+            const bool dig = ch - '0' <= 9u;
+            if (ch == '.') {
+                ok &= !sawdot;
+                sawdot = true;
+                dp = nd;
+            } else if (dig) {
+                sawdigits = true;
+                if (ch == '0' && nd == 0) {
+                    --dp;
+                } else {
+                    ++nd;
+                    mant = mant * 10u + (ch - '0');
+                    ++ndmant;
+                }
+            } else {
+                ok = false;
+            }
         }
     }
-    if (neg) v = -v;
-    if (v < 0.0f || v > 100.0f) return false;
-    *out = v;
-    return true;
+    if (!ok || !sawdigits) return parse_pct_generic(s, n, out);
+    if (!sawdot) dp = nd;
+    return pct_finish(s, false, false, false, mant, ndmant, dp, 0u, n, out);
 }
 
 // netlink Percentage2u32: float32 arithmetic, amd64 float→uint32 (via int64, truncate).

@@ -1,0 +1,8 @@
+# r02ag: table powers of ten in the percentage tail
+set -euo pipefail
+O=gpurun_out/r02ag; mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests/test_parity_gpu.py -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+timeout -k 10 250 python -u tools/ablate.py --pods 1000000 --reps 20 --masks none --env KDTN_PD_ONLY=0,1,2,4,12 > $O/pd_1m.json 2>&1
+timeout -k 10 200 python -u tools/ablate.py --pods 125000 --reps 30 --masks none --env KDTN_PD_ONLY=0,1,2,4,12 > $O/pd_125k.json 2>&1
+grep "PD_ONLY\|pdict" $O/pd_*.json
