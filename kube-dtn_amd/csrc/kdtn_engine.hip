@@ -749,6 +749,7 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
             if (sub == 4) k_kdict_flags<4, false><<<nblocks(nk, BLOCK * 4), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
             else if (sub == 2) k_kdict_flags<2, false><<<nblocks(nk, BLOCK * 2), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
             else if (sub == 8) k_kdict_flags<1, true><<<nblocks(nk), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
+            else if (sub == 16) k_kdict_flags_ws<<<nblocks(nk), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
             else
 #endif
             k_kdict_flags<1, false><<<nblocks(nk), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);

@@ -279,6 +279,53 @@ __global__ void __launch_bounds__(BLOCK) k_kdict_flags(const uint8_t* bytes, con
     }
 }
 template __global__ void k_kdict_flags<1, false>(const uint8_t*, const uint32_t*, uint32_t, uint32_t, uint32_t*, uint32_t, uint32_t*);
+
+// Wave-staged form: the wave's 64 strings are contiguous in the arena, so the wave loads their
+// span once with 16-B coalesced loads into its LDS slot (one 128-B line per 8 lanes instead of
+// seven unaligned dword loads per lane touching ~10 lines each) and every lane reads its
+// seven window dwords from LDS. A span over KD_WS_BYTES (long strings) reads global memory.
+constexpr int KD_WS_BYTES = 2048;
+__global__ void __launch_bounds__(BLOCK) k_kdict_flags_ws(const uint8_t* bytes, const uint32_t* offs, uint32_t first,
+                                                          uint32_t n, uint32_t* kbits, uint32_t kb_words,
+                                                          uint32_t* special) {
+    __shared__ uint4 stage[BLOCK / 64][KD_WS_BYTES / 16];
+    const uint32_t i = first + blockIdx.x * BLOCK + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    uint4* st = stage[threadIdx.x >> 6];
+    const uint32_t ic = i < n ? i : n;                 // offs[n] exists
+    const uint32_t b = offs[ic];
+    const uint32_t len = (i < n ? offs[ic + 1] : b) - b;
+    const uint32_t base = (uint32_t)__shfl((int)b, 0, 64) & ~15u;
+    const uint32_t end = (uint32_t)__shfl((int)b, 63, 64) + 28u;     // the last lane's 7-dword window
+    const uint32_t n16 = (end - base + 15u) >> 4;
+    uint32_t d[7];
+    if (n16 <= (uint32_t)(KD_WS_BYTES / 16)) {                       // wave-uniform
+        const uint4* src = reinterpret_cast<const uint4*>(bytes + base);   // arena has 64 B slack
+        for (uint32_t w = lane; w < n16; w += 64) st[w] = src[w];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t* lw = reinterpret_cast<const uint32_t*>(st) + (((b & ~3u) - base) >> 2);
+#pragma unroll
+        for (int k = 0; k < 7; ++k) d[k] = lw[k];
+    } else {
+        const uint32_t* p = reinterpret_cast<const uint32_t*>(bytes + (b & ~3u));
+#pragma unroll
+        for (int k = 0; k < 7; ++k) d[k] = p[k];
+    }
+    const uint32_t sh = (b & 3u) * 8u;
+    uint32_t w[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) w[k] = sh ? (d[k] >> sh) | (d[k + 1] << (32u - sh)) : d[k];
+    const uint32_t f = i < n ? kdict_bits(bytes, b, len, w, i, special) : 0u;
+    const uint32_t w0 = (i - lane) >> 5;                   // first word of this wave
+#pragma unroll
+    for (int k = 0; k < KB_NSETS; ++k) {
+        const uint64_t m = __ballot((f >> k) & 1u);
+        if (w0 < kb_words && (lane == 0 || lane == 32))
+            kbits[(size_t)k * kb_words + w0 + (lane >> 5)] = lane ? (uint32_t)(m >> 32) : (uint32_t)m;
+    }
+}
 #if KDTN_PROFILING
 template __global__ void k_kdict_flags<1, true>(const uint8_t*, const uint32_t*, uint32_t, uint32_t, uint32_t*, uint32_t, uint32_t*);
 template __global__ void k_kdict_flags<2, false>(const uint8_t*, const uint32_t*, uint32_t, uint32_t, uint32_t*, uint32_t, uint32_t*);
