@@ -48,7 +48,7 @@ KD_INLINE uint64_t duration_unit(const uint8_t* u, uint32_t n) {
     return 0;
 }
 
-KD_INLINE bool parse_duration_generic(const uint8_t* s, uint32_t n, uint32_t* out_us) {
+KD_INLINE bool parse_duration_us(const uint8_t* s, uint32_t n, uint32_t* out_us) {
     *out_us = 0;
     if (n == 0) return true;  // "" → 0, nil
     const uint64_t TOP = 1ull << 63;
@@ -112,69 +112,6 @@ KD_INLINE bool parse_duration_generic(const uint8_t* s, uint32_t n, uint32_t* ou
     return true;
 }
 
-// ParseDuration of one unsigned component of at most 16 bytes ([digits][.digits]unit): the
-// bytes are loaded at once and scanned by a fully unrolled, predicated loop (the unit's last
-// three bytes kept in registers); signs, several components, "0" and anything unusual take
-// the generic parser. Up to 15 digits cannot overflow before the unit multiply, whose
-// checks are the generic ones.
-KD_INLINE bool parse_duration_us(const uint8_t* s, uint32_t n, uint32_t* out_us) {
-    if (n == 0 || n > 16) return parse_duration_generic(s, n, out_us);
-    uint32_t c[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) c[k] = (uint32_t)k < n ? s[k] : 0u;
-    int phase = 0;                         // 0 integer digits, 1 fraction digits, 2 unit
-    bool ok = true, pre = false, post = false;
-    uint64_t v = 0, f = 0;
-    int nfrac = 0;
-    uint32_t us = n, u0 = 0, u1 = 0, u2 = 0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        if ((uint32_t)k < n) {
-            const uint32_t ch = c[k];
-            const bool dig = ch - '0' <= 9u;
-            if (phase == 2) {
-                ok &= !(dig || ch == '.');          // a second component
-            } else if (dig) {
-                if (phase == 0) {
-                    v = v * 10u + (ch - '0');
-                    pre = true;
-                } else {
-                    f = f * 10u + (ch - '0');
-                    ++nfrac;
-                    post = true;
-                }
-            } else if (ch == '.' && phase == 0) {
-                phase = 1;
-            } else {
-                ok &= ch != '.' && ch != '+' && ch != '-';
-                phase = 2;
-                us = (uint32_t)k;
-            }
-            u2 = u1;
-            u1 = u0;
-            u0 = ch;
-        }
-    }
-    const uint32_t ulen = n - us;
-    if (!ok || !(pre || post) || ulen == 0 || ulen > 3) return parse_duration_generic(s, n, out_us);
-    *out_us = 0;
-    uint64_t unit = 0;                                   // duration_unit over the last bytes
-    if (ulen == 1) unit = u0 == 's' ? 1000000000ull : u0 == 'm' ? 60000000000ull : u0 == 'h' ? 3600000000000ull : 0;
-    else if (ulen == 2 && u0 == 's') unit = u1 == 'n' ? 1ull : u1 == 'u' ? 1000ull : u1 == 'm' ? 1000000ull : 0;
-    else if (ulen == 3 && u0 == 's' && ((u2 == 0xC2 && u1 == 0xB5) || (u2 == 0xCE && u1 == 0xBC))) unit = 1000ull;
-    if (unit == 0) return false;
-    const uint64_t TOP = 1ull << 63;
-    if (v > TOP / unit) return false;
-    v *= unit;
-    if (f > 0) {
-        const double fr = __dmul_rn((double)f, __ddiv_rn((double)unit, pow10_exact(nfrac)));
-        v += (uint64_t)fr;
-        if (v > TOP) return false;
-    }
-    if (v > TOP - 1) return false;
-    *out_us = (uint32_t)((int64_t)v / 1000);
-    return true;
-}
 
 // ------------------------------------------------------------------------------------
 // strconv.ParseFloat(s, 32) restricted to what ParseFloatPercentage can accept.
