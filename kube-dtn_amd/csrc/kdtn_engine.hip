@@ -84,7 +84,7 @@ struct kdtn_ctx {
     DevBuf v_node, v_vni, v_netns, v_ents, v_slots, v_table;
     uint32_t V = 0, vni_mask = 0;
     // kdtn_epoch_vni_apply: ops, snapshot marks, the new map's table, arrays and scan partials
-    DevBuf vx_ops, vx_dead, vx_slots, vx_node, vx_vni, vx_netns, vx_part;
+    DevBuf vx_ops, vx_dead, vx_slots, vx_node, vx_vni, vx_netns, vx_part, vx_cut;
     bool vres_ok = false;          // v_node/v_vni/v_netns hold a map usable as KDTN_VNI_RESIDENT
     uint32_t vres_n = 0, vres_D = 0;
     // pods
@@ -597,7 +597,8 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->j_olist, &c->j_ccnt, &c->j_coff, &c->j_vlist, &c->sh_keep, &c->sh_kreal,
                       &c->sh_kdes, &c->sh_tidx, &c->sh_roff64, &c->sh_noff64, &c->sh_doc, &c->sh_ns,
                       &c->sh_name, &c->sh_src, &c->sh_netns, &c->sh_flags, &c->sh_roff, &c->sh_noff,
-                      &c->sh_des.buf, &c->sh_real.buf};
+                      &c->sh_des.buf, &c->sh_real.buf, &c->vx_ops, &c->vx_dead, &c->vx_slots, &c->vx_node,
+                      &c->vx_vni, &c->vx_netns, &c->vx_part, &c->vx_cut};
     for (DevBuf* b : bufs) release(*b);
     for (int i = 0; i <= kMaxTimers; ++i)
         if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
@@ -1939,7 +1940,15 @@ int kdtn_epoch_vni_apply(kdtn_ctx* c, kdtn_vni_state* out) {
     VniOpsIn f{ReachIn{dp<uint32_t>(c->del_off), dp<uint4>(c->del_res), dp<uint32_t>(c->add_off), dp<uint4>(c->add_res),
                        dp<uint2>(c->add_qdisc), dp<uint32_t>(c->upd_off), dp<uint4>(c->upd_res), c->T, 0u},
                dp<uint32_t>(c->t_src), dp<uint32_t>(c->t_netns), dp<uint4>(c->pods), nd, na};
-    if (c->T) k_vni_ops<<<nblocks(c->T), BLOCK, 0, s>>>(f, ops);
+    TRY(ensure(c->vx_cut, (size_t)c->T * 8 + 8));
+    uint32_t* cut = dp<uint32_t>(c->vx_cut);
+    if (c->T) {
+        HIP_TRY(hipMemsetAsync(cut, 0xFF, (size_t)c->T * 8, s));
+        if (nd + na) {
+            k_vni_cuts<<<nblocks((uint64_t)nd + na), BLOCK, 0, s>>>(f, cut);
+            k_vni_ops<<<nblocks((uint64_t)nd + na), BLOCK, 0, s>>>(f, cut, ops);
+        }
+    }
     const uint4* ents = dp<uint4>(c->v_ents);
     uint8_t* dead = dp<uint8_t>(c->vx_dead);
     if (V) {                                          // the run built the snapshot table

@@ -346,7 +346,8 @@ struct VniOpsIn {
 // one op per del entry (slot e) and two per add entry (slots n_del + 2e, + 1):
 // {node, vni, net_ns, kind} with kind VOP_NONE / VOP_DEL / VOP_ADD
 enum : uint32_t { VOP_NONE = 0, VOP_DEL = 1, VOP_ADD = 2 };
-__global__ void k_vni_ops(VniOpsIn f, uint4* ops);
+__global__ void k_vni_cuts(VniOpsIn f, uint32_t* cut);
+__global__ void k_vni_ops(VniOpsIn f, const uint32_t* cut, uint4* ops);
 __global__ void k_vni_shadow(const uint4* ents, uint32_t n_ents, const uint32_t* slots, uint32_t mask, uint8_t* dead);
 __global__ void k_vni_del(const uint4* ops, uint32_t n_del, const uint4* ents, const uint32_t* slots, uint32_t mask,
                           uint8_t* dead);

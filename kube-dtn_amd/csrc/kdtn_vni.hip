@@ -9,8 +9,8 @@
 // Deterministic order (the reference's is goroutine order): every delete first, then every
 // add; per key the first add in (topology, add-list, local-before-remote) order wins.
 //
-// Kernels: k_vni_ops (one thread per topology: RPC-order reach as k_reach, one op slot per
-// del entry and two per add entry), k_vni_shadow / k_vni_del (snapshot entries that are not,
+// Kernels: k_vni_cuts / k_vni_ops (entry-parallel: where each topology's RPC sequence stops,
+// then one op slot per del entry and two per add entry), k_vni_shadow / k_vni_del (snapshot entries that are not,
 // or no longer, in the map: shadowed duplicates, deleted keys), then the
 // new map as a first-wins table over [add ops, surviving snapshot entries] (k_vni_insert)
 // and its visible entries compacted in that order (k_vni_vis_count / k_scan_top /
@@ -19,39 +19,62 @@
 
 namespace kdtn {
 
-__global__ void __launch_bounds__(BLOCK) k_vni_ops(VniOpsIn f, uint4* ops) {
-    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
-    if (t >= f.r.T) return;
-    const uint32_t src = f.t_src[t], netns = f.t_netns[t];
-    const uint4 none = make_uint4(0u, 0u, 0u, VOP_NONE);
-    bool ok = true;
-    for (uint32_t e = f.r.del_off[t], e1 = f.r.del_off[t + 1]; e < e1; ++e) {
-        uint4 op = none;
-        if (ok) {
-            const uint4 r = f.r.del_res[e];
-            if ((r.w >> 8) & 0xFFu) ok = false;                              // MakeVeth error :470-474
-            else if ((r.w >> 16) & 0xFFu) op = make_uint4(src, r.y, 0u, VOP_DEL);   // vni_hit :484-487
-        }
-        ops[e] = op;
+// topology of entry e: offs[t] <= e < offs[t + 1] (upper bound over the T + 1 offsets)
+KD_INLINE uint32_t entry_topo(const uint32_t* offs, uint32_t T, uint32_t e) {
+    uint32_t lo = 0, hi = T;                           // offs[lo] <= e < offs[hi]
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (offs[mid] <= e) lo = mid;
+        else hi = mid;
     }
-    uint4* aops = ops + f.n_del;
-    for (uint32_t e = f.r.add_off[t], e1 = f.r.add_off[t + 1]; e < e1; ++e) {
+    return lo;
+}
+
+// Where each topology's RPC sequence stops (reach rule of k_reach, entry-parallel so a hub
+// topology's thousands of entries are not walked by one thread): cut[2t] = the first DelLinks
+// entry with a MakeVeth error, cut[2t + 1] = the first AddLinks entry not reached (a failing
+// entry, or the one after a rejected RemotePod). 0xFFFFFFFF = none (memset).
+__global__ void __launch_bounds__(BLOCK) k_vni_cuts(VniOpsIn f, uint32_t* cut) {
+    const uint32_t x = blockIdx.x * BLOCK + threadIdx.x;
+    if (x < f.n_del) {
+        if ((f.r.del_res[x].w >> 8) & 0xFFu) atomicMin(&cut[2 * entry_topo(f.r.del_off, f.r.T, x)], x);
+    } else if (x < f.n_del + f.n_add) {
+        const uint32_t e = x - f.n_del;
+        const uint4 r = f.r.add_res[e];
+        uint32_t c = 0xFFFFFFFFu;
+        if (add_fails(r, qdisc_err(f.r.add_qdisc, e))) c = e;
+        else if ((r.w & 0xFFu) == KDTN_KIND_CROSS_NODE && (r.w >> 24)) c = e + 1;   // remote Update failed
+        if (c != 0xFFFFFFFFu) atomicMin(&cut[2 * entry_topo(f.r.add_off, f.r.T, e) + 1], c);
+    }
+}
+
+// One thread per entry: a del entry before its topology's del cut deletes on a vni_hit; an
+// add entry of a topology whose dels all succeeded, before the add cut, stores (vni, local
+// netns) on the local node (cross-node, physical) and, cross-node without remote_err,
+// (vni, peer netns) on the peer's node.
+__global__ void __launch_bounds__(BLOCK) k_vni_ops(VniOpsIn f, const uint32_t* cut, uint4* ops) {
+    const uint32_t x = blockIdx.x * BLOCK + threadIdx.x;
+    const uint4 none = make_uint4(0u, 0u, 0u, VOP_NONE);
+    if (x < f.n_del) {
+        const uint32_t t = entry_topo(f.r.del_off, f.r.T, x);
+        const uint4 r = f.r.del_res[x];
+        uint4 op = none;
+        if (x < cut[2 * t] && ((r.w >> 16) & 0xFFu))                       // vni_hit :484-487
+            op = make_uint4(f.t_src[t], r.y, 0u, VOP_DEL);
+        ops[x] = op;
+    } else if (x < f.n_del + f.n_add) {
+        const uint32_t e = x - f.n_del;
+        const uint32_t t = entry_topo(f.r.add_off, f.r.T, e);
         uint4 lo = none, rm = none;
-        if (ok) {
+        if (cut[2 * t] == 0xFFFFFFFFu && e < cut[2 * t + 1]) {
             const uint4 r = f.r.add_res[e];
-            const uint32_t qe = qdisc_err(f.r.add_qdisc, e);
-            if (add_fails(r, qe)) {
-                ok = false;
-            } else {
-                const uint32_t kind = r.w & 0xFFu;
-                if (kind == KDTN_KIND_CROSS_NODE || kind == KDTN_KIND_PHYSICAL)
-                    lo = make_uint4(src, r.y, netns, VOP_ADD);                // :440 / :192
-                if (kind == KDTN_KIND_CROSS_NODE) {
-                    if (r.w >> 24) ok = false;                                 // remote Update failed
-                    else rm = make_uint4(r.z, r.y, f.pods[r.x].w & 0x7FFFFFFFu, VOP_ADD);   // peer node :192
-                }
-            }
+            const uint32_t kind = r.w & 0xFFu;
+            if (kind == KDTN_KIND_CROSS_NODE || kind == KDTN_KIND_PHYSICAL)
+                lo = make_uint4(f.t_src[t], r.y, f.t_netns[t], VOP_ADD);       // :440 / :192
+            if (kind == KDTN_KIND_CROSS_NODE && (r.w >> 24) == 0)
+                rm = make_uint4(r.z, r.y, f.pods[r.x].w & 0x7FFFFFFFu, VOP_ADD);   // peer node :192
         }
+        uint4* aops = ops + f.n_del;
         aops[2 * (size_t)e] = lo;
         aops[2 * (size_t)e + 1] = rm;
     }
