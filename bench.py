@@ -264,11 +264,13 @@ def ingest_stage(eng, inp, steps: int, reps: int = 5, cpu_sample_pods: int = 20_
 def pmc_traffic(config: int, links: int):
     """HBM bytes per k_reconcile launch (+ k_place_scan / k_place when the summary has them)
     from the newest committed PMC summary of the same
-    workload (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from separate
+    workload (profiles/*pmc_traffic*.json, written by tools/pmc_traffic.py from separate
     FETCH_SIZE / WRITE_SIZE rocprofv3 passes, gfx950 correction applied), else None."""
     import glob
     best = None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json"))):
+    # newest tag last: r02 < r02m < r02zp < r02zp2 ('_' sorts as a space)
+    files = glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic*.json"))
+    for f in sorted(files, key=lambda f: os.path.basename(f).replace("_", " ")):
         with open(f) as fh:
             d = json.load(fh)
         if d.get("config", 2) != config or abs(d.get("links_per_gpu", 0) - links) > 0.01 * links:
