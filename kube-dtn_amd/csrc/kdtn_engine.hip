@@ -102,7 +102,7 @@ struct kdtn_ctx {
     uint64_t w_bytes = 0;
     bool encoded = false;
     // RemotePod fan-out
-    DevBuf f_mark, f_send, f_node_idx, f_nodes, f_counts, f_base, f_part, f_idx, f_reach_upd;
+    DevBuf f_mark, f_send, f_node_idx, f_nodes, f_counts, f_base, f_part, f_idx, f_reach_upd, f_cut;
     uint32_t f_stamp = 0;
     // tc argv
     DevBuf tc_size, tc_off, tc_part, tc_arena;
@@ -486,7 +486,17 @@ int run_reach(kdtn_ctx* c, uint32_t* mark, uint32_t stamp) {
     TRY(ensure(c->f_reach_upd, (size_t)nu + 16));
     ReachIn r{dp<uint32_t>(c->del_off), dp<uint4>(c->del_res), dp<uint32_t>(c->add_off), dp<uint4>(c->add_res),
               dp<uint2>(c->add_qdisc), dp<uint32_t>(c->upd_off), dp<uint4>(c->upd_res), c->T, stamp};
-    if (c->T) k_reach<<<nblocks(c->T), BLOCK, 0, c->stream>>>(r, mark, dp<uint8_t>(c->f_send), dp<uint8_t>(c->f_reach_upd));
+    const uint32_t nd = c->h_misc[1];
+    TRY(ensure(c->f_cut, (size_t)c->T * 12 + 12));
+    uint32_t* cut = dp<uint32_t>(c->f_cut);
+    if (c->T) {
+        HIP_TRY(hipMemsetAsync(cut, 0xFF, (size_t)c->T * 12, c->stream));
+        if ((uint64_t)nd + na + nu)
+            k_reach_cuts<<<nblocks((uint64_t)nd + na + nu), BLOCK, 0, c->stream>>>(r, nd, na, nu, cut);
+        if ((uint64_t)na + nu)
+            k_reach<<<nblocks((uint64_t)na + nu), BLOCK, 0, c->stream>>>(r, na, nu, cut, mark, dp<uint8_t>(c->f_send),
+                                                                         dp<uint8_t>(c->f_reach_upd));
+    }
     return KDTN_OK;
 }
 
@@ -598,7 +608,7 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->sh_kdes, &c->sh_tidx, &c->sh_roff64, &c->sh_noff64, &c->sh_doc, &c->sh_ns,
                       &c->sh_name, &c->sh_src, &c->sh_netns, &c->sh_flags, &c->sh_roff, &c->sh_noff,
                       &c->sh_des.buf, &c->sh_real.buf, &c->vx_ops, &c->vx_dead, &c->vx_slots, &c->vx_node,
-                      &c->vx_vni, &c->vx_netns, &c->vx_part, &c->vx_cut};
+                      &c->vx_vni, &c->vx_netns, &c->vx_part, &c->vx_cut, &c->f_cut};
     for (DevBuf* b : bufs) release(*b);
     for (int i = 0; i <= kMaxTimers; ++i)
         if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);

@@ -9,50 +9,59 @@
 // stage groups them per destination daemon, so a caller can send one batch per node:
 // nodes in ascending kdict-id order of their src_ip, entries of a node in add-list order.
 //
-// Kernels: k_reach (one thread per topology: RPC-order first-error scan, marks senders and
-// their nodes in a stamped D-sized table), k_fan_nodes_* (compaction of marked node ids → dense
+// Kernels: k_reach_cuts / k_reach (entry-parallel RPC-order first-error rule, marks senders
+// and their nodes in a stamped D-sized table), k_fan_nodes_* (compaction of marked node ids → dense
 // node index), k_fan_count / k_fan_scatter (single-wave workgroups over chunks of 4,096
 // entries: LDS histogram, node-major scan of the (node, chunk) counts, stable scatter).
 #include "kdtn_kernels.h"
 
 namespace kdtn {
 
-// Which entries the daemons reach (include/kdtn.h): one thread per topology walks its
-// DelLinks, AddLinks, UpdateLinks entries in RPC order (topology_controller.go:93-116) and
-// stops at the first failing link (handler.go:601-607, 622-628, 644-662). Writes per add
-// entry REACH_ON | REACH_SEND, per update entry REACH_ON, and (mark != nullptr) stamps the
-// destination daemon of every RemotePod sent.
-__global__ void __launch_bounds__(BLOCK) k_reach(ReachIn f, uint32_t* mark, uint8_t* reach_add, uint8_t* reach_upd) {
-    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
-    if (t >= f.T) return;
-    bool ok = true;
-    for (uint32_t e = f.del_off[t], e1 = f.del_off[t + 1]; e < e1 && ok; ++e)
-        if ((f.del_res[e].w >> 8) & 0xFFu) ok = false;                      // delLink error
-    for (uint32_t e = f.add_off[t], e1 = f.add_off[t + 1]; e < e1; ++e) {
+// Which entries the daemons reach (include/kdtn.h): Reconcile sends each topology's
+// DelLinks, AddLinks, UpdateLinks in that order (topology_controller.go:93-116) and each
+// handler stops at its first failing link (handler.go:601-607, 622-628, 644-662). Entry-
+// parallel in two launches, so a hub topology's thousands of entries are not walked by one
+// thread: k_reach_cuts records per topology the first failing del, the first add that stops
+// the batch (a failing link, or a cross-node link whose RemotePod the peer rejects — both
+// reached themselves) and the first failing update (one atomicMin per such entry into
+// cut[3t + list], 0xFFFFFFFF = none); k_reach then writes per add entry REACH_ON |
+// REACH_SEND, per update entry REACH_ON, and (mark != nullptr) stamps the destination
+// daemon of every RemotePod sent.
+__global__ void __launch_bounds__(BLOCK) k_reach_cuts(ReachIn f, uint32_t nd, uint32_t na, uint32_t nu, uint32_t* cut) {
+    const uint32_t x = blockIdx.x * BLOCK + threadIdx.x;
+    if (x < nd) {
+        if ((f.del_res[x].w >> 8) & 0xFFu) atomicMin(&cut[3 * entry_topo(f.del_off, f.T, x)], x);   // delLink error
+    } else if (x < nd + na) {
+        const uint32_t e = x - nd;
+        const uint4 r = f.add_res[e];
+        if (add_fails(r, qdisc_err(f.add_qdisc, e)) || (r.w >> 24))          // or remote Update failed
+            atomicMin(&cut[3 * entry_topo(f.add_off, f.T, e) + 1], e);
+    } else if (x < nd + na + nu) {
+        const uint32_t e = x - nd - na;
+        if ((f.upd_res[e].w >> 8) & 0xFFu) atomicMin(&cut[3 * entry_topo(f.upd_off, f.T, e) + 2], e);   // MakeVeth / MakeQdiscs
+    }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_reach(ReachIn f, uint32_t na, uint32_t nu, const uint32_t* cut,
+                                                 uint32_t* mark, uint8_t* reach_add, uint8_t* reach_upd) {
+    const uint32_t x = blockIdx.x * BLOCK + threadIdx.x;
+    if (x < na) {
+        const uint32_t t = entry_topo(f.add_off, f.T, x);
         uint8_t a = 0;
-        if (ok) {
+        if (cut[3 * t] == 0xFFFFFFFFu && x <= cut[3 * t + 1]) {
             a = REACH_ON;
-            const uint4 r = f.add_res[e];
-            const uint32_t qe = qdisc_err(f.add_qdisc, e);
-            if (add_fails(r, qe)) {
-                ok = false;
-            } else {
-                if (sends_remote(r, qe)) {
-                    a |= REACH_SEND;
-                    if (mark) mark[r.z] = f.stamp;
-                }
-                if (r.w >> 24) ok = false;                                  // remote Update failed
+            const uint4 r = f.add_res[x];
+            const uint32_t qe = qdisc_err(f.add_qdisc, x);
+            if (!add_fails(r, qe) && sends_remote(r, qe)) {
+                a |= REACH_SEND;
+                if (mark) mark[r.z] = f.stamp;
             }
         }
-        reach_add[e] = a;
-    }
-    for (uint32_t e = f.upd_off[t], e1 = f.upd_off[t + 1]; e < e1; ++e) {
-        uint8_t a = 0;
-        if (ok) {
-            a = REACH_ON;
-            if ((f.upd_res[e].w >> 8) & 0xFFu) ok = false;                  // MakeVeth / MakeQdiscs error
-        }
-        reach_upd[e] = a;
+        reach_add[x] = a;
+    } else if (x < na + nu) {
+        const uint32_t e = x - na;
+        const uint32_t t = entry_topo(f.upd_off, f.T, e);
+        reach_upd[e] = (cut[3 * t] == 0xFFFFFFFFu && cut[3 * t + 1] == 0xFFFFFFFFu && e <= cut[3 * t + 2]) ? REACH_ON : 0;
     }
 }
 

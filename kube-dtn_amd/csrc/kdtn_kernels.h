@@ -322,6 +322,17 @@ KD_INLINE bool add_fails(uint4 r, uint32_t qerr) {
     return (kind == KDTN_KIND_SAME_NODE || kind == KDTN_KIND_CROSS_NODE || kind == KDTN_KIND_PHYSICAL) && qerr != 0;
 }
 KD_INLINE uint32_t qdisc_err(const uint2* q, uint32_t e) { return (q[(size_t)e * 9 + 8].y >> 16) & 0xFFu; }
+// topology of entry e: offs[t] <= e < offs[t + 1] (upper bound over the T + 1 offsets)
+KD_INLINE uint32_t entry_topo(const uint32_t* offs, uint32_t T, uint32_t e) {
+    uint32_t lo = 0, hi = T;                           // offs[lo] <= e < offs[hi]
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (offs[mid] <= e) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
 enum : uint8_t { REACH_ON = 1, REACH_SEND = 2 };
 struct ReachIn {
     const uint32_t* del_off;
@@ -333,7 +344,9 @@ struct ReachIn {
     const uint4* upd_res;
     uint32_t T, stamp;
 };
-__global__ void k_reach(ReachIn f, uint32_t* mark, uint8_t* reach_add, uint8_t* reach_upd);
+__global__ void k_reach_cuts(ReachIn f, uint32_t nd, uint32_t na, uint32_t nu, uint32_t* cut);
+__global__ void k_reach(ReachIn f, uint32_t na, uint32_t nu, const uint32_t* cut, uint32_t* mark, uint8_t* reach_add,
+                        uint8_t* reach_upd);
 
 // VxlanManager state after the epoch (kdtn_vni.hip; include/kdtn.h kdtn_epoch_vni_apply)
 struct VniOpsIn {

@@ -19,17 +19,6 @@
 
 namespace kdtn {
 
-// topology of entry e: offs[t] <= e < offs[t + 1] (upper bound over the T + 1 offsets)
-KD_INLINE uint32_t entry_topo(const uint32_t* offs, uint32_t T, uint32_t e) {
-    uint32_t lo = 0, hi = T;                           // offs[lo] <= e < offs[hi]
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (offs[mid] <= e) lo = mid;
-        else hi = mid;
-    }
-    return lo;
-}
-
 // Where each topology's RPC sequence stops (reach rule of k_reach, entry-parallel so a hub
 // topology's thousands of entries are not walked by one thread): cut[2t] = the first DelLinks
 // entry with a MakeVeth error, cut[2t + 1] = the first AddLinks entry not reached (a failing
