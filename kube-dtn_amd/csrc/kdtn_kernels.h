@@ -130,22 +130,24 @@ struct DevLinks {
 //           non-empty), so the bulk emission is not software-pipelined and the kernel
 //           targets DIFF_WAVES waves per SIMD; kdtn_epoch_run picks it when M > 0 and N > 0
 //   bit 12: (A/B) bulk loop: the next record's segment search before this record's gathers
+//   bit 14: first bulk record's columns loaded before the gate / count / base phases (product;
+//           A/B vs 515: 0.6164 / 0.6180 ms at 1M pods, 0.0849 / 0.0869 at 125k, 0.1563 / 0.1583 config 4)
 constexpr int VAR_NT_LOAD = 1, VAR_NT_STORE = 2, VAR_NO_QSTORE = 4, VAR_NT_POD = 8, VAR_TRACE = 16,
               VAR_SKIP_POD = 32, VAR_SKIP_PCT = 64, VAR_OCC5 = 128, VAR_OCC6 = 256,
-              VAR_MASK_EMPTY = 512, VAR_NO_PREFIX = 1024, VAR_DIFF = 2048, VAR_DECODE_FIRST = 4096;
+              VAR_MASK_EMPTY = 512, VAR_NO_PREFIX = 1024, VAR_DIFF = 2048, VAR_DECODE_FIRST = 4096, VAR_PREFETCH = 16384;
 constexpr int DIFF_WAVES = 5;
 constexpr int var_waves(int v) {
-    return (v & VAR_OCC6) ? 6 : (v & VAR_OCC5) ? 5 : (v & VAR_DIFF) ? DIFF_WAVES : 1;
+    return (v & VAR_OCC6) ? 6 : (v & VAR_OCC5) ? 5 : (v & VAR_DIFF) ? DIFF_WAVES : (v & VAR_PREFETCH) ? 4 : 1;
 }
 constexpr int TRACE_WORDS = 8;   // entry, topologies loaded, counts done, bases known, end, hw ids,
                                   // CalcDiff window phase A done, phase B done (fast path)
-constexpr int DEFAULT_VARIANT = VAR_NT_LOAD | VAR_NT_STORE | VAR_MASK_EMPTY;   // 515
+constexpr int DEFAULT_VARIANT = VAR_NT_LOAD | VAR_NT_STORE | VAR_MASK_EMPTY | VAR_PREFETCH;   // 16899
 // instantiations of the profiling build (DEFAULT_VARIANT is always instantiated): e.g. 547 / 579
 // / 611 skip the pod-slot / percentage / both gathers, 519 skips the qdisc stores, 531 the
 // trace build of the default
 #define KDTN_PROFILING_VARIANTS(X) X(0) X(1) X(2) X(3) X(4) X(5) X(9) X(11) X(17) X(33) X(65) X(97) \
     X(101) X(113) X(129) X(257) X(513) X(521) X(523) X(529) X(531) X(545) X(547) X(579) X(611) X(519) \
-    X(641) X(643) X(771) X(1025) X(1537) X(2579) X(4611)
+    X(641) X(643) X(771) X(1025) X(1537) X(2579) X(4611) X(515)
 
 struct DevTopos {
     const uint32_t* ns;

@@ -1418,6 +1418,19 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
     const bool fast = tot <= (uint32_t)CAP;
     const bool do_res = out.stages & KDTN_STAGE_RESOLVE;
     const bool do_q = out.stages & KDTN_STAGE_QDISC;
+    // (VAR_PREFETCH) the thread's first bulk record's columns, issued before the gate, count
+    // and base phases (speculatively: the records a shared bulk chunk gives this part)
+    RecCols pre;
+    uint32_t pre_r = 0xFFFFFFFFu;
+    if constexpr ((V & VAR_PREFETCH) != 0 && !kDefer) {
+        const uint32_t per_s = (tot + wk.split - 1) / wk.split;
+        const uint32_t lo_s = min(tot, part * per_s), r = lo_s + tid;
+        if (r < min(tot, lo_s + per_s)) {
+            const bool old = r < no;
+            load_cols<(V & VAR_NT_LOAD) != 0>(old ? O : N, old ? o0 + r : n0 + (r - no), do_res, !old && do_q, pre);
+            pre_r = r;
+        }
+    }
     if (tid < 64) {
         const uint64_t b = __ballot(tid < nt && need_cmp(s, tid));
         if (tid == 0) s.any_cmp = b != 0ull;
@@ -1604,7 +1617,8 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
         }
         Slot cs = decode(rlo + tid);
         RecCols cc;
-        fetch(cs, cc);
+        if (pre_r == rlo + tid && cs.on) cc = pre;
+        else fetch(cs, cc);
         for (uint32_t b = rlo; b < rhi; b += BLOCK) {
             // the next record's segment search (LDS) runs after this record's gathers issue
             Slot nx;

@@ -71,7 +71,8 @@ def test_product_library_reads_no_environment():
     the default k_reconcile instantiation is present (the variants live in the profiling
     build, kube-dtn_amd/prof/libkdtn_prof.so)."""
     data = open(engine.LIB_PATH, "rb").read()
-    for knob in (b"KDTN_VARIANT", b"KDTN_KD_SUB", b"KDTN_JS_VARIANT"):
+    for knob in (b"KDTN_VARIANT", b"KDTN_KD_SUB", b"KDTN_JS_VARIANT", b"KDTN_SPLIT", b"KDTN_PD_SPLIT",
+                 b"KDTN_PD_ONLY"):
         assert knob not in data, knob
     names = set(re.findall(rb"_ZN4kdtn11k_reconcileILi(\d+)E", data))
-    assert names == {b"515", b"2563"}, names      # default and comparison-heavy builds
+    assert names == {b"16899", b"18947"}, names   # default and comparison-heavy builds
