@@ -84,7 +84,7 @@ struct kdtn_ctx {
     DevBuf v_node, v_vni, v_netns, v_ents, v_slots, v_table;
     uint32_t V = 0, vni_mask = 0;
     // kdtn_epoch_vni_apply: ops, snapshot marks, the new map's table, arrays and scan partials
-    DevBuf vx_ops, vx_dead, vx_slots, vx_node, vx_vni, vx_netns, vx_part, vx_cut;
+    DevBuf vx_ops, vx_dead, vx_slots, vx_node, vx_vni, vx_netns, vx_part, vx_cut, vx_vis;
     bool vres_ok = false;          // v_node/v_vni/v_netns hold a map usable as KDTN_VNI_RESIDENT
     uint32_t vres_n = 0, vres_D = 0;
     // pods
@@ -608,7 +608,7 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->sh_kdes, &c->sh_tidx, &c->sh_roff64, &c->sh_noff64, &c->sh_doc, &c->sh_ns,
                       &c->sh_name, &c->sh_src, &c->sh_netns, &c->sh_flags, &c->sh_roff, &c->sh_noff,
                       &c->sh_des.buf, &c->sh_real.buf, &c->vx_ops, &c->vx_dead, &c->vx_slots, &c->vx_node,
-                      &c->vx_vni, &c->vx_netns, &c->vx_part, &c->vx_cut, &c->f_cut};
+                      &c->vx_vni, &c->vx_netns, &c->vx_part, &c->vx_cut, &c->f_cut, &c->vx_vis};
     for (DevBuf* b : bufs) release(*b);
     for (int i = 0; i <= kMaxTimers; ++i)
         if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
@@ -1976,13 +1976,16 @@ int kdtn_epoch_vni_apply(kdtn_ctx* c, kdtn_vni_state* out) {
     TRY(ensure(c->vx_node, (size_t)n_ext * 4));
     TRY(ensure(c->vx_vni, (size_t)n_ext * 4));
     TRY(ensure(c->vx_netns, (size_t)n_ext * 4));
+    TRY(ensure(c->vx_vis, (size_t)n_ext + 16));
     uint32_t* n_out = dp<uint32_t>(c->misc) + MISC_VNI_N;
     HIP_TRY(hipMemsetAsync(n_out, 0, 4, s));
     if (n_ext) {
         k_vni_insert<<<nblocks(n_ext), BLOCK, 0, s>>>(aops, (uint32_t)n_ops, ents, dead, V, slots, mask);
-        k_vni_vis_count<<<nb, BLOCK, 0, s>>>(aops, (uint32_t)n_ops, ents, dead, V, slots, mask, dp<uint64_t>(c->vx_part));
+        uint8_t* vis = dp<uint8_t>(c->vx_vis);
+        k_vni_vis_count<<<nb, BLOCK, 0, s>>>(aops, (uint32_t)n_ops, ents, dead, V, slots, mask, vis,
+                                            dp<uint64_t>(c->vx_part));
         k_scan_top<<<1, BLOCK, 0, s>>>(dp<uint64_t>(c->vx_part), nb);
-        k_vni_vis_write<<<nb, BLOCK, 0, s>>>(aops, (uint32_t)n_ops, ents, dead, V, slots, mask, dp<uint64_t>(c->vx_part),
+        k_vni_vis_write<<<nb, BLOCK, 0, s>>>(aops, (uint32_t)n_ops, ents, dead, V, vis, dp<uint64_t>(c->vx_part),
                                             dp<uint32_t>(c->vx_node), dp<int32_t>(c->vx_vni), dp<uint32_t>(c->vx_netns),
                                             n_out);
     }

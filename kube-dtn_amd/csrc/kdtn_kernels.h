@@ -369,10 +369,10 @@ __global__ void k_vni_del(const uint4* ops, uint32_t n_del, const uint4* ents, c
 __global__ void k_vni_insert(const uint4* add_ops, uint32_t n_ops, const uint4* ents, const uint8_t* dead, uint32_t n_ents,
                              uint32_t* slots, uint32_t mask);
 __global__ void k_vni_vis_count(const uint4* add_ops, uint32_t n_ops, const uint4* ents, const uint8_t* dead,
-                                uint32_t n_ents, const uint32_t* slots, uint32_t mask, uint64_t* part);
+                                uint32_t n_ents, const uint32_t* slots, uint32_t mask, uint8_t* vis, uint64_t* part);
 __global__ void k_vni_vis_write(const uint4* add_ops, uint32_t n_ops, const uint4* ents, const uint8_t* dead,
-                                uint32_t n_ents, const uint32_t* slots, uint32_t mask, const uint64_t* part,
-                                uint32_t* node, int32_t* vni, uint32_t* net_ns, uint32_t* n_out);
+                                uint32_t n_ents, const uint8_t* vis, const uint64_t* part, uint32_t* node,
+                                int32_t* vni, uint32_t* net_ns, uint32_t* n_out);
 __global__ void k_fan_nodes_count(const uint32_t* mark, uint32_t nd, uint32_t stamp, uint64_t* part);
 __global__ void k_fan_nodes_write(const uint32_t* mark, uint32_t nd, uint32_t stamp, const uint64_t* part,
                                   uint32_t* node_idx, uint32_t* nodes, uint32_t* n_nodes);

@@ -143,24 +143,30 @@ KD_INLINE bool ext_visible(const uint4* add_ops, uint32_t n_ops, const uint4* en
     }
 }
 
+// Visible entries per scan chunk; each entry's visibility is kept as a byte (vis) for the
+// write pass, so the table is probed once per entry.
 __global__ void __launch_bounds__(BLOCK) k_vni_vis_count(const uint4* add_ops, uint32_t n_ops, const uint4* ents,
                                                          const uint8_t* dead, uint32_t n_ents, const uint32_t* slots,
-                                                         uint32_t mask, uint64_t* part) {
+                                                         uint32_t mask, uint8_t* vis, uint64_t* part) {
     __shared__ uint64_t sh[BLOCK / 64];
     const uint32_t b0 = blockIdx.x * SCAN_CHUNK + threadIdx.x * 4;
     uint64_t v = 0;
     uint4 e;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) v += ext_visible(add_ops, n_ops, ents, dead, n_ents, slots, mask, b0 + k, &e) ? 1u : 0u;
+    for (int k = 0; k < 4; ++k) {
+        const bool m = ext_visible(add_ops, n_ops, ents, dead, n_ents, slots, mask, b0 + k, &e);
+        if (b0 + k < n_ops + n_ents) vis[b0 + k] = m;
+        v += m ? 1u : 0u;
+    }
     uint64_t tot;
     block_exclusive(v, sh, &tot);
     if (threadIdx.x == 0) part[blockIdx.x] = tot;
 }
 
 __global__ void __launch_bounds__(BLOCK) k_vni_vis_write(const uint4* add_ops, uint32_t n_ops, const uint4* ents,
-                                                         const uint8_t* dead, uint32_t n_ents, const uint32_t* slots,
-                                                         uint32_t mask, const uint64_t* part, uint32_t* node,
-                                                         int32_t* vni, uint32_t* net_ns, uint32_t* n_out) {
+                                                         const uint8_t* dead, uint32_t n_ents, const uint8_t* vis,
+                                                         const uint64_t* part, uint32_t* node, int32_t* vni,
+                                                         uint32_t* net_ns, uint32_t* n_out) {
     __shared__ uint64_t sh[BLOCK / 64];
     const uint32_t b0 = blockIdx.x * SCAN_CHUNK + threadIdx.x * 4;
     bool m[4];
@@ -168,7 +174,8 @@ __global__ void __launch_bounds__(BLOCK) k_vni_vis_write(const uint4* add_ops, u
     uint64_t v = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        m[k] = ext_visible(add_ops, n_ops, ents, dead, n_ents, slots, mask, b0 + k, &e[k]);
+        m[k] = b0 + k < n_ops + n_ents && vis[b0 + k];
+        if (m[k]) ext_entry(add_ops, n_ops, ents, dead, b0 + k, &e[k]);
         v += m[k] ? 1u : 0u;
     }
     uint64_t tot;
