@@ -757,13 +757,15 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
 #if KDTN_PROFILING
             int sub = 1;                                               // strings per thread (2, 4: slower)
             if (const char* ev = std::getenv("KDTN_KD_SUB")) sub = std::atoi(ev);
-            if (sub == 4) k_kdict_flags<4, false><<<nblocks(nk, BLOCK * 4), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
-            else if (sub == 2) k_kdict_flags<2, false><<<nblocks(nk, BLOCK * 2), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
-            else if (sub == 8) k_kdict_flags<1, true><<<nblocks(nk), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
+            if (sub == 4) k_kdict_flags<4, false, BLOCK><<<nblocks(nk, BLOCK * 4), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
+            else if (sub == 2) k_kdict_flags<2, false, BLOCK><<<nblocks(nk, BLOCK * 2), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
+            else if (sub == 8) k_kdict_flags<1, true, BLOCK><<<nblocks(nk), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
             else if (sub == 16) k_kdict_flags_ws<<<nblocks(nk), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
+            else if (sub == 64) k_kdict_flags<1, false, 64><<<nblocks(nk, 64), 64, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
+            else if (sub == 1024) k_kdict_flags<1, false, 1024><<<nblocks(nk, 1024), 1024, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
             else
 #endif
-            k_kdict_flags<1, false><<<nblocks(nk), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
+            k_kdict_flags<1, false, BLOCK><<<nblocks(nk), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
         }
     }
     timer_mark(c, "kdict_parse", 2);

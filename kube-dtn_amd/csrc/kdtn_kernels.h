@@ -218,7 +218,7 @@ __global__ void k_place(DevTopos T, const uint32_t* wcount, const uint32_t* wbas
 constexpr int PLACE_SCAN_BLOCK = 1024, PLACE_PER = 8;    // k_place_scan: workgroups per thread per tile
 
 __global__ void k_special_clip(uint32_t* special, uint32_t k0);
-template <int SUB, bool X4>
+template <int SUB, bool X4, int NT>
 __global__ void k_kdict_flags(const uint8_t* bytes, const uint32_t* offs, uint32_t first, uint32_t n,
                               uint32_t* kbits, uint32_t kb_words, uint32_t* special);
 __global__ void k_kdict_flags_ws(const uint8_t* bytes, const uint32_t* offs, uint32_t first, uint32_t n,

@@ -229,15 +229,15 @@ __global__ void k_special_clip(uint32_t* special, uint32_t k0) {
 // the kernel is latency-bound, so a wave keeps SUB strings' round trips in flight at once.
 // Strings [first, n) (first a multiple of 64: every wave writes whole predicate words).
 // X4: the window comes from three 16-B aligned loads (48 bytes) instead of seven dwords.
-template <int SUB, bool X4>
-__global__ void __launch_bounds__(BLOCK) k_kdict_flags(const uint8_t* bytes, const uint32_t* offs,
+template <int SUB, bool X4, int NT>
+__global__ void __launch_bounds__(NT) k_kdict_flags(const uint8_t* bytes, const uint32_t* offs,
                                                        uint32_t first, uint32_t n, uint32_t* kbits,
                                                        uint32_t kb_words, uint32_t* special) {
-    const uint32_t i0 = first + blockIdx.x * BLOCK * SUB + threadIdx.x;
+    const uint32_t i0 = first + blockIdx.x * NT * SUB + threadIdx.x;
     uint32_t b[SUB], len[SUB];
 #pragma unroll
     for (int s = 0; s < SUB; ++s) {
-        const uint32_t i = i0 + s * BLOCK;
+        const uint32_t i = i0 + s * NT;
         const uint32_t ic = i < n ? i : n;                 // offs[n] exists
         b[s] = offs[ic];
         len[s] = (i < n ? offs[ic + 1] : b[s]) - b[s];
@@ -262,7 +262,7 @@ __global__ void __launch_bounds__(BLOCK) k_kdict_flags(const uint8_t* bytes, con
     const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int s = 0; s < SUB; ++s) {
-        const uint32_t i = i0 + s * BLOCK;
+        const uint32_t i = i0 + s * NT;
         const uint32_t sh = (b[s] & 3u) * 8u;
         uint32_t w[6];
 #pragma unroll
@@ -278,7 +278,7 @@ __global__ void __launch_bounds__(BLOCK) k_kdict_flags(const uint8_t* bytes, con
         }
     }
 }
-template __global__ void k_kdict_flags<1, false>(const uint8_t*, const uint32_t*, uint32_t, uint32_t, uint32_t*, uint32_t, uint32_t*);
+template __global__ void k_kdict_flags<1, false, BLOCK>(const uint8_t*, const uint32_t*, uint32_t, uint32_t, uint32_t*, uint32_t, uint32_t*);
 
 #if KDTN_PROFILING
 // (A/B, measured slower: 0.122 vs 0.112 ms at 1M pods, `KDTN_KD_SUB=16`) Wave-staged form:
@@ -328,9 +328,13 @@ __global__ void __launch_bounds__(BLOCK) k_kdict_flags_ws(const uint8_t* bytes, 
             kbits[(size_t)k * kb_words + w0 + (lane >> 5)] = lane ? (uint32_t)(m >> 32) : (uint32_t)m;
     }
 }
-template __global__ void k_kdict_flags<1, true>(const uint8_t*, const uint32_t*, uint32_t, uint32_t, uint32_t*, uint32_t, uint32_t*);
-template __global__ void k_kdict_flags<2, false>(const uint8_t*, const uint32_t*, uint32_t, uint32_t, uint32_t*, uint32_t, uint32_t*);
-template __global__ void k_kdict_flags<4, false>(const uint8_t*, const uint32_t*, uint32_t, uint32_t, uint32_t*, uint32_t, uint32_t*);
+template __global__ void k_kdict_flags<1, true, BLOCK>(const uint8_t*, const uint32_t*, uint32_t, uint32_t, uint32_t*, uint32_t, uint32_t*);
+template __global__ void k_kdict_flags<2, false, BLOCK>(const uint8_t*, const uint32_t*, uint32_t, uint32_t, uint32_t*, uint32_t, uint32_t*);
+template __global__ void k_kdict_flags<4, false, BLOCK>(
+    const uint8_t*, const uint32_t*, uint32_t, uint32_t, uint32_t*, uint32_t, uint32_t*);
+template __global__ void k_kdict_flags<1, false, 64>(
+    const uint8_t*, const uint32_t*, uint32_t, uint32_t, uint32_t*, uint32_t, uint32_t*);
+template __global__ void k_kdict_flags<1, false, 1024>(const uint8_t*, const uint32_t*, uint32_t, uint32_t, uint32_t*, uint32_t, uint32_t*);
 #endif
 
 // One property string's interpretations: WHICH = 7 all three, else one of PD_DUR / PD_PCT /
