@@ -129,6 +129,7 @@ struct kdtn_ctx {
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
     bool pods_imported = false;   // host transport: this epoch's global pod table is in place
+    bool pods_rank_major = true;  // pod table rank-major (uploads) vs document order (sharded ingest)
     // timers: 0 none, 1 k_reconcile (+ placement) only, 2 every stage (kdtn_set_timing)
     int timing = 2;
     hipEvent_t ev[kMaxTimers + 1] = {};
@@ -694,6 +695,7 @@ int kdtn_epoch_upload(kdtn_ctx* c, const kdtn_epoch_in* in) {
     TRY(upload_links(c, c->real, in->realised, D, P, "realised"));
     TRY(upload_links(c, c->des, in->desired, D, P, "desired"));
 
+    c->pods_rank_major = true;
     TRY(prepare_epoch(c, in->vnis, slice, in->realised.n, in->desired.n));
     HIP_TRY(hipStreamSynchronize(c->stream));   // host arrays may be released after return
     c->uploaded = true;
@@ -787,7 +789,7 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         if (c->pod_total) {
             k_pod_direct_scatter<<<nblocks(c->pod_total), BLOCK, 0, s>>>(
                 dp<uint4>(c->pods), c->pod_total, dp<uint32_t>(c->kd_bits) + (size_t)KB_PHYSICAL * c->kb_words,
-                dp<uint4>(c->pod_direct), c->pod_stamp, c->D);
+                dp<uint4>(c->pod_direct), c->pod_stamp, c->D, c->pods_rank_major ? (uint32_t)c->nranks : 1u);
         }
         if (c->V) {
             const size_t vcap = (size_t)c->vni_mask + 1;
@@ -863,7 +865,8 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
             const uint32_t nbp = (uint32_t)std::min<uint64_t>(4 * FP_GRID, (c->T + 4 * BLOCK - 1) / (4 * BLOCK));
             k_pod_verify_prefix<<<nbv + std::max<uint32_t>(nbp, 1), BLOCK, 0, s>>>(
                 dp<uint4>(c->pods), c->pod_total, dp<uint4>(c->pod_direct), c->pod_stamp,
-                dp<unsigned long long>(c->pod_ovf), c->ovf_mask, c->D, T, sync + SYNC_FIRST_PARTIAL_INV, nbv);
+                dp<unsigned long long>(c->pod_ovf), c->ovf_mask, c->D, T, sync + SYNC_FIRST_PARTIAL_INV, nbv,
+                c->pods_rank_major ? (uint32_t)c->nranks : 1u);
             timer_mark(c, "verify_prefix", 2);
         } else {
             k_full_prefix<<<(unsigned)std::min<uint64_t>(FP_GRID, (c->T + 4 * FP_BLOCK - 1) / (4 * FP_BLOCK)), FP_BLOCK, 0, s>>>(
@@ -1752,6 +1755,7 @@ int kdtn_json_ingest_shard(kdtn_ctx* c, const kdtn_vni_table* vnis, uint32_t nsh
     // 3. a rank of nshards with every Topology's pod-status row: pod index = document index
     const uint32_t slice = (Tf + nshards - 1) / nshards;
     c->nranks = (int)nshards;
+    c->pods_rank_major = false;                         // pod index = document index
     c->rank = (int)shard;
     c->T = Ts;
     const kdtn_vni_table none{0, nullptr, nullptr, nullptr};

@@ -234,7 +234,7 @@ __global__ void k_pods_fill(DevTopos T, uint32_t slice, uint32_t rank_base, uint
 __global__ void k_epoch_begin(uint4* sync, uint32_t n16, uint32_t nbz, DevTopos T, uint32_t slice, uint32_t rank_base,
                               uint4* pods);
 __global__ void k_pod_direct_scatter(const uint4* pods, uint32_t total, const uint32_t* phys_bits,
-                                     uint4* slots, uint32_t stamp, uint32_t nd);
+                                     uint4* slots, uint32_t stamp, uint32_t nd, uint32_t nr);
 __global__ void k_pod_direct_verify(const uint4* pods, uint32_t total, uint4* slots, uint32_t stamp,
                                     unsigned long long* ovf, uint32_t mask, uint32_t nd);
 __global__ void k_vni_ht_build(const uint4* ents, uint32_t n, uint32_t* slots, uint32_t mask);
@@ -413,7 +413,7 @@ constexpr int FP_BLOCK = 1024, FP_GRID = 256;       // k_full_prefix launch shap
 __global__ void k_full_prefix(DevTopos T, uint32_t* first_partial_inv);
 __global__ void k_pod_verify_prefix(const uint4* pods, uint32_t total, uint4* slots, uint32_t stamp,
                                     unsigned long long* ovf, uint32_t mask, uint32_t nd, DevTopos T,
-                                    uint32_t* first_partial_inv, uint32_t nbv);
+                                    uint32_t* first_partial_inv, uint32_t nbv, uint32_t nr);
 
 // ---- CR ingest: TopologyList JSON → epoch tables (kdtn_ingest.hip) ------------------------
 // token word: {byte offset, pre-depth | kind << 24}

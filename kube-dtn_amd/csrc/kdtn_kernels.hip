@@ -499,11 +499,23 @@ KD_INLINE void ovf_insert(const uint4* pods, uint32_t g, uint32_t ns, uint32_t n
     }
 }
 
+// Thread t's pod in the gathered table of nr ranks (rank-major, total = slice * nr): rank
+// t % nr, local index t / nr, so a wave's pods come from every rank at about the same informer
+// position and their name slots lie close together (in rank-major order consecutive rows
+// are ~nr informer positions apart: at N = 8 the slot stores and verify loads touched 2x the
+// lines of N = 1).
+KD_INLINE uint32_t pod_order(uint32_t t, uint32_t total, uint32_t nr) {
+    if (nr <= 1) return t;
+    const uint32_t slice = total / nr;
+    return (t % nr) * slice + t / nr;
+}
+
 __global__ void __launch_bounds__(BLOCK) k_pod_direct_scatter(const uint4* pods, uint32_t total,
                                                               const uint32_t* phys_bits, uint4* slots,
-                                                              uint32_t stamp, uint32_t nd) {
-    const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
-    if (g >= total) return;
+                                                              uint32_t stamp, uint32_t nd, uint32_t nr) {
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= total) return;
+    const uint32_t g = pod_order(t, total, nr);
     const uint4 e = pods[g];
     if (e.x == 0xFFFFFFFFu || e.y >= nd) return;           // padding row / name outside this dictionary
     const uint32_t phys = (phys_bits[e.y >> 5] >> (e.y & 31)) & 1u;
@@ -1330,10 +1342,11 @@ __global__ void __launch_bounds__(FP_BLOCK) k_full_prefix(DevTopos T, uint32_t* 
 __global__ void __launch_bounds__(BLOCK) k_pod_verify_prefix(const uint4* pods, uint32_t total, uint4* slots,
                                                              uint32_t stamp, unsigned long long* ovf, uint32_t mask,
                                                              uint32_t nd, DevTopos T, uint32_t* first_partial_inv,
-                                                             uint32_t nbv) {
+                                                             uint32_t nbv, uint32_t nr) {
     __shared__ uint32_t bmin;
     if (blockIdx.x < nbv) {
-        pod_verify_one(pods, total, slots, stamp, ovf, mask, nd, blockIdx.x * BLOCK + threadIdx.x);
+        const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+        if (t < total) pod_verify_one(pods, total, slots, stamp, ovf, mask, nd, pod_order(t, total, nr));
         return;
     }
     full_prefix_blocks<BLOCK>(T, first_partial_inv, blockIdx.x - nbv, gridDim.x - nbv, &bmin);
