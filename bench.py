@@ -39,7 +39,7 @@ sys.path.insert(0, os.path.join(ROOT, "kube-dtn_amd"))
 
 import numpy as np  # noqa: E402
 
-from kdtn import Engine, abi, comm_unique_id, synth  # noqa: E402
+from kdtn import Engine, KdtnError, abi, comm_unique_id, synth  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 DEFAULT_PODS = {2: 1_000_000, 3: 1_000_000, 4: 100_000}
@@ -347,7 +347,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         dist.init_process_group("gloo")
-    torch.cuda.set_device(local)
+    ndev = torch.cuda.device_count()
+    dev = local % ndev if ndev else local           # (ranks share a GPU only in host-transport tests)
+    torch.cuda.set_device(dev)
     total_pods = pods if args.scaling == "strong" else pods * world
 
     t0 = time.time()
@@ -358,11 +360,35 @@ def main():
     else:
         inp = synth.make(args.config, total_pods=total_pods, shard=rank, nshards=world)
     gen_s = time.time() - t0
-    eng = Engine(device=local)
+    eng = Engine(device=dev)
+    exchange = "none"
+    host_x = False
     if world > 1:
-        uid = [comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        eng.comm_init(uid[0], world, rank)
+        # production transport: RCCL all-gather of the pod-status rows on the engine's comm
+        # stream; KDTN_BENCH_HOST_XCHG=1 (or a failed RCCL init) uses the host transport, the
+        # rows all-gathered over gloo inside every timed epoch
+        host_x = os.environ.get("KDTN_BENCH_HOST_XCHG") == "1"
+        if not host_x:
+            uid = [comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            try:
+                eng.comm_init(uid[0], world, rank)
+                exchange = "rccl all-gather"
+            except KdtnError as e:
+                print(f"rank {rank}: RCCL communicator failed ({e}); host transport", file=sys.stderr, flush=True)
+                host_x = True
+        if host_x:
+            eng.set_ranks(world, rank)
+            exchange = "host transport (gloo all-gather per epoch)"
+
+    def run(stages: int = abi.STAGE_ALL) -> None:
+        if host_x and (stages & abi.STAGE_RESOLVE):
+            mine = torch.from_numpy(eng.pods_export(inp.pod_slice).view(np.int32).copy())
+            parts = [torch.empty_like(mine) for _ in range(world)]
+            dist.all_gather(parts, mine)
+            eng.pods_import(torch.cat(parts).numpy().view(np.uint32))
+        eng.run(stages)
+
     eng.upload(inp)
     # timed epochs record HIP events around k_reconcile (+ placement) only: every event costs
     # ≈5 µs of stream time; the per-stage breakdown comes from separate untimed epochs
@@ -379,13 +405,13 @@ def main():
     pstats = None
     if not churn:
         for _ in range(warmup):
-            eng.run()
+            run()
             eng.sync()
         barrier(world)
         t_start = time.perf_counter()
         counts = None
         for _ in range(steps):
-            eng.run()
+            run()
             counts = eng.sync()
             for k, v in eng.kernel_times().items():
                 ksum[k] = ksum.get(k, 0.0) + v
@@ -396,7 +422,7 @@ def main():
         links_local = inp.desired.n * steps
         eng.set_timing(2)
         for _ in range(min(steps, 5)):                    # per-stage breakdown (untimed)
-            eng.run()
+            run()
             eng.sync()
             for k, v in eng.kernel_times().items():
                 bsum[k] = bsum.get(k, 0.0) + v
@@ -417,7 +443,7 @@ def main():
             timed = ep >= warmup
             barrier(world)
             t = time.perf_counter()
-            eng.run()
+            run()
             counts = eng.sync()
             torch.cuda.synchronize()
             dt = time.perf_counter() - t
@@ -433,11 +459,11 @@ def main():
             counts_acc += np.array([counts.n_add, counts.n_upd, counts.n_del])
             bytes_acc += reconcile_bytes(inp, counts.n_add, counts.n_upd, counts.n_del)
             epoch_acc += epoch_bytes(inp, counts.n_add, counts.n_upd, counts.n_del)
-            eng.run(abi.STAGE_DIFF)                      # gate + CalcDiff + lists alone (report)
+            run(abi.STAGE_DIFF)                      # gate + CalcDiff + lists alone (report)
             eng.sync()
             diff_ms.append(reconcile_ms(eng.kernel_times()))
             eng.set_timing(2)                            # per-stage breakdown (untimed re-run)
-            eng.run()
+            run()
             eng.sync()
             for k, v in eng.kernel_times().items():
                 bsum[k] = bsum.get(k, 0.0) + v
@@ -483,7 +509,7 @@ def main():
                                                             steps=nsteps),
                    "config": args.config, "pods_total": total_pods, "links_per_epoch": int(links_per_epoch),
                    "links_rank0": int(links_local / nsteps), "pods_rank0": inp.topos.n,
-                   "parallelism": f"shard{world} (hash64(ns/name) mod {world})"},
+                   "parallelism": f"shard{world} (hash64(ns/name) mod {world})", "exchange": exchange},
         "roofline": roof,
         "epoch_roofline": {"bytes": eb, "achieved": eb / (ms_step * 1e-3) / 1e9,
                            "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -500,19 +526,19 @@ def main():
         # (kdict_keep / pdict_keep = everything); a separate report, not `value`
         eng.upload(inp, inp.kdict.n, inp.pdict.n)
         for _ in range(2):
-            eng.run()
+            run()
             eng.sync()
         barrier(world)
         t = time.perf_counter()
         for _ in range(steps):
-            eng.run()
+            run()
             eng.sync()
         torch.cuda.synchronize()
         el = allmax(time.perf_counter() - t, world)
         eng.set_timing(2)
         rsum: dict[str, float] = {}
         for _ in range(3):                                # per-stage breakdown (untimed)
-            eng.run()
+            run()
             eng.sync()
             for k, v in eng.kernel_times().items():
                 rsum[k] = rsum.get(k, 0.0) + v / 3
@@ -532,7 +558,7 @@ def main():
         threads = args.cpu_threads or min(32, share)
         result["cpu_baseline"] = cpu_baseline(inp, args.cpu_budget_s, threads, info)
     if world == 1 and args.config == 4:                    # VxlanManager maps after the epoch
-        eng.run()
+        run()
         eng.sync()
         eng.vni_apply()                                    # first call sizes the work buffers
         t = time.perf_counter()
