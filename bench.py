@@ -19,8 +19,14 @@ hash64(namespace/name) mod N (kdtn_topology_shard), one process per GPU:
       epoch parses only its new strings.
   --config 4 (WAN twin): 100k sites in namespaces of 100, power-law degrees, 256 nodes.
 
+  --config 1 (fat-tree): 10k pods, 100k links, uniform props; realised = the same keys with
+      empty props, so every record is an UpdateLinks entry (MakeQdiscs-dominated). 1 GPU.
+
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C] [--scaling strong|weak]
-For N > 1 launch with torch.distributed.run (one process per GPU).
+One process per GPU. `--gpus N` (N > 1) run without a launcher spawns the N ranks itself:
+the parent starts `torch.distributed.run --nproc-per-node N` as a child process before it
+touches the GPU and exits with the child's status; under an external launcher (WORLD_SIZE
+set) WORLD_SIZE must equal --gpus.
 """
 from __future__ import annotations
 
@@ -42,8 +48,11 @@ import numpy as np  # noqa: E402
 from kdtn import Engine, KdtnError, abi, comm_unique_id, synth  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
-DEFAULT_PODS = {2: 1_000_000, 3: 1_000_000, 4: 100_000}
+DEFAULT_PODS = {1: 10_000, 2: 1_000_000, 3: 1_000_000, 4: 100_000}
 WORKLOAD = {
+    1: "config1: fat-tree of {pods} pods (1000 spines + 9000 leaves, {links} Link records), uniform "
+       "props {{latency 10ms, loss 0.1, rate 1Gbit}} over a realised side with the same keys and empty "
+       "props: every record is an UpdateLinks entry (MakeQdiscs on every link)",
     2: "config2: random 10-regular topology of {pods} pods ({links} Link records), heterogeneous "
        "netem/tbf props, all AddLinks (resolve + qdisc on every link)",
     3: "config3: churn epochs on a random 10-regular topology of {pods} pods (~{links} Link records): "
@@ -261,24 +270,44 @@ def ingest_stage(eng, inp, steps: int, reps: int = 5, cpu_sample_pods: int = 20_
     return res
 
 
-def pmc_traffic(config: int, links: int):
-    """HBM bytes per k_reconcile launch (+ k_place_scan / k_place when the summary has them)
-    from the newest committed PMC summary of the same
-    workload (profiles/*pmc_traffic*.json, written by tools/pmc_traffic.py from separate
-    FETCH_SIZE / WRITE_SIZE rocprofv3 passes, gfx950 correction applied), else None."""
+KERNEL_SOURCES = ("kube-dtn_amd/csrc/kdtn_kernels.hip", "kube-dtn_amd/csrc/kdtn_kernels.h",
+                  "kube-dtn_amd/csrc/kdtn_parse.h", "kube-dtn_amd/csrc/kdtn_engine.hip")
+
+
+def kernel_src_sha16() -> str:
+    """Hash of the sources that define k_reconcile and its launch (tools/pmc_traffic.py
+    stamps the same hash into every PMC summary it writes)."""
+    import hashlib
+    h = hashlib.sha256()
+    for p in KERNEL_SOURCES:
+        with open(os.path.join(ROOT, p), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_traffic(config: int, links: int, placed: bool):
+    """HBM bytes per k_reconcile launch (+ k_place_scan / k_place for the comparison build)
+    from a committed PMC summary (profiles/*pmc_traffic*.json, written by
+    tools/pmc_traffic.py from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes, gfx950
+    correction applied) of the same workload AND the same kernel sources (kernel_src_sha16):
+    a summary measured on other sources is never attached. The k_reconcile instantiation
+    must be the build this epoch ran (the comparison build comes with k_place*). Else None."""
     import glob
+    sha = kernel_src_sha16()
     best = None
-    # newest tag last: r02 < r02m < r02zp < r02zp2 ('_' sorts as a space)
-    files = glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic*.json"))
-    for f in sorted(files, key=lambda f: os.path.basename(f).replace("_", " ")):
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic*.json"))):
         with open(f) as fh:
             d = json.load(fh)
+        if d.get("kernel_src_sha16") != sha:
+            continue
         if d.get("config", 2) != config or abs(d.get("links_per_gpu", 0) - links) > 0.01 * links:
             continue
-        tot = [v["traffic_bytes"] for k, v in d["kernels"].items()
-               if (k.startswith("k_reconcile") or k.startswith("k_place")) and "traffic_bytes" in v]
-        if tot:
-            best = (sum(tot), os.path.basename(f))
+        ks = d["kernels"]
+        rec = [k for k in ks if k.startswith("k_reconcile") and "traffic_bytes" in ks[k]]
+        plc = [k for k in ks if k.startswith("k_place") and "traffic_bytes" in ks[k]]
+        if len(rec) != 1 or bool(plc) != placed:
+            continue
+        best = (sum(ks[k]["traffic_bytes"] for k in rec + plc), os.path.basename(f), rec[0])
     return best
 
 
@@ -321,12 +350,46 @@ def barrier(world: int) -> None:
     torch.cuda.synchronize()
 
 
+def dump_outputs(d: str, rank: int, world: int, eng, inp) -> None:
+    """--dump: the epoch outputs of this rank (kdtn_epoch_download) with the shard's global
+    pod ids, for a parity check outside the bench (the bench itself never runs the oracle
+    outside cpu_baseline)."""
+    out = eng.download()
+    os.makedirs(d, exist_ok=True)
+    np.savez(os.path.join(d, f"rank{rank}.npz"), world=world, pod_slice=inp.pod_slice,
+             gid=inp.gid if inp.gid is not None else np.arange(inp.topos.n),
+             **{f: getattr(out, f) for f in out.FIELDS})
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int) -> int:
+    """`bench.py --gpus N` without a launcher: run the N ranks as children under
+    torch.distributed.run (one process per GPU, rendezvous on 127.0.0.1) and return the
+    launcher's exit status. This process has not touched the GPU (nothing here initialises
+    HIP), so the children own the devices; it replaces the reference's worker pool
+    (controllers/topology_controller.go:335-337) with one engine process per GPU."""
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env["KDTN_BENCH_LAUNCHER"] = "bench.py --gpus (torch.distributed.run child)"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)]
+    cmd += sys.argv[1:]
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None, help="timed epochs (default 20; config 3: 10)")
     ap.add_argument("--warmup", type=int, default=None, help="untimed epochs (default 3; config 3: 1)")
-    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4))
+    ap.add_argument("--config", type=int, default=2, choices=(1, 2, 3, 4))
     ap.add_argument("--pods", type=int, default=None,
                     help="pods of the whole topology (strong) or per GPU (weak)")
     ap.add_argument("--scaling", default="strong", choices=("strong", "weak"))
@@ -336,15 +399,28 @@ def main():
     ap.add_argument("--no-wire", action="store_true", help="skip the wire-encoding stage report")
     ap.add_argument("--no-ingest", action="store_true", help="skip the CR-ingest stage report")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive epoch report")
+    ap.add_argument("--dump", default=None,
+                    help="directory: each rank saves its last timed epoch's outputs (rank<r>.npz) for "
+                         "an external parity check (tests/test_bench_gpu.py)")
     args = ap.parse_args()
     churn = args.config == 3
     steps = args.steps if args.steps is not None else (10 if churn else 20)
     warmup = args.warmup if args.warmup is not None else (1 if churn else 3)
     pods = args.pods or DEFAULT_PODS[args.config]
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: one process per GPU is required",
+              file=sys.stderr, flush=True)
+        sys.exit(2)
+    if args.config == 1 and world > 1:
+        print("bench.py: config 1 is a one-GPU workload (SURVEY §8(d))", file=sys.stderr, flush=True)
+        sys.exit(2)
+    launcher = os.environ.get("KDTN_BENCH_LAUNCHER", "external" if world > 1 else "none")
     if world > 1:
         dist.init_process_group("gloo")
     ndev = torch.cuda.device_count()
@@ -357,29 +433,44 @@ def main():
     if churn:
         cs = synth.ChurnSequence(total_pods=total_pods, shard=rank, nshards=world)
         inp = cs.epoch_input()
+    elif args.config == 1:
+        inp = synth.make(1)
+        total_pods = inp.topos.n
     else:
         inp = synth.make(args.config, total_pods=total_pods, shard=rank, nshards=world)
     gen_s = time.time() - t0
     eng = Engine(device=dev)
     exchange = "none"
+    comm_ranks = 1
     host_x = False
     if world > 1:
         # production transport: RCCL all-gather of the pod-status rows on the engine's comm
-        # stream; KDTN_BENCH_HOST_XCHG=1 (or a failed RCCL init) uses the host transport, the
-        # rows all-gathered over gloo inside every timed epoch
-        host_x = os.environ.get("KDTN_BENCH_HOST_XCHG") == "1"
-        if not host_x:
+        # stream. The host transport (rows all-gathered over gloo inside every timed epoch)
+        # is used when KDTN_BENCH_HOST_XCHG=1, when ranks share a device (RCCL cannot put two
+        # ranks of one communicator on one GPU) or when any rank's RCCL init fails: the
+        # decision is all-reduced so every rank takes the same transport.
+        shared = world > max(ndev, 1)
+        want_host = os.environ.get("KDTN_BENCH_HOST_XCHG") == "1" or shared
+        fail = 0
+        if not want_host:
             uid = [comm_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(uid, src=0)
             try:
                 eng.comm_init(uid[0], world, rank)
-                exchange = "rccl all-gather"
             except KdtnError as e:
-                print(f"rank {rank}: RCCL communicator failed ({e}); host transport", file=sys.stderr, flush=True)
-                host_x = True
+                print(f"rank {rank}: RCCL communicator failed ({e})", file=sys.stderr, flush=True)
+                fail = 1
+        flag = torch.tensor([1 if (want_host or fail) else 0], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+        host_x = bool(flag[0])
         if host_x:
-            eng.set_ranks(world, rank)
-            exchange = "host transport (gloo all-gather per epoch)"
+            eng.set_ranks(world, rank)          # also releases a communicator this rank built
+            why = ("KDTN_BENCH_HOST_XCHG=1" if os.environ.get("KDTN_BENCH_HOST_XCHG") == "1" else
+                   f"{world} ranks on {ndev} device(s)" if shared else "RCCL init failed on a rank")
+            exchange = f"host transport (gloo all-gather per epoch; {why})"
+        else:
+            exchange = "rccl all-gather"
+        comm_ranks = world
 
     def run(stages: int = abi.STAGE_ALL) -> None:
         if host_x and (stages & abi.STAGE_RESOLVE):
@@ -429,6 +520,8 @@ def main():
             nbreak += 1
         eng.set_timing(1)
         counts_acc += np.array([counts.n_add, counts.n_upd, counts.n_del]) * steps
+        if args.dump:
+            dump_outputs(args.dump, rank, world, eng, inp)
         bytes_acc = reconcile_bytes(inp, counts.n_add, counts.n_upd, counts.n_del) * steps
         epoch_acc = epoch_bytes(inp, counts.n_add, counts.n_upd, counts.n_del) * steps
         pstats = path_stats(inp)
@@ -486,10 +579,14 @@ def main():
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "traffic": None,
             "bytes_per_launch": bytes_launch, "avg_ms": rec_ms, "dominant_stage": dom}
     roof["frac"] = roof["achieved"] / roof["peak"]
-    tr = pmc_traffic(args.config, inp.desired.n) if world == 1 else None
+    tr = pmc_traffic(args.config, inp.desired.n, placed) if world == 1 else None
+    roof["kernel_src_sha16"] = kernel_src_sha16()
     if tr is not None:
         roof["traffic"] = tr[0]
-        roof["traffic_source"] = f"profiles/{tr[1]} (2*FETCH_SIZE + WRITE_SIZE per launch)"
+        roof["traffic_source"] = (f"profiles/{tr[1]} ({tr[2]}; 2*FETCH_SIZE + WRITE_SIZE per launch, "
+                                  f"measured on these kernel sources)")
+    else:
+        roof["traffic_source"] = "no PMC summary of this workload on these kernel sources"
     eb = epoch_acc / nsteps
     links_per_epoch = links_total / nsteps
     result = {
@@ -509,7 +606,8 @@ def main():
                                                             steps=nsteps),
                    "config": args.config, "pods_total": total_pods, "links_per_epoch": int(links_per_epoch),
                    "links_rank0": int(links_local / nsteps), "pods_rank0": inp.topos.n,
-                   "parallelism": f"shard{world} (hash64(ns/name) mod {world})", "exchange": exchange},
+                   "parallelism": f"shard{world} (hash64(ns/name) mod {world})", "exchange": exchange,
+                   "comm_ranks": comm_ranks, "launcher": launcher},
         "roofline": roof,
         "epoch_roofline": {"bytes": eb, "achieved": eb / (ms_step * 1e-3) / 1e9,
                            "peak": HBM_PEAK_GBS, "unit": "GB/s",

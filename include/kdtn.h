@@ -26,6 +26,8 @@
  *   kdtn_epoch_fanout     groups the daemons' UpdateRemote RPCs (common/utils.go:39-67)
  *                         per destination daemon
  *   kdtn_epoch_tc         synthesises SetVethQdiscs' `tc ... tbf` argv (common/qdisc.go:252-266)
+ *   kdtn_epoch_remote_encode  marshals the RemotePod bodies of Remote.Update
+ *                         (common/utils.go:39-67, daemon/kubedtn/handler.go:348-371)
  *
  * Conventions
  *   - No C++ or HIP types cross this ABI: plain pointers, sizes and PODs.
@@ -159,8 +161,11 @@ typedef struct kdtn_vni_table {
 } kdtn_vni_table;
 
 /* kdtn_epoch_in.vnis.n = KDTN_VNI_RESIDENT: use the context's resident map (the last uploaded
- * snapshot, or the state kdtn_epoch_vni_apply left) instead of uploading one; its ids must
- * still name the same strings (append-only kdict). */
+ * snapshot, or the state kdtn_epoch_vni_apply left) instead of uploading one. Its ids must still
+ * name the same strings, so the upload must keep (kdict_keep) at least the dictionary the map
+ * was made for; KDTN_EINVAL otherwise, and always for kdtn_json_ingest (the engine interns
+ * that dictionary itself). The snapshot an upload starts from stays its epoch-start map: a
+ * re-run of the same upload after kdtn_epoch_vni_apply decides vni_hit as the first run did. */
 #define KDTN_VNI_RESIDENT 0xFFFFFFFFu
 
 typedef struct kdtn_epoch_in {
@@ -384,6 +389,43 @@ typedef struct kdtn_fanout {
 } kdtn_fanout;
 int kdtn_epoch_fanout(kdtn_ctx* ctx, kdtn_fanout* out);
 
+/* ---- RemotePod messages (proto/v1 RemotePod, kube_dtn.proto:65-79) ------------------- */
+/* The request bodies of the Remote.Update calls the epoch's AddLinks make, marshalled on the
+ * GPU so a daemon hands pre-encoded bytes to its gRPC stream (a raw codec) instead of
+ * building and marshalling one RemotePod per link:
+ *   - messages [0, n_remote): UpdateRemote (common/utils.go:39-67) of every add entry that
+ *     sends one — exactly kdtn_epoch_fanout's senders, in its order (destination daemons
+ *     ascending, add-list order within), so daemon k's stream is messages
+ *     [fanout.off[k], fanout.off[k+1]). Payload {NetNs: peer status.net_ns, IntfName:
+ *     link.PeerIntf, IntfIp: link.PeerIp, PeerVtep: local status.src_ip, Vni, KubeNs: local
+ *     namespace, Properties: link.Properties, Name: link.PeerPod} (utils.go:42-51);
+ *   - messages [n_remote, n_msgs): the local Update a PHYSICAL peer makes the daemon run on
+ *     itself (daemon/kubedtn/handler.go:348-371) for every reached PHYSICAL add entry whose
+ *     MakeVeth passed, add-list order: {NetNs: local status.net_ns, IntfName: link.LocalIntf,
+ *     IntfIp: link.LocalIp, PeerVtep: PeerPod without "physical/", Vni, KubeNs, Properties,
+ *     Name: link.PeerPod}.
+ * Message m = bytes[off[m], off[m+1]): varint length + RemotePod (a delimited stream); empty
+ * when a string is not valid UTF-8 (proto.Marshal fails). entry[m] = its add-list entry.
+ * Beside each remote message, the receiving daemon's SetVethQdiscs argv for IntfName
+ * (Update → SetupVxLan → MakeQdiscs → SetVethQdiscs, daemon/vxlan/vxlan.go:31-51; same
+ * format as kdtn_epoch_tc) = tc_bytes[tc_off[m], tc_off[m+1]): present when the link has a
+ * TBF and the peer's CreateOrUpdate accepts IntfIp (remote_err == 0); physical messages
+ * have none here (their tc is kdtn_epoch_tc's slot 2e). Needs a run with RESOLVE and QDISC. */
+typedef struct kdtn_remote_info {
+    uint32_t n_msgs, n_remote;
+    uint64_t n_bytes, n_tc_bytes;
+} kdtn_remote_info;
+typedef struct kdtn_remote_pods {
+    uint8_t*  bytes;    uint64_t cap;          /* [n_bytes] messages                          */
+    uint64_t* off;                             /* [n_msgs + 1]                                */
+    uint32_t* entry;                           /* [n_msgs] add-list entry of each message     */
+    uint8_t*  tc_bytes; uint64_t tc_cap;       /* [n_tc_bytes] receiving daemon's tc argv     */
+    uint64_t* tc_off;                          /* [n_msgs + 1]                                */
+    uint32_t  msg_cap;                         /* capacity of off / entry / tc_off (messages) */
+} kdtn_remote_pods;
+int kdtn_epoch_remote_encode(kdtn_ctx* ctx, kdtn_remote_info* info);      /* after run + sync */
+int kdtn_epoch_download_remote(kdtn_ctx* ctx, kdtn_remote_pods* out);
+
 /* ---- tc argv of the TBF qdiscs -------------------------------------------------------- */
 /* SetVethQdiscs (common/qdisc.go:252-266) applies the TBF by exec'ing
  *   tc qdisc add dev <LinkName> parent 1:1 handle 10:0 tbf rate <Rate> burst <Buffer>
@@ -475,7 +517,8 @@ int kdtn_ingest_download(kdtn_ctx* ctx, kdtn_ingest_tables* out);
  * name, nshards) == shard, document order kept; topology table and both link stores
  * compacted), and peers are reported as document indices (kdtn_resolved.peer_topo = the
  * unsharded topology index). Leaves the context as rank `shard` of `nshards` with its pod
- * table in place, so kdtn_epoch_run follows directly. info: the shard's n_topos /
+ * table in place, so kdtn_epoch_run follows directly (the next kdtn_epoch_upload or ingest
+ * restores the rank setup the context had before). info: the shard's n_topos /
  * n_desired / n_realised and the document's dictionaries; kdtn_ingest_download returns the
  * shard's tables. A context with an RCCL communicator is refused. */
 int kdtn_json_ingest_shard(kdtn_ctx* ctx, const kdtn_vni_table* vnis, uint32_t nshards, uint32_t shard,

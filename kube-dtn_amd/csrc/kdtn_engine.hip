@@ -85,8 +85,13 @@ struct kdtn_ctx {
     uint32_t V = 0, vni_mask = 0;
     // kdtn_epoch_vni_apply: ops, snapshot marks, the new map's table, arrays and scan partials
     DevBuf vx_ops, vx_dead, vx_slots, vx_node, vx_vni, vx_netns, vx_part, vx_cut, vx_vis;
-    bool vres_ok = false;          // v_node/v_vni/v_netns hold a map usable as KDTN_VNI_RESIDENT
-    uint32_t vres_n = 0, vres_D = 0;
+    // v_node/v_vni/v_netns: the snapshot of the current upload (what vni_hit is decided
+    // against, re-runs included); r_*: the map kdtn_epoch_vni_apply produced, which becomes
+    // the next KDTN_VNI_RESIDENT upload's snapshot. The resident map is r_* when vres_in_r.
+    DevBuf r_node, r_vni, r_netns;
+    bool vres_ok = false;          // a map usable as KDTN_VNI_RESIDENT exists
+    bool vres_in_r = false;
+    uint32_t vres_n = 0, vres_D = 0;   // its entries; the dictionary size its ids were made for
     // pods
     DevBuf pods, pod_ovf, pod_direct;
     uint32_t slice = 0, pod_total = 0, ovf_mask = 0, kb_words = 0, pod_stamp = 0;
@@ -104,6 +109,13 @@ struct kdtn_ctx {
     // RemotePod fan-out
     DevBuf f_mark, f_send, f_node_idx, f_nodes, f_counts, f_base, f_part, f_idx, f_reach_upd, f_cut;
     uint32_t f_stamp = 0;
+    bool fan_valid = false;                    // the fan-out of the last run is in f_* (fanout_compute)
+    uint32_t fan_nn = 0, fan_nsend = 0;
+    // RemotePod messages (kdtn_epoch_remote_encode)
+    DevBuf rp_flag, rp_pos, rp_phys, rp_msz, rp_moff, rp_tsz, rp_toff, rp_part, rp_arena, rp_tc;
+    uint32_t rp_n = 0, rp_nr = 0;
+    uint64_t rp_bytes = 0, rp_tc_bytes = 0;
+    bool rp_done = false;
     // tc argv
     DevBuf tc_size, tc_off, tc_part, tc_arena;
     uint64_t tc_bytes = 0;
@@ -130,6 +142,10 @@ struct kdtn_ctx {
     int nranks = 1, rank = 0;
     bool pods_imported = false;   // host transport: this epoch's global pod table is in place
     bool pods_rank_major = true;  // pod table rank-major (uploads) vs document order (sharded ingest)
+    // kdtn_json_ingest_shard leaves the context as rank `shard` of `nshards` for its epoch; the
+    // next upload or ingest restores the rank setup the caller had before (sh_saved_*)
+    bool sh_active = false;
+    int sh_saved_nranks = 1, sh_saved_rank = 0;
     // timers: 0 none, 1 k_reconcile (+ placement) only, 2 every stage (kdtn_set_timing)
     int timing = 2;
     hipEvent_t ev[kMaxTimers + 1] = {};
@@ -380,7 +396,8 @@ int prepare_dicts(kdtn_ctx* c) {
     hipStream_t s = c->stream;
     const uint32_t need = (uint32_t)(((uint64_t)D + 63) / 64 * 2);
     if (need > c->kb_cap || !c->kd_bits.p) {
-        const uint32_t cap = std::max<uint32_t>(need, c->kd_valid ? c->kb_cap + c->kb_cap / 2 : 0);
+        // stride a multiple of 2 words (kdtn_kernels.h kb_words): growth by 1.5x rounded up
+        const uint32_t cap = (std::max<uint32_t>(need, c->kd_valid ? c->kb_cap + c->kb_cap / 2 : 0) + 1u) & ~1u;
         DevBuf nb;
         TRY(ensure(nb, (size_t)KB_NSETS * cap * 4 + 4));
         const uint32_t keepw = (uint32_t)(((uint64_t)c->kd_valid + 63) / 64 * 2);
@@ -403,18 +420,34 @@ int prepare_dicts(kdtn_ctx* c) {
     return KDTN_OK;
 }
 
-// VxlanManager snapshot ids valid for a dictionary of D strings; KDTN_VNI_RESIDENT needs a
-// resident map whose ids all exist (the dictionary only grew since it was made)
-int check_vnis(kdtn_ctx* c, const kdtn_vni_table& vn, uint32_t D) {
+// VxlanManager snapshot ids valid for a dictionary of D strings. KDTN_VNI_RESIDENT needs a
+// resident map whose ids still name the same strings: the upload keeps (kdict_keep) at least
+// the vres_D strings the map was made for — every upload since kept that prefix, since an
+// upload that kept less either replaced the map or was refused here. A dictionary the engine
+// builds itself (JSON ingest) cannot keep a prefix (keep = 0).
+int check_vnis(kdtn_ctx* c, const kdtn_vni_table& vn, uint32_t D, uint32_t keep) {
     if (vn.n == KDTN_VNI_RESIDENT) {
-        if (!c->vres_ok || D < c->vres_D) {
-            std::snprintf(g_last_error, sizeof(g_last_error), "KDTN_VNI_RESIDENT: no resident VXLAN map for this dictionary");
+        if (!c->vres_ok || keep < c->vres_D || D < c->vres_D) {
+            std::snprintf(g_last_error, sizeof(g_last_error),
+                          "KDTN_VNI_RESIDENT: the resident VXLAN map's ids (%u strings) are not a kept prefix "
+                          "of this dictionary (kdict_keep %u)", c->vres_D, keep);
             return KDTN_EINVAL;
         }
         return KDTN_OK;
     }
     TRY(check_ids(vn.node, vn.n, D, "vnis.node"));
     return check_ids(vn.net_ns, vn.n, D, "vnis.net_ns");
+}
+
+// A sharded ingest's rank setup ends when the next upload or ingest starts.
+void end_shard_ingest(kdtn_ctx* c) {
+    if (!c->sh_active) return;
+    c->nranks = c->sh_saved_nranks;
+    c->rank = c->sh_saved_rank;
+    c->pods_rank_major = true;
+    c->pods_imported = false;
+    c->sh_T = 0;
+    c->sh_active = false;
 }
 
 // everything an epoch needs besides its input tables: VNI snapshot, pod tables, work and
@@ -429,8 +462,14 @@ int prepare_epoch(kdtn_ctx* c, const kdtn_vni_table& vn, uint32_t slice, uint32_
         TRY(upload(c, c->v_vni, vn.vni, (size_t)V * 4));
         TRY(upload(c, c->v_netns, vn.net_ns, (size_t)V * 4));
         c->vres_ok = true;                      // the uploaded map stays resident
+        c->vres_in_r = false;
         c->vres_n = V;
         c->vres_D = D;
+    } else if (c->vres_in_r) {                  // the applied map becomes this upload's snapshot
+        std::swap(c->v_node, c->r_node);
+        std::swap(c->v_vni, c->r_vni);
+        std::swap(c->v_netns, c->r_netns);
+        c->vres_in_r = false;
     }
     c->vni_mask = V ? next_pow2((uint64_t)V * 2) - 1 : 0;
     TRY(ensure(c->v_ents, (size_t)V * 16));
@@ -609,7 +648,9 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->sh_kdes, &c->sh_tidx, &c->sh_roff64, &c->sh_noff64, &c->sh_doc, &c->sh_ns,
                       &c->sh_name, &c->sh_src, &c->sh_netns, &c->sh_flags, &c->sh_roff, &c->sh_noff,
                       &c->sh_des.buf, &c->sh_real.buf, &c->vx_ops, &c->vx_dead, &c->vx_slots, &c->vx_node,
-                      &c->vx_vni, &c->vx_netns, &c->vx_part, &c->vx_cut, &c->f_cut, &c->vx_vis};
+                      &c->vx_vni, &c->vx_netns, &c->vx_part, &c->vx_cut, &c->f_cut, &c->vx_vis,
+                      &c->r_node, &c->r_vni, &c->r_netns, &c->rp_flag, &c->rp_pos, &c->rp_phys,
+                      &c->rp_msz, &c->rp_moff, &c->rp_tsz, &c->rp_toff, &c->rp_part, &c->rp_arena, &c->rp_tc};
     for (DevBuf* b : bufs) release(*b);
     for (int i = 0; i <= kMaxTimers; ++i)
         if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
@@ -632,6 +673,7 @@ int kdtn_epoch_upload(kdtn_ctx* c, const kdtn_epoch_in* in) {
     if (!c || !in) return KDTN_EINVAL;
     HIP_TRY(hipSetDevice(c->device));
     g_last_error[0] = 0;
+    end_shard_ingest(c);
     TRY(check_strtab(in->kdict, "kdict"));
     TRY(check_strtab(in->pdict, "pdict"));
     const kdtn_topo_table& T = in->topos;
@@ -653,7 +695,7 @@ int kdtn_epoch_upload(kdtn_ctx* c, const kdtn_epoch_in* in) {
             return KDTN_EINVAL;
         }
     }
-    TRY(check_vnis(c, in->vnis, D));
+    TRY(check_vnis(c, in->vnis, D, in->kdict_keep));
     const uint32_t slice = in->pod_slice ? in->pod_slice : T.n;
     if (slice < T.n) return KDTN_EINVAL;
 
@@ -922,6 +964,8 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
     c->ran = true;
     c->encoded = false;
     c->tc_done = false;
+    c->fan_valid = false;
+    c->rp_done = false;
     return KDTN_OK;
 }
 
@@ -1182,14 +1226,17 @@ int kdtn_epoch_download_wire(kdtn_ctx* c, kdtn_wire* o) {
     return KDTN_OK;
 }
 
-int kdtn_epoch_fanout(kdtn_ctx* c, kdtn_fanout* o) {
-    if (!c || !o || !c->ran) return KDTN_EINVAL;
-    if ((c->last_stages & (KDTN_STAGE_RESOLVE | KDTN_STAGE_QDISC)) != (KDTN_STAGE_RESOLVE | KDTN_STAGE_QDISC))
-        return KDTN_EINVAL;
-    HIP_TRY(hipSetDevice(c->device));
+}  // extern "C"
+
+namespace {
+
+// The RemotePod fan-out of the last run (k_reach, node compaction, stable grouping) into
+// f_nodes / f_idx / f_base; cached until the next run.
+int fanout_compute(kdtn_ctx* c) {
+    if (c->fan_valid) return KDTN_OK;
     HIP_TRY(hipStreamSynchronize(c->stream));
     hipStream_t s = c->stream;
-    const uint32_t na = c->h_misc[3], T = c->T, D = c->D;
+    const uint32_t na = c->h_misc[3], D = c->D;
     if (c->f_mark.cap < (size_t)D * 4) {                      // stamps start from a zeroed table
         TRY(ensure(c->f_mark, (size_t)D * 4));
         HIP_TRY(hipMemsetAsync(c->f_mark.p, 0, c->f_mark.cap, s));
@@ -1209,9 +1256,7 @@ int kdtn_epoch_fanout(kdtn_ctx* c, kdtn_fanout* o) {
     TRY(ensure(c->f_idx, (size_t)na * 4 + 16));
     uint32_t* misc = dp<uint32_t>(c->misc);
     uint32_t* n_nodes = misc + MISC_FAN_NODES;
-    c->n_ev = 0;
-    (void)hipEventRecord(c->ev[0], s);
-    FanIn f{dp<uint32_t>(c->add_off), dp<uint4>(c->add_res), dp<uint2>(c->add_qdisc), T, na, c->f_stamp};
+    FanIn f{dp<uint32_t>(c->add_off), dp<uint4>(c->add_res), dp<uint2>(c->add_qdisc), c->T, na, c->f_stamp};
     TRY(run_reach(c, dp<uint32_t>(c->f_mark), c->f_stamp));
     k_fan_nodes_count<<<nbd, BLOCK, 0, s>>>(dp<uint32_t>(c->f_mark), D, c->f_stamp, dp<uint64_t>(c->f_part));
     k_scan_top<<<1, BLOCK, 0, s>>>(dp<uint64_t>(c->f_part), nbd);
@@ -1246,6 +1291,31 @@ int kdtn_epoch_fanout(kdtn_ctx* c, kdtn_fanout* o) {
         nsend = (uint32_t)tot;
     }
     timer_mark(c, "fanout_group");
+    c->fan_nn = nn;
+    c->fan_nsend = nsend;
+    c->fan_valid = true;
+    return KDTN_OK;
+}
+
+bool fanout_stages_ok(const kdtn_ctx* c) {
+    return (c->last_stages & (KDTN_STAGE_RESOLVE | KDTN_STAGE_QDISC)) == (KDTN_STAGE_RESOLVE | KDTN_STAGE_QDISC);
+}
+
+}  // namespace
+
+extern "C" {
+
+int kdtn_epoch_fanout(kdtn_ctx* c, kdtn_fanout* o) {
+    if (!c || !o || !c->ran) return KDTN_EINVAL;
+    if (!fanout_stages_ok(c)) return KDTN_EINVAL;
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    c->n_ev = 0;
+    (void)hipEventRecord(c->ev[0], s);
+    c->fan_valid = false;                                    // recomputed per call (timed stage)
+    TRY(fanout_compute(c));
+    const uint32_t nn = c->fan_nn, nsend = c->fan_nsend, na = c->h_misc[3];
+    const uint32_t nchunks = nblocks(na, FAN_CHUNK);
     o->n_nodes = nn;
     o->n_send = nsend;
     if (nn > o->node_cap || nsend > o->idx_cap) return KDTN_ENOSPC;
@@ -1260,6 +1330,133 @@ int kdtn_epoch_fanout(kdtn_ctx* c, kdtn_fanout* o) {
         HIP_TRY(hipStreamSynchronize(s));
         for (uint32_t k = 0; k < nn; ++k) o->off[k] = na ? (uint32_t)b[k] : 0u;
         o->off[nn] = nsend;
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    return KDTN_OK;
+}
+
+int kdtn_epoch_remote_encode(kdtn_ctx* c, kdtn_remote_info* info) {
+    if (!c || !c->ran || !fanout_stages_ok(c)) return KDTN_EINVAL;
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    c->n_ev = 0;
+    (void)hipEventRecord(c->ev[0], s);
+    TRY(fanout_compute(c));                                  // f_idx (fan-out order) and f_send (reach)
+    const uint32_t na = c->h_misc[3], nr = c->fan_nsend;
+    // physical peers' local Updates: reached PHYSICAL adds whose MakeVeth passed, add-list order
+    const uint32_t nbp = nblocks((uint64_t)na + 1, SCAN_CHUNK);
+    TRY(ensure(c->rp_flag, (size_t)na * 4 + 16));
+    TRY(ensure(c->rp_pos, ((size_t)na + 1) * 8));
+    TRY(ensure(c->rp_part, (size_t)nbp * 8 + 16));
+    TRY(ensure(c->rp_phys, (size_t)na * 4 + 16));
+    if (na) k_remote_phys_flags<<<nblocks(na), BLOCK, 0, s>>>(dp<uint8_t>(c->f_send), dp<uint4>(c->add_res), na,
+                                                              dp<uint32_t>(c->rp_flag));
+    k_scan_partial<<<nbp, BLOCK, 0, s>>>(dp<uint32_t>(c->rp_flag), na, dp<uint64_t>(c->rp_part));
+    k_scan_top<<<1, BLOCK, 0, s>>>(dp<uint64_t>(c->rp_part), nbp);
+    k_scan_final<<<nbp, BLOCK, 0, s>>>(dp<uint32_t>(c->rp_flag), na, dp<uint64_t>(c->rp_part), dp<uint64_t>(c->rp_pos));
+    if (na) k_remote_phys_scatter<<<nblocks(na), BLOCK, 0, s>>>(dp<uint32_t>(c->rp_flag), dp<uint64_t>(c->rp_pos), na,
+                                                                dp<uint32_t>(c->rp_phys));
+    uint64_t nphys = 0;
+    HIP_TRY(hipMemcpyAsync(&nphys, dp<uint64_t>(c->rp_pos) + na, 8, hipMemcpyDeviceToHost, s));
+    // UTF-8 validity of every dictionary string (proto.Marshal fails on invalid strings)
+    const uint32_t kw = (uint32_t)(((uint64_t)c->D + 63) / 64 * 2), pw = (uint32_t)(((uint64_t)c->P + 63) / 64 * 2);
+    TRY(ensure(c->kd_utf8, (size_t)kw * 4));
+    TRY(ensure(c->pd_utf8, (size_t)pw * 4));
+    if (c->D) k_utf8_bits<<<nblocks(c->D), BLOCK, 0, s>>>(dp<uint8_t>(c->kd_bytes), dp<uint32_t>(c->kd_offs), c->D,
+                                                          dp<uint32_t>(c->kd_utf8));
+    if (c->P) k_utf8_bits<<<nblocks(c->P), BLOCK, 0, s>>>(dp<uint8_t>(c->pd_bytes), dp<uint32_t>(c->pd_offs), c->P,
+                                                          dp<uint32_t>(c->pd_utf8));
+    HIP_TRY(hipStreamSynchronize(s));
+    timer_mark(c, "remote_select");
+    const uint64_t n = (uint64_t)nr + nphys;
+    if (n >= 0xFFFFFFFFull) return KDTN_EINVAL;
+    RemoteIn r{};
+    r.kd_bytes = dp<uint8_t>(c->kd_bytes);
+    r.kd_offs = dp<uint32_t>(c->kd_offs);
+    r.kd_utf8 = dp<uint32_t>(c->kd_utf8);
+    r.pd_bytes = dp<uint8_t>(c->pd_bytes);
+    r.pd_offs = dp<uint32_t>(c->pd_offs);
+    r.pd_utf8 = dp<uint32_t>(c->pd_utf8);
+    r.t_ns = dp<uint32_t>(c->t_ns);
+    r.t_src = dp<uint32_t>(c->t_src);
+    r.t_netns = dp<uint32_t>(c->t_netns);
+    r.add_off = dp<uint32_t>(c->add_off);
+    r.add_idx = dp<uint32_t>(c->add_idx);
+    r.add_res = dp<uint4>(c->add_res);
+    r.add_qdisc = dp<uint2>(c->add_qdisc);
+    r.pods = dp<uint4>(c->pods);
+    r.rem_idx = dp<uint32_t>(c->f_idx);
+    r.phys_idx = dp<uint32_t>(c->rp_phys);
+    r.N = c->des.view;
+    r.n_msgs = (uint32_t)n;
+    r.n_remote = nr;
+    r.T = c->T;
+    const uint32_t nbm = nblocks(n + 1, SCAN_CHUNK);
+    TRY(ensure(c->rp_msz, (size_t)n * 4 + 16));
+    TRY(ensure(c->rp_tsz, (size_t)n * 4 + 16));
+    TRY(ensure(c->rp_moff, (n + 1) * 8));
+    TRY(ensure(c->rp_toff, (n + 1) * 8));
+    TRY(ensure(c->rp_part, (size_t)nbm * 8 + 16));
+    TRY(ensure(c->w_part, (size_t)nbm * 8 + 16));
+    if (n) {
+        k_remote_sizes<<<nblocks(n), BLOCK, 0, s>>>(r, dp<uint32_t>(c->rp_msz));
+        k_tc_remote_sizes<<<nblocks(n), BLOCK, 0, s>>>(r, dp<uint32_t>(c->rp_tsz));
+    }
+    k_scan_partial<<<nbm, BLOCK, 0, s>>>(dp<uint32_t>(c->rp_msz), (uint32_t)n, dp<uint64_t>(c->rp_part));
+    k_scan_top<<<1, BLOCK, 0, s>>>(dp<uint64_t>(c->rp_part), nbm);
+    k_scan_final<<<nbm, BLOCK, 0, s>>>(dp<uint32_t>(c->rp_msz), (uint32_t)n, dp<uint64_t>(c->rp_part),
+                                       dp<uint64_t>(c->rp_moff));
+    k_scan_partial<<<nbm, BLOCK, 0, s>>>(dp<uint32_t>(c->rp_tsz), (uint32_t)n, dp<uint64_t>(c->w_part));
+    k_scan_top<<<1, BLOCK, 0, s>>>(dp<uint64_t>(c->w_part), nbm);
+    k_scan_final<<<nbm, BLOCK, 0, s>>>(dp<uint32_t>(c->rp_tsz), (uint32_t)n, dp<uint64_t>(c->w_part),
+                                       dp<uint64_t>(c->rp_toff));
+    timer_mark(c, "remote_sizes");
+    HIP_TRY(hipGetLastError());
+    uint64_t tot[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(tot, dp<uint64_t>(c->rp_moff) + n, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(tot + 1, dp<uint64_t>(c->rp_toff) + n, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    TRY(ensure(c->rp_arena, (size_t)tot[0] + 16));
+    TRY(ensure(c->rp_tc, (size_t)tot[1] + 16));
+    timer_mark(c, "remote_host_sync");
+    if (n) {
+        k_remote_write<<<nblocks(n), BLOCK, 0, s>>>(r, dp<uint64_t>(c->rp_moff), dp<uint8_t>(c->rp_arena));
+        timer_mark(c, "remote_write");
+        k_tc_remote_write<<<nblocks(n), BLOCK, 0, s>>>(r, dp<uint64_t>(c->rp_toff), dp<uint8_t>(c->rp_tc));
+        timer_mark(c, "remote_tc_write");
+    }
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(s));
+    c->rp_n = (uint32_t)n;
+    c->rp_nr = nr;
+    c->rp_bytes = tot[0];
+    c->rp_tc_bytes = tot[1];
+    c->rp_done = true;
+    if (info) {
+        info->n_msgs = c->rp_n;
+        info->n_remote = nr;
+        info->n_bytes = tot[0];
+        info->n_tc_bytes = tot[1];
+    }
+    return KDTN_OK;
+}
+
+int kdtn_epoch_download_remote(kdtn_ctx* c, kdtn_remote_pods* o) {
+    if (!c || !o || !c->rp_done) return KDTN_EINVAL;
+    HIP_TRY(hipSetDevice(c->device));
+    if ((o->bytes && c->rp_bytes > o->cap) || (o->tc_bytes && c->rp_tc_bytes > o->tc_cap) ||
+        ((o->off || o->entry || o->tc_off) && c->rp_n > o->msg_cap))
+        return KDTN_ENOSPC;
+    hipStream_t s = c->stream;
+    const size_t n = c->rp_n, nr = c->rp_nr;
+    if (o->bytes && c->rp_bytes) HIP_TRY(hipMemcpyAsync(o->bytes, c->rp_arena.p, c->rp_bytes, hipMemcpyDeviceToHost, s));
+    if (o->tc_bytes && c->rp_tc_bytes)
+        HIP_TRY(hipMemcpyAsync(o->tc_bytes, c->rp_tc.p, c->rp_tc_bytes, hipMemcpyDeviceToHost, s));
+    if (o->off) HIP_TRY(hipMemcpyAsync(o->off, c->rp_moff.p, (n + 1) * 8, hipMemcpyDeviceToHost, s));
+    if (o->tc_off) HIP_TRY(hipMemcpyAsync(o->tc_off, c->rp_toff.p, (n + 1) * 8, hipMemcpyDeviceToHost, s));
+    if (o->entry) {
+        if (nr) HIP_TRY(hipMemcpyAsync(o->entry, c->f_idx.p, nr * 4, hipMemcpyDeviceToHost, s));
+        if (n > nr) HIP_TRY(hipMemcpyAsync(o->entry + nr, c->rp_phys.p, (n - nr) * 4, hipMemcpyDeviceToHost, s));
     }
     HIP_TRY(hipStreamSynchronize(s));
     return KDTN_OK;
@@ -1669,7 +1866,7 @@ static int json_ingest_full(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest
     TRY(prepare_dicts(c));
     const kdtn_vni_table none{0, nullptr, nullptr, nullptr};
     const kdtn_vni_table& vn = vnis ? *vnis : none;
-    TRY(check_vnis(c, vn, c->D));
+    TRY(check_vnis(c, vn, c->D, 0u));             // the engine's own dictionary: no kept prefix
     TRY(prepare_epoch(c, vn, T, M, N));
     HIP_TRY(hipStreamSynchronize(s));
     c->j_info.n_topos = T;
@@ -1686,6 +1883,7 @@ static int json_ingest_full(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest
 }
 
 int kdtn_json_ingest(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest_info* info) {
+    if (c) end_shard_ingest(c);
     if (c && c->nranks > 1) {
         std::snprintf(g_last_error, sizeof(g_last_error),
                       "kdtn_json_ingest: single-shard contexts (kdtn_json_ingest_shard for a rank of several)");
@@ -1706,10 +1904,16 @@ int kdtn_json_ingest_shard(kdtn_ctx* c, const kdtn_vni_table* vnis, uint32_t nsh
                       "kdtn_json_ingest_shard: the context has an RCCL communicator (no exchange is needed)");
         return KDTN_EINVAL;
     }
+    end_shard_ingest(c);
+    const int saved_nranks = c->nranks, saved_rank = c->rank;
     c->nranks = 1;
     c->rank = 0;
-    TRY(json_ingest_full(c, vnis, info));
-    if (nshards == 1) return KDTN_OK;
+    const int rc = json_ingest_full(c, vnis, info);
+    if (rc != KDTN_OK || nshards == 1) {
+        c->nranks = saved_nranks;
+        c->rank = saved_rank;
+        return rc;
+    }
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t s = c->stream;
     const uint32_t Tf = c->T, Mf = c->real.n, Nf = c->des.n;
@@ -1754,6 +1958,9 @@ int kdtn_json_ingest_shard(kdtn_ctx* c, const kdtn_vni_table* vnis, uint32_t nsh
     HIP_TRY(hipGetLastError());
     // 3. a rank of nshards with every Topology's pod-status row: pod index = document index
     const uint32_t slice = (Tf + nshards - 1) / nshards;
+    c->sh_active = true;
+    c->sh_saved_nranks = saved_nranks;
+    c->sh_saved_rank = saved_rank;
     c->nranks = (int)nshards;
     c->pods_rank_major = false;                         // pod index = document index
     c->rank = (int)shard;
@@ -1866,6 +2073,8 @@ int kdtn_comm_init(kdtn_ctx* c, const uint8_t uid[128], int nranks, int rank) {
     c->nranks = nranks;
     c->rank = rank;
     c->uploaded = false;
+    c->sh_active = false;
+    c->pods_rank_major = true;
     if (!c->comm_stream) {
         HIP_TRY(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
         HIP_TRY(hipEventCreateWithFlags(&c->ev_fill, hipEventDisableTiming));
@@ -1895,6 +2104,8 @@ int kdtn_comm_set_ranks(kdtn_ctx* c, int nranks, int rank) {
     c->rank = rank;
     c->uploaded = false;
     c->pods_imported = false;
+    c->sh_active = false;                 // a new rank setup replaces a sharded ingest's
+    c->pods_rank_major = true;
     return KDTN_OK;
 }
 
@@ -2000,11 +2211,14 @@ int kdtn_epoch_vni_apply(kdtn_ctx* c, kdtn_vni_state* out) {
     HIP_TRY(hipMemcpyAsync(c->h_misc + 5, n_out, 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     const uint32_t n = c->h_misc[5];
-    // the new map becomes the resident one (the next upload's KDTN_VNI_RESIDENT)
-    std::swap(c->v_node, c->vx_node);
-    std::swap(c->v_vni, c->vx_vni);
-    std::swap(c->v_netns, c->vx_netns);
+    // the new map becomes the resident one (the next upload's KDTN_VNI_RESIDENT); this upload's
+    // snapshot (v_*, v_ents, V) stays as it is, so a re-run or a second apply of this upload
+    // sees the same epoch-start map
+    std::swap(c->r_node, c->vx_node);
+    std::swap(c->r_vni, c->vx_vni);
+    std::swap(c->r_netns, c->vx_netns);
     c->vres_ok = true;
+    c->vres_in_r = true;
     c->vres_n = n;
     c->vres_D = c->D;
     return out ? kdtn_vni_download(c, out) : KDTN_OK;
@@ -2022,9 +2236,12 @@ int kdtn_vni_download(kdtn_ctx* c, kdtn_vni_state* out) {
     if (!out->node && !out->vni && !out->net_ns) return KDTN_OK;
     if (n > out->cap) return KDTN_ENOSPC;
     hipStream_t s = c->stream;
-    if (n && out->node) HIP_TRY(hipMemcpyAsync(out->node, c->v_node.p, (size_t)n * 4, hipMemcpyDeviceToHost, s));
-    if (n && out->vni) HIP_TRY(hipMemcpyAsync(out->vni, c->v_vni.p, (size_t)n * 4, hipMemcpyDeviceToHost, s));
-    if (n && out->net_ns) HIP_TRY(hipMemcpyAsync(out->net_ns, c->v_netns.p, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    DevBuf& bn = c->vres_in_r ? c->r_node : c->v_node;
+    DevBuf& bv = c->vres_in_r ? c->r_vni : c->v_vni;
+    DevBuf& bs = c->vres_in_r ? c->r_netns : c->v_netns;
+    if (n && out->node) HIP_TRY(hipMemcpyAsync(out->node, bn.p, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    if (n && out->vni) HIP_TRY(hipMemcpyAsync(out->vni, bv.p, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    if (n && out->net_ns) HIP_TRY(hipMemcpyAsync(out->net_ns, bs.p, (size_t)n * 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     return KDTN_OK;
 }

@@ -289,6 +289,36 @@ struct TcIn {
 __global__ void k_tc_sizes(TcIn w, uint32_t* size);
 __global__ void k_tc_write(TcIn w, const uint64_t* off, uint8_t* arena);
 
+// ---- RemotePod messages (kdtn_wire.hip) and the receiving daemon's tc argv (kdtn_tc.hip) ----
+// message m: the UpdateRemote payload of add entry rem_idx[m] (m < n_remote, fan-out order) or
+// the physical peer's local Update payload of add entry phys_idx[m - n_remote]
+struct RemoteIn {
+    const uint8_t* kd_bytes;
+    const uint32_t* kd_offs;
+    const uint32_t* kd_utf8;
+    const uint8_t* pd_bytes;
+    const uint32_t* pd_offs;
+    const uint32_t* pd_utf8;
+    const uint32_t* t_ns;
+    const uint32_t* t_src;
+    const uint32_t* t_netns;
+    const uint32_t* add_off;
+    const uint32_t* add_idx;
+    const uint4* add_res;
+    const uint2* add_qdisc;
+    const uint4* pods;              // global pod-status rows (the peer's status.net_ns)
+    const uint32_t* rem_idx;
+    const uint32_t* phys_idx;
+    DevLinks N;
+    uint32_t n_msgs, n_remote, T;
+};
+__global__ void k_remote_phys_flags(const uint8_t* reach_add, const uint4* add_res, uint32_t na, uint32_t* flag);
+__global__ void k_remote_phys_scatter(const uint32_t* flag, const uint64_t* pos, uint32_t na, uint32_t* phys_idx);
+__global__ void k_remote_sizes(RemoteIn r, uint32_t* size);
+__global__ void k_remote_write(RemoteIn r, const uint64_t* off, uint8_t* arena);
+__global__ void k_tc_remote_sizes(RemoteIn r, uint32_t* size);
+__global__ void k_tc_remote_write(RemoteIn r, const uint64_t* off, uint8_t* arena);
+
 // ---- RemotePod fan-out grouping (kdtn_fanout.hip) ---------------------------------------
 constexpr int FAN_CHUNK = 4096;        // add entries per single-wave workgroup
 constexpr int FAN_NODE_CAP = 8192;     // destination daemons per epoch (LDS histogram)

@@ -85,17 +85,12 @@ struct Out {
     }
 };
 
-__global__ void __launch_bounds__(BLOCK) k_tc_write(TcIn w, const uint64_t* off, uint8_t* arena) {
-    const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
-    if (g >= 2u * w.n_add + w.n_upd) return;
-    const TcEntry t = tc_entry(w, g);
-    if (!t.on) return;
-    Out o{arena + off[g]};
+KD_INLINE void write_tbf_argv(Out& o, const uint8_t* kd_bytes, const uint32_t* kd_offs, const TcEntry& t) {
     o.lit("qdisc");
     o.lit("add");
     o.lit("dev");
-    const uint32_t b = w.kd_offs[t.intf], len = w.kd_offs[t.intf + 1] - b;
-    for (uint32_t k = 0; k < len; ++k) *o.p++ = w.kd_bytes[b + k];
+    const uint32_t b = kd_offs[t.intf], len = kd_offs[t.intf + 1] - b;
+    for (uint32_t k = 0; k < len; ++k) *o.p++ = kd_bytes[b + k];
     *o.p++ = 0;
     o.lit("parent");
     o.lit("1:1");
@@ -110,6 +105,53 @@ __global__ void __launch_bounds__(BLOCK) k_tc_write(TcIn w, const uint64_t* off,
     o.lit("50ms");
     o.lit("minburst");
     o.num(t.minburst);
+}
+
+__global__ void __launch_bounds__(BLOCK) k_tc_write(TcIn w, const uint64_t* off, uint8_t* arena) {
+    const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
+    if (g >= 2u * w.n_add + w.n_upd) return;
+    const TcEntry t = tc_entry(w, g);
+    if (!t.on) return;
+    Out o{arena + off[g]};
+    write_tbf_argv(o, w.kd_bytes, w.kd_offs, t);
+}
+
+// The receiving daemon's TBF command for RemotePod message m (m < n_remote): the peer
+// daemon's Update runs SetupVxLan on link.PeerIntf → MakeQdiscs (the same properties, which
+// built on the sending side) → SetVethQdiscs (daemon/vxlan/vxlan.go:31-51), unless its
+// CreateOrUpdate rejects IntfIp (kdtn_resolved.remote_err). Physical messages have none here
+// (their tc runs on LocalIntf: kdtn_epoch_tc slot 2e).
+KD_INLINE TcEntry tc_remote_entry(const RemoteIn& r, uint32_t m) {
+    TcEntry t{0, 0, 0, 0, false};
+    if (m >= r.n_remote) return t;
+    const uint32_t e = r.rem_idx[m];
+    const uint2* q = r.add_qdisc + (size_t)e * 9;
+    const uint32_t flags = q[8].y;
+    if (((flags >> 8) & 0xFFu) == 0 || (r.add_res[e].w >> 24) != 0) return t;
+    t.intf = r.N.key(KDTN_K_PEER_INTF, r.add_idx[e]);
+    t.buffer = q[6].y;
+    t.rate = ((uint64_t)q[7].y << 32) | q[7].x;
+    t.minburst = q[8].x;
+    t.on = true;
+    return t;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_tc_remote_sizes(RemoteIn r, uint32_t* size) {
+    const uint32_t m = blockIdx.x * BLOCK + threadIdx.x;
+    if (m >= r.n_msgs) return;
+    const TcEntry t = tc_remote_entry(r, m);
+    size[m] = t.on ? TC_FIXED + (r.kd_offs[t.intf + 1] - r.kd_offs[t.intf]) + ndigits(t.rate) + ndigits(t.buffer) +
+                         ndigits(t.minburst)
+                   : 0u;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_tc_remote_write(RemoteIn r, const uint64_t* off, uint8_t* arena) {
+    const uint32_t m = blockIdx.x * BLOCK + threadIdx.x;
+    if (m >= r.n_msgs) return;
+    const TcEntry t = tc_remote_entry(r, m);
+    if (!t.on) return;
+    Out o{arena + off[m]};
+    write_tbf_argv(o, r.kd_bytes, r.kd_offs, t);
 }
 
 }  // namespace kdtn

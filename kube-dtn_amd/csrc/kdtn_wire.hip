@@ -390,4 +390,194 @@ __global__ void __launch_bounds__(BLOCK) k_wire_write(WireIn w, DevLinks O, DevL
     }
 }
 
+// ==========================================================================================
+// RemotePod messages (proto/v1/kube_dtn.proto:65-79): the UpdateRemote payload of every
+// add entry the fan-out groups (common/utils.go:42-51), in fan-out order, then the physical
+// peers' local Update payloads (daemon/kubedtn/handler.go:353-362) in add-list order. Each
+// message is preceded by its varint length; a message with a string that is not valid UTF-8
+// fails to marshal and is empty. Fields: net_ns 1, intf_name 2, intf_ip 3, peer_vtep 4,
+// kube_ns 5, int32 vni 6 (10-byte varint when negative), properties 7 (always present:
+// Link.ToProto sets it), name 8.
+// ==========================================================================================
+__global__ void __launch_bounds__(BLOCK) k_remote_phys_flags(const uint8_t* reach_add, const uint4* add_res,
+                                                             uint32_t na, uint32_t* flag) {
+    const uint32_t e = blockIdx.x * BLOCK + threadIdx.x;
+    if (e >= na) return;
+    const uint32_t w = add_res[e].w;
+    flag[e] = ((reach_add[e] & REACH_ON) && (w & 0xFFu) == KDTN_KIND_PHYSICAL && ((w >> 8) & 0xFFu) == 0) ? 1u : 0u;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_remote_phys_scatter(const uint32_t* flag, const uint64_t* pos, uint32_t na,
+                                                               uint32_t* phys_idx) {
+    const uint32_t e = blockIdx.x * BLOCK + threadIdx.x;
+    if (e < na && flag[e]) phys_idx[pos[e]] = e;
+}
+
+// the strings of message m as kdict arena ranges, in field order net_ns, intf_name, intf_ip,
+// peer_vtep, kube_ns, name; record j carries the properties
+struct RemoteMsg {
+    uint32_t b[6], l[6];
+    int32_t vni;
+    uint32_t j;
+    bool ok;                        // every string valid UTF-8
+};
+
+KD_INLINE RemoteMsg remote_msg(const RemoteIn& r, uint32_t m) {
+    RemoteMsg q;
+    const bool remote = m < r.n_remote;
+    const uint32_t e = remote ? r.rem_idx[m] : r.phys_idx[m - r.n_remote];
+    const uint32_t t = entry_topo(r.add_off, r.T, e);
+    const uint32_t j = r.add_idx[e];
+    const uint4 res = r.add_res[e];
+    const uint32_t peer_pod = r.N.key(KDTN_K_PEER_POD, j);
+    uint32_t id[6];
+    if (remote) {                                   // UpdateRemote: the peer daemon's side
+        id[0] = r.pods[res.x].w & 0x7FFFFFFFu;      // peerPod.NetNs
+        id[1] = r.N.key(KDTN_K_PEER_INTF, j);
+        id[2] = r.N.key(KDTN_K_PEER_IP, j);
+        id[3] = r.t_src[t];                         // localPod.SrcIp
+    } else {                                        // physical: the local pod's side
+        id[0] = r.t_netns[t];
+        id[1] = r.N.key(KDTN_K_LOCAL_INTF, j);
+        id[2] = r.N.key(KDTN_K_LOCAL_IP, j);
+        id[3] = peer_pod;                           // TrimPrefix(PeerPod, "physical/") below
+    }
+    id[4] = r.t_ns[t];                              // localPod.KubeNs
+    id[5] = peer_pod;
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        q.b[k] = r.kd_offs[id[k]];
+        q.l[k] = r.kd_offs[id[k] + 1];
+        ok = ok && !bit(r.kd_utf8, id[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) q.l[k] -= q.b[k];
+    if (!remote) {
+        q.b[3] += 9u;
+        q.l[3] -= 9u;
+    }
+#pragma unroll
+    for (int k = 0; k < KDTN_NPROP; ++k) ok = ok && !bit(r.pd_utf8, r.N.prop(k, j));
+    q.vni = (int32_t)res.y;
+    q.j = j;
+    q.ok = ok;
+    return q;
+}
+
+KD_INLINE uint32_t remote_props_size(const RemoteIn& r, uint32_t j) {
+    uint32_t p = 0;
+#pragma unroll
+    for (int k = 0; k < KDTN_NPROP; ++k) p += str_field(slen(r.pd_offs, r.N.prop(k, j)));
+    const uint32_t gap = r.N.gap(j);
+    if (gap) p += 1u + vlen(gap);
+    return p;
+}
+
+KD_INLINE uint32_t remote_body_size(const RemoteIn& r, const RemoteMsg& q, uint32_t* psz) {
+    uint32_t n = 0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) n += str_field(q.l[k]);
+    if (q.vni) n += 1u + vlen((uint64_t)(int64_t)q.vni);
+    const uint32_t p = remote_props_size(r, q.j);
+    *psz = p;
+    return n + 1u + vlen(p) + p;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_remote_sizes(RemoteIn r, uint32_t* size) {
+    const uint32_t m = blockIdx.x * BLOCK + threadIdx.x;
+    if (m >= r.n_msgs) return;
+    const RemoteMsg q = remote_msg(r, m);
+    uint32_t psz;
+    const uint32_t body = remote_body_size(r, q, &psz);
+    size[m] = q.ok ? vlen(body) + body : 0u;
+}
+
+KD_INLINE void write_remote(Sink& o, const RemoteIn& r, const RemoteMsg& q) {
+    uint32_t psz;
+    o.varint(remote_body_size(r, q, &psz));
+#pragma unroll
+    for (int k = 0; k < 5; ++k) o.strb((uint32_t)k + 1, r.kd_bytes, q.b[k], q.l[k]);
+    if (q.vni) {
+        o.byte(6u << 3);
+        o.varint((uint64_t)(int64_t)q.vni);
+    }
+    o.byte(7u << 3 | 2u);
+    o.varint(psz);
+    uint32_t pb[KDTN_NPROP], pl[KDTN_NPROP];
+#pragma unroll
+    for (int k = 0; k < KDTN_NPROP; ++k) {
+        const uint32_t id = r.N.prop(k, q.j);
+        pb[k] = id ? r.pd_offs[id] : 0u;
+        pl[k] = id ? r.pd_offs[id + 1] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < KDTN_NPROP; ++k) pl[k] -= pb[k];
+    for (int k = 0; k < KDTN_NPROP; ++k) {
+        if (k == KDTN_P_DUPLICATE) {
+            const uint32_t gap = r.N.gap(q.j);
+            if (gap) {
+                o.byte(7u << 3);
+                o.varint(gap);
+            }
+        }
+        o.strb((uint32_t)(k < KDTN_P_DUPLICATE ? k + 1 : k + 2), r.pd_bytes, pb[k], pl[k]);
+    }
+    o.strb(8, r.kd_bytes, q.b[5], q.l[5]);
+}
+
+// one thread per message; a wave's messages are one contiguous range, assembled in the
+// wave's LDS image and stored with coalesced dword stores (as k_wire_write)
+__global__ void __launch_bounds__(BLOCK) k_remote_write(RemoteIn r, const uint64_t* off, uint8_t* arena) {
+    __shared__ uint32_t img[BLOCK / 64][WIRE_IMG / 4];
+    const uint32_t m = blockIdx.x * BLOCK + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    bool on = m < r.n_msgs;
+    uint64_t s0 = 0, s1 = 0;
+    if (on) {
+        s0 = off[m];
+        s1 = off[m + 1];
+        on = s1 > s0;                               // empty: Marshal error
+    }
+    uint64_t r0 = on ? s0 : ~0ull, r1 = on ? s1 : 0ull;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint64_t a = __shfl_xor(r0, d, 64), b = __shfl_xor(r1, d, 64);
+        r0 = a < r0 ? a : r0;
+        r1 = b > r1 ? b : r1;
+    }
+    if (r1 <= r0) return;                           // no active lane (wave-uniform)
+    RemoteMsg q{};
+    if (on) q = remote_msg(r, m);
+    const uint32_t lead = (uint32_t)(r0 & 3u);
+    if (r1 - r0 + lead > (uint64_t)WIRE_IMG) {      // too large for the image: direct byte stores
+        if (on) {
+            Sink o{arena + s0};
+            write_remote(o, r, q);
+        }
+        return;
+    }
+    uint8_t* im = reinterpret_cast<uint8_t*>(img[threadIdx.x >> 6]);
+    if (on) {
+        Sink o{im + lead + (uint32_t)(s0 - r0)};
+        write_remote(o, r, q);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint64_t a0 = r0 - lead;
+    const uint32_t nw = (uint32_t)((r1 - a0 + 3) >> 2);
+    const uint32_t* iw = img[threadIdx.x >> 6];
+    for (uint32_t k = lane; k < nw; k += 64) {
+        const uint64_t ga = a0 + 4ull * k;
+        const uint32_t v = iw[k];
+        if (ga >= r0 && ga + 4 <= r1) {
+            *reinterpret_cast<uint32_t*>(arena + ga) = v;
+        } else {
+            for (uint32_t c = 0; c < 4; ++c)
+                if (ga + c >= r0 && ga + c < r1) arena[ga + c] = (uint8_t)(v >> (8 * c));
+        }
+    }
+}
+
 }  // namespace kdtn

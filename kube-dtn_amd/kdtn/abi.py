@@ -126,6 +126,16 @@ class TcArgv(C.Structure):
     _fields_ = [("bytes", C.c_void_p), ("cap", C.c_uint64), ("off", C.c_void_p), ("n_bytes", C.c_uint64)]
 
 
+class RemoteInfo(C.Structure):
+    _fields_ = [("n_msgs", C.c_uint32), ("n_remote", C.c_uint32), ("n_bytes", C.c_uint64),
+                ("n_tc_bytes", C.c_uint64)]
+
+
+class RemotePods(C.Structure):
+    _fields_ = [("bytes", C.c_void_p), ("cap", C.c_uint64), ("off", C.c_void_p), ("entry", C.c_void_p),
+                ("tc_bytes", C.c_void_p), ("tc_cap", C.c_uint64), ("tc_off", C.c_void_p), ("msg_cap", C.c_uint32)]
+
+
 class PodTable(C.Structure):
     _fields_ = [("n", C.c_uint32), ("ns", u32p), ("name", u32p), ("src_ip", u32p), ("net_ns", u32p),
                 ("flags", u8p)]
@@ -178,7 +188,7 @@ EXPORTS = ["kdtn_version", "kdtn_strerror", "kdtn_err_name", "kdtn_init", "kdtn_
            "kdtn_host_free", "kdtn_epoch_fanout", "kdtn_epoch_tc", "kdtn_epoch_download_tc",
            "kdtn_json_upload", "kdtn_json_ingest", "kdtn_ingest_download", "kdtn_topology_shard",
            "kdtn_comm_set_ranks", "kdtn_pods_export", "kdtn_pods_import", "kdtn_json_ingest_shard",
-           "kdtn_ingest_shard_topos"]
+           "kdtn_ingest_shard_topos", "kdtn_epoch_remote_encode", "kdtn_epoch_download_remote"]
 
 
 def ptr(a: np.ndarray, t):

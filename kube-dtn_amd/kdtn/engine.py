@@ -99,6 +99,8 @@ def lib() -> C.CDLL:
         "kdtn_comm_set_ranks": (C.c_int, [vp, C.c_int, C.c_int]),
         "kdtn_pods_export": (C.c_int, [vp, vp]),
         "kdtn_pods_import": (C.c_int, [vp, vp, C.c_uint64]),
+        "kdtn_epoch_remote_encode": (C.c_int, [vp, C.POINTER(abi.RemoteInfo)]),
+        "kdtn_epoch_download_remote": (C.c_int, [vp, C.POINTER(abi.RemotePods)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -358,6 +360,26 @@ class Engine:
         f.node_cap, f.idx_cap = node.size, idx.size
         _check(lib().kdtn_epoch_fanout(self._ctx, C.byref(f)), "kdtn_epoch_fanout")
         return node[:f.n_nodes], off, idx[:f.n_send]
+
+    def remote_encode(self) -> abi.RemoteInfo:
+        """kdtn_epoch_remote_encode: marshal the epoch's RemotePod messages on the GPU."""
+        info = abi.RemoteInfo()
+        _check(lib().kdtn_epoch_remote_encode(self._ctx, C.byref(info)), "kdtn_epoch_remote_encode")
+        return info
+
+    def remote_pods(self):
+        """RemotePod messages of the last epoch: (arena uint8, off uint64[n+1], entry uint32[n],
+        n_remote, tc arena uint8, tc_off uint64[n+1]); messages [0, n_remote) follow the
+        fan-out order (fanout()), the rest are the physical peers' local Updates."""
+        info = self.remote_encode()
+        n = info.n_msgs
+        arena, tca = np.zeros(max(info.n_bytes, 1), np.uint8), np.zeros(max(info.n_tc_bytes, 1), np.uint8)
+        off, tc_off = np.zeros(n + 1, np.uint64), np.zeros(n + 1, np.uint64)
+        entry = np.zeros(max(n, 1), np.uint32)
+        o = abi.RemotePods(arena.ctypes.data, arena.size, off.ctypes.data, entry.ctypes.data, tca.ctypes.data,
+                           tca.size, tc_off.ctypes.data, n)
+        _check(lib().kdtn_epoch_download_remote(self._ctx, C.byref(o)), "kdtn_epoch_download_remote")
+        return arena[:info.n_bytes], off, entry[:n], int(info.n_remote), tca[:info.n_tc_bytes], tc_off
 
     def vni_apply(self) -> Vnis:
         """kdtn_epoch_vni_apply: the daemons' VxlanManager maps after the last epoch's reached

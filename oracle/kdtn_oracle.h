@@ -84,6 +84,15 @@ uint32_t or_fanout(const kdtn_batches* b, uint32_t T, uint32_t* node, uint32_t* 
 /* SetVethQdiscs' tc argv per add (veth/VXLAN kinds) then update entry with a TBF and no
  * error (common/qdisc.go:252-266); off has n_add + n_upd + 1 entries. */
 uint64_t or_tc_epoch(const kdtn_epoch_in* in, const kdtn_batches* b, uint8_t* bytes, uint64_t* off);
+/* RemotePod messages of the epoch: the UpdateRemote payloads of or_fanout (first n_remote,
+ * fan-out order) then the PHYSICAL peers' local Update payloads (add-list order). entry[m]
+ * = add entry of message m; message m = bytes[off[m], off[m+1]) (varint length + RemotePod;
+ * empty = Marshal error); the receiving daemon's tc argv = tc[tc_off[m], tc_off[m+1]).
+ * peer_netns: net_ns id per peer_topo index. Capacities: entry >= n_add, off/tc_off >=
+ * n_add + 1; bytes / tc NULL = sizes only. Returns the message count. */
+uint32_t or_remote_epoch(const kdtn_epoch_in* in, const kdtn_batches* b, const uint32_t* peer_netns,
+                         uint32_t* entry, uint32_t* n_remote, uint8_t* bytes, uint64_t* off,
+                         uint8_t* tc, uint64_t* tc_off, uint64_t* n_bytes, uint64_t* n_tc);
 /* VxlanManager maps after the epoch's reached entries (deletes, then first-wins adds);
  * returns the entry count (out_* may be NULL to count). pod_netns: net_ns id per global pod. */
 uint32_t or_vni_apply(const kdtn_batches* b, uint32_t T, const uint32_t* t_src, const uint32_t* t_netns,

@@ -337,6 +337,135 @@ uint64_t or_tc_epoch(const kdtn_epoch_in* in, const kdtn_batches* b, uint8_t* by
 }
 
 /* ======================================================================================
+ * RemotePod messages (proto/v1/kube_dtn.proto:65-79: net_ns 1, intf_name 2, intf_ip 3,
+ * peer_vtep 4, kube_ns 5, int32 vni 6, properties 7, name 8). Two sources:
+ *  - UpdateRemote (common/utils.go:39-51), sent by a reached cross-node addLink after its
+ *    own SetupVxLan (handler.go:419-453): {NetNs: peerPod.NetNs, IntfName: link.PeerIntf,
+ *    IntfIp: link.PeerIp, PeerVtep: localPod.SrcIp, Vni, KubeNs: localPod.KubeNs,
+ *    Properties: link.Properties, Name: link.PeerPod}; messages in or_fanout order (per
+ *    destination daemon, add-list order within);
+ *  - the physical peer's local Update (handler.go:348-371), built by every reached PHYSICAL
+ *    addLink whose MakeVeth passed: {NetNs: localPod.NetNs, IntfName: link.LocalIntf,
+ *    IntfIp: link.LocalIp, PeerVtep: PeerPod[len("physical/"):], Vni, KubeNs, Properties,
+ *    Name: link.PeerPod}; after the remote ones, in add-list order.
+ * localPod is the LinksBatchQuery's LocalPod (controllers/topology_controller.go:180-188:
+ * topology name / status src_ip / status net_ns / namespace); peerPod.NetNs is the peer
+ * topology's status.net_ns (ToProtoPod, handler.go:62-88). Properties is always a non-nil
+ * message (Link.ToProto), so field 7 is always written. Each message is preceded by its
+ * varint length (a delimited stream); a message with a string that is not valid UTF-8
+ * fails to marshal and is empty (no prefix). Next to each remote message: the receiving
+ * daemon's SetVethQdiscs tc argv on IntfName (Update → SetupVxLan → MakeQdiscs →
+ * SetVethQdiscs, daemon/vxlan/vxlan.go:31-51), present when the link has a TBF and the
+ * daemon's CreateOrUpdate accepts IntfIp (remote_err == 0); physical messages carry none
+ * (their tc runs on LocalIntf and is or_tc_epoch's slot 2e).
+ * ==================================================================================== */
+typedef struct { wstr s[6]; int32_t vni; wrec r; } rpod;   /* s: net_ns intf_name intf_ip peer_vtep kube_ns name */
+
+static uint32_t rpod_size(const rpod* m) {
+    uint32_t n = 0;
+    for (int k = 0; k < 5; k++) n += str_size(m->s[k]);
+    if (m->vni) n += 1 + vlen((uint64_t)(int64_t)m->vni);
+    uint32_t ps = props_size(m->r);
+    n += 1 + vlen(ps) + ps;
+    n += str_size(m->s[5]);
+    return n;
+}
+static int rpod_utf8_ok(const rpod* m) {
+    for (int k = 0; k < 6; k++)
+        if (!or_utf8_valid(m->s[k].p, m->s[k].n)) return 0;
+    for (int k = 0; k < KDTN_NPROP; k++) {
+        wstr q = wget(&m->r.in->pdict, m->r.L->prop[k][m->r.j]);
+        if (!or_utf8_valid(q.p, q.n)) return 0;
+    }
+    return 1;
+}
+static uint8_t* put_rpod(uint8_t* p, const rpod* m) {
+    for (int k = 0; k < 5; k++) p = put_str(p, (uint32_t)k + 1, m->s[k]);
+    if (m->vni) {
+        *p++ = 6 << 3 | 0;
+        p = put_varint(p, (uint64_t)(int64_t)m->vni);
+    }
+    *p++ = 7 << 3 | 2;
+    p = put_varint(p, props_size(m->r));
+    for (int k = 0; k < KDTN_NPROP; k++) {
+        if (PROP_FIELD[k] == 8 && m->r.L->gap[m->r.j]) {
+            *p++ = 7 << 3 | 0;
+            p = put_varint(p, m->r.L->gap[m->r.j]);
+        }
+        p = put_str(p, PROP_FIELD[k], wget(&m->r.in->pdict, m->r.L->prop[k][m->r.j]));
+    }
+    return put_str(p, 8, m->s[5]);
+}
+
+uint32_t or_remote_epoch(const kdtn_epoch_in* in, const kdtn_batches* b, const uint32_t* peer_netns,
+                         uint32_t* entry, uint32_t* n_remote, uint8_t* bytes, uint64_t* off,
+                         uint8_t* tc, uint64_t* tc_off, uint64_t* n_bytes, uint64_t* n_tc) {
+    const uint32_t T = in->topos.n, na = b->add_off[T], nu = b->upd_off[T];
+    uint32_t* node = (uint32_t*)malloc(sizeof(uint32_t) * (na + 1));
+    uint32_t* noff = (uint32_t*)malloc(sizeof(uint32_t) * (na + 2));
+    uint32_t* topo = (uint32_t*)malloc(sizeof(uint32_t) * (na + 1));
+    uint8_t* ra = (uint8_t*)malloc(na + 1);
+    uint8_t* ru = (uint8_t*)malloc(nu + 1);
+    uint32_t nn = 0;
+    const uint32_t nr = or_fanout(b, T, node, noff, entry, &nn);
+    or_reach(b, T, ra, ru);
+    for (uint32_t t = 0; t < T; t++)
+        for (uint32_t e = b->add_off[t]; e < b->add_off[t + 1]; e++) topo[e] = t;
+    uint32_t n = nr;
+    for (uint32_t e = 0; e < na; e++)
+        if ((ra[e] & 1) && b->add_res[e].kind == KDTN_KIND_PHYSICAL && !b->add_res[e].err) entry[n++] = e;
+    uint64_t pos = 0, tpos = 0;
+    for (uint32_t m = 0; m < n; m++) {
+        const uint32_t e = entry[m], t = topo[e], j = b->add_idx[e];
+        const kdtn_link_table* L = &in->desired;
+        rpod q;
+        q.r.in = in;
+        q.r.L = L;
+        q.r.j = j;
+        q.vni = b->add_res[e].vni;
+        q.s[4] = wget(&in->kdict, in->topos.ns[t]);
+        q.s[5] = wget(&in->kdict, L->key[KDTN_K_PEER_POD][j]);
+        if (m < nr) {
+            q.s[0] = wget(&in->kdict, peer_netns[b->add_res[e].peer_topo]);
+            q.s[1] = wget(&in->kdict, L->key[KDTN_K_PEER_INTF][j]);
+            q.s[2] = wget(&in->kdict, L->key[KDTN_K_PEER_IP][j]);
+            q.s[3] = wget(&in->kdict, in->topos.src_ip[t]);
+        } else {
+            q.s[0] = wget(&in->kdict, in->topos.net_ns[t]);
+            q.s[1] = wget(&in->kdict, L->key[KDTN_K_LOCAL_INTF][j]);
+            q.s[2] = wget(&in->kdict, L->key[KDTN_K_LOCAL_IP][j]);
+            q.s[3] = q.s[5];
+            q.s[3].p += 9;                                   /* strings.TrimPrefix "physical/" */
+            q.s[3].n -= 9;
+        }
+        off[m] = pos;
+        if (rpod_utf8_ok(&q)) {
+            const uint32_t sz = rpod_size(&q);
+            if (bytes) {
+                uint8_t* w = put_varint(bytes + pos, sz);
+                put_rpod(w, &q);
+            }
+            pos += vlen(sz) + sz;
+        }
+        tc_off[m] = tpos;
+        const kdtn_qdisc* qd = &b->add_qdisc[e];
+        if (m < nr && qd->has_tbf && !b->add_res[e].remote_err)
+            tpos += tc_one(in, j, KDTN_K_PEER_INTF, qd, tc ? tc + tpos : NULL);
+    }
+    off[n] = pos;
+    tc_off[n] = tpos;
+    *n_remote = nr;
+    *n_bytes = pos;
+    *n_tc = tpos;
+    free(node);
+    free(noff);
+    free(topo);
+    free(ra);
+    free(ru);
+    return n;
+}
+
+/* ======================================================================================
  * VxlanManager state after the epoch (daemon/vxlan/manager.go:57-63 Add / Delete as
  * sync.Map Store / Delete): delLink deletes VNI 5000+uid on the local node when Get(vni) is
  * the local pod's netns (daemon/kubedtn/handler.go:480-487); a cross-node addLink stores

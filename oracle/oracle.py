@@ -239,6 +239,34 @@ def tc_epoch(inp: EpochInput, out: BatchesOut):
     return arena[:int(n)], off
 
 
+def remote_epoch(inp: EpochInput, out: BatchesOut, peer_netns=None):
+    """RemotePod messages of an epoch (or_remote_epoch): (arena uint8, off uint64[n+1],
+    entry uint32[n], n_remote, tc arena uint8, tc_off uint64[n+1]). The first n_remote are
+    the UpdateRemote payloads in fan-out order, the rest the PHYSICAL local Updates.
+    peer_netns: net_ns id per peer_topo index (default: this epoch's topologies)."""
+    L = _wire_lib()
+    if not getattr(L, "_remote_bound", False):
+        L.or_remote_epoch.argtypes = [C.POINTER(abi.EpochIn), C.POINTER(abi.Batches), C.c_void_p, C.c_void_p,
+                                      C.POINTER(C.c_uint32), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                      C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        L.or_remote_epoch.restype = C.c_uint32
+        L._remote_bound = True
+    cin = inp.to_c()
+    b = out.to_c((max(len(out.del_idx), 1), max(len(out.add_idx), 1), max(len(out.upd_idx), 1)))
+    b.n_del, b.n_add, b.n_upd = len(out.del_idx), len(out.add_idx), len(out.upd_idx)
+    pn = np.ascontiguousarray(inp.topos.net_ns if peer_netns is None else peer_netns, np.uint32)
+    na = max(len(out.add_idx), 1)
+    entry = np.zeros(na, np.uint32)
+    off, tc_off = np.zeros(na + 1, np.uint64), np.zeros(na + 1, np.uint64)
+    nr, nb, nt = C.c_uint32(), C.c_uint64(), C.c_uint64()
+    args = lambda by, tc: (C.byref(cin), C.byref(b), pn.ctypes.data, entry.ctypes.data, C.byref(nr), by,
+                           off.ctypes.data, tc, tc_off.ctypes.data, C.byref(nb), C.byref(nt))
+    L.or_remote_epoch(*args(None, None))
+    arena, tca = np.zeros(max(nb.value, 1), np.uint8), np.zeros(max(nt.value, 1), np.uint8)
+    n = L.or_remote_epoch(*args(arena.ctypes.data, tca.ctypes.data))
+    return arena[:nb.value], off[:n + 1], entry[:n], int(nr.value), tca[:nt.value], tc_off[:n + 1]
+
+
 # ---- CR ingest (kdtn_oracle_json.c) ------------------------------------------------------
 class JsonTables(C.Structure):
     _fields_ = [("json_err", C.c_int32), ("err_offset", C.c_uint64),

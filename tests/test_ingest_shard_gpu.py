@@ -75,20 +75,27 @@ def test_sharded_ingest_equals_unsharded(config, nshards):
         eng.close()
 
 
-def test_sharded_ingest_refuses_plain_ingest_until_reset():
-    """a context left as rank r of G takes kdtn_json_ingest only after kdtn_comm_set_ranks(1, 0)"""
-    from kdtn import Engine, KdtnError, abi, synth
+def test_sharded_ingest_rank_setup_ends_with_next_ingest():
+    """A sharded ingest leaves the context as rank r of G for its own epoch only: the next
+    plain ingest (or upload) restores the single-shard setup, so it decodes the whole
+    document and the VXLAN apply (single-shard contexts) works again."""
+    from kdtn import Engine, synth
     inp = synth.make(1)
     doc = synth.topology_list_json(inp)
     eng = Engine(device=0, tick_in_usec=TICK)
     try:
-        eng.ingest(doc, shard=(2, 1))
-        with pytest.raises(KdtnError) as e:
-            eng.ingest(doc)
-        assert e.value.code == abi.EINVAL
-        eng.set_ranks(1, 0)
+        info = eng.ingest(doc, shard=(2, 1))
+        assert info.n_topos < inp.topos.n
         info = eng.ingest(doc)
         assert info.n_topos == inp.topos.n
         assert (eng.ingest_doc_index() == np.arange(inp.topos.n)).all()
+        eng.run()
+        eng.sync()
+        eng.vni_apply()
+        eng.ingest(doc, shard=(2, 0))
+        eng.upload(inp)                         # a plain upload after a sharded ingest
+        eng.run()
+        eng.sync()
+        assert len(eng.download().upd_idx) == inp.desired.n
     finally:
         eng.close()

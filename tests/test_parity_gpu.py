@@ -404,6 +404,34 @@ def test_remote_fanout_grouping(engine):
     assert _fanout_same(engine, synth.make(4, pods_per_shard=5000), "config 4") > 1000
 
 
+def _remote_same(engine, inp, ctx):
+    out = engine.reconcile(inp)
+    got = engine.remote_pods()
+    want = O.remote_epoch(inp, O.reconcile(inp, tick=TICK))
+    names = ("arena", "off", "entry", "n_remote", "tc", "tc_off")
+    for name, g, w in zip(names, got, want):
+        if name == "n_remote":
+            assert g == w, (ctx, name)
+        else:
+            assert np.array_equal(np.asarray(g), np.asarray(w)), (ctx, name)
+    return got[3], len(got[2]) - got[3]
+
+
+def test_remote_pod_messages(engine):
+    """RemotePod request bodies (UpdateRemote payloads in fan-out order, then the physical
+    peers' local Updates) and the receiving daemons' tc argv, bit-exact against the oracle
+    (pinned to the Python protobuf runtime, tests/test_wire_cpu.py) on adversarial random
+    epochs (invalid UTF-8, negative uids / VNIs, 2-byte length varints) and configs 2 and 4."""
+    from helpers import wire_epoch_input
+    for seed in range(4):
+        _remote_same(engine, wire_epoch_input(seed, T=120)[1], f"wire seed {seed}")
+        _remote_same(engine, random_epoch_input(seed + 40, T=150, p_err=0.1)[1], f"seed {seed}")
+    nr, _ = _remote_same(engine, synth.make(2, pods_per_shard=20000), "config 2")
+    assert nr > 100000
+    nr, nph = _remote_same(engine, synth.make(4, pods_per_shard=5000), "config 4")
+    assert nr > 1000 and nph > 0
+
+
 def test_tc_argv_synthesis(engine):
     """`tc qdisc add ... tbf` argv per AddLinks / UpdateLinks entry (common/qdisc.go:252-266)
     equals the oracle's on random epochs and the synthetic configs."""

@@ -51,8 +51,9 @@ def test_vni_resident_chain(config):
             else:
                 keep = inp.vnis
                 inp.vnis = Vnis.keep_resident()
-                eng.upload(inp)
+                eng.upload(inp, kd_keep)                       # the map's ids: a kept prefix
                 inp.vnis = keep
+            kd_keep = inp.kdict.n
             eng.run()
             eng.sync()
             got_out = eng.download()
@@ -67,3 +68,55 @@ def test_vni_resident_chain(config):
                 cs.advance()
                 inp = cs.epoch_input()
         assert hits > 0
+
+
+def test_rerun_after_apply_keeps_epoch_start_snapshot():
+    """run → vni_apply → run on one upload: the second run decides vni_hit against the same
+    epoch-start snapshot (identical outputs), a second apply gives the same map, and the
+    next upload with KDTN_VNI_RESIDENT starts from the applied map."""
+    inp = synth.make(4, total_pods=3000)
+    want_out = O.reconcile(inp, tick=15.625)
+    want = O.vni_apply(inp, want_out)
+    with Engine(device=0, tick_in_usec=15.625) as eng:
+        eng.upload(inp)
+        eng.run()
+        eng.sync()
+        first = eng.download()
+        assert not first.mismatches(want_out)
+        got = eng.vni_apply()
+        assert same((got.node, got.vni, got.net_ns), want)
+        eng.run()
+        eng.sync()
+        assert not eng.download().mismatches(want_out), "re-run saw the applied map"
+        got2 = eng.vni_apply()
+        assert same((got2.node, got2.vni, got2.net_ns), want)
+        keep = inp.vnis
+        inp.vnis = Vnis.keep_resident()
+        eng.upload(inp, inp.kdict.n)
+        inp.vnis = Vnis(*[np.array(a, copy=True) for a in want])
+        next_want = O.reconcile(inp, tick=15.625)
+        inp.vnis = keep
+        eng.run()
+        eng.sync()
+        assert not eng.download().mismatches(next_want)
+
+
+def test_resident_map_needs_kept_dictionary():
+    """KDTN_VNI_RESIDENT is refused when the upload does not keep the dictionary the map's ids
+    were made for, and always for a JSON ingest (its dictionary is the engine's own)."""
+    from kdtn import KdtnError, abi
+    inp = synth.make(4, total_pods=2000)
+    with Engine(device=0, tick_in_usec=15.625) as eng:
+        eng.reconcile(inp)
+        eng.vni_apply()
+        keep = inp.vnis
+        inp.vnis = Vnis.keep_resident()
+        try:
+            with pytest.raises(KdtnError) as e:
+                eng.upload(inp)                                # kdict_keep = 0
+            assert e.value.code == abi.EINVAL
+            with pytest.raises(KdtnError) as e:
+                eng.ingest(synth.topology_list_json(synth.make(1)), vnis=Vnis.keep_resident())
+            assert e.value.code == abi.EINVAL
+        finally:
+            inp.vnis = keep

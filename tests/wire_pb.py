@@ -1,6 +1,7 @@
 """Independent encoder for the wire-format checks: the Python protobuf runtime
-(google.protobuf, upb) driven by a descriptor that restates proto/v1/kube_dtn.proto:8-53,65-68
-(Pod, Link, LinkProperties, LinksBatchQuery; field numbers and types as in the reference).
+(google.protobuf, upb) driven by a descriptor that restates proto/v1/kube_dtn.proto:8-53,65-79
+(Pod, Link, LinkProperties, LinksBatchQuery, RemotePod; field numbers and types as in the
+reference).
 
 `batch_bytes` builds the request Reconcile sends for one list of one Topology
 (controllers/topology_controller.go:180-188, 223-231, 266-274): LocalPod is always set, every
@@ -31,6 +32,9 @@ _SCHEMA = {
                        ("corrupt_prob", 12, _STR), ("corrupt_corr", 13, _STR)],
     "LinksBatchQuery": [("local_pod", 1, _MSG, ".proto.v1.Pod"),
                         ("links", 2, _MSG, ".proto.v1.Link", _REP)],
+    "RemotePod": [("net_ns", 1, _STR), ("intf_name", 2, _STR), ("intf_ip", 3, _STR),
+                  ("peer_vtep", 4, _STR), ("kube_ns", 5, _STR), ("vni", 6, _F.TYPE_INT32),
+                  ("properties", 7, _MSG, ".proto.v1.LinkProperties"), ("name", 8, _STR)],
 }
 
 
@@ -96,3 +100,44 @@ def epoch_bytes(inp, out):
             e0, e1 = int(offs[lst][t]), int(offs[lst][t + 1])
             res[(lst, t)] = batch_bytes(inp, t, lst, idxs[lst][e0:e1])
     return res
+
+
+def _varint(v: int) -> bytes:
+    out = bytearray()
+    while v >= 0x80:
+        out.append((v & 0x7F) | 0x80)
+        v >>= 7
+    out.append(v)
+    return bytes(out)
+
+
+def remote_pod_bytes(inp, out, e: int, t: int, physical: bool, peer_netns) -> bytes | None:
+    """Length-delimited RemotePod of add entry e (topology t): UpdateRemote's payload
+    (common/utils.go:42-51) or, for a physical peer, the local Update's
+    (daemon/kubedtn/handler.go:353-362); None on a Marshal error (invalid UTF-8)."""
+    kd, pd, T, L = inp.kdict, inp.pdict, inp.topos, inp.desired
+    j = int(out.add_idx[e])
+    r = out.add_res[e]
+    key = lambda c: kd.get(int(L.key[abi.KEY_COLS.index(c), j]))
+    try:
+        m = _C["RemotePod"]()
+        if physical:
+            m.net_ns = _s(kd, T.net_ns[t])
+            m.intf_name, m.intf_ip = key("local_intf").decode(), key("local_ip").decode()
+            m.peer_vtep = key("peer_pod")[len(b"physical/"):].decode()
+        else:
+            m.net_ns = _s(kd, peer_netns[int(r["peer_topo"])])
+            m.intf_name, m.intf_ip = key("peer_intf").decode(), key("peer_ip").decode()
+            m.peer_vtep = _s(kd, T.src_ip[t])
+        m.kube_ns = _s(kd, T.ns[t])
+        m.vni = int(r["vni"])
+        p = m.properties
+        p.SetInParent()
+        for k, col in enumerate(abi.PROP_COLS):
+            setattr(p, col, _s(pd, L.prop[k, j]))
+        p.gap = int(L.gap[j])
+        m.name = key("peer_pod").decode()
+        b = m.SerializeToString()
+        return _varint(len(b)) + b
+    except (UnicodeDecodeError, ValueError):
+        return None

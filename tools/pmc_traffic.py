@@ -11,8 +11,24 @@ the workload matches.
 import collections
 import csv
 import glob
+import hashlib
 import json
+import os
 import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# the sources bench.py's kernel_src_sha16() hashes: a summary is attached to a bench line only
+# when it was measured on the same k_reconcile sources
+KERNEL_SOURCES = ("kube-dtn_amd/csrc/kdtn_kernels.hip", "kube-dtn_amd/csrc/kdtn_kernels.h",
+                  "kube-dtn_amd/csrc/kdtn_parse.h", "kube-dtn_amd/csrc/kdtn_engine.hip")
+
+
+def kernel_src_sha16() -> str:
+    h = hashlib.sha256()
+    for p in KERNEL_SOURCES:
+        with open(os.path.join(ROOT, p), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
 
 
 def main():
@@ -25,7 +41,8 @@ def main():
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"].split("(")[0].replace("kdtn::", "").replace("void ", "")
             vals[(k, r["Counter_Name"])].append(float(r["Counter_Value"]))
-    out = {"source": root, "links_per_gpu": links, "config": config, "kernels": {}}
+    out = {"source": root, "links_per_gpu": links, "config": config,
+           "kernel_src_sha16": kernel_src_sha16(), "kernels": {}}
     for (k, c), v in sorted(vals.items()):
         if k.startswith("__amd"):
             continue
