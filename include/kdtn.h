@@ -342,6 +342,43 @@ void  kdtn_host_free(void* p);
 int kdtn_make_qdiscs(kdtn_ctx* ctx, const kdtn_strtab* pdict, const kdtn_props_table* props,
                      kdtn_qdisc* out);
 
+/* ---- resident epoch state: status commit and delta upload ----------------------------
+ * Reconcile ends with Status.Links = Spec.Links for a Topology it saw for the first time
+ * (CREATED) or whose DelLinks / AddLinks / UpdateLinks RPCs all succeeded; a failed RPC
+ * returns before the status write (controllers/topology_controller.go:81-85, 93-116, 125-138).
+ * kdtn_epoch_commit applies that to the context's resident link stores on the GPU: the
+ * realised store (status.links) becomes, per Topology, its desired segment when committed,
+ * else its old realised segment (KDTN_TOPO_STATUS_NIL follows: a nil spec commits a nil
+ * status). mask = NULL commits what the engine predicts (CREATED, and DIFF Topologies none
+ * of whose batch entries fails — the kdtn_epoch_fanout reach rule; needs a run with RESOLVE
+ * and QDISC); else mask[t] != 0 commits Topology t (the caller saw its RPCs and status
+ * update succeed). Call the output stages (encode, fanout, tc, remote, vni_apply) first:
+ * after a commit the context needs a run. n_committed (may be NULL) = committed Topologies. */
+int kdtn_epoch_commit(kdtn_ctx* ctx, const uint8_t* mask, uint32_t* n_committed);
+
+/* The next epoch's inputs as a delta against the context's resident state (the status
+ * after kdtn_epoch_commit, the previous desired store, the topology rows): only the
+ * Topologies whose spec (or status.src_ip / status.net_ns) changed, and for each of them its
+ * new spec.links as references — a record of the previous desired store by index, or
+ * KDTN_DELTA_NEW | k for inline record k of `records`. The Topology set is unchanged (a new
+ * or deleted Topology needs kdtn_epoch_upload). Dictionaries as kdtn_epoch_in (kdict_keep /
+ * pdict_keep: the kept prefix is not re-uploaded). */
+#define KDTN_DELTA_NEW 0x80000000u
+typedef struct kdtn_epoch_delta {
+    kdtn_strtab     kdict, pdict;
+    uint32_t        kdict_keep, pdict_keep;
+    uint32_t        n_changed;
+    const uint32_t* topo;       /* [n_changed] strictly ascending topology indices            */
+    const uint32_t* src_ip;     /* [n_changed] status.src_ip (kdict id)                        */
+    const uint32_t* net_ns;     /* [n_changed] status.net_ns                                   */
+    const uint8_t*  spec_nil;   /* [n_changed] 1: spec.links nil (no records)                  */
+    const uint32_t* des_off;    /* [n_changed + 1] offsets into ref                            */
+    const uint32_t* ref;        /* [des_off[n_changed]] previous desired record | NEW-tagged   */
+    kdtn_link_table records;    /* inline records                                              */
+    kdtn_vni_table  vnis;       /* VxlanManager snapshot or KDTN_VNI_RESIDENT                  */
+} kdtn_epoch_delta;
+int kdtn_epoch_upload_delta(kdtn_ctx* ctx, const kdtn_epoch_delta* delta);
+
 /* ---- wire encoding of the batches (proto/v1 LinksBatchQuery) ------------------------ */
 /* The request bodies Reconcile sends after CalcDiff: for topology t and list l (0 DelLinks,
  * 1 AddLinks, 2 UpdateLinks) the bytes of proto.Marshal(&pb.LinksBatchQuery{LocalPod:
@@ -507,6 +544,10 @@ int kdtn_json_upload(kdtn_ctx* ctx, const uint8_t* doc, uint64_t n);
 int kdtn_json_ingest(kdtn_ctx* ctx, const kdtn_vni_table* vnis, kdtn_ingest_info* info);
 /* D2H of the decoded tables of the last successful ingest. */
 int kdtn_ingest_download(kdtn_ctx* ctx, kdtn_ingest_tables* out);
+/* Sizes of the context's current epoch tables — after an upload, a delta upload, a commit
+ * or an ingest — into info (n_topos, n_desired, n_realised, dictionary sizes); after it,
+ * kdtn_ingest_download returns those tables (the resident state after a commit). */
+int kdtn_epoch_tables_info(kdtn_ctx* ctx, kdtn_ingest_info* info);
 
 /* Sharded ingest for one rank of nshards (SURVEY §8(e) with §8(f) rank 2). Every controller
  * replica's informer holds the whole Topology store (the controller watches all Topologies,

@@ -116,6 +116,11 @@ struct kdtn_ctx {
     uint32_t rp_n = 0, rp_nr = 0;
     uint64_t rp_bytes = 0, rp_tc_bytes = 0;
     bool rp_done = false;
+    // resident state: commit / delta plans, the delta's arrays and inline records
+    DevBuf st_len, st_base, st_mode, st_flags, st_off64, st_part, st_off32, st_mask, st_chg;
+    DevBuf dl_topo, dl_src, dl_netns, dl_nil, dl_off, dl_ref;
+    DevLinkStore dl_rec;
+    bool tables_cur = false;                   // j_info describes the current tables (kdtn_epoch_tables_info)
     // tc argv
     DevBuf tc_size, tc_off, tc_part, tc_arena;
     uint64_t tc_bytes = 0;
@@ -439,6 +444,39 @@ int check_vnis(kdtn_ctx* c, const kdtn_vni_table& vn, uint32_t D, uint32_t keep)
     return check_ids(vn.net_ns, vn.n, D, "vnis.net_ns");
 }
 
+// Append-only dictionaries: the first *_keep strings equal the previous upload's (the arena
+// offset of the kept prefix is checked against the device copy).
+int check_keep(kdtn_ctx* c, const kdtn_strtab& kd, const kdtn_strtab& pd, uint32_t kk, uint32_t pk) {
+    const uint32_t D = kd.n, P = pd.n;
+    uint32_t dev_off[2] = {0, 0};
+    if (kk <= c->kd_valid && kk && kk <= D)
+        HIP_TRY(hipMemcpyAsync(dev_off, dp<uint32_t>(c->kd_offs) + kk, 4, hipMemcpyDeviceToHost, c->stream));
+    if (pk <= c->pd_valid && pk && pk <= P)
+        HIP_TRY(hipMemcpyAsync(dev_off + 1, dp<uint32_t>(c->pd_offs) + pk, 4, hipMemcpyDeviceToHost, c->stream));
+    if (kk || pk) HIP_TRY(hipStreamSynchronize(c->stream));
+    if (kk > D || pk > P || kk > c->kd_valid || pk > c->pd_valid || (kk && kd.offs[kk] != dev_off[0]) ||
+        (pk && pd.offs[pk] != dev_off[1])) {
+        std::snprintf(g_last_error, sizeof(g_last_error),
+                      "kdict_keep %u / pdict_keep %u: not a prefix of the previous upload's parsed dictionaries "
+                      "(%u / %u strings)", kk, pk, c->kd_valid, c->pd_valid);
+        return KDTN_EINVAL;
+    }
+    return KDTN_OK;
+}
+
+// upload the dictionaries past the kept prefixes and size their parsed tables
+int upload_dicts(kdtn_ctx* c, const kdtn_strtab& kd, const kdtn_strtab& pd, uint32_t kk, uint32_t pk) {
+    c->D = kd.n;
+    c->P = pd.n;
+    c->kd_valid = kk;
+    c->pd_valid = pk;
+    c->kd_from = kk;
+    c->pd_from = pk;
+    TRY(upload_dict(c, c->kd_bytes, c->kd_offs, kd, kk));
+    TRY(upload_dict(c, c->pd_bytes, c->pd_offs, pd, pk));
+    return prepare_dicts(c);
+}
+
 // A sharded ingest's rank setup ends when the next upload or ingest starts.
 void end_shard_ingest(kdtn_ctx* c) {
     if (!c->sh_active) return;
@@ -452,7 +490,7 @@ void end_shard_ingest(kdtn_ctx* c) {
 
 // everything an epoch needs besides its input tables: VNI snapshot, pod tables, work and
 // output buffers (c->D, c->T set; shared by kdtn_epoch_upload and kdtn_json_ingest)
-int prepare_epoch(kdtn_ctx* c, const kdtn_vni_table& vn, uint32_t slice, uint32_t M, uint32_t N) {
+int prepare_vnis(kdtn_ctx* c, const kdtn_vni_table& vn) {
     const uint32_t D = c->D;
     const bool resident = vn.n == KDTN_VNI_RESIDENT;
     const uint32_t V = resident ? c->vres_n : vn.n;
@@ -475,7 +513,12 @@ int prepare_epoch(kdtn_ctx* c, const kdtn_vni_table& vn, uint32_t slice, uint32_
     TRY(ensure(c->v_ents, (size_t)V * 16));
     TRY(ensure(c->v_slots, (size_t)(c->vni_mask + 1) * 4));
     TRY(ensure(c->v_table, (size_t)(c->vni_mask + 1) * 16));
+    return KDTN_OK;
+}
 
+// pod tables, work and output buffers for T = c->T topologies, M realised and N desired records
+int prepare_work(kdtn_ctx* c, uint32_t slice, uint32_t M, uint32_t N) {
+    const uint32_t D = c->D;
     c->slice = slice;
     if ((uint64_t)slice * (uint64_t)c->nranks > POD_INDEX) {
         std::snprintf(g_last_error, sizeof(g_last_error), "pod table of %llu entries exceeds 2^30",
@@ -516,6 +559,11 @@ int prepare_epoch(kdtn_ctx* c, const kdtn_vni_table& vn, uint32_t slice, uint32_
     TRY(ensure(c->upd_qdisc, h * M * 72));
     TRY(ensure(c->add_qdisc, h * N * 72));
     return KDTN_OK;
+}
+
+int prepare_epoch(kdtn_ctx* c, const kdtn_vni_table& vn, uint32_t slice, uint32_t M, uint32_t N) {
+    TRY(prepare_vnis(c, vn));
+    return prepare_work(c, slice, M, N);
 }
 
 // Which batch entries the daemons reach (k_reach; include/kdtn.h): c->f_send (add) and
@@ -650,7 +698,10 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->sh_des.buf, &c->sh_real.buf, &c->vx_ops, &c->vx_dead, &c->vx_slots, &c->vx_node,
                       &c->vx_vni, &c->vx_netns, &c->vx_part, &c->vx_cut, &c->f_cut, &c->vx_vis,
                       &c->r_node, &c->r_vni, &c->r_netns, &c->rp_flag, &c->rp_pos, &c->rp_phys,
-                      &c->rp_msz, &c->rp_moff, &c->rp_tsz, &c->rp_toff, &c->rp_part, &c->rp_arena, &c->rp_tc};
+                      &c->rp_msz, &c->rp_moff, &c->rp_tsz, &c->rp_toff, &c->rp_part, &c->rp_arena, &c->rp_tc,
+                      &c->st_len, &c->st_base, &c->st_mode, &c->st_flags, &c->st_off64, &c->st_part,
+                      &c->st_off32, &c->st_mask, &c->st_chg, &c->dl_topo, &c->dl_src, &c->dl_netns, &c->dl_nil,
+                      &c->dl_off, &c->dl_ref, &c->dl_rec.buf};
     for (DevBuf* b : bufs) release(*b);
     for (int i = 0; i <= kMaxTimers; ++i)
         if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
@@ -699,32 +750,9 @@ int kdtn_epoch_upload(kdtn_ctx* c, const kdtn_epoch_in* in) {
     const uint32_t slice = in->pod_slice ? in->pod_slice : T.n;
     if (slice < T.n) return KDTN_EINVAL;
 
-    // append-only dictionaries: the first *_keep strings equal the previous upload's (the
-    // arena offset of the kept prefix is checked against the device copy)
-    const uint32_t kk = in->kdict_keep, pk = in->pdict_keep;
-    uint32_t dev_off[2] = {0, 0};
-    if (kk <= c->kd_valid && kk && kk <= D)
-        HIP_TRY(hipMemcpyAsync(dev_off, dp<uint32_t>(c->kd_offs) + kk, 4, hipMemcpyDeviceToHost, c->stream));
-    if (pk <= c->pd_valid && pk && pk <= P)
-        HIP_TRY(hipMemcpyAsync(dev_off + 1, dp<uint32_t>(c->pd_offs) + pk, 4, hipMemcpyDeviceToHost, c->stream));
-    if (kk || pk) HIP_TRY(hipStreamSynchronize(c->stream));
-    if (kk > D || pk > P || kk > c->kd_valid || pk > c->pd_valid || (kk && in->kdict.offs[kk] != dev_off[0]) ||
-        (pk && in->pdict.offs[pk] != dev_off[1])) {
-        std::snprintf(g_last_error, sizeof(g_last_error),
-                      "kdict_keep %u / pdict_keep %u: not a prefix of the previous upload's parsed dictionaries "
-                      "(%u / %u strings)", kk, pk, c->kd_valid, c->pd_valid);
-        return KDTN_EINVAL;
-    }
-    c->D = D;
-    c->P = P;
+    TRY(check_keep(c, in->kdict, in->pdict, in->kdict_keep, in->pdict_keep));
     c->T = T.n;
-    c->kd_valid = kk;
-    c->pd_valid = pk;
-    c->kd_from = kk;
-    c->pd_from = pk;
-    TRY(upload_dict(c, c->kd_bytes, c->kd_offs, in->kdict, kk));
-    TRY(upload_dict(c, c->pd_bytes, c->pd_offs, in->pdict, pk));
-    TRY(prepare_dicts(c));
+    TRY(upload_dicts(c, in->kdict, in->pdict, in->kdict_keep, in->pdict_keep));
 
     TRY(upload(c, c->t_ns, T.ns, (size_t)T.n * 4));
     TRY(upload(c, c->t_name, T.name, (size_t)T.n * 4));
@@ -743,6 +771,8 @@ int kdtn_epoch_upload(kdtn_ctx* c, const kdtn_epoch_in* in) {
     c->uploaded = true;
     c->ran = false;
     c->pods_imported = false;
+    c->j_done = false;                             // the tables are no ingest's any more
+    c->tables_cur = false;
     return KDTN_OK;
 }
 
@@ -2003,7 +2033,7 @@ int kdtn_ingest_shard_topos(kdtn_ctx* c, uint32_t* doc_index) {
 }
 
 int kdtn_ingest_download(kdtn_ctx* c, kdtn_ingest_tables* o) {
-    if (!c || !o || !c->j_done) return KDTN_EINVAL;
+    if (!c || !o || !(c->j_done || c->tables_cur)) return KDTN_EINVAL;
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t s = c->stream;
     const kdtn_ingest_info& I = c->j_info;
@@ -2264,6 +2294,195 @@ int kdtn_last_kernel_times(kdtn_ctx* c, const char** names, float* ms, int cap) 
         if (ms) ms[i] = t;
     }
     return n;
+}
+
+// ---- resident epoch state (kdtn_state.hip) ----------------------------------------------
+}  // extern "C"
+
+namespace {
+
+// new u32 offsets of a store from per-topology lengths (st_len) into st_off32; returns the total
+int plan_offsets(kdtn_ctx* c, uint32_t T, uint64_t* total) {
+    hipStream_t s = c->stream;
+    const uint32_t nb = nblocks((uint64_t)T + 1, SCAN_CHUNK);
+    TRY(ensure(c->st_off64, ((size_t)T + 1) * 8));
+    TRY(ensure(c->st_part, (size_t)nb * 8 + 16));
+    TRY(ensure(c->st_off32, ((size_t)T + 1) * 4));
+    k_scan_partial<<<nb, BLOCK, 0, s>>>(dp<uint32_t>(c->st_len), T, dp<uint64_t>(c->st_part));
+    k_scan_top<<<1, BLOCK, 0, s>>>(dp<uint64_t>(c->st_part), nb);
+    k_scan_final<<<nb, BLOCK, 0, s>>>(dp<uint32_t>(c->st_len), T, dp<uint64_t>(c->st_part), dp<uint64_t>(c->st_off64));
+    k_off_narrow<<<nblocks((uint64_t)T + 1), BLOCK, 0, s>>>(dp<uint64_t>(c->st_off64), T, dp<uint32_t>(c->st_off32));
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(total, dp<uint64_t>(c->st_off64) + T, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (*total >= 0x7FFFFFFFull) {
+        std::snprintf(g_last_error, sizeof(g_last_error), "link store of %llu records", (unsigned long long)*total);
+        return KDTN_EINVAL;
+    }
+    return KDTN_OK;
+}
+
+// per-topology plan arrays for T topologies
+int plan_alloc(kdtn_ctx* c, uint32_t T) {
+    TRY(ensure(c->st_len, (size_t)T * 4 + 16));
+    TRY(ensure(c->st_base, (size_t)T * 4 + 16));
+    TRY(ensure(c->st_mode, (size_t)T + 16));
+    TRY(ensure(c->st_flags, (size_t)T + 16));
+    return KDTN_OK;
+}
+
+void state_changed(kdtn_ctx* c) {
+    c->ran = false;
+    c->encoded = false;
+    c->tc_done = false;
+    c->fan_valid = false;
+    c->rp_done = false;
+    c->j_done = false;
+    c->tables_cur = false;
+}
+
+}  // namespace
+
+extern "C" {
+
+int kdtn_epoch_commit(kdtn_ctx* c, const uint8_t* mask, uint32_t* n_committed) {
+    if (!c || !c->uploaded) return KDTN_EINVAL;
+    if (!mask && (!c->ran || !fanout_stages_ok(c))) {
+        std::snprintf(g_last_error, sizeof(g_last_error),
+                      "kdtn_epoch_commit without a mask needs a run with the resolve and qdisc stages");
+        return KDTN_EINVAL;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    HIP_TRY(hipStreamSynchronize(s));
+    const uint32_t T = c->T;
+    TRY(plan_alloc(c, T));
+    const uint8_t* dmask = nullptr;
+    const uint32_t* cut = nullptr;
+    if (mask) {
+        TRY(upload(c, c->st_mask, mask, T));
+        dmask = dp<uint8_t>(c->st_mask);
+    } else {
+        TRY(run_reach(c, nullptr, 0));                      // per-topology first failing entries
+        cut = dp<uint32_t>(c->f_cut);
+    }
+    uint32_t* ncnt = dp<uint32_t>(c->misc) + MISC_COMMIT_N;
+    HIP_TRY(hipMemsetAsync(ncnt, 0, 4, s));
+    if (T)
+        k_commit_plan<<<nblocks(T), BLOCK, 0, s>>>(topo_view(c), dp<uint8_t>(c->action), cut, dmask,
+                                                   dp<uint32_t>(c->st_len), dp<uint32_t>(c->st_base),
+                                                   dp<uint8_t>(c->st_mode), dp<uint8_t>(c->st_flags), ncnt);
+    uint64_t M = 0;
+    TRY(plan_offsets(c, T, &M));
+    TRY(link_store_alloc(c, c->sh_real, (uint32_t)M));
+    if (M)
+        k_store_assemble<<<nblocks(M), BLOCK, 0, s>>>(dp<uint32_t>(c->st_off32), T, dp<uint32_t>(c->st_base),
+                                                      dp<uint8_t>(c->st_mode), nullptr, c->real.view, c->des.view,
+                                                      (uint32_t)M, dp<uint32_t>(c->sh_real.buf));
+    HIP_TRY(hipGetLastError());
+    uint32_t nc = 0;
+    HIP_TRY(hipMemcpyAsync(&nc, ncnt, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    std::swap(c->real, c->sh_real);
+    std::swap(c->t_roff, c->st_off32);
+    std::swap(c->t_flags, c->st_flags);
+    TRY(prepare_work(c, c->slice, c->real.n, c->des.n));
+    HIP_TRY(hipStreamSynchronize(s));
+    state_changed(c);
+    c->pods_imported = false;
+    if (n_committed) *n_committed = nc;
+    return KDTN_OK;
+}
+
+int kdtn_epoch_upload_delta(kdtn_ctx* c, const kdtn_epoch_delta* d) {
+    if (!c || !d || !c->uploaded) return KDTN_EINVAL;
+    HIP_TRY(hipSetDevice(c->device));
+    g_last_error[0] = 0;
+    end_shard_ingest(c);
+    TRY(check_strtab(d->kdict, "kdict"));
+    TRY(check_strtab(d->pdict, "pdict"));
+    const uint32_t T = c->T, n = d->n_changed, N0 = c->des.n, D = d->kdict.n, P = d->pdict.n;
+    auto bad = [&](const char* what, uint32_t i) {
+        std::snprintf(g_last_error, sizeof(g_last_error), "delta: %s (at %u)", what, i);
+        return KDTN_EINVAL;
+    };
+    if (n > T) return bad("more changed topologies than topologies", n);
+    if (n && (!d->topo || !d->src_ip || !d->net_ns || !d->spec_nil || !d->des_off)) return bad("missing column", 0);
+    if (!d->des_off && n) return bad("missing des_off", 0);
+    const uint32_t nref = n ? d->des_off[n] : 0;
+    if (n && d->des_off[0] != 0) return bad("des_off[0] != 0", 0);
+    if (nref && !d->ref) return bad("missing ref", 0);
+    for (uint32_t k = 0; k < n; ++k) {
+        if (d->topo[k] >= T || (k && d->topo[k] <= d->topo[k - 1])) return bad("topo not strictly ascending below T", k);
+        if (d->des_off[k + 1] < d->des_off[k]) return bad("des_off not monotone", k);
+        if (d->spec_nil[k] && d->des_off[k + 1] != d->des_off[k]) return bad("spec nil but records", k);
+    }
+    for (uint32_t i = 0; i < nref; ++i) {
+        const uint32_t r = d->ref[i];
+        if ((r & KDTN_DELTA_NEW) ? (r & ~KDTN_DELTA_NEW) >= d->records.n : r >= N0) return bad("ref out of range", i);
+    }
+    TRY(check_ids(d->src_ip, n, D, "delta.src_ip"));
+    TRY(check_ids(d->net_ns, n, D, "delta.net_ns"));
+    TRY(check_vnis(c, d->vnis, D, d->kdict_keep));
+    TRY(check_keep(c, d->kdict, d->pdict, d->kdict_keep, d->pdict_keep));
+    TRY(upload_dicts(c, d->kdict, d->pdict, d->kdict_keep, d->pdict_keep));
+    TRY(upload_links(c, c->dl_rec, d->records, D, P, "delta.records"));
+    TRY(upload(c, c->dl_topo, d->topo, (size_t)n * 4));
+    TRY(upload(c, c->dl_src, d->src_ip, (size_t)n * 4));
+    TRY(upload(c, c->dl_netns, d->net_ns, (size_t)n * 4));
+    TRY(upload(c, c->dl_nil, d->spec_nil, (size_t)n));
+    TRY(upload(c, c->dl_off, d->des_off, ((size_t)n + 1) * 4 * (n ? 1 : 0)));
+    TRY(upload(c, c->dl_ref, d->ref, (size_t)nref * 4));
+    hipStream_t s = c->stream;
+    TRY(plan_alloc(c, T));
+    TRY(ensure(c->st_chg, (size_t)T * 4 + 16));
+    HIP_TRY(hipMemsetAsync(c->st_chg.p, 0xFF, (size_t)T * 4, s));
+    if (n) k_delta_map<<<nblocks(n), BLOCK, 0, s>>>(dp<uint32_t>(c->dl_topo), n, dp<uint32_t>(c->st_chg));
+    if (T)
+        k_delta_plan<<<nblocks(T), BLOCK, 0, s>>>(topo_view(c), dp<uint32_t>(c->st_chg), dp<uint32_t>(c->dl_off),
+                                                  dp<uint32_t>(c->dl_src), dp<uint32_t>(c->dl_netns),
+                                                  dp<uint8_t>(c->dl_nil), dp<uint32_t>(c->st_len),
+                                                  dp<uint32_t>(c->st_base), dp<uint8_t>(c->st_mode),
+                                                  dp<uint32_t>(c->t_src), dp<uint32_t>(c->t_netns),
+                                                  dp<uint8_t>(c->t_flags));
+    uint64_t N = 0;
+    TRY(plan_offsets(c, T, &N));
+    TRY(link_store_alloc(c, c->sh_des, (uint32_t)N));
+    if (N)
+        k_store_assemble<<<nblocks(N), BLOCK, 0, s>>>(dp<uint32_t>(c->st_off32), T, dp<uint32_t>(c->st_base),
+                                                      dp<uint8_t>(c->st_mode), dp<uint32_t>(c->dl_ref), c->des.view,
+                                                      c->dl_rec.view, (uint32_t)N, dp<uint32_t>(c->sh_des.buf));
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(s));
+    std::swap(c->des, c->sh_des);
+    std::swap(c->t_noff, c->st_off32);
+    TRY(prepare_vnis(c, d->vnis));
+    TRY(prepare_work(c, c->slice, c->real.n, c->des.n));
+    HIP_TRY(hipStreamSynchronize(s));              // host arrays may be released after return
+    state_changed(c);
+    c->pods_imported = false;
+    return KDTN_OK;
+}
+
+int kdtn_epoch_tables_info(kdtn_ctx* c, kdtn_ingest_info* info) {
+    if (!c || !c->uploaded) return KDTN_EINVAL;
+    HIP_TRY(hipSetDevice(c->device));
+    uint32_t kb = 0, pb = 0;
+    HIP_TRY(hipMemcpyAsync(&kb, dp<uint32_t>(c->kd_offs) + c->D, 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(&pb, dp<uint32_t>(c->pd_offs) + c->P, 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    kdtn_ingest_info& I = c->j_info;
+    I = kdtn_ingest_info{};
+    I.n_topos = c->T;
+    I.n_desired = c->des.n;
+    I.n_realised = c->real.n;
+    I.n_kdict = c->D;
+    I.n_pdict = c->P;
+    I.kdict_bytes = kb;
+    I.pdict_bytes = pb;
+    c->tables_cur = true;
+    if (info) *info = I;
+    return KDTN_OK;
 }
 
 }  // extern "C"

@@ -48,7 +48,8 @@ enum : int {
     KB_NSETS = 3,
 };
 // special key-string ids found by k_kdict_flags (0xFFFFFFFF when absent)
-enum : int { SPECIAL_DEFAULT = 0, SPECIAL_LOCALHOST = 4, MISC_FAN_NODES = 12, MISC_VNI_N = 13 };   // misc words
+enum : int { SPECIAL_DEFAULT = 0, SPECIAL_LOCALHOST = 4, MISC_FAN_NODES = 12, MISC_VNI_N = 13,
+             MISC_COMMIT_N = 14 };   // misc words
 // epoch sync header (u32 words; zeroed by the epoch's only memset, the look-back status
 // follows at SYNC_HEADER_BYTES). The ticket counter, which every k_reconcile workgroup
 // increments, has a 128-B line to itself; the host reads words [SYNC_TOTALS, SYNC_TOTALS + 4)
@@ -288,6 +289,18 @@ struct TcIn {
 };
 __global__ void k_tc_sizes(TcIn w, uint32_t* size);
 __global__ void k_tc_write(TcIn w, const uint64_t* off, uint8_t* arena);
+
+// ---- resident epoch state: status commit and delta upload (kdtn_state.hip) -----------------
+enum : uint8_t { ASM_SEG_A = 0, ASM_SEG_B = 1, ASM_REF = 2 };   // source of a topology's new segment
+__global__ void k_commit_plan(DevTopos T, const uint8_t* action, const uint32_t* cut, const uint8_t* mask,
+                              uint32_t* len, uint32_t* base, uint8_t* mode, uint8_t* flags_out, uint32_t* n_commit);
+__global__ void k_delta_map(const uint32_t* topo, uint32_t n, uint32_t* chg);
+__global__ void k_delta_plan(DevTopos T, const uint32_t* chg, const uint32_t* d_off, const uint32_t* d_src,
+                             const uint32_t* d_netns, const uint8_t* d_nil, uint32_t* len, uint32_t* base,
+                             uint8_t* mode, uint32_t* src_ip, uint32_t* net_ns, uint8_t* flags);
+__global__ void k_off_narrow(const uint64_t* in, uint32_t n, uint32_t* out);
+__global__ void k_store_assemble(const uint32_t* off, uint32_t nt, const uint32_t* base, const uint8_t* mode,
+                                 const uint32_t* ref, DevLinks A, DevLinks B, uint32_t n, uint32_t* out);
 
 // ---- RemotePod messages (kdtn_wire.hip) and the receiving daemon's tc argv (kdtn_tc.hip) ----
 // message m: the UpdateRemote payload of add entry rem_idx[m] (m < n_remote, fan-out order) or

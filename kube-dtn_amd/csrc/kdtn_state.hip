@@ -1,0 +1,121 @@
+// kdtn_state.hip — device-resident epoch state across reconciles (SURVEY §8(a2) commit,
+// §8(b) ownership): the Topology status commit and the delta upload.
+//
+// Reconcile ends, for a Topology whose batches all succeeded (or that it saw for the first
+// time), with Status.Links = Spec.Links (controllers/topology_controller.go:125-138); one that
+// failed returns before the status write and keeps its old status. kdtn_epoch_commit applies
+// that to the resident link stores: the realised store is rebuilt from the desired segments
+// of the committed Topologies and the realised segments of the others, on the GPU, so the
+// next epoch needs no realised upload at all. kdtn_epoch_upload_delta then replaces the
+// desired segments of the Topologies whose spec changed: each new record is either a
+// reference to a record of the previous desired store or an inline record of the delta, so
+// the host link carries only what changed.
+//
+// Both are one "assemble" pass: every output record of Topology t comes from a per-topology
+// source — a contiguous segment of store A, of store B, or a list of record references
+// (A record, or B record with ASM_B) — with new offsets from a scan of the lengths.
+#include "kdtn_kernels.h"
+
+namespace kdtn {
+
+// commit plan: committed Topologies take their desired segment (B), the others keep their
+// realised one (A). cut: k_reach_cuts' first failing entry per (topology, list), NONE = none;
+// mask (optional): the caller's commit decision per topology.
+__global__ void __launch_bounds__(BLOCK) k_commit_plan(DevTopos T, const uint8_t* action, const uint32_t* cut,
+                                                       const uint8_t* mask, uint32_t* len, uint32_t* base,
+                                                       uint8_t* mode, uint8_t* flags_out, uint32_t* n_commit) {
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    bool commit = false;
+    if (t < T.n) {
+        const uint8_t a = action[t];
+        if (mask) commit = mask[t] != 0;
+        else if (a == KDTN_ACT_CREATED) commit = true;                         // :81-85, then :136
+        else if (a == KDTN_ACT_DIFF)                                           // every RPC succeeded
+            commit = cut[3 * t] == 0xFFFFFFFFu && cut[3 * t + 1] == 0xFFFFFFFFu && cut[3 * t + 2] == 0xFFFFFFFFu;
+        const uint8_t fl = T.flags[t];
+        if (commit) {
+            len[t] = T.des_off[t + 1] - T.des_off[t];
+            base[t] = T.des_off[t];
+            mode[t] = ASM_SEG_B;
+            // Status.Links = Spec.Links: a nil spec makes the status nil
+            flags_out[t] = (uint8_t)((fl & ~KDTN_TOPO_STATUS_NIL) | ((fl & KDTN_TOPO_SPEC_NIL) ? KDTN_TOPO_STATUS_NIL : 0));
+        } else {
+            len[t] = T.real_off[t + 1] - T.real_off[t];
+            base[t] = T.real_off[t];
+            mode[t] = ASM_SEG_A;
+            flags_out[t] = fl;
+        }
+    }
+    const uint64_t m = __ballot(commit);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(n_commit, (uint32_t)__popcll(m));
+}
+
+// delta plan: changed Topologies (chg[t] = index into the delta, NONE = unchanged) take their
+// reference list; the others keep their previous desired segment. Changed rows also take
+// their new status.src_ip / status.net_ns / spec-nil bit.
+__global__ void __launch_bounds__(BLOCK) k_delta_plan(DevTopos T, const uint32_t* chg, const uint32_t* d_off,
+                                                      const uint32_t* d_src, const uint32_t* d_netns,
+                                                      const uint8_t* d_nil, uint32_t* len, uint32_t* base,
+                                                      uint8_t* mode, uint32_t* src_ip, uint32_t* net_ns,
+                                                      uint8_t* flags) {
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= T.n) return;
+    const uint32_t c = chg[t];
+    if (c == 0xFFFFFFFFu) {
+        len[t] = T.des_off[t + 1] - T.des_off[t];
+        base[t] = T.des_off[t];
+        mode[t] = ASM_SEG_A;
+        return;
+    }
+    len[t] = d_off[c + 1] - d_off[c];
+    base[t] = d_off[c];
+    mode[t] = ASM_REF;
+    src_ip[t] = d_src[c];
+    net_ns[t] = d_netns[c];
+    flags[t] = (uint8_t)((flags[t] & ~KDTN_TOPO_SPEC_NIL) | (d_nil[c] ? KDTN_TOPO_SPEC_NIL : 0));
+}
+
+__global__ void __launch_bounds__(BLOCK) k_delta_map(const uint32_t* topo, uint32_t n, uint32_t* chg) {
+    const uint32_t c = blockIdx.x * BLOCK + threadIdx.x;
+    if (c < n) chg[topo[c]] = c;
+}
+
+// u64 exclusive offsets (k_scan_final) → the u32 offsets of a topology table
+__global__ void __launch_bounds__(BLOCK) k_off_narrow(const uint64_t* in, uint32_t n, uint32_t* out) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i <= n) out[i] = (uint32_t)in[i];
+}
+
+KD_INLINE void copy_record(const uint32_t* sbase, uint32_t j, uint32_t* dbase, uint32_t d) {
+    const uint32_t* src = sbase + (size_t)(j >> 6) * TILE_WORDS + (j & 63u);
+    uint32_t* dst = dbase + (size_t)(d >> 6) * TILE_WORDS + (d & 63u);
+    uint32_t v[LINK_COLS32];
+#pragma unroll
+    for (int c = 0; c < LINK_COLS32; ++c) v[c] = src[c * TILE_RECS];
+    const int64_t u = reinterpret_cast<const int64_t*>(sbase + (size_t)(j >> 6) * TILE_WORDS + LINK_COLS32 * TILE_RECS)[j & 63u];
+#pragma unroll
+    for (int c = 0; c < LINK_COLS32; ++c) dst[c * TILE_RECS] = v[c];
+    reinterpret_cast<int64_t*>(dbase + (size_t)(d >> 6) * TILE_WORDS + LINK_COLS32 * TILE_RECS)[d & 63u] = u;
+}
+
+// one thread per output record d: its topology by binary search over the new offsets, then
+// one record copied from the plan's source (coalesced within a segment: consecutive outputs
+// read consecutive source records)
+__global__ void __launch_bounds__(BLOCK) k_store_assemble(const uint32_t* off, uint32_t nt, const uint32_t* base,
+                                                          const uint8_t* mode, const uint32_t* ref, DevLinks A,
+                                                          DevLinks B, uint32_t n, uint32_t* out) {
+    const uint32_t d = blockIdx.x * BLOCK + threadIdx.x;
+    if (d >= n) return;
+    const uint32_t t = entry_topo(off, nt, d);
+    const uint32_t k = base[t] + (d - off[t]);
+    const uint8_t m = mode[t];
+    if (m == ASM_SEG_A) copy_record(A.base, k, out, d);
+    else if (m == ASM_SEG_B) copy_record(B.base, k, out, d);
+    else {
+        const uint32_t r = ref[k];
+        if (r & KDTN_DELTA_NEW) copy_record(B.base, r & ~KDTN_DELTA_NEW, out, d);
+        else copy_record(A.base, r, out, d);
+    }
+}
+
+}  // namespace kdtn

@@ -76,6 +76,15 @@ class EpochIn(C.Structure):
                 ("pod_slice", C.c_uint32), ("kdict_keep", C.c_uint32), ("pdict_keep", C.c_uint32)]
 
 
+DELTA_NEW = 0x80000000     # kdtn_epoch_delta.ref: inline record k of the delta
+
+
+class EpochDelta(C.Structure):
+    _fields_ = [("kdict", Strtab), ("pdict", Strtab), ("kdict_keep", C.c_uint32), ("pdict_keep", C.c_uint32),
+                ("n_changed", C.c_uint32), ("topo", u32p), ("src_ip", u32p), ("net_ns", u32p), ("spec_nil", u8p),
+                ("des_off", u32p), ("ref", u32p), ("records", LinkTable), ("vnis", VniTable)]
+
+
 class PropsTable(C.Structure):
     _fields_ = [("n", C.c_uint32), ("prop", u32p * NPROP), ("gap", u32p)]
 
@@ -188,7 +197,8 @@ EXPORTS = ["kdtn_version", "kdtn_strerror", "kdtn_err_name", "kdtn_init", "kdtn_
            "kdtn_host_free", "kdtn_epoch_fanout", "kdtn_epoch_tc", "kdtn_epoch_download_tc",
            "kdtn_json_upload", "kdtn_json_ingest", "kdtn_ingest_download", "kdtn_topology_shard",
            "kdtn_comm_set_ranks", "kdtn_pods_export", "kdtn_pods_import", "kdtn_json_ingest_shard",
-           "kdtn_ingest_shard_topos", "kdtn_epoch_remote_encode", "kdtn_epoch_download_remote"]
+           "kdtn_ingest_shard_topos", "kdtn_epoch_remote_encode", "kdtn_epoch_download_remote",
+           "kdtn_epoch_commit", "kdtn_epoch_upload_delta", "kdtn_epoch_tables_info"]
 
 
 def ptr(a: np.ndarray, t):

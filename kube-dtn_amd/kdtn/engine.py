@@ -100,6 +100,9 @@ def lib() -> C.CDLL:
         "kdtn_pods_export": (C.c_int, [vp, vp]),
         "kdtn_pods_import": (C.c_int, [vp, vp, C.c_uint64]),
         "kdtn_epoch_remote_encode": (C.c_int, [vp, C.POINTER(abi.RemoteInfo)]),
+        "kdtn_epoch_commit": (C.c_int, [vp, vp, C.POINTER(C.c_uint32)]),
+        "kdtn_epoch_upload_delta": (C.c_int, [vp, C.POINTER(abi.EpochDelta)]),
+        "kdtn_epoch_tables_info": (C.c_int, [vp, C.POINTER(abi.IngestInfo)]),
         "kdtn_epoch_download_remote": (C.c_int, [vp, C.POINTER(abi.RemotePods)]),
     }
     for name, (res, args) in sig.items():
@@ -233,6 +236,14 @@ class Engine:
         _check(lib().kdtn_ingest_shard_topos(self._ctx, out.ctypes.data), "kdtn_ingest_shard_topos")
         return out[:self._T]
 
+    def tables(self) -> EpochInput:
+        """D2H of the context's current epoch tables (kdtn_epoch_tables_info +
+        kdtn_ingest_download): the resident state after a commit or delta upload."""
+        info = abi.IngestInfo()
+        _check(lib().kdtn_epoch_tables_info(self._ctx, C.byref(info)), "kdtn_epoch_tables_info")
+        self._ingest = info
+        return self.ingest_tables()
+
     def ingest_tables(self) -> EpochInput:
         """D2H of the tables the last json_ingest decoded (kdtn_ingest_download)."""
         from .tables import Links, StrTab, Topos
@@ -258,6 +269,33 @@ class Engine:
         _check(lib().kdtn_ingest_download(self._ctx, C.byref(t)), "kdtn_ingest_download")
         return EpochInput(StrTab(kd[:I.kdict_bytes], kdo), StrTab(pd[:I.pdict_bytes], pdo),
                           Topos(*tp), real, des)
+
+    # ---- resident state: status commit and delta upload -----------------------------------
+    def commit(self, mask=None) -> int:
+        """kdtn_epoch_commit: Status.Links = Spec.Links on the device for the committed
+        Topologies (mask None: the engine's prediction; else mask[t] != 0). Returns how many."""
+        n = C.c_uint32()
+        m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+        _check(lib().kdtn_epoch_commit(self._ctx, m.ctypes.data if m is not None else None, C.byref(n)),
+               "kdtn_epoch_commit")
+        info = self.state_sizes()
+        self._caps = (info.n_realised, info.n_desired, info.n_realised)
+        return int(n.value)
+
+    def upload_delta(self, delta) -> None:
+        """kdtn_epoch_upload_delta: the next epoch as a delta (kdtn.delta.Delta) against the
+        resident state."""
+        cd = delta.to_c()
+        _check(lib().kdtn_epoch_upload_delta(self._ctx, C.byref(cd)), "kdtn_epoch_upload_delta")
+        info = abi.IngestInfo()
+        _check(lib().kdtn_epoch_tables_info(self._ctx, C.byref(info)), "kdtn_epoch_tables_info")
+        self._T = info.n_topos
+        self._caps = (info.n_realised, info.n_desired, info.n_realised)
+
+    def state_sizes(self) -> abi.IngestInfo:
+        info = abi.IngestInfo()
+        _check(lib().kdtn_epoch_tables_info(self._ctx, C.byref(info)), "kdtn_epoch_tables_info")
+        return info
 
     def run(self, stages: int = abi.STAGE_ALL) -> None:
         _check(lib().kdtn_epoch_run(self._ctx, stages), "kdtn_epoch_run")

@@ -100,3 +100,91 @@ def test_config4_wan_full_size(engine):
     assert kinds[abi.KIND_PHYSICAL] > 0 and kinds[abi.KIND_MACVLAN] > 0
     hub = np.diff(inp.topos.des_off.astype(np.int64)).max()
     assert hub >= 500                                           # power-law hubs
+
+
+def test_config2_sharded_8_full_size():
+    """BASELINE config 2 in its sharded 8xMI355X form: the 1M-pod / 10M-link
+    topology hash-sharded over 8 engine contexts (one per rank; here all on one GPU, so the
+    pod-status rows are all-gathered by the host transport: kdtn_pods_export of every rank,
+    concatenated in rank order, kdtn_pods_import). Size-independent properties on every
+    shard (every record an AddLinks entry in spec order, VNIs, every resolved peer's row
+    names the link's peer_pod in the local namespace), the shards together cover every
+    topology once, and every shard's topologies in the global window [400k, 420k) equal the
+    unsharded oracle bit for bit (peers as global pod ids)."""
+    from kdtn import Engine
+    from multishard import NONE, gid_table
+    G, P = 8, 1_000_000
+    shards = [synth.make(2, total_pods=P, shard=r, nshards=G) for r in range(G)]
+    slice_ = shards[0].pod_slice
+    assert all(s.pod_slice == slice_ for s in shards)
+    gids = [s.gid for s in shards]
+    allg = np.sort(np.concatenate(gids))
+    assert np.array_equal(allg, np.arange(P))                     # each topology on one shard
+    engines = [Engine(device=0, tick_in_usec=TICK) for _ in range(G)]
+    outs, table = [], None
+    try:
+        rows = []
+        for r, (e, inp) in enumerate(zip(engines, shards)):
+            e.set_ranks(G, r)
+            e.upload(inp)
+            rows.append(e.pods_export(inp.pod_slice))
+        table = np.concatenate(rows)                               # the all-gather, rank order
+        for e in engines:
+            e.pods_import(table)
+            e.run()
+            e.sync()
+            outs.append(e.download())
+            e.close()
+    finally:
+        for e in engines:
+            e.close()
+    peer_gid = gid_table(slice_, gids)
+    owner = np.zeros(P, np.int64)
+    for r, g in enumerate(gids):
+        owner[g] = r
+    total = cross = 0
+    for r, (inp, out) in enumerate(zip(shards, outs)):
+        N = inp.desired.n
+        total += N
+        assert 1_150_000 < N < 1_350_000
+        assert len(out.add_idx) == N and len(out.del_idx) == 0 and len(out.upd_idx) == 0
+        assert np.array_equal(out.add_idx, np.arange(N, dtype=np.uint32))
+        assert np.array_equal(out.add_off, inp.topos.des_off) and (out.action == abi.ACT_DIFF).all()
+        assert (out.add_res["vni"] == (5000 + inp.desired.uid).astype(np.int32)).all()
+        p = out.add_res["peer_topo"]
+        hit = p != NONE
+        assert hit.mean() > 0.95
+        tn = _seg(inp.topos.des_off, N)
+        assert np.array_equal(table[p[hit], 1], inp.desired.key[abi.KEY_COLS.index("peer_pod"), hit])
+        assert np.array_equal(table[p[hit], 0], inp.topos.ns[tn[hit]])
+        cross += int((owner[peer_gid[p[hit]]] != r).sum())
+    assert total == 10_000_000 and cross > 0.8 * total               # the exchange matters
+    # oracle window over the unsharded topology: every shard owns part of it
+    a, b = 400_000, 420_000
+    full = synth.make(2, pods_per_shard=P)
+    ora = O.reconcile(full, tick=TICK, t_begin=a, t_end=b)
+    ora_rel = ora.add_idx.astype(np.int64) - np.repeat(full.topos.des_off[a:b].astype(np.int64),
+                                                       np.diff(ora.add_off.astype(np.int64)))
+    got_res = np.zeros(len(ora.add_idx), ora.add_res.dtype)
+    got_q = np.zeros(len(ora.add_idx), ora.add_qdisc.dtype)
+    got_rel = np.zeros(len(ora.add_idx), np.int64)
+    seen = 0
+    for r, (inp, out) in enumerate(zip(shards, outs)):
+        loc = np.nonzero((gids[r] >= a) & (gids[r] < b))[0]
+        assert len(loc) > 1000
+        for t in loc.tolist():
+            g = int(gids[r][t])
+            s0, s1 = int(out.add_off[t]), int(out.add_off[t + 1])
+            w0, w1 = int(ora.add_off[g - a]), int(ora.add_off[g - a + 1])
+            assert s1 - s0 == w1 - w0, (r, t)
+            res = out.add_res[s0:s1].copy()
+            hitw = res["peer_topo"] != NONE
+            res["peer_topo"][hitw] = peer_gid[res["peer_topo"][hitw]].astype(np.uint32)
+            got_res[w0:w1] = res
+            got_q[w0:w1] = out.add_qdisc[s0:s1]
+            got_rel[w0:w1] = out.add_idx[s0:s1].astype(np.int64) - int(inp.topos.des_off[t])
+            seen += 1
+    assert seen == b - a
+    assert np.array_equal(got_rel, ora_rel)
+    assert got_res.tobytes() == ora.add_res.tobytes()
+    assert got_q.tobytes() == ora.add_qdisc.tobytes()

@@ -1,0 +1,92 @@
+"""Resident epoch state on the GPU: kdtn_epoch_commit (Status.Links = Spec.Links for the
+committed Topologies, controllers/topology_controller.go:125-138) and kdtn_epoch_upload_delta
+(only the changed Topologies' specs, as references into the previous desired store plus
+inline records) against the host restatement (tests/state.py), and every epoch of a
+resident chain bit-exact against the oracle on the tables the chain should hold."""
+import copy
+
+import numpy as np
+import pytest
+
+import oracle as O
+from helpers import random_epoch
+from kdtn import Engine, abi, synth
+from kdtn.delta import build_delta
+from kdtn.model import pack
+from kdtn.tables import EpochInput, Interner, Topos
+from state import apply_delta, commit, predicted_commit, same_tables
+from test_state_cpu import mutate
+
+pytestmark = pytest.mark.gpu
+TICK = 15.625
+
+
+def _run_same(eng, expect, ctx):
+    eng.run()
+    eng.sync()
+    out = eng.download()
+    ora = O.reconcile(expect, tick=TICK)
+    bad = out.mismatches(ora)
+    assert not bad, f"{ctx}: {bad}"
+    return ora
+
+
+def test_commit_and_delta_random_epochs():
+    """Adversarial epochs (failing links, nil lists, SKIP / CREATED / DIFF): the predicted
+    commit and explicit masks, then a delta with spec edits, nil specs and node moves."""
+    for seed in range(4):
+        topos, vnis = random_epoch(seed, T=150, p_err=0.2)
+        kd, pd = Interner(), Interner()
+        a = pack(topos, vnis, kdict=kd, pdict=pd)
+        with Engine(device=0, tick_in_usec=TICK) as eng:
+            eng.upload(a)
+            ora = _run_same(eng, a, f"seed {seed} epoch 0")
+            if seed % 2 == 0:
+                mask = predicted_commit(a, ora)
+                n = eng.commit()
+            else:
+                mask = np.random.default_rng(seed).random(a.topos.n) < 0.6
+                n = eng.commit(mask)
+            assert n == int(mask.sum())
+            state = commit(a, mask)
+            assert not same_tables(eng.tables(), state), seed
+            b = pack(mutate(topos, seed + 7), vnis, kdict=kd, pdict=pd)
+            d = build_delta(a, b, a.kdict.n, a.pdict.n, vnis=b.vnis)
+            eng.upload_delta(d)
+            want = apply_delta(state, d)
+            assert not same_tables(eng.tables(), want), seed
+            _run_same(eng, want, f"seed {seed} epoch 1")
+
+
+@pytest.mark.parametrize("pods", [20000])
+def test_resident_churn_chain(pods):
+    """Ten config-3 churn epochs through one context: after each epoch the status commit
+    (alternately the engine's prediction and an all-succeeded mask) and a delta upload of the
+    next epoch; the device tables equal the restatement's and every epoch's batches equal
+    the oracle's on those tables."""
+    cs = synth.ChurnSequence(total_pods=pods)
+    prev = cs.epoch_input(copy=True)
+    with Engine(device=0, tick_in_usec=TICK) as eng:
+        eng.upload(prev)
+        ora = _run_same(eng, prev, "epoch 0")
+        state = prev
+        moved = 0
+        for ep in range(1, 10):
+            if ep % 2:
+                mask = predicted_commit(state, ora)
+                assert eng.commit() == int(mask.sum())
+            else:
+                mask = np.ones(state.topos.n, bool)
+                eng.commit(mask)
+            state = commit(state, mask)
+            cs.advance()
+            new = cs.epoch_input(copy=True)
+            d = build_delta(state, new, state.kdict.n, state.pdict.n)
+            moved += d.upload_bytes()
+            eng.upload_delta(d)
+            state = apply_delta(state, d)
+            assert not same_tables(eng.tables(), state), ep
+            ora = _run_same(eng, state, f"epoch {ep}")
+            assert len(ora.del_idx) and len(ora.add_idx) and len(ora.upd_idx)
+        full = 9 * (88 * new.desired.n + 25 * new.topos.n)
+        assert moved < 0.1 * full, (moved, full)
