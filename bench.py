@@ -175,31 +175,93 @@ def wire_stage(eng, reps: int = 5):
 
 def e2e_stage(eng, inp, reps: int = 3):
     """PCIe-inclusive epoch (separate report, never `value`): kdtn_reconcile_epoch's pieces —
-    upload of the host tables (pageable numpy arrays), run + sync, download of every output
-    — timed separately, median of `reps`."""
-    ups, runs, downs = [], [], []
-    for _ in range(reps):
-        t0 = time.perf_counter()
-        eng.upload(inp)
-        t1 = time.perf_counter()
-        eng.run()
-        eng.sync()
-        t2 = time.perf_counter()
-        out = eng.download()
-        t3 = time.perf_counter()
-        ups.append(t1 - t0)
-        runs.append(t2 - t1)
-        downs.append(t3 - t2)
-    med = lambda x: sorted(x)[len(x) // 2]
+    upload of the host tables, run + sync, download of every output — timed separately,
+    median of `reps`, from page-locked host buffers (kdtn_host_alloc: the tables and the
+    output arrays), and once more from pageable numpy arrays for comparison."""
+    from kdtn.engine import pin_input
+    from kdtn.tables import BatchesOut
+
+    def timed(src, into):
+        ups, runs, downs = [], [], []
+        out = None
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            eng.upload(src)
+            t1 = time.perf_counter()
+            eng.run()
+            eng.sync()
+            t2 = time.perf_counter()
+            out = eng.download(into)
+            t3 = time.perf_counter()
+            ups.append(t1 - t0)
+            runs.append(t2 - t1)
+            downs.append(t3 - t2)
+        med = lambda x: sorted(x)[len(x) // 2]
+        return med(ups), med(runs), med(downs), out
+
     up_b = (88 * (inp.realised.n + inp.desired.n) + 25 * inp.topos.n + len(inp.kdict.bytes_)
             + 4 * inp.kdict.n + len(inp.pdict.bytes_) + 4 * inp.pdict.n)
+    pin = pin_input(inp)
+    into = BatchesOut.alloc(inp.topos.n, inp.realised.n, inp.desired.n, inp.realised.n, pinned=True)
+    u, r, d, out = timed(pin, into)
     down_b = sum(getattr(out, f).nbytes for f in out.FIELDS)
-    tot = med(ups) + med(runs) + med(downs)
-    return {"links_per_s": inp.desired.n / tot, "ms": tot * 1e3, "upload_ms": med(ups) * 1e3,
-            "run_ms": med(runs) * 1e3, "download_ms": med(downs) * 1e3, "upload_bytes": up_b,
-            "download_bytes": down_b, "host_link_GBps": (up_b + down_b) / (med(ups) + med(downs)) / 1e9,
-            "note": "not part of value: upload + epoch + download of caller-owned pageable host "
-                    "memory, as one kdtn_reconcile_epoch call would do"}
+    tot = u + r + d
+    res = {"links_per_s": inp.desired.n / tot, "ms": tot * 1e3, "upload_ms": u * 1e3, "run_ms": r * 1e3,
+           "download_ms": d * 1e3, "upload_bytes": up_b, "download_bytes": down_b,
+           "upload_GBps": up_b / u / 1e9, "download_GBps": down_b / d / 1e9, "host_memory": "pinned (kdtn_host_alloc)",
+           "note": "not part of value: full upload + epoch + download of caller-owned page-locked host memory "
+                   "(one kdtn_reconcile_epoch); a resident controller uploads deltas instead (config-3 "
+                   "resident_chain)"}
+    del pin, into
+    u, r, d, out = timed(inp, None)
+    res["pageable"] = {"ms": (u + r + d) * 1e3, "upload_ms": u * 1e3, "download_ms": d * 1e3,
+                       "host_link_GBps": (up_b + down_b) / (u + d) / 1e9}
+    return res
+
+
+def resident_chain_stage(eng, cs, prev, epochs: int):
+    """Config 3 as a resident controller runs it (separate report, never `value`): each epoch
+    uploads only a delta against the engine's state (kdtn_epoch_upload_delta: the changed
+    Topologies' specs as references into the previous desired store + new records), runs,
+    downloads the batches, and commits the status on the device (kdtn_epoch_commit, every
+    Topology's RPCs taken as succeeded, as the churn generator assumes). Host buffers
+    page-locked; the delta is built on the host outside the timed region."""
+    from kdtn.delta import build_delta
+    from kdtn.engine import pin_delta
+    from kdtn.tables import BatchesOut
+    T = prev.topos.n
+    cap = max(1 << 20, prev.desired.n // 8)              # entries per list (5 % churn: ~1.7 %)
+    into = BatchesOut.alloc(T, cap, cap, cap, pinned=True)
+    ones = np.ones(T, np.uint8)
+    eng.commit(ones)
+    rows = []
+    for _ in range(epochs):
+        cs.advance()
+        new = cs.epoch_input(copy=True)
+        d = pin_delta(build_delta(prev, new, prev.kdict.n, prev.pdict.n))
+        t0 = time.perf_counter()
+        eng.upload_delta(d)
+        t1 = time.perf_counter()
+        eng.run()
+        c = eng.sync()
+        t2 = time.perf_counter()
+        out = eng.download(into)
+        t3 = time.perf_counter()
+        eng.commit(ones)
+        t4 = time.perf_counter()
+        down_b = sum(getattr(out, f).nbytes for f in out.FIELDS)
+        rows.append((d.upload_bytes(), t1 - t0, t2 - t1, t3 - t2, t4 - t3, down_b, new.desired.n,
+                     d.n_changed, d.records.n, c.n_add + c.n_del + c.n_upd))
+        prev = new
+    a = np.array(rows, dtype=np.float64).mean(axis=0)
+    full_b = 88 * (2 * prev.desired.n) + 25 * T
+    e2e = a[1] + a[2] + a[3] + a[4]
+    return {"epochs": epochs, "upload_bytes": a[0], "full_upload_bytes": full_b, "upload_frac": a[0] / full_b,
+            "changed_topologies": a[7], "inline_records": a[8], "entries": a[9],
+            "upload_ms": a[1] * 1e3, "run_ms": a[2] * 1e3, "download_ms": a[3] * 1e3, "download_bytes": a[5],
+            "commit_ms": a[4] * 1e3, "e2e_ms": e2e * 1e3, "links_per_s": a[6] / e2e,
+            "note": "not part of value: per epoch delta upload + run + download + on-device status commit, "
+                    "page-locked host memory, mean over the epochs"}
 
 
 def ingest_stage(eng, inp, steps: int, reps: int = 5, cpu_sample_pods: int = 20_000):
@@ -398,7 +460,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-wire", action="store_true", help="skip the wire-encoding stage report")
     ap.add_argument("--no-ingest", action="store_true", help="skip the CR-ingest stage report")
-    ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive epoch report")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive epoch reports")
+    ap.add_argument("--resident-epochs", type=int, default=5, help="config 3: epochs of the resident-chain report")
     ap.add_argument("--dump", default=None,
                     help="directory: each rank saves its last timed epoch's outputs (rank<r>.npz) for "
                          "an external parity check (tests/test_bench_gpu.py)")
@@ -644,6 +707,8 @@ def main():
                                         "kernels_ms": rsum,
                                         "note": "same epoch re-run with kdict_keep/pdict_keep = all strings "
                                                 "(append-only interner, nothing new to parse)"}
+    if churn and world == 1 and not args.no_e2e:
+        result["resident_chain"] = resident_chain_stage(eng, cs, cs.epoch_input(copy=True), args.resident_epochs)
     if diff_ms:
         result["diff_only_reconcile_ms"] = float(np.mean(diff_ms))
         result["diff_share_of_reconcile"] = float(np.mean(diff_ms)) / rec_ms

@@ -612,8 +612,14 @@ int kdtn_pods_import(kdtn_ctx* ctx, const kdtn_pod_row* rows, uint64_t n);   /* 
  * key (node, vni) in (topology, add-list, local-before-remote) order wins. The result
  * becomes the context's resident map (KDTN_VNI_RESIDENT) and, with out->node / vni / net_ns
  * (capacity out->cap entries; NULL = count only), is downloaded: entries of the epoch's adds
- * first, then the surviving snapshot entries, keys unique. Needs a single-shard run with
- * the resolve and qdisc stages; KDTN_ENOSPC when cap < n (the map is applied anyway). */
+ * first, then the surviving snapshot entries, keys unique. Needs a run with
+ * the resolve and qdisc stages; KDTN_ENOSPC when cap < n (the map is applied anyway).
+ * Sharded (nranks > 1): the daemons' maps are node-global, so every rank applies the ops of
+ * EVERY rank — in rank order (rank r's ops before rank r+1's; within a rank the order above) —
+ * against the replicated snapshot, and all ranks leave the same map. RCCL contexts gather the
+ * ops themselves (two all-gathers: counts, then the lists padded to the largest); host
+ * transport: kdtn_vni_ops_export on every rank, all-gather by the caller, kdtn_vni_ops_import
+ * of the concatenations (dels of ranks 0..G-1, adds of ranks 0..G-1), then this call. */
 typedef struct kdtn_vni_state {
     uint64_t  cap;
     uint32_t  n;                /* out: entries of the map after the epoch */
@@ -622,6 +628,15 @@ typedef struct kdtn_vni_state {
     uint32_t* net_ns;
 } kdtn_vni_state;
 int kdtn_epoch_vni_apply(kdtn_ctx* ctx, kdtn_vni_state* out);
+/* One VxlanManager op (16 B): kind 0 none, 1 Delete(vni) on node, 2 Store(vni, net_ns) on node. */
+typedef struct kdtn_vni_op { uint32_t node; int32_t vni; uint32_t net_ns; uint32_t kind; } kdtn_vni_op;
+/* This rank's ops of the last run: n_del delete slots, n_add add slots (two per AddLinks
+ * entry: local node, then peer node); NULL arrays = counts only. */
+int kdtn_vni_ops_export(kdtn_ctx* ctx, kdtn_vni_op* dels, uint32_t del_cap, kdtn_vni_op* adds, uint32_t add_cap,
+                        uint32_t* n_del, uint32_t* n_add);
+/* Host transport: every rank's exported lists concatenated in rank order. */
+int kdtn_vni_ops_import(kdtn_ctx* ctx, const kdtn_vni_op* dels, uint32_t n_del, const kdtn_vni_op* adds,
+                        uint32_t n_add);
 /* The resident map (the last uploaded snapshot or applied state): out->n, and the arrays
  * when given (KDTN_ENOSPC when out->cap < n). */
 int kdtn_vni_download(kdtn_ctx* ctx, kdtn_vni_state* out);

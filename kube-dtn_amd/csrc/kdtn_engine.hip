@@ -91,6 +91,10 @@ struct kdtn_ctx {
     DevBuf r_node, r_vni, r_netns;
     bool vres_ok = false;          // a map usable as KDTN_VNI_RESIDENT exists
     bool vres_in_r = false;
+    // sharded apply: every rank's ops gathered in rank order ([dels][adds]), by RCCL or imported
+    DevBuf vx_cnt, vx_send, vx_recv, vx_gops;
+    uint64_t vx_gd = 0, vx_ga = 0;
+    bool vx_imported = false;
     uint32_t vres_n = 0, vres_D = 0;   // its entries; the dictionary size its ids were made for
     // pods
     DevBuf pods, pod_ovf, pod_direct;
@@ -701,7 +705,8 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->rp_msz, &c->rp_moff, &c->rp_tsz, &c->rp_toff, &c->rp_part, &c->rp_arena, &c->rp_tc,
                       &c->st_len, &c->st_base, &c->st_mode, &c->st_flags, &c->st_off64, &c->st_part,
                       &c->st_off32, &c->st_mask, &c->st_chg, &c->dl_topo, &c->dl_src, &c->dl_netns, &c->dl_nil,
-                      &c->dl_off, &c->dl_ref, &c->dl_rec.buf};
+                      &c->dl_off, &c->dl_ref, &c->dl_rec.buf, &c->vx_cnt, &c->vx_send, &c->vx_recv,
+                      &c->vx_gops};
     for (DevBuf* b : bufs) release(*b);
     for (int i = 0; i <= kMaxTimers; ++i)
         if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
@@ -996,6 +1001,7 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
     c->tc_done = false;
     c->fan_valid = false;
     c->rp_done = false;
+    c->vx_imported = false;
     return KDTN_OK;
 }
 
@@ -1281,8 +1287,6 @@ int fanout_compute(kdtn_ctx* c) {
     TRY(ensure(c->f_node_idx, (size_t)D * 4));
     TRY(ensure(c->f_nodes, (size_t)FAN_NODE_CAP * 4 + 16));
     TRY(ensure(c->f_part, (size_t)nbd * 8 + 16));
-    TRY(ensure(c->f_counts, (size_t)FAN_NODE_CAP * nchunks * 4 + 16));
-    TRY(ensure(c->f_base, ((size_t)FAN_NODE_CAP * nchunks + 1) * 8 + 16));
     TRY(ensure(c->f_idx, (size_t)na * 4 + 16));
     uint32_t* misc = dp<uint32_t>(c->misc);
     uint32_t* n_nodes = misc + MISC_FAN_NODES;
@@ -1302,9 +1306,12 @@ int fanout_compute(kdtn_ctx* c) {
     }
     timer_mark(c, "fanout_host_sync");
     const uint32_t ncells = nn * nchunks;
+    TRY(ensure(c->f_counts, (size_t)ncells * 4 + 16));
+    TRY(ensure(c->f_base, ((size_t)ncells + 1) * 8 + 16));
     uint32_t nsend = 0;
     if (na && nn) {
-        k_fan_count<<<nchunks, 64, 0, s>>>(f, dp<uint8_t>(c->f_send), dp<uint32_t>(c->f_node_idx), n_nodes,
+        const size_t lds = (size_t)nn * 4;
+        k_fan_count<<<nchunks, 64, lds, s>>>(f, dp<uint8_t>(c->f_send), dp<uint32_t>(c->f_node_idx), n_nodes,
                                            dp<uint32_t>(c->f_counts), nchunks);
         const uint32_t nbc = nblocks((uint64_t)ncells + 1, SCAN_CHUNK);
         TRY(ensure(c->w_part, (size_t)nbc * 8 + 16));
@@ -1312,7 +1319,7 @@ int fanout_compute(kdtn_ctx* c) {
         k_scan_top<<<1, BLOCK, 0, s>>>(dp<uint64_t>(c->w_part), nbc);
         k_scan_final<<<nbc, BLOCK, 0, s>>>(dp<uint32_t>(c->f_counts), ncells, dp<uint64_t>(c->w_part),
                                            dp<uint64_t>(c->f_base));
-        k_fan_scatter<<<nchunks, 64, 0, s>>>(f, dp<uint8_t>(c->f_send), dp<uint32_t>(c->f_node_idx), n_nodes,
+        k_fan_scatter<<<nchunks, 64, lds, s>>>(f, dp<uint8_t>(c->f_send), dp<uint32_t>(c->f_node_idx), n_nodes,
                                              dp<uint64_t>(c->f_base), nchunks, dp<uint32_t>(c->f_idx));
         HIP_TRY(hipGetLastError());
         uint64_t tot = 0;
@@ -2175,25 +2182,23 @@ int kdtn_debug_wg_trace(kdtn_ctx* c, uint64_t* out, uint32_t cap) {
     return (int)n;
 }
 
-int kdtn_epoch_vni_apply(kdtn_ctx* c, kdtn_vni_state* out) {
-    if (!c || !c->ran) return KDTN_EINVAL;
+}  // extern "C"
+
+namespace {
+
+// this rank's VxlanManager ops of the last run into vx_ops: [n_del del slots][2 n_add add slots]
+int vni_ops_compute(kdtn_ctx* c, uint32_t* nd_out, uint32_t* na_out) {
     const uint32_t need = KDTN_STAGE_RESOLVE | KDTN_STAGE_QDISC;
-    if ((c->last_stages & need) != need || c->nranks != 1) {
+    if (!c->ran || (c->last_stages & need) != need) {
         std::snprintf(g_last_error, sizeof(g_last_error),
-                      "kdtn_epoch_vni_apply: needs a single-shard epoch run with resolve and qdisc stages");
+                      "VXLAN ops: need an epoch run with the resolve and qdisc stages");
         return KDTN_EINVAL;
     }
-    HIP_TRY(hipSetDevice(c->device));
     hipStream_t s = c->stream;
     HIP_TRY(hipStreamSynchronize(s));                 // counts of the run (h_misc)
-    const uint32_t nd = c->h_misc[1], na = c->h_misc[3], V = c->V;
-    const uint64_t n_ops = 2ull * na, n_ext = n_ops + V;
-    if (n_ext >= 0x7FFFFFFFull) return KDTN_EINVAL;
-    c->n_ev = 0;
-    (void)hipEventRecord(c->ev[0], s);
-    TRY(ensure(c->vx_ops, ((size_t)nd + n_ops) * 16));
-    TRY(ensure(c->vx_dead, (size_t)V + 16));
-    uint4* ops = dp<uint4>(c->vx_ops);
+    const uint32_t nd = c->h_misc[1], na = c->h_misc[3];
+    if (2ull * na + nd + c->V >= 0x7FFFFFFFull) return KDTN_EINVAL;
+    TRY(ensure(c->vx_ops, ((size_t)nd + 2ull * na) * 16));
     VniOpsIn f{ReachIn{dp<uint32_t>(c->del_off), dp<uint4>(c->del_res), dp<uint32_t>(c->add_off), dp<uint4>(c->add_res),
                        dp<uint2>(c->add_qdisc), dp<uint32_t>(c->upd_off), dp<uint4>(c->upd_res), c->T, 0u},
                dp<uint32_t>(c->t_src), dp<uint32_t>(c->t_netns), dp<uint4>(c->pods), nd, na};
@@ -2203,21 +2208,154 @@ int kdtn_epoch_vni_apply(kdtn_ctx* c, kdtn_vni_state* out) {
         HIP_TRY(hipMemsetAsync(cut, 0xFF, (size_t)c->T * 8, s));
         if (nd + na) {
             k_vni_cuts<<<nblocks((uint64_t)nd + na), BLOCK, 0, s>>>(f, cut);
-            k_vni_ops<<<nblocks((uint64_t)nd + na), BLOCK, 0, s>>>(f, cut, ops);
+            k_vni_ops<<<nblocks((uint64_t)nd + na), BLOCK, 0, s>>>(f, cut, dp<uint4>(c->vx_ops));
         }
     }
+    HIP_TRY(hipGetLastError());
+    *nd_out = nd;
+    *na_out = na;
+    return KDTN_OK;
+}
+
+// Every rank's ops in rank order, [all del slots][all add slots], into vx_gops over RCCL:
+// the per-rank counts first, then one all-gather of lists padded to the largest rank's.
+int vni_ops_gather_rccl(kdtn_ctx* c, uint32_t nd, uint32_t na, uint64_t* gd, uint64_t* ga) {
+    hipStream_t s = c->stream;
+    const int G = c->nranks;
+    TRY(ensure(c->vx_cnt, (size_t)G * 8 + 16));
+    uint32_t* cnt = dp<uint32_t>(c->vx_cnt);
+    const uint32_t mine[2] = {nd, na};
+    HIP_TRY(hipMemcpyAsync(cnt + 2 * c->rank, mine, 8, hipMemcpyHostToDevice, s));
+    ncclResult_t r = ncclAllGather(cnt + 2 * c->rank, cnt, 2, ncclUint32, c->comm, s);
+    if (r != ncclSuccess) {
+        std::snprintf(g_last_error, sizeof(g_last_error), "ncclAllGather (VXLAN op counts): %s", ncclGetErrorString(r));
+        return KDTN_EIO;
+    }
+    std::vector<uint32_t> h(2 * (size_t)G);
+    HIP_TRY(hipMemcpyAsync(h.data(), cnt, 8 * (size_t)G, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    uint32_t md = 0, ma = 0;
+    for (int g = 0; g < G; ++g) {
+        md = std::max(md, h[2 * g]);
+        ma = std::max(ma, h[2 * g + 1]);
+    }
+    const size_t row = (size_t)md + 2ull * ma;                 // ops per rank, padded
+    TRY(ensure(c->vx_send, row * 16 + 16));
+    TRY(ensure(c->vx_recv, row * G * 16 + 16));
+    TRY(ensure(c->vx_gops, row * G * 16 + 16));
+    uint8_t* send = dp<uint8_t>(c->vx_send);
+    HIP_TRY(hipMemsetAsync(send, 0, row * 16, s));             // VOP_NONE padding
+    if (nd) HIP_TRY(hipMemcpyAsync(send, c->vx_ops.p, (size_t)nd * 16, hipMemcpyDeviceToDevice, s));
+    if (na)
+        HIP_TRY(hipMemcpyAsync(send + (size_t)md * 16, dp<uint8_t>(c->vx_ops) + (size_t)nd * 16, 2ull * na * 16,
+                               hipMemcpyDeviceToDevice, s));
+    if (row) {
+        r = ncclAllGather(send, c->vx_recv.p, row * 4, ncclUint32, c->comm, s);
+        if (r != ncclSuccess) {
+            std::snprintf(g_last_error, sizeof(g_last_error), "ncclAllGather (VXLAN ops): %s", ncclGetErrorString(r));
+            return KDTN_EIO;
+        }
+        uint8_t* g = dp<uint8_t>(c->vx_gops);
+        const uint8_t* rv = dp<uint8_t>(c->vx_recv);
+        if (md) HIP_TRY(hipMemcpy2DAsync(g, (size_t)md * 16, rv, row * 16, (size_t)md * 16, G, hipMemcpyDeviceToDevice, s));
+        if (ma)
+            HIP_TRY(hipMemcpy2DAsync(g + (size_t)md * G * 16, 2ull * ma * 16, rv + (size_t)md * 16, row * 16,
+                                     2ull * ma * 16, G, hipMemcpyDeviceToDevice, s));
+    }
+    *gd = (uint64_t)md * G;
+    *ga = 2ull * ma * G;
+    return KDTN_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int kdtn_vni_ops_export(kdtn_ctx* c, kdtn_vni_op* dels, uint32_t del_cap, kdtn_vni_op* adds, uint32_t add_cap,
+                        uint32_t* n_del, uint32_t* n_add) {
+    if (!c || !n_del || !n_add) return KDTN_EINVAL;
+    HIP_TRY(hipSetDevice(c->device));
+    uint32_t nd = 0, na = 0;
+    TRY(vni_ops_compute(c, &nd, &na));
+    *n_del = nd;
+    *n_add = 2 * na;
+    if ((dels && nd > del_cap) || (adds && 2 * na > add_cap)) return KDTN_ENOSPC;
+    hipStream_t s = c->stream;
+    if (dels && nd) HIP_TRY(hipMemcpyAsync(dels, c->vx_ops.p, (size_t)nd * 16, hipMemcpyDeviceToHost, s));
+    if (adds && na)
+        HIP_TRY(hipMemcpyAsync(adds, dp<uint8_t>(c->vx_ops) + (size_t)nd * 16, 2ull * na * 16, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return KDTN_OK;
+}
+
+int kdtn_vni_ops_import(kdtn_ctx* c, const kdtn_vni_op* dels, uint32_t n_del, const kdtn_vni_op* adds, uint32_t n_add) {
+    if (!c || !c->ran || (n_del && !dels) || (n_add && !adds) || (uint64_t)n_del + n_add + c->V >= 0x7FFFFFFFull)
+        return KDTN_EINVAL;
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    TRY(ensure(c->vx_gops, ((size_t)n_del + n_add) * 16 + 16));
+    if (n_del) HIP_TRY(hipMemcpyAsync(c->vx_gops.p, dels, (size_t)n_del * 16, hipMemcpyHostToDevice, s));
+    if (n_add)
+        HIP_TRY(hipMemcpyAsync(dp<uint8_t>(c->vx_gops) + (size_t)n_del * 16, adds, (size_t)n_add * 16,
+                               hipMemcpyHostToDevice, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    c->vx_gd = n_del;
+    c->vx_ga = n_add;
+    c->vx_imported = true;
+    return KDTN_OK;
+}
+
+int kdtn_epoch_vni_apply(kdtn_ctx* c, kdtn_vni_state* out) {
+    if (!c || !c->ran) return KDTN_EINVAL;
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const bool host_xchg = c->nranks > 1 && !c->comm;
+    if (host_xchg && !c->vx_imported) {
+        std::snprintf(g_last_error, sizeof(g_last_error),
+                      "host transport: kdtn_vni_ops_import every rank's VXLAN ops before kdtn_epoch_vni_apply");
+        return KDTN_EINVAL;
+    }
+    if (c->nranks > 1 && !c->pods_rank_major && !host_xchg) {
+        std::snprintf(g_last_error, sizeof(g_last_error), "kdtn_epoch_vni_apply: sharded ingest contexts use the host transport");
+        return KDTN_EINVAL;
+    }
+    c->n_ev = 0;
+    (void)hipEventRecord(c->ev[0], s);
+    const uint32_t V = c->V;
+    uint64_t nd_all = 0, n_ops = 0;
+    const uint4* ops = nullptr;
+    if (!host_xchg) {
+        uint32_t nd = 0, na = 0;
+        TRY(vni_ops_compute(c, &nd, &na));
+        if (c->nranks > 1) {
+            TRY(vni_ops_gather_rccl(c, nd, na, &nd_all, &n_ops));
+            ops = dp<uint4>(c->vx_gops);
+        } else {
+            nd_all = nd;
+            n_ops = 2ull * na;
+            ops = dp<uint4>(c->vx_ops);
+        }
+    } else {
+        nd_all = c->vx_gd;
+        n_ops = c->vx_ga;
+        ops = dp<uint4>(c->vx_gops);
+    }
+    const uint64_t n_ext = n_ops + V;
+    if (n_ext + nd_all >= 0x7FFFFFFFull) return KDTN_EINVAL;
+    TRY(ensure(c->vx_dead, (size_t)V + 16));
     const uint4* ents = dp<uint4>(c->v_ents);
     uint8_t* dead = dp<uint8_t>(c->vx_dead);
     if (V) {                                          // the run built the snapshot table
         k_vni_shadow<<<nblocks(V), BLOCK, 0, s>>>(ents, V, dp<uint32_t>(c->v_slots), c->vni_mask, dead);
-        if (nd) k_vni_del<<<nblocks(nd), BLOCK, 0, s>>>(ops, nd, ents, dp<uint32_t>(c->v_slots), c->vni_mask, dead);
+        if (nd_all) k_vni_del<<<nblocks(nd_all), BLOCK, 0, s>>>(ops, (uint32_t)nd_all, ents, dp<uint32_t>(c->v_slots),
+                                                                c->vni_mask, dead);
     }
     timer_mark(c, "vni_ops");
     const uint32_t mask = next_pow2(n_ext * 2) - 1;
     TRY(ensure(c->vx_slots, ((size_t)mask + 1) * 4));
     HIP_TRY(hipMemsetAsync(c->vx_slots.p, 0xFF, ((size_t)mask + 1) * 4, s));
     uint32_t* slots = dp<uint32_t>(c->vx_slots);
-    const uint4* aops = ops + nd;
+    const uint4* aops = ops + nd_all;
     const uint32_t nb = nblocks(n_ext, SCAN_CHUNK);
     TRY(ensure(c->vx_part, (size_t)nb * 8 + 8));
     TRY(ensure(c->vx_node, (size_t)n_ext * 4));

@@ -105,7 +105,7 @@ __global__ void __launch_bounds__(BLOCK) k_fan_nodes_write(const uint32_t* mark,
 // (node, chunk) counts: one wave per chunk of FAN_CHUNK entries, LDS histogram
 __global__ void __launch_bounds__(64) k_fan_count(FanIn f, const uint8_t* send, const uint32_t* node_idx,
                                                   const uint32_t* n_nodes, uint32_t* counts, uint32_t nchunks) {
-    __shared__ uint32_t h[FAN_NODE_CAP];
+    extern __shared__ uint32_t h[];                          // [n_nodes] (dynamic: occupancy)
     const uint32_t nn = *n_nodes;
     if (nn > FAN_NODE_CAP) return;                          // reported by the host
     for (uint32_t k = threadIdx.x; k < nn; k += 64) h[k] = 0;
@@ -117,13 +117,14 @@ __global__ void __launch_bounds__(64) k_fan_count(FanIn f, const uint8_t* send, 
     for (uint32_t k = threadIdx.x; k < nn; k += 64) counts[(size_t)k * nchunks + c] = h[k];
 }
 
-// stable scatter: rounds of 64 entries in order; within a round, lanes with the same node
-// are ranked by lane (peeling one node per step); a running per-node counter in LDS
-// carries the order across rounds
+// stable scatter: rounds of 64 entries in order. Within a round, the lanes that share a
+// node find each other with one ballot per bit of the dense node index (mask = lanes whose
+// index agrees on every bit), so a lane's rank among them is a popcount of the lower lanes;
+// a running per-node counter in LDS carries the order across rounds.
 __global__ void __launch_bounds__(64) k_fan_scatter(FanIn f, const uint8_t* send, const uint32_t* node_idx,
                                                     const uint32_t* n_nodes, const uint64_t* base, uint32_t nchunks,
                                                     uint32_t* out_idx) {
-    __shared__ uint32_t run[FAN_NODE_CAP];
+    extern __shared__ uint32_t run[];                        // [n_nodes]
     const uint32_t nn = *n_nodes;
     if (nn > FAN_NODE_CAP) return;
     const uint32_t c = blockIdx.x, e0 = c * FAN_CHUNK, e1 = min(e0 + FAN_CHUNK, f.n_add);
@@ -131,26 +132,29 @@ __global__ void __launch_bounds__(64) k_fan_scatter(FanIn f, const uint8_t* send
     __syncthreads();
     const int lane = threadIdx.x;
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    const int nbits = nn > 1 ? 32 - __clz((int)(nn - 1)) : 0;
     for (uint32_t r = e0; r < e1; r += 64) {
         const uint32_t e = r + lane;
         const bool on = e < e1 && (send[e] & REACH_SEND);
         const uint32_t node = on ? node_idx[f.add_res[e].z] : 0u;
-        uint64_t pending = __ballot(on);
-        uint32_t pos = 0;
-        while (pending) {
-            const int leader = __ffsll((long long)pending) - 1;
-            const uint32_t ln = __shfl(node, leader, 64);
-            const uint64_t same = __ballot(on && node == ln) & pending;
-            const uint32_t b0 = run[ln];                    // uniform read
-            if ((same >> lane) & 1ull) pos = b0 + __popcll(same & lt);
-            __builtin_amdgcn_wave_barrier();
-            if (lane == leader) run[ln] = b0 + __popcll(same);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            pending &= ~same;
+        const uint64_t act = __ballot(on);
+        if (!act) continue;                                  // wave-uniform
+        uint64_t same = act;
+        for (int b = 0; b < nbits; ++b) {
+            const bool bit = (node >> b) & 1u;
+            const uint64_t m = __ballot(on && bit);
+            same &= bit ? m : ~m;
         }
-        if (on) out_idx[pos] = e;
+        const uint32_t b0 = on ? run[node] : 0u;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const uint32_t rank = (uint32_t)__popcll(same & lt);
+        if (on && rank == 0) run[node] = b0 + (uint32_t)__popcll(same);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        if (on) out_idx[b0 + rank] = e;
     }
 }
 

@@ -333,7 +333,7 @@ __global__ void k_tc_remote_sizes(RemoteIn r, uint32_t* size);
 __global__ void k_tc_remote_write(RemoteIn r, const uint64_t* off, uint8_t* arena);
 
 // ---- RemotePod fan-out grouping (kdtn_fanout.hip) ---------------------------------------
-constexpr int FAN_CHUNK = 4096;        // add entries per single-wave workgroup
+constexpr int FAN_CHUNK = 1024;        // add entries per single-wave workgroup
 constexpr int FAN_NODE_CAP = 8192;     // destination daemons per epoch (LDS histogram)
 struct FanIn {
     const uint32_t* add_off;

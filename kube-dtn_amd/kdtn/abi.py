@@ -185,6 +185,7 @@ RESOLVED_DTYPE = np.dtype([("peer_topo", np.uint32), ("vni", np.int32), ("vtep",
                            ("kind", np.uint8), ("err", np.uint8), ("vni_hit", np.uint8),
                            ("remote_err", np.uint8)], align=True)
 assert QDISC_DTYPE.itemsize == 72 and RESOLVED_DTYPE.itemsize == 16
+VNI_OP_DTYPE = np.dtype([("node", np.uint32), ("vni", np.int32), ("net_ns", np.uint32), ("kind", np.uint32)])
 
 # symbols include/kdtn.h declares (checked by the CPU test suite)
 EXPORTS = ["kdtn_version", "kdtn_strerror", "kdtn_err_name", "kdtn_init", "kdtn_destroy",
@@ -198,7 +199,8 @@ EXPORTS = ["kdtn_version", "kdtn_strerror", "kdtn_err_name", "kdtn_init", "kdtn_
            "kdtn_json_upload", "kdtn_json_ingest", "kdtn_ingest_download", "kdtn_topology_shard",
            "kdtn_comm_set_ranks", "kdtn_pods_export", "kdtn_pods_import", "kdtn_json_ingest_shard",
            "kdtn_ingest_shard_topos", "kdtn_epoch_remote_encode", "kdtn_epoch_download_remote",
-           "kdtn_epoch_commit", "kdtn_epoch_upload_delta", "kdtn_epoch_tables_info"]
+           "kdtn_epoch_commit", "kdtn_epoch_upload_delta", "kdtn_epoch_tables_info",
+           "kdtn_vni_ops_export", "kdtn_vni_ops_import"]
 
 
 def ptr(a: np.ndarray, t):

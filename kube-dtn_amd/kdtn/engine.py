@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import weakref
 
 import numpy as np
 
@@ -101,6 +102,9 @@ def lib() -> C.CDLL:
         "kdtn_pods_import": (C.c_int, [vp, vp, C.c_uint64]),
         "kdtn_epoch_remote_encode": (C.c_int, [vp, C.POINTER(abi.RemoteInfo)]),
         "kdtn_epoch_commit": (C.c_int, [vp, vp, C.POINTER(C.c_uint32)]),
+        "kdtn_vni_ops_export": (C.c_int, [vp, vp, C.c_uint32, vp, C.c_uint32, C.POINTER(C.c_uint32),
+                                          C.POINTER(C.c_uint32)]),
+        "kdtn_vni_ops_import": (C.c_int, [vp, vp, C.c_uint32, vp, C.c_uint32]),
         "kdtn_epoch_upload_delta": (C.c_int, [vp, C.POINTER(abi.EpochDelta)]),
         "kdtn_epoch_tables_info": (C.c_int, [vp, C.POINTER(abi.IngestInfo)]),
         "kdtn_epoch_download_remote": (C.c_int, [vp, C.POINTER(abi.RemotePods)]),
@@ -116,6 +120,53 @@ def lib() -> C.CDLL:
 def _check(code: int, what: str) -> None:
     if code != abi.OK:
         raise KdtnError(code, what)
+
+
+def pinned_empty(shape, dtype) -> np.ndarray:
+    """A numpy array in page-locked host memory (kdtn_host_alloc), freed with the array."""
+    dtype = np.dtype(dtype)
+    n = int(np.prod(shape, dtype=np.int64)) * dtype.itemsize
+    L = lib()
+    p = L.kdtn_host_alloc(max(n, 1))
+    if not p:
+        raise MemoryError(f"kdtn_host_alloc({n})")
+    buf = (C.c_uint8 * max(n, 1)).from_address(p)
+    weakref.finalize(buf, L.kdtn_host_free, p)
+    return np.frombuffer(buf, dtype=np.uint8, count=n).view(dtype).reshape(shape)
+
+
+def pinned_copy(a: np.ndarray) -> np.ndarray:
+    out = pinned_empty(a.shape, a.dtype)
+    out[...] = a
+    return out
+
+
+def pin_input(inp: EpochInput) -> EpochInput:
+    """The epoch tables copied into page-locked host memory (what a controller that packs its
+    SoA straight into kdtn_host_alloc buffers uploads from)."""
+    from .tables import Links, Topos
+    P = pinned_copy
+    links = lambda L: Links(P(np.ascontiguousarray(L.key)), P(L.uid), P(np.ascontiguousarray(L.prop)), P(L.gap))
+    T = inp.topos
+    out = EpochInput(StrTab(P(inp.kdict.bytes_), P(inp.kdict.offs)), StrTab(P(inp.pdict.bytes_), P(inp.pdict.offs)),
+                     Topos(*[P(getattr(T, f)) for f in ("ns", "name", "src_ip", "net_ns", "flags", "real_off",
+                                                        "des_off")]),
+                     links(inp.realised), links(inp.desired), Vnis(P(inp.vnis.node), P(inp.vnis.vni), P(inp.vnis.net_ns)),
+                     pod_slice=inp.pod_slice, pod_base=inp.pod_base)
+    out.total_pods, out.gid = getattr(inp, "total_pods", 0), inp.gid
+    return out
+
+
+def pin_delta(d):
+    """A kdtn.delta.Delta copied into page-locked host memory."""
+    from dataclasses import replace
+    from .tables import Links
+    P = pinned_copy
+    r = d.records
+    return replace(d, kdict=StrTab(P(d.kdict.bytes_), P(d.kdict.offs)), pdict=StrTab(P(d.pdict.bytes_), P(d.pdict.offs)),
+                   topo=P(d.topo), src_ip=P(d.src_ip), net_ns=P(d.net_ns), spec_nil=P(d.spec_nil),
+                   des_off=P(d.des_off), ref=P(d.ref),
+                   records=Links(P(np.ascontiguousarray(r.key)), P(r.uid), P(np.ascontiguousarray(r.prop)), P(r.gap)))
 
 
 def topology_shard(namespace, name, nshards: int) -> int:
@@ -305,10 +356,12 @@ class Engine:
         _check(lib().kdtn_epoch_sync(self._ctx, C.byref(c)), "kdtn_epoch_sync")
         return c
 
-    def download(self) -> BatchesOut:
+    def download(self, into: BatchesOut | None = None) -> BatchesOut:
+        """kdtn_epoch_download into fresh arrays, or into `into` (e.g. BatchesOut.alloc with
+        pinned=True, reused across epochs)."""
         cd, ca, cu = self._caps
-        out = BatchesOut.alloc(self._T, cd, ca, cu)
-        b = out.to_c((max(cd, 1), max(ca, 1), max(cu, 1)))
+        out = into if into is not None else BatchesOut.alloc(self._T, cd, ca, cu)
+        b = out.to_c((len(out.del_idx), len(out.add_idx), len(out.upd_idx)))
         _check(lib().kdtn_epoch_download(self._ctx, C.byref(b)), "kdtn_epoch_download")
         return out.trim(b.n_del, b.n_add, b.n_upd)
 
@@ -424,6 +477,24 @@ class Engine:
         entries; the result also becomes the engine's resident map (Vnis.keep_resident())."""
         _check(lib().kdtn_epoch_vni_apply(self._ctx, None), "kdtn_epoch_vni_apply")
         return self.vni_download()
+
+    def vni_ops_export(self):
+        """This rank's VxlanManager ops of the last run (kdtn_vni_ops_export): (dels, adds) as
+        abi.VNI_OP_DTYPE arrays — the host transport's contribution to a sharded apply."""
+        nd, na = C.c_uint32(), C.c_uint32()
+        _check(lib().kdtn_vni_ops_export(self._ctx, None, 0, None, 0, C.byref(nd), C.byref(na)), "kdtn_vni_ops_export")
+        dels = np.zeros(max(nd.value, 1), abi.VNI_OP_DTYPE)
+        adds = np.zeros(max(na.value, 1), abi.VNI_OP_DTYPE)
+        _check(lib().kdtn_vni_ops_export(self._ctx, dels.ctypes.data, dels.size, adds.ctypes.data, adds.size,
+                                         C.byref(nd), C.byref(na)), "kdtn_vni_ops_export")
+        return dels[:nd.value], adds[:na.value]
+
+    def vni_ops_import(self, dels: np.ndarray, adds: np.ndarray) -> None:
+        """Every rank's ops concatenated in rank order (kdtn_vni_ops_import)."""
+        dels = np.ascontiguousarray(dels, abi.VNI_OP_DTYPE)
+        adds = np.ascontiguousarray(adds, abi.VNI_OP_DTYPE)
+        _check(lib().kdtn_vni_ops_import(self._ctx, dels.ctypes.data if len(dels) else None, len(dels),
+                                         adds.ctypes.data if len(adds) else None, len(adds)), "kdtn_vni_ops_import")
 
     def vni_download(self) -> Vnis:
         """kdtn_vni_download: the engine's resident VXLAN map."""

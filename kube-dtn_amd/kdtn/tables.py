@@ -190,8 +190,12 @@ class BatchesOut:
     upd_qdisc: np.ndarray
 
     @classmethod
-    def alloc(cls, T: int, cap_del: int, cap_add: int, cap_upd: int) -> "BatchesOut":
-        z = np.zeros
+    def alloc(cls, T: int, cap_del: int, cap_add: int, cap_upd: int, pinned: bool = False) -> "BatchesOut":
+        if pinned:                                       # page-locked host memory (kdtn_host_alloc)
+            from .engine import pinned_empty
+            z = pinned_empty
+        else:
+            z = np.zeros
         return cls(z(T, np.uint8), z(T + 1, np.uint32), z(T + 1, np.uint32), z(T + 1, np.uint32),
                    z(max(cap_del, 1), np.uint32), z(max(cap_add, 1), np.uint32),
                    z(max(cap_upd, 1), np.uint32),

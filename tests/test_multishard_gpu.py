@@ -115,3 +115,72 @@ def test_rccl_one_rank_communicator_equals_local_epoch():
             assert "pods_allgather" in eng.kernel_times()
             bad = got.mismatches(want)
             assert not bad, f"RCCL one-rank epoch differs from the oracle in {bad}"
+
+
+def _vni_rank(rank: int, world: int, port: int, config: int, outdir: str):
+    import torch.distributed as dist
+    from kdtn import Engine, synth
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    inp = synth.make(config, total_pods=PODS, shard=rank, nshards=world)
+    eng = Engine(device=0, tick_in_usec=15.625)
+    eng.set_ranks(world, rank)
+    eng.upload(inp)
+    mine = eng.pods_export(inp.pod_slice)
+    rows = [None] * world
+    dist.all_gather_object(rows, mine)
+    table = np.concatenate(rows)
+    eng.pods_import(table)
+    eng.run()
+    eng.sync()
+    out = eng.download()
+    dels, adds = eng.vni_ops_export()
+    got = [None] * world
+    dist.all_gather_object(got, (dels, adds))
+    eng.vni_ops_import(np.concatenate([g[0] for g in got]), np.concatenate([g[1] for g in got]))
+    vm = eng.vni_apply()
+    np.savez(os.path.join(outdir, f"v{rank}.npz"), node=vm.node, vni=vm.vni, net_ns=vm.net_ns, table=table,
+             t_src=inp.topos.src_ip, t_netns=inp.topos.net_ns, snap_node=inp.vnis.node, snap_vni=inp.vnis.vni,
+             snap_netns=inp.vnis.net_ns, **{f: getattr(out, f) for f in out.FIELDS})
+    eng.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("config,world", [(4, 2), (3, 3)])
+def test_sharded_vni_apply_equals_rank_order_oracle(config, world):
+    """kdtn_epoch_vni_apply on engine shards (host transport): every rank exports its VXLAN
+    ops, imports everyone's in rank order, and applies them against the replicated snapshot.
+    All ranks leave the same map, equal to the oracle's apply of the ranks' batches
+    concatenated in rank order (the sharded order: rank r's ops before rank r+1's)."""
+    import types
+    import torch.multiprocessing as mp
+    import oracle as O
+    from kdtn.tables import BatchesOut, Topos, Vnis
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_vni_rank, args=(world, free_port(), config, d), nprocs=world, join=True,
+                           start_method="spawn")
+        z = [dict(np.load(os.path.join(d, f"v{r}.npz"))) for r in range(world)]
+    for r in range(1, world):                                   # one node-global map
+        for f in ("node", "vni", "net_ns", "snap_node", "snap_vni", "snap_netns"):
+            assert np.array_equal(z[r][f], z[0][f]), (r, f)
+    # the ranks' batches as one rank-ordered epoch
+    cat = {}
+    for f in ("action", "del_idx", "add_idx", "upd_idx", "del_res", "add_res", "upd_res", "add_qdisc", "upd_qdisc"):
+        cat[f] = np.concatenate([x[f] for x in z])
+    for f in ("del_off", "add_off", "upd_off"):
+        parts, base = [], 0
+        for x in z:
+            parts.append(x[f][:-1].astype(np.int64) + base)
+            base += int(x[f][-1])
+        cat[f] = np.concatenate(parts + [np.array([base])]).astype(np.uint32)
+    out = BatchesOut(*[cat[f] for f in BatchesOut.FIELDS])
+    T = len(cat["action"])
+    t_src = np.concatenate([x["t_src"] for x in z])
+    t_netns = np.concatenate([x["t_netns"] for x in z])
+    fake = types.SimpleNamespace(topos=types.SimpleNamespace(n=T, src_ip=t_src, net_ns=t_netns),
+                                 vnis=Vnis(z[0]["snap_node"], z[0]["snap_vni"], z[0]["snap_netns"]))
+    want = O.vni_apply(fake, out, pod_netns=z[0]["table"][:, 3] & 0x7FFFFFFF)
+    assert np.array_equal(z[0]["node"], want[0]) and np.array_equal(z[0]["vni"], want[1])
+    assert np.array_equal(z[0]["net_ns"], want[2])
+    assert len(want[0]) > 100
