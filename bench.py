@@ -170,6 +170,18 @@ def wire_stage(eng, reps: int = 5):
     res["fanout"] = {"daemons": int(len(node)), "remote_rpcs": int(len(idx)),
                      "gpu_ms": sum(v for k, v in facc.items() if k != "fanout_host_sync"),
                      "kernels_ms": facc}
+    eng.remote_encode()
+    racc: dict[str, float] = {}
+    info = None
+    for _ in range(reps):
+        info = eng.remote_encode()            # the fan-out is cached per run: message kernels only
+        for k, v in eng.kernel_times().items():
+            racc[k] = racc.get(k, 0.0) + v / reps
+    rms = sum(v for k, v in racc.items() if k != "remote_host_sync")
+    res["remote_pods"] = {"messages": int(info.n_msgs), "remote": int(info.n_remote), "bytes": int(info.n_bytes),
+                          "tc_bytes": int(info.n_tc_bytes), "gpu_ms": rms,
+                          "out_GBps": (info.n_bytes + info.n_tc_bytes) / (rms * 1e-3) / 1e9, "kernels_ms": racc,
+                          "note": "RemotePod request bodies (kdtn_epoch_remote_encode) after the fan-out"}
     return res
 
 

@@ -592,6 +592,20 @@ int run_reach(kdtn_ctx* c, uint32_t* mark, uint32_t stamp) {
     return KDTN_OK;
 }
 
+// The encoders' string tables {offset, length | STR_BAD} of both dictionaries (kd_utf8 /
+// pd_utf8 hold them), on the context stream.
+int str_tables(kdtn_ctx* c) {
+    hipStream_t s = c->stream;
+    TRY(ensure(c->kd_utf8, (size_t)c->D * 8 + 16));
+    TRY(ensure(c->pd_utf8, (size_t)c->P * 8 + 16));
+    if (c->D) k_str_table<<<nblocks(c->D), BLOCK, 0, s>>>(dp<uint8_t>(c->kd_bytes), dp<uint32_t>(c->kd_offs), c->D,
+                                                          dp<uint2>(c->kd_utf8));
+    if (c->P) k_str_table<<<nblocks(c->P), BLOCK, 0, s>>>(dp<uint8_t>(c->pd_bytes), dp<uint32_t>(c->pd_offs), c->P,
+                                                          dp<uint2>(c->pd_utf8));
+    HIP_TRY(hipGetLastError());
+    return KDTN_OK;
+}
+
 }  // namespace
 
 // ======================================================================================
@@ -1182,9 +1196,7 @@ int kdtn_epoch_encode(kdtn_ctx* c, uint64_t* n_bytes) {
     const uint32_t T = c->T;
     const uint64_t ne = (uint64_t)nd + na + nu;
     if (ne > 0xFFFFFFFFull || 3ull * T + 1 > 0xFFFFFFFFull) return KDTN_EINVAL;
-    const uint32_t kw = (uint32_t)(((uint64_t)c->D + 63) / 64 * 2), pw = (uint32_t)(((uint64_t)c->P + 63) / 64 * 2);
-    TRY(ensure(c->kd_utf8, (size_t)kw * 4));
-    TRY(ensure(c->pd_utf8, (size_t)pw * 4));
+    TRY(str_tables(c));
     TRY(ensure(c->w_rel, (size_t)ne * 4));
     TRY(ensure(c->w_topo, (size_t)ne * 4));
     TRY(ensure(c->w_size, (size_t)3 * T * 4));
@@ -1194,19 +1206,14 @@ int kdtn_epoch_encode(kdtn_ctx* c, uint64_t* n_bytes) {
     TRY(ensure(c->w_part, (size_t)nb * 8));
     c->n_ev = 0;
     (void)hipEventRecord(c->ev[0], s);
-    if (c->D) k_utf8_bits<<<nblocks(c->D), BLOCK, 0, s>>>(dp<uint8_t>(c->kd_bytes), dp<uint32_t>(c->kd_offs), c->D,
-                                                          dp<uint32_t>(c->kd_utf8));
-    if (c->P) k_utf8_bits<<<nblocks(c->P), BLOCK, 0, s>>>(dp<uint8_t>(c->pd_bytes), dp<uint32_t>(c->pd_offs), c->P,
-                                                          dp<uint32_t>(c->pd_utf8));
-    timer_mark(c, "wire_utf8");
+
+    timer_mark(c, "wire_strtab");
     HIP_TRY(hipMemsetAsync(c->w_err.p, 0, align_up((size_t)T * 4, 16), s));
     WireIn w{};
     w.kd_bytes = dp<uint8_t>(c->kd_bytes);
-    w.kd_offs = dp<uint32_t>(c->kd_offs);
-    w.kd_utf8 = dp<uint32_t>(c->kd_utf8);
+    w.kd_tab = dp<uint2>(c->kd_utf8);
     w.pd_bytes = dp<uint8_t>(c->pd_bytes);
-    w.pd_offs = dp<uint32_t>(c->pd_offs);
-    w.pd_utf8 = dp<uint32_t>(c->pd_utf8);
+    w.pd_tab = dp<uint2>(c->pd_utf8);
     w.t_name = dp<uint32_t>(c->t_name);
     w.t_src = dp<uint32_t>(c->t_src);
     w.t_netns = dp<uint32_t>(c->t_netns);
@@ -1396,13 +1403,8 @@ int kdtn_epoch_remote_encode(kdtn_ctx* c, kdtn_remote_info* info) {
     uint64_t nphys = 0;
     HIP_TRY(hipMemcpyAsync(&nphys, dp<uint64_t>(c->rp_pos) + na, 8, hipMemcpyDeviceToHost, s));
     // UTF-8 validity of every dictionary string (proto.Marshal fails on invalid strings)
-    const uint32_t kw = (uint32_t)(((uint64_t)c->D + 63) / 64 * 2), pw = (uint32_t)(((uint64_t)c->P + 63) / 64 * 2);
-    TRY(ensure(c->kd_utf8, (size_t)kw * 4));
-    TRY(ensure(c->pd_utf8, (size_t)pw * 4));
-    if (c->D) k_utf8_bits<<<nblocks(c->D), BLOCK, 0, s>>>(dp<uint8_t>(c->kd_bytes), dp<uint32_t>(c->kd_offs), c->D,
-                                                          dp<uint32_t>(c->kd_utf8));
-    if (c->P) k_utf8_bits<<<nblocks(c->P), BLOCK, 0, s>>>(dp<uint8_t>(c->pd_bytes), dp<uint32_t>(c->pd_offs), c->P,
-                                                          dp<uint32_t>(c->pd_utf8));
+    TRY(str_tables(c));
+
     HIP_TRY(hipStreamSynchronize(s));
     timer_mark(c, "remote_select");
     const uint64_t n = (uint64_t)nr + nphys;
@@ -1410,10 +1412,9 @@ int kdtn_epoch_remote_encode(kdtn_ctx* c, kdtn_remote_info* info) {
     RemoteIn r{};
     r.kd_bytes = dp<uint8_t>(c->kd_bytes);
     r.kd_offs = dp<uint32_t>(c->kd_offs);
-    r.kd_utf8 = dp<uint32_t>(c->kd_utf8);
+    r.kd_tab = dp<uint2>(c->kd_utf8);
     r.pd_bytes = dp<uint8_t>(c->pd_bytes);
-    r.pd_offs = dp<uint32_t>(c->pd_offs);
-    r.pd_utf8 = dp<uint32_t>(c->pd_utf8);
+    r.pd_tab = dp<uint2>(c->pd_utf8);
     r.t_ns = dp<uint32_t>(c->t_ns);
     r.t_src = dp<uint32_t>(c->t_src);
     r.t_netns = dp<uint32_t>(c->t_netns);

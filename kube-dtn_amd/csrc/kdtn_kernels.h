@@ -249,13 +249,14 @@ __global__ void k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, Re
 // ---- wire encoding of the batches (kdtn_wire.hip) --------------------------------------
 constexpr int SCAN_CHUNK = BLOCK * 4;   // values per block of the batch-offset scan
 constexpr int WIRE_IMG = 12288;         // LDS bytes per wave for a wave's wire output
+// string table of a dictionary for the encoders: {arena offset, length | STR_BAD} per string,
+// STR_BAD = not valid UTF-8 — one 8-B gather gives everything a string field needs
+constexpr uint32_t STR_BAD = 0x80000000u;
 struct WireIn {
     const uint8_t* kd_bytes;
-    const uint32_t* kd_offs;
-    const uint32_t* kd_utf8;        // bitset: kdict string is not valid UTF-8
+    const uint2* kd_tab;
     const uint8_t* pd_bytes;
-    const uint32_t* pd_offs;
-    const uint32_t* pd_utf8;
+    const uint2* pd_tab;
     const uint32_t* t_name;
     const uint32_t* t_src;
     const uint32_t* t_netns;
@@ -308,10 +309,9 @@ __global__ void k_store_assemble(const uint32_t* off, uint32_t nt, const uint32_
 struct RemoteIn {
     const uint8_t* kd_bytes;
     const uint32_t* kd_offs;
-    const uint32_t* kd_utf8;
+    const uint2* kd_tab;
     const uint8_t* pd_bytes;
-    const uint32_t* pd_offs;
-    const uint32_t* pd_utf8;
+    const uint2* pd_tab;
     const uint32_t* t_ns;
     const uint32_t* t_src;
     const uint32_t* t_netns;
@@ -445,6 +445,7 @@ KD_INLINE uint64_t block_exclusive(uint64_t v, uint64_t* sh, uint64_t* total) {
 }
 
 __global__ void k_utf8_bits(const uint8_t* bytes, const uint32_t* offs, uint32_t n, uint32_t* bits);
+__global__ void k_str_table(const uint8_t* bytes, const uint32_t* offs, uint32_t n, uint2* tab);
 __global__ void k_wire_entry_sizes(WireIn w, DevLinks O, DevLinks N, WireWork wk);
 __global__ void k_wire_sizes(WireIn w, DevLinks O, DevLinks N, WireWork wk);
 __global__ void k_scan_partial(const uint32_t* size, uint32_t n, uint64_t* part);

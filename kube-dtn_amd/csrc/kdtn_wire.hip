@@ -66,6 +66,18 @@ __global__ void __launch_bounds__(BLOCK) k_utf8_bits(const uint8_t* bytes, const
     if (lane == 0 || lane == 32) bits[((i - lane) >> 5) + (lane >> 5)] = lane ? (uint32_t)(m >> 32) : (uint32_t)m;
 }
 
+// {offset, length | STR_BAD} per dictionary string (the encoders' one gather per string field)
+__global__ void __launch_bounds__(BLOCK) k_str_table(const uint8_t* bytes, const uint32_t* offs, uint32_t n,
+                                                     uint2* tab) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t b = offs[i], len = offs[i + 1] - b;
+    bool ascii = true;
+    for (uint32_t k = 0; k < len && ascii; ++k) ascii = bytes[b + k] < 0x80u;
+    const bool bad = !ascii && !utf8_ok(bytes + b, len);
+    tab[i] = make_uint2(b, len | (bad ? STR_BAD : 0u));
+}
+
 // ---- sizes ---------------------------------------------------------------------------------
 KD_INLINE uint32_t vlen(uint64_t v) {
     uint32_t n = 1;
@@ -74,45 +86,57 @@ KD_INLINE uint32_t vlen(uint64_t v) {
 }
 KD_INLINE uint32_t str_field(uint32_t len) { return len ? 1u + vlen(len) + len : 0u; }
 KD_INLINE bool bit(const uint32_t* bits, uint32_t id) { return (bits[id >> 5] >> (id & 31)) & 1u; }
-KD_INLINE uint32_t slen(const uint32_t* offs, uint32_t id) { return offs[id + 1] - offs[id]; }
+KD_INLINE uint32_t slen(uint2 r) { return r.y & ~STR_BAD; }
+// string-table entry of id (id 0 = "": no gather)
+KD_INLINE uint2 sref(const uint2* tab, uint32_t id) { return id ? tab[id] : make_uint2(0u, 0u); }
 
-// pb.LinkProperties / pb.Link sizes of record j; false if one of its strings is invalid UTF-8
-KD_INLINE bool link_sizes(const WireIn& w, const DevLinks& L, uint32_t j, uint32_t* psz, uint32_t* lsz) {
-    bool ok = true;
-    uint32_t p = 0;
+// the arena ranges of one Link record's 7 key and 12 property strings, gathered at once
+struct LinkRefs {
+    uint2 k[KDTN_NKEY], p[KDTN_NPROP];
+    uint32_t gap;
+    int64_t uid;
+};
+KD_INLINE LinkRefs link_refs(const uint2* kd_tab, const uint2* pd_tab, const DevLinks& L, uint32_t j) {
+    LinkRefs r;
+#pragma unroll
+    for (int k = 0; k < KDTN_NKEY; ++k) r.k[k] = sref(kd_tab, L.key(k, j));
+#pragma unroll
+    for (int k = 0; k < KDTN_NPROP; ++k) r.p[k] = sref(pd_tab, L.prop(k, j));
+    r.gap = L.gap(j);
+    r.uid = L.uid(j);
+    return r;
+}
+// pb.LinkProperties size (psz) and pb.Link size (lsz); false if a string is invalid UTF-8
+KD_INLINE bool link_sizes(const LinkRefs& r, uint32_t* psz, uint32_t* lsz) {
+    uint32_t bad = 0, p = 0, l = 0;
 #pragma unroll
     for (int k = 0; k < KDTN_NPROP; ++k) {
-        const uint32_t id = L.prop(k, j);
-        p += str_field(slen(w.pd_offs, id));
-        ok = ok && !bit(w.pd_utf8, id);
+        p += str_field(slen(r.p[k]));
+        bad |= r.p[k].y;
     }
-    const uint32_t gap = L.gap(j);
-    if (gap) p += 1u + vlen(gap);
-    uint32_t l = 0;
+    if (r.gap) p += 1u + vlen(r.gap);
 #pragma unroll
     for (int k = 0; k < KDTN_NKEY; ++k) {
-        const uint32_t id = L.key(k, j);
-        l += str_field(slen(w.kd_offs, id));
-        ok = ok && !bit(w.kd_utf8, id);
+        l += str_field(slen(r.k[k]));
+        bad |= r.k[k].y;
     }
-    const int64_t uid = L.uid(j);
-    if (uid) l += 1u + vlen((uint64_t)uid);
+    if (r.uid) l += 1u + vlen((uint64_t)r.uid);
     l += 1u + vlen(p) + p;
     *psz = p;
     *lsz = l;
-    return ok;
+    return (bad & STR_BAD) == 0;
 }
 
 KD_INLINE uint32_t pod_size(const WireIn& w, uint32_t t, bool* ok) {
     const uint32_t ids[4] = {w.t_name[t], w.t_src[t], w.t_netns[t], w.t_ns[t]};
-    uint32_t s = 0;
-    bool good = true;
+    uint32_t s = 0, bad = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        s += str_field(slen(w.kd_offs, ids[k]));
-        good = good && !bit(w.kd_utf8, ids[k]);
+        const uint2 r = sref(w.kd_tab, ids[k]);
+        s += str_field(slen(r));
+        bad |= r.y;
     }
-    *ok = good;
+    *ok = (bad & STR_BAD) == 0;
     return s;
 }
 
@@ -124,7 +148,7 @@ __global__ void __launch_bounds__(BLOCK) k_wire_entry_sizes(WireIn w, DevLinks O
     const uint32_t lst = g < w.list_base[1] ? 0u : (g < w.list_base[2] ? 1u : 2u);
     const uint32_t j = w.list_idx[lst][g - w.list_base[lst]];
     uint32_t psz, lsz;
-    const bool ok = link_sizes(w, lst == 0 ? O : N, j, &psz, &lsz);
+    const bool ok = link_sizes(link_refs(w.kd_tab, w.pd_tab, lst == 0 ? O : N, j), &psz, &lsz);
     wk.rel[g] = ok ? 1u + vlen(lsz) + lsz : 0xFFFFFFFFu;
 }
 
@@ -224,9 +248,10 @@ struct Sink {
         varint(len);
         const uint32_t* a32 = reinterpret_cast<const uint32_t*>(arena) + (b >> 2);
         const uint32_t sh = b & 3u;
+        const uint32_t nw = (sh + len + 3u) >> 2;          // dwords the string touches (loads only those)
         uint32_t w[9];
 #pragma unroll
-        for (int q = 0; q < 9; ++q) w[q] = a32[q];
+        for (int q = 0; q < 9; ++q) w[q] = (uint32_t)q < nw ? a32[q] : 0u;
         const uint32_t head = len < 32u ? len : 32u;
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
@@ -237,86 +262,47 @@ struct Sink {
         }
         for (uint32_t k = 32; k < len; ++k) *p++ = arena[b + k];
     }
-    KD_INLINE void str(uint32_t field, const uint8_t* arena, const uint32_t* offs, uint32_t id) {
-        const uint32_t b = offs[id], len = offs[id + 1] - b;
-        if (!len) return;
-        byte((uint8_t)(field << 3 | 2u));
-        varint(len);
-        const uint32_t* a32 = reinterpret_cast<const uint32_t*>(arena) + (b >> 2);
-        uint32_t sh = b & 3u, k = 0;
-        while (k < len) {
-            const uint32_t d = *a32++;
-            for (; sh < 4u && k < len; ++sh, ++k) *p++ = (uint8_t)(d >> (8u * sh));
-            sh = 0;
-        }
-    }
+    KD_INLINE void strr(uint32_t field, const uint8_t* arena, uint2 r) { strb(field, arena, r.x, slen(r)); }
 };
-
-KD_INLINE uint32_t pod_header_size(const WireIn& w, uint32_t t) {
-    bool ok;
-    const uint32_t ps = pod_size(w, t, &ok);
-    return 1u + vlen(ps) + ps;
-}
 
 KD_INLINE void write_entry(Sink& o, const WireIn& w, const DevLinks& L, uint32_t j, bool header, uint32_t t) {
     if (header) {                                         // LinksBatchQuery.local_pod
         bool ok;
         o.byte(1u << 3 | 2u);
         o.varint(pod_size(w, t, &ok));
-        o.str(1, w.kd_bytes, w.kd_offs, w.t_name[t]);
-        o.str(2, w.kd_bytes, w.kd_offs, w.t_src[t]);
-        o.str(3, w.kd_bytes, w.kd_offs, w.t_netns[t]);
-        o.str(4, w.kd_bytes, w.kd_offs, w.t_ns[t]);
+        o.strr(1, w.kd_bytes, sref(w.kd_tab, w.t_name[t]));
+        o.strr(2, w.kd_bytes, sref(w.kd_tab, w.t_src[t]));
+        o.strr(3, w.kd_bytes, sref(w.kd_tab, w.t_netns[t]));
+        o.strr(4, w.kd_bytes, sref(w.kd_tab, w.t_ns[t]));
     }
+    const LinkRefs r = link_refs(w.kd_tab, w.pd_tab, L, j);   // every string's range: one round trip
     uint32_t psz, lsz;
-    link_sizes(w, L, j, &psz, &lsz);
+    link_sizes(r, &psz, &lsz);
     o.byte(2u << 3 | 2u);                                 // LinksBatchQuery.links
     o.varint(lsz);
-    // every string's arena range first (independent gathers, one round trip)
-    uint32_t kb[KDTN_NKEY], kl[KDTN_NKEY], pb[KDTN_NPROP], pl[KDTN_NPROP];
-#pragma unroll
-    for (int k = 0; k < KDTN_NKEY; ++k) {
-        const uint32_t id = L.key(k, j);
-        kb[k] = w.kd_offs[id];
-        kl[k] = w.kd_offs[id + 1];
-    }
-#pragma unroll
-    for (int k = 0; k < KDTN_NPROP; ++k) {
-        const uint32_t id = L.prop(k, j);
-        pb[k] = id ? w.pd_offs[id] : 0u;              // id 0 = "" (empty: no field)
-        pl[k] = id ? w.pd_offs[id + 1] : 0u;
-    }
-#pragma unroll
-    for (int k = 0; k < KDTN_NKEY; ++k) kl[k] -= kb[k];
-#pragma unroll
-    for (int k = 0; k < KDTN_NPROP; ++k) pl[k] -= pb[k];
     // pb.Link fields in number order: peer_pod 1, local_intf 2, peer_intf 3, local_ip 4,
     // peer_ip 5, uid 6, properties 7, local_mac 8, peer_mac 9
-    o.strb(1, w.kd_bytes, kb[KDTN_K_PEER_POD], kl[KDTN_K_PEER_POD]);
-    o.strb(2, w.kd_bytes, kb[KDTN_K_LOCAL_INTF], kl[KDTN_K_LOCAL_INTF]);
-    o.strb(3, w.kd_bytes, kb[KDTN_K_PEER_INTF], kl[KDTN_K_PEER_INTF]);
-    o.strb(4, w.kd_bytes, kb[KDTN_K_LOCAL_IP], kl[KDTN_K_LOCAL_IP]);
-    o.strb(5, w.kd_bytes, kb[KDTN_K_PEER_IP], kl[KDTN_K_PEER_IP]);
-    const int64_t uid = L.uid(j);
-    if (uid) {
+    o.strr(1, w.kd_bytes, r.k[KDTN_K_PEER_POD]);
+    o.strr(2, w.kd_bytes, r.k[KDTN_K_LOCAL_INTF]);
+    o.strr(3, w.kd_bytes, r.k[KDTN_K_PEER_INTF]);
+    o.strr(4, w.kd_bytes, r.k[KDTN_K_LOCAL_IP]);
+    o.strr(5, w.kd_bytes, r.k[KDTN_K_PEER_IP]);
+    if (r.uid) {
         o.byte(6u << 3);
-        o.varint((uint64_t)uid);
+        o.varint((uint64_t)r.uid);
     }
     o.byte(7u << 3 | 2u);
     o.varint(psz);
     // pb.LinkProperties: latency 1 .. rate 6, gap 7, duplicate 8 .. corrupt_corr 13 (KDTN_P_* order)
     for (int k = 0; k < KDTN_NPROP; ++k) {
-        if (k == KDTN_P_DUPLICATE) {
-            const uint32_t gap = L.gap(j);
-            if (gap) {
-                o.byte(7u << 3);
-                o.varint(gap);
-            }
+        if (k == KDTN_P_DUPLICATE && r.gap) {
+            o.byte(7u << 3);
+            o.varint(r.gap);
         }
-        o.strb((uint32_t)(k < KDTN_P_DUPLICATE ? k + 1 : k + 2), w.pd_bytes, pb[k], pl[k]);
+        o.strr((uint32_t)(k < KDTN_P_DUPLICATE ? k + 1 : k + 2), w.pd_bytes, r.p[k]);
     }
-    o.strb(8, w.kd_bytes, kb[KDTN_K_LOCAL_MAC], kl[KDTN_K_LOCAL_MAC]);
-    o.strb(9, w.kd_bytes, kb[KDTN_K_PEER_MAC], kl[KDTN_K_PEER_MAC]);
+    o.strr(8, w.kd_bytes, r.k[KDTN_K_LOCAL_MAC]);
+    o.strr(9, w.kd_bytes, r.k[KDTN_K_PEER_MAC]);
 }
 
 // One thread per entry of the three lists (global entry index g). Consecutive entries
@@ -413,12 +399,12 @@ __global__ void __launch_bounds__(BLOCK) k_remote_phys_scatter(const uint32_t* f
     if (e < na && flag[e]) phys_idx[pos[e]] = e;
 }
 
-// the strings of message m as kdict arena ranges, in field order net_ns, intf_name, intf_ip,
-// peer_vtep, kube_ns, name; record j carries the properties
+// the strings of message m as arena ranges, in field order net_ns, intf_name, intf_ip,
+// peer_vtep, kube_ns, name, and the link's properties
 struct RemoteMsg {
-    uint32_t b[6], l[6];
+    uint2 s[6], p[KDTN_NPROP];
+    uint32_t gap;
     int32_t vni;
-    uint32_t j;
     bool ok;                        // every string valid UTF-8
 };
 
@@ -444,42 +430,35 @@ KD_INLINE RemoteMsg remote_msg(const RemoteIn& r, uint32_t m) {
     }
     id[4] = r.t_ns[t];                              // localPod.KubeNs
     id[5] = peer_pod;
-    bool ok = true;
+    uint32_t bad = 0;
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
-        q.b[k] = r.kd_offs[id[k]];
-        q.l[k] = r.kd_offs[id[k] + 1];
-        ok = ok && !bit(r.kd_utf8, id[k]);
+        q.s[k] = sref(r.kd_tab, id[k]);
+        bad |= q.s[k].y;
     }
 #pragma unroll
-    for (int k = 0; k < 6; ++k) q.l[k] -= q.b[k];
+    for (int k = 0; k < KDTN_NPROP; ++k) {
+        q.p[k] = sref(r.pd_tab, r.N.prop(k, j));
+        bad |= q.p[k].y;
+    }
     if (!remote) {
-        q.b[3] += 9u;
-        q.l[3] -= 9u;
+        q.s[3].x += 9u;
+        q.s[3].y -= 9u;
     }
-#pragma unroll
-    for (int k = 0; k < KDTN_NPROP; ++k) ok = ok && !bit(r.pd_utf8, r.N.prop(k, j));
+    q.gap = r.N.gap(j);
     q.vni = (int32_t)res.y;
-    q.j = j;
-    q.ok = ok;
+    q.ok = (bad & STR_BAD) == 0;
     return q;
 }
 
-KD_INLINE uint32_t remote_props_size(const RemoteIn& r, uint32_t j) {
-    uint32_t p = 0;
+KD_INLINE uint32_t remote_body_size(const RemoteMsg& q, uint32_t* psz) {
+    uint32_t n = 0, p = 0;
 #pragma unroll
-    for (int k = 0; k < KDTN_NPROP; ++k) p += str_field(slen(r.pd_offs, r.N.prop(k, j)));
-    const uint32_t gap = r.N.gap(j);
-    if (gap) p += 1u + vlen(gap);
-    return p;
-}
-
-KD_INLINE uint32_t remote_body_size(const RemoteIn& r, const RemoteMsg& q, uint32_t* psz) {
-    uint32_t n = 0;
-#pragma unroll
-    for (int k = 0; k < 6; ++k) n += str_field(q.l[k]);
+    for (int k = 0; k < 6; ++k) n += str_field(slen(q.s[k]));
     if (q.vni) n += 1u + vlen((uint64_t)(int64_t)q.vni);
-    const uint32_t p = remote_props_size(r, q.j);
+#pragma unroll
+    for (int k = 0; k < KDTN_NPROP; ++k) p += str_field(slen(q.p[k]));
+    if (q.gap) p += 1u + vlen(q.gap);
     *psz = p;
     return n + 1u + vlen(p) + p;
 }
@@ -489,41 +468,29 @@ __global__ void __launch_bounds__(BLOCK) k_remote_sizes(RemoteIn r, uint32_t* si
     if (m >= r.n_msgs) return;
     const RemoteMsg q = remote_msg(r, m);
     uint32_t psz;
-    const uint32_t body = remote_body_size(r, q, &psz);
+    const uint32_t body = remote_body_size(q, &psz);
     size[m] = q.ok ? vlen(body) + body : 0u;
 }
 
 KD_INLINE void write_remote(Sink& o, const RemoteIn& r, const RemoteMsg& q) {
     uint32_t psz;
-    o.varint(remote_body_size(r, q, &psz));
+    o.varint(remote_body_size(q, &psz));
 #pragma unroll
-    for (int k = 0; k < 5; ++k) o.strb((uint32_t)k + 1, r.kd_bytes, q.b[k], q.l[k]);
+    for (int k = 0; k < 5; ++k) o.strr((uint32_t)k + 1, r.kd_bytes, q.s[k]);
     if (q.vni) {
         o.byte(6u << 3);
         o.varint((uint64_t)(int64_t)q.vni);
     }
     o.byte(7u << 3 | 2u);
     o.varint(psz);
-    uint32_t pb[KDTN_NPROP], pl[KDTN_NPROP];
-#pragma unroll
     for (int k = 0; k < KDTN_NPROP; ++k) {
-        const uint32_t id = r.N.prop(k, q.j);
-        pb[k] = id ? r.pd_offs[id] : 0u;
-        pl[k] = id ? r.pd_offs[id + 1] : 0u;
-    }
-#pragma unroll
-    for (int k = 0; k < KDTN_NPROP; ++k) pl[k] -= pb[k];
-    for (int k = 0; k < KDTN_NPROP; ++k) {
-        if (k == KDTN_P_DUPLICATE) {
-            const uint32_t gap = r.N.gap(q.j);
-            if (gap) {
-                o.byte(7u << 3);
-                o.varint(gap);
-            }
+        if (k == KDTN_P_DUPLICATE && q.gap) {
+            o.byte(7u << 3);
+            o.varint(q.gap);
         }
-        o.strb((uint32_t)(k < KDTN_P_DUPLICATE ? k + 1 : k + 2), r.pd_bytes, pb[k], pl[k]);
+        o.strr((uint32_t)(k < KDTN_P_DUPLICATE ? k + 1 : k + 2), r.pd_bytes, q.p[k]);
     }
-    o.strb(8, r.kd_bytes, q.b[5], q.l[5]);
+    o.strr(8, r.kd_bytes, q.s[5]);
 }
 
 // one thread per message; a wave's messages are one contiguous range, assembled in the
