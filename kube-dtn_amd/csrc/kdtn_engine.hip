@@ -101,7 +101,7 @@ struct kdtn_ctx {
     uint32_t slice = 0, pod_total = 0, ovf_mask = 0, kb_words = 0, pod_stamp = 0;
     bool traced = false;
     // work
-    DevBuf otarget, sync, misc, hscratch, fscratch, trace;
+    DevBuf otarget, sync, misc, hscratch, fscratch, trace, stage;
     uint32_t nwg = 0;
     // outputs
     DevBuf action, del_off, add_off, upd_off, del_idx, add_idx, upd_idx;
@@ -299,21 +299,61 @@ int check_offsets(const uint32_t* off, uint32_t T, uint32_t n, const char* what)
     return KDTN_OK;
 }
 
+constexpr uint32_t STAGED_UPLOAD_MIN = 1u << 16;   // records: below it, 2-D copies straight into tiles
+
 int upload_links(kdtn_ctx* c, DevLinkStore& s, const kdtn_link_table& L, uint32_t D, uint32_t P,
                  const char* what) {
     const uint32_t n = L.n;
-    for (int k = 0; k < KDTN_NKEY; ++k) TRY(check_ids(L.key[k], n, D, what));
-    for (int k = 0; k < KDTN_NPROP; ++k) TRY(check_ids(L.prop[k], n, P, what));
+    for (int k = 0; k < KDTN_NKEY; ++k)
+        if (n && !L.key[k]) return check_ids(L.key[k], n, D, what);          // missing column
+    for (int k = 0; k < KDTN_NPROP; ++k)
+        if (n && !L.prop[k]) return check_ids(L.prop[k], n, P, what);
     if (n && (!L.uid || !L.gap)) {
         std::snprintf(g_last_error, sizeof(g_last_error), "%s: missing uid/gap", what);
         return KDTN_EINVAL;
     }
-    // tiles of 64 records (kdtn_kernels.h DevLinks): each column is a 2-D copy with a
-    // 256-B (uid: 512-B) run per tile
     const size_t tiles = ((size_t)std::max<uint32_t>(n, 1) + TILE_RECS - 1) / TILE_RECS;
     const size_t tile_bytes = (size_t)TILE_WORDS * 4;
     TRY(ensure(s.buf, tiles * tile_bytes));
     uint8_t* base = static_cast<uint8_t*>(s.buf.p);
+    s.view.base = reinterpret_cast<const uint32_t*>(base);
+    s.view.n = n;
+    s.n = n;
+    if (n >= STAGED_UPLOAD_MIN) {
+        // large tables: one linear copy per column (full host-link rate) into a staging buffer,
+        // then the tiles and the id-range check in one GPU pass (no host pass over the columns)
+        const size_t col = (size_t)n * 4, uid_at = align_up(col * LINK_COLS32, 8);
+        TRY(ensure(c->stage, uid_at + (size_t)n * 8 + 128));
+        uint8_t* st = static_cast<uint8_t*>(c->stage.p);
+        for (int k = 0; k < KDTN_NKEY; ++k)
+            HIP_TRY(hipMemcpyAsync(st + (COL_KEY0 + k) * col, L.key[k], col, hipMemcpyHostToDevice, c->stream));
+        for (int k = 0; k < KDTN_NPROP; ++k)
+            HIP_TRY(hipMemcpyAsync(st + (COL_PROP0 + k) * col, L.prop[k], col, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(st + COL_GAP * col, L.gap, col, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(st + uid_at, L.uid, (size_t)n * 8, hipMemcpyHostToDevice, c->stream));
+        TRY(ensure(c->misc, 256));
+        uint32_t* colmax = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(c->misc.p) + MISC_COLMAX * 4);
+        HIP_TRY(hipMemsetAsync(colmax, 0, COL_GAP * 4, c->stream));
+        k_soa_to_tiles<<<std::min<uint32_t>((n + BLOCK - 1) / BLOCK, 4 * c->n_cus), BLOCK, 0, c->stream>>>(
+            reinterpret_cast<const uint32_t*>(st), reinterpret_cast<const int64_t*>(st + uid_at), n,
+            reinterpret_cast<uint32_t*>(base), colmax);
+        HIP_TRY(hipGetLastError());
+        uint32_t mx[COL_GAP];
+        HIP_TRY(hipMemcpyAsync(mx, colmax, sizeof(mx), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        for (int k = 0; k < COL_GAP; ++k) {
+            const uint32_t lim = k < KDTN_NKEY ? D : P;
+            if (mx[k] >= lim) {
+                std::snprintf(g_last_error, sizeof(g_last_error), "%s: id %u out of range (%u strings)", what, mx[k], lim);
+                return KDTN_EINVAL;
+            }
+        }
+        return KDTN_OK;
+    }
+    for (int k = 0; k < KDTN_NKEY; ++k) TRY(check_ids(L.key[k], n, D, what));
+    for (int k = 0; k < KDTN_NPROP; ++k) TRY(check_ids(L.prop[k], n, P, what));
+    // tiles of 64 records (kdtn_kernels.h DevLinks): each column is a 2-D copy with a
+    // 256-B (uid: 512-B) run per tile
     auto put = [&](int col, const void* src, size_t esz) -> int {
         const size_t full = n / TILE_RECS, tail = n % TILE_RECS;
         const size_t run = TILE_RECS * esz;
@@ -331,9 +371,6 @@ int upload_links(kdtn_ctx* c, DevLinkStore& s, const kdtn_link_table& L, uint32_
         TRY(put(COL_GAP, L.gap, 4));
         TRY(put(COL_UID, L.uid, 8));
     }
-    s.view.base = reinterpret_cast<const uint32_t*>(base);
-    s.view.n = n;
-    s.n = n;
     return KDTN_OK;
 }
 
@@ -545,7 +582,7 @@ int prepare_work(kdtn_ctx* c, uint32_t slice, uint32_t M, uint32_t N) {
     c->nwg = nwg;
     TRY(ensure(c->otarget, (size_t)M * 4));
     TRY(ensure(c->sync, sync_bytes(nwg)));
-    TRY(ensure(c->misc, 64));
+    TRY(ensure(c->misc, 256));
     TRY(ensure(c->hscratch, ((size_t)M + N) * 4));
     TRY(ensure(c->fscratch, (size_t)M + N));
     TRY(ensure(c->action, c->T));
@@ -719,7 +756,7 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->rp_msz, &c->rp_moff, &c->rp_tsz, &c->rp_toff, &c->rp_part, &c->rp_arena, &c->rp_tc,
                       &c->st_len, &c->st_base, &c->st_mode, &c->st_flags, &c->st_off64, &c->st_part,
                       &c->st_off32, &c->st_mask, &c->st_chg, &c->dl_topo, &c->dl_src, &c->dl_netns, &c->dl_nil,
-                      &c->dl_off, &c->dl_ref, &c->dl_rec.buf, &c->vx_cnt, &c->vx_send, &c->vx_recv,
+                      &c->dl_off, &c->dl_ref, &c->dl_rec.buf, &c->stage, &c->vx_cnt, &c->vx_send, &c->vx_recv,
                       &c->vx_gops};
     for (DevBuf* b : bufs) release(*b);
     for (int i = 0; i <= kMaxTimers; ++i)
@@ -770,6 +807,7 @@ int kdtn_epoch_upload(kdtn_ctx* c, const kdtn_epoch_in* in) {
     if (slice < T.n) return KDTN_EINVAL;
 
     TRY(check_keep(c, in->kdict, in->pdict, in->kdict_keep, in->pdict_keep));
+    c->uploaded = false;                            // a failure from here on leaves no usable epoch
     c->T = T.n;
     TRY(upload_dicts(c, in->kdict, in->pdict, in->kdict_keep, in->pdict_keep));
 
@@ -2564,6 +2602,7 @@ int kdtn_epoch_upload_delta(kdtn_ctx* c, const kdtn_epoch_delta* d) {
     TRY(check_ids(d->net_ns, n, D, "delta.net_ns"));
     TRY(check_vnis(c, d->vnis, D, d->kdict_keep));
     TRY(check_keep(c, d->kdict, d->pdict, d->kdict_keep, d->pdict_keep));
+    c->uploaded = false;                            // a failure from here on leaves no usable epoch
     TRY(upload_dicts(c, d->kdict, d->pdict, d->kdict_keep, d->pdict_keep));
     TRY(upload_links(c, c->dl_rec, d->records, D, P, "delta.records"));
     TRY(upload(c, c->dl_topo, d->topo, (size_t)n * 4));
@@ -2600,6 +2639,7 @@ int kdtn_epoch_upload_delta(kdtn_ctx* c, const kdtn_epoch_delta* d) {
     HIP_TRY(hipStreamSynchronize(s));              // host arrays may be released after return
     state_changed(c);
     c->pods_imported = false;
+    c->uploaded = true;
     return KDTN_OK;
 }
 

@@ -118,4 +118,45 @@ __global__ void __launch_bounds__(BLOCK) k_store_assemble(const uint32_t* off, u
     }
 }
 
+// Link-store upload from SoA columns: the host columns arrive by linear copies into a staging
+// buffer (stage + c*n: the 7 key, 12 property and gap columns; the uid column after them), and
+// this pass writes the 64-record tiles (coalesced on both sides) and takes the maximum of every
+// id column (colmax[0..18]) for the range check the host makes before the upload is accepted.
+__global__ void __launch_bounds__(BLOCK) k_soa_to_tiles(const uint32_t* stage, const int64_t* uid, uint32_t n,
+                                                        uint32_t* out, uint32_t* colmax) {
+    __shared__ uint32_t red[BLOCK / 64][COL_GAP];
+    uint32_t mx[COL_GAP];
+#pragma unroll
+    for (int c = 0; c < COL_GAP; ++c) mx[c] = 0;
+    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
+        uint32_t* dst = out + (size_t)(i >> 6) * TILE_WORDS + (i & 63u);
+#pragma unroll
+        for (int c = 0; c < LINK_COLS32; ++c) {
+            const uint32_t v = __builtin_nontemporal_load(stage + (size_t)c * n + i);
+            if (c < COL_GAP) mx[c] = v > mx[c] ? v : mx[c];
+            dst[c * TILE_RECS] = v;
+        }
+        reinterpret_cast<int64_t*>(out + (size_t)(i >> 6) * TILE_WORDS + LINK_COLS32 * TILE_RECS)[i & 63u] =
+            __builtin_nontemporal_load(uid + i);
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int c = 0; c < COL_GAP; ++c) {
+        uint32_t v = mx[c];
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            const uint32_t o = __shfl_xor(v, d, 64);
+            v = o > v ? o : v;
+        }
+        if (lane == 0) red[wave][c] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < COL_GAP) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int w = 0; w < BLOCK / 64; ++w) v = red[w][threadIdx.x] > v ? red[w][threadIdx.x] : v;
+        atomicMax(colmax + threadIdx.x, v);
+    }
+}
+
 }  // namespace kdtn

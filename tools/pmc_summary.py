@@ -6,7 +6,7 @@ import sys
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
 agg = collections.defaultdict(list)
-for f in sorted(glob.glob(f"{root}/[pv]*/run_counter_collection.csv")):
+for f in sorted(glob.glob(f"{root}/*/**/*counter_collection.csv", recursive=True)):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"].split("(")[0].replace("kdtn::", "")
         agg[(k, r["Counter_Name"])].append(float(r["Counter_Value"]))

@@ -1,0 +1,55 @@
+"""One config-2 epoch and its output stages in one process, for rocprofv3 runs.
+
+    python tools/stage_run.py [--pods N] [--reps R] [--cache DIR] [--stages run,encode,fanout,remote,tc]
+Prints the HIP-event kernel times per stage (mean over reps) as JSON.
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch  # noqa: F401  (one HIP runtime)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "kube-dtn_amd"))
+from kdtn import Engine, synth  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--pods", type=int, default=1_000_000)
+ap.add_argument("--config", type=int, default=2)
+ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--cache", default="/tmp/kdtn_cache")
+ap.add_argument("--stages", default="run,encode,fanout,remote,tc")
+a = ap.parse_args()
+inp = synth.make(a.config, pods_per_shard=a.pods, cache_dir=a.cache or None)
+eng = Engine(device=0)
+eng.upload(inp)
+stages = a.stages.split(",")
+res = {}
+
+
+def timed(name, fn):
+    acc = {}
+    for _ in range(a.reps):
+        fn()
+        for k, v in eng.kernel_times().items():
+            acc[k] = acc.get(k, 0.0) + v / a.reps
+    res[name] = {k: round(v, 4) for k, v in acc.items()}
+
+
+def run():
+    eng.run()
+    eng.sync()
+
+
+timed("run", run)
+if "encode" in stages:
+    timed("encode", eng.encode)
+if "fanout" in stages:
+    timed("fanout", eng.fanout)
+if "remote" in stages:
+    timed("remote", eng.remote_encode)
+if "tc" in stages:
+    c = eng.sync()
+    timed("tc", lambda: eng.tc_argv(c.n_add, c.n_upd))
+print(json.dumps({"config": a.config, "pods": a.pods, "links": inp.desired.n, "ms": res}, indent=1))
