@@ -99,6 +99,11 @@ struct kdtn_ctx {
     // pods
     DevBuf pods, pod_ovf, pod_direct;
     uint32_t slice = 0, pod_total = 0, ovf_mask = 0, kb_words = 0, pod_stamp = 0;
+    // pods_ready: pods / pod_direct / pod_ovf hold the complete tables of the current rows (a
+    // full build ran and every later row change was patched). pods_delta: this upload's rows were
+    // patched in kdtn_epoch_upload_delta, so its runs do no pod-table work.
+    bool pods_ready = false, pods_delta = false;
+    DevBuf pd_send, pd_recv, pd_cnt;
     bool traced = false;
     // work
     DevBuf otarget, sync, misc, hscratch, fscratch, trace, stage;
@@ -122,7 +127,7 @@ struct kdtn_ctx {
     bool rp_done = false;
     // resident state: commit / delta plans, the delta's arrays and inline records
     DevBuf st_len, st_base, st_mode, st_flags, st_off64, st_part, st_off32, st_mask, st_chg;
-    DevBuf dl_topo, dl_src, dl_netns, dl_nil, dl_off, dl_ref;
+    DevBuf dl_topo, dl_src, dl_netns, dl_nil, dl_off, dl_ref, dl_rows;
     DevLinkStore dl_rec;
     bool tables_cur = false;                   // j_info describes the current tables (kdtn_epoch_tables_info)
     // tc argv
@@ -525,6 +530,7 @@ void end_shard_ingest(kdtn_ctx* c) {
     c->rank = c->sh_saved_rank;
     c->pods_rank_major = true;
     c->pods_imported = false;
+    c->pods_ready = false;                        // the pod table was in document order
     c->sh_T = 0;
     c->sh_active = false;
 }
@@ -560,6 +566,7 @@ int prepare_vnis(kdtn_ctx* c, const kdtn_vni_table& vn) {
 // pod tables, work and output buffers for T = c->T topologies, M realised and N desired records
 int prepare_work(kdtn_ctx* c, uint32_t slice, uint32_t M, uint32_t N) {
     const uint32_t D = c->D;
+    if (slice != c->slice) c->pods_ready = false;
     c->slice = slice;
     if ((uint64_t)slice * (uint64_t)c->nranks > POD_INDEX) {
         std::snprintf(g_last_error, sizeof(g_last_error), "pod table of %llu entries exceeds 2^30",
@@ -574,8 +581,11 @@ int prepare_work(kdtn_ctx* c, uint32_t slice, uint32_t M, uint32_t N) {
         HIP_TRY(hipMemsetAsync(c->pod_ovf.p, 0, c->pod_ovf.cap, c->stream));
     }
     if (c->pod_direct.cap < (size_t)D * 16) {                  // stamps start from a zeroed table
-        TRY(ensure(c->pod_direct, (size_t)D * 16));
+        // headroom for append-only dictionaries: slots of ids past the last build read as empty
+        // (stamp 0), so a delta upload that adds strings keeps the built table
+        TRY(ensure(c->pod_direct, (size_t)D * 16 + (size_t)D * 4 + 4096));
         HIP_TRY(hipMemsetAsync(c->pod_direct.p, 0, c->pod_direct.cap, c->stream));   // stamp 0 = empty
+        c->pods_ready = false;
     }
 
     const uint32_t nwg = (c->T + TPW - 1) / TPW;
@@ -757,7 +767,7 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->st_len, &c->st_base, &c->st_mode, &c->st_flags, &c->st_off64, &c->st_part,
                       &c->st_off32, &c->st_mask, &c->st_chg, &c->dl_topo, &c->dl_src, &c->dl_netns, &c->dl_nil,
                       &c->dl_off, &c->dl_ref, &c->dl_rec.buf, &c->stage, &c->vx_cnt, &c->vx_send, &c->vx_recv,
-                      &c->vx_gops};
+                      &c->vx_gops, &c->pd_send, &c->pd_recv, &c->pd_cnt, &c->dl_rows};
     for (DevBuf* b : bufs) release(*b);
     for (int i = 0; i <= kMaxTimers; ++i)
         if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
@@ -830,6 +840,8 @@ int kdtn_epoch_upload(kdtn_ctx* c, const kdtn_epoch_in* in) {
     c->pods_imported = false;
     c->j_done = false;                             // the tables are no ingest's any more
     c->tables_cur = false;
+    c->pods_ready = false;                         // new rows: the next run builds the pod tables
+    c->pods_delta = false;
     return KDTN_OK;
 }
 
@@ -842,8 +854,10 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
     hipStream_t s = c->stream;
     const DevTopos T = topo_view(c);
     const bool resolve = stages & KDTN_STAGE_RESOLVE;
-    const bool host_xchg = resolve && c->nranks > 1 && !c->comm;      // rows imported by the caller
-    const bool exchange = resolve && c->comm;                          // RCCL (a 1-rank comm too)
+    // pod tables already current (patched by kdtn_epoch_upload_delta): no fill, exchange or build
+    const bool pods_cur = resolve && c->pods_delta && c->pods_ready;
+    const bool host_xchg = resolve && !pods_cur && c->nranks > 1 && !c->comm;   // rows imported by the caller
+    const bool exchange = resolve && !pods_cur && c->comm;                       // RCCL (a 1-rank comm too)
     if (host_xchg && !c->pods_imported) {
         std::snprintf(g_last_error, sizeof(g_last_error),
                       "host transport: kdtn_pods_import the gathered pod table before kdtn_epoch_run");
@@ -857,7 +871,7 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         // while this stream parses the dictionaries (the exchange needs neither)
         const uint32_t n16 = (uint32_t)(sync_bytes(c->nwg) / 16);
         const uint32_t nbz = std::min<uint32_t>(nblocks(n16), 256);
-        const uint32_t fill = (resolve && !host_xchg) ? c->slice : 0u;
+        const uint32_t fill = (resolve && !host_xchg && !pods_cur) ? c->slice : 0u;
         const uint32_t rank_base = c->slice * (uint32_t)c->rank;
         k_epoch_begin<<<nbz + nblocks(fill), BLOCK, 0, s>>>(reinterpret_cast<uint4*>(sync), n16, nbz, T, fill,
                                                             rank_base, dp<uint4>(c->pods));
@@ -910,12 +924,12 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
     if (resolve) {
         if (exchange) HIP_TRY(hipStreamWaitEvent(s, c->ev_ag, 0));   // exchange not hidden by the parses
         timer_mark(c, "pods_allgather", 2);
-        if (++c->pod_stamp >= 0x7FFFFFFFu) {                          // stamp wrap: clear once
+        if (!pods_cur && ++c->pod_stamp >= 0x7FFFFFFFu) {             // stamp wrap: clear once
             HIP_TRY(hipMemsetAsync(c->pod_direct.p, 0, c->pod_direct.cap, s));
             HIP_TRY(hipMemsetAsync(c->pod_ovf.p, 0, c->pod_ovf.cap, s));
             c->pod_stamp = 1;
         }
-        if (c->pod_total) {
+        if (c->pod_total && !pods_cur) {
             k_pod_direct_scatter<<<nblocks(c->pod_total), BLOCK, 0, s>>>(
                 dp<uint4>(c->pods), c->pod_total, dp<uint32_t>(c->kd_bits) + (size_t)KB_PHYSICAL * c->kb_words,
                 dp<uint4>(c->pod_direct), c->pod_stamp, c->D, c->pods_rank_major ? (uint32_t)c->nranks : 1u);
@@ -989,7 +1003,7 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
 #if KDTN_PROFILING
         if (const char* ev = std::getenv("KDTN_SPLIT")) if (std::atoi(ev) > 0) w.split = (uint32_t)std::atoi(ev);
 #endif
-        if (resolve && c->pod_total) {                  // the pod-table verify with the full-prefix scan
+        if (resolve && c->pod_total && !pods_cur) {     // the pod-table verify with the full-prefix scan
             const uint32_t nbv = nblocks(c->pod_total);
             const uint32_t nbp = (uint32_t)std::min<uint64_t>(4 * FP_GRID, (c->T + 4 * BLOCK - 1) / (4 * BLOCK));
             k_pod_verify_prefix<<<nbv + std::max<uint32_t>(nbp, 1), BLOCK, 0, s>>>(
@@ -1048,6 +1062,7 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
     }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(c->h_misc + 1, sync + SYNC_TOTALS, 16, hipMemcpyDeviceToHost, s));   // totals, look-back error
+    if (resolve && !pods_cur) c->pods_ready = true;           // the full build of this upload's rows
     c->ran = true;
     c->encoded = false;
     c->tc_done = false;
@@ -1955,6 +1970,8 @@ static int json_ingest_full(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest
     if (info) *info = c->j_info;
     c->j_done = true;
     c->uploaded = true;
+    c->pods_ready = false;
+    c->pods_delta = false;
     return KDTN_OK;
 }
 
@@ -2499,6 +2516,63 @@ int plan_offsets(kdtn_ctx* c, uint32_t T, uint64_t* total) {
     return KDTN_OK;
 }
 
+// The resident pod tables after a delta: the changed Topologies' rows (dl_topo, n of them on
+// this rank) patched into the pod table and their lookup slots, instead of the next runs
+// refilling, exchanging and rebuilding all of them. Across RCCL ranks the changed rows are
+// all-gathered (the per-rank counts first, then the rows padded to the largest count); when
+// some rank changed more than a quarter of a slice, or the tables are not resident (host
+// transport, no full build yet), the next run does the full build instead.
+int patch_pods(kdtn_ctx* c, uint32_t n) {
+    c->pods_delta = false;
+    if (!c->pods_ready) return KDTN_OK;
+    const bool rccl = c->comm != nullptr;
+    if (c->nranks > 1 && (!rccl || !c->pods_rank_major)) {
+        c->pods_ready = false;
+        return KDTN_OK;
+    }
+    hipStream_t s = c->stream;
+    const int G = rccl ? c->nranks : 1;
+    uint32_t m = n;
+    if (G > 1) {
+        TRY(ensure(c->pd_cnt, (size_t)G * 4 + 16));
+        uint32_t* cnt = dp<uint32_t>(c->pd_cnt);
+        HIP_TRY(hipMemcpyAsync(cnt + c->rank, &n, 4, hipMemcpyHostToDevice, s));
+        ncclResult_t r = ncclAllGather(cnt + c->rank, cnt, 1, ncclUint32, c->comm, s);
+        if (r != ncclSuccess) {
+            std::snprintf(g_last_error, sizeof(g_last_error), "ncclAllGather (changed pod rows): %s", ncclGetErrorString(r));
+            return KDTN_EIO;
+        }
+        std::vector<uint32_t> h((size_t)G);
+        HIP_TRY(hipMemcpyAsync(h.data(), cnt, (size_t)G * 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        m = *std::max_element(h.begin(), h.end());
+    }
+    if ((uint64_t)m * 4 > (uint64_t)c->slice + 4096) {      // a full exchange is cheaper
+        c->pods_ready = false;
+        return KDTN_OK;
+    }
+    if (m) {
+        TRY(ensure(c->pd_send, (size_t)m * 32));
+        TRY(ensure(c->pd_recv, (size_t)m * G * 32));
+        k_pods_pack<<<nblocks(m), BLOCK, 0, s>>>(topo_view(c), dp<uint32_t>(c->dl_rows), n, m,
+                                                 c->slice * (uint32_t)c->rank, dp<uint4>(c->pd_send));
+        const uint4* ent = dp<uint4>(c->pd_send);
+        if (G > 1) {
+            ncclResult_t r = ncclAllGather(c->pd_send.p, c->pd_recv.p, (size_t)m * 8, ncclUint32, c->comm, s);
+            if (r != ncclSuccess) {
+                std::snprintf(g_last_error, sizeof(g_last_error), "ncclAllGather (pod rows): %s", ncclGetErrorString(r));
+                return KDTN_EIO;
+            }
+            ent = dp<uint4>(c->pd_recv);
+        }
+        k_pods_patch<<<nblocks((uint64_t)m * G), BLOCK, 0, s>>>(ent, m * (uint32_t)G, dp<uint4>(c->pods),
+                                                               dp<uint4>(c->pod_direct), c->pod_stamp, c->D);
+        HIP_TRY(hipGetLastError());
+    }
+    c->pods_delta = true;
+    return KDTN_OK;
+}
+
 // per-topology plan arrays for T topologies
 int plan_alloc(kdtn_ctx* c, uint32_t T) {
     TRY(ensure(c->st_len, (size_t)T * 4 + 16));
@@ -2616,13 +2690,18 @@ int kdtn_epoch_upload_delta(kdtn_ctx* c, const kdtn_epoch_delta* d) {
     TRY(ensure(c->st_chg, (size_t)T * 4 + 16));
     HIP_TRY(hipMemsetAsync(c->st_chg.p, 0xFF, (size_t)T * 4, s));
     if (n) k_delta_map<<<nblocks(n), BLOCK, 0, s>>>(dp<uint32_t>(c->dl_topo), n, dp<uint32_t>(c->st_chg));
+    TRY(ensure(c->dl_rows, (size_t)n * 4 + 16));
+    uint32_t* rown = dp<uint32_t>(c->misc) + MISC_ROWCHG_N;
+    HIP_TRY(hipMemsetAsync(rown, 0, 4, s));
     if (T)
         k_delta_plan<<<nblocks(T), BLOCK, 0, s>>>(topo_view(c), dp<uint32_t>(c->st_chg), dp<uint32_t>(c->dl_off),
                                                   dp<uint32_t>(c->dl_src), dp<uint32_t>(c->dl_netns),
                                                   dp<uint8_t>(c->dl_nil), dp<uint32_t>(c->st_len),
                                                   dp<uint32_t>(c->st_base), dp<uint8_t>(c->st_mode),
                                                   dp<uint32_t>(c->t_src), dp<uint32_t>(c->t_netns),
-                                                  dp<uint8_t>(c->t_flags));
+                                                  dp<uint8_t>(c->t_flags), dp<uint32_t>(c->dl_rows), rown);
+    uint32_t n_rows = 0;
+    HIP_TRY(hipMemcpyAsync(&n_rows, rown, 4, hipMemcpyDeviceToHost, s));
     uint64_t N = 0;
     TRY(plan_offsets(c, T, &N));
     TRY(link_store_alloc(c, c->sh_des, (uint32_t)N));
@@ -2636,6 +2715,7 @@ int kdtn_epoch_upload_delta(kdtn_ctx* c, const kdtn_epoch_delta* d) {
     std::swap(c->t_noff, c->st_off32);
     TRY(prepare_vnis(c, d->vnis));
     TRY(prepare_work(c, c->slice, c->real.n, c->des.n));
+    TRY(patch_pods(c, n_rows));
     HIP_TRY(hipStreamSynchronize(s));              // host arrays may be released after return
     state_changed(c);
     c->pods_imported = false;

@@ -49,7 +49,7 @@ enum : int {
 };
 // special key-string ids found by k_kdict_flags (0xFFFFFFFF when absent)
 enum : int { SPECIAL_DEFAULT = 0, SPECIAL_LOCALHOST = 4, MISC_FAN_NODES = 12, MISC_VNI_N = 13,
-             MISC_COMMIT_N = 14, MISC_COLMAX = 16 /* [19] */ };   // misc words (64 = 256 B)
+             MISC_COMMIT_N = 14, MISC_ROWCHG_N = 15, MISC_COLMAX = 16 /* [19] */ };   // misc words (64 = 256 B)
 // epoch sync header (u32 words; zeroed by the epoch's only memset, the look-back status
 // follows at SYNC_HEADER_BYTES). The ticket counter, which every k_reconcile workgroup
 // increments, has a 128-B line to itself; the host reads words [SYNC_TOTALS, SYNC_TOTALS + 4)
@@ -298,8 +298,12 @@ __global__ void k_commit_plan(DevTopos T, const uint8_t* action, const uint32_t*
 __global__ void k_delta_map(const uint32_t* topo, uint32_t n, uint32_t* chg);
 __global__ void k_delta_plan(DevTopos T, const uint32_t* chg, const uint32_t* d_off, const uint32_t* d_src,
                              const uint32_t* d_netns, const uint8_t* d_nil, uint32_t* len, uint32_t* base,
-                             uint8_t* mode, uint32_t* src_ip, uint32_t* net_ns, uint8_t* flags);
+                             uint8_t* mode, uint32_t* src_ip, uint32_t* net_ns, uint8_t* flags,
+                             uint32_t* row_list, uint32_t* row_n);
 __global__ void k_off_narrow(const uint64_t* in, uint32_t n, uint32_t* out);
+__global__ void k_pods_pack(DevTopos T, const uint32_t* topo, uint32_t n, uint32_t cap, uint32_t rank_base,
+                            uint4* out);
+__global__ void k_pods_patch(const uint4* ent, uint32_t n, uint4* pods, uint4* slots, uint32_t stamp, uint32_t nd);
 __global__ void k_soa_to_tiles(const uint32_t* stage, const int64_t* uid, uint32_t n, uint32_t* out, uint32_t* colmax);
 __global__ void k_store_assemble(const uint32_t* off, uint32_t nt, const uint32_t* base, const uint8_t* mode,
                                  const uint32_t* ref, DevLinks A, DevLinks B, uint32_t n, uint32_t* out);

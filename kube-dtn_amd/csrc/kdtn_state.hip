@@ -57,7 +57,7 @@ __global__ void __launch_bounds__(BLOCK) k_delta_plan(DevTopos T, const uint32_t
                                                       const uint32_t* d_src, const uint32_t* d_netns,
                                                       const uint8_t* d_nil, uint32_t* len, uint32_t* base,
                                                       uint8_t* mode, uint32_t* src_ip, uint32_t* net_ns,
-                                                      uint8_t* flags) {
+                                                      uint8_t* flags, uint32_t* row_list, uint32_t* row_n) {
     const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
     if (t >= T.n) return;
     const uint32_t c = chg[t];
@@ -70,9 +70,13 @@ __global__ void __launch_bounds__(BLOCK) k_delta_plan(DevTopos T, const uint32_t
     len[t] = d_off[c + 1] - d_off[c];
     base[t] = d_off[c];
     mode[t] = ASM_REF;
+    const uint8_t fl = flags[t];
+    const uint8_t nfl = (uint8_t)((fl & ~KDTN_TOPO_SPEC_NIL) | (d_nil[c] ? KDTN_TOPO_SPEC_NIL : 0));
+    if (src_ip[t] != d_src[c] || net_ns[t] != d_netns[c] || fl != nfl)
+        row_list[atomicAdd(row_n, 1u)] = t;            // a changed pod-status row (any order)
     src_ip[t] = d_src[c];
     net_ns[t] = d_netns[c];
-    flags[t] = (uint8_t)((flags[t] & ~KDTN_TOPO_SPEC_NIL) | (d_nil[c] ? KDTN_TOPO_SPEC_NIL : 0));
+    flags[t] = nfl;
 }
 
 __global__ void __launch_bounds__(BLOCK) k_delta_map(const uint32_t* topo, uint32_t n, uint32_t* chg) {
@@ -157,6 +161,42 @@ __global__ void __launch_bounds__(BLOCK) k_soa_to_tiles(const uint32_t* stage, c
         for (int w = 0; w < BLOCK / 64; ++w) v = red[w][threadIdx.x] > v ? red[w][threadIdx.x] : v;
         atomicMax(colmax + threadIdx.x, v);
     }
+}
+
+// Pod-status rows of the Topologies a delta changed (status.src_ip / net_ns / spec nil), as
+// {pod index, 0, 0, 0}, row entries; entries past n are padding (pod index ~0). Exchanged
+// between ranks instead of the whole table when the tables of the previous rows are resident.
+__global__ void __launch_bounds__(BLOCK) k_pods_pack(DevTopos T, const uint32_t* topo, uint32_t n, uint32_t cap,
+                                                     uint32_t rank_base, uint4* out) {
+    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+    if (k >= cap) return;
+    if (k >= n) {
+        out[2 * k] = make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
+        return;
+    }
+    const uint32_t t = topo[k];
+    out[2 * k] = make_uint4(rank_base + t, 0u, 0u, 0u);
+    out[2 * k + 1] = make_uint4(T.ns[t], T.name[t], T.src_ip[t],
+                                T.net_ns[t] | ((T.flags[t] & KDTN_TOPO_SPEC_NIL) ? 0x80000000u : 0u));
+}
+
+// Apply changed rows to the resident pod table and to their pods' direct lookup slots (the
+// slot of the pod's name when this pod owns it in the current build; a name shared by several
+// pods is answered from the overflow table, which reads the row itself). The name, its
+// namespace and the PHYSICAL bit of the name string do not change.
+__global__ void __launch_bounds__(BLOCK) k_pods_patch(const uint4* ent, uint32_t n, uint4* pods, uint4* slots,
+                                                      uint32_t stamp, uint32_t nd) {
+    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+    if (k >= n) return;
+    const uint32_t g = ent[2 * k].x;
+    if (g == 0xFFFFFFFFu) return;
+    const uint4 row = ent[2 * k + 1];
+    pods[g] = row;
+    if (row.y >= nd) return;
+    const uint4 w = slots[row.y];
+    if ((w.w >> 1) != stamp || (w.w & 1u) || (w.y >> 2) != g) return;
+    slots[row.y] = make_uint4(w.x, (g << 2) | (w.y & 2u) | (row.w >> 31),
+                              row.z | ((row.w & 0x7FFFFFFFu) == 0 ? 0x80000000u : 0u), w.w);
 }
 
 }  // namespace kdtn

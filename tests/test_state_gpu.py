@@ -55,7 +55,19 @@ def test_commit_and_delta_random_epochs():
             eng.upload_delta(d)
             want = apply_delta(state, d)
             assert not same_tables(eng.tables(), want), seed
+            eng.run()
+            eng.sync()
+            kt = eng.kernel_times()          # the pod tables were patched by the delta: no rebuild
+            assert "full_prefix" in kt and "verify_prefix" not in kt, kt
             _run_same(eng, want, f"seed {seed} epoch 1")
+            # a further delta on the patched tables (rows moving again)
+            c = mutate(b_topos := mutate(topos, seed + 7), seed + 11)
+            st2 = commit(want, predicted_commit(want, O.reconcile(want, tick=TICK)))
+            eng.commit()
+            c_in = pack(c, vnis, kdict=kd, pdict=pd)
+            d2 = build_delta(b, c_in, b.kdict.n, b.pdict.n, vnis=c_in.vnis)
+            eng.upload_delta(d2)
+            _run_same(eng, apply_delta(st2, d2), f"seed {seed} epoch 2")
 
 
 @pytest.mark.parametrize("pods", [20000])
