@@ -45,8 +45,10 @@ __global__ void __launch_bounds__(BLOCK) k_reach_cuts(ReachIn f, uint32_t nd, ui
 __global__ void __launch_bounds__(BLOCK) k_reach(ReachIn f, uint32_t na, uint32_t nu, const uint32_t* cut,
                                                  uint32_t* mark, uint8_t* reach_add, uint8_t* reach_upd) {
     const uint32_t x = blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t ta = entry_topo_wave(f.add_off, f.T, x, x < na);
+    const uint32_t tu = entry_topo_wave(f.upd_off, f.T, x - na, x >= na && x < na + nu);
     if (x < na) {
-        const uint32_t t = entry_topo(f.add_off, f.T, x);
+        const uint32_t t = ta;
         uint8_t a = 0;
         if (cut[3 * t] == 0xFFFFFFFFu && x <= cut[3 * t + 1]) {
             a = REACH_ON;
@@ -60,7 +62,7 @@ __global__ void __launch_bounds__(BLOCK) k_reach(ReachIn f, uint32_t na, uint32_
         reach_add[x] = a;
     } else if (x < na + nu) {
         const uint32_t e = x - na;
-        const uint32_t t = entry_topo(f.upd_off, f.T, e);
+        const uint32_t t = tu;
         reach_upd[e] = (cut[3 * t] == 0xFFFFFFFFu && cut[3 * t + 1] == 0xFFFFFFFFu && e <= cut[3 * t + 2]) ? REACH_ON : 0;
     }
 }

@@ -248,7 +248,8 @@ __global__ void k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, Re
 
 // ---- wire encoding of the batches (kdtn_wire.hip) --------------------------------------
 constexpr int SCAN_CHUNK = BLOCK * 4;   // values per block of the batch-offset scan
-constexpr int WIRE_IMG = 12288;         // LDS bytes per wave for a wave's wire output
+constexpr int WIRE_IMG = 8192;          // LDS bytes per wave for a wave's wire output (32 KB per
+                                        // block: 5 blocks per CU; a longer wave range stores directly)
 // string table of a dictionary for the encoders: {arena offset, length | STR_BAD} per string,
 // STR_BAD = not valid UTF-8 — one 8-B gather gives everything a string field needs
 constexpr uint32_t STR_BAD = 0x80000000u;
@@ -375,6 +376,28 @@ KD_INLINE uint32_t qdisc_err(const uint2* q, uint32_t e) { return (q[(size_t)e *
 // topology of entry e: offs[t] <= e < offs[t + 1] (upper bound over the T + 1 offsets)
 KD_INLINE uint32_t entry_topo(const uint32_t* offs, uint32_t T, uint32_t e) {
     uint32_t lo = 0, hi = T;                           // offs[lo] <= e < offs[hi]
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (offs[mid] <= e) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// entry_topo for every lane of a wave at once (all lanes must call it; on = the lane has an
+// entry): the search range is narrowed to the topologies of the wave's smallest and largest
+// entry, found by two wave-uniform searches (one address per step), so each lane's own search
+// spans a few topologies instead of all T — a wave's entries are usually neighbours.
+KD_INLINE uint32_t entry_topo_wave(const uint32_t* offs, uint32_t T, uint32_t e, bool on) {
+    uint32_t lo_e = on ? e : 0xFFFFFFFFu, hi_e = on ? e : 0u;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint32_t a = __shfl_xor(lo_e, d, 64), b = __shfl_xor(hi_e, d, 64);
+        lo_e = a < lo_e ? a : lo_e;
+        hi_e = b > hi_e ? b : hi_e;
+    }
+    if (lo_e > hi_e) return 0;                         // no lane has an entry (wave-uniform)
+    uint32_t lo = entry_topo(offs, T, lo_e), hi = entry_topo(offs, T, hi_e) + 1;   // offs[lo] <= e < offs[hi]
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
         if (offs[mid] <= e) lo = mid;

@@ -44,8 +44,10 @@ __global__ void __launch_bounds__(BLOCK) k_vni_cuts(VniOpsIn f, uint32_t* cut) {
 __global__ void __launch_bounds__(BLOCK) k_vni_ops(VniOpsIn f, const uint32_t* cut, uint4* ops) {
     const uint32_t x = blockIdx.x * BLOCK + threadIdx.x;
     const uint4 none = make_uint4(0u, 0u, 0u, VOP_NONE);
+    const uint32_t td = entry_topo_wave(f.r.del_off, f.r.T, x, x < f.n_del);
+    const uint32_t ta = entry_topo_wave(f.r.add_off, f.r.T, x - f.n_del, x >= f.n_del && x < f.n_del + f.n_add);
     if (x < f.n_del) {
-        const uint32_t t = entry_topo(f.r.del_off, f.r.T, x);
+        const uint32_t t = td;
         const uint4 r = f.r.del_res[x];
         uint4 op = none;
         if (x < cut[2 * t] && ((r.w >> 16) & 0xFFu))                       // vni_hit :484-487
@@ -53,7 +55,7 @@ __global__ void __launch_bounds__(BLOCK) k_vni_ops(VniOpsIn f, const uint32_t* c
         ops[x] = op;
     } else if (x < f.n_del + f.n_add) {
         const uint32_t e = x - f.n_del;
-        const uint32_t t = entry_topo(f.r.add_off, f.r.T, e);
+        const uint32_t t = ta;
         uint4 lo = none, rm = none;
         if (cut[2 * t] == 0xFFFFFFFFu && e < cut[2 * t + 1]) {
             const uint4 r = f.r.add_res[e];

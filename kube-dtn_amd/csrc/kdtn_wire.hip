@@ -294,6 +294,7 @@ KD_INLINE void write_entry(Sink& o, const WireIn& w, const DevLinks& L, uint32_t
     o.byte(7u << 3 | 2u);
     o.varint(psz);
     // pb.LinkProperties: latency 1 .. rate 6, gap 7, duplicate 8 .. corrupt_corr 13 (KDTN_P_* order)
+#pragma unroll
     for (int k = 0; k < KDTN_NPROP; ++k) {
         if (k == KDTN_P_DUPLICATE && r.gap) {
             o.byte(7u << 3);
@@ -408,11 +409,16 @@ struct RemoteMsg {
     bool ok;                        // every string valid UTF-8
 };
 
-KD_INLINE RemoteMsg remote_msg(const RemoteIn& r, uint32_t m) {
+// every lane of the wave calls it (the topology search is wave-cooperative); on = m < n_msgs
+KD_INLINE RemoteMsg remote_msg(const RemoteIn& r, uint32_t m, bool on) {
     RemoteMsg q;
     const bool remote = m < r.n_remote;
-    const uint32_t e = remote ? r.rem_idx[m] : r.phys_idx[m - r.n_remote];
-    const uint32_t t = entry_topo(r.add_off, r.T, e);
+    const uint32_t e = on ? (remote ? r.rem_idx[m] : r.phys_idx[m - r.n_remote]) : 0u;
+    const uint32_t t = entry_topo_wave(r.add_off, r.T, e, on);
+    if (!on) {
+        q.ok = false;
+        return q;
+    }
     const uint32_t j = r.add_idx[e];
     const uint4 res = r.add_res[e];
     const uint32_t peer_pod = r.N.key(KDTN_K_PEER_POD, j);
@@ -465,8 +471,8 @@ KD_INLINE uint32_t remote_body_size(const RemoteMsg& q, uint32_t* psz) {
 
 __global__ void __launch_bounds__(BLOCK) k_remote_sizes(RemoteIn r, uint32_t* size) {
     const uint32_t m = blockIdx.x * BLOCK + threadIdx.x;
+    const RemoteMsg q = remote_msg(r, m, m < r.n_msgs);
     if (m >= r.n_msgs) return;
-    const RemoteMsg q = remote_msg(r, m);
     uint32_t psz;
     const uint32_t body = remote_body_size(q, &psz);
     size[m] = q.ok ? vlen(body) + body : 0u;
@@ -483,6 +489,7 @@ KD_INLINE void write_remote(Sink& o, const RemoteIn& r, const RemoteMsg& q) {
     }
     o.byte(7u << 3 | 2u);
     o.varint(psz);
+#pragma unroll
     for (int k = 0; k < KDTN_NPROP; ++k) {
         if (k == KDTN_P_DUPLICATE && q.gap) {
             o.byte(7u << 3);
@@ -514,8 +521,7 @@ __global__ void __launch_bounds__(BLOCK) k_remote_write(RemoteIn r, const uint64
         r1 = b > r1 ? b : r1;
     }
     if (r1 <= r0) return;                           // no active lane (wave-uniform)
-    RemoteMsg q{};
-    if (on) q = remote_msg(r, m);
+    const RemoteMsg q = remote_msg(r, m, on);
     const uint32_t lead = (uint32_t)(r0 & 3u);
     if (r1 - r0 + lead > (uint64_t)WIRE_IMG) {      // too large for the image: direct byte stores
         if (on) {
