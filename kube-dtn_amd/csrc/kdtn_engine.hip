@@ -116,12 +116,12 @@ struct kdtn_ctx {
     uint64_t w_bytes = 0;
     bool encoded = false;
     // RemotePod fan-out
-    DevBuf f_mark, f_send, f_node_idx, f_nodes, f_counts, f_base, f_part, f_idx, f_reach_upd, f_cut;
+    DevBuf f_mark, f_send, f_node_idx, f_nodes, f_counts, f_base, f_part, f_idx, f_inv, f_reach_upd, f_cut;
     uint32_t f_stamp = 0;
     bool fan_valid = false;                    // the fan-out of the last run is in f_* (fanout_compute)
     uint32_t fan_nn = 0, fan_nsend = 0;
     // RemotePod messages (kdtn_epoch_remote_encode)
-    DevBuf rp_flag, rp_pos, rp_phys, rp_msz, rp_moff, rp_tsz, rp_toff, rp_part, rp_arena, rp_tc;
+    DevBuf rp_flag, rp_pos, rp_phys, rp_msz, rp_moff, rp_tsz, rp_toff, rp_part, rp_arena, rp_tc, rp_msz_e, rp_tsz_e;
     uint32_t rp_n = 0, rp_nr = 0;
     uint64_t rp_bytes = 0, rp_tc_bytes = 0;
     bool rp_done = false;
@@ -750,7 +750,7 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->add_qdisc, &c->upd_qdisc, &c->kd_utf8, &c->pd_utf8, &c->w_rel,
                       &c->w_topo, &c->w_size, &c->w_err, &c->w_off, &c->w_part, &c->w_arena,
                       &c->f_mark, &c->f_send, &c->f_node_idx, &c->f_nodes, &c->f_counts, &c->f_base,
-                      &c->f_part, &c->f_idx, &c->f_reach_upd, &c->tc_size, &c->tc_off, &c->tc_part, &c->tc_arena,
+                      &c->f_part, &c->f_idx, &c->f_inv, &c->f_reach_upd, &c->tc_size, &c->tc_off, &c->tc_part, &c->tc_arena,
                       &c->j_doc, &c->j_q, &c->j_bs, &c->j_hb, &c->j_qcnt, &c->j_qoff, &c->j_tok, &c->j_open,
                       &c->j_close, &c->j_tcnt, &c->j_dcnt, &c->j_toff, &c->j_doff, &c->j_toks, &c->j_par,
                       &c->j_role, &c->j_ecls, &c->j_odep, &c->j_ord, &c->j_tagg, &c->j_gagg, &c->j_cnt3, &c->j_coff3, &c->j_small,
@@ -763,7 +763,7 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->sh_des.buf, &c->sh_real.buf, &c->vx_ops, &c->vx_dead, &c->vx_slots, &c->vx_node,
                       &c->vx_vni, &c->vx_netns, &c->vx_part, &c->vx_cut, &c->f_cut, &c->vx_vis,
                       &c->r_node, &c->r_vni, &c->r_netns, &c->rp_flag, &c->rp_pos, &c->rp_phys,
-                      &c->rp_msz, &c->rp_moff, &c->rp_tsz, &c->rp_toff, &c->rp_part, &c->rp_arena, &c->rp_tc,
+                      &c->rp_msz, &c->rp_moff, &c->rp_tsz, &c->rp_toff, &c->rp_part, &c->rp_arena, &c->rp_tc, &c->rp_msz_e, &c->rp_tsz_e,
                       &c->st_len, &c->st_base, &c->st_mode, &c->st_flags, &c->st_off64, &c->st_part,
                       &c->st_off32, &c->st_mask, &c->st_chg, &c->dl_topo, &c->dl_src, &c->dl_netns, &c->dl_nil,
                       &c->dl_off, &c->dl_ref, &c->dl_rec.buf, &c->stage, &c->vx_cnt, &c->vx_send, &c->vx_recv,
@@ -1249,19 +1249,19 @@ int kdtn_epoch_encode(kdtn_ctx* c, uint64_t* n_bytes) {
     const uint32_t T = c->T;
     const uint64_t ne = (uint64_t)nd + na + nu;
     if (ne > 0xFFFFFFFFull || 3ull * T + 1 > 0xFFFFFFFFull) return KDTN_EINVAL;
-    TRY(str_tables(c));
-    TRY(ensure(c->w_rel, (size_t)ne * 4));
-    TRY(ensure(c->w_topo, (size_t)ne * 4));
-    TRY(ensure(c->w_size, (size_t)3 * T * 4));
-    TRY(ensure(c->w_err, align_up((size_t)T * 4, 16)));
+    TRY(ensure(c->w_rel, (size_t)ne * 4 + 16));                 // entry sizes
+    TRY(ensure(c->w_topo, (size_t)ne * 4 + 16));
+    TRY(ensure(c->w_size, ((size_t)ne + 1) * 8));                // entry offsets (u64)
+    const size_t err_bytes = align_up(((size_t)T + 1) * 4, 16);  // err[T]: a batch over 4 GiB
+    TRY(ensure(c->w_err, err_bytes));
     TRY(ensure(c->w_off, ((size_t)3 * T + 1) * 8));
-    const uint32_t nb = nblocks((uint64_t)3 * T + 1, SCAN_CHUNK);
-    TRY(ensure(c->w_part, (size_t)nb * 8));
+    const uint32_t nb = nblocks(ne + 1, SCAN_CHUNK);
+    TRY(ensure(c->w_part, (size_t)nb * 8 + 16));
     c->n_ev = 0;
     (void)hipEventRecord(c->ev[0], s);
-
+    TRY(str_tables(c));
     timer_mark(c, "wire_strtab");
-    HIP_TRY(hipMemsetAsync(c->w_err.p, 0, align_up((size_t)T * 4, 16), s));
+    HIP_TRY(hipMemsetAsync(c->w_err.p, 0, err_bytes, s));
     WireIn w{};
     w.kd_bytes = dp<uint8_t>(c->kd_bytes);
     w.kd_tab = dp<uint2>(c->kd_utf8);
@@ -1282,20 +1282,25 @@ int kdtn_epoch_encode(kdtn_ctx* c, uint64_t* n_bytes) {
     w.list_base[2] = nd + na;
     w.n_entries = (uint32_t)ne;
     w.T = T;
-    WireWork wk{dp<uint32_t>(c->w_rel), dp<uint32_t>(c->w_topo), dp<uint32_t>(c->w_size), dp<uint32_t>(c->w_err),
+    WireWork wk{dp<uint32_t>(c->w_rel), dp<uint32_t>(c->w_topo), dp<uint64_t>(c->w_size), dp<uint32_t>(c->w_err),
                 dp<uint64_t>(c->w_off)};
     if (ne) k_wire_entry_sizes<<<nblocks(ne), BLOCK, 0, s>>>(w, c->real.view, c->des.view, wk);
-    if (T) k_wire_sizes<<<nblocks((uint64_t)3 * T), BLOCK, 0, s>>>(w, c->real.view, c->des.view, wk);
     timer_mark(c, "wire_sizes");
-    const uint32_t n = 3 * T;
-    k_scan_partial<<<nb, BLOCK, 0, s>>>(dp<uint32_t>(c->w_size), n, dp<uint64_t>(c->w_part));
+    k_wire_scan_partial<<<nb, BLOCK, 0, s>>>(w, wk, dp<uint64_t>(c->w_part));
     k_scan_top<<<1, BLOCK, 0, s>>>(dp<uint64_t>(c->w_part), nb);
-    k_scan_final<<<nb, BLOCK, 0, s>>>(dp<uint32_t>(c->w_size), n, dp<uint64_t>(c->w_part), dp<uint64_t>(c->w_off));
+    k_wire_scan_final<<<nb, BLOCK, 0, s>>>(w, wk, dp<uint64_t>(c->w_part));
+    k_wire_batch_off<<<nblocks((uint64_t)3 * T + 1), BLOCK, 0, s>>>(w, wk);
     timer_mark(c, "wire_scan");
     HIP_TRY(hipGetLastError());
     uint64_t total = 0;
-    HIP_TRY(hipMemcpyAsync(&total, dp<uint64_t>(c->w_off) + n, 8, hipMemcpyDeviceToHost, s));
+    uint32_t big = 0;
+    HIP_TRY(hipMemcpyAsync(&total, dp<uint64_t>(c->w_size) + ne, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(&big, dp<uint32_t>(c->w_err) + T, 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    if (big) {
+        std::snprintf(g_last_error, sizeof(g_last_error), "a LinksBatchQuery of more than 4 GiB");
+        return KDTN_EINVAL;
+    }
     TRY(ensure(c->w_arena, (size_t)total + 16));
     timer_mark(c, "wire_host_sync");                // the arena size crosses to the host
     if (ne) k_wire_write<<<nblocks(ne), BLOCK, 0, s>>>(w, c->real.view, c->des.view, wk, dp<uint8_t>(c->w_arena));
@@ -1348,6 +1353,7 @@ int fanout_compute(kdtn_ctx* c) {
     TRY(ensure(c->f_nodes, (size_t)FAN_NODE_CAP * 4 + 16));
     TRY(ensure(c->f_part, (size_t)nbd * 8 + 16));
     TRY(ensure(c->f_idx, (size_t)na * 4 + 16));
+    TRY(ensure(c->f_inv, (size_t)na * 4 + 16));
     uint32_t* misc = dp<uint32_t>(c->misc);
     uint32_t* n_nodes = misc + MISC_FAN_NODES;
     FanIn f{dp<uint32_t>(c->add_off), dp<uint4>(c->add_res), dp<uint2>(c->add_qdisc), c->T, na, c->f_stamp};
@@ -1380,7 +1386,8 @@ int fanout_compute(kdtn_ctx* c) {
         k_scan_final<<<nbc, BLOCK, 0, s>>>(dp<uint32_t>(c->f_counts), ncells, dp<uint64_t>(c->w_part),
                                            dp<uint64_t>(c->f_base));
         k_fan_scatter<<<nchunks, 64, lds, s>>>(f, dp<uint8_t>(c->f_send), dp<uint32_t>(c->f_node_idx), n_nodes,
-                                             dp<uint64_t>(c->f_base), nchunks, dp<uint32_t>(c->f_idx));
+                                             dp<uint64_t>(c->f_base), nchunks, dp<uint32_t>(c->f_idx),
+                                             dp<uint32_t>(c->f_inv));
         HIP_TRY(hipGetLastError());
         uint64_t tot = 0;
         HIP_TRY(hipMemcpyAsync(&tot, dp<uint64_t>(c->f_base) + ncells, 8, hipMemcpyDeviceToHost, s));
@@ -1478,20 +1485,29 @@ int kdtn_epoch_remote_encode(kdtn_ctx* c, kdtn_remote_info* info) {
     r.pods = dp<uint4>(c->pods);
     r.rem_idx = dp<uint32_t>(c->f_idx);
     r.phys_idx = dp<uint32_t>(c->rp_phys);
+    r.send = dp<uint8_t>(c->f_send);
+    r.phys_flag = dp<uint32_t>(c->rp_flag);
+    r.phys_pos = dp<uint64_t>(c->rp_pos);
+    r.rem_inv = dp<uint32_t>(c->f_inv);
     r.N = c->des.view;
     r.n_msgs = (uint32_t)n;
     r.n_remote = nr;
     r.T = c->T;
+    r.n_add = na;
     const uint32_t nbm = nblocks(n + 1, SCAN_CHUNK);
     TRY(ensure(c->rp_msz, (size_t)n * 4 + 16));
     TRY(ensure(c->rp_tsz, (size_t)n * 4 + 16));
+    TRY(ensure(c->rp_msz_e, (size_t)na * 4 + 16));
+    TRY(ensure(c->rp_tsz_e, (size_t)na * 4 + 16));
     TRY(ensure(c->rp_moff, (n + 1) * 8));
     TRY(ensure(c->rp_toff, (n + 1) * 8));
     TRY(ensure(c->rp_part, (size_t)nbm * 8 + 16));
     TRY(ensure(c->w_part, (size_t)nbm * 8 + 16));
-    if (n) {
-        k_remote_sizes<<<nblocks(n), BLOCK, 0, s>>>(r, dp<uint32_t>(c->rp_msz));
-        k_tc_remote_sizes<<<nblocks(n), BLOCK, 0, s>>>(r, dp<uint32_t>(c->rp_tsz));
+    if (n) {   // sizes per add entry (coalesced columns), then gathered into message order
+        k_remote_entry_sizes<<<nblocks(na), BLOCK, 0, s>>>(r, dp<uint32_t>(c->rp_msz_e));
+        if (nr) k_tc_remote_entry_sizes<<<nblocks(na), BLOCK, 0, s>>>(r, dp<uint32_t>(c->rp_tsz_e));
+        k_remote_msg_sizes<<<nblocks(n), BLOCK, 0, s>>>(r, dp<uint32_t>(c->rp_msz_e), dp<uint32_t>(c->rp_tsz_e),
+                                                        dp<uint32_t>(c->rp_msz), dp<uint32_t>(c->rp_tsz));
     }
     k_scan_partial<<<nbm, BLOCK, 0, s>>>(dp<uint32_t>(c->rp_msz), (uint32_t)n, dp<uint64_t>(c->rp_part));
     k_scan_top<<<1, BLOCK, 0, s>>>(dp<uint64_t>(c->rp_part), nbm);
@@ -1511,9 +1527,9 @@ int kdtn_epoch_remote_encode(kdtn_ctx* c, kdtn_remote_info* info) {
     TRY(ensure(c->rp_tc, (size_t)tot[1] + 16));
     timer_mark(c, "remote_host_sync");
     if (n) {
-        k_remote_write<<<nblocks(n), BLOCK, 0, s>>>(r, dp<uint64_t>(c->rp_moff), dp<uint8_t>(c->rp_arena));
+        k_remote_write<<<nblocks(na), BLOCK, 0, s>>>(r, dp<uint64_t>(c->rp_moff), dp<uint8_t>(c->rp_arena));
         timer_mark(c, "remote_write");
-        k_tc_remote_write<<<nblocks(n), BLOCK, 0, s>>>(r, dp<uint64_t>(c->rp_toff), dp<uint8_t>(c->rp_tc));
+        if (nr) k_tc_remote_write<<<nblocks(na), BLOCK, 0, s>>>(r, dp<uint64_t>(c->rp_toff), dp<uint8_t>(c->rp_tc));
         timer_mark(c, "remote_tc_write");
     }
     HIP_TRY(hipGetLastError());

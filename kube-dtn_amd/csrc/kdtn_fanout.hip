@@ -56,7 +56,9 @@ __global__ void __launch_bounds__(BLOCK) k_reach(ReachIn f, uint32_t na, uint32_
             const uint32_t qe = qdisc_err(f.add_qdisc, x);
             if (!add_fails(r, qe) && sends_remote(r, qe)) {
                 a |= REACH_SEND;
-                if (mark) mark[r.z] = f.stamp;
+                // a few dozen daemons take millions of stamps: store only a missing one (a
+                // stale read stores again, harmlessly), so the words are not written per entry
+                if (mark && mark[r.z] != f.stamp) mark[r.z] = f.stamp;
             }
         }
         reach_add[x] = a;
@@ -125,7 +127,7 @@ __global__ void __launch_bounds__(64) k_fan_count(FanIn f, const uint8_t* send, 
 // a running per-node counter in LDS carries the order across rounds.
 __global__ void __launch_bounds__(64) k_fan_scatter(FanIn f, const uint8_t* send, const uint32_t* node_idx,
                                                     const uint32_t* n_nodes, const uint64_t* base, uint32_t nchunks,
-                                                    uint32_t* out_idx) {
+                                                    uint32_t* out_idx, uint32_t* out_inv) {
     extern __shared__ uint32_t run[];                        // [n_nodes]
     const uint32_t nn = *n_nodes;
     if (nn > FAN_NODE_CAP) return;
@@ -156,7 +158,10 @@ __global__ void __launch_bounds__(64) k_fan_scatter(FanIn f, const uint8_t* send
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        if (on) out_idx[b0 + rank] = e;
+        if (on) {
+            out_idx[b0 + rank] = e;
+            out_inv[e] = b0 + rank;                          // the entry's message index
+        }
     }
 }
 

@@ -268,11 +268,14 @@ struct WireIn {
     uint32_t n_entries, T;
 };
 struct WireWork {
-    uint32_t* rel;                  // [entries] offset of the entry inside its batch
+    uint32_t* size;                 // [entries] encoded bytes of the entry (its Link field, plus the
+                                    // LocalPod header for the batch's first entry)
     uint32_t* topo;                 // [entries] topology of the entry
-    uint32_t* size;                 // [3T] batch sizes (0: empty list or Marshal error)
-    uint32_t* err;                  // [T] bit l: list l failed to marshal
-    const uint64_t* off;            // [3T+1] batch byte offsets
+    uint64_t* pos;                  // [entries+1] arena offset of every entry (scan of the sizes of
+                                    // entries whose batch marshals), pos[entries] = total
+    uint32_t* err;                  // [T+1] bit l of err[t]: list l of topology t failed to marshal;
+                                    // err[T] != 0: a batch of more than 4 GiB
+    uint64_t* off;                  // [3T+1] batch byte offsets
 };
 // ---- tc argv synthesis (kdtn_tc.hip) ---------------------------------------------------
 struct TcIn {
@@ -328,14 +331,19 @@ struct RemoteIn {
     const uint4* pods;              // global pod-status rows (the peer's status.net_ns)
     const uint32_t* rem_idx;
     const uint32_t* phys_idx;
+    const uint8_t* send;            // k_reach flags per add entry (REACH_SEND: an UpdateRemote)
+    const uint32_t* phys_flag;      // per add entry: a physical peer's local Update
+    const uint64_t* phys_pos;       // exclusive scan of phys_flag
+    const uint32_t* rem_inv;        // per add entry with REACH_SEND: its message index
     DevLinks N;
-    uint32_t n_msgs, n_remote, T;
+    uint32_t n_msgs, n_remote, T, n_add;
 };
 __global__ void k_remote_phys_flags(const uint8_t* reach_add, const uint4* add_res, uint32_t na, uint32_t* flag);
 __global__ void k_remote_phys_scatter(const uint32_t* flag, const uint64_t* pos, uint32_t na, uint32_t* phys_idx);
-__global__ void k_remote_sizes(RemoteIn r, uint32_t* size);
+__global__ void k_remote_entry_sizes(RemoteIn r, uint32_t* msz_e);
+__global__ void k_remote_msg_sizes(RemoteIn r, const uint32_t* msz_e, const uint32_t* tsz_e, uint32_t* msz, uint32_t* tsz);
 __global__ void k_remote_write(RemoteIn r, const uint64_t* off, uint8_t* arena);
-__global__ void k_tc_remote_sizes(RemoteIn r, uint32_t* size);
+__global__ void k_tc_remote_entry_sizes(RemoteIn r, uint32_t* tsz_e);
 __global__ void k_tc_remote_write(RemoteIn r, const uint64_t* off, uint8_t* arena);
 
 // ---- RemotePod fan-out grouping (kdtn_fanout.hip) ---------------------------------------
@@ -407,6 +415,14 @@ KD_INLINE uint32_t entry_topo_wave(const uint32_t* offs, uint32_t T, uint32_t e,
 }
 
 enum : uint8_t { REACH_ON = 1, REACH_SEND = 2 };
+// message kind of add entry e: 1 = UpdateRemote, 2 = physical local Update, 0 = none
+KD_INLINE uint32_t remote_kind(const RemoteIn& r, uint32_t e) {
+    if (r.send[e] & REACH_SEND) return 1u;
+    return r.phys_flag[e] ? 2u : 0u;
+}
+KD_INLINE uint32_t remote_msg_index(const RemoteIn& r, uint32_t e, uint32_t kind) {
+    return kind == 1u ? r.rem_inv[e] : r.n_remote + (uint32_t)r.phys_pos[e];
+}
 struct ReachIn {
     const uint32_t* del_off;
     const uint4* del_res;
@@ -450,7 +466,7 @@ __global__ void k_fan_nodes_write(const uint32_t* mark, uint32_t nd, uint32_t st
 __global__ void k_fan_count(FanIn f, const uint8_t* send, const uint32_t* node_idx, const uint32_t* n_nodes,
                             uint32_t* counts, uint32_t nchunks);
 __global__ void k_fan_scatter(FanIn f, const uint8_t* send, const uint32_t* node_idx, const uint32_t* n_nodes,
-                              const uint64_t* base, uint32_t nchunks, uint32_t* out_idx);
+                              const uint64_t* base, uint32_t nchunks, uint32_t* out_idx, uint32_t* out_inv);
 KD_INLINE uint64_t block_exclusive(uint64_t v, uint64_t* sh, uint64_t* total) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint64_t x = v;
@@ -472,10 +488,149 @@ KD_INLINE uint64_t block_exclusive(uint64_t v, uint64_t* sh, uint64_t* total) {
     return base + x - v;
 }
 
+// ---- byte-stream writer of the encoders (wire, RemotePod, tc argv) ---------------------------
+// Bytes are appended 1-4 at a time into a 64-bit register and stored as whole dwords; only the
+// first and the last dword of a writer's range — shared with the neighbouring writers — take
+// byte stores. (One dword store per 4 output bytes instead of one byte store per byte.)
+struct WSink {
+    uint32_t* d;                 // the dword acc's byte 0 belongs to
+    uint32_t* d0;                // the writer's first dword
+    uint64_t acc;                // pending bytes, little-endian
+    uint32_t fill;               // bytes in acc, counting the `head` bytes of d0 that are not ours
+    uint32_t head;               // bytes [0, head) of d0 belong to the previous writer
+    uint32_t first;              // d0's bytes, stored by finish() when head != 0
+    bool hp;                     // d0 not flushed yet and shared (head != 0)
+    KD_INLINE void init(uint8_t* p) {
+        const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3u);
+        d = d0 = reinterpret_cast<uint32_t*>(p - mis);     // pointer arithmetic keeps the address space
+        head = fill = mis;
+        hp = mis != 0;
+        acc = 0;
+        first = 0;
+    }
+    // bytes [lo, hi) of v into dword q, one byte store each
+    KD_INLINE static void part(uint32_t* q, uint32_t v, uint32_t lo, uint32_t hi) {
+        uint8_t* b = reinterpret_cast<uint8_t*>(q);
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k)
+            if (k >= lo && k < hi) b[k] = (uint8_t)(v >> (8u * k));
+    }
+    // the low n (1..4) bytes of v
+    KD_INLINE void put(uint32_t v, uint32_t n) {
+        if (n < 4u) v &= (1u << (8u * n)) - 1u;
+        acc |= (uint64_t)v << (8u * fill);
+        fill += n;
+        if (fill >= 4u) {
+            if (hp) {
+                first = (uint32_t)acc;
+                hp = false;
+            } else {
+                *d = (uint32_t)acc;
+            }
+            ++d;
+            acc >>= 32;
+            fill -= 4u;
+        }
+    }
+    KD_INLINE void finish() {
+        if (head && !hp) part(d0, first, head, 4u);     // shared first dword, flushed
+        if (fill) part(d, (uint32_t)acc, hp ? head : 0u, fill);
+    }
+    KD_INLINE void byte(uint32_t v) { put(v, 1u); }
+    // protobuf base-128 varint: four 7-bit groups per put
+    KD_INLINE void varint(uint64_t v) {
+        while (v >= (1ull << 28)) {
+            const uint32_t x = (uint32_t)v;
+            put((x & 0x7Fu) | 0x80u | (((x >> 7) & 0x7Fu) | 0x80u) << 8 | (((x >> 14) & 0x7Fu) | 0x80u) << 16 |
+                    (((x >> 21) & 0x7Fu) | 0x80u) << 24, 4u);
+            v >>= 28;
+        }
+        const uint32_t x = (uint32_t)v;
+        uint32_t w = x & 0x7Fu, n = 1;
+        if (x >= 0x80u) { w |= 0x80u | ((x >> 7) & 0x7Fu) << 8; n = 2; }
+        if (x >= 0x4000u) { w |= 0x8000u | ((x >> 14) & 0x7Fu) << 16; n = 3; }
+        if (x >= 0x200000u) { w |= 0x800000u | ((x >> 21) & 0x7Fu) << 24; n = 4; }
+        put(w, n);
+    }
+    // bytes [b, b + len) of an arena with >= 40 B of readable slack past its end: the string's
+    // dwords come from one or two 16-B loads (+ one dword) issued together, the bytes past 32
+    // one at a time
+    KD_INLINE void str(const uint8_t* arena, uint32_t b, uint32_t len) {
+        if (!len) return;
+        typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+        const uint32_t* a32 = reinterpret_cast<const uint32_t*>(arena) + (b >> 2);
+        const uint32_t sh = b & 3u, nw = (sh + len + 3u) >> 2;
+        const u32x4a A = *reinterpret_cast<const u32x4a*>(a32);
+        u32x4a B = {0u, 0u, 0u, 0u};
+        if (nw > 4u) B = *reinterpret_cast<const u32x4a*>(a32 + 4);
+        const uint32_t c8 = nw > 8u ? a32[8] : 0u;
+        const uint32_t w[9] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w, c8};
+#pragma unroll
+        for (uint32_t q = 0; q < 8; ++q) {
+            if (4u * q < len) {
+                const uint32_t r = len - 4u * q;
+                put(__builtin_amdgcn_alignbyte(w[q + 1], w[q], sh), r < 4u ? r : 4u);
+            }
+        }
+        for (uint32_t k = 32; k < len; ++k) put(arena[b + k], 1u);
+    }
+};
+
+// One wave writes the bytes of its active lanes, which are consecutive ranges [s0, s1) of one
+// arena (in lane order, empty lanes between them): each lane's body(WSink&) writes into the
+// wave's LDS image (`img`, WIRE_IMG bytes), then the wave stores the image with coalesced
+// dword stores — byte stores only at the two dwords shared with the neighbouring waves. A
+// range larger than the image is written straight to global memory. Every lane of the wave
+// must call it.
+template <typename F>
+KD_INLINE void wave_image_write(uint32_t* img, bool on, uint64_t s0, uint64_t s1, uint8_t* arena, F&& body) {
+    const int lane = threadIdx.x & 63;
+    uint64_t r0 = on ? s0 : ~0ull, r1 = on ? s1 : 0ull;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint64_t a = __shfl_xor(r0, d, 64), b = __shfl_xor(r1, d, 64);
+        r0 = a < r0 ? a : r0;
+        r1 = b > r1 ? b : r1;
+    }
+    if (r1 <= r0) return;                                 // no active lane (wave-uniform)
+    const uint32_t lead = (uint32_t)(r0 & 3u);
+    WSink o;
+    if (r1 - r0 + lead > (uint64_t)WIRE_IMG) {            // too large: straight to global memory
+        if (on) {
+            o.init(arena + s0);
+            body(o);
+            o.finish();
+        }
+        return;
+    }
+    if (on) {
+        o.init(reinterpret_cast<uint8_t*>(img) + lead + (uint32_t)(s0 - r0));
+        body(o);
+        o.finish();
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint64_t a0 = r0 - lead;                        // dword-aligned global start
+    const uint32_t nw = (uint32_t)((r1 - a0 + 3) >> 2);
+    for (uint32_t q = lane; q < nw; q += 64) {
+        const uint64_t ga = a0 + 4ull * q;
+        const uint32_t v = img[q];
+        if (ga >= r0 && ga + 4 <= r1) {
+            *reinterpret_cast<uint32_t*>(arena + ga) = v;
+        } else {
+            for (uint32_t k = 0; k < 4; ++k)
+                if (ga + k >= r0 && ga + k < r1) arena[ga + k] = (uint8_t)(v >> (8 * k));
+        }
+    }
+}
+
 __global__ void k_utf8_bits(const uint8_t* bytes, const uint32_t* offs, uint32_t n, uint32_t* bits);
 __global__ void k_str_table(const uint8_t* bytes, const uint32_t* offs, uint32_t n, uint2* tab);
 __global__ void k_wire_entry_sizes(WireIn w, DevLinks O, DevLinks N, WireWork wk);
-__global__ void k_wire_sizes(WireIn w, DevLinks O, DevLinks N, WireWork wk);
+__global__ void k_wire_scan_partial(WireIn w, WireWork wk, uint64_t* part);
+__global__ void k_wire_scan_final(WireIn w, WireWork wk, const uint64_t* part);
+__global__ void k_wire_batch_off(WireIn w, WireWork wk);
 __global__ void k_scan_partial(const uint32_t* size, uint32_t n, uint64_t* part);
 __global__ void k_scan_top(uint64_t* part, uint32_t nb);
 __global__ void k_scan_final(const uint32_t* size, uint32_t n, const uint64_t* part, uint64_t* off);

@@ -68,52 +68,79 @@ __global__ void __launch_bounds__(BLOCK) k_tc_sizes(TcIn w, uint32_t* size) {
                    : 0u;
 }
 
-struct Out {
-    uint8_t* p;
-    KD_INLINE void lit(const char* s) {
-        while (*s) *p++ = (uint8_t)*s++;
-        *p++ = 0;
+// one argv element + its NUL separator: a literal, packed 4 bytes per put (constant-folded)
+template <int N>
+KD_INLINE void lit(WSink& o, const char (&s)[N]) {
+#pragma unroll
+    for (int k = 0; k < N; k += 4) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            if (k + c < N) w |= (uint32_t)(uint8_t)s[k + c] << (8 * c);
+        o.put(w, (uint32_t)(N - k < 4 ? N - k : 4));
     }
-    KD_INLINE void num(uint64_t v) {
-        const uint32_t n = ndigits(v);
-        for (uint32_t k = n; k-- > 0;) {
-            p[k] = (uint8_t)('0' + v % 10u);
-            v /= 10u;
-        }
-        p += n;
-        *p++ = 0;
-    }
-};
-
-KD_INLINE void write_tbf_argv(Out& o, const uint8_t* kd_bytes, const uint32_t* kd_offs, const TcEntry& t) {
-    o.lit("qdisc");
-    o.lit("add");
-    o.lit("dev");
-    const uint32_t b = kd_offs[t.intf], len = kd_offs[t.intf + 1] - b;
-    for (uint32_t k = 0; k < len; ++k) *o.p++ = kd_bytes[b + k];
-    *o.p++ = 0;
-    o.lit("parent");
-    o.lit("1:1");
-    o.lit("handle");
-    o.lit("10:0");
-    o.lit("tbf");
-    o.lit("rate");
-    o.num(t.rate);
-    o.lit("burst");
-    o.num(t.buffer);
-    o.lit("latency");
-    o.lit("50ms");
-    o.lit("minburst");
-    o.num(t.minburst);
+}
+// four ASCII digits of l < 10000, most significant first
+KD_INLINE uint32_t dig4(uint32_t l) {
+    return (0x30u + l / 1000u) | (0x30u + (l / 100u) % 10u) << 8 | (0x30u + (l / 10u) % 10u) << 16 |
+           (0x30u + l % 10u) << 24;
+}
+// fmt.Sprint of an unsigned integer + NUL: base-10000 limbs, the top one without leading zeros
+KD_INLINE void num(WSink& o, uint64_t v) {
+    const uint32_t l0 = (uint32_t)(v % 10000u);
+    v /= 10000u;
+    const uint32_t l1 = (uint32_t)(v % 10000u);
+    v /= 10000u;
+    const uint32_t l2 = (uint32_t)(v % 10000u);
+    v /= 10000u;
+    const uint32_t l3 = (uint32_t)(v % 10000u);
+    const uint32_t l4 = (uint32_t)(v / 10000u);          // < 1845 (2^64 < 10^20)
+    const int k = l4 ? 4 : l3 ? 3 : l2 ? 2 : l1 ? 1 : 0;
+    const uint32_t top = k == 4 ? l4 : k == 3 ? l3 : k == 2 ? l2 : k == 1 ? l1 : l0;
+    const uint32_t nd = ndigits(top);
+    o.put(dig4(top) >> (8u * (4u - nd)), nd);
+    if (k >= 4) o.put(dig4(l3), 4u);
+    if (k >= 3) o.put(dig4(l2), 4u);
+    if (k >= 2) o.put(dig4(l1), 4u);
+    if (k >= 1) o.put(dig4(l0), 4u);
+    o.byte(0u);
 }
 
+KD_INLINE void write_tbf_argv(WSink& o, const uint8_t* kd_bytes, const uint32_t* kd_offs, const TcEntry& t) {
+    lit(o, "qdisc");
+    lit(o, "add");
+    lit(o, "dev");
+    const uint32_t b = kd_offs[t.intf], len = kd_offs[t.intf + 1] - b;
+    o.str(kd_bytes, b, len);
+    o.byte(0u);
+    lit(o, "parent");
+    lit(o, "1:1");
+    lit(o, "handle");
+    lit(o, "10:0");
+    lit(o, "tbf");
+    lit(o, "rate");
+    num(o, t.rate);
+    lit(o, "burst");
+    num(o, t.buffer);
+    lit(o, "latency");
+    lit(o, "50ms");
+    lit(o, "minburst");
+    num(o, t.minburst);
+}
+
+// slot g's argv at [off[g], off[g+1]): a wave's slots are one contiguous range (wave_image_write)
 __global__ void __launch_bounds__(BLOCK) k_tc_write(TcIn w, const uint64_t* off, uint8_t* arena) {
+    __shared__ uint32_t img[BLOCK / 64][WIRE_IMG / 4];
     const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
-    if (g >= 2u * w.n_add + w.n_upd) return;
-    const TcEntry t = tc_entry(w, g);
-    if (!t.on) return;
-    Out o{arena + off[g]};
-    write_tbf_argv(o, w.kd_bytes, w.kd_offs, t);
+    TcEntry t{0, 0, 0, 0, false};
+    uint64_t s0 = 0, s1 = 0;
+    if (g < 2u * w.n_add + w.n_upd) {
+        t = tc_entry(w, g);
+        s0 = off[g];
+        s1 = off[g + 1];
+    }
+    wave_image_write(img[threadIdx.x >> 6], t.on, s0, s1, arena,
+                     [&](WSink& o) __attribute__((always_inline)) { write_tbf_argv(o, w.kd_bytes, w.kd_offs, t); });
 }
 
 // The receiving daemon's TBF command for RemotePod message m (m < n_remote): the peer
@@ -121,10 +148,9 @@ __global__ void __launch_bounds__(BLOCK) k_tc_write(TcIn w, const uint64_t* off,
 // built on the sending side) → SetVethQdiscs (daemon/vxlan/vxlan.go:31-51), unless its
 // CreateOrUpdate rejects IntfIp (kdtn_resolved.remote_err). Physical messages have none here
 // (their tc runs on LocalIntf: kdtn_epoch_tc slot 2e).
-KD_INLINE TcEntry tc_remote_entry(const RemoteIn& r, uint32_t m) {
+KD_INLINE TcEntry tc_remote_entry(const RemoteIn& r, uint32_t e) {
     TcEntry t{0, 0, 0, 0, false};
-    if (m >= r.n_remote) return t;
-    const uint32_t e = r.rem_idx[m];
+    if (!(r.send[e] & REACH_SEND)) return t;
     const uint2* q = r.add_qdisc + (size_t)e * 9;
     const uint32_t flags = q[8].y;
     if (((flags >> 8) & 0xFFu) == 0 || (r.add_res[e].w >> 24) != 0) return t;
@@ -136,22 +162,29 @@ KD_INLINE TcEntry tc_remote_entry(const RemoteIn& r, uint32_t m) {
     return t;
 }
 
-__global__ void __launch_bounds__(BLOCK) k_tc_remote_sizes(RemoteIn r, uint32_t* size) {
-    const uint32_t m = blockIdx.x * BLOCK + threadIdx.x;
-    if (m >= r.n_msgs) return;
-    const TcEntry t = tc_remote_entry(r, m);
-    size[m] = t.on ? TC_FIXED + (r.kd_offs[t.intf + 1] - r.kd_offs[t.intf]) + ndigits(t.rate) + ndigits(t.buffer) +
-                         ndigits(t.minburst)
-                   : 0u;
+// one thread per add entry (add-list order); the sizes are gathered into message order by
+// k_remote_msg_sizes
+__global__ void __launch_bounds__(BLOCK) k_tc_remote_entry_sizes(RemoteIn r, uint32_t* tsz_e) {
+    const uint32_t e = blockIdx.x * BLOCK + threadIdx.x;
+    if (e >= r.n_add || !(r.send[e] & REACH_SEND)) return;
+    const TcEntry t = tc_remote_entry(r, e);
+    tsz_e[e] = t.on ? TC_FIXED + (r.kd_offs[t.intf + 1] - r.kd_offs[t.intf]) + ndigits(t.rate) + ndigits(t.buffer) +
+                          ndigits(t.minburst)
+                    : 0u;
 }
 
+// one thread per add entry, writing its command at its message's position (add-list order)
 __global__ void __launch_bounds__(BLOCK) k_tc_remote_write(RemoteIn r, const uint64_t* off, uint8_t* arena) {
-    const uint32_t m = blockIdx.x * BLOCK + threadIdx.x;
-    if (m >= r.n_msgs) return;
-    const TcEntry t = tc_remote_entry(r, m);
+    const uint32_t e = blockIdx.x * BLOCK + threadIdx.x;
+    if (e >= r.n_add) return;
+    const TcEntry t = tc_remote_entry(r, e);
     if (!t.on) return;
-    Out o{arena + off[m]};
+    const uint32_t m = r.rem_inv[e];
+    if (off[m + 1] <= off[m]) return;
+    WSink o;
+    o.init(arena + off[m]);
     write_tbf_argv(o, r.kd_bytes, r.kd_offs, t);
+    o.finish();
 }
 
 }  // namespace kdtn

@@ -14,13 +14,16 @@
 //
 // Kernels (launch order, kdtn_epoch_encode):
 //   k_utf8_bits      unicode/utf8.ValidString per dictionary string → bitset (1 = invalid)
-//   k_wire_entry_sizes  one thread per entry: encoded size of its Link (UTF-8 checked)
-//   k_wire_sizes     one thread per (list, topology): entry offsets inside the batch,
-//                    batch size (0 on error)
-//   k_scan_*         exclusive scan of the 3T batch sizes → u64 offsets
-//   k_wire_write     one thread per entry: writes its Link (and, for the batch's first
-//                    entry, the LocalPod header) into the wave's LDS image, which the wave
-//                    then stores with coalesced dword stores
+//   k_str_table      {offset, length | STR_BAD} per dictionary string (STR_BAD: not valid
+//                    UTF-8, unicode/utf8.ValidString)
+//   k_wire_entry_sizes  one thread per entry: its topology and encoded size (its Link, plus
+//                    the LocalPod header for a batch's first entry); a string that is not
+//                    valid UTF-8 fails its batch (err bit)
+//   k_wire_scan_*    exclusive scan of the sizes of entries whose batch marshals → u64 arena
+//                    offset of every entry; k_wire_batch_off: batch offsets [3T+1]
+//   k_wire_write     one thread per entry: writes its bytes into the wave's LDS image (dwords
+//                    assembled in registers, WSink), which the wave then stores with
+//                    coalesced dword stores
 #include "kdtn_kernels.h"
 
 namespace kdtn {
@@ -140,47 +143,95 @@ KD_INLINE uint32_t pod_size(const WireIn& w, uint32_t t, bool* ok) {
     return s;
 }
 
-// One thread per entry (all three lists): the encoded size of its Link field (tag +
-// length varint + message), or 0xFFFFFFFF if one of its strings is not valid UTF-8.
+// list of global entry g (entries of the del, add, upd lists in that order)
+KD_INLINE uint32_t wire_list(const WireIn& w, uint32_t g) {
+    return g < w.list_base[1] ? 0u : (g < w.list_base[2] ? 1u : 2u);
+}
+
+// One thread per entry (all three lists): its topology (a wave-cooperative search per list the
+// wave holds) and its encoded size — the Link field (tag + length varint + message), plus the
+// LinksBatchQuery.local_pod field for the first entry of a batch. A string that is not valid
+// UTF-8 makes the batch's Marshal fail: err[t] bit l, and the size does not count.
 __global__ void __launch_bounds__(BLOCK) k_wire_entry_sizes(WireIn w, DevLinks O, DevLinks N, WireWork wk) {
     const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
-    if (g >= w.n_entries) return;
-    const uint32_t lst = g < w.list_base[1] ? 0u : (g < w.list_base[2] ? 1u : 2u);
-    const uint32_t j = w.list_idx[lst][g - w.list_base[lst]];
-    uint32_t psz, lsz;
-    const bool ok = link_sizes(link_refs(w.kd_tab, w.pd_tab, lst == 0 ? O : N, j), &psz, &lsz);
-    wk.rel[g] = ok ? 1u + vlen(lsz) + lsz : 0xFFFFFFFFu;
-}
-
-// One thread per (list, topology): turns its entries' sizes into offsets inside the batch
-// (in place), records the entries' topology, and writes the batch size (0 on error).
-__global__ void __launch_bounds__(BLOCK) k_wire_sizes(WireIn w, DevLinks O, DevLinks N, WireWork wk) {
-    const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
-    if (g >= 3u * w.T) return;
-    const uint32_t lst = g / w.T, t = g - lst * w.T;
-    const uint32_t* off = w.list_off[lst];
-    const uint32_t e0 = off[t], e1 = off[t + 1];
-    uint32_t size = 0;
-    if (e1 > e0) {
-        bool ok;
-        const uint32_t ps = pod_size(w, t, &ok);
-        uint64_t pos = 1u + vlen(ps) + ps;
-        uint32_t* rel = wk.rel + w.list_base[lst];
-        uint32_t* tp = wk.topo + w.list_base[lst];
-        for (uint32_t e = e0; e < e1; ++e) {
-            const uint32_t sz = rel[e];
-            ok = ok && sz != 0xFFFFFFFFu;
-            rel[e] = (uint32_t)pos;
-            tp[e] = t;
-            pos += sz;
+    const bool on = g < w.n_entries;
+    const uint32_t lst = on ? wire_list(w, g) : 3u;
+    const uint32_t e = on ? g - w.list_base[lst] : 0u;
+    uint32_t t = 0;
+#pragma unroll
+    for (uint32_t l = 0; l < 3; ++l)
+        if (__ballot(lst == l)) {                          // wave-uniform
+            const uint32_t tl = entry_topo_wave(w.list_off[l], w.T, e, lst == l);
+            if (lst == l) t = tl;
         }
-        if (!ok || pos > 0xFFFFFFFFull) atomicOr(wk.err + t, 1u << lst);
-        else size = (uint32_t)pos;
+    if (!on) return;
+    uint32_t psz, lsz;
+    bool ok = link_sizes(link_refs(w.kd_tab, w.pd_tab, lst == 0 ? O : N, w.list_idx[lst][e]), &psz, &lsz);
+    uint32_t size = 1u + vlen(lsz) + lsz;
+    if (e == w.list_off[lst][t]) {                         // the batch's first entry carries the header
+        bool pok;
+        const uint32_t ps = pod_size(w, t, &pok);
+        ok = ok && pok;
+        size += 1u + vlen(ps) + ps;
     }
-    wk.size[g] = size;
+    wk.size[g] = ok ? size : 0u;
+    wk.topo[g] = t;
+    if (!ok) atomicOr(wk.err + t, 1u << lst);
 }
 
-// ---- exclusive scan of the 3T batch sizes into u64 offsets -----------------------------
+// size of entry g as the arena lays it out: 0 when its batch does not marshal
+KD_INLINE uint32_t wire_masked_size(const WireIn& w, const WireWork& wk, uint32_t g) {
+    if (g >= w.n_entries) return 0u;
+    return ((wk.err[wk.topo[g]] >> wire_list(w, g)) & 1u) ? 0u : wk.size[g];
+}
+
+// ---- exclusive scan of the entry sizes into u64 arena offsets ----------------------------
+__global__ void __launch_bounds__(BLOCK) k_wire_scan_partial(WireIn w, WireWork wk, uint64_t* part) {
+    __shared__ uint64_t sh[BLOCK / 64];
+    const uint32_t b0 = blockIdx.x * SCAN_CHUNK + threadIdx.x * 4;
+    uint64_t v = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v += wire_masked_size(w, wk, b0 + k);
+    uint64_t tot;
+    block_exclusive(v, sh, &tot);
+    if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_wire_scan_final(WireIn w, WireWork wk, const uint64_t* part) {
+    __shared__ uint64_t sh[BLOCK / 64];
+    const uint32_t b0 = blockIdx.x * SCAN_CHUNK + threadIdx.x * 4;
+    uint32_t v[4];
+    uint64_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        v[k] = wire_masked_size(w, wk, b0 + k);
+        sum += v[k];
+    }
+    uint64_t tot;
+    uint64_t x = part[blockIdx.x] + block_exclusive(sum, sh, &tot);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (b0 + k <= w.n_entries) wk.pos[b0 + k] = x;     // pos[n] = grand total
+        x += v[k];
+    }
+}
+
+// batch (l, t) starts where its first entry does (an empty or failed batch: where the next
+// batch starts); off[3T] = total. A batch of more than 4 GiB is flagged in err[T].
+__global__ void __launch_bounds__(BLOCK) k_wire_batch_off(WireIn w, WireWork wk) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i > 3u * w.T) return;
+    if (i == 3u * w.T) {
+        wk.off[i] = wk.pos[w.n_entries];
+        return;
+    }
+    const uint32_t l = i / w.T, t = i - l * w.T;
+    const uint64_t a = wk.pos[w.list_base[l] + w.list_off[l][t]], b = wk.pos[w.list_base[l] + w.list_off[l][t + 1]];
+    wk.off[i] = a;
+    if (b - a > 0xFFFFFFFFull) atomicOr(wk.err + w.T, 1u);
+}
+
+// ---- exclusive scan of u32 sizes into u64 offsets (fan-out, RemotePod, tc) ---------------
 __global__ void __launch_bounds__(BLOCK) k_scan_partial(const uint32_t* size, uint32_t n, uint64_t* part) {
     __shared__ uint64_t sh[BLOCK / 64];
     const uint32_t b0 = blockIdx.x * SCAN_CHUNK + threadIdx.x * 4;
@@ -227,53 +278,28 @@ __global__ void __launch_bounds__(BLOCK) k_scan_final(const uint32_t* size, uint
 }
 
 // ---- writer --------------------------------------------------------------------------------
-// Byte sink: the wave's LDS image (staged) or global memory (fallback), same code path.
-struct Sink {
-    uint8_t* p;
-    KD_INLINE void byte(uint8_t v) { *p++ = v; }
-    KD_INLINE void varint(uint64_t v) {
-        while (v >= 0x80u) {
-            *p++ = (uint8_t)(v | 0x80u);
-            v >>= 7;
-        }
-        *p++ = (uint8_t)v;
+// string field: tag, length, bytes
+KD_INLINE void str_field_out(WSink& o, uint32_t field, const uint8_t* arena, uint2 r) {
+    const uint32_t len = slen(r);
+    if (!len) return;
+    if (len < 0x80u) {
+        o.put((field << 3 | 2u) | (len << 8), 2u);
+    } else {
+        o.byte(field << 3 | 2u);
+        o.varint(len);
     }
-    // string field: tag, length, bytes read from the arena as aligned dwords (arenas carry
-    // 64 B of slack, so reading past a string's end is safe)
-    // string field whose arena range [b, b + len) is already known: the first 32 bytes come
-    // from nine aligned dword loads issued together (one round trip), the rest dword by dword
-    KD_INLINE void strb(uint32_t field, const uint8_t* arena, uint32_t b, uint32_t len) {
-        if (!len) return;
-        byte((uint8_t)(field << 3 | 2u));
-        varint(len);
-        const uint32_t* a32 = reinterpret_cast<const uint32_t*>(arena) + (b >> 2);
-        const uint32_t sh = b & 3u;
-        const uint32_t nw = (sh + len + 3u) >> 2;          // dwords the string touches (loads only those)
-        uint32_t w[9];
-#pragma unroll
-        for (int q = 0; q < 9; ++q) w[q] = (uint32_t)q < nw ? a32[q] : 0u;
-        const uint32_t head = len < 32u ? len : 32u;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const uint32_t d = __builtin_amdgcn_alignbyte(w[q + 1], w[q], sh);   // string bytes 4q..4q+3
-#pragma unroll
-            for (uint32_t c = 0; c < 4; ++c)
-                if (4u * q + c < head) *p++ = (uint8_t)(d >> (8u * c));
-        }
-        for (uint32_t k = 32; k < len; ++k) *p++ = arena[b + k];
-    }
-    KD_INLINE void strr(uint32_t field, const uint8_t* arena, uint2 r) { strb(field, arena, r.x, slen(r)); }
-};
+    o.str(arena, r.x, len);
+}
 
-KD_INLINE void write_entry(Sink& o, const WireIn& w, const DevLinks& L, uint32_t j, bool header, uint32_t t) {
+KD_INLINE void write_entry(WSink& o, const WireIn& w, const DevLinks& L, uint32_t j, bool header, uint32_t t) {
     if (header) {                                         // LinksBatchQuery.local_pod
         bool ok;
         o.byte(1u << 3 | 2u);
         o.varint(pod_size(w, t, &ok));
-        o.strr(1, w.kd_bytes, sref(w.kd_tab, w.t_name[t]));
-        o.strr(2, w.kd_bytes, sref(w.kd_tab, w.t_src[t]));
-        o.strr(3, w.kd_bytes, sref(w.kd_tab, w.t_netns[t]));
-        o.strr(4, w.kd_bytes, sref(w.kd_tab, w.t_ns[t]));
+        str_field_out(o, 1, w.kd_bytes, sref(w.kd_tab, w.t_name[t]));
+        str_field_out(o, 2, w.kd_bytes, sref(w.kd_tab, w.t_src[t]));
+        str_field_out(o, 3, w.kd_bytes, sref(w.kd_tab, w.t_netns[t]));
+        str_field_out(o, 4, w.kd_bytes, sref(w.kd_tab, w.t_ns[t]));
     }
     const LinkRefs r = link_refs(w.kd_tab, w.pd_tab, L, j);   // every string's range: one round trip
     uint32_t psz, lsz;
@@ -282,11 +308,11 @@ KD_INLINE void write_entry(Sink& o, const WireIn& w, const DevLinks& L, uint32_t
     o.varint(lsz);
     // pb.Link fields in number order: peer_pod 1, local_intf 2, peer_intf 3, local_ip 4,
     // peer_ip 5, uid 6, properties 7, local_mac 8, peer_mac 9
-    o.strr(1, w.kd_bytes, r.k[KDTN_K_PEER_POD]);
-    o.strr(2, w.kd_bytes, r.k[KDTN_K_LOCAL_INTF]);
-    o.strr(3, w.kd_bytes, r.k[KDTN_K_PEER_INTF]);
-    o.strr(4, w.kd_bytes, r.k[KDTN_K_LOCAL_IP]);
-    o.strr(5, w.kd_bytes, r.k[KDTN_K_PEER_IP]);
+    str_field_out(o, 1, w.kd_bytes, r.k[KDTN_K_PEER_POD]);
+    str_field_out(o, 2, w.kd_bytes, r.k[KDTN_K_LOCAL_INTF]);
+    str_field_out(o, 3, w.kd_bytes, r.k[KDTN_K_PEER_INTF]);
+    str_field_out(o, 4, w.kd_bytes, r.k[KDTN_K_LOCAL_IP]);
+    str_field_out(o, 5, w.kd_bytes, r.k[KDTN_K_PEER_IP]);
     if (r.uid) {
         o.byte(6u << 3);
         o.varint((uint64_t)r.uid);
@@ -300,81 +326,33 @@ KD_INLINE void write_entry(Sink& o, const WireIn& w, const DevLinks& L, uint32_t
             o.byte(7u << 3);
             o.varint(r.gap);
         }
-        o.strr((uint32_t)(k < KDTN_P_DUPLICATE ? k + 1 : k + 2), w.pd_bytes, r.p[k]);
+        str_field_out(o, (uint32_t)(k < KDTN_P_DUPLICATE ? k + 1 : k + 2), w.pd_bytes, r.p[k]);
     }
-    o.strr(8, w.kd_bytes, r.k[KDTN_K_LOCAL_MAC]);
-    o.strr(9, w.kd_bytes, r.k[KDTN_K_PEER_MAC]);
+    str_field_out(o, 8, w.kd_bytes, r.k[KDTN_K_LOCAL_MAC]);
+    str_field_out(o, 9, w.kd_bytes, r.k[KDTN_K_PEER_MAC]);
 }
 
 // One thread per entry of the three lists (global entry index g). Consecutive entries
-// write consecutive arena bytes (empty and failed batches occupy none), so a wave's
-// output is one contiguous range: the lanes assemble it in the wave's LDS image with byte
-// writes, then the wave stores it with coalesced dword stores (byte stores only at the
-// two partial dwords shared with the neighbouring waves). A range larger than the image
-// is written straight to global memory.
+// write consecutive arena bytes (failed batches occupy none), so a wave's output is one
+// contiguous range, assembled in the wave's LDS image (wave_image_write).
 __global__ void __launch_bounds__(BLOCK) k_wire_write(WireIn w, DevLinks O, DevLinks N, WireWork wk,
                                                       uint8_t* arena) {
     __shared__ uint32_t img[BLOCK / 64][WIRE_IMG / 4];
     const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
-    const int lane = threadIdx.x & 63;
     bool on = g < w.n_entries;
-    uint32_t lst = 0, t = 0, j = 0;
-    bool header = false;
+    uint32_t lst = 0, t = 0, e = 0;
     uint64_t s0 = 0, s1 = 0;
     if (on) {
-        lst = g < w.list_base[1] ? 0u : (g < w.list_base[2] ? 1u : 2u);
-        const uint32_t e = g - w.list_base[lst];
+        lst = wire_list(w, g);
+        e = g - w.list_base[lst];
         t = wk.topo[g];
         on = ((wk.err[t] >> lst) & 1u) == 0;
-        if (on) {
-            j = w.list_idx[lst][e];
-            const uint64_t bo = wk.off[lst * w.T + t];
-            const uint32_t rel = wk.rel[g];
-            header = e == w.list_off[lst][t];
-            s0 = bo + (header ? 0u : rel);
-            const uint32_t nxt = e + 1 < w.list_off[lst][t + 1] ? wk.rel[g + 1] : (uint32_t)(wk.off[lst * w.T + t + 1] - bo);
-            s1 = bo + nxt;
-        }
+        s0 = wk.pos[g];
+        s1 = wk.pos[g + 1];
     }
-    // wave range
-    uint64_t r0 = on ? s0 : ~0ull, r1 = on ? s1 : 0ull;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        const uint64_t a = __shfl_xor(r0, d, 64), b = __shfl_xor(r1, d, 64);
-        r0 = a < r0 ? a : r0;
-        r1 = b > r1 ? b : r1;
-    }
-    if (r1 <= r0) return;                                 // no active lane (wave-uniform)
-    const DevLinks& L = lst == 0 ? O : N;
-    const uint32_t lead = (uint32_t)(r0 & 3u);
-    if (r1 - r0 + lead > (uint64_t)WIRE_IMG) {            // too large: direct byte stores
-        if (on) {
-            Sink o{arena + s0};
-            write_entry(o, w, L, j, header, t);
-        }
-        return;
-    }
-    uint8_t* im = reinterpret_cast<uint8_t*>(img[threadIdx.x >> 6]);
-    if (on) {
-        Sink o{im + lead + (uint32_t)(s0 - r0)};
-        write_entry(o, w, L, j, header, t);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const uint64_t a0 = r0 - lead;                        // dword-aligned global start
-    const uint32_t nw = (uint32_t)((r1 - a0 + 3) >> 2);
-    const uint32_t* iw = img[threadIdx.x >> 6];
-    for (uint32_t q = lane; q < nw; q += 64) {
-        const uint64_t ga = a0 + 4ull * q;
-        const uint32_t v = iw[q];
-        if (ga >= r0 && ga + 4 <= r1) {
-            *reinterpret_cast<uint32_t*>(arena + ga) = v;
-        } else {
-            for (uint32_t k = 0; k < 4; ++k)
-                if (ga + k >= r0 && ga + k < r1) arena[ga + k] = (uint8_t)(v >> (8 * k));
-        }
-    }
+    wave_image_write(img[threadIdx.x >> 6], on, s0, s1, arena, [&](WSink& o) __attribute__((always_inline)) {
+        write_entry(o, w, lst == 0 ? O : N, w.list_idx[lst][e], e == w.list_off[lst][t], t);
+    });
 }
 
 // ==========================================================================================
@@ -409,16 +387,10 @@ struct RemoteMsg {
     bool ok;                        // every string valid UTF-8
 };
 
-// every lane of the wave calls it (the topology search is wave-cooperative); on = m < n_msgs
-KD_INLINE RemoteMsg remote_msg(const RemoteIn& r, uint32_t m, bool on) {
+// the strings of add entry e's message (remote: the UpdateRemote payload, else the physical
+// peer's local Update payload); t = the entry's topology
+KD_INLINE RemoteMsg remote_msg(const RemoteIn& r, uint32_t e, uint32_t t, bool remote) {
     RemoteMsg q;
-    const bool remote = m < r.n_remote;
-    const uint32_t e = on ? (remote ? r.rem_idx[m] : r.phys_idx[m - r.n_remote]) : 0u;
-    const uint32_t t = entry_topo_wave(r.add_off, r.T, e, on);
-    if (!on) {
-        q.ok = false;
-        return q;
-    }
     const uint32_t j = r.add_idx[e];
     const uint4 res = r.add_res[e];
     const uint32_t peer_pod = r.N.key(KDTN_K_PEER_POD, j);
@@ -469,20 +441,36 @@ KD_INLINE uint32_t remote_body_size(const RemoteMsg& q, uint32_t* psz) {
     return n + 1u + vlen(p) + p;
 }
 
-__global__ void __launch_bounds__(BLOCK) k_remote_sizes(RemoteIn r, uint32_t* size) {
-    const uint32_t m = blockIdx.x * BLOCK + threadIdx.x;
-    const RemoteMsg q = remote_msg(r, m, m < r.n_msgs);
-    if (m >= r.n_msgs) return;
+// One thread per add entry (add-list order: the entry's columns are read coalesced): the
+// size of its message, if it has one (0 when a string is not valid UTF-8).
+__global__ void __launch_bounds__(BLOCK) k_remote_entry_sizes(RemoteIn r, uint32_t* msz_e) {
+    const uint32_t e = blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t kind = e < r.n_add ? remote_kind(r, e) : 0u;
+    if (__ballot(kind != 0) == 0) return;           // wave-uniform
+    const uint32_t t = entry_topo_wave(r.add_off, r.T, e, kind != 0);
+    if (!kind) return;
+    const RemoteMsg q = remote_msg(r, e, t, kind == 1);
     uint32_t psz;
     const uint32_t body = remote_body_size(q, &psz);
-    size[m] = q.ok ? vlen(body) + body : 0u;
+    msz_e[e] = q.ok ? vlen(body) + body : 0u;
 }
 
-KD_INLINE void write_remote(Sink& o, const RemoteIn& r, const RemoteMsg& q) {
+// message m's size from its add entry's (one gather per message, fan-out order)
+__global__ void __launch_bounds__(BLOCK) k_remote_msg_sizes(RemoteIn r, const uint32_t* msz_e, const uint32_t* tsz_e,
+                                                            uint32_t* msz, uint32_t* tsz) {
+    const uint32_t m = blockIdx.x * BLOCK + threadIdx.x;
+    if (m >= r.n_msgs) return;
+    const bool remote = m < r.n_remote;
+    const uint32_t e = remote ? r.rem_idx[m] : r.phys_idx[m - r.n_remote];
+    msz[m] = msz_e[e];
+    tsz[m] = remote ? tsz_e[e] : 0u;
+}
+
+KD_INLINE void write_remote(WSink& o, const RemoteIn& r, const RemoteMsg& q) {
     uint32_t psz;
     o.varint(remote_body_size(q, &psz));
 #pragma unroll
-    for (int k = 0; k < 5; ++k) o.strr((uint32_t)k + 1, r.kd_bytes, q.s[k]);
+    for (int k = 0; k < 5; ++k) str_field_out(o, (uint32_t)k + 1, r.kd_bytes, q.s[k]);
     if (q.vni) {
         o.byte(6u << 3);
         o.varint((uint64_t)(int64_t)q.vni);
@@ -495,62 +483,28 @@ KD_INLINE void write_remote(Sink& o, const RemoteIn& r, const RemoteMsg& q) {
             o.byte(7u << 3);
             o.varint(q.gap);
         }
-        o.strr((uint32_t)(k < KDTN_P_DUPLICATE ? k + 1 : k + 2), r.pd_bytes, q.p[k]);
+        str_field_out(o, (uint32_t)(k < KDTN_P_DUPLICATE ? k + 1 : k + 2), r.pd_bytes, q.p[k]);
     }
-    o.strr(8, r.kd_bytes, q.s[5]);
+    str_field_out(o, 8, r.kd_bytes, q.s[5]);
 }
 
-// one thread per message; a wave's messages are one contiguous range, assembled in the
-// wave's LDS image and stored with coalesced dword stores (as k_wire_write)
+// One thread per add entry with a message, in add-list order (its columns read coalesced),
+// writing the message straight to its fan-out position: dwords assembled in registers, byte
+// stores only where a message shares a dword with its neighbours.
 __global__ void __launch_bounds__(BLOCK) k_remote_write(RemoteIn r, const uint64_t* off, uint8_t* arena) {
-    __shared__ uint32_t img[BLOCK / 64][WIRE_IMG / 4];
-    const uint32_t m = blockIdx.x * BLOCK + threadIdx.x;
-    const int lane = threadIdx.x & 63;
-    bool on = m < r.n_msgs;
-    uint64_t s0 = 0, s1 = 0;
-    if (on) {
-        s0 = off[m];
-        s1 = off[m + 1];
-        on = s1 > s0;                               // empty: Marshal error
-    }
-    uint64_t r0 = on ? s0 : ~0ull, r1 = on ? s1 : 0ull;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        const uint64_t a = __shfl_xor(r0, d, 64), b = __shfl_xor(r1, d, 64);
-        r0 = a < r0 ? a : r0;
-        r1 = b > r1 ? b : r1;
-    }
-    if (r1 <= r0) return;                           // no active lane (wave-uniform)
-    const RemoteMsg q = remote_msg(r, m, on);
-    const uint32_t lead = (uint32_t)(r0 & 3u);
-    if (r1 - r0 + lead > (uint64_t)WIRE_IMG) {      // too large for the image: direct byte stores
-        if (on) {
-            Sink o{arena + s0};
-            write_remote(o, r, q);
-        }
-        return;
-    }
-    uint8_t* im = reinterpret_cast<uint8_t*>(img[threadIdx.x >> 6]);
-    if (on) {
-        Sink o{im + lead + (uint32_t)(s0 - r0)};
-        write_remote(o, r, q);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const uint64_t a0 = r0 - lead;
-    const uint32_t nw = (uint32_t)((r1 - a0 + 3) >> 2);
-    const uint32_t* iw = img[threadIdx.x >> 6];
-    for (uint32_t k = lane; k < nw; k += 64) {
-        const uint64_t ga = a0 + 4ull * k;
-        const uint32_t v = iw[k];
-        if (ga >= r0 && ga + 4 <= r1) {
-            *reinterpret_cast<uint32_t*>(arena + ga) = v;
-        } else {
-            for (uint32_t c = 0; c < 4; ++c)
-                if (ga + c >= r0 && ga + c < r1) arena[ga + c] = (uint8_t)(v >> (8 * c));
-        }
-    }
+    const uint32_t e = blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t kind = e < r.n_add ? remote_kind(r, e) : 0u;
+    if (__ballot(kind != 0) == 0) return;           // wave-uniform
+    const uint32_t t = entry_topo_wave(r.add_off, r.T, e, kind != 0);
+    if (!kind) return;
+    const uint32_t m = remote_msg_index(r, e, kind);
+    const uint64_t s0 = off[m], s1 = off[m + 1];
+    if (s1 <= s0) return;                           // Marshal error: empty
+    const RemoteMsg q = remote_msg(r, e, t, kind == 1);
+    WSink o;
+    o.init(arena + s0);
+    write_remote(o, r, q);
+    o.finish();
 }
 
 }  // namespace kdtn
