@@ -27,15 +27,19 @@ namespace kdtn {
 // cut[3t + list], 0xFFFFFFFF = none); k_reach then writes per add entry REACH_ON |
 // REACH_SEND, per update entry REACH_ON, and (mark != nullptr) stamps the destination
 // daemon of every RemotePod sent.
-__global__ void __launch_bounds__(BLOCK) k_reach_cuts(ReachIn f, uint32_t nd, uint32_t na, uint32_t nu, uint32_t* cut) {
+__global__ void __launch_bounds__(BLOCK) k_reach_cuts(ReachIn f, uint32_t nd, uint32_t na, uint32_t nu, uint32_t* cut,
+                                                      uint8_t* st_add) {
     const uint32_t x = blockIdx.x * BLOCK + threadIdx.x;
     if (x < nd) {
         if ((f.del_res[x].w >> 8) & 0xFFu) atomicMin(&cut[3 * entry_topo(f.del_off, f.T, x)], x);   // delLink error
     } else if (x < nd + na) {
         const uint32_t e = x - nd;
         const uint4 r = f.add_res[e];
-        if (add_fails(r, qdisc_err(f.add_qdisc, e)) || (r.w >> 24))          // or remote Update failed
+        const uint32_t qe = qdisc_err(f.add_qdisc, e);
+        const bool fails = add_fails(r, qe);
+        if (fails || (r.w >> 24))                                            // or remote Update failed
             atomicMin(&cut[3 * entry_topo(f.add_off, f.T, e) + 1], e);
+        st_add[e] = (!fails && sends_remote(r, qe)) ? REACH_SEND : 0;        // k_reach reads this byte
     } else if (x < nd + na + nu) {
         const uint32_t e = x - nd - na;
         if ((f.upd_res[e].w >> 8) & 0xFFu) atomicMin(&cut[3 * entry_topo(f.upd_off, f.T, e) + 2], e);   // MakeVeth / MakeQdiscs
@@ -43,7 +47,8 @@ __global__ void __launch_bounds__(BLOCK) k_reach_cuts(ReachIn f, uint32_t nd, ui
 }
 
 __global__ void __launch_bounds__(BLOCK) k_reach(ReachIn f, uint32_t na, uint32_t nu, const uint32_t* cut,
-                                                 uint32_t* mark, uint8_t* reach_add, uint8_t* reach_upd) {
+                                                 const uint8_t* st_add, uint32_t* mark, uint8_t* reach_add,
+                                                 uint8_t* reach_upd) {
     const uint32_t x = blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t ta = entry_topo_wave(f.add_off, f.T, x, x < na);
     const uint32_t tu = entry_topo_wave(f.upd_off, f.T, x - na, x >= na && x < na + nu);
@@ -52,13 +57,14 @@ __global__ void __launch_bounds__(BLOCK) k_reach(ReachIn f, uint32_t na, uint32_
         uint8_t a = 0;
         if (cut[3 * t] == 0xFFFFFFFFu && x <= cut[3 * t + 1]) {
             a = REACH_ON;
-            const uint4 r = f.add_res[x];
-            const uint32_t qe = qdisc_err(f.add_qdisc, x);
-            if (!add_fails(r, qe) && sends_remote(r, qe)) {
+            if (st_add[x] & REACH_SEND) {               // no failure, RemotePod sent (k_reach_cuts)
                 a |= REACH_SEND;
                 // a few dozen daemons take millions of stamps: store only a missing one (a
                 // stale read stores again, harmlessly), so the words are not written per entry
-                if (mark && mark[r.z] != f.stamp) mark[r.z] = f.stamp;
+                if (mark) {
+                    const uint32_t node = f.add_res[x].z;
+                    if (mark[node] != f.stamp) mark[node] = f.stamp;
+                }
             }
         }
         reach_add[x] = a;

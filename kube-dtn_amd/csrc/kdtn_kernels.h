@@ -131,11 +131,14 @@ struct DevLinks {
 //           non-empty), so the bulk emission is not software-pipelined and the kernel
 //           targets DIFF_WAVES waves per SIMD; kdtn_epoch_run picks it when M > 0 and N > 0
 //   bit 12: (A/B) bulk loop: the next record's segment search before this record's gathers
+//   bit 15: (A/B) bulk emission stages the wave's 64 qdisc structs at once and stores them with
+//           16-B stores (about half the store instructions of two 32-struct halves of 8-B stores)
 //   bit 14: first bulk record's columns loaded before the gate / count / base phases (product;
 //           A/B vs 515: 0.6164 / 0.6180 ms at 1M pods, 0.0849 / 0.0869 at 125k, 0.1563 / 0.1583 config 4)
 constexpr int VAR_NT_LOAD = 1, VAR_NT_STORE = 2, VAR_NO_QSTORE = 4, VAR_NT_POD = 8, VAR_TRACE = 16,
               VAR_SKIP_POD = 32, VAR_SKIP_PCT = 64, VAR_OCC5 = 128, VAR_OCC6 = 256,
-              VAR_MASK_EMPTY = 512, VAR_NO_PREFIX = 1024, VAR_DIFF = 2048, VAR_DECODE_FIRST = 4096, VAR_PREFETCH = 16384;
+              VAR_MASK_EMPTY = 512, VAR_NO_PREFIX = 1024, VAR_DIFF = 2048, VAR_DECODE_FIRST = 4096, VAR_PREFETCH = 16384,
+              VAR_Q16 = 32768;
 constexpr int DIFF_WAVES = 5;
 constexpr int var_waves(int v) {
     return (v & VAR_OCC6) ? 6 : (v & VAR_OCC5) ? 5 : (v & VAR_DIFF) ? DIFF_WAVES : (v & VAR_PREFETCH) ? 4 : 1;
@@ -148,7 +151,7 @@ constexpr int DEFAULT_VARIANT = VAR_NT_LOAD | VAR_NT_STORE | VAR_MASK_EMPTY | VA
 // trace build of the default
 #define KDTN_PROFILING_VARIANTS(X) X(0) X(1) X(2) X(3) X(4) X(5) X(9) X(11) X(17) X(33) X(65) X(97) \
     X(101) X(113) X(129) X(257) X(513) X(521) X(523) X(529) X(531) X(545) X(547) X(579) X(611) X(519) \
-    X(641) X(643) X(771) X(1025) X(1537) X(2579) X(4611) X(515)
+    X(641) X(643) X(771) X(1025) X(1537) X(2579) X(4611) X(515) X(16915) X(16963) X(16931) X(16995) X(16903) X(49667)
 
 struct DevTopos {
     const uint32_t* ns;
@@ -433,9 +436,9 @@ struct ReachIn {
     const uint4* upd_res;
     uint32_t T, stamp;
 };
-__global__ void k_reach_cuts(ReachIn f, uint32_t nd, uint32_t na, uint32_t nu, uint32_t* cut);
-__global__ void k_reach(ReachIn f, uint32_t na, uint32_t nu, const uint32_t* cut, uint32_t* mark, uint8_t* reach_add,
-                        uint8_t* reach_upd);
+__global__ void k_reach_cuts(ReachIn f, uint32_t nd, uint32_t na, uint32_t nu, uint32_t* cut, uint8_t* st_add);
+__global__ void k_reach(ReachIn f, uint32_t na, uint32_t nu, const uint32_t* cut, const uint8_t* st_add, uint32_t* mark,
+                        uint8_t* reach_add, uint8_t* reach_upd);
 
 // VxlanManager state after the epoch (kdtn_vni.hip; include/kdtn.h kdtn_epoch_vni_apply)
 struct VniOpsIn {
@@ -536,6 +539,19 @@ struct WSink {
         if (head && !hp) part(d0, first, head, 4u);     // shared first dword, flushed
         if (fill) part(d, (uint32_t)acc, hp ? head : 0u, fill);
     }
+    // owned mode: the writer owns every byte of its dwords (a private LDS slot); `lead` zero
+    // bytes put the output at the alignment of its destination
+    KD_INLINE void init_owned(uint32_t* slot, uint32_t lead) {
+        d = d0 = slot;
+        head = 0;
+        fill = lead;
+        hp = false;
+        acc = 0;
+        first = 0;
+    }
+    KD_INLINE void finish_owned() {
+        if (fill) *d = (uint32_t)acc;
+    }
     KD_INLINE void byte(uint32_t v) { put(v, 1u); }
     // protobuf base-128 varint: four 7-bit groups per put
     KD_INLINE void varint(uint64_t v) {
@@ -625,12 +641,95 @@ KD_INLINE void wave_image_write(uint32_t* img, bool on, uint64_t s0, uint64_t s1
     }
 }
 
+// One wave writes its lanes' byte ranges [s0, s1) when they are NOT one contiguous range (the
+// RemotePod messages of consecutive add entries go to their daemons' runs): in two rounds of 32
+// lanes, every lane writes its range into a private dword slot of the wave's LDS image at the
+// alignment of its destination (owned WSink), then the wave copies the slots out dword by
+// dword — lane q takes image dword q, finds its slot by binary search, and stores it whole, or
+// by bytes where the dword is shared with a neighbouring range. Consecutive lanes thus store
+// consecutive dwords of each range instead of every lane storing its own range alone. A round
+// larger than the image is written straight to global memory. Every lane must call it.
+constexpr int SEG_META = 4 * 32 + 1;            // dwords of slot metadata at the image's end
+template <int R, typename F>
+KD_INLINE void wave_segments_round(uint32_t* img, bool on, uint64_t s0, uint32_t len, uint32_t ndw, uint8_t* arena,
+                                   F& body) {
+    const int lane = threadIdx.x & 63;
+    uint32_t* mq = img + WIRE_IMG / 4 - SEG_META;  // [33] slot starts (dwords), then per slot: dst lo, hi, lead|len
+    uint32_t* mlo = mq + 33;
+    uint32_t* mhi = mlo + 32;
+    uint32_t* mll = mhi + 32;
+    constexpr uint32_t budget = WIRE_IMG / 4 - SEG_META;
+    const uint32_t lead = (uint32_t)s0 & 3u;
+    const bool mine = (lane >> 5) == R;
+    const uint32_t x = mine ? ndw : 0u;
+    uint32_t inc = x;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += o;
+    }
+    const uint32_t q0 = __shfl(inc - x, 32 * R, 64);            // the round's first slot start
+    const uint32_t total = __shfl(inc, 32 * R + 31, 64) - q0;
+    const uint32_t qi = inc - x - q0;
+    if (total == 0) return;                                      // wave-uniform
+    const bool direct = total > budget;                          // too large: straight to global memory
+    const int sl = lane - 32 * R;
+    if (mine && !direct) {
+        mq[sl] = qi;
+        mlo[sl] = (uint32_t)(s0 & ~3ull);
+        mhi[sl] = (uint32_t)(s0 >> 32);
+        mll[sl] = lead | (len << 2);
+    }
+    if (mine && on) {                                            // one call site of the body
+        WSink o;
+        if (direct) o.init(arena + s0);
+        else o.init_owned(img + qi, lead);
+        body(o);
+        if (direct) o.finish();
+        else o.finish_owned();
+    }
+    if (direct) return;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (uint32_t q = lane; q < total; q += 64) {
+        int i = 0;                                               // the last slot starting at or before q
+#pragma unroll
+        for (int step = 16; step >= 1; step >>= 1)
+            if (i + step < 32 && mq[i + step] <= q) i += step;
+        const uint32_t k = q - mq[i], ll = mll[i];
+        const uint32_t ld = ll & 3u, end = ld + (ll >> 2);      // valid bytes of the slot: [ld, end)
+        uint8_t* dst = arena + ((((uint64_t)mhi[i]) << 32) | mlo[i]) + 4ull * k;
+        const uint32_t v = img[q];
+        const uint32_t lo = k == 0 ? ld : 0u;
+        const uint32_t hi = end - 4u * k < 4u ? end - 4u * k : 4u;
+        if (lo == 0 && hi == 4u) {
+            *reinterpret_cast<uint32_t*>(dst) = v;
+        } else {
+#pragma unroll
+            for (uint32_t c = 0; c < 4; ++c)
+                if (c >= lo && c < hi) dst[c] = (uint8_t)(v >> (8 * c));
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+template <typename F>
+KD_INLINE void wave_segments_write(uint32_t* img, bool on, uint64_t s0, uint64_t s1, uint8_t* arena, F&& body) {
+    const uint32_t len = on ? (uint32_t)(s1 - s0) : 0u;
+    const uint32_t ndw = on ? (((uint32_t)s0 & 3u) + len + 3u) >> 2 : 0u;
+    wave_segments_round<0>(img, on, s0, len, ndw, arena, body);   // lanes 0-31, then 32-63
+    wave_segments_round<1>(img, on, s0, len, ndw, arena, body);
+}
+
 __global__ void k_utf8_bits(const uint8_t* bytes, const uint32_t* offs, uint32_t n, uint32_t* bits);
 __global__ void k_str_table(const uint8_t* bytes, const uint32_t* offs, uint32_t n, uint2* tab);
 __global__ void k_wire_entry_sizes(WireIn w, DevLinks O, DevLinks N, WireWork wk);
 __global__ void k_wire_scan_partial(WireIn w, WireWork wk, uint64_t* part);
 __global__ void k_wire_scan_final(WireIn w, WireWork wk, const uint64_t* part);
 __global__ void k_wire_batch_off(WireIn w, WireWork wk);
+
 __global__ void k_scan_partial(const uint32_t* size, uint32_t n, uint64_t* part);
 __global__ void k_scan_top(uint64_t* part, uint32_t nb);
 __global__ void k_scan_final(const uint32_t* size, uint32_t n, const uint64_t* part, uint64_t* off);

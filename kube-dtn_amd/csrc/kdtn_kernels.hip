@@ -1017,6 +1017,45 @@ __device__ __forceinline__ void wave_store_qdisc(uint2* outq, bool active, uint3
     }
 }
 
+// (VAR_Q16) the wave's 64 structs staged at once and stored as 16-B words: the destination
+// range starts 8-B aligned, so at most one leading and one trailing 8-B word go alone
+template <int V>
+__device__ __forceinline__ void wave_store_qdisc16(uint2* outq, bool active, uint32_t e, const uint32_t* q,
+                                                   uint2* stage) {
+    const uint64_t m = __ballot(active);
+    if (m == 0) return;
+    const int lane = threadIdx.x & 63;
+    const uint32_t p0 = __shfl(e, __ffsll((long long)m) - 1, 64);
+    const uint32_t rank = __popcll(m & lanemask_lt()), cnt = __popcll(m);
+    if (active) {
+        uint2* slot = stage + rank * 9;
+#pragma unroll
+        for (int w = 0; w < 9; ++w) slot[w] = make_uint2(q[2 * w], q[2 * w + 1]);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const size_t base = (size_t)p0 * 9;
+    uint2* dst = outq + base;
+    const uint32_t nq = cnt * 9, head = (uint32_t)(base & 1u), n16 = (nq - head) >> 1;
+    if (head && lane == 0) store_q8<V>(dst, stage[0]);
+    u32x4* d16 = reinterpret_cast<u32x4*>(dst + head);
+    for (uint32_t k = lane; k < n16; k += 64) {
+        const uint2 a = stage[head + 2 * k], b = stage[head + 2 * k + 1];
+        u32x4 v;
+        v.x = a.x;
+        v.y = a.y;
+        v.z = b.x;
+        v.w = b.y;
+        if constexpr ((V & VAR_NT_STORE) != 0) __builtin_nontemporal_store(v, d16 + k);
+        else d16[k] = v;
+    }
+    if (((nq - head) & 1u) && lane == 0) store_q8<V>(dst + nq - 1, stage[nq - 1]);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // ======================================================================================
 // k_reconcile: one workgroup = TPW consecutive topologies (dynamic ticket order).
 // ======================================================================================
@@ -1364,6 +1403,7 @@ template <int V>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(var_waves(V))))
 k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWork wk) {
     __shared__ RecShared s;
+    __shared__ uint2 stage64[BLOCK / 64][(V & VAR_Q16) ? 64 * 9 : 1];   // (VAR_Q16 only)
     const int tid = threadIdx.x;
     unsigned long long t_entry = 0;
     if constexpr ((V & VAR_TRACE) != 0) t_entry = __builtin_amdgcn_s_memrealtime();
@@ -1666,7 +1706,8 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
                 next();
                 fetch(nx, nc);
             }
-            wave_store_qdisc<V>(out.add_qdisc, qa, e, q, stage);
+            if constexpr ((V & VAR_Q16) != 0) wave_store_qdisc16<V>(out.add_qdisc, qa, e, q, stage64[tid >> 6]);
+            else wave_store_qdisc<V>(out.add_qdisc, qa, e, q, stage);
             cs = nx;
             cc = nc;
         }

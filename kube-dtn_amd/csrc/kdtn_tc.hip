@@ -173,18 +173,24 @@ __global__ void __launch_bounds__(BLOCK) k_tc_remote_entry_sizes(RemoteIn r, uin
                     : 0u;
 }
 
-// one thread per add entry, writing its command at its message's position (add-list order)
+// one thread per add entry, writing its command at its message's position (add-list order;
+// per-daemon runs stored through the wave's LDS image, wave_segments_write)
 __global__ void __launch_bounds__(BLOCK) k_tc_remote_write(RemoteIn r, const uint64_t* off, uint8_t* arena) {
+    __shared__ uint32_t img[BLOCK / 64][WIRE_IMG / 4];
     const uint32_t e = blockIdx.x * BLOCK + threadIdx.x;
-    if (e >= r.n_add) return;
-    const TcEntry t = tc_remote_entry(r, e);
-    if (!t.on) return;
-    const uint32_t m = r.rem_inv[e];
-    if (off[m + 1] <= off[m]) return;
-    WSink o;
-    o.init(arena + off[m]);
-    write_tbf_argv(o, r.kd_bytes, r.kd_offs, t);
-    o.finish();
+    TcEntry t{0, 0, 0, 0, false};
+    uint64_t s0 = 0, s1 = 0;
+    if (e < r.n_add) {
+        t = tc_remote_entry(r, e);
+        if (t.on) {
+            const uint32_t m = r.rem_inv[e];
+            s0 = off[m];
+            s1 = off[m + 1];
+        }
+    }
+    if (__ballot(s1 > s0) == 0) return;             // wave-uniform
+    wave_segments_write(img[threadIdx.x >> 6], s1 > s0, s0, s1, arena,
+                        [&](WSink& o) __attribute__((always_inline)) { write_tbf_argv(o, r.kd_bytes, r.kd_offs, t); });
 }
 
 }  // namespace kdtn

@@ -69,15 +69,35 @@ __global__ void __launch_bounds__(BLOCK) k_utf8_bits(const uint8_t* bytes, const
     if (lane == 0 || lane == 32) bits[((i - lane) >> 5) + (lane >> 5)] = lane ? (uint32_t)(m >> 32) : (uint32_t)m;
 }
 
-// {offset, length | STR_BAD} per dictionary string (the encoders' one gather per string field)
+// {offset, length | STR_BAD} per dictionary string (the encoders' one gather per string field).
+// The high-bit test reads the string's first 32 bytes as one 16-B load pair (+ a dword)
+// instead of byte by byte; only strings with a byte >= 0x80 run the UTF-8 automaton.
 __global__ void __launch_bounds__(BLOCK) k_str_table(const uint8_t* bytes, const uint32_t* offs, uint32_t n,
                                                      uint2* tab) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n) return;
     const uint32_t b = offs[i], len = offs[i + 1] - b;
-    bool ascii = true;
-    for (uint32_t k = 0; k < len && ascii; ++k) ascii = bytes[b + k] < 0x80u;
-    const bool bad = !ascii && !utf8_ok(bytes + b, len);
+    uint32_t hi = 0;
+    if (len) {
+        typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+        const uint32_t* a32 = reinterpret_cast<const uint32_t*>(bytes) + (b >> 2);
+        const uint32_t sh = b & 3u, nw = (sh + len + 3u) >> 2;
+        const u32x4a A = *reinterpret_cast<const u32x4a*>(a32);
+        u32x4a B = {0u, 0u, 0u, 0u};
+        if (nw > 4u) B = *reinterpret_cast<const u32x4a*>(a32 + 4);
+        const uint32_t c8 = nw > 8u ? a32[8] : 0u;
+        const uint32_t w[9] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w, c8};
+#pragma unroll
+        for (uint32_t q = 0; q < 8; ++q) {
+            if (4u * q < len) {
+                const uint32_t r = len - 4u * q;
+                const uint32_t m = r >= 4u ? 0x80808080u : (0x80808080u & ((1u << (8u * r)) - 1u));
+                hi |= __builtin_amdgcn_alignbyte(w[q + 1], w[q], sh) & m;
+            }
+        }
+        for (uint32_t k = 32; k < len; ++k) hi |= bytes[b + k] & 0x80u;
+    }
+    const bool bad = hi != 0 && !utf8_ok(bytes + b, len);
     tab[i] = make_uint2(b, len | (bad ? STR_BAD : 0u));
 }
 
@@ -291,7 +311,9 @@ KD_INLINE void str_field_out(WSink& o, uint32_t field, const uint8_t* arena, uin
     o.str(arena, r.x, len);
 }
 
-KD_INLINE void write_entry(WSink& o, const WireIn& w, const DevLinks& L, uint32_t j, bool header, uint32_t t) {
+// one entry's bytes from its gathered string ranges r (and sizes psz / lsz)
+KD_INLINE void write_entry_refs(WSink& o, const WireIn& w, const LinkRefs& r, uint32_t psz, uint32_t lsz, bool header,
+                                uint32_t t) {
     if (header) {                                         // LinksBatchQuery.local_pod
         bool ok;
         o.byte(1u << 3 | 2u);
@@ -301,9 +323,6 @@ KD_INLINE void write_entry(WSink& o, const WireIn& w, const DevLinks& L, uint32_
         str_field_out(o, 3, w.kd_bytes, sref(w.kd_tab, w.t_netns[t]));
         str_field_out(o, 4, w.kd_bytes, sref(w.kd_tab, w.t_ns[t]));
     }
-    const LinkRefs r = link_refs(w.kd_tab, w.pd_tab, L, j);   // every string's range: one round trip
-    uint32_t psz, lsz;
-    link_sizes(r, &psz, &lsz);
     o.byte(2u << 3 | 2u);                                 // LinksBatchQuery.links
     o.varint(lsz);
     // pb.Link fields in number order: peer_pod 1, local_intf 2, peer_intf 3, local_ip 4,
@@ -330,6 +349,13 @@ KD_INLINE void write_entry(WSink& o, const WireIn& w, const DevLinks& L, uint32_
     }
     str_field_out(o, 8, w.kd_bytes, r.k[KDTN_K_LOCAL_MAC]);
     str_field_out(o, 9, w.kd_bytes, r.k[KDTN_K_PEER_MAC]);
+}
+
+KD_INLINE void write_entry(WSink& o, const WireIn& w, const DevLinks& L, uint32_t j, bool header, uint32_t t) {
+    const LinkRefs r = link_refs(w.kd_tab, w.pd_tab, L, j);   // every string's range: one round trip
+    uint32_t psz, lsz;
+    link_sizes(r, &psz, &lsz);
+    write_entry_refs(o, w, r, psz, lsz, header, t);
 }
 
 // One thread per entry of the three lists (global entry index g). Consecutive entries
@@ -489,22 +515,26 @@ KD_INLINE void write_remote(WSink& o, const RemoteIn& r, const RemoteMsg& q) {
 }
 
 // One thread per add entry with a message, in add-list order (its columns read coalesced),
-// writing the message straight to its fan-out position: dwords assembled in registers, byte
-// stores only where a message shares a dword with its neighbours.
+// writing the message at its fan-out position. A wave's messages for one daemon are one
+// contiguous run of the arena (fan-out order keeps add-list order within a daemon), so the
+// wave stores them through its LDS image dword by dword (wave_segments_write).
 __global__ void __launch_bounds__(BLOCK) k_remote_write(RemoteIn r, const uint64_t* off, uint8_t* arena) {
+    __shared__ uint32_t img[BLOCK / 64][WIRE_IMG / 4];
     const uint32_t e = blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t kind = e < r.n_add ? remote_kind(r, e) : 0u;
     if (__ballot(kind != 0) == 0) return;           // wave-uniform
     const uint32_t t = entry_topo_wave(r.add_off, r.T, e, kind != 0);
-    if (!kind) return;
-    const uint32_t m = remote_msg_index(r, e, kind);
-    const uint64_t s0 = off[m], s1 = off[m + 1];
-    if (s1 <= s0) return;                           // Marshal error: empty
-    const RemoteMsg q = remote_msg(r, e, t, kind == 1);
-    WSink o;
-    o.init(arena + s0);
-    write_remote(o, r, q);
-    o.finish();
+    uint64_t s0 = 0, s1 = 0;
+    if (kind) {
+        const uint32_t m = remote_msg_index(r, e, kind);
+        s0 = off[m];
+        s1 = off[m + 1];
+    }
+    const bool on = s1 > s0;                        // empty: no message or a Marshal error
+    RemoteMsg q{};
+    if (on) q = remote_msg(r, e, t, kind == 1);
+    wave_segments_write(img[threadIdx.x >> 6], on, s0, s1, arena,
+                        [&](WSink& o) __attribute__((always_inline)) { write_remote(o, r, q); });
 }
 
 }  // namespace kdtn

@@ -1,4 +1,4 @@
-# r03g: RemotePod messages and the receiving daemon's tc argv in add-list order (sizes per add
+# r03g: single-pass wire writer (look-back scan, two-pass fallback); RemotePod messages and the receiving daemon's tc argv in add-list order (sizes per add
 # entry gathered into fan-out order; writer stores each message at its fan-out position)
 set -uo pipefail
 O=gpurun_out/r03g; mkdir -p $O
