@@ -396,10 +396,13 @@ KD_INLINE uint32_t entry_topo(const uint32_t* offs, uint32_t T, uint32_t e) {
 }
 
 // entry_topo for every lane of a wave at once (all lanes must call it; on = the lane has an
-// entry): the search range is narrowed to the topologies of the wave's smallest and largest
-// entry, found by two wave-uniform searches (one address per step), so each lane's own search
-// spans a few topologies instead of all T — a wave's entries are usually neighbours.
+// entry). The topologies of the wave's smallest and largest entry are found together by a
+// 32-ary search (lanes 0-31 for one, 32-63 for the other; each step one load per lane and a
+// ballot, so about log32(T) dependent loads instead of log2(T)); when the wave's entries span
+// fewer than 64 topologies, one more load gives every lane the boundaries between them and a
+// register search (shuffles) finds its own. A wave's entries are usually neighbours.
 KD_INLINE uint32_t entry_topo_wave(const uint32_t* offs, uint32_t T, uint32_t e, bool on) {
+    const int lane = threadIdx.x & 63;
     uint32_t lo_e = on ? e : 0xFFFFFFFFu, hi_e = on ? e : 0u;
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) {
@@ -408,7 +411,37 @@ KD_INLINE uint32_t entry_topo_wave(const uint32_t* offs, uint32_t T, uint32_t e,
         hi_e = b > hi_e ? b : hi_e;
     }
     if (lo_e > hi_e) return 0;                         // no lane has an entry (wave-uniform)
-    uint32_t lo = entry_topo(offs, T, lo_e), hi = entry_topo(offs, T, hi_e) + 1;   // offs[lo] <= e < offs[hi]
+    // offs[lo] <= key < offs[hi] for key = lo_e (lanes 0-31) / hi_e (lanes 32-63)
+    const uint32_t key = lane < 32 ? lo_e : hi_e, j = (uint32_t)lane & 31u;
+    uint32_t lo = 0, hi = T;
+    for (;;) {
+        const bool open = hi - lo > 1;
+        if (!__ballot(open)) break;                    // both searches done (wave-uniform)
+        const uint32_t step = (hi - lo + 31u) >> 5;
+        const uint32_t probe = lo + j * step;
+        const bool ok = open && probe < hi && offs[probe] <= key;
+        const uint64_t b = __ballot(ok);
+        const uint32_t bh = (uint32_t)(lane < 32 ? b : (b >> 32));   // this half's probes, monotone
+        if (open) {
+            const uint32_t jj = 31u - (uint32_t)__clz((int)bh);       // last probe <= key (j = 0 always is)
+            lo = lo + jj * step;
+            hi = min(hi, lo + step);
+        }
+    }
+    const uint32_t tlo = __shfl(lo, 0, 64), thi = __shfl(lo, 32, 64);   // topologies of lo_e, hi_e
+    if (thi - tlo < 64u) {
+        // boundary l: the first entry of topology tlo + 1 + l (lanes past thi: never <= e)
+        const uint32_t bnd = tlo + 1u + (uint32_t)lane <= thi ? offs[tlo + 1u + lane] : 0xFFFFFFFFu;
+        uint32_t c = 0;                                // boundaries <= e (a prefix of the lanes)
+#pragma unroll
+        for (int s = 32; s >= 1; s >>= 1) {
+            const uint32_t v = __shfl(bnd, (int)(c + (uint32_t)s - 1u), 64);
+            if (c + (uint32_t)s <= 64u && v <= e) c += (uint32_t)s;
+        }
+        return tlo + c;
+    }
+    lo = tlo;
+    hi = thi + 1;                                      // offs[lo] <= e < offs[hi]
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
         if (offs[mid] <= e) lo = mid;
