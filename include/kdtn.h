@@ -628,7 +628,19 @@ typedef struct kdtn_vni_state {
     uint32_t* net_ns;
 } kdtn_vni_state;
 int kdtn_epoch_vni_apply(kdtn_ctx* ctx, kdtn_vni_state* out);
-/* One VxlanManager op (16 B): kind 0 none, 1 Delete(vni) on node, 2 Store(vni, net_ns) on node. */
+/* Keys (node, vni) of the last kdtn_epoch_vni_apply whose result depends on the order the
+ * reference's goroutines run the epoch's map ops (one Reconcile worker and one gRPC handler
+ * goroutine per batch: no order is defined, daemon/vxlan/manager.go:57-71): a key Stored by
+ * two entries with different netns (first vs last store wins), or Stored with the very netns a
+ * reached delLink of the key compares Get(vni) against (handler.go:484-487: delete-then-store
+ * keeps it, store-then-delete removes it). The apply fixes one order (above); these keys are
+ * where a caller that needs the daemons' exact state must serialise the batches involved.
+ * n = their count; node / vni (capacity cap, NULL = count only) in the order of the key's
+ * winning store. KDTN_EINVAL before an apply of the last run. */
+int kdtn_vni_contested(kdtn_ctx* ctx, uint32_t* node, int32_t* vni, uint32_t cap, uint32_t* n);
+/* One VxlanManager op (16 B): kind 0 none, 1 Delete(vni) on node, 2 Store(vni, net_ns) on node,
+ * 3 a reached delLink whose Get(vni) missed (no effect; net_ns of a delete = the local netns
+ * its Get compares against). */
 typedef struct kdtn_vni_op { uint32_t node; int32_t vni; uint32_t net_ns; uint32_t kind; } kdtn_vni_op;
 /* This rank's ops of the last run: n_del delete slots, n_add add slots (two per AddLinks
  * entry: local node, then peer node); NULL arrays = counts only. */

@@ -93,6 +93,9 @@ struct kdtn_ctx {
     bool vres_in_r = false;
     // sharded apply: every rank's ops gathered in rank order ([dels][adds]), by RCCL or imported
     DevBuf vx_cnt, vx_send, vx_recv, vx_gops;
+    DevBuf vx_flag, vx_dkeys, vx_dused, vx_cpos, vx_cpart, vx_cnode, vx_cvni;   // order-dependent keys
+    uint32_t vx_ncont = 0;
+    bool vx_contest_ok = false;      // a vni_apply ran since the last run
     uint64_t vx_gd = 0, vx_ga = 0;
     bool vx_imported = false;
     uint32_t vres_n = 0, vres_D = 0;   // its entries; the dictionary size its ids were made for
@@ -770,7 +773,8 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->st_len, &c->st_base, &c->st_mode, &c->st_flags, &c->st_off64, &c->st_part,
                       &c->st_off32, &c->st_mask, &c->st_chg, &c->dl_topo, &c->dl_src, &c->dl_netns, &c->dl_nil,
                       &c->dl_off, &c->dl_ref, &c->dl_rec.buf, &c->stage, &c->vx_cnt, &c->vx_send, &c->vx_recv,
-                      &c->vx_gops, &c->pd_send, &c->pd_recv, &c->pd_cnt, &c->dl_rows};
+                      &c->vx_gops, &c->pd_send, &c->pd_recv, &c->pd_cnt, &c->dl_rows, &c->vx_flag,
+                      &c->vx_dkeys, &c->vx_dused, &c->vx_cpos, &c->vx_cpart, &c->vx_cnode, &c->vx_cvni};
     for (DevBuf* b : bufs) release(*b);
     for (int i = 0; i <= kMaxTimers; ++i)
         if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
@@ -1072,6 +1076,7 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
     c->fan_valid = false;
     c->rp_done = false;
     c->vx_imported = false;
+    c->vx_contest_ok = false;
     return KDTN_OK;
 }
 
@@ -1294,7 +1299,7 @@ int kdtn_epoch_encode(kdtn_ctx* c, uint64_t* n_bytes) {
         if (ne) k_wire_entry_sizes<<<nblocks(ne), BLOCK, 0, s>>>(w, c->real.view, c->des.view, wk);
         timer_mark(c, "wire_sizes");
         k_wire_scan_partial<<<nb, BLOCK, 0, s>>>(w, wk, dp<uint64_t>(c->w_part));
-        k_scan_top<<<1, BLOCK, 0, s>>>(dp<uint64_t>(c->w_part), nb);
+        k_scan_top<<<1, SCAN_TOP_BLOCK, 0, s>>>(dp<uint64_t>(c->w_part), nb);
         k_wire_scan_final<<<nb, BLOCK, 0, s>>>(w, wk, dp<uint64_t>(c->w_part));
         k_wire_batch_off<<<nblocks((uint64_t)3 * T + 1), BLOCK, 0, s>>>(w, wk);
         timer_mark(c, "wire_scan");
@@ -1365,7 +1370,7 @@ int fanout_compute(kdtn_ctx* c) {
     FanIn f{dp<uint32_t>(c->add_off), dp<uint4>(c->add_res), dp<uint2>(c->add_qdisc), c->T, na, c->f_stamp};
     TRY(run_reach(c, dp<uint32_t>(c->f_mark), c->f_stamp));
     k_fan_nodes_count<<<nbd, BLOCK, 0, s>>>(dp<uint32_t>(c->f_mark), D, c->f_stamp, dp<uint64_t>(c->f_part));
-    k_scan_top<<<1, BLOCK, 0, s>>>(dp<uint64_t>(c->f_part), nbd);
+    k_scan_top<<<1, SCAN_TOP_BLOCK, 0, s>>>(dp<uint64_t>(c->f_part), nbd);
     k_fan_nodes_write<<<nbd, BLOCK, 0, s>>>(dp<uint32_t>(c->f_mark), D, c->f_stamp, dp<uint64_t>(c->f_part),
                                            dp<uint32_t>(c->f_node_idx), dp<uint32_t>(c->f_nodes), n_nodes);
     timer_mark(c, "fanout_nodes");
@@ -1388,7 +1393,7 @@ int fanout_compute(kdtn_ctx* c) {
         const uint32_t nbc = nblocks((uint64_t)ncells + 1, SCAN_CHUNK);
         TRY(ensure(c->w_part, (size_t)nbc * 8 + 16));
         k_scan_partial<<<nbc, BLOCK, 0, s>>>(dp<uint32_t>(c->f_counts), ncells, dp<uint64_t>(c->w_part));
-        k_scan_top<<<1, BLOCK, 0, s>>>(dp<uint64_t>(c->w_part), nbc);
+        k_scan_top<<<1, SCAN_TOP_BLOCK, 0, s>>>(dp<uint64_t>(c->w_part), nbc);
         k_scan_final<<<nbc, BLOCK, 0, s>>>(dp<uint32_t>(c->f_counts), ncells, dp<uint64_t>(c->w_part),
                                            dp<uint64_t>(c->f_base));
         k_fan_scatter<<<nchunks, 64, lds, s>>>(f, dp<uint8_t>(c->f_send), dp<uint32_t>(c->f_node_idx), n_nodes,
@@ -1462,7 +1467,7 @@ int kdtn_epoch_remote_encode(kdtn_ctx* c, kdtn_remote_info* info) {
     if (na) k_remote_phys_flags<<<nblocks(na), BLOCK, 0, s>>>(dp<uint8_t>(c->f_send), dp<uint4>(c->add_res), na,
                                                               dp<uint32_t>(c->rp_flag));
     k_scan_partial<<<nbp, BLOCK, 0, s>>>(dp<uint32_t>(c->rp_flag), na, dp<uint64_t>(c->rp_part));
-    k_scan_top<<<1, BLOCK, 0, s>>>(dp<uint64_t>(c->rp_part), nbp);
+    k_scan_top<<<1, SCAN_TOP_BLOCK, 0, s>>>(dp<uint64_t>(c->rp_part), nbp);
     k_scan_final<<<nbp, BLOCK, 0, s>>>(dp<uint32_t>(c->rp_flag), na, dp<uint64_t>(c->rp_part), dp<uint64_t>(c->rp_pos));
     if (na) k_remote_phys_scatter<<<nblocks(na), BLOCK, 0, s>>>(dp<uint32_t>(c->rp_flag), dp<uint64_t>(c->rp_pos), na,
                                                                 dp<uint32_t>(c->rp_phys));
@@ -1516,11 +1521,11 @@ int kdtn_epoch_remote_encode(kdtn_ctx* c, kdtn_remote_info* info) {
                                                         dp<uint32_t>(c->rp_msz), dp<uint32_t>(c->rp_tsz));
     }
     k_scan_partial<<<nbm, BLOCK, 0, s>>>(dp<uint32_t>(c->rp_msz), (uint32_t)n, dp<uint64_t>(c->rp_part));
-    k_scan_top<<<1, BLOCK, 0, s>>>(dp<uint64_t>(c->rp_part), nbm);
+    k_scan_top<<<1, SCAN_TOP_BLOCK, 0, s>>>(dp<uint64_t>(c->rp_part), nbm);
     k_scan_final<<<nbm, BLOCK, 0, s>>>(dp<uint32_t>(c->rp_msz), (uint32_t)n, dp<uint64_t>(c->rp_part),
                                        dp<uint64_t>(c->rp_moff));
     k_scan_partial<<<nbm, BLOCK, 0, s>>>(dp<uint32_t>(c->rp_tsz), (uint32_t)n, dp<uint64_t>(c->w_part));
-    k_scan_top<<<1, BLOCK, 0, s>>>(dp<uint64_t>(c->w_part), nbm);
+    k_scan_top<<<1, SCAN_TOP_BLOCK, 0, s>>>(dp<uint64_t>(c->w_part), nbm);
     k_scan_final<<<nbm, BLOCK, 0, s>>>(dp<uint32_t>(c->rp_tsz), (uint32_t)n, dp<uint64_t>(c->w_part),
                                        dp<uint64_t>(c->rp_toff));
     timer_mark(c, "remote_sizes");
@@ -1599,7 +1604,7 @@ int kdtn_epoch_tc(kdtn_ctx* c, uint64_t* n_bytes) {
            dp<uint32_t>(c->kd_offs), na, nu};
     if (n) k_tc_sizes<<<nblocks(n), BLOCK, 0, s>>>(w, dp<uint32_t>(c->tc_size));
     k_scan_partial<<<nb, BLOCK, 0, s>>>(dp<uint32_t>(c->tc_size), (uint32_t)n, dp<uint64_t>(c->tc_part));
-    k_scan_top<<<1, BLOCK, 0, s>>>(dp<uint64_t>(c->tc_part), nb);
+    k_scan_top<<<1, SCAN_TOP_BLOCK, 0, s>>>(dp<uint64_t>(c->tc_part), nb);
     k_scan_final<<<nb, BLOCK, 0, s>>>(dp<uint32_t>(c->tc_size), (uint32_t)n, dp<uint64_t>(c->tc_part),
                                       dp<uint64_t>(c->tc_off));
     timer_mark(c, "tc_sizes");
@@ -1645,7 +1650,7 @@ int scan_u32(kdtn_ctx* c, const uint32_t* in, uint32_t n, uint64_t* out) {
     TRY(ensure(c->j_part, (size_t)nb * 8));
     hipStream_t s = c->stream;
     k_scan_partial<<<nb, BLOCK, 0, s>>>(in, n, dp<uint64_t>(c->j_part));
-    k_scan_top<<<1, BLOCK, 0, s>>>(dp<uint64_t>(c->j_part), nb);
+    k_scan_top<<<1, SCAN_TOP_BLOCK, 0, s>>>(dp<uint64_t>(c->j_part), nb);
     k_scan_final<<<nb, BLOCK, 0, s>>>(in, n, dp<uint64_t>(c->j_part), out);
     return KDTN_OK;
 }
@@ -2447,16 +2452,45 @@ int kdtn_epoch_vni_apply(kdtn_ctx* c, kdtn_vni_state* out) {
         uint8_t* vis = dp<uint8_t>(c->vx_vis);
         k_vni_vis_count<<<nb, BLOCK, 0, s>>>(aops, (uint32_t)n_ops, ents, dead, V, slots, mask, vis,
                                             dp<uint64_t>(c->vx_part));
-        k_scan_top<<<1, BLOCK, 0, s>>>(dp<uint64_t>(c->vx_part), nb);
+        k_scan_top<<<1, SCAN_TOP_BLOCK, 0, s>>>(dp<uint64_t>(c->vx_part), nb);
         k_vni_vis_write<<<nb, BLOCK, 0, s>>>(aops, (uint32_t)n_ops, ents, dead, V, vis, dp<uint64_t>(c->vx_part),
                                             dp<uint32_t>(c->vx_node), dp<int32_t>(c->vx_vni), dp<uint32_t>(c->vx_netns),
                                             n_out);
     }
     HIP_TRY(hipGetLastError());
     timer_mark(c, "vni_map");
+    // keys whose result depends on the reference's goroutine order (kdtn_vni_contested)
+    const uint32_t dmask = nd_all ? next_pow2(nd_all * 2) - 1 : 0u;
+    const uint32_t nbf = nblocks(n_ops + 1, SCAN_CHUNK);
+    TRY(ensure(c->vx_flag, (size_t)n_ops * 4 + 16));
+    TRY(ensure(c->vx_dkeys, ((size_t)dmask + 1) * 16));
+    TRY(ensure(c->vx_dused, ((size_t)dmask + 1) * 4));
+    TRY(ensure(c->vx_cpos, ((size_t)n_ops + 1) * 8));
+    TRY(ensure(c->vx_cpart, (size_t)nbf * 8 + 8));
+    TRY(ensure(c->vx_cnode, (size_t)n_ops * 4 + 16));
+    TRY(ensure(c->vx_cvni, (size_t)n_ops * 4 + 16));
+    HIP_TRY(hipMemsetAsync(c->vx_flag.p, 0, (size_t)n_ops * 4 + 16, s));
+    HIP_TRY(hipMemsetAsync(c->vx_dused.p, 0, ((size_t)dmask + 1) * 4, s));
+    if (nd_all) k_vni_dtab_insert<<<nblocks(nd_all), BLOCK, 0, s>>>(ops, (uint32_t)nd_all, dp<uint4>(c->vx_dkeys),
+                                                                     dp<uint32_t>(c->vx_dused), dmask);
+    if (n_ops) k_vni_contest<<<nblocks(n_ops), BLOCK, 0, s>>>(aops, (uint32_t)n_ops, ents, dead, slots, mask,
+                                                             dp<uint4>(c->vx_dkeys), dp<uint32_t>(c->vx_dused),
+                                                             nd_all ? dmask : 0u, dp<uint32_t>(c->vx_flag));
+    k_scan_partial<<<nbf, BLOCK, 0, s>>>(dp<uint32_t>(c->vx_flag), (uint32_t)n_ops, dp<uint64_t>(c->vx_cpart));
+    k_scan_top<<<1, SCAN_TOP_BLOCK, 0, s>>>(dp<uint64_t>(c->vx_cpart), nbf);
+    k_scan_final<<<nbf, BLOCK, 0, s>>>(dp<uint32_t>(c->vx_flag), (uint32_t)n_ops, dp<uint64_t>(c->vx_cpart),
+                                       dp<uint64_t>(c->vx_cpos));
+    if (n_ops) k_vni_contest_write<<<nblocks(n_ops), BLOCK, 0, s>>>(aops, dp<uint32_t>(c->vx_flag),
+                                                                   dp<uint64_t>(c->vx_cpos), (uint32_t)n_ops,
+                                                                   dp<uint32_t>(c->vx_cnode), dp<int32_t>(c->vx_cvni));
+    HIP_TRY(hipGetLastError());
+    timer_mark(c, "vni_contested");
     HIP_TRY(hipMemcpyAsync(c->h_misc + 5, n_out, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(c->h_misc + 6, dp<uint64_t>(c->vx_cpos) + n_ops, 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     const uint32_t n = c->h_misc[5];
+    c->vx_ncont = c->h_misc[6];
+    c->vx_contest_ok = true;
     // the new map becomes the resident one (the next upload's KDTN_VNI_RESIDENT); this upload's
     // snapshot (v_*, v_ents, V) stays as it is, so a re-run or a second apply of this upload
     // sees the same epoch-start map
@@ -2468,6 +2502,20 @@ int kdtn_epoch_vni_apply(kdtn_ctx* c, kdtn_vni_state* out) {
     c->vres_n = n;
     c->vres_D = c->D;
     return out ? kdtn_vni_download(c, out) : KDTN_OK;
+}
+
+int kdtn_vni_contested(kdtn_ctx* c, uint32_t* node, int32_t* vni, uint32_t cap, uint32_t* n) {
+    if (!c || !n || !c->vx_contest_ok) return KDTN_EINVAL;
+    HIP_TRY(hipSetDevice(c->device));
+    *n = c->vx_ncont;
+    if (!node && !vni) return KDTN_OK;
+    if (c->vx_ncont > cap) return KDTN_ENOSPC;
+    hipStream_t s = c->stream;
+    if (c->vx_ncont && node)
+        HIP_TRY(hipMemcpyAsync(node, c->vx_cnode.p, (size_t)c->vx_ncont * 4, hipMemcpyDeviceToHost, s));
+    if (c->vx_ncont && vni) HIP_TRY(hipMemcpyAsync(vni, c->vx_cvni.p, (size_t)c->vx_ncont * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return KDTN_OK;
 }
 
 int kdtn_vni_download(kdtn_ctx* c, kdtn_vni_state* out) {
@@ -2525,7 +2573,7 @@ int plan_offsets(kdtn_ctx* c, uint32_t T, uint64_t* total) {
     TRY(ensure(c->st_part, (size_t)nb * 8 + 16));
     TRY(ensure(c->st_off32, ((size_t)T + 1) * 4));
     k_scan_partial<<<nb, BLOCK, 0, s>>>(dp<uint32_t>(c->st_len), T, dp<uint64_t>(c->st_part));
-    k_scan_top<<<1, BLOCK, 0, s>>>(dp<uint64_t>(c->st_part), nb);
+    k_scan_top<<<1, SCAN_TOP_BLOCK, 0, s>>>(dp<uint64_t>(c->st_part), nb);
     k_scan_final<<<nb, BLOCK, 0, s>>>(dp<uint32_t>(c->st_len), T, dp<uint64_t>(c->st_part), dp<uint64_t>(c->st_off64));
     k_off_narrow<<<nblocks((uint64_t)T + 1), BLOCK, 0, s>>>(dp<uint64_t>(c->st_off64), T, dp<uint32_t>(c->st_off32));
     HIP_TRY(hipGetLastError());

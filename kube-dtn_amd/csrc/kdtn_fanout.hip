@@ -121,8 +121,20 @@ __global__ void __launch_bounds__(64) k_fan_count(FanIn f, const uint8_t* send, 
     for (uint32_t k = threadIdx.x; k < nn; k += 64) h[k] = 0;
     __syncthreads();
     const uint32_t c = blockIdx.x, e0 = c * FAN_CHUNK, e1 = min(e0 + FAN_CHUNK, f.n_add);
-    for (uint32_t e = e0 + threadIdx.x; e < e1; e += 64)
-        if (send[e] & REACH_SEND) atomicAdd(&h[node_idx[f.add_res[e].z]], 1u);
+    // every round's loads first (two dependent levels for the chunk instead of per round)
+    constexpr int RND = FAN_CHUNK / 64;
+    uint32_t z[RND];
+#pragma unroll
+    for (int r = 0; r < RND; ++r) {
+        const uint32_t e = e0 + r * 64 + threadIdx.x;
+        z[r] = (e < e1 && (send[e] & REACH_SEND)) ? f.add_res[e].z : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int r = 0; r < RND; ++r)
+        if (z[r] != 0xFFFFFFFFu) z[r] = node_idx[z[r]];
+#pragma unroll
+    for (int r = 0; r < RND; ++r)
+        if (z[r] != 0xFFFFFFFFu) atomicAdd(&h[z[r]], 1u);
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < nn; k += 64) counts[(size_t)k * nchunks + c] = h[k];
 }
@@ -143,10 +155,21 @@ __global__ void __launch_bounds__(64) k_fan_scatter(FanIn f, const uint8_t* send
     const int lane = threadIdx.x;
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     const int nbits = nn > 1 ? 32 - __clz((int)(nn - 1)) : 0;
-    for (uint32_t r = e0; r < e1; r += 64) {
-        const uint32_t e = r + lane;
-        const bool on = e < e1 && (send[e] & REACH_SEND);
-        const uint32_t node = on ? node_idx[f.add_res[e].z] : 0u;
+    constexpr int RND = FAN_CHUNK / 64;
+    uint32_t z[RND];                                         // every round's node first
+#pragma unroll
+    for (int q = 0; q < RND; ++q) {
+        const uint32_t e = e0 + q * 64 + lane;
+        z[q] = (e < e1 && (send[e] & REACH_SEND)) ? f.add_res[e].z : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int q = 0; q < RND; ++q)
+        if (z[q] != 0xFFFFFFFFu) z[q] = node_idx[z[q]];
+#pragma unroll
+    for (int q = 0; q < RND; ++q) {
+        const uint32_t e = e0 + q * 64 + lane;
+        const bool on = z[q] != 0xFFFFFFFFu;
+        const uint32_t node = on ? z[q] : 0u;
         const uint64_t act = __ballot(on);
         if (!act) continue;                                  // wave-uniform
         uint64_t same = act;

@@ -251,16 +251,18 @@ __global__ void k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, Re
 
 // ---- wire encoding of the batches (kdtn_wire.hip) --------------------------------------
 constexpr int SCAN_CHUNK = BLOCK * 4;   // values per block of the batch-offset scan
+constexpr int SCAN_TOP_BLOCK = 1024, SCAN_TOP_PER = 16;   // k_scan_top: one block, totals per thread
 constexpr int WIRE_IMG = 8192;          // LDS bytes per wave for a wave's wire output (32 KB per
                                         // block: 5 blocks per CU; a longer wave range stores directly)
 // string table of a dictionary for the encoders: {arena offset, length | STR_BAD} per string,
 // STR_BAD = not valid UTF-8 — one 8-B gather gives everything a string field needs
 constexpr uint32_t STR_BAD = 0x80000000u;
+typedef uint2 SRef;   // {arena offset, length | STR_BAD}
 struct WireIn {
     const uint8_t* kd_bytes;
-    const uint2* kd_tab;
+    const SRef* kd_tab;
     const uint8_t* pd_bytes;
-    const uint2* pd_tab;
+    const SRef* pd_tab;
     const uint32_t* t_name;
     const uint32_t* t_src;
     const uint32_t* t_netns;
@@ -321,9 +323,9 @@ __global__ void k_store_assemble(const uint32_t* off, uint32_t nt, const uint32_
 struct RemoteIn {
     const uint8_t* kd_bytes;
     const uint32_t* kd_offs;
-    const uint2* kd_tab;
+    const SRef* kd_tab;
     const uint8_t* pd_bytes;
-    const uint2* pd_tab;
+    const SRef* pd_tab;
     const uint32_t* t_ns;
     const uint32_t* t_src;
     const uint32_t* t_netns;
@@ -482,8 +484,10 @@ struct VniOpsIn {
     uint32_t n_del, n_add;
 };
 // one op per del entry (slot e) and two per add entry (slots n_del + 2e, + 1):
-// {node, vni, net_ns, kind} with kind VOP_NONE / VOP_DEL / VOP_ADD
-enum : uint32_t { VOP_NONE = 0, VOP_DEL = 1, VOP_ADD = 2 };
+// {node, vni, net_ns, kind} with kind VOP_NONE / VOP_DEL / VOP_ADD / VOP_DEL_MISS (a reached
+// delLink whose Get(vni) missed the snapshot: no effect on the map, kept for the order check);
+// net_ns of a delete = the local pod's netns its Get compares against
+enum : uint32_t { VOP_NONE = 0, VOP_DEL = 1, VOP_ADD = 2, VOP_DEL_MISS = 3 };
 __global__ void k_vni_cuts(VniOpsIn f, uint32_t* cut);
 __global__ void k_vni_ops(VniOpsIn f, const uint32_t* cut, uint4* ops);
 __global__ void k_vni_shadow(const uint4* ents, uint32_t n_ents, const uint32_t* slots, uint32_t mask, uint8_t* dead);
@@ -496,6 +500,13 @@ __global__ void k_vni_vis_count(const uint4* add_ops, uint32_t n_ops, const uint
 __global__ void k_vni_vis_write(const uint4* add_ops, uint32_t n_ops, const uint4* ents, const uint8_t* dead,
                                 uint32_t n_ents, const uint8_t* vis, const uint64_t* part, uint32_t* node,
                                 int32_t* vni, uint32_t* net_ns, uint32_t* n_out);
+// order-dependent keys (kdtn_vni_contested)
+__global__ void k_vni_dtab_insert(const uint4* dels, uint32_t n_del, uint4* dkeys, uint32_t* dused, uint32_t dmask);
+__global__ void k_vni_contest(const uint4* add_ops, uint32_t n_ops, const uint4* ents, const uint8_t* dead,
+                              const uint32_t* slots, uint32_t mask, const uint4* dkeys, const uint32_t* dused,
+                              uint32_t dmask, uint32_t* flag);
+__global__ void k_vni_contest_write(const uint4* add_ops, const uint32_t* flag, const uint64_t* pos, uint32_t n_ops,
+                                    uint32_t* node, int32_t* vni);
 __global__ void k_fan_nodes_count(const uint32_t* mark, uint32_t nd, uint32_t stamp, uint64_t* part);
 __global__ void k_fan_nodes_write(const uint32_t* mark, uint32_t nd, uint32_t stamp, const uint64_t* part,
                                   uint32_t* node_idx, uint32_t* nodes, uint32_t* n_nodes);

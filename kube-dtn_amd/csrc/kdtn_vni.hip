@@ -9,6 +9,13 @@
 // Deterministic order (the reference's is goroutine order): every delete first, then every
 // add; per key the first add in (topology, add-list, local-before-remote) order wins.
 //
+// Order dependence (kdtn_vni_contested): a key's result depends on the goroutine order when
+// two entries Store different netns values under it, or when an entry Stores exactly the netns
+// a reached delLink of the same key compares Get(vni) against (delete-then-store keeps it,
+// store-then-delete removes it). k_vni_dtab_insert puts every reached delete {node, vni,
+// netns} in a table, k_vni_contest flags the winning add of each such key, and the flags are
+// compacted in the winners' order.
+//
 // Kernels: k_vni_cuts / k_vni_ops (entry-parallel: where each topology's RPC sequence stops,
 // then one op slot per del entry and two per add entry), k_vni_shadow / k_vni_del (snapshot entries that are not,
 // or no longer, in the map: shadowed duplicates, deleted keys), then the
@@ -50,8 +57,8 @@ __global__ void __launch_bounds__(BLOCK) k_vni_ops(VniOpsIn f, const uint32_t* c
         const uint32_t t = td;
         const uint4 r = f.r.del_res[x];
         uint4 op = none;
-        if (x < cut[2 * t] && ((r.w >> 16) & 0xFFu))                       // vni_hit :484-487
-            op = make_uint4(f.t_src[t], r.y, 0u, VOP_DEL);
+        if (x < cut[2 * t])                                                  // reached; vni_hit :484-487
+            op = make_uint4(f.t_src[t], r.y, f.t_netns[t], ((r.w >> 16) & 0xFFu) ? VOP_DEL : VOP_DEL_MISS);
         ops[x] = op;
     } else if (x < f.n_del + f.n_add) {
         const uint32_t e = x - f.n_del;
@@ -191,6 +198,69 @@ __global__ void __launch_bounds__(BLOCK) k_vni_vis_write(const uint4* add_ops, u
             ++x;
         }
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *n_out = (uint32_t)(part[blockIdx.x] + tot);
+}
+
+// every reached delete (hit or miss) as a key {node, vni, netns} (duplicates allowed)
+__global__ void __launch_bounds__(BLOCK) k_vni_dtab_insert(const uint4* dels, uint32_t n_del, uint4* dkeys,
+                                                           uint32_t* dused, uint32_t dmask) {
+    const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= n_del) return;
+    const uint4 d = dels[j];
+    if (d.w != VOP_DEL && d.w != VOP_DEL_MISS) return;
+    for (uint32_t h = (uint32_t)hash64(((uint64_t)d.x << 32) ^ ((uint64_t)d.y << 16) ^ d.z) & dmask;;
+         h = (h + 1) & dmask) {
+        if (atomicCAS(&dused[h], 0u, 1u) == 0u) {
+            dkeys[h] = make_uint4(d.x, d.y, d.z, 0u);
+            return;
+        }
+    }
+}
+
+KD_INLINE bool dtab_has(const uint4* dkeys, const uint32_t* dused, uint32_t dmask, uint32_t node, uint32_t vni,
+                        uint32_t netns) {
+    if (dmask == 0) return false;
+    for (uint32_t h = (uint32_t)hash64(((uint64_t)node << 32) ^ ((uint64_t)vni << 16) ^ netns) & dmask;;
+         h = (h + 1) & dmask) {
+        if (!dused[h]) return false;
+        const uint4 k = dkeys[h];
+        if (k.x == node && k.y == vni && k.z == netns) return true;
+    }
+}
+
+// One thread per add op: flag the winning add of its key when this op stores another netns
+// than the winner, or stores the netns a reached delete of the key compares against.
+__global__ void __launch_bounds__(BLOCK) k_vni_contest(const uint4* add_ops, uint32_t n_ops, const uint4* ents,
+                                                       const uint8_t* dead, const uint32_t* slots, uint32_t mask,
+                                                       const uint4* dkeys, const uint32_t* dused, uint32_t dmask,
+                                                       uint32_t* flag) {
+    const uint32_t x = blockIdx.x * BLOCK + threadIdx.x;
+    if (x >= n_ops) return;
+    const uint4 op = add_ops[x];
+    if (op.w != VOP_ADD) return;
+    uint32_t w = 0xFFFFFFFFu;                          // the key's winner (an add op: adds come first)
+    for (uint32_t h = vni_home(op.x, op.y, mask);; h = (h + 1) & mask) {
+        const uint32_t sl = slots[h];
+        if (sl == 0xFFFFFFFFu) break;
+        uint4 o;
+        ext_entry(add_ops, n_ops, ents, dead, sl, &o);
+        if (o.x == op.x && o.y == op.y) {
+            w = sl;
+            break;
+        }
+    }
+    if (w >= n_ops) return;                            // (cannot happen: x itself was inserted)
+    const bool other = w != x && add_ops[w].z != op.z;
+    if (other || dtab_has(dkeys, dused, dmask, op.x, op.y, op.z)) flag[w] = 1u;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_vni_contest_write(const uint4* add_ops, const uint32_t* flag,
+                                                             const uint64_t* pos, uint32_t n_ops, uint32_t* node,
+                                                             int32_t* vni) {
+    const uint32_t x = blockIdx.x * BLOCK + threadIdx.x;
+    if (x >= n_ops || !flag[x]) return;
+    const uint4 op = add_ops[x];
+    node[pos[x]] = op.x;
+    vni[pos[x]] = (int32_t)op.y;
 }
 
 }  // namespace kdtn

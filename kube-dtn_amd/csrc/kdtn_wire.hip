@@ -28,6 +28,7 @@
 
 namespace kdtn {
 
+
 // ---- dictionary UTF-8 validity (Go unicode/utf8.ValidString) ---------------------------
 KD_INLINE bool utf8_ok(const uint8_t* s, uint32_t n) {
     uint32_t i = 0;
@@ -71,7 +72,10 @@ __global__ void __launch_bounds__(BLOCK) k_utf8_bits(const uint8_t* bytes, const
 
 // {offset, length | STR_BAD} per dictionary string (the encoders' one gather per string field).
 // The high-bit test reads the string's first 32 bytes as one 16-B load pair (+ a dword)
-// instead of byte by byte; only strings with a byte >= 0x80 run the UTF-8 automaton.
+// instead of byte by byte; only strings with a byte >= 0x80 run the UTF-8 automaton. (16-B
+// entries holding strings of <= 12 bytes inline measured slower: wire_write 1.83 vs 1.77 ms,
+// sizes 0.72 vs 0.63 ms — the table doubles and the writer loses a wave per SIMD,
+// profiles/r03k_stages.json.)
 __global__ void __launch_bounds__(BLOCK) k_str_table(const uint8_t* bytes, const uint32_t* offs, uint32_t n,
                                                      uint2* tab) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
@@ -109,22 +113,28 @@ KD_INLINE uint32_t vlen(uint64_t v) {
 }
 KD_INLINE uint32_t str_field(uint32_t len) { return len ? 1u + vlen(len) + len : 0u; }
 KD_INLINE bool bit(const uint32_t* bits, uint32_t id) { return (bits[id >> 5] >> (id & 31)) & 1u; }
-KD_INLINE uint32_t slen(uint2 r) { return r.y & ~STR_BAD; }
-// string-table entry of id (id 0 = "": no gather)
-KD_INLINE uint2 sref(const uint2* tab, uint32_t id) { return id ? tab[id] : make_uint2(0u, 0u); }
+KD_INLINE uint32_t slen(SRef r) { return r.y & ~STR_BAD; }
+// string-table entry of id (id 0 = "": no gather); FULL = false: the length word only (sizes)
+template <bool FULL = true>
+KD_INLINE SRef sref(const SRef* tab, uint32_t id) {
+    if (!id) return make_uint2(0u, 0u);
+    if constexpr (FULL) return tab[id];
+    else return make_uint2(0u, reinterpret_cast<const uint32_t*>(tab)[2 * (size_t)id + 1]);
+}
 
-// the arena ranges of one Link record's 7 key and 12 property strings, gathered at once
+// the table entries of one Link record's 7 key and 12 property strings, gathered at once
 struct LinkRefs {
-    uint2 k[KDTN_NKEY], p[KDTN_NPROP];
+    SRef k[KDTN_NKEY], p[KDTN_NPROP];
     uint32_t gap;
     int64_t uid;
 };
-KD_INLINE LinkRefs link_refs(const uint2* kd_tab, const uint2* pd_tab, const DevLinks& L, uint32_t j) {
+template <bool FULL = true>
+KD_INLINE LinkRefs link_refs(const SRef* kd_tab, const SRef* pd_tab, const DevLinks& L, uint32_t j) {
     LinkRefs r;
 #pragma unroll
-    for (int k = 0; k < KDTN_NKEY; ++k) r.k[k] = sref(kd_tab, L.key(k, j));
+    for (int k = 0; k < KDTN_NKEY; ++k) r.k[k] = sref<FULL>(kd_tab, L.key(k, j));
 #pragma unroll
-    for (int k = 0; k < KDTN_NPROP; ++k) r.p[k] = sref(pd_tab, L.prop(k, j));
+    for (int k = 0; k < KDTN_NPROP; ++k) r.p[k] = sref<FULL>(pd_tab, L.prop(k, j));
     r.gap = L.gap(j);
     r.uid = L.uid(j);
     return r;
@@ -155,7 +165,7 @@ KD_INLINE uint32_t pod_size(const WireIn& w, uint32_t t, bool* ok) {
     uint32_t s = 0, bad = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const uint2 r = sref(w.kd_tab, ids[k]);
+        const SRef r = sref<false>(w.kd_tab, ids[k]);
         s += str_field(slen(r));
         bad |= r.y;
     }
@@ -186,7 +196,7 @@ __global__ void __launch_bounds__(BLOCK) k_wire_entry_sizes(WireIn w, DevLinks O
         }
     if (!on) return;
     uint32_t psz, lsz;
-    bool ok = link_sizes(link_refs(w.kd_tab, w.pd_tab, lst == 0 ? O : N, w.list_idx[lst][e]), &psz, &lsz);
+    bool ok = link_sizes(link_refs<false>(w.kd_tab, w.pd_tab, lst == 0 ? O : N, w.list_idx[lst][e]), &psz, &lsz);
     uint32_t size = 1u + vlen(lsz) + lsz;
     if (e == w.list_off[lst][t]) {                         // the batch's first entry carries the header
         bool pok;
@@ -263,16 +273,42 @@ __global__ void __launch_bounds__(BLOCK) k_scan_partial(const uint32_t* size, ui
     if (threadIdx.x == 0) part[blockIdx.x] = tot;
 }
 
-// single block: exclusive scan of the block totals in place
-__global__ void __launch_bounds__(BLOCK) k_scan_top(uint64_t* part, uint32_t nb) {
-    __shared__ uint64_t sh[BLOCK / 64];
+// single block: exclusive scan of the block totals in place. 1024 threads x 16 consecutive
+// totals each per pass, so the usual few-thousand totals take one pass (a 256-thread loop of
+// one total per thread took ~40 dependent passes, ~0.1 ms, for 10M entries)
+__global__ void __launch_bounds__(SCAN_TOP_BLOCK) k_scan_top(uint64_t* part, uint32_t nb) {
+    __shared__ uint64_t wsum[SCAN_TOP_BLOCK / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint64_t carry = 0;
-    for (uint32_t c = 0; c < nb; c += BLOCK) {
-        const uint32_t i = c + threadIdx.x;
-        const uint64_t v = i < nb ? part[i] : 0u;
-        uint64_t tot;
-        const uint64_t ex = block_exclusive(v, sh, &tot);
-        if (i < nb) part[i] = carry + ex;
+    for (uint32_t c0 = 0; c0 < nb; c0 += SCAN_TOP_BLOCK * SCAN_TOP_PER) {
+        const uint32_t b = c0 + (uint32_t)tid * SCAN_TOP_PER;
+        uint64_t v[SCAN_TOP_PER], sum = 0;
+#pragma unroll
+        for (int k = 0; k < SCAN_TOP_PER; ++k) {
+            v[k] = b + k < nb ? part[b + k] : 0ull;
+            sum += v[k];
+        }
+        uint64_t x = sum;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t o = __shfl_up(x, d, 64);
+            if (lane >= d) x += o;
+        }
+        if (lane == 63) wsum[wave] = x;
+        __syncthreads();
+        uint64_t base = carry, tot = 0;
+#pragma unroll
+        for (int w = 0; w < SCAN_TOP_BLOCK / 64; ++w) {
+            if (w < wave) base += wsum[w];
+            tot += wsum[w];
+        }
+        __syncthreads();
+        uint64_t run = base + x - sum;
+#pragma unroll
+        for (int k = 0; k < SCAN_TOP_PER; ++k) {
+            if (b + k < nb) part[b + k] = run;
+            run += v[k];
+        }
         carry += tot;
     }
 }
@@ -299,7 +335,7 @@ __global__ void __launch_bounds__(BLOCK) k_scan_final(const uint32_t* size, uint
 
 // ---- writer --------------------------------------------------------------------------------
 // string field: tag, length, bytes
-KD_INLINE void str_field_out(WSink& o, uint32_t field, const uint8_t* arena, uint2 r) {
+KD_INLINE void str_field_out(WSink& o, uint32_t field, const uint8_t* arena, SRef r) {
     const uint32_t len = slen(r);
     if (!len) return;
     if (len < 0x80u) {
@@ -407,7 +443,7 @@ __global__ void __launch_bounds__(BLOCK) k_remote_phys_scatter(const uint32_t* f
 // the strings of message m as arena ranges, in field order net_ns, intf_name, intf_ip,
 // peer_vtep, kube_ns, name, and the link's properties
 struct RemoteMsg {
-    uint2 s[6], p[KDTN_NPROP];
+    SRef s[6], p[KDTN_NPROP];
     uint32_t gap;
     int32_t vni;
     bool ok;                        // every string valid UTF-8
@@ -415,6 +451,7 @@ struct RemoteMsg {
 
 // the strings of add entry e's message (remote: the UpdateRemote payload, else the physical
 // peer's local Update payload); t = the entry's topology
+template <bool FULL = true>
 KD_INLINE RemoteMsg remote_msg(const RemoteIn& r, uint32_t e, uint32_t t, bool remote) {
     RemoteMsg q;
     const uint32_t j = r.add_idx[e];
@@ -437,15 +474,15 @@ KD_INLINE RemoteMsg remote_msg(const RemoteIn& r, uint32_t e, uint32_t t, bool r
     uint32_t bad = 0;
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
-        q.s[k] = sref(r.kd_tab, id[k]);
+        q.s[k] = sref<FULL>(r.kd_tab, id[k]);
         bad |= q.s[k].y;
     }
 #pragma unroll
     for (int k = 0; k < KDTN_NPROP; ++k) {
-        q.p[k] = sref(r.pd_tab, r.N.prop(k, j));
+        q.p[k] = sref<FULL>(r.pd_tab, r.N.prop(k, j));
         bad |= q.p[k].y;
     }
-    if (!remote) {
+    if (!remote) {                                  // TrimPrefix(PeerPod, "physical/")
         q.s[3].x += 9u;
         q.s[3].y -= 9u;
     }
@@ -475,7 +512,7 @@ __global__ void __launch_bounds__(BLOCK) k_remote_entry_sizes(RemoteIn r, uint32
     if (__ballot(kind != 0) == 0) return;           // wave-uniform
     const uint32_t t = entry_topo_wave(r.add_off, r.T, e, kind != 0);
     if (!kind) return;
-    const RemoteMsg q = remote_msg(r, e, t, kind == 1);
+    const RemoteMsg q = remote_msg<false>(r, e, t, kind == 1);
     uint32_t psz;
     const uint32_t body = remote_body_size(q, &psz);
     msz_e[e] = q.ok ? vlen(body) + body : 0u;

@@ -76,6 +76,7 @@ def lib() -> C.CDLL:
         "kdtn_comm_init": (C.c_int, [vp, C.POINTER(C.c_uint8 * 128), C.c_int, C.c_int]),
         "kdtn_set_timing": (C.c_int, [vp, C.c_int]),
         "kdtn_epoch_vni_apply": (C.c_int, [vp, C.POINTER(abi.VniState)]),
+        "kdtn_vni_contested": (C.c_int, [vp, vp, vp, C.c_uint32, C.POINTER(C.c_uint32)]),
         "kdtn_vni_download": (C.c_int, [vp, C.POINTER(abi.VniState)]),
         "kdtn_last_kernel_times": (C.c_int, [vp, C.POINTER(C.c_char_p), C.POINTER(C.c_float), C.c_int]),
         "kdtn_debug_wg_trace": (C.c_int, [vp, C.POINTER(C.c_uint64), C.c_uint32]),
@@ -477,6 +478,17 @@ class Engine:
         entries; the result also becomes the engine's resident map (Vnis.keep_resident())."""
         _check(lib().kdtn_epoch_vni_apply(self._ctx, None), "kdtn_epoch_vni_apply")
         return self.vni_download()
+
+    def vni_contested(self):
+        """kdtn_vni_contested: (node, vni) keys of the last vni_apply whose result depends on the
+        reference's goroutine order, in the order of each key's winning store."""
+        n = C.c_uint32()
+        _check(lib().kdtn_vni_contested(self._ctx, None, None, 0, C.byref(n)), "kdtn_vni_contested")
+        node = np.zeros(max(n.value, 1), np.uint32)
+        vni = np.zeros(max(n.value, 1), np.int32)
+        _check(lib().kdtn_vni_contested(self._ctx, node.ctypes.data, vni.ctypes.data, node.size, C.byref(n)),
+               "kdtn_vni_contested")
+        return node[:n.value], vni[:n.value]
 
     def vni_ops_export(self):
         """This rank's VxlanManager ops of the last run (kdtn_vni_ops_export): (dels, adds) as

@@ -561,3 +561,87 @@ uint32_t or_vni_apply(const kdtn_batches* b, uint32_t T, const uint32_t* t_src, 
     free(snapm.key); free(snapm.val); free(addm.key); free(addm.val); free(gone); free(an); free(av); free(as);
     return n;
 }
+
+/* ======================================================================================
+ * Keys whose VxlanManager result depends on the goroutine order (kdtn_vni_contested): over
+ * the same reached entries and add order as or_vni_apply, a key is contested when two of its
+ * Stores carry different netns (first vs last store wins), or when a Store carries the netns a
+ * reached delLink of the key compares Get(vni) against (daemon/kubedtn/handler.go:484-487:
+ * delete-then-store keeps the entry, store-then-delete removes it). Output: the contested keys
+ * in the order of their first (winning) store.
+ * ==================================================================================== */
+typedef struct { uint32_t node, vni, netns, used; } dkey;
+static uint64_t dhash(uint32_t node, uint32_t vni, uint32_t netns) {
+    return (((uint64_t)node << 32) ^ ((uint64_t)vni << 16) ^ netns) * 0x9E3779B97F4A7C15ull;
+}
+
+uint32_t or_vni_contested(const kdtn_batches* b, uint32_t T, const uint32_t* t_src, const uint32_t* t_netns,
+                          const uint32_t* pod_netns, uint32_t* out_node, int32_t* out_vni) {
+    const uint32_t nd = b->del_off[T], na = b->add_off[T];
+    uint64_t dcap = 64;
+    while (dcap < 2ull * nd + 2) dcap <<= 1;
+    dkey* dels = calloc(dcap, sizeof(dkey));                          /* reached deletes {node, vni, netns} */
+    uint64_t acap = 64;
+    while (acap < 4ull * na + 2) acap <<= 1;
+    vmap addm = {calloc(acap, 8), malloc(acap * 4), (uint32_t)acap - 1};   /* key → winning store */
+    memset(addm.val, 0xFF, acap * 4);
+    uint32_t* an = malloc(sizeof(uint32_t) * (2 * na + 1));
+    int32_t* av = malloc(sizeof(int32_t) * (2 * na + 1));
+    uint32_t* as = malloc(sizeof(uint32_t) * (2 * na + 1));
+    uint32_t* aw = malloc(sizeof(uint32_t) * (2 * na + 1));          /* each store's winner */
+    uint32_t nst = 0;
+    for (uint32_t t = 0; t < T; t++) {
+        int ok = 1;
+        for (uint32_t e = b->del_off[t]; e < b->del_off[t + 1]; e++) {
+            const kdtn_resolved* r = &b->del_res[e];
+            if (r->err) { ok = 0; break; }
+            const uint32_t node = t_src[t], vni = (uint32_t)r->vni, ns = t_netns[t];
+            for (uint64_t i = dhash(node, vni, ns) & (dcap - 1);; i = (i + 1) & (dcap - 1)) {
+                if (!dels[i].used) { dels[i] = (dkey){node, vni, ns, 1}; break; }
+                if (dels[i].node == node && dels[i].vni == vni && dels[i].netns == ns) break;
+            }
+        }
+        if (!ok) continue;
+        for (uint32_t e = b->add_off[t]; e < b->add_off[t + 1]; e++) {
+            const kdtn_resolved* r = &b->add_res[e];
+            if (fan_fails(r, &b->add_qdisc[e])) break;
+            uint32_t node[2], netns[2], k = 0;
+            if (r->kind == KDTN_KIND_CROSS_NODE || r->kind == KDTN_KIND_PHYSICAL) {
+                node[k] = t_src[t];
+                netns[k++] = t_netns[t];
+            }
+            int stop = 0;
+            if (r->kind == KDTN_KIND_CROSS_NODE) {
+                if (r->remote_err) stop = 1;
+                else {
+                    node[k] = r->vtep;
+                    netns[k++] = pod_netns[r->peer_topo];
+                }
+            }
+            for (uint32_t q = 0; q < k; q++) {
+                uint32_t* v = vslot(&addm, vkey(node[q], r->vni));
+                if (*v == UINT32_MAX) *v = nst;
+                an[nst] = node[q];
+                av[nst] = r->vni;
+                as[nst] = netns[q];
+                aw[nst++] = *v;
+            }
+            if (stop) break;
+        }
+    }
+    uint8_t* flag = calloc(nst + 1, 1);
+    for (uint32_t q = 0; q < nst; q++) {
+        const uint32_t w = aw[q];
+        if (as[w] != as[q]) flag[w] = 1;
+        for (uint64_t i = dhash(an[q], (uint32_t)av[q], as[q]) & (dcap - 1); dels[i].used; i = (i + 1) & (dcap - 1))
+            if (dels[i].node == an[q] && dels[i].vni == (uint32_t)av[q] && dels[i].netns == as[q]) { flag[w] = 1; break; }
+    }
+    uint32_t n = 0;
+    for (uint32_t q = 0; q < nst; q++)
+        if (flag[q]) {
+            if (out_node) { out_node[n] = an[q]; out_vni[n] = av[q]; }
+            n++;
+        }
+    free(dels); free(addm.key); free(addm.val); free(an); free(av); free(as); free(aw); free(flag);
+    return n;
+}

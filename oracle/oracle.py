@@ -322,6 +322,27 @@ def json_ingest(doc: bytes):
         L.or_json_free(C.byref(t))
 
 
+def vni_contested(inp: EpochInput, out: BatchesOut, pod_netns=None):
+    """Keys (node, vni) whose VxlanManager result depends on the goroutine order
+    (or_vni_contested), in the order of their winning store."""
+    L = _wire_lib()
+    if not getattr(L, "_vnic_bound", False):
+        L.or_vni_contested.argtypes = [C.POINTER(abi.Batches), C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                       C.c_void_p, C.c_void_p]
+        L.or_vni_contested.restype = C.c_uint32
+        L._vnic_bound = True
+    T = inp.topos.n
+    b = out.to_c((max(len(out.del_idx), 1), max(len(out.add_idx), 1), max(len(out.upd_idx), 1)))
+    src = np.ascontiguousarray(inp.topos.src_ip, np.uint32)
+    ns = np.ascontiguousarray(inp.topos.net_ns, np.uint32)
+    pn = np.ascontiguousarray(ns if pod_netns is None else pod_netns, np.uint32)
+    n = L.or_vni_contested(C.byref(b), T, src.ctypes.data, ns.ctypes.data, pn.ctypes.data, None, None)
+    node, vni = np.zeros(max(n, 1), np.uint32), np.zeros(max(n, 1), np.int32)
+    L.or_vni_contested(C.byref(b), T, src.ctypes.data, ns.ctypes.data, pn.ctypes.data, node.ctypes.data,
+                       vni.ctypes.data)
+    return node[:n], vni[:n]
+
+
 def vni_apply(inp: EpochInput, out: BatchesOut, pod_netns=None):
     """VxlanManager maps after the epoch's reached entries (or_vni_apply): (node, vni, net_ns)
     arrays — the winning adds in (topology, add-list, local-before-remote) order, then the

@@ -82,3 +82,73 @@ def test_oracle_vni_apply_churn_chain():
         vn = Vnis(*[np.array(a, copy=True) for a in got])
         cs.advance()
     assert hits > 0
+
+
+def dict_contested(inp, out):
+    """Keys whose result depends on the goroutine order: two Stores of different netns, or a
+    Store of the netns a reached delLink of the key compares Get(vni) against."""
+    T = inp.topos.n
+    src, netns = inp.topos.src_ip, inp.topos.net_ns
+    dels, stores = set(), []
+
+    def fails(r, q):
+        if r["err"]:
+            return True
+        return r["kind"] in (abi.KIND_SAME_NODE, abi.KIND_CROSS_NODE, abi.KIND_PHYSICAL) and q["err"] != 0
+
+    for t in range(T):
+        ok = True
+        for e in range(out.del_off[t], out.del_off[t + 1]):
+            r = out.del_res[e]
+            if r["err"]:
+                ok = False
+                break
+            dels.add((int(src[t]), int(r["vni"]), int(netns[t])))
+        if not ok:
+            continue
+        for e in range(out.add_off[t], out.add_off[t + 1]):
+            r = out.add_res[e]
+            if fails(r, out.add_qdisc[e]):
+                break
+            k = int(r["kind"])
+            if k in (abi.KIND_CROSS_NODE, abi.KIND_PHYSICAL):
+                stores.append(((int(src[t]), int(r["vni"])), int(netns[t])))
+            if k == abi.KIND_CROSS_NODE:
+                if r["remote_err"]:
+                    break
+                stores.append(((int(r["vtep"]), int(r["vni"])), int(netns[int(r["peer_topo"])])))
+    first = {}
+    for key, ns in stores:
+        first.setdefault(key, ns)
+    hot = set()
+    for key, ns in stores:
+        if ns != first[key] or (key[0], key[1], ns) in dels:
+            hot.add(key)
+    return [k for k in first if k in hot]                 # order of the winning store
+
+
+def test_oracle_vni_contested_random_epochs():
+    total = 0
+    for seed in range(16):
+        _, inp = random_epoch_input(seed, T=80)
+        out = O.reconcile(inp, tick=15.625)
+        node, vni = O.vni_contested(inp, out)
+        got = list(zip(node.tolist(), vni.tolist()))
+        assert got == dict_contested(inp, out), seed
+        total += len(got)
+    assert total > 0                                      # the adversarial epochs do collide
+
+
+def test_oracle_vni_contested_churn_chain():
+    cs = synth.ChurnSequence(total_pods=3000)
+    vn = None
+    for ep in range(3):
+        inp = cs.epoch_input()
+        if vn is not None:
+            inp.vnis = vn
+        out = O.reconcile(inp, tick=15.625)
+        node, vni = O.vni_contested(inp, out)
+        assert list(zip(node.tolist(), vni.tolist())) == dict_contested(inp, out)
+        from kdtn.tables import Vnis
+        vn = Vnis(*[np.array(a, copy=True) for a in O.vni_apply(inp, out)])
+        cs.advance()

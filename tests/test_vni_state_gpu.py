@@ -7,6 +7,7 @@ import pytest
 
 from helpers import random_epoch_input
 from kdtn import Engine, synth
+from kdtn.engine import KdtnError
 from kdtn.tables import Vnis
 
 import oracle as O
@@ -29,6 +30,8 @@ def test_vni_apply_random_epochs(seed):
         got = eng.vni_apply()
         assert same((got.node, got.vni, got.net_ns), want)
         assert np.array_equal(eng.vni_download().node, want[0])
+        # the keys whose result depends on the reference's goroutine order (kdtn_vni_contested)
+        assert same(eng.vni_contested(), O.vni_contested(inp, want_out))
 
 
 @pytest.mark.parametrize("config", [3, 4])
@@ -63,6 +66,7 @@ def test_vni_resident_chain(config):
             want = O.vni_apply(oin, want_out)
             got = eng.vni_apply()
             assert same((got.node, got.vni, got.net_ns), want), f"epoch {ep}: map differs"
+            assert same(eng.vni_contested(), O.vni_contested(oin, want_out)), f"epoch {ep}: contested keys differ"
             vn = Vnis(*[np.array(a, copy=True) for a in want])
             if cs:
                 cs.advance()
@@ -120,3 +124,22 @@ def test_resident_map_needs_kept_dictionary():
             assert e.value.code == abi.EINVAL
         finally:
             inp.vnis = keep
+
+
+def test_vni_contested_counts_random_epochs():
+    """kdtn_vni_contested over adversarial epochs (VNI collisions, deletes of stored keys) equals
+    the oracle, and the epochs do produce contested keys; KDTN_EINVAL before an apply."""
+    total = 0
+    with Engine(device=0, tick_in_usec=15.625) as eng:
+        for seed in range(16):
+            _, inp = random_epoch_input(seed, T=80)
+            want_out = O.reconcile(inp, tick=15.625)
+            got_out = eng.reconcile(inp)
+            assert not got_out.mismatches(want_out)
+            with pytest.raises(KdtnError):
+                eng.vni_contested()                      # no apply since this run
+            eng.vni_apply()
+            want = O.vni_contested(inp, want_out)
+            assert same(eng.vni_contested(), want), seed
+            total += len(want[0])
+    assert total > 0

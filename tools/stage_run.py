@@ -20,7 +20,11 @@ ap.add_argument("--config", type=int, default=2)
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--cache", default="/tmp/kdtn_cache")
 ap.add_argument("--stages", default="run,encode,fanout,remote,tc")
+ap.add_argument("--prof", action="store_true", help="load the profiling build (A/B variants)")
 a = ap.parse_args()
+if a.prof:
+    from kdtn import engine as _kdtn_engine
+    _kdtn_engine.use_profiling_library()
 inp = synth.make(a.config, pods_per_shard=a.pods, cache_dir=a.cache or None)
 eng = Engine(device=0)
 eng.upload(inp)
