@@ -1,0 +1,297 @@
+// kdtn_encode.h — device helpers of the output stages (wire encoding, RemotePod messages,
+// tc argv, fan-out, VXLAN ops): the wave-cooperative entry -> topology search, the
+// dword-assembling byte writer and the wave-image stores. Kept apart from kdtn_kernels.h so the
+// k_reconcile sources (whose hash tags its PMC profiles) do not change with them.
+#pragma once
+#include "kdtn_kernels.h"
+
+namespace kdtn {
+
+// entry_topo for every lane of a wave at once (all lanes must call it; on = the lane has an
+// entry). The topologies of the wave's smallest and largest entry are found together by a
+// 32-ary search (lanes 0-31 for one, 32-63 for the other; each step one load per lane and a
+// ballot, so about log32(T) dependent loads instead of log2(T)); when the wave's entries span
+// fewer than 64 topologies, one more load gives every lane the boundaries between them and a
+// register search (shuffles) finds its own. A wave's entries are usually neighbours.
+KD_INLINE uint32_t entry_topo_wave(const uint32_t* offs, uint32_t T, uint32_t e, bool on) {
+    const int lane = threadIdx.x & 63;
+    uint32_t lo_e = on ? e : 0xFFFFFFFFu, hi_e = on ? e : 0u;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint32_t a = __shfl_xor(lo_e, d, 64), b = __shfl_xor(hi_e, d, 64);
+        lo_e = a < lo_e ? a : lo_e;
+        hi_e = b > hi_e ? b : hi_e;
+    }
+    if (lo_e > hi_e) return 0;                         // no lane has an entry (wave-uniform)
+    // offs[lo] <= key < offs[hi] for key = lo_e (lanes 0-31) / hi_e (lanes 32-63)
+    const uint32_t key = lane < 32 ? lo_e : hi_e, j = (uint32_t)lane & 31u;
+    uint32_t lo = 0, hi = T;
+    for (;;) {
+        const bool open = hi - lo > 1;
+        if (!__ballot(open)) break;                    // both searches done (wave-uniform)
+        const uint32_t step = (hi - lo + 31u) >> 5;
+        const uint32_t probe = lo + j * step;
+        const bool ok = open && probe < hi && offs[probe] <= key;
+        const uint64_t b = __ballot(ok);
+        const uint32_t bh = (uint32_t)(lane < 32 ? b : (b >> 32));   // this half's probes, monotone
+        if (open) {
+            const uint32_t jj = 31u - (uint32_t)__clz((int)bh);       // last probe <= key (j = 0 always is)
+            lo = lo + jj * step;
+            hi = min(hi, lo + step);
+        }
+    }
+    const uint32_t tlo = __shfl(lo, 0, 64), thi = __shfl(lo, 32, 64);   // topologies of lo_e, hi_e
+    if (thi - tlo < 64u) {
+        // boundary l: the first entry of topology tlo + 1 + l (lanes past thi: never <= e)
+        const uint32_t bnd = tlo + 1u + (uint32_t)lane <= thi ? offs[tlo + 1u + lane] : 0xFFFFFFFFu;
+        uint32_t c = 0;                                // boundaries <= e (a prefix of the lanes)
+#pragma unroll
+        for (int s = 32; s >= 1; s >>= 1) {
+            const uint32_t v = __shfl(bnd, (int)(c + (uint32_t)s - 1u), 64);
+            if (c + (uint32_t)s <= 64u && v <= e) c += (uint32_t)s;
+        }
+        return tlo + c;
+    }
+    lo = tlo;
+    hi = thi + 1;                                      // offs[lo] <= e < offs[hi]
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (offs[mid] <= e) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// ---- byte-stream writer of the encoders (wire, RemotePod, tc argv) ---------------------------
+// Bytes are appended 1-4 at a time into a 64-bit register and stored as whole dwords; only the
+// first and the last dword of a writer's range — shared with the neighbouring writers — take
+// byte stores. (One dword store per 4 output bytes instead of one byte store per byte.)
+struct WSink {
+    uint32_t* d;                 // the dword acc's byte 0 belongs to
+    uint32_t* d0;                // the writer's first dword
+    uint64_t acc;                // pending bytes, little-endian
+    uint32_t fill;               // bytes in acc, counting the `head` bytes of d0 that are not ours
+    uint32_t head;               // bytes [0, head) of d0 belong to the previous writer
+    uint32_t first;              // d0's bytes, stored by finish() when head != 0
+    bool hp;                     // d0 not flushed yet and shared (head != 0)
+    KD_INLINE void init(uint8_t* p) {
+        const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3u);
+        d = d0 = reinterpret_cast<uint32_t*>(p - mis);     // pointer arithmetic keeps the address space
+        head = fill = mis;
+        hp = mis != 0;
+        acc = 0;
+        first = 0;
+    }
+    // bytes [lo, hi) of v into dword q, one byte store each
+    KD_INLINE static void part(uint32_t* q, uint32_t v, uint32_t lo, uint32_t hi) {
+        uint8_t* b = reinterpret_cast<uint8_t*>(q);
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k)
+            if (k >= lo && k < hi) b[k] = (uint8_t)(v >> (8u * k));
+    }
+    // the low n (1..4) bytes of v
+    KD_INLINE void put(uint32_t v, uint32_t n) {
+        if (n < 4u) v &= (1u << (8u * n)) - 1u;
+        acc |= (uint64_t)v << (8u * fill);
+        fill += n;
+        if (fill >= 4u) {
+            if (hp) {
+                first = (uint32_t)acc;
+                hp = false;
+            } else {
+                *d = (uint32_t)acc;
+            }
+            ++d;
+            acc >>= 32;
+            fill -= 4u;
+        }
+    }
+    KD_INLINE void finish() {
+        if (head && !hp) part(d0, first, head, 4u);     // shared first dword, flushed
+        if (fill) part(d, (uint32_t)acc, hp ? head : 0u, fill);
+    }
+    // owned mode: the writer owns every byte of its dwords (a private LDS slot); `lead` zero
+    // bytes put the output at the alignment of its destination
+    KD_INLINE void init_owned(uint32_t* slot, uint32_t lead) {
+        d = d0 = slot;
+        head = 0;
+        fill = lead;
+        hp = false;
+        acc = 0;
+        first = 0;
+    }
+    KD_INLINE void finish_owned() {
+        if (fill) *d = (uint32_t)acc;
+    }
+    KD_INLINE void byte(uint32_t v) { put(v, 1u); }
+    // protobuf base-128 varint: four 7-bit groups per put
+    KD_INLINE void varint(uint64_t v) {
+        while (v >= (1ull << 28)) {
+            const uint32_t x = (uint32_t)v;
+            put((x & 0x7Fu) | 0x80u | (((x >> 7) & 0x7Fu) | 0x80u) << 8 | (((x >> 14) & 0x7Fu) | 0x80u) << 16 |
+                    (((x >> 21) & 0x7Fu) | 0x80u) << 24, 4u);
+            v >>= 28;
+        }
+        const uint32_t x = (uint32_t)v;
+        uint32_t w = x & 0x7Fu, n = 1;
+        if (x >= 0x80u) { w |= 0x80u | ((x >> 7) & 0x7Fu) << 8; n = 2; }
+        if (x >= 0x4000u) { w |= 0x8000u | ((x >> 14) & 0x7Fu) << 16; n = 3; }
+        if (x >= 0x200000u) { w |= 0x800000u | ((x >> 21) & 0x7Fu) << 24; n = 4; }
+        put(w, n);
+    }
+    // bytes [b, b + len) of an arena with >= 40 B of readable slack past its end: the string's
+    // dwords come from one or two 16-B loads (+ one dword) issued together, the bytes past 32
+    // one at a time
+    KD_INLINE void str(const uint8_t* arena, uint32_t b, uint32_t len) {
+        if (!len) return;
+        typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+        const uint32_t* a32 = reinterpret_cast<const uint32_t*>(arena) + (b >> 2);
+        const uint32_t sh = b & 3u, nw = (sh + len + 3u) >> 2;
+        const u32x4a A = *reinterpret_cast<const u32x4a*>(a32);
+        u32x4a B = {0u, 0u, 0u, 0u};
+        if (nw > 4u) B = *reinterpret_cast<const u32x4a*>(a32 + 4);
+        const uint32_t c8 = nw > 8u ? a32[8] : 0u;
+        const uint32_t w[9] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w, c8};
+#pragma unroll
+        for (uint32_t q = 0; q < 8; ++q) {
+            if (4u * q < len) {
+                const uint32_t r = len - 4u * q;
+                put(__builtin_amdgcn_alignbyte(w[q + 1], w[q], sh), r < 4u ? r : 4u);
+            }
+        }
+        for (uint32_t k = 32; k < len; ++k) put(arena[b + k], 1u);
+    }
+};
+
+// One wave writes the bytes of its active lanes, which are consecutive ranges [s0, s1) of one
+// arena (in lane order, empty lanes between them): each lane's body(WSink&) writes into the
+// wave's LDS image (`img`, WIRE_IMG bytes), then the wave stores the image with coalesced
+// dword stores — byte stores only at the two dwords shared with the neighbouring waves. A
+// range larger than the image is written straight to global memory. Every lane of the wave
+// must call it.
+template <typename F>
+KD_INLINE void wave_image_write(uint32_t* img, bool on, uint64_t s0, uint64_t s1, uint8_t* arena, F&& body) {
+    const int lane = threadIdx.x & 63;
+    uint64_t r0 = on ? s0 : ~0ull, r1 = on ? s1 : 0ull;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint64_t a = __shfl_xor(r0, d, 64), b = __shfl_xor(r1, d, 64);
+        r0 = a < r0 ? a : r0;
+        r1 = b > r1 ? b : r1;
+    }
+    if (r1 <= r0) return;                                 // no active lane (wave-uniform)
+    const uint32_t lead = (uint32_t)(r0 & 3u);
+    WSink o;
+    if (r1 - r0 + lead > (uint64_t)WIRE_IMG) {            // too large: straight to global memory
+        if (on) {
+            o.init(arena + s0);
+            body(o);
+            o.finish();
+        }
+        return;
+    }
+    if (on) {
+        o.init(reinterpret_cast<uint8_t*>(img) + lead + (uint32_t)(s0 - r0));
+        body(o);
+        o.finish();
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint64_t a0 = r0 - lead;                        // dword-aligned global start
+    const uint32_t nw = (uint32_t)((r1 - a0 + 3) >> 2);
+    for (uint32_t q = lane; q < nw; q += 64) {
+        const uint64_t ga = a0 + 4ull * q;
+        const uint32_t v = img[q];
+        if (ga >= r0 && ga + 4 <= r1) {
+            *reinterpret_cast<uint32_t*>(arena + ga) = v;
+        } else {
+            for (uint32_t k = 0; k < 4; ++k)
+                if (ga + k >= r0 && ga + k < r1) arena[ga + k] = (uint8_t)(v >> (8 * k));
+        }
+    }
+}
+
+// One wave writes its lanes' byte ranges [s0, s1) when they are NOT one contiguous range (the
+// RemotePod messages of consecutive add entries go to their daemons' runs): in two rounds of 32
+// lanes, every lane writes its range into a private dword slot of the wave's LDS image at the
+// alignment of its destination (owned WSink), then the wave copies the slots out dword by
+// dword — lane q takes image dword q, finds its slot by binary search, and stores it whole, or
+// by bytes where the dword is shared with a neighbouring range. Consecutive lanes thus store
+// consecutive dwords of each range instead of every lane storing its own range alone. A round
+// larger than the image is written straight to global memory. Every lane must call it.
+constexpr int SEG_META = 4 * 32 + 1;            // dwords of slot metadata at the image's end
+template <int R, typename F>
+KD_INLINE void wave_segments_round(uint32_t* img, bool on, uint64_t s0, uint32_t len, uint32_t ndw, uint8_t* arena,
+                                   F& body) {
+    const int lane = threadIdx.x & 63;
+    uint32_t* mq = img + WIRE_IMG / 4 - SEG_META;  // [33] slot starts (dwords), then per slot: dst lo, hi, lead|len
+    uint32_t* mlo = mq + 33;
+    uint32_t* mhi = mlo + 32;
+    uint32_t* mll = mhi + 32;
+    constexpr uint32_t budget = WIRE_IMG / 4 - SEG_META;
+    const uint32_t lead = (uint32_t)s0 & 3u;
+    const bool mine = (lane >> 5) == R;
+    const uint32_t x = mine ? ndw : 0u;
+    uint32_t inc = x;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += o;
+    }
+    const uint32_t q0 = __shfl(inc - x, 32 * R, 64);            // the round's first slot start
+    const uint32_t total = __shfl(inc, 32 * R + 31, 64) - q0;
+    const uint32_t qi = inc - x - q0;
+    if (total == 0) return;                                      // wave-uniform
+    const bool direct = total > budget;                          // too large: straight to global memory
+    const int sl = lane - 32 * R;
+    if (mine && !direct) {
+        mq[sl] = qi;
+        mlo[sl] = (uint32_t)(s0 & ~3ull);
+        mhi[sl] = (uint32_t)(s0 >> 32);
+        mll[sl] = lead | (len << 2);
+    }
+    if (mine && on) {                                            // one call site of the body
+        WSink o;
+        if (direct) o.init(arena + s0);
+        else o.init_owned(img + qi, lead);
+        body(o);
+        if (direct) o.finish();
+        else o.finish_owned();
+    }
+    if (direct) return;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (uint32_t q = lane; q < total; q += 64) {
+        int i = 0;                                               // the last slot starting at or before q
+#pragma unroll
+        for (int step = 16; step >= 1; step >>= 1)
+            if (i + step < 32 && mq[i + step] <= q) i += step;
+        const uint32_t k = q - mq[i], ll = mll[i];
+        const uint32_t ld = ll & 3u, end = ld + (ll >> 2);      // valid bytes of the slot: [ld, end)
+        uint8_t* dst = arena + ((((uint64_t)mhi[i]) << 32) | mlo[i]) + 4ull * k;
+        const uint32_t v = img[q];
+        const uint32_t lo = k == 0 ? ld : 0u;
+        const uint32_t hi = end - 4u * k < 4u ? end - 4u * k : 4u;
+        if (lo == 0 && hi == 4u) {
+            *reinterpret_cast<uint32_t*>(dst) = v;
+        } else {
+#pragma unroll
+            for (uint32_t c = 0; c < 4; ++c)
+                if (c >= lo && c < hi) dst[c] = (uint8_t)(v >> (8 * c));
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+template <typename F>
+KD_INLINE void wave_segments_write(uint32_t* img, bool on, uint64_t s0, uint64_t s1, uint8_t* arena, F&& body) {
+    const uint32_t len = on ? (uint32_t)(s1 - s0) : 0u;
+    const uint32_t ndw = on ? (((uint32_t)s0 & 3u) + len + 3u) >> 2 : 0u;
+    wave_segments_round<0>(img, on, s0, len, ndw, arena, body);   // lanes 0-31, then 32-63
+    wave_segments_round<1>(img, on, s0, len, ndw, arena, body);
+}
+
+}  // namespace kdtn

@@ -13,7 +13,7 @@
 // and their nodes in a stamped D-sized table), k_fan_nodes_* (compaction of marked node ids → dense
 // node index), k_fan_count / k_fan_scatter (single-wave workgroups over chunks of 4,096
 // entries: LDS histogram, node-major scan of the (node, chunk) counts, stable scatter).
-#include "kdtn_kernels.h"
+#include "kdtn_encode.h"
 
 namespace kdtn {
 

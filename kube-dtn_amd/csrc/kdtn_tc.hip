@@ -13,7 +13,7 @@
 // earlier failing link in the topology's Del/Add/Update RPC sequence) run tc. Layout: two
 // command slots per add entry, then one per update entry; slot g's argv =
 // bytes[off[g], off[g+1]) (empty when it runs no tc command).
-#include "kdtn_kernels.h"
+#include "kdtn_encode.h"
 
 namespace kdtn {
 

@@ -22,7 +22,7 @@
 // new map as a first-wins table over [add ops, surviving snapshot entries] (k_vni_insert)
 // and its visible entries compacted in that order (k_vni_vis_count / k_scan_top /
 // k_vni_vis_write).
-#include "kdtn_kernels.h"
+#include "kdtn_encode.h"
 
 namespace kdtn {
 

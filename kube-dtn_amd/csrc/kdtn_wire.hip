@@ -24,7 +24,7 @@
 //   k_wire_write     one thread per entry: writes its bytes into the wave's LDS image (dwords
 //                    assembled in registers, WSink), which the wave then stores with
 //                    coalesced dword stores
-#include "kdtn_kernels.h"
+#include "kdtn_encode.h"
 
 namespace kdtn {
 
