@@ -255,7 +255,9 @@ int upload_dict(kdtn_ctx* c, DevBuf& bytes, DevBuf& offs, const kdtn_strtab& t, 
 size_t sync_counts_at(uint32_t nwg) { return align_up(SYNC_HEADER_BYTES + (size_t)nwg * 24, 16); }
 size_t sync_bytes(uint32_t nwg) { return sync_counts_at(nwg) + 2 * align_up((size_t)nwg * 12, 16); }
 
-int check_strtab(const kdtn_strtab& t, const char* what) {
+// from: the kept prefix of an append-only upload (its offsets were checked when uploaded and
+// check_keep compares offs[keep] with the device copy), so only [from, n] is walked
+int check_strtab(const kdtn_strtab& t, const char* what, uint32_t from = 0) {
     if (t.n == 0 || !t.offs || (!t.bytes && t.offs[t.n] != 0)) {
         std::snprintf(g_last_error, sizeof(g_last_error), "%s: empty dictionary (id 0 must be \"\")", what);
         return KDTN_EINVAL;
@@ -268,7 +270,7 @@ int check_strtab(const kdtn_strtab& t, const char* what) {
         std::snprintf(g_last_error, sizeof(g_last_error), "%s: id 0 must be the empty string", what);
         return KDTN_EINVAL;
     }
-    for (uint32_t i = 0; i < t.n; ++i)
+    for (uint32_t i = from < t.n ? from : t.n; i < t.n; ++i)
         if (t.offs[i + 1] < t.offs[i]) {
             std::snprintf(g_last_error, sizeof(g_last_error), "%s: offsets not monotone at %u", what, i);
             return KDTN_EINVAL;
@@ -798,8 +800,8 @@ int kdtn_epoch_upload(kdtn_ctx* c, const kdtn_epoch_in* in) {
     HIP_TRY(hipSetDevice(c->device));
     g_last_error[0] = 0;
     end_shard_ingest(c);
-    TRY(check_strtab(in->kdict, "kdict"));
-    TRY(check_strtab(in->pdict, "pdict"));
+    TRY(check_strtab(in->kdict, "kdict", in->kdict_keep));
+    TRY(check_strtab(in->pdict, "pdict", in->pdict_keep));
     const kdtn_topo_table& T = in->topos;
     const uint32_t D = in->kdict.n, P = in->pdict.n;
     TRY(check_offsets(T.real_off, T.n, in->realised.n, "topos.real_off"));
@@ -2720,8 +2722,8 @@ int kdtn_epoch_upload_delta(kdtn_ctx* c, const kdtn_epoch_delta* d) {
     HIP_TRY(hipSetDevice(c->device));
     g_last_error[0] = 0;
     end_shard_ingest(c);
-    TRY(check_strtab(d->kdict, "kdict"));
-    TRY(check_strtab(d->pdict, "pdict"));
+    TRY(check_strtab(d->kdict, "kdict", d->kdict_keep));
+    TRY(check_strtab(d->pdict, "pdict", d->pdict_keep));
     const uint32_t T = c->T, n = d->n_changed, N0 = c->des.n, D = d->kdict.n, P = d->pdict.n;
     auto bad = [&](const char* what, uint32_t i) {
         std::snprintf(g_last_error, sizeof(g_last_error), "delta: %s (at %u)", what, i);
@@ -2738,9 +2740,20 @@ int kdtn_epoch_upload_delta(kdtn_ctx* c, const kdtn_epoch_delta* d) {
         if (d->des_off[k + 1] < d->des_off[k]) return bad("des_off not monotone", k);
         if (d->spec_nil[k] && d->des_off[k + 1] != d->des_off[k]) return bad("spec nil but records", k);
     }
-    for (uint32_t i = 0; i < nref; ++i) {
-        const uint32_t r = d->ref[i];
-        if ((r & KDTN_DELTA_NEW) ? (r & ~KDTN_DELTA_NEW) >= d->records.n : r >= N0) return bad("ref out of range", i);
+    {   // the largest reference of each kind (a loop the compiler vectorises), then the culprit
+        uint32_t top_new = 0, top_old = 0;
+        for (uint32_t i = 0; i < nref; ++i) {
+            const uint32_t r = d->ref[i];
+            const uint32_t nw = (r & KDTN_DELTA_NEW) ? (r & ~KDTN_DELTA_NEW) + 1u : 0u;
+            const uint32_t od = (r & KDTN_DELTA_NEW) ? 0u : r + 1u;
+            top_new = nw > top_new ? nw : top_new;
+            top_old = od > top_old ? od : top_old;
+        }
+        if (top_new > d->records.n || top_old > N0)
+            for (uint32_t i = 0; i < nref; ++i) {
+                const uint32_t r = d->ref[i];
+                if ((r & KDTN_DELTA_NEW) ? (r & ~KDTN_DELTA_NEW) >= d->records.n : r >= N0) return bad("ref out of range", i);
+            }
     }
     TRY(check_ids(d->src_ip, n, D, "delta.src_ip"));
     TRY(check_ids(d->net_ns, n, D, "delta.net_ns"));

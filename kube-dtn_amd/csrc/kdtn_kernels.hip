@@ -126,6 +126,29 @@ KD_INLINE uint32_t window4(const uint32_t* w, uint32_t q) {
     return __builtin_amdgcn_alignbyte(hi, lo, q & 3u);
 }
 KD_INLINE bool hexb(uint32_t c) { return (c - '0' < 10u) | ((c | 0x20u) - 'a' < 6u); }
+// high bit of each byte set where the byte is a hex digit [0-9a-fA-F]
+KD_INLINE uint32_t swar_hex(uint32_t x) {
+    const uint32_t t = (x | 0x20202020u) & 0x7F7F7F7Fu;                 // lower case, 7 bits
+    const uint32_t ge_a = (t | 0x80808080u) - 0x61616161u;               // byte >= 'a' (no borrow)
+    const uint32_t le_f = 0xE6E6E6E6u - t;                               // byte <= 'f' (no borrow)
+    return swar_digit(x) | (ge_a & le_f & ~x & 0x80808080u);
+}
+// net.ParseMAC of the 6- and 8-group colon / hyphen forms (17 / 23 bytes) from the register
+// image: hex digits at 3g and 3g+1, the separator s[2] at 3g+2 (common/veth.go:33; Go's
+// xtoi2 groups). The byte-wise mac_ok decides the other layouts.
+KD_INLINE bool mac_swar(const uint32_t* w, uint32_t len) {
+    const uint32_t sep = wbyte(w, 2) * 0x01010101u;
+    uint32_t H = 0, S = 0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        H |= swar_nib(swar_hex(w[k])) << (4 * k);
+        S |= swar_nib(swar_eq(w[k], sep)) << (4 * k);
+    }
+    // 17 bytes: hex at 0,1 3,4 ... 15,16; separators at 2,5,8,11,14
+    constexpr uint32_t H17 = 0x1B6DBu, S17 = 0x4924u, H23 = 0x6DB6DBu, S23 = 0x124924u;
+    const uint32_t hm = len == 17u ? H17 : H23, sm = len == 17u ? S17 : S23;
+    return (H & hm) == hm && (S & sm) == sm;
+}
 // one dotted-quad field of n digits starting with the 4-byte window c: dtoi, <= 255 and no
 // leading zero (net.parseIPv4, Go 1.18)
 KD_INLINE uint32_t octet_ok(uint32_t c, uint32_t n) {
@@ -137,10 +160,13 @@ KD_INLINE uint32_t octet_ok(uint32_t c, uint32_t n) {
 // net.ParseCIDR validity from the register image of a string of <= 24 bytes
 // (common/veth.go:22). Decides every string without ':' whose prefix has <= 2 digits;
 // sets *slow for the rest (IPv6 candidates, long prefixes), which take cidr_ok().
+// NW: words of the image classified (4 when every string of the wave has <= 16 bytes — an
+// IPv4 CIDR has at most 18 — so the wave skips a third of the class work)
+template <int NW = 6>
 KD_INLINE bool cidr_swar(const uint32_t* w, uint32_t len, bool* slow) {
     uint32_t D = 0, P = 0, S = 0, C = 0;
 #pragma unroll
-    for (int k = 0; k < 6; ++k) {
+    for (int k = 0; k < NW; ++k) {
         D |= swar_nib(swar_digit(w[k])) << (4 * k);
         P |= swar_nib(swar_eq(w[k], 0x2E2E2E2Eu)) << (4 * k);   // '.'
         S |= swar_nib(swar_eq(w[k], 0x2F2F2F2Fu)) << (4 * k);   // '/'
@@ -155,7 +181,8 @@ KD_INLINE bool cidr_swar(const uint32_t* w, uint32_t len, bool* slow) {
     const uint32_t m = len - s - 1u;                             // prefix digits
     // generic parser only for IPv6 candidates (any IPv6 text has a colon) and for IPv4-looking
     // strings (first byte a digit) with a prefix of 3+ digits; anything else cannot parse
-    *slow = (C != 0u) | ((D & 1u) != 0u && m > 2u && s < len);
+    // (ParseCIDR fails at once without a '/': MAC-shaped strings with ':' need no IPv6 parse)
+    *slow = (C != 0u && S != 0u) | ((D & 1u) != 0u && m > 2u && s < len);
     const uint32_t sep = P | S;
     uint32_t ok = ((D | sep) == L) & (__builtin_popcount(P) == 3) & (__builtin_popcount(S) == 1) &
                   ((P >> s) == 0u) & ((sep & (sep << 1)) == 0u) & (D & 1u) & (s + 1u < len) & (s <= 15u);
@@ -182,7 +209,7 @@ KD_INLINE bool cidr_swar(const uint32_t* w, uint32_t len, bool* slow) {
 // predicate bits per set with a ballot (two u32 words per set, lanes 0 and 32).
 // Predicate bits of one key string from its register image (first 24 bytes in w[]).
 KD_INLINE uint32_t kdict_bits(const uint8_t* bytes, uint32_t b, uint32_t len, const uint32_t* w, uint32_t i,
-                              uint32_t* special) {
+                              uint32_t* special, bool short_wave) {
     uint32_t f = 0;
     const uint32_t c0 = w[0] & 0xFFu;
     if (len && !hexb(c0) && c0 != ':') {
@@ -191,7 +218,8 @@ KD_INLINE uint32_t kdict_bits(const uint8_t* bytes, uint32_t b, uint32_t len, co
         f = (1u << KB_CIDR_BAD) | (1u << KB_MAC_BAD);
     } else if (len) {
         bool slow = true, cok = false;
-        if (len <= 24) cok = cidr_swar(w, len, &slow);
+        if (short_wave) cok = cidr_swar<4>(w, len, &slow);
+        else if (len <= 24) cok = cidr_swar<6>(w, len, &slow);
         if (slow) cok = cidr_ok(bytes + b, len);                       // common/veth.go:22
         if (!cok) f |= 1u << KB_CIDR_BAD;
         const uint32_t c2 = wbyte(w, 2), c4 = wbyte(w, 4);
@@ -204,7 +232,7 @@ KD_INLINE uint32_t kdict_bits(const uint8_t* bytes, uint32_t b, uint32_t len, co
         if (c2 == ':' || c2 == '-') cand = (len == 17 || len == 23 || len == 59) && hexb(wbyte(w, 0)) && hexb(wbyte(w, 1));
         else if (c4 == '.') cand = (len == 14 || len == 19 || len == 49) && hexb(wbyte(w, 0)) && hexb(wbyte(w, 1)) &&
                                    hexb(c2) && hexb(wbyte(w, 3));
-        if (cand) mok = mac_ok(bytes + b, len);
+        if (cand) mok = (len == 17 || len == 23) ? mac_swar(w, len) : mac_ok(bytes + b, len);
         if (!mok) f |= 1u << KB_MAC_BAD;
     }
     const uint32_t w2b = w[2] & 0xFFu;
@@ -268,7 +296,8 @@ __global__ void __launch_bounds__(NT) k_kdict_flags(const uint8_t* bytes, const 
 #pragma unroll
         for (int k = 0; k < 6; ++k)
             w[k] = sh ? (d[s][k] >> sh) | (d[s][k + 1] << (32u - sh)) : d[s][k];
-        const uint32_t f = i < n ? kdict_bits(bytes, b[s], len[s], w, i, special) : 0u;
+        const bool short_wave = __ballot(i < n && len[s] > 16u) == 0;   // wave-uniform
+        const uint32_t f = i < n ? kdict_bits(bytes, b[s], len[s], w, i, special, short_wave) : 0u;
         const uint32_t w0 = (i - lane) >> 5;                   // first word of this wave
 #pragma unroll
         for (int k = 0; k < KB_NSETS; ++k) {
@@ -319,7 +348,8 @@ __global__ void __launch_bounds__(BLOCK) k_kdict_flags_ws(const uint8_t* bytes, 
     uint32_t w[6];
 #pragma unroll
     for (int k = 0; k < 6; ++k) w[k] = sh ? (d[k] >> sh) | (d[k + 1] << (32u - sh)) : d[k];
-    const uint32_t f = i < n ? kdict_bits(bytes, b, len, w, i, special) : 0u;
+    const bool short_wave = __ballot(i < n && len > 16u) == 0;
+    const uint32_t f = i < n ? kdict_bits(bytes, b, len, w, i, special, short_wave) : 0u;
     const uint32_t w0 = (i - lane) >> 5;                   // first word of this wave
 #pragma unroll
     for (int k = 0; k < KB_NSETS; ++k) {

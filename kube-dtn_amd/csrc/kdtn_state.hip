@@ -14,7 +14,7 @@
 // Both are one "assemble" pass: every output record of Topology t comes from a per-topology
 // source — a contiguous segment of store A, of store B, or a list of record references
 // (A record, or B record with ASM_B) — with new offsets from a scan of the lengths.
-#include "kdtn_kernels.h"
+#include "kdtn_encode.h"
 
 namespace kdtn {
 
@@ -109,8 +109,8 @@ __global__ void __launch_bounds__(BLOCK) k_store_assemble(const uint32_t* off, u
                                                           const uint8_t* mode, const uint32_t* ref, DevLinks A,
                                                           DevLinks B, uint32_t n, uint32_t* out) {
     const uint32_t d = blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t t = entry_topo_wave(off, nt, d, d < n);   // (all lanes: wave-cooperative)
     if (d >= n) return;
-    const uint32_t t = entry_topo(off, nt, d);
     const uint32_t k = base[t] + (d - off[t]);
     const uint8_t m = mode[t];
     if (m == ASM_SEG_A) copy_record(A.base, k, out, d);

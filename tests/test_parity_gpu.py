@@ -156,6 +156,13 @@ def test_key_predicates_fuzz(engine):
             for _ in range(300)]
     macs += [_mutate(rng, rng.choice(macs), maca) for _ in range(700)]
     macs += ["".join(rng.choice(maca) for _ in range(rng.randint(10, 26))) for _ in range(300)]
+    # the register (SWAR) form decides 17- and 23-byte ':' / '-' layouts: both separators,
+    # mixed separators, upper case, non-hex and non-ASCII bytes in any position
+    macs += [rng.choice(":-").join(f"{rng.randint(0, 255):02X}" for _ in range(rng.choice([6, 8])))
+             for _ in range(200)]
+    macs += [_mutate(rng, rng.choice(macs[-200:]), maca + "gG@`/\u00e9") for _ in range(400)]
+    macs += ["aa:bb:cc:dd:ee:f\u00e9", "aa-bb-cc-dd-ee-ff", "aa-bb:cc-dd-ee-ff", "AA:BB:CC:DD:EE:FF:00:11",
+             "aa:bb:cc:dd:ee:ff:00:1g", "0a:1b:2c:3d:4e:5f"]
     peers = ["b", "localhost", "localhos", "localhostx", "physical/10.0.0.9", "physical/", "physical",
              "Physical/1"]
     links = []
