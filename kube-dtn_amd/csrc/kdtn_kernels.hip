@@ -160,13 +160,10 @@ KD_INLINE uint32_t octet_ok(uint32_t c, uint32_t n) {
 // net.ParseCIDR validity from the register image of a string of <= 24 bytes
 // (common/veth.go:22). Decides every string without ':' whose prefix has <= 2 digits;
 // sets *slow for the rest (IPv6 candidates, long prefixes), which take cidr_ok().
-// NW: words of the image classified (4 when every string of the wave has <= 16 bytes — an
-// IPv4 CIDR has at most 18 — so the wave skips a third of the class work)
-template <int NW = 6>
 KD_INLINE bool cidr_swar(const uint32_t* w, uint32_t len, bool* slow) {
     uint32_t D = 0, P = 0, S = 0, C = 0;
 #pragma unroll
-    for (int k = 0; k < NW; ++k) {
+    for (int k = 0; k < 6; ++k) {
         D |= swar_nib(swar_digit(w[k])) << (4 * k);
         P |= swar_nib(swar_eq(w[k], 0x2E2E2E2Eu)) << (4 * k);   // '.'
         S |= swar_nib(swar_eq(w[k], 0x2F2F2F2Fu)) << (4 * k);   // '/'
@@ -209,7 +206,7 @@ KD_INLINE bool cidr_swar(const uint32_t* w, uint32_t len, bool* slow) {
 // predicate bits per set with a ballot (two u32 words per set, lanes 0 and 32).
 // Predicate bits of one key string from its register image (first 24 bytes in w[]).
 KD_INLINE uint32_t kdict_bits(const uint8_t* bytes, uint32_t b, uint32_t len, const uint32_t* w, uint32_t i,
-                              uint32_t* special, bool short_wave) {
+                              uint32_t* special) {
     uint32_t f = 0;
     const uint32_t c0 = w[0] & 0xFFu;
     if (len && !hexb(c0) && c0 != ':') {
@@ -218,8 +215,7 @@ KD_INLINE uint32_t kdict_bits(const uint8_t* bytes, uint32_t b, uint32_t len, co
         f = (1u << KB_CIDR_BAD) | (1u << KB_MAC_BAD);
     } else if (len) {
         bool slow = true, cok = false;
-        if (short_wave) cok = cidr_swar<4>(w, len, &slow);
-        else if (len <= 24) cok = cidr_swar<6>(w, len, &slow);
+        if (len <= 24) cok = cidr_swar(w, len, &slow);
         if (slow) cok = cidr_ok(bytes + b, len);                       // common/veth.go:22
         if (!cok) f |= 1u << KB_CIDR_BAD;
         const uint32_t c2 = wbyte(w, 2), c4 = wbyte(w, 4);
@@ -296,8 +292,7 @@ __global__ void __launch_bounds__(NT) k_kdict_flags(const uint8_t* bytes, const 
 #pragma unroll
         for (int k = 0; k < 6; ++k)
             w[k] = sh ? (d[s][k] >> sh) | (d[s][k + 1] << (32u - sh)) : d[s][k];
-        const bool short_wave = __ballot(i < n && len[s] > 16u) == 0;   // wave-uniform
-        const uint32_t f = i < n ? kdict_bits(bytes, b[s], len[s], w, i, special, short_wave) : 0u;
+        const uint32_t f = i < n ? kdict_bits(bytes, b[s], len[s], w, i, special) : 0u;
         const uint32_t w0 = (i - lane) >> 5;                   // first word of this wave
 #pragma unroll
         for (int k = 0; k < KB_NSETS; ++k) {
@@ -348,8 +343,7 @@ __global__ void __launch_bounds__(BLOCK) k_kdict_flags_ws(const uint8_t* bytes, 
     uint32_t w[6];
 #pragma unroll
     for (int k = 0; k < 6; ++k) w[k] = sh ? (d[k] >> sh) | (d[k + 1] << (32u - sh)) : d[k];
-    const bool short_wave = __ballot(i < n && len > 16u) == 0;
-    const uint32_t f = i < n ? kdict_bits(bytes, b, len, w, i, special, short_wave) : 0u;
+    const uint32_t f = i < n ? kdict_bits(bytes, b, len, w, i, special) : 0u;
     const uint32_t w0 = (i - lane) >> 5;                   // first word of this wave
 #pragma unroll
     for (int k = 0; k < KB_NSETS; ++k) {
