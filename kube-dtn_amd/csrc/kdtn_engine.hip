@@ -915,6 +915,12 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
             else if (sub == 2) k_kdict_flags<2, false, BLOCK><<<nblocks(nk, BLOCK * 2), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
             else if (sub == 8) k_kdict_flags<1, true, BLOCK><<<nblocks(nk), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
             else if (sub == 16) k_kdict_flags_ws<<<nblocks(nk), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
+            else if (sub >= 32 && sub < 40) {
+                const uint32_t nb = std::min(nblocks(nk), (uint32_t)(c->n_cus * 8 * (sub - 31)));
+                k_kdict_flags_pp<<<nb, BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
+            }
+            else if (sub == 40) k_kdict_null<<<nblocks(nk), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
+            else if (sub == 41) k_kdict_loadonly<<<nblocks(nk), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
             else if (sub == 64) k_kdict_flags<1, false, 64><<<nblocks(nk, 64), 64, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
             else if (sub == 1024) k_kdict_flags<1, false, 1024><<<nblocks(nk, 1024), 1024, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
             else

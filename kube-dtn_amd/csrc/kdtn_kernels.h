@@ -227,6 +227,12 @@ __global__ void k_kdict_flags(const uint8_t* bytes, const uint32_t* offs, uint32
                               uint32_t* kbits, uint32_t kb_words, uint32_t* special);
 __global__ void k_kdict_flags_ws(const uint8_t* bytes, const uint32_t* offs, uint32_t first, uint32_t n,
                                  uint32_t* kbits, uint32_t kb_words, uint32_t* special);
+__global__ void k_kdict_flags_pp(const uint8_t* bytes, const uint32_t* offs, uint32_t first, uint32_t n,
+                                 uint32_t* kbits, uint32_t kb_words, uint32_t* special);
+__global__ void k_kdict_null(const uint8_t* bytes, const uint32_t* offs, uint32_t first, uint32_t n,
+                             uint32_t* kbits, uint32_t kb_words, uint32_t* special);
+__global__ void k_kdict_loadonly(const uint8_t* bytes, const uint32_t* offs, uint32_t first, uint32_t n,
+                                 uint32_t* kbits, uint32_t kb_words, uint32_t* special);
 template <int WHICH>
 __global__ void k_pdict_only(const uint8_t* bytes, const uint32_t* offs, uint32_t first, uint32_t n, double tick,
                              uint32_t* ppct, uint2* pdur, uint2* prate, uint32_t* rate_err);

@@ -352,6 +352,79 @@ __global__ void __launch_bounds__(BLOCK) k_kdict_flags_ws(const uint8_t* bytes, 
             kbits[(size_t)k * kb_words + w0 + (lane >> 5)] = lane ? (uint32_t)(m >> 32) : (uint32_t)m;
     }
 }
+// (A/B, KDTN_KD_SUB=32) Persistent waves, software-pipelined: each wave walks 64-string
+// chunks c = wave, wave + W, ... and issues chunk c + W's offset and window loads before it
+// parses chunk c, so a wave keeps one chunk's round trips in flight while it computes.
+__global__ void __launch_bounds__(BLOCK) k_kdict_flags_pp(const uint8_t* bytes, const uint32_t* offs, uint32_t first,
+                                                          uint32_t n, uint32_t* kbits, uint32_t kb_words,
+                                                          uint32_t* special) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t W = gridDim.x * (BLOCK / 64);
+    uint32_t c = blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
+    const uint32_t nch = (n - first + 63) >> 6;
+    auto load = [&](uint32_t ch, uint32_t& b, uint32_t& len, uint32_t* d) {
+        const uint32_t i = first + ch * 64 + lane;
+        const uint32_t ic = i < n ? i : n;
+        b = offs[ic];
+        len = (i < n ? offs[ic + 1] : b) - b;
+        const uint32_t* p = reinterpret_cast<const uint32_t*>(bytes + (b & ~3u));
+#pragma unroll
+        for (int k = 0; k < 7; ++k) d[k] = p[k];
+    };
+    if (c >= nch) return;
+    uint32_t b, len, d[7];
+    load(c, b, len, d);
+    for (; c < nch; c += W) {
+        uint32_t nb = 0, nlen = 0, nd[7] = {0, 0, 0, 0, 0, 0, 0};
+        if (c + W < nch) load(c + W, nb, nlen, nd);
+        const uint32_t i = first + c * 64 + lane;
+        const uint32_t sh = (b & 3u) * 8u;
+        uint32_t w[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) w[k] = sh ? (d[k] >> sh) | (d[k + 1] << (32u - sh)) : d[k];
+        const uint32_t f = i < n ? kdict_bits(bytes, b, len, w, i, special) : 0u;
+        const uint32_t w0 = (i - lane) >> 5;
+#pragma unroll
+        for (int k = 0; k < KB_NSETS; ++k) {
+            const uint64_t m = __ballot((f >> k) & 1u);
+            if (w0 < kb_words && (lane == 0 || lane == 32))
+                kbits[(size_t)k * kb_words + w0 + (lane >> 5)] = lane ? (uint32_t)(m >> 32) : (uint32_t)m;
+        }
+        b = nb;
+        len = nlen;
+#pragma unroll
+        for (int k = 0; k < 7; ++k) d[k] = nd[k];
+    }
+}
+// (A/B, KDTN_KD_SUB=33) the launch floor: offsets only, one ballot store per wave and set
+__global__ void __launch_bounds__(BLOCK) k_kdict_null(const uint8_t* bytes, const uint32_t* offs, uint32_t first,
+                                                      uint32_t n, uint32_t* kbits, uint32_t kb_words, uint32_t*) {
+    const uint32_t i = first + blockIdx.x * BLOCK + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const uint32_t ic = i < n ? i : n;
+    const uint32_t b = offs[ic];
+    const uint32_t len = (i < n ? offs[ic + 1] : b) - b;
+    const uint64_t m = __ballot(len > 12u);
+    const uint32_t w0 = (i - lane) >> 5;
+    if (w0 < kb_words && (lane == 0 || lane == 32))
+        kbits[w0 + (lane >> 5)] = lane ? (uint32_t)(m >> 32) : (uint32_t)m;
+}
+// (A/B, KDTN_KD_SUB=34) the load floor: offsets and the 7-dword window, a hash ballot
+__global__ void __launch_bounds__(BLOCK) k_kdict_loadonly(const uint8_t* bytes, const uint32_t* offs, uint32_t first,
+                                                          uint32_t n, uint32_t* kbits, uint32_t kb_words, uint32_t*) {
+    const uint32_t i = first + blockIdx.x * BLOCK + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const uint32_t ic = i < n ? i : n;
+    const uint32_t b = offs[ic];
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(bytes + (b & ~3u));
+    uint32_t h = 0;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) h = h * 31u + p[k];
+    const uint64_t m = __ballot(h & 1u);
+    const uint32_t w0 = (i - lane) >> 5;
+    if (w0 < kb_words && (lane == 0 || lane == 32))
+        kbits[w0 + (lane >> 5)] = lane ? (uint32_t)(m >> 32) : (uint32_t)m;
+}
 template __global__ void k_kdict_flags<1, true, BLOCK>(const uint8_t*, const uint32_t*, uint32_t, uint32_t, uint32_t*, uint32_t, uint32_t*);
 template __global__ void k_kdict_flags<2, false, BLOCK>(const uint8_t*, const uint32_t*, uint32_t, uint32_t, uint32_t*, uint32_t, uint32_t*);
 template __global__ void k_kdict_flags<4, false, BLOCK>(

@@ -135,9 +135,13 @@ def reconcile(inp: EpochInput, tick: float = 15.625, vxlan_base: int = 5000, pod
     if t_end is None:
         t_end = T
     cin = inp.to_c()
-    out = BatchesOut.alloc(t_end - t_begin, max(inp.realised.n, 1), max(inp.desired.n, 1),
-                           max(inp.realised.n, 1))
-    b = out.to_c((max(inp.realised.n, 1), max(inp.desired.n, 1), max(inp.realised.n, 1)))
+    # a range's lists hold at most its own records: del and upd (one per realised record,
+    # repeated for duplicate old keys) its realised records, add its desired records
+    T0 = inp.topos
+    cap_r = max(int(T0.real_off[t_end]) - int(T0.real_off[t_begin]), 1)
+    cap_d = max(int(T0.des_off[t_end]) - int(T0.des_off[t_begin]), 1)
+    out = BatchesOut.alloc(t_end - t_begin, cap_r, cap_d, cap_r)
+    b = out.to_c((cap_r, cap_d, cap_r))
     pp = None
     if pods is not None:
         keep = {k: np.ascontiguousarray(v, dtype=np.uint8 if k == "flags" else np.uint32)
@@ -153,6 +157,41 @@ def reconcile(inp: EpochInput, tick: float = 15.625, vxlan_base: int = 5000, pod
     if rc != 0:
         raise RuntimeError(f"oracle reconcile failed: {rc}")
     return out.trim(b.n_del, b.n_add, b.n_upd)
+
+
+def reconcile_parallel(inp: EpochInput, tick: float = 15.625, vxlan_base: int = 5000, pods=None,
+                       t_begin: int = 0, t_end: int | None = None, threads: int = 0) -> BatchesOut:
+    """reconcile() over [t_begin, t_end) split into `threads` disjoint topology ranges of
+    about equal record counts (the reference's concurrent reconcilers, each topology
+    independent), run concurrently (the ctypes call releases the GIL) and concatenated: the
+    same BatchesOut as one reconcile() call, so full-size epochs check bit for bit in seconds."""
+    from concurrent.futures import ThreadPoolExecutor
+    T = inp.topos.n
+    if t_end is None:
+        t_end = T
+    threads = threads or max(1, min(16, len(os.sched_getaffinity(0))))
+    w = (inp.topos.des_off.astype(np.int64) + inp.topos.real_off.astype(np.int64))
+    cuts = np.searchsorted(w, np.linspace(w[t_begin], w[t_end], threads + 1))
+    cuts = np.clip(cuts, t_begin, t_end)
+    cuts[0], cuts[-1] = t_begin, t_end
+    bounds = sorted(set(int(c) for c in cuts))
+    parts_ = list(zip(bounds[:-1], bounds[1:]))
+    if not parts_:
+        return reconcile(inp, tick, vxlan_base, pods, t_begin, t_end)
+    with ThreadPoolExecutor(len(parts_)) as ex:
+        parts = list(ex.map(lambda r: reconcile(inp, tick, vxlan_base, pods, r[0], r[1]), parts_))
+
+    def offs(name):
+        out, base = [np.zeros(1, np.uint32)], 0
+        for p in parts:
+            o = getattr(p, name).astype(np.int64)
+            out.append((o[1:] + base).astype(np.uint32))
+            base += int(o[-1])
+        return np.concatenate(out)
+    cat = lambda name: np.concatenate([getattr(p, name) for p in parts])
+    return BatchesOut(cat("action"), offs("del_off"), offs("add_off"), offs("upd_off"),
+                      cat("del_idx"), cat("add_idx"), cat("upd_idx"), cat("del_res"), cat("add_res"),
+                      cat("upd_res"), cat("add_qdisc"), cat("upd_qdisc"))
 
 
 def _wire_lib():
