@@ -920,6 +920,7 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
                 k_kdict_flags_pp<<<nb, BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
             }
             else if (sub == 40) k_kdict_null<<<nblocks(nk), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
+            else if (sub == 42) k_kdict_flags_v1<<<nblocks(nk), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
             else if (sub == 41) k_kdict_loadonly<<<nblocks(nk), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
             else if (sub == 64) k_kdict_flags<1, false, 64><<<nblocks(nk, 64), 64, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
             else if (sub == 1024) k_kdict_flags<1, false, 1024><<<nblocks(nk, 1024), 1024, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);

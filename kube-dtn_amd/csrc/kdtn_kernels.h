@@ -229,6 +229,8 @@ __global__ void k_kdict_flags_ws(const uint8_t* bytes, const uint32_t* offs, uin
                                  uint32_t* kbits, uint32_t kb_words, uint32_t* special);
 __global__ void k_kdict_flags_pp(const uint8_t* bytes, const uint32_t* offs, uint32_t first, uint32_t n,
                                  uint32_t* kbits, uint32_t kb_words, uint32_t* special);
+__global__ void k_kdict_flags_v1(const uint8_t* bytes, const uint32_t* offs, uint32_t first, uint32_t n,
+                                 uint32_t* kbits, uint32_t kb_words, uint32_t* special);
 __global__ void k_kdict_null(const uint8_t* bytes, const uint32_t* offs, uint32_t first, uint32_t n,
                              uint32_t* kbits, uint32_t kb_words, uint32_t* special);
 __global__ void k_kdict_loadonly(const uint8_t* bytes, const uint32_t* offs, uint32_t first, uint32_t n,

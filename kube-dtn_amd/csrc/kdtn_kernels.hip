@@ -197,6 +197,74 @@ KD_INLINE bool cidr_swar(const uint32_t* w, uint32_t len, bool* slow) {
     return ok && bits <= 32u;
 }
 
+// High-bit byte masks of two words → 8 position bits (bytes of lo at bits 0-3, of hi at 4-7):
+// lo >> 7 and hi >> 3 put the flags at bits 8j and 8j + 4, and one multiply by
+// 2^21 + 2^14 + 2^7 + 1 moves byte j's pair to bits 21 + j and 25 + j; the cross products land
+// on distinct bits outside [21, 29), so nothing carries into the field.
+KD_INLINE uint32_t swar_nib8(uint32_t lo, uint32_t hi) {
+    return __builtin_amdgcn_ubfe(((lo >> 7) | (hi >> 3)) * 0x204081u, 21, 8);
+}
+// net.ParseCIDR validity from the register image, same contract as cidr_swar (decides every
+// string of <= 24 bytes except the ones it routes to cidr_ok through *slow), with fewer VALU
+// operations — k_kdict_flags is VALU-issue bound (380 VALU instructions per wave at HEAD,
+// 4 cycles each on a SIMD16 = the kernel's time). No IPv4 CIDR with a prefix of <= 2 digits is
+// longer than 18 bytes ("255.255.255.255/32"), so strings of <= 18 bytes are classified over
+// five words in byte space with one range test: every byte of a valid one is in '.'..'9'
+// (0x2E-0x39), the separators are the bytes below '0', and bit 0 tells '/' from '.'.
+// Longer strings only need the routing decision: every slow case contains a '/'.
+KD_INLINE bool cidr_swar2(const uint32_t* w, uint32_t len, bool* slow) {
+    if (len > 18u) {
+        uint32_t any = 0;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const uint32_t lm = len >= 4u * k + 4u ? 0xFFFFFFFFu : len <= 4u * k ? 0u : (1u << (8u * (len - 4u * k))) - 1u;
+            any |= swar_eq(w[k], 0x2F2F2F2Fu) & lm;
+        }
+        *slow = any != 0u;
+        return false;
+    }
+    uint32_t r[5], d[5], s[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const uint32_t x = w[k], t = x & 0x7F7F7F7Fu;
+        const uint32_t ge2e = t + 0x52525252u, ge3a = t + 0x46464646u, ge30 = t + 0x50505050u;
+        r[k] = ge2e & ~ge3a & ~x & 0x80808080u;                 // '.' .. '9'
+        const uint32_t sep = r[k] & ~ge30;                       // '.' or '/'
+        s[k] = sep & (x << 7);                                   // '/'
+        d[k] = sep & ~(x << 7);                                  // '.'
+    }
+    const uint32_t L = (1u << len) - 1u;
+    const uint32_t R = (swar_nib8(r[0], r[1]) | (swar_nib8(r[2], r[3]) << 8) | (swar_nib8(r[4], 0u) << 16)) & L;
+    const uint32_t P = (swar_nib8(d[0], d[1]) | (swar_nib8(d[2], d[3]) << 8) | (swar_nib8(d[4], 0u) << 16)) & L;
+    const uint32_t S = (swar_nib8(s[0], s[1]) | (swar_nib8(s[2], s[3]) << 8) | (swar_nib8(s[4], 0u) << 16)) & L;
+    const uint32_t D = R & ~(P | S);
+    const uint32_t sl = __builtin_ctz(S | 0x1000000u);          // first '/' (24 if none)
+    const uint32_t m = len - sl - 1u;                            // prefix digits
+    bool sv = (D & 1u) != 0u && m > 2u && sl < len;              // long prefix: generic parser
+    if (R != L && S != 0u) {                                     // IPv6 candidate: a ':' and a '/'
+        uint32_t c = 0;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) c |= swar_nib(swar_eq(w[k], 0x3A3A3A3Au)) << (4 * k);
+        sv |= (c & L) != 0u;
+    }
+    *slow = sv;
+    const uint32_t sep = P | S;
+    uint32_t ok = (R == L) & (__builtin_popcount(P) == 3) & (__builtin_popcount(S) == 1) &
+                  ((P >> sl) == 0u) & ((sep & (sep << 1)) == 0u) & (D & 1u) & (sl + 1u < len) & (sl <= 15u);
+    if (!ok) return false;                                       // positions below are in range
+    const uint32_t p1 = __builtin_ctz(P);
+    const uint32_t P2 = P & (P - 1u);
+    const uint32_t p2 = __builtin_ctz(P2);
+    const uint32_t p3 = __builtin_ctz(P2 & (P2 - 1u));
+    ok &= octet_ok(window4(w, 0), p1);
+    ok &= octet_ok(window4(w, p1 + 1u), p2 - p1 - 1u);
+    ok &= octet_ok(window4(w, p2 + 1u), p3 - p2 - 1u);
+    ok &= octet_ok(window4(w, p3 + 1u), sl - p3 - 1u);
+    const uint32_t c = window4(w, sl + 1u);                      // dtoi(prefix) <= 32
+    const uint32_t bits = m == 1u ? (c & 0xFFu) - '0' : ((c & 0xFFu) - '0') * 10u + (((c >> 8) & 0xFFu) - '0');
+    return ok && bits <= 32u;
+}
+
 // One thread per key string, no LDS: the first 24 bytes are loaded as 7 aligned dwords and
 // funnel-shifted into registers; CIDR/MAC validity, "localhost", "physical/" and "default"
 // are decided there with SWAR class masks (no per-character control flow: the scalar unit,
@@ -205,6 +273,7 @@ KD_INLINE bool cidr_swar(const uint32_t* w, uint32_t len, bool* slow) {
 // the generic parsers (kdtn_parse.h) on global memory. Each wave packs its 64
 // predicate bits per set with a ballot (two u32 words per set, lanes 0 and 32).
 // Predicate bits of one key string from its register image (first 24 bytes in w[]).
+template <bool V1 = false>          // V1: the round-2 classifier (cidr_swar), A/B only
 KD_INLINE uint32_t kdict_bits(const uint8_t* bytes, uint32_t b, uint32_t len, const uint32_t* w, uint32_t i,
                               uint32_t* special) {
     uint32_t f = 0;
@@ -215,7 +284,7 @@ KD_INLINE uint32_t kdict_bits(const uint8_t* bytes, uint32_t b, uint32_t len, co
         f = (1u << KB_CIDR_BAD) | (1u << KB_MAC_BAD);
     } else if (len) {
         bool slow = true, cok = false;
-        if (len <= 24) cok = cidr_swar(w, len, &slow);
+        if (len <= 24) cok = V1 ? cidr_swar(w, len, &slow) : cidr_swar2(w, len, &slow);
         if (slow) cok = cidr_ok(bytes + b, len);                       // common/veth.go:22
         if (!cok) f |= 1u << KB_CIDR_BAD;
         const uint32_t c2 = wbyte(w, 2), c4 = wbyte(w, 4);
@@ -396,7 +465,33 @@ __global__ void __launch_bounds__(BLOCK) k_kdict_flags_pp(const uint8_t* bytes, 
         for (int k = 0; k < 7; ++k) d[k] = nd[k];
     }
 }
-// (A/B, KDTN_KD_SUB=33) the launch floor: offsets only, one ballot store per wave and set
+// (A/B, KDTN_KD_SUB=42) the product kernel with the round-2 classifier (cidr_swar)
+__global__ void __launch_bounds__(BLOCK) k_kdict_flags_v1(const uint8_t* bytes, const uint32_t* offs, uint32_t first,
+                                                          uint32_t n, uint32_t* kbits, uint32_t kb_words,
+                                                          uint32_t* special) {
+    const uint32_t i = first + blockIdx.x * BLOCK + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const uint32_t ic = i < n ? i : n;
+    const uint32_t b = offs[ic];
+    const uint32_t len = (i < n ? offs[ic + 1] : b) - b;
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(bytes + (b & ~3u));
+    uint32_t d[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) d[k] = p[k];
+    const uint32_t sh = (b & 3u) * 8u;
+    uint32_t w[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) w[k] = sh ? (d[k] >> sh) | (d[k + 1] << (32u - sh)) : d[k];
+    const uint32_t f = i < n ? kdict_bits<true>(bytes, b, len, w, i, special) : 0u;
+    const uint32_t w0 = (i - lane) >> 5;
+#pragma unroll
+    for (int k = 0; k < KB_NSETS; ++k) {
+        const uint64_t m = __ballot((f >> k) & 1u);
+        if (w0 < kb_words && (lane == 0 || lane == 32))
+            kbits[(size_t)k * kb_words + w0 + (lane >> 5)] = lane ? (uint32_t)(m >> 32) : (uint32_t)m;
+    }
+}
+// (A/B, KDTN_KD_SUB=40) the launch floor: offsets only, one ballot store per wave and set
 __global__ void __launch_bounds__(BLOCK) k_kdict_null(const uint8_t* bytes, const uint32_t* offs, uint32_t first,
                                                       uint32_t n, uint32_t* kbits, uint32_t kb_words, uint32_t*) {
     const uint32_t i = first + blockIdx.x * BLOCK + threadIdx.x;
@@ -409,7 +504,7 @@ __global__ void __launch_bounds__(BLOCK) k_kdict_null(const uint8_t* bytes, cons
     if (w0 < kb_words && (lane == 0 || lane == 32))
         kbits[w0 + (lane >> 5)] = lane ? (uint32_t)(m >> 32) : (uint32_t)m;
 }
-// (A/B, KDTN_KD_SUB=34) the load floor: offsets and the 7-dword window, a hash ballot
+// (A/B, KDTN_KD_SUB=41) the load floor: offsets and the 7-dword window, a hash ballot
 __global__ void __launch_bounds__(BLOCK) k_kdict_loadonly(const uint8_t* bytes, const uint32_t* offs, uint32_t first,
                                                           uint32_t n, uint32_t* kbits, uint32_t kb_words, uint32_t*) {
     const uint32_t i = first + blockIdx.x * BLOCK + threadIdx.x;

@@ -152,6 +152,16 @@ def test_key_predicates_fuzz(engine):
     ips += ["0" * 30 + "1.2.3.4/8", "1.2.3.4/" + "0" * 25 + "8", "255.255.255.255/32", "1.2.3.4/32x"]
     ips += ["1" * k + ".2.3.4/8" for k in (1500, 1800, 2100, 2400, 2700, 3000, 3300, 3600)]
     ips += ["localhost", "default", "physical/1.2.3.4"] + [f"10.{k}.0.1/24" for k in range(40)]
+    # the byte-range classifier: bytes next to '.'..'9' (',' '-' ':' ';'), non-ASCII bytes whose
+    # low 7 bits are '.' / '/' / digits (U+00AE, U+00AF, U+00B1), lengths around 18 / 19 / 24
+    near = "0123456789./:-,;\u00ae\u00af\u00b1"
+    ips += ["".join(rng.choice(near) for _ in range(rng.randint(1, 24))) for _ in range(600)]
+    ips += [_mutate(rng, f"{rng.randint(0, 255)}.{rng.randint(0, 255)}.{rng.randint(0, 255)}."
+                         f"{rng.randint(0, 255)}/{rng.randint(0, 32)}", near) for _ in range(600)]
+    ips += ["::1/128", "1::/64", "fe80::1/64", "::ffff:1.2.3.4/96", "1.2.3.4/00000000032", "10.10.10.10/000032",
+            "255.255.255.255/032", "255.255.255.255/3", "255.255.255.25/32", "1.2.3.4/\u00b2", "1.2.3.4\u00ae5/8",
+            "1.2.3.4/8/", "1.2.3.4//8", "1..3.4/8", ".1.2.3/8", "1.2.3.4./8", "01.2.3.4/8", "1.2.3.04/8",
+            "0.0.0.0/0", "1.2.3.256/8", "1.2.3.4/33", "1.2.3.4/-1", "123.123.123.123/12", "123.123.123.123/1"]
     macs = [":".join(f"{rng.randint(0, 255):02x}" for _ in range(rng.choice([6, 8, 20])))
             for _ in range(300)]
     macs += [_mutate(rng, rng.choice(macs), maca) for _ in range(700)]
