@@ -125,6 +125,16 @@ KD_INLINE uint32_t window4(const uint32_t* w, uint32_t q) {
     const uint32_t hi = i == 0 ? w[1] : i == 1 ? w[2] : i == 2 ? w[3] : i == 3 ? w[4] : w[5];
     return __builtin_amdgcn_alignbyte(hi, lo, q & 3u);
 }
+// the same for q <= 19 without control flow: word pairs selected by the bits of q >> 2
+// (window4's nested selects compiled to branches and exec-mask updates per window)
+KD_INLINE uint32_t window4_bf(const uint32_t* w, uint32_t q) {
+    const uint32_t i = q >> 2;
+    const bool o = i & 1u, t = i & 2u, f = i & 4u;
+    const uint32_t l0 = o ? w[1] : w[0], h0 = o ? w[2] : w[1];
+    const uint32_t l1 = o ? w[3] : w[2], h1 = o ? w[4] : w[3];
+    const uint32_t lo = f ? w[4] : t ? l1 : l0, hi = f ? w[5] : t ? h1 : h0;
+    return __builtin_amdgcn_alignbyte(hi, lo, q & 3u);
+}
 KD_INLINE bool hexb(uint32_t c) { return (c - '0' < 10u) | ((c | 0x20u) - 'a' < 6u); }
 // high bit of each byte set where the byte is a hex digit [0-9a-fA-F]
 KD_INLINE uint32_t swar_hex(uint32_t x) {
@@ -256,11 +266,11 @@ KD_INLINE bool cidr_swar2(const uint32_t* w, uint32_t len, bool* slow) {
     const uint32_t P2 = P & (P - 1u);
     const uint32_t p2 = __builtin_ctz(P2);
     const uint32_t p3 = __builtin_ctz(P2 & (P2 - 1u));
-    ok &= octet_ok(window4(w, 0), p1);
-    ok &= octet_ok(window4(w, p1 + 1u), p2 - p1 - 1u);
-    ok &= octet_ok(window4(w, p2 + 1u), p3 - p2 - 1u);
-    ok &= octet_ok(window4(w, p3 + 1u), sl - p3 - 1u);
-    const uint32_t c = window4(w, sl + 1u);                      // dtoi(prefix) <= 32
+    ok &= octet_ok(w[0], p1);
+    ok &= octet_ok(window4_bf(w, p1 + 1u), p2 - p1 - 1u);
+    ok &= octet_ok(window4_bf(w, p2 + 1u), p3 - p2 - 1u);
+    ok &= octet_ok(window4_bf(w, p3 + 1u), sl - p3 - 1u);
+    const uint32_t c = window4_bf(w, sl + 1u);                      // dtoi(prefix) <= 32
     const uint32_t bits = m == 1u ? (c & 0xFFu) - '0' : ((c & 0xFFu) - '0') * 10u + (((c >> 8) & 0xFFu) - '0');
     return ok && bits <= 32u;
 }
