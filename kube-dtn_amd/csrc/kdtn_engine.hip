@@ -62,6 +62,9 @@ struct kdtn_ctx {
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
     hipStream_t comm_stream = nullptr;          // RCCL pod-status exchange (nranks > 1)
+    hipStream_t pod_stream = nullptr;           // pod lookup tables, beside the dictionary parses
+    hipStream_t pod_stream_hi = nullptr;        // the same at the highest stream priority
+    hipEvent_t ev_begin = nullptr, ev_pods = nullptr;
     hipEvent_t ev_fill = nullptr, ev_ag = nullptr;
     // dictionaries; parsed tables persist across uploads for an append-only interner
     // (kdtn_epoch_in.kdict_keep / pdict_keep): *_valid strings have valid parsed tables, a run
@@ -748,6 +751,8 @@ void kdtn_destroy(kdtn_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
+    if (c->pod_stream) (void)hipStreamSynchronize(c->pod_stream);
+    if (c->pod_stream_hi) (void)hipStreamSynchronize(c->pod_stream_hi);
     DevBuf* bufs[] = {&c->kd_bytes, &c->kd_offs, &c->kd_bits, &c->pd_bytes, &c->pd_offs,
                       &c->pd_pct, &c->pd_dur, &c->pd_rate, &c->pd_rerr, &c->t_ns, &c->t_name, &c->t_src,
                       &c->t_netns, &c->t_flags, &c->t_roff, &c->t_noff, &c->real.buf, &c->des.buf,
@@ -784,6 +789,10 @@ void kdtn_destroy(kdtn_ctx* c) {
     if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
     if (c->ev_fill) (void)hipEventDestroy(c->ev_fill);
     if (c->ev_ag) (void)hipEventDestroy(c->ev_ag);
+    if (c->pod_stream) (void)hipStreamDestroy(c->pod_stream);
+    if (c->pod_stream_hi) (void)hipStreamDestroy(c->pod_stream_hi);
+    if (c->ev_begin) (void)hipEventDestroy(c->ev_begin);
+    if (c->ev_pods) (void)hipEventDestroy(c->ev_pods);
     if (c->h_misc) (void)hipHostFree(c->h_misc);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
@@ -874,18 +883,49 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
     }
     if (c->timing >= 2) (void)hipEventRecord(c->ev[0], s);
     uint32_t* sync = dp<uint32_t>(c->sync);
+    // The epoch's first launch (sync header, look-back area, this rank's pod-status rows), the
+    // exchange, the pod lookup tables (direct slots, overflow verify) and the full-prefix scan
+    // need nothing from the dictionary parses (the scatter can read the name's "physical/"
+    // prefix from its bytes), so they could run on a side stream beside the parses, with
+    // k_reconcile waiting for them (the side stream starting after everything enqueued before).
+    // side_mode (A/B, profiling build only, KDTN_SIDE): 0 everything on this stream, 1 the
+    // lookup tables on a side stream, 2 also the first launch, 3 as 2 on a high-priority stream
+    // Measured (tools/side_ab.py, profiles/r03u_side_ab.json, config 2): 0.789 / 0.791 / 0.796 /
+    // 0.796 ms per epoch for modes 0-3 — the side-stream kernels only get CUs as the parse's
+    // waves retire and slow it down — so the product keeps everything on one stream.
+#if KDTN_PROFILING
+    int side_mode = 0;
+    if (const char* ev = std::getenv("KDTN_SIDE")) side_mode = std::atoi(ev);
+#else
+    constexpr int side_mode = 0;
+#endif
+    const bool side = side_mode > 0 && resolve && c->pod_total && !pods_cur;
+    hipStream_t bs = s, ps = nullptr;
+    if (side) {
+        if (!c->pod_stream) {
+            int lo = 0, hi = 0;
+            HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+            HIP_TRY(hipStreamCreateWithFlags(&c->pod_stream, hipStreamNonBlocking));
+            HIP_TRY(hipStreamCreateWithPriority(&c->pod_stream_hi, hipStreamNonBlocking, hi));
+            HIP_TRY(hipEventCreateWithFlags(&c->ev_begin, hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&c->ev_pods, hipEventDisableTiming));
+        }
+        ps = side_mode >= 3 ? c->pod_stream_hi : c->pod_stream;
+        if (side_mode >= 2) bs = ps;
+        HIP_TRY(hipEventRecord(c->ev_begin, s));
+        HIP_TRY(hipStreamWaitEvent(ps, c->ev_begin, 0));
+    }
     {
         // one launch zeroes the sync header (SYNC_*) and look-back area and fills this rank's
         // pod-status rows: across ranks they are all-gathered over RCCL on the comm stream
-        // while this stream parses the dictionaries (the exchange needs neither)
         const uint32_t n16 = (uint32_t)(sync_bytes(c->nwg) / 16);
         const uint32_t nbz = std::min<uint32_t>(nblocks(n16), 256);
         const uint32_t fill = (resolve && !host_xchg && !pods_cur) ? c->slice : 0u;
         const uint32_t rank_base = c->slice * (uint32_t)c->rank;
-        k_epoch_begin<<<nbz + nblocks(fill), BLOCK, 0, s>>>(reinterpret_cast<uint4*>(sync), n16, nbz, T, fill,
-                                                            rank_base, dp<uint4>(c->pods));
+        k_epoch_begin<<<nbz + nblocks(fill), BLOCK, 0, bs>>>(reinterpret_cast<uint4*>(sync), n16, nbz, T, fill,
+                                                             rank_base, dp<uint4>(c->pods));
         if (exchange) {
-            HIP_TRY(hipEventRecord(c->ev_fill, s));
+            HIP_TRY(hipEventRecord(c->ev_fill, bs));
             HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_fill, 0));
             uint4* pods = dp<uint4>(c->pods);
             ncclResult_t r = ncclAllGather(pods + rank_base, pods, (size_t)c->slice * 4, ncclUint32, c->comm,
@@ -897,6 +937,25 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
             HIP_TRY(hipEventRecord(c->ev_ag, c->comm_stream));
         }
         timer_mark(c, "pods_fill", 2);
+    }
+    if (side) {
+        if (exchange) HIP_TRY(hipStreamWaitEvent(ps, c->ev_ag, 0));
+        if (++c->pod_stamp >= 0x7FFFFFFFu) {                          // stamp wrap: clear once
+            HIP_TRY(hipMemsetAsync(c->pod_direct.p, 0, c->pod_direct.cap, ps));
+            HIP_TRY(hipMemsetAsync(c->pod_ovf.p, 0, c->pod_ovf.cap, ps));
+            c->pod_stamp = 1;
+        }
+        const uint32_t nr = c->pods_rank_major ? (uint32_t)c->nranks : 1u;
+        k_pod_direct_scatter_str<<<nblocks(c->pod_total), BLOCK, 0, ps>>>(
+            dp<uint4>(c->pods), c->pod_total, dp<uint8_t>(c->kd_bytes), dp<uint32_t>(c->kd_offs),
+            dp<uint4>(c->pod_direct), c->pod_stamp, c->D, nr);
+        const uint32_t nbv = nblocks(c->pod_total);
+        const uint32_t nbp = (uint32_t)std::min<uint64_t>(4 * FP_GRID, (c->T + 4 * BLOCK - 1) / (4 * BLOCK));
+        k_pod_verify_prefix<<<nbv + std::max<uint32_t>(nbp, 1), BLOCK, 0, ps>>>(
+            dp<uint4>(c->pods), c->pod_total, dp<uint4>(c->pod_direct), c->pod_stamp,
+            dp<unsigned long long>(c->pod_ovf), c->ovf_mask, c->D, T, sync + SYNC_FIRST_PARTIAL_INV, nbv, nr);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(c->ev_pods, ps));
     }
     // dictionaries: the strings this upload added (all of them unless kdict_keep /
     // pdict_keep), from a multiple of 64 so every wave writes whole predicate words
@@ -938,18 +997,16 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
     c->pd_valid = c->P;
     timer_mark(c, "pdict_parse", 2);
     if (resolve) {
-        if (exchange) HIP_TRY(hipStreamWaitEvent(s, c->ev_ag, 0));   // exchange not hidden by the parses
-        timer_mark(c, "pods_allgather", 2);
-        if (!pods_cur && ++c->pod_stamp >= 0x7FFFFFFFu) {             // stamp wrap: clear once
+        if (exchange && !side) HIP_TRY(hipStreamWaitEvent(s, c->ev_ag, 0));
+        if (!side && !pods_cur && ++c->pod_stamp >= 0x7FFFFFFFu) {    // (no pods: the stamp still ticks)
             HIP_TRY(hipMemsetAsync(c->pod_direct.p, 0, c->pod_direct.cap, s));
             HIP_TRY(hipMemsetAsync(c->pod_ovf.p, 0, c->pod_ovf.cap, s));
             c->pod_stamp = 1;
         }
-        if (c->pod_total && !pods_cur) {
+        if (!side && c->pod_total && !pods_cur)
             k_pod_direct_scatter<<<nblocks(c->pod_total), BLOCK, 0, s>>>(
                 dp<uint4>(c->pods), c->pod_total, dp<uint32_t>(c->kd_bits) + (size_t)KB_PHYSICAL * c->kb_words,
                 dp<uint4>(c->pod_direct), c->pod_stamp, c->D, c->pods_rank_major ? (uint32_t)c->nranks : 1u);
-        }
         if (c->V) {
             const size_t vcap = (size_t)c->vni_mask + 1;
             HIP_TRY(hipMemsetAsync(c->v_slots.p, 0xFF, vcap * 4, s));
@@ -1019,7 +1076,10 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
 #if KDTN_PROFILING
         if (const char* ev = std::getenv("KDTN_SPLIT")) if (std::atoi(ev) > 0) w.split = (uint32_t)std::atoi(ev);
 #endif
-        if (resolve && c->pod_total && !pods_cur) {     // the pod-table verify with the full-prefix scan
+        if (side) {                                     // pod tables + full-prefix scan (side stream)
+            HIP_TRY(hipStreamWaitEvent(s, c->ev_pods, 0));
+            timer_mark(c, exchange ? "pods_allgather" : "pod_tables_wait", 2);   // exchange + tables
+        } else if (resolve && c->pod_total && !pods_cur) {   // the pod-table verify with the full-prefix scan
             const uint32_t nbv = nblocks(c->pod_total);
             const uint32_t nbp = (uint32_t)std::min<uint64_t>(4 * FP_GRID, (c->T + 4 * BLOCK - 1) / (4 * BLOCK));
             k_pod_verify_prefix<<<nbv + std::max<uint32_t>(nbp, 1), BLOCK, 0, s>>>(

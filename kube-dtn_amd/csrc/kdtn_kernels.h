@@ -247,6 +247,9 @@ __global__ void k_epoch_begin(uint4* sync, uint32_t n16, uint32_t nbz, DevTopos 
                               uint4* pods);
 __global__ void k_pod_direct_scatter(const uint4* pods, uint32_t total, const uint32_t* phys_bits,
                                      uint4* slots, uint32_t stamp, uint32_t nd, uint32_t nr);
+__global__ void k_pod_direct_scatter_str(const uint4* pods, uint32_t total, const uint8_t* kd_bytes,
+                                         const uint32_t* kd_offs, uint4* slots, uint32_t stamp, uint32_t nd,
+                                         uint32_t nr);
 __global__ void k_pod_direct_verify(const uint4* pods, uint32_t total, uint4* slots, uint32_t stamp,
                                     unsigned long long* ovf, uint32_t mask, uint32_t nd);
 __global__ void k_vni_ht_build(const uint4* ents, uint32_t n, uint32_t* slots, uint32_t mask);

@@ -725,6 +725,28 @@ __global__ void __launch_bounds__(BLOCK) k_pod_direct_scatter(const uint4* pods,
                             e.z | ((e.w & 0x7FFFFFFFu) == 0 ? 0x80000000u : 0u), stamp << 1);
 }
 
+// The same with the name's "physical/" prefix (handler.go:348) read from its bytes instead of
+// k_kdict_flags' PHYSICAL bit, so the lookup tables need nothing from the dictionary parse and
+// are built on a side stream while the parses run (the arena has 64 B of slack past its end).
+__global__ void __launch_bounds__(BLOCK) k_pod_direct_scatter_str(const uint4* pods, uint32_t total,
+                                                                  const uint8_t* kd_bytes, const uint32_t* kd_offs,
+                                                                  uint4* slots, uint32_t stamp, uint32_t nd,
+                                                                  uint32_t nr) {
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= total) return;
+    const uint32_t g = pod_order(t, total, nr);
+    const uint4 e = pods[g];
+    if (e.x == 0xFFFFFFFFu || e.y >= nd) return;           // padding row / name outside this dictionary
+    const uint32_t b = kd_offs[e.y], len = kd_offs[e.y + 1] - b;
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(kd_bytes + (b & ~3u));
+    const uint32_t d0 = p[0], d1 = p[1], d2 = p[2], d3 = p[3], sh = b & 3u;
+    const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh), w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+    const uint32_t w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
+    const uint32_t phys = (len >= 9 && w0 == 0x73796870u && w1 == 0x6C616369u && (w2 & 0xFFu) == '/') ? 1u : 0u;
+    slots[e.y] = make_uint4(e.x, (g << 2) | (phys << 1) | (e.w >> 31),
+                            e.z | ((e.w & 0x7FFFFFFFu) == 0 ? 0x80000000u : 0u), stamp << 1);
+}
+
 // Pods whose name slot was won by another pod: mark the name `multi` and put both pods
 // into the overflow table (duplicates are rare; the table then answers every lookup of
 // that name).
