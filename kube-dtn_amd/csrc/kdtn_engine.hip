@@ -62,9 +62,6 @@ struct kdtn_ctx {
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
     hipStream_t comm_stream = nullptr;          // RCCL pod-status exchange (nranks > 1)
-    hipStream_t pod_stream = nullptr;           // pod lookup tables, beside the dictionary parses
-    hipStream_t pod_stream_hi = nullptr;        // the same at the highest stream priority
-    hipEvent_t ev_begin = nullptr, ev_pods = nullptr;
     hipEvent_t ev_fill = nullptr, ev_ag = nullptr;
     // dictionaries; parsed tables persist across uploads for an append-only interner
     // (kdtn_epoch_in.kdict_keep / pdict_keep): *_valid strings have valid parsed tables, a run
@@ -751,8 +748,6 @@ void kdtn_destroy(kdtn_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
-    if (c->pod_stream) (void)hipStreamSynchronize(c->pod_stream);
-    if (c->pod_stream_hi) (void)hipStreamSynchronize(c->pod_stream_hi);
     DevBuf* bufs[] = {&c->kd_bytes, &c->kd_offs, &c->kd_bits, &c->pd_bytes, &c->pd_offs,
                       &c->pd_pct, &c->pd_dur, &c->pd_rate, &c->pd_rerr, &c->t_ns, &c->t_name, &c->t_src,
                       &c->t_netns, &c->t_flags, &c->t_roff, &c->t_noff, &c->real.buf, &c->des.buf,
@@ -789,10 +784,6 @@ void kdtn_destroy(kdtn_ctx* c) {
     if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
     if (c->ev_fill) (void)hipEventDestroy(c->ev_fill);
     if (c->ev_ag) (void)hipEventDestroy(c->ev_ag);
-    if (c->pod_stream) (void)hipStreamDestroy(c->pod_stream);
-    if (c->pod_stream_hi) (void)hipStreamDestroy(c->pod_stream_hi);
-    if (c->ev_begin) (void)hipEventDestroy(c->ev_begin);
-    if (c->ev_pods) (void)hipEventDestroy(c->ev_pods);
     if (c->h_misc) (void)hipHostFree(c->h_misc);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
@@ -863,6 +854,20 @@ int kdtn_epoch_upload(kdtn_ctx* c, const kdtn_epoch_in* in) {
     return KDTN_OK;
 }
 
+// The VxlanManager snapshot's lookup table on the context stream (k_vni_pack / _ht_build / _fill).
+static int build_vni_table(kdtn_ctx* c) {
+    hipStream_t s = c->stream;
+    const size_t vcap = (size_t)c->vni_mask + 1;
+    HIP_TRY(hipMemsetAsync(c->v_slots.p, 0xFF, vcap * 4, s));
+    k_vni_pack<<<nblocks(c->V), BLOCK, 0, s>>>(dp<uint32_t>(c->v_node), dp<int32_t>(c->v_vni),
+                                              dp<uint32_t>(c->v_netns), c->V, dp<uint4>(c->v_ents));
+    k_vni_ht_build<<<nblocks(c->V), BLOCK, 0, s>>>(dp<uint4>(c->v_ents), c->V, dp<uint32_t>(c->v_slots),
+                                                  c->vni_mask);
+    k_vni_fill<<<nblocks(vcap), BLOCK, 0, s>>>(dp<uint4>(c->v_ents), dp<uint32_t>(c->v_slots), (uint32_t)vcap,
+                                               dp<uint4>(c->v_table));
+    return KDTN_OK;
+}
+
 int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
     if (!c || !c->uploaded) return KDTN_EINVAL;
     HIP_TRY(hipSetDevice(c->device));
@@ -883,142 +888,133 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
     }
     if (c->timing >= 2) (void)hipEventRecord(c->ev[0], s);
     uint32_t* sync = dp<uint32_t>(c->sync);
-    // The epoch's first launch (sync header, look-back area, this rank's pod-status rows), the
-    // exchange, the pod lookup tables (direct slots, overflow verify) and the full-prefix scan
-    // need nothing from the dictionary parses (the scatter can read the name's "physical/"
-    // prefix from its bytes), so they could run on a side stream beside the parses, with
-    // k_reconcile waiting for them (the side stream starting after everything enqueued before).
-    // side_mode (A/B, profiling build only, KDTN_SIDE): 0 everything on this stream, 1 the
-    // lookup tables on a side stream, 2 also the first launch, 3 as 2 on a high-priority stream
-    // Measured (tools/side_ab.py, profiles/r03u_side_ab.json, config 2): 0.789 / 0.791 / 0.796 /
-    // 0.796 ms per epoch for modes 0-3 — the side-stream kernels only get CUs as the parse's
-    // waves retire and slow it down — so the product keeps everything on one stream.
+    // Epoch front: first launch (sync header, look-back area, pod-status rows) + RCCL
+    // all-gather, the dictionary parses, the pod lookup tables, in sequence. The tables need
+    // nothing from the parses, but running them beside the parses did not shorten the epoch
+    // (config 2): on a side stream 0.791-0.796 vs 0.789 ms (profiles/r03u_side_ab.json), fused
+    // into the parse launches (k_epoch_front + k_pdict_verify, profiling build, KDTN_FUSE=1)
+    // 0.7895 vs 0.7882 ms (profiles/r03v_fuse_ab.json): the launch's blocks add up, they do not
+    // overlap.
 #if KDTN_PROFILING
-    int side_mode = 0;
-    if (const char* ev = std::getenv("KDTN_SIDE")) side_mode = std::atoi(ev);
+    int fuse_mode = 0;
+    if (const char* ev = std::getenv("KDTN_FUSE")) fuse_mode = std::atoi(ev);
 #else
-    constexpr int side_mode = 0;
+    constexpr int fuse_mode = 0;
 #endif
-    const bool side = side_mode > 0 && resolve && c->pod_total && !pods_cur;
-    hipStream_t bs = s, ps = nullptr;
-    if (side) {
-        if (!c->pod_stream) {
-            int lo = 0, hi = 0;
-            HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-            HIP_TRY(hipStreamCreateWithFlags(&c->pod_stream, hipStreamNonBlocking));
-            HIP_TRY(hipStreamCreateWithPriority(&c->pod_stream_hi, hipStreamNonBlocking, hi));
-            HIP_TRY(hipEventCreateWithFlags(&c->ev_begin, hipEventDisableTiming));
-            HIP_TRY(hipEventCreateWithFlags(&c->ev_pods, hipEventDisableTiming));
-        }
-        ps = side_mode >= 3 ? c->pod_stream_hi : c->pod_stream;
-        if (side_mode >= 2) bs = ps;
-        HIP_TRY(hipEventRecord(c->ev_begin, s));
-        HIP_TRY(hipStreamWaitEvent(ps, c->ev_begin, 0));
-    }
-    {
-        // one launch zeroes the sync header (SYNC_*) and look-back area and fills this rank's
-        // pod-status rows: across ranks they are all-gathered over RCCL on the comm stream
-        const uint32_t n16 = (uint32_t)(sync_bytes(c->nwg) / 16);
-        const uint32_t nbz = std::min<uint32_t>(nblocks(n16), 256);
-        const uint32_t fill = (resolve && !host_xchg && !pods_cur) ? c->slice : 0u;
-        const uint32_t rank_base = c->slice * (uint32_t)c->rank;
-        k_epoch_begin<<<nbz + nblocks(fill), BLOCK, 0, bs>>>(reinterpret_cast<uint4*>(sync), n16, nbz, T, fill,
-                                                             rank_base, dp<uint4>(c->pods));
-        if (exchange) {
-            HIP_TRY(hipEventRecord(c->ev_fill, bs));
-            HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_fill, 0));
-            uint4* pods = dp<uint4>(c->pods);
-            ncclResult_t r = ncclAllGather(pods + rank_base, pods, (size_t)c->slice * 4, ncclUint32, c->comm,
-                                           c->comm_stream);
-            if (r != ncclSuccess) {
-                std::snprintf(g_last_error, sizeof(g_last_error), "ncclAllGather: %s", ncclGetErrorString(r));
-                return KDTN_EIO;
-            }
-            HIP_TRY(hipEventRecord(c->ev_ag, c->comm_stream));
-        }
-        timer_mark(c, "pods_fill", 2);
-    }
-    if (side) {
-        if (exchange) HIP_TRY(hipStreamWaitEvent(ps, c->ev_ag, 0));
-        if (++c->pod_stamp >= 0x7FFFFFFFu) {                          // stamp wrap: clear once
-            HIP_TRY(hipMemsetAsync(c->pod_direct.p, 0, c->pod_direct.cap, ps));
-            HIP_TRY(hipMemsetAsync(c->pod_ovf.p, 0, c->pod_ovf.cap, ps));
-            c->pod_stamp = 1;
-        }
-        const uint32_t nr = c->pods_rank_major ? (uint32_t)c->nranks : 1u;
-        k_pod_direct_scatter_str<<<nblocks(c->pod_total), BLOCK, 0, ps>>>(
-            dp<uint4>(c->pods), c->pod_total, dp<uint8_t>(c->kd_bytes), dp<uint32_t>(c->kd_offs),
-            dp<uint4>(c->pod_direct), c->pod_stamp, c->D, nr);
-        const uint32_t nbv = nblocks(c->pod_total);
-        const uint32_t nbp = (uint32_t)std::min<uint64_t>(4 * FP_GRID, (c->T + 4 * BLOCK - 1) / (4 * BLOCK));
-        k_pod_verify_prefix<<<nbv + std::max<uint32_t>(nbp, 1), BLOCK, 0, ps>>>(
-            dp<uint4>(c->pods), c->pod_total, dp<uint4>(c->pod_direct), c->pod_stamp,
-            dp<unsigned long long>(c->pod_ovf), c->ovf_mask, c->D, T, sync + SYNC_FIRST_PARTIAL_INV, nbv, nr);
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(c->ev_pods, ps));
-    }
-    // dictionaries: the strings this upload added (all of them unless kdict_keep /
-    // pdict_keep), from a multiple of 64 so every wave writes whole predicate words
+    const bool fused = fuse_mode && resolve && !pods_cur && c->nranks == 1 && !c->comm && c->pod_total &&
+                       c->pod_total == c->slice;
     uint32_t* special = dp<uint32_t>(c->kd_special);
-    {
-        const uint32_t k0 = c->kd_from & ~63u;                        // (clip_specials ran at upload)
-        if (c->D > k0) {
-            const uint8_t* kb = dp<uint8_t>(c->kd_bytes);
-            const uint32_t* ko = dp<uint32_t>(c->kd_offs);
-            uint32_t* bits = dp<uint32_t>(c->kd_bits);
-            const uint32_t nk = c->D - k0;
+    const uint32_t n16 = (uint32_t)(sync_bytes(c->nwg) / 16);
+    const uint32_t nbz = std::min<uint32_t>(nblocks(n16), 256);
 #if KDTN_PROFILING
-            int sub = 1;                                               // strings per thread (2, 4: slower)
-            if (const char* ev = std::getenv("KDTN_KD_SUB")) sub = std::atoi(ev);
-            if (sub == 4) k_kdict_flags<4, false, BLOCK><<<nblocks(nk, BLOCK * 4), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
-            else if (sub == 2) k_kdict_flags<2, false, BLOCK><<<nblocks(nk, BLOCK * 2), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
-            else if (sub == 8) k_kdict_flags<1, true, BLOCK><<<nblocks(nk), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
-            else if (sub == 16) k_kdict_flags_ws<<<nblocks(nk), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
-            else if (sub >= 32 && sub < 40) {
-                const uint32_t nb = std::min(nblocks(nk), (uint32_t)(c->n_cus * 8 * (sub - 31)));
-                k_kdict_flags_pp<<<nb, BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
-            }
-            else if (sub == 40) k_kdict_null<<<nblocks(nk), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
-            else if (sub == 42) k_kdict_flags_v1<<<nblocks(nk), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
-            else if (sub == 41) k_kdict_loadonly<<<nblocks(nk), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
-            else if (sub == 64) k_kdict_flags<1, false, 64><<<nblocks(nk, 64), 64, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
-            else if (sub == 1024) k_kdict_flags<1, false, 1024><<<nblocks(nk, 1024), 1024, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
-            else
-#endif
-            k_kdict_flags<1, false, BLOCK><<<nblocks(nk), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
-        }
-    }
-    timer_mark(c, "kdict_parse", 2);
-    {
-        const uint32_t p0 = c->pd_from & ~63u;
-        if (c->P > p0) launch_pdict(c, p0, c->P);
-    }
-    c->kd_valid = c->D;
-    c->pd_valid = c->P;
-    timer_mark(c, "pdict_parse", 2);
-    if (resolve) {
-        if (exchange && !side) HIP_TRY(hipStreamWaitEvent(s, c->ev_ag, 0));
-        if (!side && !pods_cur && ++c->pod_stamp >= 0x7FFFFFFFu) {    // (no pods: the stamp still ticks)
+    if (fused) {
+        if (++c->pod_stamp >= 0x7FFFFFFFu) {                             // stamp wrap: clear once
             HIP_TRY(hipMemsetAsync(c->pod_direct.p, 0, c->pod_direct.cap, s));
             HIP_TRY(hipMemsetAsync(c->pod_ovf.p, 0, c->pod_ovf.cap, s));
             c->pod_stamp = 1;
         }
-        if (!side && c->pod_total && !pods_cur)
-            k_pod_direct_scatter<<<nblocks(c->pod_total), BLOCK, 0, s>>>(
-                dp<uint4>(c->pods), c->pod_total, dp<uint32_t>(c->kd_bits) + (size_t)KB_PHYSICAL * c->kb_words,
-                dp<uint4>(c->pod_direct), c->pod_stamp, c->D, c->pods_rank_major ? (uint32_t)c->nranks : 1u);
+        const uint32_t k0 = c->kd_from & ~63u, p0 = c->pd_from & ~63u;  // (clip_specials ran at upload)
+        const uint32_t nbs = nblocks(c->slice);
+        const uint32_t nbk = c->D > k0 ? nblocks(c->D - k0) : 0u;
+        k_epoch_front<<<nbz + nbs + nbk, BLOCK, 0, s>>>(
+            reinterpret_cast<uint4*>(sync), n16, nbz, nbs, T, c->slice, dp<uint4>(c->pods), dp<uint4>(c->pod_direct),
+            c->pod_stamp, dp<uint8_t>(c->kd_bytes), dp<uint32_t>(c->kd_offs), k0, c->D, dp<uint32_t>(c->kd_bits),
+            c->kb_words, special);
+        timer_mark(c, "epoch_front", 2);
         if (c->V) {
-            const size_t vcap = (size_t)c->vni_mask + 1;
-            HIP_TRY(hipMemsetAsync(c->v_slots.p, 0xFF, vcap * 4, s));
-            k_vni_pack<<<nblocks(c->V), BLOCK, 0, s>>>(dp<uint32_t>(c->v_node), dp<int32_t>(c->v_vni),
-                                                      dp<uint32_t>(c->v_netns), c->V, dp<uint4>(c->v_ents));
-            k_vni_ht_build<<<nblocks(c->V), BLOCK, 0, s>>>(dp<uint4>(c->v_ents), c->V, dp<uint32_t>(c->v_slots),
-                                                          c->vni_mask);
-            k_vni_fill<<<nblocks(vcap), BLOCK, 0, s>>>(dp<uint4>(c->v_ents), dp<uint32_t>(c->v_slots), (uint32_t)vcap,
-                                                       dp<uint4>(c->v_table));
+            TRY(build_vni_table(c));
+            timer_mark(c, "hash_build", 2);
         }
-        timer_mark(c, "hash_build", 2);
+        const uint32_t nbv = nblocks(c->pod_total);
+        const uint32_t nbp = std::max<uint32_t>(1, (uint32_t)std::min<uint64_t>(4 * FP_GRID, (c->T + 4 * BLOCK - 1) / (4 * BLOCK)));
+        const uint32_t nbd = c->P > p0 ? nblocks(c->P - p0) : 0u;
+        k_pdict_verify<<<nbv + nbp + 3 * nbd, BLOCK, 0, s>>>(
+            dp<uint4>(c->pods), c->pod_total, dp<uint4>(c->pod_direct), c->pod_stamp, dp<unsigned long long>(c->pod_ovf),
+            c->ovf_mask, c->D, T, sync + SYNC_FIRST_PARTIAL_INV, nbv, nbp, dp<uint8_t>(c->pd_bytes),
+            dp<uint32_t>(c->pd_offs), p0, c->P, nbd, c->cfg.tick_in_usec, dp<uint32_t>(c->pd_pct), dp<uint2>(c->pd_dur),
+            dp<uint2>(c->pd_rate), dp<uint32_t>(c->pd_rerr));
+        timer_mark(c, "pdict_verify", 2);
+    } else
+#endif
+    {
+        {
+            // one launch zeroes the sync header (SYNC_*) and look-back area and fills this rank's
+            // pod-status rows: across ranks they are all-gathered over RCCL on the comm stream
+            // while this stream parses the dictionaries (the exchange needs neither)
+            const uint32_t fill = (resolve && !host_xchg && !pods_cur) ? c->slice : 0u;
+            const uint32_t rank_base = c->slice * (uint32_t)c->rank;
+            k_epoch_begin<<<nbz + nblocks(fill), BLOCK, 0, s>>>(reinterpret_cast<uint4*>(sync), n16, nbz, T, fill,
+                                                                rank_base, dp<uint4>(c->pods));
+            if (exchange) {
+                HIP_TRY(hipEventRecord(c->ev_fill, s));
+                HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_fill, 0));
+                uint4* pods = dp<uint4>(c->pods);
+                ncclResult_t r = ncclAllGather(pods + rank_base, pods, (size_t)c->slice * 4, ncclUint32, c->comm,
+                                               c->comm_stream);
+                if (r != ncclSuccess) {
+                    std::snprintf(g_last_error, sizeof(g_last_error), "ncclAllGather: %s", ncclGetErrorString(r));
+                    return KDTN_EIO;
+                }
+                HIP_TRY(hipEventRecord(c->ev_ag, c->comm_stream));
+            }
+            timer_mark(c, "pods_fill", 2);
+        }
+        // dictionaries: the strings this upload added (all of them unless kdict_keep /
+        // pdict_keep), from a multiple of 64 so every wave writes whole predicate words
+        uint32_t* special = dp<uint32_t>(c->kd_special);
+        {
+            const uint32_t k0 = c->kd_from & ~63u;                        // (clip_specials ran at upload)
+            if (c->D > k0) {
+                const uint8_t* kb = dp<uint8_t>(c->kd_bytes);
+                const uint32_t* ko = dp<uint32_t>(c->kd_offs);
+                uint32_t* bits = dp<uint32_t>(c->kd_bits);
+                const uint32_t nk = c->D - k0;
+    #if KDTN_PROFILING
+                int sub = 1;                                               // strings per thread (2, 4: slower)
+                if (const char* ev = std::getenv("KDTN_KD_SUB")) sub = std::atoi(ev);
+                if (sub == 4) k_kdict_flags<4, false, BLOCK><<<nblocks(nk, BLOCK * 4), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
+                else if (sub == 2) k_kdict_flags<2, false, BLOCK><<<nblocks(nk, BLOCK * 2), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
+                else if (sub == 8) k_kdict_flags<1, true, BLOCK><<<nblocks(nk), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
+                else if (sub == 16) k_kdict_flags_ws<<<nblocks(nk), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
+                else if (sub >= 32 && sub < 40) {
+                    const uint32_t nb = std::min(nblocks(nk), (uint32_t)(c->n_cus * 8 * (sub - 31)));
+                    k_kdict_flags_pp<<<nb, BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
+                }
+                else if (sub == 40) k_kdict_null<<<nblocks(nk), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
+                else if (sub == 42) k_kdict_flags_v1<<<nblocks(nk), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
+                else if (sub == 41) k_kdict_loadonly<<<nblocks(nk), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
+                else if (sub == 64) k_kdict_flags<1, false, 64><<<nblocks(nk, 64), 64, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
+                else if (sub == 1024) k_kdict_flags<1, false, 1024><<<nblocks(nk, 1024), 1024, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
+                else
+    #endif
+                k_kdict_flags<1, false, BLOCK><<<nblocks(nk), BLOCK, 0, s>>>(kb, ko, k0, c->D, bits, c->kb_words, special);
+            }
+        }
+        timer_mark(c, "kdict_parse", 2);
+        {
+            const uint32_t p0 = c->pd_from & ~63u;
+            if (c->P > p0) launch_pdict(c, p0, c->P);
+        }
+        timer_mark(c, "pdict_parse", 2);
+        if (resolve) {
+            if (exchange) HIP_TRY(hipStreamWaitEvent(s, c->ev_ag, 0));   // exchange not hidden by the parses
+            timer_mark(c, "pods_allgather", 2);
+            if (!pods_cur && ++c->pod_stamp >= 0x7FFFFFFFu) {             // stamp wrap: clear once
+                HIP_TRY(hipMemsetAsync(c->pod_direct.p, 0, c->pod_direct.cap, s));
+                HIP_TRY(hipMemsetAsync(c->pod_ovf.p, 0, c->pod_ovf.cap, s));
+                c->pod_stamp = 1;
+            }
+            if (c->pod_total && !pods_cur) {
+                k_pod_direct_scatter<<<nblocks(c->pod_total), BLOCK, 0, s>>>(
+                    dp<uint4>(c->pods), c->pod_total, dp<uint32_t>(c->kd_bits) + (size_t)KB_PHYSICAL * c->kb_words,
+                    dp<uint4>(c->pod_direct), c->pod_stamp, c->D, c->pods_rank_major ? (uint32_t)c->nranks : 1u);
+            }
+            if (c->V) TRY(build_vni_table(c));
+            timer_mark(c, "hash_build", 2);
+        }
     }
+    c->kd_valid = c->D;
+    c->pd_valid = c->P;
     if (c->T) {
         DevTables tb{};
         tb.kbits = dp<uint32_t>(c->kd_bits);
@@ -1076,9 +1072,7 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
 #if KDTN_PROFILING
         if (const char* ev = std::getenv("KDTN_SPLIT")) if (std::atoi(ev) > 0) w.split = (uint32_t)std::atoi(ev);
 #endif
-        if (side) {                                     // pod tables + full-prefix scan (side stream)
-            HIP_TRY(hipStreamWaitEvent(s, c->ev_pods, 0));
-            timer_mark(c, exchange ? "pods_allgather" : "pod_tables_wait", 2);   // exchange + tables
+        if (fused) {                                    // verify + prefix ran in k_pdict_verify
         } else if (resolve && c->pod_total && !pods_cur) {   // the pod-table verify with the full-prefix scan
             const uint32_t nbv = nblocks(c->pod_total);
             const uint32_t nbp = (uint32_t)std::min<uint64_t>(4 * FP_GRID, (c->T + 4 * BLOCK - 1) / (4 * BLOCK));

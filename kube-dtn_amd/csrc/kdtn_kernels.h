@@ -247,9 +247,15 @@ __global__ void k_epoch_begin(uint4* sync, uint32_t n16, uint32_t nbz, DevTopos 
                               uint4* pods);
 __global__ void k_pod_direct_scatter(const uint4* pods, uint32_t total, const uint32_t* phys_bits,
                                      uint4* slots, uint32_t stamp, uint32_t nd, uint32_t nr);
-__global__ void k_pod_direct_scatter_str(const uint4* pods, uint32_t total, const uint8_t* kd_bytes,
-                                         const uint32_t* kd_offs, uint4* slots, uint32_t stamp, uint32_t nd,
-                                         uint32_t nr);
+__global__ void k_epoch_front(uint4* sync, uint32_t n16, uint32_t nbz, uint32_t nbs, DevTopos T, uint32_t slice,
+                              uint4* pods, uint4* slots, uint32_t stamp, const uint8_t* kd_bytes,
+                              const uint32_t* kd_offs, uint32_t k0, uint32_t D, uint32_t* kbits, uint32_t kb_words,
+                              uint32_t* special);
+__global__ void k_pdict_verify(const uint4* pods, uint32_t total, uint4* slots, uint32_t stamp,
+                               unsigned long long* ovf, uint32_t mask, uint32_t nd, DevTopos T,
+                               uint32_t* first_partial_inv, uint32_t nbv, uint32_t nbp, const uint8_t* pbytes,
+                               const uint32_t* poffs, uint32_t p0, uint32_t np, uint32_t nbd, double tick,
+                               uint32_t* ppct, uint2* pdur, uint2* prate, uint32_t* rate_err);
 __global__ void k_pod_direct_verify(const uint4* pods, uint32_t total, uint4* slots, uint32_t stamp,
                                     unsigned long long* ovf, uint32_t mask, uint32_t nd);
 __global__ void k_vni_ht_build(const uint4* ents, uint32_t n, uint32_t* slots, uint32_t mask);

@@ -327,6 +327,33 @@ __global__ void k_special_clip(uint32_t* special, uint32_t k0) {
     if ((t == SPECIAL_DEFAULT || t == SPECIAL_LOCALHOST) && special[t] >= k0) special[t] = 0xFFFFFFFFu;
 }
 
+// One block of k_kdict_flags (strings [i0 - tid, +BLOCK), i0 = this thread's string; the block
+// start a multiple of 64: every wave writes whole predicate words).
+KD_INLINE void kdict_block(const uint8_t* bytes, const uint32_t* offs, uint32_t s0, uint32_t n, uint32_t* kbits,
+                           uint32_t kb_words, uint32_t* special) {
+    const uint32_t i = s0 + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const uint32_t ic = i < n ? i : n;                   // offs[n] exists
+    const uint32_t b = offs[ic];
+    const uint32_t len = (i < n ? offs[ic + 1] : b) - b;
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(bytes + (b & ~3u));   // arena has 64 B slack
+    uint32_t d[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) d[k] = p[k];
+    const uint32_t sh = (b & 3u) * 8u;
+    uint32_t w[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) w[k] = sh ? (d[k] >> sh) | (d[k + 1] << (32u - sh)) : d[k];
+    const uint32_t f = i < n ? kdict_bits(bytes, b, len, w, i, special) : 0u;
+    const uint32_t w0 = (i - lane) >> 5;                 // first word of this wave
+#pragma unroll
+    for (int k = 0; k < KB_NSETS; ++k) {
+        const uint64_t m = __ballot((f >> k) & 1u);
+        if (w0 < kb_words && (lane == 0 || lane == 32))
+            kbits[(size_t)k * kb_words + w0 + (lane >> 5)] = lane ? (uint32_t)(m >> 32) : (uint32_t)m;
+    }
+}
+
 // SUB strings per thread (block covers SUB*BLOCK consecutive strings): every offset load
 // of the thread's strings is issued, then every string's 7 dwords, then the parses run —
 // the kernel is latency-bound, so a wave keeps SUB strings' round trips in flight at once.
@@ -721,28 +748,6 @@ __global__ void __launch_bounds__(BLOCK) k_pod_direct_scatter(const uint4* pods,
     const uint4 e = pods[g];
     if (e.x == 0xFFFFFFFFu || e.y >= nd) return;           // padding row / name outside this dictionary
     const uint32_t phys = (phys_bits[e.y >> 5] >> (e.y & 31)) & 1u;
-    slots[e.y] = make_uint4(e.x, (g << 2) | (phys << 1) | (e.w >> 31),
-                            e.z | ((e.w & 0x7FFFFFFFu) == 0 ? 0x80000000u : 0u), stamp << 1);
-}
-
-// The same with the name's "physical/" prefix (handler.go:348) read from its bytes instead of
-// k_kdict_flags' PHYSICAL bit, so the lookup tables need nothing from the dictionary parse and
-// are built on a side stream while the parses run (the arena has 64 B of slack past its end).
-__global__ void __launch_bounds__(BLOCK) k_pod_direct_scatter_str(const uint4* pods, uint32_t total,
-                                                                  const uint8_t* kd_bytes, const uint32_t* kd_offs,
-                                                                  uint4* slots, uint32_t stamp, uint32_t nd,
-                                                                  uint32_t nr) {
-    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
-    if (t >= total) return;
-    const uint32_t g = pod_order(t, total, nr);
-    const uint4 e = pods[g];
-    if (e.x == 0xFFFFFFFFu || e.y >= nd) return;           // padding row / name outside this dictionary
-    const uint32_t b = kd_offs[e.y], len = kd_offs[e.y + 1] - b;
-    const uint32_t* p = reinterpret_cast<const uint32_t*>(kd_bytes + (b & ~3u));
-    const uint32_t d0 = p[0], d1 = p[1], d2 = p[2], d3 = p[3], sh = b & 3u;
-    const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh), w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
-    const uint32_t w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
-    const uint32_t phys = (len >= 9 && w0 == 0x73796870u && w1 == 0x6C616369u && (w2 & 0xFFu) == '/') ? 1u : 0u;
     slots[e.y] = make_uint4(e.x, (g << 2) | (phys << 1) | (e.w >> 31),
                             e.z | ((e.w & 0x7FFFFFFFu) == 0 ? 0x80000000u : 0u), stamp << 1);
 }
@@ -1614,6 +1619,76 @@ __global__ void __launch_bounds__(BLOCK) k_pod_verify_prefix(const uint4* pods, 
     }
     full_prefix_blocks<BLOCK>(T, first_partial_inv, blockIdx.x - nbv, gridDim.x - nbv, &bmin);
 }
+
+#if KDTN_PROFILING
+// ---- (A/B, KDTN_FUSE=1) fused epoch front (one local rank: no exchange) ------------------
+// Measured no faster than the launches in sequence (0.7895 vs 0.7882 ms per config-2 epoch,
+// profiles/r03v_fuse_ab.json), so only the profiling build has these kernels.
+// The pod tables' memory-bound work shares launches with the VALU-bound dictionary parses (a
+// side stream only got CUs as the parse's waves retired: profiles/r03u_side_ab.json).
+// k_epoch_front: blocks [0, nbz) zero the sync header and look-back area; [nbz, nbz + nbs)
+// fill this rank's pod-status rows and scatter each into its direct lookup slot (the row is
+// computed from the topology table here, the "physical/" prefix of the name read from its
+// bytes, so nothing waits for the parse); the rest parse the key strings (k_kdict_flags).
+// Memory-bound blocks come first, so they are dispatched before the parse's.
+__global__ void __launch_bounds__(BLOCK) k_epoch_front(uint4* sync, uint32_t n16, uint32_t nbz, uint32_t nbs,
+                                                       DevTopos T, uint32_t slice, uint4* pods, uint4* slots,
+                                                       uint32_t stamp, const uint8_t* kd_bytes,
+                                                       const uint32_t* kd_offs, uint32_t k0, uint32_t D,
+                                                       uint32_t* kbits, uint32_t kb_words, uint32_t* special) {
+    const uint32_t b = blockIdx.x;
+    if (b < nbz) {
+        for (uint32_t i = b * BLOCK + threadIdx.x; i < n16; i += nbz * BLOCK) sync[i] = make_uint4(0u, 0u, 0u, 0u);
+        return;
+    }
+    if (b < nbz + nbs) {
+        const uint32_t t = (b - nbz) * BLOCK + threadIdx.x;
+        if (t >= slice) return;
+        pods_fill_one(T, slice, 0u, pods, t);
+        if (t >= T.n) return;                                   // padding row
+        const uint32_t name = T.name[t];
+        if (name >= D) return;
+        const uint32_t ob = kd_offs[name], len = kd_offs[name + 1] - ob;
+        const uint32_t* p = reinterpret_cast<const uint32_t*>(kd_bytes + (ob & ~3u));
+        const uint32_t d0 = p[0], d1 = p[1], d2 = p[2], d3 = p[3], sh = ob & 3u;
+        const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh), w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+        const uint32_t w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
+        const uint32_t phys = (len >= 9 && w0 == 0x73796870u && w1 == 0x6C616369u && (w2 & 0xFFu) == '/') ? 1u : 0u;
+        const uint32_t netns = T.net_ns[t];
+        const uint32_t nil = (T.flags[t] & KDTN_TOPO_SPEC_NIL) ? 1u : 0u;
+        slots[name] = make_uint4(T.ns[t], (t << 2) | (phys << 1) | nil, T.src_ip[t] | (netns == 0 ? 0x80000000u : 0u),
+                                 stamp << 1);
+        return;
+    }
+    kdict_block(kd_bytes, kd_offs, k0 + (b - nbz - nbs) * BLOCK, D, kbits, kb_words, special);
+}
+
+// k_pdict_verify: blocks [0, nbv) verify the lookup slots (names shared by several pods →
+// overflow table), [nbv, nbv + nbp) scan the topologies for the first partial chunk
+// (k_full_prefix), the rest parse the property strings, interpretation (b - nbv - nbp) / nbd.
+__global__ void __launch_bounds__(BLOCK) k_pdict_verify(const uint4* pods, uint32_t total, uint4* slots, uint32_t stamp,
+                                                        unsigned long long* ovf, uint32_t mask, uint32_t nd,
+                                                        DevTopos T, uint32_t* first_partial_inv, uint32_t nbv,
+                                                        uint32_t nbp, const uint8_t* pbytes, const uint32_t* poffs,
+                                                        uint32_t p0, uint32_t np, uint32_t nbd, double tick,
+                                                        uint32_t* ppct, uint2* pdur, uint2* prate, uint32_t* rate_err) {
+    __shared__ uint4 buf[STAGE / 16];
+    const uint32_t b = blockIdx.x;
+    if (b < nbv) {
+        const uint32_t t = b * BLOCK + threadIdx.x;
+        if (t < total) pod_verify_one(pods, total, slots, stamp, ovf, mask, nd, t);
+        return;
+    }
+    if (b < nbv + nbp) {
+        full_prefix_blocks<BLOCK>(T, first_partial_inv, b - nbv, nbp, reinterpret_cast<uint32_t*>(buf));
+        return;
+    }
+    const uint32_t q = b - nbv - nbp, y = q / nbd, s0 = p0 + (q - y * nbd) * BLOCK;
+    if (y == 0) pdict_parse_block<PD_PCT>(pbytes, poffs, s0, np, tick, ppct, pdur, prate, rate_err, buf);
+    else if (y == 1) pdict_parse_block<PD_DUR>(pbytes, poffs, s0, np, tick, ppct, pdur, prate, rate_err, buf);
+    else pdict_parse_block<PD_RATE>(pbytes, poffs, s0, np, tick, ppct, pdur, prate, rate_err, buf);
+}
+#endif
 
 // (VAR_TRACE) phase timestamp of this workgroup: 100 MHz chip-wide clock
 template <int V>

@@ -1,8 +1,9 @@
-"""A/B of where the epoch's pod-table work runs (KDTN_SIDE, profiling build): 0 all on the
-engine stream, 1 lookup tables on a side stream beside the dictionary parses, 2 also the first
-launch, 3 as 2 at the highest stream priority. Config-2 epochs at timing level 0, modes
-interleaved, median wall time of run + sync per epoch.
-Usage: python tools/side_ab.py [--pods 1000000] [--reps 30] [--modes 0,1,2,3]"""
+"""A/B of the epoch front (profiling build): --knob KDTN_FUSE (0 the launches in sequence,
+1 the pod-table work fused into the dictionary-parse launches; round 3 also measured KDTN_SIDE,
+a side stream for the tables, since removed: profiles/r03u_side_ab.json). Config-2 epochs at
+timing level 0, modes interleaved, median wall time of run + sync per epoch; every mode must
+produce the same epoch.
+Usage: python tools/side_ab.py [--pods 1000000] [--reps 30] [--knob KDTN_FUSE] [--modes 0,1]"""
 import argparse
 import json
 import os
@@ -18,7 +19,8 @@ from kdtn import engine as _e  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--pods", type=int, default=1_000_000)
 ap.add_argument("--reps", type=int, default=30)
-ap.add_argument("--modes", default="0,1,2,3")
+ap.add_argument("--modes", default="0,1")
+ap.add_argument("--knob", default="KDTN_FUSE")
 ap.add_argument("--cache", default="")
 a = ap.parse_args()
 _e.use_profiling_library()
@@ -30,7 +32,7 @@ with Engine(device=0) as eng:
     acc = {m: [] for m in modes}
     kt = {}
     for m in modes:                                     # level-2 stage times, one per mode
-        os.environ["KDTN_SIDE"] = m
+        os.environ[a.knob] = m
         eng.set_timing(2)
         for _ in range(3):
             eng.run()
@@ -43,7 +45,7 @@ with Engine(device=0) as eng:
     eng.set_timing(0)
     for r in range(a.reps + 3):
         for m in modes:
-            os.environ["KDTN_SIDE"] = m
+            os.environ[a.knob] = m
             t0 = time.perf_counter()
             eng.run()
             eng.sync()
