@@ -574,17 +574,19 @@ def main():
             run()
             eng.sync()
         barrier(world)
+        eng.timer_totals(reset=True)
         t_start = time.perf_counter()
         counts = None
         for _ in range(steps):
             run()
-            counts = eng.sync()
-            for k, v in eng.kernel_times().items():
-                ksum[k] = ksum.get(k, 0.0) + v
+            counts = eng.sync()                  # also sums this epoch's HIP-event times
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t_start
         barrier(world)
         elapsed = allmax(elapsed, world)
+        for k, (v, n) in eng.timer_totals(reset=True).items():
+            assert n == steps, (k, n, steps)                  # every timed epoch was marked
+            ksum[k] = ksum.get(k, 0.0) + v
         links_local = inp.desired.n * steps
         eng.set_timing(2)
         for _ in range(min(steps, 5)):                    # per-stage breakdown (untimed)

@@ -658,6 +658,12 @@ int kdtn_vni_download(kdtn_ctx* ctx, kdtn_vni_state* out);
  * 1 k_reconcile and the placement kernels only, 2 every stage (default). */
 int kdtn_set_timing(kdtn_ctx* ctx, int level);
 int kdtn_last_kernel_times(kdtn_ctx* ctx, const char** names, float* ms, int cap);
+/* The same marks summed over every epoch synced (kdtn_epoch_sync) since the last reset:
+ * names[i], ms[i] (sum over epochs), epochs[i] (epochs that marked it); returns the count.
+ * reset != 0 clears the totals after reading (call once with reset = 1 before a timed loop).
+ * Instrumentation only (no reference counterpart): lets a timed loop read the HIP-event
+ * times once instead of once per epoch. */
+int kdtn_timer_totals(kdtn_ctx* ctx, const char** names, double* ms, uint32_t* epochs, int cap, int reset);
 /* Per-workgroup phase timestamps of k_reconcile (100 MHz clock; 8 words per workgroup:
  * entry, topologies loaded, counts done, batch bases known, end, XCC_ID<<32|HW_ID, CalcDiff
  * window phase A done, phase B done) of the

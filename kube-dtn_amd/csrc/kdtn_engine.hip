@@ -168,6 +168,12 @@ struct kdtn_ctx {
     hipEvent_t ev[kMaxTimers + 1] = {};
     const char* ev_name[kMaxTimers] = {};
     int n_ev = 0;
+    // per-stage HIP-event times summed over the epochs synced since the last reset
+    // (kdtn_timer_totals): a timed loop reads them once instead of once per epoch
+    const char* acc_name[kMaxTimers] = {};
+    double acc_ms[kMaxTimers] = {};
+    uint32_t acc_n[kMaxTimers] = {};
+    int n_acc = 0;
 };
 
 namespace {
@@ -738,7 +744,9 @@ int kdtn_init(kdtn_ctx** out, const kdtn_config* cfg) {
         delete c;
         return KDTN_ENOMEM;
     }
-    for (int i = 0; i <= kMaxTimers; ++i) (void)hipEventCreate(&c->ev[i]);
+    // timing events only (read after a stream sync): no system-scope fence, whose L2 write-back
+    // and invalidate at every mark cost the timed epoch stream time
+    for (int i = 0; i <= kMaxTimers; ++i) (void)hipEventCreateWithFlags(&c->ev[i], hipEventDisableSystemFence);
     *out = c;
     return KDTN_OK;
 }
@@ -1157,7 +1165,36 @@ int kdtn_epoch_sync(kdtn_ctx* c, kdtn_counts* counts) {
         counts->n_add = c->h_misc[3];
         counts->n_topos = c->T;
     }
+    for (int i = 0; i < c->n_ev; ++i) {                 // this epoch's marks into the totals
+        float t = 0.f;
+        (void)hipEventElapsedTime(&t, c->ev[i], c->ev[i + 1]);
+        int k = 0;
+        while (k < c->n_acc && std::strcmp(c->acc_name[k], c->ev_name[i]) != 0) ++k;
+        if (k == c->n_acc) {
+            if (k == kMaxTimers) continue;
+            c->acc_name[k] = c->ev_name[i];
+            c->acc_ms[k] = 0.0;
+            c->acc_n[k] = 0;
+            ++c->n_acc;
+        }
+        c->acc_ms[k] += t;
+        bool first = true;                              // a stage marked in pieces counts once
+        for (int j = 0; j < i; ++j) first &= std::strcmp(c->ev_name[j], c->ev_name[i]) != 0;
+        if (first) ++c->acc_n[k];
+    }
     return KDTN_OK;
+}
+
+int kdtn_timer_totals(kdtn_ctx* c, const char** names, double* ms, uint32_t* epochs, int cap, int reset) {
+    if (!c || cap < 0) return KDTN_EINVAL;
+    const int n = std::min(cap, c->n_acc);
+    for (int i = 0; i < n; ++i) {
+        if (names) names[i] = c->acc_name[i];
+        if (ms) ms[i] = c->acc_ms[i];
+        if (epochs) epochs[i] = c->acc_n[i];
+    }
+    if (reset) c->n_acc = 0;
+    return n;
 }
 
 int kdtn_epoch_download(kdtn_ctx* c, kdtn_batches* o) {

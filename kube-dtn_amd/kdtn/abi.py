@@ -193,7 +193,7 @@ EXPORTS = ["kdtn_version", "kdtn_strerror", "kdtn_err_name", "kdtn_init", "kdtn_
            "kdtn_interner_free", "kdtn_intern", "kdtn_intern_batch", "kdtn_interner_table",
            "kdtn_reconcile_epoch", "kdtn_epoch_upload", "kdtn_epoch_run", "kdtn_epoch_sync",
            "kdtn_epoch_download", "kdtn_make_qdiscs", "kdtn_comm_unique_id", "kdtn_comm_init",
-           "kdtn_set_timing", "kdtn_epoch_vni_apply", "kdtn_vni_contested", "kdtn_vni_download", "kdtn_last_kernel_times", "kdtn_debug_wg_trace", "kdtn_epoch_encode",
+           "kdtn_set_timing", "kdtn_epoch_vni_apply", "kdtn_vni_contested", "kdtn_vni_download", "kdtn_last_kernel_times", "kdtn_timer_totals", "kdtn_debug_wg_trace", "kdtn_epoch_encode",
            "kdtn_epoch_download_wire", "kdtn_diff", "kdtn_resolve", "kdtn_host_alloc",
            "kdtn_host_free", "kdtn_epoch_fanout", "kdtn_epoch_tc", "kdtn_epoch_download_tc",
            "kdtn_json_upload", "kdtn_json_ingest", "kdtn_ingest_download", "kdtn_topology_shard",

@@ -79,6 +79,8 @@ def lib() -> C.CDLL:
         "kdtn_vni_contested": (C.c_int, [vp, vp, vp, C.c_uint32, C.POINTER(C.c_uint32)]),
         "kdtn_vni_download": (C.c_int, [vp, C.POINTER(abi.VniState)]),
         "kdtn_last_kernel_times": (C.c_int, [vp, C.POINTER(C.c_char_p), C.POINTER(C.c_float), C.c_int]),
+        "kdtn_timer_totals": (C.c_int, [vp, C.POINTER(C.c_char_p), C.POINTER(C.c_double),
+                                        C.POINTER(C.c_uint32), C.c_int, C.c_int]),
         "kdtn_debug_wg_trace": (C.c_int, [vp, C.POINTER(C.c_uint64), C.c_uint32]),
         "kdtn_epoch_encode": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
         "kdtn_diff": (C.c_int, [vp, C.POINTER(abi.EpochIn), C.POINTER(abi.Batches)]),
@@ -531,6 +533,15 @@ class Engine:
             k = names[i].decode()
             out[k] = out.get(k, 0.0) + float(ms[i])
         return out
+
+    def timer_totals(self, reset: bool = False) -> dict[str, tuple[float, int]]:
+        """kdtn_timer_totals: {stage: (ms summed over the epochs synced since the last reset,
+        epochs that marked it)}; reset=True clears the totals after reading."""
+        names = (C.c_char_p * 32)()
+        ms = (C.c_double * 32)()
+        ep = (C.c_uint32 * 32)()
+        n = lib().kdtn_timer_totals(self._ctx, names, ms, ep, 32, 1 if reset else 0)
+        return {names[i].decode(): (float(ms[i]), int(ep[i])) for i in range(max(n, 0))}
 
     def wg_trace(self) -> np.ndarray:
         """(nwg, 8) uint64 phase timestamps of the last traced run (KDTN_VARIANT bit 16)."""
