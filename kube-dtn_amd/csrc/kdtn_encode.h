@@ -213,25 +213,29 @@ KD_INLINE void wave_image_write(uint32_t* img, bool on, uint64_t s0, uint64_t s1
 }
 
 // One wave writes its lanes' byte ranges [s0, s1) when they are NOT one contiguous range (the
-// RemotePod messages of consecutive add entries go to their daemons' runs): in two rounds of 32
-// lanes, every lane writes its range into a private dword slot of the wave's LDS image at the
-// alignment of its destination (owned WSink), then the wave copies the slots out dword by
-// dword — lane q takes image dword q, finds its slot by binary search, and stores it whole, or
-// by bytes where the dword is shared with a neighbouring range. Consecutive lanes thus store
-// consecutive dwords of each range instead of every lane storing its own range alone. A round
-// larger than the image is written straight to global memory. Every lane must call it.
-constexpr int SEG_META = 4 * 32 + 1;            // dwords of slot metadata at the image's end
-template <int R, typename F>
+// RemotePod messages of consecutive add entries go to their daemons' runs): every lane writes
+// its range into a private dword slot of the wave's LDS image (IMGB bytes) at the alignment of
+// its destination (owned WSink), then the wave copies the slots out dword by dword — lane q
+// takes image dword q, finds its slot by binary search, and stores it whole, or by bytes where
+// the dword is shared with a neighbouring range. Consecutive lanes thus store consecutive
+// dwords of each range instead of every lane storing its own range alone. All 64 lanes build
+// their ranges in one round when the wave's slots fit the image; otherwise in two rounds of 32
+// lanes (the range assembly then runs twice at half the lanes: round 2 measured 2x the VALU
+// instructions of a one-round wave), and a round larger than the image goes straight to global
+// memory. Every lane must call it.
+template <int NL> constexpr int seg_meta() { return 4 * NL + 1; }   // dwords of slot metadata
+template <int NL, int R, int IMGB, typename F>
 KD_INLINE void wave_segments_round(uint32_t* img, bool on, uint64_t s0, uint32_t len, uint32_t ndw, uint8_t* arena,
                                    F& body) {
     const int lane = threadIdx.x & 63;
-    uint32_t* mq = img + WIRE_IMG / 4 - SEG_META;  // [33] slot starts (dwords), then per slot: dst lo, hi, lead|len
-    uint32_t* mlo = mq + 33;
-    uint32_t* mhi = mlo + 32;
-    uint32_t* mll = mhi + 32;
-    constexpr uint32_t budget = WIRE_IMG / 4 - SEG_META;
+    constexpr int META = seg_meta<NL>();
+    uint32_t* mq = img + IMGB / 4 - META;       // [NL + 1] slot starts (dwords), then per slot: dst lo, hi, lead|len
+    uint32_t* mlo = mq + NL + 1;
+    uint32_t* mhi = mlo + NL;
+    uint32_t* mll = mhi + NL;
+    constexpr uint32_t budget = IMGB / 4 - META;
     const uint32_t lead = (uint32_t)s0 & 3u;
-    const bool mine = (lane >> 5) == R;
+    const bool mine = NL == 64 || (lane >> 5) == R;
     const uint32_t x = mine ? ndw : 0u;
     uint32_t inc = x;
 #pragma unroll
@@ -239,12 +243,12 @@ KD_INLINE void wave_segments_round(uint32_t* img, bool on, uint64_t s0, uint32_t
         const uint32_t o = __shfl_up(inc, d, 64);
         if (lane >= d) inc += o;
     }
-    const uint32_t q0 = __shfl(inc - x, 32 * R, 64);            // the round's first slot start
-    const uint32_t total = __shfl(inc, 32 * R + 31, 64) - q0;
+    const uint32_t q0 = NL == 64 ? 0u : __shfl(inc - x, 32 * R, 64);         // the round's first slot start
+    const uint32_t total = __shfl(inc, NL == 64 ? 63 : 32 * R + 31, 64) - q0;
     const uint32_t qi = inc - x - q0;
     if (total == 0) return;                                      // wave-uniform
     const bool direct = total > budget;                          // too large: straight to global memory
-    const int sl = lane - 32 * R;
+    const int sl = NL == 64 ? lane : lane - 32 * R;
     if (mine && !direct) {
         mq[sl] = qi;
         mlo[sl] = (uint32_t)(s0 & ~3ull);
@@ -266,8 +270,8 @@ KD_INLINE void wave_segments_round(uint32_t* img, bool on, uint64_t s0, uint32_t
     for (uint32_t q = lane; q < total; q += 64) {
         int i = 0;                                               // the last slot starting at or before q
 #pragma unroll
-        for (int step = 16; step >= 1; step >>= 1)
-            if (i + step < 32 && mq[i + step] <= q) i += step;
+        for (int step = NL / 2; step >= 1; step >>= 1)
+            if (i + step < NL && mq[i + step] <= q) i += step;
         const uint32_t k = q - mq[i], ll = mll[i];
         const uint32_t ld = ll & 3u, end = ld + (ll >> 2);      // valid bytes of the slot: [ld, end)
         uint8_t* dst = arena + ((((uint64_t)mhi[i]) << 32) | mlo[i]) + 4ull * k;
@@ -286,12 +290,19 @@ KD_INLINE void wave_segments_round(uint32_t* img, bool on, uint64_t s0, uint32_t
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
-template <typename F>
+template <int IMGB = WIRE_IMG, typename F>
 KD_INLINE void wave_segments_write(uint32_t* img, bool on, uint64_t s0, uint64_t s1, uint8_t* arena, F&& body) {
     const uint32_t len = on ? (uint32_t)(s1 - s0) : 0u;
     const uint32_t ndw = on ? (((uint32_t)s0 & 3u) + len + 3u) >> 2 : 0u;
-    wave_segments_round<0>(img, on, s0, len, ndw, arena, body);   // lanes 0-31, then 32-63
-    wave_segments_round<1>(img, on, s0, len, ndw, arena, body);
+    uint32_t sum = ndw;                                          // the wave's slot dwords
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, 64);
+    if (sum <= (uint32_t)(IMGB / 4 - seg_meta<64>())) {          // wave-uniform: one round
+        wave_segments_round<64, 0, IMGB>(img, on, s0, len, ndw, arena, body);
+        return;
+    }
+    wave_segments_round<32, 0, IMGB>(img, on, s0, len, ndw, arena, body);   // lanes 0-31, then 32-63
+    wave_segments_round<32, 1, IMGB>(img, on, s0, len, ndw, arena, body);
 }
 
 }  // namespace kdtn

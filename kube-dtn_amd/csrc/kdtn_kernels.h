@@ -271,6 +271,9 @@ constexpr int SCAN_CHUNK = BLOCK * 4;   // values per block of the batch-offset 
 constexpr int SCAN_TOP_BLOCK = 1024, SCAN_TOP_PER = 16;   // k_scan_top: one block, totals per thread
 constexpr int WIRE_IMG = 8192;          // LDS bytes per wave for a wave's wire output (32 KB per
                                         // block: 5 blocks per CU; a longer wave range stores directly)
+constexpr int REMOTE_IMG = 10240;       // k_remote_write: 64 RemotePod messages (~124 B each) and their
+                                        // slot metadata fit one round (40 KB per block: 4 blocks per
+                                        // CU, the occupancy its ~100 VGPRs allow anyway)
 // string table of a dictionary for the encoders: {arena offset, length | STR_BAD} per string,
 // STR_BAD = not valid UTF-8 — one 8-B gather gives everything a string field needs
 constexpr uint32_t STR_BAD = 0x80000000u;

@@ -556,7 +556,7 @@ KD_INLINE void write_remote(WSink& o, const RemoteIn& r, const RemoteMsg& q) {
 // contiguous run of the arena (fan-out order keeps add-list order within a daemon), so the
 // wave stores them through its LDS image dword by dword (wave_segments_write).
 __global__ void __launch_bounds__(BLOCK) k_remote_write(RemoteIn r, const uint64_t* off, uint8_t* arena) {
-    __shared__ uint32_t img[BLOCK / 64][WIRE_IMG / 4];
+    __shared__ uint32_t img[BLOCK / 64][REMOTE_IMG / 4];
     const uint32_t e = blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t kind = e < r.n_add ? remote_kind(r, e) : 0u;
     if (__ballot(kind != 0) == 0) return;           // wave-uniform
@@ -570,8 +570,8 @@ __global__ void __launch_bounds__(BLOCK) k_remote_write(RemoteIn r, const uint64
     const bool on = s1 > s0;                        // empty: no message or a Marshal error
     RemoteMsg q{};
     if (on) q = remote_msg(r, e, t, kind == 1);
-    wave_segments_write(img[threadIdx.x >> 6], on, s0, s1, arena,
-                        [&](WSink& o) __attribute__((always_inline)) { write_remote(o, r, q); });
+    wave_segments_write<REMOTE_IMG>(img[threadIdx.x >> 6], on, s0, s1, arena,
+                                    [&](WSink& o) __attribute__((always_inline)) { write_remote(o, r, q); });
 }
 
 }  // namespace kdtn
