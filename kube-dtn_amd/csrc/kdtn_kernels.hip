@@ -93,7 +93,8 @@ KD_INLINE const uint8_t* stage_slice(const uint8_t* bytes, const uint32_t* offs,
     const uint32_t a0 = b0 & ~15u;
     *a0_out = a0;
     const uint32_t words = (b1 - a0 + 15) >> 4;
-    if (words * 16 > (uint32_t)CAPB) return nullptr;    // uniform across the block
+    if (words * 16 + 32 > (uint32_t)CAPB) return nullptr;   // uniform across the block; 32 B of
+                                                           // slack for the parsers' dword reads
     const uint4* src = reinterpret_cast<const uint4*>(bytes + a0);
     for (uint32_t w = threadIdx.x; w < words; w += BLOCK) buf[w] = src[w];
     return reinterpret_cast<const uint8_t*>(buf);

@@ -249,6 +249,19 @@ KD_INLINE bool pct_finish(const uint8_t* s, bool neg, bool hex, bool trunc, uint
         if (dp >= 4) return false;               // |V| >= 100.0 × 10: > 100 or < 0
         if (dp <= -46) { *out = 0.0f; return true; }  // |V| < 1e-46 < 2^-150 → ±0
         int e10 = (int)(dp - ndmant);            // V ≈ mant × 10^e10
+        if (e10 >= -8 && e10 <= 0 && !trunc && mant < (1ull << 53)) {
+            // V = mant / 10^k with k <= 8: the quotient rounded once to double, then to float32,
+            // is V correctly rounded. Were it not, the double would have to lie on a float32
+            // midpoint m = M / 2^e (M < 2^25) while V does not: then |V - m| >= 1 / (10^k 2^e)
+            // >= V / (10^k 2^25) > V 2^-53 (10^8 < 2^28), beyond the division's rounding
+            // error; and a V that is a midpoint is exact in double and rounds to even. (k = 0:
+            // V = mant, exact.)
+            v = (float)(e10 == 0 ? (double)mant : __ddiv_rn((double)mant, pow10_exact(-e10)));
+            if (neg) v = -v;
+            if (v < 0.0f || v > 100.0f) return false;
+            *out = v;
+            return true;
+        }
         double approx = (double)mant;
         if (e10 >= 0) approx = __dmul_rn(approx, pow10_exact(e10));
         else if (e10 >= -22) approx = __ddiv_rn(approx, pow10_exact(-e10));
@@ -388,17 +401,21 @@ KD_INLINE bool parse_pct_generic(const uint8_t* s, uint32_t n, float* out) {
 // 16 digits never reach the 19-digit mantissa limit); anything else takes the generic parser.
 KD_INLINE bool parse_pct(const uint8_t* s, uint32_t n, float* out) {
     if (n == 0 || n > 16) return parse_pct_generic(s, n, out);
-    uint32_t c[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) c[k] = (uint32_t)k < n ? s[k] : 0u;
+    // the 16 bytes from five dword loads (the arena and the LDS slices have slack past a string)
+    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(s) & 3u);
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(s - mis);
+    const uint32_t d0 = p[0], d1 = p[1], d2 = p[2], d3 = p[3], d4 = p[4];
+    const uint32_t w[4] = {__builtin_amdgcn_alignbyte(d1, d0, mis), __builtin_amdgcn_alignbyte(d2, d1, mis),
+                           __builtin_amdgcn_alignbyte(d3, d2, mis), __builtin_amdgcn_alignbyte(d4, d3, mis)};
     bool ok = true, sawdot = false, sawdigits = false;
     long nd = 0, dp = 0;
     uint64_t mant = 0;
     int ndmant = 0;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
+        if (__ballot((uint32_t)k < n) == 0) break;      // no lane of the wave has byte k
         if ((uint32_t)k < n) {
-            const uint32_t ch = c[k];
+            const uint32_t ch = (w[k >> 2] >> (8 * (k & 3))) & 0xFFu;
             const bool dig = ch - '0' <= 9u;
             if (ch == '.') {
                 ok &= !sawdot;
