@@ -514,3 +514,26 @@ def test_append_only_dictionaries_keep_parsed_tables(engine):
     engine.run()
     engine.sync()
     assert_same(engine.download(), O.reconcile(inp, tick=TICK), "shorter prefix")
+
+
+def test_timer_totals_sum_the_synced_epochs(engine):
+    """kdtn_timer_totals: the HIP-event marks of every synced epoch since the last reset, per
+    stage (bench.py reads them once per timed loop); equal to the per-epoch marks summed."""
+    _, inp = random_epoch_input(5, T=400)
+    engine.upload(inp)
+    engine.set_timing(1)
+    try:
+        engine.timer_totals(reset=True)
+        per = []
+        for _ in range(3):
+            engine.run()
+            engine.sync()
+            per.append(engine.kernel_times())
+        tot = engine.timer_totals(reset=True)
+        assert set(tot) == set(per[0]) and "reconcile" in tot, (tot, per[0])
+        for k, (ms, n) in tot.items():
+            assert n == 3, (k, n)
+            assert abs(ms - sum(p[k] for p in per)) <= 1e-3 * max(ms, 1e-3), (k, ms, per)
+        assert engine.timer_totals() == {}                # reset cleared them
+    finally:
+        engine.set_timing(2)                              # the context's default
