@@ -129,7 +129,7 @@ struct kdtn_ctx {
     uint64_t rp_bytes = 0, rp_tc_bytes = 0;
     bool rp_done = false;
     // resident state: commit / delta plans, the delta's arrays and inline records
-    DevBuf st_len, st_base, st_mode, st_flags, st_off64, st_part, st_off32, st_mask, st_chg;
+    DevBuf st_cnt, st_len, st_base, st_mode, st_flags, st_off64, st_part, st_off32, st_mask, st_chg;
     DevBuf dl_topo, dl_src, dl_netns, dl_nil, dl_off, dl_ref, dl_rows;
     DevLinkStore dl_rec;
     bool tables_cur = false;                   // j_info describes the current tables (kdtn_epoch_tables_info)
@@ -181,6 +181,10 @@ namespace {
 int ensure(DevBuf& b, size_t bytes) {
     bytes = std::max<size_t>(bytes, 256);
     if (b.cap >= bytes) return KDTN_OK;
+    // grown buffers get 1/8 headroom (from 1 MB on): epoch sizes drift from epoch to epoch
+    // (a churn chain's record counts), and every regrowth is a hipFree (a device-wide
+    // synchronisation) plus a hipMalloc
+    if (bytes >= (1u << 20)) bytes = (bytes + bytes / 8 + 0xFFFFF) & ~(size_t)0xFFFFF;
     if (b.p) (void)hipFree(b.p);
     b.p = nullptr;
     b.cap = 0;
@@ -780,7 +784,7 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->vx_vni, &c->vx_netns, &c->vx_part, &c->vx_cut, &c->f_cut, &c->vx_vis,
                       &c->r_node, &c->r_vni, &c->r_netns, &c->rp_flag, &c->rp_pos, &c->rp_phys,
                       &c->rp_msz, &c->rp_moff, &c->rp_tsz, &c->rp_toff, &c->rp_part, &c->rp_arena, &c->rp_tc, &c->rp_msz_e, &c->rp_tsz_e,
-                      &c->st_len, &c->st_base, &c->st_mode, &c->st_flags, &c->st_off64, &c->st_part,
+                      &c->st_cnt, &c->st_len, &c->st_base, &c->st_mode, &c->st_flags, &c->st_off64, &c->st_part,
                       &c->st_off32, &c->st_mask, &c->st_chg, &c->dl_topo, &c->dl_src, &c->dl_netns, &c->dl_nil,
                       &c->dl_off, &c->dl_ref, &c->dl_rec.buf, &c->stage, &c->vx_cnt, &c->vx_send, &c->vx_recv,
                       &c->vx_gops, &c->pd_send, &c->pd_recv, &c->pd_cnt, &c->dl_rows, &c->vx_flag,
@@ -2248,7 +2252,7 @@ int kdtn_ingest_download(kdtn_ctx* c, kdtn_ingest_tables* o) {
         const uint32_t n = st.n;
         if (!n) return KDTN_OK;
         const size_t full = n / TILE_RECS, tail = n % TILE_RECS, tile_bytes = (size_t)TILE_WORDS * 4;
-        const uint8_t* base = static_cast<const uint8_t*>(st.buf.p);
+        const uint8_t* base = reinterpret_cast<const uint8_t*>(st.view.base);   // (des may read real's buffer)
         auto col = [&](int cidx, void* dst, size_t esz) -> int {
             if (!dst) return KDTN_OK;
             const size_t run = TILE_RECS * esz;
@@ -2745,6 +2749,7 @@ int patch_pods(kdtn_ctx* c, uint32_t n) {
 
 // per-topology plan arrays for T topologies
 int plan_alloc(kdtn_ctx* c, uint32_t T) {
+    TRY(ensure(c->st_cnt, 32 * 4));
     TRY(ensure(c->st_len, (size_t)T * 4 + 16));
     TRY(ensure(c->st_base, (size_t)T * 4 + 16));
     TRY(ensure(c->st_mode, (size_t)T + 16));
@@ -2777,6 +2782,24 @@ int kdtn_epoch_commit(kdtn_ctx* c, const uint8_t* mask, uint32_t* n_committed) {
     hipStream_t s = c->stream;
     HIP_TRY(hipStreamSynchronize(s));
     const uint32_t T = c->T;
+    if (mask && T && std::memchr(mask, 0, T) == nullptr) {
+        // every Topology committed: the realised store IS the desired store (the same records at
+        // the same offsets), so no reassembly — real takes the desired store's buffer, des keeps
+        // reading that memory (every writer of des resets its view to its own buffer first),
+        // real_off := des_off and the status-nil flags follow the spec's
+        k_commit_all_flags<<<nblocks(T), BLOCK, 0, s>>>(dp<uint8_t>(c->t_flags), T);
+        HIP_TRY(hipMemcpyAsync(c->t_roff.p, c->t_noff.p, ((size_t)T + 1) * 4, hipMemcpyDeviceToDevice, s));
+        HIP_TRY(hipGetLastError());
+        std::swap(c->real, c->des);
+        c->des.view = c->real.view;
+        c->des.n = c->real.n;
+        TRY(prepare_work(c, c->slice, c->real.n, c->des.n));
+        HIP_TRY(hipStreamSynchronize(s));
+        state_changed(c);
+        c->pods_imported = false;
+        if (n_committed) *n_committed = T;
+        return KDTN_OK;
+    }
     TRY(plan_alloc(c, T));
     const uint8_t* dmask = nullptr;
     const uint32_t* cut = nullptr;
@@ -2787,8 +2810,8 @@ int kdtn_epoch_commit(kdtn_ctx* c, const uint8_t* mask, uint32_t* n_committed) {
         TRY(run_reach(c, nullptr, 0));                      // per-topology first failing entries
         cut = dp<uint32_t>(c->f_cut);
     }
-    uint32_t* ncnt = dp<uint32_t>(c->misc) + MISC_COMMIT_N;
-    HIP_TRY(hipMemsetAsync(ncnt, 0, 4, s));
+    uint32_t* ncnt = dp<uint32_t>(c->st_cnt);
+    HIP_TRY(hipMemsetAsync(ncnt, 0, 32 * 4, s));
     if (T)
         k_commit_plan<<<nblocks(T), BLOCK, 0, s>>>(topo_view(c), dp<uint8_t>(c->action), cut, dmask,
                                                    dp<uint32_t>(c->st_len), dp<uint32_t>(c->st_base),
@@ -2801,9 +2824,11 @@ int kdtn_epoch_commit(kdtn_ctx* c, const uint8_t* mask, uint32_t* n_committed) {
                                                       dp<uint8_t>(c->st_mode), nullptr, c->real.view, c->des.view,
                                                       (uint32_t)M, dp<uint32_t>(c->sh_real.buf));
     HIP_TRY(hipGetLastError());
-    uint32_t nc = 0;
-    HIP_TRY(hipMemcpyAsync(&nc, ncnt, 4, hipMemcpyDeviceToHost, s));
+    uint32_t cnt[32] = {};
+    HIP_TRY(hipMemcpyAsync(cnt, ncnt, sizeof cnt, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    uint32_t nc = 0;
+    for (uint32_t v : cnt) nc += v;
     std::swap(c->real, c->sh_real);
     std::swap(c->t_roff, c->st_off32);
     std::swap(c->t_flags, c->st_flags);

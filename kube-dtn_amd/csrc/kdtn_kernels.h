@@ -324,6 +324,7 @@ __global__ void k_tc_write(TcIn w, const uint64_t* off, uint8_t* arena);
 enum : uint8_t { ASM_SEG_A = 0, ASM_SEG_B = 1, ASM_REF = 2 };   // source of a topology's new segment
 __global__ void k_commit_plan(DevTopos T, const uint8_t* action, const uint32_t* cut, const uint8_t* mask,
                               uint32_t* len, uint32_t* base, uint8_t* mode, uint8_t* flags_out, uint32_t* n_commit);
+__global__ void k_commit_all_flags(uint8_t* flags, uint32_t T);
 __global__ void k_delta_map(const uint32_t* topo, uint32_t n, uint32_t* chg);
 __global__ void k_delta_plan(DevTopos T, const uint32_t* chg, const uint32_t* d_off, const uint32_t* d_src,
                              const uint32_t* d_netns, const uint8_t* d_nil, uint32_t* len, uint32_t* base,

@@ -102,3 +102,32 @@ def test_resident_churn_chain(pods):
             assert len(ora.del_idx) and len(ora.add_idx) and len(ora.upd_idx)
         full = 9 * (88 * new.desired.n + 25 * new.topos.n)
         assert moved < 0.1 * full, (moved, full)
+
+
+def test_all_committed_commit_keeps_every_view():
+    """kdtn_epoch_commit with every Topology committed takes the fast path (the desired store
+    becomes the realised one without reassembly): the tables, a re-run without a new upload,
+    a delta upload, a partial commit after it and a full upload all stay exact."""
+    topos, vnis = random_epoch(3, T=200, p_err=0.1)
+    kd, pd = Interner(), Interner()
+    a = pack(topos, vnis, kdict=kd, pdict=pd)
+    with Engine(device=0, tick_in_usec=TICK) as eng:
+        eng.upload(a)
+        _run_same(eng, a, "epoch 0")
+        assert eng.commit(np.ones(a.topos.n, bool)) == a.topos.n
+        state = commit(a, np.ones(a.topos.n, bool))
+        assert not same_tables(eng.tables(), state)
+        _run_same(eng, state, "re-run on the committed state")          # status == spec: no diff
+        b = pack(mutate(topos, 5), vnis, kdict=kd, pdict=pd)
+        d = build_delta(a, b, a.kdict.n, a.pdict.n, vnis=b.vnis)
+        eng.upload_delta(d)
+        want = apply_delta(state, d)
+        assert not same_tables(eng.tables(), want)
+        ora = _run_same(eng, want, "delta after the fast commit")
+        mask = np.random.default_rng(1).random(want.topos.n) < 0.5
+        assert eng.commit(mask) == int(mask.sum())
+        st2 = commit(want, mask)
+        assert not same_tables(eng.tables(), st2)
+        _run_same(eng, st2, "partial commit after the fast one")
+        eng.upload(b)
+        _run_same(eng, b, "full upload after the commits")
