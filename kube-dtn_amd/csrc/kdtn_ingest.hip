@@ -1047,7 +1047,7 @@ KD_INLINE const uint8_t* key_bytes(const JsIntern& in, uint64_t kw) {
 
 // returns the table slot of the string [p, p+len) (len ≥ 1), or JS_NONE on overflow
 KD_INLINE uint32_t intern(const JsIntern& in, const JsDict& dt, const uint8_t* p, uint32_t len, uint64_t kw_self,
-                          uint64_t h, uint32_t occ, const uint32_t* pw = nullptr) {
+                          uint64_t h, uint32_t occ, const uint32_t (&pw)[8], bool have_pw) {
     const uint64_t tag = h >> 57;
     const uint64_t kw = (tag << 57) | kw_self;
     uint32_t s = (uint32_t)h & dt.mask;
@@ -1075,7 +1075,7 @@ KD_INLINE uint32_t intern(const JsIntern& in, const JsDict& dt, const uint8_t* p
                     if (((wd >> (8 * ((off + k) & 3))) & 0xFFu) != p[k]) break;
                     ++k;
                 }
-            } else if (pw && len <= WIN) {            // both in the document: compare windows
+            } else if (have_pw && len <= WIN) {       // both in the document: compare windows
                 uint32_t qw[8];
                 load_window(in.doc, (uint32_t)cur, qw);
                 k = window_eq(pw, qw, len) ? len : 0u;
@@ -1114,7 +1114,7 @@ KD_INLINE uint32_t string_slot(const JsDoc& j, const JsIntern& in, const JsDict&
             for (uint32_t k = a; k < e; ++k) h = fnv_step(h, j.doc[k]);
         }
         h ^= h >> 29;
-        const uint32_t s = intern(in, dt, j.doc + a, len, ((uint64_t)len << 32) | a, h, i, win ? pw : nullptr);
+        const uint32_t s = intern(in, dt, j.doc + a, len, ((uint64_t)len << 32) | a, h, i, pw, win);
         return s == JS_NONE ? JS_NONE : s + 1;
     }
     const uint32_t len = unquote_len(j.doc, a, e);
@@ -1133,7 +1133,7 @@ KD_INLINE uint32_t string_slot(const JsDoc& j, const JsIntern& in, const JsDict&
         for (uint32_t k = 0; k < len; ++k) h = fnv_step(h, out[k]);
     }
     h ^= h >> 29;
-    const uint32_t s = intern(in, dt, out, len, (1ull << 56) | ((uint64_t)len << 32) | (uint32_t)at, h, i);
+    const uint32_t s = intern(in, dt, out, len, (1ull << 56) | ((uint64_t)len << 32) | (uint32_t)at, h, i, pw, false);
     return s == JS_NONE ? JS_NONE : s + 1;
 }
 
@@ -1244,7 +1244,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, const uint2* toks,
     int f, bit;
     uint32_t own;                                      // owner slot of (object, field): duplicate check
     uint32_t topo = 0, rec = 0;
-    const JsStore* st = nullptr;
+    JsStore st{};                                      // by value: a pointer to an argument lives in scratch
     switch (r) {
     case R_ROOT:
         f = key_match(kn, kItems, 1);
@@ -1269,12 +1269,12 @@ __global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, const uint2* toks,
     case R_LINK_S:
     case R_LINK_R:
         f = key_match(kn, kLink, KDTN_NKEY + 2);
-        st = r == R_LINK_S ? &des : &real;
+        st = r == R_LINK_S ? des : real;
         rec = ord[o]; bit = f; own = (r == R_LINK_S ? in.own_des : in.own_real) + rec * 22;
         break;
     default: {                                                    // R_PROPS_S / R_PROPS_R
         f = key_match(kn, kProps, KDTN_NPROP + 1);
-        st = r == R_PROPS_S ? &des : &real;
+        st = r == R_PROPS_S ? des : real;
         rec = ord[po]; bit = 9 + f; own = (r == R_PROPS_S ? in.own_des : in.own_real) + rec * 22;
         break;
     }
@@ -1314,7 +1314,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, const uint2* toks,
             int64_t v;
             ok = kind == TK_SCALAR && parse_int64(j, t.x, &v);
             if (ok) {
-                uint32_t* w = store_word(*st, rec, COL_UID) - (rec & 63u);        // i64 column of the tile
+                uint32_t* w = store_word(st, rec, COL_UID) - (rec & 63u);        // i64 column of the tile
                 reinterpret_cast<int64_t*>(w)[rec & 63u] = v;
             }
             break;
@@ -1323,14 +1323,14 @@ __global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, const uint2* toks,
             if (null) break;
             uint32_t v;
             ok = kind == TK_SCALAR && parse_uint32(j, t.x, &v);
-            if (ok) *store_word(*st, rec, COL_GAP) = v;
+            if (ok) *store_word(st, rec, COL_GAP) = v;
             break;
         }
         if (null) break;
         if (kind != TK_STR) { ok = false; break; }
         const uint32_t v = (KDTN_PROFILING && (in.variant & JSV_NO_INTERN)) ? 1u : string_slot(j, in, props ? in.pd : in.kd, i, t.x);
         if (v == JS_NONE) return;
-        *store_word(*st, rec, props ? COL_PROP0 + f : COL_KEY0 + f) = v;
+        *store_word(st, rec, props ? COL_PROP0 + f : COL_KEY0 + f) = v;
         break;
     }
     }
