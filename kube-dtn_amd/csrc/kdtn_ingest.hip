@@ -1084,7 +1084,12 @@ KD_INLINE uint32_t intern(const JsIntern& in, const JsDict& dt, const uint8_t* p
                 while (k < len && q[k] == p[k]) ++k;
             }
             if (k == len) {                           // hot strings: skip the atomic when it cannot lower
-                if (!(KDTN_PROFILING && (in.variant & JSV_NO_REP)) && occ < dt.rep[s]) atomicMin(dt.rep + s, occ);
+                // an occurrence later in the document than the one that inserted the key cannot
+                // lower the first occurrence (the inserter's own atomicMin is <= its index, and
+                // document offsets grow with token indices): no rep read, no atomic
+                const bool later = !((kw_self >> 56) & 1) && !((cur >> 56) & 1) && (uint32_t)kw_self > (uint32_t)cur;
+                if (!later && !(KDTN_PROFILING && (in.variant & JSV_NO_REP)) && occ < dt.rep[s])
+                    atomicMin(dt.rep + s, occ);
                 return s;
             }
         }
