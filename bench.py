@@ -231,26 +231,31 @@ def e2e_stage(eng, inp, reps: int = 3):
     return res
 
 
-def resident_chain_stage(eng, cs, prev, epochs: int):
+def resident_chain_stage(eng, cs, prev, epochs: int, topology_set: bool = False):
     """Config 3 as a resident controller runs it (separate report, never `value`): each epoch
     uploads only a delta against the engine's state (kdtn_epoch_upload_delta: the changed
     Topologies' specs as references into the previous desired store + new records), runs,
     downloads the batches, and commits the status on the device (kdtn_epoch_commit, every
     Topology's RPCs taken as succeeded, as the churn generator assumes). Host buffers
-    page-locked; the delta is built on the host outside the timed region."""
+    page-locked; the delta is built on the host outside the timed region. topology_set: `cs`
+    is a synth.TopologySetChurn (1 % of the Topologies deleted / re-created per epoch) and
+    `prev` was fully uploaded first."""
     from kdtn.delta import build_delta
     from kdtn.engine import pin_delta
     from kdtn.tables import BatchesOut
     T = prev.topos.n
     cap = max(1 << 20, prev.desired.n // 8)              # entries per list (5 % churn: ~1.7 %)
-    into = BatchesOut.alloc(T, cap, cap, cap, pinned=True)
-    ones = np.ones(T, np.uint8)
-    eng.commit(ones)
+    into = None
     rows = []
+    state_T = T
+    eng.commit(np.ones(T, np.uint8))
     for _ in range(epochs):
         cs.advance()
         new = cs.epoch_input(copy=True)
         d = pin_delta(build_delta(prev, new, prev.kdict.n, prev.pdict.n))
+        if into is None or len(into.action) != new.topos.n:
+            into = BatchesOut.alloc(new.topos.n, cap, cap, cap, pinned=True)
+        ones = np.ones(new.topos.n, np.uint8)
         t0 = time.perf_counter()
         eng.upload_delta(d)
         t1 = time.perf_counter()
@@ -262,18 +267,25 @@ def resident_chain_stage(eng, cs, prev, epochs: int):
         eng.commit(ones)
         t4 = time.perf_counter()
         down_b = sum(getattr(out, f).nbytes for f in out.FIELDS)
+        created = int((d.prev == abi.DELTA_NEW).sum()) if d.prev is not None else 0
+        deleted = state_T - (new.topos.n - created)
+        state_T = new.topos.n
         rows.append((d.upload_bytes(), t1 - t0, t2 - t1, t3 - t2, t4 - t3, down_b, new.desired.n,
-                     d.n_changed, d.records.n, c.n_add + c.n_del + c.n_upd))
+                     d.n_changed, d.records.n, c.n_add + c.n_del + c.n_upd, created, deleted))
         prev = new
     a = np.array(rows, dtype=np.float64).mean(axis=0)
     full_b = 88 * (2 * prev.desired.n) + 25 * T
     e2e = a[1] + a[2] + a[3] + a[4]
-    return {"epochs": epochs, "upload_bytes": a[0], "full_upload_bytes": full_b, "upload_frac": a[0] / full_b,
-            "changed_topologies": a[7], "inline_records": a[8], "entries": a[9],
-            "upload_ms": a[1] * 1e3, "run_ms": a[2] * 1e3, "download_ms": a[3] * 1e3, "download_bytes": a[5],
-            "commit_ms": a[4] * 1e3, "e2e_ms": e2e * 1e3, "links_per_s": a[6] / e2e,
-            "note": "not part of value: per epoch delta upload + run + download + on-device status commit, "
-                    "page-locked host memory, mean over the epochs"}
+    res = {"epochs": epochs, "upload_bytes": a[0], "full_upload_bytes": full_b, "upload_frac": a[0] / full_b,
+           "changed_topologies": a[7], "inline_records": a[8], "entries": a[9],
+           "upload_ms": a[1] * 1e3, "upload_GBps": a[0] / a[1] / 1e9, "run_ms": a[2] * 1e3,
+           "download_ms": a[3] * 1e3, "download_bytes": a[5], "download_GBps": a[5] / a[3] / 1e9,
+           "commit_ms": a[4] * 1e3, "e2e_ms": e2e * 1e3, "links_per_s": a[6] / e2e,
+           "note": "not part of value: per epoch delta upload + run + download + on-device status commit, "
+                   "page-locked host memory, mean over the epochs"}
+    if topology_set:
+        res["created_topologies"], res["deleted_topologies"] = a[10], a[11]
+    return res
 
 
 def ingest_stage(eng, inp, steps: int, reps: int = 5, cpu_sample_pods: int = 20_000):
@@ -721,8 +733,20 @@ def main():
                                         "kernels_ms": rsum,
                                         "note": "same epoch re-run with kdict_keep/pdict_keep = all strings "
                                                 "(append-only interner, nothing new to parse)"}
+    if churn:
+        inp = cs.epoch_input(copy=True)          # (the generator's arrays move when it advances)
     if churn and world == 1 and not args.no_e2e:
-        result["resident_chain"] = resident_chain_stage(eng, cs, cs.epoch_input(copy=True), args.resident_epochs)
+        result["resident_chain"] = resident_chain_stage(eng, cs, inp, args.resident_epochs)
+        # the same with Topologies created and deleted (informer add / delete events)
+        del cs
+        tc = synth.TopologySetChurn(frac=0.01, total_pods=total_pods)
+        p0 = tc.epoch_input()
+        eng.upload(p0)
+        eng.run()
+        eng.sync()
+        result["resident_chain_topology_set"] = resident_chain_stage(eng, tc, p0, args.resident_epochs,
+                                                                     topology_set=True)
+        del tc, p0
     if diff_ms:
         result["diff_only_reconcile_ms"] = float(np.mean(diff_ms))
         result["diff_share_of_reconcile"] = float(np.mean(diff_ms)) / rec_ms

@@ -360,9 +360,22 @@ int kdtn_epoch_commit(kdtn_ctx* ctx, const uint8_t* mask, uint32_t* n_committed)
  * after kdtn_epoch_commit, the previous desired store, the topology rows): only the
  * Topologies whose spec (or status.src_ip / status.net_ns) changed, and for each of them its
  * new spec.links as references — a record of the previous desired store by index, or
- * KDTN_DELTA_NEW | k for inline record k of `records`. The Topology set is unchanged (a new
- * or deleted Topology needs kdtn_epoch_upload). Dictionaries as kdtn_epoch_in (kdict_keep /
- * pdict_keep: the kept prefix is not re-uploaded). */
+ * KDTN_DELTA_NEW | k for inline record k of `records`.
+ * Dictionaries: a delta EXTENDS the resident dictionaries (append-only interning): kdict_keep
+ * and pdict_keep must equal the context's dictionary sizes (the resident records' ids stay
+ * valid), only the suffix is uploaded; KDTN_EINVAL otherwise (a shrunk or rewritten
+ * dictionary needs kdtn_epoch_upload).
+ * Topology set (informer add / delete events: a Topology CR created — the Reconcile CREATED
+ * path, controllers/topology_controller.go:81-85 — or deleted): prev == NULL keeps the set.
+ * Otherwise the new table has n_topos Topologies and prev[t] names the previous index of new
+ * Topology t (each at most once, any order), or is KDTN_DELTA_NEW for a Topology this delta
+ * creates: a created Topology must be listed in topo[] (its spec), takes metadata ns / name
+ * from ns[] / name[] at its changed-list position, and its status.links are nil (a new CR has
+ * no status). Previous Topologies no prev[t] names are deleted with their spec and status.
+ * topo[] indices are new-table indices. pod_slice as kdtn_epoch_in (0 = n_topos); the pod
+ * tables are rebuilt by the next run.
+ * Validation runs on the GPU with one host synchronisation per call; a rejected delta
+ * (KDTN_EINVAL) leaves the resident state as it was (a new run is needed). */
 #define KDTN_DELTA_NEW 0x80000000u
 typedef struct kdtn_epoch_delta {
     kdtn_strtab     kdict, pdict;
@@ -376,6 +389,12 @@ typedef struct kdtn_epoch_delta {
     const uint32_t* ref;        /* [des_off[n_changed]] previous desired record | NEW-tagged   */
     kdtn_link_table records;    /* inline records                                              */
     kdtn_vni_table  vnis;       /* VxlanManager snapshot or KDTN_VNI_RESIDENT                  */
+    /* Topology set changes (prev == NULL: unchanged; the fields below are then ignored)      */
+    uint32_t        n_topos;    /* new T                                                       */
+    const uint32_t* prev;       /* [n_topos] previous index, or KDTN_DELTA_NEW (created)       */
+    const uint32_t* ns;         /* [n_changed] metadata.namespace (read for created ones)      */
+    const uint32_t* name;       /* [n_changed] metadata.name      (read for created ones)      */
+    uint32_t        pod_slice;  /* multi-GPU pod-table entries per rank; 0 = n_topos           */
 } kdtn_epoch_delta;
 int kdtn_epoch_upload_delta(kdtn_ctx* ctx, const kdtn_epoch_delta* delta);
 

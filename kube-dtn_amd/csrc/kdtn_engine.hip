@@ -5,6 +5,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -19,6 +20,7 @@ using namespace kdtn;
 namespace {
 
 constexpr int kMaxTimers = 32;
+constexpr int kSyncSpinUs = 2000;     // kdtn_epoch_sync: event polling before the blocking wait
 
 struct DevBuf {
     void* p = nullptr;
@@ -62,6 +64,8 @@ struct kdtn_ctx {
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
     hipStream_t comm_stream = nullptr;          // RCCL pod-status exchange (nranks > 1)
+    hipStream_t copy_stream = nullptr;          // delta uploads: host-to-device copies beside the kernels
+    hipEvent_t ev_cp[4] = {};
     hipEvent_t ev_fill = nullptr, ev_ag = nullptr;
     // dictionaries; parsed tables persist across uploads for an append-only interner
     // (kdtn_epoch_in.kdict_keep / pdict_keep): *_valid strings have valid parsed tables, a run
@@ -131,6 +135,9 @@ struct kdtn_ctx {
     // resident state: commit / delta plans, the delta's arrays and inline records
     DevBuf st_cnt, st_len, st_base, st_mode, st_flags, st_off64, st_part, st_off32, st_mask, st_chg;
     DevBuf dl_topo, dl_src, dl_netns, dl_nil, dl_off, dl_ref, dl_rows;
+    // delta with a topology-set change: the map, created rows' names, the realised plan
+    DevBuf dl_prev, dl_ns, dl_name, st_rlen, st_rbase, st_roff64, st_rpart, st_roff32, st_seen;
+    uint64_t kd_arena = 0, pd_arena = 0;       // dictionary arena bytes (host-known: tables_info)
     DevLinkStore dl_rec;
     bool tables_cur = false;                   // j_info describes the current tables (kdtn_epoch_tables_info)
     // tc argv
@@ -247,15 +254,19 @@ int upload_arena(kdtn_ctx* c, DevBuf& b, const void* src, size_t bytes) {
     return KDTN_OK;
 }
 
-// Dictionary arena + offsets, uploading only what follows the first `keep` strings.
-int upload_dict(kdtn_ctx* c, DevBuf& bytes, DevBuf& offs, const kdtn_strtab& t, uint32_t keep) {
+// Dictionary arena + offsets, uploading only what follows the first `keep` strings (offs[keep],
+// the kept prefix's end, stays the device's own: the keep checks compare it with the host's).
+// The copies go on `hs` (the context stream unless a delta overlaps them with its kernels).
+int upload_dict(kdtn_ctx* c, DevBuf& bytes, DevBuf& offs, const kdtn_strtab& t, uint32_t keep, hipStream_t hs) {
     const size_t b0 = t.offs[keep], b1 = t.offs[t.n];
     TRY(ensure_keep(bytes, b1 + 64, keep ? b0 : 0, c->stream));
     TRY(ensure_keep(offs, ((size_t)t.n + 1) * 4, keep ? ((size_t)keep + 1) * 4 : 0, c->stream));
     if (b1 > b0) HIP_TRY(hipMemcpyAsync(static_cast<uint8_t*>(bytes.p) + b0, t.bytes + b0, b1 - b0,
-                                        hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(static_cast<uint32_t*>(offs.p) + keep, t.offs + keep, ((size_t)t.n - keep + 1) * 4,
-                           hipMemcpyHostToDevice, c->stream));
+                                        hipMemcpyHostToDevice, hs));
+    const uint32_t o0 = keep ? keep + 1 : 0;
+    if (t.n + 1 > o0)
+        HIP_TRY(hipMemcpyAsync(static_cast<uint32_t*>(offs.p) + o0, t.offs + o0, ((size_t)t.n + 1 - o0) * 4,
+                               hipMemcpyHostToDevice, hs));
     return KDTN_OK;
 }
 
@@ -322,8 +333,28 @@ int check_offsets(const uint32_t* off, uint32_t T, uint32_t n, const char* what)
 
 constexpr uint32_t STAGED_UPLOAD_MIN = 1u << 16;   // records: below it, 2-D copies straight into tiles
 
+// A link table's columns as host runs: consecutive columns whose host arrays are adjacent (a
+// caller holding key[7][n] / prop[12][n] blocks) become one copy into the staging buffer.
+int stage_columns(kdtn_ctx* c, uint8_t* st, const kdtn_link_table& L, size_t col, hipStream_t hs) {
+    const uint32_t* src[LINK_COLS32];
+    for (int k = 0; k < KDTN_NKEY; ++k) src[COL_KEY0 + k] = L.key[k];
+    for (int k = 0; k < KDTN_NPROP; ++k) src[COL_PROP0 + k] = L.prop[k];
+    src[COL_GAP] = L.gap;
+    for (int a = 0; a < LINK_COLS32;) {
+        int b = a + 1;
+        while (b < LINK_COLS32 && reinterpret_cast<const uint8_t*>(src[b]) ==
+                                      reinterpret_cast<const uint8_t*>(src[b - 1]) + col)
+            ++b;
+        HIP_TRY(hipMemcpyAsync(st + (size_t)a * col, src[a], (size_t)(b - a) * col, hipMemcpyHostToDevice, hs));
+        a = b;
+    }
+    return KDTN_OK;
+}
+
+// defer: the id-range check's column maxima stay in misc[MISC_COLMAX..] for the caller to read
+// back with its own synchronisation (the staged path is then taken for any size)
 int upload_links(kdtn_ctx* c, DevLinkStore& s, const kdtn_link_table& L, uint32_t D, uint32_t P,
-                 const char* what) {
+                 const char* what, bool defer = false) {
     const uint32_t n = L.n;
     for (int k = 0; k < KDTN_NKEY; ++k)
         if (n && !L.key[k]) return check_ids(L.key[k], n, D, what);          // missing column
@@ -340,25 +371,23 @@ int upload_links(kdtn_ctx* c, DevLinkStore& s, const kdtn_link_table& L, uint32_
     s.view.base = reinterpret_cast<const uint32_t*>(base);
     s.view.n = n;
     s.n = n;
-    if (n >= STAGED_UPLOAD_MIN) {
+    if (n >= STAGED_UPLOAD_MIN || defer) {
         // large tables: one linear copy per column (full host-link rate) into a staging buffer,
         // then the tiles and the id-range check in one GPU pass (no host pass over the columns)
         const size_t col = (size_t)n * 4, uid_at = align_up(col * LINK_COLS32, 8);
         TRY(ensure(c->stage, uid_at + (size_t)n * 8 + 128));
         uint8_t* st = static_cast<uint8_t*>(c->stage.p);
-        for (int k = 0; k < KDTN_NKEY; ++k)
-            HIP_TRY(hipMemcpyAsync(st + (COL_KEY0 + k) * col, L.key[k], col, hipMemcpyHostToDevice, c->stream));
-        for (int k = 0; k < KDTN_NPROP; ++k)
-            HIP_TRY(hipMemcpyAsync(st + (COL_PROP0 + k) * col, L.prop[k], col, hipMemcpyHostToDevice, c->stream));
-        HIP_TRY(hipMemcpyAsync(st + COL_GAP * col, L.gap, col, hipMemcpyHostToDevice, c->stream));
-        HIP_TRY(hipMemcpyAsync(st + uid_at, L.uid, (size_t)n * 8, hipMemcpyHostToDevice, c->stream));
         TRY(ensure(c->misc, 256));
         uint32_t* colmax = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(c->misc.p) + MISC_COLMAX * 4);
         HIP_TRY(hipMemsetAsync(colmax, 0, COL_GAP * 4, c->stream));
+        if (!n) return KDTN_OK;
+        TRY(stage_columns(c, st, L, col, c->stream));
+        HIP_TRY(hipMemcpyAsync(st + uid_at, L.uid, (size_t)n * 8, hipMemcpyHostToDevice, c->stream));
         k_soa_to_tiles<<<std::min<uint32_t>((n + BLOCK - 1) / BLOCK, 4 * c->n_cus), BLOCK, 0, c->stream>>>(
             reinterpret_cast<const uint32_t*>(st), reinterpret_cast<const int64_t*>(st + uid_at), n,
             reinterpret_cast<uint32_t*>(base), colmax);
         HIP_TRY(hipGetLastError());
+        if (defer) return KDTN_OK;
         uint32_t mx[COL_GAP];
         HIP_TRY(hipMemcpyAsync(mx, colmax, sizeof(mx), hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
@@ -527,15 +556,19 @@ int check_keep(kdtn_ctx* c, const kdtn_strtab& kd, const kdtn_strtab& pd, uint32
 }
 
 // upload the dictionaries past the kept prefixes and size their parsed tables
-int upload_dicts(kdtn_ctx* c, const kdtn_strtab& kd, const kdtn_strtab& pd, uint32_t kk, uint32_t pk) {
+int upload_dicts(kdtn_ctx* c, const kdtn_strtab& kd, const kdtn_strtab& pd, uint32_t kk, uint32_t pk,
+                 hipStream_t hs = nullptr) {
+    if (!hs) hs = c->stream;
     c->D = kd.n;
     c->P = pd.n;
+    c->kd_arena = kd.offs[kd.n];
+    c->pd_arena = pd.offs[pd.n];
     c->kd_valid = kk;
     c->pd_valid = pk;
     c->kd_from = kk;
     c->pd_from = pk;
-    TRY(upload_dict(c, c->kd_bytes, c->kd_offs, kd, kk));
-    TRY(upload_dict(c, c->pd_bytes, c->pd_offs, pd, pk));
+    TRY(upload_dict(c, c->kd_bytes, c->kd_offs, kd, kk, hs));
+    TRY(upload_dict(c, c->pd_bytes, c->pd_offs, pd, pk, hs));
     return prepare_dicts(c);
 }
 
@@ -744,7 +777,8 @@ int kdtn_init(kdtn_ctx** out, const kdtn_config* cfg) {
         return KDTN_EIO;
     }
     c->stream = c->own_stream;
-    if (hipHostMalloc(reinterpret_cast<void**>(&c->h_misc), 64, hipHostMallocDefault) != hipSuccess) {
+    // words [0, 16): epoch sync header copy; [64, 128): the misc words a delta reads back
+    if (hipHostMalloc(reinterpret_cast<void**>(&c->h_misc), 512, hipHostMallocDefault) != hipSuccess) {
         (void)hipStreamDestroy(c->own_stream);
         delete c;
         return KDTN_ENOMEM;
@@ -753,6 +787,8 @@ int kdtn_init(kdtn_ctx** out, const kdtn_config* cfg) {
     // and invalidate at every mark cost the timed epoch stream time
     for (int i = 0; i <= kMaxTimers; ++i) (void)hipEventCreateWithFlags(&c->ev[i], hipEventDisableSystemFence);
     (void)hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming);
+    for (hipEvent_t& e : c->ev_cp) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    if (hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess) c->copy_stream = nullptr;
     *out = c;
     return KDTN_OK;
 }
@@ -790,7 +826,9 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->st_off32, &c->st_mask, &c->st_chg, &c->dl_topo, &c->dl_src, &c->dl_netns, &c->dl_nil,
                       &c->dl_off, &c->dl_ref, &c->dl_rec.buf, &c->stage, &c->vx_cnt, &c->vx_send, &c->vx_recv,
                       &c->vx_gops, &c->pd_send, &c->pd_recv, &c->pd_cnt, &c->dl_rows, &c->vx_flag,
-                      &c->vx_dkeys, &c->vx_dused, &c->vx_cpos, &c->vx_cpart, &c->vx_cnode, &c->vx_cvni};
+                      &c->vx_dkeys, &c->vx_dused, &c->vx_cpos, &c->vx_cpart, &c->vx_cnode, &c->vx_cvni,
+                      &c->dl_prev, &c->dl_ns, &c->dl_name, &c->st_rlen, &c->st_rbase, &c->st_roff64,
+                      &c->st_rpart, &c->st_roff32, &c->st_seen};
     for (DevBuf* b : bufs) release(*b);
     for (int i = 0; i <= kMaxTimers; ++i)
         if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
@@ -799,6 +837,12 @@ void kdtn_destroy(kdtn_ctx* c) {
     if (c->ev_fill) (void)hipEventDestroy(c->ev_fill);
     if (c->ev_ag) (void)hipEventDestroy(c->ev_ag);
     if (c->ev_done) (void)hipEventDestroy(c->ev_done);
+    for (hipEvent_t e : c->ev_cp)
+        if (e) (void)hipEventDestroy(e);
+    if (c->copy_stream) {
+        (void)hipStreamSynchronize(c->copy_stream);
+        (void)hipStreamDestroy(c->copy_stream);
+    }
     if (c->h_misc) (void)hipHostFree(c->h_misc);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
@@ -1162,11 +1206,15 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
 int kdtn_epoch_sync(kdtn_ctx* c, kdtn_counts* counts) {
     if (!c || !c->ran) return KDTN_EINVAL;
     HIP_TRY(hipSetDevice(c->device));
-    // poll the epoch's completion event (a host-memory signal) before the stream sync, which
-    // then returns at once: the caller learns of the epoch's end sooner than from a sleeping wait
-    if (c->ev_done)
-        while (hipEventQuery(c->ev_done) == hipErrorNotReady) {
+    // poll the epoch's completion event (a host-memory signal) for a bounded time before the
+    // blocking stream sync: a sub-millisecond epoch is seen ending sooner than from a sleeping
+    // wait, and a long one (or a hung GPU) does not hold a host core
+    if (c->ev_done) {
+        const auto t0 = std::chrono::steady_clock::now();
+        while (hipEventQuery(c->ev_done) == hipErrorNotReady &&
+               std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(kSyncSpinUs)) {
         }
+    }
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (c->h_misc[4] != 0) {
         std::snprintf(g_last_error, sizeof(g_last_error), "k_reconcile look-back timed out (0x%x)", c->h_misc[4]);
@@ -2107,6 +2155,8 @@ static int json_ingest_full(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest
     c->j_info.n_pdict = c->P;
     c->j_info.kdict_bytes = kbytes;
     c->j_info.pdict_bytes = pbytes;
+    c->kd_arena = kbytes;
+    c->pd_arena = pbytes;
     if (info) *info = c->j_info;
     c->j_done = true;
     c->uploaded = true;
@@ -2678,18 +2728,25 @@ int kdtn_last_kernel_times(kdtn_ctx* c, const char** names, float* ms, int cap) 
 
 namespace {
 
+// offsets of a store from per-topology lengths: u64 (off64[T] = total) and u32, no readback
+int scan_lengths(kdtn_ctx* c, DevBuf& len, uint32_t T, DevBuf& off64, DevBuf& part, DevBuf& off32) {
+    hipStream_t s = c->stream;
+    const uint32_t nb = nblocks((uint64_t)T + 1, SCAN_CHUNK);
+    TRY(ensure(off64, ((size_t)T + 1) * 8));
+    TRY(ensure(part, (size_t)nb * 8 + 16));
+    TRY(ensure(off32, ((size_t)T + 1) * 4));
+    k_scan_partial<<<nb, BLOCK, 0, s>>>(dp<uint32_t>(len), T, dp<uint64_t>(part));
+    k_scan_top<<<1, SCAN_TOP_BLOCK, 0, s>>>(dp<uint64_t>(part), nb);
+    k_scan_final<<<nb, BLOCK, 0, s>>>(dp<uint32_t>(len), T, dp<uint64_t>(part), dp<uint64_t>(off64));
+    k_off_narrow<<<nblocks((uint64_t)T + 1), BLOCK, 0, s>>>(dp<uint64_t>(off64), T, dp<uint32_t>(off32));
+    HIP_TRY(hipGetLastError());
+    return KDTN_OK;
+}
+
 // new u32 offsets of a store from per-topology lengths (st_len) into st_off32; returns the total
 int plan_offsets(kdtn_ctx* c, uint32_t T, uint64_t* total) {
     hipStream_t s = c->stream;
-    const uint32_t nb = nblocks((uint64_t)T + 1, SCAN_CHUNK);
-    TRY(ensure(c->st_off64, ((size_t)T + 1) * 8));
-    TRY(ensure(c->st_part, (size_t)nb * 8 + 16));
-    TRY(ensure(c->st_off32, ((size_t)T + 1) * 4));
-    k_scan_partial<<<nb, BLOCK, 0, s>>>(dp<uint32_t>(c->st_len), T, dp<uint64_t>(c->st_part));
-    k_scan_top<<<1, SCAN_TOP_BLOCK, 0, s>>>(dp<uint64_t>(c->st_part), nb);
-    k_scan_final<<<nb, BLOCK, 0, s>>>(dp<uint32_t>(c->st_len), T, dp<uint64_t>(c->st_part), dp<uint64_t>(c->st_off64));
-    k_off_narrow<<<nblocks((uint64_t)T + 1), BLOCK, 0, s>>>(dp<uint64_t>(c->st_off64), T, dp<uint32_t>(c->st_off32));
-    HIP_TRY(hipGetLastError());
+    TRY(scan_lengths(c, c->st_len, T, c->st_off64, c->st_part, c->st_off32));
     HIP_TRY(hipMemcpyAsync(total, dp<uint64_t>(c->st_off64) + T, 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     if (*total >= 0x7FFFFFFFull) {
@@ -2831,7 +2888,7 @@ int kdtn_epoch_commit(kdtn_ctx* c, const uint8_t* mask, uint32_t* n_committed) {
     if (M)
         k_store_assemble<<<nblocks(M), BLOCK, 0, s>>>(dp<uint32_t>(c->st_off32), T, dp<uint32_t>(c->st_base),
                                                       dp<uint8_t>(c->st_mode), nullptr, c->real.view, c->des.view,
-                                                      (uint32_t)M, dp<uint32_t>(c->sh_real.buf));
+                                                      (uint32_t)M, AsmGuard{}, dp<uint32_t>(c->sh_real.buf));
     HIP_TRY(hipGetLastError());
     uint32_t cnt[32] = {};
     HIP_TRY(hipMemcpyAsync(cnt, ncnt, sizeof cnt, hipMemcpyDeviceToHost, s));
@@ -2856,82 +2913,227 @@ int kdtn_epoch_upload_delta(kdtn_ctx* c, const kdtn_epoch_delta* d) {
     end_shard_ingest(c);
     TRY(check_strtab(d->kdict, "kdict", d->kdict_keep));
     TRY(check_strtab(d->pdict, "pdict", d->pdict_keep));
-    const uint32_t T = c->T, n = d->n_changed, N0 = c->des.n, D = d->kdict.n, P = d->pdict.n;
+    const bool remap = d->prev != nullptr;                 // the Topology set changes
+    const uint32_t T0 = c->T, Tn = remap ? d->n_topos : T0, n = d->n_changed;
+    const uint32_t N0 = c->des.n, M0 = c->real.n, D = d->kdict.n, P = d->pdict.n;
+    const uint32_t kk = d->kdict_keep, pk = d->pdict_keep;
     auto bad = [&](const char* what, uint32_t i) {
         std::snprintf(g_last_error, sizeof(g_last_error), "delta: %s (at %u)", what, i);
         return KDTN_EINVAL;
     };
-    if (n > T) return bad("more changed topologies than topologies", n);
+    // O(1) host checks; everything per element is checked on the GPU (k_delta_check, k_delta_plan,
+    // the inline records' column maxima) and read back with the call's one synchronisation
+    if (kk != c->D || pk != c->P) {
+        std::snprintf(g_last_error, sizeof(g_last_error),
+                      "delta: kdict_keep %u / pdict_keep %u must equal the resident dictionaries' sizes %u / %u "
+                      "(a delta extends them; a shrunk or rewritten dictionary needs kdtn_epoch_upload)",
+                      kk, pk, c->D, c->P);
+        return KDTN_EINVAL;
+    }
+    if (kk > c->kd_valid || pk > c->pd_valid) return bad("the resident dictionaries were not parsed (run first)", kk);
+    if (n > Tn) return bad("more changed topologies than topologies", n);
     if (n && (!d->topo || !d->src_ip || !d->net_ns || !d->spec_nil || !d->des_off)) return bad("missing column", 0);
-    if (!d->des_off && n) return bad("missing des_off", 0);
+    if (remap && n && (!d->ns || !d->name)) return bad("missing ns / name of the changed topologies", 0);
     const uint32_t nref = n ? d->des_off[n] : 0;
     if (n && d->des_off[0] != 0) return bad("des_off[0] != 0", 0);
     if (nref && !d->ref) return bad("missing ref", 0);
-    for (uint32_t k = 0; k < n; ++k) {
-        if (d->topo[k] >= T || (k && d->topo[k] <= d->topo[k - 1])) return bad("topo not strictly ascending below T", k);
-        if (d->des_off[k + 1] < d->des_off[k]) return bad("des_off not monotone", k);
-        if (d->spec_nil[k] && d->des_off[k + 1] != d->des_off[k]) return bad("spec nil but records", k);
+    const uint32_t slice = remap ? (d->pod_slice ? d->pod_slice : Tn) : c->slice;
+    if (slice < Tn) return bad("pod_slice below n_topos", slice);
+    const uint64_t nbound = (uint64_t)N0 + nref;            // kept segments + the changed lists
+    if (nbound >= 0x7FFFFFFFull) return bad("desired store over 2^31 records", (uint32_t)(nbound >> 32));
+    TRY(check_vnis(c, d->vnis, D, kk));
+    const kdtn_link_table& L = d->records;
+    const uint32_t nr = L.n;
+    if (nr) {
+        for (int k = 0; k < KDTN_NKEY; ++k)
+            if (!L.key[k]) return bad("records: missing key column", k);
+        for (int k = 0; k < KDTN_NPROP; ++k)
+            if (!L.prop[k]) return bad("records: missing prop column", k);
+        if (!L.uid || !L.gap) return bad("records: missing uid / gap", 0);
     }
-    {   // the largest reference of each kind (a loop the compiler vectorises), then the culprit
-        uint32_t top_new = 0, top_old = 0;
-        for (uint32_t i = 0; i < nref; ++i) {
-            const uint32_t r = d->ref[i];
-            const uint32_t nw = (r & KDTN_DELTA_NEW) ? (r & ~KDTN_DELTA_NEW) + 1u : 0u;
-            const uint32_t od = (r & KDTN_DELTA_NEW) ? 0u : r + 1u;
-            top_new = nw > top_new ? nw : top_new;
-            top_old = od > top_old ? od : top_old;
-        }
-        if (top_new > d->records.n || top_old > N0)
-            for (uint32_t i = 0; i < nref; ++i) {
-                const uint32_t r = d->ref[i];
-                if ((r & KDTN_DELTA_NEW) ? (r & ~KDTN_DELTA_NEW) >= d->records.n : r >= N0) return bad("ref out of range", i);
-            }
-    }
-    TRY(check_ids(d->src_ip, n, D, "delta.src_ip"));
-    TRY(check_ids(d->net_ns, n, D, "delta.net_ns"));
-    TRY(check_vnis(c, d->vnis, D, d->kdict_keep));
-    TRY(check_keep(c, d->kdict, d->pdict, d->kdict_keep, d->pdict_keep));
-    c->uploaded = false;                            // a failure from here on leaves no usable epoch
-    TRY(upload_dicts(c, d->kdict, d->pdict, d->kdict_keep, d->pdict_keep));
-    TRY(upload_links(c, c->dl_rec, d->records, D, P, "delta.records"));
-    TRY(upload(c, c->dl_topo, d->topo, (size_t)n * 4));
-    TRY(upload(c, c->dl_src, d->src_ip, (size_t)n * 4));
-    TRY(upload(c, c->dl_netns, d->net_ns, (size_t)n * 4));
-    TRY(upload(c, c->dl_nil, d->spec_nil, (size_t)n));
-    TRY(upload(c, c->dl_off, d->des_off, ((size_t)n + 1) * 4 * (n ? 1 : 0)));
-    TRY(upload(c, c->dl_ref, d->ref, (size_t)nref * 4));
+    // Two streams: the host-to-device copies on the copy stream, in the order the kernels need
+    // them (the delta's arrays, its references, the dictionary suffixes, the inline records),
+    // and the kernels on the context stream, each waiting only for its inputs — so the plan and
+    // the assembly of the kept and referenced records run while the inline records cross the
+    // host link. Buffers are sized first (an allocation may synchronise the device).
     hipStream_t s = c->stream;
-    TRY(plan_alloc(c, T));
-    TRY(ensure(c->st_chg, (size_t)T * 4 + 16));
-    HIP_TRY(hipMemsetAsync(c->st_chg.p, 0xFF, (size_t)T * 4, s));
-    if (n) k_delta_map<<<nblocks(n), BLOCK, 0, s>>>(dp<uint32_t>(c->dl_topo), n, dp<uint32_t>(c->st_chg));
+    hipStream_t cs = c->copy_stream ? c->copy_stream : s;
+    TRY(ensure(c->misc, 256));
+    uint32_t* misc = dp<uint32_t>(c->misc);
+    TRY(ensure(c->dl_topo, (size_t)n * 4));
+    TRY(ensure(c->dl_src, (size_t)n * 4));
+    TRY(ensure(c->dl_netns, (size_t)n * 4));
+    TRY(ensure(c->dl_nil, (size_t)n));
+    TRY(ensure(c->dl_off, ((size_t)n + 1) * 4));
+    TRY(ensure(c->dl_ref, (size_t)nref * 4));
+    if (remap) {
+        TRY(ensure(c->dl_prev, (size_t)Tn * 4));
+        TRY(ensure(c->dl_ns, (size_t)n * 4));
+        TRY(ensure(c->dl_name, (size_t)n * 4));
+    }
+    TRY(link_store_alloc(c, c->dl_rec, nr));
+    const size_t col = (size_t)nr * 4, uid_at = align_up(col * LINK_COLS32, 8);
+    TRY(ensure(c->stage, uid_at + (size_t)nr * 8 + 128));
+    TRY(plan_alloc(c, Tn));
+    TRY(ensure(c->st_chg, (size_t)Tn * 4 + 16));
     TRY(ensure(c->dl_rows, (size_t)n * 4 + 16));
-    uint32_t* rown = dp<uint32_t>(c->misc) + MISC_ROWCHG_N;
-    HIP_TRY(hipMemsetAsync(rown, 0, 4, s));
-    if (T)
-        k_delta_plan<<<nblocks(T), BLOCK, 0, s>>>(topo_view(c), dp<uint32_t>(c->st_chg), dp<uint32_t>(c->dl_off),
-                                                  dp<uint32_t>(c->dl_src), dp<uint32_t>(c->dl_netns),
-                                                  dp<uint8_t>(c->dl_nil), dp<uint32_t>(c->st_len),
-                                                  dp<uint32_t>(c->st_base), dp<uint8_t>(c->st_mode),
-                                                  dp<uint32_t>(c->t_src), dp<uint32_t>(c->t_netns),
-                                                  dp<uint8_t>(c->t_flags), dp<uint32_t>(c->dl_rows), rown);
-    uint32_t n_rows = 0;
-    HIP_TRY(hipMemcpyAsync(&n_rows, rown, 4, hipMemcpyDeviceToHost, s));
-    uint64_t N = 0;
-    TRY(plan_offsets(c, T, &N));
-    TRY(link_store_alloc(c, c->sh_des, (uint32_t)N));
-    if (N)
-        k_store_assemble<<<nblocks(N), BLOCK, 0, s>>>(dp<uint32_t>(c->st_off32), T, dp<uint32_t>(c->st_base),
-                                                      dp<uint8_t>(c->st_mode), dp<uint32_t>(c->dl_ref), c->des.view,
-                                                      c->dl_rec.view, (uint32_t)N, dp<uint32_t>(c->sh_des.buf));
+    TRY(ensure(c->sh_src, (size_t)Tn * 4));
+    TRY(ensure(c->sh_netns, (size_t)Tn * 4));
+    TRY(ensure(c->sh_flags, (size_t)Tn));
+    if (remap) {
+        TRY(ensure(c->sh_ns, (size_t)Tn * 4));
+        TRY(ensure(c->sh_name, (size_t)Tn * 4));
+        TRY(ensure(c->st_rlen, (size_t)Tn * 4 + 16));
+        TRY(ensure(c->st_rbase, (size_t)Tn * 4 + 16));
+        TRY(ensure(c->st_mask, (size_t)Tn + 16));
+        TRY(ensure(c->st_seen, ((size_t)T0 + 31) / 32 * 4 + 16));
+    }
+    TRY(link_store_alloc(c, c->sh_des, (uint32_t)nbound));
+    if (remap) TRY(link_store_alloc(c, c->sh_real, M0));
+    // --- copies (copy stream), after everything already queued on the context stream
+    auto h2d = [&](DevBuf& b, const void* src, size_t bytes) -> int {
+        if (bytes) HIP_TRY(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, cs));
+        return KDTN_OK;
+    };
+    HIP_TRY(hipEventRecord(c->ev_cp[0], s));
+    if (cs != s) HIP_TRY(hipStreamWaitEvent(cs, c->ev_cp[0], 0));
+    TRY(h2d(c->dl_topo, d->topo, (size_t)n * 4));
+    TRY(h2d(c->dl_src, d->src_ip, (size_t)n * 4));
+    TRY(h2d(c->dl_netns, d->net_ns, (size_t)n * 4));
+    TRY(h2d(c->dl_nil, d->spec_nil, (size_t)n));
+    TRY(h2d(c->dl_off, d->des_off, n ? ((size_t)n + 1) * 4 : 0));
+    if (remap) {
+        TRY(h2d(c->dl_prev, d->prev, (size_t)Tn * 4));
+        TRY(h2d(c->dl_ns, d->ns, (size_t)n * 4));
+        TRY(h2d(c->dl_name, d->name, (size_t)n * 4));
+    }
+    HIP_TRY(hipEventRecord(c->ev_cp[1], cs));
+    TRY(h2d(c->dl_ref, d->ref, (size_t)nref * 4));
+    HIP_TRY(hipEventRecord(c->ev_cp[2], cs));
+    c->uploaded = false;                            // (restored below when the delta is rejected)
+    const uint32_t saved[6] = {c->D, c->P, c->kd_valid, c->pd_valid, c->kd_from, c->pd_from};
+    const uint64_t saved_arena[2] = {c->kd_arena, c->pd_arena};
+    // appends past the resident strings (the kept prefix's end offset is not rewritten: the
+    // check below compares it with the host's)
+    TRY(upload_dicts(c, d->kdict, d->pdict, kk, pk, cs));
+    uint8_t* st = static_cast<uint8_t*>(c->stage.p);
+    if (nr) {
+        TRY(stage_columns(c, st, L, col, cs));
+        HIP_TRY(hipMemcpyAsync(st + uid_at, L.uid, (size_t)nr * 8, hipMemcpyHostToDevice, cs));
+    }
+    HIP_TRY(hipEventRecord(c->ev_cp[3], cs));
+    // --- kernels (context stream)
+    uint32_t* colmax = misc + MISC_COLMAX;
+    HIP_TRY(hipMemsetAsync(misc + MISC_DELTA_ERR, 0, 4, s));
+    HIP_TRY(hipMemsetAsync(misc + MISC_ROWCHG_N, 0, 4, s));
+    HIP_TRY(hipMemsetAsync(colmax, 0, COL_GAP * 4, s));
+    HIP_TRY(hipMemsetAsync(c->st_chg.p, 0xFF, (size_t)Tn * 4, s));
+    if (remap) {
+        HIP_TRY(hipMemsetAsync(c->st_seen.p, 0, ((size_t)T0 + 31) / 32 * 4 + 16, s));
+        HIP_TRY(hipMemsetAsync(c->st_mask.p, ASM_SEG_A, (size_t)Tn + 16, s));
+    }
+    if (cs != s) HIP_TRY(hipStreamWaitEvent(s, c->ev_cp[1], 0));
+    if (n) k_delta_map<<<nblocks(n), BLOCK, 0, s>>>(dp<uint32_t>(c->dl_topo), n, Tn, dp<uint32_t>(c->st_chg));
+    if (cs != s) HIP_TRY(hipStreamWaitEvent(s, c->ev_cp[2], 0));
+    {
+        DeltaCheckIn ci{dp<uint32_t>(c->dl_topo), dp<uint32_t>(c->dl_off), dp<uint8_t>(c->dl_nil),
+                        dp<uint32_t>(c->dl_src), dp<uint32_t>(c->dl_netns), dp<uint32_t>(c->dl_ref),
+                        dp<uint32_t>(c->kd_offs), dp<uint32_t>(c->pd_offs), n, nref, Tn, D, nr, N0,
+                        kk, pk, d->kdict.offs[kk], d->pdict.offs[pk]};
+        const uint32_t grid = std::max<uint32_t>({1u, nblocks(n), std::min<uint32_t>(nblocks(nref), 4 * c->n_cus)});
+        k_delta_check<<<grid, BLOCK, 0, s>>>(ci, misc + MISC_DELTA_ERR);
+    }
+    // plan over the new topology table: new rows into scratch columns, the state is untouched
+    DeltaPlanIn pi{topo_view(c), dp<uint32_t>(c->st_chg), remap ? dp<uint32_t>(c->dl_prev) : nullptr,
+                   dp<uint32_t>(c->dl_off), dp<uint32_t>(c->dl_src), dp<uint32_t>(c->dl_netns), dp<uint8_t>(c->dl_nil),
+                   dp<uint32_t>(c->dl_ns), dp<uint32_t>(c->dl_name), Tn, D};
+    DeltaPlanOut po{dp<uint32_t>(c->sh_ns), dp<uint32_t>(c->sh_name), dp<uint32_t>(c->sh_src),
+                    dp<uint32_t>(c->sh_netns), dp<uint8_t>(c->sh_flags), dp<uint32_t>(c->st_len),
+                    dp<uint32_t>(c->st_base), dp<uint8_t>(c->st_mode), dp<uint32_t>(c->st_rlen),
+                    dp<uint32_t>(c->st_rbase), dp<uint32_t>(c->dl_rows), misc + MISC_ROWCHG_N,
+                    dp<uint32_t>(c->st_seen), misc + MISC_DELTA_ERR};
+    if (Tn) k_delta_plan<<<nblocks(Tn), BLOCK, 0, s>>>(pi, po);
+    // the new desired store: kept segments and previous-record references now (grid over the
+    // bound, the exact count stays on the device), the inline records once they have arrived
+    TRY(scan_lengths(c, c->st_len, Tn, c->st_off64, c->st_part, c->st_off32));
+    const AsmGuard g{misc + MISC_DELTA_ERR, dp<uint64_t>(c->st_off64) + Tn, 1u};
+    if (nbound)
+        k_store_assemble<<<nblocks(nbound), BLOCK, 0, s>>>(dp<uint32_t>(c->st_off32), Tn, dp<uint32_t>(c->st_base),
+                                                           dp<uint8_t>(c->st_mode), dp<uint32_t>(c->dl_ref), c->des.view,
+                                                           c->dl_rec.view, (uint32_t)nbound, g,
+                                                           dp<uint32_t>(c->sh_des.buf));
+    if (remap) {                                    // kept Topologies' status segments move with them
+        TRY(scan_lengths(c, c->st_rlen, Tn, c->st_roff64, c->st_rpart, c->st_roff32));
+        const AsmGuard gr{misc + MISC_DELTA_ERR, dp<uint64_t>(c->st_roff64) + Tn, 0u};
+        if (M0)
+            k_store_assemble<<<nblocks(M0), BLOCK, 0, s>>>(dp<uint32_t>(c->st_roff32), Tn, dp<uint32_t>(c->st_rbase),
+                                                           dp<uint8_t>(c->st_mask), nullptr, c->real.view, c->real.view,
+                                                           M0, gr, dp<uint32_t>(c->sh_real.buf));
+    }
+    if (cs != s) HIP_TRY(hipStreamWaitEvent(s, c->ev_cp[3], 0));
+    if (nr) {
+        k_soa_to_tiles<<<std::min<uint32_t>(nblocks(nr), 4 * c->n_cus), BLOCK, 0, s>>>(
+            reinterpret_cast<const uint32_t*>(st), reinterpret_cast<const int64_t*>(st + uid_at), nr,
+            dp<uint32_t>(c->dl_rec.buf), colmax);
+        if (nref) k_delta_inline<<<nblocks(nref), BLOCK, 0, s>>>(dp<uint32_t>(c->dl_off), dp<uint32_t>(c->dl_topo), n,
+                                                       dp<uint32_t>(c->dl_ref), nref, dp<uint32_t>(c->st_off32),
+                                                       c->dl_rec.view, misc + MISC_DELTA_ERR,
+                                                       dp<uint32_t>(c->sh_des.buf));
+    }
+    k_delta_totals<<<1, 64, 0, s>>>(dp<uint64_t>(c->st_off64), Tn, remap ? dp<uint64_t>(c->st_roff64) : nullptr, misc);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipStreamSynchronize(s));
+    uint32_t* hm = c->h_misc + 64;
+    HIP_TRY(hipMemcpyAsync(hm, misc, 64 * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));              // the call's one synchronisation
+    uint32_t err = hm[MISC_DELTA_ERR];
+    if (d->records.n)
+        for (int k = 0; k < COL_GAP; ++k)
+            if (hm[MISC_COLMAX + k] >= (k < KDTN_NKEY ? D : P)) err |= DERR_COLS;
+    if (err) {
+        static const char* what[] = {"topo not strictly ascending below n_topos", "des_off not monotone",
+                                     "spec nil but records", "status / name id out of range", "ref out of range",
+                                     "prev: index out of range or named twice", "a created topology has no spec",
+                                     "kept dictionary prefix differs from the resident one",
+                                     "inline record id out of range"};
+        int b = 0;
+        while (!(err & (1u << b))) ++b;
+        bad(what[b], err);
+        state_changed(c);
+        // nothing resident was replaced: the dictionaries only wrote past the resident strings
+        // (unless their kept prefix itself disagreed), so their sizes go back and a corrected
+        // delta can follow; the next run re-parses the previous upload's suffix
+        c->D = saved[0], c->P = saved[1], c->kd_valid = saved[2], c->pd_valid = saved[3];
+        c->kd_from = saved[4], c->pd_from = saved[5];
+        c->kd_arena = saved_arena[0], c->pd_arena = saved_arena[1];
+        c->uploaded = !(err & DERR_KEEP);
+        return KDTN_EINVAL;
+    }
+    const uint64_t N = (uint64_t)hm[MISC_DELTA_N] | ((uint64_t)hm[MISC_DELTA_N + 1] << 32);
     std::swap(c->des, c->sh_des);
+    c->des.n = c->des.view.n = (uint32_t)N;
     std::swap(c->t_noff, c->st_off32);
+    std::swap(c->t_src, c->sh_src);
+    std::swap(c->t_netns, c->sh_netns);
+    std::swap(c->t_flags, c->sh_flags);
+    if (remap) {
+        const uint64_t M = (uint64_t)hm[MISC_DELTA_M] | ((uint64_t)hm[MISC_DELTA_M + 1] << 32);
+        std::swap(c->real, c->sh_real);
+        c->real.n = c->real.view.n = (uint32_t)M;
+        std::swap(c->t_roff, c->st_roff32);
+        std::swap(c->t_ns, c->sh_ns);
+        std::swap(c->t_name, c->sh_name);
+        c->T = Tn;
+    }
     TRY(prepare_vnis(c, d->vnis));
-    TRY(prepare_work(c, c->slice, c->real.n, c->des.n));
-    TRY(patch_pods(c, n_rows));
-    HIP_TRY(hipStreamSynchronize(s));              // host arrays may be released after return
+    TRY(prepare_work(c, slice, c->real.n, c->des.n));
+    if (remap) {                                    // rows moved: the next run builds the pod tables
+        c->pods_ready = false;
+        c->pods_delta = false;
+    } else {
+        TRY(patch_pods(c, hm[MISC_ROWCHG_N]));
+    }
+    if (d->vnis.n && d->vnis.n != KDTN_VNI_RESIDENT)
+        HIP_TRY(hipStreamSynchronize(s));          // the snapshot's host arrays may be released after return
     state_changed(c);
     c->pods_imported = false;
     c->uploaded = true;
@@ -2940,20 +3142,15 @@ int kdtn_epoch_upload_delta(kdtn_ctx* c, const kdtn_epoch_delta* d) {
 
 int kdtn_epoch_tables_info(kdtn_ctx* c, kdtn_ingest_info* info) {
     if (!c || !c->uploaded) return KDTN_EINVAL;
-    HIP_TRY(hipSetDevice(c->device));
-    uint32_t kb = 0, pb = 0;
-    HIP_TRY(hipMemcpyAsync(&kb, dp<uint32_t>(c->kd_offs) + c->D, 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(&pb, dp<uint32_t>(c->pd_offs) + c->P, 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    kdtn_ingest_info& I = c->j_info;
+    kdtn_ingest_info& I = c->j_info;             // host-known sizes: no device access
     I = kdtn_ingest_info{};
     I.n_topos = c->T;
     I.n_desired = c->des.n;
     I.n_realised = c->real.n;
     I.n_kdict = c->D;
     I.n_pdict = c->P;
-    I.kdict_bytes = kb;
-    I.pdict_bytes = pb;
+    I.kdict_bytes = c->kd_arena;
+    I.pdict_bytes = c->pd_arena;
     c->tables_cur = true;
     if (info) *info = I;
     return KDTN_OK;

@@ -49,7 +49,8 @@ enum : int {
 };
 // special key-string ids found by k_kdict_flags (0xFFFFFFFF when absent)
 enum : int { SPECIAL_DEFAULT = 0, SPECIAL_LOCALHOST = 4, MISC_FAN_NODES = 12, MISC_VNI_N = 13,
-             MISC_COMMIT_N = 14, MISC_ROWCHG_N = 15, MISC_COLMAX = 16 /* [19] */ };   // misc words (64 = 256 B)
+             MISC_COMMIT_N = 14, MISC_ROWCHG_N = 15, MISC_COLMAX = 16 /* [19] */, MISC_DELTA_ERR = 36,
+             MISC_DELTA_N = 38 /* u64 */, MISC_DELTA_M = 40 /* u64 */ };   // misc words (64 = 256 B)
 // epoch sync header (u32 words; zeroed by the epoch's only memset, the look-back status
 // follows at SYNC_HEADER_BYTES). The ticket counter, which every k_reconcile workgroup
 // increments, has a 128-B line to itself; the host reads words [SYNC_TOTALS, SYNC_TOTALS + 4)
@@ -325,18 +326,67 @@ enum : uint8_t { ASM_SEG_A = 0, ASM_SEG_B = 1, ASM_REF = 2 };   // source of a t
 __global__ void k_commit_plan(DevTopos T, const uint8_t* action, const uint32_t* cut, const uint8_t* mask,
                               uint32_t* len, uint32_t* base, uint8_t* mode, uint8_t* flags_out, uint32_t* n_commit);
 __global__ void k_commit_all_flags(uint8_t* flags, uint32_t T);
-__global__ void k_delta_map(const uint32_t* topo, uint32_t n, uint32_t* chg);
-__global__ void k_delta_plan(DevTopos T, const uint32_t* chg, const uint32_t* d_off, const uint32_t* d_src,
-                             const uint32_t* d_netns, const uint8_t* d_nil, uint32_t* len, uint32_t* base,
-                             uint8_t* mode, uint32_t* src_ip, uint32_t* net_ns, uint8_t* flags,
-                             uint32_t* row_list, uint32_t* row_n);
+__global__ void k_delta_map(const uint32_t* topo, uint32_t n, uint32_t T, uint32_t* chg);
+// delta validation error bits (misc word MISC_DELTA_ERR)
+enum : uint32_t { DERR_TOPO = 1, DERR_OFF = 2, DERR_NIL = 4, DERR_IDS = 8, DERR_REF = 16, DERR_PREV = 32,
+                  DERR_NEW = 64, DERR_KEEP = 128, DERR_COLS = 256 };
+struct DeltaPlanIn {
+    DevTopos T0;                          // the resident (previous) topology table
+    const uint32_t* chg;                  // [n_topos] changed-list index, NONE = unchanged
+    const uint32_t* prev;                 // [n_topos] previous index | KDTN_DELTA_NEW; NULL = identity
+    const uint32_t* d_off;
+    const uint32_t* d_src;
+    const uint32_t* d_netns;
+    const uint8_t* d_nil;
+    const uint32_t* d_ns;
+    const uint32_t* d_name;
+    uint32_t n_topos, D;
+};
+struct DeltaPlanOut {
+    uint32_t* ns;                         // (prev only)
+    uint32_t* name;                       // (prev only)
+    uint32_t* src_ip;
+    uint32_t* net_ns;
+    uint8_t* flags;
+    uint32_t* dlen;                       // desired plan
+    uint32_t* dbase;
+    uint8_t* dmode;
+    uint32_t* rlen;                       // realised plan (prev only; mode ASM_SEG_A)
+    uint32_t* rbase;
+    uint32_t* row_list;                   // changed pod-status rows (identity only)
+    uint32_t* row_n;
+    uint32_t* seen;                       // [ceil(T0/32)] previous indices named (prev only)
+    uint32_t* err;
+};
+struct DeltaCheckIn {
+    const uint32_t* topo;
+    const uint32_t* off;
+    const uint8_t* nil;
+    const uint32_t* src;
+    const uint32_t* netns;
+    const uint32_t* ref;
+    const uint32_t* kd_offs;              // resident dictionary offsets (kept prefix)
+    const uint32_t* pd_offs;
+    uint32_t n, nref, n_topos, D, n_new, n_old;
+    uint32_t kd_keep, pd_keep, kd_expect, pd_expect;
+};
+__global__ void k_delta_plan(DeltaPlanIn in, DeltaPlanOut o);
+__global__ void k_delta_check(DeltaCheckIn in, uint32_t* err);
+__global__ void k_delta_totals(const uint64_t* doff, uint32_t Tn, const uint64_t* roff, uint32_t* misc);
 __global__ void k_off_narrow(const uint64_t* in, uint32_t n, uint32_t* out);
 __global__ void k_pods_pack(DevTopos T, const uint32_t* topo, uint32_t n, uint32_t cap, uint32_t rank_base,
                             uint4* out);
 __global__ void k_pods_patch(const uint4* ent, uint32_t n, uint4* pods, uint4* slots, uint32_t stamp, uint32_t nd);
 __global__ void k_soa_to_tiles(const uint32_t* stage, const int64_t* uid, uint32_t n, uint32_t* out, uint32_t* colmax);
+struct AsmGuard {                         // k_store_assemble in a delta upload (all zero otherwise)
+    const uint32_t* err;                  // the delta's error word: nothing is copied once set
+    const uint64_t* n_dev;                // exact record count (the grid covers a bound)
+    uint32_t skip_new;                    // inline records are placed by k_delta_inline
+};
 __global__ void k_store_assemble(const uint32_t* off, uint32_t nt, const uint32_t* base, const uint8_t* mode,
-                                 const uint32_t* ref, DevLinks A, DevLinks B, uint32_t n, uint32_t* out);
+                                 const uint32_t* ref, DevLinks A, DevLinks B, uint32_t n, AsmGuard g, uint32_t* out);
+__global__ void k_delta_inline(const uint32_t* d_off, const uint32_t* topo, uint32_t n, const uint32_t* ref,
+                               uint32_t nref, const uint32_t* off, DevLinks B, const uint32_t* err, uint32_t* out);
 
 // ---- RemotePod messages (kdtn_wire.hip) and the receiving daemon's tc argv (kdtn_tc.hip) ----
 // message m: the UpdateRemote payload of add entry rem_idx[m] (m < n_remote, fan-out order) or

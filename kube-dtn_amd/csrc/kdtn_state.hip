@@ -70,38 +70,126 @@ __global__ void __launch_bounds__(BLOCK) k_commit_all_flags(uint8_t* flags, uint
     flags[t] = (uint8_t)((fl & ~KDTN_TOPO_STATUS_NIL) | ((fl & KDTN_TOPO_SPEC_NIL) ? KDTN_TOPO_STATUS_NIL : 0));
 }
 
-// delta plan: changed Topologies (chg[t] = index into the delta, NONE = unchanged) take their
-// reference list; the others keep their previous desired segment. Changed rows also take
-// their new status.src_ip / status.net_ns / spec-nil bit.
-__global__ void __launch_bounds__(BLOCK) k_delta_plan(DevTopos T, const uint32_t* chg, const uint32_t* d_off,
-                                                      const uint32_t* d_src, const uint32_t* d_netns,
-                                                      const uint8_t* d_nil, uint32_t* len, uint32_t* base,
-                                                      uint8_t* mode, uint32_t* src_ip, uint32_t* net_ns,
-                                                      uint8_t* flags, uint32_t* row_list, uint32_t* row_n) {
-    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
-    if (t >= T.n) return;
-    const uint32_t c = chg[t];
-    if (c == 0xFFFFFFFFu) {
-        len[t] = T.des_off[t + 1] - T.des_off[t];
-        base[t] = T.des_off[t];
-        mode[t] = ASM_SEG_A;
-        return;
-    }
-    len[t] = d_off[c + 1] - d_off[c];
-    base[t] = d_off[c];
-    mode[t] = ASM_REF;
-    const uint8_t fl = flags[t];
-    const uint8_t nfl = (uint8_t)((fl & ~KDTN_TOPO_SPEC_NIL) | (d_nil[c] ? KDTN_TOPO_SPEC_NIL : 0));
-    if (src_ip[t] != d_src[c] || net_ns[t] != d_netns[c] || fl != nfl)
-        row_list[atomicAdd(row_n, 1u)] = t;            // a changed pod-status row (any order)
-    src_ip[t] = d_src[c];
-    net_ns[t] = d_netns[c];
-    flags[t] = nfl;
+// wave-OR of an error word, one atomic per wave
+KD_INLINE void delta_err(uint32_t e, uint32_t* err) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) e |= __shfl_xor(e, d, 64);
+    if ((threadIdx.x & 63) == 0 && e) atomicOr(err, e);
 }
 
-__global__ void __launch_bounds__(BLOCK) k_delta_map(const uint32_t* topo, uint32_t n, uint32_t* chg) {
+// delta plan, one thread per topology t of the NEW table: changed Topologies (chg[t] = index
+// into the delta, NONE = unchanged) take their reference list, the others their previous
+// desired segment. With a topology map (prev) every row comes from its previous row or, for a
+// created Topology, from the delta (ns / name; status.links nil, no realised records), and the
+// realised plan (rlen / rbase) carries each kept Topology's status segment to its new position;
+// a previous index named twice or out of range, or a created Topology absent from the changed
+// list, is an error. Without a map (identity) a changed row whose pod-status fields move is
+// listed for the resident pod-table patch. New columns go to `out` (the state is untouched
+// until the host accepts the delta).
+__global__ void __launch_bounds__(BLOCK) k_delta_plan(DeltaPlanIn in, DeltaPlanOut o) {
+    if (*o.err) return;                             // k_delta_check refused the delta's arrays
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    uint32_t e = 0;
+    if (t < in.n_topos) {
+        const DevTopos& T = in.T0;
+        const uint32_t c = in.chg[t];
+        uint32_t p = t;
+        if (in.prev) {
+            p = in.prev[t];
+            if (p != KDTN_DELTA_NEW) {
+                if (p >= T.n) {
+                    e |= DERR_PREV;
+                    p = KDTN_DELTA_NEW;
+                } else if (atomicOr(o.seen + (p >> 5), 1u << (p & 31u)) & (1u << (p & 31u))) {
+                    e |= DERR_PREV;                                  // named twice
+                }
+            } else if (c == 0xFFFFFFFFu) {
+                e |= DERR_NEW;                                       // created without a spec
+            }
+        }
+        uint32_t ns = 0, name = 0, src = 0, netns = 0, dlen = 0, dbase = 0, rlen = 0, rbase = 0;
+        uint8_t fl = KDTN_TOPO_STATUS_NIL, mode = ASM_SEG_A;
+        if (p != KDTN_DELTA_NEW) {
+            ns = T.ns[p];
+            name = T.name[p];
+            src = T.src_ip[p];
+            netns = T.net_ns[p];
+            fl = T.flags[p];
+            dbase = T.des_off[p];
+            dlen = T.des_off[p + 1] - dbase;
+            rbase = T.real_off[p];
+            rlen = T.real_off[p + 1] - rbase;
+        } else if (c != 0xFFFFFFFFu) {
+            ns = in.d_ns[c];
+            name = in.d_name[c];
+            if (ns >= in.D || name >= in.D) e |= DERR_IDS;
+        }
+        if (c != 0xFFFFFFFFu) {
+            dbase = in.d_off[c];
+            dlen = in.d_off[c + 1] - dbase;
+            mode = ASM_REF;
+            const uint8_t nfl = (uint8_t)((fl & ~KDTN_TOPO_SPEC_NIL) | (in.d_nil[c] ? KDTN_TOPO_SPEC_NIL : 0));
+            if (!in.prev && (src != in.d_src[c] || netns != in.d_netns[c] || fl != nfl))
+                o.row_list[atomicAdd(o.row_n, 1u)] = t;              // a changed pod-status row (any order)
+            src = in.d_src[c];
+            netns = in.d_netns[c];
+            fl = nfl;
+        }
+        o.dlen[t] = dlen;
+        o.dbase[t] = dbase;
+        o.dmode[t] = mode;
+        o.src_ip[t] = src;
+        o.net_ns[t] = netns;
+        o.flags[t] = fl;
+        if (in.prev) {
+            o.ns[t] = ns;
+            o.name[t] = name;
+            o.rlen[t] = rlen;
+            o.rbase[t] = rbase;
+        }
+    }
+    delta_err(e, o.err);
+}
+
+__global__ void __launch_bounds__(BLOCK) k_delta_map(const uint32_t* topo, uint32_t n, uint32_t T, uint32_t* chg) {
     const uint32_t c = blockIdx.x * BLOCK + threadIdx.x;
-    if (c < n) chg[topo[c]] = c;
+    if (c < n && topo[c] < T) chg[topo[c]] = c;
+}
+
+// The delta's arrays checked on the GPU instead of host loops: thread i checks changed entry i
+// (topology index in range and strictly ascending, offsets monotone, a nil spec without
+// records, status ids in the dictionary) and references i, i + grid, ... (previous record in
+// range, inline record in range); thread 0 also compares the kept dictionaries' arena offsets
+// with the ones the resident state was parsed from (before this call's upload overwrites them).
+__global__ void __launch_bounds__(BLOCK) k_delta_check(DeltaCheckIn in, uint32_t* err) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    uint32_t e = 0;
+    if (i < in.n) {
+        const uint32_t t = in.topo[i];
+        if (t >= in.n_topos || (i && t <= in.topo[i - 1])) e |= DERR_TOPO;
+        if (in.off[i + 1] < in.off[i]) e |= DERR_OFF;
+        if (in.nil[i] && in.off[i + 1] != in.off[i]) e |= DERR_NIL;
+        if (in.src[i] >= in.D || in.netns[i] >= in.D) e |= DERR_IDS;
+    }
+    for (uint32_t k = i; k < in.nref; k += gridDim.x * BLOCK) {
+        const uint32_t r = in.ref[k];
+        if ((r & KDTN_DELTA_NEW) ? (r & ~KDTN_DELTA_NEW) >= in.n_new : r >= in.n_old) e |= DERR_REF;
+    }
+    if (i == 0) {
+        if (in.kd_keep && in.kd_offs[in.kd_keep] != in.kd_expect) e |= DERR_KEEP;
+        if (in.pd_keep && in.pd_offs[in.pd_keep] != in.pd_expect) e |= DERR_KEEP;
+    }
+    delta_err(e, err);
+}
+
+// the totals the host reads back with the delta's one synchronisation
+__global__ void k_delta_totals(const uint64_t* doff, uint32_t Tn, const uint64_t* roff, uint32_t* misc) {
+    if (threadIdx.x != 0) return;
+    const uint64_t n = doff[Tn], m = roff ? roff[Tn] : 0ull;
+    misc[MISC_DELTA_N] = (uint32_t)n;
+    misc[MISC_DELTA_N + 1] = (uint32_t)(n >> 32);
+    misc[MISC_DELTA_M] = (uint32_t)m;
+    misc[MISC_DELTA_M + 1] = (uint32_t)(m >> 32);
 }
 
 // u64 exclusive offsets (k_scan_final) → the u32 offsets of a topology table
@@ -124,10 +212,18 @@ KD_INLINE void copy_record(const uint32_t* sbase, uint32_t j, uint32_t* dbase, u
 
 // one thread per output record d: its topology by binary search over the new offsets, then
 // one record copied from the plan's source (coalesced within a segment: consecutive outputs
-// read consecutive source records)
+// read consecutive source records). Delta uploads (g != NULL): n bounds the grid and the exact
+// count is the one the offsets' scan left on the device (no host readback first); nothing is
+// copied when the delta was refused (its references are not trusted); with skip_new the
+// inline records (still in flight over the host link) are left to k_delta_inline.
 __global__ void __launch_bounds__(BLOCK) k_store_assemble(const uint32_t* off, uint32_t nt, const uint32_t* base,
                                                           const uint8_t* mode, const uint32_t* ref, DevLinks A,
-                                                          DevLinks B, uint32_t n, uint32_t* out) {
+                                                          DevLinks B, uint32_t n, AsmGuard g, uint32_t* out) {
+    if (g.err) {
+        if (*g.err) return;
+        const uint64_t m = *g.n_dev;
+        n = m < n ? (uint32_t)m : n;
+    }
     const uint32_t d = blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t t = entry_topo_wave(off, nt, d, d < n);   // (all lanes: wave-cooperative)
     if (d >= n) return;
@@ -137,9 +233,27 @@ __global__ void __launch_bounds__(BLOCK) k_store_assemble(const uint32_t* off, u
     else if (m == ASM_SEG_B) copy_record(B.base, k, out, d);
     else {
         const uint32_t r = ref[k];
-        if (r & KDTN_DELTA_NEW) copy_record(B.base, r & ~KDTN_DELTA_NEW, out, d);
-        else copy_record(A.base, r, out, d);
+        if (r & KDTN_DELTA_NEW) {
+            if (!g.skip_new) copy_record(B.base, r & ~KDTN_DELTA_NEW, out, d);
+        } else {
+            copy_record(A.base, r, out, d);
+        }
     }
+}
+
+// The inline records of a delta into their places in the new desired store, one thread per
+// reference k: its changed Topology c (upper bound over the delta's offsets), that Topology's
+// new index topo[c], and the output position off[topo[c]] + (k - d_off[c]).
+__global__ void __launch_bounds__(BLOCK) k_delta_inline(const uint32_t* d_off, const uint32_t* topo, uint32_t n,
+                                                        const uint32_t* ref, uint32_t nref, const uint32_t* off,
+                                                        DevLinks B, const uint32_t* err, uint32_t* out) {
+    if (*err) return;
+    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+    if (k >= nref) return;
+    const uint32_t r = ref[k];
+    if (!(r & KDTN_DELTA_NEW)) return;
+    const uint32_t c = entry_topo(d_off, n, k);
+    copy_record(B.base, r & ~KDTN_DELTA_NEW, out, off[topo[c]] + (k - d_off[c]));
 }
 
 // Link-store upload from SoA columns: the host columns arrive by linear copies into a staging

@@ -82,7 +82,8 @@ DELTA_NEW = 0x80000000     # kdtn_epoch_delta.ref: inline record k of the delta
 class EpochDelta(C.Structure):
     _fields_ = [("kdict", Strtab), ("pdict", Strtab), ("kdict_keep", C.c_uint32), ("pdict_keep", C.c_uint32),
                 ("n_changed", C.c_uint32), ("topo", u32p), ("src_ip", u32p), ("net_ns", u32p), ("spec_nil", u8p),
-                ("des_off", u32p), ("ref", u32p), ("records", LinkTable), ("vnis", VniTable)]
+                ("des_off", u32p), ("ref", u32p), ("records", LinkTable), ("vnis", VniTable),
+                ("n_topos", C.c_uint32), ("prev", u32p), ("ns", u32p), ("name", u32p), ("pod_slice", C.c_uint32)]
 
 
 class PropsTable(C.Structure):

@@ -166,10 +166,14 @@ def pin_delta(d):
     from .tables import Links
     P = pinned_copy
     r = d.records
+    extra = {} if d.prev is None else {"prev": P(d.prev), "ns": P(d.ns), "name": P(d.name)}
+    v = d.vnis
+    vn = v if v.resident else Vnis(P(v.node), P(v.vni), P(v.net_ns))
     return replace(d, kdict=StrTab(P(d.kdict.bytes_), P(d.kdict.offs)), pdict=StrTab(P(d.pdict.bytes_), P(d.pdict.offs)),
                    topo=P(d.topo), src_ip=P(d.src_ip), net_ns=P(d.net_ns), spec_nil=P(d.spec_nil),
-                   des_off=P(d.des_off), ref=P(d.ref),
-                   records=Links(P(np.ascontiguousarray(r.key)), P(r.uid), P(np.ascontiguousarray(r.prop)), P(r.gap)))
+                   des_off=P(d.des_off), ref=P(d.ref), vnis=vn,
+                   records=Links(P(np.ascontiguousarray(r.key)), P(r.uid), P(np.ascontiguousarray(r.prop)), P(r.gap)),
+                   **extra)
 
 
 def topology_shard(namespace, name, nshards: int) -> int:
@@ -364,6 +368,14 @@ class Engine:
         pinned=True, reused across epochs)."""
         cd, ca, cu = self._caps
         out = into if into is not None else BatchesOut.alloc(self._T, cd, ca, cu)
+        T = self._T
+        if (len(out.action) != T or any(len(getattr(out, f)) != T + 1 for f in ("del_off", "add_off", "upd_off"))
+                or len(out.del_res) < len(out.del_idx) or len(out.add_res) < len(out.add_idx)
+                or len(out.upd_res) < len(out.upd_idx) or len(out.add_qdisc) < len(out.add_idx)
+                or len(out.upd_qdisc) < len(out.upd_idx)):
+            # kdtn_epoch_download writes T action bytes and T+1 offsets per list unchecked
+            raise ValueError(f"download(into=...): buffers sized for {len(out.action)} topologies, "
+                             f"the epoch has {T}")
         b = out.to_c((len(out.del_idx), len(out.add_idx), len(out.upd_idx)))
         _check(lib().kdtn_epoch_download(self._ctx, C.byref(b)), "kdtn_epoch_download")
         return out.trim(b.n_del, b.n_add, b.n_upd)

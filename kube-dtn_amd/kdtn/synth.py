@@ -189,6 +189,62 @@ class ChurnSequence:
         self.epoch = _load().kdtn_synth_advance(self._h.ptr)
 
 
+def select_topologies(inp: EpochInput, keep: np.ndarray) -> EpochInput:
+    """The epoch restricted to the Topologies with keep[t] (order kept): their rows and both
+    link segments; the dictionaries and the VXLAN snapshot are shared. Peers of a dropped
+    Topology stay in the kept ones' links (their lookups then fail, as for a deleted CR)."""
+    keep = np.asarray(keep, bool)
+    sel = np.nonzero(keep)[0]
+    T = inp.topos
+
+    def side(L: Links, off: np.ndarray):
+        off = off.astype(np.int64)
+        lens = off[sel + 1] - off[sel]
+        start = np.repeat(off[sel], lens)
+        idx = start + np.arange(int(lens.sum()), dtype=np.int64) - np.repeat(np.cumsum(lens) - lens, lens)
+        new_off = np.zeros(len(sel) + 1, np.uint32)
+        np.cumsum(lens, out=new_off[1:])
+        return L.take(idx) if L.n else Links.empty(0), new_off
+
+    real, roff = side(inp.realised, T.real_off)
+    des, doff = side(inp.desired, T.des_off)
+    topos = Topos(T.ns[sel].copy(), T.name[sel].copy(), T.src_ip[sel].copy(), T.net_ns[sel].copy(),
+                  T.flags[sel].copy(), roff, doff)
+    out = EpochInput(inp.kdict, inp.pdict, topos, real, des, inp.vnis)
+    out.total_pods = getattr(inp, "total_pods", 0)
+    out.gid = inp.gid[sel] if inp.gid is not None else None
+    return out
+
+
+class TopologySetChurn:
+    """Config 3 with a changing Topology set: on top of ChurnSequence's link churn, every
+    advance() deletes frac/2 of the live Topologies (a CR deleted: spec and status gone,
+    DestroyPod) and re-creates as many of the absent ones (a new CR with its current spec and
+    no status: the CREATED path, controllers/topology_controller.go:81-85; SetupPod). The
+    epoch lists the live Topologies in generator order; links to an absent pod stay and fail
+    their peer lookup. frac of the Topologies start absent."""
+
+    def __init__(self, frac: float = 0.01, seed: int = 7, **kw):
+        self.cs = ChurnSequence(**kw)
+        T = self.cs.epoch_input().topos.n
+        self.rng = np.random.default_rng(seed)
+        self.frac = frac
+        self.alive = np.ones(T, bool)
+        self.alive[self.rng.choice(T, int(T * frac), replace=False)] = False
+
+    def epoch_input(self, copy: bool = True) -> EpochInput:
+        return select_topologies(self.cs.epoch_input(copy=True), self.alive)
+
+    def advance(self) -> None:
+        self.cs.advance()
+        k = max(1, int(len(self.alive) * self.frac / 2))
+        live, dead = np.nonzero(self.alive)[0], np.nonzero(~self.alive)[0]
+        kill = self.rng.choice(live, min(k, len(live)), replace=False)
+        back = self.rng.choice(dead, min(k, len(dead)), replace=False)
+        self.alive[kill] = False
+        self.alive[back] = True
+
+
 def topology_list_json(inp: EpochInput, pretty: bool = False) -> bytes:
     """The epoch's Topology CRs as a Kubernetes TopologyList JSON document, the way the API
     server serves them (sorted keys, encoding/json escaping) — the CR-ingest workload."""

@@ -65,39 +65,82 @@ def commit(inp: EpochInput, mask: np.ndarray) -> EpochInput:
     return EpochInput(inp.kdict, inp.pdict, topos, L, inp.desired, inp.vnis, pod_slice=inp.pod_slice)
 
 
+def _gather(L: Links, idx: np.ndarray, out: Links, sel: np.ndarray) -> None:
+    out.key[:, sel] = L.key[:, idx]
+    out.prop[:, sel] = L.prop[:, idx]
+    out.uid[sel] = L.uid[idx]
+    out.gap[sel] = L.gap[idx]
+
+
+def _segments(off: np.ndarray, which: np.ndarray) -> np.ndarray:
+    """Concatenated record indices of the segments [off[t], off[t+1]) for t in `which`."""
+    off = np.asarray(off, np.int64)
+    lens = off[which + 1] - off[which]
+    if not len(which) or lens.sum() == 0:
+        return np.zeros(0, np.int64)
+    start = np.repeat(off[which], lens)
+    within = np.arange(int(lens.sum()), dtype=np.int64) - np.repeat(np.cumsum(lens) - lens, lens)
+    return start + within
+
+
 def apply_delta(state: EpochInput, delta) -> EpochInput:
-    """The epoch tables after kdtn_epoch_upload_delta(delta) on `state`."""
-    T = state.topos
-    no = T.des_off.astype(np.int64)
-    pos = {int(t): k for k, t in enumerate(delta.topo)}
-    parts = []
-    lens = np.diff(no).copy()
-    src, net, fl = T.src_ip.copy(), T.net_ns.copy(), T.flags.copy()
-    for t in range(T.n):
-        k = pos.get(t)
-        if k is None:
-            parts.append(("old", np.arange(no[t], no[t + 1])))
-            continue
-        r = delta.ref[delta.des_off[k]:delta.des_off[k + 1]].astype(np.int64)
-        parts.append(("ref", r))
-        lens[t] = len(r)
-        src[t], net[t] = delta.src_ip[k], delta.net_ns[k]
-        fl[t] = (int(fl[t]) & (0xFF ^ abi.TOPO_SPEC_NIL)) | (abi.TOPO_SPEC_NIL if delta.spec_nil[k] else 0)
-    n = int(lens.sum())
-    L = Links.empty(n)
-    d = 0
-    for kind, r in parts:
-        for x in r.tolist():
-            if kind == "ref" and x & abi.DELTA_NEW:
-                s, j = delta.records, x & ~abi.DELTA_NEW
-            else:
-                s, j = state.desired, x
-            L.key[:, d], L.prop[:, d], L.uid[d], L.gap[d] = s.key[:, j], s.prop[:, j], s.uid[j], s.gap[j]
-            d += 1
-    off = np.zeros(T.n + 1, np.int64)
-    np.cumsum(lens, out=off[1:])
-    topos = Topos(T.ns, T.name, src, net, fl, T.real_off, off.astype(np.uint32))
-    return EpochInput(delta.kdict, delta.pdict, topos, state.realised, L, delta.vnis, pod_slice=state.pod_slice)
+    """The epoch tables after kdtn_epoch_upload_delta(delta) on `state`: per new Topology its
+    previous row (or, created, the delta's ns / name with a nil status and no realised
+    records), the changed Topologies' spec from their reference lists, the rest unchanged."""
+    T0 = state.topos
+    if delta.prev is None:
+        pmap = np.arange(T0.n, dtype=np.int64)
+    else:
+        pv = delta.prev.astype(np.int64)
+        pmap = np.where(pv == abi.DELTA_NEW, -1, pv)
+    Tn = len(pmap)
+    kept = pmap >= 0
+    pk = np.where(kept, pmap, 0)
+    chg = np.full(Tn, -1, np.int64)
+    chg[delta.topo.astype(np.int64)] = np.arange(delta.n_changed)
+    ro, no = T0.real_off.astype(np.int64), T0.des_off.astype(np.int64)
+    # topology rows
+    ns = np.where(kept, T0.ns[pk] if T0.n else 0, 0).astype(np.uint32)
+    name = np.where(kept, T0.name[pk] if T0.n else 0, 0).astype(np.uint32)
+    src = np.where(kept, T0.src_ip[pk] if T0.n else 0, 0).astype(np.uint32)
+    net = np.where(kept, T0.net_ns[pk] if T0.n else 0, 0).astype(np.uint32)
+    fl = np.where(kept, T0.flags[pk] if T0.n else 0, abi.TOPO_STATUS_NIL).astype(np.uint8)
+    c = chg >= 0
+    k = chg[c]
+    if delta.prev is not None:
+        created = c & ~kept
+        ns[created], name[created] = delta.ns[chg[created]], delta.name[chg[created]]
+    src[c], net[c] = delta.src_ip[k], delta.net_ns[k]
+    fl[c] = (fl[c] & np.uint8(0xFF ^ abi.TOPO_SPEC_NIL)) | np.where(delta.spec_nil[k] != 0, abi.TOPO_SPEC_NIL, 0).astype(np.uint8)
+    # realised: kept Topologies' status segments in the new order
+    rlen = np.where(kept, (ro[pk + 1] - ro[pk]) if T0.n else 0, 0)
+    roff = np.zeros(Tn + 1, np.int64)
+    np.cumsum(rlen, out=roff[1:])
+    ridx = _segments(T0.real_off, pk[kept]) if kept.any() else np.zeros(0, np.int64)
+    R = Links.empty(int(roff[-1]))
+    _gather(state.realised, ridx, R, np.arange(len(ridx)))
+    # desired: unchanged kept Topologies keep their segment, changed ones take their references
+    dlen = np.where(kept, (no[pk + 1] - no[pk]) if T0.n else 0, 0)
+    dlen[c] = delta.des_off[k + 1].astype(np.int64) - delta.des_off[k].astype(np.int64)
+    doff = np.zeros(Tn + 1, np.int64)
+    np.cumsum(dlen, out=doff[1:])
+    L = Links.empty(int(doff[-1]))
+    src_kind = np.zeros(L.n, np.int8)          # 0 previous desired record, 1 inline record
+    src_idx = np.zeros(L.n, np.int64)
+    keep_t = np.nonzero(~c & kept)[0]
+    dst = _segments(doff, keep_t)
+    src_idx[dst] = _segments(T0.des_off, pk[keep_t])
+    chg_t = np.nonzero(c)[0]
+    dst = _segments(doff, chg_t)
+    refs = delta.ref[_segments(delta.des_off, chg[chg_t])].astype(np.int64)
+    inl = (refs & abi.DELTA_NEW) != 0
+    src_kind[dst] = inl
+    src_idx[dst] = np.where(inl, refs & ~abi.DELTA_NEW, refs)
+    _gather(state.desired, src_idx[src_kind == 0], L, src_kind == 0)
+    _gather(delta.records, src_idx[src_kind == 1], L, src_kind == 1)
+    topos = Topos(ns, name, src, net, fl, roff.astype(np.uint32), doff.astype(np.uint32))
+    slice_ = state.pod_slice if delta.prev is None else (delta.pod_slice or 0)
+    return EpochInput(delta.kdict, delta.pdict, topos, R, L, delta.vnis, pod_slice=slice_)
 
 
 def same_tables(a: EpochInput, b: EpochInput) -> list[str]:

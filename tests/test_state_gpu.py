@@ -131,3 +131,81 @@ def test_all_committed_commit_keeps_every_view():
         _run_same(eng, st2, "partial commit after the fast one")
         eng.upload(b)
         _run_same(eng, b, "full upload after the commits")
+
+
+def test_topology_set_churn_chain():
+    """Ten config-3 churn epochs with 1 % of the Topologies deleted / re-created per epoch
+    (informer delete / add events; CREATED path, controllers/topology_controller.go:81-85)
+    through kdtn_epoch_upload_delta: the device tables equal the restatement's — the generator's
+    epoch with the status the commits left — and every epoch's batches equal the oracle's on
+    those tables; the last epoch also equals a second engine fed by a full upload."""
+    from kdtn.delta import record_hash
+    tc = synth.TopologySetChurn(frac=0.01, total_pods=20000)
+    prev = tc.epoch_input()
+    with Engine(device=0, tick_in_usec=TICK) as eng:
+        eng.upload(prev)
+        ora = _run_same(eng, prev, "epoch 0")
+        state = prev
+        for ep in range(1, 10):
+            mask = predicted_commit(state, ora) if ep % 2 else np.ones(state.topos.n, bool)
+            assert eng.commit(mask if ep % 2 == 0 else None) == int(mask.sum())
+            state = commit(state, mask)
+            tc.advance()
+            new = tc.epoch_input()
+            d = build_delta(state, new, state.kdict.n, state.pdict.n)
+            assert d.prev is not None and (d.prev == abi.DELTA_NEW).any()
+            eng.upload_delta(d)
+            state = apply_delta(state, d)
+            assert np.array_equal(record_hash(state.desired), record_hash(new.desired))
+            assert np.array_equal(state.topos.name, new.topos.name)
+            assert not same_tables(eng.tables(), state), ep
+            ora = _run_same(eng, state, f"epoch {ep}")
+            created = d.prev[d.topo] == abi.DELTA_NEW
+            assert (ora.action[d.topo[created]] == abi.ACT_CREATED).all()
+    with Engine(device=0, tick_in_usec=TICK) as full:
+        full.upload(state)
+        _run_same(full, state, "full upload of the last epoch")
+
+
+def test_delta_rejections_leave_the_state():
+    """A delta the engine refuses (kept dictionary not the resident one, references / inline
+    ids / topology map out of range, a created Topology without a spec) returns KDTN_EINVAL
+    and leaves the resident state: the tables, a run on them, and the corrected delta after."""
+    import dataclasses
+    from kdtn.engine import KdtnError
+    topos, vnis = random_epoch(5, T=120, p_err=0.1)
+    kd, pd = Interner(), Interner()
+    a = pack(topos, vnis, kdict=kd, pdict=pd)
+    with Engine(device=0, tick_in_usec=TICK) as eng:
+        eng.upload(a)
+        _run_same(eng, a, "epoch 0")
+        eng.commit(np.ones(a.topos.n, bool))
+        state = commit(a, np.ones(a.topos.n, bool))
+        b = pack(mutate(topos, 9), vnis, kdict=kd, pdict=pd)
+        good = build_delta(a, b, a.kdict.n, a.pdict.n, vnis=b.vnis)
+        assert good.n_changed > 2 and good.records.n > 0 and len(good.ref) > 0
+        R = dataclasses.replace
+        bads = {"shrunk kept dictionary": R(good, kdict_keep=a.kdict.n - 1),
+                "ref out of range": R(good, ref=np.where(np.arange(len(good.ref)) == len(good.ref) - 1,
+                                                        np.uint32(a.desired.n + 7), good.ref).astype(np.uint32)),
+                # far outside any allocation: the GPU checks must stop every later kernel
+                "ref far out of range": R(good, ref=np.full(len(good.ref), 0x7FFFFFF0, np.uint32)),
+                "inline ref far out of range": R(good, ref=np.full(len(good.ref), abi.DELTA_NEW | 0x7FFFFFF,
+                                                                   np.uint32)),
+                "topo far out of range": R(good, topo=np.full(good.n_changed, 0x7FFFFFF0, np.uint32)),
+                "topo not ascending": R(good, topo=good.topo[::-1].copy()),
+                "inline id out of range": R(good, records=dataclasses.replace(
+                    good.records, key=np.where(np.arange(good.records.n) == 0, np.uint32(b.kdict.n + 3),
+                                               good.records.key).astype(np.uint32))),
+                "prev named twice": R(good, prev=np.r_[0, np.arange(a.topos.n - 1)].astype(np.uint32),
+                                      ns=b.topos.ns[good.topo], name=b.topos.name[good.topo]),
+                "created without spec": R(good, prev=np.r_[np.arange(a.topos.n), abi.DELTA_NEW].astype(np.uint32),
+                                          ns=b.topos.ns[good.topo], name=b.topos.name[good.topo])}
+        for what, d in bads.items():
+            with pytest.raises(KdtnError) as e:
+                eng.upload_delta(d)
+            assert e.value.code == abi.EINVAL, what
+            assert not same_tables(eng.tables(), state), what
+            _run_same(eng, state, f"after a rejected delta ({what})")
+        eng.upload_delta(good)
+        _run_same(eng, apply_delta(state, good), "the corrected delta")
