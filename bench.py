@@ -104,7 +104,32 @@ def cpu_share():
         pass
     share = aff if quota is None else max(1, min(aff, int(math.ceil(quota))))
     return share, {"nproc": os.cpu_count(), "affinity": aff, "cgroup_quota_cpus": quota,
-                   "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+                   "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "cpu_model": cpu_model()}
+
+
+def cpu_model() -> dict:
+    """The host CPU as lscpu reports it (model, sockets, cores), /proc/cpuinfo
+    when lscpu is absent."""
+    import subprocess
+    out = {}
+    try:
+        txt = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in txt.splitlines():
+            k, _, v = line.partition(":")
+            if k.strip() in ("Model name", "Socket(s)", "Core(s) per socket", "Thread(s) per core", "CPU(s)",
+                             "CPU max MHz", "L3 cache", "NUMA node(s)"):
+                out[k.strip()] = v.strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    if "Model name" not in out:
+        try:
+            for line in open("/proc/cpuinfo"):
+                if line.startswith("model name"):
+                    out["Model name"] = line.split(":", 1)[1].strip()
+                    break
+        except OSError:
+            pass
+    return out
 
 
 def cpu_baseline(inp, budget_s: float, threads: int, share_info: dict):
@@ -249,7 +274,9 @@ def resident_chain_stage(eng, cs, prev, epochs: int, topology_set: bool = False)
     rows = []
     state_T = T
     eng.commit(np.ones(T, np.uint8))
-    for _ in range(epochs):
+    warm = 2                                             # first deltas size the rotating buffers
+    for ep in range(warm + epochs):
+        progress(f"  resident epoch {ep}")
         cs.advance()
         new = cs.epoch_input(copy=True)
         d = pin_delta(build_delta(prev, new, prev.kdict.n, prev.pdict.n))
@@ -270,8 +297,9 @@ def resident_chain_stage(eng, cs, prev, epochs: int, topology_set: bool = False)
         created = int((d.prev == abi.DELTA_NEW).sum()) if d.prev is not None else 0
         deleted = state_T - (new.topos.n - created)
         state_T = new.topos.n
-        rows.append((d.upload_bytes(), t1 - t0, t2 - t1, t3 - t2, t4 - t3, down_b, new.desired.n,
-                     d.n_changed, d.records.n, c.n_add + c.n_del + c.n_upd, created, deleted))
+        if ep >= warm:
+            rows.append((d.upload_bytes(), t1 - t0, t2 - t1, t3 - t2, t4 - t3, down_b, new.desired.n,
+                         d.n_changed, d.records.n, c.n_add + c.n_del + c.n_upd, created, deleted))
         prev = new
     a = np.array(rows, dtype=np.float64).mean(axis=0)
     full_b = 88 * (2 * prev.desired.n) + 25 * T
@@ -282,7 +310,7 @@ def resident_chain_stage(eng, cs, prev, epochs: int, topology_set: bool = False)
            "download_ms": a[3] * 1e3, "download_bytes": a[5], "download_GBps": a[5] / a[3] / 1e9,
            "commit_ms": a[4] * 1e3, "e2e_ms": e2e * 1e3, "links_per_s": a[6] / e2e,
            "note": "not part of value: per epoch delta upload + run + download + on-device status commit, "
-                   "page-locked host memory, mean over the epochs"}
+                   f"page-locked host memory, mean over {epochs} epochs after {warm} warm-up epochs"}
     if topology_set:
         res["created_topologies"], res["deleted_topologies"] = a[10], a[11]
     return res
@@ -430,6 +458,16 @@ def allsum(x: float, world: int) -> float:
     return float(t[0])
 
 
+_T0 = time.time()
+
+
+def progress(msg: str) -> None:
+    """A progress line on stderr (rank 0): long stages (generation, CPU baseline, ingest,
+    resident chains) keep the run visibly alive; stdout stays the one JSON line."""
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(f"[bench +{time.time() - _T0:6.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
 def barrier(world: int) -> None:
     if world > 1:
         dist.barrier()
@@ -515,6 +553,7 @@ def main():
     torch.cuda.set_device(dev)
     total_pods = pods if args.scaling == "strong" else pods * world
 
+    progress(f"config {args.config}: generating the workload")
     t0 = time.time()
     cs = None
     if churn:
@@ -526,6 +565,7 @@ def main():
     else:
         inp = synth.make(args.config, total_pods=total_pods, shard=rank, nshards=world)
     gen_s = time.time() - t0
+    progress(f"generated in {gen_s:.1f} s; timed epochs")
     eng = Engine(device=dev)
     exchange = "none"
     comm_ranks = 1
@@ -736,9 +776,11 @@ def main():
     if churn:
         inp = cs.epoch_input(copy=True)          # (the generator's arrays move when it advances)
     if churn and world == 1 and not args.no_e2e:
+        progress("resident chain")
         result["resident_chain"] = resident_chain_stage(eng, cs, inp, args.resident_epochs)
         # the same with Topologies created and deleted (informer add / delete events)
         del cs
+        progress("resident chain with a changing Topology set")
         tc = synth.TopologySetChurn(frac=0.01, total_pods=total_pods)
         p0 = tc.epoch_input()
         eng.upload(p0)
@@ -751,12 +793,15 @@ def main():
         result["diff_only_reconcile_ms"] = float(np.mean(diff_ms))
         result["diff_share_of_reconcile"] = float(np.mean(diff_ms)) / rec_ms
     if world == 1 and not args.no_e2e and not churn:
+        progress("PCIe-inclusive epoch")
         result["e2e_pcie"] = e2e_stage(eng, inp)
     if world == 1 and not args.no_wire and args.config == 2:
+        progress("output stages")
         result["wire_stage"] = wire_stage(eng)
     if world == 1 and not args.no_cpu_baseline:            # CPU baseline: rank 0 at N=1 only
         share, info = cpu_share()
         threads = args.cpu_threads or min(32, share)
+        progress(f"CPU baseline on {threads} threads")
         result["cpu_baseline"] = cpu_baseline(inp, args.cpu_budget_s, threads, info)
     if world == 1 and args.config == 4:                    # VxlanManager maps after the epoch
         run()
@@ -771,6 +816,7 @@ def main():
                                      "note": "not part of value: kdtn_epoch_vni_apply (deletes, then first-wins "
                                              "adds of the reached entries) + download of the map"}
     if world == 1 and not args.no_ingest and args.config == 2:
+        progress("CR ingest stage")
         result["ingest_stage"] = ingest_stage(eng, inp, steps)
     if rank == 0:
         print(json.dumps(result), flush=True)

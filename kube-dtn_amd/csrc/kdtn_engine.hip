@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -136,7 +137,7 @@ struct kdtn_ctx {
     DevBuf st_cnt, st_len, st_base, st_mode, st_flags, st_off64, st_part, st_off32, st_mask, st_chg;
     DevBuf dl_topo, dl_src, dl_netns, dl_nil, dl_off, dl_ref, dl_rows;
     // delta with a topology-set change: the map, created rows' names, the realised plan
-    DevBuf dl_prev, dl_ns, dl_name, st_rlen, st_rbase, st_roff64, st_rpart, st_roff32, st_seen;
+    DevBuf dl_prev, dl_ns, dl_name, dl_dest, st_rlen, st_rbase, st_roff64, st_rpart, st_roff32, st_seen;
     uint64_t kd_arena = 0, pd_arena = 0;       // dictionary arena bytes (host-known: tables_info)
     DevLinkStore dl_rec;
     bool tables_cur = false;                   // j_info describes the current tables (kdtn_epoch_tables_info)
@@ -186,14 +187,49 @@ struct kdtn_ctx {
 
 namespace {
 
+// Replaced device buffers are retired, not freed at once: hipFree synchronises the whole
+// device (measured: 1.3-1.5 ms inside a delta upload whose copies and kernels were in flight
+// on two streams, every overlap lost), so they are freed together once more than
+// kRetireBytes are waiting (one synchronisation for many regrowths) or when a context is
+// destroyed. Retired buffers belong to no context: nothing enqueues work on them any more, and
+// hipFree completes the work already in flight first.
+constexpr size_t kRetireBytes = (size_t)8 << 30;
+struct Retired {
+    std::mutex m;
+    std::vector<void*> p;
+    size_t bytes = 0;
+};
+Retired& retired() {
+    static Retired r;
+    return r;
+}
+void retired_flush() {
+    Retired& r = retired();
+    std::lock_guard<std::mutex> lk(r.m);
+    for (void* p : r.p) (void)hipFree(p);
+    r.p.clear();
+    r.bytes = 0;
+}
+void retire(void* p, size_t bytes) {
+    if (!p) return;
+    Retired& r = retired();
+    bool flush;
+    {
+        std::lock_guard<std::mutex> lk(r.m);
+        r.p.push_back(p);
+        r.bytes += bytes;
+        flush = r.bytes > kRetireBytes;
+    }
+    if (flush) retired_flush();
+}
+
 int ensure(DevBuf& b, size_t bytes) {
     bytes = std::max<size_t>(bytes, 256);
     if (b.cap >= bytes) return KDTN_OK;
     // grown buffers get 1/8 headroom (from 1 MB on): epoch sizes drift from epoch to epoch
-    // (a churn chain's record counts), and every regrowth is a hipFree (a device-wide
-    // synchronisation) plus a hipMalloc
+    // (a churn chain's record counts); the old buffer is retired (no device synchronisation)
     if (bytes >= (1u << 20)) bytes = (bytes + bytes / 8 + 0xFFFFF) & ~(size_t)0xFFFFF;
-    if (b.p) (void)hipFree(b.p);
+    retire(b.p, b.cap);
     b.p = nullptr;
     b.cap = 0;
     hipError_t e = hipMalloc(&b.p, bytes);
@@ -219,15 +255,14 @@ int ensure_keep(DevBuf& b, size_t bytes, size_t keep, hipStream_t s) {
         return KDTN_ENOMEM;
     }
     HIP_TRY(hipMemcpyAsync(np, b.p, std::min(keep, b.cap), hipMemcpyDeviceToDevice, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    (void)hipFree(b.p);
+    retire(b.p, b.cap);                  // (stream-ordered after the copy: no synchronisation)
     b.p = np;
     b.cap = cap;
     return KDTN_OK;
 }
 
 void release(DevBuf& b) {
-    if (b.p) (void)hipFree(b.p);
+    retire(b.p, b.cap);
     b.p = nullptr;
     b.cap = 0;
 }
@@ -500,8 +535,7 @@ int prepare_dicts(kdtn_ctx* c) {
         if (keepw && c->kd_bits.p)
             HIP_TRY(hipMemcpy2DAsync(nb.p, (size_t)cap * 4, c->kd_bits.p, (size_t)c->kb_cap * 4, (size_t)keepw * 4,
                                      KB_NSETS, hipMemcpyDeviceToDevice, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        release(c->kd_bits);
+        release(c->kd_bits);                 // retired: stream-ordered after the copy
         c->kd_bits = nb;
         c->kb_cap = cap;
     }
@@ -827,9 +861,10 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->dl_off, &c->dl_ref, &c->dl_rec.buf, &c->stage, &c->vx_cnt, &c->vx_send, &c->vx_recv,
                       &c->vx_gops, &c->pd_send, &c->pd_recv, &c->pd_cnt, &c->dl_rows, &c->vx_flag,
                       &c->vx_dkeys, &c->vx_dused, &c->vx_cpos, &c->vx_cpart, &c->vx_cnode, &c->vx_cvni,
-                      &c->dl_prev, &c->dl_ns, &c->dl_name, &c->st_rlen, &c->st_rbase, &c->st_roff64,
+                      &c->dl_prev, &c->dl_ns, &c->dl_name, &c->dl_dest, &c->st_rlen, &c->st_rbase, &c->st_roff64,
                       &c->st_rpart, &c->st_roff32, &c->st_seen};
     for (DevBuf* b : bufs) release(*b);
+    retired_flush();
     for (int i = 0; i <= kMaxTimers; ++i)
         if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
     if (c->comm) (void)ncclCommDestroy(c->comm);
@@ -2974,6 +3009,7 @@ int kdtn_epoch_upload_delta(kdtn_ctx* c, const kdtn_epoch_delta* d) {
     TRY(link_store_alloc(c, c->dl_rec, nr));
     const size_t col = (size_t)nr * 4, uid_at = align_up(col * LINK_COLS32, 8);
     TRY(ensure(c->stage, uid_at + (size_t)nr * 8 + 128));
+    TRY(ensure(c->dl_dest, (size_t)nr * 4));
     TRY(plan_alloc(c, Tn));
     TRY(ensure(c->st_chg, (size_t)Tn * 4 + 16));
     TRY(ensure(c->dl_rows, (size_t)n * 4 + 16));
@@ -3027,6 +3063,8 @@ int kdtn_epoch_upload_delta(kdtn_ctx* c, const kdtn_epoch_delta* d) {
     HIP_TRY(hipMemsetAsync(misc + MISC_DELTA_ERR, 0, 4, s));
     HIP_TRY(hipMemsetAsync(misc + MISC_ROWCHG_N, 0, 4, s));
     HIP_TRY(hipMemsetAsync(colmax, 0, COL_GAP * 4, s));
+    HIP_TRY(hipMemsetAsync(misc + MISC_DELTA_MULTI, 0, 4, s));
+    if (nr) HIP_TRY(hipMemsetAsync(c->dl_dest.p, 0xFF, (size_t)nr * 4, s));
     HIP_TRY(hipMemsetAsync(c->st_chg.p, 0xFF, (size_t)Tn * 4, s));
     if (remap) {
         HIP_TRY(hipMemsetAsync(c->st_seen.p, 0, ((size_t)T0 + 31) / 32 * 4 + 16, s));
@@ -3070,16 +3108,17 @@ int kdtn_epoch_upload_delta(kdtn_ctx* c, const kdtn_epoch_delta* d) {
                                                            dp<uint8_t>(c->st_mask), nullptr, c->real.view, c->real.view,
                                                            M0, gr, dp<uint32_t>(c->sh_real.buf));
     }
+    // the inline records' destinations, still before they have arrived
+    if (nr && nref)
+        k_delta_dest<<<nblocks(nref), BLOCK, 0, s>>>(dp<uint32_t>(c->dl_off), dp<uint32_t>(c->dl_topo), n,
+                                                     dp<uint32_t>(c->dl_ref), nref, dp<uint32_t>(c->st_off32),
+                                                     misc + MISC_DELTA_ERR, dp<uint32_t>(c->dl_dest),
+                                                     misc + MISC_DELTA_MULTI);
     if (cs != s) HIP_TRY(hipStreamWaitEvent(s, c->ev_cp[3], 0));
-    if (nr) {
-        k_soa_to_tiles<<<std::min<uint32_t>(nblocks(nr), 4 * c->n_cus), BLOCK, 0, s>>>(
+    if (nr)          // staging columns straight to their places, with the id-range column maxima
+        k_delta_place<<<std::min<uint32_t>(nblocks(nr), 4 * c->n_cus), BLOCK, 0, s>>>(
             reinterpret_cast<const uint32_t*>(st), reinterpret_cast<const int64_t*>(st + uid_at), nr,
-            dp<uint32_t>(c->dl_rec.buf), colmax);
-        if (nref) k_delta_inline<<<nblocks(nref), BLOCK, 0, s>>>(dp<uint32_t>(c->dl_off), dp<uint32_t>(c->dl_topo), n,
-                                                       dp<uint32_t>(c->dl_ref), nref, dp<uint32_t>(c->st_off32),
-                                                       c->dl_rec.view, misc + MISC_DELTA_ERR,
-                                                       dp<uint32_t>(c->sh_des.buf));
-    }
+            dp<uint32_t>(c->dl_dest), misc + MISC_DELTA_ERR, dp<uint32_t>(c->sh_des.buf), colmax);
     k_delta_totals<<<1, 64, 0, s>>>(dp<uint64_t>(c->st_off64), Tn, remap ? dp<uint64_t>(c->st_roff64) : nullptr, misc);
     HIP_TRY(hipGetLastError());
     uint32_t* hm = c->h_misc + 64;
@@ -3107,6 +3146,19 @@ int kdtn_epoch_upload_delta(kdtn_ctx* c, const kdtn_epoch_delta* d) {
         c->kd_arena = saved_arena[0], c->pd_arena = saved_arena[1];
         c->uploaded = !(err & DERR_KEEP);
         return KDTN_EINVAL;
+    }
+    if (hm[MISC_DELTA_MULTI]) {
+        // an inline record referenced more than once: the staged delta's tiles, then every
+        // reference placed from them (rare; one more synchronisation)
+        k_soa_to_tiles<<<std::min<uint32_t>(nblocks(nr), 4 * c->n_cus), BLOCK, 0, s>>>(
+            reinterpret_cast<const uint32_t*>(st), reinterpret_cast<const int64_t*>(st + uid_at), nr,
+            dp<uint32_t>(c->dl_rec.buf), colmax);
+        k_delta_inline<<<nblocks(nref), BLOCK, 0, s>>>(dp<uint32_t>(c->dl_off), dp<uint32_t>(c->dl_topo), n,
+                                                       dp<uint32_t>(c->dl_ref), nref, dp<uint32_t>(c->st_off32),
+                                                       c->dl_rec.view, misc + MISC_DELTA_ERR,
+                                                       dp<uint32_t>(c->sh_des.buf));
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipStreamSynchronize(s));
     }
     const uint64_t N = (uint64_t)hm[MISC_DELTA_N] | ((uint64_t)hm[MISC_DELTA_N + 1] << 32);
     std::swap(c->des, c->sh_des);

@@ -50,7 +50,8 @@ enum : int {
 // special key-string ids found by k_kdict_flags (0xFFFFFFFF when absent)
 enum : int { SPECIAL_DEFAULT = 0, SPECIAL_LOCALHOST = 4, MISC_FAN_NODES = 12, MISC_VNI_N = 13,
              MISC_COMMIT_N = 14, MISC_ROWCHG_N = 15, MISC_COLMAX = 16 /* [19] */, MISC_DELTA_ERR = 36,
-             MISC_DELTA_N = 38 /* u64 */, MISC_DELTA_M = 40 /* u64 */ };   // misc words (64 = 256 B)
+             MISC_DELTA_N = 38 /* u64 */, MISC_DELTA_M = 40 /* u64 */,
+             MISC_DELTA_MULTI = 42 };   // misc words (64 = 256 B)
 // epoch sync header (u32 words; zeroed by the epoch's only memset, the look-back status
 // follows at SYNC_HEADER_BYTES). The ticket counter, which every k_reconcile workgroup
 // increments, has a 128-B line to itself; the host reads words [SYNC_TOTALS, SYNC_TOTALS + 4)
@@ -385,6 +386,10 @@ struct AsmGuard {                         // k_store_assemble in a delta upload 
 };
 __global__ void k_store_assemble(const uint32_t* off, uint32_t nt, const uint32_t* base, const uint8_t* mode,
                                  const uint32_t* ref, DevLinks A, DevLinks B, uint32_t n, AsmGuard g, uint32_t* out);
+__global__ void k_delta_dest(const uint32_t* d_off, const uint32_t* topo, uint32_t n, const uint32_t* ref,
+                             uint32_t nref, const uint32_t* off, const uint32_t* err, uint32_t* dest, uint32_t* multi);
+__global__ void k_delta_place(const uint32_t* stage, const int64_t* uid, uint32_t n, const uint32_t* dest,
+                              const uint32_t* err, uint32_t* out, uint32_t* colmax);
 __global__ void k_delta_inline(const uint32_t* d_off, const uint32_t* topo, uint32_t n, const uint32_t* ref,
                                uint32_t nref, const uint32_t* off, DevLinks B, const uint32_t* err, uint32_t* out);
 

@@ -241,9 +241,69 @@ __global__ void __launch_bounds__(BLOCK) k_store_assemble(const uint32_t* off, u
     }
 }
 
-// The inline records of a delta into their places in the new desired store, one thread per
-// reference k: its changed Topology c (upper bound over the delta's offsets), that Topology's
-// new index topo[c], and the output position off[topo[c]] + (k - d_off[c]).
+// Where each inline record of a delta goes in the new desired store, computed while the
+// records are still crossing the host link: one thread per reference k, its changed Topology c
+// (upper bound over the delta's offsets), that Topology's new index topo[c], output position
+// off[topo[c]] + (k - d_off[c]). dest[i] takes the position of inline record i; a record
+// referenced twice raises `multi` (k_delta_inline then places every reference).
+__global__ void __launch_bounds__(BLOCK) k_delta_dest(const uint32_t* d_off, const uint32_t* topo, uint32_t n,
+                                                      const uint32_t* ref, uint32_t nref, const uint32_t* off,
+                                                      const uint32_t* err, uint32_t* dest, uint32_t* multi) {
+    if (*err) return;
+    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+    if (k >= nref) return;
+    const uint32_t r = ref[k];
+    if (!(r & KDTN_DELTA_NEW)) return;
+    const uint32_t c = entry_topo(d_off, n, k);
+    if (atomicExch(dest + (r & ~KDTN_DELTA_NEW), off[topo[c]] + (k - d_off[c])) != 0xFFFFFFFFu) atomicOr(multi, 1u);
+}
+
+// Inline records of a delta from the staging columns (k_soa_to_tiles' input) straight to their
+// positions in the new desired store, plus the id-range column maxima; unreferenced records
+// (dest ~0) are skipped. Nothing is written when the delta was refused.
+__global__ void __launch_bounds__(BLOCK) k_delta_place(const uint32_t* stage, const int64_t* uid, uint32_t n,
+                                                       const uint32_t* dest, const uint32_t* err, uint32_t* out,
+                                                       uint32_t* colmax) {
+    __shared__ uint32_t red[BLOCK / 64][COL_GAP];
+    uint32_t mx[COL_GAP];
+#pragma unroll
+    for (int c = 0; c < COL_GAP; ++c) mx[c] = 0;
+    const bool ok = *err == 0;
+    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
+        const uint32_t d = ok ? dest[i] : 0xFFFFFFFFu;
+        uint32_t* dst = out + (size_t)(d >> 6) * TILE_WORDS + (d & 63u);
+#pragma unroll
+        for (int c = 0; c < LINK_COLS32; ++c) {
+            const uint32_t v = __builtin_nontemporal_load(stage + (size_t)c * n + i);
+            if (c < COL_GAP) mx[c] = v > mx[c] ? v : mx[c];
+            if (d != 0xFFFFFFFFu) dst[c * TILE_RECS] = v;
+        }
+        if (d != 0xFFFFFFFFu)
+            reinterpret_cast<int64_t*>(out + (size_t)(d >> 6) * TILE_WORDS + LINK_COLS32 * TILE_RECS)[d & 63u] =
+                __builtin_nontemporal_load(uid + i);
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int c = 0; c < COL_GAP; ++c) {
+        uint32_t v = mx[c];
+#pragma unroll
+        for (int dd = 32; dd >= 1; dd >>= 1) {
+            const uint32_t o = __shfl_xor(v, dd, 64);
+            v = o > v ? o : v;
+        }
+        if (lane == 0) red[wave][c] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < COL_GAP) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int w = 0; w < BLOCK / 64; ++w) v = red[w][threadIdx.x] > v ? red[w][threadIdx.x] : v;
+        atomicMax(colmax + threadIdx.x, v);
+    }
+}
+
+// The general placement when an inline record is referenced more than once (k_delta_dest's
+// multi flag): one thread per reference k, records from the tiles of the staged delta.
 __global__ void __launch_bounds__(BLOCK) k_delta_inline(const uint32_t* d_off, const uint32_t* topo, uint32_t n,
                                                         const uint32_t* ref, uint32_t nref, const uint32_t* off,
                                                         DevLinks B, const uint32_t* err, uint32_t* out) {

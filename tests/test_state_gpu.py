@@ -209,3 +209,30 @@ def test_delta_rejections_leave_the_state():
             _run_same(eng, state, f"after a rejected delta ({what})")
         eng.upload_delta(good)
         _run_same(eng, apply_delta(state, good), "the corrected delta")
+
+
+def test_delta_inline_record_referenced_twice():
+    """An inline record referenced by several entries (allowed by the ABI: references are
+    free-form) is placed at every position (the general placement path), and a record no
+    entry references is ignored."""
+    import dataclasses
+    topos, vnis = random_epoch(8, T=150, p_err=0.1)
+    kd, pd = Interner(), Interner()
+    a = pack(topos, vnis, kdict=kd, pdict=pd)
+    b = pack(mutate(topos, 21), vnis, kdict=kd, pdict=pd)
+    good = build_delta(a, b, a.kdict.n, a.pdict.n, vnis=b.vnis)
+    new_at = np.nonzero(good.ref & abi.DELTA_NEW)[0]
+    assert len(new_at) >= 3
+    ref = good.ref.copy()
+    ref[new_at[1]] = ref[new_at[0]]           # record of new_at[1] now unreferenced, new_at[0]'s twice
+    ref[new_at[2]] = ref[new_at[0]]
+    d = dataclasses.replace(good, ref=ref)
+    with Engine(device=0, tick_in_usec=TICK) as eng:
+        eng.upload(a)
+        _run_same(eng, a, "epoch 0")
+        eng.commit(np.ones(a.topos.n, bool))
+        state = commit(a, np.ones(a.topos.n, bool))
+        eng.upload_delta(d)
+        want = apply_delta(state, d)
+        assert not same_tables(eng.tables(), want)
+        _run_same(eng, want, "inline record referenced three times")

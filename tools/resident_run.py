@@ -1,0 +1,68 @@
+"""The config-3 resident controller loop, epoch by epoch (profiling tool): a full upload, then
+per epoch kdtn_epoch_upload_delta + run + download + commit, each phase timed on the host.
+Deltas are built and pinned before the loop. Prints one JSON line per epoch and a summary.
+
+    python tools/resident_run.py [--pods 1000000] [--epochs 6] [--topology-set FRAC]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch  # noqa: F401  (one HIP runtime)
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "kube-dtn_amd"))
+import numpy as np  # noqa: E402
+
+from kdtn import Engine, synth  # noqa: E402
+from kdtn.delta import build_delta  # noqa: E402
+from kdtn.engine import pin_delta  # noqa: E402
+from kdtn.tables import BatchesOut  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--pods", type=int, default=1_000_000)
+ap.add_argument("--epochs", type=int, default=6)
+ap.add_argument("--topology-set", type=float, default=0.0, help="fraction of Topologies deleted/created per epoch")
+a = ap.parse_args()
+src = (synth.TopologySetChurn(frac=a.topology_set, total_pods=a.pods) if a.topology_set
+       else synth.ChurnSequence(total_pods=a.pods))
+prev = src.epoch_input(copy=True)
+deltas = []
+p = prev
+for _ in range(a.epochs):
+    src.advance()
+    new = src.epoch_input(copy=True)
+    deltas.append((pin_delta(build_delta(p, new, p.kdict.n, p.pdict.n)), new.topos.n, new.desired.n))
+    p = new
+eng = Engine(device=0)
+eng.upload(prev)
+eng.run()
+eng.sync()
+eng.commit(np.ones(prev.topos.n, np.uint8))
+cap = max(1 << 20, prev.desired.n // 8)
+into = None
+rows = []
+for ep, (d, T, N) in enumerate(deltas):
+    if into is None or len(into.action) != T:
+        into = BatchesOut.alloc(T, cap, cap, cap, pinned=True)
+    t0 = time.perf_counter()
+    eng.upload_delta(d)
+    t1 = time.perf_counter()
+    eng.run()
+    eng.sync()
+    t2 = time.perf_counter()
+    eng.download(into)
+    t3 = time.perf_counter()
+    eng.commit(np.ones(T, np.uint8))
+    t4 = time.perf_counter()
+    r = {"epoch": ep, "upload_ms": (t1 - t0) * 1e3, "upload_bytes": d.upload_bytes(),
+         "upload_GBps": d.upload_bytes() / (t1 - t0) / 1e9, "run_ms": (t2 - t1) * 1e3,
+         "download_ms": (t3 - t2) * 1e3, "commit_ms": (t4 - t3) * 1e3, "e2e_ms": (t4 - t0) * 1e3,
+         "refs": int(len(d.ref)), "inline": int(d.records.n), "changed": d.n_changed}
+    rows.append(r)
+    print(json.dumps(r), flush=True)
+steady = rows[1:] if len(rows) > 1 else rows
+print(json.dumps({"summary_excluding_first": {k: float(np.mean([r[k] for r in steady]))
+                                              for k in ("upload_ms", "upload_GBps", "run_ms", "download_ms",
+                                                        "commit_ms", "e2e_ms")}}), flush=True)

@@ -27,9 +27,11 @@ ap.add_argument("--rank", type=int, default=0)
 ap.add_argument("--reps", type=int, default=30)
 a = ap.parse_args()
 t0 = time.time()
+print(f"[shard_epoch] N={a.nshards}: generating", file=sys.stderr, flush=True)
 full = synth.make(2, total_pods=a.pods)
 sh = synth.make(2, total_pods=a.pods, shard=a.rank, nshards=a.nshards)
 gen_s = time.time() - t0
+print(f"[shard_epoch] generated in {gen_s:.1f} s", file=sys.stderr, flush=True)
 kb, ko = full.kdict.bytes_, full.kdict.offs
 s = lambda i: bytes(kb[ko[i]:ko[i + 1]])
 T = full.topos
