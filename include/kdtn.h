@@ -563,6 +563,26 @@ int kdtn_json_upload(kdtn_ctx* ctx, const uint8_t* doc, uint64_t n);
 int kdtn_json_ingest(kdtn_ctx* ctx, const kdtn_vni_table* vnis, kdtn_ingest_info* info);
 /* D2H of the decoded tables of the last successful ingest. */
 int kdtn_ingest_download(kdtn_ctx* ctx, kdtn_ingest_tables* out);
+/* Incremental CR ingest on the resident state (the informer's event stream,
+ * daemon/kubedtn/kubedtn.go:128-142; a controller that keeps the engine resident no longer
+ * re-decodes its whole store): the uploaded document (kdtn_json_upload) is a TopologyList of
+ * the Topology CRs added or updated since the resident state, deleted[] the resident table
+ * indices of the deleted ones. The document is decoded as by kdtn_json_ingest into scratch
+ * tables, its strings are interned into the RESIDENT dictionaries on the GPU (a string already
+ * there keeps its id, so the resident link stores and the resident VXLAN map stay valid; new
+ * strings are appended in first-occurrence order), and the result is applied as
+ * kdtn_epoch_upload_delta would: an item whose (namespace, name) is resident replaces that
+ * Topology's spec.links and status.src_ip / net_ns (status.links stay the engine's committed
+ * status); any other item is a created Topology (status nil: the CREATED path,
+ * controllers/topology_controller.go:81-85); deleted Topologies leave the table. The new table
+ * keeps the remaining resident rows in order and appends the created ones in document order.
+ * vnis: a VXLAN snapshot in resident ids, NULL = KDTN_VNI_RESIDENT. info: the new table's sizes
+ * and the document's token count. KDTN_EBADMSG (info->json_err) for a rejected document and
+ * KDTN_EINVAL (an item listed twice, deleted and listed, a deleted index out of range) leave
+ * the resident state as it was. Single-shard contexts; needs a run since the last upload (the
+ * resident dictionaries parsed). */
+int kdtn_json_ingest_delta(kdtn_ctx* ctx, const uint32_t* deleted, uint32_t n_deleted, const kdtn_vni_table* vnis,
+                           kdtn_ingest_info* info);
 /* Sizes of the context's current epoch tables — after an upload, a delta upload, a commit
  * or an ingest — into info (n_topos, n_desired, n_realised, dictionary sizes); after it,
  * kdtn_ingest_download returns those tables (the resident state after a commit). */

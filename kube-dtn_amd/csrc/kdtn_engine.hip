@@ -138,6 +138,17 @@ struct kdtn_ctx {
     DevBuf dl_topo, dl_src, dl_netns, dl_nil, dl_off, dl_ref, dl_rows;
     // delta with a topology-set change: the map, created rows' names, the realised plan
     DevBuf dl_prev, dl_ns, dl_name, dl_dest, st_rlen, st_rbase, st_roff64, st_rpart, st_roff32, st_seen;
+    // incremental CR ingest (kdtn_json_ingest_delta): the document's scratch tables and local
+    // dictionaries, the id maps into the resident dictionaries, the topology-key match
+    DevBuf ji_ns, ji_name, ji_src, ji_netns, ji_flags, ji_roff, ji_noff, ji_kb, ji_ko, ji_pb, ji_po;
+    DevLinkStore ji_des, ji_real;
+    DevBuf ji_kmap, ji_pmap, ji_miss, ji_mlen, ji_rank, ji_boff, ji_nil, ji_keep, ji_kpos, ji_claim, ji_res,
+        ji_created, ji_cpos, ji_keys, ji_vals, ji_del, ji_ref;
+    // resident string indexes (string → id) of the dictionaries' first n strings
+    struct StrIndex {
+        DevBuf slots;
+        uint32_t n = 0, mask = 0;
+    } ix_k, ix_p;
     uint64_t kd_arena = 0, pd_arena = 0;       // dictionary arena bytes (host-known: tables_info)
     DevLinkStore dl_rec;
     bool tables_cur = false;                   // j_info describes the current tables (kdtn_epoch_tables_info)
@@ -595,6 +606,9 @@ int upload_dicts(kdtn_ctx* c, const kdtn_strtab& kd, const kdtn_strtab& pd, uint
     if (!hs) hs = c->stream;
     c->D = kd.n;
     c->P = pd.n;
+    // strings past the kept prefix may differ: an index that covers them is rebuilt (mask 0)
+    if (kk < c->ix_k.n) c->ix_k.n = c->ix_k.mask = 0;
+    if (pk < c->ix_p.n) c->ix_p.n = c->ix_p.mask = 0;
     c->kd_arena = kd.offs[kd.n];
     c->pd_arena = pd.offs[pd.n];
     c->kd_valid = kk;
@@ -862,7 +876,12 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->vx_gops, &c->pd_send, &c->pd_recv, &c->pd_cnt, &c->dl_rows, &c->vx_flag,
                       &c->vx_dkeys, &c->vx_dused, &c->vx_cpos, &c->vx_cpart, &c->vx_cnode, &c->vx_cvni,
                       &c->dl_prev, &c->dl_ns, &c->dl_name, &c->dl_dest, &c->st_rlen, &c->st_rbase, &c->st_roff64,
-                      &c->st_rpart, &c->st_roff32, &c->st_seen};
+                      &c->st_rpart, &c->st_roff32, &c->st_seen, &c->ji_ns, &c->ji_name, &c->ji_src, &c->ji_netns,
+                      &c->ji_flags, &c->ji_roff, &c->ji_noff, &c->ji_kb, &c->ji_ko, &c->ji_pb, &c->ji_po,
+                      &c->ji_des.buf, &c->ji_real.buf, &c->ji_kmap, &c->ji_pmap, &c->ji_miss, &c->ji_mlen,
+                      &c->ji_rank, &c->ji_boff, &c->ji_nil, &c->ji_keep, &c->ji_kpos, &c->ji_claim, &c->ji_res,
+                      &c->ji_created, &c->ji_cpos, &c->ji_keys, &c->ji_vals, &c->ji_del, &c->ji_ref,
+                      &c->ix_k.slots, &c->ix_p.slots};
     for (DevBuf* b : bufs) release(*b);
     retired_flush();
     for (int i = 0; i <= kMaxTimers; ++i)
@@ -1411,6 +1430,7 @@ int kdtn_make_qdiscs(kdtn_ctx* c, const kdtn_strtab* pdict, const kdtn_props_tab
     for (int k = 0; k < KDTN_NPROP; ++k) TRY(check_ids(props->prop[k], n, P, "props"));
     if (n && !props->gap) return KDTN_EINVAL;
     c->pd_valid = c->pd_from = 0;                          // this call owns the property tables now
+    c->ix_p.n = c->ix_p.mask = 0;
     c->uploaded = false;
     TRY(upload_arena(c, c->pd_bytes, pdict->bytes, pdict->offs[P]));
     TRY(upload(c, c->pd_offs, pdict->offs, (size_t)(P + 1) * 4));
@@ -1857,6 +1877,17 @@ int d2h(kdtn_ctx* c, T* host, const void* dev, size_t count = 1) {
     return KDTN_OK;
 }
 
+// where a decode writes its tables (the context's own, or an incremental ingest's scratch)
+struct JsTargets {
+    DevBuf *ns, *name, *src, *netns, *flags, *roff, *noff;
+    DevLinkStore *des, *real;
+    DevBuf *kd_bytes, *kd_offs, *pd_bytes, *pd_offs;
+};
+struct JsCounts {
+    uint32_t T, N, M, D, P;
+    uint64_t kbytes, pbytes;
+};
+
 // small control block: [0] syntax error, [1] decode error (pos << 8 | code, ~0 = none),
 // [2] heap bytes used, [3] status | seen_root << 32, [4] kd fill | pd fill << 32
 constexpr size_t J_SMALL = 64;
@@ -1952,16 +1983,12 @@ int kdtn_json_upload(kdtn_ctx* c, const uint8_t* doc, uint64_t n) {
     return KDTN_OK;
 }
 
-static int json_ingest_full(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest_info* info) {
-    if (!c || !c->j_loaded) return KDTN_EINVAL;
-    HIP_TRY(hipSetDevice(c->device));
-    c->sh_T = 0;
-    g_last_error[0] = 0;
+// The decode of the uploaded document into `tg` (the context's own tables for a full ingest,
+// scratch tables for an incremental one): topology columns, both link stores, first-occurrence
+// dictionaries. Counts into `o`. A rejected document returns KDTN_EBADMSG (json_reject).
+static int json_decode(kdtn_ctx* c, const JsTargets& tg, JsCounts* o, kdtn_ingest_info* info) {
     hipStream_t s = c->stream;
     c->j_info = kdtn_ingest_info{};
-    c->uploaded = false;
-    c->ran = false;
-    c->kd_valid = c->pd_valid = c->kd_from = c->pd_from = 0;   // the document's dictionaries are new
     c->n_ev = 0;
     (void)hipEventRecord(c->ev[0], s);
     const uint32_t nb = c->j_nb;
@@ -2069,14 +2096,12 @@ static int json_ingest_full(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest
     const uint32_t T = (uint32_t)tot[0], N = (uint32_t)tot[1], M = (uint32_t)tot[2];
 
     // 4. output tables
-    c->T = T;
-    for (DevBuf* b : {&c->t_ns, &c->t_name, &c->t_src, &c->t_netns, &c->j_tflags})
-        TRY(ensure(*b, (size_t)T * 4));
-    TRY(ensure(c->t_flags, (size_t)T));
-    TRY(ensure(c->t_roff, ((size_t)T + 1) * 4));
-    TRY(ensure(c->t_noff, ((size_t)T + 1) * 4));
-    TRY(link_store_alloc(c, c->des, N));
-    TRY(link_store_alloc(c, c->real, M));
+    for (DevBuf* b : {tg.ns, tg.name, tg.src, tg.netns, &c->j_tflags}) TRY(ensure(*b, (size_t)T * 4));
+    TRY(ensure(*tg.flags, (size_t)T));
+    TRY(ensure(*tg.roff, ((size_t)T + 1) * 4));
+    TRY(ensure(*tg.noff, ((size_t)T + 1) * 4));
+    TRY(link_store_alloc(c, *tg.des, N));
+    TRY(link_store_alloc(c, *tg.real, M));
     const uint64_t owners = 1 + 9ull * T + 22ull * ((uint64_t)N + M);
     if (owners >= JS_NONE) {
         std::snprintf(g_last_error, sizeof(g_last_error), "ingest: too many records for one document");
@@ -2084,13 +2109,13 @@ static int json_ingest_full(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest
     }
     TRY(ensure(c->j_owner, (size_t)owners * 4));
     TRY(ensure(c->j_vown, (size_t)nval * 4));
-    JsTopoOut to{dp<uint32_t>(c->t_ns), dp<uint32_t>(c->t_name), dp<uint32_t>(c->t_src), dp<uint32_t>(c->t_netns),
-                 dp<uint32_t>(c->j_tflags), dp<uint32_t>(c->t_roff), dp<uint32_t>(c->t_noff)};
+    JsTopoOut to{dp<uint32_t>(*tg.ns), dp<uint32_t>(*tg.name), dp<uint32_t>(*tg.src), dp<uint32_t>(*tg.netns),
+                 dp<uint32_t>(c->j_tflags), dp<uint32_t>(*tg.roff), dp<uint32_t>(*tg.noff)};
     k_js_elems_write<<<ntiles, BLOCK, 0, s>>>(dp<uint8_t>(c->j_ecls), ntok, dp<uint64_t>(c->j_coff3), ntiles, ord, to);
     HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(to.real_off + T), (int)M, 1, s));
     HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(to.des_off + T), (int)N, 1, s));
-    JsStore des{dp<uint32_t>(c->des.buf)};
-    JsStore real{dp<uint32_t>(c->real.buf)};
+    JsStore des{dp<uint32_t>(tg.des->buf)};
+    JsStore real{dp<uint32_t>(tg.real->buf)};
 
     // 5. schema values + interning; a table or heap that fills up is grown and the pass rerun
     uint32_t kcap = std::max(c->j_kcap, next_pow2(std::max<uint64_t>(1024, 2ull * ((uint64_t)N + M) + 4ull * T)));
@@ -2109,12 +2134,12 @@ static int json_ingest_full(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest
         HIP_TRY(hipMemsetAsync(c->j_prep.p, 0xFF, (size_t)pcap * 4, s));
         HIP_TRY(hipMemsetAsync(small + 2, 0, J_SMALL - 16, s));
         HIP_TRY(hipMemsetAsync(small + 1, 0xFF, 8, s));
-        for (DevBuf* b : {&c->t_ns, &c->t_name, &c->t_src, &c->t_netns})
+        for (DevBuf* b : {tg.ns, tg.name, tg.src, tg.netns})
             HIP_TRY(hipMemsetAsync(b->p, 0, (size_t)T * 4, s));
         HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(to.flags), (int)(KDTN_TOPO_SPEC_NIL | KDTN_TOPO_STATUS_NIL),
                                   T, s));
-        HIP_TRY(hipMemsetAsync(c->des.buf.p, 0, c->des.buf.cap, s));
-        HIP_TRY(hipMemsetAsync(c->real.buf.p, 0, c->real.buf.cap, s));
+        HIP_TRY(hipMemsetAsync(tg.des->buf.p, 0, tg.des->buf.cap, s));
+        HIP_TRY(hipMemsetAsync(tg.real->buf.p, 0, tg.real->buf.cap, s));
         if (nval) HIP_TRY(hipMemsetAsync(c->j_vown.p, 0xFF, (size_t)nval * 4, s));
         in.doc = j.doc;
         in.heap = dp<uint8_t>(c->j_heap);
@@ -2162,19 +2187,43 @@ static int json_ingest_full(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest
 
     // 6. ids in first-occurrence order, dictionaries, id columns
     uint64_t kbytes = 0, pbytes = 0;
-    TRY(json_dict(c, in.kd, in, ntok, c->j_kslot_id, c->kd_bytes, c->kd_offs, &c->D, &kbytes));
-    TRY(json_dict(c, in.pd, in, ntok, c->j_pslot_id, c->pd_bytes, c->pd_offs, &c->P, &pbytes));
+    uint32_t D = 0, P = 0;
+    TRY(json_dict(c, in.kd, in, ntok, c->j_kslot_id, *tg.kd_bytes, *tg.kd_offs, &D, &kbytes));
+    TRY(json_dict(c, in.pd, in, ntok, c->j_pslot_id, *tg.pd_bytes, *tg.pd_offs, &P, &pbytes));
     // keep the intern tables at most half full for the next document of this shape
-    c->j_kcap = std::max(kcap, next_pow2(2ull * c->D));
-    c->j_pcap = std::max(pcap, next_pow2(2ull * c->P));
+    c->j_kcap = std::max(kcap, next_pow2(2ull * D));
+    c->j_pcap = std::max(pcap, next_pow2(2ull * P));
     constexpr uint32_t IDW = (KDTN_NKEY + KDTN_NPROP) * TILE_RECS;
     if (N) k_js_finalize_links<<<nblocks((uint64_t)(N + TILE_RECS - 1) / TILE_RECS * IDW), BLOCK, 0, s>>>(
         des, N, dp<uint32_t>(c->j_kslot_id), dp<uint32_t>(c->j_pslot_id));
     if (M) k_js_finalize_links<<<nblocks((uint64_t)(M + TILE_RECS - 1) / TILE_RECS * IDW), BLOCK, 0, s>>>(
         real, M, dp<uint32_t>(c->j_kslot_id), dp<uint32_t>(c->j_pslot_id));
-    if (T) k_js_finalize_topos<<<nblocks(T), BLOCK, 0, s>>>(to, T, dp<uint32_t>(c->j_kslot_id), dp<uint8_t>(c->t_flags));
+    if (T) k_js_finalize_topos<<<nblocks(T), BLOCK, 0, s>>>(to, T, dp<uint32_t>(c->j_kslot_id), dp<uint8_t>(*tg.flags));
     timer_mark(c, "js_intern");
     HIP_TRY(hipGetLastError());
+    *o = JsCounts{T, N, M, D, P, kbytes, pbytes};
+    return KDTN_OK;
+}
+
+static int json_ingest_full(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest_info* info) {
+    if (!c || !c->j_loaded) return KDTN_EINVAL;
+    HIP_TRY(hipSetDevice(c->device));
+    c->sh_T = 0;
+    g_last_error[0] = 0;
+    hipStream_t s = c->stream;
+    c->uploaded = false;
+    c->ran = false;
+    c->kd_valid = c->pd_valid = c->kd_from = c->pd_from = 0;   // the document's dictionaries are new
+    c->ix_k.n = c->ix_k.mask = c->ix_p.n = c->ix_p.mask = 0;     // (their string indexes too)
+    const JsTargets tg{&c->t_ns, &c->t_name, &c->t_src, &c->t_netns, &c->t_flags, &c->t_roff, &c->t_noff,
+                       &c->des, &c->real, &c->kd_bytes, &c->kd_offs, &c->pd_bytes, &c->pd_offs};
+    JsCounts k{};
+    TRY(json_decode(c, tg, &k, info));
+    const uint32_t T = k.T, N = k.N, M = k.M;
+    const uint64_t kbytes = k.kbytes, pbytes = k.pbytes;
+    c->T = T;
+    c->D = k.D;
+    c->P = k.P;
 
     // 7. the epoch inputs are in place: finish what kdtn_epoch_upload would set up
     TRY(prepare_dicts(c));
@@ -3205,6 +3254,314 @@ int kdtn_epoch_tables_info(kdtn_ctx* c, kdtn_ingest_info* info) {
     I.pdict_bytes = c->pd_arena;
     c->tables_cur = true;
     if (info) *info = I;
+    return KDTN_OK;
+}
+
+}  // extern "C"
+
+// ======================================================================================
+// Incremental CR ingest on the resident state (kdtn_informer.hip kernels)
+// ======================================================================================
+namespace {
+
+// The resident string index of one dictionary (bytes / offs, D strings) brought up to date:
+// extended with the strings appended since it was built, rebuilt (twice the capacity) when it
+// would pass half full with `extra` more strings, or when the dictionary was rewritten.
+int strix_update(kdtn_ctx* c, kdtn_ctx::StrIndex& ix, DevBuf& bytes, DevBuf& offs, uint32_t D, uint32_t extra) {
+    hipStream_t s = c->stream;
+    const uint64_t want = next_pow2(2ull * ((uint64_t)D + extra) + 64);
+    uint32_t from = ix.n;
+    if (ix.n > D || !ix.slots.p || !ix.mask || (uint64_t)ix.mask + 1 < want) {
+        const uint64_t cap = std::max<uint64_t>(want, (uint64_t)ix.mask + 1);
+        if (cap > (1ull << 31)) {
+            std::snprintf(g_last_error, sizeof(g_last_error), "string index of %llu slots", (unsigned long long)cap);
+            return KDTN_ENOMEM;
+        }
+        TRY(ensure(ix.slots, (size_t)cap * 8));
+        HIP_TRY(hipMemsetAsync(ix.slots.p, 0, (size_t)cap * 8, s));
+        ix.mask = (uint32_t)cap - 1;
+        from = 0;
+    }
+    if (D > from)
+        k_strix_insert<<<nblocks(D - from), BLOCK, 0, s>>>(dp<uint8_t>(bytes), dp<uint32_t>(offs), from, D,
+                                                             dp<unsigned long long>(ix.slots), ix.mask);
+    ix.n = D;
+    return KDTN_OK;
+}
+
+// Local (document) strings → resident ids; misses ranked (new ids) and sized (arena offsets)
+int strix_lookup(kdtn_ctx* c, kdtn_ctx::StrIndex& ix, DevBuf& lb, DevBuf& lo, uint32_t nl, DevBuf& rb,
+                 DevBuf& ro, DevBuf& map, DevBuf& rank, DevBuf& boff) {
+    hipStream_t s = c->stream;
+    TRY(ensure(map, (size_t)nl * 4));
+    TRY(ensure(c->ji_miss, (size_t)nl * 4));
+    TRY(ensure(c->ji_mlen, (size_t)nl * 4));
+    TRY(ensure(rank, ((size_t)nl + 1) * 8));
+    TRY(ensure(boff, ((size_t)nl + 1) * 8));
+    if (nl)
+        k_strix_lookup<<<nblocks(nl), BLOCK, 0, s>>>(dp<uint8_t>(lb), dp<uint32_t>(lo), nl, dp<uint8_t>(rb),
+                                                     dp<uint32_t>(ro), dp<unsigned long long>(ix.slots), ix.mask,
+                                                     dp<uint32_t>(map), dp<uint32_t>(c->ji_miss),
+                                                     dp<uint32_t>(c->ji_mlen));
+    TRY(scan_u32(c, dp<uint32_t>(c->ji_miss), nl, dp<uint64_t>(rank)));
+    TRY(scan_u32(c, dp<uint32_t>(c->ji_mlen), nl, dp<uint64_t>(boff)));
+    return KDTN_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+// Incremental CR ingest (include/kdtn.h): the informer's added / updated Topology CRs as a
+// TopologyList document decoded into scratch tables, interned into the resident dictionaries,
+// matched to the resident rows by (namespace, name), and applied as a delta.
+int kdtn_json_ingest_delta(kdtn_ctx* c, const uint32_t* deleted, uint32_t n_deleted, const kdtn_vni_table* vnis,
+                           kdtn_ingest_info* info) {
+    if (!c || !c->j_loaded || !c->uploaded || (n_deleted && !deleted)) return KDTN_EINVAL;
+    HIP_TRY(hipSetDevice(c->device));
+    end_shard_ingest(c);
+    g_last_error[0] = 0;
+    if (c->nranks > 1) {
+        std::snprintf(g_last_error, sizeof(g_last_error), "kdtn_json_ingest_delta: single-shard contexts");
+        return KDTN_EINVAL;
+    }
+    if (c->kd_valid < c->D || c->pd_valid < c->P) {
+        std::snprintf(g_last_error, sizeof(g_last_error),
+                      "kdtn_json_ingest_delta: the resident dictionaries were not parsed (run the epoch first)");
+        return KDTN_EINVAL;
+    }
+    const kdtn_vni_table resident{KDTN_VNI_RESIDENT, nullptr, nullptr, nullptr};
+    const kdtn_vni_table& vn = vnis ? *vnis : resident;
+    hipStream_t s = c->stream;
+    const uint32_t T0 = c->T, N0 = c->des.n, M0 = c->real.n, D0 = c->D, P0 = c->P;
+    // 1. decode into scratch (the resident tables are untouched; a rejected document leaves them)
+    const JsTargets tg{&c->ji_ns, &c->ji_name, &c->ji_src, &c->ji_netns, &c->ji_flags, &c->ji_roff, &c->ji_noff,
+                       &c->ji_des, &c->ji_real, &c->ji_kb, &c->ji_ko, &c->ji_pb, &c->ji_po};
+    JsCounts k{};
+    {
+        const int rc = json_decode(c, tg, &k, info);
+        c->uploaded = true;                          // (json_reject clears it: the state stands)
+        if (rc != KDTN_OK) return rc;
+    }
+    const uint32_t Tl = k.T, Nl = k.N;
+    const uint64_t n_tokens = c->j_info.n_tokens;
+    // 2. intern the document's strings into the resident dictionaries
+    TRY(strix_update(c, c->ix_k, c->kd_bytes, c->kd_offs, D0, k.D));
+    TRY(strix_update(c, c->ix_p, c->pd_bytes, c->pd_offs, P0, k.P));
+    TRY(strix_lookup(c, c->ix_k, c->ji_kb, c->ji_ko, k.D, c->kd_bytes, c->kd_offs, c->ji_kmap, c->ji_rank, c->ji_boff));
+    uint64_t cnt[4] = {0, 0, 0, 0};                  // new key strings, their bytes, new prop strings, bytes
+    TRY(d2h(c, cnt, dp<uint64_t>(c->ji_rank) + k.D));
+    TRY(d2h(c, cnt + 1, dp<uint64_t>(c->ji_boff) + k.D));
+    HIP_TRY(hipStreamSynchronize(s));
+    const uint32_t D1 = D0 + (uint32_t)cnt[0];
+    const uint64_t kar1 = c->kd_arena + cnt[1];
+    TRY(ensure_keep(c->kd_bytes, kar1 + 64, c->kd_arena, s));
+    TRY(ensure_keep(c->kd_offs, ((size_t)D1 + 1) * 4, ((size_t)D0 + 1) * 4, s));
+    if (k.D)
+        k_strix_append<<<nblocks(k.D), BLOCK, 0, s>>>(dp<uint8_t>(c->ji_kb), dp<uint32_t>(c->ji_ko), k.D,
+                                                      dp<uint64_t>(c->ji_rank), dp<uint64_t>(c->ji_boff), D0,
+                                                      (uint32_t)c->kd_arena, dp<uint32_t>(c->ji_kmap),
+                                                      dp<uint8_t>(c->kd_bytes), dp<uint32_t>(c->kd_offs));
+    // (the rank / offset scratch is reused for the property dictionary after the key append)
+    TRY(strix_lookup(c, c->ix_p, c->ji_pb, c->ji_po, k.P, c->pd_bytes, c->pd_offs, c->ji_pmap, c->ji_kpos, c->ji_cpos));
+    TRY(d2h(c, cnt + 2, dp<uint64_t>(c->ji_kpos) + k.P));
+    TRY(d2h(c, cnt + 3, dp<uint64_t>(c->ji_cpos) + k.P));
+    HIP_TRY(hipStreamSynchronize(s));
+    const uint32_t P1 = P0 + (uint32_t)cnt[2];
+    const uint64_t par1 = c->pd_arena + cnt[3];
+    if (kar1 > 0xFFFFFF00ull || par1 > 0xFFFFFF00ull || (uint64_t)D1 >= 0x7FFFFFFFu || (uint64_t)P1 >= 0x7FFFFFFFu) {
+        std::snprintf(g_last_error, sizeof(g_last_error), "kdtn_json_ingest_delta: dictionaries over 4 GiB / 2^31");
+        return KDTN_EINVAL;
+    }
+    TRY(ensure_keep(c->pd_bytes, par1 + 64, c->pd_arena, s));
+    TRY(ensure_keep(c->pd_offs, ((size_t)P1 + 1) * 4, ((size_t)P0 + 1) * 4, s));
+    if (k.P)
+        k_strix_append<<<nblocks(k.P), BLOCK, 0, s>>>(dp<uint8_t>(c->ji_pb), dp<uint32_t>(c->ji_po), k.P,
+                                                      dp<uint64_t>(c->ji_kpos), dp<uint64_t>(c->ji_cpos), P0,
+                                                      (uint32_t)c->pd_arena, dp<uint32_t>(c->ji_pmap),
+                                                      dp<uint8_t>(c->pd_bytes), dp<uint32_t>(c->pd_offs));
+    // the appended strings join the indexes
+    if (D1 > D0)
+        k_strix_insert<<<nblocks(D1 - D0), BLOCK, 0, s>>>(dp<uint8_t>(c->kd_bytes), dp<uint32_t>(c->kd_offs), D0, D1,
+                                                          dp<unsigned long long>(c->ix_k.slots), c->ix_k.mask);
+    if (P1 > P0)
+        k_strix_insert<<<nblocks(P1 - P0), BLOCK, 0, s>>>(dp<uint8_t>(c->pd_bytes), dp<uint32_t>(c->pd_offs), P0, P1,
+                                                          dp<unsigned long long>(c->ix_p.slots), c->ix_p.mask);
+    c->ix_k.n = D1;
+    c->ix_p.n = P1;
+    // 3. the document's tables in resident ids
+    TRY(ensure(c->ji_nil, (size_t)Tl + 16));
+    if (Tl)
+        k_ix_map_topos<<<nblocks(Tl), BLOCK, 0, s>>>(dp<uint32_t>(c->ji_ns), dp<uint32_t>(c->ji_name),
+                                                     dp<uint32_t>(c->ji_src), dp<uint32_t>(c->ji_netns),
+                                                     dp<uint8_t>(c->ji_flags), Tl, dp<uint32_t>(c->ji_kmap),
+                                                     dp<uint8_t>(c->ji_nil));
+    constexpr uint32_t IDW = (KDTN_NKEY + KDTN_NPROP) * TILE_RECS;
+    if (Nl)
+        k_ix_map_links<<<nblocks((uint64_t)(Nl + TILE_RECS - 1) / TILE_RECS * IDW), BLOCK, 0, s>>>(
+            dp<uint32_t>(c->ji_des.buf), Nl, dp<uint32_t>(c->ji_kmap), dp<uint32_t>(c->ji_pmap));
+    // 4. the document's Topologies against the resident rows; the deletions; the new table
+    const uint64_t kcap = next_pow2(2ull * T0 + 64);
+    TRY(ensure(c->ji_keys, (size_t)kcap * 8));
+    TRY(ensure(c->ji_vals, (size_t)kcap * 4));
+    TRY(ensure(c->ji_keep, (size_t)T0 * 4 + 16));
+    TRY(ensure(c->ji_kpos, ((size_t)T0 + 1) * 8));
+    TRY(ensure(c->ji_claim, (size_t)T0 * 4 + 16));
+    TRY(ensure(c->ji_res, (size_t)Tl * 4 + 16));
+    TRY(ensure(c->ji_created, (size_t)Tl * 4 + 16));
+    TRY(ensure(c->ji_cpos, ((size_t)Tl + 1) * 8));
+    TRY(ensure(c->misc, 256));
+    uint32_t* misc = dp<uint32_t>(c->misc);
+    HIP_TRY(hipMemsetAsync(misc + MISC_DELTA_ERR, 0, 4, s));
+    HIP_TRY(hipMemsetAsync(c->ji_keys.p, 0, (size_t)kcap * 8, s));
+    HIP_TRY(hipMemsetAsync(c->ji_vals.p, 0xFF, (size_t)kcap * 4, s));
+    HIP_TRY(hipMemsetAsync(c->ji_claim.p, 0xFF, (size_t)T0 * 4 + 16, s));
+    if (T0) HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(c->ji_keep.p), 1, T0, s));
+    if (T0)
+        k_topokey_insert<<<nblocks(T0), BLOCK, 0, s>>>(dp<uint32_t>(c->t_ns), dp<uint32_t>(c->t_name), T0,
+                                                       dp<unsigned long long>(c->ji_keys), dp<uint32_t>(c->ji_vals),
+                                                       (uint32_t)kcap - 1);
+    if (n_deleted) {
+        TRY(upload(c, c->ji_del, deleted, (size_t)n_deleted * 4));
+        k_topo_delete<<<nblocks(n_deleted), BLOCK, 0, s>>>(dp<uint32_t>(c->ji_del), n_deleted, T0,
+                                                           dp<uint32_t>(c->ji_keep), misc + MISC_DELTA_ERR);
+    }
+    if (Tl)
+        k_topokey_match<<<nblocks(Tl), BLOCK, 0, s>>>(dp<uint32_t>(c->ji_ns), dp<uint32_t>(c->ji_name), Tl,
+                                                      dp<unsigned long long>(c->ji_keys), dp<uint32_t>(c->ji_vals),
+                                                      (uint32_t)kcap - 1, dp<uint32_t>(c->ji_keep),
+                                                      dp<uint32_t>(c->ji_claim), dp<uint32_t>(c->ji_res),
+                                                      dp<uint32_t>(c->ji_created), misc + MISC_DELTA_ERR);
+    TRY(scan_u32(c, dp<uint32_t>(c->ji_keep), T0, dp<uint64_t>(c->ji_kpos)));
+    TRY(scan_u32(c, dp<uint32_t>(c->ji_created), Tl, dp<uint64_t>(c->ji_cpos)));
+    uint64_t tot[2] = {0, 0};
+    uint32_t err = 0;
+    TRY(d2h(c, tot, dp<uint64_t>(c->ji_kpos) + T0));
+    TRY(d2h(c, tot + 1, dp<uint64_t>(c->ji_cpos) + Tl));
+    TRY(d2h(c, &err, misc + MISC_DELTA_ERR));
+    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(hipGetLastError());
+    auto refuse = [&](const char* what) {
+        // the dictionaries only grew past the resident strings: their sizes stay, the arena
+        // tails are overwritten later, and the indexes (which hold the appended strings) are
+        // rebuilt by the next incremental ingest (mask 0)
+        c->ix_k.n = c->ix_k.mask = c->ix_p.n = c->ix_p.mask = 0;
+        std::snprintf(g_last_error, sizeof(g_last_error), "kdtn_json_ingest_delta: %s", what);
+        state_changed(c);
+        return KDTN_EINVAL;
+    };
+    if (err & 4u) return refuse("a deleted index is out of range");
+    if (err & 1u) return refuse("a Topology is both deleted and listed in the document");
+    if (err & 2u) return refuse("a Topology is listed twice in the document");
+    const uint32_t n_kept = (uint32_t)tot[0], n_created = (uint32_t)tot[1], Tn = n_kept + n_created;
+    const bool remap = n_kept != T0 || n_created;
+    // 5. the delta: the document's Topologies are the changed list (row l: spec from its
+    // records, all inline), laid out over the new table
+    TRY(plan_alloc(c, Tn));
+    TRY(ensure(c->st_chg, (size_t)Tn * 4 + 16));
+    HIP_TRY(hipMemsetAsync(c->st_chg.p, 0xFF, (size_t)Tn * 4 + 16, s));
+    if (remap) TRY(ensure(c->dl_prev, (size_t)Tn * 4 + 16));
+    const uint32_t nl = std::max(T0, Tl);
+    if (nl)
+        k_ix_layout<<<nblocks(nl), BLOCK, 0, s>>>(dp<uint32_t>(c->ji_keep), dp<uint64_t>(c->ji_kpos), T0,
+                                                  dp<uint32_t>(c->ji_claim), dp<uint32_t>(c->ji_created),
+                                                  dp<uint64_t>(c->ji_cpos), Tl, n_kept,
+                                                  remap ? dp<uint32_t>(c->dl_prev) : nullptr, dp<uint32_t>(c->st_chg));
+    TRY(ensure(c->ji_ref, (size_t)Nl * 4 + 16));
+    if (Nl) k_ix_refs<<<nblocks(Nl), BLOCK, 0, s>>>(dp<uint32_t>(c->ji_ref), Nl);
+    TRY(ensure(c->dl_rows, (size_t)Tl * 4 + 16));
+    TRY(ensure(c->sh_src, (size_t)Tn * 4));
+    TRY(ensure(c->sh_netns, (size_t)Tn * 4));
+    TRY(ensure(c->sh_flags, (size_t)Tn));
+    if (remap) {
+        TRY(ensure(c->sh_ns, (size_t)Tn * 4));
+        TRY(ensure(c->sh_name, (size_t)Tn * 4));
+        TRY(ensure(c->st_rlen, (size_t)Tn * 4 + 16));
+        TRY(ensure(c->st_rbase, (size_t)Tn * 4 + 16));
+        TRY(ensure(c->st_mask, (size_t)Tn + 16));
+        TRY(ensure(c->st_seen, ((size_t)T0 + 31) / 32 * 4 + 16));
+        HIP_TRY(hipMemsetAsync(c->st_seen.p, 0, ((size_t)T0 + 31) / 32 * 4 + 16, s));
+        HIP_TRY(hipMemsetAsync(c->st_mask.p, ASM_SEG_A, (size_t)Tn + 16, s));
+    }
+    HIP_TRY(hipMemsetAsync(misc + MISC_ROWCHG_N, 0, 4, s));
+    const uint64_t nbound = (uint64_t)N0 + Nl;
+    if (nbound >= 0x7FFFFFFFull) return refuse("desired store over 2^31 records");
+    TRY(link_store_alloc(c, c->sh_des, (uint32_t)nbound));
+    if (remap) TRY(link_store_alloc(c, c->sh_real, M0));
+    DeltaPlanIn pi{topo_view(c), dp<uint32_t>(c->st_chg), remap ? dp<uint32_t>(c->dl_prev) : nullptr,
+                   dp<uint32_t>(c->ji_noff), dp<uint32_t>(c->ji_src), dp<uint32_t>(c->ji_netns), dp<uint8_t>(c->ji_nil),
+                   dp<uint32_t>(c->ji_ns), dp<uint32_t>(c->ji_name), Tn, D1};
+    DeltaPlanOut po{dp<uint32_t>(c->sh_ns), dp<uint32_t>(c->sh_name), dp<uint32_t>(c->sh_src),
+                    dp<uint32_t>(c->sh_netns), dp<uint8_t>(c->sh_flags), dp<uint32_t>(c->st_len),
+                    dp<uint32_t>(c->st_base), dp<uint8_t>(c->st_mode), dp<uint32_t>(c->st_rlen),
+                    dp<uint32_t>(c->st_rbase), dp<uint32_t>(c->dl_rows), misc + MISC_ROWCHG_N,
+                    dp<uint32_t>(c->st_seen), misc + MISC_DELTA_ERR};
+    if (Tn) k_delta_plan<<<nblocks(Tn), BLOCK, 0, s>>>(pi, po);
+    TRY(scan_lengths(c, c->st_len, Tn, c->st_off64, c->st_part, c->st_off32));
+    const AsmGuard g{misc + MISC_DELTA_ERR, dp<uint64_t>(c->st_off64) + Tn, 0u};
+    if (nbound)
+        k_store_assemble<<<nblocks(nbound), BLOCK, 0, s>>>(dp<uint32_t>(c->st_off32), Tn, dp<uint32_t>(c->st_base),
+                                                           dp<uint8_t>(c->st_mode), dp<uint32_t>(c->ji_ref), c->des.view,
+                                                           c->ji_des.view, (uint32_t)nbound, g,
+                                                           dp<uint32_t>(c->sh_des.buf));
+    if (remap) {
+        TRY(scan_lengths(c, c->st_rlen, Tn, c->st_roff64, c->st_rpart, c->st_roff32));
+        const AsmGuard gr{misc + MISC_DELTA_ERR, dp<uint64_t>(c->st_roff64) + Tn, 0u};
+        if (M0)
+            k_store_assemble<<<nblocks(M0), BLOCK, 0, s>>>(dp<uint32_t>(c->st_roff32), Tn, dp<uint32_t>(c->st_rbase),
+                                                           dp<uint8_t>(c->st_mask), nullptr, c->real.view, c->real.view,
+                                                           M0, gr, dp<uint32_t>(c->sh_real.buf));
+    }
+    k_delta_totals<<<1, 64, 0, s>>>(dp<uint64_t>(c->st_off64), Tn, remap ? dp<uint64_t>(c->st_roff64) : nullptr, misc);
+    HIP_TRY(hipGetLastError());
+    uint32_t* hm = c->h_misc + 64;
+    HIP_TRY(hipMemcpyAsync(hm, misc, 64 * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (hm[MISC_DELTA_ERR]) return refuse("the document's tables failed the delta checks");
+    // 6. the new state
+    const uint64_t N = (uint64_t)hm[MISC_DELTA_N] | ((uint64_t)hm[MISC_DELTA_N + 1] << 32);
+    std::swap(c->des, c->sh_des);
+    c->des.n = c->des.view.n = (uint32_t)N;
+    std::swap(c->t_noff, c->st_off32);
+    std::swap(c->t_src, c->sh_src);
+    std::swap(c->t_netns, c->sh_netns);
+    std::swap(c->t_flags, c->sh_flags);
+    if (remap) {
+        const uint64_t M = (uint64_t)hm[MISC_DELTA_M] | ((uint64_t)hm[MISC_DELTA_M + 1] << 32);
+        std::swap(c->real, c->sh_real);
+        c->real.n = c->real.view.n = (uint32_t)M;
+        std::swap(c->t_roff, c->st_roff32);
+        std::swap(c->t_ns, c->sh_ns);
+        std::swap(c->t_name, c->sh_name);
+        c->T = Tn;
+    }
+    // dictionaries: the appended strings are parsed by the next run (kd_from / pd_from)
+    c->D = D1;
+    c->P = P1;
+    c->kd_arena = kar1;
+    c->pd_arena = par1;
+    c->kd_valid = c->kd_from = D0;
+    c->pd_valid = c->pd_from = P0;
+    TRY(prepare_dicts(c));
+    TRY(check_vnis(c, vn, D1, D0));
+    TRY(prepare_vnis(c, vn));
+    TRY(prepare_work(c, remap ? Tn : c->slice, c->real.n, c->des.n));
+    c->pods_ready = false;                         // rows changed: the next run rebuilds the pod tables
+    c->pods_delta = false;
+    HIP_TRY(hipStreamSynchronize(s));
+    state_changed(c);
+    c->pods_imported = false;
+    c->uploaded = true;
+    c->j_info = kdtn_ingest_info{};
+    c->j_info.n_topos = c->T;
+    c->j_info.n_desired = c->des.n;
+    c->j_info.n_realised = c->real.n;
+    c->j_info.n_kdict = D1;
+    c->j_info.n_pdict = P1;
+    c->j_info.n_tokens = n_tokens;
+    c->j_info.kdict_bytes = kar1;
+    c->j_info.pdict_bytes = par1;
+    if (info) *info = c->j_info;
     return KDTN_OK;
 }
 

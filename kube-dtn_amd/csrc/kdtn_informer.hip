@@ -1,0 +1,202 @@
+// kdtn_informer.hip — incremental CR ingest on a resident state (SURVEY §8(f) rank 2 with the
+// informer's event stream, daemon/kubedtn/kubedtn.go:128-142): the added / updated Topology
+// CRs arrive as a TopologyList document and are decoded by the ingest kernels into scratch
+// tables with document-local dictionaries; these kernels then intern the local strings into
+// the resident, append-only dictionaries (a string already resident keeps its id, so the
+// resident link stores and the resident VXLAN map stay valid; a new one is appended in
+// first-occurrence order), rewrite every id column, match each document Topology to its
+// resident row by (namespace, name), and lay out the delta that kdtn_epoch_upload_delta's
+// plan / assembly kernels apply.
+#include "kdtn_encode.h"
+
+namespace kdtn {
+
+// FNV-1a 64 over the string's bytes, murmur3-finalised; tag = high half | 1 (never 0 = empty)
+KD_INLINE uint64_t str_hash(const uint8_t* b, uint32_t n) {
+    uint64_t h = 0xCBF29CE484222325ull;
+    for (uint32_t i = 0; i < n; ++i) h = (h ^ b[i]) * 0x100000001B3ull;
+    return hash64(h);
+}
+KD_INLINE bool str_eq(const uint8_t* a, const uint8_t* b, uint32_t n) {
+    for (uint32_t i = 0; i < n; ++i)
+        if (a[i] != b[i]) return false;
+    return true;
+}
+
+// Resident string index: open addressing over {tag:32 | id:32} words (0 = empty), one thread
+// per dictionary id in [from, n). A string stored twice keeps its smaller id.
+__global__ void __launch_bounds__(BLOCK) k_strix_insert(const uint8_t* bytes, const uint32_t* offs, uint32_t from,
+                                                        uint32_t n, unsigned long long* slots, uint32_t mask) {
+    const uint32_t i = from + blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t o = offs[i], len = offs[i + 1] - o;
+    const uint64_t h = str_hash(bytes + o, len);
+    const unsigned long long mine = ((h >> 32) | 1ull) << 32 | i;
+    for (uint32_t p = (uint32_t)h & mask;; p = (p + 1) & mask) {
+        unsigned long long cur = slots[p];
+        if (cur == 0) {
+            cur = atomicCAS(slots + p, 0ull, mine);
+            if (cur == 0) return;
+        }
+        if ((cur >> 32) == (mine >> 32)) {
+            const uint32_t j = (uint32_t)cur, oj = offs[j];
+            if (offs[j + 1] - oj == len && str_eq(bytes + oj, bytes + o, len)) {
+                atomicMin(slots + p, mine);
+                return;
+            }
+        }
+    }
+}
+
+// Local (document) string l → resident id, or a miss: miss[l] = 1 and mlen[l] = its length
+// (scanned for the appended ids and arena offsets).
+__global__ void __launch_bounds__(BLOCK) k_strix_lookup(const uint8_t* lb, const uint32_t* lo, uint32_t nl,
+                                                        const uint8_t* rb, const uint32_t* ro,
+                                                        const unsigned long long* slots, uint32_t mask, uint32_t* map,
+                                                        uint32_t* miss, uint32_t* mlen) {
+    const uint32_t l = blockIdx.x * BLOCK + threadIdx.x;
+    if (l >= nl) return;
+    const uint32_t o = lo[l], len = lo[l + 1] - o;
+    const uint64_t h = str_hash(lb + o, len);
+    const unsigned long long tag = (h >> 32) | 1ull;
+    uint32_t id = 0xFFFFFFFFu;
+    for (uint32_t p = (uint32_t)h & mask;; p = (p + 1) & mask) {
+        const unsigned long long cur = slots[p];
+        if (cur == 0) break;
+        if ((cur >> 32) == tag) {
+            const uint32_t j = (uint32_t)cur, oj = ro[j];
+            if (ro[j + 1] - oj == len && str_eq(rb + oj, lb + o, len)) {
+                id = j;
+                break;
+            }
+        }
+    }
+    map[l] = id;
+    miss[l] = id == 0xFFFFFFFFu;
+    mlen[l] = id == 0xFFFFFFFFu ? len : 0u;
+}
+
+// The missed strings appended to the resident dictionary: id D0 + rank, bytes at arena0 + boff
+__global__ void __launch_bounds__(BLOCK) k_strix_append(const uint8_t* lb, const uint32_t* lo, uint32_t nl,
+                                                        const uint64_t* rank, const uint64_t* boff, uint32_t D0,
+                                                        uint32_t arena0, uint32_t* map, uint8_t* rb, uint32_t* ro) {
+    const uint32_t l = blockIdx.x * BLOCK + threadIdx.x;
+    if (l >= nl || map[l] != 0xFFFFFFFFu) return;
+    const uint32_t id = D0 + (uint32_t)rank[l], o = lo[l], len = lo[l + 1] - o;
+    const uint32_t at = arena0 + (uint32_t)boff[l];
+    for (uint32_t i = 0; i < len; ++i) rb[at + i] = lb[o + i];
+    ro[id + 1] = at + len;
+    map[l] = id;
+}
+
+// Document topology rows into resident ids; spec-nil as the delta's byte
+__global__ void __launch_bounds__(BLOCK) k_ix_map_topos(uint32_t* ns, uint32_t* name, uint32_t* src, uint32_t* netns,
+                                                        const uint8_t* flags, uint32_t T, const uint32_t* kmap,
+                                                        uint8_t* nil) {
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= T) return;
+    ns[t] = kmap[ns[t]];
+    name[t] = kmap[name[t]];
+    src[t] = kmap[src[t]];
+    netns[t] = kmap[netns[t]];
+    nil[t] = (flags[t] & KDTN_TOPO_SPEC_NIL) ? 1 : 0;
+}
+
+// Every id column of a document link store into resident ids (one thread per tile word of the
+// 19 id columns: coalesced on both sides)
+__global__ void __launch_bounds__(BLOCK) k_ix_map_links(uint32_t* base, uint32_t n, const uint32_t* kmap,
+                                                        const uint32_t* pmap) {
+    constexpr uint32_t IDW = (KDTN_NKEY + KDTN_NPROP) * TILE_RECS;
+    const uint64_t w = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t tile = (uint32_t)(w / IDW), r = (uint32_t)(w % IDW);
+    const uint32_t rec = tile * TILE_RECS + (r & 63u), col = r >> 6;
+    if (rec >= n) return;
+    uint32_t* p = base + (size_t)tile * TILE_WORDS + r;
+    *p = col < KDTN_NKEY ? kmap[*p] : pmap[*p];
+}
+
+// Resident topology rows by informer key (namespace, name ids): {key | 1<<63} slots with the
+// smallest row index as value
+KD_INLINE uint64_t topo_key(uint32_t ns, uint32_t name) { return ((uint64_t)ns << 32 | name) | (1ull << 63); }
+__global__ void __launch_bounds__(BLOCK) k_topokey_insert(const uint32_t* ns, const uint32_t* name, uint32_t T,
+                                                          unsigned long long* keys, uint32_t* vals, uint32_t mask) {
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= T) return;
+    const unsigned long long k = topo_key(ns[t], name[t]);
+    for (uint32_t p = (uint32_t)hash64(k) & mask;; p = (p + 1) & mask) {
+        const unsigned long long cur = atomicCAS(keys + p, 0ull, k);
+        if (cur == 0 || cur == k) {
+            atomicMin(vals + p, t);
+            return;
+        }
+    }
+}
+
+// Each document Topology against the resident rows: res[l] = its resident row or NONE
+// (created); claims[row] = l, and a row claimed twice (an object listed twice), or claimed and
+// deleted, is an error. created[l] = 1 for the scan that places created rows.
+__global__ void __launch_bounds__(BLOCK) k_topokey_match(const uint32_t* ns, const uint32_t* name, uint32_t Tl,
+                                                         const unsigned long long* keys, const uint32_t* vals,
+                                                         uint32_t mask, const uint32_t* keep, uint32_t* claim,
+                                                         uint32_t* res, uint32_t* created, uint32_t* err) {
+    const uint32_t l = blockIdx.x * BLOCK + threadIdx.x;
+    uint32_t e = 0;
+    if (l < Tl) {
+        const unsigned long long k = topo_key(ns[l], name[l]);
+        uint32_t row = 0xFFFFFFFFu;
+        for (uint32_t p = (uint32_t)hash64(k) & mask;; p = (p + 1) & mask) {
+            const unsigned long long cur = keys[p];
+            if (cur == 0) break;
+            if (cur == k) {
+                row = vals[p];
+                break;
+            }
+        }
+        res[l] = row;
+        created[l] = row == 0xFFFFFFFFu;
+        if (row != 0xFFFFFFFFu) {
+            if (!keep[row]) e |= 1u;                                   // updated and deleted
+            if (atomicExch(claim + row, l) != 0xFFFFFFFFu) e |= 2u;   // listed twice
+        }
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) e |= __shfl_xor(e, d, 64);
+    if ((threadIdx.x & 63) == 0 && e) atomicOr(err, e);
+}
+
+// Deleted resident rows (host list): keep[row] = 0; an index out of range is an error
+__global__ void __launch_bounds__(BLOCK) k_topo_delete(const uint32_t* del, uint32_t n, uint32_t T, uint32_t* keep,
+                                                       uint32_t* err) {
+    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+    if (k >= n) return;
+    if (del[k] >= T) atomicOr(err, 4u);
+    else keep[del[k]] = 0;
+}
+
+// The new table: kept rows in resident order (exclusive scan kpos of keep), then the created
+// Topologies in document order (cpos of created). prev / chg over the new table as
+// k_delta_plan takes them; chg = the document row (the delta's changed-list index).
+__global__ void __launch_bounds__(BLOCK) k_ix_layout(const uint32_t* keep, const uint64_t* kpos, uint32_t T0,
+                                                     const uint32_t* claim, const uint32_t* created,
+                                                     const uint64_t* cpos, uint32_t Tl, uint32_t n_kept, uint32_t* prev,
+                                                     uint32_t* chg) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i < T0 && keep[i]) {
+        const uint32_t t = (uint32_t)kpos[i];
+        if (prev) prev[t] = i;
+        chg[t] = claim[i];
+    }
+    if (i < Tl && created[i]) {
+        const uint32_t t = n_kept + (uint32_t)cpos[i];
+        if (prev) prev[t] = KDTN_DELTA_NEW;
+        chg[t] = i;
+    }
+}
+
+// the delta's references: every record of the document store, in order (inline)
+__global__ void __launch_bounds__(BLOCK) k_ix_refs(uint32_t* ref, uint32_t n) {
+    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+    if (k < n) ref[k] = KDTN_DELTA_NEW | k;
+}
+
+}  // namespace kdtn

@@ -393,6 +393,29 @@ __global__ void k_delta_place(const uint32_t* stage, const int64_t* uid, uint32_
 __global__ void k_delta_inline(const uint32_t* d_off, const uint32_t* topo, uint32_t n, const uint32_t* ref,
                                uint32_t nref, const uint32_t* off, DevLinks B, const uint32_t* err, uint32_t* out);
 
+// ---- incremental CR ingest on a resident state (kdtn_informer.hip) ------------------------
+__global__ void k_strix_insert(const uint8_t* bytes, const uint32_t* offs, uint32_t from, uint32_t n,
+                               unsigned long long* slots, uint32_t mask);
+__global__ void k_strix_lookup(const uint8_t* lb, const uint32_t* lo, uint32_t nl, const uint8_t* rb, const uint32_t* ro,
+                               const unsigned long long* slots, uint32_t mask, uint32_t* map, uint32_t* miss,
+                               uint32_t* mlen);
+__global__ void k_strix_append(const uint8_t* lb, const uint32_t* lo, uint32_t nl, const uint64_t* rank,
+                               const uint64_t* boff, uint32_t D0, uint32_t arena0, uint32_t* map, uint8_t* rb,
+                               uint32_t* ro);
+__global__ void k_ix_map_topos(uint32_t* ns, uint32_t* name, uint32_t* src, uint32_t* netns, const uint8_t* flags,
+                               uint32_t T, const uint32_t* kmap, uint8_t* nil);
+__global__ void k_ix_map_links(uint32_t* base, uint32_t n, const uint32_t* kmap, const uint32_t* pmap);
+__global__ void k_topokey_insert(const uint32_t* ns, const uint32_t* name, uint32_t T, unsigned long long* keys,
+                                 uint32_t* vals, uint32_t mask);
+__global__ void k_topokey_match(const uint32_t* ns, const uint32_t* name, uint32_t Tl, const unsigned long long* keys,
+                                const uint32_t* vals, uint32_t mask, const uint32_t* keep, uint32_t* claim,
+                                uint32_t* res, uint32_t* created, uint32_t* err);
+__global__ void k_topo_delete(const uint32_t* del, uint32_t n, uint32_t T, uint32_t* keep, uint32_t* err);
+__global__ void k_ix_layout(const uint32_t* keep, const uint64_t* kpos, uint32_t T0, const uint32_t* claim,
+                            const uint32_t* created, const uint64_t* cpos, uint32_t Tl, uint32_t n_kept,
+                            uint32_t* prev, uint32_t* chg);
+__global__ void k_ix_refs(uint32_t* ref, uint32_t n);
+
 // ---- RemotePod messages (kdtn_wire.hip) and the receiving daemon's tc argv (kdtn_tc.hip) ----
 // message m: the UpdateRemote payload of add entry rem_idx[m] (m < n_remote, fan-out order) or
 // the physical peer's local Update payload of add entry phys_idx[m - n_remote]

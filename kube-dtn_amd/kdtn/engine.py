@@ -111,6 +111,7 @@ def lib() -> C.CDLL:
         "kdtn_epoch_upload_delta": (C.c_int, [vp, C.POINTER(abi.EpochDelta)]),
         "kdtn_epoch_tables_info": (C.c_int, [vp, C.POINTER(abi.IngestInfo)]),
         "kdtn_epoch_download_remote": (C.c_int, [vp, C.POINTER(abi.RemotePods)]),
+        "kdtn_json_ingest_delta": (C.c_int, [vp, vp, C.c_uint32, C.POINTER(abi.VniTable), C.POINTER(abi.IngestInfo)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -282,6 +283,26 @@ class Engine:
         self._T = info.n_topos
         self._caps = (info.n_realised, info.n_desired, info.n_realised)
         self._ingest = info
+        return info
+
+    def ingest_delta(self, doc: bytes, deleted=None, vnis=None) -> abi.IngestInfo:
+        """kdtn_json_ingest_delta: the added / updated Topology CRs (a TopologyList document)
+        and the resident indices of the deleted ones applied to the resident state; their
+        strings are interned into the resident dictionaries. vnis None keeps the resident
+        VXLAN map."""
+        self.json_upload(doc)
+        info = abi.IngestInfo()
+        dl = np.ascontiguousarray(deleted if deleted is not None else np.zeros(0), dtype=np.uint32)
+        cv = vnis.to_c() if vnis is not None else None
+        rc = lib().kdtn_json_ingest_delta(self._ctx, dl.ctypes.data if len(dl) else None, len(dl),
+                                          C.byref(cv) if cv is not None else None, C.byref(info))
+        if rc == abi.EBADMSG:
+            e = KdtnError(rc, "kdtn_json_ingest_delta")
+            e.info = info
+            raise e
+        _check(rc, "kdtn_json_ingest_delta")
+        self._T = info.n_topos
+        self._caps = (info.n_realised, info.n_desired, info.n_realised)
         return info
 
     def ingest(self, doc: bytes, vnis=None, shard=None) -> abi.IngestInfo:

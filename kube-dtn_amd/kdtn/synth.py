@@ -190,11 +190,11 @@ class ChurnSequence:
 
 
 def select_topologies(inp: EpochInput, keep: np.ndarray) -> EpochInput:
-    """The epoch restricted to the Topologies with keep[t] (order kept): their rows and both
+    """The epoch restricted to the Topologies with keep[t] (order kept; or an index array): their rows and both
     link segments; the dictionaries and the VXLAN snapshot are shared. Peers of a dropped
     Topology stay in the kept ones' links (their lookups then fail, as for a deleted CR)."""
-    keep = np.asarray(keep, bool)
-    sel = np.nonzero(keep)[0]
+    keep = np.asarray(keep)
+    sel = np.nonzero(keep)[0] if keep.dtype == bool else keep.astype(np.int64)   # (indices: any order)
     T = inp.topos
 
     def side(L: Links, off: np.ndarray):
