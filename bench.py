@@ -316,6 +316,47 @@ def resident_chain_stage(eng, cs, prev, epochs: int, topology_set: bool = False)
     return res
 
 
+def resident_pipeline_stage(eng, cs, prev, epochs: int):
+    """The same resident controller loop pipelined over the full-duplex host link (separate
+    report, never `value`): epoch k's outputs are copied out asynchronously
+    (kdtn_epoch_download_async into one of two page-locked buffer sets) while epoch k+1's delta
+    is uploaded; the next run waits for the copies on the GPU. Per-epoch time = wall time of
+    the loop / epochs, after 2 warm-up epochs; every epoch's outputs are complete in host
+    memory (download_wait) before the next-but-one reuses their buffers."""
+    from kdtn.delta import build_delta
+    from kdtn.engine import pin_delta
+    from kdtn.tables import BatchesOut
+    T = prev.topos.n
+    cap = max(1 << 20, prev.desired.n // 8)
+    warm = 2
+    deltas = []
+    p = prev
+    for _ in range(warm + epochs):
+        cs.advance()
+        new = cs.epoch_input(copy=True)
+        deltas.append(pin_delta(build_delta(p, new, p.kdict.n, p.pdict.n)))
+        p = new
+    bufs = [BatchesOut.alloc(T, cap, cap, cap, pinned=True) for _ in range(2)]
+    ones = np.ones(T, np.uint8)
+    eng.commit(ones)
+    t0 = None
+    for ep, d in enumerate(deltas):
+        if ep == warm:
+            eng.download_wait()
+            t0 = time.perf_counter()
+        eng.upload_delta(d)                   # H2D beside the previous epoch's D2H
+        eng.run()
+        eng.sync()
+        eng.download_wait()                   # epoch ep-1's outputs are in host memory
+        eng.download_async(bufs[ep % 2])
+        eng.commit(ones)
+    eng.download_wait()
+    wall = time.perf_counter() - t0
+    return {"epochs": epochs, "e2e_ms": wall / epochs * 1e3, "links_per_s": p.desired.n * epochs / wall,
+            "note": "not part of value: resident loop with epoch k's download overlapping epoch k+1's delta "
+                    f"upload (full-duplex link), mean over {epochs} epochs after {warm} warm-up epochs"}
+
+
 def ingest_stage(eng, inp, steps: int, reps: int = 5, cpu_sample_pods: int = 20_000):
     """Separate report (not part of `value`): CR ingest of this shard's Topology CRs as a
     TopologyList JSON document (kdtn_json_ingest: json.Unmarshal + SoA + interning on the
@@ -780,6 +821,8 @@ def main():
         result["resident_chain"] = resident_chain_stage(eng, cs, inp, args.resident_epochs)
         # the same with Topologies created and deleted (informer add / delete events)
         del cs
+        progress("resident chain, pipelined")
+        result["resident_pipeline"] = resident_pipeline_stage(eng, cs, cs.epoch_input(copy=True), args.resident_epochs)
         progress("resident chain with a changing Topology set")
         tc = synth.TopologySetChurn(frac=0.01, total_pods=total_pods)
         p0 = tc.epoch_input()

@@ -305,6 +305,13 @@ int kdtn_epoch_upload(kdtn_ctx* ctx, const kdtn_epoch_in* in);
 int kdtn_epoch_run(kdtn_ctx* ctx, uint32_t stages);          /* async on the ctx stream   */
 int kdtn_epoch_sync(kdtn_ctx* ctx, kdtn_counts* counts);     /* waits; counts may be NULL */
 int kdtn_epoch_download(kdtn_ctx* ctx, kdtn_batches* out);   /* after sync                */
+/* Asynchronous download (after sync): the copies into `out` (page-locked, kdtn_host_alloc) run
+ * on a stream of their own while the caller goes on (commit, the next kdtn_epoch_upload_delta,
+ * whose host-to-device copies share the full-duplex link); the next kdtn_epoch_run waits for
+ * them on the GPU before overwriting the outputs. Counts in `out` are set at return; the
+ * arrays are valid after kdtn_epoch_download_wait. */
+int kdtn_epoch_download_async(kdtn_ctx* ctx, kdtn_batches* out);
+int kdtn_epoch_download_wait(kdtn_ctx* ctx);
 
 /* Gate + CalcDiff only (KDTN_STAGE_DIFF): the Del/Add/Update index lists per Topology,
  * without resolve or qdisc records (out->*_res / *_qdisc are not written). Replaces

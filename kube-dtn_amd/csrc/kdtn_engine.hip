@@ -67,6 +67,9 @@ struct kdtn_ctx {
     hipStream_t comm_stream = nullptr;          // RCCL pod-status exchange (nranks > 1)
     hipStream_t copy_stream = nullptr;          // delta uploads: host-to-device copies beside the kernels
     hipEvent_t ev_cp[4] = {};
+    hipStream_t d2h_stream = nullptr;           // kdtn_epoch_download_async: the outputs' copies
+    hipEvent_t ev_dl_ready = nullptr, ev_dl_done = nullptr;
+    bool dl_pending = false;                    // an async download's copies may still be reading outputs
     hipEvent_t ev_fill = nullptr, ev_ag = nullptr;
     // dictionaries; parsed tables persist across uploads for an append-only interner
     // (kdtn_epoch_in.kdict_keep / pdict_keep): *_valid strings have valid parsed tables, a run
@@ -837,6 +840,9 @@ int kdtn_init(kdtn_ctx** out, const kdtn_config* cfg) {
     (void)hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming);
     for (hipEvent_t& e : c->ev_cp) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
     if (hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess) c->copy_stream = nullptr;
+    if (hipStreamCreateWithFlags(&c->d2h_stream, hipStreamNonBlocking) != hipSuccess) c->d2h_stream = nullptr;
+    (void)hipEventCreateWithFlags(&c->ev_dl_ready, hipEventDisableTiming);
+    (void)hipEventCreateWithFlags(&c->ev_dl_done, hipEventDisableTiming);
     *out = c;
     return KDTN_OK;
 }
@@ -897,6 +903,12 @@ void kdtn_destroy(kdtn_ctx* c) {
         (void)hipStreamSynchronize(c->copy_stream);
         (void)hipStreamDestroy(c->copy_stream);
     }
+    if (c->d2h_stream) {
+        (void)hipStreamSynchronize(c->d2h_stream);
+        (void)hipStreamDestroy(c->d2h_stream);
+    }
+    if (c->ev_dl_ready) (void)hipEventDestroy(c->ev_dl_ready);
+    if (c->ev_dl_done) (void)hipEventDestroy(c->ev_dl_done);
     if (c->h_misc) (void)hipHostFree(c->h_misc);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
@@ -999,6 +1011,7 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
                       "host transport: kdtn_pods_import the gathered pod table before kdtn_epoch_run");
         return KDTN_EINVAL;
     }
+    if (c->dl_pending) HIP_TRY(hipStreamWaitEvent(s, c->ev_dl_done, 0));   // outputs still being copied out
     if (c->timing >= 2) (void)hipEventRecord(c->ev[0], s);
     uint32_t* sync = dp<uint32_t>(c->sync);
     // Epoch front: first launch (sync header, look-back area, pod-status rows) + RCCL
@@ -1312,18 +1325,15 @@ int kdtn_timer_totals(kdtn_ctx* c, const char** names, double* ms, uint32_t* epo
     return n;
 }
 
-int kdtn_epoch_download(kdtn_ctx* c, kdtn_batches* o) {
-    if (!c || !o || !c->ran) return KDTN_EINVAL;
-    HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+// the output copies of kdtn_epoch_download(_async) on stream `hs`
+static int download_enqueue(kdtn_ctx* c, kdtn_batches* o, hipStream_t hs) {
     const uint32_t nd = c->h_misc[1], nu = c->h_misc[2], na = c->h_misc[3];
     o->n_del = nd;
     o->n_upd = nu;
     o->n_add = na;
     if (nd > o->del_cap || nu > o->upd_cap || na > o->add_cap) return KDTN_ENOSPC;
-    hipStream_t s = c->stream;
     auto d2h = [&](void* dst, DevBuf& b, size_t bytes) -> int {
-        if (dst && bytes) HIP_TRY(hipMemcpyAsync(dst, b.p, bytes, hipMemcpyDeviceToHost, s));
+        if (dst && bytes) HIP_TRY(hipMemcpyAsync(dst, b.p, bytes, hipMemcpyDeviceToHost, hs));
         return KDTN_OK;
     };
     const bool res = c->last_stages & KDTN_STAGE_RESOLVE, q = c->last_stages & KDTN_STAGE_QDISC;
@@ -1343,7 +1353,42 @@ int kdtn_epoch_download(kdtn_ctx* c, kdtn_batches* o) {
         TRY(d2h(o->add_qdisc, c->add_qdisc, (size_t)na * 72));
         TRY(d2h(o->upd_qdisc, c->upd_qdisc, (size_t)nu * 72));
     }
-    HIP_TRY(hipStreamSynchronize(s));
+    return KDTN_OK;
+}
+
+int kdtn_epoch_download(kdtn_ctx* c, kdtn_batches* o) {
+    if (!c || !o || !c->ran) return KDTN_EINVAL;
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    TRY(kdtn_epoch_download_wait(c));
+    TRY(download_enqueue(c, o, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return KDTN_OK;
+}
+
+// Asynchronous form: the copies run on a stream of their own after the epoch, beside whatever
+// the caller enqueues next (commit, the next delta upload's host-to-device copies: the link is
+// full duplex); the next kdtn_epoch_run waits for them on the GPU before it overwrites the
+// outputs. The host buffers (page-locked, kdtn_host_alloc) hold the outputs once
+// kdtn_epoch_download_wait returns. Counts are known at return (after kdtn_epoch_sync).
+int kdtn_epoch_download_async(kdtn_ctx* c, kdtn_batches* o) {
+    if (!c || !o || !c->ran) return KDTN_EINVAL;
+    HIP_TRY(hipSetDevice(c->device));
+    TRY(kdtn_epoch_download_wait(c));
+    hipStream_t hs = c->d2h_stream ? c->d2h_stream : c->stream;
+    HIP_TRY(hipEventRecord(c->ev_dl_ready, c->stream));
+    HIP_TRY(hipStreamWaitEvent(hs, c->ev_dl_ready, 0));
+    TRY(download_enqueue(c, o, hs));
+    HIP_TRY(hipEventRecord(c->ev_dl_done, hs));
+    c->dl_pending = true;
+    return KDTN_OK;
+}
+
+int kdtn_epoch_download_wait(kdtn_ctx* c) {
+    if (!c) return KDTN_EINVAL;
+    if (!c->dl_pending) return KDTN_OK;
+    HIP_TRY(hipEventSynchronize(c->ev_dl_done));
+    c->dl_pending = false;
     return KDTN_OK;
 }
 

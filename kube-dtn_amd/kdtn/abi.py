@@ -201,7 +201,8 @@ EXPORTS = ["kdtn_version", "kdtn_strerror", "kdtn_err_name", "kdtn_init", "kdtn_
            "kdtn_comm_set_ranks", "kdtn_pods_export", "kdtn_pods_import", "kdtn_json_ingest_shard",
            "kdtn_ingest_shard_topos", "kdtn_epoch_remote_encode", "kdtn_epoch_download_remote",
            "kdtn_epoch_commit", "kdtn_epoch_upload_delta", "kdtn_epoch_tables_info",
-           "kdtn_vni_ops_export", "kdtn_vni_ops_import", "kdtn_json_ingest_delta"]
+           "kdtn_vni_ops_export", "kdtn_vni_ops_import", "kdtn_json_ingest_delta",
+           "kdtn_epoch_download_async", "kdtn_epoch_download_wait"]
 
 
 def ptr(a: np.ndarray, t):

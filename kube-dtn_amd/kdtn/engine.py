@@ -112,6 +112,8 @@ def lib() -> C.CDLL:
         "kdtn_epoch_tables_info": (C.c_int, [vp, C.POINTER(abi.IngestInfo)]),
         "kdtn_epoch_download_remote": (C.c_int, [vp, C.POINTER(abi.RemotePods)]),
         "kdtn_json_ingest_delta": (C.c_int, [vp, vp, C.c_uint32, C.POINTER(abi.VniTable), C.POINTER(abi.IngestInfo)]),
+        "kdtn_epoch_download_async": (C.c_int, [vp, C.POINTER(abi.Batches)]),
+        "kdtn_epoch_download_wait": (C.c_int, [vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -400,6 +402,21 @@ class Engine:
         b = out.to_c((len(out.del_idx), len(out.add_idx), len(out.upd_idx)))
         _check(lib().kdtn_epoch_download(self._ctx, C.byref(b)), "kdtn_epoch_download")
         return out.trim(b.n_del, b.n_add, b.n_upd)
+
+    def download_async(self, into: BatchesOut) -> BatchesOut:
+        """kdtn_epoch_download_async into page-locked `into` (BatchesOut.alloc(pinned=True)):
+        returns the trimmed view at once; its arrays hold the outputs after download_wait()."""
+        T = self._T
+        if len(into.action) != T or len(into.del_off) != T + 1:
+            raise ValueError(f"download_async(into=...): buffers sized for {len(into.action)} topologies, "
+                             f"the epoch has {T}")
+        b = into.to_c((len(into.del_idx), len(into.add_idx), len(into.upd_idx)))
+        self._dl_keep = b
+        _check(lib().kdtn_epoch_download_async(self._ctx, C.byref(b)), "kdtn_epoch_download_async")
+        return into.trim(b.n_del, b.n_add, b.n_upd)
+
+    def download_wait(self) -> None:
+        _check(lib().kdtn_epoch_download_wait(self._ctx), "kdtn_epoch_download_wait")
 
     def reconcile(self, inp: EpochInput, stages: int = abi.STAGE_ALL) -> BatchesOut:
         """Reconcile gate + CalcDiff + resolve + MakeQdiscs over every topology of `inp`."""

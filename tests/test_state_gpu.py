@@ -236,3 +236,37 @@ def test_delta_inline_record_referenced_twice():
         want = apply_delta(state, d)
         assert not same_tables(eng.tables(), want)
         _run_same(eng, want, "inline record referenced three times")
+
+
+def test_async_download_pipelined_chain():
+    """kdtn_epoch_download_async overlapping the next delta upload: every epoch's outputs, read
+    after download_wait, equal the oracle's, while the next epoch's upload and run go on."""
+    from kdtn.tables import BatchesOut
+    cs = synth.ChurnSequence(total_pods=5000)
+    prev = cs.epoch_input(copy=True)
+    with Engine(device=0, tick_in_usec=TICK) as eng:
+        eng.upload(prev)
+        eng.run()
+        eng.sync()
+        T = prev.topos.n
+        bufs = [BatchesOut.alloc(T, prev.desired.n, prev.desired.n, prev.desired.n, pinned=True) for _ in range(2)]
+        pend = (eng.download_async(bufs[0]), O.reconcile(prev, tick=TICK))
+        eng.commit(np.ones(T, np.uint8))
+        state = commit(prev, np.ones(T, bool))
+        for ep in range(1, 6):
+            cs.advance()
+            new = cs.epoch_input(copy=True)
+            d = build_delta(state, new, state.kdict.n, state.pdict.n)
+            eng.upload_delta(d)                   # beside the previous epoch's copies
+            state = apply_delta(state, d)
+            eng.run()
+            eng.sync()
+            eng.download_wait()
+            got, want = pend
+            assert not got.mismatches(want), f"epoch {ep - 1}: {got.mismatches(want)}"
+            pend = (eng.download_async(bufs[ep % 2]), O.reconcile(state, tick=TICK))
+            eng.commit(np.ones(T, np.uint8))
+            state = commit(state, np.ones(T, bool))
+        eng.download_wait()
+        got, want = pend
+        assert not got.mismatches(want)
