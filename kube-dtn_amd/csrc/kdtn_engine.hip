@@ -140,7 +140,7 @@ struct kdtn_ctx {
     DevBuf st_cnt, st_len, st_base, st_mode, st_flags, st_off64, st_part, st_off32, st_mask, st_chg;
     DevBuf dl_topo, dl_src, dl_netns, dl_nil, dl_off, dl_ref, dl_rows;
     // delta with a topology-set change: the map, created rows' names, the realised plan
-    DevBuf dl_prev, dl_ns, dl_name, dl_dest, st_rlen, st_rbase, st_roff64, st_rpart, st_roff32, st_seen;
+    DevBuf dl_prev, dl_ns, dl_name, dl_dest, dl_pack, st_rlen, st_rbase, st_roff64, st_rpart, st_roff32, st_seen;
     // incremental CR ingest (kdtn_json_ingest_delta): the document's scratch tables and local
     // dictionaries, the id maps into the resident dictionaries, the topology-key match
     DevBuf ji_ns, ji_name, ji_src, ji_netns, ji_flags, ji_roff, ji_noff, ji_kb, ji_ko, ji_pb, ji_po;
@@ -881,7 +881,7 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->dl_off, &c->dl_ref, &c->dl_rec.buf, &c->stage, &c->vx_cnt, &c->vx_send, &c->vx_recv,
                       &c->vx_gops, &c->pd_send, &c->pd_recv, &c->pd_cnt, &c->dl_rows, &c->vx_flag,
                       &c->vx_dkeys, &c->vx_dused, &c->vx_cpos, &c->vx_cpart, &c->vx_cnode, &c->vx_cvni,
-                      &c->dl_prev, &c->dl_ns, &c->dl_name, &c->dl_dest, &c->st_rlen, &c->st_rbase, &c->st_roff64,
+                      &c->dl_prev, &c->dl_ns, &c->dl_name, &c->dl_dest, &c->dl_pack, &c->st_rlen, &c->st_rbase, &c->st_roff64,
                       &c->st_rpart, &c->st_roff32, &c->st_seen, &c->ji_ns, &c->ji_name, &c->ji_src, &c->ji_netns,
                       &c->ji_flags, &c->ji_roff, &c->ji_noff, &c->ji_kb, &c->ji_ko, &c->ji_pb, &c->ji_po,
                       &c->ji_des.buf, &c->ji_real.buf, &c->ji_kmap, &c->ji_pmap, &c->ji_miss, &c->ji_mlen,
@@ -2857,6 +2857,25 @@ int kdtn_last_kernel_times(kdtn_ctx* c, const char** names, float* ms, int cap) 
 
 namespace {
 
+// Device layout of a delta's arrays (and the host layout that lets them travel in one copy,
+// kdtn.engine.pin_delta): topo, src_ip, net_ns, des_off, [prev, ns, name], spec_nil, then the
+// references 4-B aligned.
+struct DeltaPack {
+    size_t topo, src, netns, off, prev, ns, name, nil, ref, total;
+    DeltaPack(uint32_t n, uint32_t nref, uint32_t remap_T) {
+        topo = 0;
+        src = topo + (size_t)n * 4;
+        netns = src + (size_t)n * 4;
+        off = netns + (size_t)n * 4;
+        prev = off + (n ? ((size_t)n + 1) * 4 : 0);
+        ns = prev + (size_t)remap_T * 4;
+        name = ns + (remap_T ? (size_t)n * 4 : 0);
+        nil = name + (remap_T ? (size_t)n * 4 : 0);
+        ref = align_up(nil + n, 4);
+        total = ref + (size_t)nref * 4;
+    }
+};
+
 // offsets of a store from per-topology lengths: u64 (off64[T] = total) and u32, no readback
 int scan_lengths(kdtn_ctx* c, DevBuf& len, uint32_t T, DevBuf& off64, DevBuf& part, DevBuf& off32) {
     hipStream_t s = c->stream;
@@ -3089,17 +3108,20 @@ int kdtn_epoch_upload_delta(kdtn_ctx* c, const kdtn_epoch_delta* d) {
     hipStream_t cs = c->copy_stream ? c->copy_stream : s;
     TRY(ensure(c->misc, 256));
     uint32_t* misc = dp<uint32_t>(c->misc);
-    TRY(ensure(c->dl_topo, (size_t)n * 4));
-    TRY(ensure(c->dl_src, (size_t)n * 4));
-    TRY(ensure(c->dl_netns, (size_t)n * 4));
-    TRY(ensure(c->dl_nil, (size_t)n));
-    TRY(ensure(c->dl_off, ((size_t)n + 1) * 4));
-    TRY(ensure(c->dl_ref, (size_t)nref * 4));
-    if (remap) {
-        TRY(ensure(c->dl_prev, (size_t)Tn * 4));
-        TRY(ensure(c->dl_ns, (size_t)n * 4));
-        TRY(ensure(c->dl_name, (size_t)n * 4));
-    }
+    // the delta's arrays in one device block (DeltaPack): a caller whose host arrays sit in the
+    // same layout (kdtn.engine.pin_delta) has them copied by one or two copies
+    const DeltaPack pk_{n, nref, remap ? Tn : 0u};
+    TRY(ensure(c->dl_pack, pk_.total + 64));
+    uint8_t* pack = dp<uint8_t>(c->dl_pack);
+    uint32_t* p_topo = reinterpret_cast<uint32_t*>(pack + pk_.topo);
+    uint32_t* p_src = reinterpret_cast<uint32_t*>(pack + pk_.src);
+    uint32_t* p_netns = reinterpret_cast<uint32_t*>(pack + pk_.netns);
+    uint32_t* p_off = reinterpret_cast<uint32_t*>(pack + pk_.off);
+    uint32_t* p_prev = reinterpret_cast<uint32_t*>(pack + pk_.prev);
+    uint32_t* p_ns = reinterpret_cast<uint32_t*>(pack + pk_.ns);
+    uint32_t* p_name = reinterpret_cast<uint32_t*>(pack + pk_.name);
+    uint8_t* p_nil = pack + pk_.nil;
+    uint32_t* p_ref = reinterpret_cast<uint32_t*>(pack + pk_.ref);
     TRY(link_store_alloc(c, c->dl_rec, nr));
     const size_t col = (size_t)nr * 4, uid_at = align_up(col * LINK_COLS32, 8);
     TRY(ensure(c->stage, uid_at + (size_t)nr * 8 + 128));
@@ -3121,24 +3143,31 @@ int kdtn_epoch_upload_delta(kdtn_ctx* c, const kdtn_epoch_delta* d) {
     TRY(link_store_alloc(c, c->sh_des, (uint32_t)nbound));
     if (remap) TRY(link_store_alloc(c, c->sh_real, M0));
     // --- copies (copy stream), after everything already queued on the context stream
-    auto h2d = [&](DevBuf& b, const void* src, size_t bytes) -> int {
-        if (bytes) HIP_TRY(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, cs));
-        return KDTN_OK;
-    };
     HIP_TRY(hipEventRecord(c->ev_cp[0], s));
     if (cs != s) HIP_TRY(hipStreamWaitEvent(cs, c->ev_cp[0], 0));
-    TRY(h2d(c->dl_topo, d->topo, (size_t)n * 4));
-    TRY(h2d(c->dl_src, d->src_ip, (size_t)n * 4));
-    TRY(h2d(c->dl_netns, d->net_ns, (size_t)n * 4));
-    TRY(h2d(c->dl_nil, d->spec_nil, (size_t)n));
-    TRY(h2d(c->dl_off, d->des_off, n ? ((size_t)n + 1) * 4 : 0));
-    if (remap) {
-        TRY(h2d(c->dl_prev, d->prev, (size_t)Tn * 4));
-        TRY(h2d(c->dl_ns, d->ns, (size_t)n * 4));
-        TRY(h2d(c->dl_name, d->name, (size_t)n * 4));
+    {   // segments in pack order; host-adjacent neighbours merge into one copy
+        const void* src[9] = {d->topo, d->src_ip, d->net_ns, d->des_off, d->prev, d->ns, d->name, d->spec_nil, d->ref};
+        const size_t at[9] = {pk_.topo, pk_.src, pk_.netns, pk_.off, pk_.prev, pk_.ns, pk_.name, pk_.nil, pk_.ref};
+        const size_t len[9] = {(size_t)n * 4, (size_t)n * 4, (size_t)n * 4, pk_.prev - pk_.off, pk_.ns - pk_.prev,
+                               pk_.name - pk_.ns, pk_.nil - pk_.name, (size_t)n, (size_t)nref * 4};
+        int i = 0;
+        while (i < 9) {
+            if (!len[i]) { ++i; continue; }
+            const uint8_t* h0 = static_cast<const uint8_t*>(src[i]);
+            size_t bytes = len[i];
+            int j = i + 1;
+            // the device block is contiguous (padding included): the host array must sit at the
+            // same distance from the run's start
+            while (j < 9 && (!len[j] || static_cast<const uint8_t*>(src[j]) == h0 + (at[j] - at[i]))) {
+                if (len[j]) bytes = at[j] + len[j] - at[i];
+                ++j;
+            }
+            HIP_TRY(hipMemcpyAsync(pack + at[i], h0, bytes, hipMemcpyHostToDevice, cs));
+            if (i <= 7 && j > 7) HIP_TRY(hipEventRecord(c->ev_cp[1], cs));   // the small arrays are in
+            i = j;
+        }
+        if (!n) HIP_TRY(hipEventRecord(c->ev_cp[1], cs));
     }
-    HIP_TRY(hipEventRecord(c->ev_cp[1], cs));
-    TRY(h2d(c->dl_ref, d->ref, (size_t)nref * 4));
     HIP_TRY(hipEventRecord(c->ev_cp[2], cs));
     c->uploaded = false;                            // (restored below when the delta is rejected)
     const uint32_t saved[6] = {c->D, c->P, c->kd_valid, c->pd_valid, c->kd_from, c->pd_from};
@@ -3165,20 +3194,20 @@ int kdtn_epoch_upload_delta(kdtn_ctx* c, const kdtn_epoch_delta* d) {
         HIP_TRY(hipMemsetAsync(c->st_mask.p, ASM_SEG_A, (size_t)Tn + 16, s));
     }
     if (cs != s) HIP_TRY(hipStreamWaitEvent(s, c->ev_cp[1], 0));
-    if (n) k_delta_map<<<nblocks(n), BLOCK, 0, s>>>(dp<uint32_t>(c->dl_topo), n, Tn, dp<uint32_t>(c->st_chg));
+    if (n) k_delta_map<<<nblocks(n), BLOCK, 0, s>>>(p_topo, n, Tn, dp<uint32_t>(c->st_chg));
     if (cs != s) HIP_TRY(hipStreamWaitEvent(s, c->ev_cp[2], 0));
     {
-        DeltaCheckIn ci{dp<uint32_t>(c->dl_topo), dp<uint32_t>(c->dl_off), dp<uint8_t>(c->dl_nil),
-                        dp<uint32_t>(c->dl_src), dp<uint32_t>(c->dl_netns), dp<uint32_t>(c->dl_ref),
+        DeltaCheckIn ci{p_topo, p_off, p_nil,
+                        p_src, p_netns, p_ref,
                         dp<uint32_t>(c->kd_offs), dp<uint32_t>(c->pd_offs), n, nref, Tn, D, nr, N0,
                         kk, pk, d->kdict.offs[kk], d->pdict.offs[pk]};
         const uint32_t grid = std::max<uint32_t>({1u, nblocks(n), std::min<uint32_t>(nblocks(nref), 4 * c->n_cus)});
         k_delta_check<<<grid, BLOCK, 0, s>>>(ci, misc + MISC_DELTA_ERR);
     }
     // plan over the new topology table: new rows into scratch columns, the state is untouched
-    DeltaPlanIn pi{topo_view(c), dp<uint32_t>(c->st_chg), remap ? dp<uint32_t>(c->dl_prev) : nullptr,
-                   dp<uint32_t>(c->dl_off), dp<uint32_t>(c->dl_src), dp<uint32_t>(c->dl_netns), dp<uint8_t>(c->dl_nil),
-                   dp<uint32_t>(c->dl_ns), dp<uint32_t>(c->dl_name), Tn, D};
+    DeltaPlanIn pi{topo_view(c), dp<uint32_t>(c->st_chg), remap ? p_prev : nullptr,
+                   p_off, p_src, p_netns, p_nil,
+                   p_ns, p_name, Tn, D};
     DeltaPlanOut po{dp<uint32_t>(c->sh_ns), dp<uint32_t>(c->sh_name), dp<uint32_t>(c->sh_src),
                     dp<uint32_t>(c->sh_netns), dp<uint8_t>(c->sh_flags), dp<uint32_t>(c->st_len),
                     dp<uint32_t>(c->st_base), dp<uint8_t>(c->st_mode), dp<uint32_t>(c->st_rlen),
@@ -3191,7 +3220,7 @@ int kdtn_epoch_upload_delta(kdtn_ctx* c, const kdtn_epoch_delta* d) {
     const AsmGuard g{misc + MISC_DELTA_ERR, dp<uint64_t>(c->st_off64) + Tn, 1u};
     if (nbound)
         k_store_assemble<<<nblocks(nbound), BLOCK, 0, s>>>(dp<uint32_t>(c->st_off32), Tn, dp<uint32_t>(c->st_base),
-                                                           dp<uint8_t>(c->st_mode), dp<uint32_t>(c->dl_ref), c->des.view,
+                                                           dp<uint8_t>(c->st_mode), p_ref, c->des.view,
                                                            c->dl_rec.view, (uint32_t)nbound, g,
                                                            dp<uint32_t>(c->sh_des.buf));
     if (remap) {                                    // kept Topologies' status segments move with them
@@ -3204,8 +3233,8 @@ int kdtn_epoch_upload_delta(kdtn_ctx* c, const kdtn_epoch_delta* d) {
     }
     // the inline records' destinations, still before they have arrived
     if (nr && nref)
-        k_delta_dest<<<nblocks(nref), BLOCK, 0, s>>>(dp<uint32_t>(c->dl_off), dp<uint32_t>(c->dl_topo), n,
-                                                     dp<uint32_t>(c->dl_ref), nref, dp<uint32_t>(c->st_off32),
+        k_delta_dest<<<nblocks(nref), BLOCK, 0, s>>>(p_off, p_topo, n,
+                                                     p_ref, nref, dp<uint32_t>(c->st_off32),
                                                      misc + MISC_DELTA_ERR, dp<uint32_t>(c->dl_dest),
                                                      misc + MISC_DELTA_MULTI);
     if (cs != s) HIP_TRY(hipStreamWaitEvent(s, c->ev_cp[3], 0));
@@ -3247,8 +3276,8 @@ int kdtn_epoch_upload_delta(kdtn_ctx* c, const kdtn_epoch_delta* d) {
         k_soa_to_tiles<<<std::min<uint32_t>(nblocks(nr), 4 * c->n_cus), BLOCK, 0, s>>>(
             reinterpret_cast<const uint32_t*>(st), reinterpret_cast<const int64_t*>(st + uid_at), nr,
             dp<uint32_t>(c->dl_rec.buf), colmax);
-        k_delta_inline<<<nblocks(nref), BLOCK, 0, s>>>(dp<uint32_t>(c->dl_off), dp<uint32_t>(c->dl_topo), n,
-                                                       dp<uint32_t>(c->dl_ref), nref, dp<uint32_t>(c->st_off32),
+        k_delta_inline<<<nblocks(nref), BLOCK, 0, s>>>(p_off, p_topo, n,
+                                                       p_ref, nref, dp<uint32_t>(c->st_off32),
                                                        c->dl_rec.view, misc + MISC_DELTA_ERR,
                                                        dp<uint32_t>(c->sh_des.buf));
         HIP_TRY(hipGetLastError());

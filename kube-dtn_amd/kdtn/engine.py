@@ -163,20 +163,48 @@ def pin_input(inp: EpochInput) -> EpochInput:
     return out
 
 
+def delta_pack_layout(n: int, nref: int, remap_T: int) -> dict:
+    """Byte offsets of a delta's arrays in the engine's device block (kdtn_engine.hip
+    DeltaPack): arrays placed at these offsets in one host block travel in one copy."""
+    o = {"topo": 0, "src_ip": 4 * n, "net_ns": 8 * n, "des_off": 12 * n}
+    o["prev"] = o["des_off"] + (4 * (n + 1) if n else 0)
+    o["ns"] = o["prev"] + 4 * remap_T
+    o["name"] = o["ns"] + (4 * n if remap_T else 0)
+    o["spec_nil"] = o["name"] + (4 * n if remap_T else 0)
+    o["ref"] = (o["spec_nil"] + n + 3) // 4 * 4
+    o["total"] = o["ref"] + 4 * nref
+    return o
+
+
 def pin_delta(d):
-    """A kdtn.delta.Delta copied into page-locked host memory."""
+    """A kdtn.delta.Delta copied into page-locked host memory; its per-Topology arrays and
+    references share one block in the engine's layout (delta_pack_layout)."""
     from dataclasses import replace
     from .tables import Links
     P = pinned_copy
     r = d.records
-    extra = {} if d.prev is None else {"prev": P(d.prev), "ns": P(d.ns), "name": P(d.name)}
+    n, nref = d.n_changed, len(d.ref)
+    remap_T = 0 if d.prev is None else len(d.prev)
+    lay = delta_pack_layout(n, nref, remap_T)
+    block = pinned_empty((max(lay["total"], 1),), np.uint8)
+    arrs = {}
+    for f, dt in (("topo", np.uint32), ("src_ip", np.uint32), ("net_ns", np.uint32), ("des_off", np.uint32),
+                  ("prev", np.uint32), ("ns", np.uint32), ("name", np.uint32), ("spec_nil", np.uint8),
+                  ("ref", np.uint32)):
+        a = getattr(d, f)
+        if a is None:
+            continue
+        a = np.ascontiguousarray(a, dt)
+        view = block[lay[f]:lay[f] + a.nbytes].view(dt)
+        view[...] = a
+        arrs[f] = view
     v = d.vnis
     vn = v if v.resident else Vnis(P(v.node), P(v.vni), P(v.net_ns))
-    return replace(d, kdict=StrTab(P(d.kdict.bytes_), P(d.kdict.offs)), pdict=StrTab(P(d.pdict.bytes_), P(d.pdict.offs)),
-                   topo=P(d.topo), src_ip=P(d.src_ip), net_ns=P(d.net_ns), spec_nil=P(d.spec_nil),
-                   des_off=P(d.des_off), ref=P(d.ref), vnis=vn,
-                   records=Links(P(np.ascontiguousarray(r.key)), P(r.uid), P(np.ascontiguousarray(r.prop)), P(r.gap)),
-                   **extra)
+    out = replace(d, kdict=StrTab(P(d.kdict.bytes_), P(d.kdict.offs)), pdict=StrTab(P(d.pdict.bytes_), P(d.pdict.offs)),
+                  vnis=vn, records=Links(P(np.ascontiguousarray(r.key)), P(r.uid), P(np.ascontiguousarray(r.prop)),
+                                         P(r.gap)), **arrs)
+    out._block = block
+    return out
 
 
 def topology_shard(namespace, name, nshards: int) -> int:

@@ -12,6 +12,7 @@ import oracle as O
 from helpers import random_epoch
 from kdtn import Engine, abi, synth
 from kdtn.delta import build_delta
+from kdtn.engine import pin_delta
 from kdtn.model import pack
 from kdtn.tables import EpochInput, Interner, Topos
 from state import apply_delta, commit, predicted_commit, same_tables
@@ -95,7 +96,7 @@ def test_resident_churn_chain(pods):
             new = cs.epoch_input(copy=True)
             d = build_delta(state, new, state.kdict.n, state.pdict.n)
             moved += d.upload_bytes()
-            eng.upload_delta(d)
+            eng.upload_delta(pin_delta(d) if ep % 2 else d)      # (one host block: merged copies)
             state = apply_delta(state, d)
             assert not same_tables(eng.tables(), state), ep
             ora = _run_same(eng, state, f"epoch {ep}")

@@ -68,6 +68,23 @@ with Engine(device=0) as eng:
             eng.sync()
             tot.append(time.perf_counter() - t)
         res[f"L{level}"] = {"ms_epoch": sorted(tot)[len(tot) // 2] * 1e3, "kernels_ms": eng.kernel_times() if level else {}}
+    # the same rank epoch with its dictionaries resident and parsed (kdict_keep / pdict_keep =
+    # every string: a controller's steady state over append-only interners)
+    eng.upload(sh, sh.kdict.n, sh.pdict.n)
+    eng.pods_import(rows)
+    for level in (2, 0):
+        eng.set_timing(level)
+        for _ in range(3):
+            eng.run()
+            eng.sync()
+        tot = []
+        for _ in range(a.reps):
+            t = time.perf_counter()
+            eng.run()
+            eng.sync()
+            tot.append(time.perf_counter() - t)
+        res[f"parsed_L{level}"] = {"ms_epoch": sorted(tot)[len(tot) // 2] * 1e3,
+                                   "kernels_ms": eng.kernel_times() if level else {}}
     ms = res["L0"]["ms_epoch"]
     res["projected_links_per_s_at_N"] = a.pods * 10 / (ms * 1e-3)
     res["note"] = ("rank epoch without the RCCL all-gather wait (rows imported once); links_per_s projected as "
