@@ -166,6 +166,8 @@ struct kdtn_ctx {
     uint32_t j_kcap = 0, j_pcap = 0;   // intern table sizes that fit the last document
     DevBuf j_toks, j_par, j_role, j_ecls, j_odep, j_ord, j_tagg, j_gagg, j_cnt3, j_coff3, j_small, j_part;
     DevBuf j_tflags, j_owner, j_vown, j_kslots, j_krep, j_pslots, j_prep, j_heap;
+    DevBuf j_kkeys, j_pkeys;     // dense key words of the intern tables
+    DevBuf j_rows;               // row-major staging of the decoded link records (JS_ROW words each)
     DevBuf j_bits, j_bcnt, j_wrank, j_kslot_id, j_pslot_id, j_len, j_off64;
     uint64_t j_n = 0;
     uint32_t j_nb = 0;
@@ -719,7 +721,7 @@ int prepare_epoch(kdtn_ctx* c, const kdtn_vni_table& vn, uint32_t slice, uint32_
 
 // Which batch entries the daemons reach (k_reach; include/kdtn.h): c->f_send (add) and
 // c->f_reach_upd (update) flags of the last run; stamps destination daemons into `mark`.
-int run_reach(kdtn_ctx* c, uint32_t* mark, uint32_t stamp) {
+int run_reach(kdtn_ctx* c, uint32_t* mark, uint32_t stamp, uint32_t* nlist = nullptr) {
     const uint32_t nu = c->h_misc[2], na = c->h_misc[3];
     TRY(ensure(c->f_send, (size_t)na + 16));
     TRY(ensure(c->f_reach_upd, (size_t)nu + 16));
@@ -736,7 +738,7 @@ int run_reach(kdtn_ctx* c, uint32_t* mark, uint32_t stamp) {
                                                                                     dp<uint8_t>(c->f_st));
         if ((uint64_t)na + nu)
             k_reach<<<nblocks((uint64_t)na + nu), BLOCK, 0, c->stream>>>(r, na, nu, cut, dp<uint8_t>(c->f_st), mark,
-                                                                         dp<uint8_t>(c->f_send),
+                                                                         nlist, dp<uint8_t>(c->f_send),
                                                                          dp<uint8_t>(c->f_reach_upd));
     }
     return KDTN_OK;
@@ -866,7 +868,7 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->j_doc, &c->j_q, &c->j_bs, &c->j_hb, &c->j_qcnt, &c->j_qoff, &c->j_tok, &c->j_open,
                       &c->j_close, &c->j_tcnt, &c->j_dcnt, &c->j_toff, &c->j_doff, &c->j_toks, &c->j_par,
                       &c->j_role, &c->j_ecls, &c->j_odep, &c->j_ord, &c->j_tagg, &c->j_gagg, &c->j_cnt3, &c->j_coff3, &c->j_small,
-                      &c->j_part, &c->j_tflags, &c->j_owner, &c->j_vown, &c->j_kslots, &c->j_krep,
+                      &c->j_part, &c->j_tflags, &c->j_owner, &c->j_rows, &c->j_kkeys, &c->j_pkeys, &c->j_vown, &c->j_kslots, &c->j_krep,
                       &c->j_pslots, &c->j_prep, &c->j_heap, &c->j_bits, &c->j_bcnt, &c->j_wrank,
                       &c->j_kslot_id, &c->j_pslot_id, &c->j_len, &c->j_off64, &c->j_ocnt, &c->j_ooff,
                       &c->j_olist, &c->j_ccnt, &c->j_coff, &c->j_vlist, &c->sh_keep, &c->sh_kreal,
@@ -1620,20 +1622,18 @@ int fanout_compute(kdtn_ctx* c) {
         c->f_stamp = 1;
     }
     const uint32_t nchunks = nblocks(na, FAN_CHUNK);
-    const uint32_t nbd = nblocks(D, SCAN_CHUNK);
     TRY(ensure(c->f_node_idx, (size_t)D * 4));
     TRY(ensure(c->f_nodes, (size_t)FAN_NODE_CAP * 4 + 16));
-    TRY(ensure(c->f_part, (size_t)nbd * 8 + 16));
+    TRY(ensure(c->f_part, ((size_t)FAN_NODE_CAP + 1) * 4 + 16));      // the node list
     TRY(ensure(c->f_idx, (size_t)na * 4 + 16));
     TRY(ensure(c->f_inv, (size_t)na * 4 + 16));
     uint32_t* misc = dp<uint32_t>(c->misc);
     uint32_t* n_nodes = misc + MISC_FAN_NODES;
     FanIn f{dp<uint32_t>(c->add_off), dp<uint4>(c->add_res), dp<uint2>(c->add_qdisc), c->T, na, c->f_stamp};
-    TRY(run_reach(c, dp<uint32_t>(c->f_mark), c->f_stamp));
-    k_fan_nodes_count<<<nbd, BLOCK, 0, s>>>(dp<uint32_t>(c->f_mark), D, c->f_stamp, dp<uint64_t>(c->f_part));
-    k_scan_top<<<1, SCAN_TOP_BLOCK, 0, s>>>(dp<uint64_t>(c->f_part), nbd);
-    k_fan_nodes_write<<<nbd, BLOCK, 0, s>>>(dp<uint32_t>(c->f_mark), D, c->f_stamp, dp<uint64_t>(c->f_part),
-                                           dp<uint32_t>(c->f_node_idx), dp<uint32_t>(c->f_nodes), n_nodes);
+    uint32_t* nlist = dp<uint32_t>(c->f_part);
+    HIP_TRY(hipMemsetAsync(nlist, 0, 4, s));
+    TRY(run_reach(c, dp<uint32_t>(c->f_mark), c->f_stamp, nlist));
+    k_fan_nodes_sort<<<1, 1024, 0, s>>>(nlist, dp<uint32_t>(c->f_node_idx), dp<uint32_t>(c->f_nodes), n_nodes);
     timer_mark(c, "fanout_nodes");
     uint32_t nn = 0;
     HIP_TRY(hipMemcpyAsync(&nn, n_nodes, 4, hipMemcpyDeviceToHost, s));
@@ -2159,8 +2159,13 @@ static int json_decode(kdtn_ctx* c, const JsTargets& tg, JsCounts* o, kdtn_inges
     k_js_elems_write<<<ntiles, BLOCK, 0, s>>>(dp<uint8_t>(c->j_ecls), ntok, dp<uint64_t>(c->j_coff3), ntiles, ord, to);
     HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(to.real_off + T), (int)M, 1, s));
     HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(to.des_off + T), (int)N, 1, s));
-    JsStore des{dp<uint32_t>(tg.des->buf)};
-    JsStore real{dp<uint32_t>(tg.real->buf)};
+    // the values land in row-major staging (one record's 88 B written by the wave that decodes
+    // it), whole tiles per side so the finalize pass reads full tiles; it writes the AoSoA tiles
+    const uint64_t des_tiles = ((uint64_t)N + TILE_RECS - 1) / TILE_RECS, real_tiles = ((uint64_t)M + TILE_RECS - 1) / TILE_RECS;
+    const size_t rows_bytes = (size_t)(des_tiles + real_tiles) * TILE_WORDS * 4;
+    TRY(ensure(c->j_rows, std::max<size_t>(rows_bytes, 16)));
+    JsStore des{dp<uint32_t>(c->j_rows)};
+    JsStore real{dp<uint32_t>(c->j_rows) + (size_t)des_tiles * TILE_WORDS};
 
     // 5. schema values + interning; a table or heap that fills up is grown and the pass rerun
     uint32_t kcap = std::max(c->j_kcap, next_pow2(std::max<uint64_t>(1024, 2ull * ((uint64_t)N + M) + 4ull * T)));
@@ -2168,14 +2173,18 @@ static int json_decode(kdtn_ctx* c, const JsTargets& tg, JsCounts* o, kdtn_inges
     uint64_t hcap = std::max<uint64_t>(1 << 20, c->j_n / 16);
     JsIntern in{};
     for (int attempt = 0;; ++attempt) {
-        TRY(ensure(c->j_kslots, (size_t)kcap * 8));
+        TRY(ensure(c->j_kslots, (size_t)kcap * sizeof(JsSlot)));
         TRY(ensure(c->j_krep, (size_t)kcap * 4));
-        TRY(ensure(c->j_pslots, (size_t)pcap * 8));
+        TRY(ensure(c->j_pslots, (size_t)pcap * sizeof(JsSlot)));
         TRY(ensure(c->j_prep, (size_t)pcap * 4));
         TRY(ensure(c->j_heap, (size_t)hcap + 64));
-        HIP_TRY(hipMemsetAsync(c->j_kslots.p, 0, (size_t)kcap * 8, s));
+        TRY(ensure(c->j_kkeys, (size_t)kcap * 8));
+        TRY(ensure(c->j_pkeys, (size_t)pcap * 8));
+        HIP_TRY(hipMemsetAsync(c->j_kslots.p, 0, (size_t)kcap * sizeof(JsSlot), s));
+        HIP_TRY(hipMemsetAsync(c->j_kkeys.p, 0, (size_t)kcap * 8, s));
+        HIP_TRY(hipMemsetAsync(c->j_pkeys.p, 0, (size_t)pcap * 8, s));
         HIP_TRY(hipMemsetAsync(c->j_krep.p, 0xFF, (size_t)kcap * 4, s));
-        HIP_TRY(hipMemsetAsync(c->j_pslots.p, 0, (size_t)pcap * 8, s));
+        HIP_TRY(hipMemsetAsync(c->j_pslots.p, 0, (size_t)pcap * sizeof(JsSlot), s));
         HIP_TRY(hipMemsetAsync(c->j_prep.p, 0xFF, (size_t)pcap * 4, s));
         HIP_TRY(hipMemsetAsync(small + 2, 0, J_SMALL - 16, s));
         HIP_TRY(hipMemsetAsync(small + 1, 0xFF, 8, s));
@@ -2183,8 +2192,7 @@ static int json_decode(kdtn_ctx* c, const JsTargets& tg, JsCounts* o, kdtn_inges
             HIP_TRY(hipMemsetAsync(b->p, 0, (size_t)T * 4, s));
         HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(to.flags), (int)(KDTN_TOPO_SPEC_NIL | KDTN_TOPO_STATUS_NIL),
                                   T, s));
-        HIP_TRY(hipMemsetAsync(tg.des->buf.p, 0, tg.des->buf.cap, s));
-        HIP_TRY(hipMemsetAsync(tg.real->buf.p, 0, tg.real->buf.cap, s));
+        if (rows_bytes) HIP_TRY(hipMemsetAsync(c->j_rows.p, 0, rows_bytes, s));   // absent fields: id 0, uid 0
         if (nval) HIP_TRY(hipMemsetAsync(c->j_vown.p, 0xFF, (size_t)nval * 4, s));
         in.doc = j.doc;
         in.heap = dp<uint8_t>(c->j_heap);
@@ -2201,8 +2209,8 @@ static int json_decode(kdtn_ctx* c, const JsTargets& tg, JsCounts* o, kdtn_inges
 #else
         in.variant = 0;
 #endif
-        in.kd = JsDict{dp<unsigned long long>(c->j_kslots), dp<uint32_t>(c->j_krep), kcap - 1};
-        in.pd = JsDict{dp<unsigned long long>(c->j_pslots), dp<uint32_t>(c->j_prep), pcap - 1};
+        in.kd = JsDict{dp<JsSlot>(c->j_kslots), dp<unsigned long long>(c->j_kkeys), dp<uint32_t>(c->j_krep), kcap - 1};
+        in.pd = JsDict{dp<JsSlot>(c->j_pslots), dp<unsigned long long>(c->j_pkeys), dp<uint32_t>(c->j_prep), pcap - 1};
         if (nval)
             k_js_values<<<nblocks(nval), BLOCK, 0, s>>>(j, toks, dp<uint32_t>(c->j_vlist), nval, par, role, ord, to,
                                                         des, real, in, small + 1);
@@ -2238,11 +2246,10 @@ static int json_decode(kdtn_ctx* c, const JsTargets& tg, JsCounts* o, kdtn_inges
     // keep the intern tables at most half full for the next document of this shape
     c->j_kcap = std::max(kcap, next_pow2(2ull * D));
     c->j_pcap = std::max(pcap, next_pow2(2ull * P));
-    constexpr uint32_t IDW = (KDTN_NKEY + KDTN_NPROP) * TILE_RECS;
-    if (N) k_js_finalize_links<<<nblocks((uint64_t)(N + TILE_RECS - 1) / TILE_RECS * IDW), BLOCK, 0, s>>>(
-        des, N, dp<uint32_t>(c->j_kslot_id), dp<uint32_t>(c->j_pslot_id));
-    if (M) k_js_finalize_links<<<nblocks((uint64_t)(M + TILE_RECS - 1) / TILE_RECS * IDW), BLOCK, 0, s>>>(
-        real, M, dp<uint32_t>(c->j_kslot_id), dp<uint32_t>(c->j_pslot_id));
+    if (N) k_js_finalize_links<<<(uint32_t)des_tiles, BLOCK, 0, s>>>(des.base, dp<uint32_t>(tg.des->buf),
+                                                                       dp<uint32_t>(c->j_kslot_id), dp<uint32_t>(c->j_pslot_id));
+    if (M) k_js_finalize_links<<<(uint32_t)real_tiles, BLOCK, 0, s>>>(real.base, dp<uint32_t>(tg.real->buf),
+                                                                        dp<uint32_t>(c->j_kslot_id), dp<uint32_t>(c->j_pslot_id));
     if (T) k_js_finalize_topos<<<nblocks(T), BLOCK, 0, s>>>(to, T, dp<uint32_t>(c->j_kslot_id), dp<uint8_t>(*tg.flags));
     timer_mark(c, "js_intern");
     HIP_TRY(hipGetLastError());

@@ -1045,29 +1045,55 @@ KD_INLINE const uint8_t* key_bytes(const JsIntern& in, uint64_t kw) {
     return ((kw >> 56) & 1 ? in.heap : in.doc) + (uint32_t)kw;
 }
 
+// a zero byte among the first len (<= JS_INL) bytes of w: inline bytes not (yet) available
+KD_INLINE bool inline_has_zero(const uint32_t w[6], uint32_t len) {
+    bool z = false;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        const uint32_t lo = 4u * k;
+        const uint32_t m = len >= lo + 4 ? 0xFFFFFFFFu : len <= lo ? 0u : (1u << (8 * (len - lo))) - 1u;
+        z |= (((w[k] - 0x01010101u) & ~w[k] & 0x80808080u) & (m & 0x80808080u)) != 0;
+    }
+    return z;
+}
+
 // returns the table slot of the string [p, p+len) (len ≥ 1), or JS_NONE on overflow
 KD_INLINE uint32_t intern(const JsIntern& in, const JsDict& dt, const uint8_t* p, uint32_t len, uint64_t kw_self,
                           uint64_t h, uint32_t occ, const uint32_t (&pw)[8], bool have_pw) {
     const uint64_t tag = h >> 57;
     const uint64_t kw = (tag << 57) | kw_self;
+    const bool inl = have_pw && len <= JS_INL && !(KDTN_PROFILING && (in.variant & JSV_NO_INLINE));
     uint32_t s = (uint32_t)h & dt.mask;
     for (uint32_t probe = 0; probe <= dt.mask; ++probe) {
         // slots are written once (CAS from 0): a plain load is either that final key or a stale 0,
-        // and a stale 0 only sends us to the CAS, which returns the real key
-        unsigned long long cur = (KDTN_PROFILING && (in.variant & JSV_COHERENT)) ? __hip_atomic_load(dt.slots + s, __ATOMIC_RELAXED,
-                                                                                 __HIP_MEMORY_SCOPE_AGENT)
-                                                             : dt.slots[s];
+        // and a stale 0 only sends us to the CAS, which returns the real key. The key word and
+        // the inline bytes come from one 32-byte slot (two 16-B loads of one line).
+        const uint4 q0 = *reinterpret_cast<const uint4*>(dt.slots + s);
+        const uint4 q1 = *reinterpret_cast<const uint4*>(&dt.slots[s].b[2]);
+        unsigned long long cur = (KDTN_PROFILING && (in.variant & JSV_COHERENT))
+                                     ? __hip_atomic_load(&dt.slots[s].kw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                     : ((unsigned long long)q0.y << 32) | q0.x;
         if (cur == 0) {
             if ((kw >> 56) & 1) __threadfence();       // heap bytes visible before the key
-            cur = atomicCAS(dt.slots + s, 0ull, (unsigned long long)kw);
+            cur = atomicCAS(&dt.slots[s].kw, 0ull, (unsigned long long)kw);
             if (cur == 0) {
                 atomicMin(dt.rep + s, occ);
+                dt.keys[s] = kw;
+                if (inl && !inline_has_zero(pw, len)) {   // bytes past len stored as they are (ignored)
+                    *reinterpret_cast<uint2*>(&dt.slots[s].b[0]) = make_uint2(pw[0], pw[1]);
+                    *reinterpret_cast<uint4*>(&dt.slots[s].b[2]) = make_uint4(pw[2], pw[3], pw[4], pw[5]);
+                }
                 return s;
             }
         }
         if ((cur >> 57) == tag && ((cur >> 32) & 0xFFFFFFu) == len) {
             uint32_t k = 0;
-            if ((cur >> 56) & 1) {                    // heap bytes of another thread: coherent loads
+            const uint32_t ib[8] = {q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, 0u, 0u};
+            if (inl && !((cur >> 56) & 1) && !inline_has_zero(ib, len)) {
+                // the inserter's bytes, final (a string with a zero byte is never stored inline,
+                // a word not yet stored reads as zero): they decide equality
+                k = window_eq(pw, ib, len) ? len : 0u;
+            } else if ((cur >> 56) & 1) {             // heap bytes of another thread: coherent loads
                 const uint32_t off = (uint32_t)cur;
                 while (k < len) {
                     const uint32_t wd = __hip_atomic_load(reinterpret_cast<const uint32_t*>(in.heap) + ((off + k) >> 2),
@@ -1223,8 +1249,11 @@ KD_INLINE bool parse_uint32(const JsDoc& j, uint32_t pos, uint32_t* out) {
     return true;
 }
 
+// a record's word in the row-major staging: the wave decoding a link writes its 88 bytes, where
+// column-major tile stores put each 4-byte value in a line of its own, written back partially
+// by every XCD whose workgroups touched the tile
 KD_INLINE uint32_t* store_word(const JsStore& st, uint32_t rec, int col) {
-    return st.base + (size_t)(rec >> 6) * TILE_WORDS + col * TILE_RECS + (rec & 63u);
+    return st.base + (size_t)rec * JS_ROW + col;
 }
 
 __global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, const uint2* toks, const uint32_t* vlist, uint32_t nval,
@@ -1319,8 +1348,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, const uint2* toks,
             int64_t v;
             ok = kind == TK_SCALAR && parse_int64(j, t.x, &v);
             if (ok) {
-                uint32_t* w = store_word(st, rec, COL_UID) - (rec & 63u);        // i64 column of the tile
-                reinterpret_cast<int64_t*>(w)[rec & 63u] = v;
+                *reinterpret_cast<int64_t*>(store_word(st, rec, COL_UID)) = v;   // 8-B aligned (88-B rows)
             }
             break;
         }
@@ -1358,7 +1386,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_dups(const uint2* toks, const uint
 // ---------------------------------------------------------------- ids in first-occurrence order
 __global__ void __launch_bounds__(BLOCK) k_js_rep_mark(JsDict dt, uint32_t* bits) {
     const uint32_t s = blockIdx.x * BLOCK + threadIdx.x;
-    if (s > dt.mask || dt.slots[s] == 0) return;
+    if (s > dt.mask || dt.keys[s] == 0) return;
     const uint32_t occ = dt.rep[s];
     atomicOr(bits + (occ >> 5), 1u << (occ & 31));
 }
@@ -1373,7 +1401,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_ids(JsDict dt, const uint32_t* bit
                                                   uint32_t* slot_id, uint32_t* len_by_id) {
     const uint32_t s = blockIdx.x * BLOCK + threadIdx.x;
     if (s > dt.mask) return;
-    const unsigned long long kw = dt.slots[s];
+    const unsigned long long kw = dt.keys[s];
     if (kw == 0) return;
     const uint32_t occ = dt.rep[s];
     const uint32_t id = 1u + (uint32_t)wrank[occ >> 5] + __popc(bits[occ >> 5] & ((1u << (occ & 31)) - 1u));
@@ -1385,7 +1413,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_dict_copy(JsDict dt, JsIntern in, 
                                                         const uint64_t* off64, uint32_t* offs, uint8_t* arena) {
     const uint32_t s = blockIdx.x * BLOCK + threadIdx.x;
     if (s > dt.mask) return;
-    const unsigned long long kw = dt.slots[s];
+    const unsigned long long kw = dt.keys[s];
     if (kw == 0) return;
     const uint32_t id = slot_id[s];
     const uint32_t len = (uint32_t)(kw >> 32) & 0xFFFFFFu;
@@ -1403,17 +1431,29 @@ __global__ void __launch_bounds__(BLOCK) k_js_dict_copy(JsDict dt, JsIntern in, 
     for (uint32_t k = 0; k < len; ++k) arena[at + k] = src[k];
 }
 
-// slot + 1 → id in every id column; topology flags to bytes
-__global__ void __launch_bounds__(BLOCK) k_js_finalize_links(JsStore st, uint32_t n, const uint32_t* kslot_id,
-                                                             const uint32_t* pslot_id) {
-    constexpr uint32_t IDW = (KDTN_NKEY + KDTN_NPROP) * TILE_RECS;   // id words per tile
-    const uint64_t g = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-    const uint64_t tile = g / IDW;
-    const uint32_t r = (uint32_t)(g % IDW), col = r / TILE_RECS, lane = r % TILE_RECS;
-    if (tile * TILE_RECS + lane >= n) return;
-    uint32_t* w = st.base + tile * TILE_WORDS + r;
-    const uint32_t v = *w;
-    if (v) *w = (col < KDTN_NKEY ? kslot_id : pslot_id)[v - 1];
+// One workgroup per tile: the 64 staged rows (5.5 KB, read with 16-B loads) through LDS into
+// the tile's columns (coalesced stores), slot + 1 → id in the id columns (records past n are
+// zero rows, so the tail of the last tile is written too).
+__global__ void __launch_bounds__(BLOCK) k_js_finalize_links(const uint32_t* rows, uint32_t* tiles,
+                                                             const uint32_t* kslot_id, const uint32_t* pslot_id) {
+    __shared__ uint4 row4[TILE_WORDS / 4];
+    const uint32_t* row = reinterpret_cast<const uint32_t*>(row4);
+    const uint4* src = reinterpret_cast<const uint4*>(rows + (size_t)blockIdx.x * TILE_WORDS);
+    for (uint32_t k = threadIdx.x; k < TILE_WORDS / 4; k += BLOCK) row4[k] = src[k];
+    __syncthreads();
+    uint32_t* dst = tiles + (size_t)blockIdx.x * TILE_WORDS;
+    for (uint32_t k = threadIdx.x; k < TILE_WORDS; k += BLOCK) {
+        const uint32_t col = k / TILE_RECS, lane = k % TILE_RECS;
+        uint32_t v;
+        if (col < (uint32_t)LINK_COLS32) {
+            v = row[lane * JS_ROW + col];
+            if (col < (uint32_t)COL_GAP && v) v = (col < (uint32_t)COL_PROP0 ? kslot_id : pslot_id)[v - 1];
+        } else {                                    // the i64 uid column: record u / 2, word u % 2
+            const uint32_t u = k - LINK_COLS32 * TILE_RECS;
+            v = row[(u >> 1) * JS_ROW + LINK_COLS32 + (u & 1u)];
+        }
+        dst[k] = v;
+    }
 }
 
 __global__ void __launch_bounds__(BLOCK) k_js_finalize_topos(JsTopoOut to, uint32_t T, const uint32_t* kslot_id,

@@ -517,7 +517,7 @@ struct ReachIn {
 };
 __global__ void k_reach_cuts(ReachIn f, uint32_t nd, uint32_t na, uint32_t nu, uint32_t* cut, uint8_t* st_add);
 __global__ void k_reach(ReachIn f, uint32_t na, uint32_t nu, const uint32_t* cut, const uint8_t* st_add, uint32_t* mark,
-                        uint8_t* reach_add, uint8_t* reach_upd);
+                        uint32_t* nlist, uint8_t* reach_add, uint8_t* reach_upd);
 
 // VxlanManager state after the epoch (kdtn_vni.hip; include/kdtn.h kdtn_epoch_vni_apply)
 struct VniOpsIn {
@@ -551,9 +551,7 @@ __global__ void k_vni_contest(const uint4* add_ops, uint32_t n_ops, const uint4*
                               uint32_t dmask, uint32_t* flag);
 __global__ void k_vni_contest_write(const uint4* add_ops, const uint32_t* flag, const uint64_t* pos, uint32_t n_ops,
                                     uint32_t* node, int32_t* vni);
-__global__ void k_fan_nodes_count(const uint32_t* mark, uint32_t nd, uint32_t stamp, uint64_t* part);
-__global__ void k_fan_nodes_write(const uint32_t* mark, uint32_t nd, uint32_t stamp, const uint64_t* part,
-                                  uint32_t* node_idx, uint32_t* nodes, uint32_t* n_nodes);
+__global__ void k_fan_nodes_sort(const uint32_t* nlist, uint32_t* node_idx, uint32_t* nodes, uint32_t* n_nodes);
 __global__ void k_fan_count(FanIn f, const uint8_t* send, const uint32_t* node_idx, const uint32_t* n_nodes,
                             uint32_t* counts, uint32_t nchunks);
 __global__ void k_fan_scatter(FanIn f, const uint8_t* send, const uint32_t* node_idx, const uint32_t* n_nodes,
@@ -611,7 +609,7 @@ enum : uint32_t { R_NONE = 0, R_ROOT, R_ITEMS, R_ITEM, R_META, R_SPEC, R_STATUS,
                   R_LINK_S, R_LINK_R, R_PROPS_S, R_PROPS_R };
 constexpr uint32_t JS_ST_OVERFLOW = 1, JS_ST_LONG = 2;   // intern status bits
 // ingest variants (KDTN_JS_VARIANT, profiling build only; bits 1-3 give wrong tables)
-constexpr uint32_t JSV_COHERENT = 1, JSV_NO_SEEN = 2, JSV_NO_REP = 4, JSV_NO_INTERN = 8;
+constexpr uint32_t JSV_COHERENT = 1, JSV_NO_SEEN = 2, JSV_NO_REP = 4, JSV_NO_INTERN = 8, JSV_NO_INLINE = 16;
 
 struct JsDoc {
     const uint8_t* doc;        // padded with spaces to nb*64 (+64 B)
@@ -639,11 +637,29 @@ struct JsTopoOut {
     uint32_t* real_off;
     uint32_t* des_off;
 };
+// A decoded link record in the row-major staging: JS_ROW words in the tile's column order
+// (keys, properties, gap, then the i64 uid as two words); k_js_finalize_links transposes whole
+// tiles into the AoSoA store and maps the id columns' slot + 1 to the dictionary ids.
+constexpr int JS_ROW = LINK_COLS32 + 2;
+static_assert(JS_ROW * TILE_RECS == TILE_WORDS, "a staged tile is a store tile");
 struct JsStore {
-    uint32_t* base;            // AoSoA link store (DevLinks layout)
+    uint32_t* base;            // row-major staging, JS_ROW words per record, whole tiles
 };
+// An intern table slot (32 B, one per aligned quarter line): the key word (0 = empty) and, for
+// a document string of at most JS_INL bytes with no zero byte, its bytes, stored by the
+// inserting thread after its CAS. A repeated string compares against those bytes instead of
+// re-reading its first occurrence's window in the document (a random position). A slot whose
+// bytes are not stored yet reads as zeros (the table is cleared per decode), and no inline
+// string has a zero byte, so a zero byte within the length means "not available".
+constexpr uint32_t JS_INL = 24;
+struct JsSlot {
+    unsigned long long kw;
+    uint32_t b[6];
+};
+static_assert(sizeof(JsSlot) == 32, "32-byte slots");
 struct JsDict {
-    unsigned long long* slots; // key words, 0 = empty
+    JsSlot* slots;             // key words + inline bytes (the probes)
+    unsigned long long* keys;  // the key words again, dense (the per-slot passes after the decode)
     uint32_t* rep;             // first occurrence (token index) per slot
     uint32_t mask;
 };
@@ -688,7 +704,8 @@ __global__ void k_js_popc(const uint32_t* bits, uint32_t nw, uint32_t* cnt);
 __global__ void k_js_ids(JsDict dt, const uint32_t* bits, const uint64_t* wrank, uint32_t* slot_id, uint32_t* len_by_id);
 __global__ void k_js_dict_copy(JsDict dt, JsIntern in, const uint32_t* slot_id, const uint64_t* off64, uint32_t* offs,
                                uint8_t* arena);
-__global__ void k_js_finalize_links(JsStore st, uint32_t n, const uint32_t* kslot_id, const uint32_t* pslot_id);
+__global__ void k_js_finalize_links(const uint32_t* rows, uint32_t* tiles, const uint32_t* kslot_id,
+                                    const uint32_t* pslot_id);
 __global__ void k_js_finalize_topos(JsTopoOut to, uint32_t T, const uint32_t* kslot_id, uint8_t* flags8);
 
 // sharded ingest (kdtn_json_ingest_shard): keep[t] = this shard owns topology t; then the

@@ -11,6 +11,7 @@
 #     shard      one rank of N = 2 / 4 / 8 on this GPU (tools/shard_epoch.py); $SHARD_NS overrides
 #     ingest     config-2 ingest stage with kernel times (tools/ingest_run.py)
 #     ipmc       ingest FETCH_SIZE / WRITE_SIZE passes (tools/ingest_pmc_traffic.sh)
+#     iab        ingest A/B of profiling variants $IAB_VARIANTS (tools/ingest_ablate.py, default 0,16)
 #     stages     output-stage kernel times (tools/stage_run.py)
 #   default: tests,smoke,bench,stats,pmc
 # Every GPU step has its own time limit and the script stops at the first failure.
@@ -50,6 +51,10 @@ fi
 if has ingest; then
   timeout -k 10 400 python -u tools/ingest_run.py --pods 1000000 --doc /tmp/kdtn_doc_1000000.json > $OUT/ingest.json 2> $OUT/ingest.err
   tail -5 $OUT/ingest.json
+fi
+if has iab; then
+  timeout -k 10 500 python -u tools/ingest_ablate.py 1000000 ${IAB_VARIANTS:-0,16} > $OUT/ingest_ab.jsonl 2> $OUT/ingest_ab.err
+  cat $OUT/ingest_ab.jsonl
 fi
 if has stages; then
   timeout -k 10 400 python -u tools/stage_run.py > $OUT/stages.json 2> $OUT/stages.err
