@@ -2104,8 +2104,9 @@ static int json_decode(kdtn_ctx* c, const JsTargets& tg, JsCounts* o, kdtn_inges
     k_js_par_group<<<ng, BLOCK, 0, s>>>(dp<uint32_t>(c->j_tagg), ntiles, dp<uint32_t>(c->j_gagg));
     k_js_par_top<<<1, BLOCK, 0, s>>>(dp<uint32_t>(c->j_gagg), ng);
     k_js_par_tiles<<<ng, BLOCK, 0, s>>>(dp<uint32_t>(c->j_tagg), ntiles, dp<uint32_t>(c->j_gagg));
-    k_js_par_apply<<<ntiles, BLOCK, 0, s>>>(toks, ntok, dp<uint32_t>(c->j_tagg), par);
-    k_js_deep<<<nblocks(ntok), BLOCK, 0, s>>>(toks, ntok, par);
+    uint32_t* deep = reinterpret_cast<uint32_t*>(small + 4);   // zeroed with the small words above
+    k_js_par_apply<<<ntiles, BLOCK, 0, s>>>(toks, ntok, dp<uint32_t>(c->j_tagg), par, deep);
+    k_js_deep<<<std::min<uint32_t>(nblocks(ntok), 2048), BLOCK, 0, s>>>(toks, ntok, par, deep);
     timer_mark(c, "js_parents");
     k_js_validate<<<nblocks(ntok), BLOCK, 0, s>>>(j, toks, ntok, par, dp<uint8_t>(c->j_ecls), small);
     timer_mark(c, "js_validate");
@@ -2193,7 +2194,6 @@ static int json_decode(kdtn_ctx* c, const JsTargets& tg, JsCounts* o, kdtn_inges
         HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(to.flags), (int)(KDTN_TOPO_SPEC_NIL | KDTN_TOPO_STATUS_NIL),
                                   T, s));
         if (rows_bytes) HIP_TRY(hipMemsetAsync(c->j_rows.p, 0, rows_bytes, s));   // absent fields: id 0, uid 0
-        if (nval) HIP_TRY(hipMemsetAsync(c->j_vown.p, 0xFF, (size_t)nval * 4, s));
         in.doc = j.doc;
         in.heap = dp<uint8_t>(c->j_heap);
         in.heap_used = small + 2;

@@ -41,6 +41,26 @@ KD_INLINE uint32_t eqb(uint32_t w, uint32_t c) {                                
 KD_INLINE uint32_t ltb(uint32_t w, uint32_t n) {                                 // byte < n (n ≤ 128)
     return ~(((w & 0x7F7F7F7Fu) + (128u - n) * 0x01010101u) | w) & 0x80808080u;
 }
+KD_INLINE uint32_t digb(uint32_t w) { return ltb(w, 0x3Au) & ~ltb(w, 0x30u); }  // byte in '0'..'9'
+// bit k = byte k of a 32-byte register window is a decimal digit
+KD_INLINE uint32_t digit_mask(const uint32_t u[8]) {
+    uint32_t D = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) D |= mm4(digb(u[k])) << (4 * k);
+    return D;
+}
+// byte q (< 32, not a compile-time constant) of a register window
+KD_INLINE uint32_t win_byte_at(const uint32_t u[8], uint32_t q) {
+    const uint32_t i = q >> 2;
+    uint32_t w = u[0];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) w = i == (uint32_t)k ? u[k] : w;
+    return (w >> (8 * (q & 3u))) & 0xFFu;
+}
+// first non-digit byte at or after st (0 or 1) of the window: 32 when the rest is digits
+KD_INLINE uint32_t first_non_digit(uint32_t D, uint32_t st) {
+    return st + (uint32_t)__builtin_ctzll(~((uint64_t)D >> st));
+}
 KD_INLINE uint64_t prefix_xor(uint64_t x) {
     x ^= x << 1; x ^= x << 2; x ^= x << 4; x ^= x << 8; x ^= x << 16; x ^= x << 32;
     return x;
@@ -370,7 +390,7 @@ KD_INLINE uint32_t tpad(uint32_t l) { return l + l / JS_PER; }
 constexpr int JS_TPAD = JS_TILE + JS_TILE / JS_PER;
 
 __global__ void __launch_bounds__(BLOCK) k_js_par_apply(const uint2* toks, uint32_t ntok, const uint32_t* texcl,
-                                                        uint32_t* par) {
+                                                        uint32_t* par, uint32_t* deep) {
     __shared__ uint32_t wt[BLOCK / 64][JS_PD];
     __shared__ uint32_t st[BLOCK * (JS_PD + 1)];
     __shared__ uint32_t tm[JS_TPAD];              // token metas in, parents out
@@ -415,6 +435,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_par_apply(const uint2* toks, uint3
         for (uint32_t w = 0; w < wave; ++w) ex = max(ex, wt[w][d]);
         row[d] = max(ex, texcl[(size_t)blockIdx.x * JS_PD + d]);
     }
+    bool any_deep = false;
     for (int k = 0; k < JS_PER; ++k) {
         const uint32_t i = base + k;
         if (i >= ntok) break;
@@ -422,10 +443,11 @@ __global__ void __launch_bounds__(BLOCK) k_js_par_apply(const uint2* toks, uint3
         const uint32_t d = meta & TK_DEPTH_MASK;
         uint32_t p = JS_NONE;
         if (d >= 1 && d <= JS_PD) p = row[d - 1] - 1;          // 0 - 1 = JS_NONE (malformed)
-        else if (d > JS_PD) p = JS_DEEP;
+        else if (d > JS_PD) { p = JS_DEEP; any_deep = true; }
         mine[k] = p;
         if (tk_open(meta) && d < JS_PD) row[d] = i + 1;
     }
+    if (__ballot(any_deep) && (threadIdx.x & 63u) == 0) atomicOr(deep, 1u);   // k_js_deep has work
     __syncthreads();
     for (int q = 0; q < JS_PER; ++q) {            // coalesced write-out
         const uint32_t l = q * BLOCK + threadIdx.x;
@@ -433,17 +455,21 @@ __global__ void __launch_bounds__(BLOCK) k_js_par_apply(const uint2* toks, uint3
     }
 }
 
-// tokens nested deeper than JS_PD: nearest earlier token with a smaller pre-depth
-__global__ void __launch_bounds__(BLOCK) k_js_deep(const uint2* toks, uint32_t ntok, uint32_t* par) {
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= ntok || par[i] != JS_DEEP) return;
-    const uint32_t d = toks[i].y & TK_DEPTH_MASK;
-    uint32_t k = i;
-    while (k > 0) {
-        --k;
-        if ((toks[k].y & TK_DEPTH_MASK) < d) break;
+// tokens nested deeper than JS_PD: nearest earlier token with a smaller pre-depth. A small
+// grid-stride launch that returns at once when k_js_par_apply met no such token (the usual
+// document: reading every parent word for nothing cost a 2.4 GB pass)
+__global__ void __launch_bounds__(BLOCK) k_js_deep(const uint2* toks, uint32_t ntok, uint32_t* par, const uint32_t* deep) {
+    if (*deep == 0) return;
+    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < ntok; i += gridDim.x * BLOCK) {
+        if (par[i] != JS_DEEP) continue;
+        const uint32_t d = toks[i].y & TK_DEPTH_MASK;
+        uint32_t k = i;
+        while (k > 0) {
+            --k;
+            if ((toks[k].y & TK_DEPTH_MASK) < d) break;
+        }
+        par[i] = k;
     }
-    par[i] = k;
 }
 
 // ---------------------------------------------------------------- validation
@@ -536,6 +562,20 @@ KD_INLINE int valid_scalar_window(const JsDoc& j, uint32_t pos) {
     if (c0 == 't') return u[0] == 0x65757274u && term(b4);            // "true"
     if (c0 == 'f') return u[0] == 0x736c6166u && b4 == 'e' && term(b5); // "fals" "e"
     if (c0 == 'n') return u[0] == 0x6c6c756eu && term(b4);            // "null"
+    // Plain integers (the common scalar) from the window's digit mask: an optional '-', digits
+    // without a leading zero, a terminator. Every lane of a wave holding one scalar ran the
+    // byte DFA below; now only a fraction or an exponent ('.', 'e', 'E' after the digits) does.
+    {
+        const uint32_t st = c0 == '-' ? 1u : 0u;
+        const uint32_t p = first_non_digit(digit_mask(u), st);
+        if (p == st) return 0;                                          // no digit: not a number
+        if (p >= 32u) return -1;                                        // longer than the window
+        const uint32_t c = win_byte_at(u, p);
+        if (c != '.' && (c | 32u) != 'e') {
+            const bool lead0 = win_byte_at(u, st) == '0' && p > st + 1u;   // "0" then more digits
+            return (!lead0 && term(c)) ? 1 : 0;
+        }
+    }
     // 0 start, 1 after '-', 2 leading 0, 3 integer digits, 4 after '.', 5 fraction digits,
     // 6 after e/E, 7 after the exponent sign, 8 exponent digits
     uint32_t st = 0;
@@ -1062,7 +1102,11 @@ KD_INLINE uint32_t intern(const JsIntern& in, const JsDict& dt, const uint8_t* p
                           uint64_t h, uint32_t occ, const uint32_t (&pw)[8], bool have_pw) {
     const uint64_t tag = h >> 57;
     const uint64_t kw = (tag << 57) | kw_self;
-    const bool inl = have_pw && len <= JS_INL && !(KDTN_PROFILING && (in.variant & JSV_NO_INLINE));
+    bool inl = have_pw && len <= JS_INL;
+    if constexpr (KDTN_PROFILING != 0) {
+        const uint32_t off = in.variant & (JSV_NO_INLINE | (dt.slots == in.kd.slots ? JSV_NO_INLINE_K : JSV_NO_INLINE_P));
+        if (off) inl = false;
+    }
     uint32_t s = (uint32_t)h & dt.mask;
     for (uint32_t probe = 0; probe <= dt.mask; ++probe) {
         // slots are written once (CAS from 0): a plain load is either that final key or a stale 0,
@@ -1176,23 +1220,32 @@ KD_INLINE bool scalar_window(const JsDoc& j, uint32_t pos, uint64_t* v, uint32_t
     uint32_t u[8];
     load_window(j.doc, pos, u);
     *neg = (u[0] & 0xFFu) == '-';
-    uint64_t x = 0;
-    uint32_t n = 0;
-    bool done = false, b = false;
+    const uint32_t st = *neg ? 1u : 0u;
+    // the digits run from st to the first non-digit p (digit mask: no per-byte loop); p must be
+    // a terminator, anything else is a parse error like any non-digit before the terminator
+    const uint32_t p = first_non_digit(digit_mask(u), st);
+    if (p >= 32u) return false;                                         // no terminator in the window
+    const uint32_t c = win_byte_at(u, p);
+    bool b = !(c <= 0x20 || c == ',' || c == '}' || c == ']');
+    uint32_t w[8];                                                      // digit k at byte k
 #pragma unroll
-    for (int k = 0; k < (int)WIN; ++k) {
-        const uint32_t c = win_byte(u, k);
-        if (done || (k == 0 && *neg)) continue;
-        if (c <= 0x20 || c == ',' || c == '}' || c == ']') { done = true; continue; }
-        if (c - '0' >= 10u) b = true;
-        if (x > (~0ull - 9) / 10) b = true;
-        x = x * 10 + (c - '0');
-        ++n;
+    for (int k = 0; k < 7; ++k) w[k] = st ? __builtin_amdgcn_alignbyte(u[k + 1], u[k], 1) : u[k];
+    w[7] = st ? u[7] >> 8 : u[7];
+    const uint32_t n = p - st;
+    uint64_t x = 0;
+#pragma unroll
+    for (int k = 0; k < 20; ++k) {
+        if (!__ballot(k < (int)n)) break;                               // the wave's longest number
+        if (k < (int)n) {
+            if (x > (~0ull - 9) / 10) b = true;
+            x = x * 10 + (((w[k >> 2] >> (8 * (k & 3))) & 0xFFu) - '0');
+        }
     }
+    if (n > 20u) b = true;                                              // beyond 2^64 (and the loop)
     *v = x;
     *nd = n;
     *bad = b;
-    return done;
+    return true;
 }
 KD_INLINE bool parse_int64(const JsDoc& j, uint32_t pos, int64_t* out) {
     {
@@ -1266,13 +1319,15 @@ __global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, const uint2* toks,
     const uint2 t = toks[i];
     const uint32_t kpos = toks[i - 2].x;
     const uint32_t dv = tdepth(t);                     // members of root 1, item 3, meta/spec/status 4,
-    if (dv != 1 && dv != 3 && dv != 4 && dv != 6 && dv != 7) return;   // link 6, properties 7
+    // every member value gets its vown word here (JS_NONE: not a schema field), so the array
+    // needs no clearing pass
+    if (dv != 1 && dv != 3 && dv != 4 && dv != 6 && dv != 7) { in.vown[k] = JS_NONE; return; }   // link 6, props 7
     const uint32_t o = par[i];
-    if (o >= JS_DEEP) return;
+    if (o >= JS_DEEP) { in.vown[k] = JS_NONE; return; }
     const uint32_t r = role[o];
     const uint32_t po = par[o];                        // the grandparent, loaded with the role
     const KeyName kn = key_name(j, kpos);              // decoded while role[o] is in flight
-    if (r == R_NONE || r == R_ITEMS || r == R_SPEC_LINKS || r == R_STATUS_LINKS) return;
+    if (r == R_NONE || r == R_ITEMS || r == R_SPEC_LINKS || r == R_STATUS_LINKS) { in.vown[k] = JS_NONE; return; }
     const uint32_t kind = tkind(t);
     const bool null = kind == TK_SCALAR && j.doc[t.x] == 'n';
     int f, bit;
@@ -1313,7 +1368,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, const uint2* toks,
         break;
     }
     }
-    if (f < 0) return;
+    if (f < 0) { in.vown[k] = JS_NONE; return; }
     // a plain store of this member's token index; k_js_dups then flags every member whose
     // (object, field) slot another member overwrote (no atomics on the hot path)
     own += bit;

@@ -609,7 +609,8 @@ enum : uint32_t { R_NONE = 0, R_ROOT, R_ITEMS, R_ITEM, R_META, R_SPEC, R_STATUS,
                   R_LINK_S, R_LINK_R, R_PROPS_S, R_PROPS_R };
 constexpr uint32_t JS_ST_OVERFLOW = 1, JS_ST_LONG = 2;   // intern status bits
 // ingest variants (KDTN_JS_VARIANT, profiling build only; bits 1-3 give wrong tables)
-constexpr uint32_t JSV_COHERENT = 1, JSV_NO_SEEN = 2, JSV_NO_REP = 4, JSV_NO_INTERN = 8, JSV_NO_INLINE = 16;
+constexpr uint32_t JSV_COHERENT = 1, JSV_NO_SEEN = 2, JSV_NO_REP = 4, JSV_NO_INTERN = 8, JSV_NO_INLINE = 16,
+                   JSV_NO_INLINE_K = 32, JSV_NO_INLINE_P = 64;   // 16: neither dictionary, 32 / 64: keys / props
 
 struct JsDoc {
     const uint8_t* doc;        // padded with spaces to nb*64 (+64 B)
@@ -684,8 +685,8 @@ __global__ void k_js_par_agg(const uint2* toks, uint32_t ntok, uint32_t* tagg);
 __global__ void k_js_par_group(const uint32_t* tagg, uint32_t ntiles, uint32_t* gagg);
 __global__ void k_js_par_top(uint32_t* gagg, uint32_t ng);
 __global__ void k_js_par_tiles(uint32_t* tagg, uint32_t ntiles, const uint32_t* gagg);
-__global__ void k_js_par_apply(const uint2* toks, uint32_t ntok, const uint32_t* texcl, uint32_t* par);
-__global__ void k_js_deep(const uint2* toks, uint32_t ntok, uint32_t* par);
+__global__ void k_js_par_apply(const uint2* toks, uint32_t ntok, const uint32_t* texcl, uint32_t* par, uint32_t* deep);
+__global__ void k_js_deep(const uint2* toks, uint32_t ntok, uint32_t* par, const uint32_t* deep);
 __global__ void k_js_validate(JsDoc j, const uint2* toks, uint32_t ntok, const uint32_t* par, uint8_t* ecand,
                               unsigned long long* err);
 __global__ void k_js_roles(JsDoc j, const uint2* toks, const uint32_t* olist, uint32_t nopen, const uint32_t* par,

@@ -176,7 +176,11 @@ WIN_SCALARS = [b"0", b"-0", b"7", b"-12", b"0.5", b"-0.25e+3", b"1E9", b"1e-7", 
                b"1.25E+10", b"true", b"false", b"null", b"01", b"-", b"1.", b"1e", b"1e+", b".5", b"+1",
                b"-a", b"1.e3", b"1x", b"0x1", b"truex", b"fals", b"nul", b"nulll", b"tru", b"falsee",
                b"1" * 31, b"1" * 32, b"1" * 40, b"1." + b"5" * 35, b"1e" + b"9" * 33, b"-" + b"0" * 2,
-               b"00", b"1.5.2", b"1e5e5", b"1-2", b"NaN", b"Infinity"]
+               b"00", b"1.5.2", b"1e5e5", b"1-2", b"NaN", b"Infinity",
+               # integer fast paths (digit masks): int64 / uint64 edges, signs, leading zeros
+               b"-01", b"-0.0", b"0e0", b"9223372036854775807", b"-9223372036854775808", b"9223372036854775808",
+               b"-9223372036854775809", b"18446744073709551615", b"18446744073709551616", b"1" * 19, b"1" * 20,
+               b"1" * 21, b"-" + b"1" * 30, b"-" + b"1" * 31, b"4294967295", b"4294967296", b"--1", b"1a"]
 
 
 @pytest.mark.parametrize("sep", [b"", b" ", b"\t\n"])
@@ -186,6 +190,10 @@ def test_window_scalars(engine, sep):
             doc = (b'{"' + b"p" * pad + b'":[' + s + sep + b"]," + b'"q":"' + b"z" * 40 + b'",'
                    b'"items":[{"metadata":{"name":"a"},"spec":{"links":[{"uid":' + s + sep + b"}]}}]}")
             check_doc(engine, doc, f"scalar {s!r} pad {pad}")
+            doc = (b'{"' + b"p" * pad + b'":"' + b"z" * 40 + b'",'                      # gap: ParseUint32
+                   b'"items":[{"metadata":{"name":"a"},"spec":{"links":[{"uid":1,"properties":{"gap":' + s + sep +
+                   b"}}]}}]}")
+            check_doc(engine, doc, f"gap {s!r} pad {pad}")
 
 
 def test_window_strings(engine):

@@ -87,6 +87,22 @@ with Engine(device=0) as eng:
                                    "kernels_ms": eng.kernel_times() if level else {}}
     ms = res["L0"]["ms_epoch"]
     res["projected_links_per_s_at_N"] = a.pods * 10 / (ms * 1e-3)
+    # Estimated RCCL all-gather of the pod-status rows (not measured: one GPU here). It starts
+    # on the comm stream before the dictionary parses and is waited on only before the lookup
+    # tables, so the parses hide it up to their own time. Ring model: a fixed latency plus
+    # (N-1)/N of the gathered bytes at an assumed bus bandwidth (two assumptions bracket it).
+    kt = res["L2"]["kernels_ms"]
+    hidden_us = (kt.get("kdict_parse", 0.0) + kt.get("pdict_parse", 0.0) + kt.get("pods_fill", 0.0)) * 1e3
+    gathered = 16 * a.nshards * slice_
+    est = {"bytes": gathered, "model": "ring all-gather: 15 us + bytes * (N-1)/N / bus bandwidth (assumed)",
+           "hidden_under_parses_us": round(hidden_us, 1)}
+    for bw in (150, 300):
+        us = 15.0 + gathered * (a.nshards - 1) / a.nshards / (bw * 1e9) * 1e6
+        exposed = max(0.0, us - hidden_us)
+        est[f"at_{bw}GBps"] = {"allgather_us": round(us, 1), "exposed_us": round(exposed, 1),
+                               "rank_epoch_ms": round(ms + exposed * 1e-3, 4),
+                               "links_per_s": a.pods * 10 / ((ms + exposed * 1e-3) * 1e-3)}
+    res["allgather_estimate"] = est
     res["note"] = ("rank epoch without the RCCL all-gather wait (rows imported once); links_per_s projected as "
                    "10 links per pod over the rank's epoch")
 print(json.dumps(res), flush=True)
