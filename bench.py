@@ -819,10 +819,10 @@ def main():
     if churn and world == 1 and not args.no_e2e:
         progress("resident chain")
         result["resident_chain"] = resident_chain_stage(eng, cs, inp, args.resident_epochs)
-        # the same with Topologies created and deleted (informer add / delete events)
-        del cs
         progress("resident chain, pipelined")
         result["resident_pipeline"] = resident_pipeline_stage(eng, cs, cs.epoch_input(copy=True), args.resident_epochs)
+        del cs
+        # the same with Topologies created and deleted (informer add / delete events)
         progress("resident chain with a changing Topology set")
         tc = synth.TopologySetChurn(frac=0.01, total_pods=total_pods)
         p0 = tc.epoch_input()

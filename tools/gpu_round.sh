@@ -35,6 +35,10 @@ if has smoke; then
   timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
   tail -1 $OUT/smoke.log
 fi
+if has iab; then
+  timeout -k 10 500 python -u tools/ingest_ablate.py 1000000 ${IAB_VARIANTS:-0,16} > $OUT/ingest_ab.jsonl 2> $OUT/ingest_ab.err
+  cat $OUT/ingest_ab.jsonl
+fi
 for C in 2 1 3 4; do
   B=bench; [[ $C != 2 ]] && B=bench$C
   if has $B; then
@@ -51,10 +55,6 @@ fi
 if has ingest; then
   timeout -k 10 400 python -u tools/ingest_run.py --pods 1000000 --doc /tmp/kdtn_doc_1000000.json > $OUT/ingest.json 2> $OUT/ingest.err
   tail -5 $OUT/ingest.json
-fi
-if has iab; then
-  timeout -k 10 500 python -u tools/ingest_ablate.py 1000000 ${IAB_VARIANTS:-0,16} > $OUT/ingest_ab.jsonl 2> $OUT/ingest_ab.err
-  cat $OUT/ingest_ab.jsonl
 fi
 if has stages; then
   timeout -k 10 400 python -u tools/stage_run.py > $OUT/stages.json 2> $OUT/stages.err
