@@ -67,6 +67,7 @@ struct kdtn_ctx {
     hipStream_t comm_stream = nullptr;          // RCCL pod-status exchange (nranks > 1)
     hipStream_t copy_stream = nullptr;          // delta uploads: host-to-device copies beside the kernels
     hipEvent_t ev_cp[4] = {};
+    hipEvent_t ev_col[LINK_COLS32 + 1] = {};   // a delta's staged column copies (+ uid), each placed on arrival
     hipStream_t d2h_stream = nullptr;           // kdtn_epoch_download_async: the outputs' copies
     hipEvent_t ev_dl_ready = nullptr, ev_dl_done = nullptr;
     bool dl_pending = false;                    // an async download's copies may still be reading outputs
@@ -386,19 +387,30 @@ constexpr uint32_t STAGED_UPLOAD_MIN = 1u << 16;   // records: below it, 2-D cop
 
 // A link table's columns as host runs: consecutive columns whose host arrays are adjacent (a
 // caller holding key[7][n] / prop[12][n] blocks) become one copy into the staging buffer.
-int stage_columns(kdtn_ctx* c, uint8_t* st, const kdtn_link_table& L, size_t col, hipStream_t hs) {
+// segs (optional): the column ranges of the copies, in copy order, each followed by an event
+// on hs (c->ev_col[k]); returns their count in *nseg
+int stage_columns(kdtn_ctx* c, uint8_t* st, const kdtn_link_table& L, size_t col, hipStream_t hs,
+                  uint32_t (*segs)[2] = nullptr, int* nseg = nullptr) {
     const uint32_t* src[LINK_COLS32];
     for (int k = 0; k < KDTN_NKEY; ++k) src[COL_KEY0 + k] = L.key[k];
     for (int k = 0; k < KDTN_NPROP; ++k) src[COL_PROP0 + k] = L.prop[k];
     src[COL_GAP] = L.gap;
+    int ns = 0;
     for (int a = 0; a < LINK_COLS32;) {
         int b = a + 1;
         while (b < LINK_COLS32 && reinterpret_cast<const uint8_t*>(src[b]) ==
                                       reinterpret_cast<const uint8_t*>(src[b - 1]) + col)
             ++b;
         HIP_TRY(hipMemcpyAsync(st + (size_t)a * col, src[a], (size_t)(b - a) * col, hipMemcpyHostToDevice, hs));
+        if (segs) {
+            segs[ns][0] = (uint32_t)a;
+            segs[ns][1] = (uint32_t)b;
+            HIP_TRY(hipEventRecord(c->ev_col[ns], hs));
+        }
+        ++ns;
         a = b;
     }
+    if (nseg) *nseg = ns;
     return KDTN_OK;
 }
 
@@ -841,6 +853,7 @@ int kdtn_init(kdtn_ctx** out, const kdtn_config* cfg) {
     for (int i = 0; i <= kMaxTimers; ++i) (void)hipEventCreateWithFlags(&c->ev[i], hipEventDisableSystemFence);
     (void)hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming);
     for (hipEvent_t& e : c->ev_cp) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    for (hipEvent_t& e : c->ev_col) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
     if (hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess) c->copy_stream = nullptr;
     if (hipStreamCreateWithFlags(&c->d2h_stream, hipStreamNonBlocking) != hipSuccess) c->d2h_stream = nullptr;
     (void)hipEventCreateWithFlags(&c->ev_dl_ready, hipEventDisableTiming);
@@ -900,6 +913,8 @@ void kdtn_destroy(kdtn_ctx* c) {
     if (c->ev_ag) (void)hipEventDestroy(c->ev_ag);
     if (c->ev_done) (void)hipEventDestroy(c->ev_done);
     for (hipEvent_t e : c->ev_cp)
+        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->ev_col)
         if (e) (void)hipEventDestroy(e);
     if (c->copy_stream) {
         (void)hipStreamSynchronize(c->copy_stream);
@@ -3152,7 +3167,9 @@ int kdtn_epoch_upload_delta(kdtn_ctx* c, const kdtn_epoch_delta* d) {
     // --- copies (copy stream), after everything already queued on the context stream
     HIP_TRY(hipEventRecord(c->ev_cp[0], s));
     if (cs != s) HIP_TRY(hipStreamWaitEvent(cs, c->ev_cp[0], 0));
-    {   // segments in pack order; host-adjacent neighbours merge into one copy
+    {   // segments in pack order; host-adjacent neighbours merge into one copy. The per-Topology
+        // arrays go first and alone (the plan and the kept segments' assembly need only them),
+        // then the references
         const void* src[9] = {d->topo, d->src_ip, d->net_ns, d->des_off, d->prev, d->ns, d->name, d->spec_nil, d->ref};
         const size_t at[9] = {pk_.topo, pk_.src, pk_.netns, pk_.off, pk_.prev, pk_.ns, pk_.name, pk_.nil, pk_.ref};
         const size_t len[9] = {(size_t)n * 4, (size_t)n * 4, (size_t)n * 4, pk_.prev - pk_.off, pk_.ns - pk_.prev,
@@ -3165,17 +3182,17 @@ int kdtn_epoch_upload_delta(kdtn_ctx* c, const kdtn_epoch_delta* d) {
             int j = i + 1;
             // the device block is contiguous (padding included): the host array must sit at the
             // same distance from the run's start
-            while (j < 9 && (!len[j] || static_cast<const uint8_t*>(src[j]) == h0 + (at[j] - at[i]))) {
+            while (j < (i < 8 ? 8 : 9) && (!len[j] || static_cast<const uint8_t*>(src[j]) == h0 + (at[j] - at[i]))) {
                 if (len[j]) bytes = at[j] + len[j] - at[i];
                 ++j;
             }
             HIP_TRY(hipMemcpyAsync(pack + at[i], h0, bytes, hipMemcpyHostToDevice, cs));
-            if (i <= 7 && j > 7) HIP_TRY(hipEventRecord(c->ev_cp[1], cs));   // the small arrays are in
+            if (i <= 7 && j >= 8) HIP_TRY(hipEventRecord(c->ev_cp[1], cs));   // the small arrays are in
             i = j;
         }
         if (!n) HIP_TRY(hipEventRecord(c->ev_cp[1], cs));
     }
-    HIP_TRY(hipEventRecord(c->ev_cp[2], cs));
+    HIP_TRY(hipEventRecord(c->ev_cp[2], cs));                                   // and the references
     c->uploaded = false;                            // (restored below when the delta is rejected)
     const uint32_t saved[6] = {c->D, c->P, c->kd_valid, c->pd_valid, c->kd_from, c->pd_from};
     const uint64_t saved_arena[2] = {c->kd_arena, c->pd_arena};
@@ -3183,9 +3200,12 @@ int kdtn_epoch_upload_delta(kdtn_ctx* c, const kdtn_epoch_delta* d) {
     // check below compares it with the host's)
     TRY(upload_dicts(c, d->kdict, d->pdict, kk, pk, cs));
     uint8_t* st = static_cast<uint8_t*>(c->stage.p);
+    uint32_t segs[LINK_COLS32][2];
+    int nseg = 0;
     if (nr) {
-        TRY(stage_columns(c, st, L, col, cs));
+        TRY(stage_columns(c, st, L, col, cs, segs, &nseg));
         HIP_TRY(hipMemcpyAsync(st + uid_at, L.uid, (size_t)nr * 8, hipMemcpyHostToDevice, cs));
+        HIP_TRY(hipEventRecord(c->ev_col[nseg], cs));
     }
     HIP_TRY(hipEventRecord(c->ev_cp[3], cs));
     // --- kernels (context stream)
@@ -3202,14 +3222,14 @@ int kdtn_epoch_upload_delta(kdtn_ctx* c, const kdtn_epoch_delta* d) {
     }
     if (cs != s) HIP_TRY(hipStreamWaitEvent(s, c->ev_cp[1], 0));
     if (n) k_delta_map<<<nblocks(n), BLOCK, 0, s>>>(p_topo, n, Tn, dp<uint32_t>(c->st_chg));
-    if (cs != s) HIP_TRY(hipStreamWaitEvent(s, c->ev_cp[2], 0));
-    {
-        DeltaCheckIn ci{p_topo, p_off, p_nil,
-                        p_src, p_netns, p_ref,
-                        dp<uint32_t>(c->kd_offs), dp<uint32_t>(c->pd_offs), n, nref, Tn, D, nr, N0,
-                        kk, pk, d->kdict.offs[kk], d->pdict.offs[pk]};
-        const uint32_t grid = std::max<uint32_t>({1u, nblocks(n), std::min<uint32_t>(nblocks(nref), 4 * c->n_cus)});
-        k_delta_check<<<grid, BLOCK, 0, s>>>(ci, misc + MISC_DELTA_ERR);
+    const DeltaCheckIn ci{p_topo, p_off, p_nil,
+                          p_src, p_netns, p_ref,
+                          dp<uint32_t>(c->kd_offs), dp<uint32_t>(c->pd_offs), n, nref, Tn, D, nr, N0,
+                          kk, pk, d->kdict.offs[kk], d->pdict.offs[pk]};
+    {   // the per-Topology arrays and the kept dictionaries now; the references once they are in
+        DeltaCheckIn c1 = ci;
+        c1.nref = 0;
+        k_delta_check<<<std::max<uint32_t>(1u, nblocks(n)), BLOCK, 0, s>>>(c1, misc + MISC_DELTA_ERR);
     }
     // plan over the new topology table: new rows into scratch columns, the state is untouched
     DeltaPlanIn pi{topo_view(c), dp<uint32_t>(c->st_chg), remap ? p_prev : nullptr,
@@ -3224,7 +3244,7 @@ int kdtn_epoch_upload_delta(kdtn_ctx* c, const kdtn_epoch_delta* d) {
     // the new desired store: kept segments and previous-record references now (grid over the
     // bound, the exact count stays on the device), the inline records once they have arrived
     TRY(scan_lengths(c, c->st_len, Tn, c->st_off64, c->st_part, c->st_off32));
-    const AsmGuard g{misc + MISC_DELTA_ERR, dp<uint64_t>(c->st_off64) + Tn, 1u};
+    const AsmGuard g{misc + MISC_DELTA_ERR, dp<uint64_t>(c->st_off64) + Tn, 1u, 1u};
     if (nbound)
         k_store_assemble<<<nblocks(nbound), BLOCK, 0, s>>>(dp<uint32_t>(c->st_off32), Tn, dp<uint32_t>(c->st_base),
                                                            dp<uint8_t>(c->st_mode), p_ref, c->des.view,
@@ -3232,23 +3252,35 @@ int kdtn_epoch_upload_delta(kdtn_ctx* c, const kdtn_epoch_delta* d) {
                                                            dp<uint32_t>(c->sh_des.buf));
     if (remap) {                                    // kept Topologies' status segments move with them
         TRY(scan_lengths(c, c->st_rlen, Tn, c->st_roff64, c->st_rpart, c->st_roff32));
-        const AsmGuard gr{misc + MISC_DELTA_ERR, dp<uint64_t>(c->st_roff64) + Tn, 0u};
+        const AsmGuard gr{misc + MISC_DELTA_ERR, dp<uint64_t>(c->st_roff64) + Tn, 0u, 0u};
         if (M0)
             k_store_assemble<<<nblocks(M0), BLOCK, 0, s>>>(dp<uint32_t>(c->st_roff32), Tn, dp<uint32_t>(c->st_rbase),
                                                            dp<uint8_t>(c->st_mask), nullptr, c->real.view, c->real.view,
                                                            M0, gr, dp<uint32_t>(c->sh_real.buf));
     }
-    // the inline records' destinations, still before they have arrived
-    if (nr && nref)
-        k_delta_dest<<<nblocks(nref), BLOCK, 0, s>>>(p_off, p_topo, n,
-                                                     p_ref, nref, dp<uint32_t>(c->st_off32),
-                                                     misc + MISC_DELTA_ERR, dp<uint32_t>(c->dl_dest),
-                                                     misc + MISC_DELTA_MULTI);
-    if (cs != s) HIP_TRY(hipStreamWaitEvent(s, c->ev_cp[3], 0));
-    if (nr)          // staging columns straight to their places, with the id-range column maxima
-        k_delta_place<<<std::min<uint32_t>(nblocks(nr), 4 * c->n_cus), BLOCK, 0, s>>>(
+    // the references once they have arrived: checked, previous records copied to their places,
+    // the inline records' destinations noted (before the records themselves have arrived)
+    if (cs != s) HIP_TRY(hipStreamWaitEvent(s, c->ev_cp[2], 0));
+    if (nref) {
+        DeltaCheckIn c2 = ci;
+        c2.n = 0;
+        c2.kd_keep = c2.pd_keep = 0;                   // (checked above)
+        k_delta_check<<<std::min<uint32_t>(nblocks(nref), 4 * c->n_cus), BLOCK, 0, s>>>(c2, misc + MISC_DELTA_ERR);
+        k_delta_refs<<<nblocks(nref), BLOCK, 0, s>>>(p_off, p_topo, n, p_ref, nref, dp<uint32_t>(c->st_off32),
+                                                     c->des.view, misc + MISC_DELTA_ERR, dp<uint32_t>(c->dl_dest),
+                                                     misc + MISC_DELTA_MULTI, dp<uint32_t>(c->sh_des.buf));
+    }
+    // staging columns straight to their places as each copy arrives, with the id-range maxima
+    const uint32_t place_grid = std::min<uint32_t>(nblocks(nr), 4 * c->n_cus);
+    for (int k = 0; nr && k <= nseg; ++k) {
+        if (cs != s) HIP_TRY(hipStreamWaitEvent(s, c->ev_col[k], 0));
+        const bool uid_seg = k == nseg;
+        k_delta_place<<<place_grid, BLOCK, 0, s>>>(
             reinterpret_cast<const uint32_t*>(st), reinterpret_cast<const int64_t*>(st + uid_at), nr,
-            dp<uint32_t>(c->dl_dest), misc + MISC_DELTA_ERR, dp<uint32_t>(c->sh_des.buf), colmax);
+            dp<uint32_t>(c->dl_dest), misc + MISC_DELTA_ERR, dp<uint32_t>(c->sh_des.buf), colmax,
+            uid_seg ? (uint32_t)LINK_COLS32 : segs[k][0], uid_seg ? (uint32_t)LINK_COLS32 : segs[k][1], uid_seg ? 1u : 0u);
+    }
+    if (cs != s) HIP_TRY(hipStreamWaitEvent(s, c->ev_cp[3], 0));
     k_delta_totals<<<1, 64, 0, s>>>(dp<uint64_t>(c->st_off64), Tn, remap ? dp<uint64_t>(c->st_roff64) : nullptr, misc);
     HIP_TRY(hipGetLastError());
     uint32_t* hm = c->h_misc + 64;

@@ -383,13 +383,16 @@ struct AsmGuard {                         // k_store_assemble in a delta upload 
     const uint32_t* err;                  // the delta's error word: nothing is copied once set
     const uint64_t* n_dev;                // exact record count (the grid covers a bound)
     uint32_t skip_new;                    // inline records are placed by k_delta_inline
+    uint32_t skip_ref;                    // reference lists are placed by k_delta_refs
 };
 __global__ void k_store_assemble(const uint32_t* off, uint32_t nt, const uint32_t* base, const uint8_t* mode,
                                  const uint32_t* ref, DevLinks A, DevLinks B, uint32_t n, AsmGuard g, uint32_t* out);
-__global__ void k_delta_dest(const uint32_t* d_off, const uint32_t* topo, uint32_t n, const uint32_t* ref,
-                             uint32_t nref, const uint32_t* off, const uint32_t* err, uint32_t* dest, uint32_t* multi);
+__global__ void k_delta_refs(const uint32_t* d_off, const uint32_t* topo, uint32_t n, const uint32_t* ref,
+                             uint32_t nref, const uint32_t* off, DevLinks A, const uint32_t* err, uint32_t* dest,
+                             uint32_t* multi, uint32_t* out);
 __global__ void k_delta_place(const uint32_t* stage, const int64_t* uid, uint32_t n, const uint32_t* dest,
-                              const uint32_t* err, uint32_t* out, uint32_t* colmax);
+                              const uint32_t* err, uint32_t* out, uint32_t* colmax, uint32_t c0, uint32_t c1,
+                              uint32_t with_uid);
 __global__ void k_delta_inline(const uint32_t* d_off, const uint32_t* topo, uint32_t n, const uint32_t* ref,
                                uint32_t nref, const uint32_t* off, DevLinks B, const uint32_t* err, uint32_t* out);
 

@@ -231,7 +231,7 @@ __global__ void __launch_bounds__(BLOCK) k_store_assemble(const uint32_t* off, u
     const uint8_t m = mode[t];
     if (m == ASM_SEG_A) copy_record(A.base, k, out, d);
     else if (m == ASM_SEG_B) copy_record(B.base, k, out, d);
-    else {
+    else if (!g.skip_ref) {
         const uint32_t r = ref[k];
         if (r & KDTN_DELTA_NEW) {
             if (!g.skip_new) copy_record(B.base, r & ~KDTN_DELTA_NEW, out, d);
@@ -241,29 +241,36 @@ __global__ void __launch_bounds__(BLOCK) k_store_assemble(const uint32_t* off, u
     }
 }
 
-// Where each inline record of a delta goes in the new desired store, computed while the
-// records are still crossing the host link: one thread per reference k, its changed Topology c
-// (upper bound over the delta's offsets), that Topology's new index topo[c], output position
-// off[topo[c]] + (k - d_off[c]). dest[i] takes the position of inline record i; a record
-// referenced twice raises `multi` (k_delta_inline then places every reference).
-__global__ void __launch_bounds__(BLOCK) k_delta_dest(const uint32_t* d_off, const uint32_t* topo, uint32_t n,
+// The reference lists of a delta once they have arrived (k_store_assemble placed the kept
+// segments meanwhile): one thread per reference k, its changed Topology c (wave-cooperative
+// search over the delta's offsets), output position off[topo[c]] + (k - d_off[c]); a previous
+// record is copied there, an inline record's position goes to dest (k_delta_place writes the
+// record when its columns have arrived; a record referenced twice raises `multi`).
+__global__ void __launch_bounds__(BLOCK) k_delta_refs(const uint32_t* d_off, const uint32_t* topo, uint32_t n,
                                                       const uint32_t* ref, uint32_t nref, const uint32_t* off,
-                                                      const uint32_t* err, uint32_t* dest, uint32_t* multi) {
-    if (*err) return;
+                                                      DevLinks A, const uint32_t* err, uint32_t* dest,
+                                                      uint32_t* multi, uint32_t* out) {
+    if (*err) return;                                  // (wave-uniform: the search below is cooperative)
     const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t c = entry_topo_wave(d_off, n, k, k < nref);
     if (k >= nref) return;
     const uint32_t r = ref[k];
-    if (!(r & KDTN_DELTA_NEW)) return;
-    const uint32_t c = entry_topo(d_off, n, k);
-    if (atomicExch(dest + (r & ~KDTN_DELTA_NEW), off[topo[c]] + (k - d_off[c])) != 0xFFFFFFFFu) atomicOr(multi, 1u);
+    const uint32_t d = off[topo[c]] + (k - d_off[c]);
+    if (r & KDTN_DELTA_NEW) {
+        if (atomicExch(dest + (r & ~KDTN_DELTA_NEW), d) != 0xFFFFFFFFu) atomicOr(multi, 1u);
+    } else {
+        copy_record(A.base, r, out, d);
+    }
 }
 
 // Inline records of a delta from the staging columns (k_soa_to_tiles' input) straight to their
 // positions in the new desired store, plus the id-range column maxima; unreferenced records
-// (dest ~0) are skipped. Nothing is written when the delta was refused.
+// (dest ~0) are skipped. Nothing is written when the delta was refused. One launch per staged
+// copy: columns [c0, c1) (and the uid column when with_uid), so each group of columns is placed
+// as soon as its copy has arrived while the next group still crosses the host link.
 __global__ void __launch_bounds__(BLOCK) k_delta_place(const uint32_t* stage, const int64_t* uid, uint32_t n,
                                                        const uint32_t* dest, const uint32_t* err, uint32_t* out,
-                                                       uint32_t* colmax) {
+                                                       uint32_t* colmax, uint32_t c0, uint32_t c1, uint32_t with_uid) {
     __shared__ uint32_t red[BLOCK / 64][COL_GAP];
     uint32_t mx[COL_GAP];
 #pragma unroll
@@ -274,14 +281,16 @@ __global__ void __launch_bounds__(BLOCK) k_delta_place(const uint32_t* stage, co
         uint32_t* dst = out + (size_t)(d >> 6) * TILE_WORDS + (d & 63u);
 #pragma unroll
         for (int c = 0; c < LINK_COLS32; ++c) {
+            if ((uint32_t)c < c0 || (uint32_t)c >= c1) continue;
             const uint32_t v = __builtin_nontemporal_load(stage + (size_t)c * n + i);
             if (c < COL_GAP) mx[c] = v > mx[c] ? v : mx[c];
             if (d != 0xFFFFFFFFu) dst[c * TILE_RECS] = v;
         }
-        if (d != 0xFFFFFFFFu)
+        if (with_uid && d != 0xFFFFFFFFu)
             reinterpret_cast<int64_t*>(out + (size_t)(d >> 6) * TILE_WORDS + LINK_COLS32 * TILE_RECS)[d & 63u] =
                 __builtin_nontemporal_load(uid + i);
     }
+    if (c0 >= (uint32_t)COL_GAP) return;                 // no id column in this launch
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
     for (int c = 0; c < COL_GAP; ++c) {
@@ -294,7 +303,7 @@ __global__ void __launch_bounds__(BLOCK) k_delta_place(const uint32_t* stage, co
         if (lane == 0) red[wave][c] = v;
     }
     __syncthreads();
-    if (threadIdx.x < COL_GAP) {
+    if (threadIdx.x >= c0 && threadIdx.x < c1 && threadIdx.x < (uint32_t)COL_GAP) {
         uint32_t v = 0;
 #pragma unroll
         for (int w = 0; w < BLOCK / 64; ++w) v = red[w][threadIdx.x] > v ? red[w][threadIdx.x] : v;
@@ -302,7 +311,7 @@ __global__ void __launch_bounds__(BLOCK) k_delta_place(const uint32_t* stage, co
     }
 }
 
-// The general placement when an inline record is referenced more than once (k_delta_dest's
+// The general placement when an inline record is referenced more than once (k_delta_refs'
 // multi flag): one thread per reference k, records from the tiles of the staged delta.
 __global__ void __launch_bounds__(BLOCK) k_delta_inline(const uint32_t* d_off, const uint32_t* topo, uint32_t n,
                                                         const uint32_t* ref, uint32_t nref, const uint32_t* off,

@@ -24,6 +24,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--pods", type=int, default=1_000_000)
 ap.add_argument("--epochs", type=int, default=6)
 ap.add_argument("--topology-set", type=float, default=0.0, help="fraction of Topologies deleted/created per epoch")
+ap.add_argument("--pipeline", action="store_true", help="epoch k's download overlapping epoch k+1's upload")
 a = ap.parse_args()
 src = (synth.TopologySetChurn(frac=a.topology_set, total_pods=a.pods) if a.topology_set
        else synth.ChurnSequence(total_pods=a.pods))
@@ -43,6 +44,29 @@ eng.commit(np.ones(prev.topos.n, np.uint8))
 cap = max(1 << 20, prev.desired.n // 8)
 into = None
 rows = []
+if a.pipeline:
+    bufs = [BatchesOut.alloc(prev.topos.n, cap, cap, cap, pinned=True) for _ in range(2)]
+    for ep, (d, T, N) in enumerate(deltas):
+        t0 = time.perf_counter()
+        eng.upload_delta(d)
+        t1 = time.perf_counter()
+        eng.run()
+        eng.sync()
+        t2 = time.perf_counter()
+        eng.download_wait()
+        t3 = time.perf_counter()
+        eng.download_async(bufs[ep % 2])
+        eng.commit(np.ones(T, np.uint8))
+        t4 = time.perf_counter()
+        r = {"epoch": ep, "upload_ms": (t1 - t0) * 1e3, "run_ms": (t2 - t1) * 1e3, "wait_prev_download_ms": (t3 - t2) * 1e3,
+             "async_commit_ms": (t4 - t3) * 1e3, "e2e_ms": (t4 - t0) * 1e3}
+        rows.append(r)
+        print(json.dumps(r), flush=True)
+    eng.download_wait()
+    steady = rows[1:]
+    print(json.dumps({"summary_excluding_first": {k: float(np.mean([r[k] for r in steady])) for k in rows[0] if k != "epoch"}}),
+          flush=True)
+    sys.exit(0)
 for ep, (d, T, N) in enumerate(deltas):
     if into is None or len(into.action) != T:
         into = BatchesOut.alloc(T, cap, cap, cap, pinned=True)
