@@ -209,8 +209,11 @@ namespace {
 // on two streams, every overlap lost), so they are freed together once more than
 // kRetireBytes are waiting (one synchronisation for many regrowths) or when a context is
 // destroyed. Retired buffers belong to no context: nothing enqueues work on them any more, and
-// hipFree completes the work already in flight first.
-constexpr size_t kRetireBytes = (size_t)8 << 30;
+// hipFree completes the work already in flight first. The bound is 32 GB of the 288 GB: a
+// resident config-3 chain retires ≈ 8.5 GB while its rotating buffers reach their sizes, and
+// at 8 GB that flush (≈ 10 frees, 5.6 ms) landed inside an epoch of the steady state
+// (profiles/r04p_resident_alloc_log.txt).
+constexpr size_t kRetireBytes = (size_t)32 << 30;
 struct Retired {
     std::mutex m;
     std::vector<void*> p;
@@ -220,9 +223,20 @@ Retired& retired() {
     static Retired r;
     return r;
 }
+// (profiling build, KDTN_ALLOC_LOG set) allocations of 16 MB and more and the flushes, on stderr
+void alloc_log(const char* what, size_t bytes) {
+#if KDTN_PROFILING
+    static const bool on = std::getenv("KDTN_ALLOC_LOG") != nullptr;
+    if (on && bytes >= (16u << 20)) std::fprintf(stderr, "[kdtn alloc] %s %zu MB\n", what, bytes >> 20);
+#else
+    (void)what;
+    (void)bytes;
+#endif
+}
 void retired_flush() {
     Retired& r = retired();
     std::lock_guard<std::mutex> lk(r.m);
+    alloc_log("flush", r.bytes);
     for (void* p : r.p) (void)hipFree(p);
     r.p.clear();
     r.bytes = 0;
@@ -249,6 +263,7 @@ int ensure(DevBuf& b, size_t bytes) {
     retire(b.p, b.cap);
     b.p = nullptr;
     b.cap = 0;
+    alloc_log("ensure", bytes);
     hipError_t e = hipMalloc(&b.p, bytes);
     if (e != hipSuccess) {
         std::snprintf(g_last_error, sizeof(g_last_error), "hipMalloc(%zu): %s", bytes,
@@ -265,6 +280,7 @@ int ensure_keep(DevBuf& b, size_t bytes, size_t keep, hipStream_t s) {
     if (b.cap >= bytes) return KDTN_OK;
     if (!keep || !b.p) return ensure(b, bytes);
     const size_t cap = std::max(bytes, b.cap + b.cap / 2);
+    alloc_log("ensure_keep", cap);
     void* np = nullptr;
     hipError_t e = hipMalloc(&np, cap);
     if (e != hipSuccess) {
@@ -733,7 +749,7 @@ int prepare_epoch(kdtn_ctx* c, const kdtn_vni_table& vn, uint32_t slice, uint32_
 
 // Which batch entries the daemons reach (k_reach; include/kdtn.h): c->f_send (add) and
 // c->f_reach_upd (update) flags of the last run; stamps destination daemons into `mark`.
-int run_reach(kdtn_ctx* c, uint32_t* mark, uint32_t stamp, uint32_t* nlist = nullptr) {
+int run_reach(kdtn_ctx* c, uint32_t* mark, uint32_t stamp) {
     const uint32_t nu = c->h_misc[2], na = c->h_misc[3];
     TRY(ensure(c->f_send, (size_t)na + 16));
     TRY(ensure(c->f_reach_upd, (size_t)nu + 16));
@@ -750,7 +766,7 @@ int run_reach(kdtn_ctx* c, uint32_t* mark, uint32_t stamp, uint32_t* nlist = nul
                                                                                     dp<uint8_t>(c->f_st));
         if ((uint64_t)na + nu)
             k_reach<<<nblocks((uint64_t)na + nu), BLOCK, 0, c->stream>>>(r, na, nu, cut, dp<uint8_t>(c->f_st), mark,
-                                                                         nlist, dp<uint8_t>(c->f_send),
+                                                                         dp<uint8_t>(c->f_send),
                                                                          dp<uint8_t>(c->f_reach_upd));
     }
     return KDTN_OK;
@@ -1637,18 +1653,20 @@ int fanout_compute(kdtn_ctx* c) {
         c->f_stamp = 1;
     }
     const uint32_t nchunks = nblocks(na, FAN_CHUNK);
+    const uint32_t nbd = nblocks(D, SCAN_CHUNK);
     TRY(ensure(c->f_node_idx, (size_t)D * 4));
     TRY(ensure(c->f_nodes, (size_t)FAN_NODE_CAP * 4 + 16));
-    TRY(ensure(c->f_part, ((size_t)FAN_NODE_CAP + 1) * 4 + 16));      // the node list
+    TRY(ensure(c->f_part, (size_t)nbd * 8 + 16));
     TRY(ensure(c->f_idx, (size_t)na * 4 + 16));
     TRY(ensure(c->f_inv, (size_t)na * 4 + 16));
     uint32_t* misc = dp<uint32_t>(c->misc);
     uint32_t* n_nodes = misc + MISC_FAN_NODES;
     FanIn f{dp<uint32_t>(c->add_off), dp<uint4>(c->add_res), dp<uint2>(c->add_qdisc), c->T, na, c->f_stamp};
-    uint32_t* nlist = dp<uint32_t>(c->f_part);
-    HIP_TRY(hipMemsetAsync(nlist, 0, 4, s));
-    TRY(run_reach(c, dp<uint32_t>(c->f_mark), c->f_stamp, nlist));
-    k_fan_nodes_sort<<<1, 1024, 0, s>>>(nlist, dp<uint32_t>(c->f_node_idx), dp<uint32_t>(c->f_nodes), n_nodes);
+    TRY(run_reach(c, dp<uint32_t>(c->f_mark), c->f_stamp));
+    k_fan_nodes_count<<<nbd, BLOCK, 0, s>>>(dp<uint32_t>(c->f_mark), D, c->f_stamp, dp<uint64_t>(c->f_part));
+    k_scan_top<<<1, SCAN_TOP_BLOCK, 0, s>>>(dp<uint64_t>(c->f_part), nbd);
+    k_fan_nodes_write<<<nbd, BLOCK, 0, s>>>(dp<uint32_t>(c->f_mark), D, c->f_stamp, dp<uint64_t>(c->f_part),
+                                           dp<uint32_t>(c->f_node_idx), dp<uint32_t>(c->f_nodes), n_nodes);
     timer_mark(c, "fanout_nodes");
     uint32_t nn = 0;
     HIP_TRY(hipMemcpyAsync(&nn, n_nodes, 4, hipMemcpyDeviceToHost, s));

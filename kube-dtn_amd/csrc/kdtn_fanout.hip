@@ -10,10 +10,9 @@
 // nodes in ascending kdict-id order of their src_ip, entries of a node in add-list order.
 //
 // Kernels: k_reach_cuts / k_reach (entry-parallel RPC-order first-error rule, marks senders
-// and their nodes in a stamped D-sized table; the entry that first stamps a node appends it to
-// a short list), k_fan_nodes_sort (the listed node ids sorted → dense node index),
-// k_fan_count / k_fan_scatter (single-wave workgroups over chunks of 4,096 entries: LDS
-// histogram, node-major scan of the (node, chunk) counts, stable scatter).
+// and their nodes in a stamped D-sized table), k_fan_nodes_* (compaction of marked node ids → dense
+// node index), k_fan_count / k_fan_scatter (single-wave workgroups over chunks of 4,096
+// entries: LDS histogram, node-major scan of the (node, chunk) counts, stable scatter).
 #include "kdtn_encode.h"
 
 namespace kdtn {
@@ -48,8 +47,8 @@ __global__ void __launch_bounds__(BLOCK) k_reach_cuts(ReachIn f, uint32_t nd, ui
 }
 
 __global__ void __launch_bounds__(BLOCK) k_reach(ReachIn f, uint32_t na, uint32_t nu, const uint32_t* cut,
-                                                 const uint8_t* st_add, uint32_t* mark, uint32_t* nlist,
-                                                 uint8_t* reach_add, uint8_t* reach_upd) {
+                                                 const uint8_t* st_add, uint32_t* mark, uint8_t* reach_add,
+                                                 uint8_t* reach_upd) {
     const uint32_t x = blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t ta = entry_topo_wave(f.add_off, f.T, x, x < na);
     const uint32_t tu = entry_topo_wave(f.upd_off, f.T, x - na, x >= na && x < na + nu);
@@ -60,15 +59,11 @@ __global__ void __launch_bounds__(BLOCK) k_reach(ReachIn f, uint32_t na, uint32_
             a = REACH_ON;
             if (st_add[x] & REACH_SEND) {               // no failure, RemotePod sent (k_reach_cuts)
                 a |= REACH_SEND;
-                // a few dozen daemons take millions of stamps: only a missing one is exchanged
-                // (a stale read exchanges again and gets the stamp back), and the one exchange
-                // that replaced an older value lists the node (nlist[0] = count)
+                // a few dozen daemons take millions of stamps: store only a missing one (a
+                // stale read stores again, harmlessly), so the words are not written per entry
                 if (mark) {
                     const uint32_t node = f.add_res[x].z;
-                    if (mark[node] != f.stamp && atomicExch(&mark[node], f.stamp) != f.stamp) {
-                        const uint32_t k = atomicAdd(nlist, 1u);
-                        if (k < (uint32_t)FAN_NODE_CAP) nlist[1 + k] = node;
-                    }
+                    if (mark[node] != f.stamp) mark[node] = f.stamp;
                 }
             }
         }
@@ -80,38 +75,41 @@ __global__ void __launch_bounds__(BLOCK) k_reach(ReachIn f, uint32_t na, uint32_
     }
 }
 
-// The listed node ids (each once) in ascending id order → nodes[] and node_idx[node]; one
-// workgroup, bitonic sort in LDS over the list padded to a power of two. More than
-// FAN_NODE_CAP nodes: only the count is written (the host reports it).
-__global__ void __launch_bounds__(1024) k_fan_nodes_sort(const uint32_t* nlist, uint32_t* node_idx, uint32_t* nodes,
-                                                         uint32_t* n_nodes) {
-    __shared__ uint32_t v[FAN_NODE_CAP];
-    const uint32_t cnt = nlist[0], tid = threadIdx.x;
-    if (tid == 0) *n_nodes = cnt;
-    if (cnt > (uint32_t)FAN_NODE_CAP) return;
-    uint32_t P = 1;
-    while (P < cnt) P <<= 1;
-    for (uint32_t k = tid; k < P; k += 1024) v[k] = k < cnt ? nlist[1 + k] : 0xFFFFFFFFu;
-    __syncthreads();
-    for (uint32_t size = 2; size <= P; size <<= 1) {
-        for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-            for (uint32_t k = tid; k < P; k += 1024) {
-                const uint32_t l = k ^ stride;
-                if (l > k) {
-                    const uint32_t a = v[k], b = v[l];
-                    if ((a > b) == ((k & size) == 0)) {
-                        v[k] = b;
-                        v[l] = a;
-                    }
-                }
-            }
-            __syncthreads();
+// marked node ids → dense node indices in id order (chunks of SCAN_CHUNK ids)
+__global__ void __launch_bounds__(BLOCK) k_fan_nodes_count(const uint32_t* mark, uint32_t nd, uint32_t stamp,
+                                                           uint64_t* part) {
+    __shared__ uint64_t sh[BLOCK / 64];
+    const uint32_t b0 = blockIdx.x * SCAN_CHUNK + threadIdx.x * 4;
+    uint64_t v = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v += (b0 + k < nd && mark[b0 + k] == stamp) ? 1u : 0u;
+    uint64_t tot;
+    block_exclusive(v, sh, &tot);
+    if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_fan_nodes_write(const uint32_t* mark, uint32_t nd, uint32_t stamp,
+                                                           const uint64_t* part, uint32_t* node_idx,
+                                                           uint32_t* nodes, uint32_t* n_nodes) {
+    __shared__ uint64_t sh[BLOCK / 64];
+    const uint32_t b0 = blockIdx.x * SCAN_CHUNK + threadIdx.x * 4;
+    bool m[4];
+    uint64_t v = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        m[k] = b0 + k < nd && mark[b0 + k] == stamp;
+        v += m[k] ? 1u : 0u;
+    }
+    uint64_t tot;
+    uint64_t x = part[blockIdx.x] + block_exclusive(v, sh, &tot);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (m[k]) {
+            node_idx[b0 + k] = (uint32_t)x;
+            nodes[x] = b0 + k;
+            ++x;
         }
-    }
-    for (uint32_t k = tid; k < cnt; k += 1024) {
-        nodes[k] = v[k];
-        node_idx[v[k]] = k;
-    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *n_nodes = (uint32_t)(part[blockIdx.x] + tot);
 }
 
 // (node, chunk) counts: one wave per chunk of FAN_CHUNK entries, LDS histogram

@@ -520,7 +520,7 @@ struct ReachIn {
 };
 __global__ void k_reach_cuts(ReachIn f, uint32_t nd, uint32_t na, uint32_t nu, uint32_t* cut, uint8_t* st_add);
 __global__ void k_reach(ReachIn f, uint32_t na, uint32_t nu, const uint32_t* cut, const uint8_t* st_add, uint32_t* mark,
-                        uint32_t* nlist, uint8_t* reach_add, uint8_t* reach_upd);
+                        uint8_t* reach_add, uint8_t* reach_upd);
 
 // VxlanManager state after the epoch (kdtn_vni.hip; include/kdtn.h kdtn_epoch_vni_apply)
 struct VniOpsIn {
@@ -554,7 +554,9 @@ __global__ void k_vni_contest(const uint4* add_ops, uint32_t n_ops, const uint4*
                               uint32_t dmask, uint32_t* flag);
 __global__ void k_vni_contest_write(const uint4* add_ops, const uint32_t* flag, const uint64_t* pos, uint32_t n_ops,
                                     uint32_t* node, int32_t* vni);
-__global__ void k_fan_nodes_sort(const uint32_t* nlist, uint32_t* node_idx, uint32_t* nodes, uint32_t* n_nodes);
+__global__ void k_fan_nodes_count(const uint32_t* mark, uint32_t nd, uint32_t stamp, uint64_t* part);
+__global__ void k_fan_nodes_write(const uint32_t* mark, uint32_t nd, uint32_t stamp, const uint64_t* part,
+                                  uint32_t* node_idx, uint32_t* nodes, uint32_t* n_nodes);
 __global__ void k_fan_count(FanIn f, const uint8_t* send, const uint32_t* node_idx, const uint32_t* n_nodes,
                             uint32_t* counts, uint32_t nchunks);
 __global__ void k_fan_scatter(FanIn f, const uint8_t* send, const uint32_t* node_idx, const uint32_t* n_nodes,

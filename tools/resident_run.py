@@ -15,6 +15,9 @@ import torch  # noqa: F401  (one HIP runtime)
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "kube-dtn_amd"))
 import numpy as np  # noqa: E402
 
+if os.environ.get("KDTN_ALLOC_LOG"):                       # allocation log: profiling build only
+    from kdtn import engine as _e  # noqa: E402
+    _e.use_profiling_library()
 from kdtn import Engine, synth  # noqa: E402
 from kdtn.delta import build_delta  # noqa: E402
 from kdtn.engine import pin_delta  # noqa: E402
@@ -63,6 +66,7 @@ if a.pipeline:
         rows.append(r)
         print(json.dumps(r), flush=True)
     eng.download_wait()
+    eng.close()
     steady = rows[1:]
     print(json.dumps({"summary_excluding_first": {k: float(np.mean([r[k] for r in steady])) for k in rows[0] if k != "epoch"}}),
           flush=True)
@@ -90,3 +94,4 @@ steady = rows[1:] if len(rows) > 1 else rows
 print(json.dumps({"summary_excluding_first": {k: float(np.mean([r[k] for r in steady]))
                                               for k in ("upload_ms", "upload_GBps", "run_ms", "download_ms",
                                                         "commit_ms", "e2e_ms")}}), flush=True)
+eng.close()
