@@ -50,6 +50,7 @@ rows = []
 if a.pipeline:
     bufs = [BatchesOut.alloc(prev.topos.n, cap, cap, cap, pinned=True) for _ in range(2)]
     for ep, (d, T, N) in enumerate(deltas):
+        print(f"[resident_run] epoch {ep}", file=sys.stderr, flush=True)
         t0 = time.perf_counter()
         eng.upload_delta(d)
         t1 = time.perf_counter()
@@ -74,6 +75,7 @@ if a.pipeline:
 for ep, (d, T, N) in enumerate(deltas):
     if into is None or len(into.action) != T:
         into = BatchesOut.alloc(T, cap, cap, cap, pinned=True)
+    print(f"[resident_run] epoch {ep}", file=sys.stderr, flush=True)
     t0 = time.perf_counter()
     eng.upload_delta(d)
     t1 = time.perf_counter()
