@@ -723,12 +723,39 @@ __global__ void __launch_bounds__(BLOCK) k_js_validate(JsDoc j, const uint2* tok
 // Decodes the member name at string token pos (escapes included) into two little-endian
 // words; ok = false when it cannot equal a schema name (names are ASCII, at most 15 bytes).
 struct KeyName { uint64_t lo, hi; bool ok; };
-KD_INLINE KeyName key_name(const JsDoc& j, uint32_t pos) {
+// bit k (k < 4): byte k of w is c
+KD_INLINE uint32_t eq4(uint32_t w, uint32_t c) { return mm4(eqb(w, c)); }
+KD_INLINE KeyName key_name(const JsDoc& j, uint32_t pos, bool fast = true) {
     uint64_t lo = 0, hi = 0;
     uint32_t len = 0;
     // the three aligned words a plain name needs are loaded with the mask words (one round trip)
     const uint64_t* w = reinterpret_cast<const uint64_t*>(j.doc + ((pos + 1) & ~7u));
     const uint64_t w0 = w[0], w1 = w[1], w2 = w[2];
+    if (fast) {
+        // the name's first 17 bytes from those words: its closing quote and any backslash before
+        // it found by SWAR, so a plain name needs no mask words (no escape before the first quote
+        // means that quote ends the string; no quote in 17 bytes and no backslash means a name
+        // of 17+ bytes, which no schema name is)
+        const uint32_t sh = ((pos + 1) & 7u) * 8;
+        const uint64_t l = sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;
+        const uint64_t h = sh ? (w1 >> sh) | (w2 << (64 - sh)) : w1;
+        const uint32_t b16 = (uint32_t)((sh ? (w2 >> sh) : w2) & 0xFFu);
+        const uint32_t x[4] = {(uint32_t)l, (uint32_t)(l >> 32), (uint32_t)h, (uint32_t)(h >> 32)};
+        uint32_t Q = (b16 == '"') ? 1u << 16 : 0u, B = (b16 == '\\') ? 1u << 16 : 0u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            Q |= eq4(x[k], '"') << (4 * k);
+            B |= eq4(x[k], '\\') << (4 * k);
+        }
+        const uint32_t L = Q ? (uint32_t)__builtin_ctz(Q) : 17u;
+        if (!(B & ((1u << L) - 1u))) {                        // no escape before the end (or window)
+            if (L > 15u) return {0, 0, false};
+            uint64_t a = l, b = h;
+            if (L < 8) { a &= (1ull << (8 * L)) - 1; b = 0; }
+            else b &= L == 8 ? 0ull : (1ull << (8 * (L - 8))) - 1;
+            return {a, b, true};
+        }
+    }
     bool bs;
     const uint32_t e = str_end_bs(j, pos, &bs);
     if (e - pos - 1 > 6 * 16) return {0, 0, false};
@@ -1173,9 +1200,31 @@ KD_INLINE uint32_t intern(const JsIntern& in, const JsDict& dt, const uint8_t* p
 KD_INLINE uint32_t string_slot(const JsDoc& j, const JsIntern& in, const JsDict& dt, uint32_t i, uint32_t pos) {
     const uint32_t a = pos + 1;
     uint32_t pw[8];
-    load_window(j.doc, a, pw);                         // issued with the mask loads (one round trip)
-    bool bs, hb;
-    const uint32_t e = str_end_bs(j, pos, &bs, &hb);
+    load_window(j.doc, a, pw);
+    bool bs = false, hb = false;
+    uint32_t e = 0;
+    bool found = false;
+    if (!(KDTN_PROFILING && (in.variant & JSV_MASKS))) {
+        // a string that ends within the window: its closing quote, escapes and high bytes from
+        // the window itself (SWAR), no mask words (the first quote with no backslash before it
+        // is the end: a quote inside a string is always escaped)
+        uint32_t Q = 0, B = 0, H = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            Q |= mm4(eqb(pw[k], '"')) << (4 * k);
+            B |= mm4(eqb(pw[k], '\\')) << (4 * k);
+            H |= mm4(pw[k] & 0x80808080u) << (4 * k);
+        }
+        if (Q) {
+            const uint32_t L = (uint32_t)__builtin_ctz(Q), below = (1u << L) - 1u;   // L < 32
+            if (!(B & below)) {
+                e = a + L;
+                hb = (H & below) != 0;
+                found = true;
+            }
+        }
+    }
+    if (!found) e = str_end_bs(j, pos, &bs, &hb);
     if (e == a) return 0;
     if (!bs && !hb) {                                  // plain ASCII: the bytes themselves
         const uint32_t len = e - a;
@@ -1326,7 +1375,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, const uint2* toks,
     if (o >= JS_DEEP) { in.vown[k] = JS_NONE; return; }
     const uint32_t r = role[o];
     const uint32_t po = par[o];                        // the grandparent, loaded with the role
-    const KeyName kn = key_name(j, kpos);              // decoded while role[o] is in flight
+    const KeyName kn = key_name(j, kpos, !(KDTN_PROFILING && (in.variant & JSV_MASKS)));   // while role[o] is in flight
     if (r == R_NONE || r == R_ITEMS || r == R_SPEC_LINKS || r == R_STATUS_LINKS) { in.vown[k] = JS_NONE; return; }
     const uint32_t kind = tkind(t);
     const bool null = kind == TK_SCALAR && j.doc[t.x] == 'n';

@@ -615,7 +615,8 @@ enum : uint32_t { R_NONE = 0, R_ROOT, R_ITEMS, R_ITEM, R_META, R_SPEC, R_STATUS,
 constexpr uint32_t JS_ST_OVERFLOW = 1, JS_ST_LONG = 2;   // intern status bits
 // ingest variants (KDTN_JS_VARIANT, profiling build only; bits 1-3 give wrong tables)
 constexpr uint32_t JSV_COHERENT = 1, JSV_NO_SEEN = 2, JSV_NO_REP = 4, JSV_NO_INTERN = 8, JSV_NO_INLINE = 16,
-                   JSV_NO_INLINE_K = 32, JSV_NO_INLINE_P = 64;   // 16: neither dictionary, 32 / 64: keys / props
+                   JSV_NO_INLINE_K = 32, JSV_NO_INLINE_P = 64,   // 16: neither dictionary, 32 / 64: keys / props
+                   JSV_MASKS = 128;            // string ends from the mask words only (no window SWAR)
 
 struct JsDoc {
     const uint8_t* doc;        // padded with spaces to nb*64 (+64 B)

@@ -213,3 +213,20 @@ def test_window_strings(engine):
                 doc = (b'{"' + b"p" * pad + b'":"' + v + b'","items":[{"metadata":{"name":"' + v + b'",'
                        b'"namespace":"n"}}], "t":"' + b"w" * 40 + b'"}')
                 check_doc(engine, doc, f"string len {L} pad {pad} {v[:20]!r}")
+
+
+# Member names decoded from their first 17 bytes (key_name's SWAR path) or, with an escape before
+# the closing quote, by the byte loop: schema names spelled with escapes, names of 15-18 bytes,
+# an escaped quote inside a name, at several alignments.
+KEY_VARIANTS = [b"name", b"n\\u0061me", b"na\\u006de", b"\\u006eame", b"namespace", b"namespac\\u0065",
+                b"x" * 15, b"x" * 16, b"x" * 17, b"x" * 18, b'na\\"me', b"na\\\\me", b"nam", b"names",
+                b"peer_ip", b"peer\\u005fip", b"properties", b"propertie\\u0073", b"properties2", b"uid", b"u\\u0069d"]
+
+
+def test_window_keys(engine):
+    for k in KEY_VARIANTS:
+        for pad in (0, 1, 5, 7, 62):
+            doc = (b'{"' + b"p" * pad + b'":"z","items":[{"metadata":{"' + k + b'":"a","namespace":"n"},'
+                   b'"spec":{"links":[{"' + k + b'":"v","peer_pod":"q","uid":3,"properties":{"' + k +
+                   b'":"1ms","latency":"2ms"}}]}}]}')
+            check_doc(engine, doc, f"key {k!r} pad {pad}")
