@@ -2247,9 +2247,14 @@ static int json_decode(kdtn_ctx* c, const JsTargets& tg, JsCounts* o, kdtn_inges
         if (nval)
             k_js_values<<<nblocks(nval), BLOCK, 0, s>>>(j, toks, dp<uint32_t>(c->j_vlist), nval, par, role, ord, to,
                                                         des, real, in, small + 1);
-        if (nval && !(KDTN_PROFILING && (in.variant & JSV_NO_SEEN)))
+        if (nval && !(KDTN_PROFILING && (in.variant & JSV_NO_SEEN))) {
+            uint32_t* any_dup = reinterpret_cast<uint32_t*>(small + 5);   // zeroed with the small words
             k_js_dups<<<nblocks(nval), BLOCK, 0, s>>>(toks, dp<uint32_t>(c->j_vlist), nval, dp<uint32_t>(c->j_vown),
-                                                      dp<uint32_t>(c->j_owner), small + 1);
+                                                      dp<uint32_t>(c->j_owner), any_dup);
+            k_js_dups_report<<<std::min<uint32_t>(nblocks(nval), 2048), BLOCK, 0, s>>>(
+                toks, dp<uint32_t>(c->j_vlist), nval, dp<uint32_t>(c->j_vown), dp<uint32_t>(c->j_owner), any_dup,
+                small + 1);
+        }
         timer_mark(c, "js_values");
         unsigned long long ctl[3];
         TRY(d2h(c, ctl, small + 1, 3));

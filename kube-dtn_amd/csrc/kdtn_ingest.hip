@@ -1418,7 +1418,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, const uint2* toks,
     }
     }
     if (f < 0) { in.vown[k] = JS_NONE; return; }
-    // a plain store of this member's token index; k_js_dups then flags every member whose
+    // a plain store of this member's token index; k_js_dups then finds every member whose
     // (object, field) slot another member overwrote (no atomics on the hot path)
     own += bit;
     in.owner[own] = i;
@@ -1474,17 +1474,34 @@ __global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, const uint2* toks,
     if (!ok) js_fail(derr, t.x, KDTN_JSON_TYPE);
 }
 
-// a schema field repeated in one object: both members stored into the same owner slot and
-// only one of them can find itself there
+// A schema field repeated in one object: its members stored into the same owner slot and only
+// one of them finds itself there. Each other member lowers the slot to its own index, so the
+// slot ends at the group's first member (the plain store's winner included), and k_js_dups_report
+// then reports every later member at its key — the first repeat in document order is the
+// earliest, the position a sequential decoder stops at. `any` gates the report pass.
 __global__ void __launch_bounds__(BLOCK) k_js_dups(const uint2* toks, const uint32_t* vlist, uint32_t nval,
-                                                   const uint32_t* vown, const uint32_t* owner,
-                                                   unsigned long long* derr) {
+                                                   const uint32_t* vown, uint32_t* owner, uint32_t* any) {
     const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
     if (k >= nval) return;
     const uint32_t own = vown[k];
     if (own == JS_NONE) return;
     const uint32_t i = vlist[k];
-    if (owner[own] != i) js_fail(derr, toks[i - 2].x, KDTN_JSON_DUPKEY);
+    if (owner[own] != i) {
+        atomicMin(owner + own, i);
+        if (*any == 0) atomicOr(any, 1u);
+    }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_js_dups_report(const uint2* toks, const uint32_t* vlist, uint32_t nval,
+                                                          const uint32_t* vown, const uint32_t* owner,
+                                                          const uint32_t* any, unsigned long long* derr) {
+    if (*any == 0) return;
+    for (uint32_t k = blockIdx.x * BLOCK + threadIdx.x; k < nval; k += gridDim.x * BLOCK) {
+        const uint32_t own = vown[k];
+        if (own == JS_NONE) continue;
+        const uint32_t i = vlist[k];
+        if (owner[own] < i) js_fail(derr, toks[i - 2].x, KDTN_JSON_DUPKEY);
+    }
 }
 
 // ---------------------------------------------------------------- ids in first-occurrence order

@@ -705,7 +705,9 @@ __global__ void k_js_values(JsDoc j, const uint2* toks, const uint32_t* vlist, u
                             const uint8_t* role, const uint32_t* ord, JsTopoOut to, JsStore des, JsStore real,
                             JsIntern in, unsigned long long* derr);
 __global__ void k_js_dups(const uint2* toks, const uint32_t* vlist, uint32_t nval, const uint32_t* vown,
-                          const uint32_t* owner, unsigned long long* derr);
+                          uint32_t* owner, uint32_t* any);
+__global__ void k_js_dups_report(const uint2* toks, const uint32_t* vlist, uint32_t nval, const uint32_t* vown,
+                                 const uint32_t* owner, const uint32_t* any, unsigned long long* derr);
 __global__ void k_js_rep_mark(JsDict dt, uint32_t* bits);
 __global__ void k_js_popc(const uint32_t* bits, uint32_t nw, uint32_t* cnt);
 __global__ void k_js_ids(JsDict dt, const uint32_t* bits, const uint64_t* wrank, uint32_t* slot_id, uint32_t* len_by_id);
