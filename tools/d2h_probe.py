@@ -8,8 +8,12 @@ copies are DMA engine copies and which are blit kernels.
 """
 import ctypes as C
 import json
+import sys
 import time
 
+if "--torch" in sys.argv:                 # the engine's process has torch's HIP runtime loaded
+    import torch  # noqa: F401
+    torch.zeros(1, device="cuda")
 hip = C.CDLL("libamdhip64.so")
 hip.hipMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
 hip.hipHostMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t, C.c_uint]
@@ -39,10 +43,12 @@ def alloc_host(n, flags):
     return p
 
 
+hip.hipStreamCreateWithFlags.argtypes = [C.POINTER(C.c_void_p), C.c_uint]
 s1, s2 = C.c_void_p(), C.c_void_p()
-chk(hip.hipStreamCreate(C.byref(s1)))
-chk(hip.hipStreamCreate(C.byref(s2)))
-for mb in (4, 16, 64):
+flags = 1 if "--nonblocking" in sys.argv else 0      # hipStreamNonBlocking, as the engine's streams
+chk(hip.hipStreamCreateWithFlags(C.byref(s1), flags))
+chk(hip.hipStreamCreateWithFlags(C.byref(s2), flags))
+for mb in (1, 4, 16, 64):
     n = mb << 20
     d_src, d_dst = alloc_dev(n), alloc_dev(n)
     h_up = alloc_host(n, 0)
