@@ -14,7 +14,7 @@ from kdtn import Engine, abi, synth
 from kdtn.delta import build_delta
 from kdtn.engine import pin_delta
 from kdtn.model import pack
-from kdtn.tables import EpochInput, Interner, Topos
+from kdtn.tables import EpochInput, Interner, Links, Topos
 from state import apply_delta, commit, predicted_commit, same_tables
 from test_state_cpu import mutate
 
@@ -271,3 +271,55 @@ def test_async_download_pipelined_chain():
         eng.download_wait()
         got, want = pend
         assert not got.mismatches(want)
+
+
+class _ScatteredLinks(Links):
+    """The same records with no two columns adjacent in host memory (each id column, the gap
+    and the uid in one buffer, in reverse column order with a gap between them), so a delta
+    upload copies every column on its own and places each as it arrives."""
+
+    def to_c(self) -> abi.LinkTable:
+        n = self.n
+        w = n + 16
+        buf = np.zeros((abi.NKEY + abi.NPROP + 1) * w, np.uint32)
+        cols = [self.key[k] for k in range(abi.NKEY)] + [self.prop[k] for k in range(abi.NPROP)] + [self.gap]
+        views = []
+        for c, a in enumerate(cols):
+            at = (len(cols) - 1 - c) * w
+            buf[at:at + n] = a
+            views.append(buf[at:at + n])
+        self._buf, self._uid = buf, np.array(self.uid, np.int64)
+        t = abi.LinkTable()
+        t.n = n
+        for k in range(abi.NKEY):
+            t.key[k] = abi.ptr(views[k], abi.u32p)
+        for k in range(abi.NPROP):
+            t.prop[k] = abi.ptr(views[abi.NKEY + k], abi.u32p)
+        t.gap = abi.ptr(views[-1], abi.u32p)
+        t.uid = abi.ptr(self._uid, abi.i64p)
+        return t
+
+
+def test_delta_records_in_separate_columns():
+    """Churn epochs whose inline records come as 20 separate column arrays (plus the uid): every
+    column is its own copy and its own placement launch; tables and batches stay exact."""
+    cs = synth.ChurnSequence(total_pods=20000)
+    prev = cs.epoch_input(copy=True)
+    with Engine(device=0, tick_in_usec=TICK) as eng:
+        eng.upload(prev)
+        _run_same(eng, prev, "epoch 0")
+        state = prev
+        for ep in range(1, 5):
+            eng.commit(np.ones(state.topos.n, bool))
+            state = commit(state, np.ones(state.topos.n, bool))
+            cs.advance()
+            new = cs.epoch_input(copy=True)
+            d = build_delta(state, new, state.kdict.n, state.pdict.n)
+            r = d.records
+            if ep % 2:
+                d = copy.copy(d)
+                d.records = _ScatteredLinks(r.key, r.uid, r.prop, r.gap)
+            eng.upload_delta(d)
+            state = apply_delta(state, d)
+            assert not same_tables(eng.tables(), state), ep
+            _run_same(eng, state, f"epoch {ep} ({'separate' if ep % 2 else 'adjacent'} columns)")
