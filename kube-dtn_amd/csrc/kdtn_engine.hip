@@ -169,7 +169,7 @@ struct kdtn_ctx {
     DevBuf j_tflags, j_owner, j_vown, j_kslots, j_krep, j_pslots, j_prep, j_heap;
     DevBuf j_kkeys, j_pkeys;     // dense key words of the intern tables
     DevBuf j_rows;               // row-major staging of the decoded link records (JS_ROW words each)
-    DevBuf j_bits, j_bcnt, j_wrank, j_kslot_id, j_pslot_id, j_len, j_off64;
+    DevBuf j_bits, j_bcnt, j_wrank, j_kslot_id, j_pslot_id, j_len, j_off64, j_sofid;
     uint64_t j_n = 0;
     uint32_t j_nb = 0;
     bool j_loaded = false, j_done = false;
@@ -899,7 +899,7 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->j_role, &c->j_ecls, &c->j_odep, &c->j_ord, &c->j_tagg, &c->j_gagg, &c->j_cnt3, &c->j_coff3, &c->j_small,
                       &c->j_part, &c->j_tflags, &c->j_owner, &c->j_rows, &c->j_kkeys, &c->j_pkeys, &c->j_vown, &c->j_kslots, &c->j_krep,
                       &c->j_pslots, &c->j_prep, &c->j_heap, &c->j_bits, &c->j_bcnt, &c->j_wrank,
-                      &c->j_kslot_id, &c->j_pslot_id, &c->j_len, &c->j_off64, &c->j_ocnt, &c->j_ooff,
+                      &c->j_kslot_id, &c->j_pslot_id, &c->j_len, &c->j_off64, &c->j_sofid, &c->j_ocnt, &c->j_ooff,
                       &c->j_olist, &c->j_ccnt, &c->j_coff, &c->j_vlist, &c->sh_keep, &c->sh_kreal,
                       &c->sh_kdes, &c->sh_tidx, &c->sh_roff64, &c->sh_noff64, &c->sh_doc, &c->sh_ns,
                       &c->sh_name, &c->sh_src, &c->sh_netns, &c->sh_flags, &c->sh_roff, &c->sh_noff,
@@ -2002,9 +2002,10 @@ int json_dict(kdtn_ctx* c, const JsDict& dt, const JsIntern& in, uint32_t ntok, 
     TRY(ensure(slot_id, (size_t)cap * 4));
     TRY(ensure(c->j_len, (size_t)n * 4));
     TRY(ensure(c->j_off64, ((size_t)n + 1) * 8));
+    TRY(ensure(c->j_sofid, (size_t)n * 4));
     HIP_TRY(hipMemsetAsync(c->j_len.p, 0, (size_t)n * 4, s));
     k_js_ids<<<nblocks(cap), BLOCK, 0, s>>>(dt, dp<uint32_t>(c->j_bits), dp<uint64_t>(c->j_wrank),
-                                            dp<uint32_t>(slot_id), dp<uint32_t>(c->j_len));
+                                            dp<uint32_t>(slot_id), dp<uint32_t>(c->j_len), dp<uint32_t>(c->j_sofid));
     TRY(scan_u32(c, dp<uint32_t>(c->j_len), n, dp<uint64_t>(c->j_off64)));
     timer_mark(c, "js_intern");
     uint64_t total = 0;
@@ -2020,8 +2021,9 @@ int json_dict(kdtn_ctx* c, const JsDict& dt, const JsIntern& in, uint32_t ntok, 
     TRY(ensure(offs, ((size_t)n + 1) * 4));
     HIP_TRY(hipMemsetAsync(offs.p, 0, 4, s));
     HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(dp<uint32_t>(offs) + n), (int)(uint32_t)total, 1, s));
-    k_js_dict_copy<<<nblocks(cap), BLOCK, 0, s>>>(dt, in, dp<uint32_t>(slot_id), dp<uint64_t>(c->j_off64),
-                                                  dp<uint32_t>(offs), dp<uint8_t>(bytes));
+    if (n > 1)
+        k_js_dict_copy<<<nblocks(n - 1), BLOCK, 0, s>>>(dt, in, dp<uint32_t>(c->j_sofid), n, dp<uint64_t>(c->j_off64),
+                                                        dp<uint32_t>(offs), dp<uint8_t>(bytes));
     *n_out = n;
     *bytes_out = total;
     return KDTN_OK;

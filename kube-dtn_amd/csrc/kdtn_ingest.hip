@@ -1517,9 +1517,9 @@ __global__ void __launch_bounds__(BLOCK) k_js_popc(const uint32_t* bits, uint32_
     if (w < nw) cnt[w] = __popc(bits[w]);
 }
 
-// per slot: id = 1 + rank of its first occurrence; length by id
+// per slot: id = 1 + rank of its first occurrence; length by id, and the slot of each id
 __global__ void __launch_bounds__(BLOCK) k_js_ids(JsDict dt, const uint32_t* bits, const uint64_t* wrank,
-                                                  uint32_t* slot_id, uint32_t* len_by_id) {
+                                                  uint32_t* slot_id, uint32_t* len_by_id, uint32_t* slot_of_id) {
     const uint32_t s = blockIdx.x * BLOCK + threadIdx.x;
     if (s > dt.mask) return;
     const unsigned long long kw = dt.keys[s];
@@ -1528,15 +1528,17 @@ __global__ void __launch_bounds__(BLOCK) k_js_ids(JsDict dt, const uint32_t* bit
     const uint32_t id = 1u + (uint32_t)wrank[occ >> 5] + __popc(bits[occ >> 5] & ((1u << (occ & 31)) - 1u));
     slot_id[s] = id;
     len_by_id[id] = (uint32_t)(kw >> 32) & 0xFFFFFFu;
+    slot_of_id[id] = s;
 }
 
-__global__ void __launch_bounds__(BLOCK) k_js_dict_copy(JsDict dt, JsIntern in, const uint32_t* slot_id,
+// One thread per id (1 .. n-1), in id order: consecutive threads write consecutive arena
+// ranges, and first occurrences in id order sit in document order, so both the reads and the
+// writes of a wave stay within a few lines (one thread per hash slot scattered both).
+__global__ void __launch_bounds__(BLOCK) k_js_dict_copy(JsDict dt, JsIntern in, const uint32_t* slot_of_id, uint32_t n,
                                                         const uint64_t* off64, uint32_t* offs, uint8_t* arena) {
-    const uint32_t s = blockIdx.x * BLOCK + threadIdx.x;
-    if (s > dt.mask) return;
-    const unsigned long long kw = dt.keys[s];
-    if (kw == 0) return;
-    const uint32_t id = slot_id[s];
+    const uint32_t id = 1u + blockIdx.x * BLOCK + threadIdx.x;
+    if (id >= n) return;
+    const unsigned long long kw = dt.keys[slot_of_id[id]];
     const uint32_t len = (uint32_t)(kw >> 32) & 0xFFFFFFu;
     const uint64_t at = off64[id];
     offs[id] = (uint32_t)at;
@@ -1552,6 +1554,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_dict_copy(JsDict dt, JsIntern in, 
     for (uint32_t k = 0; k < len; ++k) arena[at + k] = src[k];
 }
 
+// slot + 1 → id in every id column; topology flags to bytes
 // One workgroup per tile: the 64 staged rows (5.5 KB, read with 16-B loads) through LDS into
 // the tile's columns (coalesced stores), slot + 1 → id in the id columns (records past n are
 // zero rows, so the tail of the last tile is written too).

@@ -710,9 +710,10 @@ __global__ void k_js_dups_report(const uint2* toks, const uint32_t* vlist, uint3
                                  const uint32_t* owner, const uint32_t* any, unsigned long long* derr);
 __global__ void k_js_rep_mark(JsDict dt, uint32_t* bits);
 __global__ void k_js_popc(const uint32_t* bits, uint32_t nw, uint32_t* cnt);
-__global__ void k_js_ids(JsDict dt, const uint32_t* bits, const uint64_t* wrank, uint32_t* slot_id, uint32_t* len_by_id);
-__global__ void k_js_dict_copy(JsDict dt, JsIntern in, const uint32_t* slot_id, const uint64_t* off64, uint32_t* offs,
-                               uint8_t* arena);
+__global__ void k_js_ids(JsDict dt, const uint32_t* bits, const uint64_t* wrank, uint32_t* slot_id, uint32_t* len_by_id,
+                         uint32_t* slot_of_id);
+__global__ void k_js_dict_copy(JsDict dt, JsIntern in, const uint32_t* slot_of_id, uint32_t n, const uint64_t* off64,
+                               uint32_t* offs, uint8_t* arena);
 __global__ void k_js_finalize_links(const uint32_t* rows, uint32_t* tiles, const uint32_t* kslot_id,
                                     const uint32_t* pslot_id);
 __global__ void k_js_finalize_topos(JsTopoOut to, uint32_t T, const uint32_t* kslot_id, uint8_t* flags8);
