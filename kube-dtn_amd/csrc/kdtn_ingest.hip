@@ -659,11 +659,13 @@ __global__ void __launch_bounds__(BLOCK) k_js_validate(JsDoc j, const uint2* tok
     const uint32_t ck = d == 0 ? 0xFFu : pkind;                   // container kind
     bool ok;
     {
-        // element candidate (see k_js_elems_count), from the staged neighbours:
-        // k_js_elems_count then reads one byte per token instead of the token stream
+        // element candidate (see k_js_elems_count), from the staged neighbours, with its value's
+        // class (1 object, 2 null, 3 anything else): k_js_elems_count then reads one byte per
+        // token instead of the token stream, and the element's own token only for an error
         const uint32_t pk = i ? tkind(st[threadIdx.x + 1]) : 0xFFu;
-        ecand[i] = (uint8_t)(i != 0 && (d == 2 || d == 5) && (pk == TK_ARR || pk == TK_COMMA) && value_start(kind) &&
-                             p < JS_DEEP && pkind == TK_ARR);
+        const bool cand = i != 0 && (d == 2 || d == 5) && (pk == TK_ARR || pk == TK_COMMA) && value_start(kind) &&
+                          p < JS_DEEP && pkind == TK_ARR;
+        ecand[i] = (uint8_t)(!cand ? 0u : kind == TK_OBJ ? 1u : (kind == TK_SCALAR && j.doc[pos] == 'n') ? 2u : 3u);
     }
     if (i == 0) {
         ok = value_start(kind) && d == 0;
@@ -903,15 +905,14 @@ __global__ void __launch_bounds__(BLOCK) k_js_elems_count(JsDoc j, const uint2* 
 #pragma unroll
         for (int h = 0; h < 4; ++h) {
             const uint32_t i = base + q * 4 + h;
-            if (i >= ntok || !((w[q] >> (8 * h)) & 0xFFu)) continue;
+            const uint32_t vc = (w[q] >> (8 * h)) & 0xFFu;             // k_js_validate's value class
+            if (i >= ntok || !vc) continue;
             const uint32_t r = role[par[i]];
             const uint32_t cls = r == R_ITEMS ? 1 : r == R_SPEC_LINKS ? 2 : r == R_STATUS_LINKS ? 3 : 0;
             w[q] = (w[q] & ~(0xFFu << (8 * h))) | (cls << (8 * h));   // the class, for k_js_elems_write
             changed = true;
             if (!cls) continue;
-            const uint2 t = toks[i];
-            const uint32_t kind = tkind(t);
-            if (!(kind == TK_OBJ || (kind == TK_SCALAR && j.doc[t.x] == 'n'))) js_fail(derr, t.x, KDTN_JSON_TYPE);
+            if (vc == 3u) js_fail(derr, toks[i].x, KDTN_JSON_TYPE);     // neither an object nor null
             c[cls - 1]++;
         }
     }
