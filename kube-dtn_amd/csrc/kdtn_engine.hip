@@ -163,7 +163,7 @@ struct kdtn_ctx {
     bool tc_done = false;
     // CR ingest (kdtn_ingest.hip): document, block masks, token stream, decode scratch
     DevBuf j_doc, j_q, j_bs, j_hb, j_qcnt, j_qoff, j_tok, j_open, j_close, j_tcnt, j_dcnt, j_toff, j_doff;
-    DevBuf j_ocnt, j_ooff, j_olist, j_ccnt, j_coff, j_vlist;
+    DevBuf j_ocnt, j_ooff, j_olist, j_ccnt, j_coff, j_vlist, j_scnt, j_soff, j_slist;
     uint32_t j_kcap = 0, j_pcap = 0;   // intern table sizes that fit the last document
     DevBuf j_toks, j_par, j_role, j_ecls, j_odep, j_ord, j_tagg, j_gagg, j_cnt3, j_coff3, j_small, j_part;
     DevBuf j_tflags, j_owner, j_vown, j_kslots, j_krep, j_pslots, j_prep, j_heap;
@@ -900,7 +900,7 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->j_part, &c->j_tflags, &c->j_owner, &c->j_rows, &c->j_kkeys, &c->j_pkeys, &c->j_vown, &c->j_kslots, &c->j_krep,
                       &c->j_pslots, &c->j_prep, &c->j_heap, &c->j_bits, &c->j_bcnt, &c->j_wrank,
                       &c->j_kslot_id, &c->j_pslot_id, &c->j_len, &c->j_off64, &c->j_sofid, &c->j_ocnt, &c->j_ooff,
-                      &c->j_olist, &c->j_ccnt, &c->j_coff, &c->j_vlist, &c->sh_keep, &c->sh_kreal,
+                      &c->j_olist, &c->j_ccnt, &c->j_coff, &c->j_vlist, &c->j_scnt, &c->j_soff, &c->j_slist, &c->sh_keep, &c->sh_kreal,
                       &c->sh_kdes, &c->sh_tidx, &c->sh_roff64, &c->sh_noff64, &c->sh_doc, &c->sh_ns,
                       &c->sh_name, &c->sh_src, &c->sh_netns, &c->sh_flags, &c->sh_roff, &c->sh_noff,
                       &c->sh_des.buf, &c->sh_real.buf, &c->vx_ops, &c->vx_dead, &c->vx_slots, &c->vx_node,
@@ -2080,13 +2080,16 @@ static int json_decode(kdtn_ctx* c, const JsTargets& tg, JsCounts* o, kdtn_inges
     HIP_TRY(hipMemsetAsync(small + 2, 0, J_SMALL - 16, s));
     // one word past the end: any_in reads the word after a string's first (its bits are masked)
     for (DevBuf* b : {&c->j_q, &c->j_bs, &c->j_hb, &c->j_tok, &c->j_open, &c->j_close}) TRY(ensure(*b, ((size_t)nb + 1) * 8));
-    for (DevBuf* b : {&c->j_qcnt, &c->j_tcnt, &c->j_dcnt, &c->j_ocnt, &c->j_ccnt}) TRY(ensure(*b, (size_t)nb * 4));
-    for (DevBuf* b : {&c->j_qoff, &c->j_toff, &c->j_doff, &c->j_ooff, &c->j_coff})
+    for (DevBuf* b : {&c->j_qcnt, &c->j_tcnt, &c->j_dcnt, &c->j_ocnt, &c->j_ccnt, &c->j_scnt}) TRY(ensure(*b, (size_t)nb * 4));
+    for (DevBuf* b : {&c->j_qoff, &c->j_toff, &c->j_doff, &c->j_ooff, &c->j_coff, &c->j_soff})
         TRY(ensure(*b, ((size_t)nb + 1) * 8));
     JsDoc j{dp<uint8_t>(c->j_doc), (uint32_t)c->j_n, nb, dp<uint64_t>(c->j_q), dp<uint64_t>(c->j_bs),
-            dp<uint64_t>(c->j_hb)};
+            dp<uint64_t>(c->j_hb), 0u};
+#if KDTN_PROFILING
+    j.variant = (uint32_t)std::strtoul(std::getenv("KDTN_JS_VARIANT") ? std::getenv("KDTN_JS_VARIANT") : "0", nullptr, 0);
+#endif
     JsMasks m{dp<uint64_t>(c->j_tok), dp<uint64_t>(c->j_open), dp<uint64_t>(c->j_close), dp<uint32_t>(c->j_tcnt),
-              dp<uint32_t>(c->j_dcnt), dp<uint32_t>(c->j_ocnt), dp<uint32_t>(c->j_ccnt)};
+              dp<uint32_t>(c->j_dcnt), dp<uint32_t>(c->j_ocnt), dp<uint32_t>(c->j_ccnt), dp<uint32_t>(c->j_scnt)};
 
     // 1. block masks, string state, token counts, depth
     k_js_quotes<<<nblocks(nb), BLOCK, 0, s>>>(j, dp<uint64_t>(c->j_q), dp<uint64_t>(c->j_bs), dp<uint64_t>(c->j_hb),
@@ -2097,11 +2100,14 @@ static int json_decode(kdtn_ctx* c, const JsTargets& tg, JsCounts* o, kdtn_inges
     TRY(scan_u32(c, dp<uint32_t>(c->j_dcnt), nb, dp<uint64_t>(c->j_doff)));
     TRY(scan_u32(c, dp<uint32_t>(c->j_ocnt), nb, dp<uint64_t>(c->j_ooff)));
     TRY(scan_u32(c, dp<uint32_t>(c->j_ccnt), nb, dp<uint64_t>(c->j_coff)));
+    TRY(scan_u32(c, dp<uint32_t>(c->j_scnt), nb, dp<uint64_t>(c->j_soff)));
     timer_mark(c, "js_blocks");
     uint64_t quotes = 0, ntok64 = 0, nopen64 = 0;
     TRY(d2h(c, &nopen64, dp<uint64_t>(c->j_ooff) + nb));
     uint64_t nval64 = 0;
     TRY(d2h(c, &nval64, dp<uint64_t>(c->j_coff) + nb));
+    uint64_t nscal64 = 0;
+    TRY(d2h(c, &nscal64, dp<uint64_t>(c->j_soff) + nb));
     unsigned long long serr = 0;
     TRY(d2h(c, &quotes, dp<uint64_t>(c->j_qoff) + nb));
     TRY(d2h(c, &ntok64, dp<uint64_t>(c->j_toff) + nb));
@@ -2126,11 +2132,14 @@ static int json_decode(kdtn_ctx* c, const JsTargets& tg, JsCounts* o, kdtn_inges
     TRY(ensure(c->j_odep, (size_t)nopen));
     const uint32_t nval = (uint32_t)nval64;
     TRY(ensure(c->j_vlist, (size_t)nval * 4));
+    const uint32_t nscal = (uint32_t)nscal64;
+    TRY(ensure(c->j_slist, (size_t)nscal * 4 + 4));
     const uint2* toks = dp<uint2>(c->j_toks);
     uint32_t* par = dp<uint32_t>(c->j_par);
     k_js_tokens<<<nblocks(nb), BLOCK, 0, s>>>(j, m, dp<uint64_t>(c->j_toff), dp<uint64_t>(c->j_doff),
-                                             dp<uint64_t>(c->j_ooff), dp<uint64_t>(c->j_coff), dp<uint2>(c->j_toks),
-                                             dp<uint32_t>(c->j_olist), dp<uint32_t>(c->j_vlist), small);
+                                             dp<uint64_t>(c->j_ooff), dp<uint64_t>(c->j_coff), dp<uint64_t>(c->j_soff),
+                                             dp<uint2>(c->j_toks), dp<uint32_t>(c->j_olist), dp<uint32_t>(c->j_vlist),
+                                             dp<uint32_t>(c->j_slist), small);
     timer_mark(c, "js_tokens");
     const uint32_t ntiles = (ntok + JS_TILE - 1) / JS_TILE, ng = (ntiles + BLOCK - 1) / BLOCK;
     TRY(ensure(c->j_tagg, (size_t)ntiles * JS_PD * 4));
@@ -2144,6 +2153,7 @@ static int json_decode(kdtn_ctx* c, const JsTargets& tg, JsCounts* o, kdtn_inges
     k_js_deep<<<std::min<uint32_t>(nblocks(ntok), 2048), BLOCK, 0, s>>>(toks, ntok, par, deep);
     timer_mark(c, "js_parents");
     k_js_validate<<<nblocks(ntok), BLOCK, 0, s>>>(j, toks, ntok, par, dp<uint8_t>(c->j_ecls), small);
+    if (nscal) k_js_scalars<<<nblocks(nscal), BLOCK, 0, s>>>(j, toks, dp<uint32_t>(c->j_slist), nscal, small);
     timer_mark(c, "js_validate");
     TRY(d2h(c, &serr, small));
     HIP_TRY(hipStreamSynchronize(s));

@@ -184,6 +184,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_classify(JsDoc j, const uint64_t* 
     m.dcnt[b] = 64u + __popcll(op & out) - __popcll(cl & out);
     m.ocnt[b] = __popcll(op & out);
     m.ccnt[b] = __popcll(colon & out);
+    m.scnt[b] = __popcll(scalar_start);
 }
 
 // ---------------------------------------------------------------- k_js_tokens
@@ -217,12 +218,13 @@ KD_INLINE uint32_t select_bit(uint64_t m, uint32_t r) {
 // search over the wave's token prefix, bit by select): coalesced 8-byte stores instead of
 // every lane walking its own block's tokens into its own region.
 __global__ void __launch_bounds__(BLOCK) k_js_tokens(JsDoc j, JsMasks m, const uint64_t* toff, const uint64_t* doff,
-                                                     const uint64_t* ooff, const uint64_t* coff, uint2* toks,
-                                                     uint32_t* olist, uint32_t* vlist, unsigned long long* err) {
+                                                     const uint64_t* ooff, const uint64_t* coff, const uint64_t* soff,
+                                                     uint2* toks, uint32_t* olist, uint32_t* vlist, uint32_t* slist,
+                                                     unsigned long long* err) {
     __shared__ uint4 blk[BLOCK * 4];
-    __shared__ uint64_t stok[BLOCK], sop[BLOCK], scl[BLOCK], scol[BLOCK];
+    __shared__ uint64_t stok[BLOCK], sop[BLOCK], scl[BLOCK], scol[BLOCK], ssc[BLOCK];
     __shared__ int64_t sd0[BLOCK];
-    __shared__ uint32_t sex[BLOCK], soo[BLOCK], sco[BLOCK];
+    __shared__ uint32_t sex[BLOCK], soo[BLOCK], sco[BLOCK], sso[BLOCK];
     const uint32_t lane = threadIdx.x & 63u, w0 = threadIdx.x & ~63u;
     const uint32_t b = blockIdx.x * BLOCK + threadIdx.x;
     uint64_t tok = 0, ti = 0;
@@ -238,15 +240,22 @@ __global__ void __launch_bounds__(BLOCK) k_js_tokens(JsDoc j, JsMasks m, const u
         sd0[threadIdx.x] = (int64_t)doff[b] - 64ll * b;
         soo[threadIdx.x] = (uint32_t)ooff[b];
         sco[threadIdx.x] = (uint32_t)coff[b];
-        uint64_t col = 0;
+        sso[threadIdx.x] = (uint32_t)soff[b];
+        uint64_t col = 0, nsc = 0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             blk[threadIdx.x * 4 + q] = v[q];
             const uint32_t wd[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
 #pragma unroll
-            for (int h = 0; h < 4; ++h) col |= (uint64_t)mm4(eqb(wd[h], ':')) << (4 * (q * 4 + h));
+            for (int h = 0; h < 4; ++h) {
+                const uint32_t x = wd[h], lx = x | 0x20202020u;       // '[' → '{', ']' → '}'
+                const uint32_t cn = mm4(eqb(x, ':'));
+                col |= (uint64_t)cn << (4 * (q * 4 + h));
+                nsc |= (uint64_t)(cn | mm4(eqb(lx, '{') | eqb(lx, '}') | eqb(x, ',') | eqb(x, '"'))) << (4 * (q * 4 + h));
+            }
         }
         scol[threadIdx.x] = col & tok;                 // structural colons
+        ssc[threadIdx.x] = tok & ~nsc;                 // scalar token starts (the token's first byte)
     }
     stok[threadIdx.x] = tok;
     const uint32_t cnt = __popcll(tok);
@@ -282,6 +291,8 @@ __global__ void __launch_bounds__(BLOCK) k_js_tokens(JsDoc j, JsMasks m, const u
             olist[soo[o] + __popcll(sop[o] & below)] = idx;
         } else if (kind == TK_COLON) {
             vlist[sco[o] + __popcll(scol[o] & below)] = idx + 1;   // the member value follows its colon
+        } else if (kind == TK_SCALAR) {
+            slist[sso[o] + __popcll(ssc[o] & below)] = idx;         // checked by k_js_scalars
         }
         if (d > (int64_t)TK_DEPTH_MASK) d = TK_DEPTH_MASK;
         toks[idx] = make_uint2(pos, (uint32_t)d | (kind << 24));
@@ -696,11 +707,9 @@ __global__ void __launch_bounds__(BLOCK) k_js_validate(JsDoc j, const uint2* tok
     if (ok && i == ntok - 1) {                                    // the document ends here
         ok = (kind == TK_STR || kind == TK_SCALAR) ? d == 0 : ((kind == TK_OBJ_END || kind == TK_ARR_END) && d == 1);
     }
-    if (ok && kind == TK_SCALAR) {
-        const int w = valid_scalar_window(j, pos);
-        ok = w >= 0 ? w != 0 : valid_scalar(j, pos);
-    }
-    if (ok && kind == TK_STR) {
+    // (a scalar's own grammar is checked by k_js_scalars over the compacted list of scalar
+    // tokens: here, one scalar in a wave of 64 tokens made the whole wave run its check)
+    if (ok && kind == TK_STR && !(KDTN_PROFILING && (j.variant & JSV_NO_STRCHK))) {
         bool bs;
         const uint32_t e = str_end_bs(j, pos, &bs);
         if (bs) {                                                 // escapes: \" \\ \/ \b \f \n \r \t \uXXXX
@@ -719,6 +728,17 @@ __global__ void __launch_bounds__(BLOCK) k_js_validate(JsDoc j, const uint2* tok
         }
     }
     if (!ok) js_fail(err, pos, KDTN_JSON_SYNTAX);
+}
+
+// checkValid's literal / number grammar for every scalar token, over the list k_js_tokens
+// compacted (full waves of scalars instead of one scalar lane per token wave)
+__global__ void __launch_bounds__(BLOCK) k_js_scalars(JsDoc j, const uint2* toks, const uint32_t* slist, uint32_t nscal,
+                                                      unsigned long long* err) {
+    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+    if (k >= nscal || (KDTN_PROFILING && (j.variant & JSV_NO_SCALAR))) return;
+    const uint32_t pos = toks[slist[k]].x;
+    const int w = valid_scalar_window(j, pos);
+    if (!(w >= 0 ? w != 0 : valid_scalar(j, pos))) js_fail(err, pos, KDTN_JSON_SYNTAX);
 }
 
 // ---------------------------------------------------------------- key matching

@@ -616,7 +616,8 @@ constexpr uint32_t JS_ST_OVERFLOW = 1, JS_ST_LONG = 2;   // intern status bits
 // ingest variants (KDTN_JS_VARIANT, profiling build only; bits 1-3 give wrong tables)
 constexpr uint32_t JSV_COHERENT = 1, JSV_NO_SEEN = 2, JSV_NO_REP = 4, JSV_NO_INTERN = 8, JSV_NO_INLINE = 16,
                    JSV_NO_INLINE_K = 32, JSV_NO_INLINE_P = 64,   // 16: neither dictionary, 32 / 64: keys / props
-                   JSV_MASKS = 128;            // string ends from the mask words only (no window SWAR)
+                   JSV_MASKS = 128,            // string ends from the mask words only (no window SWAR)
+                   JSV_NO_STRCHK = 256, JSV_NO_SCALAR = 512;   // k_js_validate without string / scalar checks
 
 struct JsDoc {
     const uint8_t* doc;        // padded with spaces to nb*64 (+64 B)
@@ -625,6 +626,7 @@ struct JsDoc {
     const uint64_t* qmask;     // unescaped quotes
     const uint64_t* bsmask;    // backslashes
     const uint64_t* hbmask;    // bytes >= 0x80
+    uint32_t variant;          // (profiling build) KDTN_JS_VARIANT bits, 0 otherwise
 };
 struct JsMasks {
     uint64_t* tok;             // token starts
@@ -634,6 +636,7 @@ struct JsMasks {
     uint32_t* dcnt;            // 64 + opens - closes per block
     uint32_t* ocnt;            // opens per block
     uint32_t* ccnt;            // colons per block
+    uint32_t* scnt;            // scalar tokens per block
 };
 struct JsTopoOut {
     uint32_t* ns;
@@ -685,8 +688,9 @@ struct JsIntern {
 __global__ void k_js_quotes(JsDoc j, uint64_t* qmask, uint64_t* bsmask, uint64_t* hbmask, uint32_t* qcnt);
 __global__ void k_js_classify(JsDoc j, const uint64_t* qoff, JsMasks m, unsigned long long* err);
 __global__ void k_js_tokens(JsDoc j, JsMasks m, const uint64_t* toff, const uint64_t* doff, const uint64_t* ooff,
-                            const uint64_t* coff, uint2* toks, uint32_t* olist, uint32_t* vlist,
-                            unsigned long long* err);
+                            const uint64_t* coff, const uint64_t* soff, uint2* toks, uint32_t* olist, uint32_t* vlist,
+                            uint32_t* slist, unsigned long long* err);
+__global__ void k_js_scalars(JsDoc j, const uint2* toks, const uint32_t* slist, uint32_t nscal, unsigned long long* err);
 __global__ void k_js_par_agg(const uint2* toks, uint32_t ntok, uint32_t* tagg);
 __global__ void k_js_par_group(const uint32_t* tagg, uint32_t ntiles, uint32_t* gagg);
 __global__ void k_js_par_top(uint32_t* gagg, uint32_t ng);
