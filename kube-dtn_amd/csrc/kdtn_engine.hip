@@ -2138,8 +2138,8 @@ static int json_decode(kdtn_ctx* c, const JsTargets& tg, JsCounts* o, kdtn_inges
     uint32_t* par = dp<uint32_t>(c->j_par);
     k_js_tokens<<<nblocks(nb), BLOCK, 0, s>>>(j, m, dp<uint64_t>(c->j_toff), dp<uint64_t>(c->j_doff),
                                              dp<uint64_t>(c->j_ooff), dp<uint64_t>(c->j_coff), dp<uint64_t>(c->j_soff),
-                                             dp<uint2>(c->j_toks), dp<uint32_t>(c->j_olist), dp<uint32_t>(c->j_vlist),
-                                             dp<uint32_t>(c->j_slist), small);
+                                             dp<uint2>(c->j_toks), dp<uint32_t>(c->j_olist), dp<uint8_t>(c->j_odep),
+                                             dp<uint32_t>(c->j_vlist), dp<uint32_t>(c->j_slist), small);
     timer_mark(c, "js_tokens");
     const uint32_t ntiles = (ntok + JS_TILE - 1) / JS_TILE, ng = (ntiles + BLOCK - 1) / BLOCK;
     TRY(ensure(c->j_tagg, (size_t)ntiles * JS_PD * 4));
@@ -2165,13 +2165,16 @@ static int json_decode(kdtn_ctx* c, const JsTargets& tg, JsCounts* o, kdtn_inges
     uint8_t* role = dp<uint8_t>(c->j_role);
     uint32_t* ord = dp<uint32_t>(c->j_ord);
     HIP_TRY(hipMemsetAsync(role, 0, ntok, s));                  // R_NONE below the schema levels
-    for (uint32_t level = 0; level <= 6 && nopen; ++level)
-        k_js_roles<<<nblocks(nopen), BLOCK, 0, s>>>(j, toks, dp<uint32_t>(c->j_olist), nopen, par, role,
+    for (uint32_t level : {0u, 1u, 3u, 4u})            // levels 2 and 5: k_js_elems_count
+        if (nopen) k_js_roles<<<nblocks(nopen), BLOCK, 0, s>>>(j, toks, dp<uint32_t>(c->j_olist), nopen, par, role,
                                                     dp<uint8_t>(c->j_odep), level);
     TRY(ensure(c->j_cnt3, (size_t)3 * ntiles * 4));
     TRY(ensure(c->j_coff3, (size_t)3 * (ntiles + 1) * 8));
     k_js_elems_count<<<ntiles, BLOCK, 0, s>>>(j, toks, ntok, par, role, dp<uint32_t>(c->j_cnt3),
                                               dp<uint8_t>(c->j_ecls), small + 1);
+    if (nopen)                                          // properties objects, under the links elements
+        k_js_roles<<<nblocks(nopen), BLOCK, 0, s>>>(j, toks, dp<uint32_t>(c->j_olist), nopen, par, role,
+                                                    dp<uint8_t>(c->j_odep), 6u);
     for (int q = 0; q < 3; ++q)
         TRY(scan_u32(c, dp<uint32_t>(c->j_cnt3) + (size_t)q * ntiles, ntiles,
                      dp<uint64_t>(c->j_coff3) + (size_t)q * (ntiles + 1)));

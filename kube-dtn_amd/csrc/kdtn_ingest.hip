@@ -219,8 +219,8 @@ KD_INLINE uint32_t select_bit(uint64_t m, uint32_t r) {
 // every lane walking its own block's tokens into its own region.
 __global__ void __launch_bounds__(BLOCK) k_js_tokens(JsDoc j, JsMasks m, const uint64_t* toff, const uint64_t* doff,
                                                      const uint64_t* ooff, const uint64_t* coff, const uint64_t* soff,
-                                                     uint2* toks, uint32_t* olist, uint32_t* vlist, uint32_t* slist,
-                                                     unsigned long long* err) {
+                                                     uint2* toks, uint32_t* olist, uint8_t* odep, uint32_t* vlist,
+                                                     uint32_t* slist, unsigned long long* err) {
     __shared__ uint4 blk[BLOCK * 4];
     __shared__ uint64_t stok[BLOCK], sop[BLOCK], scl[BLOCK], scol[BLOCK], ssc[BLOCK];
     __shared__ int64_t sd0[BLOCK];
@@ -288,7 +288,9 @@ __global__ void __launch_bounds__(BLOCK) k_js_tokens(JsDoc j, JsMasks m, const u
         const uint32_t idx = base + r;
         if (kind == TK_OBJ || kind == TK_ARR) {
             if (d >= 10000) js_fail(err, pos, KDTN_JSON_DEPTH);
-            olist[soo[o] + __popcll(sop[o] & below)] = idx;
+            const uint32_t oi = soo[o] + __popcll(sop[o] & below);
+            olist[oi] = idx;
+            odep[oi] = (uint8_t)(d > 254 ? 255 : d);             // k_js_roles picks its level by this byte
         } else if (kind == TK_COLON) {
             vlist[sco[o] + __popcll(scol[o] & below)] = idx + 1;   // the member value follows its colon
         } else if (kind == TK_SCALAR) {
@@ -873,26 +875,31 @@ KD_INLINE uint32_t child_role(const JsDoc& j, const uint2* toks, uint32_t r, uin
     }
 }
 
-// one nesting level at a time over the open brackets: a container's role follows from its
-// parent's (already set by the previous level), its kind and its member name
+// one nesting level at a time over the open brackets (levels 0, 1, 3, 4, then 6): a container's
+// role follows from its parent's (set by an earlier level), its kind and its member name. The
+// array elements of levels 2 and 5 are set by k_js_elems_count, which classifies them anyway
+// (level 6 runs after it); level 3 therefore derives its parent's role (an items element)
+// from the grandparent's. The roles start zeroed (R_NONE) and only the schema's containers
+// are written.
 __global__ void __launch_bounds__(BLOCK) k_js_roles(JsDoc j, const uint2* toks, const uint32_t* olist, uint32_t nopen,
-                                                    const uint32_t* par, uint8_t* role, uint8_t* odep,
+                                                    const uint32_t* par, uint8_t* role, const uint8_t* odep,
                                                     uint32_t level) {
     const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
-    if (k >= nopen) return;
-    // level 0 records every open bracket's depth (one byte, saturated); later levels read
-    // that byte coalesced and touch the token only at their own level
-    if (level != 0 && odep[k] != level) return;
+    if (k >= nopen || odep[k] != level) return;             // the depth byte k_js_tokens wrote
     const uint32_t i = olist[k];
-    const uint2 t = toks[i];
+    uint32_t r;
     if (level == 0) {
-        const uint32_t d = tdepth(t);
-        odep[k] = (uint8_t)(d > 254u ? 255u : d);
-        if (d != 0) return;
+        r = tkind(toks[i]) == TK_OBJ ? R_ROOT : R_NONE;
+    } else {
+        const uint32_t p = par[i];
+        uint32_t rp;
+        if (level == 3)                                      // p: an items element (an object) or nothing
+            rp = (role[par[p]] == R_ITEMS && tkind(toks[p]) == TK_OBJ) ? R_ITEM : R_NONE;
+        else
+            rp = role[p];
+        r = child_role(j, toks, rp, i);
     }
-    const uint32_t r = level == 0 ? (tkind(t) == TK_OBJ ? R_ROOT : R_NONE)
-                                  : child_role(j, toks, role[par[i]], i);
-    role[i] = (uint8_t)r;
+    if (r != R_NONE) role[i] = (uint8_t)r;
 }
 
 // ---------------------------------------------------------------- element ordinals
@@ -900,7 +907,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_roles(JsDoc j, const uint2* toks, 
 // element}, or 0. k_js_validate marks the candidates (depth 2 for items elements, 5 for links
 // elements; after '[' or ','; a value; parent an array); the parent array's role decides.
 __global__ void __launch_bounds__(BLOCK) k_js_elems_count(JsDoc j, const uint2* toks, uint32_t ntok, const uint32_t* par,
-                                                          const uint8_t* role, uint32_t* cnt3, uint8_t* ecls,
+                                                          uint8_t* role, uint32_t* cnt3, uint8_t* ecls,
                                                           unsigned long long* derr) {
     __shared__ uint32_t sh[3];
     if (threadIdx.x < 3) sh[threadIdx.x] = 0;
@@ -927,12 +934,13 @@ __global__ void __launch_bounds__(BLOCK) k_js_elems_count(JsDoc j, const uint2* 
             const uint32_t i = base + q * 4 + h;
             const uint32_t vc = (w[q] >> (8 * h)) & 0xFFu;             // k_js_validate's value class
             if (i >= ntok || !vc) continue;
+            changed = true;
             const uint32_t r = role[par[i]];
             const uint32_t cls = r == R_ITEMS ? 1 : r == R_SPEC_LINKS ? 2 : r == R_STATUS_LINKS ? 3 : 0;
             w[q] = (w[q] & ~(0xFFu << (8 * h))) | (cls << (8 * h));   // the class, for k_js_elems_write
-            changed = true;
             if (!cls) continue;
             if (vc == 3u) js_fail(derr, toks[i].x, KDTN_JSON_TYPE);     // neither an object nor null
+            if (vc == 1u) role[i] = (uint8_t)(cls == 1 ? R_ITEM : cls == 2 ? R_LINK_S : R_LINK_R);
             c[cls - 1]++;
         }
     }

@@ -688,8 +688,8 @@ struct JsIntern {
 __global__ void k_js_quotes(JsDoc j, uint64_t* qmask, uint64_t* bsmask, uint64_t* hbmask, uint32_t* qcnt);
 __global__ void k_js_classify(JsDoc j, const uint64_t* qoff, JsMasks m, unsigned long long* err);
 __global__ void k_js_tokens(JsDoc j, JsMasks m, const uint64_t* toff, const uint64_t* doff, const uint64_t* ooff,
-                            const uint64_t* coff, const uint64_t* soff, uint2* toks, uint32_t* olist, uint32_t* vlist,
-                            uint32_t* slist, unsigned long long* err);
+                            const uint64_t* coff, const uint64_t* soff, uint2* toks, uint32_t* olist, uint8_t* odep,
+                            uint32_t* vlist, uint32_t* slist, unsigned long long* err);
 __global__ void k_js_scalars(JsDoc j, const uint2* toks, const uint32_t* slist, uint32_t nscal, unsigned long long* err);
 __global__ void k_js_par_agg(const uint2* toks, uint32_t ntok, uint32_t* tagg);
 __global__ void k_js_par_group(const uint32_t* tagg, uint32_t ntiles, uint32_t* gagg);
@@ -700,8 +700,8 @@ __global__ void k_js_deep(const uint2* toks, uint32_t ntok, uint32_t* par, const
 __global__ void k_js_validate(JsDoc j, const uint2* toks, uint32_t ntok, const uint32_t* par, uint8_t* ecand,
                               unsigned long long* err);
 __global__ void k_js_roles(JsDoc j, const uint2* toks, const uint32_t* olist, uint32_t nopen, const uint32_t* par,
-                           uint8_t* role, uint8_t* odep, uint32_t level);
-__global__ void k_js_elems_count(JsDoc j, const uint2* toks, uint32_t ntok, const uint32_t* par, const uint8_t* role,
+                           uint8_t* role, const uint8_t* odep, uint32_t level);
+__global__ void k_js_elems_count(JsDoc j, const uint2* toks, uint32_t ntok, const uint32_t* par, uint8_t* role,
                                  uint32_t* cnt3, uint8_t* ecls, unsigned long long* derr);
 __global__ void k_js_elems_write(const uint8_t* ecls, uint32_t ntok, const uint64_t* coff3, uint32_t ntiles,
                                  uint32_t* ord, JsTopoOut to);

@@ -11,6 +11,7 @@
 #     shard      one rank of N = 2 / 4 / 8 on this GPU (tools/shard_epoch.py); $SHARD_NS overrides
 #     ingest     config-2 ingest stage with kernel times (tools/ingest_run.py)
 #     ipmc       ingest FETCH_SIZE / WRITE_SIZE passes (tools/ingest_pmc_traffic.sh)
+#     istats     rocprofv3 --kernel-trace --stats of the config-2 ingest (tools/ingest_run.py)
 #     iab        ingest A/B of profiling variants $IAB_VARIANTS (tools/ingest_ablate.py, default 0,16)
 #     stages     output-stage kernel times (tools/stage_run.py)
 #   default: tests,smoke,bench,stats,pmc
@@ -83,6 +84,11 @@ for C in 2 3 4; do
     echo "$PM done"
   fi
 done
+if has istats; then
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/istats -o run \
+      -- python3 $R/tools/ingest_run.py --pods 1000000 --doc /tmp/kdtn_doc_1000000.json > $OUT/istats_ingest.json 2> $OUT/istats.err
+  cat $OUT/istats_ingest.json
+fi
 if has ipmc; then
   (cd $R && bash tools/ingest_pmc_traffic.sh $TAG/ipmc 1000000)
 fi
