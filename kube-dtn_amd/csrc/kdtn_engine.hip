@@ -162,8 +162,8 @@ struct kdtn_ctx {
     uint32_t tc_n = 0;
     bool tc_done = false;
     // CR ingest (kdtn_ingest.hip): document, block masks, token stream, decode scratch
-    DevBuf j_doc, j_q, j_bs, j_hb, j_qcnt, j_qoff, j_tok, j_open, j_close, j_tcnt, j_dcnt, j_toff, j_doff;
-    DevBuf j_ocnt, j_ooff, j_olist, j_ccnt, j_coff, j_vlist, j_scnt, j_soff, j_slist;
+    DevBuf j_doc, j_q, j_bs, j_hb, j_qcnt, j_qoff, j_tok, j_open, j_close, j_gcnt, j_goff;
+    DevBuf j_olist, j_vlist, j_slist;
     uint32_t j_kcap = 0, j_pcap = 0;   // intern table sizes that fit the last document
     DevBuf j_toks, j_par, j_role, j_ecls, j_odep, j_ord, j_tagg, j_gagg, j_cnt3, j_coff3, j_small, j_part;
     DevBuf j_tflags, j_owner, j_vown, j_kslots, j_krep, j_pslots, j_prep, j_heap;
@@ -895,12 +895,12 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->f_mark, &c->f_send, &c->f_node_idx, &c->f_nodes, &c->f_counts, &c->f_base,
                       &c->f_part, &c->f_idx, &c->f_inv, &c->f_st, &c->f_reach_upd, &c->tc_size, &c->tc_off, &c->tc_part, &c->tc_arena,
                       &c->j_doc, &c->j_q, &c->j_bs, &c->j_hb, &c->j_qcnt, &c->j_qoff, &c->j_tok, &c->j_open,
-                      &c->j_close, &c->j_tcnt, &c->j_dcnt, &c->j_toff, &c->j_doff, &c->j_toks, &c->j_par,
+                      &c->j_close, &c->j_gcnt, &c->j_goff, &c->j_toks, &c->j_par,
                       &c->j_role, &c->j_ecls, &c->j_odep, &c->j_ord, &c->j_tagg, &c->j_gagg, &c->j_cnt3, &c->j_coff3, &c->j_small,
                       &c->j_part, &c->j_tflags, &c->j_owner, &c->j_rows, &c->j_kkeys, &c->j_pkeys, &c->j_vown, &c->j_kslots, &c->j_krep,
                       &c->j_pslots, &c->j_prep, &c->j_heap, &c->j_bits, &c->j_bcnt, &c->j_wrank,
-                      &c->j_kslot_id, &c->j_pslot_id, &c->j_len, &c->j_off64, &c->j_sofid, &c->j_ocnt, &c->j_ooff,
-                      &c->j_olist, &c->j_ccnt, &c->j_coff, &c->j_vlist, &c->j_scnt, &c->j_soff, &c->j_slist, &c->sh_keep, &c->sh_kreal,
+                      &c->j_kslot_id, &c->j_pslot_id, &c->j_len, &c->j_off64, &c->j_sofid,
+                      &c->j_olist, &c->j_vlist, &c->j_slist, &c->sh_keep, &c->sh_kreal,
                       &c->sh_kdes, &c->sh_tidx, &c->sh_roff64, &c->sh_noff64, &c->sh_doc, &c->sh_ns,
                       &c->sh_name, &c->sh_src, &c->sh_netns, &c->sh_flags, &c->sh_roff, &c->sh_noff,
                       &c->sh_des.buf, &c->sh_real.buf, &c->vx_ops, &c->vx_dead, &c->vx_slots, &c->vx_node,
@@ -2080,37 +2080,38 @@ static int json_decode(kdtn_ctx* c, const JsTargets& tg, JsCounts* o, kdtn_inges
     HIP_TRY(hipMemsetAsync(small + 2, 0, J_SMALL - 16, s));
     // one word past the end: any_in reads the word after a string's first (its bits are masked)
     for (DevBuf* b : {&c->j_q, &c->j_bs, &c->j_hb, &c->j_tok, &c->j_open, &c->j_close}) TRY(ensure(*b, ((size_t)nb + 1) * 8));
-    for (DevBuf* b : {&c->j_qcnt, &c->j_tcnt, &c->j_dcnt, &c->j_ocnt, &c->j_ccnt, &c->j_scnt}) TRY(ensure(*b, (size_t)nb * 4));
-    for (DevBuf* b : {&c->j_qoff, &c->j_toff, &c->j_doff, &c->j_ooff, &c->j_coff, &c->j_soff})
-        TRY(ensure(*b, ((size_t)nb + 1) * 8));
+    // per-workgroup counts (quotes; tokens, depth, opens, colons, scalars) and their offsets
+    const uint32_t nwg = nblocks(nb);
+    TRY(ensure(c->j_qcnt, (size_t)nwg * 4));
+    TRY(ensure(c->j_qoff, ((size_t)nwg + 1) * 8));
+    TRY(ensure(c->j_gcnt, (size_t)5 * nwg * 4));
+    TRY(ensure(c->j_goff, (size_t)5 * (nwg + 1) * 8));
     JsDoc j{dp<uint8_t>(c->j_doc), (uint32_t)c->j_n, nb, dp<uint64_t>(c->j_q), dp<uint64_t>(c->j_bs),
             dp<uint64_t>(c->j_hb), 0u};
 #if KDTN_PROFILING
     j.variant = (uint32_t)std::strtoul(std::getenv("KDTN_JS_VARIANT") ? std::getenv("KDTN_JS_VARIANT") : "0", nullptr, 0);
 #endif
-    JsMasks m{dp<uint64_t>(c->j_tok), dp<uint64_t>(c->j_open), dp<uint64_t>(c->j_close), dp<uint32_t>(c->j_tcnt),
-              dp<uint32_t>(c->j_dcnt), dp<uint32_t>(c->j_ocnt), dp<uint32_t>(c->j_ccnt), dp<uint32_t>(c->j_scnt)};
+    JsMasks m{dp<uint64_t>(c->j_tok), dp<uint64_t>(c->j_open), dp<uint64_t>(c->j_close), dp<uint32_t>(c->j_gcnt)};
+    const uint64_t* goff = dp<uint64_t>(c->j_goff);
+    auto gtotal = [&](int f) { return goff + (size_t)f * (nwg + 1) + nwg; };   // f: 0 tokens, 2 opens, 3 colons, 4 scalars
 
     // 1. block masks, string state, token counts, depth
     k_js_quotes<<<nblocks(nb), BLOCK, 0, s>>>(j, dp<uint64_t>(c->j_q), dp<uint64_t>(c->j_bs), dp<uint64_t>(c->j_hb),
                                              dp<uint32_t>(c->j_qcnt));
-    TRY(scan_u32(c, dp<uint32_t>(c->j_qcnt), nb, dp<uint64_t>(c->j_qoff)));
-    k_js_classify<<<nblocks(nb), BLOCK, 0, s>>>(j, dp<uint64_t>(c->j_qoff), m, small);
-    TRY(scan_u32(c, dp<uint32_t>(c->j_tcnt), nb, dp<uint64_t>(c->j_toff)));
-    TRY(scan_u32(c, dp<uint32_t>(c->j_dcnt), nb, dp<uint64_t>(c->j_doff)));
-    TRY(scan_u32(c, dp<uint32_t>(c->j_ocnt), nb, dp<uint64_t>(c->j_ooff)));
-    TRY(scan_u32(c, dp<uint32_t>(c->j_ccnt), nb, dp<uint64_t>(c->j_coff)));
-    TRY(scan_u32(c, dp<uint32_t>(c->j_scnt), nb, dp<uint64_t>(c->j_soff)));
+    TRY(scan_u32(c, dp<uint32_t>(c->j_qcnt), nwg, dp<uint64_t>(c->j_qoff)));
+    k_js_classify<<<nwg, BLOCK, 0, s>>>(j, dp<uint64_t>(c->j_qoff), m, nwg, small);
+    for (int f = 0; f < 5; ++f)
+        TRY(scan_u32(c, dp<uint32_t>(c->j_gcnt) + (size_t)f * nwg, nwg, dp<uint64_t>(c->j_goff) + (size_t)f * (nwg + 1)));
     timer_mark(c, "js_blocks");
     uint64_t quotes = 0, ntok64 = 0, nopen64 = 0;
-    TRY(d2h(c, &nopen64, dp<uint64_t>(c->j_ooff) + nb));
+    TRY(d2h(c, &nopen64, gtotal(2)));
     uint64_t nval64 = 0;
-    TRY(d2h(c, &nval64, dp<uint64_t>(c->j_coff) + nb));
+    TRY(d2h(c, &nval64, gtotal(3)));
     uint64_t nscal64 = 0;
-    TRY(d2h(c, &nscal64, dp<uint64_t>(c->j_soff) + nb));
+    TRY(d2h(c, &nscal64, gtotal(4)));
     unsigned long long serr = 0;
-    TRY(d2h(c, &quotes, dp<uint64_t>(c->j_qoff) + nb));
-    TRY(d2h(c, &ntok64, dp<uint64_t>(c->j_toff) + nb));
+    TRY(d2h(c, &quotes, dp<uint64_t>(c->j_qoff) + nwg));
+    TRY(d2h(c, &ntok64, gtotal(0)));
     TRY(d2h(c, &serr, small));
     HIP_TRY(hipStreamSynchronize(s));
     timer_mark(c, "js_sync");                       // host round trips are timed apart
@@ -2136,9 +2137,7 @@ static int json_decode(kdtn_ctx* c, const JsTargets& tg, JsCounts* o, kdtn_inges
     TRY(ensure(c->j_slist, (size_t)nscal * 4 + 4));
     const uint2* toks = dp<uint2>(c->j_toks);
     uint32_t* par = dp<uint32_t>(c->j_par);
-    k_js_tokens<<<nblocks(nb), BLOCK, 0, s>>>(j, m, dp<uint64_t>(c->j_toff), dp<uint64_t>(c->j_doff),
-                                             dp<uint64_t>(c->j_ooff), dp<uint64_t>(c->j_coff), dp<uint64_t>(c->j_soff),
-                                             dp<uint2>(c->j_toks), dp<uint32_t>(c->j_olist), dp<uint8_t>(c->j_odep),
+    k_js_tokens<<<nwg, BLOCK, 0, s>>>(j, m, goff, nwg, dp<uint2>(c->j_toks), dp<uint32_t>(c->j_olist), dp<uint8_t>(c->j_odep),
                                              dp<uint32_t>(c->j_vlist), dp<uint32_t>(c->j_slist), small);
     timer_mark(c, "js_tokens");
     const uint32_t ntiles = (ntok + JS_TILE - 1) / JS_TILE, ng = (ntiles + BLOCK - 1) / BLOCK;

@@ -91,10 +91,54 @@ KD_INLINE uint32_t esc_byte(uint32_t x) {          // \b \f \n \r \t; \" \\ \/ s
     }
 }
 // ---------------------------------------------------------------- k_js_quotes
+// Per-workgroup sums of per-block counts (BLOCK blocks of 64 bytes per workgroup): the scans
+// run over these group partials only, and the consumer rebuilds a block's offset as its group's
+// offset plus a workgroup scan of counts it derives from its own masks (no per-block count or
+// offset arrays). Fields of `a` are 16-bit (≤ 64 per block, ≤ 16384 per group).
+KD_INLINE void group_sums(uint64_t a, uint64_t d, uint64_t* sh, uint32_t* g, uint32_t ng) {
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        a += __shfl_xor(a, o, 64);
+        d += __shfl_xor(d, o, 64);
+    }
+    if (lane == 0) { sh[wave] = a; sh[BLOCK / 64 + wave] = d; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t ta = 0, td = 0;
+#pragma unroll
+        for (int k = 0; k < BLOCK / 64; ++k) { ta += sh[k]; td += sh[BLOCK / 64 + k]; }
+        const uint32_t x = blockIdx.x;
+        g[x] = (uint32_t)(ta & 0xFFFFu);                    // tokens
+        g[ng + x] = (uint32_t)td;                            // 64 + opens - closes
+        g[2 * ng + x] = (uint32_t)((ta >> 16) & 0xFFFFu);    // opens
+        g[3 * ng + x] = (uint32_t)((ta >> 32) & 0xFFFFu);    // colons
+        g[4 * ng + x] = (uint32_t)(ta >> 48);                // scalars
+    }
+}
+
+KD_INLINE uint32_t quote_block(const JsDoc& j, uint32_t b, uint64_t* qmask, uint64_t* bsmask, uint64_t* hbmask);
+
 __global__ void __launch_bounds__(BLOCK) k_js_quotes(JsDoc j, uint64_t* qmask, uint64_t* bsmask,
-                                                     uint64_t* hbmask, uint32_t* qcnt) {
+                                                     uint64_t* hbmask, uint32_t* gq) {
+    __shared__ uint64_t sh[BLOCK / 64];
     const uint32_t b = blockIdx.x * BLOCK + threadIdx.x;
-    if (b >= j.nb) return;
+    uint32_t nq = 0;
+    if (b < j.nb) nq = quote_block(j, b, qmask, bsmask, hbmask);
+    uint32_t x = nq;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
+    if ((threadIdx.x & 63u) == 0) sh[threadIdx.x >> 6] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t t = 0;
+#pragma unroll
+        for (int k = 0; k < BLOCK / 64; ++k) t += sh[k];
+        gq[blockIdx.x] = (uint32_t)t;
+    }
+}
+
+KD_INLINE uint32_t quote_block(const JsDoc& j, uint32_t b, uint64_t* qmask, uint64_t* bsmask, uint64_t* hbmask) {
     uint32_t w[16];
     load_block(j.doc, b, w);
     uint64_t bs = 0, q = 0, hb = 0;
@@ -128,14 +172,28 @@ __global__ void __launch_bounds__(BLOCK) k_js_quotes(JsDoc j, uint64_t* qmask, u
     qmask[b] = quote;
     bsmask[b] = bs;
     hbmask[b] = hb;
-    qcnt[b] = __popcll(quote);
+    return __popcll(quote);
 }
 
 // ---------------------------------------------------------------- k_js_classify
-__global__ void __launch_bounds__(BLOCK) k_js_classify(JsDoc j, const uint64_t* qoff, JsMasks m,
+KD_INLINE void classify_block(const JsDoc& j, uint32_t b, uint64_t quote, bool S, const JsMasks& m,
+                              unsigned long long* err, uint64_t* pa, uint64_t* pd);
+
+__global__ void __launch_bounds__(BLOCK) k_js_classify(JsDoc j, const uint64_t* gqoff, JsMasks m, uint32_t ng,
                                                        unsigned long long* err) {
+    __shared__ uint64_t sh[2 * (BLOCK / 64)];
     const uint32_t b = blockIdx.x * BLOCK + threadIdx.x;
-    if (b >= j.nb) return;
+    const bool valid = b < j.nb;
+    const uint64_t quote = valid ? j.qmask[b] : 0;
+    uint64_t qt;
+    const uint64_t qo = gqoff[blockIdx.x] + block_exclusive(__popcll(quote), sh, &qt);
+    uint64_t pa = 0, pd = 0;
+    if (valid) classify_block(j, b, quote, qo & 1, m, err, &pa, &pd);
+    group_sums(pa, pd, sh, m.gcnt, ng);
+}
+
+KD_INLINE void classify_block(const JsDoc& j, uint32_t b, uint64_t quote, bool S, const JsMasks& m,
+                              unsigned long long* err, uint64_t* pa, uint64_t* pd) {
     uint32_t w[16];
     load_block(j.doc, b, w);
     uint64_t op = 0, cl = 0, pun = 0, ctl = 0, wsc = 0, colon = 0;
@@ -151,8 +209,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_classify(JsDoc j, const uint64_t* 
         ctl |= (uint64_t)mm4(ltb(w[k], 0x20)) << (4 * k);
         wsc |= (uint64_t)mm4(ltb(w[k], 0x21)) << (4 * k);
     }
-    const uint64_t quote = j.qmask[b];
-    const bool S = qoff[b] & 1;                            // inside a string at byte 0
+    // S: inside a string at byte 0 (odd number of quotes before the block)
     const uint64_t instr = prefix_xor(quote) ^ (S ? ~0ull : 0ull);
     const uint64_t out = ~instr;
     const uint64_t structural = (op | cl | pun) & out;
@@ -180,11 +237,9 @@ __global__ void __launch_bounds__(BLOCK) k_js_classify(JsDoc j, const uint64_t* 
     m.tok[b] = tok;
     m.open[b] = op & out;
     m.close[b] = cl & out;
-    m.tcnt[b] = __popcll(tok);
-    m.dcnt[b] = 64u + __popcll(op & out) - __popcll(cl & out);
-    m.ocnt[b] = __popcll(op & out);
-    m.ccnt[b] = __popcll(colon & out);
-    m.scnt[b] = __popcll(scalar_start);
+    *pa = (uint64_t)__popcll(tok) | (uint64_t)__popcll(op & out) << 16 | (uint64_t)__popcll(colon & out) << 32 |
+          (uint64_t)__popcll(scalar_start) << 48;
+    *pd = 64u + __popcll(op & out) - __popcll(cl & out);
 }
 
 // ---------------------------------------------------------------- k_js_tokens
@@ -217,30 +272,26 @@ KD_INLINE uint32_t select_bit(uint64_t m, uint32_t r) {
 // round by round, lane l taking the wave's token r = round * 64 + l (owner block by binary
 // search over the wave's token prefix, bit by select): coalesced 8-byte stores instead of
 // every lane walking its own block's tokens into its own region.
-__global__ void __launch_bounds__(BLOCK) k_js_tokens(JsDoc j, JsMasks m, const uint64_t* toff, const uint64_t* doff,
-                                                     const uint64_t* ooff, const uint64_t* coff, const uint64_t* soff,
+__global__ void __launch_bounds__(BLOCK) k_js_tokens(JsDoc j, JsMasks m, const uint64_t* goff, uint32_t ng,
                                                      uint2* toks, uint32_t* olist, uint8_t* odep, uint32_t* vlist,
                                                      uint32_t* slist, unsigned long long* err) {
     __shared__ uint4 blk[BLOCK * 4];
     __shared__ uint64_t stok[BLOCK], sop[BLOCK], scl[BLOCK], scol[BLOCK], ssc[BLOCK];
     __shared__ int64_t sd0[BLOCK];
     __shared__ uint32_t sex[BLOCK], soo[BLOCK], sco[BLOCK], sso[BLOCK];
+    __shared__ uint64_t shs[BLOCK / 64];
     const uint32_t lane = threadIdx.x & 63u, w0 = threadIdx.x & ~63u;
     const uint32_t b = blockIdx.x * BLOCK + threadIdx.x;
-    uint64_t tok = 0, ti = 0;
+    uint64_t tok = 0, pa = 0, pd = 0;
     if (b < j.nb) {
         const uint4* p = reinterpret_cast<const uint4*>(j.doc + (size_t)b * 64);
         uint4 v[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] = p[q];
         tok = m.tok[b];
-        ti = toff[b];
-        sop[threadIdx.x] = m.open[b];
-        scl[threadIdx.x] = m.close[b];
-        sd0[threadIdx.x] = (int64_t)doff[b] - 64ll * b;
-        soo[threadIdx.x] = (uint32_t)ooff[b];
-        sco[threadIdx.x] = (uint32_t)coff[b];
-        sso[threadIdx.x] = (uint32_t)soff[b];
+        const uint64_t op = m.open[b], cl = m.close[b];
+        sop[threadIdx.x] = op;
+        scl[threadIdx.x] = cl;
         uint64_t col = 0, nsc = 0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -256,7 +307,21 @@ __global__ void __launch_bounds__(BLOCK) k_js_tokens(JsDoc j, JsMasks m, const u
         }
         scol[threadIdx.x] = col & tok;                 // structural colons
         ssc[threadIdx.x] = tok & ~nsc;                 // scalar token starts (the token's first byte)
+        // the block's counts, as k_js_classify summed them per workgroup
+        pa = (uint64_t)__popcll(tok) | (uint64_t)__popcll(op) << 16 | (uint64_t)__popcll(col & tok) << 32 |
+             (uint64_t)__popcll(tok & ~nsc) << 48;
+        pd = 64u + __popcll(op) - __popcll(cl);
     }
+    // the block's offsets: its workgroup's (scanned group partials) + a workgroup scan
+    uint64_t ta, td;
+    const uint64_t ea = block_exclusive(pa, shs, &ta);
+    const uint64_t ed = block_exclusive(pd, shs, &td);
+    const uint32_t g = blockIdx.x, G = ng + 1;
+    const uint64_t ti = goff[g] + (ea & 0xFFFFu);
+    sd0[threadIdx.x] = (int64_t)(goff[G + g] + ed) - 64ll * b;
+    soo[threadIdx.x] = (uint32_t)(goff[2 * G + g] + ((ea >> 16) & 0xFFFFu));
+    sco[threadIdx.x] = (uint32_t)(goff[3 * G + g] + ((ea >> 32) & 0xFFFFu));
+    sso[threadIdx.x] = (uint32_t)(goff[4 * G + g] + (ea >> 48));
     stok[threadIdx.x] = tok;
     const uint32_t cnt = __popcll(tok);
     uint32_t inc = cnt;

@@ -632,11 +632,8 @@ struct JsMasks {
     uint64_t* tok;             // token starts
     uint64_t* open;            // { [ outside strings
     uint64_t* close;           // } ] outside strings
-    uint32_t* tcnt;            // tokens per block
-    uint32_t* dcnt;            // 64 + opens - closes per block
-    uint32_t* ocnt;            // opens per block
-    uint32_t* ccnt;            // colons per block
-    uint32_t* scnt;            // scalar tokens per block
+    uint32_t* gcnt;            // per workgroup of BLOCK blocks, 5 arrays of ng: tokens, 64 + opens -
+                               // closes, opens, colons, scalar tokens (group_sums)
 };
 struct JsTopoOut {
     uint32_t* ns;
@@ -685,11 +682,10 @@ struct JsIntern {
     JsDict kd, pd;
     uint32_t variant;
 };
-__global__ void k_js_quotes(JsDoc j, uint64_t* qmask, uint64_t* bsmask, uint64_t* hbmask, uint32_t* qcnt);
-__global__ void k_js_classify(JsDoc j, const uint64_t* qoff, JsMasks m, unsigned long long* err);
-__global__ void k_js_tokens(JsDoc j, JsMasks m, const uint64_t* toff, const uint64_t* doff, const uint64_t* ooff,
-                            const uint64_t* coff, const uint64_t* soff, uint2* toks, uint32_t* olist, uint8_t* odep,
-                            uint32_t* vlist, uint32_t* slist, unsigned long long* err);
+__global__ void k_js_quotes(JsDoc j, uint64_t* qmask, uint64_t* bsmask, uint64_t* hbmask, uint32_t* gq);
+__global__ void k_js_classify(JsDoc j, const uint64_t* gqoff, JsMasks m, uint32_t ng, unsigned long long* err);
+__global__ void k_js_tokens(JsDoc j, JsMasks m, const uint64_t* goff, uint32_t ng, uint2* toks, uint32_t* olist,
+                            uint8_t* odep, uint32_t* vlist, uint32_t* slist, unsigned long long* err);
 __global__ void k_js_scalars(JsDoc j, const uint2* toks, const uint32_t* slist, uint32_t nscal, unsigned long long* err);
 __global__ void k_js_par_agg(const uint2* toks, uint32_t ntok, uint32_t* tagg);
 __global__ void k_js_par_group(const uint32_t* tagg, uint32_t ntiles, uint32_t* gagg);
