@@ -1020,19 +1020,18 @@ __global__ void __launch_bounds__(BLOCK) k_js_elems_count(JsDoc j, const uint2* 
 __global__ void __launch_bounds__(BLOCK) k_js_elems_write(const uint8_t* ecls, uint32_t ntok, const uint64_t* coff3,
                                                           uint32_t ntiles, uint32_t* ord, JsTopoOut to) {
     __shared__ uint64_t sh[BLOCK / 64];
-    __shared__ uint8_t tc[JS_TPAD];                // element class per tile token
-    const uint32_t t0 = blockIdx.x * JS_TILE;
-    for (int q = 0; q < JS_PER; ++q) {            // classes: coalesced order
-        const uint32_t l = q * BLOCK + threadIdx.x;
-        tc[tpad(l)] = t0 + l < ntok ? ecls[t0 + l] : (uint8_t)0;
-    }
-    __syncthreads();
-    const uint8_t* mine = tc + threadIdx.x * (JS_PER + 1);
+    // the thread's JS_PER classes as one 16-byte load (whole tiles; bytes past ntok ignored)
+    const uint32_t base = blockIdx.x * JS_TILE + threadIdx.x * JS_PER;
+    const uint4 cv = *reinterpret_cast<const uint4*>(ecls + base);
+    const uint32_t w[4] = {cv.x, cv.y, cv.z, cv.w};
     uint32_t c[3] = {0, 0, 0};
-    const uint32_t base = t0 + threadIdx.x * JS_PER;
-    for (int k = 0; k < JS_PER; ++k) {
-        const uint32_t cls = mine[k];
-        if (cls) c[cls - 1]++;
+    const bool any = (cv.x | cv.y | cv.z | cv.w) != 0;
+    if (any) {
+#pragma unroll
+        for (int k = 0; k < JS_PER; ++k) {
+            const uint32_t cls = (w[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+            if (cls && base + k < ntok) c[cls - 1]++;
+        }
     }
     uint32_t run[3];
 #pragma unroll
@@ -1040,11 +1039,11 @@ __global__ void __launch_bounds__(BLOCK) k_js_elems_write(const uint8_t* ecls, u
         uint64_t tot;
         run[q] = (uint32_t)(coff3[(size_t)q * (ntiles + 1) + blockIdx.x] + block_exclusive(c[q], sh, &tot));
     }
+    if (!any) return;
     for (int k = 0; k < JS_PER; ++k) {
         const uint32_t i = base + k;
-        if (i >= ntok) break;
-        const uint32_t cls = mine[k];
-        if (!cls) continue;
+        const uint32_t cls = (w[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+        if (!cls || i >= ntok) continue;
         const uint32_t o = run[cls - 1]++;
         ord[i] = o;
         if (cls == 1) {                                            // a Topology: its record offsets
