@@ -745,31 +745,24 @@ __global__ void __launch_bounds__(BLOCK) k_js_validate(JsDoc j, const uint2* tok
                           p < JS_DEEP && pkind == TK_ARR;
         ecand[i] = (uint8_t)(!cand ? 0u : kind == TK_OBJ ? 1u : (kind == TK_SCALAR && j.doc[pos] == 'n') ? 2u : 3u);
     }
-    if (i == 0) {
-        ok = value_start(kind) && d == 0;
-    } else {
-        if (d == 0) ok = false;                                   // a second top-level value
-        else {
-            const uint32_t pk = tkind(st[threadIdx.x + 1]);
-            switch (pk) {
-            case TK_OBJ: ok = kind == TK_STR || kind == TK_OBJ_END; break;
-            case TK_ARR: ok = value_start(kind) || kind == TK_ARR_END; break;
-            case TK_COLON: ok = value_start(kind); break;
-            case TK_COMMA: ok = ck == TK_OBJ ? kind == TK_STR : (ck == TK_ARR && value_start(kind)); break;
-            case TK_STR: {
-                // tk_key(toks, par, i - 1) from the staged neighbours
-                const uint32_t ppk = i >= 2 ? tkind(st[threadIdx.x]) : 0xFFu, pp = sp[threadIdx.x];
-                const bool key = i >= 2 && (ppk == TK_OBJ || ppk == TK_COMMA) && pp < JS_DEEP &&
-                                 (pp == p ? pkind : kind_of(pp)) == TK_OBJ;
-                if (key) { ok = kind == TK_COLON; break; }
-            }
-                [[fallthrough]];
-            default:                                              // after a value
-                ok = kind == TK_COMMA || kind == TK_OBJ_END || kind == TK_ARR_END;
-            }
-        }
-        if (ok && kind == TK_OBJ_END) ok = ck == TK_OBJ;
-        if (ok && kind == TK_ARR_END) ok = ck == TK_ARR;
+    // the grammar as a set of admissible kinds per predecessor (bit k = kind k), selected
+    // branch-free: the switch it replaces ran every arm for a wave of mixed tokens
+    {
+        const uint32_t pk = i ? tkind(st[threadIdx.x + 1]) : 0xFFu;
+        // token i - 1 is a member name: a string after '{' or ',' inside an object (its parent
+        // is token i's: a string neither opens nor closes a container)
+        const uint32_t ppk = i >= 2 ? tkind(st[threadIdx.x]) : 0xFFu;
+        const bool key = pk == TK_STR && i >= 2 && (ppk == TK_OBJ || ppk == TK_COMMA) && p < JS_DEEP && pkind == TK_OBJ;
+        constexpr uint32_t VS = 1u << TK_OBJ | 1u << TK_ARR | 1u << TK_STR | 1u << TK_SCALAR;   // a value
+        const uint32_t allow = pk == TK_OBJ ? (1u << TK_STR | 1u << TK_OBJ_END)
+                             : pk == TK_ARR ? (VS | 1u << TK_ARR_END)
+                             : pk == TK_COLON ? VS
+                             : pk == TK_COMMA ? (ck == TK_OBJ ? 1u << TK_STR : ck == TK_ARR ? VS : 0u)
+                             : key ? 1u << TK_COLON
+                             : (1u << TK_COMMA | 1u << TK_OBJ_END | 1u << TK_ARR_END);   // after a value
+        ok = (allow >> kind) & 1u;
+        ok = ok && !(kind == TK_OBJ_END && ck != TK_OBJ) && !(kind == TK_ARR_END && ck != TK_ARR);
+        ok = i == 0 ? (((VS >> kind) & 1u) && d == 0) : (ok && d != 0);   // d == 0: a second top-level value
     }
     if (ok && i == ntok - 1) {                                    // the document ends here
         ok = (kind == TK_STR || kind == TK_SCALAR) ? d == 0 : ((kind == TK_OBJ_END || kind == TK_ARR_END) && d == 1);
