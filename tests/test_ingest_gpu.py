@@ -104,6 +104,16 @@ def test_block_boundaries(engine):
         check_doc(engine, doc, f"trial {trial}")
 
 
+def test_dense_tokens(engine):
+    """waves of more tokens than k_js_tokens lists per wave (TK_MAP = 2048: 64 blocks of "0,")
+    around schema values, and one-byte tokens across block and wave edges"""
+    for n in (1000, 2100, 5000, 20000):
+        arr = b"[" + b",".join([b"0"] * n) + b"]"
+        doc = (b'{"items":[{"metadata":{"name":"p","annotations":{"a":' + arr + b'}},"spec":{"links":[{"uid":1,'
+               b'"x":' + arr + b',"peer_pod":"q","properties":{"gap":7}},{"uid":2}]}}]}')
+        check_doc(engine, doc, f"dense {n}")
+
+
 def test_many_tiles(engine):
     """a document with > 2 groups of 4096-token tiles (parent scan across groups)"""
     rng = random.Random(11)
