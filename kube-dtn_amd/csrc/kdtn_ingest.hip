@@ -901,6 +901,22 @@ __constant__ __attribute__((aligned(16))) char kProps[KDTN_NPROP + 1][16] = {"la
                                                 "duplicate", "duplicate_corr", "reorder_prob", "reorder_corr",
                                                 "corrupt_prob", "corrupt_corr", "gap"};
 
+// all schema member names, each role's list contiguous (k_js_values): root | item | metadata |
+// spec / status (spec uses "links" only) | link | properties
+constexpr int KA_ROOT = 0, KA_ITEM = 1, KA_META = 4, KA_LINKS = 6, KA_LINK = 9, KA_PROPS = 18,
+              KN_ALL = KA_PROPS + KDTN_NPROP + 1;
+__constant__ __attribute__((aligned(16))) char kAll[KN_ALL][16] = {
+    "items", "metadata", "spec", "status", "name", "namespace", "links", "src_ip", "net_ns",
+    "local_intf", "local_ip", "local_mac", "peer_intf", "peer_ip", "peer_mac", "peer_pod", "uid", "properties",
+    "latency", "latency_corr", "jitter", "loss", "loss_corr", "rate", "duplicate", "duplicate_corr",
+    "reorder_prob", "reorder_corr", "corrupt_prob", "corrupt_corr", "gap"};
+static_assert(KN_ALL == 31, "schema names");
+// 7-bit hash of a name's zero-padded 16 bytes, distinct over kAll (multiplier found by search;
+// tests/test_ingest_cpu.py checks the property)
+KD_INLINE uint32_t name_hash(uint64_t lo, uint64_t hi) {
+    return (uint32_t)(((lo ^ (hi * 0x9E3779B97F4A7C15ull)) * 0x1BA1621582283D15ull) >> 57);
+}
+
 // ---------------------------------------------------------------- roles
 // role of the container c whose enclosing container has role r (c is the child token)
 KD_INLINE uint32_t child_role(const JsDoc& j, const uint2* toks, uint32_t r, uint32_t c) {
@@ -1448,6 +1464,20 @@ __global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, const uint2* toks,
                                                      const uint32_t* par, const uint8_t* role, const uint32_t* ord,
                                                      JsTopoOut to, JsStore des, JsStore real, JsIntern in,
                                                      unsigned long long* derr) {
+    // every schema member name in one table, looked up by a perfect hash of its 16 bytes (the
+    // per-role name lists it replaces were compared one by one, and a wave of mixed roles ran
+    // every role's list)
+    __shared__ uint64_t s_nm[KN_ALL][2];
+    __shared__ int8_t s_slot[128];
+    if (threadIdx.x < 128) s_slot[threadIdx.x] = -1;
+    __syncthreads();
+    if (threadIdx.x < KN_ALL) {
+        const uint64_t* nm = reinterpret_cast<const uint64_t*>(kAll[threadIdx.x]);
+        s_nm[threadIdx.x][0] = nm[0];
+        s_nm[threadIdx.x][1] = nm[1];
+        s_slot[name_hash(nm[0], nm[1])] = (int8_t)threadIdx.x;
+    }
+    __syncthreads();
     const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
     if (k >= nval) return;
     const uint32_t i = vlist[k];                       // object member values, document order
@@ -1466,38 +1496,41 @@ __global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, const uint2* toks,
     const uint32_t kind = tkind(t);
     const bool null = kind == TK_SCALAR && j.doc[t.x] == 'n';
     int f, bit;
+    {
+        const int g0 = s_slot[name_hash(kn.lo, kn.hi)];
+        const int g = (kn.ok && g0 >= 0 && s_nm[g0][0] == kn.lo && s_nm[g0][1] == kn.hi) ? g0 : -1;
+        const bool link = r == R_LINK_S || r == R_LINK_R;
+        const int lo = r == R_ROOT ? KA_ROOT : r == R_ITEM ? KA_ITEM : r == R_META ? KA_META
+                     : (r == R_SPEC || r == R_STATUS) ? KA_LINKS : link ? KA_LINK : KA_PROPS;
+        const int hi = r == R_ROOT ? KA_ITEM : r == R_ITEM ? KA_META : r == R_META ? KA_LINKS
+                     : r == R_SPEC ? KA_LINKS + 1 : r == R_STATUS ? KA_LINK : link ? KA_PROPS : KN_ALL;
+        f = (g >= lo && g < hi) ? g - lo : -1;                  // index in the role's name list
+    }
     uint32_t own;                                      // owner slot of (object, field): duplicate check
     uint32_t topo = 0, rec = 0;
     JsStore st{};                                      // by value: a pointer to an argument lives in scratch
     switch (r) {
     case R_ROOT:
-        f = key_match(kn, kItems, 1);
         bit = f; own = 0;
         break;
     case R_ITEM:
-        f = key_match(kn, kItem, 3);
         topo = ord[o]; bit = f; own = 1 + topo * 9;
         break;
     case R_META:
-        f = key_match(kn, kMeta, 2);
         topo = ord[po]; bit = 3 + f; own = 1 + topo * 9;
         break;
     case R_SPEC:
-        f = key_match(kn, kLinks, 1);
         topo = ord[po]; bit = 5 + f; own = 1 + topo * 9;
         break;
     case R_STATUS:
-        f = key_match(kn, kStatus, 3);
         topo = ord[po]; bit = 6 + f; own = 1 + topo * 9;
         break;
     case R_LINK_S:
     case R_LINK_R:
-        f = key_match(kn, kLink, KDTN_NKEY + 2);
         st = r == R_LINK_S ? des : real;
         rec = ord[o]; bit = f; own = (r == R_LINK_S ? in.own_des : in.own_real) + rec * 22;
         break;
     default: {                                                    // R_PROPS_S / R_PROPS_R
-        f = key_match(kn, kProps, KDTN_NPROP + 1);
         st = r == R_PROPS_S ? des : real;
         rec = ord[po]; bit = 9 + f; own = (r == R_PROPS_S ? in.own_des : in.own_real) + rec * 22;
         break;

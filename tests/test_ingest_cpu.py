@@ -276,3 +276,21 @@ def test_window_scalars_oracle_pinned():
         except ValueError:
             std_ok = False
         assert (e1 != jr.SYNTAX) == std_ok, (s, e1)
+
+
+def test_schema_name_hash_is_perfect():
+    """k_js_values looks member names up by a 7-bit hash of their zero-padded 16 bytes
+    (kdtn_ingest.hip: kAll / name_hash): the 31 schema names must land in distinct slots"""
+    import re
+    import struct
+    from pathlib import Path
+    src = (Path(__file__).resolve().parents[1] / "kube-dtn_amd" / "csrc" / "kdtn_ingest.hip").read_text()
+    table = src[src.index("kAll[KN_ALL][16] = {"):]
+    names = re.findall(r'"([a-z_]+)"', table[:table.index("};")])
+    k1, k2 = (int(x, 16) for x in re.findall(r"\* (0x[0-9A-F]+)ull", src[src.index("uint32_t name_hash"):])[:2])
+    m = (1 << 64) - 1
+    slots = set()
+    for n in names:
+        lo, hi = struct.unpack("<QQ", n.encode().ljust(16, b"\0"))
+        slots.add((((lo ^ ((hi * k1) & m)) * k2) & m) >> 57)
+    assert len(names) == 31 and len(slots) == 31
