@@ -467,6 +467,19 @@ __global__ void __launch_bounds__(BLOCK) k_js_par_tiles(uint32_t* tagg, uint32_t
 KD_INLINE uint32_t tpad(uint32_t l) { return l + l / JS_PER; }
 constexpr int JS_TPAD = JS_TILE + JS_TILE / JS_PER;
 
+// inclusive max-scan over the wave by DPP moves (row shifts 1/2/4/8, then the row broadcasts of
+// lanes 15 and 31): VALU data movement instead of six LDS-crossbar permutes per scan; the
+// identity 0 fills lanes without a source
+KD_INLINE uint32_t wave_incl_max(uint32_t v) {
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));   // row_shr:1
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));   // row_shr:2
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));   // row_shr:4
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));   // row_shr:8
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));   // row_bcast:15
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));   // row_bcast:31
+    return v;
+}
+
 __global__ void __launch_bounds__(BLOCK) k_js_par_apply(const uint2* toks, uint32_t ntok, const uint32_t* texcl,
                                                         uint32_t* par, uint32_t* deep) {
     __shared__ uint32_t wt[BLOCK / 64][JS_PD];
@@ -496,12 +509,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_par_apply(const uint2* toks, uint3
     uint32_t incl[JS_PD];
 #pragma unroll
     for (int d = 0; d < JS_PD; ++d) {
-        uint32_t v = row[d];
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t o = __shfl_up(v, off, 64);
-            if (lane >= (uint32_t)off) v = max(v, o);
-        }
+        const uint32_t v = wave_incl_max(row[d]);
         incl[d] = v;
         if (lane == 63) wt[wave][d] = v;
     }
