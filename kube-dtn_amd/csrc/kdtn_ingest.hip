@@ -389,9 +389,22 @@ __global__ void __launch_bounds__(BLOCK) k_js_par_agg(const uint2* toks, uint32_
         if (tk_open(meta) && d < JS_PD) row[d] = i + 1;
     }
     __syncthreads();
+    // the max over the 256 rows per lane in two levels (16 parts of 16 rows, then the parts):
+    // one thread walking all 256 rows per lane was a serial chain of dependent LDS reads
+    __shared__ uint32_t red[BLOCK];
+    {
+        constexpr int NP = BLOCK / JS_PD, RP = BLOCK / NP;          // 16 parts of 16 rows
+        const uint32_t d = threadIdx.x & (JS_PD - 1), part = threadIdx.x / JS_PD;
+        uint32_t v = 0;
+#pragma unroll
+        for (int t = 0; t < RP; ++t) v = max(v, sh[(part * RP + t) * (JS_PD + 1) + d]);
+        red[threadIdx.x] = v;
+    }
+    __syncthreads();
     if (threadIdx.x < JS_PD) {
         uint32_t v = 0;
-        for (int t = 0; t < BLOCK; ++t) v = max(v, sh[t * (JS_PD + 1) + threadIdx.x]);
+#pragma unroll
+        for (int p = 0; p < BLOCK / JS_PD; ++p) v = max(v, red[p * JS_PD + threadIdx.x]);
         tagg[(size_t)blockIdx.x * JS_PD + threadIdx.x] = v;
     }
 }
