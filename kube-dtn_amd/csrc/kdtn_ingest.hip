@@ -529,8 +529,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_par_apply(const uint2* toks, uint3
     __syncthreads();
 #pragma unroll
     for (int d = 0; d < JS_PD; ++d) {
-        uint32_t ex = __shfl_up(incl[d], 1, 64);
-        if (lane == 0) ex = 0;
+        uint32_t ex = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl[d], 0x138, 0xf, 0xf, false);   // wave_shr:1
         for (uint32_t w = 0; w < wave; ++w) ex = max(ex, wt[w][d]);
         row[d] = max(ex, texcl[(size_t)blockIdx.x * JS_PD + d]);
     }
