@@ -256,13 +256,21 @@ KD_INLINE uint32_t kind_of(uint32_t c) {
     }
 }
 
-// position of the r-th (0-based) set bit of m (r < popcount(m))
+// position of the r-th (0-based) set bit of m (r < popcount(m)): the 32-bit half first, then
+// a 32-bit binary search (halves the 64-bit popcount / shift work of a 64-bit search)
 KD_INLINE uint32_t select_bit(uint64_t m, uint32_t r) {
-    uint32_t pos = 0;
+    const uint32_t lo = (uint32_t)m, c = __popc(lo);
+    const bool up = r >= c;
+    uint32_t x = up ? (uint32_t)(m >> 32) : lo;
+    r = up ? r - c : r;
+    uint32_t pos = up ? 32u : 0u;
 #pragma unroll
-    for (int w = 32; w >= 1; w >>= 1) {
-        const uint32_t c = __popcll(m & ((1ull << w) - 1));
-        if (r >= c) { r -= c; m >>= w; pos += w; }
+    for (int w = 16; w >= 1; w >>= 1) {
+        const uint32_t cw = __popc(x & ((1u << w) - 1u));
+        const bool hi = r >= cw;
+        r = hi ? r - cw : r;
+        x = hi ? x >> w : x;
+        pos += hi ? (uint32_t)w : 0u;
     }
     return pos;
 }
