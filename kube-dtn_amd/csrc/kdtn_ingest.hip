@@ -969,9 +969,12 @@ KD_INLINE uint32_t child_role(const JsDoc& j, const uint2* toks, uint32_t r, uin
     case R_STATUS:
         return (kind == TK_ARR && match_key(j, kpos, kLinks, 1) == 0) ? R_STATUS_LINKS : R_NONE;
     case R_LINK_S:
-    case R_LINK_R:
-        return (kind == TK_OBJ && match_key(j, kpos, kLink, KDTN_NKEY + 2) == KDTN_NKEY + 1)
-                   ? (r == R_LINK_S ? R_PROPS_S : R_PROPS_R) : R_NONE;
+    case R_LINK_R: {                                  // only "properties" opens a container here
+        if (kind != TK_OBJ) return R_NONE;
+        const KeyName k = key_name(j, kpos);
+        const uint64_t* nm = reinterpret_cast<const uint64_t*>(kLink[KDTN_NKEY + 1]);
+        return (k.ok && k.lo == nm[0] && k.hi == nm[1]) ? (r == R_LINK_S ? R_PROPS_S : R_PROPS_R) : R_NONE;
+    }
     default:
         return R_NONE;
     }
