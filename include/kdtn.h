@@ -28,6 +28,8 @@
  *   kdtn_epoch_tc         synthesises SetVethQdiscs' `tc ... tbf` argv (common/qdisc.go:252-266)
  *   kdtn_epoch_remote_encode  marshals the RemotePod bodies of Remote.Update
  *                         (common/utils.go:39-67, daemon/kubedtn/handler.go:348-371)
+ *   kdtn_epoch_late_pods  getPod's API-server fallback on an informer miss
+ *                         (daemon/kubedtn/handler.go:35-39): late pod rows for the lookup
  *
  * Conventions
  *   - No C++ or HIP types cross this ABI: plain pointers, sizes and PODs.
@@ -267,6 +269,11 @@ typedef struct kdtn_counts { uint32_t n_del, n_add, n_upd, n_topos; } kdtn_count
 #define KDTN_STAGE_QDISC   0x4u   /* MakeQdiscs for add ∪ update entries                */
 #define KDTN_STAGE_ALL     0x7u
 
+/* One context drives one GPU, and one process (rank) drives one context: SURVEY §8(b)'s
+ * num_gpus / device-id list / capacities are deliberately not fields here. A controller
+ * over G GPUs runs G ranks (kdtn_comm_init / kdtn_comm_set_ranks) and routes each Topology
+ * with kdtn_topology_shard; buffers are sized from each upload (and grow with headroom), so
+ * there is no capacity to declare up front. */
 typedef struct kdtn_config {
     int32_t  device;         /* HIP device ordinal; -1 = current device                */
     int32_t  vxlan_base;     /* common/constants.go:8 VxlanBase (5000)                  */
@@ -645,6 +652,27 @@ int kdtn_comm_init(kdtn_ctx* ctx, const uint8_t unique_id[128], int nranks, int 
 int kdtn_comm_set_ranks(kdtn_ctx* ctx, int nranks, int rank);          /* host transport */
 int kdtn_pods_export(kdtn_ctx* ctx, kdtn_pod_row* rows);                /* [pod_slice] rows */
 int kdtn_pods_import(kdtn_ctx* ctx, const kdtn_pod_row* rows, uint64_t n);   /* n = pod_slice*nranks */
+
+/* ---- getPod's API-server fallback (daemon/kubedtn/handler.go:27-41) -------------------
+ * getPod reads the informer store and, on a miss, GETs the Topology from the API server
+ * (m.tClient.Topology(ns).Get). The engine resolves peers against the uploaded table only: a
+ * peer absent from it is KDTN_E_PEER_LOOKUP in kdtn_resolved.err. The driver contract:
+ *   1. after kdtn_epoch_sync / download, list the AddLinks entries with err ==
+ *      KDTN_E_PEER_LOOKUP; each names the key (topology namespace, or "default" when empty;
+ *      link.PeerPod) — handler.go:375 getPod(ctx, link.PeerPod, localPod.KubeNs);
+ *   2. GET each distinct key; a key the API server does not have stays a miss (the
+ *      reference returns that GET's error, which is the same failing step);
+ *   3. intern the fetched Topologies' status.src_ip / net_ns strings (a dictionary that
+ *      grows goes up first as a kdtn_epoch_upload_delta with n_changed = 0 and
+ *      kdict_keep = the resident size), then pass their pod rows here;
+ *   4. kdtn_epoch_run + sync + download again, and only then take each batch's first error.
+ * The late rows join the peer lookup of every following run as global pod indices
+ * nranks*pod_slice + i (kdtn_resolved.peer_topo; the downstream stages read their rows like
+ * any other pod's), after the gathered table, so a key the table already holds keeps its
+ * table row (the informer store wins, as in getPod). They belong to no batch. Every rank of
+ * a sharded run passes the same rows. Cleared by the next kdtn_epoch_upload, upload_delta,
+ * JSON ingest or kdtn_epoch_commit. Ids must be below the resident kdict size (KDTN_EINVAL). */
+int kdtn_epoch_late_pods(kdtn_ctx* ctx, const kdtn_pod_row* rows, uint32_t n);
 
 /* ---- VxlanManager state after the epoch ---------------------------------------------
  * Replaces the daemons' map mutations (daemon/vxlan/manager.go:57-63 Add / Delete, called at

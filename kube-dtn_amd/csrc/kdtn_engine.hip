@@ -111,6 +111,9 @@ struct kdtn_ctx {
     // pods
     DevBuf pods, pod_ovf, pod_direct;
     uint32_t slice = 0, pod_total = 0, ovf_mask = 0, kb_words = 0, pod_stamp = 0;
+    // late pods (kdtn_epoch_late_pods): rows [pod_total, pod_total + n_late) of `pods`, after
+    // the gathered table; cleared by the next upload, delta, ingest or commit (prepare_work)
+    uint32_t n_late = 0;
     // pods_ready: pods / pod_direct / pod_ovf hold the complete tables of the current rows (a
     // full build ran and every later row change was patched). pods_delta: this upload's rows were
     // patched in kdtn_epoch_upload_delta, so its runs do no pod-table work.
@@ -147,7 +150,7 @@ struct kdtn_ctx {
     DevBuf ji_ns, ji_name, ji_src, ji_netns, ji_flags, ji_roff, ji_noff, ji_kb, ji_ko, ji_pb, ji_po;
     DevLinkStore ji_des, ji_real;
     DevBuf ji_kmap, ji_pmap, ji_miss, ji_mlen, ji_rank, ji_boff, ji_nil, ji_keep, ji_kpos, ji_claim, ji_res,
-        ji_created, ji_cpos, ji_keys, ji_vals, ji_del, ji_ref;
+        ji_created, ji_cpos, ji_keys, ji_vals, ji_dkeys, ji_del, ji_ref;
     // resident string indexes (string → id) of the dictionaries' first n strings
     struct StrIndex {
         DevBuf slots;
@@ -254,6 +257,18 @@ void retire(void* p, size_t bytes) {
     if (flush) retired_flush();
 }
 
+// hipMalloc that first gives back the retired buffers when the device is out of memory (up to
+// kRetireBytes may only be waiting to be freed; hipFree waits for the work that uses them)
+hipError_t dev_malloc(void** p, size_t bytes) {
+    hipError_t e = hipMalloc(p, bytes);
+    if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) {
+        (void)hipGetLastError();
+        retired_flush();
+        e = hipMalloc(p, bytes);
+    }
+    return e;
+}
+
 int ensure(DevBuf& b, size_t bytes) {
     bytes = std::max<size_t>(bytes, 256);
     if (b.cap >= bytes) return KDTN_OK;
@@ -264,7 +279,7 @@ int ensure(DevBuf& b, size_t bytes) {
     b.p = nullptr;
     b.cap = 0;
     alloc_log("ensure", bytes);
-    hipError_t e = hipMalloc(&b.p, bytes);
+    hipError_t e = dev_malloc(&b.p, bytes);
     if (e != hipSuccess) {
         std::snprintf(g_last_error, sizeof(g_last_error), "hipMalloc(%zu): %s", bytes,
                       hipGetErrorString(e));
@@ -282,7 +297,7 @@ int ensure_keep(DevBuf& b, size_t bytes, size_t keep, hipStream_t s) {
     const size_t cap = std::max(bytes, b.cap + b.cap / 2);
     alloc_log("ensure_keep", cap);
     void* np = nullptr;
-    hipError_t e = hipMalloc(&np, cap);
+    hipError_t e = dev_malloc(&np, cap);
     if (e != hipSuccess) {
         std::snprintf(g_last_error, sizeof(g_last_error), "hipMalloc(%zu): %s", cap, hipGetErrorString(e));
         return KDTN_ENOMEM;
@@ -305,6 +320,18 @@ void release(DevBuf& b) {
         int _r = (expr);            \
         if (_r != KDTN_OK) return _r; \
     } while (0)
+
+// Scope guard of a call that enqueued copies from caller memory: an early (error) return waits
+// for the streams; the normal path disarms it once it has synchronised itself.
+struct StreamsDrain {
+    hipStream_t a, b;
+    bool armed = true;
+    ~StreamsDrain() {
+        if (!armed) return;
+        (void)hipStreamSynchronize(a);
+        if (b != a) (void)hipStreamSynchronize(b);
+    }
+};
 
 int upload(kdtn_ctx* c, DevBuf& b, const void* src, size_t bytes) {
     TRY(ensure(b, bytes));
@@ -704,6 +731,8 @@ int prepare_work(kdtn_ctx* c, uint32_t slice, uint32_t M, uint32_t N) {
         return KDTN_EINVAL;
     }
     c->pod_total = slice * (uint32_t)c->nranks;
+    if (c->n_late) c->pods_ready = false;
+    c->n_late = 0;
     c->ovf_mask = next_pow2((uint64_t)c->pod_total * 2) - 1;
     TRY(ensure(c->pods, (size_t)c->pod_total * 16));
     if (c->pod_ovf.cap < (size_t)(c->ovf_mask + 1) * 8) {       // stamped slots start zeroed
@@ -917,7 +946,7 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->ji_flags, &c->ji_roff, &c->ji_noff, &c->ji_kb, &c->ji_ko, &c->ji_pb, &c->ji_po,
                       &c->ji_des.buf, &c->ji_real.buf, &c->ji_kmap, &c->ji_pmap, &c->ji_miss, &c->ji_mlen,
                       &c->ji_rank, &c->ji_boff, &c->ji_nil, &c->ji_keep, &c->ji_kpos, &c->ji_claim, &c->ji_res,
-                      &c->ji_created, &c->ji_cpos, &c->ji_keys, &c->ji_vals, &c->ji_del, &c->ji_ref,
+                      &c->ji_created, &c->ji_cpos, &c->ji_keys, &c->ji_vals, &c->ji_dkeys, &c->ji_del, &c->ji_ref,
                       &c->ix_k.slots, &c->ix_p.slots};
     for (DevBuf* b : bufs) release(*b);
     retired_flush();
@@ -1061,7 +1090,8 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
     constexpr int fuse_mode = 0;
 #endif
     const bool fused = fuse_mode && resolve && !pods_cur && c->nranks == 1 && !c->comm && c->pod_total &&
-                       c->pod_total == c->slice;
+                       c->pod_total == c->slice && !c->n_late;
+    const uint32_t pod_rows = c->pod_total + c->n_late;             // gathered table + late pods
     uint32_t* special = dp<uint32_t>(c->kd_special);
     const uint32_t n16 = (uint32_t)(sync_bytes(c->nwg) / 16);
     const uint32_t nbz = std::min<uint32_t>(nblocks(n16), 256);
@@ -1163,10 +1193,11 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
                 HIP_TRY(hipMemsetAsync(c->pod_ovf.p, 0, c->pod_ovf.cap, s));
                 c->pod_stamp = 1;
             }
-            if (c->pod_total && !pods_cur) {
-                k_pod_direct_scatter<<<nblocks(c->pod_total), BLOCK, 0, s>>>(
-                    dp<uint4>(c->pods), c->pod_total, dp<uint32_t>(c->kd_bits) + (size_t)KB_PHYSICAL * c->kb_words,
-                    dp<uint4>(c->pod_direct), c->pod_stamp, c->D, c->pods_rank_major ? (uint32_t)c->nranks : 1u);
+            if (pod_rows && !pods_cur) {
+                k_pod_direct_scatter<<<nblocks(pod_rows), BLOCK, 0, s>>>(
+                    dp<uint4>(c->pods), pod_rows, dp<uint32_t>(c->kd_bits) + (size_t)KB_PHYSICAL * c->kb_words,
+                    dp<uint4>(c->pod_direct), c->pod_stamp, c->D, c->pods_rank_major ? (uint32_t)c->nranks : 1u,
+                    c->pod_total);
             }
             if (c->V) TRY(build_vni_table(c));
             timer_mark(c, "hash_build", 2);
@@ -1232,13 +1263,13 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         if (const char* ev = std::getenv("KDTN_SPLIT")) if (std::atoi(ev) > 0) w.split = (uint32_t)std::atoi(ev);
 #endif
         if (fused) {                                    // verify + prefix ran in k_pdict_verify
-        } else if (resolve && c->pod_total && !pods_cur) {   // the pod-table verify with the full-prefix scan
-            const uint32_t nbv = nblocks(c->pod_total);
+        } else if (resolve && pod_rows && !pods_cur) {   // the pod-table verify with the full-prefix scan
+            const uint32_t nbv = nblocks(pod_rows);
             const uint32_t nbp = (uint32_t)std::min<uint64_t>(4 * FP_GRID, (c->T + 4 * BLOCK - 1) / (4 * BLOCK));
             k_pod_verify_prefix<<<nbv + std::max<uint32_t>(nbp, 1), BLOCK, 0, s>>>(
-                dp<uint4>(c->pods), c->pod_total, dp<uint4>(c->pod_direct), c->pod_stamp,
+                dp<uint4>(c->pods), pod_rows, dp<uint4>(c->pod_direct), c->pod_stamp,
                 dp<unsigned long long>(c->pod_ovf), c->ovf_mask, c->D, T, sync + SYNC_FIRST_PARTIAL_INV, nbv,
-                c->pods_rank_major ? (uint32_t)c->nranks : 1u);
+                c->pods_rank_major ? (uint32_t)c->nranks : 1u, c->pod_total);
             timer_mark(c, "verify_prefix", 2);
         } else {
             k_full_prefix<<<(unsigned)std::min<uint64_t>(FP_GRID, (c->T + 4 * FP_BLOCK - 1) / (4 * FP_BLOCK)), FP_BLOCK, 0, s>>>(
@@ -2607,6 +2638,44 @@ int kdtn_pods_import(kdtn_ctx* c, const kdtn_pod_row* rows, uint64_t n) {
     return KDTN_OK;
 }
 
+// getPod's API-server fallback (include/kdtn.h): rows of Topologies the informer store missed,
+// after the gathered pod table, in every following run's peer lookup
+int kdtn_epoch_late_pods(kdtn_ctx* c, const kdtn_pod_row* rows, uint32_t n) {
+    if (!c || !c->uploaded || (n && !rows)) return KDTN_EINVAL;
+    HIP_TRY(hipSetDevice(c->device));
+    g_last_error[0] = 0;
+    const uint32_t D = c->D;
+    for (uint32_t i = 0; i < n; ++i) {
+        const kdtn_pod_row& r = rows[i];
+        if (r.ns >= D || r.name >= D || r.src_ip >= D || (r.net_ns_nil & 0x7FFFFFFFu) >= D) {
+            std::snprintf(g_last_error, sizeof(g_last_error),
+                          "kdtn_epoch_late_pods: row %u names a string past the dictionary (%u strings)", i, D);
+            return KDTN_EINVAL;
+        }
+    }
+    const uint64_t all = (uint64_t)c->pod_total + n;
+    if (all > POD_INDEX) {
+        std::snprintf(g_last_error, sizeof(g_last_error), "kdtn_epoch_late_pods: pod table of %llu entries exceeds 2^30",
+                      (unsigned long long)all);
+        return KDTN_EINVAL;
+    }
+    hipStream_t s = c->stream;
+    if (c->dl_pending) HIP_TRY(hipStreamWaitEvent(s, c->ev_dl_done, 0));
+    // the gathered rows stay (a host-transport import, a sharded ingest's fill)
+    TRY(ensure_keep(c->pods, (size_t)all * 16, (size_t)c->pod_total * 16, s));
+    c->ovf_mask = next_pow2(all * 2) - 1;
+    if (c->pod_ovf.cap < (size_t)(c->ovf_mask + 1) * 8) {       // stamped slots start zeroed
+        TRY(ensure(c->pod_ovf, (size_t)(c->ovf_mask + 1) * 8));
+        HIP_TRY(hipMemsetAsync(c->pod_ovf.p, 0, c->pod_ovf.cap, s));
+    }
+    if (n) HIP_TRY(hipMemcpyAsync(dp<uint4>(c->pods) + c->pod_total, rows, (size_t)n * 16, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipStreamSynchronize(s));             // the caller's rows may be released on return
+    c->n_late = n;
+    c->pods_ready = false;                        // the next run builds the lookup over every row
+    c->pods_delta = false;
+    return KDTN_OK;
+}
+
 int kdtn_debug_wg_trace(kdtn_ctx* c, uint64_t* out, uint32_t cap) {
     if (!c || !c->traced) return KDTN_EINVAL;
     HIP_TRY(hipSetDevice(c->device));
@@ -3138,6 +3207,15 @@ int kdtn_epoch_upload_delta(kdtn_ctx* c, const kdtn_epoch_delta* d) {
         return KDTN_EINVAL;
     }
     if (kk > c->kd_valid || pk > c->pd_valid) return bad("the resident dictionaries were not parsed (run first)", kk);
+    // the kept prefixes end where the resident arenas end (before any copy is enqueued: the
+    // suffixes are written at the host's offsets, which must not overlap resident bytes)
+    if (d->kdict.offs[kk] != c->kd_arena || d->pdict.offs[pk] != c->pd_arena) {
+        std::snprintf(g_last_error, sizeof(g_last_error),
+                      "delta: the kept dictionary prefixes end at byte %u / %u, the resident arenas at %llu / %llu",
+                      d->kdict.offs[kk], d->pdict.offs[pk], (unsigned long long)c->kd_arena,
+                      (unsigned long long)c->pd_arena);
+        return KDTN_EINVAL;
+    }
     if (n > Tn) return bad("more changed topologies than topologies", n);
     if (n && (!d->topo || !d->src_ip || !d->net_ns || !d->spec_nil || !d->des_off)) return bad("missing column", 0);
     if (remap && n && (!d->ns || !d->name)) return bad("missing ns / name of the changed topologies", 0);
@@ -3201,7 +3279,10 @@ int kdtn_epoch_upload_delta(kdtn_ctx* c, const kdtn_epoch_delta* d) {
     }
     TRY(link_store_alloc(c, c->sh_des, (uint32_t)nbound));
     if (remap) TRY(link_store_alloc(c, c->sh_real, M0));
-    // --- copies (copy stream), after everything already queued on the context stream
+    // --- copies (copy stream), after everything already queued on the context stream. From here
+    // on an error return first waits for both streams: the copies read the caller's arrays,
+    // which it may release once the call has returned
+    StreamsDrain drain{s, cs};
     HIP_TRY(hipEventRecord(c->ev_cp[0], s));
     if (cs != s) HIP_TRY(hipStreamWaitEvent(cs, c->ev_cp[0], 0));
     {   // segments in pack order; host-adjacent neighbours merge into one copy. The per-Topology
@@ -3344,6 +3425,11 @@ int kdtn_epoch_upload_delta(kdtn_ctx* c, const kdtn_epoch_delta* d) {
         c->kd_from = saved[4], c->pd_from = saved[5];
         c->kd_arena = saved_arena[0], c->pd_arena = saved_arena[1];
         c->uploaded = !(err & DERR_KEEP);
+        if (err & DERR_KEEP) {                     // the resident strings themselves are suspect
+            c->kd_valid = c->pd_valid = 0;
+            c->ix_k.n = c->ix_k.mask = 0;
+            c->ix_p.n = c->ix_p.mask = 0;
+        }
         return KDTN_EINVAL;
     }
     if (hm[MISC_DELTA_MULTI]) {
@@ -3388,6 +3474,7 @@ int kdtn_epoch_upload_delta(kdtn_ctx* c, const kdtn_epoch_delta* d) {
     state_changed(c);
     c->pods_imported = false;
     c->uploaded = true;
+    drain.armed = false;
     return KDTN_OK;
 }
 
@@ -3503,8 +3590,14 @@ int kdtn_json_ingest_delta(kdtn_ctx* c, const uint32_t* deleted, uint32_t n_dele
     TRY(d2h(c, cnt, dp<uint64_t>(c->ji_rank) + k.D));
     TRY(d2h(c, cnt + 1, dp<uint64_t>(c->ji_boff) + k.D));
     HIP_TRY(hipStreamSynchronize(s));
-    const uint32_t D1 = D0 + (uint32_t)cnt[0];
+    const uint64_t D1w = (uint64_t)D0 + cnt[0];
     const uint64_t kar1 = c->kd_arena + cnt[1];
+    // offsets are u32 (arena0 + boff): bounded before anything is appended
+    if (kar1 > 0xFFFFFF00ull || D1w >= 0x7FFFFFFFull) {
+        std::snprintf(g_last_error, sizeof(g_last_error), "kdtn_json_ingest_delta: key dictionary over 4 GiB / 2^31");
+        return KDTN_EINVAL;
+    }
+    const uint32_t D1 = (uint32_t)D1w;
     TRY(ensure_keep(c->kd_bytes, kar1 + 64, c->kd_arena, s));
     TRY(ensure_keep(c->kd_offs, ((size_t)D1 + 1) * 4, ((size_t)D0 + 1) * 4, s));
     if (k.D)
@@ -3517,9 +3610,10 @@ int kdtn_json_ingest_delta(kdtn_ctx* c, const uint32_t* deleted, uint32_t n_dele
     TRY(d2h(c, cnt + 2, dp<uint64_t>(c->ji_kpos) + k.P));
     TRY(d2h(c, cnt + 3, dp<uint64_t>(c->ji_cpos) + k.P));
     HIP_TRY(hipStreamSynchronize(s));
-    const uint32_t P1 = P0 + (uint32_t)cnt[2];
+    const uint64_t P1w = (uint64_t)P0 + cnt[2];
     const uint64_t par1 = c->pd_arena + cnt[3];
-    if (kar1 > 0xFFFFFF00ull || par1 > 0xFFFFFF00ull || (uint64_t)D1 >= 0x7FFFFFFFu || (uint64_t)P1 >= 0x7FFFFFFFu) {
+    const uint32_t P1 = (uint32_t)P1w;
+    if (par1 > 0xFFFFFF00ull || P1w >= 0x7FFFFFFFull) {
         std::snprintf(g_last_error, sizeof(g_last_error), "kdtn_json_ingest_delta: dictionaries over 4 GiB / 2^31");
         return KDTN_EINVAL;
     }
@@ -3554,6 +3648,8 @@ int kdtn_json_ingest_delta(kdtn_ctx* c, const uint32_t* deleted, uint32_t n_dele
     const uint64_t kcap = next_pow2(2ull * T0 + 64);
     TRY(ensure(c->ji_keys, (size_t)kcap * 8));
     TRY(ensure(c->ji_vals, (size_t)kcap * 4));
+    const uint64_t dcap = next_pow2(2ull * Tl + 64);
+    TRY(ensure(c->ji_dkeys, (size_t)dcap * 8));
     TRY(ensure(c->ji_keep, (size_t)T0 * 4 + 16));
     TRY(ensure(c->ji_kpos, ((size_t)T0 + 1) * 8));
     TRY(ensure(c->ji_claim, (size_t)T0 * 4 + 16));
@@ -3565,6 +3661,7 @@ int kdtn_json_ingest_delta(kdtn_ctx* c, const uint32_t* deleted, uint32_t n_dele
     HIP_TRY(hipMemsetAsync(misc + MISC_DELTA_ERR, 0, 4, s));
     HIP_TRY(hipMemsetAsync(c->ji_keys.p, 0, (size_t)kcap * 8, s));
     HIP_TRY(hipMemsetAsync(c->ji_vals.p, 0xFF, (size_t)kcap * 4, s));
+    HIP_TRY(hipMemsetAsync(c->ji_dkeys.p, 0, (size_t)dcap * 8, s));
     HIP_TRY(hipMemsetAsync(c->ji_claim.p, 0xFF, (size_t)T0 * 4 + 16, s));
     if (T0) HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(c->ji_keep.p), 1, T0, s));
     if (T0)
@@ -3579,7 +3676,8 @@ int kdtn_json_ingest_delta(kdtn_ctx* c, const uint32_t* deleted, uint32_t n_dele
     if (Tl)
         k_topokey_match<<<nblocks(Tl), BLOCK, 0, s>>>(dp<uint32_t>(c->ji_ns), dp<uint32_t>(c->ji_name), Tl,
                                                       dp<unsigned long long>(c->ji_keys), dp<uint32_t>(c->ji_vals),
-                                                      (uint32_t)kcap - 1, dp<uint32_t>(c->ji_keep),
+                                                      (uint32_t)kcap - 1, dp<unsigned long long>(c->ji_dkeys),
+                                                      (uint32_t)dcap - 1, dp<uint32_t>(c->ji_keep),
                                                       dp<uint32_t>(c->ji_claim), dp<uint32_t>(c->ji_res),
                                                       dp<uint32_t>(c->ji_created), misc + MISC_DELTA_ERR);
     TRY(scan_u32(c, dp<uint32_t>(c->ji_keep), T0, dp<uint64_t>(c->ji_kpos)));

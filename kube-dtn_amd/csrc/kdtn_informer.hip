@@ -134,10 +134,12 @@ __global__ void __launch_bounds__(BLOCK) k_topokey_insert(const uint32_t* ns, co
 
 // Each document Topology against the resident rows: res[l] = its resident row or NONE
 // (created); claims[row] = l, and a row claimed twice (an object listed twice), or claimed and
-// deleted, is an error. created[l] = 1 for the scan that places created rows.
+// deleted, is an error. A created key is claimed in its own table (dkeys): a second claim is an
+// object listed twice too. created[l] = 1 for the scan that places created rows.
 __global__ void __launch_bounds__(BLOCK) k_topokey_match(const uint32_t* ns, const uint32_t* name, uint32_t Tl,
                                                          const unsigned long long* keys, const uint32_t* vals,
-                                                         uint32_t mask, const uint32_t* keep, uint32_t* claim,
+                                                         uint32_t mask, unsigned long long* dkeys, uint32_t dmask,
+                                                         const uint32_t* keep, uint32_t* claim,
                                                          uint32_t* res, uint32_t* created, uint32_t* err) {
     const uint32_t l = blockIdx.x * BLOCK + threadIdx.x;
     uint32_t e = 0;
@@ -157,6 +159,15 @@ __global__ void __launch_bounds__(BLOCK) k_topokey_match(const uint32_t* ns, con
         if (row != 0xFFFFFFFFu) {
             if (!keep[row]) e |= 1u;                                   // updated and deleted
             if (atomicExch(claim + row, l) != 0xFFFFFFFFu) e |= 2u;   // listed twice
+        } else {
+            for (uint32_t p = (uint32_t)hash64(k) & dmask;; p = (p + 1) & dmask) {
+                const unsigned long long cur = atomicCAS(dkeys + p, 0ull, k);
+                if (cur == 0) break;
+                if (cur == k) {                                        // created twice
+                    e |= 2u;
+                    break;
+                }
+            }
         }
     }
 #pragma unroll

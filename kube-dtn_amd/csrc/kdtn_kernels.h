@@ -248,7 +248,7 @@ __global__ void k_pods_fill(DevTopos T, uint32_t slice, uint32_t rank_base, uint
 __global__ void k_epoch_begin(uint4* sync, uint32_t n16, uint32_t nbz, DevTopos T, uint32_t slice, uint32_t rank_base,
                               uint4* pods);
 __global__ void k_pod_direct_scatter(const uint4* pods, uint32_t total, const uint32_t* phys_bits,
-                                     uint4* slots, uint32_t stamp, uint32_t nd, uint32_t nr);
+                                     uint4* slots, uint32_t stamp, uint32_t nd, uint32_t nr, uint32_t gathered);
 __global__ void k_epoch_front(uint4* sync, uint32_t n16, uint32_t nbz, uint32_t nbs, DevTopos T, uint32_t slice,
                               uint4* pods, uint4* slots, uint32_t stamp, const uint8_t* kd_bytes,
                               const uint32_t* kd_offs, uint32_t k0, uint32_t D, uint32_t* kbits, uint32_t kb_words,
@@ -411,7 +411,8 @@ __global__ void k_ix_map_links(uint32_t* base, uint32_t n, const uint32_t* kmap,
 __global__ void k_topokey_insert(const uint32_t* ns, const uint32_t* name, uint32_t T, unsigned long long* keys,
                                  uint32_t* vals, uint32_t mask);
 __global__ void k_topokey_match(const uint32_t* ns, const uint32_t* name, uint32_t Tl, const unsigned long long* keys,
-                                const uint32_t* vals, uint32_t mask, const uint32_t* keep, uint32_t* claim,
+                                const uint32_t* vals, uint32_t mask, unsigned long long* dkeys, uint32_t dmask,
+                                const uint32_t* keep, uint32_t* claim,
                                 uint32_t* res, uint32_t* created, uint32_t* err);
 __global__ void k_topo_delete(const uint32_t* del, uint32_t n, uint32_t T, uint32_t* keep, uint32_t* err);
 __global__ void k_ix_layout(const uint32_t* keep, const uint64_t* kpos, uint32_t T0, const uint32_t* claim,
@@ -598,7 +599,7 @@ constexpr int FP_BLOCK = 1024, FP_GRID = 256;       // k_full_prefix launch shap
 __global__ void k_full_prefix(DevTopos T, uint32_t* first_partial_inv);
 __global__ void k_pod_verify_prefix(const uint4* pods, uint32_t total, uint4* slots, uint32_t stamp,
                                     unsigned long long* ovf, uint32_t mask, uint32_t nd, DevTopos T,
-                                    uint32_t* first_partial_inv, uint32_t nbv, uint32_t nr);
+                                    uint32_t* first_partial_inv, uint32_t nbv, uint32_t nr, uint32_t gathered);
 
 // ---- CR ingest: TopologyList JSON → epoch tables (kdtn_ingest.hip) ------------------------
 // token word: {byte offset, pre-depth | kind << 24}

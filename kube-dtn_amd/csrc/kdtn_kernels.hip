@@ -734,18 +734,20 @@ KD_INLINE void ovf_insert(const uint4* pods, uint32_t g, uint32_t ns, uint32_t n
 // position and their name slots lie close together (in rank-major order consecutive rows
 // are ~nr informer positions apart: at N = 8 the slot stores and verify loads touched 2x the
 // lines of N = 1).
+// Rows past the gathered table (total) are the late pods of kdtn_epoch_late_pods, in order.
 KD_INLINE uint32_t pod_order(uint32_t t, uint32_t total, uint32_t nr) {
-    if (nr <= 1) return t;
+    if (nr <= 1 || t >= total) return t;
     const uint32_t slice = total / nr;
     return (t % nr) * slice + t / nr;
 }
 
 __global__ void __launch_bounds__(BLOCK) k_pod_direct_scatter(const uint4* pods, uint32_t total,
                                                               const uint32_t* phys_bits, uint4* slots,
-                                                              uint32_t stamp, uint32_t nd, uint32_t nr) {
+                                                              uint32_t stamp, uint32_t nd, uint32_t nr,
+                                                              uint32_t gathered) {
     const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
     if (t >= total) return;
-    const uint32_t g = pod_order(t, total, nr);
+    const uint32_t g = pod_order(t, gathered, nr);
     const uint4 e = pods[g];
     if (e.x == 0xFFFFFFFFu || e.y >= nd) return;           // padding row / name outside this dictionary
     const uint32_t phys = (phys_bits[e.y >> 5] >> (e.y & 31)) & 1u;
@@ -1611,11 +1613,11 @@ __global__ void __launch_bounds__(FP_BLOCK) k_full_prefix(DevTopos T, uint32_t* 
 __global__ void __launch_bounds__(BLOCK) k_pod_verify_prefix(const uint4* pods, uint32_t total, uint4* slots,
                                                              uint32_t stamp, unsigned long long* ovf, uint32_t mask,
                                                              uint32_t nd, DevTopos T, uint32_t* first_partial_inv,
-                                                             uint32_t nbv, uint32_t nr) {
+                                                             uint32_t nbv, uint32_t nr, uint32_t gathered) {
     __shared__ uint32_t bmin;
     if (blockIdx.x < nbv) {
         const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
-        if (t < total) pod_verify_one(pods, total, slots, stamp, ovf, mask, nd, pod_order(t, total, nr));
+        if (t < total) pod_verify_one(pods, total, slots, stamp, ovf, mask, nd, pod_order(t, gathered, nr));
         return;
     }
     full_prefix_blocks<BLOCK>(T, first_partial_inv, blockIdx.x - nbv, gridDim.x - nbv, &bmin);

@@ -202,7 +202,7 @@ EXPORTS = ["kdtn_version", "kdtn_strerror", "kdtn_err_name", "kdtn_init", "kdtn_
            "kdtn_ingest_shard_topos", "kdtn_epoch_remote_encode", "kdtn_epoch_download_remote",
            "kdtn_epoch_commit", "kdtn_epoch_upload_delta", "kdtn_epoch_tables_info",
            "kdtn_vni_ops_export", "kdtn_vni_ops_import", "kdtn_json_ingest_delta",
-           "kdtn_epoch_download_async", "kdtn_epoch_download_wait"]
+           "kdtn_epoch_download_async", "kdtn_epoch_download_wait", "kdtn_epoch_late_pods"]
 
 
 def ptr(a: np.ndarray, t):

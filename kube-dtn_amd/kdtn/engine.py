@@ -6,6 +6,7 @@ calls raise — the reconcile path only runs on the GPU.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes as C
 import os
 import weakref
@@ -114,13 +115,40 @@ def lib() -> C.CDLL:
         "kdtn_json_ingest_delta": (C.c_int, [vp, vp, C.c_uint32, C.POINTER(abi.VniTable), C.POINTER(abi.IngestInfo)]),
         "kdtn_epoch_download_async": (C.c_int, [vp, C.POINTER(abi.Batches)]),
         "kdtn_epoch_download_wait": (C.c_int, [vp]),
+        "kdtn_epoch_late_pods": (C.c_int, [vp, vp, C.c_uint32]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
     _lib = L
+    # registered after torch's import, so it runs before the HIP runtime's own teardown
+    atexit.register(_teardown)
     return L
+
+
+# Live contexts and page-locked buffers. At interpreter exit the contexts are destroyed (their
+# streams drained) and only then the page-locked buffers freed, while the HIP runtime is still
+# up — not from weakref finalizers in whatever order shutdown reaches them.
+_engines: "weakref.WeakSet[Engine]" = weakref.WeakSet()
+_pinned: dict[int, weakref.finalize] = {}
+
+
+def _teardown() -> None:
+    for e in list(_engines):
+        try:
+            e.close()
+        except Exception:
+            pass
+    for f in list(_pinned.values()):
+        f()
+    _pinned.clear()
+
+
+def _host_free(p: int) -> None:
+    _pinned.pop(p, None)
+    if _lib is not None:
+        _lib.kdtn_host_free(p)
 
 
 def _check(code: int, what: str) -> None:
@@ -137,7 +165,9 @@ def pinned_empty(shape, dtype) -> np.ndarray:
     if not p:
         raise MemoryError(f"kdtn_host_alloc({n})")
     buf = (C.c_uint8 * max(n, 1)).from_address(p)
-    weakref.finalize(buf, L.kdtn_host_free, p)
+    f = weakref.finalize(buf, _host_free, p)
+    f.atexit = False                       # _teardown frees it, after the contexts
+    _pinned[p] = f
     return np.frombuffer(buf, dtype=np.uint8, count=n).view(dtype).reshape(shape)
 
 
@@ -235,11 +265,17 @@ class Engine:
         self._ctx = ctx
         self._T = 0
         self._caps = (0, 0, 0)
+        _engines.add(self)
 
     def close(self) -> None:
+        """Drain an outstanding kdtn_epoch_download_async, then kdtn_destroy (which waits for
+        every stream of the context before it frees anything)."""
         if self._ctx:
-            lib().kdtn_destroy(self._ctx)
+            L = lib()
+            L.kdtn_epoch_download_wait(self._ctx)
+            L.kdtn_destroy(self._ctx)
             self._ctx = None
+            self._dl_keep = None
 
     def __enter__(self):
         return self
@@ -273,6 +309,15 @@ class Engine:
         """The gathered table of every rank's rows, rank order ((pod_slice*nranks) × 4 u32)."""
         rows = np.ascontiguousarray(rows, dtype=np.uint32)
         _check(lib().kdtn_pods_import(self._ctx, rows.ctypes.data, rows.shape[0]), "kdtn_pods_import")
+
+    def late_pods(self, rows: np.ndarray) -> None:
+        """kdtn_epoch_late_pods: pod rows (n × 4 u32 as pods_export gives them) of Topologies
+        the informer store missed and the API server returned (getPod's fallback,
+        handler.go:35-39); they join the peer lookup of the following runs as global pod
+        indices nranks*pod_slice + i."""
+        rows = np.ascontiguousarray(rows, dtype=np.uint32).reshape(-1, 4)
+        _check(lib().kdtn_epoch_late_pods(self._ctx, rows.ctypes.data if len(rows) else None, len(rows)),
+               "kdtn_epoch_late_pods")
 
     def set_stream(self, stream_handle: int | None) -> None:
         _check(lib().kdtn_set_stream(self._ctx, C.c_void_p(stream_handle or 0)), "kdtn_set_stream")

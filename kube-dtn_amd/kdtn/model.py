@@ -7,6 +7,7 @@ surface the engine replaces, so callers (and the parity tests) read like the ref
   TopologyReconciler.reconcile_all(topos)     ↔ Reconcile :61-156 for every dirty Topology
   make_qdiscs(engine, props)                  ↔ common/qdisc.go:20 MakeQdiscs
   KubeDTN.add_links / del_links / update_links↔ daemon/kubedtn/handler.go:592-671 (pure prefix)
+  peer_misses + Engine.late_pods              ↔ getPod's API-server fallback, handler.go:27-41
 
 Everything here only packs/unpacks tables; the work happens in libkdtn.so on the GPU.
 """
@@ -170,10 +171,56 @@ class TopologyReconciler:
             return [], [], []
         return b.add, b.delete, b.properties_changed
 
-    def reconcile_all(self, topos: list[Topology], vnis=()) -> list[TopologyBatches]:
-        inp = pack(topos, vnis)
+    def reconcile_all(self, topos: list[Topology], vnis=(), fetch=None) -> list[TopologyBatches]:
+        """fetch(namespace, name) -> Topology | None: the API-server GET getPod falls back to
+        when the informer store (`topos`) misses a peer (handler.go:35-39). The misses of the
+        first run are fetched, their pod rows passed to kdtn_epoch_late_pods and the epoch run
+        again; a key fetch does not know stays KDTN_E_PEER_LOOKUP."""
+        kd, pd = Interner(), Interner()
+        inp = pack(topos, vnis, kd, pd)
         out = self.engine.reconcile(inp)
+        misses = peer_misses(inp, out) if fetch is not None else []
+        late = [x for x in (fetch(ns.decode(), name.decode()) for ns, name in misses) if x is not None]
+        if late:
+            rows = late_pod_rows(late, kd)
+            D0 = inp.kdict.n
+            if len(kd) > D0:                     # the fetched pods' strings extend the dictionary
+                from .delta import build_delta
+                grown = EpochInput(kd.table(), inp.pdict, inp.topos, inp.realised, inp.desired, inp.vnis)
+                self.engine.upload_delta(build_delta(inp, grown, D0, inp.pdict.n))
+            self.engine.late_pods(rows)
+            self.engine.run()
+            self.engine.sync()
+            out = self.engine.download()
         return unpack(topos, out)
+
+
+def peer_misses(inp: EpochInput, out: BatchesOut) -> list[tuple[bytes, bytes]]:
+    """Distinct getPod keys (namespace, or "default" when empty; link.PeerPod) of the AddLinks
+    entries whose peer lookup missed (kdtn_resolved.err == KDTN_E_PEER_LOOKUP), in first-entry
+    order: what the driver GETs from the API server (handler.go:35-39, :375) before
+    kdtn_epoch_late_pods."""
+    e = np.nonzero(out.add_res["err"] == abi.E_PEER_LOOKUP)[0]
+    if not len(e):
+        return []
+    t = np.searchsorted(out.add_off.astype(np.int64), e, side="right") - 1
+    kb, ko = inp.kdict.bytes_, inp.kdict.offs
+    s = lambda i: bytes(kb[ko[i]:ko[i + 1]])
+    pcol = abi.KEY_COLS.index("peer_pod")
+    keys: dict[tuple[bytes, bytes], None] = {}
+    for ei, ti in zip(e, t):
+        keys.setdefault((s(inp.topos.ns[ti]) or b"default", s(inp.desired.key[pcol, out.add_idx[ei]])), None)
+    return list(keys)
+
+
+def late_pod_rows(late: list[Topology], kd: Interner) -> np.ndarray:
+    """kdtn_pod_row of each fetched Topology (ns, name, status src_ip, net_ns | spec-nil << 31),
+    interning its strings into `kd` (append-only)."""
+    rows = np.zeros((len(late), 4), np.uint32)
+    for i, tp in enumerate(late):
+        nil = 0x80000000 if tp.spec_links is None else 0
+        rows[i] = (kd(tp.namespace), kd(tp.name), kd(tp.src_ip), kd(tp.net_ns) | nil)
+    return rows
 
 
 def unpack(topos: list[Topology], out: BatchesOut) -> list[TopologyBatches]:

@@ -6,6 +6,9 @@ churn epochs with Topologies created and deleted is compared, epoch by epoch, wi
 delta chain (kdtn_epoch_upload_delta over the generator's tables, tests/state.py restatement):
 the same CRs with the same status and spec, id-free and order-free, and every epoch's
 batches equal the oracle's on the engine's own tables."""
+import copy
+import json
+
 import numpy as np
 import pytest
 
@@ -117,7 +120,13 @@ def test_ingest_delta_rejections_leave_the_state():
         dup_doc = synth.topology_list_json(synth.select_topologies(prev, np.array([3, 7, 3])))
         rows = key_rows(t0)
         k3 = (prev.kdict.get(int(prev.topos.ns[3])), prev.kdict.get(int(prev.topos.name[3])))
+        # a CR the state does not hold yet (an informer add and update batched together)
+        doc = json.loads(synth.topology_list_json(synth.select_topologies(prev, np.array([3]))))
+        doc["items"][0]["metadata"]["name"] = "created-twice"
+        doc["items"].append(copy.deepcopy(doc["items"][0]))
+        new_dup_doc = json.dumps(doc).encode()
         cases = [("listed twice", dup_doc, [], abi.EINVAL),
+                 ("created twice", new_dup_doc, [], abi.EINVAL),
                  ("deleted and listed", part, [rows[k3]], abi.EINVAL),
                  ("deleted out of range", part, [prev.topos.n + 5], abi.EINVAL),
                  ("malformed document", part[:-3], [], abi.EBADMSG)]

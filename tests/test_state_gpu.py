@@ -14,7 +14,7 @@ from kdtn import Engine, abi, synth
 from kdtn.delta import build_delta
 from kdtn.engine import pin_delta
 from kdtn.model import pack
-from kdtn.tables import EpochInput, Interner, Links, Topos
+from kdtn.tables import EpochInput, Interner, Links, StrTab, Topos
 from state import apply_delta, commit, predicted_commit, same_tables
 from test_state_cpu import mutate
 
@@ -186,7 +186,11 @@ def test_delta_rejections_leave_the_state():
         good = build_delta(a, b, a.kdict.n, a.pdict.n, vnis=b.vnis)
         assert good.n_changed > 2 and good.records.n > 0 and len(good.ref) > 0
         R = dataclasses.replace
+        kb, ko = good.kdict.bytes_, good.kdict.offs
+        strs = [bytes(kb[ko[i]:ko[i + 1]]) for i in range(good.kdict.n)]
+        strs[1] += b"-longer"                 # same string count, the kept prefix ends elsewhere
         bads = {"shrunk kept dictionary": R(good, kdict_keep=a.kdict.n - 1),
+                "kept prefix at another offset": R(good, kdict=StrTab.from_list(strs)),
                 "ref out of range": R(good, ref=np.where(np.arange(len(good.ref)) == len(good.ref) - 1,
                                                         np.uint32(a.desired.n + 7), good.ref).astype(np.uint32)),
                 # far outside any allocation: the GPU checks must stop every later kernel
