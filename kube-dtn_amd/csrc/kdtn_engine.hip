@@ -180,6 +180,10 @@ struct kdtn_ctx {
     // host-visible counters
     hipEvent_t ev_done = nullptr;  // the epoch's last command (kdtn_epoch_sync polls it)
     uint32_t* h_misc = nullptr;   // pinned: [1]=del, [2]=upd, [3]=add, [4]=look-back error (sync header words)
+    // coherent page-locked words the epoch's last kernel writes itself ([0..2] list totals, [3]
+    // look-back error): no readback copy per epoch (a 16-B blit kernel, 5.6 µs + a dispatch);
+    // kdtn_epoch_sync moves them to h_misc[1..4]
+    uint32_t* h_tot = nullptr;
     bool uploaded = false;
     bool ran = false;
     uint32_t last_stages = 0;
@@ -888,7 +892,9 @@ int kdtn_init(kdtn_ctx** out, const kdtn_config* cfg) {
     }
     c->stream = c->own_stream;
     // words [0, 16): epoch sync header copy; [64, 128): the misc words a delta reads back
-    if (hipHostMalloc(reinterpret_cast<void**>(&c->h_misc), 512, hipHostMallocDefault) != hipSuccess) {
+    if (hipHostMalloc(reinterpret_cast<void**>(&c->h_misc), 512, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void**>(&c->h_tot), 64, hipHostMallocCoherent) != hipSuccess) {
+        if (c->h_misc) (void)hipHostFree(c->h_misc);
         (void)hipStreamDestroy(c->own_stream);
         delete c;
         return KDTN_ENOMEM;
@@ -972,6 +978,7 @@ void kdtn_destroy(kdtn_ctx* c) {
     if (c->ev_dl_ready) (void)hipEventDestroy(c->ev_dl_ready);
     if (c->ev_dl_done) (void)hipEventDestroy(c->ev_dl_done);
     if (c->h_misc) (void)hipHostFree(c->h_misc);
+    if (c->h_tot) (void)hipHostFree(c->h_tot);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
 }
@@ -1074,6 +1081,9 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         return KDTN_EINVAL;
     }
     if (c->dl_pending) HIP_TRY(hipStreamWaitEvent(s, c->ev_dl_done, 0));   // outputs still being copied out
+    // the previous epoch's kernels are done once its sync returned, so these host stores cannot
+    // race a device write; an epoch without topologies leaves them zero
+    for (int i = 0; i < 4; ++i) __atomic_store_n(c->h_tot + i, 0u, __ATOMIC_RELAXED);
     if (c->timing >= 2) (void)hipEventRecord(c->ev[0], s);
     uint32_t* sync = dp<uint32_t>(c->sync);
     // Epoch front: first launch (sync header, look-back area, pod-status rows) + RCCL
@@ -1151,6 +1161,20 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         // dictionaries: the strings this upload added (all of them unless kdict_keep /
         // pdict_keep), from a multiple of 64 so every wave writes whole predicate words
         uint32_t* special = dp<uint32_t>(c->kd_special);
+#if KDTN_PROFILING
+        const bool dict_fuse = std::getenv("KDTN_DICT_FUSE") && std::atoi(std::getenv("KDTN_DICT_FUSE"));
+#else
+        constexpr bool dict_fuse = KDTN_DICT_FUSE_DEFAULT;
+#endif
+        const uint32_t k0f = c->kd_from & ~63u, p0f = c->pd_from & ~63u;
+        if (dict_fuse && c->D > k0f && c->P > p0f) {              // both parses in one launch
+            const uint32_t nbk = nblocks(c->D - k0f), nbp = nblocks(c->P - p0f);
+            k_dict_parse<<<3 * nbp + nbk, BLOCK, 0, s>>>(
+                dp<uint8_t>(c->kd_bytes), dp<uint32_t>(c->kd_offs), k0f, c->D, dp<uint32_t>(c->kd_bits), c->kb_words,
+                special, dp<uint8_t>(c->pd_bytes), dp<uint32_t>(c->pd_offs), p0f, c->P, nbp, c->cfg.tick_in_usec,
+                dp<uint32_t>(c->pd_pct), dp<uint2>(c->pd_dur), dp<uint2>(c->pd_rate), dp<uint32_t>(c->pd_rerr));
+            timer_mark(c, "dict_parse", 2);
+        } else {
         {
             const uint32_t k0 = c->kd_from & ~63u;                        // (clip_specials ran at upload)
             if (c->D > k0) {
@@ -1185,6 +1209,7 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
             if (c->P > p0) launch_pdict(c, p0, c->P);
         }
         timer_mark(c, "pdict_parse", 2);
+        }
         if (resolve) {
             if (exchange) HIP_TRY(hipStreamWaitEvent(s, c->ev_ag, 0));   // exchange not hidden by the parses
             timer_mark(c, "pods_allgather", 2);
@@ -1237,9 +1262,11 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         o.add_qdisc = dp<uint2>(c->add_qdisc);
         o.upd_qdisc = dp<uint2>(c->upd_qdisc);
         o.totals = sync + SYNC_TOTALS;
+        o.htotals = c->h_tot;
         o.stages = stages;
         RecWork w;
         w.sync = sync;
+        w.herr = c->h_tot + 3;
         w.status = reinterpret_cast<unsigned long long*>(static_cast<char*>(c->sync.p) + SYNC_HEADER_BYTES);
         w.hscratch = dp<uint32_t>(c->hscratch);
         w.fscratch = dp<uint8_t>(c->fscratch);
@@ -1316,12 +1343,12 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
             timer_mark(c, "place", 1);
         }
     } else {
+        HIP_TRY(hipMemsetAsync(c->h_tot, 0, 16, s));   // (an earlier run may not have been synced)
         HIP_TRY(hipMemsetAsync(c->del_off.p, 0, 4, s));
         HIP_TRY(hipMemsetAsync(c->add_off.p, 0, 4, s));
         HIP_TRY(hipMemsetAsync(c->upd_off.p, 0, 4, s));
     }
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(c->h_misc + 1, sync + SYNC_TOTALS, 16, hipMemcpyDeviceToHost, s));   // totals, look-back error
     if (c->ev_done) HIP_TRY(hipEventRecord(c->ev_done, s));
     if (resolve && !pods_cur) c->pods_ready = true;           // the full build of this upload's rows
     c->ran = true;
@@ -1347,6 +1374,7 @@ int kdtn_epoch_sync(kdtn_ctx* c, kdtn_counts* counts) {
         }
     }
     HIP_TRY(hipStreamSynchronize(c->stream));
+    for (int i = 0; i < 4; ++i) c->h_misc[1 + i] = __atomic_load_n(c->h_tot + i, __ATOMIC_ACQUIRE);
     if (c->h_misc[4] != 0) {
         std::snprintf(g_last_error, sizeof(g_last_error), "k_reconcile look-back timed out (0x%x)", c->h_misc[4]);
         return KDTN_EIO;

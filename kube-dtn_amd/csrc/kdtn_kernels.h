@@ -115,6 +115,10 @@ struct DevLinks {
 #ifndef KDTN_PROFILING
 #define KDTN_PROFILING 0
 #endif
+// epoch front: k_kdict_flags and k_pdict_parse as one launch (k_dict_parse)
+#ifndef KDTN_DICT_FUSE_DEFAULT
+#define KDTN_DICT_FUSE_DEFAULT true     // N = 8 rank epoch 0.2163 -> 0.1990 ms (profiles/r05b_fuse_ab.jsonl)
+#endif
 // k_pdict_parse: one thread per (string, interpretation) instead of one per string
 #ifndef KDTN_PD_SPLIT_DEFAULT
 #define KDTN_PD_SPLIT_DEFAULT true    // 125k-pod config 2: 0.0374 -> 0.0341 ms; 1M: equal
@@ -199,11 +203,13 @@ struct RecOut {
     uint2* add_qdisc;          // kdtn_qdisc as 9 × 8 B
     uint2* upd_qdisc;
     uint32_t* totals;          // [3] del, upd, add
+    uint32_t* htotals;         // the same [3] in page-locked host memory (no readback copy), or null
     uint32_t stages;
 };
 
 struct RecWork {
     uint32_t* sync;            // header (SYNC_*), then status at SYNC_HEADER_BYTES
+    uint32_t* herr;            // page-locked host word for a look-back error, or null
     unsigned long long* status;   // [nwg*3] look-back granules: state<<32 | count
     uint32_t* hscratch;        // [M+N] window hashes of topologies larger than CAP
     uint8_t* fscratch;         // [M+N] record flags when a workgroup exceeds CAP
@@ -245,6 +251,10 @@ template <bool SPLIT>
 __global__ void k_pdict_parse(const uint8_t* bytes, const uint32_t* offs, uint32_t first, uint32_t n, double tick,
                               uint32_t* ppct, uint2* pdur, uint2* prate, uint32_t* rate_err);
 __global__ void k_pods_fill(DevTopos T, uint32_t slice, uint32_t rank_base, uint4* pods);
+__global__ void k_dict_parse(const uint8_t* kd_bytes, const uint32_t* kd_offs, uint32_t k0, uint32_t D, uint32_t* kbits,
+                             uint32_t kb_words, uint32_t* special, const uint8_t* pd_bytes, const uint32_t* pd_offs,
+                             uint32_t p0, uint32_t P, uint32_t nbp, double tick, uint32_t* ppct, uint2* pdur,
+                             uint2* prate, uint32_t* rate_err);
 __global__ void k_epoch_begin(uint4* sync, uint32_t n16, uint32_t nbz, DevTopos T, uint32_t slice, uint32_t rank_base,
                               uint4* pods);
 __global__ void k_pod_direct_scatter(const uint4* pods, uint32_t total, const uint32_t* phys_bits,

@@ -328,6 +328,22 @@ __global__ void k_special_clip(uint32_t* special, uint32_t k0) {
     if ((t == SPECIAL_DEFAULT || t == SPECIAL_LOCALHOST) && special[t] >= k0) special[t] = 0xFFFFFFFFu;
 }
 
+// The 7 aligned dwords holding a key string's first 24 bytes. The first 3 decide the cheap
+// rejects (a first byte that starts neither an IP nor a MAC: kdict_bits then reads only bytes
+// 0-8, for "physical/" / "localhost"); only the other lanes load the rest, so a wave of pod
+// names or netns paths issues 3 window loads instead of 7.
+KD_INLINE void kdict_window(const uint8_t* bytes, uint32_t b, uint32_t len, uint32_t* d) {
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(bytes + (b & ~3u));   // arena has 64 B slack
+#pragma unroll
+    for (int k = 0; k < 3; ++k) d[k] = p[k];
+    const uint32_t c0 = (d[0] >> ((b & 3u) * 8u)) & 0xFFu;
+#pragma unroll
+    for (int k = 3; k < 7; ++k) d[k] = 0u;
+    if (len && (hexb(c0) || c0 == ':'))
+#pragma unroll
+        for (int k = 3; k < 7; ++k) d[k] = p[k];
+}
+
 // One block of k_kdict_flags (strings [i0 - tid, +BLOCK), i0 = this thread's string; the block
 // start a multiple of 64: every wave writes whole predicate words).
 KD_INLINE void kdict_block(const uint8_t* bytes, const uint32_t* offs, uint32_t s0, uint32_t n, uint32_t* kbits,
@@ -337,10 +353,8 @@ KD_INLINE void kdict_block(const uint8_t* bytes, const uint32_t* offs, uint32_t 
     const uint32_t ic = i < n ? i : n;                   // offs[n] exists
     const uint32_t b = offs[ic];
     const uint32_t len = (i < n ? offs[ic + 1] : b) - b;
-    const uint32_t* p = reinterpret_cast<const uint32_t*>(bytes + (b & ~3u));   // arena has 64 B slack
     uint32_t d[7];
-#pragma unroll
-    for (int k = 0; k < 7; ++k) d[k] = p[k];
+    kdict_window(bytes, b, len, d);
     const uint32_t sh = (b & 3u) * 8u;
     uint32_t w[6];
 #pragma unroll
@@ -385,9 +399,7 @@ __global__ void __launch_bounds__(NT) k_kdict_flags(const uint8_t* bytes, const 
             for (int k = 0; k < 7; ++k)
                 d[s][k] = o == 0 ? D[k] : o == 1 ? D[k + 1] : o == 2 ? D[k + 2] : D[k + 3];
         } else {
-            const uint32_t* p = reinterpret_cast<const uint32_t*>(bytes + (b[s] & ~3u));   // arena has 64 B slack
-#pragma unroll
-            for (int k = 0; k < 7; ++k) d[s][k] = p[k];
+            kdict_window(bytes, b[s], len[s], d[s]);
         }
     }
     const int lane = threadIdx.x & 63;
@@ -632,6 +644,27 @@ __global__ void __launch_bounds__(BLOCK) k_pdict_parse(const uint8_t* bytes, con
         pdict_parse_block<PD_DUR | PD_PCT | PD_RATE>(bytes, offs, s0, n, tick, ppct, pdur, prate, rate_err, buf);
     }
 }
+// Both dictionaries' parses in one launch (independent work, one kernel boundary less per
+// epoch): blocks [0, 3 * nbp) parse property strings [p0, P), interpretation b / nbp (the
+// heavier blocks first), the rest classify key strings [k0, D) as k_kdict_flags does.
+__global__ void __launch_bounds__(BLOCK) k_dict_parse(const uint8_t* kd_bytes, const uint32_t* kd_offs, uint32_t k0,
+                                                      uint32_t D, uint32_t* kbits, uint32_t kb_words,
+                                                      uint32_t* special, const uint8_t* pd_bytes,
+                                                      const uint32_t* pd_offs, uint32_t p0, uint32_t P, uint32_t nbp,
+                                                      double tick, uint32_t* ppct, uint2* pdur, uint2* prate,
+                                                      uint32_t* rate_err) {
+    __shared__ uint4 buf[STAGE / 16];
+    const uint32_t b = blockIdx.x;
+    if (b >= 3 * nbp) {
+        kdict_block(kd_bytes, kd_offs, k0 + (b - 3 * nbp) * BLOCK, D, kbits, kb_words, special);
+        return;
+    }
+    const uint32_t y = b / nbp, s0 = p0 + (b - y * nbp) * BLOCK;
+    if (y == 0) pdict_parse_block<PD_PCT>(pd_bytes, pd_offs, s0, P, tick, ppct, pdur, prate, rate_err, buf);
+    else if (y == 1) pdict_parse_block<PD_DUR>(pd_bytes, pd_offs, s0, P, tick, ppct, pdur, prate, rate_err, buf);
+    else pdict_parse_block<PD_RATE>(pd_bytes, pd_offs, s0, P, tick, ppct, pdur, prate, rate_err, buf);
+}
+
 #if KDTN_PROFILING
 // (profiling) one interpretation alone: WHICH = PD_DUR / PD_PCT / PD_RATE
 template <int WHICH>
@@ -1524,7 +1557,10 @@ __device__ void lookback(RecShared& s, const RecWork& wk, uint32_t wg) {
                 }
                 if (!ready) {
                     if (++spins > (1u << 24)) {              // bounded spin: report, never hang
-                        if (lane == 0) atomicOr(&wk.sync[SYNC_ERR], 1u);
+                        if (lane == 0) {
+                            atomicOr(&wk.sync[SYNC_ERR], 1u);
+                            if (wk.herr) *wk.herr = 1u;
+                        }
                         break;
                     }
                     __builtin_amdgcn_s_sleep(2);
@@ -1921,6 +1957,7 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
     if (!kDefer && lead && wg == wk.nwg - 1 && tid < 3) {             // comparison build: k_place_scan
         const uint32_t total = s.base[tid] + s.wtot[tid];
         out.totals[tid] = total;
+        if (out.htotals) out.htotals[tid] = total;
         (tid == 0 ? out.del_off : tid == 1 ? out.upd_off : out.add_off)[T.n] = total;
     }
     if (lead && tid < nt) {
@@ -2188,6 +2225,7 @@ __global__ void __launch_bounds__(PLACE_SCAN_BLOCK) k_place_scan(const uint32_t*
     }
     if (tid < 3) {
         out.totals[tid] = carry[tid];
+        if (out.htotals) out.htotals[tid] = carry[tid];
         (tid == 0 ? out.del_off : tid == 1 ? out.upd_off : out.add_off)[T] = carry[tid];
     }
 }

@@ -14,6 +14,8 @@
 #     istats     rocprofv3 --kernel-trace --stats of the config-2 ingest (tools/ingest_run.py)
 #     iab        ingest A/B of profiling variants $IAB_VARIANTS (tools/ingest_ablate.py, default 0,16)
 #     stages     output-stage kernel times (tools/stage_run.py)
+#     restrace   rocprofv3 kernel + memory-copy trace of the pipelined resident loop (exit check)
+#     shardstats rocprofv3 kernel stats of one rank of N = $SHARD_N (default 8)
 #   default: tests,smoke,bench,stats,pmc
 # Every GPU step has its own time limit and the script stops at the first failure.
 set -euo pipefail
@@ -84,6 +86,18 @@ for C in 2 3 4; do
     echo "$PM done"
   fi
 done
+if has restrace; then
+  # traced pipelined resident loop (the round-4 exit-time SIGSEGV): library map written at exit
+  timeout -k 10 400 rocprofv3 ${RT_FLAGS:---kernel-trace --memory-copy-trace --stats} --output-format csv -d $OUT/restrace -o run \
+      -- python3 $R/tools/resident_run.py ${RT_ARGS:---epochs 4 --pipeline} --maps $OUT/restrace_maps.txt \
+      > $OUT/restrace.jsonl 2> $OUT/restrace.log
+  tail -2 $OUT/restrace.jsonl
+fi
+if has shardstats; then
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/shardstats -o run \
+      -- python3 $R/tools/shard_epoch.py --nshards ${SHARD_N:-8} > $OUT/shardstats.json 2> $OUT/shardstats.err
+  cat $OUT/shardstats.json
+fi
 if has istats; then
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/istats -o run \
       -- python3 $R/tools/ingest_run.py --pods 1000000 --doc /tmp/kdtn_doc_1000000.json > $OUT/istats_ingest.json 2> $OUT/istats.err

@@ -28,7 +28,12 @@ ap.add_argument("--pods", type=int, default=1_000_000)
 ap.add_argument("--epochs", type=int, default=6)
 ap.add_argument("--topology-set", type=float, default=0.0, help="fraction of Topologies deleted/created per epoch")
 ap.add_argument("--pipeline", action="store_true", help="epoch k's download overlapping epoch k+1's upload")
+ap.add_argument("--maps", default="", help="write /proc/self/maps here at exit (symbolising a crash's PCs)")
 a = ap.parse_args()
+if a.maps:
+    import atexit
+    import shutil
+    atexit.register(lambda: shutil.copyfile("/proc/self/maps", a.maps))
 src = (synth.TopologySetChurn(frac=a.topology_set, total_pods=a.pods) if a.topology_set
        else synth.ChurnSequence(total_pods=a.pods))
 prev = src.epoch_input(copy=True)

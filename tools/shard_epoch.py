@@ -18,9 +18,13 @@ import torch  # noqa: F401  (one HIP runtime)
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "kube-dtn_amd"))
 import numpy as np  # noqa: E402
 
+if "--prof" in sys.argv:                 # A/B variants of the profiling build (KDTN_* environment)
+    from kdtn import engine as _e  # noqa: E402
+    _e.use_profiling_library()
 from kdtn import Engine, abi, synth, topology_shard  # noqa: E402
 
 ap = argparse.ArgumentParser()
+ap.add_argument("--prof", action="store_true", help="use prof/libkdtn_prof.so (variants from the environment)")
 ap.add_argument("--pods", type=int, default=1_000_000)
 ap.add_argument("--nshards", type=int, default=8)
 ap.add_argument("--rank", type=int, default=0)
@@ -49,7 +53,8 @@ for k in range(a.nshards):
 
 res = {"config": 2, "pods_total": a.pods, "nshards": a.nshards, "rank": a.rank, "links_rank": int(sh.desired.n),
        "topos_rank": int(sh.topos.n), "pod_slice": int(slice_), "kdict": int(sh.kdict.n), "pdict": int(sh.pdict.n),
-       "gen_s": round(gen_s, 1)}
+       "gen_s": round(gen_s, 1), "lib": "prof" if a.prof else "product",
+       "env": {k: v for k, v in os.environ.items() if k.startswith("KDTN_")}}
 with Engine(device=0) as eng:
     eng.set_ranks(a.nshards, a.rank)
     eng.upload(sh)
