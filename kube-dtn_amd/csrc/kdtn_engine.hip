@@ -66,6 +66,9 @@ struct kdtn_ctx {
     hipStream_t stream = nullptr;
     hipStream_t comm_stream = nullptr;          // RCCL pod-status exchange (nranks > 1)
     hipStream_t copy_stream = nullptr;          // delta uploads: host-to-device copies beside the kernels
+    hipStream_t side_stream = nullptr;          // the pod lookup build beside the dictionary parses
+    hipStream_t side_hi = nullptr;              // (profiling A/B: the same at the highest priority)
+    hipEvent_t ev_front = nullptr, ev_side = nullptr;
     hipEvent_t ev_cp[4] = {};
     hipEvent_t ev_col[LINK_COLS32 + 1] = {};   // a delta's staged column copies (+ uid), each placed on arrival
     hipStream_t d2h_stream = nullptr;           // kdtn_epoch_download_async: the outputs' copies
@@ -906,6 +909,15 @@ int kdtn_init(kdtn_ctx** out, const kdtn_config* cfg) {
     for (hipEvent_t& e : c->ev_cp) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
     for (hipEvent_t& e : c->ev_col) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
     if (hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess) c->copy_stream = nullptr;
+    if (hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking) != hipSuccess) c->side_stream = nullptr;
+    {
+        int lo = 0, hi = 0;
+        if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
+            hipStreamCreateWithPriority(&c->side_hi, hipStreamNonBlocking, hi) != hipSuccess)
+            c->side_hi = nullptr;
+    }
+    if (hipEventCreateWithFlags(&c->ev_front, hipEventDisableTiming) != hipSuccess) c->ev_front = nullptr;
+    if (hipEventCreateWithFlags(&c->ev_side, hipEventDisableTiming) != hipSuccess) c->ev_side = nullptr;
     if (hipStreamCreateWithFlags(&c->d2h_stream, hipStreamNonBlocking) != hipSuccess) c->d2h_stream = nullptr;
     (void)hipEventCreateWithFlags(&c->ev_dl_ready, hipEventDisableTiming);
     (void)hipEventCreateWithFlags(&c->ev_dl_done, hipEventDisableTiming);
@@ -971,6 +983,13 @@ void kdtn_destroy(kdtn_ctx* c) {
         (void)hipStreamSynchronize(c->copy_stream);
         (void)hipStreamDestroy(c->copy_stream);
     }
+    for (hipStream_t st : {c->side_stream, c->side_hi})
+        if (st) {
+            (void)hipStreamSynchronize(st);
+            (void)hipStreamDestroy(st);
+        }
+    if (c->ev_front) (void)hipEventDestroy(c->ev_front);
+    if (c->ev_side) (void)hipEventDestroy(c->ev_side);
     if (c->d2h_stream) {
         (void)hipStreamSynchronize(c->d2h_stream);
         (void)hipStreamDestroy(c->d2h_stream);
@@ -1105,6 +1124,37 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
     uint32_t* special = dp<uint32_t>(c->kd_special);
     const uint32_t n16 = (uint32_t)(sync_bytes(c->nwg) / 16);
     const uint32_t nbz = std::min<uint32_t>(nblocks(n16), 256);
+    // the pod lookup tables (scatter, then verify fused with the full-prefix scan) on a side
+    // stream beside the dictionary parses, which they do not need (the PHYSICAL bit of a pod's
+    // name comes from its bytes): the comm stream right after the RCCL all-gather, else
+    // side_stream after the first launch; k_reconcile waits for them
+#if KDTN_PROFILING
+    int side_mode = KDTN_LOOKUP_SIDE_DEFAULT;
+    if (const char* ev = std::getenv("KDTN_LOOKUP_SIDE")) side_mode = std::atoi(ev);
+#else
+    constexpr int side_mode = KDTN_LOOKUP_SIDE_DEFAULT;
+#endif
+    hipStream_t ls = exchange ? c->comm_stream : (side_mode == 2 && c->side_hi ? c->side_hi : c->side_stream);
+    const bool side = side_mode && !fused && resolve && pod_rows && !pods_cur && c->T && ls && c->ev_front && c->ev_side;
+    auto lookup_build = [&](hipStream_t q) -> int {
+        if (++c->pod_stamp >= 0x7FFFFFFFu) {                             // stamp wrap: clear once
+            HIP_TRY(hipMemsetAsync(c->pod_direct.p, 0, c->pod_direct.cap, q));
+            HIP_TRY(hipMemsetAsync(c->pod_ovf.p, 0, c->pod_ovf.cap, q));
+            c->pod_stamp = 1;
+        }
+        k_pod_direct_scatter<<<nblocks(pod_rows), BLOCK, 0, q>>>(
+            dp<uint4>(c->pods), pod_rows, dp<uint8_t>(c->kd_bytes), dp<uint32_t>(c->kd_offs), dp<uint4>(c->pod_direct),
+            c->pod_stamp, c->D, c->pods_rank_major ? (uint32_t)c->nranks : 1u, c->pod_total);
+        return KDTN_OK;
+    };
+    auto verify_prefix = [&](hipStream_t q) {
+        const uint32_t nbv = nblocks(pod_rows);
+        const uint32_t nbp = (uint32_t)std::min<uint64_t>(4 * FP_GRID, (c->T + 4 * BLOCK - 1) / (4 * BLOCK));
+        k_pod_verify_prefix<<<nbv + std::max<uint32_t>(nbp, 1), BLOCK, 0, q>>>(
+            dp<uint4>(c->pods), pod_rows, dp<uint4>(c->pod_direct), c->pod_stamp,
+            dp<unsigned long long>(c->pod_ovf), c->ovf_mask, c->D, T, sync + SYNC_FIRST_PARTIAL_INV, nbv,
+            c->pods_rank_major ? (uint32_t)c->nranks : 1u, c->pod_total);
+    };
 #if KDTN_PROFILING
     if (fused) {
         if (++c->pod_stamp >= 0x7FFFFFFFu) {                             // stamp wrap: clear once
@@ -1155,6 +1205,15 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
                     return KDTN_EIO;
                 }
                 HIP_TRY(hipEventRecord(c->ev_ag, c->comm_stream));
+            }
+            if (side) {
+                if (!exchange) {
+                    HIP_TRY(hipEventRecord(c->ev_front, s));
+                    HIP_TRY(hipStreamWaitEvent(ls, c->ev_front, 0));
+                }
+                TRY(lookup_build(ls));
+                verify_prefix(ls);
+                HIP_TRY(hipEventRecord(c->ev_side, ls));
             }
             timer_mark(c, "pods_fill", 2);
         }
@@ -1211,21 +1270,22 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         timer_mark(c, "pdict_parse", 2);
         }
         if (resolve) {
-            if (exchange) HIP_TRY(hipStreamWaitEvent(s, c->ev_ag, 0));   // exchange not hidden by the parses
-            timer_mark(c, "pods_allgather", 2);
-            if (!pods_cur && ++c->pod_stamp >= 0x7FFFFFFFu) {             // stamp wrap: clear once
-                HIP_TRY(hipMemsetAsync(c->pod_direct.p, 0, c->pod_direct.cap, s));
-                HIP_TRY(hipMemsetAsync(c->pod_ovf.p, 0, c->pod_ovf.cap, s));
-                c->pod_stamp = 1;
+            if (side) {
+                if (c->V) TRY(build_vni_table(c));
+                HIP_TRY(hipStreamWaitEvent(s, c->ev_side, 0));             // lookup tables not hidden by the parses
+                timer_mark(c, "lookup_wait", 2);
+            } else {
+                if (exchange) HIP_TRY(hipStreamWaitEvent(s, c->ev_ag, 0));   // exchange not hidden by the parses
+                timer_mark(c, "pods_allgather", 2);
+                if (pod_rows && !pods_cur) TRY(lookup_build(s));
+                else if (!pods_cur && ++c->pod_stamp >= 0x7FFFFFFFu) {     // (no rows: the stamp still moves)
+                    HIP_TRY(hipMemsetAsync(c->pod_direct.p, 0, c->pod_direct.cap, s));
+                    HIP_TRY(hipMemsetAsync(c->pod_ovf.p, 0, c->pod_ovf.cap, s));
+                    c->pod_stamp = 1;
+                }
+                if (c->V) TRY(build_vni_table(c));
+                timer_mark(c, "hash_build", 2);
             }
-            if (pod_rows && !pods_cur) {
-                k_pod_direct_scatter<<<nblocks(pod_rows), BLOCK, 0, s>>>(
-                    dp<uint4>(c->pods), pod_rows, dp<uint32_t>(c->kd_bits) + (size_t)KB_PHYSICAL * c->kb_words,
-                    dp<uint4>(c->pod_direct), c->pod_stamp, c->D, c->pods_rank_major ? (uint32_t)c->nranks : 1u,
-                    c->pod_total);
-            }
-            if (c->V) TRY(build_vni_table(c));
-            timer_mark(c, "hash_build", 2);
         }
     }
     c->kd_valid = c->D;
@@ -1289,14 +1349,9 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
 #if KDTN_PROFILING
         if (const char* ev = std::getenv("KDTN_SPLIT")) if (std::atoi(ev) > 0) w.split = (uint32_t)std::atoi(ev);
 #endif
-        if (fused) {                                    // verify + prefix ran in k_pdict_verify
+        if (fused || side) {                            // verify + prefix ran in k_pdict_verify / on the side stream
         } else if (resolve && pod_rows && !pods_cur) {   // the pod-table verify with the full-prefix scan
-            const uint32_t nbv = nblocks(pod_rows);
-            const uint32_t nbp = (uint32_t)std::min<uint64_t>(4 * FP_GRID, (c->T + 4 * BLOCK - 1) / (4 * BLOCK));
-            k_pod_verify_prefix<<<nbv + std::max<uint32_t>(nbp, 1), BLOCK, 0, s>>>(
-                dp<uint4>(c->pods), pod_rows, dp<uint4>(c->pod_direct), c->pod_stamp,
-                dp<unsigned long long>(c->pod_ovf), c->ovf_mask, c->D, T, sync + SYNC_FIRST_PARTIAL_INV, nbv,
-                c->pods_rank_major ? (uint32_t)c->nranks : 1u, c->pod_total);
+            verify_prefix(s);
             timer_mark(c, "verify_prefix", 2);
         } else {
             k_full_prefix<<<(unsigned)std::min<uint64_t>(FP_GRID, (c->T + 4 * FP_BLOCK - 1) / (4 * FP_BLOCK)), FP_BLOCK, 0, s>>>(

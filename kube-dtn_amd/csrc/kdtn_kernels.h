@@ -115,6 +115,11 @@ struct DevLinks {
 #ifndef KDTN_PROFILING
 #define KDTN_PROFILING 0
 #endif
+// epoch front: the pod lookup build (scatter, verify + full-prefix scan) on a side stream (the
+// comm stream after the all-gather when RCCL exchanges the rows) beside the dictionary parses
+#ifndef KDTN_LOOKUP_SIDE_DEFAULT
+#define KDTN_LOOKUP_SIDE_DEFAULT 0
+#endif
 // epoch front: k_kdict_flags and k_pdict_parse as one launch (k_dict_parse)
 #ifndef KDTN_DICT_FUSE_DEFAULT
 #define KDTN_DICT_FUSE_DEFAULT true     // N = 8 rank epoch 0.2163 -> 0.1990 ms (profiles/r05b_fuse_ab.jsonl)
@@ -257,8 +262,9 @@ __global__ void k_dict_parse(const uint8_t* kd_bytes, const uint32_t* kd_offs, u
                              uint2* prate, uint32_t* rate_err);
 __global__ void k_epoch_begin(uint4* sync, uint32_t n16, uint32_t nbz, DevTopos T, uint32_t slice, uint32_t rank_base,
                               uint4* pods);
-__global__ void k_pod_direct_scatter(const uint4* pods, uint32_t total, const uint32_t* phys_bits,
-                                     uint4* slots, uint32_t stamp, uint32_t nd, uint32_t nr, uint32_t gathered);
+__global__ void k_pod_direct_scatter(const uint4* pods, uint32_t total, const uint8_t* kd_bytes,
+                                     const uint32_t* kd_offs, uint4* slots, uint32_t stamp, uint32_t nd, uint32_t nr,
+                                     uint32_t gathered);
 __global__ void k_epoch_front(uint4* sync, uint32_t n16, uint32_t nbz, uint32_t nbs, DevTopos T, uint32_t slice,
                               uint4* pods, uint4* slots, uint32_t stamp, const uint8_t* kd_bytes,
                               const uint32_t* kd_offs, uint32_t k0, uint32_t D, uint32_t* kbits, uint32_t kb_words,

@@ -774,16 +774,28 @@ KD_INLINE uint32_t pod_order(uint32_t t, uint32_t total, uint32_t nr) {
     return (t % nr) * slice + t / nr;
 }
 
+// "physical/" prefix of key string `id` from its bytes (the KB_PHYSICAL predicate, without
+// waiting for k_kdict_flags: the lookup build runs beside the dictionary parses)
+KD_INLINE uint32_t name_physical(const uint8_t* kd_bytes, const uint32_t* kd_offs, uint32_t id) {
+    const uint32_t ob = kd_offs[id], len = kd_offs[id + 1] - ob;
+    if (len < 9) return 0u;
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(kd_bytes + (ob & ~3u));   // arena has 64 B slack
+    const uint32_t d0 = p[0], d1 = p[1], d2 = p[2], d3 = p[3], sh = ob & 3u;
+    const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh), w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+    const uint32_t w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
+    return (w0 == 0x73796870u && w1 == 0x6C616369u && (w2 & 0xFFu) == '/') ? 1u : 0u;   // "phys" "ical" '/'
+}
+
 __global__ void __launch_bounds__(BLOCK) k_pod_direct_scatter(const uint4* pods, uint32_t total,
-                                                              const uint32_t* phys_bits, uint4* slots,
-                                                              uint32_t stamp, uint32_t nd, uint32_t nr,
+                                                              const uint8_t* kd_bytes, const uint32_t* kd_offs,
+                                                              uint4* slots, uint32_t stamp, uint32_t nd, uint32_t nr,
                                                               uint32_t gathered) {
     const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
     if (t >= total) return;
     const uint32_t g = pod_order(t, gathered, nr);
     const uint4 e = pods[g];
     if (e.x == 0xFFFFFFFFu || e.y >= nd) return;           // padding row / name outside this dictionary
-    const uint32_t phys = (phys_bits[e.y >> 5] >> (e.y & 31)) & 1u;
+    const uint32_t phys = name_physical(kd_bytes, kd_offs, e.y);
     slots[e.y] = make_uint4(e.x, (g << 2) | (phys << 1) | (e.w >> 31),
                             e.z | ((e.w & 0x7FFFFFFFu) == 0 ? 0x80000000u : 0u), stamp << 1);
 }

@@ -23,6 +23,7 @@ ap.add_argument("--masks", default="ALL,DIFF|RESOLVE,DIFF|QDISC,DIFF")
 ap.add_argument("--cache", default="")
 ap.add_argument("--variants", default="", help="comma list of KDTN_VARIANT values, interleaved")
 ap.add_argument("--env", default="", help="NAME=v1,v2,...: interleaved A/B of an env knob, all stages timed")
+ap.add_argument("--wall", action="store_true", help="--env: also the wall time of run + sync at timing level 0")
 a = ap.parse_args()
 if a.variants or a.env:                 # A/B variants live in the profiling build
     from kdtn import engine as _kdtn_engine
@@ -57,6 +58,17 @@ if a.env:
             if rep >= 2:
                 for k, t in eng.kernel_times().items():
                     acc[v].setdefault(k, []).append(t)
+    if a.wall:                            # epoch wall time, no timing events
+        import time
+        eng.set_timing(0)
+        for rep in range(a.reps + 2):
+            for v in acc:
+                os.environ[name] = v
+                t = time.perf_counter()
+                eng.run(abi.STAGE_ALL)
+                eng.sync()
+                if rep >= 2:
+                    acc[v].setdefault("epoch_L0", []).append((time.perf_counter() - t) * 1e3)
     os.environ.pop(name)
     for v, d in acc.items():
         res[f"{name}={v}"] = {k: round(sorted(x)[len(x) // 2], 4) for k, x in d.items()}
