@@ -2,6 +2,8 @@
 // HIP kernels of kdtn_kernels.hip. One kdtn_ctx per process/GPU; device buffers are
 // owned by the context and reused across epochs (high-water-mark growth).
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -74,6 +76,14 @@ struct kdtn_ctx {
     hipStream_t d2h_stream = nullptr;           // kdtn_epoch_download_async: the outputs' copies
     hipEvent_t ev_dl_ready = nullptr, ev_dl_done = nullptr;
     bool dl_pending = false;                    // an async download's copies may still be reading outputs
+    // Downloads on one SDMA engine (hsa_amd_memory_async_copy_on_engine): the copy engine alone
+    // reaches the host link's rate (56 GB/s D2H, profiles/r05d_sdma_probe.jsonl) and takes no
+    // CUs, where the runtime's device-to-host copies in this process run as blit kernels. Used
+    // when every destination is page-locked host memory, else the HIP copies.
+    bool sdma_tried = false, sdma_ok = false, dl_sdma = false;
+    hsa_agent_t sdma_gpu{}, sdma_cpu{};
+    uint32_t sdma_engine = 0;
+    hsa_signal_t dl_sig{};
     hipEvent_t ev_fill = nullptr, ev_ag = nullptr;
     // dictionaries; parsed tables persist across uploads for an append-only interner
     // (kdtn_epoch_in.kdict_keep / pdict_keep): *_valid strings have valid parsed tables, a run
@@ -243,7 +253,25 @@ void alloc_log(const char* what, size_t bytes) {
     (void)bytes;
 #endif
 }
+// SDMA downloads in flight (any context): a retired buffer may be one they read
+struct SdmaInflight {
+    std::mutex m;
+    std::vector<uint64_t> sig;
+};
+SdmaInflight& sdma_inflight() {
+    static SdmaInflight f;
+    return f;
+}
+void sdma_wait(hsa_signal_t sg) {
+    while (hsa_signal_wait_scacquire(sg, HSA_SIGNAL_CONDITION_EQ, 0, UINT64_MAX, HSA_WAIT_STATE_ACTIVE) != 0) {
+    }
+}
 void retired_flush() {
+    {
+        SdmaInflight& f = sdma_inflight();
+        std::lock_guard<std::mutex> lk(f.m);
+        for (uint64_t h : f.sig) sdma_wait(hsa_signal_t{h});
+    }
     Retired& r = retired();
     std::lock_guard<std::mutex> lk(r.m);
     alloc_log("flush", r.bytes);
@@ -928,6 +956,7 @@ int kdtn_init(kdtn_ctx** out, const kdtn_config* cfg) {
 void kdtn_destroy(kdtn_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
+    (void)kdtn_epoch_download_wait(c);
     (void)hipStreamSynchronize(c->stream);
     if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
     DevBuf* bufs[] = {&c->kd_bytes, &c->kd_offs, &c->kd_bits, &c->pd_bytes, &c->pd_offs,
@@ -996,6 +1025,10 @@ void kdtn_destroy(kdtn_ctx* c) {
     }
     if (c->ev_dl_ready) (void)hipEventDestroy(c->ev_dl_ready);
     if (c->ev_dl_done) (void)hipEventDestroy(c->ev_dl_done);
+    if (c->sdma_ok) {
+        (void)hsa_signal_destroy(c->dl_sig);
+        (void)hsa_shut_down();                      // (balances sdma_setup's hsa_init)
+    }
     if (c->h_misc) (void)hipHostFree(c->h_misc);
     if (c->h_tot) (void)hipHostFree(c->h_tot);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -1099,7 +1132,10 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
                       "host transport: kdtn_pods_import the gathered pod table before kdtn_epoch_run");
         return KDTN_EINVAL;
     }
-    if (c->dl_pending) HIP_TRY(hipStreamWaitEvent(s, c->ev_dl_done, 0));   // outputs still being copied out
+    if (c->dl_pending) {                                          // outputs still being copied out
+        if (c->dl_sdma) TRY(kdtn_epoch_download_wait(c));
+        else HIP_TRY(hipStreamWaitEvent(s, c->ev_dl_done, 0));
+    }
     // the previous epoch's kernels are done once its sync returned, so these host stores cannot
     // race a device write; an epoch without topologies leaves them zero
     for (int i = 0; i < 4; ++i) __atomic_store_n(c->h_tot + i, 0u, __ATOMIC_RELAXED);
@@ -1221,9 +1257,10 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         // pdict_keep), from a multiple of 64 so every wave writes whole predicate words
         uint32_t* special = dp<uint32_t>(c->kd_special);
 #if KDTN_PROFILING
-        const bool dict_fuse = std::getenv("KDTN_DICT_FUSE") && std::atoi(std::getenv("KDTN_DICT_FUSE"));
+        int dict_fuse = KDTN_DICT_FUSE_DEFAULT ? 1 : 0;
+        if (const char* ev = std::getenv("KDTN_DICT_FUSE")) dict_fuse = std::atoi(ev);
 #else
-        constexpr bool dict_fuse = KDTN_DICT_FUSE_DEFAULT;
+        constexpr int dict_fuse = KDTN_DICT_FUSE_DEFAULT ? 1 : 0;
 #endif
         const uint32_t k0f = c->kd_from & ~63u, p0f = c->pd_from & ~63u;
         if (dict_fuse && c->D > k0f && c->P > p0f) {              // both parses in one launch
@@ -1231,7 +1268,8 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
             k_dict_parse<<<3 * nbp + nbk, BLOCK, 0, s>>>(
                 dp<uint8_t>(c->kd_bytes), dp<uint32_t>(c->kd_offs), k0f, c->D, dp<uint32_t>(c->kd_bits), c->kb_words,
                 special, dp<uint8_t>(c->pd_bytes), dp<uint32_t>(c->pd_offs), p0f, c->P, nbp, c->cfg.tick_in_usec,
-                dp<uint32_t>(c->pd_pct), dp<uint2>(c->pd_dur), dp<uint2>(c->pd_rate), dp<uint32_t>(c->pd_rerr));
+                dp<uint32_t>(c->pd_pct), dp<uint2>(c->pd_dur), dp<uint2>(c->pd_rate), dp<uint32_t>(c->pd_rerr),
+                dict_fuse == 2 ? nbk : 0u);
             timer_mark(c, "dict_parse", 2);
         } else {
         {
@@ -1503,11 +1541,108 @@ static int download_enqueue(kdtn_ctx* c, kdtn_batches* o, hipStream_t hs) {
     return KDTN_OK;
 }
 
+// HSA agents and the SDMA engine for device-to-host copies, once per context
+static bool sdma_setup(kdtn_ctx* c) {
+    if (c->sdma_tried) return c->sdma_ok;
+    c->sdma_tried = true;
+    if (hsa_init() != HSA_STATUS_SUCCESS) return false;
+    hsa_amd_pointer_info_t dv{}, hv{};
+    dv.size = hv.size = sizeof(hsa_amd_pointer_info_t);
+    uint32_t mask = 0, pref = 0;
+    bool ok = c->sync.p && hsa_amd_pointer_info(c->sync.p, &dv, nullptr, nullptr, nullptr) == HSA_STATUS_SUCCESS &&
+              dv.type == HSA_EXT_POINTER_TYPE_HSA &&
+              hsa_amd_pointer_info(c->h_misc, &hv, nullptr, nullptr, nullptr) == HSA_STATUS_SUCCESS &&
+              hv.type == HSA_EXT_POINTER_TYPE_HSA;
+    if (ok) {
+        hsa_device_type_t tg = HSA_DEVICE_TYPE_CPU, th = HSA_DEVICE_TYPE_GPU;
+        ok = hsa_agent_get_info(dv.agentOwner, HSA_AGENT_INFO_DEVICE, &tg) == HSA_STATUS_SUCCESS &&
+             hsa_agent_get_info(hv.agentOwner, HSA_AGENT_INFO_DEVICE, &th) == HSA_STATUS_SUCCESS &&
+             tg == HSA_DEVICE_TYPE_GPU && th == HSA_DEVICE_TYPE_CPU &&
+             hsa_amd_memory_copy_engine_status(hv.agentOwner, dv.agentOwner, &mask) == HSA_STATUS_SUCCESS && mask;
+    }
+    if (ok) {
+        (void)hsa_amd_memory_get_preferred_copy_engine(hv.agentOwner, dv.agentOwner, &pref);
+        const uint32_t pick = (pref & mask) ? (pref & mask) : mask;
+        c->sdma_engine = pick & (~pick + 1u);                       // lowest available engine bit
+        c->sdma_gpu = dv.agentOwner;
+        c->sdma_cpu = hv.agentOwner;
+        ok = hsa_signal_create(0, 0, nullptr, &c->dl_sig) == HSA_STATUS_SUCCESS;
+    }
+    if (!ok) (void)hsa_shut_down();
+    c->sdma_ok = ok;
+    return ok;
+}
+
+// The download's copies on the context's SDMA engine, completion on dl_sig. false (nothing
+// issued) when a destination is not page-locked host memory the engine can write, or the
+// setup failed: the caller takes the HIP copies. The epoch's kernels have completed (after
+// kdtn_epoch_sync, whose completion event carries the system-scope release).
+static bool sdma_download(kdtn_ctx* c, kdtn_batches* o) {
+    if (!sdma_setup(c)) return false;
+    const uint32_t nd = c->h_misc[1], nu = c->h_misc[2], na = c->h_misc[3];
+    o->n_del = nd;
+    o->n_upd = nu;
+    o->n_add = na;
+    if (nd > o->del_cap || nu > o->upd_cap || na > o->add_cap) return false;   // (the HIP path reports it)
+    struct Piece { void* dst; const void* src; size_t bytes; };
+    Piece pc[12];
+    int n = 0;
+    auto add = [&](void* dst, DevBuf& b, size_t bytes) {
+        if (dst && bytes) pc[n++] = Piece{dst, b.p, bytes};
+    };
+    const bool res = c->last_stages & KDTN_STAGE_RESOLVE, q = c->last_stages & KDTN_STAGE_QDISC;
+    add(o->action, c->action, c->T);
+    add(o->del_off, c->del_off, (size_t)(c->T + 1) * 4);
+    add(o->add_off, c->add_off, (size_t)(c->T + 1) * 4);
+    add(o->upd_off, c->upd_off, (size_t)(c->T + 1) * 4);
+    add(o->del_idx, c->del_idx, (size_t)nd * 4);
+    add(o->add_idx, c->add_idx, (size_t)na * 4);
+    add(o->upd_idx, c->upd_idx, (size_t)nu * 4);
+    if (res) {
+        add(o->del_res, c->del_res, (size_t)nd * 16);
+        add(o->add_res, c->add_res, (size_t)na * 16);
+        add(o->upd_res, c->upd_res, (size_t)nu * 16);
+    }
+    if (q) {
+        add(o->add_qdisc, c->add_qdisc, (size_t)na * 72);
+        add(o->upd_qdisc, c->upd_qdisc, (size_t)nu * 72);
+    }
+    for (int i = 0; i < n; ++i) {                   // page-locked, and the whole range inside it
+        hsa_amd_pointer_info_t pi{};
+        pi.size = sizeof pi;
+        if (hsa_amd_pointer_info(pc[i].dst, &pi, nullptr, nullptr, nullptr) != HSA_STATUS_SUCCESS) return false;
+        if (pi.type != HSA_EXT_POINTER_TYPE_HSA && pi.type != HSA_EXT_POINTER_TYPE_LOCKED) return false;
+        const uint8_t* b = static_cast<const uint8_t*>(pi.hostBaseAddress);
+        const uint8_t* d = static_cast<const uint8_t*>(pc[i].dst);
+        if (!b || d < b || d + pc[i].bytes > b + pi.sizeInBytes) return false;
+    }
+    if (!n) return true;
+    hsa_signal_store_screlease(c->dl_sig, n);
+    {
+        SdmaInflight& f = sdma_inflight();
+        std::lock_guard<std::mutex> lk(f.m);
+        f.sig.push_back(c->dl_sig.handle);
+    }
+    c->dl_sdma = c->dl_pending = true;
+    for (int i = 0; i < n; ++i) {
+        if (hsa_amd_memory_async_copy_on_engine(pc[i].dst, c->sdma_cpu, pc[i].src, c->sdma_gpu, pc[i].bytes, 0, nullptr,
+                                                c->dl_sig, (hsa_amd_sdma_engine_id_t)c->sdma_engine,
+                                                true) != HSA_STATUS_SUCCESS) {
+            hsa_signal_subtract_screlease(c->dl_sig, n - i);       // the pieces never issued
+            (void)kdtn_epoch_download_wait(c);
+            c->sdma_ok = false;                                    // HIP copies from now on
+            return false;
+        }
+    }
+    return true;
+}
+
 int kdtn_epoch_download(kdtn_ctx* c, kdtn_batches* o) {
     if (!c || !o || !c->ran) return KDTN_EINVAL;
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipStreamSynchronize(c->stream));
     TRY(kdtn_epoch_download_wait(c));
+    if (sdma_download(c, o)) return kdtn_epoch_download_wait(c);
     TRY(download_enqueue(c, o, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return KDTN_OK;
@@ -1522,6 +1657,8 @@ int kdtn_epoch_download_async(kdtn_ctx* c, kdtn_batches* o) {
     if (!c || !o || !c->ran) return KDTN_EINVAL;
     HIP_TRY(hipSetDevice(c->device));
     TRY(kdtn_epoch_download_wait(c));
+    HIP_TRY(hipStreamSynchronize(c->stream));       // (idle after kdtn_epoch_sync: returns at once)
+    if (sdma_download(c, o)) return KDTN_OK;
     hipStream_t hs = c->d2h_stream ? c->d2h_stream : c->stream;
     HIP_TRY(hipEventRecord(c->ev_dl_ready, c->stream));
     HIP_TRY(hipStreamWaitEvent(hs, c->ev_dl_ready, 0));
@@ -1534,6 +1671,14 @@ int kdtn_epoch_download_async(kdtn_ctx* c, kdtn_batches* o) {
 int kdtn_epoch_download_wait(kdtn_ctx* c) {
     if (!c) return KDTN_EINVAL;
     if (!c->dl_pending) return KDTN_OK;
+    if (c->dl_sdma) {
+        sdma_wait(c->dl_sig);
+        SdmaInflight& f = sdma_inflight();
+        std::lock_guard<std::mutex> lk(f.m);
+        f.sig.erase(std::remove(f.sig.begin(), f.sig.end(), c->dl_sig.handle), f.sig.end());
+        c->dl_sdma = c->dl_pending = false;
+        return KDTN_OK;
+    }
     HIP_TRY(hipEventSynchronize(c->ev_dl_done));
     c->dl_pending = false;
     return KDTN_OK;
@@ -2743,7 +2888,6 @@ int kdtn_epoch_late_pods(kdtn_ctx* c, const kdtn_pod_row* rows, uint32_t n) {
         return KDTN_EINVAL;
     }
     hipStream_t s = c->stream;
-    if (c->dl_pending) HIP_TRY(hipStreamWaitEvent(s, c->ev_dl_done, 0));
     // the gathered rows stay (a host-transport import, a sharded ingest's fill)
     TRY(ensure_keep(c->pods, (size_t)all * 16, (size_t)c->pod_total * 16, s));
     c->ovf_mask = next_pow2(all * 2) - 1;

@@ -259,7 +259,7 @@ __global__ void k_pods_fill(DevTopos T, uint32_t slice, uint32_t rank_base, uint
 __global__ void k_dict_parse(const uint8_t* kd_bytes, const uint32_t* kd_offs, uint32_t k0, uint32_t D, uint32_t* kbits,
                              uint32_t kb_words, uint32_t* special, const uint8_t* pd_bytes, const uint32_t* pd_offs,
                              uint32_t p0, uint32_t P, uint32_t nbp, double tick, uint32_t* ppct, uint2* pdur,
-                             uint2* prate, uint32_t* rate_err);
+                             uint2* prate, uint32_t* rate_err, uint32_t nbk_first);
 __global__ void k_epoch_begin(uint4* sync, uint32_t n16, uint32_t nbz, DevTopos T, uint32_t slice, uint32_t rank_base,
                               uint4* pods);
 __global__ void k_pod_direct_scatter(const uint4* pods, uint32_t total, const uint8_t* kd_bytes,

@@ -652,10 +652,16 @@ __global__ void __launch_bounds__(BLOCK) k_dict_parse(const uint8_t* kd_bytes, c
                                                       uint32_t* special, const uint8_t* pd_bytes,
                                                       const uint32_t* pd_offs, uint32_t p0, uint32_t P, uint32_t nbp,
                                                       double tick, uint32_t* ppct, uint2* pdur, uint2* prate,
-                                                      uint32_t* rate_err) {
+                                                      uint32_t* rate_err, uint32_t nbk) {
     __shared__ uint4 buf[STAGE / 16];
-    const uint32_t b = blockIdx.x;
-    if (b >= 3 * nbp) {
+    uint32_t b = blockIdx.x;
+    if (nbk) {                              // (key-string blocks first)
+        if (b < nbk) {
+            kdict_block(kd_bytes, kd_offs, k0 + b * BLOCK, D, kbits, kb_words, special);
+            return;
+        }
+        b -= nbk;
+    } else if (b >= 3 * nbp) {
         kdict_block(kd_bytes, kd_offs, k0 + (b - 3 * nbp) * BLOCK, D, kbits, kb_words, special);
         return;
     }

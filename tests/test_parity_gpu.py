@@ -537,3 +537,23 @@ def test_timer_totals_sum_the_synced_epochs(engine):
         assert engine.timer_totals() == {}                # reset cleared them
     finally:
         engine.set_timing(2)                              # the context's default
+
+
+def test_download_into_page_locked_buffers(engine):
+    """kdtn_epoch_download / _async into page-locked buffers (the SDMA engine copies them)
+    equal the copies into pageable memory, every field; a second epoch reuses the buffers."""
+    from kdtn.tables import BatchesOut
+    for seed in (3, 4):
+        topos, inp = random_epoch_input(seed, T=150)
+        engine.upload(inp)
+        engine.run()
+        engine.sync()
+        plain = engine.download()
+        cap = max(inp.realised.n, inp.desired.n, 1)
+        pinned = BatchesOut.alloc(inp.topos.n, cap, cap, cap, pinned=True)
+        assert_same(engine.download(into=pinned), plain, f"seed {seed}: sync download")
+        again = BatchesOut.alloc(inp.topos.n, cap, cap, cap, pinned=True)
+        view = engine.download_async(again)
+        engine.download_wait()
+        assert_same(view, plain, f"seed {seed}: async download")
+        assert_same(plain, O.reconcile(inp, tick=TICK), f"seed {seed}")
