@@ -1172,15 +1172,16 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
 #endif
     hipStream_t ls = exchange ? c->comm_stream : (side_mode == 2 && c->side_hi ? c->side_hi : c->side_stream);
     const bool side = side_mode && !fused && resolve && pod_rows && !pods_cur && c->T && ls && c->ev_front && c->ev_side;
-    auto lookup_build = [&](hipStream_t q) -> int {
+    auto lookup_build = [&](hipStream_t q, bool parsed) -> int {
         if (++c->pod_stamp >= 0x7FFFFFFFu) {                             // stamp wrap: clear once
             HIP_TRY(hipMemsetAsync(c->pod_direct.p, 0, c->pod_direct.cap, q));
             HIP_TRY(hipMemsetAsync(c->pod_ovf.p, 0, c->pod_ovf.cap, q));
             c->pod_stamp = 1;
         }
         k_pod_direct_scatter<<<nblocks(pod_rows), BLOCK, 0, q>>>(
-            dp<uint4>(c->pods), pod_rows, dp<uint8_t>(c->kd_bytes), dp<uint32_t>(c->kd_offs), dp<uint4>(c->pod_direct),
-            c->pod_stamp, c->D, c->pods_rank_major ? (uint32_t)c->nranks : 1u, c->pod_total);
+            dp<uint4>(c->pods), pod_rows, parsed ? dp<uint32_t>(c->kd_bits) + (size_t)KB_PHYSICAL * c->kb_words : nullptr,
+            dp<uint8_t>(c->kd_bytes), dp<uint32_t>(c->kd_offs), dp<uint4>(c->pod_direct), c->pod_stamp, c->D,
+            c->pods_rank_major ? (uint32_t)c->nranks : 1u, c->pod_total);
         return KDTN_OK;
     };
     auto verify_prefix = [&](hipStream_t q) {
@@ -1222,36 +1223,43 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
     } else
 #endif
     {
-        {
-            // one launch zeroes the sync header (SYNC_*) and look-back area and fills this rank's
-            // pod-status rows: across ranks they are all-gathered over RCCL on the comm stream
-            // while this stream parses the dictionaries (the exchange needs neither)
-            const uint32_t fill = (resolve && !host_xchg && !pods_cur) ? c->slice : 0u;
-            const uint32_t rank_base = c->slice * (uint32_t)c->rank;
-            k_epoch_begin<<<nbz + nblocks(fill), BLOCK, 0, s>>>(reinterpret_cast<uint4*>(sync), n16, nbz, T, fill,
+        // k_epoch_begin zeroes the sync header (SYNC_*) and look-back area and fills this rank's
+        // pod-status rows. With RCCL it runs on the comm stream, followed there by the
+        // all-gather, beside this stream's dictionary parses; otherwise it follows the parses on
+        // this stream, so the epoch's first launch is a long one and the host's later launches
+        // are queued while it runs (a 2.5-µs first kernel left the GPU idle ≈ 5 µs for the next
+        // launch, profiles/r05c_shardstats_trace.csv)
+        const uint32_t fill = (resolve && !host_xchg && !pods_cur) ? c->slice : 0u;
+        const uint32_t rank_base = c->slice * (uint32_t)c->rank;
+        auto begin = [&](hipStream_t q) {
+            k_epoch_begin<<<nbz + nblocks(fill), BLOCK, 0, q>>>(reinterpret_cast<uint4*>(sync), n16, nbz, T, fill,
                                                                 rank_base, dp<uint4>(c->pods));
-            if (exchange) {
-                HIP_TRY(hipEventRecord(c->ev_fill, s));
-                HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_fill, 0));
-                uint4* pods = dp<uint4>(c->pods);
-                ncclResult_t r = ncclAllGather(pods + rank_base, pods, (size_t)c->slice * 4, ncclUint32, c->comm,
-                                               c->comm_stream);
-                if (r != ncclSuccess) {
-                    std::snprintf(g_last_error, sizeof(g_last_error), "ncclAllGather: %s", ncclGetErrorString(r));
-                    return KDTN_EIO;
-                }
-                HIP_TRY(hipEventRecord(c->ev_ag, c->comm_stream));
+        };
+        const bool begin_first = side && !exchange;                 // (A/B: the lookup build waits for it)
+        if (exchange) {
+            HIP_TRY(hipEventRecord(c->ev_fill, s));                   // after the previous epoch's kernels
+            HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_fill, 0));
+            begin(c->comm_stream);
+            uint4* pods = dp<uint4>(c->pods);
+            ncclResult_t r = ncclAllGather(pods + rank_base, pods, (size_t)c->slice * 4, ncclUint32, c->comm,
+                                           c->comm_stream);
+            if (r != ncclSuccess) {
+                std::snprintf(g_last_error, sizeof(g_last_error), "ncclAllGather: %s", ncclGetErrorString(r));
+                return KDTN_EIO;
             }
-            if (side) {
-                if (!exchange) {
-                    HIP_TRY(hipEventRecord(c->ev_front, s));
-                    HIP_TRY(hipStreamWaitEvent(ls, c->ev_front, 0));
-                }
-                TRY(lookup_build(ls));
-                verify_prefix(ls);
-                HIP_TRY(hipEventRecord(c->ev_side, ls));
-            }
+            HIP_TRY(hipEventRecord(c->ev_ag, c->comm_stream));
+        } else if (begin_first) {
+            begin(s);
             timer_mark(c, "pods_fill", 2);
+        }
+        if (side) {
+            if (!exchange) {
+                HIP_TRY(hipEventRecord(c->ev_front, s));
+                HIP_TRY(hipStreamWaitEvent(ls, c->ev_front, 0));
+            }
+            TRY(lookup_build(ls, false));
+            verify_prefix(ls);
+            HIP_TRY(hipEventRecord(c->ev_side, ls));
         }
         // dictionaries: the strings this upload added (all of them unless kdict_keep /
         // pdict_keep), from a multiple of 64 so every wave writes whole predicate words
@@ -1265,11 +1273,15 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         const uint32_t k0f = c->kd_from & ~63u, p0f = c->pd_from & ~63u;
         if (dict_fuse && c->D > k0f && c->P > p0f) {              // both parses in one launch
             const uint32_t nbk = nblocks(c->D - k0f), nbp = nblocks(c->P - p0f);
-            k_dict_parse<<<3 * nbp + nbk, BLOCK, 0, s>>>(
+            auto kern = k_dict_parse;
+#if KDTN_PROFILING
+            if (dict_fuse >= 3) kern = k_dict_parse_w7;                  // (3: values first, 4: keys first)
+#endif
+            kern<<<3 * nbp + nbk, BLOCK, 0, s>>>(
                 dp<uint8_t>(c->kd_bytes), dp<uint32_t>(c->kd_offs), k0f, c->D, dp<uint32_t>(c->kd_bits), c->kb_words,
                 special, dp<uint8_t>(c->pd_bytes), dp<uint32_t>(c->pd_offs), p0f, c->P, nbp, c->cfg.tick_in_usec,
                 dp<uint32_t>(c->pd_pct), dp<uint2>(c->pd_dur), dp<uint2>(c->pd_rate), dp<uint32_t>(c->pd_rerr),
-                dict_fuse == 2 ? nbk : 0u);
+                (dict_fuse == 2 || dict_fuse == 4) ? nbk : 0u);
             timer_mark(c, "dict_parse", 2);
         } else {
         {
@@ -1307,6 +1319,10 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         }
         timer_mark(c, "pdict_parse", 2);
         }
+        if (!exchange && !begin_first) {
+            begin(s);
+            timer_mark(c, "pods_fill", 2);
+        }
         if (resolve) {
             if (side) {
                 if (c->V) TRY(build_vni_table(c));
@@ -1315,7 +1331,7 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
             } else {
                 if (exchange) HIP_TRY(hipStreamWaitEvent(s, c->ev_ag, 0));   // exchange not hidden by the parses
                 timer_mark(c, "pods_allgather", 2);
-                if (pod_rows && !pods_cur) TRY(lookup_build(s));
+                if (pod_rows && !pods_cur) TRY(lookup_build(s, true));
                 else if (!pods_cur && ++c->pod_stamp >= 0x7FFFFFFFu) {     // (no rows: the stamp still moves)
                     HIP_TRY(hipMemsetAsync(c->pod_direct.p, 0, c->pod_direct.cap, s));
                     HIP_TRY(hipMemsetAsync(c->pod_ovf.p, 0, c->pod_ovf.cap, s));

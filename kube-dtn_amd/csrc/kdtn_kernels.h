@@ -122,7 +122,7 @@ struct DevLinks {
 #endif
 // epoch front: k_kdict_flags and k_pdict_parse as one launch (k_dict_parse)
 #ifndef KDTN_DICT_FUSE_DEFAULT
-#define KDTN_DICT_FUSE_DEFAULT true     // N = 8 rank epoch 0.2163 -> 0.1990 ms (profiles/r05b_fuse_ab.jsonl)
+#define KDTN_DICT_FUSE_DEFAULT false    // A/B in one process: N = 1 0.797 vs 0.811 ms, N = 8 0.183 vs 0.185 (r05e)
 #endif
 // k_pdict_parse: one thread per (string, interpretation) instead of one per string
 #ifndef KDTN_PD_SPLIT_DEFAULT
@@ -260,11 +260,15 @@ __global__ void k_dict_parse(const uint8_t* kd_bytes, const uint32_t* kd_offs, u
                              uint32_t kb_words, uint32_t* special, const uint8_t* pd_bytes, const uint32_t* pd_offs,
                              uint32_t p0, uint32_t P, uint32_t nbp, double tick, uint32_t* ppct, uint2* pdur,
                              uint2* prate, uint32_t* rate_err, uint32_t nbk_first);
+__global__ void k_dict_parse_w7(const uint8_t* kd_bytes, const uint32_t* kd_offs, uint32_t k0, uint32_t D,
+                                uint32_t* kbits, uint32_t kb_words, uint32_t* special, const uint8_t* pd_bytes,
+                                const uint32_t* pd_offs, uint32_t p0, uint32_t P, uint32_t nbp, double tick,
+                                uint32_t* ppct, uint2* pdur, uint2* prate, uint32_t* rate_err, uint32_t nbk_first);
 __global__ void k_epoch_begin(uint4* sync, uint32_t n16, uint32_t nbz, DevTopos T, uint32_t slice, uint32_t rank_base,
                               uint4* pods);
-__global__ void k_pod_direct_scatter(const uint4* pods, uint32_t total, const uint8_t* kd_bytes,
-                                     const uint32_t* kd_offs, uint4* slots, uint32_t stamp, uint32_t nd, uint32_t nr,
-                                     uint32_t gathered);
+__global__ void k_pod_direct_scatter(const uint4* pods, uint32_t total, const uint32_t* phys_bits,
+                                     const uint8_t* kd_bytes, const uint32_t* kd_offs, uint4* slots, uint32_t stamp,
+                                     uint32_t nd, uint32_t nr, uint32_t gathered);
 __global__ void k_epoch_front(uint4* sync, uint32_t n16, uint32_t nbz, uint32_t nbs, DevTopos T, uint32_t slice,
                               uint4* pods, uint4* slots, uint32_t stamp, const uint8_t* kd_bytes,
                               const uint32_t* kd_offs, uint32_t k0, uint32_t D, uint32_t* kbits, uint32_t kb_words,

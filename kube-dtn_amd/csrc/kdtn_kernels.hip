@@ -647,13 +647,11 @@ __global__ void __launch_bounds__(BLOCK) k_pdict_parse(const uint8_t* bytes, con
 // Both dictionaries' parses in one launch (independent work, one kernel boundary less per
 // epoch): blocks [0, 3 * nbp) parse property strings [p0, P), interpretation b / nbp (the
 // heavier blocks first), the rest classify key strings [k0, D) as k_kdict_flags does.
-__global__ void __launch_bounds__(BLOCK) k_dict_parse(const uint8_t* kd_bytes, const uint32_t* kd_offs, uint32_t k0,
-                                                      uint32_t D, uint32_t* kbits, uint32_t kb_words,
-                                                      uint32_t* special, const uint8_t* pd_bytes,
-                                                      const uint32_t* pd_offs, uint32_t p0, uint32_t P, uint32_t nbp,
-                                                      double tick, uint32_t* ppct, uint2* pdur, uint2* prate,
-                                                      uint32_t* rate_err, uint32_t nbk) {
-    __shared__ uint4 buf[STAGE / 16];
+KD_INLINE void dict_parse_block(const uint8_t* kd_bytes, const uint32_t* kd_offs, uint32_t k0, uint32_t D,
+                                 uint32_t* kbits, uint32_t kb_words, uint32_t* special, const uint8_t* pd_bytes,
+                                 const uint32_t* pd_offs, uint32_t p0, uint32_t P, uint32_t nbp, double tick,
+                                 uint32_t* ppct, uint2* pdur, uint2* prate, uint32_t* rate_err, uint32_t nbk,
+                                 uint4* buf) {
     uint32_t b = blockIdx.x;
     if (nbk) {                              // (key-string blocks first)
         if (b < nbk) {
@@ -670,6 +668,29 @@ __global__ void __launch_bounds__(BLOCK) k_dict_parse(const uint8_t* kd_bytes, c
     else if (y == 1) pdict_parse_block<PD_DUR>(pd_bytes, pd_offs, s0, P, tick, ppct, pdur, prate, rate_err, buf);
     else pdict_parse_block<PD_RATE>(pd_bytes, pd_offs, s0, P, tick, ppct, pdur, prate, rate_err, buf);
 }
+__global__ void __launch_bounds__(BLOCK) k_dict_parse(const uint8_t* kd_bytes, const uint32_t* kd_offs, uint32_t k0,
+                                                      uint32_t D, uint32_t* kbits, uint32_t kb_words,
+                                                      uint32_t* special, const uint8_t* pd_bytes,
+                                                      const uint32_t* pd_offs, uint32_t p0, uint32_t P, uint32_t nbp,
+                                                      double tick, uint32_t* ppct, uint2* pdur, uint2* prate,
+                                                      uint32_t* rate_err, uint32_t nbk) {
+    __shared__ uint4 buf[STAGE / 16];
+    dict_parse_block(kd_bytes, kd_offs, k0, D, kbits, kb_words, special, pd_bytes, pd_offs, p0, P, nbp, tick, ppct,
+                     pdur, prate, rate_err, nbk, buf);
+}
+#if KDTN_PROFILING
+// (A/B) the same held to the SGPR budget of 7 waves per SIMD (k_kdict_flags alone runs at 7;
+// the fused kernel's 112 SGPRs allow 6)
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(7, 8)))
+k_dict_parse_w7(const uint8_t* kd_bytes, const uint32_t* kd_offs, uint32_t k0, uint32_t D, uint32_t* kbits,
+                uint32_t kb_words, uint32_t* special, const uint8_t* pd_bytes, const uint32_t* pd_offs, uint32_t p0,
+                uint32_t P, uint32_t nbp, double tick, uint32_t* ppct, uint2* pdur, uint2* prate, uint32_t* rate_err,
+                uint32_t nbk) {
+    __shared__ uint4 buf[STAGE / 16];
+    dict_parse_block(kd_bytes, kd_offs, k0, D, kbits, kb_words, special, pd_bytes, pd_offs, p0, P, nbp, tick, ppct,
+                     pdur, prate, rate_err, nbk, buf);
+}
+#endif
 
 #if KDTN_PROFILING
 // (profiling) one interpretation alone: WHICH = PD_DUR / PD_PCT / PD_RATE
@@ -792,16 +813,18 @@ KD_INLINE uint32_t name_physical(const uint8_t* kd_bytes, const uint32_t* kd_off
     return (w0 == 0x73796870u && w1 == 0x6C616369u && (w2 & 0xFFu) == '/') ? 1u : 0u;   // "phys" "ical" '/'
 }
 
+// phys_bits: the KB_PHYSICAL bitset of a finished key-string parse, or null (the PHYSICAL bit
+// from the name's bytes: the lookup build beside the parses, A/B)
 __global__ void __launch_bounds__(BLOCK) k_pod_direct_scatter(const uint4* pods, uint32_t total,
-                                                              const uint8_t* kd_bytes, const uint32_t* kd_offs,
-                                                              uint4* slots, uint32_t stamp, uint32_t nd, uint32_t nr,
-                                                              uint32_t gathered) {
+                                                              const uint32_t* phys_bits, const uint8_t* kd_bytes,
+                                                              const uint32_t* kd_offs, uint4* slots, uint32_t stamp,
+                                                              uint32_t nd, uint32_t nr, uint32_t gathered) {
     const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
     if (t >= total) return;
     const uint32_t g = pod_order(t, gathered, nr);
     const uint4 e = pods[g];
     if (e.x == 0xFFFFFFFFu || e.y >= nd) return;           // padding row / name outside this dictionary
-    const uint32_t phys = name_physical(kd_bytes, kd_offs, e.y);
+    const uint32_t phys = phys_bits ? (phys_bits[e.y >> 5] >> (e.y & 31)) & 1u : name_physical(kd_bytes, kd_offs, e.y);
     slots[e.y] = make_uint4(e.x, (g << 2) | (phys << 1) | (e.w >> 31),
                             e.z | ((e.w & 0x7FFFFFFFu) == 0 ? 0x80000000u : 0u), stamp << 1);
 }
