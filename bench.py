@@ -326,11 +326,12 @@ def resident_chain_stage(eng, cs, prev, epochs: int, topology_set: bool = False)
 
 def resident_pipeline_stage(eng, cs, prev, epochs: int):
     """The same resident controller loop pipelined over the full-duplex host link (separate
-    report, never `value`): epoch k's outputs are copied out asynchronously
-    (kdtn_epoch_download_async into one of two page-locked buffer sets) while epoch k+1's delta
-    is uploaded; the next run waits for the copies on the GPU. Per-epoch time = wall time of
+    report, never `value`): epoch k's outputs are copied out asynchronously on an SDMA engine
+    (kdtn_epoch_download_async into one of two page-locked buffer sets: no CUs) while epoch
+    k+1's delta is uploaded; the next run waits for the copies. Per-epoch time = wall time of
     the loop / epochs, after 2 warm-up epochs; every epoch's outputs are complete in host
-    memory (download_wait) before the next-but-one reuses their buffers."""
+    memory (download_wait) before the next-but-one reuses their buffers. `cs` may change the
+    Topology set (synth.TopologySetChurn) as long as the count stays."""
     from kdtn.delta import build_delta
     from kdtn.engine import pin_delta
     from kdtn.tables import BatchesOut
@@ -344,6 +345,8 @@ def resident_pipeline_stage(eng, cs, prev, epochs: int):
         new = cs.epoch_input(copy=True)
         deltas.append(pin_delta(build_delta(p, new, p.kdict.n, p.pdict.n)))
         p = new
+    Ts = {T} | {len(d.prev) for d in deltas if d.prev is not None}
+    assert len(Ts) == 1, "the pipelined loop reuses buffers sized for one topology count"
     bufs = [BatchesOut.alloc(T, cap, cap, cap, pinned=True) for _ in range(2)]
     ones = np.ones(T, np.uint8)
     eng.commit(ones)
@@ -839,6 +842,14 @@ def main():
         eng.sync()
         result["resident_chain_topology_set"] = resident_chain_stage(eng, tc, p0, args.resident_epochs,
                                                                      topology_set=True)
+        del tc, p0
+        progress("resident chain with a changing Topology set, pipelined")
+        tc = synth.TopologySetChurn(frac=0.01, total_pods=total_pods)
+        p0 = tc.epoch_input()
+        eng.upload(p0)
+        eng.run()
+        eng.sync()
+        result["resident_pipeline_topology_set"] = resident_pipeline_stage(eng, tc, p0, args.resident_epochs)
         del tc, p0
     if diff_ms:
         result["diff_only_reconcile_ms"] = float(np.mean(diff_ms))

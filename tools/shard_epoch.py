@@ -90,6 +90,23 @@ with Engine(device=0) as eng:
             tot.append(time.perf_counter() - t)
         res[f"parsed_L{level}"] = {"ms_epoch": sorted(tot)[len(tot) // 2] * 1e3,
                                    "kernels_ms": eng.kernel_times() if level else {}}
+    # the rank's strings fresh, the shared dictionary prefix (pod names, namespaces, netns paths,
+    # node IPs: one interner prefix on every rank) kept: a controller whose prefix interner is
+    # append-only re-parses only its own link strings and property strings each epoch
+    prefix = int(max(full.topos.net_ns.max(), full.topos.name.max())) + 1
+    eng.upload(sh, prefix, 0)
+    eng.pods_import(rows)
+    eng.set_timing(0)
+    for _ in range(3):
+        eng.run()
+        eng.sync()
+    tot = []
+    for _ in range(a.reps):
+        t = time.perf_counter()
+        eng.run()
+        eng.sync()
+        tot.append(time.perf_counter() - t)
+    res["prefix_kept_L0"] = {"ms_epoch": sorted(tot)[len(tot) // 2] * 1e3, "kdict_keep": prefix}
     ms = res["L0"]["ms_epoch"]
     res["projected_links_per_s_at_N"] = a.pods * 10 / (ms * 1e-3)
     # Estimated RCCL all-gather of the pod-status rows (not measured: one GPU here). It starts
