@@ -1172,22 +1172,38 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
 #endif
     hipStream_t ls = exchange ? c->comm_stream : (side_mode == 2 && c->side_hi ? c->side_hi : c->side_stream);
     const bool side = side_mode && !fused && resolve && pod_rows && !pods_cur && c->T && ls && c->ev_front && c->ev_side;
+#if KDTN_PROFILING
+    int pod_per = 1;                                                 // (A/B: pod rows per thread)
+    if (const char* ev = std::getenv("KDTN_POD_PER")) pod_per = std::atoi(ev);
+#else
+    constexpr int pod_per = 1;
+#endif
     auto lookup_build = [&](hipStream_t q, bool parsed) -> int {
         if (++c->pod_stamp >= 0x7FFFFFFFu) {                             // stamp wrap: clear once
             HIP_TRY(hipMemsetAsync(c->pod_direct.p, 0, c->pod_direct.cap, q));
             HIP_TRY(hipMemsetAsync(c->pod_ovf.p, 0, c->pod_ovf.cap, q));
             c->pod_stamp = 1;
         }
-        k_pod_direct_scatter<<<nblocks(pod_rows), BLOCK, 0, q>>>(
+        auto kern = k_pod_direct_scatter<1>;
+#if KDTN_PROFILING
+        if (pod_per == 2) kern = k_pod_direct_scatter<2>;
+        else if (pod_per == 4) kern = k_pod_direct_scatter<4>;
+#endif
+        kern<<<nblocks(pod_rows, BLOCK * pod_per), BLOCK, 0, q>>>(
             dp<uint4>(c->pods), pod_rows, parsed ? dp<uint32_t>(c->kd_bits) + (size_t)KB_PHYSICAL * c->kb_words : nullptr,
             dp<uint8_t>(c->kd_bytes), dp<uint32_t>(c->kd_offs), dp<uint4>(c->pod_direct), c->pod_stamp, c->D,
             c->pods_rank_major ? (uint32_t)c->nranks : 1u, c->pod_total);
         return KDTN_OK;
     };
     auto verify_prefix = [&](hipStream_t q) {
-        const uint32_t nbv = nblocks(pod_rows);
+        const uint32_t nbv = nblocks(pod_rows, BLOCK * pod_per);
         const uint32_t nbp = (uint32_t)std::min<uint64_t>(4 * FP_GRID, (c->T + 4 * BLOCK - 1) / (4 * BLOCK));
-        k_pod_verify_prefix<<<nbv + std::max<uint32_t>(nbp, 1), BLOCK, 0, q>>>(
+        auto kern = k_pod_verify_prefix<1>;
+#if KDTN_PROFILING
+        if (pod_per == 2) kern = k_pod_verify_prefix<2>;
+        else if (pod_per == 4) kern = k_pod_verify_prefix<4>;
+#endif
+        kern<<<nbv + std::max<uint32_t>(nbp, 1), BLOCK, 0, q>>>(
             dp<uint4>(c->pods), pod_rows, dp<uint4>(c->pod_direct), c->pod_stamp,
             dp<unsigned long long>(c->pod_ovf), c->ovf_mask, c->D, T, sync + SYNC_FIRST_PARTIAL_INV, nbv,
             c->pods_rank_major ? (uint32_t)c->nranks : 1u, c->pod_total);

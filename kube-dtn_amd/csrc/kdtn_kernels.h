@@ -266,6 +266,7 @@ __global__ void k_dict_parse_w7(const uint8_t* kd_bytes, const uint32_t* kd_offs
                                 uint32_t* ppct, uint2* pdur, uint2* prate, uint32_t* rate_err, uint32_t nbk_first);
 __global__ void k_epoch_begin(uint4* sync, uint32_t n16, uint32_t nbz, DevTopos T, uint32_t slice, uint32_t rank_base,
                               uint4* pods);
+template <int PER>
 __global__ void k_pod_direct_scatter(const uint4* pods, uint32_t total, const uint32_t* phys_bits,
                                      const uint8_t* kd_bytes, const uint32_t* kd_offs, uint4* slots, uint32_t stamp,
                                      uint32_t nd, uint32_t nr, uint32_t gathered);
@@ -617,6 +618,7 @@ __global__ void k_wire_write(WireIn w, DevLinks O, DevLinks N, WireWork wk, uint
 __global__ void k_qdisc_batch(DevLinks props, DevTables tb, uint2* out);
 constexpr int FP_BLOCK = 1024, FP_GRID = 256;       // k_full_prefix launch shape
 __global__ void k_full_prefix(DevTopos T, uint32_t* first_partial_inv);
+template <int PER>
 __global__ void k_pod_verify_prefix(const uint4* pods, uint32_t total, uint4* slots, uint32_t stamp,
                                     unsigned long long* ovf, uint32_t mask, uint32_t nd, DevTopos T,
                                     uint32_t* first_partial_inv, uint32_t nbv, uint32_t nr, uint32_t gathered);

@@ -815,19 +815,38 @@ KD_INLINE uint32_t name_physical(const uint8_t* kd_bytes, const uint32_t* kd_off
 
 // phys_bits: the KB_PHYSICAL bitset of a finished key-string parse, or null (the PHYSICAL bit
 // from the name's bytes: the lookup build beside the parses, A/B)
+template <int PER>
 __global__ void __launch_bounds__(BLOCK) k_pod_direct_scatter(const uint4* pods, uint32_t total,
                                                               const uint32_t* phys_bits, const uint8_t* kd_bytes,
                                                               const uint32_t* kd_offs, uint4* slots, uint32_t stamp,
                                                               uint32_t nd, uint32_t nr, uint32_t gathered) {
-    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
-    if (t >= total) return;
-    const uint32_t g = pod_order(t, gathered, nr);
-    const uint4 e = pods[g];
-    if (e.x == 0xFFFFFFFFu || e.y >= nd) return;           // padding row / name outside this dictionary
-    const uint32_t phys = phys_bits ? (phys_bits[e.y >> 5] >> (e.y & 31)) & 1u : name_physical(kd_bytes, kd_offs, e.y);
-    slots[e.y] = make_uint4(e.x, (g << 2) | (phys << 1) | (e.w >> 31),
-                            e.z | ((e.w & 0x7FFFFFFFu) == 0 ? 0x80000000u : 0u), stamp << 1);
+    // PER rows per thread, every row load issued before the first slot store (latency-bound)
+    const uint32_t t0 = blockIdx.x * BLOCK * PER + threadIdx.x;
+    uint32_t g[PER];
+    uint4 e[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t t = t0 + q * BLOCK;
+        g[q] = t < total ? pod_order(t, gathered, nr) : 0u;
+        e[q] = t < total ? pods[g[q]] : make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
+    }
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        if (e[q].x == 0xFFFFFFFFu || e[q].y >= nd) continue;   // padding row / name outside this dictionary
+        const uint32_t y = e[q].y;
+        const uint32_t phys = phys_bits ? (phys_bits[y >> 5] >> (y & 31)) & 1u : name_physical(kd_bytes, kd_offs, y);
+        slots[y] = make_uint4(e[q].x, (g[q] << 2) | (phys << 1) | (e[q].w >> 31),
+                              e[q].z | ((e[q].w & 0x7FFFFFFFu) == 0 ? 0x80000000u : 0u), stamp << 1);
+    }
 }
+template __global__ void k_pod_direct_scatter<1>(const uint4*, uint32_t, const uint32_t*, const uint8_t*, const uint32_t*,
+                                                 uint4*, uint32_t, uint32_t, uint32_t, uint32_t);
+#if KDTN_PROFILING
+template __global__ void k_pod_direct_scatter<2>(const uint4*, uint32_t, const uint32_t*, const uint8_t*, const uint32_t*,
+                                                 uint4*, uint32_t, uint32_t, uint32_t, uint32_t);
+template __global__ void k_pod_direct_scatter<4>(const uint4*, uint32_t, const uint32_t*, const uint8_t*, const uint32_t*,
+                                                 uint4*, uint32_t, uint32_t, uint32_t, uint32_t);
+#endif
 
 // Pods whose name slot was won by another pod: mark the name `multi` and put both pods
 // into the overflow table (duplicates are rare; the table then answers every lookup of
@@ -1687,19 +1706,47 @@ __global__ void __launch_bounds__(FP_BLOCK) k_full_prefix(DevTopos T, uint32_t* 
 
 // k_pod_direct_verify and k_full_prefix in one launch (independent work; one kernel boundary
 // less per epoch): blocks [0, nbv) verify pods, the rest scan topologies.
+template <int PER>
 __global__ void __launch_bounds__(BLOCK) k_pod_verify_prefix(const uint4* pods, uint32_t total, uint4* slots,
                                                              uint32_t stamp, unsigned long long* ovf, uint32_t mask,
                                                              uint32_t nd, DevTopos T, uint32_t* first_partial_inv,
                                                              uint32_t nbv, uint32_t nr, uint32_t gathered) {
     __shared__ uint32_t bmin;
     if (blockIdx.x < nbv) {
-        const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
-        if (t < total) pod_verify_one(pods, total, slots, stamp, ovf, mask, nd, pod_order(t, gathered, nr));
+        if constexpr (PER == 1) {
+            const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+            if (t < total) pod_verify_one(pods, total, slots, stamp, ovf, mask, nd, pod_order(t, gathered, nr));
+        } else {                                  // PER rows per thread: row loads, then slot owner words
+            const uint32_t t0 = blockIdx.x * BLOCK * PER + threadIdx.x;
+            uint32_t g[PER], own[PER];
+            uint4 e[PER];
+#pragma unroll
+            for (int q = 0; q < PER; ++q) {
+                const uint32_t t = t0 + q * BLOCK;
+                g[q] = t < total ? pod_order(t, gathered, nr) : 0u;
+                e[q] = t < total ? pods[g[q]] : make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
+            }
+#pragma unroll
+            for (int q = 0; q < PER; ++q)
+                own[q] = (e[q].x == 0xFFFFFFFFu || e[q].y >= nd) ? g[q] << 2
+                         : reinterpret_cast<const uint32_t*>(slots + e[q].y)[1];
+#pragma unroll
+            for (int q = 0; q < PER; ++q)
+                if ((own[q] >> 2) != g[q]) pod_verify_one(pods, total, slots, stamp, ovf, mask, nd, g[q]);
+        }
         return;
     }
     full_prefix_blocks<BLOCK>(T, first_partial_inv, blockIdx.x - nbv, gridDim.x - nbv, &bmin);
 }
 
+template __global__ void k_pod_verify_prefix<1>(const uint4*, uint32_t, uint4*, uint32_t, unsigned long long*, uint32_t,
+                                                uint32_t, DevTopos, uint32_t*, uint32_t, uint32_t, uint32_t);
+#if KDTN_PROFILING
+template __global__ void k_pod_verify_prefix<2>(const uint4*, uint32_t, uint4*, uint32_t, unsigned long long*, uint32_t,
+                                                uint32_t, DevTopos, uint32_t*, uint32_t, uint32_t, uint32_t);
+template __global__ void k_pod_verify_prefix<4>(const uint4*, uint32_t, uint4*, uint32_t, unsigned long long*, uint32_t,
+                                                uint32_t, DevTopos, uint32_t*, uint32_t, uint32_t, uint32_t);
+#endif
 #if KDTN_PROFILING
 // ---- (A/B, KDTN_FUSE=1) fused epoch front (one local rank: no exchange) ------------------
 // Measured no faster than the launches in sequence (0.7895 vs 0.7882 ms per config-2 epoch,

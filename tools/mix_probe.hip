@@ -9,7 +9,8 @@
 // predicate word) and 3 dwords from a 64 KB table (hot parsed values). Kernels:
 //   stream   the loads and stores only
 //   gather   the random lanes only (ids from a hash of the record index)
-//   mix      both, the ids taken from the loaded columns (the dependency k_reconcile has)
+//   mix      both, the ids taken from the loaded columns (the dependency k_reconcile has;
+//            the columns hold random words)
 //   mix_ind  both, ids from the hash (no load → gather dependency)
 // 10M records (config 2), 256-thread workgroups held to 4 per CU by 28 KB of LDS like
 // k_reconcile. One JSON line per kernel (best of 5).
@@ -71,6 +72,12 @@ __global__ void __launch_bounds__(BLOCK) k_mix(const uint32_t* __restrict__ cols
     if (acc == 0x9E3779B9u) sink[0] = acc + lds[0];
 }
 
+// random column contents (a memset would make every dependent id the same address)
+__global__ void k_fill(uint32_t* a, uint64_t n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        a[i] = mix32((uint32_t)i * 0x9E3779B9u + 0x7F4A7C15u);
+}
+
 int main() {
     int ncu = 0;
     CK(hipSetDevice(0));
@@ -84,7 +91,7 @@ int main() {
     CK(hipMalloc(&mid, (size_t)MID * 4));
     CK(hipMalloc(&hot, (size_t)HOT * 4));
     CK(hipMalloc(&sink, 64));
-    CK(hipMemset(cols, 7, (size_t)n * NLOAD * 4));
+    k_fill<<<1024, 256>>>(cols, (uint64_t)n * NLOAD);
     CK(hipMemset(big, 1, (size_t)BIG * 16));
     CK(hipMemset(mid, 2, (size_t)MID * 4));
     CK(hipMemset(hot, 3, (size_t)HOT * 4));
