@@ -1172,11 +1172,14 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
 #endif
     hipStream_t ls = exchange ? c->comm_stream : (side_mode == 2 && c->side_hi ? c->side_hi : c->side_stream);
     const bool side = side_mode && !fused && resolve && pod_rows && !pods_cur && c->T && ls && c->ev_front && c->ev_side;
+    // 4 pod rows per thread in the lookup build (every row load issued before the dependent
+    // accesses): rank of 8 0.1761 / 0.1770 → 0.1735 / 0.1744 ms, N = 1 0.7895 → 0.7883 ms
+    // (profiles/r05h_pod_per_ab_*)
 #if KDTN_PROFILING
-    int pod_per = 1;                                                 // (A/B: pod rows per thread)
+    int pod_per = 4;                                                 // (A/B: KDTN_POD_PER = 1, 2, 4)
     if (const char* ev = std::getenv("KDTN_POD_PER")) pod_per = std::atoi(ev);
 #else
-    constexpr int pod_per = 1;
+    constexpr int pod_per = 4;
 #endif
     auto lookup_build = [&](hipStream_t q, bool parsed) -> int {
         if (++c->pod_stamp >= 0x7FFFFFFFu) {                             // stamp wrap: clear once
@@ -1184,10 +1187,9 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
             HIP_TRY(hipMemsetAsync(c->pod_ovf.p, 0, c->pod_ovf.cap, q));
             c->pod_stamp = 1;
         }
-        auto kern = k_pod_direct_scatter<1>;
+        auto kern = pod_per == 4 ? k_pod_direct_scatter<4> : k_pod_direct_scatter<1>;
 #if KDTN_PROFILING
         if (pod_per == 2) kern = k_pod_direct_scatter<2>;
-        else if (pod_per == 4) kern = k_pod_direct_scatter<4>;
 #endif
         kern<<<nblocks(pod_rows, BLOCK * pod_per), BLOCK, 0, q>>>(
             dp<uint4>(c->pods), pod_rows, parsed ? dp<uint32_t>(c->kd_bits) + (size_t)KB_PHYSICAL * c->kb_words : nullptr,
@@ -1198,10 +1200,9 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
     auto verify_prefix = [&](hipStream_t q) {
         const uint32_t nbv = nblocks(pod_rows, BLOCK * pod_per);
         const uint32_t nbp = (uint32_t)std::min<uint64_t>(4 * FP_GRID, (c->T + 4 * BLOCK - 1) / (4 * BLOCK));
-        auto kern = k_pod_verify_prefix<1>;
+        auto kern = pod_per == 4 ? k_pod_verify_prefix<4> : k_pod_verify_prefix<1>;
 #if KDTN_PROFILING
         if (pod_per == 2) kern = k_pod_verify_prefix<2>;
-        else if (pod_per == 4) kern = k_pod_verify_prefix<4>;
 #endif
         kern<<<nbv + std::max<uint32_t>(nbp, 1), BLOCK, 0, q>>>(
             dp<uint4>(c->pods), pod_rows, dp<uint4>(c->pod_direct), c->pod_stamp,

@@ -841,10 +841,10 @@ __global__ void __launch_bounds__(BLOCK) k_pod_direct_scatter(const uint4* pods,
 }
 template __global__ void k_pod_direct_scatter<1>(const uint4*, uint32_t, const uint32_t*, const uint8_t*, const uint32_t*,
                                                  uint4*, uint32_t, uint32_t, uint32_t, uint32_t);
+template __global__ void k_pod_direct_scatter<4>(const uint4*, uint32_t, const uint32_t*, const uint8_t*, const uint32_t*,
+                                                 uint4*, uint32_t, uint32_t, uint32_t, uint32_t);
 #if KDTN_PROFILING
 template __global__ void k_pod_direct_scatter<2>(const uint4*, uint32_t, const uint32_t*, const uint8_t*, const uint32_t*,
-                                                 uint4*, uint32_t, uint32_t, uint32_t, uint32_t);
-template __global__ void k_pod_direct_scatter<4>(const uint4*, uint32_t, const uint32_t*, const uint8_t*, const uint32_t*,
                                                  uint4*, uint32_t, uint32_t, uint32_t, uint32_t);
 #endif
 
@@ -1741,10 +1741,10 @@ __global__ void __launch_bounds__(BLOCK) k_pod_verify_prefix(const uint4* pods, 
 
 template __global__ void k_pod_verify_prefix<1>(const uint4*, uint32_t, uint4*, uint32_t, unsigned long long*, uint32_t,
                                                 uint32_t, DevTopos, uint32_t*, uint32_t, uint32_t, uint32_t);
+template __global__ void k_pod_verify_prefix<4>(const uint4*, uint32_t, uint4*, uint32_t, unsigned long long*, uint32_t,
+                                                uint32_t, DevTopos, uint32_t*, uint32_t, uint32_t, uint32_t);
 #if KDTN_PROFILING
 template __global__ void k_pod_verify_prefix<2>(const uint4*, uint32_t, uint4*, uint32_t, unsigned long long*, uint32_t,
-                                                uint32_t, DevTopos, uint32_t*, uint32_t, uint32_t, uint32_t);
-template __global__ void k_pod_verify_prefix<4>(const uint4*, uint32_t, uint4*, uint32_t, unsigned long long*, uint32_t,
                                                 uint32_t, DevTopos, uint32_t*, uint32_t, uint32_t, uint32_t);
 #endif
 #if KDTN_PROFILING
