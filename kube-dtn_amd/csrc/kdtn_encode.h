@@ -163,6 +163,100 @@ struct WSink {
     }
 };
 
+// ---- inline string tables (StrTab, kdtn_kernels.h) ------------------------------------------
+template <int W>
+struct SIE {
+    uint32_t w[W];
+};
+// length of string id (id 0 = ""), from the byte table (a long or invalid string: its entry);
+// bad |= 1 when the string is not valid UTF-8
+template <int W>
+KD_INLINE uint32_t si_len(const StrTab& t, uint32_t id, uint32_t& bad) {
+    if (!id) return 0u;
+    const uint32_t l = t.len1[id];
+    if (l != 255u) return l;
+    const uint32_t* e = t.inl + (size_t)id * W;
+    if (e[0] & SI_BAD) bad = 1u;
+    return e[2];
+}
+// entry of string id (id 0: zero, no gather). A key entry (W = 6) loads its last 8 bytes only
+// for an inline string of more than 15 bytes (its first 16 bytes and the rest share a line
+// three times in four).
+template <int W>
+KD_INLINE SIE<W> si_load(const StrTab& t, uint32_t id) {
+    SIE<W> e;
+#pragma unroll
+    for (int k = 0; k < W; ++k) e.w[k] = 0u;
+    if (!id) return e;
+    typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+    const uint32_t* p = t.inl + (size_t)id * W;
+    const u32x4a a = *reinterpret_cast<const u32x4a*>(p);
+    e.w[0] = a.x;
+    e.w[1] = a.y;
+    e.w[2] = a.z;
+    e.w[3] = a.w;
+    if constexpr (W > 4) {
+        const uint32_t b0 = a.x & 0xFFu;
+        if (b0 > 15u && b0 < SI_LONG) {
+            const uint2 b = *reinterpret_cast<const uint2*>(p + 4);
+            e.w[4] = b.x;
+            e.w[5] = b.y;
+        }
+    }
+    return e;
+}
+// length of a loaded entry's string (an invalid one's too); its SI_BAD bit
+template <int W>
+KD_INLINE uint32_t si_elen(const SIE<W>& e) {
+    const uint32_t b0 = e.w[0] & 0xFFu;
+    return b0 < SI_LONG ? b0 : e.w[2];
+}
+template <int W>
+KD_INLINE uint32_t si_ebad(const SIE<W>& e) { return e.w[0] & SI_BAD; }
+
+// protobuf string field `field` (nothing for ""): the tag, then bytes 0..len of an inline entry
+// (byte 0 is the string's one-byte length varint), or the tag, the length varint and the arena
+// bytes of a long string
+template <int W>
+KD_INLINE void si_field(WSink& o, uint32_t field, const SIE<W>& e, const uint8_t* arena) {
+    const uint32_t b0 = e.w[0] & 0xFFu;
+    if (b0 == 0u) return;
+    if (b0 < SI_LONG) {
+        o.byte(field << 3 | 2u);
+        const uint32_t n = b0 + 1u;
+        o.put(e.w[0], n < 4u ? n : 4u);
+#pragma unroll
+        for (int q = 1; q < W; ++q) {
+            if (!__ballot(4u * q < n)) break;              // the wave's longest string written
+            if (4u * q < n) o.put(e.w[q], n - 4u * q < 4u ? n - 4u * q : 4u);
+        }
+        return;
+    }
+    const uint32_t len = e.w[2];
+    if (len < 0x80u) {
+        o.put((field << 3 | 2u) | (len << 8), 2u);
+    } else {
+        o.byte(field << 3 | 2u);
+        o.varint(len);
+    }
+    o.str(arena, e.w[1], len);
+}
+// the string's bytes alone (an argv element)
+template <int W>
+KD_INLINE void si_bytes(WSink& o, const SIE<W>& e, const uint8_t* arena) {
+    const uint32_t b0 = e.w[0] & 0xFFu;
+    if (b0 >= SI_LONG) {
+        o.str(arena, e.w[1], e.w[2]);
+        return;
+    }
+#pragma unroll
+    for (int q = 0; q < W; ++q) {
+        if (!__ballot(4u * q < b0)) break;
+        if (4u * q < b0)
+            o.put(__builtin_amdgcn_alignbyte(q + 1 < W ? e.w[q + 1] : 0u, e.w[q], 1u), b0 - 4u * q < 4u ? b0 - 4u * q : 4u);
+    }
+}
+
 // One wave writes the bytes of its active lanes, which are consecutive ranges [s0, s1) of one
 // arena (in lane order, empty lanes between them): each lane's body(WSink&) writes into the
 // wave's LDS image (`img`, WIRE_IMG bytes), then the wave stores the image with coalesced
@@ -303,6 +397,91 @@ KD_INLINE void wave_segments_write(uint32_t* img, bool on, uint64_t s0, uint64_t
     }
     wave_segments_round<32, 0, IMGB>(img, on, s0, len, ndw, arena, body);   // lanes 0-31, then 32-63
     wave_segments_round<32, 1, IMGB>(img, on, s0, len, ndw, arena, body);
+}
+
+// ---- tc argv (kdtn_tc.hip: kdtn_epoch_tc; kdtn_wire.hip: the receiving daemons' commands) ----
+KD_INLINE uint32_t ndigits(uint64_t v) {
+    uint32_t n = 1;
+    while (v >= 10u) { v /= 10u; ++n; }
+    return n;
+}
+// fixed argument bytes: "qdisc add dev " + " parent 1:1 handle 10:0 tbf rate " + " burst " +
+// " latency 50ms minburst " + final NUL (every separator is a NUL)
+constexpr uint32_t TC_FIXED = 14 + 1 + 32 + 1 + 6 + 1 + 22 + 1;
+
+struct TcEntry {
+    uint32_t intf;      // kdict id of LocalIntf
+    uint64_t rate;
+    uint32_t buffer, minburst;
+    bool on;
+};
+
+// bytes of a TBF command's argv (0 when it runs none)
+KD_INLINE uint32_t tc_size(const StrTab& kd, const TcEntry& t) {
+    uint32_t bad = 0;                                      // argv bytes need no UTF-8
+    return t.on ? TC_FIXED + si_len<SI_KW>(kd, t.intf, bad) + ndigits(t.rate) + ndigits(t.buffer) +
+                      ndigits(t.minburst)
+                : 0u;
+}
+
+// one argv element + its NUL separator: a literal, packed 4 bytes per put (constant-folded)
+template <int N>
+KD_INLINE void lit(WSink& o, const char (&s)[N]) {
+#pragma unroll
+    for (int k = 0; k < N; k += 4) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            if (k + c < N) w |= (uint32_t)(uint8_t)s[k + c] << (8 * c);
+        o.put(w, (uint32_t)(N - k < 4 ? N - k : 4));
+    }
+}
+// four ASCII digits of l < 10000, most significant first
+KD_INLINE uint32_t dig4(uint32_t l) {
+    return (0x30u + l / 1000u) | (0x30u + (l / 100u) % 10u) << 8 | (0x30u + (l / 10u) % 10u) << 16 |
+           (0x30u + l % 10u) << 24;
+}
+// fmt.Sprint of an unsigned integer + NUL: base-10000 limbs, the top one without leading zeros
+KD_INLINE void num(WSink& o, uint64_t v) {
+    const uint32_t l0 = (uint32_t)(v % 10000u);
+    v /= 10000u;
+    const uint32_t l1 = (uint32_t)(v % 10000u);
+    v /= 10000u;
+    const uint32_t l2 = (uint32_t)(v % 10000u);
+    v /= 10000u;
+    const uint32_t l3 = (uint32_t)(v % 10000u);
+    const uint32_t l4 = (uint32_t)(v / 10000u);          // < 1845 (2^64 < 10^20)
+    const int k = l4 ? 4 : l3 ? 3 : l2 ? 2 : l1 ? 1 : 0;
+    const uint32_t top = k == 4 ? l4 : k == 3 ? l3 : k == 2 ? l2 : k == 1 ? l1 : l0;
+    const uint32_t nd = ndigits(top);
+    o.put(dig4(top) >> (8u * (4u - nd)), nd);
+    if (k >= 4) o.put(dig4(l3), 4u);
+    if (k >= 3) o.put(dig4(l2), 4u);
+    if (k >= 2) o.put(dig4(l1), 4u);
+    if (k >= 1) o.put(dig4(l0), 4u);
+    o.byte(0u);
+}
+
+KD_INLINE void write_tbf_argv(WSink& o, const StrTab& kd, const TcEntry& t) {
+    const SIE<SI_KW> dev = si_load<SI_KW>(kd, t.intf);    // the interface name: one gather
+    lit(o, "qdisc");
+    lit(o, "add");
+    lit(o, "dev");
+    si_bytes(o, dev, kd.bytes);
+    o.byte(0u);
+    lit(o, "parent");
+    lit(o, "1:1");
+    lit(o, "handle");
+    lit(o, "10:0");
+    lit(o, "tbf");
+    lit(o, "rate");
+    num(o, t.rate);
+    lit(o, "burst");
+    num(o, t.buffer);
+    lit(o, "latency");
+    lit(o, "50ms");
+    lit(o, "minburst");
+    num(o, t.minburst);
 }
 
 }  // namespace kdtn

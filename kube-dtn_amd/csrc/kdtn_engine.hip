@@ -91,6 +91,7 @@ struct kdtn_ctx {
     DevBuf kd_bytes, kd_offs, kd_bits, pd_bytes, pd_offs, pd_pct, pd_dur, pd_rate, pd_rerr, kd_special;
     uint32_t D = 0, P = 0;
     uint32_t kd_from = 0, pd_from = 0, kd_valid = 0, pd_valid = 0, kb_cap = 0;
+    uint32_t si_k = 0, si_p = 0;           // leading strings whose inline encoder entries are built
 
     // topologies
     DevBuf t_ns, t_name, t_src, t_netns, t_flags, t_roff, t_noff;
@@ -138,13 +139,13 @@ struct kdtn_ctx {
     uint32_t nwg = 0;
     // outputs
     DevBuf action, del_off, add_off, upd_off, del_idx, add_idx, upd_idx;
-    DevBuf del_res, add_res, upd_res, add_qdisc, upd_qdisc;
+    DevBuf del_res, add_res, upd_res, add_qdisc, upd_qdisc, add_qerr;
     // wire encoding
-    DevBuf kd_utf8, pd_utf8, w_rel, w_topo, w_size, w_err, w_off, w_part, w_arena;
+    DevBuf kd_si, kd_len1, pd_si, pd_len1, w_rel, w_topo, w_size, w_err, w_off, w_part, w_arena;
     uint64_t w_bytes = 0;
     bool encoded = false;
     // RemotePod fan-out
-    DevBuf f_mark, f_send, f_node_idx, f_nodes, f_counts, f_base, f_part, f_idx, f_inv, f_reach_upd, f_cut, f_st;
+    DevBuf f_mark, f_send, f_node_idx, f_nodes, f_counts, f_base, f_part, f_idx, f_inv, f_reach_upd, f_cut, f_st, f_node;
     uint32_t f_stamp = 0;
     bool fan_valid = false;                    // the fan-out of the last run is in f_* (fanout_compute)
     uint32_t fan_nn = 0, fan_nsend = 0;
@@ -710,6 +711,8 @@ int upload_dicts(kdtn_ctx* c, const kdtn_strtab& kd, const kdtn_strtab& pd, uint
     c->pd_valid = pk;
     c->kd_from = kk;
     c->pd_from = pk;
+    c->si_k = std::min(c->si_k, kk);
+    c->si_p = std::min(c->si_p, pk);
     TRY(upload_dict(c, c->kd_bytes, c->kd_offs, kd, kk, hs));
     TRY(upload_dict(c, c->pd_bytes, c->pd_offs, pd, pk, hs));
     return prepare_dicts(c);
@@ -803,6 +806,7 @@ int prepare_work(kdtn_ctx* c, uint32_t slice, uint32_t M, uint32_t N) {
     TRY(ensure(c->add_res, h * N * 16));
     TRY(ensure(c->upd_qdisc, h * M * 72));
     TRY(ensure(c->add_qdisc, h * N * 72));
+    TRY(ensure(c->add_qerr, h * N + 16));
     return KDTN_OK;
 }
 
@@ -818,7 +822,12 @@ int run_reach(kdtn_ctx* c, uint32_t* mark, uint32_t stamp) {
     TRY(ensure(c->f_send, (size_t)na + 16));
     TRY(ensure(c->f_reach_upd, (size_t)nu + 16));
     ReachIn r{dp<uint32_t>(c->del_off), dp<uint4>(c->del_res), dp<uint32_t>(c->add_off), dp<uint4>(c->add_res),
-              dp<uint2>(c->add_qdisc), dp<uint32_t>(c->upd_off), dp<uint4>(c->upd_res), c->T, stamp};
+              dp<uint2>(c->add_qdisc), dp<uint32_t>(c->upd_off), dp<uint4>(c->upd_res), c->T, stamp,
+              dp<uint8_t>(c->add_qerr), nullptr};
+    if (mark) {                                     // the fan-out: dense node ids for its passes
+        TRY(ensure(c->f_node, (size_t)na * 4 + 16));
+        r.add_node = dp<uint32_t>(c->f_node);
+    }
     const uint32_t nd = c->h_misc[1];
     TRY(ensure(c->f_cut, (size_t)c->T * 12 + 12));
     TRY(ensure(c->f_st, (size_t)na + 16));
@@ -836,19 +845,52 @@ int run_reach(kdtn_ctx* c, uint32_t* mark, uint32_t stamp) {
     return KDTN_OK;
 }
 
-// The encoders' string tables {offset, length | STR_BAD} of both dictionaries (kd_utf8 /
-// pd_utf8 hold them), on the context stream.
+// The encoders' inline string tables (StrTab) of both dictionaries, on the context stream.
+// Like the dictionary parses, the work is a function of the upload: the strings from the
+// upload's keep index (and any never built) on; the entries before it are kept.
 int str_tables(kdtn_ctx* c) {
     hipStream_t s = c->stream;
-    TRY(ensure(c->kd_utf8, (size_t)c->D * 8 + 16));
-    TRY(ensure(c->pd_utf8, (size_t)c->P * 8 + 16));
-    if (c->D) k_str_table<<<nblocks(c->D), BLOCK, 0, s>>>(dp<uint8_t>(c->kd_bytes), dp<uint32_t>(c->kd_offs), c->D,
-                                                          dp<uint2>(c->kd_utf8));
-    if (c->P) k_str_table<<<nblocks(c->P), BLOCK, 0, s>>>(dp<uint8_t>(c->pd_bytes), dp<uint32_t>(c->pd_offs), c->P,
-                                                          dp<uint2>(c->pd_utf8));
+    const uint32_t k0 = std::min(c->si_k, c->kd_from), p0 = std::min(c->si_p, c->pd_from);
+    TRY(ensure_keep(c->kd_si, (size_t)c->D * SI_KW * 4 + 16, (size_t)k0 * SI_KW * 4, s));
+    TRY(ensure_keep(c->kd_len1, (size_t)c->D + 16, k0, s));
+    TRY(ensure_keep(c->pd_si, (size_t)c->P * SI_PW * 4 + 16, (size_t)p0 * SI_PW * 4, s));
+    TRY(ensure_keep(c->pd_len1, (size_t)c->P + 16, p0, s));
+    if (c->D > k0)
+        k_str_inline<SI_KW><<<nblocks(c->D - k0), BLOCK, 0, s>>>(dp<uint8_t>(c->kd_bytes), dp<uint32_t>(c->kd_offs) + k0,
+                                                                c->D - k0, dp<uint32_t>(c->kd_si) + (size_t)k0 * SI_KW,
+                                                                dp<uint8_t>(c->kd_len1) + k0);
+    if (c->P > p0)
+        k_str_inline<SI_PW><<<nblocks(c->P - p0), BLOCK, 0, s>>>(dp<uint8_t>(c->pd_bytes), dp<uint32_t>(c->pd_offs) + p0,
+                                                                c->P - p0, dp<uint32_t>(c->pd_si) + (size_t)p0 * SI_PW,
+                                                                dp<uint8_t>(c->pd_len1) + p0);
+    HIP_TRY(hipGetLastError());
+    c->si_k = c->D;
+    c->si_p = c->P;
+    return KDTN_OK;
+}
+
+StrTab str_tab_kd(kdtn_ctx* c) {
+    return StrTab{dp<uint32_t>(c->kd_si), dp<uint8_t>(c->kd_len1), dp<uint8_t>(c->kd_bytes)};
+}
+StrTab str_tab_pd(kdtn_ctx* c) {
+    return StrTab{dp<uint32_t>(c->pd_si), dp<uint8_t>(c->pd_len1), dp<uint8_t>(c->pd_bytes)};
+}
+
+// exclusive scan of n u32 values into n+1 u64 offsets (out[n] = total): partial sums, a
+// one-block scan of the partials, the final pass. (A single-pass decoupled look-back over
+// 1024-value blocks measured slower on the output stages: 132 vs 52 us for 10M values, the
+// look-back round trips of ~10k small blocks in the critical path.)
+int scan_u32(kdtn_ctx* c, const uint32_t* in, uint32_t n, uint64_t* out) {
+    const uint32_t nb = nblocks((uint64_t)n + 1, SCAN_CHUNK);
+    TRY(ensure(c->j_part, (size_t)nb * 8));
+    hipStream_t s = c->stream;
+    k_scan_partial<<<nb, BLOCK, 0, s>>>(in, n, dp<uint64_t>(c->j_part));
+    k_scan_top<<<1, SCAN_TOP_BLOCK, 0, s>>>(dp<uint64_t>(c->j_part), nb);
+    k_scan_final<<<nb, BLOCK, 0, s>>>(in, n, dp<uint64_t>(c->j_part), out);
     HIP_TRY(hipGetLastError());
     return KDTN_OK;
 }
+
 
 }  // namespace
 
@@ -930,6 +972,7 @@ int kdtn_init(kdtn_ctx** out, const kdtn_config* cfg) {
         delete c;
         return KDTN_ENOMEM;
     }
+    std::memset(c->h_tot, 0, 64);
     // timing events only (read after a stream sync): no system-scope fence, whose L2 write-back
     // and invalidate at every mark cost the timed epoch stream time
     for (int i = 0; i <= kMaxTimers; ++i) (void)hipEventCreateWithFlags(&c->ev[i], hipEventDisableSystemFence);
@@ -966,10 +1009,10 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->pod_ovf, &c->pod_direct, &c->otarget, &c->sync, &c->misc, &c->hscratch,
                       &c->fscratch, &c->action, &c->del_off, &c->add_off, &c->upd_off, &c->del_idx,
                       &c->add_idx, &c->upd_idx, &c->del_res, &c->add_res, &c->upd_res,
-                      &c->add_qdisc, &c->upd_qdisc, &c->kd_utf8, &c->pd_utf8, &c->w_rel,
+                      &c->add_qdisc, &c->upd_qdisc, &c->add_qerr, &c->kd_si, &c->kd_len1, &c->pd_si, &c->pd_len1, &c->w_rel,
                       &c->w_topo, &c->w_size, &c->w_err, &c->w_off, &c->w_part, &c->w_arena,
                       &c->f_mark, &c->f_send, &c->f_node_idx, &c->f_nodes, &c->f_counts, &c->f_base,
-                      &c->f_part, &c->f_idx, &c->f_inv, &c->f_st, &c->f_reach_upd, &c->tc_size, &c->tc_off, &c->tc_part, &c->tc_arena,
+                      &c->f_part, &c->f_idx, &c->f_inv, &c->f_st, &c->f_node, &c->f_reach_upd, &c->tc_size, &c->tc_off, &c->tc_part, &c->tc_arena,
                       &c->j_doc, &c->j_q, &c->j_bs, &c->j_hb, &c->j_qcnt, &c->j_qoff, &c->j_tok, &c->j_open,
                       &c->j_close, &c->j_gcnt, &c->j_goff, &c->j_toks, &c->j_par,
                       &c->j_role, &c->j_ecls, &c->j_odep, &c->j_ord, &c->j_tagg, &c->j_gagg, &c->j_cnt3, &c->j_coff3, &c->j_small,
@@ -1392,6 +1435,7 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         o.upd_res = dp<uint4>(c->upd_res);
         o.add_qdisc = dp<uint2>(c->add_qdisc);
         o.upd_qdisc = dp<uint2>(c->upd_qdisc);
+        o.add_qerr = dp<uint8_t>(c->add_qerr);
         o.totals = sync + SYNC_TOTALS;
         o.htotals = c->h_tot;
         o.stages = stages;
@@ -1799,7 +1843,7 @@ int kdtn_make_qdiscs(kdtn_ctx* c, const kdtn_strtab* pdict, const kdtn_props_tab
     const uint32_t P = pdict->n, n = props->n;
     for (int k = 0; k < KDTN_NPROP; ++k) TRY(check_ids(props->prop[k], n, P, "props"));
     if (n && !props->gap) return KDTN_EINVAL;
-    c->pd_valid = c->pd_from = 0;                          // this call owns the property tables now
+    c->pd_valid = c->pd_from = c->si_p = 0;                // this call owns the property tables now
     c->ix_p.n = c->ix_p.mask = 0;
     c->uploaded = false;
     TRY(upload_arena(c, c->pd_bytes, pdict->bytes, pdict->offs[P]));
@@ -1857,10 +1901,8 @@ int kdtn_epoch_encode(kdtn_ctx* c, uint64_t* n_bytes) {
     timer_mark(c, "wire_strtab");
     HIP_TRY(hipMemsetAsync(c->w_err.p, 0, err_bytes, s));
     WireIn w{};
-    w.kd_bytes = dp<uint8_t>(c->kd_bytes);
-    w.kd_tab = dp<uint2>(c->kd_utf8);
-    w.pd_bytes = dp<uint8_t>(c->pd_bytes);
-    w.pd_tab = dp<uint2>(c->pd_utf8);
+    w.kd = str_tab_kd(c);
+    w.pd = str_tab_pd(c);
     w.t_name = dp<uint32_t>(c->t_name);
     w.t_src = dp<uint32_t>(c->t_src);
     w.t_netns = dp<uint32_t>(c->t_netns);
@@ -1953,8 +1995,9 @@ int fanout_compute(kdtn_ctx* c) {
     TRY(ensure(c->f_inv, (size_t)na * 4 + 16));
     uint32_t* misc = dp<uint32_t>(c->misc);
     uint32_t* n_nodes = misc + MISC_FAN_NODES;
-    FanIn f{dp<uint32_t>(c->add_off), dp<uint4>(c->add_res), dp<uint2>(c->add_qdisc), c->T, na, c->f_stamp};
     TRY(run_reach(c, dp<uint32_t>(c->f_mark), c->f_stamp));
+    const FanIn f{dp<uint32_t>(c->add_off), dp<uint4>(c->add_res), dp<uint2>(c->add_qdisc), c->T, na, c->f_stamp,
+                  dp<uint32_t>(c->f_node)};            // (after run_reach: it sizes f_node)
     k_fan_nodes_count<<<nbd, BLOCK, 0, s>>>(dp<uint32_t>(c->f_mark), D, c->f_stamp, dp<uint64_t>(c->f_part));
     k_scan_top<<<1, SCAN_TOP_BLOCK, 0, s>>>(dp<uint64_t>(c->f_part), nbd);
     k_fan_nodes_write<<<nbd, BLOCK, 0, s>>>(dp<uint32_t>(c->f_mark), D, c->f_stamp, dp<uint64_t>(c->f_part),
@@ -1976,12 +2019,7 @@ int fanout_compute(kdtn_ctx* c) {
         const size_t lds = (size_t)nn * 4;
         k_fan_count<<<nchunks, 64, lds, s>>>(f, dp<uint8_t>(c->f_send), dp<uint32_t>(c->f_node_idx), n_nodes,
                                            dp<uint32_t>(c->f_counts), nchunks);
-        const uint32_t nbc = nblocks((uint64_t)ncells + 1, SCAN_CHUNK);
-        TRY(ensure(c->w_part, (size_t)nbc * 8 + 16));
-        k_scan_partial<<<nbc, BLOCK, 0, s>>>(dp<uint32_t>(c->f_counts), ncells, dp<uint64_t>(c->w_part));
-        k_scan_top<<<1, SCAN_TOP_BLOCK, 0, s>>>(dp<uint64_t>(c->w_part), nbc);
-        k_scan_final<<<nbc, BLOCK, 0, s>>>(dp<uint32_t>(c->f_counts), ncells, dp<uint64_t>(c->w_part),
-                                           dp<uint64_t>(c->f_base));
+        TRY(scan_u32(c, dp<uint32_t>(c->f_counts), ncells, dp<uint64_t>(c->f_base)));
         k_fan_scatter<<<nchunks, 64, lds, s>>>(f, dp<uint8_t>(c->f_send), dp<uint32_t>(c->f_node_idx), n_nodes,
                                              dp<uint64_t>(c->f_base), nchunks, dp<uint32_t>(c->f_idx),
                                              dp<uint32_t>(c->f_inv));
@@ -2045,16 +2083,12 @@ int kdtn_epoch_remote_encode(kdtn_ctx* c, kdtn_remote_info* info) {
     TRY(fanout_compute(c));                                  // f_idx (fan-out order) and f_send (reach)
     const uint32_t na = c->h_misc[3], nr = c->fan_nsend;
     // physical peers' local Updates: reached PHYSICAL adds whose MakeVeth passed, add-list order
-    const uint32_t nbp = nblocks((uint64_t)na + 1, SCAN_CHUNK);
     TRY(ensure(c->rp_flag, (size_t)na * 4 + 16));
     TRY(ensure(c->rp_pos, ((size_t)na + 1) * 8));
-    TRY(ensure(c->rp_part, (size_t)nbp * 8 + 16));
     TRY(ensure(c->rp_phys, (size_t)na * 4 + 16));
     if (na) k_remote_phys_flags<<<nblocks(na), BLOCK, 0, s>>>(dp<uint8_t>(c->f_send), dp<uint4>(c->add_res), na,
                                                               dp<uint32_t>(c->rp_flag));
-    k_scan_partial<<<nbp, BLOCK, 0, s>>>(dp<uint32_t>(c->rp_flag), na, dp<uint64_t>(c->rp_part));
-    k_scan_top<<<1, SCAN_TOP_BLOCK, 0, s>>>(dp<uint64_t>(c->rp_part), nbp);
-    k_scan_final<<<nbp, BLOCK, 0, s>>>(dp<uint32_t>(c->rp_flag), na, dp<uint64_t>(c->rp_part), dp<uint64_t>(c->rp_pos));
+    TRY(scan_u32(c, dp<uint32_t>(c->rp_flag), na, dp<uint64_t>(c->rp_pos)));
     if (na) k_remote_phys_scatter<<<nblocks(na), BLOCK, 0, s>>>(dp<uint32_t>(c->rp_flag), dp<uint64_t>(c->rp_pos), na,
                                                                 dp<uint32_t>(c->rp_phys));
     uint64_t nphys = 0;
@@ -2067,11 +2101,9 @@ int kdtn_epoch_remote_encode(kdtn_ctx* c, kdtn_remote_info* info) {
     const uint64_t n = (uint64_t)nr + nphys;
     if (n >= 0xFFFFFFFFull) return KDTN_EINVAL;
     RemoteIn r{};
-    r.kd_bytes = dp<uint8_t>(c->kd_bytes);
+    r.kd = str_tab_kd(c);
+    r.pd = str_tab_pd(c);
     r.kd_offs = dp<uint32_t>(c->kd_offs);
-    r.kd_tab = dp<uint2>(c->kd_utf8);
-    r.pd_bytes = dp<uint8_t>(c->pd_bytes);
-    r.pd_tab = dp<uint2>(c->pd_utf8);
     r.t_ns = dp<uint32_t>(c->t_ns);
     r.t_src = dp<uint32_t>(c->t_src);
     r.t_netns = dp<uint32_t>(c->t_netns);
@@ -2091,29 +2123,14 @@ int kdtn_epoch_remote_encode(kdtn_ctx* c, kdtn_remote_info* info) {
     r.n_remote = nr;
     r.T = c->T;
     r.n_add = na;
-    const uint32_t nbm = nblocks(n + 1, SCAN_CHUNK);
     TRY(ensure(c->rp_msz, (size_t)n * 4 + 16));
     TRY(ensure(c->rp_tsz, (size_t)n * 4 + 16));
-    TRY(ensure(c->rp_msz_e, (size_t)na * 4 + 16));
-    TRY(ensure(c->rp_tsz_e, (size_t)na * 4 + 16));
     TRY(ensure(c->rp_moff, (n + 1) * 8));
     TRY(ensure(c->rp_toff, (n + 1) * 8));
-    TRY(ensure(c->rp_part, (size_t)nbm * 8 + 16));
-    TRY(ensure(c->w_part, (size_t)nbm * 8 + 16));
-    if (n) {   // sizes per add entry (coalesced columns), then gathered into message order
-        k_remote_entry_sizes<<<nblocks(na), BLOCK, 0, s>>>(r, dp<uint32_t>(c->rp_msz_e));
-        if (nr) k_tc_remote_entry_sizes<<<nblocks(na), BLOCK, 0, s>>>(r, dp<uint32_t>(c->rp_tsz_e));
-        k_remote_msg_sizes<<<nblocks(n), BLOCK, 0, s>>>(r, dp<uint32_t>(c->rp_msz_e), dp<uint32_t>(c->rp_tsz_e),
-                                                        dp<uint32_t>(c->rp_msz), dp<uint32_t>(c->rp_tsz));
-    }
-    k_scan_partial<<<nbm, BLOCK, 0, s>>>(dp<uint32_t>(c->rp_msz), (uint32_t)n, dp<uint64_t>(c->rp_part));
-    k_scan_top<<<1, SCAN_TOP_BLOCK, 0, s>>>(dp<uint64_t>(c->rp_part), nbm);
-    k_scan_final<<<nbm, BLOCK, 0, s>>>(dp<uint32_t>(c->rp_msz), (uint32_t)n, dp<uint64_t>(c->rp_part),
-                                       dp<uint64_t>(c->rp_moff));
-    k_scan_partial<<<nbm, BLOCK, 0, s>>>(dp<uint32_t>(c->rp_tsz), (uint32_t)n, dp<uint64_t>(c->w_part));
-    k_scan_top<<<1, SCAN_TOP_BLOCK, 0, s>>>(dp<uint64_t>(c->w_part), nbm);
-    k_scan_final<<<nbm, BLOCK, 0, s>>>(dp<uint32_t>(c->rp_tsz), (uint32_t)n, dp<uint64_t>(c->w_part),
-                                       dp<uint64_t>(c->rp_toff));
+    // sizes per add entry (coalesced columns), stored at the message indices
+    if (n) k_remote_sizes<<<nblocks(na), BLOCK, 0, s>>>(r, dp<uint32_t>(c->rp_msz), dp<uint32_t>(c->rp_tsz));
+    TRY(scan_u32(c, dp<uint32_t>(c->rp_msz), (uint32_t)n, dp<uint64_t>(c->rp_moff)));   // message offsets
+    TRY(scan_u32(c, dp<uint32_t>(c->rp_tsz), (uint32_t)n, dp<uint64_t>(c->rp_toff)));   // tc argv offsets
     timer_mark(c, "remote_sizes");
     HIP_TRY(hipGetLastError());
     uint64_t tot[2] = {0, 0};
@@ -2123,12 +2140,11 @@ int kdtn_epoch_remote_encode(kdtn_ctx* c, kdtn_remote_info* info) {
     TRY(ensure(c->rp_arena, (size_t)tot[0] + 16));
     TRY(ensure(c->rp_tc, (size_t)tot[1] + 16));
     timer_mark(c, "remote_host_sync");
-    if (n) {
-        k_remote_write<<<nblocks(na), BLOCK, 0, s>>>(r, dp<uint64_t>(c->rp_moff), dp<uint8_t>(c->rp_arena));
-        timer_mark(c, "remote_write");
-        if (nr) k_tc_remote_write<<<nblocks(na), BLOCK, 0, s>>>(r, dp<uint64_t>(c->rp_toff), dp<uint8_t>(c->rp_tc));
-        timer_mark(c, "remote_tc_write");
-    }
+    if (n)   // the messages, then (UpdateRemote) the receiving daemons' tc argv
+        k_remote_write<<<nblocks(na), BLOCK, 0, s>>>(r, dp<uint64_t>(c->rp_moff), dp<uint8_t>(c->rp_arena),
+                                                     nr ? dp<uint64_t>(c->rp_toff) : nullptr,
+                                                     nr ? dp<uint8_t>(c->rp_tc) : nullptr);
+    timer_mark(c, "remote_write");
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(s));
     c->rp_n = (uint32_t)n;
@@ -2183,16 +2199,13 @@ int kdtn_epoch_tc(kdtn_ctx* c, uint64_t* n_bytes) {
     c->n_ev = 0;
     (void)hipEventRecord(c->ev[0], s);
     TRY(run_reach(c, nullptr, 0));
+    TRY(str_tables(c));                                   // the interface names' entries
     timer_mark(c, "tc_reach");
     TcIn w{c->des.view, dp<uint8_t>(c->f_send), dp<uint8_t>(c->f_reach_upd), dp<uint32_t>(c->add_idx),
            dp<uint32_t>(c->upd_idx), dp<uint4>(c->add_res),
-           dp<uint4>(c->upd_res), dp<uint2>(c->add_qdisc), dp<uint2>(c->upd_qdisc), dp<uint8_t>(c->kd_bytes),
-           dp<uint32_t>(c->kd_offs), na, nu};
+           dp<uint4>(c->upd_res), dp<uint2>(c->add_qdisc), dp<uint2>(c->upd_qdisc), str_tab_kd(c), na, nu};
     if (n) k_tc_sizes<<<nblocks(n), BLOCK, 0, s>>>(w, dp<uint32_t>(c->tc_size));
-    k_scan_partial<<<nb, BLOCK, 0, s>>>(dp<uint32_t>(c->tc_size), (uint32_t)n, dp<uint64_t>(c->tc_part));
-    k_scan_top<<<1, SCAN_TOP_BLOCK, 0, s>>>(dp<uint64_t>(c->tc_part), nb);
-    k_scan_final<<<nb, BLOCK, 0, s>>>(dp<uint32_t>(c->tc_size), (uint32_t)n, dp<uint64_t>(c->tc_part),
-                                      dp<uint64_t>(c->tc_off));
+    TRY(scan_u32(c, dp<uint32_t>(c->tc_size), (uint32_t)n, dp<uint64_t>(c->tc_off)));
     timer_mark(c, "tc_sizes");
     HIP_TRY(hipGetLastError());
     uint64_t total = 0;
@@ -2229,17 +2242,6 @@ int kdtn_epoch_download_tc(kdtn_ctx* c, kdtn_tc_argv* o) {
 // CR ingest: TopologyList JSON → device-resident epoch tables (kdtn_ingest.hip)
 // ======================================================================================
 namespace {
-
-// exclusive scan of n u32 values into n+1 u64 offsets (out[n] = total)
-int scan_u32(kdtn_ctx* c, const uint32_t* in, uint32_t n, uint64_t* out) {
-    const uint32_t nb = nblocks((uint64_t)n + 1, SCAN_CHUNK);
-    TRY(ensure(c->j_part, (size_t)nb * 8));
-    hipStream_t s = c->stream;
-    k_scan_partial<<<nb, BLOCK, 0, s>>>(in, n, dp<uint64_t>(c->j_part));
-    k_scan_top<<<1, SCAN_TOP_BLOCK, 0, s>>>(dp<uint64_t>(c->j_part), nb);
-    k_scan_final<<<nb, BLOCK, 0, s>>>(in, n, dp<uint64_t>(c->j_part), out);
-    return KDTN_OK;
-}
 
 template <typename T>
 int d2h(kdtn_ctx* c, T* host, const void* dev, size_t count = 1) {
@@ -2610,6 +2612,7 @@ static int json_ingest_full(kdtn_ctx* c, const kdtn_vni_table* vnis, kdtn_ingest
     c->uploaded = false;
     c->ran = false;
     c->kd_valid = c->pd_valid = c->kd_from = c->pd_from = 0;   // the document's dictionaries are new
+    c->si_k = c->si_p = 0;
     c->ix_k.n = c->ix_k.mask = c->ix_p.n = c->ix_p.mask = 0;     // (their string indexes too)
     const JsTargets tg{&c->t_ns, &c->t_name, &c->t_src, &c->t_netns, &c->t_flags, &c->t_roff, &c->t_noff,
                        &c->des, &c->real, &c->kd_bytes, &c->kd_offs, &c->pd_bytes, &c->pd_offs};
@@ -3686,7 +3689,7 @@ int kdtn_epoch_upload_delta(kdtn_ctx* c, const kdtn_epoch_delta* d) {
         c->kd_arena = saved_arena[0], c->pd_arena = saved_arena[1];
         c->uploaded = !(err & DERR_KEEP);
         if (err & DERR_KEEP) {                     // the resident strings themselves are suspect
-            c->kd_valid = c->pd_valid = 0;
+            c->kd_valid = c->pd_valid = c->si_k = c->si_p = 0;
             c->ix_k.n = c->ix_k.mask = 0;
             c->ix_p.n = c->ix_p.mask = 0;
         }
@@ -4050,6 +4053,8 @@ int kdtn_json_ingest_delta(kdtn_ctx* c, const uint32_t* deleted, uint32_t n_dele
     c->pd_arena = par1;
     c->kd_valid = c->kd_from = D0;
     c->pd_valid = c->pd_from = P0;
+    c->si_k = std::min(c->si_k, D0);
+    c->si_p = std::min(c->si_p, P0);
     TRY(prepare_dicts(c));
     TRY(check_vnis(c, vn, D1, D0));
     TRY(prepare_vnis(c, vn));

@@ -35,11 +35,12 @@ __global__ void __launch_bounds__(BLOCK) k_reach_cuts(ReachIn f, uint32_t nd, ui
     } else if (x < nd + na) {
         const uint32_t e = x - nd;
         const uint4 r = f.add_res[e];
-        const uint32_t qe = qdisc_err(f.add_qdisc, e);
+        const uint32_t qe = f.add_qerr ? f.add_qerr[e] : qdisc_err(f.add_qdisc, e);
         const bool fails = add_fails(r, qe);
         if (fails || (r.w >> 24))                                            // or remote Update failed
             atomicMin(&cut[3 * entry_topo(f.add_off, f.T, e) + 1], e);
         st_add[e] = (!fails && sends_remote(r, qe)) ? REACH_SEND : 0;        // k_reach reads this byte
+        if (f.add_node) f.add_node[e] = r.z;
     } else if (x < nd + na + nu) {
         const uint32_t e = x - nd - na;
         if ((f.upd_res[e].w >> 8) & 0xFFu) atomicMin(&cut[3 * entry_topo(f.upd_off, f.T, e) + 2], e);   // MakeVeth / MakeQdiscs
@@ -62,7 +63,7 @@ __global__ void __launch_bounds__(BLOCK) k_reach(ReachIn f, uint32_t na, uint32_
                 // a few dozen daemons take millions of stamps: store only a missing one (a
                 // stale read stores again, harmlessly), so the words are not written per entry
                 if (mark) {
-                    const uint32_t node = f.add_res[x].z;
+                    const uint32_t node = f.add_node ? f.add_node[x] : f.add_res[x].z;
                     if (mark[node] != f.stamp) mark[node] = f.stamp;
                 }
             }
@@ -127,7 +128,7 @@ __global__ void __launch_bounds__(64) k_fan_count(FanIn f, const uint8_t* send, 
 #pragma unroll
     for (int r = 0; r < RND; ++r) {
         const uint32_t e = e0 + r * 64 + threadIdx.x;
-        z[r] = (e < e1 && (send[e] & REACH_SEND)) ? f.add_res[e].z : 0xFFFFFFFFu;
+        z[r] = (e < e1 && (send[e] & REACH_SEND)) ? (f.add_node ? f.add_node[e] : f.add_res[e].z) : 0xFFFFFFFFu;
     }
 #pragma unroll
     for (int r = 0; r < RND; ++r)
@@ -160,7 +161,7 @@ __global__ void __launch_bounds__(64) k_fan_scatter(FanIn f, const uint8_t* send
 #pragma unroll
     for (int q = 0; q < RND; ++q) {
         const uint32_t e = e0 + q * 64 + lane;
-        z[q] = (e < e1 && (send[e] & REACH_SEND)) ? f.add_res[e].z : 0xFFFFFFFFu;
+        z[q] = (e < e1 && (send[e] & REACH_SEND)) ? (f.add_node ? f.add_node[e] : f.add_res[e].z) : 0xFFFFFFFFu;
     }
 #pragma unroll
     for (int q = 0; q < RND; ++q)

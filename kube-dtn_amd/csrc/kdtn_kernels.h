@@ -207,6 +207,8 @@ struct RecOut {
     uint4* upd_res;
     uint2* add_qdisc;          // kdtn_qdisc as 9 × 8 B
     uint2* upd_qdisc;
+    uint8_t* add_qerr;         // per add entry its qdisc error byte (kdtn_qdisc byte 70) in a dense array,
+                               // with RESOLVE and QDISC: the reach rule reads it instead of the 72-B records
     uint32_t* totals;          // [3] del, upd, add
     uint32_t* htotals;         // the same [3] in page-locked host memory (no readback copy), or null
     uint32_t stages;
@@ -297,15 +299,23 @@ constexpr int WIRE_IMG = 8192;          // LDS bytes per wave for a wave's wire 
 constexpr int REMOTE_IMG = 10240;       // k_remote_write: 64 RemotePod messages (~124 B each) and their
                                         // slot metadata fit one round (40 KB per block: 4 blocks per
                                         // CU, the occupancy its ~100 VGPRs allow anyway)
-// string table of a dictionary for the encoders: {arena offset, length | STR_BAD} per string,
-// STR_BAD = not valid UTF-8 — one 8-B gather gives everything a string field needs
-constexpr uint32_t STR_BAD = 0x80000000u;
-typedef uint2 SRef;   // {arena offset, length | STR_BAD}
+// Inline string tables of the encoders (per dictionary, k_str_inline): one entry per string,
+// SI_KW dwords per key string, SI_PW per property string. Byte 0 of an entry is the string's
+// length when the string is valid UTF-8 and fits (bytes 1..len hold it, so bytes 0..len are
+// the protobuf length varint and the bytes of a string field); SI_LONG: longer, dword 1 = arena
+// offset, dword 2 = length; SI_BAD: not valid UTF-8 (proto.Marshal fails; no bytes). A string
+// then costs one gather of one line instead of a table entry and its arena bytes. len1: one
+// byte per string, its length when <= 254 and valid, else 255 (read the entry) — the sizing
+// passes' table (12 MB for 12M strings instead of the 96 MB of 8-B entries).
+constexpr int SI_KW = 6, SI_PW = 4;
+constexpr uint32_t SI_LONG = 0x40u, SI_BAD = 0x80u;
+struct StrTab {
+    const uint32_t* inl;            // [n * W] entries
+    const uint8_t* len1;            // [n]
+    const uint8_t* bytes;           // the dictionary arena (long strings)
+};
 struct WireIn {
-    const uint8_t* kd_bytes;
-    const SRef* kd_tab;
-    const uint8_t* pd_bytes;
-    const SRef* pd_tab;
+    StrTab kd, pd;
     const uint32_t* t_name;
     const uint32_t* t_src;
     const uint32_t* t_netns;
@@ -336,8 +346,7 @@ struct TcIn {
     const uint4* upd_res;
     const uint2* add_qdisc;
     const uint2* upd_qdisc;
-    const uint8_t* kd_bytes;
-    const uint32_t* kd_offs;
+    StrTab kd;
     uint32_t n_add, n_upd;
 };
 __global__ void k_tc_sizes(TcIn w, uint32_t* size);
@@ -445,11 +454,8 @@ __global__ void k_ix_refs(uint32_t* ref, uint32_t n);
 // message m: the UpdateRemote payload of add entry rem_idx[m] (m < n_remote, fan-out order) or
 // the physical peer's local Update payload of add entry phys_idx[m - n_remote]
 struct RemoteIn {
-    const uint8_t* kd_bytes;
-    const uint32_t* kd_offs;
-    const SRef* kd_tab;
-    const uint8_t* pd_bytes;
-    const SRef* pd_tab;
+    StrTab kd, pd;
+    const uint32_t* kd_offs;        // physical peers: TrimPrefix(PeerPod, "physical/") from the arena
     const uint32_t* t_ns;
     const uint32_t* t_src;
     const uint32_t* t_netns;
@@ -469,11 +475,8 @@ struct RemoteIn {
 };
 __global__ void k_remote_phys_flags(const uint8_t* reach_add, const uint4* add_res, uint32_t na, uint32_t* flag);
 __global__ void k_remote_phys_scatter(const uint32_t* flag, const uint64_t* pos, uint32_t na, uint32_t* phys_idx);
-__global__ void k_remote_entry_sizes(RemoteIn r, uint32_t* msz_e);
-__global__ void k_remote_msg_sizes(RemoteIn r, const uint32_t* msz_e, const uint32_t* tsz_e, uint32_t* msz, uint32_t* tsz);
-__global__ void k_remote_write(RemoteIn r, const uint64_t* off, uint8_t* arena);
-__global__ void k_tc_remote_entry_sizes(RemoteIn r, uint32_t* tsz_e);
-__global__ void k_tc_remote_write(RemoteIn r, const uint64_t* off, uint8_t* arena);
+__global__ void k_remote_sizes(RemoteIn r, uint32_t* msz, uint32_t* tsz);
+__global__ void k_remote_write(RemoteIn r, const uint64_t* off, uint8_t* arena, const uint64_t* toff, uint8_t* tc);
 
 // ---- RemotePod fan-out grouping (kdtn_fanout.hip) ---------------------------------------
 constexpr int FAN_CHUNK = 1024;        // add entries per single-wave workgroup
@@ -483,6 +486,7 @@ struct FanIn {
     const uint4* add_res;
     const uint2* add_qdisc;
     uint32_t T, n_add, stamp;
+    const uint32_t* add_node;       // ReachIn.add_node (null: add_res.z)
 };
 // murmur3 finalizer (hash tables keyed by packed ids)
 KD_INLINE uint64_t hash64(uint64_t x) {
@@ -539,6 +543,10 @@ struct ReachIn {
     const uint32_t* upd_off;
     const uint4* upd_res;
     uint32_t T, stamp;
+    const uint8_t* add_qerr;        // RecOut.add_qerr (null: the qdisc records' error bytes)
+    uint32_t* add_node;             // k_reach_cuts: add_res.z of every add entry in a dense array
+                                    // (k_reach and the fan-out read 4 B instead of the 16-B
+                                    // records), or null
 };
 __global__ void k_reach_cuts(ReachIn f, uint32_t nd, uint32_t na, uint32_t nu, uint32_t* cut, uint8_t* st_add);
 __global__ void k_reach(ReachIn f, uint32_t na, uint32_t nu, const uint32_t* cut, const uint8_t* st_add, uint32_t* mark,
@@ -604,8 +612,8 @@ KD_INLINE uint64_t block_exclusive(uint64_t v, uint64_t* sh, uint64_t* total) {
     return base + x - v;
 }
 
-__global__ void k_utf8_bits(const uint8_t* bytes, const uint32_t* offs, uint32_t n, uint32_t* bits);
-__global__ void k_str_table(const uint8_t* bytes, const uint32_t* offs, uint32_t n, uint2* tab);
+template <int W>
+__global__ void k_str_inline(const uint8_t* bytes, const uint32_t* offs, uint32_t n, uint32_t* inl, uint8_t* len1);
 __global__ void k_wire_entry_sizes(WireIn w, DevLinks O, DevLinks N, WireWork wk);
 __global__ void k_wire_scan_partial(WireIn w, WireWork wk, uint64_t* part);
 __global__ void k_wire_scan_final(WireIn w, WireWork wk, const uint64_t* part);

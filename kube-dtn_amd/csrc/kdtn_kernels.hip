@@ -1282,6 +1282,7 @@ KD_INLINE void add_finish(const RecCols& c, const AddGath& g, const DevLinks& N,
     store_idx<V>(out.add_idx + e, j);
     const uint4 r = add_calc<V>(c, g, N, j, tc, tb, res, qd, q);
     if (res) store_res<V>(out.add_res + e, r);
+    if (res && qd) out.add_qerr[e] = (uint8_t)(q[17] >> 16);
 }
 
 template <int V>
@@ -2348,6 +2349,7 @@ __global__ void __launch_bounds__(BLOCK) k_place(DevTopos T, const uint32_t* wco
     for (uint32_t k = lane; k < ca; k += 64) {
         store_idx<V>(out.add_idx + ba + k, out.add_idx[sa + k]);
         if (res) store_res<V>(out.add_res + ba + k, out.add_res[sa + k]);
+        if (res && qd) out.add_qerr[ba + k] = out.add_qerr[sa + k];
     }
     if (qd) {
         for (uint32_t k = lane; k < cu * 9; k += 64)

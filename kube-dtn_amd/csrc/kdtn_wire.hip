@@ -13,17 +13,16 @@
 // string is not valid UTF-8, which makes Marshal fail; err[t] bit l marks the latter).
 //
 // Kernels (launch order, kdtn_epoch_encode):
-//   k_utf8_bits      unicode/utf8.ValidString per dictionary string → bitset (1 = invalid)
-//   k_str_table      {offset, length | STR_BAD} per dictionary string (STR_BAD: not valid
-//                    UTF-8, unicode/utf8.ValidString)
+//   k_str_inline     per dictionary string its inline table entry and its length byte
+//                    (StrTab, kdtn_kernels.h; unicode/utf8.ValidString decides SI_BAD)
 //   k_wire_entry_sizes  one thread per entry: its topology and encoded size (its Link, plus
-//                    the LocalPod header for a batch's first entry); a string that is not
-//                    valid UTF-8 fails its batch (err bit)
+//                    the LocalPod header for a batch's first entry) from the length bytes; a
+//                    string that is not valid UTF-8 fails its batch (err bit)
 //   k_wire_scan_*    exclusive scan of the sizes of entries whose batch marshals → u64 arena
 //                    offset of every entry; k_wire_batch_off: batch offsets [3T+1]
-//   k_wire_write     one thread per entry: writes its bytes into the wave's LDS image (dwords
-//                    assembled in registers, WSink), which the wave then stores with
-//                    coalesced dword stores
+//   k_wire_write     one thread per entry: one gather per string field (the inline entry),
+//                    its bytes assembled into the wave's LDS image (dwords built in registers,
+//                    WSink), which the wave then stores with coalesced dword stores
 #include "kdtn_encode.h"
 
 namespace kdtn {
@@ -55,33 +54,16 @@ KD_INLINE bool utf8_ok(const uint8_t* s, uint32_t n) {
     return true;
 }
 
-__global__ void __launch_bounds__(BLOCK) k_utf8_bits(const uint8_t* bytes, const uint32_t* offs,
-                                                     uint32_t n, uint32_t* bits) {
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    bool bad = false;
-    if (i < n) {
-        const uint32_t b = offs[i], len = offs[i + 1] - b;
-        bool ascii = true;
-        for (uint32_t k = 0; k < len && ascii; ++k) ascii = bytes[b + k] < 0x80u;
-        if (!ascii) bad = !utf8_ok(bytes + b, len);
-    }
-    const uint64_t m = __ballot(bad);
-    const int lane = threadIdx.x & 63;
-    if (lane == 0 || lane == 32) bits[((i - lane) >> 5) + (lane >> 5)] = lane ? (uint32_t)(m >> 32) : (uint32_t)m;
-}
-
-// {offset, length | STR_BAD} per dictionary string (the encoders' one gather per string field).
-// The high-bit test reads the string's first 32 bytes as one 16-B load pair (+ a dword)
-// instead of byte by byte; only strings with a byte >= 0x80 run the UTF-8 automaton. (16-B
-// entries holding strings of <= 12 bytes inline measured slower: wire_write 1.83 vs 1.77 ms,
-// sizes 0.72 vs 0.63 ms — the table doubles and the writer loses a wave per SIMD,
-// profiles/r03k_stages.json.)
-__global__ void __launch_bounds__(BLOCK) k_str_table(const uint8_t* bytes, const uint32_t* offs, uint32_t n,
-                                                     uint2* tab) {
+// One thread per dictionary string: its inline entry (W dwords; StrTab) and its length byte.
+// The string's first 32 bytes come from one 16-B load pair (+ a dword); only strings with a
+// byte >= 0x80 run the UTF-8 automaton. Bytes of an inline entry past the string are zero.
+template <int W>
+__global__ void __launch_bounds__(BLOCK) k_str_inline(const uint8_t* bytes, const uint32_t* offs, uint32_t n,
+                                                      uint32_t* inl, uint8_t* len1) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n) return;
     const uint32_t b = offs[i], len = offs[i + 1] - b;
-    uint32_t hi = 0;
+    uint32_t hi = 0, s[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};   // the string's dwords, zero past len
     if (len) {
         typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
         const uint32_t* a32 = reinterpret_cast<const uint32_t*>(bytes) + (b >> 2);
@@ -95,15 +77,37 @@ __global__ void __launch_bounds__(BLOCK) k_str_table(const uint8_t* bytes, const
         for (uint32_t q = 0; q < 8; ++q) {
             if (4u * q < len) {
                 const uint32_t r = len - 4u * q;
-                const uint32_t m = r >= 4u ? 0x80808080u : (0x80808080u & ((1u << (8u * r)) - 1u));
-                hi |= __builtin_amdgcn_alignbyte(w[q + 1], w[q], sh) & m;
+                const uint32_t m = r >= 4u ? 0xFFFFFFFFu : ((1u << (8u * r)) - 1u);
+                s[q] = __builtin_amdgcn_alignbyte(w[q + 1], w[q], sh) & m;
+                hi |= s[q] & 0x80808080u;
             }
         }
         for (uint32_t k = 32; k < len; ++k) hi |= bytes[b + k] & 0x80u;
     }
     const bool bad = hi != 0 && !utf8_ok(bytes + b, len);
-    tab[i] = make_uint2(b, len | (bad ? STR_BAD : 0u));
+    uint32_t e[W];
+    if (!bad && len <= 4u * W - 1u) {                      // inline: byte 0 = len, bytes 1..len
+        e[0] = len | (s[0] << 8);
+#pragma unroll
+        for (int q = 1; q < W; ++q) e[q] = (s[q - 1] >> 24) | (s[q] << 8);
+    } else {                                               // long or not valid UTF-8: the range
+#pragma unroll
+        for (int q = 0; q < W; ++q) e[q] = 0u;
+        e[0] = SI_LONG | (bad ? SI_BAD : 0u);
+        e[1] = b;
+        e[2] = len;
+    }
+    uint32_t* o = inl + (size_t)i * W;
+    if constexpr (W == 4) {
+        *reinterpret_cast<uint4*>(o) = make_uint4(e[0], e[1], e[2], e[3]);
+    } else {
+#pragma unroll
+        for (int q = 0; q < W; q += 2) *reinterpret_cast<uint2*>(o + q) = make_uint2(e[q], e[q + 1]);
+    }
+    len1[i] = (uint8_t)((!bad && len <= 254u) ? len : 255u);
 }
+template __global__ void k_str_inline<SI_KW>(const uint8_t*, const uint32_t*, uint32_t, uint32_t*, uint8_t*);
+template __global__ void k_str_inline<SI_PW>(const uint8_t*, const uint32_t*, uint32_t, uint32_t*, uint8_t*);
 
 // ---- sizes ---------------------------------------------------------------------------------
 KD_INLINE uint32_t vlen(uint64_t v) {
@@ -112,64 +116,37 @@ KD_INLINE uint32_t vlen(uint64_t v) {
     return n;
 }
 KD_INLINE uint32_t str_field(uint32_t len) { return len ? 1u + vlen(len) + len : 0u; }
-KD_INLINE bool bit(const uint32_t* bits, uint32_t id) { return (bits[id >> 5] >> (id & 31)) & 1u; }
-KD_INLINE uint32_t slen(SRef r) { return r.y & ~STR_BAD; }
-// string-table entry of id (id 0 = "": no gather); FULL = false: the length word only (sizes)
-template <bool FULL = true>
-KD_INLINE SRef sref(const SRef* tab, uint32_t id) {
-    if (!id) return make_uint2(0u, 0u);
-    if constexpr (FULL) return tab[id];
-    else return make_uint2(0u, reinterpret_cast<const uint32_t*>(tab)[2 * (size_t)id + 1]);
-}
 
-// the table entries of one Link record's 7 key and 12 property strings, gathered at once
-struct LinkRefs {
-    SRef k[KDTN_NKEY], p[KDTN_NPROP];
-    uint32_t gap;
-    int64_t uid;
-};
-template <bool FULL = true>
-KD_INLINE LinkRefs link_refs(const SRef* kd_tab, const SRef* pd_tab, const DevLinks& L, uint32_t j) {
-    LinkRefs r;
+// pb.LinkProperties size (psz) and pb.Link size (lsz) of record j from the length bytes; false
+// if a string is not valid UTF-8
+KD_INLINE bool link_sizes(const WireIn& w, const DevLinks& L, uint32_t j, uint32_t* psz, uint32_t* lsz) {
+    uint32_t kid[KDTN_NKEY], pid[KDTN_NPROP];
 #pragma unroll
-    for (int k = 0; k < KDTN_NKEY; ++k) r.k[k] = sref<FULL>(kd_tab, L.key(k, j));
+    for (int k = 0; k < KDTN_NKEY; ++k) kid[k] = L.key(k, j);
 #pragma unroll
-    for (int k = 0; k < KDTN_NPROP; ++k) r.p[k] = sref<FULL>(pd_tab, L.prop(k, j));
-    r.gap = L.gap(j);
-    r.uid = L.uid(j);
-    return r;
-}
-// pb.LinkProperties size (psz) and pb.Link size (lsz); false if a string is invalid UTF-8
-KD_INLINE bool link_sizes(const LinkRefs& r, uint32_t* psz, uint32_t* lsz) {
+    for (int k = 0; k < KDTN_NPROP; ++k) pid[k] = L.prop(k, j);
+    const uint32_t gap = L.gap(j);
+    const int64_t uid = L.uid(j);
     uint32_t bad = 0, p = 0, l = 0;
 #pragma unroll
-    for (int k = 0; k < KDTN_NPROP; ++k) {
-        p += str_field(slen(r.p[k]));
-        bad |= r.p[k].y;
-    }
-    if (r.gap) p += 1u + vlen(r.gap);
+    for (int k = 0; k < KDTN_NPROP; ++k) p += str_field(si_len<SI_PW>(w.pd, pid[k], bad));
+    if (gap) p += 1u + vlen(gap);
 #pragma unroll
-    for (int k = 0; k < KDTN_NKEY; ++k) {
-        l += str_field(slen(r.k[k]));
-        bad |= r.k[k].y;
-    }
-    if (r.uid) l += 1u + vlen((uint64_t)r.uid);
+    for (int k = 0; k < KDTN_NKEY; ++k) l += str_field(si_len<SI_KW>(w.kd, kid[k], bad));
+    if (uid) l += 1u + vlen((uint64_t)uid);
     l += 1u + vlen(p) + p;
     *psz = p;
     *lsz = l;
-    return (bad & STR_BAD) == 0;
+    return bad == 0;
 }
 
+// pb.Pod LocalPod of topology t: {Name, SrcIp, NetNs, KubeNs}
 KD_INLINE uint32_t pod_size(const WireIn& w, uint32_t t, bool* ok) {
     const uint32_t ids[4] = {w.t_name[t], w.t_src[t], w.t_netns[t], w.t_ns[t]};
     uint32_t s = 0, bad = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const SRef r = sref<false>(w.kd_tab, ids[k]);
-        s += str_field(slen(r));
-        bad |= r.y;
-    }
-    *ok = (bad & STR_BAD) == 0;
+    for (int k = 0; k < 4; ++k) s += str_field(si_len<SI_KW>(w.kd, ids[k], bad));
+    *ok = bad == 0;
     return s;
 }
 
@@ -196,7 +173,7 @@ __global__ void __launch_bounds__(BLOCK) k_wire_entry_sizes(WireIn w, DevLinks O
         }
     if (!on) return;
     uint32_t psz, lsz;
-    bool ok = link_sizes(link_refs<false>(w.kd_tab, w.pd_tab, lst == 0 ? O : N, w.list_idx[lst][e]), &psz, &lsz);
+    bool ok = link_sizes(w, lst == 0 ? O : N, w.list_idx[lst][e], &psz, &lsz);
     uint32_t size = 1u + vlen(lsz) + lsz;
     if (e == w.list_off[lst][t]) {                         // the batch's first entry carries the header
         bool pok;
@@ -334,64 +311,70 @@ __global__ void __launch_bounds__(BLOCK) k_scan_final(const uint32_t* size, uint
 }
 
 // ---- writer --------------------------------------------------------------------------------
-// string field: tag, length, bytes
-KD_INLINE void str_field_out(WSink& o, uint32_t field, const uint8_t* arena, SRef r) {
-    const uint32_t len = slen(r);
-    if (!len) return;
-    if (len < 0x80u) {
-        o.put((field << 3 | 2u) | (len << 8), 2u);
-    } else {
-        o.byte(field << 3 | 2u);
-        o.varint(len);
-    }
-    o.str(arena, r.x, len);
-}
-
-// one entry's bytes from its gathered string ranges r (and sizes psz / lsz)
-KD_INLINE void write_entry_refs(WSink& o, const WireIn& w, const LinkRefs& r, uint32_t psz, uint32_t lsz, bool header,
-                                uint32_t t) {
+// One entry's bytes: the key strings' inline entries and the property strings' length bytes
+// gathered at once (the sizes come from them), then the fields in number order, the property
+// entries gathered after the key fields are written (registers: 7 key entries + 12 property
+// entries held together cost the writer a wave per SIMD).
+KD_INLINE void write_entry(WSink& o, const WireIn& w, const DevLinks& L, uint32_t j, bool header, uint32_t t) {
+    SIE<SI_KW> k[KDTN_NKEY];
+#pragma unroll
+    for (int q = 0; q < KDTN_NKEY; ++q) k[q] = si_load<SI_KW>(w.kd, L.key(q, j));
+    uint32_t pid[KDTN_NPROP];
+#pragma unroll
+    for (int q = 0; q < KDTN_NPROP; ++q) pid[q] = L.prop(q, j);
+    const uint32_t gap = L.gap(j);
+    const int64_t uid = L.uid(j);
+    uint32_t psz = 0, lsz = 0, bad = 0;
+#pragma unroll
+    for (int q = 0; q < KDTN_NPROP; ++q) psz += str_field(si_len<SI_PW>(w.pd, pid[q], bad));
+    if (gap) psz += 1u + vlen(gap);
+#pragma unroll
+    for (int q = 0; q < KDTN_NKEY; ++q) lsz += str_field(si_elen(k[q]));
+    if (uid) lsz += 1u + vlen((uint64_t)uid);
+    lsz += 1u + vlen(psz) + psz;
     if (header) {                                         // LinksBatchQuery.local_pod
-        bool ok;
+        const uint32_t ids[4] = {w.t_name[t], w.t_src[t], w.t_netns[t], w.t_ns[t]};
+        SIE<SI_KW> h[4];
+        uint32_t hs = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            h[q] = si_load<SI_KW>(w.kd, ids[q]);
+            hs += str_field(si_elen(h[q]));
+        }
         o.byte(1u << 3 | 2u);
-        o.varint(pod_size(w, t, &ok));
-        str_field_out(o, 1, w.kd_bytes, sref(w.kd_tab, w.t_name[t]));
-        str_field_out(o, 2, w.kd_bytes, sref(w.kd_tab, w.t_src[t]));
-        str_field_out(o, 3, w.kd_bytes, sref(w.kd_tab, w.t_netns[t]));
-        str_field_out(o, 4, w.kd_bytes, sref(w.kd_tab, w.t_ns[t]));
+        o.varint(hs);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) si_field(o, (uint32_t)q + 1u, h[q], w.kd.bytes);
     }
     o.byte(2u << 3 | 2u);                                 // LinksBatchQuery.links
     o.varint(lsz);
     // pb.Link fields in number order: peer_pod 1, local_intf 2, peer_intf 3, local_ip 4,
     // peer_ip 5, uid 6, properties 7, local_mac 8, peer_mac 9
-    str_field_out(o, 1, w.kd_bytes, r.k[KDTN_K_PEER_POD]);
-    str_field_out(o, 2, w.kd_bytes, r.k[KDTN_K_LOCAL_INTF]);
-    str_field_out(o, 3, w.kd_bytes, r.k[KDTN_K_PEER_INTF]);
-    str_field_out(o, 4, w.kd_bytes, r.k[KDTN_K_LOCAL_IP]);
-    str_field_out(o, 5, w.kd_bytes, r.k[KDTN_K_PEER_IP]);
-    if (r.uid) {
+    si_field(o, 1, k[KDTN_K_PEER_POD], w.kd.bytes);
+    si_field(o, 2, k[KDTN_K_LOCAL_INTF], w.kd.bytes);
+    si_field(o, 3, k[KDTN_K_PEER_INTF], w.kd.bytes);
+    si_field(o, 4, k[KDTN_K_LOCAL_IP], w.kd.bytes);
+    si_field(o, 5, k[KDTN_K_PEER_IP], w.kd.bytes);
+    if (uid) {
         o.byte(6u << 3);
-        o.varint((uint64_t)r.uid);
+        o.varint((uint64_t)uid);
     }
     o.byte(7u << 3 | 2u);
     o.varint(psz);
+    SIE<SI_PW> p[KDTN_NPROP];
+#pragma unroll
+    for (int q = 0; q < KDTN_NPROP; ++q) p[q] = si_load<SI_PW>(w.pd, pid[q]);
     // pb.LinkProperties: latency 1 .. rate 6, gap 7, duplicate 8 .. corrupt_corr 13 (KDTN_P_* order)
 #pragma unroll
-    for (int k = 0; k < KDTN_NPROP; ++k) {
-        if (k == KDTN_P_DUPLICATE && r.gap) {
+    for (int q = 0; q < KDTN_NPROP; ++q) {
+        if (q == KDTN_P_DUPLICATE && gap) {
             o.byte(7u << 3);
-            o.varint(r.gap);
+            o.varint(gap);
         }
-        str_field_out(o, (uint32_t)(k < KDTN_P_DUPLICATE ? k + 1 : k + 2), w.pd_bytes, r.p[k]);
+        si_field(o, (uint32_t)(q < KDTN_P_DUPLICATE ? q + 1 : q + 2), p[q], w.pd.bytes);
     }
-    str_field_out(o, 8, w.kd_bytes, r.k[KDTN_K_LOCAL_MAC]);
-    str_field_out(o, 9, w.kd_bytes, r.k[KDTN_K_PEER_MAC]);
-}
-
-KD_INLINE void write_entry(WSink& o, const WireIn& w, const DevLinks& L, uint32_t j, bool header, uint32_t t) {
-    const LinkRefs r = link_refs(w.kd_tab, w.pd_tab, L, j);   // every string's range: one round trip
-    uint32_t psz, lsz;
-    link_sizes(r, &psz, &lsz);
-    write_entry_refs(o, w, r, psz, lsz, header, t);
+    si_field(o, 8, k[KDTN_K_LOCAL_MAC], w.kd.bytes);
+    si_field(o, 9, k[KDTN_K_PEER_MAC], w.kd.bytes);
 }
 
 // One thread per entry of the three lists (global entry index g). Consecutive entries
@@ -440,138 +423,194 @@ __global__ void __launch_bounds__(BLOCK) k_remote_phys_scatter(const uint32_t* f
     if (e < na && flag[e]) phys_idx[pos[e]] = e;
 }
 
-// the strings of message m as arena ranges, in field order net_ns, intf_name, intf_ip,
-// peer_vtep, kube_ns, name, and the link's properties
+// the string ids of add entry e's message (remote: the UpdateRemote payload, else the physical
+// peer's local Update payload; t = the entry's topology) in field order net_ns, intf_name,
+// intf_ip, peer_vtep, kube_ns, name, and the link's property ids
 struct RemoteMsg {
-    SRef s[6], p[KDTN_NPROP];
+    uint32_t s[6], p[KDTN_NPROP];
     uint32_t gap;
     int32_t vni;
-    bool ok;                        // every string valid UTF-8
+    bool phys;                      // peer_vtep = TrimPrefix(PeerPod, "physical/")
 };
 
-// the strings of add entry e's message (remote: the UpdateRemote payload, else the physical
-// peer's local Update payload); t = the entry's topology
-template <bool FULL = true>
 KD_INLINE RemoteMsg remote_msg(const RemoteIn& r, uint32_t e, uint32_t t, bool remote) {
     RemoteMsg q;
     const uint32_t j = r.add_idx[e];
     const uint4 res = r.add_res[e];
     const uint32_t peer_pod = r.N.key(KDTN_K_PEER_POD, j);
-    uint32_t id[6];
     if (remote) {                                   // UpdateRemote: the peer daemon's side
-        id[0] = r.pods[res.x].w & 0x7FFFFFFFu;      // peerPod.NetNs
-        id[1] = r.N.key(KDTN_K_PEER_INTF, j);
-        id[2] = r.N.key(KDTN_K_PEER_IP, j);
-        id[3] = r.t_src[t];                         // localPod.SrcIp
+        q.s[0] = r.pods[res.x].w & 0x7FFFFFFFu;     // peerPod.NetNs
+        q.s[1] = r.N.key(KDTN_K_PEER_INTF, j);
+        q.s[2] = r.N.key(KDTN_K_PEER_IP, j);
+        q.s[3] = r.t_src[t];                        // localPod.SrcIp
     } else {                                        // physical: the local pod's side
-        id[0] = r.t_netns[t];
-        id[1] = r.N.key(KDTN_K_LOCAL_INTF, j);
-        id[2] = r.N.key(KDTN_K_LOCAL_IP, j);
-        id[3] = peer_pod;                           // TrimPrefix(PeerPod, "physical/") below
+        q.s[0] = r.t_netns[t];
+        q.s[1] = r.N.key(KDTN_K_LOCAL_INTF, j);
+        q.s[2] = r.N.key(KDTN_K_LOCAL_IP, j);
+        q.s[3] = peer_pod;                          // TrimPrefix(PeerPod, "physical/")
     }
-    id[4] = r.t_ns[t];                              // localPod.KubeNs
-    id[5] = peer_pod;
-    uint32_t bad = 0;
+    q.s[4] = r.t_ns[t];                             // localPod.KubeNs
+    q.s[5] = peer_pod;
 #pragma unroll
-    for (int k = 0; k < 6; ++k) {
-        q.s[k] = sref<FULL>(r.kd_tab, id[k]);
-        bad |= q.s[k].y;
-    }
-#pragma unroll
-    for (int k = 0; k < KDTN_NPROP; ++k) {
-        q.p[k] = sref<FULL>(r.pd_tab, r.N.prop(k, j));
-        bad |= q.p[k].y;
-    }
-    if (!remote) {                                  // TrimPrefix(PeerPod, "physical/")
-        q.s[3].x += 9u;
-        q.s[3].y -= 9u;
-    }
+    for (int k = 0; k < KDTN_NPROP; ++k) q.p[k] = r.N.prop(k, j);
     q.gap = r.N.gap(j);
     q.vni = (int32_t)res.y;
-    q.ok = (bad & STR_BAD) == 0;
+    q.phys = !remote;
     return q;
 }
 
-KD_INLINE uint32_t remote_body_size(const RemoteMsg& q, uint32_t* psz) {
-    uint32_t n = 0, p = 0;
+// message body size from the string lengths (the trimmed peer_vtep of a physical message is 9
+// bytes shorter; "physical/" is ASCII, so it is valid UTF-8 iff the whole name is); false if a
+// string is not valid UTF-8 (Marshal fails)
+KD_INLINE bool remote_sizes(const RemoteIn& r, const RemoteMsg& q, uint32_t* body, uint32_t* psz) {
+    uint32_t n = 0, p = 0, bad = 0;
 #pragma unroll
-    for (int k = 0; k < 6; ++k) n += str_field(slen(q.s[k]));
+    for (int k = 0; k < 6; ++k) {
+        uint32_t l = si_len<SI_KW>(r.kd, q.s[k], bad);
+        if (k == 3 && q.phys) l -= 9u;
+        n += str_field(l);
+    }
     if (q.vni) n += 1u + vlen((uint64_t)(int64_t)q.vni);
 #pragma unroll
-    for (int k = 0; k < KDTN_NPROP; ++k) p += str_field(slen(q.p[k]));
+    for (int k = 0; k < KDTN_NPROP; ++k) p += str_field(si_len<SI_PW>(r.pd, q.p[k], bad));
     if (q.gap) p += 1u + vlen(q.gap);
     *psz = p;
-    return n + 1u + vlen(p) + p;
+    *body = n + 1u + vlen(p) + p;
+    return bad == 0;
 }
 
-// One thread per add entry (add-list order: the entry's columns are read coalesced): the
-// size of its message, if it has one (0 when a string is not valid UTF-8).
-__global__ void __launch_bounds__(BLOCK) k_remote_entry_sizes(RemoteIn r, uint32_t* msz_e) {
+// The receiving daemon's TBF command for RemotePod message m (m < n_remote): the peer
+// daemon's Update runs SetupVxLan on link.PeerIntf → MakeQdiscs (the same properties, which
+// built on the sending side) → SetVethQdiscs (daemon/vxlan/vxlan.go:31-51), unless its
+// CreateOrUpdate rejects IntfIp (kdtn_resolved.remote_err). Physical messages have none here
+// (their tc runs on LocalIntf: kdtn_epoch_tc slot 2e).
+KD_INLINE TcEntry tc_remote_entry(const RemoteIn& r, uint32_t e) {
+    TcEntry t{0, 0, 0, 0, false};
+    if (!(r.send[e] & REACH_SEND)) return t;
+    const uint2* q = r.add_qdisc + (size_t)e * 9;
+    const uint32_t flags = q[8].y;
+    if (((flags >> 8) & 0xFFu) == 0 || (r.add_res[e].w >> 24) != 0) return t;
+    t.intf = r.N.key(KDTN_K_PEER_INTF, r.add_idx[e]);
+    t.buffer = q[6].y;
+    t.rate = ((uint64_t)q[7].y << 32) | q[7].x;
+    t.minburst = q[8].x;
+    t.on = true;
+    return t;
+}
+
+// One thread per add entry (add-list order: the entry's columns are read coalesced): the size
+// of its message, if it has one (0 when a string is not valid UTF-8), and for an UpdateRemote
+// the receiving daemon's tc argv size, both stored at the message's index (every message has
+// exactly one entry, so the arrays need no clearing)
+__global__ void __launch_bounds__(BLOCK) k_remote_sizes(RemoteIn r, uint32_t* msz, uint32_t* tsz) {
     const uint32_t e = blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t kind = e < r.n_add ? remote_kind(r, e) : 0u;
     if (__ballot(kind != 0) == 0) return;           // wave-uniform
     const uint32_t t = entry_topo_wave(r.add_off, r.T, e, kind != 0);
     if (!kind) return;
-    const RemoteMsg q = remote_msg<false>(r, e, t, kind == 1);
-    uint32_t psz;
-    const uint32_t body = remote_body_size(q, &psz);
-    msz_e[e] = q.ok ? vlen(body) + body : 0u;
+    const RemoteMsg q = remote_msg(r, e, t, kind == 1);
+    uint32_t body, psz;
+    const bool ok = remote_sizes(r, q, &body, &psz);
+    const uint32_t m = remote_msg_index(r, e, kind);
+    msz[m] = ok ? vlen(body) + body : 0u;
+    tsz[m] = kind == 1 ? tc_size(r.kd, tc_remote_entry(r, e)) : 0u;
 }
 
-// message m's size from its add entry's (one gather per message, fan-out order)
-__global__ void __launch_bounds__(BLOCK) k_remote_msg_sizes(RemoteIn r, const uint32_t* msz_e, const uint32_t* tsz_e,
-                                                            uint32_t* msz, uint32_t* tsz) {
-    const uint32_t m = blockIdx.x * BLOCK + threadIdx.x;
-    if (m >= r.n_msgs) return;
-    const bool remote = m < r.n_remote;
-    const uint32_t e = remote ? r.rem_idx[m] : r.phys_idx[m - r.n_remote];
-    msz[m] = msz_e[e];
-    tsz[m] = remote ? tsz_e[e] : 0u;
+// a string field from arena bytes [b, b + len) (nothing for "")
+KD_INLINE void arena_field(WSink& o, uint32_t field, const uint8_t* arena, uint32_t b, uint32_t len) {
+    if (!len) return;
+    if (len < 0x80u) {
+        o.put((field << 3 | 2u) | (len << 8), 2u);
+    } else {
+        o.byte(field << 3 | 2u);
+        o.varint(len);
+    }
+    o.str(arena, b, len);
 }
 
+// the message's bytes: the key strings' entries and the property strings' length bytes
+// gathered at once, then the fields in number order (the property entries gathered after the
+// key fields are written, as in write_entry)
 KD_INLINE void write_remote(WSink& o, const RemoteIn& r, const RemoteMsg& q) {
-    uint32_t psz;
-    o.varint(remote_body_size(q, &psz));
+    SIE<SI_KW> s[6];
 #pragma unroll
-    for (int k = 0; k < 5; ++k) str_field_out(o, (uint32_t)k + 1, r.kd_bytes, q.s[k]);
+    for (int k = 0; k < 6; ++k) s[k] = si_load<SI_KW>(r.kd, (k == 3 && q.phys) ? 0u : q.s[k]);
+    uint32_t vb = 0, vl = 0;                        // physical: the trimmed name's arena range
+    if (q.phys) {
+        vb = r.kd_offs[q.s[3]] + 9u;
+        vl = r.kd_offs[q.s[3] + 1] - vb;
+    }
+    uint32_t n = 0, psz = 0, bad = 0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) n += str_field(k == 3 && q.phys ? vl : si_elen(s[k]));
+    if (q.vni) n += 1u + vlen((uint64_t)(int64_t)q.vni);
+#pragma unroll
+    for (int k = 0; k < KDTN_NPROP; ++k) psz += str_field(si_len<SI_PW>(r.pd, q.p[k], bad));
+    if (q.gap) psz += 1u + vlen(q.gap);
+    o.varint(n + 1u + vlen(psz) + psz);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        if (k == 3 && q.phys) arena_field(o, 4u, r.kd.bytes, vb, vl);
+        else si_field(o, (uint32_t)k + 1, s[k], r.kd.bytes);
+    }
     if (q.vni) {
         o.byte(6u << 3);
         o.varint((uint64_t)(int64_t)q.vni);
     }
     o.byte(7u << 3 | 2u);
     o.varint(psz);
+    SIE<SI_PW> p[KDTN_NPROP];
+#pragma unroll
+    for (int k = 0; k < KDTN_NPROP; ++k) p[k] = si_load<SI_PW>(r.pd, q.p[k]);
 #pragma unroll
     for (int k = 0; k < KDTN_NPROP; ++k) {
         if (k == KDTN_P_DUPLICATE && q.gap) {
             o.byte(7u << 3);
             o.varint(q.gap);
         }
-        str_field_out(o, (uint32_t)(k < KDTN_P_DUPLICATE ? k + 1 : k + 2), r.pd_bytes, q.p[k]);
+        si_field(o, (uint32_t)(k < KDTN_P_DUPLICATE ? k + 1 : k + 2), p[k], r.pd.bytes);
     }
-    str_field_out(o, 8, r.kd_bytes, q.s[5]);
+    si_field(o, 8, s[5], r.kd.bytes);
 }
 
 // One thread per add entry with a message, in add-list order (its columns read coalesced),
-// writing the message at its fan-out position. A wave's messages for one daemon are one
-// contiguous run of the arena (fan-out order keeps add-list order within a daemon), so the
-// wave stores them through its LDS image dword by dword (wave_segments_write).
-__global__ void __launch_bounds__(BLOCK) k_remote_write(RemoteIn r, const uint64_t* off, uint8_t* arena) {
+// writing the message at its fan-out position and, for an UpdateRemote, the receiving daemon's
+// tc argv at the same index of the tc arena. A wave's messages for one daemon are one contiguous
+// run of each arena (fan-out order keeps add-list order within a daemon), so the wave stores
+// them through its LDS image dword by dword (wave_segments_write), the messages first, then the
+// argv.
+__global__ void __launch_bounds__(BLOCK) k_remote_write(RemoteIn r, const uint64_t* off, uint8_t* arena,
+                                                        const uint64_t* toff, uint8_t* tc) {
     __shared__ uint32_t img[BLOCK / 64][REMOTE_IMG / 4];
     const uint32_t e = blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t kind = e < r.n_add ? remote_kind(r, e) : 0u;
     if (__ballot(kind != 0) == 0) return;           // wave-uniform
     const uint32_t t = entry_topo_wave(r.add_off, r.T, e, kind != 0);
+    uint32_t m = 0;
     uint64_t s0 = 0, s1 = 0;
     if (kind) {
-        const uint32_t m = remote_msg_index(r, e, kind);
+        m = remote_msg_index(r, e, kind);
         s0 = off[m];
         s1 = off[m + 1];
     }
     const bool on = s1 > s0;                        // empty: no message or a Marshal error
-    RemoteMsg q{};
-    if (on) q = remote_msg(r, e, t, kind == 1);
-    wave_segments_write<REMOTE_IMG>(img[threadIdx.x >> 6], on, s0, s1, arena,
-                                    [&](WSink& o) __attribute__((always_inline)) { write_remote(o, r, q); });
+    {
+        RemoteMsg q{};
+        if (on) q = remote_msg(r, e, t, kind == 1);
+        wave_segments_write<REMOTE_IMG>(img[threadIdx.x >> 6], on, s0, s1, arena,
+                                        [&](WSink& o) __attribute__((always_inline)) { write_remote(o, r, q); });
+    }
+    if (!tc) return;
+    uint64_t c0 = 0, c1 = 0;
+    if (kind == 1) {
+        c0 = toff[m];
+        c1 = toff[m + 1];
+    }
+    if (__ballot(c1 > c0) == 0) return;             // wave-uniform
+    TcEntry te{0, 0, 0, 0, false};
+    if (c1 > c0) te = tc_remote_entry(r, e);
+    wave_segments_write<REMOTE_IMG>(img[threadIdx.x >> 6], c1 > c0, c0, c1, tc,
+                                    [&](WSink& o) __attribute__((always_inline)) { write_tbf_argv(o, r.kd, te); });
 }
 
 }  // namespace kdtn

@@ -32,6 +32,25 @@ def _run_same(eng, expect, ctx):
     return ora
 
 
+def _outputs_same(eng, expect, ctx):
+    """The output stages on the resident state (the encoders' string tables built only for the
+    strings the delta appended) equal the oracle's on the tables the state should hold."""
+    out = eng.download()
+    ora = O.reconcile(expect, tick=TICK)
+    n = eng.encode()
+    arena, off, err = eng.download_wire()
+    want_a, want_off, want_err = O.encode_epoch(expect, out)
+    assert n == len(want_a) and np.array_equal(off, want_off), ctx
+    assert np.array_equal(err, want_err.astype(np.uint32)) and arena.tobytes() == want_a.tobytes(), ctx
+    got = eng.remote_pods()
+    want = O.remote_epoch(expect, ora)
+    for name, g, w in zip(("arena", "off", "entry", "n_remote", "tc", "tc_off"), got, want):
+        assert np.array_equal(np.asarray(g), np.asarray(w)), (ctx, name)
+    ta, to = eng.tc_argv(len(out.add_idx), len(out.upd_idx))
+    wa, wo = O.tc_epoch(expect, ora)
+    assert np.array_equal(to, wo) and ta.tobytes() == wa.tobytes(), ctx
+
+
 def test_commit_and_delta_random_epochs():
     """Adversarial epochs (failing links, nil lists, SKIP / CREATED / DIFF): the predicted
     commit and explicit masks, then a delta with spec edits, nil specs and node moves."""
@@ -61,6 +80,7 @@ def test_commit_and_delta_random_epochs():
             kt = eng.kernel_times()          # the pod tables were patched by the delta: no rebuild
             assert "full_prefix" in kt and "verify_prefix" not in kt, kt
             _run_same(eng, want, f"seed {seed} epoch 1")
+            _outputs_same(eng, want, f"seed {seed} epoch 1")
             # a further delta on the patched tables (rows moving again)
             c = mutate(b_topos := mutate(topos, seed + 7), seed + 11)
             st2 = commit(want, predicted_commit(want, O.reconcile(want, tick=TICK)))
@@ -68,7 +88,9 @@ def test_commit_and_delta_random_epochs():
             c_in = pack(c, vnis, kdict=kd, pdict=pd)
             d2 = build_delta(b, c_in, b.kdict.n, b.pdict.n, vnis=c_in.vnis)
             eng.upload_delta(d2)
-            _run_same(eng, apply_delta(st2, d2), f"seed {seed} epoch 2")
+            w2 = apply_delta(st2, d2)
+            _run_same(eng, w2, f"seed {seed} epoch 2")
+            _outputs_same(eng, w2, f"seed {seed} epoch 2")
 
 
 @pytest.mark.parametrize("pods", [20000])
@@ -101,6 +123,8 @@ def test_resident_churn_chain(pods):
             assert not same_tables(eng.tables(), state), ep
             ora = _run_same(eng, state, f"epoch {ep}")
             assert len(ora.del_idx) and len(ora.add_idx) and len(ora.upd_idx)
+            if ep in (1, 2, 9):
+                _outputs_same(eng, state, f"epoch {ep}")
         full = 9 * (88 * new.desired.n + 25 * new.topos.n)
         assert moved < 0.1 * full, (moved, full)
 
