@@ -170,43 +170,45 @@ def cpu_baseline(inp, budget_s: float, threads: int, share_info: dict):
 
 
 def wire_stage(eng, reps: int = 5):
-    """Separate report (not part of `value`): the protobuf wire encoding of every batch of
-    the epoch (kdtn_epoch_encode: proto.Marshal of each LinksBatchQuery Reconcile sends).
-    GPU kernel time from HIP events, excluding the one host round trip that sizes the
-    arena; bytes = serialized output."""
-    eng.run()
-    eng.sync()
-    eng.encode()
+    """Separate report (not part of `value`): the output stages of an epoch, in the order a
+    controller calls them after each run — kdtn_epoch_encode (proto.Marshal of every
+    LinksBatchQuery Reconcile sends), kdtn_epoch_fanout (RemotePod RPCs per destination
+    daemon), kdtn_epoch_remote_encode (the RemotePod bodies and the receiving daemons' tc argv).
+    Every rep runs the epoch first, so each stage's time includes the per-run tables it builds
+    (the encoders' string tables and the lists' coarse topology indexes are built by the first
+    stage, encode, and shared by the later ones). GPU kernel time from HIP events, excluding the
+    host round trips that size the arenas; bytes = serialized output. Mean over `reps` after one
+    warm-up epoch."""
     acc: dict[str, float] = {}
-    n = 0
-    for _ in range(reps):
+    facc: dict[str, float] = {}
+    racc: dict[str, float] = {}
+    n, node, idx, info = 0, [], [], None
+    for rep in range(reps + 1):
+        eng.run()
+        eng.sync()
         n = eng.encode()
-        for k, v in eng.kernel_times().items():
-            acc[k] = acc.get(k, 0.0) + v / reps
+        kt = eng.kernel_times()
+        node, off, idx = eng.fanout()
+        ft = eng.kernel_times()
+        info = eng.remote_encode()            # the fan-out is cached per run: message kernels only
+        rt = eng.kernel_times()
+        if rep == 0:
+            continue
+        for d, src in ((acc, kt), (facc, ft), (racc, rt)):
+            for k, v in src.items():
+                d[k] = d.get(k, 0.0) + v / reps
     gpu_ms = sum(v for k, v in acc.items() if k != "wire_host_sync")
     res = {"bytes": n, "gpu_ms": gpu_ms, "out_GBps": n / (gpu_ms * 1e-3) / 1e9,
-           "kernels_ms": acc, "note": "not part of value; arena-size host round trip excluded"}
-    eng.fanout()
-    facc: dict[str, float] = {}
-    for _ in range(reps):
-        node, off, idx = eng.fanout()
-        for k, v in eng.kernel_times().items():
-            facc[k] = facc.get(k, 0.0) + v / reps
+           "kernels_ms": acc, "note": "not part of value; per epoch after its run; arena-size host round trip excluded"}
     res["fanout"] = {"daemons": int(len(node)), "remote_rpcs": int(len(idx)),
                      "gpu_ms": sum(v for k, v in facc.items() if k != "fanout_host_sync"),
                      "kernels_ms": facc}
-    eng.remote_encode()
-    racc: dict[str, float] = {}
-    info = None
-    for _ in range(reps):
-        info = eng.remote_encode()            # the fan-out is cached per run: message kernels only
-        for k, v in eng.kernel_times().items():
-            racc[k] = racc.get(k, 0.0) + v / reps
     rms = sum(v for k, v in racc.items() if k != "remote_host_sync")
     res["remote_pods"] = {"messages": int(info.n_msgs), "remote": int(info.n_remote), "bytes": int(info.n_bytes),
                           "tc_bytes": int(info.n_tc_bytes), "gpu_ms": rms,
                           "out_GBps": (info.n_bytes + info.n_tc_bytes) / (rms * 1e-3) / 1e9, "kernels_ms": racc,
-                          "note": "RemotePod request bodies (kdtn_epoch_remote_encode) after the fan-out"}
+                          "note": "RemotePod request bodies and the receiving daemons' tc argv "
+                                  "(kdtn_epoch_remote_encode) after the fan-out"}
     return res
 
 

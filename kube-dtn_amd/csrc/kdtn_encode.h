@@ -62,6 +62,35 @@ KD_INLINE uint32_t entry_topo_wave(const uint32_t* offs, uint32_t T, uint32_t e,
     return lo;
 }
 
+// entry_topo_wave with a coarse index of the list (k_list_coarse: coarse[w] = topology of entry
+// 64 w): the wave starts from the topology of its first entry's 64-entry group and finds every
+// lane's topology with one load of the next 64 boundaries — two dependent loads instead of the
+// search's four or five. Falls back to the search when the wave's entries reach past those 64
+// topologies (empty topologies of the list in between).
+KD_INLINE uint32_t entry_topo_wave_c(const uint32_t* offs, const uint32_t* coarse, uint32_t T, uint32_t e, bool on) {
+    if (!coarse) return entry_topo_wave(offs, T, e, on);
+    const int lane = threadIdx.x & 63;
+    uint32_t lo_e = on ? e : 0xFFFFFFFFu, hi_e = on ? e : 0u;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint32_t a = __shfl_xor(lo_e, d, 64), b = __shfl_xor(hi_e, d, 64);
+        lo_e = a < lo_e ? a : lo_e;
+        hi_e = b > hi_e ? b : hi_e;
+    }
+    if (lo_e > hi_e) return 0;                         // no lane has an entry (wave-uniform)
+    const uint32_t tlo = coarse[lo_e >> 6];            // <= the topology of lo_e
+    // boundary l: the first entry of topology tlo + 1 + l (past T: never <= e)
+    const uint32_t bnd = tlo + 1u + (uint32_t)lane <= T ? offs[tlo + 1u + lane] : 0xFFFFFFFFu;
+    if (hi_e >= __shfl(bnd, 63, 64)) return entry_topo_wave(offs, T, e, on);   // wave-uniform
+    uint32_t c = 0;                                    // boundaries <= e (a prefix of the lanes)
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) {
+        const uint32_t v = __shfl(bnd, (int)(c + (uint32_t)s - 1u), 64);
+        if (c + (uint32_t)s <= 64u && v <= e) c += (uint32_t)s;
+    }
+    return tlo + c;
+}
+
 // ---- byte-stream writer of the encoders (wire, RemotePod, tc argv) ---------------------------
 // Bytes are appended 1-4 at a time into a 64-bit register and stored as whole dwords; only the
 // first and the last dword of a writer's range — shared with the neighbouring writers — take
@@ -361,6 +390,7 @@ KD_INLINE void wave_segments_round(uint32_t* img, bool on, uint64_t s0, uint32_t
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // whole dwords, consecutive lanes on consecutive dwords of each slot ...
     for (uint32_t q = lane; q < total; q += 64) {
         int i = 0;                                               // the last slot starting at or before q
 #pragma unroll
@@ -368,16 +398,28 @@ KD_INLINE void wave_segments_round(uint32_t* img, bool on, uint64_t s0, uint32_t
             if (i + step < NL && mq[i + step] <= q) i += step;
         const uint32_t k = q - mq[i], ll = mll[i];
         const uint32_t ld = ll & 3u, end = ld + (ll >> 2);      // valid bytes of the slot: [ld, end)
+        if ((k == 0 && ld != 0) || 4u * k + 4u > end) continue;  // an edge dword: below
         uint8_t* dst = arena + ((((uint64_t)mhi[i]) << 32) | mlo[i]) + 4ull * k;
-        const uint32_t v = img[q];
-        const uint32_t lo = k == 0 ? ld : 0u;
-        const uint32_t hi = end - 4u * k < 4u ? end - 4u * k : 4u;
-        if (lo == 0 && hi == 4u) {
-            *reinterpret_cast<uint32_t*>(dst) = v;
-        } else {
+        *reinterpret_cast<uint32_t*>(dst) = img[q];
+    }
+    // ... then every lane its own slot's partial first and last dwords, by bytes (the dwords it
+    // shares with the neighbouring ranges): at most eight byte stores per lane, instead of four
+    // byte-store instructions in every round of the loop above
+    if (mine && len) {
+        const uint32_t end = lead + len, kl = (end - 1u) >> 2;
+        uint8_t* dst = arena + (s0 & ~3ull);
+        const uint32_t v0 = img[qi], v1 = img[qi + kl];
+        const uint32_t h0 = kl == 0 ? end : 4u;                  // first dword: bytes [lead, h0)
+        if (lead != 0 || h0 < 4u) {
 #pragma unroll
             for (uint32_t c = 0; c < 4; ++c)
-                if (c >= lo && c < hi) dst[c] = (uint8_t)(v >> (8 * c));
+                if (c >= lead && c < h0) dst[c] = (uint8_t)(v0 >> (8 * c));
+        }
+        const uint32_t h1 = end - 4u * kl;                       // last dword (kl > 0): bytes [0, h1)
+        if (kl > 0 && h1 < 4u) {
+#pragma unroll
+            for (uint32_t c = 0; c < 3; ++c)
+                if (c < h1) dst[4u * kl + c] = (uint8_t)(v1 >> (8 * c));
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -148,6 +148,9 @@ struct kdtn_ctx {
     DevBuf f_mark, f_send, f_node_idx, f_nodes, f_counts, f_base, f_part, f_idx, f_inv, f_reach_upd, f_cut, f_st, f_node;
     uint32_t f_stamp = 0;
     bool fan_valid = false;                    // the fan-out of the last run is in f_* (fanout_compute)
+    bool lc_valid = false;                     // lc: coarse entry -> topology indexes of the last run's lists
+    bool si_run = false;                       // the string tables were built since the last run
+    DevBuf lc[3];
     uint32_t fan_nn = 0, fan_nsend = 0;
     // RemotePod messages (kdtn_epoch_remote_encode)
     DevBuf rp_flag, rp_pos, rp_phys, rp_msz, rp_moff, rp_tsz, rp_toff, rp_part, rp_arena, rp_tc, rp_msz_e, rp_tsz_e;
@@ -817,13 +820,32 @@ int prepare_epoch(kdtn_ctx* c, const kdtn_vni_table& vn, uint32_t slice, uint32_
 
 // Which batch entries the daemons reach (k_reach; include/kdtn.h): c->f_send (add) and
 // c->f_reach_upd (update) flags of the last run; stamps destination daemons into `mark`.
+// coarse entry -> topology indexes of the last run's del / add / upd lists (k_list_coarse),
+// built by the first output stage after a run
+int list_coarse(kdtn_ctx* c) {
+    if (c->lc_valid) return KDTN_OK;
+    const uint32_t cnt[3] = {c->h_misc[1], c->h_misc[3], c->h_misc[2]};   // del, add, upd
+    DevBuf* offs[3] = {&c->del_off, &c->add_off, &c->upd_off};
+    for (int l = 0; l < 3; ++l) {
+        TRY(ensure(c->lc[l], ((size_t)cnt[l] / 64 + 2) * 4));
+        if (c->T && cnt[l])
+            k_list_coarse<<<nblocks(c->T), BLOCK, 0, c->stream>>>(dp<uint32_t>(*offs[l]), c->T, dp<uint32_t>(c->lc[l]));
+    }
+    HIP_TRY(hipGetLastError());
+    c->lc_valid = true;
+    return KDTN_OK;
+}
+
 int run_reach(kdtn_ctx* c, uint32_t* mark, uint32_t stamp) {
     const uint32_t nu = c->h_misc[2], na = c->h_misc[3];
     TRY(ensure(c->f_send, (size_t)na + 16));
     TRY(ensure(c->f_reach_upd, (size_t)nu + 16));
     ReachIn r{dp<uint32_t>(c->del_off), dp<uint4>(c->del_res), dp<uint32_t>(c->add_off), dp<uint4>(c->add_res),
               dp<uint2>(c->add_qdisc), dp<uint32_t>(c->upd_off), dp<uint4>(c->upd_res), c->T, stamp,
-              dp<uint8_t>(c->add_qerr), nullptr};
+              dp<uint8_t>(c->add_qerr), nullptr, nullptr, nullptr};
+    TRY(list_coarse(c));
+    r.add_coarse = dp<uint32_t>(c->lc[1]);
+    r.upd_coarse = dp<uint32_t>(c->lc[2]);
     if (mark) {                                     // the fan-out: dense node ids for its passes
         TRY(ensure(c->f_node, (size_t)na * 4 + 16));
         r.add_node = dp<uint32_t>(c->f_node);
@@ -845,10 +867,12 @@ int run_reach(kdtn_ctx* c, uint32_t* mark, uint32_t stamp) {
     return KDTN_OK;
 }
 
-// The encoders' inline string tables (StrTab) of both dictionaries, on the context stream.
-// Like the dictionary parses, the work is a function of the upload: the strings from the
-// upload's keep index (and any never built) on; the entries before it are kept.
+// The encoders' inline string tables (StrTab) of both dictionaries, on the context stream,
+// built by the first output stage after a run (the later stages of the epoch share them). Like
+// the dictionary parses, the work is a function of the upload: the strings from the upload's
+// keep index (and any never built) on; the entries before it are kept.
 int str_tables(kdtn_ctx* c) {
+    if (c->si_run && c->si_k == c->D && c->si_p == c->P) return KDTN_OK;
     hipStream_t s = c->stream;
     const uint32_t k0 = std::min(c->si_k, c->kd_from), p0 = std::min(c->si_p, c->pd_from);
     TRY(ensure_keep(c->kd_si, (size_t)c->D * SI_KW * 4 + 16, (size_t)k0 * SI_KW * 4, s));
@@ -866,6 +890,7 @@ int str_tables(kdtn_ctx* c) {
     HIP_TRY(hipGetLastError());
     c->si_k = c->D;
     c->si_p = c->P;
+    c->si_run = true;
     return KDTN_OK;
 }
 
@@ -1012,7 +1037,7 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->add_qdisc, &c->upd_qdisc, &c->add_qerr, &c->kd_si, &c->kd_len1, &c->pd_si, &c->pd_len1, &c->w_rel,
                       &c->w_topo, &c->w_size, &c->w_err, &c->w_off, &c->w_part, &c->w_arena,
                       &c->f_mark, &c->f_send, &c->f_node_idx, &c->f_nodes, &c->f_counts, &c->f_base,
-                      &c->f_part, &c->f_idx, &c->f_inv, &c->f_st, &c->f_node, &c->f_reach_upd, &c->tc_size, &c->tc_off, &c->tc_part, &c->tc_arena,
+                      &c->f_part, &c->f_idx, &c->f_inv, &c->f_st, &c->f_node, &c->lc[0], &c->lc[1], &c->lc[2], &c->f_reach_upd, &c->tc_size, &c->tc_off, &c->tc_part, &c->tc_arena,
                       &c->j_doc, &c->j_q, &c->j_bs, &c->j_hb, &c->j_qcnt, &c->j_qoff, &c->j_tok, &c->j_open,
                       &c->j_close, &c->j_gcnt, &c->j_goff, &c->j_toks, &c->j_par,
                       &c->j_role, &c->j_ecls, &c->j_odep, &c->j_ord, &c->j_tagg, &c->j_gagg, &c->j_cnt3, &c->j_coff3, &c->j_small,
@@ -1525,6 +1550,8 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
     c->encoded = false;
     c->tc_done = false;
     c->fan_valid = false;
+    c->lc_valid = false;
+    c->si_run = false;
     c->rp_done = false;
     c->vx_imported = false;
     c->vx_contest_ok = false;
@@ -1903,6 +1930,8 @@ int kdtn_epoch_encode(kdtn_ctx* c, uint64_t* n_bytes) {
     WireIn w{};
     w.kd = str_tab_kd(c);
     w.pd = str_tab_pd(c);
+    TRY(list_coarse(c));
+    for (int l = 0; l < 3; ++l) w.coarse[l] = dp<uint32_t>(c->lc[l]);
     w.t_name = dp<uint32_t>(c->t_name);
     w.t_src = dp<uint32_t>(c->t_src);
     w.t_netns = dp<uint32_t>(c->t_netns);
@@ -2104,6 +2133,8 @@ int kdtn_epoch_remote_encode(kdtn_ctx* c, kdtn_remote_info* info) {
     r.kd = str_tab_kd(c);
     r.pd = str_tab_pd(c);
     r.kd_offs = dp<uint32_t>(c->kd_offs);
+    TRY(list_coarse(c));
+    r.add_coarse = dp<uint32_t>(c->lc[1]);
     r.t_ns = dp<uint32_t>(c->t_ns);
     r.t_src = dp<uint32_t>(c->t_src);
     r.t_netns = dp<uint32_t>(c->t_netns);
@@ -2140,11 +2171,12 @@ int kdtn_epoch_remote_encode(kdtn_ctx* c, kdtn_remote_info* info) {
     TRY(ensure(c->rp_arena, (size_t)tot[0] + 16));
     TRY(ensure(c->rp_tc, (size_t)tot[1] + 16));
     timer_mark(c, "remote_host_sync");
-    if (n)   // the messages, then (UpdateRemote) the receiving daemons' tc argv
-        k_remote_write<<<nblocks(na), BLOCK, 0, s>>>(r, dp<uint64_t>(c->rp_moff), dp<uint8_t>(c->rp_arena),
-                                                     nr ? dp<uint64_t>(c->rp_toff) : nullptr,
-                                                     nr ? dp<uint8_t>(c->rp_tc) : nullptr);
-    timer_mark(c, "remote_write");
+    if (n) {
+        k_remote_write<<<nblocks(na), BLOCK, 0, s>>>(r, dp<uint64_t>(c->rp_moff), dp<uint8_t>(c->rp_arena));
+        timer_mark(c, "remote_write");
+        if (nr) k_tc_remote_write<<<nblocks(na), BLOCK, 0, s>>>(r, dp<uint64_t>(c->rp_toff), dp<uint8_t>(c->rp_tc));
+        timer_mark(c, "remote_tc_write");
+    }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(s));
     c->rp_n = (uint32_t)n;
@@ -3367,6 +3399,8 @@ void state_changed(kdtn_ctx* c) {
     c->encoded = false;
     c->tc_done = false;
     c->fan_valid = false;
+    c->lc_valid = false;
+    c->si_run = false;
     c->rp_done = false;
     c->j_done = false;
     c->tables_cur = false;

@@ -51,8 +51,8 @@ __global__ void __launch_bounds__(BLOCK) k_reach(ReachIn f, uint32_t na, uint32_
                                                  const uint8_t* st_add, uint32_t* mark, uint8_t* reach_add,
                                                  uint8_t* reach_upd) {
     const uint32_t x = blockIdx.x * BLOCK + threadIdx.x;
-    const uint32_t ta = entry_topo_wave(f.add_off, f.T, x, x < na);
-    const uint32_t tu = entry_topo_wave(f.upd_off, f.T, x - na, x >= na && x < na + nu);
+    const uint32_t ta = entry_topo_wave_c(f.add_off, f.add_coarse, f.T, x, x < na);
+    const uint32_t tu = entry_topo_wave_c(f.upd_off, f.upd_coarse, f.T, x - na, x >= na && x < na + nu);
     if (x < na) {
         const uint32_t t = ta;
         uint8_t a = 0;
@@ -74,6 +74,13 @@ __global__ void __launch_bounds__(BLOCK) k_reach(ReachIn f, uint32_t na, uint32_
         const uint32_t t = tu;
         reach_upd[e] = (cut[3 * t] == 0xFFFFFFFFu && cut[3 * t + 1] == 0xFFFFFFFFu && e <= cut[3 * t + 2]) ? REACH_ON : 0;
     }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_list_coarse(const uint32_t* offs, uint32_t T, uint32_t* coarse) {
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= T) return;
+    const uint32_t a = offs[t], b = offs[t + 1];
+    for (uint32_t w = (a + 63u) >> 6; (w << 6) < b; ++w) coarse[w] = t;   // groups starting in t
 }
 
 // marked node ids → dense node indices in id order (chunks of SCAN_CHUNK ids)

@@ -316,6 +316,7 @@ struct StrTab {
 };
 struct WireIn {
     StrTab kd, pd;
+    const uint32_t* coarse[3];      // k_list_coarse of del_off, add_off, upd_off (or null)
     const uint32_t* t_name;
     const uint32_t* t_src;
     const uint32_t* t_netns;
@@ -455,6 +456,7 @@ __global__ void k_ix_refs(uint32_t* ref, uint32_t n);
 // the physical peer's local Update payload of add entry phys_idx[m - n_remote]
 struct RemoteIn {
     StrTab kd, pd;
+    const uint32_t* add_coarse;     // k_list_coarse of add_off (or null)
     const uint32_t* kd_offs;        // physical peers: TrimPrefix(PeerPod, "physical/") from the arena
     const uint32_t* t_ns;
     const uint32_t* t_src;
@@ -476,7 +478,8 @@ struct RemoteIn {
 __global__ void k_remote_phys_flags(const uint8_t* reach_add, const uint4* add_res, uint32_t na, uint32_t* flag);
 __global__ void k_remote_phys_scatter(const uint32_t* flag, const uint64_t* pos, uint32_t na, uint32_t* phys_idx);
 __global__ void k_remote_sizes(RemoteIn r, uint32_t* msz, uint32_t* tsz);
-__global__ void k_remote_write(RemoteIn r, const uint64_t* off, uint8_t* arena, const uint64_t* toff, uint8_t* tc);
+__global__ void k_remote_write(RemoteIn r, const uint64_t* off, uint8_t* arena);
+__global__ void k_tc_remote_write(RemoteIn r, const uint64_t* off, uint8_t* arena);
 
 // ---- RemotePod fan-out grouping (kdtn_fanout.hip) ---------------------------------------
 constexpr int FAN_CHUNK = 1024;        // add entries per single-wave workgroup
@@ -547,7 +550,11 @@ struct ReachIn {
     uint32_t* add_node;             // k_reach_cuts: add_res.z of every add entry in a dense array
                                     // (k_reach and the fan-out read 4 B instead of the 16-B
                                     // records), or null
+    const uint32_t* add_coarse;     // k_list_coarse of add_off / upd_off (or null)
+    const uint32_t* upd_coarse;
 };
+// coarse[w] = the topology of list entry 64 w (one thread per topology, its groups' starts)
+__global__ void k_list_coarse(const uint32_t* offs, uint32_t T, uint32_t* coarse);
 __global__ void k_reach_cuts(ReachIn f, uint32_t nd, uint32_t na, uint32_t nu, uint32_t* cut, uint8_t* st_add);
 __global__ void k_reach(ReachIn f, uint32_t na, uint32_t nu, const uint32_t* cut, const uint8_t* st_add, uint32_t* mark,
                         uint8_t* reach_add, uint8_t* reach_upd);

@@ -168,7 +168,7 @@ __global__ void __launch_bounds__(BLOCK) k_wire_entry_sizes(WireIn w, DevLinks O
 #pragma unroll
     for (uint32_t l = 0; l < 3; ++l)
         if (__ballot(lst == l)) {                          // wave-uniform
-            const uint32_t tl = entry_topo_wave(w.list_off[l], w.T, e, lst == l);
+            const uint32_t tl = entry_topo_wave_c(w.list_off[l], w.coarse[l], w.T, e, lst == l);
             if (lst == l) t = tl;
         }
     if (!on) return;
@@ -506,7 +506,7 @@ __global__ void __launch_bounds__(BLOCK) k_remote_sizes(RemoteIn r, uint32_t* ms
     const uint32_t e = blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t kind = e < r.n_add ? remote_kind(r, e) : 0u;
     if (__ballot(kind != 0) == 0) return;           // wave-uniform
-    const uint32_t t = entry_topo_wave(r.add_off, r.T, e, kind != 0);
+    const uint32_t t = entry_topo_wave_c(r.add_off, r.add_coarse, r.T, e, kind != 0);
     if (!kind) return;
     const RemoteMsg q = remote_msg(r, e, t, kind == 1);
     uint32_t body, psz;
@@ -574,43 +574,47 @@ KD_INLINE void write_remote(WSink& o, const RemoteIn& r, const RemoteMsg& q) {
 }
 
 // One thread per add entry with a message, in add-list order (its columns read coalesced),
-// writing the message at its fan-out position and, for an UpdateRemote, the receiving daemon's
-// tc argv at the same index of the tc arena. A wave's messages for one daemon are one contiguous
-// run of each arena (fan-out order keeps add-list order within a daemon), so the wave stores
-// them through its LDS image dword by dword (wave_segments_write), the messages first, then the
-// argv.
-__global__ void __launch_bounds__(BLOCK) k_remote_write(RemoteIn r, const uint64_t* off, uint8_t* arena,
-                                                        const uint64_t* toff, uint8_t* tc) {
+// writing the message at its fan-out position. A wave's messages for one daemon are one
+// contiguous run of the arena (fan-out order keeps add-list order within a daemon), so the
+// wave stores them through its LDS image dword by dword (wave_segments_write).
+__global__ void __launch_bounds__(BLOCK) k_remote_write(RemoteIn r, const uint64_t* off, uint8_t* arena) {
     __shared__ uint32_t img[BLOCK / 64][REMOTE_IMG / 4];
     const uint32_t e = blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t kind = e < r.n_add ? remote_kind(r, e) : 0u;
     if (__ballot(kind != 0) == 0) return;           // wave-uniform
-    const uint32_t t = entry_topo_wave(r.add_off, r.T, e, kind != 0);
-    uint32_t m = 0;
+    const uint32_t t = entry_topo_wave_c(r.add_off, r.add_coarse, r.T, e, kind != 0);
     uint64_t s0 = 0, s1 = 0;
     if (kind) {
-        m = remote_msg_index(r, e, kind);
+        const uint32_t m = remote_msg_index(r, e, kind);
         s0 = off[m];
         s1 = off[m + 1];
     }
     const bool on = s1 > s0;                        // empty: no message or a Marshal error
-    {
-        RemoteMsg q{};
-        if (on) q = remote_msg(r, e, t, kind == 1);
-        wave_segments_write<REMOTE_IMG>(img[threadIdx.x >> 6], on, s0, s1, arena,
-                                        [&](WSink& o) __attribute__((always_inline)) { write_remote(o, r, q); });
-    }
-    if (!tc) return;
-    uint64_t c0 = 0, c1 = 0;
-    if (kind == 1) {
-        c0 = toff[m];
-        c1 = toff[m + 1];
-    }
-    if (__ballot(c1 > c0) == 0) return;             // wave-uniform
+    RemoteMsg q{};
+    if (on) q = remote_msg(r, e, t, kind == 1);
+    wave_segments_write<REMOTE_IMG>(img[threadIdx.x >> 6], on, s0, s1, arena,
+                                    [&](WSink& o) __attribute__((always_inline)) { write_remote(o, r, q); });
+}
+
+// The receiving daemons' tc argv, one thread per add entry with an UpdateRemote (add-list
+// order), written at its message's index of the tc arena through the wave's LDS image (a
+// separate launch: with the messages in one kernel the writer held 138 VGPRs, 3 waves per SIMD)
+__global__ void __launch_bounds__(BLOCK) k_tc_remote_write(RemoteIn r, const uint64_t* off, uint8_t* arena) {
+    __shared__ uint32_t img[BLOCK / 64][WIRE_IMG / 4];
+    const uint32_t e = blockIdx.x * BLOCK + threadIdx.x;
     TcEntry te{0, 0, 0, 0, false};
-    if (c1 > c0) te = tc_remote_entry(r, e);
-    wave_segments_write<REMOTE_IMG>(img[threadIdx.x >> 6], c1 > c0, c0, c1, tc,
-                                    [&](WSink& o) __attribute__((always_inline)) { write_tbf_argv(o, r.kd, te); });
+    uint64_t s0 = 0, s1 = 0;
+    if (e < r.n_add && (r.send[e] & REACH_SEND)) {
+        te = tc_remote_entry(r, e);
+        if (te.on) {
+            const uint32_t m = r.rem_inv[e];
+            s0 = off[m];
+            s1 = off[m + 1];
+        }
+    }
+    if (__ballot(s1 > s0) == 0) return;             // wave-uniform
+    wave_segments_write(img[threadIdx.x >> 6], s1 > s0, s0, s1, arena,
+                        [&](WSink& o) __attribute__((always_inline)) { write_tbf_argv(o, r.kd, te); });
 }
 
 }  // namespace kdtn

@@ -33,27 +33,27 @@ res = {}
 
 
 def timed(name, fn):
-    acc = {}
-    for _ in range(a.reps):
-        fn()
-        for k, v in eng.kernel_times().items():
-            acc[k] = acc.get(k, 0.0) + v / a.reps
-    res[name] = {k: round(v, 4) for k, v in acc.items()}
+    acc = res.setdefault(name, {})
+    fn()
+    for k, v in eng.kernel_times().items():
+        acc[k] = acc.get(k, 0.0) + v / a.reps
 
 
-def run():
+# per epoch: the run, then the output stages in a controller's order (per-run tables are built
+# by the first stage that needs them); one warm-up epoch, then the mean over reps
+for rep in range(a.reps + 1):
+    if rep == 1:
+        res.clear()
     eng.run()
     eng.sync()
-
-
-timed("run", run)
-if "encode" in stages:
-    timed("encode", eng.encode)
-if "fanout" in stages:
-    timed("fanout", eng.fanout)
-if "remote" in stages:
-    timed("remote", eng.remote_encode)
-if "tc" in stages:
-    c = eng.sync()
-    timed("tc", lambda: eng.tc_argv(c.n_add, c.n_upd))
+    if "encode" in stages:
+        timed("encode", eng.encode)
+    if "fanout" in stages:
+        timed("fanout", eng.fanout)
+    if "remote" in stages:
+        timed("remote", eng.remote_encode)
+    if "tc" in stages:
+        c = eng.sync()
+        timed("tc", lambda: eng.tc_argv(c.n_add, c.n_upd))
+res = {s: {k: round(v, 4) for k, v in d.items()} for s, d in res.items()}
 print(json.dumps({"config": a.config, "pods": a.pods, "links": inp.desired.n, "ms": res}, indent=1))
