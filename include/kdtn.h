@@ -480,7 +480,10 @@ int kdtn_epoch_fanout(kdtn_ctx* ctx, kdtn_fanout* out);
  * (Update → SetupVxLan → MakeQdiscs → SetVethQdiscs, daemon/vxlan/vxlan.go:31-51; same
  * format as kdtn_epoch_tc) = tc_bytes[tc_off[m], tc_off[m+1]): present when the link has a
  * TBF and the peer's CreateOrUpdate accepts IntfIp (remote_err == 0); physical messages
- * have none here (their tc is kdtn_epoch_tc's slot 2e). Needs a run with RESOLVE and QDISC. */
+ * have none here (their tc is kdtn_epoch_tc's slot 2e). Needs a run with RESOLVE and QDISC.
+ * Called after kdtn_epoch_encode of the same run, it copies each message's Properties field
+ * from its AddLinks entry's Link bytes (the same pb.LinkProperties field 7) instead of
+ * re-encoding the property strings; the bytes are the same either way. */
 typedef struct kdtn_remote_info {
     uint32_t n_msgs, n_remote;
     uint64_t n_bytes, n_tc_bytes;

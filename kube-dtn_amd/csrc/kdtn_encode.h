@@ -139,6 +139,25 @@ struct WSink {
         if (head && !hp) part(d0, first, head, 4u);     // shared first dword, flushed
         if (fill) part(d, (uint32_t)acc, hp ? head : 0u, fill);
     }
+    // bytes [b, b + len) of an arena with >= 40 B of readable slack past its end, 32 per round
+    // (two 16-B loads and a dword, realigned by alignbyte)
+    KD_INLINE void copy(const uint8_t* arena, uint64_t b, uint32_t len) {
+        typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+        const uint32_t* a32 = reinterpret_cast<const uint32_t*>(arena + (b & ~3ull));
+        const uint32_t sh = (uint32_t)b & 3u;
+        for (uint32_t o = 0; o < len; o += 32u, a32 += 8) {
+            const u32x4a A = *reinterpret_cast<const u32x4a*>(a32);
+            const u32x4a B = *reinterpret_cast<const u32x4a*>(a32 + 4);
+            const uint32_t w[9] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w, a32[8]};
+#pragma unroll
+            for (uint32_t q = 0; q < 8; ++q) {
+                if (o + 4u * q < len) {
+                    const uint32_t r = len - o - 4u * q;
+                    put(__builtin_amdgcn_alignbyte(w[q + 1], w[q], sh), r < 4u ? r : 4u);
+                }
+            }
+        }
+    }
     // owned mode: the writer owns every byte of its dwords (a private LDS slot); `lead` zero
     // bytes put the output at the alignment of its destination
     KD_INLINE void init_owned(uint32_t* slot, uint32_t lead) {

@@ -141,12 +141,11 @@ struct kdtn_ctx {
     DevBuf action, del_off, add_off, upd_off, del_idx, add_idx, upd_idx;
     DevBuf del_res, add_res, upd_res, add_qdisc, upd_qdisc, add_qerr;
     // wire encoding
-    DevBuf kd_si, kd_len1, pd_si, pd_len1, w_rel, w_topo, w_size, w_err, w_off, w_part, w_arena;
+    DevBuf kd_si, kd_len1, pd_si, pd_len1, w_rel, w_topo, w_size, w_err, w_off, w_part, w_arena, w_pinfo;
     uint64_t w_bytes = 0;
     bool encoded = false;
     // RemotePod fan-out
     DevBuf f_mark, f_send, f_node_idx, f_nodes, f_counts, f_base, f_part, f_idx, f_inv, f_reach_upd, f_cut, f_st, f_node;
-    uint32_t f_stamp = 0;
     bool fan_valid = false;                    // the fan-out of the last run is in f_* (fanout_compute)
     bool lc_valid = false;                     // lc: coarse entry -> topology indexes of the last run's lists
     bool si_run = false;                       // the string tables were built since the last run
@@ -1035,7 +1034,7 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->fscratch, &c->action, &c->del_off, &c->add_off, &c->upd_off, &c->del_idx,
                       &c->add_idx, &c->upd_idx, &c->del_res, &c->add_res, &c->upd_res,
                       &c->add_qdisc, &c->upd_qdisc, &c->add_qerr, &c->kd_si, &c->kd_len1, &c->pd_si, &c->pd_len1, &c->w_rel,
-                      &c->w_topo, &c->w_size, &c->w_err, &c->w_off, &c->w_part, &c->w_arena,
+                      &c->w_topo, &c->w_size, &c->w_err, &c->w_off, &c->w_part, &c->w_arena, &c->w_pinfo,
                       &c->f_mark, &c->f_send, &c->f_node_idx, &c->f_nodes, &c->f_counts, &c->f_base,
                       &c->f_part, &c->f_idx, &c->f_inv, &c->f_st, &c->f_node, &c->lc[0], &c->lc[1], &c->lc[2], &c->f_reach_upd, &c->tc_size, &c->tc_off, &c->tc_part, &c->tc_arena,
                       &c->j_doc, &c->j_q, &c->j_bs, &c->j_hb, &c->j_qcnt, &c->j_qoff, &c->j_tok, &c->j_open,
@@ -1947,8 +1946,9 @@ int kdtn_epoch_encode(kdtn_ctx* c, uint64_t* n_bytes) {
     w.list_base[2] = nd + na;
     w.n_entries = (uint32_t)ne;
     w.T = T;
+    TRY(ensure(c->w_pinfo, (size_t)na * 8 + 16));
     WireWork wk{dp<uint32_t>(c->w_rel), dp<uint32_t>(c->w_topo), dp<uint64_t>(c->w_size), dp<uint32_t>(c->w_err),
-                dp<uint64_t>(c->w_off)};
+                dp<uint64_t>(c->w_off), dp<uint64_t>(c->w_pinfo)};
     uint64_t total = 0;
     uint32_t big = 0;
     {   // sizes, one scan, then the writer (a single pass with a look-back scan measured slower:
@@ -1964,7 +1964,7 @@ int kdtn_epoch_encode(kdtn_ctx* c, uint64_t* n_bytes) {
         HIP_TRY(hipMemcpyAsync(&total, dp<uint64_t>(c->w_size) + ne, 8, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipMemcpyAsync(&big, dp<uint32_t>(c->w_err) + T, 4, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
-        if (!big) TRY(ensure(c->w_arena, (size_t)total + 16));
+        if (!big) TRY(ensure(c->w_arena, (size_t)total + 64));   // (WSink::copy reads past a range)
         timer_mark(c, "wire_host_sync");                // the arena size crosses to the host
         if (ne && !big) k_wire_write<<<nblocks(ne), BLOCK, 0, s>>>(w, c->real.view, c->des.view, wk, dp<uint8_t>(c->w_arena));
         timer_mark(c, "wire_write");
@@ -2006,17 +2006,11 @@ int fanout_compute(kdtn_ctx* c) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     hipStream_t s = c->stream;
     const uint32_t na = c->h_misc[3], D = c->D;
-    if (c->f_mark.cap < (size_t)D * 4) {                      // stamps start from a zeroed table
-        TRY(ensure(c->f_mark, (size_t)D * 4));
-        HIP_TRY(hipMemsetAsync(c->f_mark.p, 0, c->f_mark.cap, s));
-        c->f_stamp = 0;
-    }
-    if (++c->f_stamp == 0xFFFFFFFFu) {
-        HIP_TRY(hipMemsetAsync(c->f_mark.p, 0, c->f_mark.cap, s));
-        c->f_stamp = 1;
-    }
+    const uint32_t nw = (D + 3) / 4;                          // destination-daemon flag bytes (words of 4)
+    TRY(ensure(c->f_mark, (size_t)nw * 4 + 16));
+    HIP_TRY(hipMemsetAsync(c->f_mark.p, 0, (size_t)nw * 4, s));
     const uint32_t nchunks = nblocks(na, FAN_CHUNK);
-    const uint32_t nbd = nblocks(D, SCAN_CHUNK);
+    const uint32_t nbd = nblocks(nw, SCAN_CHUNK);
     TRY(ensure(c->f_node_idx, (size_t)D * 4));
     TRY(ensure(c->f_nodes, (size_t)FAN_NODE_CAP * 4 + 16));
     TRY(ensure(c->f_part, (size_t)nbd * 8 + 16));
@@ -2024,12 +2018,12 @@ int fanout_compute(kdtn_ctx* c) {
     TRY(ensure(c->f_inv, (size_t)na * 4 + 16));
     uint32_t* misc = dp<uint32_t>(c->misc);
     uint32_t* n_nodes = misc + MISC_FAN_NODES;
-    TRY(run_reach(c, dp<uint32_t>(c->f_mark), c->f_stamp));
-    const FanIn f{dp<uint32_t>(c->add_off), dp<uint4>(c->add_res), dp<uint2>(c->add_qdisc), c->T, na, c->f_stamp,
+    TRY(run_reach(c, dp<uint32_t>(c->f_mark), 0));
+    const FanIn f{dp<uint32_t>(c->add_off), dp<uint4>(c->add_res), dp<uint2>(c->add_qdisc), c->T, na, 0u,
                   dp<uint32_t>(c->f_node)};            // (after run_reach: it sizes f_node)
-    k_fan_nodes_count<<<nbd, BLOCK, 0, s>>>(dp<uint32_t>(c->f_mark), D, c->f_stamp, dp<uint64_t>(c->f_part));
+    k_fan_nodes_count<<<nbd, BLOCK, 0, s>>>(dp<uint32_t>(c->f_mark), nw, dp<uint64_t>(c->f_part));
     k_scan_top<<<1, SCAN_TOP_BLOCK, 0, s>>>(dp<uint64_t>(c->f_part), nbd);
-    k_fan_nodes_write<<<nbd, BLOCK, 0, s>>>(dp<uint32_t>(c->f_mark), D, c->f_stamp, dp<uint64_t>(c->f_part),
+    k_fan_nodes_write<<<nbd, BLOCK, 0, s>>>(dp<uint32_t>(c->f_mark), nw, dp<uint64_t>(c->f_part),
                                            dp<uint32_t>(c->f_node_idx), dp<uint32_t>(c->f_nodes), n_nodes);
     timer_mark(c, "fanout_nodes");
     uint32_t nn = 0;
@@ -2133,6 +2127,13 @@ int kdtn_epoch_remote_encode(kdtn_ctx* c, kdtn_remote_info* info) {
     r.kd = str_tab_kd(c);
     r.pd = str_tab_pd(c);
     r.kd_offs = dp<uint32_t>(c->kd_offs);
+    if (c->encoded) {                        // the run's wire encoding: its properties fields
+        r.w_pinfo = dp<uint64_t>(c->w_pinfo);
+        r.w_pos = dp<uint64_t>(c->w_size);
+        r.w_arena = dp<uint8_t>(c->w_arena);
+        r.w_err = dp<uint32_t>(c->w_err);
+        r.w_nd = c->h_misc[1];
+    }
     TRY(list_coarse(c));
     r.add_coarse = dp<uint32_t>(c->lc[1]);
     r.t_ns = dp<uint32_t>(c->t_ns);

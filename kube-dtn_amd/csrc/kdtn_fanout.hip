@@ -10,7 +10,7 @@
 // nodes in ascending kdict-id order of their src_ip, entries of a node in add-list order.
 //
 // Kernels: k_reach_cuts / k_reach (entry-parallel RPC-order first-error rule, marks senders
-// and their nodes in a stamped D-sized table), k_fan_nodes_* (compaction of marked node ids → dense
+// and their nodes in flag bytes per key-string id), k_fan_nodes_* (compaction of marked node ids → dense
 // node index), k_fan_count / k_fan_scatter (single-wave workgroups over chunks of 4,096
 // entries: LDS histogram, node-major scan of the (node, chunk) counts, stable scatter).
 #include "kdtn_encode.h"
@@ -25,7 +25,7 @@ namespace kdtn {
 // the batch (a failing link, or a cross-node link whose RemotePod the peer rejects — both
 // reached themselves) and the first failing update (one atomicMin per such entry into
 // cut[3t + list], 0xFFFFFFFF = none); k_reach then writes per add entry REACH_ON |
-// REACH_SEND, per update entry REACH_ON, and (mark != nullptr) stamps the destination
+// REACH_SEND, per update entry REACH_ON, and (mark != nullptr) marks the destination
 // daemon of every RemotePod sent.
 __global__ void __launch_bounds__(BLOCK) k_reach_cuts(ReachIn f, uint32_t nd, uint32_t na, uint32_t nu, uint32_t* cut,
                                                       uint8_t* st_add) {
@@ -60,11 +60,13 @@ __global__ void __launch_bounds__(BLOCK) k_reach(ReachIn f, uint32_t na, uint32_
             a = REACH_ON;
             if (st_add[x] & REACH_SEND) {               // no failure, RemotePod sent (k_reach_cuts)
                 a |= REACH_SEND;
-                // a few dozen daemons take millions of stamps: store only a missing one (a
-                // stale read stores again, harmlessly), so the words are not written per entry
+                // a flag byte per key-string id: a few dozen daemons take millions of marks, so
+                // a flag is stored only while it reads clear (a stale read stores again,
+                // harmlessly; plain stores: an atomic OR into shared bitmap words serialised)
                 if (mark) {
                     const uint32_t node = f.add_node ? f.add_node[x] : f.add_res[x].z;
-                    if (mark[node] != f.stamp) mark[node] = f.stamp;
+                    uint8_t* m = reinterpret_cast<uint8_t*>(mark);
+                    if (!m[node]) m[node] = 1;
                 }
             }
         }
@@ -83,38 +85,41 @@ __global__ void __launch_bounds__(BLOCK) k_list_coarse(const uint32_t* offs, uin
     for (uint32_t w = (a + 63u) >> 6; (w << 6) < b; ++w) coarse[w] = t;   // groups starting in t
 }
 
-// marked node ids → dense node indices in id order (chunks of SCAN_CHUNK ids)
-__global__ void __launch_bounds__(BLOCK) k_fan_nodes_count(const uint32_t* mark, uint32_t nd, uint32_t stamp,
-                                                           uint64_t* part) {
+// nonzero flag bytes of a marked node id's word: bit 8k of the result = byte k is set
+KD_INLINE uint32_t flag_bytes(uint32_t w) { return ((w | (w >> 1) | (w >> 2) | (w >> 3) | (w >> 4) | (w >> 5) | (w >> 6) | (w >> 7)) & 0x01010101u); }
+
+// marked node ids (flag bytes, read as words of four) → dense node indices in id order (chunks of
+// SCAN_CHUNK words)
+__global__ void __launch_bounds__(BLOCK) k_fan_nodes_count(const uint32_t* mark, uint32_t nw, uint64_t* part) {
     __shared__ uint64_t sh[BLOCK / 64];
     const uint32_t b0 = blockIdx.x * SCAN_CHUNK + threadIdx.x * 4;
     uint64_t v = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) v += (b0 + k < nd && mark[b0 + k] == stamp) ? 1u : 0u;
+    for (int k = 0; k < 4; ++k) v += b0 + k < nw ? __popc(flag_bytes(mark[b0 + k])) : 0u;
     uint64_t tot;
     block_exclusive(v, sh, &tot);
     if (threadIdx.x == 0) part[blockIdx.x] = tot;
 }
 
-__global__ void __launch_bounds__(BLOCK) k_fan_nodes_write(const uint32_t* mark, uint32_t nd, uint32_t stamp,
-                                                           const uint64_t* part, uint32_t* node_idx,
-                                                           uint32_t* nodes, uint32_t* n_nodes) {
+__global__ void __launch_bounds__(BLOCK) k_fan_nodes_write(const uint32_t* mark, uint32_t nw, const uint64_t* part,
+                                                           uint32_t* node_idx, uint32_t* nodes, uint32_t* n_nodes) {
     __shared__ uint64_t sh[BLOCK / 64];
     const uint32_t b0 = blockIdx.x * SCAN_CHUNK + threadIdx.x * 4;
-    bool m[4];
+    uint32_t m[4];
     uint64_t v = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        m[k] = b0 + k < nd && mark[b0 + k] == stamp;
-        v += m[k] ? 1u : 0u;
+        m[k] = b0 + k < nw ? flag_bytes(mark[b0 + k]) : 0u;
+        v += __popc(m[k]);
     }
     uint64_t tot;
     uint64_t x = part[blockIdx.x] + block_exclusive(v, sh, &tot);
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-        if (m[k]) {
-            node_idx[b0 + k] = (uint32_t)x;
-            nodes[x] = b0 + k;
+        for (uint32_t w = m[k]; w; w &= w - 1u) {
+            const uint32_t id = (b0 + k) * 4u + ((uint32_t)__builtin_ctz(w) >> 3);
+            node_idx[id] = (uint32_t)x;
+            nodes[x] = id;
             ++x;
         }
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *n_nodes = (uint32_t)(part[blockIdx.x] + tot);

@@ -335,6 +335,9 @@ struct WireWork {
     uint32_t* err;                  // [T+1] bit l of err[t]: list l of topology t failed to marshal;
                                     // err[T] != 0: a batch of more than 4 GiB
     uint64_t* off;                  // [3T+1] batch byte offsets
+    uint64_t* pinfo;                // [add entries] where the entry's properties field (tag, length,
+                                    // LinkProperties) lies: offset from the entry's start << 32 | its
+                                    // length — the RemotePod writer copies those bytes (same field 7)
 };
 // ---- tc argv synthesis (kdtn_tc.hip) ---------------------------------------------------
 struct TcIn {
@@ -458,6 +461,13 @@ struct RemoteIn {
     StrTab kd, pd;
     const uint32_t* add_coarse;     // k_list_coarse of add_off (or null)
     const uint32_t* kd_offs;        // physical peers: TrimPrefix(PeerPod, "physical/") from the arena
+    // the run's wire encoding (kdtn_epoch_encode), or w_pinfo = null: an add entry whose AddLinks
+    // batch marshalled has its properties field at w_pos[w_nd + e] + (w_pinfo[e] >> 32)
+    const uint64_t* w_pinfo;
+    const uint64_t* w_pos;
+    const uint8_t* w_arena;
+    const uint32_t* w_err;
+    uint32_t w_nd;
     const uint32_t* t_ns;
     const uint32_t* t_src;
     const uint32_t* t_netns;
@@ -591,9 +601,9 @@ __global__ void k_vni_contest(const uint4* add_ops, uint32_t n_ops, const uint4*
                               uint32_t dmask, uint32_t* flag);
 __global__ void k_vni_contest_write(const uint4* add_ops, const uint32_t* flag, const uint64_t* pos, uint32_t n_ops,
                                     uint32_t* node, int32_t* vni);
-__global__ void k_fan_nodes_count(const uint32_t* mark, uint32_t nd, uint32_t stamp, uint64_t* part);
-__global__ void k_fan_nodes_write(const uint32_t* mark, uint32_t nd, uint32_t stamp, const uint64_t* part,
-                                  uint32_t* node_idx, uint32_t* nodes, uint32_t* n_nodes);
+__global__ void k_fan_nodes_count(const uint32_t* mark, uint32_t nw, uint64_t* part);
+__global__ void k_fan_nodes_write(const uint32_t* mark, uint32_t nw, const uint64_t* part, uint32_t* node_idx,
+                                  uint32_t* nodes, uint32_t* n_nodes);
 __global__ void k_fan_count(FanIn f, const uint8_t* send, const uint32_t* node_idx, const uint32_t* n_nodes,
                             uint32_t* counts, uint32_t nchunks);
 __global__ void k_fan_scatter(FanIn f, const uint8_t* send, const uint32_t* node_idx, const uint32_t* n_nodes,

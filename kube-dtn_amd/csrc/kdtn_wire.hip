@@ -117,9 +117,11 @@ KD_INLINE uint32_t vlen(uint64_t v) {
 }
 KD_INLINE uint32_t str_field(uint32_t len) { return len ? 1u + vlen(len) + len : 0u; }
 
-// pb.LinkProperties size (psz) and pb.Link size (lsz) of record j from the length bytes; false
-// if a string is not valid UTF-8
-KD_INLINE bool link_sizes(const WireIn& w, const DevLinks& L, uint32_t j, uint32_t* psz, uint32_t* lsz) {
+// pb.LinkProperties size (psz) and pb.Link size (lsz) of record j from the length bytes, and the
+// bytes of the Link's fields before its properties (pre: fields 1-6); false if a string is not
+// valid UTF-8
+KD_INLINE bool link_sizes(const WireIn& w, const DevLinks& L, uint32_t j, uint32_t* psz, uint32_t* lsz,
+                          uint32_t* pre) {
     uint32_t kid[KDTN_NKEY], pid[KDTN_NPROP];
 #pragma unroll
     for (int k = 0; k < KDTN_NKEY; ++k) kid[k] = L.key(k, j);
@@ -131,10 +133,16 @@ KD_INLINE bool link_sizes(const WireIn& w, const DevLinks& L, uint32_t j, uint32
 #pragma unroll
     for (int k = 0; k < KDTN_NPROP; ++k) p += str_field(si_len<SI_PW>(w.pd, pid[k], bad));
     if (gap) p += 1u + vlen(gap);
+    uint32_t macs = 0;
 #pragma unroll
-    for (int k = 0; k < KDTN_NKEY; ++k) l += str_field(si_len<SI_KW>(w.kd, kid[k], bad));
+    for (int k = 0; k < KDTN_NKEY; ++k) {
+        const uint32_t f = str_field(si_len<SI_KW>(w.kd, kid[k], bad));
+        if (k == KDTN_K_LOCAL_MAC || k == KDTN_K_PEER_MAC) macs += f;
+        else l += f;
+    }
     if (uid) l += 1u + vlen((uint64_t)uid);
-    l += 1u + vlen(p) + p;
+    *pre = l;
+    l += 1u + vlen(p) + p + macs;
     *psz = p;
     *lsz = l;
     return bad == 0;
@@ -172,15 +180,18 @@ __global__ void __launch_bounds__(BLOCK) k_wire_entry_sizes(WireIn w, DevLinks O
             if (lst == l) t = tl;
         }
     if (!on) return;
-    uint32_t psz, lsz;
-    bool ok = link_sizes(w, lst == 0 ? O : N, w.list_idx[lst][e], &psz, &lsz);
-    uint32_t size = 1u + vlen(lsz) + lsz;
+    uint32_t psz, lsz, pre;
+    bool ok = link_sizes(w, lst == 0 ? O : N, w.list_idx[lst][e], &psz, &lsz, &pre);
+    uint32_t size = 1u + vlen(lsz) + lsz, hdr = 0;
     if (e == w.list_off[lst][t]) {                         // the batch's first entry carries the header
         bool pok;
         const uint32_t ps = pod_size(w, t, &pok);
         ok = ok && pok;
-        size += 1u + vlen(ps) + ps;
+        hdr = 1u + vlen(ps) + ps;
+        size += hdr;
     }
+    if (lst == 1 && wk.pinfo)                              // the AddLinks entry's properties field
+        wk.pinfo[e] = ((uint64_t)(hdr + 1u + vlen(lsz) + pre) << 32) | (1u + vlen(psz) + psz);
     wk.size[g] = ok ? size : 0u;
     wk.topo[g] = t;
     if (!ok) atomicOr(wk.err + t, 1u << lst);
@@ -431,6 +442,8 @@ struct RemoteMsg {
     uint32_t gap;
     int32_t vni;
     bool phys;                      // peer_vtep = TrimPrefix(PeerPod, "physical/")
+    uint32_t plen;                  // > 0: the properties field's bytes are the wire encoding's, at
+    uint64_t psrc;                  // w_arena + psrc (its batch marshalled: every string valid)
 };
 
 KD_INLINE RemoteMsg remote_msg(const RemoteIn& r, uint32_t e, uint32_t t, bool remote) {
@@ -451,19 +464,31 @@ KD_INLINE RemoteMsg remote_msg(const RemoteIn& r, uint32_t e, uint32_t t, bool r
     }
     q.s[4] = r.t_ns[t];                             // localPod.KubeNs
     q.s[5] = peer_pod;
-#pragma unroll
-    for (int k = 0; k < KDTN_NPROP; ++k) q.p[k] = r.N.prop(k, j);
-    q.gap = r.N.gap(j);
     q.vni = (int32_t)res.y;
     q.phys = !remote;
+    q.plen = 0;
+    q.psrc = 0;
+    if (r.w_pinfo && !((r.w_err[t] >> 1) & 1u)) {   // the run's AddLinks batch of t marshalled
+        const uint64_t pi = r.w_pinfo[e];
+        q.psrc = r.w_pos[r.w_nd + e] + (pi >> 32);
+        q.plen = (uint32_t)pi;
+    }
+    q.gap = 0;
+#pragma unroll
+    for (int k = 0; k < KDTN_NPROP; ++k) q.p[k] = 0;
+    if (!q.plen) {                                  // the property strings themselves
+#pragma unroll
+        for (int k = 0; k < KDTN_NPROP; ++k) q.p[k] = r.N.prop(k, j);
+        q.gap = r.N.gap(j);
+    }
     return q;
 }
 
 // message body size from the string lengths (the trimmed peer_vtep of a physical message is 9
 // bytes shorter; "physical/" is ASCII, so it is valid UTF-8 iff the whole name is); false if a
 // string is not valid UTF-8 (Marshal fails)
-KD_INLINE bool remote_sizes(const RemoteIn& r, const RemoteMsg& q, uint32_t* body, uint32_t* psz) {
-    uint32_t n = 0, p = 0, bad = 0;
+KD_INLINE bool remote_sizes(const RemoteIn& r, const RemoteMsg& q, uint32_t* body) {
+    uint32_t n = 0, bad = 0;
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
         uint32_t l = si_len<SI_KW>(r.kd, q.s[k], bad);
@@ -471,11 +496,16 @@ KD_INLINE bool remote_sizes(const RemoteIn& r, const RemoteMsg& q, uint32_t* bod
         n += str_field(l);
     }
     if (q.vni) n += 1u + vlen((uint64_t)(int64_t)q.vni);
+    if (q.plen) {                                   // the wire encoding's properties field
+        n += q.plen;
+    } else {
+        uint32_t p = 0;
 #pragma unroll
-    for (int k = 0; k < KDTN_NPROP; ++k) p += str_field(si_len<SI_PW>(r.pd, q.p[k], bad));
-    if (q.gap) p += 1u + vlen(q.gap);
-    *psz = p;
-    *body = n + 1u + vlen(p) + p;
+        for (int k = 0; k < KDTN_NPROP; ++k) p += str_field(si_len<SI_PW>(r.pd, q.p[k], bad));
+        if (q.gap) p += 1u + vlen(q.gap);
+        n += 1u + vlen(p) + p;
+    }
+    *body = n;
     return bad == 0;
 }
 
@@ -509,8 +539,8 @@ __global__ void __launch_bounds__(BLOCK) k_remote_sizes(RemoteIn r, uint32_t* ms
     const uint32_t t = entry_topo_wave_c(r.add_off, r.add_coarse, r.T, e, kind != 0);
     if (!kind) return;
     const RemoteMsg q = remote_msg(r, e, t, kind == 1);
-    uint32_t body, psz;
-    const bool ok = remote_sizes(r, q, &body, &psz);
+    uint32_t body;
+    const bool ok = remote_sizes(r, q, &body);
     const uint32_t m = remote_msg_index(r, e, kind);
     msz[m] = ok ? vlen(body) + body : 0u;
     tsz[m] = kind == 1 ? tc_size(r.kd, tc_remote_entry(r, e)) : 0u;
@@ -528,9 +558,10 @@ KD_INLINE void arena_field(WSink& o, uint32_t field, const uint8_t* arena, uint3
     o.str(arena, b, len);
 }
 
-// the message's bytes: the key strings' entries and the property strings' length bytes
-// gathered at once, then the fields in number order (the property entries gathered after the
-// key fields are written, as in write_entry)
+// the message's bytes: the key strings' entries gathered at once, then the fields in number
+// order; the properties field copied from the wire encoding when the run has one for the entry
+// (q.plen), else from the property strings' length bytes and entries (gathered after the key
+// fields are written, as in write_entry)
 KD_INLINE void write_remote(WSink& o, const RemoteIn& r, const RemoteMsg& q) {
     SIE<SI_KW> s[6];
 #pragma unroll
@@ -544,10 +575,15 @@ KD_INLINE void write_remote(WSink& o, const RemoteIn& r, const RemoteMsg& q) {
 #pragma unroll
     for (int k = 0; k < 6; ++k) n += str_field(k == 3 && q.phys ? vl : si_elen(s[k]));
     if (q.vni) n += 1u + vlen((uint64_t)(int64_t)q.vni);
+    if (q.plen) {
+        n += q.plen;
+    } else {
 #pragma unroll
-    for (int k = 0; k < KDTN_NPROP; ++k) psz += str_field(si_len<SI_PW>(r.pd, q.p[k], bad));
-    if (q.gap) psz += 1u + vlen(q.gap);
-    o.varint(n + 1u + vlen(psz) + psz);
+        for (int k = 0; k < KDTN_NPROP; ++k) psz += str_field(si_len<SI_PW>(r.pd, q.p[k], bad));
+        if (q.gap) psz += 1u + vlen(q.gap);
+        n += 1u + vlen(psz) + psz;
+    }
+    o.varint(n);
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
         if (k == 3 && q.phys) arena_field(o, 4u, r.kd.bytes, vb, vl);
@@ -557,18 +593,22 @@ KD_INLINE void write_remote(WSink& o, const RemoteIn& r, const RemoteMsg& q) {
         o.byte(6u << 3);
         o.varint((uint64_t)(int64_t)q.vni);
     }
-    o.byte(7u << 3 | 2u);
-    o.varint(psz);
-    SIE<SI_PW> p[KDTN_NPROP];
+    if (q.plen) {
+        o.copy(r.w_arena, q.psrc, q.plen);
+    } else {
+        o.byte(7u << 3 | 2u);
+        o.varint(psz);
+        SIE<SI_PW> p[KDTN_NPROP];
 #pragma unroll
-    for (int k = 0; k < KDTN_NPROP; ++k) p[k] = si_load<SI_PW>(r.pd, q.p[k]);
+        for (int k = 0; k < KDTN_NPROP; ++k) p[k] = si_load<SI_PW>(r.pd, q.p[k]);
 #pragma unroll
-    for (int k = 0; k < KDTN_NPROP; ++k) {
-        if (k == KDTN_P_DUPLICATE && q.gap) {
-            o.byte(7u << 3);
-            o.varint(q.gap);
+        for (int k = 0; k < KDTN_NPROP; ++k) {
+            if (k == KDTN_P_DUPLICATE && q.gap) {
+                o.byte(7u << 3);
+                o.varint(q.gap);
+            }
+            si_field(o, (uint32_t)(k < KDTN_P_DUPLICATE ? k + 1 : k + 2), p[k], r.pd.bytes);
         }
-        si_field(o, (uint32_t)(k < KDTN_P_DUPLICATE ? k + 1 : k + 2), p[k], r.pd.bytes);
     }
     si_field(o, 8, s[5], r.kd.bytes);
 }
@@ -577,7 +617,7 @@ KD_INLINE void write_remote(WSink& o, const RemoteIn& r, const RemoteMsg& q) {
 // writing the message at its fan-out position. A wave's messages for one daemon are one
 // contiguous run of the arena (fan-out order keeps add-list order within a daemon), so the
 // wave stores them through its LDS image dword by dword (wave_segments_write).
-__global__ void __launch_bounds__(BLOCK) k_remote_write(RemoteIn r, const uint64_t* off, uint8_t* arena) {
+__global__ void __launch_bounds__(BLOCK, 4) k_remote_write(RemoteIn r, const uint64_t* off, uint8_t* arena) {
     __shared__ uint32_t img[BLOCK / 64][REMOTE_IMG / 4];
     const uint32_t e = blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t kind = e < r.n_add ? remote_kind(r, e) : 0u;

@@ -418,8 +418,10 @@ def test_remote_fanout_grouping(engine):
     assert _fanout_same(engine, synth.make(4, pods_per_shard=5000), "config 4") > 1000
 
 
-def _remote_same(engine, inp, ctx):
+def _remote_same(engine, inp, ctx, encode_first=False):
     out = engine.reconcile(inp)
+    if encode_first:            # the run's wire encoding supplies the properties fields
+        engine.encode()
     got = engine.remote_pods()
     want = O.remote_epoch(inp, O.reconcile(inp, tick=TICK))
     names = ("arena", "off", "entry", "n_remote", "tc", "tc_off")
@@ -443,6 +445,20 @@ def test_remote_pod_messages(engine):
     nr, _ = _remote_same(engine, synth.make(2, pods_per_shard=20000), "config 2")
     assert nr > 100000
     nr, nph = _remote_same(engine, synth.make(4, pods_per_shard=5000), "config 4")
+    assert nr > 1000 and nph > 0
+
+
+def test_remote_pod_messages_after_wire_encoding(engine):
+    """The same with the run's wire encoding done first: each message's properties field is
+    copied from its AddLinks entry's Link bytes, except in batches that failed to marshal
+    (invalid UTF-8: those messages take their strings), bit-exact against the oracle."""
+    from helpers import wire_epoch_input
+    for seed in range(4):
+        _remote_same(engine, wire_epoch_input(seed, T=120)[1], f"wire seed {seed}", encode_first=True)
+        _remote_same(engine, random_epoch_input(seed + 40, T=150, p_err=0.1)[1], f"seed {seed}", encode_first=True)
+    nr, _ = _remote_same(engine, synth.make(2, pods_per_shard=20000), "config 2", encode_first=True)
+    assert nr > 100000
+    nr, nph = _remote_same(engine, synth.make(4, pods_per_shard=5000), "config 4", encode_first=True)
     assert nr > 1000 and nph > 0
 
 
