@@ -365,16 +365,13 @@ KD_INLINE void wave_image_write(uint32_t* img, bool on, uint64_t s0, uint64_t s1
 // lanes (the range assembly then runs twice at half the lanes: round 2 measured 2x the VALU
 // instructions of a one-round wave), and a round larger than the image goes straight to global
 // memory. Every lane must call it.
-template <int NL> constexpr int seg_meta() { return 4 * NL + 1; }   // dwords of slot metadata
+template <int NL> constexpr int seg_meta() { return 4 * NL; }   // dwords of slot metadata (a uint4 per slot)
 template <int NL, int R, int IMGB, typename F>
 KD_INLINE void wave_segments_round(uint32_t* img, bool on, uint64_t s0, uint32_t len, uint32_t ndw, uint8_t* arena,
                                    F& body) {
     const int lane = threadIdx.x & 63;
     constexpr int META = seg_meta<NL>();
-    uint32_t* mq = img + IMGB / 4 - META;       // [NL + 1] slot starts (dwords), then per slot: dst lo, hi, lead|len
-    uint32_t* mlo = mq + NL + 1;
-    uint32_t* mhi = mlo + NL;
-    uint32_t* mll = mhi + NL;
+    uint4* ms = reinterpret_cast<uint4*>(img + IMGB / 4 - META);   // per slot {start dword, dst lo, hi, lead | len << 2}
     constexpr uint32_t budget = IMGB / 4 - META;
     const uint32_t lead = (uint32_t)s0 & 3u;
     const bool mine = NL == 64 || (lane >> 5) == R;
@@ -391,12 +388,7 @@ KD_INLINE void wave_segments_round(uint32_t* img, bool on, uint64_t s0, uint32_t
     if (total == 0) return;                                      // wave-uniform
     const bool direct = total > budget;                          // too large: straight to global memory
     const int sl = NL == 64 ? lane : lane - 32 * R;
-    if (mine && !direct) {
-        mq[sl] = qi;
-        mlo[sl] = (uint32_t)(s0 & ~3ull);
-        mhi[sl] = (uint32_t)(s0 >> 32);
-        mll[sl] = lead | (len << 2);
-    }
+    if (mine && !direct) ms[sl] = make_uint4(qi, (uint32_t)(s0 & ~3ull), (uint32_t)(s0 >> 32), lead | (len << 2));
     if (mine && on) {                                            // one call site of the body
         WSink o;
         if (direct) o.init(arena + s0);
@@ -409,17 +401,18 @@ KD_INLINE void wave_segments_round(uint32_t* img, bool on, uint64_t s0, uint32_t
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // whole dwords, consecutive lanes on consecutive dwords of each slot ...
-    for (uint32_t q = lane; q < total; q += 64) {
-        int i = 0;                                               // the last slot starting at or before q
-#pragma unroll
-        for (int step = NL / 2; step >= 1; step >>= 1)
-            if (i + step < NL && mq[i + step] <= q) i += step;
-        const uint32_t k = q - mq[i], ll = mll[i];
-        const uint32_t ld = ll & 3u, end = ld + (ll >> 2);      // valid bytes of the slot: [ld, end)
-        if ((k == 0 && ld != 0) || 4u * k + 4u > end) continue;  // an edge dword: below
-        uint8_t* dst = arena + ((((uint64_t)mhi[i]) << 32) | mlo[i]) + 4ull * k;
-        *reinterpret_cast<uint32_t*>(dst) = img[q];
+    // whole dwords: lanes 0-31 copy slot 2k, lanes 32-63 slot 2k + 1, 32 consecutive dwords a
+    // step (a slot of ~31 dwords takes one step; per dword a binary search over the slot starts
+    // cost six LDS reads) ...
+    const uint32_t half = (uint32_t)lane >> 5, hl = (uint32_t)lane & 31u;
+    for (int k = 0; k < NL; k += 2) {
+        const uint4 m = ms[k + half];
+        const uint32_t ld = m.w & 3u, end = ld + (m.w >> 2), nd = (end + 3u) >> 2;   // bytes [ld, end)
+        uint8_t* base = arena + ((((uint64_t)m.z) << 32) | m.y);
+        for (uint32_t kk = hl; kk < nd; kk += 32u) {
+            if ((kk == 0 && ld != 0) || 4u * kk + 4u > end) continue;   // an edge dword: below
+            *reinterpret_cast<uint32_t*>(base + 4ull * kk) = img[m.x + kk];
+        }
     }
     // ... then every lane its own slot's partial first and last dwords, by bytes (the dwords it
     // shares with the neighbouring ranges): at most eight byte stores per lane, instead of four
@@ -461,10 +454,21 @@ KD_INLINE void wave_segments_write(uint32_t* img, bool on, uint64_t s0, uint64_t
 }
 
 // ---- tc argv (kdtn_tc.hip: kdtn_epoch_tc; kdtn_wire.hip: the receiving daemons' commands) ----
+// decimal digits of v: compares against the powers of ten, no division (a u64 division loop
+// per digit was most of the tc kernels' VALU)
 KD_INLINE uint32_t ndigits(uint64_t v) {
     uint32_t n = 1;
-    while (v >= 10u) { v /= 10u; ++n; }
+    uint64_t p = 10u;
+#pragma unroll
+    for (int k = 1; k < 20; ++k) {
+        n += v >= p ? 1u : 0u;
+        p *= 10u;
+    }
     return n;
+}
+KD_INLINE uint32_t ndigits32(uint32_t v) {
+    return 1u + (v >= 10u) + (v >= 100u) + (v >= 1000u) + (v >= 10000u) + (v >= 100000u) + (v >= 1000000u) +
+           (v >= 10000000u) + (v >= 100000000u) + (v >= 1000000000u);
 }
 // fixed argument bytes: "qdisc add dev " + " parent 1:1 handle 10:0 tbf rate " + " burst " +
 // " latency 50ms minburst " + final NUL (every separator is a NUL)
@@ -480,8 +484,8 @@ struct TcEntry {
 // bytes of a TBF command's argv (0 when it runs none)
 KD_INLINE uint32_t tc_size(const StrTab& kd, const TcEntry& t) {
     uint32_t bad = 0;                                      // argv bytes need no UTF-8
-    return t.on ? TC_FIXED + si_len<SI_KW>(kd, t.intf, bad) + ndigits(t.rate) + ndigits(t.buffer) +
-                      ndigits(t.minburst)
+    return t.on ? TC_FIXED + si_len<SI_KW>(kd, t.intf, bad) + ndigits(t.rate) + ndigits32(t.buffer) +
+                      ndigits32(t.minburst)
                 : 0u;
 }
 
@@ -504,17 +508,27 @@ KD_INLINE uint32_t dig4(uint32_t l) {
 }
 // fmt.Sprint of an unsigned integer + NUL: base-10000 limbs, the top one without leading zeros
 KD_INLINE void num(WSink& o, uint64_t v) {
-    const uint32_t l0 = (uint32_t)(v % 10000u);
-    v /= 10000u;
-    const uint32_t l1 = (uint32_t)(v % 10000u);
-    v /= 10000u;
-    const uint32_t l2 = (uint32_t)(v % 10000u);
-    v /= 10000u;
-    const uint32_t l3 = (uint32_t)(v % 10000u);
-    const uint32_t l4 = (uint32_t)(v / 10000u);          // < 1845 (2^64 < 10^20)
+    uint32_t l0, l1, l2, l3, l4;
+    if (v >> 32) {                                      // u64 divisions only above 2^32
+        l0 = (uint32_t)(v % 10000u);
+        v /= 10000u;
+        l1 = (uint32_t)(v % 10000u);
+        v /= 10000u;
+        l2 = (uint32_t)(v % 10000u);
+        v /= 10000u;
+        l3 = (uint32_t)(v % 10000u);
+        l4 = (uint32_t)(v / 10000u);                    // < 1845 (2^64 < 10^20)
+    } else {                                            // u32: divisions by constants are multiplies
+        uint32_t x = (uint32_t)v;
+        l0 = x % 10000u;
+        x /= 10000u;
+        l1 = x % 10000u;
+        l2 = x / 10000u;                                // < 43
+        l3 = l4 = 0u;
+    }
     const int k = l4 ? 4 : l3 ? 3 : l2 ? 2 : l1 ? 1 : 0;
     const uint32_t top = k == 4 ? l4 : k == 3 ? l3 : k == 2 ? l2 : k == 1 ? l1 : l0;
-    const uint32_t nd = ndigits(top);
+    const uint32_t nd = ndigits32(top);
     o.put(dig4(top) >> (8u * (4u - nd)), nd);
     if (k >= 4) o.put(dig4(l3), 4u);
     if (k >= 3) o.put(dig4(l2), 4u);

@@ -539,11 +539,12 @@ __global__ void __launch_bounds__(BLOCK) k_remote_sizes(RemoteIn r, uint32_t* ms
     const uint32_t t = entry_topo_wave_c(r.add_off, r.add_coarse, r.T, e, kind != 0);
     if (!kind) return;
     const RemoteMsg q = remote_msg(r, e, t, kind == 1);
+    const uint32_t ts = kind == 1 ? tc_size(r.kd, tc_remote_entry(r, e)) : 0u;   // (its loads before the stores)
     uint32_t body;
     const bool ok = remote_sizes(r, q, &body);
     const uint32_t m = remote_msg_index(r, e, kind);
     msz[m] = ok ? vlen(body) + body : 0u;
-    tsz[m] = kind == 1 ? tc_size(r.kd, tc_remote_entry(r, e)) : 0u;
+    tsz[m] = ts;
 }
 
 // a string field from arena bytes [b, b + len) (nothing for "")
