@@ -2462,24 +2462,25 @@ static int json_decode(kdtn_ctx* c, const JsTargets& tg, JsCounts* o, kdtn_inges
     TRY(ensure(c->j_vlist, (size_t)nval * 4));
     const uint32_t nscal = (uint32_t)nscal64;
     TRY(ensure(c->j_slist, (size_t)nscal * 4 + 4));
-    const uint2* toks = dp<uint2>(c->j_toks);
+    const JsToks tk{dp<uint32_t>(c->j_toks), dp<uint32_t>(c->j_toks) + ntok};   // offsets, then meta words
     uint32_t* par = dp<uint32_t>(c->j_par);
-    k_js_tokens<<<nwg, BLOCK, 0, s>>>(j, m, goff, nwg, dp<uint2>(c->j_toks), dp<uint32_t>(c->j_olist), dp<uint8_t>(c->j_odep),
+    k_js_tokens<<<nwg, BLOCK, 0, s>>>(j, m, goff, nwg, tk, dp<uint32_t>(c->j_olist), dp<uint8_t>(c->j_odep),
                                              dp<uint32_t>(c->j_vlist), dp<uint32_t>(c->j_slist), small);
     timer_mark(c, "js_tokens");
     const uint32_t ntiles = (ntok + JS_TILE - 1) / JS_TILE, ng = (ntiles + BLOCK - 1) / BLOCK;
     TRY(ensure(c->j_tagg, (size_t)ntiles * JS_PD * 4));
     TRY(ensure(c->j_gagg, (size_t)ng * JS_PD * 4));
-    k_js_par_agg<<<ntiles, BLOCK, 0, s>>>(toks, ntok, dp<uint32_t>(c->j_tagg));
+    k_js_par_agg<<<ntiles, BLOCK, 0, s>>>(tk.meta, ntok, dp<uint32_t>(c->j_tagg));
     k_js_par_group<<<ng, BLOCK, 0, s>>>(dp<uint32_t>(c->j_tagg), ntiles, dp<uint32_t>(c->j_gagg));
     k_js_par_top<<<1, BLOCK, 0, s>>>(dp<uint32_t>(c->j_gagg), ng);
     k_js_par_tiles<<<ng, BLOCK, 0, s>>>(dp<uint32_t>(c->j_tagg), ntiles, dp<uint32_t>(c->j_gagg));
     uint32_t* deep = reinterpret_cast<uint32_t*>(small + 4);   // zeroed with the small words above
-    k_js_par_apply<<<ntiles, BLOCK, 0, s>>>(toks, ntok, dp<uint32_t>(c->j_tagg), par, deep);
-    k_js_deep<<<std::min<uint32_t>(nblocks(ntok), 2048), BLOCK, 0, s>>>(toks, ntok, par, deep);
+    k_js_par_apply<<<ntiles, BLOCK, 0, s>>>(tk.meta, ntok, dp<uint32_t>(c->j_tagg), par, deep);
+    k_js_deep<<<std::min<uint32_t>(nblocks(ntok), 2048), BLOCK, 0, s>>>(tk.meta, ntok, par, deep);
     timer_mark(c, "js_parents");
-    k_js_validate<<<nblocks(ntok), BLOCK, 0, s>>>(j, toks, ntok, par, dp<uint8_t>(c->j_ecls), small);
-    if (nscal) k_js_scalars<<<nblocks(nscal), BLOCK, 0, s>>>(j, toks, dp<uint32_t>(c->j_slist), nscal, small);
+    k_js_validate<<<nblocks(ntok), BLOCK, 0, s>>>(j, tk, ntok, par, dp<uint8_t>(c->j_ecls), small);
+    k_js_tail<<<1, 64, 0, s>>>(j, tk, ntok, par, small);
+    if (nscal) k_js_scalars<<<nblocks(nscal), BLOCK, 0, s>>>(j, tk.pos, dp<uint32_t>(c->j_slist), nscal, small);
     timer_mark(c, "js_validate");
     TRY(d2h(c, &serr, small));
     HIP_TRY(hipStreamSynchronize(s));
@@ -2492,14 +2493,14 @@ static int json_decode(kdtn_ctx* c, const JsTargets& tg, JsCounts* o, kdtn_inges
     uint32_t* ord = dp<uint32_t>(c->j_ord);
     HIP_TRY(hipMemsetAsync(role, 0, ntok, s));                  // R_NONE below the schema levels
     for (uint32_t level : {0u, 1u, 3u, 4u})            // levels 2 and 5: k_js_elems_count
-        if (nopen) k_js_roles<<<nblocks(nopen), BLOCK, 0, s>>>(j, toks, dp<uint32_t>(c->j_olist), nopen, par, role,
+        if (nopen) k_js_roles<<<nblocks(nopen), BLOCK, 0, s>>>(j, tk, dp<uint32_t>(c->j_olist), nopen, par, role,
                                                     dp<uint8_t>(c->j_odep), level);
     TRY(ensure(c->j_cnt3, (size_t)3 * ntiles * 4));
     TRY(ensure(c->j_coff3, (size_t)3 * (ntiles + 1) * 8));
-    k_js_elems_count<<<ntiles, BLOCK, 0, s>>>(j, toks, ntok, par, role, dp<uint32_t>(c->j_cnt3),
+    k_js_elems_count<<<ntiles, BLOCK, 0, s>>>(j, tk, ntok, par, role, dp<uint32_t>(c->j_cnt3),
                                               dp<uint8_t>(c->j_ecls), small + 1);
     if (nopen)                                          // properties objects, under the links elements
-        k_js_roles<<<nblocks(nopen), BLOCK, 0, s>>>(j, toks, dp<uint32_t>(c->j_olist), nopen, par, role,
+        k_js_roles<<<nblocks(nopen), BLOCK, 0, s>>>(j, tk, dp<uint32_t>(c->j_olist), nopen, par, role,
                                                     dp<uint8_t>(c->j_odep), 6u);
     for (int q = 0; q < 3; ++q)
         TRY(scan_u32(c, dp<uint32_t>(c->j_cnt3) + (size_t)q * ntiles, ntiles,
@@ -2586,14 +2587,14 @@ static int json_decode(kdtn_ctx* c, const JsTargets& tg, JsCounts* o, kdtn_inges
         in.kd = JsDict{dp<JsSlot>(c->j_kslots), dp<unsigned long long>(c->j_kkeys), dp<uint32_t>(c->j_krep), kcap - 1};
         in.pd = JsDict{dp<JsSlot>(c->j_pslots), dp<unsigned long long>(c->j_pkeys), dp<uint32_t>(c->j_prep), pcap - 1};
         if (nval)
-            k_js_values<<<nblocks(nval), BLOCK, 0, s>>>(j, toks, dp<uint32_t>(c->j_vlist), nval, par, role, ord, to,
+            k_js_values<<<nblocks(nval), BLOCK, 0, s>>>(j, tk, dp<uint32_t>(c->j_vlist), nval, par, role, ord, to,
                                                         des, real, in, small + 1);
         if (nval && !(KDTN_PROFILING && (in.variant & JSV_NO_SEEN))) {
             uint32_t* any_dup = reinterpret_cast<uint32_t*>(small + 5);   // zeroed with the small words
-            k_js_dups<<<nblocks(nval), BLOCK, 0, s>>>(toks, dp<uint32_t>(c->j_vlist), nval, dp<uint32_t>(c->j_vown),
+            k_js_dups<<<nblocks(nval), BLOCK, 0, s>>>(dp<uint32_t>(c->j_vlist), nval, dp<uint32_t>(c->j_vown),
                                                       dp<uint32_t>(c->j_owner), any_dup);
             k_js_dups_report<<<std::min<uint32_t>(nblocks(nval), 2048), BLOCK, 0, s>>>(
-                toks, dp<uint32_t>(c->j_vlist), nval, dp<uint32_t>(c->j_vown), dp<uint32_t>(c->j_owner), any_dup,
+                tk.pos, dp<uint32_t>(c->j_vlist), nval, dp<uint32_t>(c->j_vown), dp<uint32_t>(c->j_owner), any_dup,
                 small + 1);
         }
         timer_mark(c, "js_values");

@@ -234,11 +234,11 @@ KD_INLINE void classify_block(const JsDoc& j, uint32_t b, uint64_t quote, bool S
         }
         if (bad) js_fail(err, b * 64 + (__ffsll((long long)bad) - 1), KDTN_JSON_SYNTAX);
     }
-    m.tok[b] = tok;
+    m.tok[b] = tok;                                        // (with the separators: k_js_tokens tells them apart)
     m.open[b] = op & out;
     m.close[b] = cl & out;
-    *pa = (uint64_t)__popcll(tok) | (uint64_t)__popcll(op & out) << 16 | (uint64_t)__popcll(colon & out) << 32 |
-          (uint64_t)__popcll(scalar_start) << 48;
+    *pa = (uint64_t)__popcll(tok & ~(pun & out)) | (uint64_t)__popcll(op & out) << 16 |
+          (uint64_t)__popcll(colon & out) << 32 | (uint64_t)__popcll(scalar_start) << 48;
     *pd = 64u + __popcll(op & out) - __popcll(cl & out);
 }
 
@@ -275,32 +275,58 @@ KD_INLINE uint32_t select_bit(uint64_t m, uint32_t r) {
     return pos;
 }
 
+KD_INLINE bool is_ws(uint32_t c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
+
+// The separators between a token at pos and the previous one, from the bytes before pos: only
+// whitespace, ',' and ':' lie between two tokens (every other byte outside a string starts or
+// ends a token), so a backward scan needs no string state. Returns SEP_* of the earliest
+// separator (SEP_NONE: none) and, in *second, the position of the second separator in document
+// order (0xFFFFFFFF: fewer than two). byte(q) reads the document.
+template <typename B>
+KD_INLINE uint32_t sep_before(uint32_t pos, uint32_t* second, B&& byte) {
+    uint32_t q = pos, kind = SEP_NONE, p1 = 0xFFFFFFFFu, p2 = 0xFFFFFFFFu;
+    while (q > 0) {
+        const uint32_t c = byte(q - 1);
+        if (is_ws(c)) { --q; continue; }
+        if (c != ':' && c != ',') break;
+        p2 = p1;                                           // (found in reverse document order)
+        p1 = q - 1;
+        kind = c == ':' ? SEP_COLON : SEP_COMMA;
+        --q;
+    }
+    *second = p2;
+    return kind;
+}
+
 // Token writer. Each lane owns one 64-byte block (its bytes go to LDS, its masks and offsets
-// to per-lane LDS slots); the wave's tokens are contiguous in toks[], so the wave writes them
+// to per-lane LDS slots); the wave's tokens are contiguous in the stream, so the wave writes them
 // round by round, lane l taking the wave's token r = round * 64 + l (owner block by binary
-// search over the wave's token prefix, bit by select): coalesced 8-byte stores instead of
-// every lane walking its own block's tokens into its own region.
+// search over the wave's token prefix, bit by select): coalesced 4-byte stores instead of
+// every lane walking its own block's tokens into its own region. The ',' and ':' bytes are no
+// tokens (m.tok holds them; they are told apart here): a token records the separator before it
+// (sep_before), and each member value's index comes from its colon (the number of tokens before
+// the colon), written by a second loop over the wave's colons.
 __global__ void __launch_bounds__(BLOCK) k_js_tokens(JsDoc j, JsMasks m, const uint64_t* goff, uint32_t ng,
-                                                     uint2* toks, uint32_t* olist, uint8_t* odep, uint32_t* vlist,
+                                                     JsToks tk, uint32_t* olist, uint8_t* odep, uint32_t* vlist,
                                                      uint32_t* slist, unsigned long long* err) {
     __shared__ uint4 blk[BLOCK * 4];
     __shared__ uint64_t stok[BLOCK], sop[BLOCK], scl[BLOCK], scol[BLOCK], ssc[BLOCK];
     __shared__ int64_t sd0[BLOCK];
-    __shared__ uint32_t sex[BLOCK], soo[BLOCK], sco[BLOCK], sso[BLOCK];
+    __shared__ uint32_t sex[BLOCK], soo[BLOCK], sco[BLOCK], sso[BLOCK], scx[BLOCK];
     __shared__ uint64_t shs[BLOCK / 64];
     const uint32_t lane = threadIdx.x & 63u, w0 = threadIdx.x & ~63u;
     const uint32_t b = blockIdx.x * BLOCK + threadIdx.x;
-    uint64_t tok = 0, pa = 0, pd = 0;
+    uint64_t tok = 0, pa = 0, pd = 0, colm = 0;
     if (b < j.nb) {
         const uint4* p = reinterpret_cast<const uint4*>(j.doc + (size_t)b * 64);
         uint4 v[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] = p[q];
-        tok = m.tok[b];
+        const uint64_t tsep = m.tok[b];                  // tokens and the structural separators
         const uint64_t op = m.open[b], cl = m.close[b];
         sop[threadIdx.x] = op;
         scl[threadIdx.x] = cl;
-        uint64_t col = 0, nsc = 0;
+        uint64_t col = 0, cmm = 0, nsc = 0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             blk[threadIdx.x * 4 + q] = v[q];
@@ -308,15 +334,18 @@ __global__ void __launch_bounds__(BLOCK) k_js_tokens(JsDoc j, JsMasks m, const u
 #pragma unroll
             for (int h = 0; h < 4; ++h) {
                 const uint32_t x = wd[h], lx = x | 0x20202020u;       // '[' → '{', ']' → '}'
-                const uint32_t cn = mm4(eqb(x, ':'));
+                const uint32_t cn = mm4(eqb(x, ':')), cm = mm4(eqb(x, ','));
                 col |= (uint64_t)cn << (4 * (q * 4 + h));
-                nsc |= (uint64_t)(cn | mm4(eqb(lx, '{') | eqb(lx, '}') | eqb(x, ',') | eqb(x, '"'))) << (4 * (q * 4 + h));
+                cmm |= (uint64_t)cm << (4 * (q * 4 + h));
+                nsc |= (uint64_t)(cn | cm | mm4(eqb(lx, '{') | eqb(lx, '}') | eqb(x, '"'))) << (4 * (q * 4 + h));
             }
         }
-        scol[threadIdx.x] = col & tok;                 // structural colons
-        ssc[threadIdx.x] = tok & ~nsc;                 // scalar token starts (the token's first byte)
+        colm = col & tsep;                               // structural colons
+        tok = tsep & ~(col | cmm);                       // the tokens
+        scol[threadIdx.x] = colm;
+        ssc[threadIdx.x] = tok & ~nsc;                   // scalar token starts (the token's first byte)
         // the block's counts, as k_js_classify summed them per workgroup
-        pa = (uint64_t)__popcll(tok) | (uint64_t)__popcll(op) << 16 | (uint64_t)__popcll(col & tok) << 32 |
+        pa = (uint64_t)__popcll(tok) | (uint64_t)__popcll(op) << 16 | (uint64_t)__popcll(colm) << 32 |
              (uint64_t)__popcll(tok & ~nsc) << 48;
         pd = 64u + __popcll(op) - __popcll(cl);
     }
@@ -331,17 +360,24 @@ __global__ void __launch_bounds__(BLOCK) k_js_tokens(JsDoc j, JsMasks m, const u
     sco[threadIdx.x] = (uint32_t)(goff[3 * G + g] + ((ea >> 32) & 0xFFFFu));
     sso[threadIdx.x] = (uint32_t)(goff[4 * G + g] + (ea >> 48));
     stok[threadIdx.x] = tok;
-    const uint32_t cnt = __popcll(tok);
-    uint32_t inc = cnt;
+    const uint32_t cnt = __popcll(tok), ccnt = __popcll(colm);
+    uint32_t inc = cnt, cinc = ccnt;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = __shfl_up(inc, d, 64);
-        if (lane >= (uint32_t)d) inc += o;
+        const uint32_t o = __shfl_up(inc, d, 64), oc = __shfl_up(cinc, d, 64);
+        if (lane >= (uint32_t)d) { inc += o; cinc += oc; }
     }
     sex[threadIdx.x] = inc - cnt;
-    const uint32_t wtot = __shfl(inc, 63, 64);
+    scx[threadIdx.x] = cinc - ccnt;
+    const uint32_t wtot = __shfl(inc, 63, 64), wcol = __shfl(cinc, 63, 64);
     const uint32_t base = (uint32_t)__shfl(ti, 0, 64);  // toff of the wave's first block
     __syncthreads();
+    // document bytes: the workgroup's blocks from LDS, others from global memory
+    const uint32_t wg0 = blockIdx.x * BLOCK * 64u;
+    const uint8_t* bytes = reinterpret_cast<const uint8_t*>(blk);
+    auto byte_at = [&](uint32_t q) -> uint32_t {
+        return (q >= wg0 && q - wg0 < BLOCK * 64u && (q >> 6) < j.nb) ? bytes[q - wg0] : j.doc[q];
+    };
     for (uint32_t r = lane; r < wtot; r += 64) {
         uint32_t L = 0;                                    // last lane with sex <= r
 #pragma unroll
@@ -358,19 +394,32 @@ __global__ void __launch_bounds__(BLOCK) k_js_tokens(JsDoc j, JsMasks m, const u
             js_fail(err, pos, KDTN_JSON_SYNTAX);      // a close with nothing open
             d = d < 0 ? 0 : d;
         }
+        uint32_t second;
+        const uint32_t sep = sep_before(pos, &second, byte_at);
+        if (second != 0xFFFFFFFFu) js_fail(err, second, KDTN_JSON_SYNTAX);   // two separators in a row
         const uint32_t idx = base + r;
         if (kind == TK_OBJ || kind == TK_ARR) {
             if (d >= 10000) js_fail(err, pos, KDTN_JSON_DEPTH);
             const uint32_t oi = soo[o] + __popcll(sop[o] & below);
             olist[oi] = idx;
             odep[oi] = (uint8_t)(d > 254 ? 255 : d);             // k_js_roles picks its level by this byte
-        } else if (kind == TK_COLON) {
-            vlist[sco[o] + __popcll(scol[o] & below)] = idx + 1;   // the member value follows its colon
         } else if (kind == TK_SCALAR) {
             slist[sso[o] + __popcll(ssc[o] & below)] = idx;         // checked by k_js_scalars
         }
         if (d > (int64_t)TK_DEPTH_MASK) d = TK_DEPTH_MASK;
-        toks[idx] = make_uint2(pos, (uint32_t)d | (kind << 24));
+        tk.pos[idx] = pos;
+        tk.meta[idx] = (uint32_t)d | (kind << 24) | (sep << 28);
+    }
+    // member values: the token after the k-th colon is token (tokens before the colon)
+    for (uint32_t r = lane; r < wcol; r += 64) {
+        uint32_t L = 0;                                    // last lane with scx <= r
+#pragma unroll
+        for (uint32_t st = 32; st >= 1; st >>= 1)
+            if (scx[w0 + L + st] <= r) L += st;
+        const uint32_t o = w0 + L;
+        const uint32_t k = select_bit(scol[o], r - scx[o]);
+        const uint64_t below = (1ull << k) - 1;
+        vlist[sco[o] + __popcll(scol[o] & below)] = base + sex[o] + __popcll(stok[o] & below);
     }
 }
 
@@ -378,11 +427,11 @@ __global__ void __launch_bounds__(BLOCK) k_js_tokens(JsDoc j, JsMasks m, const u
 // Per tile of JS_TILE tokens: lane d (0..JS_PD-1) = 1 + index of the last open bracket whose
 // post-depth is d + 1 (pre-depth d), 0 = none; combining is an element-wise max.
 KD_INLINE bool tk_open(uint32_t meta) {
-    const uint32_t k = meta >> 24;
+    const uint32_t k = (meta >> 24) & 0xFu;
     return k == TK_OBJ || k == TK_ARR;
 }
 
-__global__ void __launch_bounds__(BLOCK) k_js_par_agg(const uint2* toks, uint32_t ntok, uint32_t* tagg) {
+__global__ void __launch_bounds__(BLOCK) k_js_par_agg(const uint32_t* tmeta, uint32_t ntok, uint32_t* tagg) {
     __shared__ uint32_t sh[BLOCK * (JS_PD + 1)];
     uint32_t* row = sh + threadIdx.x * (JS_PD + 1);
 #pragma unroll
@@ -392,7 +441,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_par_agg(const uint2* toks, uint32_
     for (int q = 0; q < JS_PER; ++q) {
         const uint32_t i = t0 + q * BLOCK + threadIdx.x;
         if (i >= ntok) break;
-        const uint32_t meta = toks[i].y;
+        const uint32_t meta = tmeta[i];
         const uint32_t d = meta & TK_DEPTH_MASK;
         if (tk_open(meta) && d < JS_PD) row[d] = i + 1;
     }
@@ -501,7 +550,7 @@ KD_INLINE uint32_t wave_incl_max(uint32_t v) {
     return v;
 }
 
-__global__ void __launch_bounds__(BLOCK) k_js_par_apply(const uint2* toks, uint32_t ntok, const uint32_t* texcl,
+__global__ void __launch_bounds__(BLOCK) k_js_par_apply(const uint32_t* tmeta, uint32_t ntok, const uint32_t* texcl,
                                                         uint32_t* par, uint32_t* deep) {
     __shared__ uint32_t wt[BLOCK / 64][JS_PD];
     __shared__ uint32_t st[BLOCK * (JS_PD + 1)];
@@ -509,7 +558,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_par_apply(const uint2* toks, uint3
     const uint32_t t0 = blockIdx.x * JS_TILE;
     for (int q = 0; q < JS_PER; ++q) {            // coalesced staging of the tile
         const uint32_t l = q * BLOCK + threadIdx.x;
-        tm[tpad(l)] = t0 + l < ntok ? toks[t0 + l].y : 0u;
+        tm[tpad(l)] = t0 + l < ntok ? tmeta[t0 + l] : 0u;
     }
     uint32_t* row = st + threadIdx.x * (JS_PD + 1);
 #pragma unroll
@@ -564,23 +613,24 @@ __global__ void __launch_bounds__(BLOCK) k_js_par_apply(const uint2* toks, uint3
 // tokens nested deeper than JS_PD: nearest earlier token with a smaller pre-depth. A small
 // grid-stride launch that returns at once when k_js_par_apply met no such token (the usual
 // document: reading every parent word for nothing cost a 2.4 GB pass)
-__global__ void __launch_bounds__(BLOCK) k_js_deep(const uint2* toks, uint32_t ntok, uint32_t* par, const uint32_t* deep) {
+__global__ void __launch_bounds__(BLOCK) k_js_deep(const uint32_t* tmeta, uint32_t ntok, uint32_t* par, const uint32_t* deep) {
     if (*deep == 0) return;
     for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < ntok; i += gridDim.x * BLOCK) {
         if (par[i] != JS_DEEP) continue;
-        const uint32_t d = toks[i].y & TK_DEPTH_MASK;
+        const uint32_t d = tmeta[i] & TK_DEPTH_MASK;
         uint32_t k = i;
         while (k > 0) {
             --k;
-            if ((toks[k].y & TK_DEPTH_MASK) < d) break;
+            if ((tmeta[k] & TK_DEPTH_MASK) < d) break;
         }
         par[i] = k;
     }
 }
 
 // ---------------------------------------------------------------- validation
-KD_INLINE uint32_t tkind(uint2 t) { return t.y >> 24; }
-KD_INLINE uint32_t tdepth(uint2 t) { return t.y & TK_DEPTH_MASK; }
+KD_INLINE uint32_t tkind(uint32_t meta) { return (meta >> 24) & 0xFu; }
+KD_INLINE uint32_t tsep(uint32_t meta) { return (meta >> 28) & 3u; }
+KD_INLINE uint32_t tdepth(uint32_t meta) { return meta & TK_DEPTH_MASK; }
 KD_INLINE bool value_start(uint32_t k) { return k == TK_OBJ || k == TK_ARR || k == TK_STR || k == TK_SCALAR; }
 KD_INLINE bool is_hexc(uint32_t c) { return (c >= '0' && c <= '9') || ((c | 32) >= 'a' && (c | 32) <= 'f'); }
 
@@ -615,14 +665,6 @@ KD_INLINE bool any_in(const uint64_t* mask, uint32_t a, uint32_t e) {
         w = mask[++b];
     }
 }
-KD_INLINE bool tk_key(const uint2* toks, const uint32_t* par, uint32_t i) {   // an object member name
-    if (i == 0 || tkind(toks[i]) != TK_STR) return false;
-    const uint32_t pk = tkind(toks[i - 1]);
-    if (pk != TK_OBJ && pk != TK_COMMA) return false;
-    const uint32_t p = par[i];
-    return p < JS_DEEP && tkind(toks[p]) == TK_OBJ;
-}
-
 KD_INLINE bool valid_scalar(const JsDoc& j, uint32_t pos) {
     const uint8_t* s = j.doc;
     const uint32_t n = j.n;
@@ -736,64 +778,84 @@ KD_INLINE uint32_t str_end_bs(const JsDoc& j, uint32_t pos, bool* bs, bool* hb =
     return e;
 }
 
-__global__ void __launch_bounds__(BLOCK) k_js_validate(JsDoc j, const uint2* toks, uint32_t ntok, const uint32_t* par,
+__global__ void __launch_bounds__(BLOCK) k_js_validate(JsDoc j, JsToks tk, uint32_t ntok, const uint32_t* par,
                                                        uint8_t* ecand, unsigned long long* err) {
     // the block's tokens (with the two before) and parents (with the one before) staged in
     // LDS with coalesced loads: a token's neighbours, and parents inside the block, come from
     // LDS instead of further global loads
-    __shared__ uint2 st[BLOCK + 2];
+    __shared__ uint32_t st[BLOCK + 2];
     __shared__ uint32_t sp[BLOCK + 1];
     const uint32_t b0 = blockIdx.x * BLOCK, i = b0 + threadIdx.x;
     if (i < ntok) {
-        st[threadIdx.x + 2] = toks[i];
+        st[threadIdx.x + 2] = tk.meta[i];
         sp[threadIdx.x + 1] = par[i];
     }
     if (threadIdx.x < 2) {
         const uint32_t k = b0 + threadIdx.x;                      // token b0 - 2 + threadIdx.x
-        st[threadIdx.x] = k >= 2 ? toks[k - 2] : make_uint2(0u, 0u);
+        st[threadIdx.x] = k >= 2 ? tk.meta[k - 2] : 0u;
         if (threadIdx.x == 1) sp[0] = b0 >= 1 ? par[b0 - 1] : JS_DEEP;
     }
     __syncthreads();
     if (i >= ntok) return;
-    auto kind_of = [&](uint32_t q) {                              // tkind(toks[q]), q < JS_DEEP
-        return q + 2 >= b0 && q < b0 + BLOCK ? tkind(st[q + 2 - b0]) : tkind(toks[q]);
+    auto kind_of = [&](uint32_t q) {                              // tkind(tk.meta[q]), q < JS_DEEP
+        return q + 2 >= b0 && q < b0 + BLOCK ? tkind(st[q + 2 - b0]) : tkind(tk.meta[q]);
     };
-    const uint2 t = st[threadIdx.x + 2];
-    const uint32_t kind = tkind(t), d = tdepth(t), pos = t.x;
+    const uint32_t t = st[threadIdx.x + 2];
+    const uint32_t kind = tkind(t), d = tdepth(t), pos = tk.pos[i];
     const uint32_t p = sp[threadIdx.x + 1];
     const uint32_t pkind = p < JS_DEEP ? kind_of(p) : 0xFEu;
     const uint32_t ck = d == 0 ? 0xFFu : pkind;                   // container kind
+    const uint32_t sep = tsep(t);                                 // the separator before the token
+    const uint32_t pk = i ? tkind(st[threadIdx.x + 1]) : 0xFFu;
     bool ok;
     {
         // element candidate (see k_js_elems_count), from the staged neighbours, with its value's
         // class (1 object, 2 null, 3 anything else): k_js_elems_count then reads one byte per
         // token instead of the token stream, and the element's own token only for an error
-        const uint32_t pk = i ? tkind(st[threadIdx.x + 1]) : 0xFFu;
-        const bool cand = i != 0 && (d == 2 || d == 5) && (pk == TK_ARR || pk == TK_COMMA) && value_start(kind) &&
-                          p < JS_DEEP && pkind == TK_ARR;
+        const bool cand = i != 0 && (d == 2 || d == 5) && (sep == SEP_COMMA || (sep == SEP_NONE && pk == TK_ARR)) &&
+                          value_start(kind) && p < JS_DEEP && pkind == TK_ARR;
         ecand[i] = (uint8_t)(!cand ? 0u : kind == TK_OBJ ? 1u : (kind == TK_SCALAR && j.doc[pos] == 'n') ? 2u : 3u);
     }
-    // the grammar as a set of admissible kinds per predecessor (bit k = kind k), selected
-    // branch-free: the switch it replaces ran every arm for a wave of mixed tokens
+    // The grammar over (previous token, separator, token): the rules the ',' / ':' tokens were
+    // checked by are applied to the separator here, and the error lands where checkValid stops —
+    // on the separator when it is out of place, else on the token. Admissible kinds are sets
+    // (bit k = kind k), selected branch-free.
+    bool sep_bad = false;
     {
-        const uint32_t pk = i ? tkind(st[threadIdx.x + 1]) : 0xFFu;
-        // token i - 1 is a member name: a string after '{' or ',' inside an object (its parent
-        // is token i's: a string neither opens nor closes a container)
+        // token i - 1 is a member name: a string inside an object after '{' or ','
+        const uint32_t tp = i ? st[threadIdx.x + 1] : 0u;
+        const uint32_t ps = tsep(tp);
         const uint32_t ppk = i >= 2 ? tkind(st[threadIdx.x]) : 0xFFu;
-        const bool key = pk == TK_STR && i >= 2 && (ppk == TK_OBJ || ppk == TK_COMMA) && p < JS_DEEP && pkind == TK_OBJ;
+        const bool key = pk == TK_STR && i >= 1 && p < JS_DEEP && pkind == TK_OBJ &&
+                         (ps == SEP_COMMA || (ps == SEP_NONE && i >= 2 && ppk == TK_OBJ));
         constexpr uint32_t VS = 1u << TK_OBJ | 1u << TK_ARR | 1u << TK_STR | 1u << TK_SCALAR;   // a value
-        const uint32_t allow = pk == TK_OBJ ? (1u << TK_STR | 1u << TK_OBJ_END)
-                             : pk == TK_ARR ? (VS | 1u << TK_ARR_END)
-                             : pk == TK_COLON ? VS
-                             : pk == TK_COMMA ? (ck == TK_OBJ ? 1u << TK_STR : ck == TK_ARR ? VS : 0u)
-                             : key ? 1u << TK_COLON
-                             : (1u << TK_COMMA | 1u << TK_OBJ_END | 1u << TK_ARR_END);   // after a value
+        uint32_t allow;
+        if (sep != SEP_NONE) {
+            // the separator in the predecessor's place: ':' only after a member name, ',' only
+            // after a value, never at the top level or before the first token
+            const bool after_value = !key && pk != TK_OBJ && pk != TK_ARR;
+            sep_bad = i == 0 || d == 0 || (sep == SEP_COLON ? !key : !after_value);
+            allow = sep == SEP_COLON ? VS : (ck == TK_OBJ ? 1u << TK_STR : ck == TK_ARR ? VS : 0u);
+        } else {
+            allow = pk == TK_OBJ ? (1u << TK_STR | 1u << TK_OBJ_END)
+                  : pk == TK_ARR ? (VS | 1u << TK_ARR_END)
+                  : key ? 0u                                       // a member name needs its ':'
+                  : (1u << TK_OBJ_END | 1u << TK_ARR_END);         // after a value: ',' or a close
+        }
         ok = (allow >> kind) & 1u;
         ok = ok && !(kind == TK_OBJ_END && ck != TK_OBJ) && !(kind == TK_ARR_END && ck != TK_ARR);
         ok = i == 0 ? (((VS >> kind) & 1u) && d == 0) : (ok && d != 0);   // d == 0: a second top-level value
     }
-    if (ok && i == ntok - 1) {                                    // the document ends here
-        ok = (kind == TK_STR || kind == TK_SCALAR) ? d == 0 : ((kind == TK_OBJ_END || kind == TK_ARR_END) && d == 1);
+    if (sep_bad) {                                                // at the run's first separator
+        uint32_t q = pos, at = pos;
+        while (q > 0) {
+            const uint32_t c = j.doc[q - 1];
+            if (is_ws(c)) { --q; continue; }
+            if (c != ':' && c != ',') break;
+            at = --q;
+        }
+        js_fail(err, at, KDTN_JSON_SYNTAX);
+        return;
     }
     // (a scalar's own grammar is checked by k_js_scalars over the compacted list of scalar
     // tokens: here, one scalar in a wave of 64 tokens made the whole wave run its check)
@@ -818,13 +880,56 @@ __global__ void __launch_bounds__(BLOCK) k_js_validate(JsDoc j, const uint2* tok
     if (!ok) js_fail(err, pos, KDTN_JSON_SYNTAX);
 }
 
+// The end of the document, one thread: separators after the last token are checked as the
+// ',' / ':' tokens were (their place after the last token, then a second one); with none, the
+// last token must end the top-level value. A document that ends inside a value fails at its
+// end, as checkValid's "unexpected end of JSON input" does.
+__global__ void k_js_tail(JsDoc j, JsToks tk, uint32_t ntok, const uint32_t* par, unsigned long long* err) {
+    if (threadIdx.x != 0 || ntok == 0) return;
+    const uint32_t t = tk.meta[ntok - 1];
+    const uint32_t kind = tkind(t), d = tdepth(t), pos = tk.pos[ntok - 1];
+    uint32_t e = pos + 1;                                     // the last token's end
+    if (kind == TK_STR) {
+        e = str_end(j, pos) + 1;
+    } else if (kind == TK_SCALAR) {
+        while (e < j.n) {
+            const uint32_t c = j.doc[e];
+            if (c <= 0x20 || c == '"' || is_struct_byte(c)) break;
+            ++e;
+        }
+    }
+    uint32_t q = e;
+    while (q < j.n && is_ws(j.doc[q])) ++q;
+    if (q >= j.n) {                                           // the document ends with the token
+        const bool ok = (kind == TK_STR || kind == TK_SCALAR) ? d == 0
+                                                              : ((kind == TK_OBJ_END || kind == TK_ARR_END) && d == 1);
+        if (!ok) js_fail(err, j.n, KDTN_JSON_SYNTAX);
+        return;
+    }
+    const uint32_t c = j.doc[q];                              // a separator: nothing else is left
+    const uint32_t p = par[ntok - 1];
+    const bool in_obj = p < JS_DEEP && tkind(tk.meta[p]) == TK_OBJ;
+    const uint32_t ps = tsep(t);
+    const bool key = kind == TK_STR && in_obj &&
+                     (ps == SEP_COMMA || (ps == SEP_NONE && ntok >= 2 && tkind(tk.meta[ntok - 2]) == TK_OBJ));
+    const int64_t ds = (int64_t)d + ((kind == TK_OBJ || kind == TK_ARR) ? 1 : (kind == TK_OBJ_END || kind == TK_ARR_END) ? -1 : 0);
+    const bool ok = ds != 0 && (c == ':' ? key : (!key && kind != TK_OBJ && kind != TK_ARR));
+    if (!ok) {
+        js_fail(err, q, KDTN_JSON_SYNTAX);
+        return;
+    }
+    uint32_t q2 = q + 1;
+    while (q2 < j.n && is_ws(j.doc[q2])) ++q2;
+    js_fail(err, q2 < j.n ? q2 : j.n, KDTN_JSON_SYNTAX);
+}
+
 // checkValid's literal / number grammar for every scalar token, over the list k_js_tokens
 // compacted (full waves of scalars instead of one scalar lane per token wave)
-__global__ void __launch_bounds__(BLOCK) k_js_scalars(JsDoc j, const uint2* toks, const uint32_t* slist, uint32_t nscal,
+__global__ void __launch_bounds__(BLOCK) k_js_scalars(JsDoc j, const uint32_t* tpos, const uint32_t* slist, uint32_t nscal,
                                                       unsigned long long* err) {
     const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
     if (k >= nscal || (KDTN_PROFILING && (j.variant & JSV_NO_SCALAR))) return;
-    const uint32_t pos = toks[slist[k]].x;
+    const uint32_t pos = tpos[slist[k]];
     const int w = valid_scalar_window(j, pos);
     if (!(w >= 0 ? w != 0 : valid_scalar(j, pos))) js_fail(err, pos, KDTN_JSON_SYNTAX);
 }
@@ -947,15 +1052,16 @@ KD_INLINE uint32_t name_hash(uint64_t lo, uint64_t hi) {
 
 // ---------------------------------------------------------------- roles
 // role of the container c whose enclosing container has role r (c is the child token)
-KD_INLINE uint32_t child_role(const JsDoc& j, const uint2* toks, uint32_t r, uint32_t c) {
+KD_INLINE uint32_t child_role(const JsDoc& j, const JsToks& tk, uint32_t r, uint32_t c) {
     if (r == R_NONE || r == R_META || r >= R_PROPS_S) return R_NONE;
-    const uint32_t kind = tkind(toks[c]);
-    const bool member = tkind(toks[c - 1]) == TK_COLON;
+    const uint32_t meta = tk.meta[c];
+    const uint32_t kind = tkind(meta);
+    const bool member = tsep(meta) == SEP_COLON;
     if (!member) {                                                // array element
         if (kind != TK_OBJ) return R_NONE;
         return r == R_ITEMS ? R_ITEM : r == R_SPEC_LINKS ? R_LINK_S : r == R_STATUS_LINKS ? R_LINK_R : R_NONE;
     }
-    const uint32_t kpos = toks[c - 2].x;
+    const uint32_t kpos = tk.pos[c - 1];
     switch (r) {
     case R_ROOT:
         return (kind == TK_ARR && match_key(j, kpos, kItems, 1) == 0) ? R_ITEMS : R_NONE;
@@ -986,7 +1092,7 @@ KD_INLINE uint32_t child_role(const JsDoc& j, const uint2* toks, uint32_t r, uin
 // (level 6 runs after it); level 3 therefore derives its parent's role (an items element)
 // from the grandparent's. The roles start zeroed (R_NONE) and only the schema's containers
 // are written.
-__global__ void __launch_bounds__(BLOCK) k_js_roles(JsDoc j, const uint2* toks, const uint32_t* olist, uint32_t nopen,
+__global__ void __launch_bounds__(BLOCK) k_js_roles(JsDoc j, JsToks tk, const uint32_t* olist, uint32_t nopen,
                                                     const uint32_t* par, uint8_t* role, const uint8_t* odep,
                                                     uint32_t level) {
     const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
@@ -994,15 +1100,15 @@ __global__ void __launch_bounds__(BLOCK) k_js_roles(JsDoc j, const uint2* toks, 
     const uint32_t i = olist[k];
     uint32_t r;
     if (level == 0) {
-        r = tkind(toks[i]) == TK_OBJ ? R_ROOT : R_NONE;
+        r = tkind(tk.meta[i]) == TK_OBJ ? R_ROOT : R_NONE;
     } else {
         const uint32_t p = par[i];
         uint32_t rp;
         if (level == 3)                                      // p: an items element (an object) or nothing
-            rp = (role[par[p]] == R_ITEMS && tkind(toks[p]) == TK_OBJ) ? R_ITEM : R_NONE;
+            rp = (role[par[p]] == R_ITEMS && tkind(tk.meta[p]) == TK_OBJ) ? R_ITEM : R_NONE;
         else
             rp = role[p];
-        r = child_role(j, toks, rp, i);
+        r = child_role(j, tk, rp, i);
     }
     if (r != R_NONE) role[i] = (uint8_t)r;
 }
@@ -1011,7 +1117,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_roles(JsDoc j, const uint2* toks, 
 // Element class of token i: 1 + {0 items element, 1 spec.links element, 2 status.links
 // element}, or 0. k_js_validate marks the candidates (depth 2 for items elements, 5 for links
 // elements; after '[' or ','; a value; parent an array); the parent array's role decides.
-__global__ void __launch_bounds__(BLOCK) k_js_elems_count(JsDoc j, const uint2* toks, uint32_t ntok, const uint32_t* par,
+__global__ void __launch_bounds__(BLOCK) k_js_elems_count(JsDoc j, JsToks tk, uint32_t ntok, const uint32_t* par,
                                                           uint8_t* role, uint32_t* cnt3, uint8_t* ecls,
                                                           unsigned long long* derr) {
     __shared__ uint32_t sh[3];
@@ -1020,8 +1126,8 @@ __global__ void __launch_bounds__(BLOCK) k_js_elems_count(JsDoc j, const uint2* 
     uint32_t c[3] = {0, 0, 0};
     const uint32_t t0 = blockIdx.x * JS_TILE;
     if (t0 + threadIdx.x == 0 && ntok) {                          // the document must be an object or null
-        const uint2 t = toks[0];
-        if (!(tkind(t) == TK_OBJ || (tkind(t) == TK_SCALAR && j.doc[t.x] == 'n'))) js_fail(derr, t.x, KDTN_JSON_TYPE);
+        const uint32_t t = tk.meta[0], p0 = tk.pos[0];
+        if (!(tkind(t) == TK_OBJ || (tkind(t) == TK_SCALAR && j.doc[p0] == 'n'))) js_fail(derr, p0, KDTN_JSON_TYPE);
     }
     // counts: the thread's 16 candidate bytes (JS_PER == 16) as one coalesced 16-byte load;
     // the buffer is padded to whole tiles, bytes past ntok are ignored
@@ -1044,7 +1150,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_elems_count(JsDoc j, const uint2* 
             const uint32_t cls = r == R_ITEMS ? 1 : r == R_SPEC_LINKS ? 2 : r == R_STATUS_LINKS ? 3 : 0;
             w[q] = (w[q] & ~(0xFFu << (8 * h))) | (cls << (8 * h));   // the class, for k_js_elems_write
             if (!cls) continue;
-            if (vc == 3u) js_fail(derr, toks[i].x, KDTN_JSON_TYPE);     // neither an object nor null
+            if (vc == 3u) js_fail(derr, tk.pos[i], KDTN_JSON_TYPE);     // neither an object nor null
             if (vc == 1u) role[i] = (uint8_t)(cls == 1 ? R_ITEM : cls == 2 ? R_LINK_S : R_LINK_R);
             c[cls - 1]++;
         }
@@ -1491,7 +1597,7 @@ KD_INLINE uint32_t* store_word(const JsStore& st, uint32_t rec, int col) {
     return st.base + (size_t)rec * JS_ROW + col;
 }
 
-__global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, const uint2* toks, const uint32_t* vlist, uint32_t nval,
+__global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, JsToks tk, const uint32_t* vlist, uint32_t nval,
                                                      const uint32_t* par, const uint8_t* role, const uint32_t* ord,
                                                      JsTopoOut to, JsStore des, JsStore real, JsIntern in,
                                                      unsigned long long* derr) {
@@ -1512,8 +1618,8 @@ __global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, const uint2* toks,
     const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
     if (k >= nval) return;
     const uint32_t i = vlist[k];                       // object member values, document order
-    const uint2 t = toks[i];
-    const uint32_t kpos = toks[i - 2].x;
+    const uint32_t t = tk.meta[i];
+    const uint32_t vpos = tk.pos[i], kpos = tk.pos[i - 1];   // the value, the member name before it
     const uint32_t dv = tdepth(t);                     // members of root 1, item 3, meta/spec/status 4,
     // every member value gets its vown word here (JS_NONE: not a schema field), so the array
     // needs no clearing pass
@@ -1525,7 +1631,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, const uint2* toks,
     const KeyName kn = key_name(j, kpos, !(KDTN_PROFILING && (in.variant & JSV_MASKS)));   // while role[o] is in flight
     if (r == R_NONE || r == R_ITEMS || r == R_SPEC_LINKS || r == R_STATUS_LINKS) { in.vown[k] = JS_NONE; return; }
     const uint32_t kind = tkind(t);
-    const bool null = kind == TK_SCALAR && j.doc[t.x] == 'n';
+    const bool null = kind == TK_SCALAR && j.doc[vpos] == 'n';
     int f, bit;
     {
         const int g0 = s_slot[name_hash(kn.lo, kn.hi)];
@@ -1588,7 +1694,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, const uint2* toks,
     case R_META: {
         if (null) break;
         if (kind != TK_STR) { ok = false; break; }
-        const uint32_t v = (KDTN_PROFILING && (in.variant & JSV_NO_INTERN)) ? 1u : string_slot(j, in, in.kd, i, t.x);
+        const uint32_t v = (KDTN_PROFILING && (in.variant & JSV_NO_INTERN)) ? 1u : string_slot(j, in, in.kd, i, vpos);
         if (v == JS_NONE) return;
         uint32_t* dst = r == R_META ? (f == 0 ? to.name : to.ns) : (f == 1 ? to.src_ip : to.net_ns);
         dst[topo] = v;
@@ -1600,7 +1706,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, const uint2* toks,
         if (!props && f == KDTN_NKEY) {                                           // uid
             if (null) break;
             int64_t v;
-            ok = kind == TK_SCALAR && parse_int64(j, t.x, &v);
+            ok = kind == TK_SCALAR && parse_int64(j, vpos, &v);
             if (ok) {
                 *reinterpret_cast<int64_t*>(store_word(st, rec, COL_UID)) = v;   // 8-B aligned (88-B rows)
             }
@@ -1609,19 +1715,19 @@ __global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, const uint2* toks,
         if (props && f == KDTN_NPROP) {                                           // gap
             if (null) break;
             uint32_t v;
-            ok = kind == TK_SCALAR && parse_uint32(j, t.x, &v);
+            ok = kind == TK_SCALAR && parse_uint32(j, vpos, &v);
             if (ok) *store_word(st, rec, COL_GAP) = v;
             break;
         }
         if (null) break;
         if (kind != TK_STR) { ok = false; break; }
-        const uint32_t v = (KDTN_PROFILING && (in.variant & JSV_NO_INTERN)) ? 1u : string_slot(j, in, props ? in.pd : in.kd, i, t.x);
+        const uint32_t v = (KDTN_PROFILING && (in.variant & JSV_NO_INTERN)) ? 1u : string_slot(j, in, props ? in.pd : in.kd, i, vpos);
         if (v == JS_NONE) return;
         *store_word(st, rec, props ? COL_PROP0 + f : COL_KEY0 + f) = v;
         break;
     }
     }
-    if (!ok) js_fail(derr, t.x, KDTN_JSON_TYPE);
+    if (!ok) js_fail(derr, vpos, KDTN_JSON_TYPE);
 }
 
 // A schema field repeated in one object: its members stored into the same owner slot and only
@@ -1629,7 +1735,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_values(JsDoc j, const uint2* toks,
 // slot ends at the group's first member (the plain store's winner included), and k_js_dups_report
 // then reports every later member at its key — the first repeat in document order is the
 // earliest, the position a sequential decoder stops at. `any` gates the report pass.
-__global__ void __launch_bounds__(BLOCK) k_js_dups(const uint2* toks, const uint32_t* vlist, uint32_t nval,
+__global__ void __launch_bounds__(BLOCK) k_js_dups(const uint32_t* vlist, uint32_t nval,
                                                    const uint32_t* vown, uint32_t* owner, uint32_t* any) {
     const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
     if (k >= nval) return;
@@ -1642,7 +1748,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_dups(const uint2* toks, const uint
     }
 }
 
-__global__ void __launch_bounds__(BLOCK) k_js_dups_report(const uint2* toks, const uint32_t* vlist, uint32_t nval,
+__global__ void __launch_bounds__(BLOCK) k_js_dups_report(const uint32_t* tpos, const uint32_t* vlist, uint32_t nval,
                                                           const uint32_t* vown, const uint32_t* owner,
                                                           const uint32_t* any, unsigned long long* derr) {
     if (*any == 0) return;
@@ -1650,7 +1756,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_dups_report(const uint2* toks, con
         const uint32_t own = vown[k];
         if (own == JS_NONE) continue;
         const uint32_t i = vlist[k];
-        if (owner[own] < i) js_fail(derr, toks[i - 2].x, KDTN_JSON_DUPKEY);
+        if (owner[own] < i) js_fail(derr, tpos[i - 1], KDTN_JSON_DUPKEY);
     }
 }
 

@@ -649,10 +649,19 @@ __global__ void k_pod_verify_prefix(const uint4* pods, uint32_t total, uint4* sl
                                     uint32_t* first_partial_inv, uint32_t nbv, uint32_t nr, uint32_t gathered);
 
 // ---- CR ingest: TopologyList JSON → epoch tables (kdtn_ingest.hip) ------------------------
-// token word: {byte offset, pre-depth | kind << 24}
+// The token stream: brackets, strings and scalars (the ',' / ':' bytes are no tokens), as two
+// arrays of 4-byte words — the byte offset, and the meta word: pre-depth (bits 0-23) | kind << 24
+// (4 bits) | sep << 28, the separator between the previous token and this one (SEP_* of the
+// earliest when several stand there, which k_js_tokens reports). Kernels that need only
+// depths and kinds (the parent scans) read the meta words alone.
 enum : uint32_t { TK_OBJ = 0, TK_OBJ_END = 1, TK_ARR = 2, TK_ARR_END = 3, TK_COLON = 4, TK_COMMA = 5,
                   TK_STR = 6, TK_SCALAR = 7 };
 constexpr uint32_t TK_DEPTH_MASK = 0xFFFFFFu;
+enum : uint32_t { SEP_NONE = 0, SEP_COLON = 1, SEP_COMMA = 2 };
+struct JsToks {
+    uint32_t* pos;             // byte offset of the token's first byte
+    uint32_t* meta;            // pre-depth | kind << 24 | sep << 28
+};
 constexpr int JS_PD = 16;                    // depth levels resolved by the parent max-scan
 constexpr int JS_PER = 16;                   // tokens per thread in tile kernels
 constexpr int JS_TILE = BLOCK * JS_PER;      // tokens per tile
@@ -732,29 +741,30 @@ struct JsIntern {
 };
 __global__ void k_js_quotes(JsDoc j, uint64_t* qmask, uint64_t* bsmask, uint64_t* hbmask, uint32_t* gq);
 __global__ void k_js_classify(JsDoc j, const uint64_t* gqoff, JsMasks m, uint32_t ng, unsigned long long* err);
-__global__ void k_js_tokens(JsDoc j, JsMasks m, const uint64_t* goff, uint32_t ng, uint2* toks, uint32_t* olist,
+__global__ void k_js_tokens(JsDoc j, JsMasks m, const uint64_t* goff, uint32_t ng, JsToks tk, uint32_t* olist,
                             uint8_t* odep, uint32_t* vlist, uint32_t* slist, unsigned long long* err);
-__global__ void k_js_scalars(JsDoc j, const uint2* toks, const uint32_t* slist, uint32_t nscal, unsigned long long* err);
-__global__ void k_js_par_agg(const uint2* toks, uint32_t ntok, uint32_t* tagg);
+__global__ void k_js_scalars(JsDoc j, const uint32_t* tpos, const uint32_t* slist, uint32_t nscal, unsigned long long* err);
+__global__ void k_js_par_agg(const uint32_t* tmeta, uint32_t ntok, uint32_t* tagg);
 __global__ void k_js_par_group(const uint32_t* tagg, uint32_t ntiles, uint32_t* gagg);
 __global__ void k_js_par_top(uint32_t* gagg, uint32_t ng);
 __global__ void k_js_par_tiles(uint32_t* tagg, uint32_t ntiles, const uint32_t* gagg);
-__global__ void k_js_par_apply(const uint2* toks, uint32_t ntok, const uint32_t* texcl, uint32_t* par, uint32_t* deep);
-__global__ void k_js_deep(const uint2* toks, uint32_t ntok, uint32_t* par, const uint32_t* deep);
-__global__ void k_js_validate(JsDoc j, const uint2* toks, uint32_t ntok, const uint32_t* par, uint8_t* ecand,
+__global__ void k_js_par_apply(const uint32_t* tmeta, uint32_t ntok, const uint32_t* texcl, uint32_t* par, uint32_t* deep);
+__global__ void k_js_deep(const uint32_t* tmeta, uint32_t ntok, uint32_t* par, const uint32_t* deep);
+__global__ void k_js_tail(JsDoc j, JsToks tk, uint32_t ntok, const uint32_t* par, unsigned long long* err);
+__global__ void k_js_validate(JsDoc j, JsToks tk, uint32_t ntok, const uint32_t* par, uint8_t* ecand,
                               unsigned long long* err);
-__global__ void k_js_roles(JsDoc j, const uint2* toks, const uint32_t* olist, uint32_t nopen, const uint32_t* par,
+__global__ void k_js_roles(JsDoc j, JsToks tk, const uint32_t* olist, uint32_t nopen, const uint32_t* par,
                            uint8_t* role, const uint8_t* odep, uint32_t level);
-__global__ void k_js_elems_count(JsDoc j, const uint2* toks, uint32_t ntok, const uint32_t* par, uint8_t* role,
+__global__ void k_js_elems_count(JsDoc j, JsToks tk, uint32_t ntok, const uint32_t* par, uint8_t* role,
                                  uint32_t* cnt3, uint8_t* ecls, unsigned long long* derr);
 __global__ void k_js_elems_write(const uint8_t* ecls, uint32_t ntok, const uint64_t* coff3, uint32_t ntiles,
                                  uint32_t* ord, JsTopoOut to);
-__global__ void k_js_values(JsDoc j, const uint2* toks, const uint32_t* vlist, uint32_t nval, const uint32_t* par,
+__global__ void k_js_values(JsDoc j, JsToks tk, const uint32_t* vlist, uint32_t nval, const uint32_t* par,
                             const uint8_t* role, const uint32_t* ord, JsTopoOut to, JsStore des, JsStore real,
                             JsIntern in, unsigned long long* derr);
-__global__ void k_js_dups(const uint2* toks, const uint32_t* vlist, uint32_t nval, const uint32_t* vown,
+__global__ void k_js_dups(const uint32_t* vlist, uint32_t nval, const uint32_t* vown,
                           uint32_t* owner, uint32_t* any);
-__global__ void k_js_dups_report(const uint2* toks, const uint32_t* vlist, uint32_t nval, const uint32_t* vown,
+__global__ void k_js_dups_report(const uint32_t* tpos, const uint32_t* vlist, uint32_t nval, const uint32_t* vown,
                                  const uint32_t* owner, const uint32_t* any, unsigned long long* derr);
 __global__ void k_js_rep_mark(JsDict dt, uint32_t* bits);
 __global__ void k_js_popc(const uint32_t* bits, uint32_t nw, uint32_t* cnt);

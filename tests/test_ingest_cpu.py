@@ -115,7 +115,13 @@ def test_empty_and_null_shapes():
 BAD_SYNTAX = [b"", b" ", b"{", b"}", b"[1,]", b'{"a":1,}', b'{"a" 1}', b'{"a":}', b"{'a':1}", b"01",
               b"-", b"1.", b"1e", b".5", b"+1", b"tru", b"nul", b'"abc', b'"a\\x"', b'"\\u12G4"',
               b'"a\x01b"', b"[1 2]", b'{"items":[]} x', b"[]]", b"[[]", b'{"a":1 "b":2}', b"[,]",
-              b'{"items":[{"spec":{"links":[{"uid":1}]}}]', b"\xef\xbb\xbf{}", b"NaN", b"[1,\x0b2]"]
+              b'{"items":[{"spec":{"links":[{"uid":1}]}}]', b"\xef\xbb\xbf{}", b"NaN", b"[1,\x0b2]",
+              # separators (no tokens of their own on the GPU: recorded on the token after them)
+              ] + [b",", b" , ", b":", b",[]", b"[],", b"[]:", b"[1,,2]", b"[1::2]", b"[1 :2]", b"[,1]", b"[:1]",
+              b'{"a"::1}', b'{"a":1,,"b":2}', b'{,"a":1}', b'{:"a":1}', b'{"a",1}', b'{"a":1:2}', b"[1,",
+              b"[1, ", b'{"a":', b'{"a" : ', b'{"a":1,', b'{"a" :, }', b"[{}:1]", b'{"a":{},:1}', b"[[]:]",
+              b'{"a":1}, {"b":2}', b'{"a":1 , , }', b'{"a"', b'["a",', b'{"a":[1,2],}']
+SEP_SYNTAX = BAD_SYNTAX[BAD_SYNTAX.index(b","):]
 
 
 @pytest.mark.parametrize("doc", BAD_SYNTAX)

@@ -15,7 +15,7 @@ import json_ref as jr
 import oracle as O
 from kdtn import abi, synth
 from kdtn.engine import KdtnError
-from test_ingest_cpu import (BAD_SYNTAX, DUPS, GO_STRINGS, TYPE_ERRORS, GOLDEN, rand_topos, s0p,
+from test_ingest_cpu import (BAD_SYNTAX, SEP_SYNTAX, DUPS, GO_STRINGS, TYPE_ERRORS, GOLDEN, rand_topos, s0p,
                              sample_doc)
 
 pytestmark = pytest.mark.gpu
@@ -69,6 +69,29 @@ def test_random_documents(engine, seed):
 @pytest.mark.parametrize("doc", BAD_SYNTAX + TYPE_ERRORS + DUPS)
 def test_rejections(engine, doc):
     check_doc(engine, doc, repr(doc[:60]))
+
+
+def test_separator_error_offsets(engine):
+    """Misplaced / repeated / trailing ',' and ':' (the GPU token stream has no separator tokens:
+    each token records the separator before it, k_js_tail checks the ones after the last token):
+    the rejection lands on the byte the oracle's checkValid stops at, the document's end for a
+    truncated one."""
+    bad = []
+    for doc in SEP_SYNTAX:
+        if not doc.strip(b" ,:"):
+            continue                                # no token at all: offset 0 by the host check
+        e0, off0, _ = O.json_ingest(doc)
+        try:
+            engine.ingest(doc)
+            bad.append((doc, "accepted"))
+            continue
+        except KdtnError as e:
+            if e.code != abi.EBADMSG:
+                raise
+            e1, off1 = e.info.json_err, e.info.err_offset
+        if (e1, off1) != (e0, off0):
+            bad.append((doc, (e1, off1), (e0, off0)))
+    assert not bad, bad
 
 
 def test_depth(engine):
