@@ -2544,6 +2544,10 @@ static int json_decode(kdtn_ctx* c, const JsTargets& tg, JsCounts* o, kdtn_inges
     JsStore real{dp<uint32_t>(c->j_rows) + (size_t)des_tiles * TILE_WORDS};
 
     // 5. schema values + interning; a table or heap that fills up is grown and the pass rerun
+    // A table that fills up (or whose probe runs grow past JS_MAX_PROBE) is grown 4x and the
+    // pass rerun. (Sized for fewer distinct strings — half a key string per record — the config-2
+    // document, 12M distinct key strings, overflowed its first table after 217 ms of ever longer
+    // probe runs; the decode time does not depend on the table's footprint at these sizes.)
     uint32_t kcap = std::max(c->j_kcap, next_pow2(std::max<uint64_t>(1024, 2ull * ((uint64_t)N + M) + 4ull * T)));
     uint32_t pcap = std::max(c->j_pcap, next_pow2(std::max<uint64_t>(1024, ((uint64_t)N + M) / 2 + 64)));
     uint64_t hcap = std::max<uint64_t>(1 << 20, c->j_n / 16);

@@ -304,15 +304,16 @@ KD_INLINE uint32_t sep_before(uint32_t pos, uint32_t* second, B&& byte) {
 // search over the wave's token prefix, bit by select): coalesced 4-byte stores instead of
 // every lane walking its own block's tokens into its own region. The ',' and ':' bytes are no
 // tokens (m.tok holds them; they are told apart here): a token records the separator before it
-// (sep_before), and each member value's index comes from its colon (the number of tokens before
-// the colon), written by a second loop over the wave's colons.
+// (sep_before), and a member value (a token after a ':') is the C-th entry of vlist, C = the
+// number of structural colons before it, less one (the colon it follows is the last of them,
+// in this block or an earlier one).
 __global__ void __launch_bounds__(BLOCK) k_js_tokens(JsDoc j, JsMasks m, const uint64_t* goff, uint32_t ng,
                                                      JsToks tk, uint32_t* olist, uint8_t* odep, uint32_t* vlist,
                                                      uint32_t* slist, unsigned long long* err) {
     __shared__ uint4 blk[BLOCK * 4];
     __shared__ uint64_t stok[BLOCK], sop[BLOCK], scl[BLOCK], scol[BLOCK], ssc[BLOCK];
     __shared__ int64_t sd0[BLOCK];
-    __shared__ uint32_t sex[BLOCK], soo[BLOCK], sco[BLOCK], sso[BLOCK], scx[BLOCK];
+    __shared__ uint32_t sex[BLOCK], soo[BLOCK], sco[BLOCK], sso[BLOCK];
     __shared__ uint64_t shs[BLOCK / 64];
     const uint32_t lane = threadIdx.x & 63u, w0 = threadIdx.x & ~63u;
     const uint32_t b = blockIdx.x * BLOCK + threadIdx.x;
@@ -360,16 +361,15 @@ __global__ void __launch_bounds__(BLOCK) k_js_tokens(JsDoc j, JsMasks m, const u
     sco[threadIdx.x] = (uint32_t)(goff[3 * G + g] + ((ea >> 32) & 0xFFFFu));
     sso[threadIdx.x] = (uint32_t)(goff[4 * G + g] + (ea >> 48));
     stok[threadIdx.x] = tok;
-    const uint32_t cnt = __popcll(tok), ccnt = __popcll(colm);
-    uint32_t inc = cnt, cinc = ccnt;
+    const uint32_t cnt = __popcll(tok);
+    uint32_t inc = cnt;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = __shfl_up(inc, d, 64), oc = __shfl_up(cinc, d, 64);
-        if (lane >= (uint32_t)d) { inc += o; cinc += oc; }
+        const uint32_t o = __shfl_up(inc, d, 64);
+        if (lane >= (uint32_t)d) inc += o;
     }
     sex[threadIdx.x] = inc - cnt;
-    scx[threadIdx.x] = cinc - ccnt;
-    const uint32_t wtot = __shfl(inc, 63, 64), wcol = __shfl(cinc, 63, 64);
+    const uint32_t wtot = __shfl(inc, 63, 64);
     const uint32_t base = (uint32_t)__shfl(ti, 0, 64);  // toff of the wave's first block
     __syncthreads();
     // document bytes: the workgroup's blocks from LDS, others from global memory
@@ -398,6 +398,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_tokens(JsDoc j, JsMasks m, const u
         const uint32_t sep = sep_before(pos, &second, byte_at);
         if (second != 0xFFFFFFFFu) js_fail(err, second, KDTN_JSON_SYNTAX);   // two separators in a row
         const uint32_t idx = base + r;
+        if (sep == SEP_COLON) vlist[sco[o] + __popcll(scol[o] & below) - 1] = idx;   // >= 1 colon before it
         if (kind == TK_OBJ || kind == TK_ARR) {
             if (d >= 10000) js_fail(err, pos, KDTN_JSON_DEPTH);
             const uint32_t oi = soo[o] + __popcll(sop[o] & below);
@@ -409,17 +410,6 @@ __global__ void __launch_bounds__(BLOCK) k_js_tokens(JsDoc j, JsMasks m, const u
         if (d > (int64_t)TK_DEPTH_MASK) d = TK_DEPTH_MASK;
         tk.pos[idx] = pos;
         tk.meta[idx] = (uint32_t)d | (kind << 24) | (sep << 28);
-    }
-    // member values: the token after the k-th colon is token (tokens before the colon)
-    for (uint32_t r = lane; r < wcol; r += 64) {
-        uint32_t L = 0;                                    // last lane with scx <= r
-#pragma unroll
-        for (uint32_t st = 32; st >= 1; st >>= 1)
-            if (scx[w0 + L + st] <= r) L += st;
-        const uint32_t o = w0 + L;
-        const uint32_t k = select_bit(scol[o], r - scx[o]);
-        const uint64_t below = (1ull << k) - 1;
-        vlist[sco[o] + __popcll(scol[o] & below)] = base + sex[o] + __popcll(stok[o] & below);
     }
 }
 
@@ -1374,7 +1364,8 @@ KD_INLINE uint32_t intern(const JsIntern& in, const JsDict& dt, const uint8_t* p
         if (off) inl = false;
     }
     uint32_t s = (uint32_t)h & dt.mask;
-    for (uint32_t probe = 0; probe <= dt.mask; ++probe) {
+    const uint32_t probes = dt.mask < JS_MAX_PROBE ? dt.mask + 1 : JS_MAX_PROBE;   // a run this long: grow the table
+    for (uint32_t probe = 0; probe < probes; ++probe) {
         // slots are written once (CAS from 0): a plain load is either that final key or a stale 0,
         // and a stale 0 only sends us to the CAS, which returns the real key. The key word and
         // the inline bytes come from one 32-byte slot (two 16-B loads of one line).

@@ -716,6 +716,7 @@ struct JsStore {
 // bytes are not stored yet reads as zeros (the table is cleared per decode), and no inline
 // string has a zero byte, so a zero byte within the length means "not available".
 constexpr uint32_t JS_INL = 24;
+constexpr uint32_t JS_MAX_PROBE = 256;         // longest probe run before the table is grown
 struct JsSlot {
     unsigned long long kw;
     uint32_t b[6];

@@ -94,6 +94,31 @@ def test_separator_error_offsets(engine):
     assert not bad, bad
 
 
+def test_intern_tables_grow():
+    """More distinct strings than the first table sizes (set from the record counts) hold: the
+    values pass reruns on tables grown 4x until they fit, and the next decode starts from the
+    sizes the last one needed; every table equals the oracle's each time."""
+    import json as _json
+    from kdtn import Engine
+    items = []
+    for t in range(300):
+        links = [{"uid": k, "peer_pod": f"q{t}_{k}", "local_intf": f"e{t}_{k}", "local_ip": f"10.{t % 250}.{k}.1/24",
+                  "local_mac": f"02:00:{t // 256:02x}:{t % 256:02x}:{k:02x}:01", "peer_intf": f"f{t}_{k}",
+                  "peer_ip": f"10.{t % 250}.{k}.2/24", "peer_mac": f"02:00:{t // 256:02x}:{t % 256:02x}:{k:02x}:02",
+                  "properties": {"latency": f"{t * 13 + k}ms", "rate": f"{t * 7 + k}mbit"}} for k in range(12)]
+        items.append({"metadata": {"name": f"p{t}", "namespace": "default"}, "spec": {"links": links}})
+    doc = _json.dumps({"items": items}).encode()
+    eng = Engine(device=0, tick_in_usec=15.625, vxlan_base=5000)
+    try:
+        for rep in range(2):
+            want = check_doc(eng, doc, f"rep {rep}")
+            assert want is not None and len(want.kdict.offs) > 24000
+        check_doc(eng, b'{"items":[{"metadata":{"name":"a"},"spec":{"links":[{"uid":1,"peer_pod":"b"}]}}]}',
+                  "small document after")
+    finally:
+        eng.close()
+
+
 def test_depth(engine):
     for d in (15, 16, 17, 40, 9999, 10000, 10001):
         for wrap in (False, True):
