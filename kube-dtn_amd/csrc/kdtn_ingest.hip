@@ -315,7 +315,13 @@ __global__ void __launch_bounds__(BLOCK) k_js_tokens(JsDoc j, JsMasks m, const u
     __shared__ int64_t sd0[BLOCK];
     __shared__ uint32_t sex[BLOCK], soo[BLOCK], sco[BLOCK], sso[BLOCK];
     __shared__ uint64_t shs[BLOCK / 64];
+    // per wave: bit t of sb = token rank t starts a block; spw = popcounts of sb's earlier words;
+    // smap = the lane of the n-th block that has tokens (the owner block of a rank in two steps)
+    __shared__ uint64_t sb[BLOCK];
+    __shared__ uint32_t spw[BLOCK];
+    __shared__ uint8_t smap[BLOCK];
     const uint32_t lane = threadIdx.x & 63u, w0 = threadIdx.x & ~63u;
+    sb[threadIdx.x] = 0;
     const uint32_t b = blockIdx.x * BLOCK + threadIdx.x;
     uint64_t tok = 0, pa = 0, pd = 0, colm = 0;
     if (b < j.nb) {
@@ -371,6 +377,25 @@ __global__ void __launch_bounds__(BLOCK) k_js_tokens(JsDoc j, JsMasks m, const u
     sex[threadIdx.x] = inc - cnt;
     const uint32_t wtot = __shfl(inc, 63, 64);
     const uint32_t base = (uint32_t)__shfl(ti, 0, 64);  // toff of the wave's first block
+    {
+        const uint64_t ne = __ballot(cnt != 0);
+        if (cnt) {
+            const uint32_t first = inc - cnt;              // < 4096: a wave holds 64 blocks
+            atomicOr(reinterpret_cast<unsigned long long*>(&sb[w0 + (first >> 6)]), 1ull << (first & 63u));
+            smap[w0 + __popcll(ne & ((1ull << lane) - 1ull))] = (uint8_t)lane;
+        }
+    }
+    __syncthreads();
+    {
+        const uint32_t c = __popcll(sb[threadIdx.x]);
+        uint32_t s = c;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = __shfl_up(s, d, 64);
+            if (lane >= (uint32_t)d) s += o;
+        }
+        spw[threadIdx.x] = s - c;
+    }
     __syncthreads();
     // document bytes: the workgroup's blocks from LDS, others from global memory
     const uint32_t wg0 = blockIdx.x * BLOCK * 64u;
@@ -379,11 +404,11 @@ __global__ void __launch_bounds__(BLOCK) k_js_tokens(JsDoc j, JsMasks m, const u
         return (q >= wg0 && q - wg0 < BLOCK * 64u && (q >> 6) < j.nb) ? bytes[q - wg0] : j.doc[q];
     };
     for (uint32_t r = lane; r < wtot; r += 64) {
-        uint32_t L = 0;                                    // last lane with sex <= r
-#pragma unroll
-        for (uint32_t st = 32; st >= 1; st >>= 1)
-            if (sex[w0 + L + st] <= r) L += st;
-        const uint32_t o = w0 + L;
+        // owner block of rank r: the blocks starting at or before r (the round's word of sb is
+        // one broadcast read), then the lane of that many-th block with tokens
+        const uint32_t wd = r >> 6;
+        const uint32_t nb = spw[w0 + wd] + (uint32_t)__popcll(sb[w0 + wd] & ((2ull << lane) - 1ull));
+        const uint32_t o = w0 + smap[w0 + nb - 1];
         const uint32_t k = select_bit(stok[o], r - sex[o]);
         const uint64_t below = (1ull << k) - 1;
         int64_t d = sd0[o] + __popcll(sop[o] & below) - __popcll(scl[o] & below);
