@@ -176,6 +176,7 @@ KD_INLINE uint32_t quote_block(const JsDoc& j, uint32_t b, uint64_t* qmask, uint
 }
 
 // ---------------------------------------------------------------- k_js_classify
+KD_INLINE bool is_hexc(uint32_t c) { return (c >= '0' && c <= '9') || ((c | 32) >= 'a' && (c | 32) <= 'f'); }
 KD_INLINE void classify_block(const JsDoc& j, uint32_t b, uint64_t quote, bool S, const JsMasks& m,
                               unsigned long long* err, uint64_t* pa, uint64_t* pd);
 
@@ -222,6 +223,38 @@ KD_INLINE void classify_block(const JsDoc& j, uint32_t b, uint64_t quote, bool S
     }
     const uint64_t scalar_start = scalar & ~((scalar << 1) | (uint64_t)prev_scalar);
     const uint64_t tok = structural | str_open | scalar_start;
+    // escapes (checkValid's stateInStringEsc*): the byte after an odd backslash run must be one
+    // of " \ / b f n r t, or u and four hex digits; reported at the backslash. A backslash
+    // outside a string fails the grammar anyway, so the check needs no string state.
+    const uint64_t bsm = j.bsmask[b];
+    const bool pe = b > 0 && (j.bsmask[b - 1] >> 63) != 0;   // a run may end right before the block
+    if (bsm || pe) {
+        bool e = false;
+        if (pe) {                                             // its parity
+            uint64_t i = (uint64_t)b * 64 - 1, run = 0;
+            for (;;) {
+                if (j.doc[i] != '\\') break;
+                ++run;
+                if (i == 0) break;
+                --i;
+            }
+            e = run & 1;
+        }
+        for (int k = 0; k < 64; ++k) {
+            if (e) {
+                e = false;
+                const uint32_t c = (w[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+                bool ok = c == '"' || c == '\\' || c == '/' || c == 'b' || c == 'f' || c == 'n' || c == 'r' || c == 't';
+                if (c == 'u') {                               // (the document is padded past its end)
+                    const size_t p = (size_t)b * 64 + k;
+                    ok = is_hexc(j.doc[p + 1]) && is_hexc(j.doc[p + 2]) && is_hexc(j.doc[p + 3]) && is_hexc(j.doc[p + 4]);
+                }
+                if (!ok) js_fail(err, (unsigned long long)b * 64 + k - 1, KDTN_JSON_SYNTAX);
+            } else if ((bsm >> k) & 1) {
+                e = true;
+            }
+        }
+    }
     // control bytes: never inside a string; outside only \t \n \r
     if (ctl) {
         uint64_t bad = ctl & instr;
@@ -647,7 +680,6 @@ KD_INLINE uint32_t tkind(uint32_t meta) { return (meta >> 24) & 0xFu; }
 KD_INLINE uint32_t tsep(uint32_t meta) { return (meta >> 28) & 3u; }
 KD_INLINE uint32_t tdepth(uint32_t meta) { return meta & TK_DEPTH_MASK; }
 KD_INLINE bool value_start(uint32_t k) { return k == TK_OBJ || k == TK_ARR || k == TK_STR || k == TK_SCALAR; }
-KD_INLINE bool is_hexc(uint32_t c) { return (c >= '0' && c <= '9') || ((c | 32) >= 'a' && (c | 32) <= 'f'); }
 
 // closing quote of the string literal whose opening quote is at pos
 KD_INLINE uint32_t str_end(const JsDoc& j, uint32_t pos) {
@@ -874,24 +906,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_validate(JsDoc j, JsToks tk, uint3
     }
     // (a scalar's own grammar is checked by k_js_scalars over the compacted list of scalar
     // tokens: here, one scalar in a wave of 64 tokens made the whole wave run its check)
-    if (ok && kind == TK_STR && !(KDTN_PROFILING && (j.variant & JSV_NO_STRCHK))) {
-        bool bs;
-        const uint32_t e = str_end_bs(j, pos, &bs);
-        if (bs) {                                                 // escapes: \" \\ \/ \b \f \n \r \t \uXXXX
-            for (uint32_t k = pos + 1; k < e && ok; ++k) {
-                if (j.doc[k] != '\\') continue;
-                const uint32_t c = j.doc[k + 1];
-                if (c == 'u') {
-                    ok = k + 5 < e && is_hexc(j.doc[k + 2]) && is_hexc(j.doc[k + 3]) && is_hexc(j.doc[k + 4]) &&
-                         is_hexc(j.doc[k + 5]);
-                    k += 5;
-                } else {
-                    ok = c == '"' || c == '\\' || c == '/' || c == 'b' || c == 'f' || c == 'n' || c == 'r' || c == 't';
-                    k += 1;
-                }
-            }
-        }
-    }
+    // (a string's escapes are checked by k_js_classify, per escaped byte of the block masks)
     if (!ok) js_fail(err, pos, KDTN_JSON_SYNTAX);
 }
 

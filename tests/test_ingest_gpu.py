@@ -94,6 +94,18 @@ def test_separator_error_offsets(engine):
     assert not bad, bad
 
 
+@pytest.mark.parametrize("doc", [b'"a\\x"', b'["\\u12G4"]', b'{"a\\q":1}', b'["ok", "b\\\\\\z"]', b'["\\u12"]',
+                                 b'{"items":[{"metadata":{"name":"' + b"x" * 70 + b'\\u00zz"}}]}'])
+def test_escape_error_offsets(engine, doc):
+    """A bad escape (checked per escaped byte from the block masks, in k_js_classify) is
+    rejected at its backslash, where the oracle's checkValid stops."""
+    e0, off0, _ = O.json_ingest(doc)
+    with pytest.raises(KdtnError) as ei:
+        engine.ingest(doc)
+    assert ei.value.code == abi.EBADMSG
+    assert (ei.value.info.json_err, ei.value.info.err_offset) == (e0, off0)
+
+
 def test_intern_tables_grow():
     """More distinct strings than the first table sizes (set from the record counts) hold: the
     values pass reruns on tables grown 4x until they fit, and the next decode starts from the
