@@ -848,7 +848,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_validate(JsDoc j, JsToks tk, uint3
         return q + 2 >= b0 && q < b0 + BLOCK ? tkind(st[q + 2 - b0]) : tkind(tk.meta[q]);
     };
     const uint32_t t = st[threadIdx.x + 2];
-    const uint32_t kind = tkind(t), d = tdepth(t), pos = tk.pos[i];
+    const uint32_t kind = tkind(t), d = tdepth(t);      // (the offset is read only where needed)
     const uint32_t p = sp[threadIdx.x + 1];
     const uint32_t pkind = p < JS_DEEP ? kind_of(p) : 0xFEu;
     const uint32_t ck = d == 0 ? 0xFFu : pkind;                   // container kind
@@ -861,7 +861,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_validate(JsDoc j, JsToks tk, uint3
         // token instead of the token stream, and the element's own token only for an error
         const bool cand = i != 0 && (d == 2 || d == 5) && (sep == SEP_COMMA || (sep == SEP_NONE && pk == TK_ARR)) &&
                           value_start(kind) && p < JS_DEEP && pkind == TK_ARR;
-        ecand[i] = (uint8_t)(!cand ? 0u : kind == TK_OBJ ? 1u : (kind == TK_SCALAR && j.doc[pos] == 'n') ? 2u : 3u);
+        ecand[i] = (uint8_t)(!cand ? 0u : kind == TK_OBJ ? 1u : (kind == TK_SCALAR && j.doc[tk.pos[i]] == 'n') ? 2u : 3u);
     }
     // The grammar over (previous token, separator, token): the rules the ',' / ':' tokens were
     // checked by are applied to the separator here, and the error lands where checkValid stops —
@@ -894,6 +894,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_validate(JsDoc j, JsToks tk, uint3
         ok = i == 0 ? (((VS >> kind) & 1u) && d == 0) : (ok && d != 0);   // d == 0: a second top-level value
     }
     if (sep_bad) {                                                // at the run's first separator
+        const uint32_t pos = tk.pos[i];
         uint32_t q = pos, at = pos;
         while (q > 0) {
             const uint32_t c = j.doc[q - 1];
@@ -907,7 +908,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_validate(JsDoc j, JsToks tk, uint3
     // (a scalar's own grammar is checked by k_js_scalars over the compacted list of scalar
     // tokens: here, one scalar in a wave of 64 tokens made the whole wave run its check)
     // (a string's escapes are checked by k_js_classify, per escaped byte of the block masks)
-    if (!ok) js_fail(err, pos, KDTN_JSON_SYNTAX);
+    if (!ok) js_fail(err, tk.pos[i], KDTN_JSON_SYNTAX);
 }
 
 // The end of the document, one thread: separators after the last token are checked as the
