@@ -1168,6 +1168,16 @@ __global__ void __launch_bounds__(BLOCK) k_js_elems_count(JsDoc j, JsToks tk, ui
     uint4 cv = *cp;
     uint32_t w[4] = {cv.x, cv.y, cv.z, cv.w};
     bool changed = false;
+    // the candidates' parents, then their roles, each as one batch of loads (in one loop with
+    // the role stores below, every candidate waited for the one before it)
+    uint32_t rr[JS_PER];
+#pragma unroll
+    for (int k = 0; k < JS_PER; ++k) {
+        const uint32_t vc = (w[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+        rr[k] = (vc && base + k < ntok) ? par[base + k] : JS_NONE;
+    }
+#pragma unroll
+    for (int k = 0; k < JS_PER; ++k) rr[k] = rr[k] < JS_DEEP ? (uint32_t)role[rr[k]] : (uint32_t)R_NONE;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         if (!w[q]) continue;
@@ -1177,7 +1187,7 @@ __global__ void __launch_bounds__(BLOCK) k_js_elems_count(JsDoc j, JsToks tk, ui
             const uint32_t vc = (w[q] >> (8 * h)) & 0xFFu;             // k_js_validate's value class
             if (i >= ntok || !vc) continue;
             changed = true;
-            const uint32_t r = role[par[i]];
+            const uint32_t r = rr[q * 4 + h];
             const uint32_t cls = r == R_ITEMS ? 1 : r == R_SPEC_LINKS ? 2 : r == R_STATUS_LINKS ? 3 : 0;
             w[q] = (w[q] & ~(0xFFu << (8 * h))) | (cls << (8 * h));   // the class, for k_js_elems_write
             if (!cls) continue;
