@@ -81,6 +81,7 @@ struct kdtn_ctx {
     // CUs, where the runtime's device-to-host copies in this process run as blit kernels. Used
     // when every destination is page-locked host memory, else the HIP copies.
     bool sdma_tried = false, sdma_ok = false, dl_sdma = false;
+    bool sdma_inited = false;   // hsa_init held and dl_sig created (outlives sdma_ok after a failed issue)
     hsa_agent_t sdma_gpu{}, sdma_cpu{};
     uint32_t sdma_engine = 0;
     hsa_signal_t dl_sig{};
@@ -181,7 +182,7 @@ struct kdtn_ctx {
     uint32_t tc_n = 0;
     bool tc_done = false;
     // CR ingest (kdtn_ingest.hip): document, block masks, token stream, decode scratch
-    DevBuf j_doc, j_q, j_bs, j_hb, j_qcnt, j_qoff, j_tok, j_open, j_close, j_gcnt, j_goff;
+    DevBuf j_doc, j_q, j_bs, j_hb, j_esc, j_qcnt, j_qoff, j_tok, j_open, j_close, j_gcnt, j_goff;
     DevBuf j_olist, j_vlist, j_slist;
     uint32_t j_kcap = 0, j_pcap = 0;   // intern table sizes that fit the last document
     DevBuf j_toks, j_par, j_role, j_ecls, j_odep, j_ord, j_tagg, j_gagg, j_cnt3, j_coff3, j_small, j_part;
@@ -202,6 +203,7 @@ struct kdtn_ctx {
     uint32_t* h_tot = nullptr;
     bool uploaded = false;
     bool ran = false;
+    bool synced = false;   // h_misc[1..4] hold the last run's list totals (kdtn_epoch_sync or counts_fresh)
     uint32_t last_stages = 0;
     // multi-GPU
     ncclComm_t comm = nullptr;
@@ -817,6 +819,22 @@ int prepare_epoch(kdtn_ctx* c, const kdtn_vni_table& vn, uint32_t slice, uint32_
     return prepare_work(c, slice, M, N);
 }
 
+// The last run's list totals in h_misc[1..3] (and the look-back error in [4]). kdtn_epoch_sync
+// reads them from the coherent host words k_reconcile writes; an output stage called without
+// it reads them here, after the run's stream, so no stage sizes its passes from the counts of
+// an earlier epoch.
+int counts_fresh(kdtn_ctx* c) {
+    if (c->synced) return KDTN_OK;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    for (int i = 0; i < 4; ++i) c->h_misc[1 + i] = __atomic_load_n(c->h_tot + i, __ATOMIC_ACQUIRE);
+    if (c->h_misc[4] != 0) {
+        std::snprintf(g_last_error, sizeof(g_last_error), "k_reconcile look-back timed out (0x%x)", c->h_misc[4]);
+        return KDTN_EIO;
+    }
+    c->synced = true;
+    return KDTN_OK;
+}
+
 // Which batch entries the daemons reach (k_reach; include/kdtn.h): c->f_send (add) and
 // c->f_reach_upd (update) flags of the last run; stamps destination daemons into `mark`.
 // coarse entry -> topology indexes of the last run's del / add / upd lists (k_list_coarse),
@@ -1037,7 +1055,7 @@ void kdtn_destroy(kdtn_ctx* c) {
                       &c->w_topo, &c->w_size, &c->w_err, &c->w_off, &c->w_part, &c->w_arena, &c->w_pinfo,
                       &c->f_mark, &c->f_send, &c->f_node_idx, &c->f_nodes, &c->f_counts, &c->f_base,
                       &c->f_part, &c->f_idx, &c->f_inv, &c->f_st, &c->f_node, &c->lc[0], &c->lc[1], &c->lc[2], &c->f_reach_upd, &c->tc_size, &c->tc_off, &c->tc_part, &c->tc_arena,
-                      &c->j_doc, &c->j_q, &c->j_bs, &c->j_hb, &c->j_qcnt, &c->j_qoff, &c->j_tok, &c->j_open,
+                      &c->j_doc, &c->j_q, &c->j_bs, &c->j_hb, &c->j_esc, &c->j_qcnt, &c->j_qoff, &c->j_tok, &c->j_open,
                       &c->j_close, &c->j_gcnt, &c->j_goff, &c->j_toks, &c->j_par,
                       &c->j_role, &c->j_ecls, &c->j_odep, &c->j_ord, &c->j_tagg, &c->j_gagg, &c->j_cnt3, &c->j_coff3, &c->j_small,
                       &c->j_part, &c->j_tflags, &c->j_owner, &c->j_rows, &c->j_kkeys, &c->j_pkeys, &c->j_vown, &c->j_kslots, &c->j_krep,
@@ -1092,7 +1110,7 @@ void kdtn_destroy(kdtn_ctx* c) {
     }
     if (c->ev_dl_ready) (void)hipEventDestroy(c->ev_dl_ready);
     if (c->ev_dl_done) (void)hipEventDestroy(c->ev_dl_done);
-    if (c->sdma_ok) {
+    if (c->sdma_inited) {
         (void)hsa_signal_destroy(c->dl_sig);
         (void)hsa_shut_down();                      // (balances sdma_setup's hsa_init)
     }
@@ -1546,6 +1564,7 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
     if (c->ev_done) HIP_TRY(hipEventRecord(c->ev_done, s));
     if (resolve && !pods_cur) c->pods_ready = true;           // the full build of this upload's rows
     c->ran = true;
+    c->synced = false;
     c->encoded = false;
     c->tc_done = false;
     c->fan_valid = false;
@@ -1570,11 +1589,8 @@ int kdtn_epoch_sync(kdtn_ctx* c, kdtn_counts* counts) {
         }
     }
     HIP_TRY(hipStreamSynchronize(c->stream));
-    for (int i = 0; i < 4; ++i) c->h_misc[1 + i] = __atomic_load_n(c->h_tot + i, __ATOMIC_ACQUIRE);
-    if (c->h_misc[4] != 0) {
-        std::snprintf(g_last_error, sizeof(g_last_error), "k_reconcile look-back timed out (0x%x)", c->h_misc[4]);
-        return KDTN_EIO;
-    }
+    c->synced = false;
+    TRY(counts_fresh(c));
     if (counts) {
         counts->n_del = c->h_misc[1];
         counts->n_upd = c->h_misc[2];
@@ -1672,7 +1688,7 @@ static bool sdma_setup(kdtn_ctx* c) {
         ok = hsa_signal_create(0, 0, nullptr, &c->dl_sig) == HSA_STATUS_SUCCESS;
     }
     if (!ok) (void)hsa_shut_down();
-    c->sdma_ok = ok;
+    c->sdma_ok = c->sdma_inited = ok;
     return ok;
 }
 
@@ -1715,9 +1731,16 @@ static bool sdma_download(kdtn_ctx* c, kdtn_batches* o) {
         pi.size = sizeof pi;
         if (hsa_amd_pointer_info(pc[i].dst, &pi, nullptr, nullptr, nullptr) != HSA_STATUS_SUCCESS) return false;
         if (pi.type != HSA_EXT_POINTER_TYPE_HSA && pi.type != HSA_EXT_POINTER_TYPE_LOCKED) return false;
-        const uint8_t* b = static_cast<const uint8_t*>(pi.hostBaseAddress);
-        const uint8_t* d = static_cast<const uint8_t*>(pc[i].dst);
+        uint8_t* b = static_cast<uint8_t*>(pi.hostBaseAddress);
+        uint8_t* d = static_cast<uint8_t*>(pc[i].dst);
         if (!b || d < b || d + pc[i].bytes > b + pi.sizeInBytes) return false;
+        // Memory registered with hipHostRegister / hsa_amd_memory_lock is reached by the copy
+        // engine through its agent address, which need not equal the host address: the
+        // engine writes agentBaseAddress + (d - hostBaseAddress). HSA allocations map both alike.
+        if (pi.type == HSA_EXT_POINTER_TYPE_LOCKED) {
+            if (!pi.agentBaseAddress) return false;
+            pc[i].dst = static_cast<uint8_t*>(pi.agentBaseAddress) + (d - b);
+        }
     }
     if (!n) return true;
     hsa_signal_store_screlease(c->dl_sig, n);
@@ -1743,6 +1766,7 @@ static bool sdma_download(kdtn_ctx* c, kdtn_batches* o) {
 int kdtn_epoch_download(kdtn_ctx* c, kdtn_batches* o) {
     if (!c || !o || !c->ran) return KDTN_EINVAL;
     HIP_TRY(hipSetDevice(c->device));
+    TRY(counts_fresh(c));
     HIP_TRY(hipStreamSynchronize(c->stream));
     TRY(kdtn_epoch_download_wait(c));
     if (sdma_download(c, o)) return kdtn_epoch_download_wait(c);
@@ -1759,6 +1783,7 @@ int kdtn_epoch_download(kdtn_ctx* c, kdtn_batches* o) {
 int kdtn_epoch_download_async(kdtn_ctx* c, kdtn_batches* o) {
     if (!c || !o || !c->ran) return KDTN_EINVAL;
     HIP_TRY(hipSetDevice(c->device));
+    TRY(counts_fresh(c));
     TRY(kdtn_epoch_download_wait(c));
     HIP_TRY(hipStreamSynchronize(c->stream));       // (idle after kdtn_epoch_sync: returns at once)
     if (sdma_download(c, o)) return KDTN_OK;
@@ -1908,6 +1933,7 @@ int kdtn_epoch_encode(kdtn_ctx* c, uint64_t* n_bytes) {
     if (!c || !c->ran) return KDTN_EINVAL;
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    TRY(counts_fresh(c));
     hipStream_t s = c->stream;
     const uint32_t nd = c->h_misc[1], nu = c->h_misc[2], na = c->h_misc[3];
     const uint32_t T = c->T;
@@ -2004,6 +2030,7 @@ namespace {
 int fanout_compute(kdtn_ctx* c) {
     if (c->fan_valid) return KDTN_OK;
     HIP_TRY(hipStreamSynchronize(c->stream));
+    TRY(counts_fresh(c));
     hipStream_t s = c->stream;
     const uint32_t na = c->h_misc[3], D = c->D;
     const uint32_t nw = (D + 3) / 4;                          // destination-daemon flag bytes (words of 4)
@@ -2071,6 +2098,7 @@ int kdtn_epoch_fanout(kdtn_ctx* c, kdtn_fanout* o) {
     if (!c || !o || !c->ran) return KDTN_EINVAL;
     if (!fanout_stages_ok(c)) return KDTN_EINVAL;
     HIP_TRY(hipSetDevice(c->device));
+    TRY(counts_fresh(c));
     hipStream_t s = c->stream;
     c->n_ev = 0;
     (void)hipEventRecord(c->ev[0], s);
@@ -2100,6 +2128,7 @@ int kdtn_epoch_fanout(kdtn_ctx* c, kdtn_fanout* o) {
 int kdtn_epoch_remote_encode(kdtn_ctx* c, kdtn_remote_info* info) {
     if (!c || !c->ran || !fanout_stages_ok(c)) return KDTN_EINVAL;
     HIP_TRY(hipSetDevice(c->device));
+    TRY(counts_fresh(c));
     hipStream_t s = c->stream;
     c->n_ev = 0;
     (void)hipEventRecord(c->ev[0], s);
@@ -2221,6 +2250,7 @@ int kdtn_epoch_tc(kdtn_ctx* c, uint64_t* n_bytes) {
         return KDTN_EINVAL;
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    TRY(counts_fresh(c));
     hipStream_t s = c->stream;
     const uint32_t nu = c->h_misc[2], na = c->h_misc[3];
     const uint64_t n = 2ull * na + nu;                    // command slots: 2 per add entry, 1 per update
@@ -2406,7 +2436,7 @@ static int json_decode(kdtn_ctx* c, const JsTargets& tg, JsCounts* o, kdtn_inges
     HIP_TRY(hipMemsetAsync(small, 0xFF, 16, s));
     HIP_TRY(hipMemsetAsync(small + 2, 0, J_SMALL - 16, s));
     // one word past the end: any_in reads the word after a string's first (its bits are masked)
-    for (DevBuf* b : {&c->j_q, &c->j_bs, &c->j_hb, &c->j_tok, &c->j_open, &c->j_close}) TRY(ensure(*b, ((size_t)nb + 1) * 8));
+    for (DevBuf* b : {&c->j_q, &c->j_bs, &c->j_hb, &c->j_esc, &c->j_tok, &c->j_open, &c->j_close}) TRY(ensure(*b, ((size_t)nb + 1) * 8));
     // per-workgroup counts (quotes; tokens, depth, opens, colons, scalars) and their offsets
     const uint32_t nwg = nblocks(nb);
     TRY(ensure(c->j_qcnt, (size_t)nwg * 4));
@@ -2414,7 +2444,7 @@ static int json_decode(kdtn_ctx* c, const JsTargets& tg, JsCounts* o, kdtn_inges
     TRY(ensure(c->j_gcnt, (size_t)5 * nwg * 4));
     TRY(ensure(c->j_goff, (size_t)5 * (nwg + 1) * 8));
     JsDoc j{dp<uint8_t>(c->j_doc), (uint32_t)c->j_n, nb, dp<uint64_t>(c->j_q), dp<uint64_t>(c->j_bs),
-            dp<uint64_t>(c->j_hb), 0u};
+            dp<uint64_t>(c->j_hb), dp<uint64_t>(c->j_esc), 0u};
 #if KDTN_PROFILING
     j.variant = (uint32_t)std::strtoul(std::getenv("KDTN_JS_VARIANT") ? std::getenv("KDTN_JS_VARIANT") : "0", nullptr, 0);
 #endif
@@ -2424,6 +2454,7 @@ static int json_decode(kdtn_ctx* c, const JsTargets& tg, JsCounts* o, kdtn_inges
 
     // 1. block masks, string state, token counts, depth
     k_js_quotes<<<nblocks(nb), BLOCK, 0, s>>>(j, dp<uint64_t>(c->j_q), dp<uint64_t>(c->j_bs), dp<uint64_t>(c->j_hb),
+                                              dp<uint64_t>(c->j_esc),
                                              dp<uint32_t>(c->j_qcnt));
     TRY(scan_u32(c, dp<uint32_t>(c->j_qcnt), nwg, dp<uint64_t>(c->j_qoff)));
     k_js_classify<<<nwg, BLOCK, 0, s>>>(j, dp<uint64_t>(c->j_qoff), m, nwg, small);
@@ -3000,6 +3031,7 @@ int vni_ops_compute(kdtn_ctx* c, uint32_t* nd_out, uint32_t* na_out) {
     }
     hipStream_t s = c->stream;
     HIP_TRY(hipStreamSynchronize(s));                 // counts of the run (h_misc)
+    TRY(counts_fresh(c));
     const uint32_t nd = c->h_misc[1], na = c->h_misc[3];
     if (2ull * na + nd + c->V >= 0x7FFFFFFFull) return KDTN_EINVAL;
     TRY(ensure(c->vx_ops, ((size_t)nd + 2ull * na) * 16));
@@ -3452,6 +3484,7 @@ int kdtn_epoch_commit(kdtn_ctx* c, const uint8_t* mask, uint32_t* n_committed) {
         TRY(upload(c, c->st_mask, mask, T));
         dmask = dp<uint8_t>(c->st_mask);
     } else {
+        TRY(counts_fresh(c));
         TRY(run_reach(c, nullptr, 0));                      // per-topology first failing entries
         cut = dp<uint32_t>(c->f_cut);
     }

@@ -117,14 +117,15 @@ KD_INLINE void group_sums(uint64_t a, uint64_t d, uint64_t* sh, uint32_t* g, uin
     }
 }
 
-KD_INLINE uint32_t quote_block(const JsDoc& j, uint32_t b, uint64_t* qmask, uint64_t* bsmask, uint64_t* hbmask);
+KD_INLINE uint32_t quote_block(const JsDoc& j, uint32_t b, uint64_t* qmask, uint64_t* bsmask, uint64_t* hbmask,
+                                uint64_t* escmask);
 
 __global__ void __launch_bounds__(BLOCK) k_js_quotes(JsDoc j, uint64_t* qmask, uint64_t* bsmask,
-                                                     uint64_t* hbmask, uint32_t* gq) {
+                                                     uint64_t* hbmask, uint64_t* escmask, uint32_t* gq) {
     __shared__ uint64_t sh[BLOCK / 64];
     const uint32_t b = blockIdx.x * BLOCK + threadIdx.x;
     uint32_t nq = 0;
-    if (b < j.nb) nq = quote_block(j, b, qmask, bsmask, hbmask);
+    if (b < j.nb) nq = quote_block(j, b, qmask, bsmask, hbmask, escmask);
     uint32_t x = nq;
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
@@ -138,7 +139,8 @@ __global__ void __launch_bounds__(BLOCK) k_js_quotes(JsDoc j, uint64_t* qmask, u
     }
 }
 
-KD_INLINE uint32_t quote_block(const JsDoc& j, uint32_t b, uint64_t* qmask, uint64_t* bsmask, uint64_t* hbmask) {
+KD_INLINE uint32_t quote_block(const JsDoc& j, uint32_t b, uint64_t* qmask, uint64_t* bsmask, uint64_t* hbmask,
+                                uint64_t* escmask) {
     uint32_t w[16];
     load_block(j.doc, b, w);
     uint64_t bs = 0, q = 0, hb = 0;
@@ -172,6 +174,7 @@ KD_INLINE uint32_t quote_block(const JsDoc& j, uint32_t b, uint64_t* qmask, uint
     qmask[b] = quote;
     bsmask[b] = bs;
     hbmask[b] = hb;
+    escmask[b] = esc;                         // k_js_classify checks these bytes (no second run scan)
     return __popcll(quote);
 }
 
@@ -223,37 +226,25 @@ KD_INLINE void classify_block(const JsDoc& j, uint32_t b, uint64_t quote, bool S
     }
     const uint64_t scalar_start = scalar & ~((scalar << 1) | (uint64_t)prev_scalar);
     const uint64_t tok = structural | str_open | scalar_start;
-    // escapes (checkValid's stateInStringEsc*): the byte after an odd backslash run must be one
-    // of " \ / b f n r t, or u and four hex digits; reported at the backslash. A backslash
-    // outside a string fails the grammar anyway, so the check needs no string state.
-    const uint64_t bsm = j.bsmask[b];
-    const bool pe = b > 0 && (j.bsmask[b - 1] >> 63) != 0;   // a run may end right before the block
-    if (bsm || pe) {
-        bool e = false;
-        if (pe) {                                             // its parity
-            uint64_t i = (uint64_t)b * 64 - 1, run = 0;
-            for (;;) {
-                if (j.doc[i] != '\\') break;
-                ++run;
-                if (i == 0) break;
-                --i;
-            }
-            e = run & 1;
+    // escapes (checkValid's stateInStringEsc*): the byte after an odd backslash run (k_js_quotes'
+    // escaped-byte mask) must be one of " \ / b f n r t, or u and four hex digits. Reported where
+    // the scanner stops: at the escape byte, or at the first non-hex digit of \uXXXX (an escape
+    // cut by the document's end at its length). A backslash outside a string fails the grammar
+    // anyway, so the check needs no string state.
+    uint64_t escm = j.escmask[b];
+    while (escm) {
+        const int k = __ffsll((long long)escm) - 1;
+        escm &= escm - 1;
+        const uint32_t c = (w[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+        const unsigned long long p = (unsigned long long)b * 64 + k;
+        unsigned long long at = ~0ull;
+        if (c == 'u') {                                       // (the document is padded past its end)
+            for (int i = 1; i <= 4 && at == ~0ull; ++i)
+                if (!is_hexc(j.doc[p + i])) at = p + i;
+        } else if (!(c == '"' || c == '\\' || c == '/' || c == 'b' || c == 'f' || c == 'n' || c == 'r' || c == 't')) {
+            at = p;
         }
-        for (int k = 0; k < 64; ++k) {
-            if (e) {
-                e = false;
-                const uint32_t c = (w[k >> 2] >> (8 * (k & 3))) & 0xFFu;
-                bool ok = c == '"' || c == '\\' || c == '/' || c == 'b' || c == 'f' || c == 'n' || c == 'r' || c == 't';
-                if (c == 'u') {                               // (the document is padded past its end)
-                    const size_t p = (size_t)b * 64 + k;
-                    ok = is_hexc(j.doc[p + 1]) && is_hexc(j.doc[p + 2]) && is_hexc(j.doc[p + 3]) && is_hexc(j.doc[p + 4]);
-                }
-                if (!ok) js_fail(err, (unsigned long long)b * 64 + k - 1, KDTN_JSON_SYNTAX);
-            } else if ((bsm >> k) & 1) {
-                e = true;
-            }
-        }
+        if (at != ~0ull) js_fail(err, at < j.n ? at : (unsigned long long)j.n, KDTN_JSON_SYNTAX);
     }
     // control bytes: never inside a string; outside only \t \n \r
     if (ctl) {

@@ -146,13 +146,24 @@ struct DevLinks {
 //           16-B stores (about half the store instructions of two 32-struct halves of 8-B stores)
 //   bit 14: first bulk record's columns loaded before the gate / count / base phases (product;
 //           A/B vs 515: 0.6164 / 0.6180 ms at 1M pods, 0.0849 / 0.0869 at 125k, 0.1563 / 0.1583 config 4)
+//   bit 16: bulk emission by LDS-DMA: each wave copies whole 64-record tiles of the link store
+//           (the 20 of 22 column units an entry reads, 1 KiB per global_load_lds_dwordx4) into its
+//           LDS slot and reads its record's columns there; the next tile's copy is issued behind
+//           this record's gathers
 constexpr int VAR_NT_LOAD = 1, VAR_NT_STORE = 2, VAR_NO_QSTORE = 4, VAR_NT_POD = 8, VAR_TRACE = 16,
               VAR_SKIP_POD = 32, VAR_SKIP_PCT = 64, VAR_OCC5 = 128, VAR_OCC6 = 256,
               VAR_MASK_EMPTY = 512, VAR_NO_PREFIX = 1024, VAR_DIFF = 2048, VAR_DECODE_FIRST = 4096, VAR_PREFETCH = 16384,
-              VAR_Q16 = 32768;
+              VAR_Q16 = 32768, VAR_GLDS = 65536,
+              VAR_PMAC_COLS = 131072;   // (internal to VAR_GLDS) the entry's peer_mac id is in RecCols
+// VAR_GLDS: the tile column units an add entry reads, in LDS order: local_ip, local_mac (key 1, 2),
+// peer_ip, peer_mac, peer_pod (key 4..6), the 12 properties, gap, uid (2 units): every column of
+// the tile but local_intf and peer_intf. A delete reads units 0, 1 and the uid (at units 2, 3).
+constexpr int GL_UNITS = 20;
+KD_INLINE int gl_col(int u) { return u < 2 ? u + 1 : u + 2; }     // add tile: LDS unit -> tile column unit
+KD_INLINE int gl_col_del(int u) { return u < 2 ? u + 1 : u + 18; }   // delete tile (units 0..3)
 constexpr int DIFF_WAVES = 5;
 constexpr int var_waves(int v) {
-    return (v & VAR_OCC6) ? 6 : (v & VAR_OCC5) ? 5 : (v & VAR_DIFF) ? DIFF_WAVES : (v & VAR_PREFETCH) ? 4 : 1;
+    return (v & VAR_OCC6) ? 6 : (v & VAR_OCC5) ? 5 : (v & VAR_DIFF) ? DIFF_WAVES : (v & (VAR_PREFETCH | VAR_GLDS)) ? 4 : 1;
 }
 constexpr int TRACE_WORDS = 8;   // entry, topologies loaded, counts done, bases known, end, hw ids,
                                   // CalcDiff window phase A done, phase B done (fast path)
@@ -162,7 +173,8 @@ constexpr int DEFAULT_VARIANT = VAR_NT_LOAD | VAR_NT_STORE | VAR_MASK_EMPTY | VA
 // trace build of the default
 #define KDTN_PROFILING_VARIANTS(X) X(0) X(1) X(2) X(3) X(4) X(5) X(9) X(11) X(17) X(33) X(65) X(97) \
     X(101) X(113) X(129) X(257) X(513) X(521) X(523) X(529) X(531) X(545) X(547) X(579) X(611) X(519) \
-    X(641) X(643) X(771) X(1025) X(1537) X(2579) X(4611) X(515) X(16915) X(16963) X(16931) X(16995) X(16903) X(49667)
+    X(641) X(643) X(771) X(1025) X(1537) X(2579) X(4611) X(515) X(16915) X(16963) X(16931) X(16995) X(16903) X(49667) \
+    X(66051) X(65539)
 
 struct DevTopos {
     const uint32_t* ns;
@@ -683,6 +695,7 @@ struct JsDoc {
     const uint64_t* qmask;     // unescaped quotes
     const uint64_t* bsmask;    // backslashes
     const uint64_t* hbmask;    // bytes >= 0x80
+    const uint64_t* escmask;   // bytes escaped by an odd backslash run right before them
     uint32_t variant;          // (profiling build) KDTN_JS_VARIANT bits, 0 otherwise
 };
 struct JsMasks {
@@ -740,7 +753,8 @@ struct JsIntern {
     JsDict kd, pd;
     uint32_t variant;
 };
-__global__ void k_js_quotes(JsDoc j, uint64_t* qmask, uint64_t* bsmask, uint64_t* hbmask, uint32_t* gq);
+__global__ void k_js_quotes(JsDoc j, uint64_t* qmask, uint64_t* bsmask, uint64_t* hbmask, uint64_t* escmask,
+                            uint32_t* gq);
 __global__ void k_js_classify(JsDoc j, const uint64_t* gqoff, JsMasks m, uint32_t ng, unsigned long long* err);
 __global__ void k_js_tokens(JsDoc j, JsMasks m, const uint64_t* goff, uint32_t ng, JsToks tk, uint32_t* olist,
                             uint8_t* odep, uint32_t* vlist, uint32_t* slist, unsigned long long* err);

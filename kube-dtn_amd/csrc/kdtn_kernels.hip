@@ -960,6 +960,7 @@ KD_INLINE uint32_t vni_lookup(const DevTables& tb, uint32_t node, int32_t vni) {
 // Columns of one link record that the outputs need, loaded together (one round trip).
 struct RecCols {
     uint32_t lip, lmac, pp, pip;      // local_ip, local_mac, peer_pod, peer_ip (kdict ids)
+    uint32_t pmac;                    // peer_mac (VAR_GLDS bulk emission only: VAR_PMAC_COLS)
     uint32_t prop[KDTN_NPROP];        // pdict ids
     uint32_t gap;
     int64_t uid;
@@ -1259,7 +1260,8 @@ KD_INLINE uint4 add_calc(const RecCols& c, const AddGath& g, const DevLinks& N, 
             } else if (p_src == tc.src) {
                 kind = KDTN_KIND_SAME_NODE;                                               // :399-418
                 err = pip_bad ? (uint32_t)KDTN_E_PEER_VETH_CIDR                         // MakeVeth(peer) :402
-                    : kbit(tb, KB_MAC_BAD, N.key_s<NTL>(KDTN_K_PEER_MAC, j)) ? (uint32_t)KDTN_E_PEER_VETH_MAC : 0u;
+                    : kbit(tb, KB_MAC_BAD, (V & VAR_PMAC_COLS) ? c.pmac : N.key_s<NTL>(KDTN_K_PEER_MAC, j))
+                        ? (uint32_t)KDTN_E_PEER_VETH_MAC : 0u;
             } else {
                 kind = KDTN_KIND_CROSS_NODE;                                              // :419-453
                 vtep = p_src;
@@ -1398,16 +1400,24 @@ struct RecShared {
     uint32_t base[3];
     uint32_t ticket;
     uint32_t any_cmp;
-    union {                       // CalcDiff hashes, then (emission) per-wave qdisc staging
-        uint32_t hash[CAP];
-        uint2 stage[BLOCK / 64][32 * 9];
-    };
-    uint16_t rank[CAP];          // entry position within the workgroup's list
-    uint16_t dense[CAP];         // fast path: the flagged records, in record order
     uint32_t n_dense;
-    uint16_t tgt[CAP];           // upd target, relative to the workgroup's first desired record
-    uint8_t flag[CAP];
-    uint8_t lt[CAP];
+    union {
+        struct {                  // comparison windows (gate + CalcDiff, fast-path emission)
+            uint16_t rank[CAP];  // entry position within the workgroup's list
+            uint16_t dense[CAP]; // fast path: the flagged records, in record order
+            uint16_t tgt[CAP];   // upd target, relative to the workgroup's first desired record
+            uint8_t flag[CAP];
+            uint8_t lt[CAP];
+            union {               // CalcDiff hashes, then (emission) per-wave qdisc staging
+                uint32_t hash[CAP];
+                uint2 stage[BLOCK / 64][32 * 9];
+            };
+        };
+        struct {                  // (VAR_GLDS, profiling build) bulk emission: one link tile per wave
+            uint32_t tiles[BLOCK / 64][KDTN_PROFILING ? GL_UNITS * TILE_RECS : 1];
+            uint2 bstage[BLOCK / 64][32 * 9];
+        };
+    };
 };
 
 // need element comparisons: both lists non-nil and non-empty
@@ -1826,6 +1836,79 @@ KD_INLINE void trace_mark(const RecWork& wk, uint32_t wg, int k, unsigned long l
     }
 }
 
+// ---- VAR_GLDS: bulk emission from LDS-DMA'd link tiles ----------------------------------
+// The records [rlo, rhi) of a bulk chunk (old part [0, no) then new part) as whole 64-record
+// tiles of the two link stores: tile g of the list is old tile to0 + g (g < nto), else new tile
+// tn0 + g - nto. A wave takes tiles wave, wave + 4, ...; lane l handles record 64 t + l.
+struct GlPlan {
+    uint32_t oa, ob, na, nb;          // old / new record ranges
+    uint32_t to0, nto, tn0, nt;       // first tiles, old tile count, all tiles
+};
+KD_INLINE GlPlan gl_plan(uint32_t rlo, uint32_t rhi, uint32_t no, uint32_t o0, uint32_t n0) {
+    GlPlan p;
+    p.oa = o0 + min(rlo, no);
+    p.ob = o0 + min(rhi, no);
+    p.na = n0 + (max(rlo, no) - no);
+    p.nb = n0 + (max(rhi, no) - no);
+    p.to0 = p.oa >> 6;
+    p.nto = p.ob > p.oa ? ((p.ob - 1) >> 6) - p.to0 + 1 : 0u;
+    p.tn0 = p.na >> 6;
+    p.nt = p.nto + (p.nb > p.na ? ((p.nb - 1) >> 6) - p.tn0 + 1 : 0u);
+    return p;
+}
+
+// One 16-B piece per lane into this wave's LDS slot: lane l of the instruction writes bytes
+// [16 l, 16 l + 16) after `dst` (wave-uniform); the source address is the lane's own.
+template <bool NT>
+KD_INLINE void glds16(const void* src, uint32_t* dst) {
+    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)dst, 16, 0, NT ? 2 : 0);
+}
+
+// Copy tile g of the plan into `slot`: an add tile as GL_UNITS column units (5 instructions of
+// 64 pieces), a delete tile as 4 (local_ip, local_mac, uid; one instruction). A piece whose
+// records all lie outside the plan's range (the chunk's edge tiles) is not copied.
+template <bool NT>
+KD_INLINE void gl_issue(const GlPlan& p, uint32_t g, const DevLinks& O, const DevLinks& N, uint32_t* slot,
+                        int lane) {
+    if (g >= p.nt) return;
+    const bool old = g < p.nto;
+    const uint32_t t = old ? p.to0 + g : p.tn0 + (g - p.nto);
+    const uint32_t lo = old ? p.oa : p.na, hi = old ? p.ob : p.nb, t64 = t * 64u;
+    const uint32_t rlo = lo > t64 ? lo - t64 : 0u, rhi = min(hi - t64, 64u);
+    const uint8_t* tile = reinterpret_cast<const uint8_t*>((old ? O.base : N.base) + (size_t)t * TILE_WORDS);
+    const int k = lane & 15;
+    if (old) {
+        const int u = lane >> 4;
+        const uint32_t r0 = u < 2 ? k * 4 : (u - 2) * 32 + k * 2, r1 = r0 + (u < 2 ? 4 : 2);
+        if (r0 < rhi && r1 > rlo) glds16<NT>(tile + gl_col_del(u) * 256 + k * 16, slot);
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < GL_UNITS / 4; ++i) {
+        const int u = i * 4 + (lane >> 4);
+        const uint32_t r0 = u < 18 ? k * 4 : (u - 18) * 32 + k * 2, r1 = r0 + (u < 18 ? 4 : 2);
+        if (r0 < rhi && r1 > rlo) glds16<NT>(tile + gl_col(u) * 256 + k * 16, slot + i * 256);
+    }
+}
+
+// This lane's record columns from the wave's tile slot
+KD_INLINE void gl_cols(const uint32_t* slot, int lane, bool old, RecCols& c) {
+    c.lip = slot[lane];
+    c.lmac = slot[64 + lane];
+    if (old) {
+        c.uid = reinterpret_cast<const int64_t*>(slot + 2 * 64)[lane];
+        return;
+    }
+    c.pip = slot[2 * 64 + lane];
+    c.pmac = slot[3 * 64 + lane];
+    c.pp = slot[4 * 64 + lane];
+#pragma unroll
+    for (int k = 0; k < KDTN_NPROP; ++k) c.prop[k] = slot[(5 + k) * 64 + lane];
+    c.gap = slot[17 * 64 + lane];
+    c.uid = reinterpret_cast<const int64_t*>(slot + 18 * 64)[lane];
+}
+
 template <int V>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(var_waves(V))))
 k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWork wk) {
@@ -2058,6 +2141,56 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
 
     // ---- 4. emission -------------------------------------------------------------------
     uint2* stage = s.stage[tid >> 6];
+    if constexpr ((V & VAR_GLDS) != 0 && !kDefer) {
+        if (bulk) {
+            // Bulk emission from LDS-DMA'd tiles: the wave's tile is read from its slot, the
+            // record's gathers are issued, then the wave's next tile is copied into the slot
+            // (its reads have retired) while the gathers are in flight.
+            const int wave = tid >> 6, lane = tid & 63;
+            GlPlan pl = gl_plan(rlo, rhi, no, o0, n0);
+            // the plan in VGPRs: the emission's scalar registers hold the table bases
+            asm volatile("" : "+v"(pl.oa), "+v"(pl.ob), "+v"(pl.na), "+v"(pl.nb), "+v"(pl.to0), "+v"(pl.tn0));
+            uint32_t* slot = s.tiles[wave];
+            uint2* bst = s.bstage[wave];
+            gl_issue<NTL>(pl, (uint32_t)wave, O, N, slot, lane);
+            for (uint32_t g = wave; g < pl.nt; g += BLOCK / 64) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");            // the tile has landed
+                const bool old = g < pl.nto;
+                const uint32_t t = old ? pl.to0 + g : pl.tn0 + (g - pl.nto);
+                const uint32_t x = t * 64u + lane;
+                const bool in = old ? (x >= pl.oa && x < pl.ob) : (x >= pl.na && x < pl.nb);
+                int tt = 0;
+                bool on = false;
+                if (in) {
+                    tt = find_seg(old ? s.ooff : s.noff, 0, nt, x);
+                    on = s.act[tt] == KDTN_ACT_DIFF;
+                }
+                RecCols cc;
+                if (on) gl_cols(slot, lane, old, cc);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");          // slot reads retired
+                bool qa = false;
+                uint32_t e = 0, q[18];
+                const TopoCtx tc{s.ns[tt], s.src[tt], s.netns[tt]};
+                if (old) {
+                    gl_issue<NTL>(pl, g + BLOCK / 64, O, N, slot, lane);
+                    if (on) emit_del<V>(cc, x, tc, tb, out, bd + s.tcnt[0][tt] + (x - s.ooff[tt]), do_res);
+                } else {
+                    AddGath ga;
+                    if (on) add_gather<V>(cc, tc, tb, do_res, do_q, ga);
+                    gl_issue<NTL>(pl, g + BLOCK / 64, O, N, slot, lane);
+                    if (on) {
+                        e = ba + s.tcnt[2][tt] + (x - s.noff[tt]);
+                        add_finish<V | VAR_PMAC_COLS>(cc, ga, N, x, tc, tb, out, e, do_res, do_q, q);
+                        qa = do_q;
+                    }
+                }
+                wave_store_qdisc<V>(out.add_qdisc, qa, e, q, bst);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            trace_mark<V>(wk, wg, 4);
+            return;
+        }
+    }
     if (bulk) {
         // Every record of a DIFF topology is an entry at topology offset + index. Software
         // pipelined: a thread's next record's columns are loaded right after this record's

@@ -136,15 +136,19 @@ static int v_string(ovp* v) {
         if (c == '"') { v->i++; return 0; }
         if (c < 0x20) return vfail(v, KDTN_JSON_SYNTAX);
         if (c == '\\') {
+            /* the scanner stops at the byte it rejects: the escape byte, or the first non-hex
+               digit of \uXXXX (stateInStringEsc / stateInStringEscU*); past the end: EOF */
             if (v->i + 1 >= v->n) { v->i = v->n; return vfail(v, KDTN_JSON_SYNTAX); }
             uint8_t e = v->s[v->i + 1];
             if (e == 'u') {
-                for (int k = 0; k < 4; ++k)
-                    if (v->i + 2 + k >= v->n || !is_hex(v->s[v->i + 2 + k])) return vfail(v, KDTN_JSON_SYNTAX);
+                for (int k = 0; k < 4; ++k) {
+                    if (v->i + 2 + k >= v->n) { v->i = v->n; return vfail(v, KDTN_JSON_SYNTAX); }
+                    if (!is_hex(v->s[v->i + 2 + k])) { v->i += 2 + k; return vfail(v, KDTN_JSON_SYNTAX); }
+                }
                 v->i += 6;
                 continue;
             }
-            if (!strchr("\"\\/bfnrt", e) || e == 0) return vfail(v, KDTN_JSON_SYNTAX);
+            if (!strchr("\"\\/bfnrt", e) || e == 0) { v->i += 1; return vfail(v, KDTN_JSON_SYNTAX); }
             v->i += 2;
             continue;
         }

@@ -135,6 +135,30 @@ def test_syntax_errors(doc):
     assert e2 == jr.SYNTAX
 
 
+# Bad escapes with the offset Go's scanner reports (encoding/json scanner.go: checkValid stops
+# at the byte a step rejects; stateInStringEsc rejects the escape byte, stateInStringEscU* the
+# first non-hex digit; SyntaxError.Offset counts the bytes read, the rejected one included, so
+# the 0-based index here is Offset - 1; an escape cut by the document's end is "unexpected end
+# of JSON input" at len(data)). Derived by hand from those state functions, byte by byte.
+GO_ESCAPE_OFFSETS = [
+    (b'"a\\x"', 3),                       # 'x' after the backslash
+    (b'["\\u12G4"]', 6),                  # 'G', the third hex digit
+    (b'{"a\\q":1}', 4),                   # 'q'
+    (b'["ok", "b\\\\\\z"]', 12),        # a run of three: the third backslash escapes 'z'
+    (b'["\\u12"]', 6),                    # the closing quote is no hex digit
+    (b'{"items":[{"metadata":{"name":"' + b"x" * 70 + b'\\u00zz"}}]}', 105),   # crosses a 64-B block
+    (b'["\\u1', 5),                       # cut by the end
+    (b'"ab\\', 4),
+    (b'"' + b"\\\\" * 40 + b'\\e"', 82),  # an even run of 80 over two blocks, then a bad escape
+]
+
+
+@pytest.mark.parametrize("doc,off", GO_ESCAPE_OFFSETS)
+def test_escape_error_offsets_go_semantics(doc, off):
+    e, o, _ = oracle.json_ingest(doc)
+    assert (e, o) == (oracle.JSON_SYNTAX if hasattr(oracle, "JSON_SYNTAX") else 1, off)
+
+
 def test_depth_limit():
     ok = b"[" * 10000 + b"]" * 10000
     deep = b"[" * 10001 + b"]" * 10001

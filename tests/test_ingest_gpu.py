@@ -15,7 +15,7 @@ import json_ref as jr
 import oracle as O
 from kdtn import abi, synth
 from kdtn.engine import KdtnError
-from test_ingest_cpu import (BAD_SYNTAX, SEP_SYNTAX, DUPS, GO_STRINGS, TYPE_ERRORS, GOLDEN, rand_topos, s0p,
+from test_ingest_cpu import (BAD_SYNTAX, GO_ESCAPE_OFFSETS, SEP_SYNTAX, DUPS, GO_STRINGS, TYPE_ERRORS, GOLDEN, rand_topos, s0p,
                              sample_doc)
 
 pytestmark = pytest.mark.gpu
@@ -94,12 +94,14 @@ def test_separator_error_offsets(engine):
     assert not bad, bad
 
 
-@pytest.mark.parametrize("doc", [b'"a\\x"', b'["\\u12G4"]', b'{"a\\q":1}', b'["ok", "b\\\\\\z"]', b'["\\u12"]',
-                                 b'{"items":[{"metadata":{"name":"' + b"x" * 70 + b'\\u00zz"}}]}'])
-def test_escape_error_offsets(engine, doc):
-    """A bad escape (checked per escaped byte from the block masks, in k_js_classify) is
-    rejected at its backslash, where the oracle's checkValid stops."""
+@pytest.mark.parametrize("doc,go_off", GO_ESCAPE_OFFSETS)
+def test_escape_error_offsets(engine, doc, go_off):
+    """A bad escape (checked per escaped byte from k_js_quotes' escaped-byte mask, in
+    k_js_classify) is rejected where Go's scanner stops: at the escape byte, or at the first
+    non-hex digit of \\uXXXX (go_off: the offending byte's index = SyntaxError.Offset - 1; the
+    document's length for an escape cut by its end), as the oracle reports it."""
     e0, off0, _ = O.json_ingest(doc)
+    assert (e0, off0) == (abi.JSON_SYNTAX, go_off)
     with pytest.raises(KdtnError) as ei:
         engine.ingest(doc)
     assert ei.value.code == abi.EBADMSG

@@ -573,3 +573,78 @@ def test_download_into_page_locked_buffers(engine):
         engine.download_wait()
         assert_same(view, plain, f"seed {seed}: async download")
         assert_same(plain, O.reconcile(inp, tick=TICK), f"seed {seed}")
+
+
+def _loaded_hip_runtime():
+    """The HIP runtime this process already loaded (torch's or ROCm's), for hipHostRegister."""
+    import ctypes
+    with open("/proc/self/maps") as f:
+        paths = {ln.split()[-1] for ln in f if "libamdhip64.so" in ln}
+    assert paths, "no HIP runtime mapped"
+    return ctypes.CDLL(sorted(paths)[0])
+
+
+def test_download_into_registered_host_memory(engine):
+    """destinations registered with hipHostRegister (LOCKED pointers) reach the SDMA
+    engine through their agent address; every field equals the pageable download."""
+    import ctypes
+    import mmap
+    from kdtn.tables import BatchesOut
+    hip = _loaded_hip_runtime()
+    topos, inp = random_epoch_input(7, T=150)
+    engine.upload(inp)
+    engine.run()
+    engine.sync()
+    plain = engine.download()
+    cap = max(inp.realised.n, inp.desired.n, 1)
+    shapes = BatchesOut.alloc(inp.topos.n, cap, cap, cap)
+    maps, regs, arrays = [], [], []
+    try:
+        for a in vars(shapes).values():
+            n = max(a.nbytes, 1)
+            m = mmap.mmap(-1, (n + 4095) // 4096 * 4096)
+            maps.append(m)
+            arr = np.frombuffer(m, dtype=np.uint8, count=a.nbytes).view(a.dtype).reshape(a.shape)
+            addr = ctypes.addressof(ctypes.c_char.from_buffer(m))
+            assert hip.hipHostRegister(ctypes.c_void_p(addr), ctypes.c_size_t(len(m)), 0) == 0
+            regs.append(addr)
+            arrays.append(arr)
+        into = BatchesOut(*arrays)
+        assert_same(engine.download(into=into), plain, "registered: sync download")
+        for a in arrays:
+            a[...] = 0
+        view = engine.download_async(into)
+        engine.download_wait()
+        assert_same(view, plain, "registered: async download")
+    finally:
+        for addr in regs:
+            hip.hipHostUnregister(ctypes.c_void_p(addr))
+        del arrays
+
+
+def test_output_stages_without_sync_use_this_runs_counts(engine):
+    """an output stage called after kdtn_epoch_run without kdtn_epoch_sync reads this
+    run's list totals (counts_fresh), not the previous epoch's: a large epoch is synced, then a
+    small one is only run, and its download and wire encoding equal the small epoch's."""
+    _, big = random_epoch_input(11, T=400)
+    _, small = random_epoch_input(12, T=60)
+    engine.upload(small)
+    engine.run()
+    engine.sync()
+    want = engine.download()
+    n_want = engine.encode()
+    wire_want = engine.download_wire()
+    engine.upload(big)
+    engine.run()
+    engine.sync()
+    engine.upload(small)
+    engine.run()                                          # no sync before the stages
+    assert engine.encode() == n_want
+    for a, b in zip(engine.download_wire(), wire_want):
+        np.testing.assert_array_equal(a, b)
+    engine.upload(big)
+    engine.run()
+    engine.sync()
+    engine.upload(small)
+    engine.run()
+    assert_same(engine.download(), want, "download without sync")
