@@ -1529,6 +1529,7 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
 #define KDTN_VARIANT_CASE(V) \
         case V: k_reconcile<V><<<c->nwg * w.split, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w); placed = (V & VAR_DIFF) != 0; break;
         KDTN_PROFILING_VARIANTS(KDTN_VARIANT_CASE)
+        KDTN_VARIANT_CASE(DIFF_VARIANT)
 #undef KDTN_VARIANT_CASE
         default:
             k_reconcile<DEFAULT_VARIANT><<<c->nwg * w.split, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w);
@@ -1536,7 +1537,7 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         }
 #else
         if (c->real.n && c->des.n) {             // CalcDiff windows: the comparison-heavy build
-            k_reconcile<DEFAULT_VARIANT | VAR_DIFF><<<c->nwg * w.split, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w);
+            k_reconcile<DIFF_VARIANT><<<c->nwg * w.split, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w);
             placed = true;
         } else {
             k_reconcile<DEFAULT_VARIANT><<<c->nwg * w.split, BLOCK, 0, s>>>(T, c->real.view, c->des.view, tb, o, w);
@@ -1683,6 +1684,10 @@ static bool sdma_setup(kdtn_ctx* c) {
         (void)hsa_amd_memory_get_preferred_copy_engine(hv.agentOwner, dv.agentOwner, &pref);
         const uint32_t pick = (pref & mask) ? (pref & mask) : mask;
         c->sdma_engine = pick & (~pick + 1u);                       // lowest available engine bit
+#if KDTN_PROFILING
+        if (const char* ev = std::getenv("KDTN_SDMA_ENGINE"))          // (A/B) an engine bit of the mask
+            if ((uint32_t)std::atoi(ev) & mask) c->sdma_engine = (uint32_t)std::atoi(ev) & mask & (~((uint32_t)std::atoi(ev) & mask) + 1u);
+#endif
         c->sdma_gpu = dv.agentOwner;
         c->sdma_cpu = hv.agentOwner;
         ok = hsa_signal_create(0, 0, nullptr, &c->dl_sig) == HSA_STATUS_SUCCESS;

@@ -1440,6 +1440,9 @@ KD_INLINE uint8_t topo_action(const RecShared& s, int tt) {
 // tgt16 valid) or global scratch (single topology; targets go to wk.otarget). Leaves the
 // MASKED flag of every window record in flg and accumulates per-topology counts.
 // TR (profiling trace build): phase timestamps into tr[6] (A done) and tr[7] (B done).
+__device__ __forceinline__ void diff_window_tail(RecShared& s, int tb, int te, const DevLinks& N, const uint32_t* hsh, uint8_t* flg,
+                                 const uint8_t* lt, uint32_t no, uint32_t nn, uint32_t tot, uint32_t wn0);
+
 template <bool TR>
 __device__ void diff_window(RecShared& s, int tb, int te, const DevLinks& O, const DevLinks& N,
                             uint32_t* hsh, uint8_t* flg, uint8_t* lt, uint16_t* tgt16,
@@ -1533,6 +1536,13 @@ __device__ void diff_window(RecShared& s, int tb, int te, const DevLinks& O, con
         if (tid == 0) tr[7] = __builtin_amdgcn_s_memrealtime();
     }
 
+    diff_window_tail(s, tb, te, N, hsh, flg, lt, no, nn, tot, wn0);
+}
+
+// Phases C-E of a CalcDiff window (both forms)
+__device__ __forceinline__ void diff_window_tail(RecShared& s, int tb, int te, const DevLinks& N, const uint32_t* hsh, uint8_t* flg,
+                                 const uint8_t* lt, uint32_t no, uint32_t nn, uint32_t tot, uint32_t wn0) {
+    const int tid = threadIdx.x;
     // C. new side: any key-equal old record (CalcDiff :305-316). Key equality is an
     //    equivalence: j has one iff it is some old record's first match (marked in B) or
     //    equals an earlier marked new record of its topology (a duplicate key in spec).
@@ -1575,6 +1585,110 @@ __device__ void diff_window(RecShared& s, int tb, int te, const DevLinks& O, con
         if (f & RF_ADD) atomicAdd(&s.tcnt[2][tt], 1u);
     }
     __syncthreads();
+}
+
+// (VAR_AB) the LDS window with its first two phases merged: every old record is loaded with
+// the new record at its position in ONE round trip (both keys and properties), both key hashes
+// go to LDS and the positional key / DeepEqual bits to the old record's flag byte; new records
+// past their topology's old count hash their own key. The scan phase then reads only LDS,
+// loading keys (and properties on a key match) for a hash hit off the positional record.
+// Saves the new records' separate key pass (a round trip and 36 B per new record).
+template <bool TR>
+__device__ void diff_window_ab(RecShared& s, int tb, int te, const DevLinks& O, const DevLinks& N, uint32_t* hsh,
+                               uint8_t* flg, uint8_t* lt, uint16_t* tgt16, unsigned long long* tr = nullptr) {
+    const uint32_t wo0 = s.ooff[tb], wo1 = s.ooff[te];
+    const uint32_t wn0 = s.noff[tb], wn1 = s.noff[te];
+    const uint32_t no = wo1 - wo0, nn = wn1 - wn0, tot = no + nn;
+    const int tid = threadIdx.x;
+    constexpr uint8_t POS_KEY = 1, POS_EQ = 2;
+
+    // A. loads and hashes
+    for (uint32_t r = tid; r < tot; r += BLOCK) {
+        const bool old = r < no;
+        const uint32_t idx = old ? wo0 + r : wn0 + (r - no);
+        const int tt = find_seg(old ? s.ooff : s.noff, tb, te, idx);
+        lt[r] = (uint8_t)tt;
+        uint8_t f = 0;
+        if (need_cmp(s, tt)) {
+            const uint32_t os_ = s.ooff[tt], ns_ = s.noff[tt], ne_ = s.noff[tt + 1];
+            const uint32_t ko = s.ooff[tt + 1] - os_;
+            if (old) {
+                const uint32_t jp = ns_ + (idx - os_);
+                const bool have_p = jp < ne_;
+                uint32_t ki[KEYW], pi[PROPW], kj[KEYW], pj[PROPW];
+                load_key(O, idx, ki);
+                load_props(O, idx, pi);
+                if (have_p) {
+                    load_key(N, jp, kj);
+                    load_props(N, jp, pj);
+                }
+                hsh[r] = key_hash_w(ki);
+                if (have_p) hsh[no + (jp - wn0)] = key_hash_w(kj);
+                const bool pos_key = have_p && words_eq<KEYW>(ki, kj);
+                const bool pos_eq = pos_key && words_eq<PROPW>(pi, pj);
+                f = (pos_key ? POS_KEY : 0) | (pos_eq ? POS_EQ : 0);
+                if (ko == ne_ - ns_ && !pos_eq) s.dirty[tt] = 1;
+            } else if (idx - ns_ >= ko) {                    // no old record at its position
+                uint32_t k[KEYW];
+                load_key(N, idx, k);
+                hsh[r] = key_hash_w(k);
+            }
+        }
+        flg[r] = f;
+    }
+    __syncthreads();
+    if constexpr (TR) {
+        if (tid == 0) tr[6] = __builtin_amdgcn_s_memrealtime();
+    }
+
+    // B. old side: first key-equal new record (CalcDiff :289-303), from the LDS hashes
+    for (uint32_t r = tid; r < no; r += BLOCK) {
+        const int tt = lt[r];
+        uint8_t f = RF_DEL;
+        if (need_cmp(s, tt)) {
+            const uint32_t i = wo0 + r;
+            const uint32_t os_ = s.ooff[tt], ns_ = s.noff[tt], ne_ = s.noff[tt + 1];
+            const uint32_t jp = ns_ + (i - os_);
+            const uint8_t pb = flg[r];
+            const bool pos_key = pb & POS_KEY, pos_eq = pb & POS_EQ;
+            const uint32_t h = hsh[r];
+            uint32_t first = 0xFFFFFFFFu;
+            bool same_props = false;
+            const uint32_t jend = pos_key ? jp : ne_;        // before jp: an earlier duplicate only
+            for (uint32_t j = ns_; j < jend; ++j) {
+                if (j == jp || hsh[no + (j - wn0)] != h) continue;
+                uint32_t ki[KEYW], kx[KEYW], pi[PROPW], px[PROPW];   // one round trip per candidate
+                load_key(O, i, ki);
+                load_key(N, j, kx);
+                load_props(O, i, pi);
+                load_props(N, j, px);
+                if (words_eq<KEYW>(ki, kx)) {
+                    first = j;
+                    same_props = words_eq<PROPW>(pi, px);
+                    break;
+                }
+            }
+            if (first == 0xFFFFFFFFu && pos_key) {
+                first = jp;
+                same_props = pos_eq;
+            }
+            if (first != 0xFFFFFFFFu) {
+                flg[no + (first - wn0)] = RF_MATCHED;
+                if (!same_props) {
+                    f = RF_UPD;
+                    tgt16[r] = (uint16_t)(first - wn0);
+                } else {
+                    f = 0;
+                }
+            }
+        }
+        flg[r] = f;
+    }
+    __syncthreads();
+    if constexpr (TR) {
+        if (tid == 0) tr[7] = __builtin_amdgcn_s_memrealtime();
+    }
+    diff_window_tail(s, tb, te, N, hsh, flg, lt, no, nn, tot, wn0);
 }
 
 // Decoupled look-back over the workgroups' list counts (3 lists), one wave, 64
@@ -2024,10 +2138,16 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
         }
         __syncthreads();
     } else if (fast) {
-        if constexpr ((V & VAR_TRACE) != 0)
+        if constexpr ((V & VAR_AB) != 0) {
+            if constexpr ((V & VAR_TRACE) != 0)
+                diff_window_ab<true>(s, 0, nt, O, N, s.hash, s.flag, s.lt, s.tgt, wk.trace + (size_t)wg * TRACE_WORDS);
+            else
+                diff_window_ab<false>(s, 0, nt, O, N, s.hash, s.flag, s.lt, s.tgt);
+        } else if constexpr ((V & VAR_TRACE) != 0) {
             diff_window<true>(s, 0, nt, O, N, s.hash, s.flag, s.lt, s.tgt, wk.otarget, n0, wk.trace + (size_t)wg * TRACE_WORDS);
-        else
+        } else {
             diff_window<false>(s, 0, nt, O, N, s.hash, s.flag, s.lt, s.tgt, wk.otarget, n0);
+        }
     } else {
         for (int tt = 0; tt < nt; ++tt) {
             const uint32_t k = (s.ooff[tt + 1] - s.ooff[tt]) + (s.noff[tt + 1] - s.noff[tt]);
@@ -2506,7 +2626,7 @@ __global__ void __launch_bounds__(BLOCK) k_qdisc_batch(DevLinks props, DevTables
 }
 
 template __global__ void k_reconcile<DEFAULT_VARIANT>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
-template __global__ void k_reconcile<DEFAULT_VARIANT | VAR_DIFF>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
+template __global__ void k_reconcile<DIFF_VARIANT>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
 #if KDTN_PROFILING
 #define KDTN_VARIANT_INST(V) template __global__ void k_reconcile<V>(DevTopos, DevLinks, DevLinks, DevTables, RecOut, RecWork);
 KDTN_PROFILING_VARIANTS(KDTN_VARIANT_INST)

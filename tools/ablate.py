@@ -24,14 +24,47 @@ ap.add_argument("--cache", default="")
 ap.add_argument("--variants", default="", help="comma list of KDTN_VARIANT values, interleaved")
 ap.add_argument("--env", default="", help="NAME=v1,v2,...: interleaved A/B of an env knob, all stages timed")
 ap.add_argument("--wall", action="store_true", help="--env: also the wall time of run + sync at timing level 0")
+ap.add_argument("--churn", type=int, default=0, help="--variants over K epochs of the config-3 churn sequence "
+                "(each epoch uploaded once, the variants interleaved on it; k_reconcile + placement)")
 a = ap.parse_args()
 if a.variants or a.env:                 # A/B variants live in the profiling build
     from kdtn import engine as _kdtn_engine
     _kdtn_engine.use_profiling_library()
+res = {}
+if a.churn:                              # config 3 as the bench runs it: the churn sequence
+    cs = synth.ChurnSequence(pods_per_shard=a.pods)
+    eng = Engine(device=0)
+    vs = a.variants.split(",")
+    per = {v: [] for v in vs}
+    inp = cs.epoch_input()
+    for ep in range(a.churn):
+        if ep:
+            keep = (inp.kdict.n, inp.pdict.n)
+            cs.advance()
+            inp = cs.epoch_input()
+            eng.upload(inp, *keep)
+        else:
+            eng.upload(inp)
+        acc = {v: [] for v in vs}
+        for rep in range(a.reps + 2):
+            for v in vs:
+                os.environ["KDTN_VARIANT"] = v
+                eng.run(abi.STAGE_ALL)
+                eng.sync()
+                if rep >= 2:
+                    kt = eng.kernel_times()
+                    acc[v].append(kt["reconcile"] + kt.get("place", 0.0))
+        for v in vs:
+            per[v].append(sorted(acc[v])[len(acc[v]) // 2])
+    os.environ.pop("KDTN_VARIANT")
+    print(json.dumps({"config": 3, "pods": a.pods, "epochs": a.churn, "reps": a.reps,
+                      "reconcile_plus_place_ms": {v: {"mean_of_epoch_medians": round(sum(x) / len(x), 4),
+                                                      "per_epoch": [round(y, 4) for y in x]} for v, x in per.items()}},
+                     indent=1))
+    sys.exit(0)
 inp = synth.make(a.config, pods_per_shard=a.pods, cache_dir=a.cache or None)
 eng = Engine(device=0)
 eng.upload(inp)
-res = {}
 if a.variants:
     vs = [v for v in a.variants.split(",")]
     acc = {v: [] for v in vs}

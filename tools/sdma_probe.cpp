@@ -12,6 +12,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <vector>
 
 #define CK(x)                                                                      \
@@ -100,6 +101,46 @@ int main(int argc, char** argv) {
             CK(hsa_signal_destroy(sig));
         }
     }
+    // every engine alone, and each engine's D2H beside a concurrent HIP host-to-device copy
+    // (the pipelined resident loop: epoch k's download beside epoch k+1's delta upload)
+    void *dev2 = nullptr, *host2 = nullptr;
+    CK(hipMalloc(&dev2, n));
+    CK(hipHostMalloc(&host2, n, hipHostMallocDefault));
+    for (int dir = 0; dir < 2; ++dir) {
+        hsa_agent_t da = dir ? g_gpu : g_cpu, sa = dir ? g_cpu : g_gpu;
+        uint32_t mask = 0;
+        (void)hsa_amd_memory_copy_engine_status(da, sa, &mask);
+        char* dst = static_cast<char*>(dir ? dev : host);
+        char* src = static_cast<char*>(dir ? host : dev);
+        for (int b = 0; b < 16; ++b) {
+            if (!(mask & (1u << b))) continue;
+            for (int duplex = 0; duplex < (dir ? 1 : 2); ++duplex) {
+                hsa_signal_t sig;
+                CK(hsa_signal_create(1, 0, nullptr, &sig));
+                std::vector<double> t;
+                for (int r = 0; r < reps + 1; ++r) {
+                    hsa_signal_store_relaxed(sig, 1);
+                    double t0 = now();
+                    if (duplex) CK(hipMemcpyAsync(dev2, host2, n, hipMemcpyHostToDevice, s));
+                    CK(hsa_amd_memory_async_copy_on_engine(dst, da, src, sa, n, 0, nullptr, sig,
+                                                           (hsa_amd_sdma_engine_id_t)(1u << b), true));
+                    while (hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_EQ, 0, UINT64_MAX,
+                                                     HSA_WAIT_STATE_ACTIVE) != 0) {
+                    }
+                    if (duplex) CK(hipStreamSynchronize(s));
+                    if (r) t.push_back(now() - t0);
+                }
+                std::sort(t.begin(), t.end());
+                std::printf("{\"dir\": \"%s\", \"path\": \"engine 0x%x%s\", \"MB\": %zu, \"median_ms\": %.4f, "
+                            "\"best_ms\": %.4f, \"GBps_median\": %.2f}\n",
+                            dir ? "h2d" : "d2h", 1u << b, duplex ? " + hip h2d beside" : "", mb, t[t.size() / 2] * 1e3,
+                            t[0] * 1e3, n / t[t.size() / 2] / 1e9);
+                CK(hsa_signal_destroy(sig));
+            }
+        }
+    }
+    CK(hipHostFree(host2));
+    CK(hipFree(dev2));
     CK(hipHostFree(host));
     CK(hipFree(dev));
     return 0;
