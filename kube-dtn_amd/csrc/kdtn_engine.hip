@@ -83,7 +83,7 @@ struct kdtn_ctx {
     bool sdma_tried = false, sdma_ok = false, dl_sdma = false;
     bool sdma_inited = false;   // hsa_init held and dl_sig created (outlives sdma_ok after a failed issue)
     hsa_agent_t sdma_gpu{}, sdma_cpu{};
-    uint32_t sdma_engine = 0;
+    uint32_t sdma_engine[2] = {0, 0};   // the download's engines (bit masks; [1] = 0: one engine)
     hsa_signal_t dl_sig{};
     hipEvent_t ev_fill = nullptr, ev_ag = nullptr;
     // dictionaries; parsed tables persist across uploads for an append-only interner
@@ -1683,10 +1683,22 @@ static bool sdma_setup(kdtn_ctx* c) {
     if (ok) {
         (void)hsa_amd_memory_get_preferred_copy_engine(hv.agentOwner, dv.agentOwner, &pref);
         const uint32_t pick = (pref & mask) ? (pref & mask) : mask;
-        c->sdma_engine = pick & (~pick + 1u);                       // lowest available engine bit
+        // one engine, the lowest preferred one: beside the runtime's host-to-device copies it
+        // keeps 48 GB/s where the H2D-preferred engine falls to 28 (tools/sdma_probe.cpp,
+        // profiles/r06c_sdma_probe.jsonl). The download's pieces split over two engines measured
+        // no faster (profiles/r06f_resident_engines.jsonl); the profiling build can still ask
+        // for two (KDTN_SDMA_ENGINE = two engine bits)
+        c->sdma_engine[0] = pick & (~pick + 1u);
+        c->sdma_engine[1] = 0;
 #if KDTN_PROFILING
-        if (const char* ev = std::getenv("KDTN_SDMA_ENGINE"))          // (A/B) an engine bit of the mask
-            if ((uint32_t)std::atoi(ev) & mask) c->sdma_engine = (uint32_t)std::atoi(ev) & mask & (~((uint32_t)std::atoi(ev) & mask) + 1u);
+        if (const char* ev = std::getenv("KDTN_SDMA_ENGINE")) {        // (A/B) engine bits of the mask
+            const uint32_t e = (uint32_t)std::atoi(ev) & mask;
+            if (e) {
+                c->sdma_engine[0] = e & (~e + 1u);
+                const uint32_t r2 = e & ~c->sdma_engine[0];
+                c->sdma_engine[1] = r2 & (~r2 + 1u);
+            }
+        }
 #endif
         c->sdma_gpu = dv.agentOwner;
         c->sdma_cpu = hv.agentOwner;
@@ -1755,11 +1767,19 @@ static bool sdma_download(kdtn_ctx* c, kdtn_batches* o) {
         f.sig.push_back(c->dl_sig.handle);
     }
     c->dl_sdma = c->dl_pending = true;
-    for (int i = 0; i < n; ++i) {
+    // pieces to the engine with fewer bytes queued, largest first (one signal counts them all)
+    int order[12];
+    for (int i = 0; i < n; ++i) order[i] = i;
+    std::sort(order, order + n, [&](int a, int b) { return pc[a].bytes > pc[b].bytes; });
+    size_t queued[2] = {0, 0};
+    for (int k = 0; k < n; ++k) {
+        const int i = order[k];
+        const int e = (c->sdma_engine[1] && queued[1] < queued[0]) ? 1 : 0;
+        queued[e] += pc[i].bytes;
         if (hsa_amd_memory_async_copy_on_engine(pc[i].dst, c->sdma_cpu, pc[i].src, c->sdma_gpu, pc[i].bytes, 0, nullptr,
-                                                c->dl_sig, (hsa_amd_sdma_engine_id_t)c->sdma_engine,
+                                                c->dl_sig, (hsa_amd_sdma_engine_id_t)c->sdma_engine[e],
                                                 true) != HSA_STATUS_SUCCESS) {
-            hsa_signal_subtract_screlease(c->dl_sig, n - i);       // the pieces never issued
+            hsa_signal_subtract_screlease(c->dl_sig, n - k);       // the pieces never issued
             (void)kdtn_epoch_download_wait(c);
             c->sdma_ok = false;                                    // HIP copies from now on
             return false;
