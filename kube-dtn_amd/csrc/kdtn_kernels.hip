@@ -1215,9 +1215,16 @@ KD_INLINE void add_gather(const RecCols& c, const TopoCtx& tc, const DevTables& 
     if (qd) gather_props<V>(c, tb, g.v);
     if (!res) return;
     g.lns = tc.ns == 0 ? tb.special[SPECIAL_DEFAULT] : tc.ns;                     // :29-31
-    g.kb_ip = ldg(tb.kbits + (size_t)KB_CIDR_BAD * tb.kb_words, c.lip >> 5);
-    g.kb_mac = ldg(tb.kbits + (size_t)KB_MAC_BAD * tb.kb_words, c.lmac >> 5);
-    g.kb_pip = ldg(tb.kbits + (size_t)KB_CIDR_BAD * tb.kb_words, c.pip >> 5);    // peer end (same / cross node)
+    if constexpr ((V & VAR_SKIP_KB3) != 0) {             // profiling only, wrong results
+        g.kb_ip = c.lip & 0x100u;
+        g.kb_mac = c.lmac & 0x100u;
+        g.kb_pip = c.pip & 0x100u;
+    } else {
+        g.kb_ip = ldg(tb.kbits + (size_t)KB_CIDR_BAD * tb.kb_words, c.lip >> 5);
+        if constexpr ((V & VAR_SKIP_KB1) != 0) g.kb_mac = c.lmac & 0x100u;   // profiling only, wrong results
+        else g.kb_mac = ldg(tb.kbits + (size_t)KB_MAC_BAD * tb.kb_words, c.lmac >> 5);
+        g.kb_pip = ldg(tb.kbits + (size_t)KB_CIDR_BAD * tb.kb_words, c.pip >> 5);    // peer end (same / cross node)
+    }
     if constexpr ((V & VAR_SKIP_POD) == 0) g.slot = pod_slot<(V & VAR_NT_POD) != 0>(tb, c.pp);
 }
 

@@ -648,3 +648,37 @@ def test_output_stages_without_sync_use_this_runs_counts(engine):
     engine.upload(small)
     engine.run()
     assert_same(engine.download(), want, "download without sync")
+
+
+def test_go_stdlib_vectors_on_the_gpu(engine):
+    """Go's published known answers (tests/test_oracle_go_stdlib.py: time parseDurationTests,
+    net parseCIDRTests / parseMACTests) through the GPU parsers: a duration as a link's latency
+    (MakeQdiscs, E_LATENCY iff Go rejects it or it is negative), a CIDR as local_ip (MakeVeth,
+    E_VETH_CIDR iff invalid and non-empty), a MAC as local_mac (E_VETH_MAC iff invalid); every
+    output also equals the oracle's."""
+    from test_oracle_go_stdlib import GO_CIDRS, GO_DURATION_ERRORS, GO_DURATIONS, GO_MACS
+    strs = [s for s, _ in GO_DURATIONS] + GO_DURATION_ERRORS
+    pd, prop, gap = _props_batch(strs, "latency")
+    got = engine.make_qdiscs(pd, prop, gap)
+    for i, s in enumerate(strs):
+        want = O.make_qdisc({"latency": s}, TICK)
+        assert got[i].tobytes() == want.tobytes(), (s, got[i], want)
+        ok = i < len(GO_DURATIONS) and GO_DURATIONS[i][1] >= 0
+        assert (got[i]["err"] == 0) == ok and (ok or got[i]["err"] == abi.E_LATENCY), (s, got[i]["err"])
+    links, want_err = [], []
+    uid = 1
+    for ip, valid in GO_CIDRS:                          # MakeVeth parses a non-empty IP only (veth.go:21)
+        links.append(Link("eth0", ip, "00:00:5e:00:53:01", "eth1", "", "", "b", uid))
+        want_err.append(0 if valid or ip == "" else abi.E_VETH_CIDR)
+        uid += 1
+    for mac, valid in GO_MACS:
+        links.append(Link("eth0", "10.0.0.1/24", mac, "eth1", "", "", "b", uid))
+        want_err.append(0 if valid else abi.E_VETH_MAC)
+        uid += 1
+    topos = [Topology("a", "default", links, [], "10.0.0.1", "/ns/a"),
+             Topology("b", "default", [], [], "10.0.0.2", "/ns/b")]
+    inp = pack(topos)
+    out = engine.reconcile(inp)
+    assert_same(out, O.reconcile(inp, tick=TICK), "Go stdlib vectors")
+    errs = out.add_res["err"][np.argsort(out.add_idx)]
+    assert errs.tolist() == want_err
