@@ -1424,6 +1424,7 @@ struct RecShared {
             uint32_t tiles[BLOCK / 64][KDTN_PROFILING ? GL_UNITS * TILE_RECS : 1];
             uint2 bstage[BLOCK / 64][32 * 9];
         };
+        uint2 stage64[BLOCK / 64][64 * 9];   // (VAR_Q16) bulk emission: a wave's 64 qdisc structs
     };
 };
 
@@ -2034,7 +2035,6 @@ template <int V>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(var_waves(V))))
 k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWork wk) {
     __shared__ RecShared s;
-    __shared__ uint2 stage64[BLOCK / 64][(V & VAR_Q16) ? 64 * 9 : 1];   // (VAR_Q16 only)
     const int tid = threadIdx.x;
     unsigned long long t_entry = 0;
     if constexpr ((V & VAR_TRACE) != 0) t_entry = __builtin_amdgcn_s_memrealtime();
@@ -2394,7 +2394,7 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
                 next();
                 fetch(nx, nc);
             }
-            if constexpr ((V & VAR_Q16) != 0) wave_store_qdisc16<V>(out.add_qdisc, qa, e, q, stage64[tid >> 6]);
+            if constexpr ((V & VAR_Q16) != 0) wave_store_qdisc16<V>(out.add_qdisc, qa, e, q, s.stage64[tid >> 6]);
             else wave_store_qdisc<V>(out.add_qdisc, qa, e, q, stage);
             cs = nx;
             cc = nc;
