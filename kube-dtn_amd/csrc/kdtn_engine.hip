@@ -1551,8 +1551,14 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
             }
             k_place_scan<<<1, PLACE_SCAN_BLOCK, 0, s>>>(w.wcount, c->nwg, wbase, o, c->T);
             timer_mark(c, "place_scan", 1);
-            k_place<<<(c->nwg + BLOCK / 64 - 1) / (BLOCK / 64), BLOCK, 0, s>>>(T, w.wcount, wbase, w.first_partial_inv, o,
-                                                                              w.m_cap, w.n_cap, c->nwg);
+            if (c->nwg >= 4u * c->n_cus) {               // enough chunks for a wave each
+                k_place<true><<<(c->nwg + BLOCK / 64 - 1) / (BLOCK / 64), BLOCK, 0, s>>>(
+                    T, w.wcount, wbase, w.first_partial_inv, o, w.m_cap, w.n_cap, c->nwg, 1u);
+            } else {                                      // workgroups per chunk to fill the chip
+                const uint32_t parts = std::min<uint32_t>(16u, std::max<uint32_t>(1u, 4u * c->n_cus / std::max<uint32_t>(c->nwg, 1u)));
+                k_place<false><<<c->nwg * parts, BLOCK, 0, s>>>(T, w.wcount, wbase, w.first_partial_inv, o, w.m_cap,
+                                                                w.n_cap, c->nwg, parts);
+            }
             timer_mark(c, "place", 1);
         }
     } else {

@@ -251,8 +251,9 @@ struct RecWork {
 // VAR_DIFF placement (after k_reconcile): exclusive bases per workgroup and list totals, then
 // the deferred chunks' entries moved from the upper halves of the output arrays.
 __global__ void k_place_scan(const uint32_t* wcount, uint32_t nwg, uint32_t* wbase, RecOut out, uint32_t T);
+template <bool WAVE>
 __global__ void k_place(DevTopos T, const uint32_t* wcount, const uint32_t* wbase, const uint32_t* first_partial_inv,
-                        RecOut out, uint32_t m_cap, uint32_t n_cap, uint32_t nwg);
+                        RecOut out, uint32_t m_cap, uint32_t n_cap, uint32_t nwg, uint32_t parts);
 constexpr int PLACE_SCAN_BLOCK = 1024, PLACE_PER = 8;    // k_place_scan: workgroups per thread per tile
 
 __global__ void k_special_clip(uint32_t* special, uint32_t k0);

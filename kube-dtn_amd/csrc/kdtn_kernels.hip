@@ -2156,18 +2156,34 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
             diff_window<false>(s, 0, nt, O, N, s.hash, s.flag, s.lt, s.tgt, wk.otarget, n0);
         }
     } else {
-        for (int tt = 0; tt < nt; ++tt) {
-            const uint32_t k = (s.ooff[tt + 1] - s.ooff[tt]) + (s.noff[tt + 1] - s.noff[tt]);
-            const uint32_t gofs = s.ooff[tt] + s.noff[tt];
-            if (k <= (uint32_t)CAP) {
-                diff_window<false>(s, tt, tt + 1, O, N, s.hash, s.flag, nullptr, nullptr, wk.otarget, 0);
-                // spill the window's masked flags to global scratch (slow-path emission reads them)
-                for (uint32_t r = tid; r < k; r += BLOCK) wk.fscratch[gofs + r] = s.flag[r];
-                __syncthreads();
-            } else {
+        // the chunk's records exceed one window: consecutive topologies are grouped into LDS
+        // windows of up to CAP records (a chunk of 64 fat-tree spines of ~100 records takes 4
+        // windows, not 64); a topology larger than CAP alone uses global scratch
+        auto recs = [&](int t) { return (s.ooff[t + 1] - s.ooff[t]) + (s.noff[t + 1] - s.noff[t]); };
+        int tt = 0;
+        while (tt < nt) {                                   // (workgroup-uniform)
+            uint32_t k = recs(tt);
+            if (k > (uint32_t)CAP) {
+                const uint32_t gofs = s.ooff[tt] + s.noff[tt];
                 diff_window<false>(s, tt, tt + 1, O, N, wk.hscratch + gofs, wk.fscratch + gofs, nullptr,
                             nullptr, wk.otarget, 0);
+                ++tt;
+                continue;
             }
+            int te = tt + 1;
+            while (te < nt && k + recs(te) <= (uint32_t)CAP) k += recs(te++);
+            diff_window<false>(s, tt, te, O, N, s.hash, s.flag, s.lt, nullptr, wk.otarget, 0);
+            // spill the window's masked flags to each topology's global scratch slots (the
+            // slow-path emission reads them: old records, then new records, per topology)
+            const uint32_t wo0 = s.ooff[tt], wn0 = s.noff[tt], no_w = s.ooff[te] - wo0;
+            for (uint32_t r = tid; r < k; r += BLOCK) {
+                const int t2 = s.lt[r];
+                const uint32_t pos = r < no_w ? wo0 + r - s.ooff[t2]
+                                              : (s.ooff[t2 + 1] - s.ooff[t2]) + (wn0 + (r - no_w) - s.noff[t2]);
+                wk.fscratch[s.ooff[t2] + s.noff[t2] + pos] = s.flag[r];
+            }
+            __syncthreads();
+            tt = te;
         }
     }
 
@@ -2579,45 +2595,69 @@ __global__ void __launch_bounds__(PLACE_SCAN_BLOCK) k_place_scan(const uint32_t*
     }
 }
 
-// One wave per deferred chunk: per-topology offsets += the chunk's bases, entries moved
-// from [cap + record offset, +count) to [base, +count) of the same arrays (never overlapping).
+// Deferred chunks: per-topology offsets += the chunk's bases, entries moved from [cap + record
+// offset, +count) to [base, +count) of the same arrays (never overlapping), PLACE_U elements per
+// thread loaded before any is stored (element by element, each store waited for its load). One
+// wave per chunk when the chunks fill the chip (config 3: 15,625 chunks of ~32 entries), else
+// `parts` workgroups per chunk (config 1: 157 chunks, a chunk of fat-tree spines moves 3,200
+// 72-B records).
+constexpr int PLACE_U = 4;
+template <typename T>
+KD_INLINE void place_move(T* dst, const T* src, uint32_t n, uint32_t me, uint32_t g) {
+    for (uint32_t b = 0; b < n; b += g * PLACE_U) {
+        T v[PLACE_U];
+#pragma unroll
+        for (int u = 0; u < PLACE_U; ++u) {
+            const uint32_t k = b + u * g + me;
+            if (k < n) v[u] = src[k];
+        }
+#pragma unroll
+        for (int u = 0; u < PLACE_U; ++u) {
+            const uint32_t k = b + u * g + me;
+            if (k < n) __builtin_nontemporal_store(v[u], dst + k);
+        }
+    }
+}
+template <bool WAVE>
 __global__ void __launch_bounds__(BLOCK) k_place(DevTopos T, const uint32_t* wcount, const uint32_t* wbase,
                                                  const uint32_t* first_partial_inv, RecOut out, uint32_t m_cap,
-                                                 uint32_t n_cap, uint32_t nwg) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wg = blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
+                                                 uint32_t n_cap, uint32_t nwg, uint32_t parts) {
+    const uint32_t G = WAVE ? 64u : BLOCK * parts;                // threads per chunk
+    const uint32_t wg = WAVE ? blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6) : blockIdx.x / parts;
+    const uint32_t me = WAVE ? threadIdx.x & 63u : (blockIdx.x % parts) * BLOCK + threadIdx.x;
     if (wg >= nwg || wg <= ~*first_partial_inv) return;          // prefix chunks wrote final positions
     const uint32_t t0 = wg * TPW, nt = min((uint32_t)TPW, T.n - t0);
     const uint32_t cd = wcount[(size_t)wg * 3], cu = wcount[(size_t)wg * 3 + 1], ca = wcount[(size_t)wg * 3 + 2];
     const uint32_t bd = wbase[(size_t)wg * 3], bu = wbase[(size_t)wg * 3 + 1], ba = wbase[(size_t)wg * 3 + 2];
-    if (lane < nt) {
-        out.del_off[t0 + lane] += bd;
-        out.upd_off[t0 + lane] += bu;
-        out.add_off[t0 + lane] += ba;
+    if (me < nt) {
+        out.del_off[t0 + me] += bd;
+        out.upd_off[t0 + me] += bu;
+        out.add_off[t0 + me] += ba;
     }
     const uint32_t sd = m_cap + T.real_off[t0], sa = n_cap + T.des_off[t0];
     const bool res = out.stages & KDTN_STAGE_RESOLVE, qd = out.stages & KDTN_STAGE_QDISC;
-    constexpr int V = DEFAULT_VARIANT;
-    for (uint32_t k = lane; k < cd; k += 64) {
-        store_idx<V>(out.del_idx + bd + k, out.del_idx[sd + k]);
-        if (res) store_res<V>(out.del_res + bd + k, out.del_res[sd + k]);
-    }
-    for (uint32_t k = lane; k < cu; k += 64) {
-        store_idx<V>(out.upd_idx + bu + k, out.upd_idx[sd + k]);
-        if (res) store_res<V>(out.upd_res + bu + k, out.upd_res[sd + k]);
-    }
-    for (uint32_t k = lane; k < ca; k += 64) {
-        store_idx<V>(out.add_idx + ba + k, out.add_idx[sa + k]);
-        if (res) store_res<V>(out.add_res + ba + k, out.add_res[sa + k]);
-        if (res && qd) out.add_qerr[ba + k] = out.add_qerr[sa + k];
+    typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+    typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
+    place_move(out.del_idx + bd, out.del_idx + sd, cd, me, G);
+    place_move(out.upd_idx + bu, out.upd_idx + sd, cu, me, G);
+    place_move(out.add_idx + ba, out.add_idx + sa, ca, me, G);
+    if (res) {
+        place_move(reinterpret_cast<u32x4v*>(out.del_res + bd), reinterpret_cast<const u32x4v*>(out.del_res + sd), cd, me, G);
+        place_move(reinterpret_cast<u32x4v*>(out.upd_res + bu), reinterpret_cast<const u32x4v*>(out.upd_res + sd), cu, me, G);
+        place_move(reinterpret_cast<u32x4v*>(out.add_res + ba), reinterpret_cast<const u32x4v*>(out.add_res + sa), ca, me, G);
+        if (qd) place_move(out.add_qerr + ba, out.add_qerr + sa, ca, me, G);
     }
     if (qd) {
-        for (uint32_t k = lane; k < cu * 9; k += 64)
-            store_q8<V>(out.upd_qdisc + (size_t)bu * 9 + k, out.upd_qdisc[(size_t)sd * 9 + k]);
-        for (uint32_t k = lane; k < ca * 9; k += 64)
-            store_q8<V>(out.add_qdisc + (size_t)ba * 9 + k, out.add_qdisc[(size_t)sa * 9 + k]);
+        place_move(reinterpret_cast<u32x2v*>(out.upd_qdisc + (size_t)bu * 9),
+                      reinterpret_cast<const u32x2v*>(out.upd_qdisc + (size_t)sd * 9), cu * 9, me, G);
+        place_move(reinterpret_cast<u32x2v*>(out.add_qdisc + (size_t)ba * 9),
+                      reinterpret_cast<const u32x2v*>(out.add_qdisc + (size_t)sa * 9), ca * 9, me, G);
     }
 }
+template __global__ void k_place<true>(DevTopos, const uint32_t*, const uint32_t*, const uint32_t*, RecOut, uint32_t,
+                                       uint32_t, uint32_t, uint32_t);
+template __global__ void k_place<false>(DevTopos, const uint32_t*, const uint32_t*, const uint32_t*, RecOut, uint32_t,
+                                        uint32_t, uint32_t, uint32_t);
 
 // Standalone MakeQdiscs over a batch of property sets (kdtn_make_qdiscs).
 __global__ void __launch_bounds__(BLOCK) k_qdisc_batch(DevLinks props, DevTables tb, uint2* out) {
