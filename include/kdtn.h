@@ -311,8 +311,13 @@ int kdtn_reconcile_epoch(kdtn_ctx* ctx, const kdtn_epoch_in* in, kdtn_batches* o
 int kdtn_epoch_upload(kdtn_ctx* ctx, const kdtn_epoch_in* in);
 int kdtn_epoch_run(kdtn_ctx* ctx, uint32_t stages);          /* async on the ctx stream   */
 int kdtn_epoch_sync(kdtn_ctx* ctx, kdtn_counts* counts);     /* waits; counts may be NULL */
-int kdtn_epoch_download(kdtn_ctx* ctx, kdtn_batches* out);   /* after sync                */
-/* Asynchronous download (after sync): the copies into `out` (page-locked, kdtn_host_alloc) run
+int kdtn_epoch_download(kdtn_ctx* ctx, kdtn_batches* out);   /* after run (+ sync)         */
+/* The download and every output stage below size their work from the run's list totals: after
+ * kdtn_epoch_sync they are at hand; without it the call waits for the run and reads them (an
+ * output stage never uses an earlier epoch's counts). Destinations that are page-locked —
+ * kdtn_host_alloc, or host memory registered with hipHostRegister / hsa_amd_memory_lock — are
+ * written by an SDMA engine (a registered range at its agent address), others by hipMemcpy.
+ * Asynchronous download (after sync): the copies into `out` (page-locked, kdtn_host_alloc) run
  * on a stream of their own while the caller goes on (commit, the next kdtn_epoch_upload_delta,
  * whose host-to-device copies share the full-duplex link); the next kdtn_epoch_run waits for
  * them on the GPU before overwriting the outputs. Counts in `out` are set at return; the

@@ -819,13 +819,11 @@ int prepare_epoch(kdtn_ctx* c, const kdtn_vni_table& vn, uint32_t slice, uint32_
     return prepare_work(c, slice, M, N);
 }
 
-// The last run's list totals in h_misc[1..3] (and the look-back error in [4]). kdtn_epoch_sync
-// reads them from the coherent host words k_reconcile writes; an output stage called without
-// it reads them here, after the run's stream, so no stage sizes its passes from the counts of
-// an earlier epoch.
-int counts_fresh(kdtn_ctx* c) {
-    if (c->synced) return KDTN_OK;
-    HIP_TRY(hipStreamSynchronize(c->stream));
+// The last run's list totals in h_misc[1..3] (and the look-back error in [4]), from the coherent
+// host words k_reconcile writes: read_totals once the run has completed (kdtn_epoch_sync);
+// counts_fresh for an output stage called without kdtn_epoch_sync waits for the run first, so
+// no stage sizes its passes from the counts of an earlier epoch.
+int read_totals(kdtn_ctx* c) {              // (the run has completed)
     for (int i = 0; i < 4; ++i) c->h_misc[1 + i] = __atomic_load_n(c->h_tot + i, __ATOMIC_ACQUIRE);
     if (c->h_misc[4] != 0) {
         std::snprintf(g_last_error, sizeof(g_last_error), "k_reconcile look-back timed out (0x%x)", c->h_misc[4]);
@@ -833,6 +831,11 @@ int counts_fresh(kdtn_ctx* c) {
     }
     c->synced = true;
     return KDTN_OK;
+}
+int counts_fresh(kdtn_ctx* c) {
+    if (c->synced) return KDTN_OK;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return read_totals(c);
 }
 
 // Which batch entries the daemons reach (k_reach; include/kdtn.h): c->f_send (add) and
@@ -1596,8 +1599,7 @@ int kdtn_epoch_sync(kdtn_ctx* c, kdtn_counts* counts) {
         }
     }
     HIP_TRY(hipStreamSynchronize(c->stream));
-    c->synced = false;
-    TRY(counts_fresh(c));
+    TRY(read_totals(c));
     if (counts) {
         counts->n_del = c->h_misc[1];
         counts->n_upd = c->h_misc[2];
