@@ -156,7 +156,8 @@ constexpr int VAR_NT_LOAD = 1, VAR_NT_STORE = 2, VAR_NO_QSTORE = 4, VAR_NT_POD =
               VAR_Q16 = 32768, VAR_GLDS = 65536,
               VAR_PMAC_COLS = 131072,
               VAR_AB = 262144,
-              VAR_SKIP_KB1 = 524288, VAR_SKIP_KB3 = 1048576;   // (profiling, wrong results) skip the local-MAC /
+              VAR_SKIP_KB1 = 524288, VAR_SKIP_KB3 = 1048576,
+              VAR_HB = 2097152;   // CalcDiff window: both sides' key hashes first, one load round per old record   // (profiling, wrong results) skip the local-MAC /
                                                                // all three key-string bitset gathers          // CalcDiff window: old + positional new records in one load phase   // (internal to VAR_GLDS) the entry's peer_mac id is in RecCols
 // VAR_GLDS: the tile column units an add entry reads, in LDS order: local_ip, local_mac (key 1, 2),
 // peer_ip, peer_mac, peer_pod (key 4..6), the 12 properties, gap, uid (2 units): every column of
@@ -171,17 +172,17 @@ constexpr int var_waves(int v) {
 constexpr int TRACE_WORDS = 8;   // entry, topologies loaded, counts done, bases known, end, hw ids,
                                   // CalcDiff window phase A done, phase B done (fast path)
 constexpr int DEFAULT_VARIANT = VAR_NT_LOAD | VAR_NT_STORE | VAR_MASK_EMPTY | VAR_PREFETCH;   // 16899
-// the comparison-heavy build kdtn_epoch_run launches when both link lists are non-empty
-// (VAR_AB measured and not kept: 0.845 -> 0.885 ms on 5 config-3 churn epochs,
-// profiles/r06d_window_ab_cfg3.json)
-constexpr int DIFF_VARIANT = DEFAULT_VARIANT | VAR_DIFF;   // 18947
+// the comparison-heavy build kdtn_epoch_run launches when both link lists are non-empty; its
+// CalcDiff windows hash both sides' keys first (VAR_HB: 0.845 -> 0.671 ms on 5 config-3 churn
+// epochs, profiles/r06q_window_hb_cfg3.json; VAR_AB measured and not kept, r06d)
+constexpr int DIFF_VARIANT = DEFAULT_VARIANT | VAR_DIFF | VAR_HB;   // 2116099
 // instantiations of the profiling build (DEFAULT_VARIANT is always instantiated): e.g. 547 / 579
 // / 611 skip the pod-slot / percentage / both gathers, 519 skips the qdisc stores, 531 the
 // trace build of the default
 #define KDTN_PROFILING_VARIANTS(X) X(0) X(1) X(2) X(3) X(4) X(5) X(9) X(11) X(17) X(33) X(65) X(97) \
     X(101) X(113) X(129) X(257) X(513) X(521) X(523) X(529) X(531) X(545) X(547) X(579) X(611) X(519) \
     X(641) X(643) X(771) X(1025) X(1537) X(2579) X(4611) X(515) X(16915) X(16963) X(16931) X(16995) X(16903) X(49667) \
-    X(66051) X(65539) X(281091) X(264723) X(541187) X(1065475)
+    X(66051) X(65539) X(281091) X(264723) X(541187) X(1065475) X(18947) X(2099731)
 
 struct DevTopos {
     const uint32_t* ns;

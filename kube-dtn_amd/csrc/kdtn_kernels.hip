@@ -1699,6 +1699,113 @@ __device__ void diff_window_ab(RecShared& s, int tb, int te, const DevLinks& O, 
     diff_window_tail(s, tb, te, N, hsh, flg, lt, no, nn, tot, wn0);
 }
 
+// (VAR_HB) the LDS window with both sides' key hashes in the first phase (each record's 9 key
+// words, two records per thread in flight), so the old side knows its first candidate before it
+// loads anything: one round trip for the old record and that candidate (keys and properties),
+// where the positional form loads the positional record first and an off-position first match
+// (every record after a deleted link of its Topology) takes a second round trip. A hash that
+// matches a different key (a collision) or a positional record other than the first match with
+// the same hash (duplicate keys in spec) load more, rarely.
+template <bool TR>
+__device__ void diff_window_hb(RecShared& s, int tb, int te, const DevLinks& O, const DevLinks& N, uint32_t* hsh,
+                               uint8_t* flg, uint8_t* lt, uint16_t* tgt16, uint32_t* otarget,
+                               unsigned long long* tr = nullptr) {
+    const uint32_t wo0 = s.ooff[tb], wo1 = s.ooff[te];
+    const uint32_t wn0 = s.noff[tb], wn1 = s.noff[te];
+    const uint32_t no = wo1 - wo0, nn = wn1 - wn0, tot = no + nn;
+    const int tid = threadIdx.x;
+
+    // A. segment and key hash of every record (old and new), two records per thread per step
+    for (uint32_t r0 = tid; r0 < tot; r0 += 2 * BLOCK) {
+        uint32_t k0[KEYW], k1[KEYW];
+        bool c0 = false, c1 = false;
+        const uint32_t r1 = r0 + BLOCK;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const uint32_t r = q ? r1 : r0;
+            if (r >= tot) continue;
+            const bool old = r < no;
+            const uint32_t idx = old ? wo0 + r : wn0 + (r - no);
+            const int tt = find_seg(old ? s.ooff : s.noff, tb, te, idx);
+            lt[r] = (uint8_t)tt;
+            if (!old) flg[r] = 0;
+            if (need_cmp(s, tt)) {
+                if (q) { load_key(old ? O : N, idx, k1); c1 = true; }
+                else { load_key(old ? O : N, idx, k0); c0 = true; }
+            }
+        }
+        if (c0) hsh[r0] = key_hash_w(k0);
+        if (c1) hsh[r1] = key_hash_w(k1);
+    }
+    __syncthreads();
+    if constexpr (TR) {
+        if (tid == 0) tr[6] = __builtin_amdgcn_s_memrealtime();
+    }
+
+    // B. old side: the first key-equal new record (CalcDiff :289-303) and the positional
+    //    DeepEqual (:77), from the first hash candidate
+    for (uint32_t r = tid; r < no; r += BLOCK) {
+        const int tt = lt[r];
+        uint8_t f = RF_DEL;
+        if (need_cmp(s, tt)) {
+            const uint32_t i = wo0 + r;
+            const uint32_t os_ = s.ooff[tt], ns_ = s.noff[tt], ne_ = s.noff[tt + 1];
+            const uint32_t jp = ns_ + (i - os_);
+            const uint32_t h = hsh[r];
+            uint32_t cand = 0xFFFFFFFFu;
+            for (uint32_t j = ns_; j < ne_; ++j)
+                if (hsh[no + (j - wn0)] == h) { cand = j; break; }
+            const bool p_hash = jp < ne_ && hsh[no + (jp - wn0)] == h;
+            uint32_t first = 0xFFFFFFFFu;
+            bool same_props = false, pos_eq = false;
+            if (cand != 0xFFFFFFFFu) {
+                uint32_t ki[KEYW], pi[PROPW], kx[KEYW], px[PROPW];
+                load_key(O, i, ki);
+                load_props(O, i, pi);
+                load_key(N, cand, kx);
+                load_props(N, cand, px);
+                uint32_t j = cand;
+                for (;;) {                                     // (a second pass only on a collision)
+                    if (words_eq<KEYW>(ki, kx)) {
+                        first = j;
+                        same_props = words_eq<PROPW>(pi, px);
+                        break;
+                    }
+                    while (++j < ne_ && hsh[no + (j - wn0)] != h) {
+                    }
+                    if (j >= ne_) break;
+                    load_key(N, j, kx);
+                    load_props(N, j, px);
+                }
+                if (first == jp) {
+                    pos_eq = same_props;
+                } else if (p_hash) {                           // the positional record shares the hash
+                    load_key(N, jp, kx);
+                    load_props(N, jp, px);
+                    pos_eq = words_eq<KEYW>(ki, kx) && words_eq<PROPW>(pi, px);
+                }
+            }
+            if (first != 0xFFFFFFFFu) {
+                flg[no + (first - wn0)] = RF_MATCHED;
+                if (!same_props) {
+                    f = RF_UPD;
+                    if (tgt16) tgt16[r] = (uint16_t)(first - wn0);
+                    else otarget[i] = first;
+                } else {
+                    f = 0;
+                }
+            }
+            if (s.ooff[tt + 1] - os_ == ne_ - ns_ && !pos_eq) s.dirty[tt] = 1;
+        }
+        flg[r] = f;
+    }
+    __syncthreads();
+    if constexpr (TR) {
+        if (tid == 0) tr[7] = __builtin_amdgcn_s_memrealtime();
+    }
+    diff_window_tail(s, tb, te, N, hsh, flg, lt, no, nn, tot, wn0);
+}
+
 // Decoupled look-back over the workgroups' list counts (3 lists), one wave, 64
 // predecessors per round trip. Granules are 8-byte {state:32 | count:32} words written and
 // read at agent scope (sc1); the data is its own flag, so no fences are needed
@@ -2145,7 +2252,13 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
         }
         __syncthreads();
     } else if (fast) {
-        if constexpr ((V & VAR_AB) != 0) {
+        if constexpr ((V & VAR_HB) != 0) {
+            if constexpr ((V & VAR_TRACE) != 0)
+                diff_window_hb<true>(s, 0, nt, O, N, s.hash, s.flag, s.lt, s.tgt, wk.otarget,
+                                     wk.trace + (size_t)wg * TRACE_WORDS);
+            else
+                diff_window_hb<false>(s, 0, nt, O, N, s.hash, s.flag, s.lt, s.tgt, wk.otarget);
+        } else if constexpr ((V & VAR_AB) != 0) {
             if constexpr ((V & VAR_TRACE) != 0)
                 diff_window_ab<true>(s, 0, nt, O, N, s.hash, s.flag, s.lt, s.tgt, wk.trace + (size_t)wg * TRACE_WORDS);
             else
@@ -2172,7 +2285,10 @@ k_reconcile(DevTopos T, DevLinks O, DevLinks N, DevTables tb, RecOut out, RecWor
             }
             int te = tt + 1;
             while (te < nt && k + recs(te) <= (uint32_t)CAP) k += recs(te++);
-            diff_window<false>(s, tt, te, O, N, s.hash, s.flag, s.lt, nullptr, wk.otarget, 0);
+            if constexpr ((V & VAR_HB) != 0)
+                diff_window_hb<false>(s, tt, te, O, N, s.hash, s.flag, s.lt, nullptr, wk.otarget);
+            else
+                diff_window<false>(s, tt, te, O, N, s.hash, s.flag, s.lt, nullptr, wk.otarget, 0);
             // spill the window's masked flags to each topology's global scratch slots (the
             // slow-path emission reads them: old records, then new records, per topology)
             const uint32_t wo0 = s.ooff[tt], wn0 = s.noff[tt], no_w = s.ooff[te] - wo0;

@@ -75,4 +75,4 @@ def test_product_library_reads_no_environment():
                  b"KDTN_PD_ONLY"):
         assert knob not in data, knob
     names = set(re.findall(rb"_ZN4kdtn11k_reconcileILi(\d+)E", data))
-    assert names == {b"16899", b"18947"}, names   # default and comparison-heavy builds
+    assert names == {b"16899", b"2116099"}, names   # default and comparison-heavy builds
