@@ -114,7 +114,8 @@ int or_parse_duration(const char* s, uint32_t n, uint32_t* us) {
 /* ======================================================================================
  * strconv.ParseFloat(s, 32) (Go 1.18 strconv/atof.go): grammar restated (special,
  * readFloat, underscoreOK); the value is the correctly rounded float32 of the number
- * Go's scanner reads, computed here by glibc strtof on a canonical spelling.
+ * Go's scanner reads: decimal by glibc strtof on a canonical spelling, hexadecimal by
+ * hex_to_f32 (integer rounding).
  * ==================================================================================== */
 static int lower_c(int c) { return (c >= 'A' && c <= 'Z') ? c + 32 : c; }
 
@@ -146,6 +147,41 @@ static int underscore_ok(const char* s, size_t n) {
         saw = '!';
     }
     return saw != '_';
+}
+
+/* A hexadecimal mantissa (its first 16 digits in mant; trunc: a nonzero digit after them)
+ * × 2^e2, correctly rounded to float32: ties to even, subnormals (lsb 2^-149), ±Inf past the
+ * largest finite value (atofHex's rounding, Go strconv/atof.go). Restated in integers because
+ * glibc's strtof rounds some hexadecimal subnormals down (0x0.1234569p-125 → 0x123456 × 2^-149
+ * where Go's atof32 table, and the exact value, give 0x123457). */
+static float hex_to_f32(uint64_t mant, int trunc, long e2, int neg) {
+    if (mant == 0) return neg ? -0.0f : 0.0f;
+    int lz = __builtin_clzll(mant);
+    uint64_t m = mant << lz;                                  /* top bit at 63 */
+    long E = e2 + 63 - lz;                                    /* value in [2^E, 2^(E+1)) */
+    double v;
+    if (E > 127) {
+        v = INFINITY;
+    } else {
+        long keep = E + 150 < 24 ? E + 150 : 24;              /* significand bits down to 2^-149 */
+        uint64_t kept;
+        int half, low;
+        if (keep <= 0) {                                      /* below 2^-149 */
+            kept = 0;
+            half = keep == 0;                                 /* [2^-150, 2^-149): the half bit is the top one */
+            low = keep == 0 ? ((m << 1) != 0 || trunc) : 1;
+            keep = 0;
+        } else {
+            kept = m >> (64 - keep);
+            uint64_t rest = keep < 64 ? m << keep : 0;
+            half = (int)(rest >> 63);
+            low = (rest << 1) != 0 || trunc;
+        }
+        if (half && (low || (kept & 1))) kept++;
+        v = ldexp((double)kept, (int)(E - keep + 1));         /* exact; 2^128 → Inf below */
+    }
+    float f = (float)v;
+    return neg ? -f : f;
 }
 
 int or_parse_float32(const char* s, uint32_t n, float* out) {
@@ -229,17 +265,32 @@ int or_parse_float32(const char* s, uint32_t n, float* out) {
     if (underscores && !underscore_ok(s, i)) { free(digs); return 1; }
     if (i != n) { free(digs); return 1; }                     /* ParseFloat: whole string */
     if (nds == 0) { free(digs); *out = neg ? -0.0f : 0.0f; return 0; }
-    /* canonical spelling: [-]0.DIGITSe<dp>  |  [-]0x0.HEXp<dp> */
+    if (hex) {
+        uint64_t mant = 0;
+        int trunc = 0;
+        size_t nm = nds < 16 ? nds : 16;
+        for (size_t q = 0; q < nds; q++) {
+            int c = lower_c((unsigned char)digs[q]);
+            int dv = c <= '9' ? c - '0' : c - 'a' + 10;
+            if (q < nm) mant = mant * 16 + (uint64_t)dv;
+            else if (dv) trunc = 1;
+        }
+        free(digs);
+        float v = hex_to_f32(mant, trunc, dp - 4L * (long)nm, neg);
+        *out = v;
+        return isinf(v) ? 1 : 0;                              /* ErrRange */
+    }
+    /* canonical spelling: [-]0.DIGITSe<dp> (decimal only; glibc strtof rounds it correctly,
+     * tests/test_oracle_golden.py::test_float32_parse_exact_rounding) */
     char* canon = (char*)malloc(nds + 48);
     if (!canon) { free(digs); return 1; }
     size_t w = 0;
     if (neg) canon[w++] = '-';
     canon[w++] = '0';
-    if (hex) canon[w++] = 'x';
     canon[w++] = '.';
     memcpy(canon + w, digs, nds);
     w += nds;
-    w += (size_t)sprintf(canon + w, "%c%ld", hex ? 'p' : 'e', dp);
+    w += (size_t)sprintf(canon + w, "e%ld", dp);
     canon[w] = 0;
     float v = strtof(canon, NULL);
     free(canon);

@@ -2,10 +2,12 @@
 against the known-answer tables Go publishes with those packages.
 
 The reference calls time.ParseDuration (common/qdisc.go:146-157, via ParseDuration),
-net.ParseCIDR and net.ParseMAC (common/veth.go:21-36, MakeVeth) from the Go standard library
-(go.mod: go 1.19). Go is absent here and on the GPU box, so the oracle (oracle/kdtn_oracle.c)
+strconv.ParseFloat(s, 32) (:128-143, ParseFloatPercentage), strconv.ParseUint(s, 10, 64)
+(:162-199, ParseRate), net.ParseCIDR and net.ParseMAC (common/veth.go:21-36, MakeVeth) from the
+Go standard library (go.mod: go 1.19). Go is absent here and on the GPU box, so the oracle (oracle/kdtn_oracle.c)
 restates them; these vectors are the expected values of Go's own package tests — time's
-parseDurationTests (time_test.go), net's parseCIDRTests (ip_test.go) and parseMACTests
+parseDurationTests (time_test.go), strconv's atof32tests / atoftests (atof_test.go) and
+parseUint64Tests (atoi_test.go), net's parseCIDRTests (ip_test.go) and parseMACTests
 (mac_test.go) — written out here as data, passed through the reference's wrappers: ParseDuration
 rejects a negative duration and returns uint32(d.Microseconds()) (Microseconds truncates toward
 zero, uint32 keeps the low 32 bits); "" is 0 without a parse. They pin the restatements to Go's
@@ -13,8 +15,11 @@ published answers, not to a run of the reference (parity stays "unpinned" in tha
 DESIGN.md §6); the GPU parsers are compared with the oracle in tests/test_parity_gpu.py.
 """
 import os
+import random
 import sys
+from fractions import Fraction
 
+import numpy as np
 import pytest
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
@@ -114,3 +119,174 @@ GO_MACS = [
 @pytest.mark.parametrize("s,valid", GO_MACS)
 def test_parse_mac_go_vectors(s, valid):
     assert O.parse_mac(s) == valid, s
+
+
+# strconv/atof_test.go atof32tests: (input, Go's answer printed with 'g' -1, or None for ErrRange)
+GO_ATOF32 = [
+    ("0x1p-100", "7.888609e-31"), ("0x1p100", "1.2676506e+30"),
+    # exactly halfway between 1 and the next float32 (ties to even), just below, just above
+    ("1.000000059604644775390625", "1"), ("1.000000059604644775390624", "1"),
+    ("1.000000059604644775390626", "1.0000001"),
+    ("1.000000059604644775390625" + "0" * 10000 + "1", "1.0000001"),
+    # the largest float32, and the border above it
+    ("340282346638528859811704183484516925440", "3.4028235e+38"),
+    ("-340282346638528859811704183484516925440", "-3.4028235e+38"),
+    ("0x.ffffffp128", "3.4028235e+38"), ("-0x.ffffffp128", "-3.4028235e+38"),
+    ("3.4028236e38", None), ("-3.4028236e38", None), ("0x1.0p128", None), ("-0x1.0p128", None),
+    ("3.402823567e38", "3.4028235e+38"), ("-3.402823567e38", "-3.4028235e+38"),
+    ("0x.ffffff7fp128", "3.4028235e+38"), ("-0x.ffffff7fp128", "-3.4028235e+38"),
+    ("3.4028235678e38", None), ("-3.4028235678e38", None), ("0x.ffffff8p128", None), ("-0x.ffffff8p128", None),
+    # subnormals
+    ("1e-38", "1e-38"), ("1e-39", "1e-39"), ("1e-40", "1e-40"), ("1e-41", "1e-41"), ("1e-42", "1e-42"),
+    ("1e-43", "1e-43"), ("1e-44", "1e-44"), ("6e-45", "6e-45"), ("5e-45", "6e-45"), ("1e-45", "1e-45"),
+    ("2e-45", "1e-45"), ("3e-45", "3e-45"),
+    ("0x0.89aBcDp-125", "1.2643093e-38"), ("0x0.8000000p-125", "1.1754944e-38"),
+    ("0x0.1234560p-125", "1.671814e-39"), ("0x0.1234567p-125", "1.671814e-39"),
+    ("0x0.1234568p-125", "1.671814e-39"), ("0x0.1234569p-125", "1.671815e-39"),
+    ("0x0.1234570p-125", "1.671815e-39"), ("0x0.0000010p-125", "1e-45"), ("0x0.0000007p-125", "0"),
+]
+# atoftests (float64) whose answers are float32 values too, so bitSize 32 gives the same answer
+GO_ATOF_EXACT = [
+    ("1", 1.0), ("+1", 1.0), ("-1", -1.0), ("-0", -0.0), ("625e-3", 0.625),
+    ("0x1p0", 1.0), ("0x1p1", 2.0), ("0x1p-1", 0.5), ("0x1ep-1", 15.0), ("-0x1ep-1", -15.0),
+    ("-0x1_ep-1", -15.0), ("0x1fFe2.p0", 131042.0), ("0x1fFe2.P0", 131042.0), ("-0x2p3", -16.0),
+    ("0x0.fp4", 15.0), ("0x0.fp0", 0.9375),
+    ("0", 0.0), ("0e0", 0.0), ("-0e0", -0.0), ("+0e0", 0.0), ("0e-0", 0.0), ("-0e-0", -0.0), ("+0e-0", 0.0),
+    ("0e+0", 0.0), ("-0e+0", -0.0), ("+0e+0", 0.0), ("0e+01234567890123456789", 0.0),
+    ("0.00e-01234567890123456789", 0.0), ("-0e+01234567890123456789", -0.0),
+    ("-0.00e-01234567890123456789", -0.0), ("0x0p+01234567890123456789", 0.0), ("-0x0p+01234567890123456789", -0.0),
+    ("1e-4294967296", 0.0), ("1e-18446744073709551616", 0.0), ("0x1p-4294967296", 0.0),
+    ("0x1p-18446744073709551616", 0.0),
+    ("0x1p+2", 4.0), ("0x.1p+2", 0.25), ("0x1p-2", 0.25), ("0x.1p-2", 0.015625),
+    ("1_23.50_0_0e+1_2", 1.235e14), ("0x_1_2.3_4_5p+1_2", 74565.0),
+]
+GO_ATOF_RANGE = ["1e+4294967296", "1e+18446744073709551616", "0x1p+4294967296", "0x1p+18446744073709551616"]
+GO_ATOF_SYNTAX = [
+    "", "1x", "1.1.", "0x1e2", "1p2", "1e", "1e-", ".e-1", "1\x00.2", "0x", "0x.", "0x1", "0x.1", "0x1p",
+    "0x.1p", "0x1p+", "0x.1p+", "0x1p-", "0x.1p-",
+    "-_123.5e+12", "+_123.5e+12", "_123.5e+12", "1__23.5e+12", "123_.5e+12", "123._5e+12", "123.5_e+12",
+    "123.5__0e+12", "123.5e_+12", "123.5e+_12", "123.5e_-12", "123.5e-_12", "123.5e+1__2", "123.5e+12_",
+    "-_0x12.345p+12", "+_0x12.345p+12", "_0x12.345p+12", "0x__12.345p+12", "0x1__2.345p+12", "0x12_.345p+12",
+    "0x12._345p+12", "0x12.3__45p+12", "0x12.345_p+12", "0x12.345p_+12", "0x12.345p+_12", "0x12.345p_-12",
+    "0x12.345p-_12", "0x12.345p+1__2", "0x12.345p+12_",
+]
+GO_ATOF_SPECIAL = ["nan", "NaN", "NAN", "inf", "-Inf", "+INF", "-Infinity", "+INFINITY", "Infinity"]
+
+
+def _bits(x) -> int:
+    return int(np.float32(x).view(np.uint32))
+
+
+@pytest.mark.parametrize("s,want", GO_ATOF32, ids=[s[:40] for s, _ in GO_ATOF32])
+def test_parse_float32_go_atof32_vectors(s, want):
+    ok, v = O.parse_float32(s)
+    if want is None:
+        assert not ok, (s, v)                       # ErrRange
+    else:
+        assert ok and _bits(v) == _bits(float(want)), (s, v, want)
+
+
+@pytest.mark.parametrize("s,want", GO_ATOF_EXACT)
+def test_parse_float32_go_atof_vectors(s, want):
+    ok, v = O.parse_float32(s)
+    assert ok and _bits(v) == _bits(want), (s, v, want)
+
+
+@pytest.mark.parametrize("s", GO_ATOF_RANGE + GO_ATOF_SYNTAX)
+def test_parse_float32_go_errors(s):
+    assert not O.parse_float32(s)[0], s
+
+
+def go_percentage(s: str):
+    """ParseFloatPercentage (common/qdisc.go:128-143) on Go's ParseFloat(s, 32) answers above:
+    None for an error, else the float32 value."""
+    if s == "":
+        return 0.0
+    if s in GO_ATOF_SYNTAX or s in GO_ATOF_RANGE or s in GO_ATOF_SPECIAL:
+        return None                                 # syntax / range error, NaN, or ±Inf out of [0, 100]
+    table = dict(GO_ATOF32)
+    v = float(table[s]) if s in table else dict(GO_ATOF_EXACT)[s]
+    if v is None or v < 0 or v > 100:
+        return None
+    return v
+
+
+GO_PCT_INPUTS = [s for s, w in GO_ATOF32 if w is not None] + [s for s, _ in GO_ATOF_EXACT] + \
+    GO_ATOF_RANGE + GO_ATOF_SYNTAX + GO_ATOF_SPECIAL
+
+
+@pytest.mark.parametrize("s", GO_PCT_INPUTS, ids=[s[:40] for s in GO_PCT_INPUTS])
+def test_parse_percentage_go_vectors(s):
+    want = go_percentage(s)
+    ok, v = O.parse_pct(s)
+    if want is None:
+        assert not ok, (s, v)
+    else:
+        assert ok and (v == want == 0 or _bits(v) == _bits(want)), (s, v, want)
+
+
+def _f32_exact(a: Fraction, neg: bool):
+    """float32 nearest to -a or a (ties to even, subnormals), None past the largest finite."""
+    if a == 0:
+        return -0.0 if neg else 0.0
+    e = a.numerator.bit_length() - a.denominator.bit_length()
+    if Fraction(2) ** e > a:
+        e -= 1
+    unit = Fraction(2) ** max(e - 23, -149)
+    q = a / unit
+    n = q.numerator // q.denominator
+    r = q - n
+    if r > Fraction(1, 2) or (r == Fraction(1, 2) and n & 1):
+        n += 1
+    v = n * unit
+    if v >= Fraction(2) ** 128:
+        return None
+    return -float(v) if neg else float(v)
+
+
+def test_hex_float32_rounding_exact():
+    """Random hexadecimal mantissas across the subnormal, normal and overflow ranges, against
+    exact rational rounding (glibc's strtof rounds some hexadecimal subnormals down)."""
+    rng = random.Random(11)
+    checked = 0
+    for _ in range(4000):
+        nd = rng.randint(1, 20)
+        digs = "".join(rng.choice("0123456789abcdefABCDEF") for _ in range(nd))
+        cut = rng.randint(0, nd)
+        mant = digs[:cut] + ("." if rng.random() < 0.6 else "") + digs[cut:]
+        if mant.strip(".") == "":
+            continue
+        e = rng.randint(-240, 140)
+        sign = rng.choice(["", "-", "+"])
+        s = f"{sign}0x{mant}p{e}"
+        ip, _, fp = mant.partition(".")
+        fr = Fraction(int(ip or "0", 16) * 16 ** len(fp) + int(fp or "0", 16), 16 ** len(fp)) * Fraction(2) ** e
+        want = _f32_exact(fr, sign == "-")
+        ok, v = O.parse_float32(s)
+        if want is None:
+            assert not ok, (s, v)
+        else:
+            assert ok and _bits(v) == _bits(want), (s, v, want)
+        checked += 1
+    assert checked > 3500
+
+
+# strconv/atoi_test.go parseUint64Tests (base 10): (input, value or None for an error), through
+# ParseRate (common/qdisc.go:162-199), whose unit stripping leaves these strings unchanged:
+# "" is 0 without a parse (:164-166), the rest go to ParseUint(rate, 10, 64) × 1.
+GO_PARSE_UINT64 = [
+    ("", 0), ("0", 0), ("1", 1), ("12345", 12345), ("012345", 12345), ("12345x", None),
+    ("98765432100", 98765432100), ("18446744073709551615", (1 << 64) - 1),
+    ("18446744073709551616", None), ("18446744073709551620", None),
+    ("1_2_3_4_5", None), ("_12345", None), ("1__2345", None), ("12345_", None),
+    ("-0", None), ("-1", None), ("+1", None),
+]
+
+
+@pytest.mark.parametrize("s,want", GO_PARSE_UINT64)
+def test_parse_rate_go_parse_uint_vectors(s, want):
+    ok, v = O.parse_rate(s)
+    if want is None:
+        assert not ok, (s, v)
+    else:
+        assert ok and v == want, (s, v, want)

@@ -79,6 +79,30 @@ def _props_batch(strings, field):
     return pd.table(), prop, np.zeros(n, np.uint32)
 
 
+def test_hex_percentages_vs_oracle(engine):
+    """Hexadecimal percentages around the float32 subnormal range (a negative value that rounds
+    to -0 is accepted, one that rounds to a nonzero subnormal is an error), around 100 and with
+    more than 16 digits (the sticky bit): GPU MakeQdiscs equals the oracle's, whose hexadecimal
+    rounding is pinned by Go's atof32 table and exact rationals (tests/test_oracle_go_stdlib.py)."""
+    rng = random.Random(23)
+    strs = []
+    for _ in range(3000):
+        nd = rng.randint(1, 22)
+        digs = "".join(rng.choice("0123456789abcdef") for _ in range(nd))
+        if rng.random() < 0.3:
+            digs = "1" + "0" * rng.randint(0, 20) + rng.choice(["", "1", "8", "80000000000000001"])
+        cut = rng.randint(0, len(digs))
+        mant = digs[:cut] + ("." if rng.random() < 0.6 else "") + digs[cut:]
+        e = rng.choice([rng.randint(-200, -120), rng.randint(-4 * len(digs) - 160, -4 * len(digs) - 140),
+                        rng.randint(-4 * len(digs) + 2, -4 * len(digs) + 12)])
+        strs.append(f"{rng.choice(['', '-', '+'])}0x{mant}p{e}")
+    pd, prop, gap = _props_batch(strs, "loss")
+    got = engine.make_qdiscs(pd, prop, gap)
+    for i, s in enumerate(strs):
+        want = O.make_qdisc({"loss": s}, TICK)
+        assert got[i].tobytes() == want.tobytes(), (s, got[i], want)
+
+
 @pytest.mark.parametrize("field,pool", [("loss", "pct"), ("jitter", "dur"), ("rate", "rate"),
                                         ("latency", "dur"), ("reorder_prob", "pct")])
 def test_parser_fuzz_vs_oracle(engine, field, pool):
@@ -652,11 +676,14 @@ def test_output_stages_without_sync_use_this_runs_counts(engine):
 
 def test_go_stdlib_vectors_on_the_gpu(engine):
     """Go's published known answers (tests/test_oracle_go_stdlib.py: time parseDurationTests,
-    net parseCIDRTests / parseMACTests) through the GPU parsers: a duration as a link's latency
-    (MakeQdiscs, E_LATENCY iff Go rejects it or it is negative), a CIDR as local_ip (MakeVeth,
+    strconv atof32tests / atoftests / parseUint64Tests, net parseCIDRTests / parseMACTests)
+    through the GPU parsers: a duration as a link's latency (MakeQdiscs, E_LATENCY iff Go rejects
+    it or it is negative), a float as its loss (E_LOSS iff ParseFloatPercentage rejects it), an
+    integer as its rate (E_RATE iff ParseUint rejects it), a CIDR as local_ip (MakeVeth,
     E_VETH_CIDR iff invalid and non-empty), a MAC as local_mac (E_VETH_MAC iff invalid); every
     output also equals the oracle's."""
-    from test_oracle_go_stdlib import GO_CIDRS, GO_DURATION_ERRORS, GO_DURATIONS, GO_MACS
+    from test_oracle_go_stdlib import (GO_CIDRS, GO_DURATION_ERRORS, GO_DURATIONS, GO_MACS, GO_PARSE_UINT64,
+                                       GO_PCT_INPUTS, go_percentage)
     strs = [s for s, _ in GO_DURATIONS] + GO_DURATION_ERRORS
     pd, prop, gap = _props_batch(strs, "latency")
     got = engine.make_qdiscs(pd, prop, gap)
@@ -665,6 +692,20 @@ def test_go_stdlib_vectors_on_the_gpu(engine):
         assert got[i].tobytes() == want.tobytes(), (s, got[i], want)
         ok = i < len(GO_DURATIONS) and GO_DURATIONS[i][1] >= 0
         assert (got[i]["err"] == 0) == ok and (ok or got[i]["err"] == abi.E_LATENCY), (s, got[i]["err"])
+    pd, prop, gap = _props_batch(GO_PCT_INPUTS, "loss")
+    got = engine.make_qdiscs(pd, prop, gap)
+    for i, s in enumerate(GO_PCT_INPUTS):
+        want = O.make_qdisc({"loss": s}, TICK)
+        assert got[i].tobytes() == want.tobytes(), (s[:40], got[i], want)
+        ok = go_percentage(s) is not None
+        assert (got[i]["err"] == 0) == ok and (ok or got[i]["err"] == abi.E_LOSS), (s[:40], got[i]["err"])
+    strs = [s for s, _ in GO_PARSE_UINT64]
+    pd, prop, gap = _props_batch(strs, "rate")
+    got = engine.make_qdiscs(pd, prop, gap)
+    for i, (s, v) in enumerate(GO_PARSE_UINT64):
+        want = O.make_qdisc({"rate": s}, TICK)
+        assert got[i].tobytes() == want.tobytes(), (s, got[i], want)
+        assert (got[i]["err"] == 0) == (v is not None) and (v is not None or got[i]["err"] == abi.E_RATE), s
     links, want_err = [], []
     uid = 1
     for ip, valid in GO_CIDRS:                          # MakeVeth parses a non-empty IP only (veth.go:21)
