@@ -7,7 +7,7 @@ strconv.ParseFloat(s, 32) (:128-143, ParseFloatPercentage), strconv.ParseUint(s,
 Go standard library (go.mod: go 1.19). Go is absent here and on the GPU box, so the oracle (oracle/kdtn_oracle.c)
 restates them; these vectors are the expected values of Go's own package tests — time's
 parseDurationTests (time_test.go), strconv's atof32tests / atoftests (atof_test.go) and
-parseUint64Tests (atoi_test.go), net's parseCIDRTests (ip_test.go) and parseMACTests
+parseUint64Tests (atoi_test.go), net's parseCIDRTests and parseIPTests (ip_test.go) and parseMACTests
 (mac_test.go) — written out here as data, passed through the reference's wrappers: ParseDuration
 rejects a negative duration and returns uint32(d.Microseconds()) (Microseconds truncates toward
 zero, uint32 keeps the low 32 bits); "" is 0 without a parse. They pin the restatements to Go's
@@ -98,6 +98,27 @@ GO_CIDRS = [
 
 @pytest.mark.parametrize("s,valid", GO_CIDRS)
 def test_parse_cidr_go_vectors(s, valid):
+    assert O.parse_cidr(s) == valid, s
+
+
+# ip_test.go parseIPTests: (address, valid). ParseCIDR parses the address part with the same
+# parseIPv4 / parseIPv6 (Go 1.19 net/ip.go), so each is checked with a prefix length appended
+# that is legal for its family ("/24" for dotted quads, "/64" otherwise).
+GO_PARSE_IP = [
+    ("127.0.1.2", True), ("127.0.0.1", True), ("::ffff:127.1.2.3", True), ("::ffff:7f01:0203", True),
+    ("0:0:0:0:0000:ffff:127.1.2.3", True), ("0:0:0:0:000000:ffff:127.1.2.3", True),
+    ("0:0:0:0::ffff:127.1.2.3", True), ("2001:4860:0:2001::68", True),
+    ("2001:4860:0000:2001:0000:0000:0000:0068", True),
+    ("-0.0.0.0", False), ("0.-1.0.0", False), ("0.0.-2.0", False), ("0.0.0.-3", False), ("127.0.0.256", False),
+    ("abc", False), ("123:", False), ("fe80::1%lo0", False), ("fe80::1%911", False), ("", False),
+    ("a1:a2:a3:a4::b1:b2:b3:b4", False), ("127.001.002.003", False), ("::ffff:127.001.002.003", False),
+    ("123.000.000.000", False), ("1.2..4", False), ("0123.0.0.1", False),
+]
+GO_PARSE_IP_CIDRS = [(ip + ("/24" if "." in ip and ":" not in ip else "/64"), ok) for ip, ok in GO_PARSE_IP]
+
+
+@pytest.mark.parametrize("s,valid", GO_PARSE_IP_CIDRS)
+def test_parse_ip_go_vectors_as_cidrs(s, valid):
     assert O.parse_cidr(s) == valid, s
 
 

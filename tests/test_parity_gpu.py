@@ -676,14 +676,15 @@ def test_output_stages_without_sync_use_this_runs_counts(engine):
 
 def test_go_stdlib_vectors_on_the_gpu(engine):
     """Go's published known answers (tests/test_oracle_go_stdlib.py: time parseDurationTests,
-    strconv atof32tests / atoftests / parseUint64Tests, net parseCIDRTests / parseMACTests)
+    strconv atof32tests / atoftests / parseUint64Tests, net parseCIDRTests / parseIPTests /
+    parseMACTests)
     through the GPU parsers: a duration as a link's latency (MakeQdiscs, E_LATENCY iff Go rejects
     it or it is negative), a float as its loss (E_LOSS iff ParseFloatPercentage rejects it), an
     integer as its rate (E_RATE iff ParseUint rejects it), a CIDR as local_ip (MakeVeth,
     E_VETH_CIDR iff invalid and non-empty), a MAC as local_mac (E_VETH_MAC iff invalid); every
     output also equals the oracle's."""
-    from test_oracle_go_stdlib import (GO_CIDRS, GO_DURATION_ERRORS, GO_DURATIONS, GO_MACS, GO_PARSE_UINT64,
-                                       GO_PCT_INPUTS, go_percentage)
+    from test_oracle_go_stdlib import (GO_CIDRS, GO_DURATION_ERRORS, GO_DURATIONS, GO_MACS, GO_PARSE_IP_CIDRS,
+                                       GO_PARSE_UINT64, GO_PCT_INPUTS, go_percentage)
     strs = [s for s, _ in GO_DURATIONS] + GO_DURATION_ERRORS
     pd, prop, gap = _props_batch(strs, "latency")
     got = engine.make_qdiscs(pd, prop, gap)
@@ -708,7 +709,7 @@ def test_go_stdlib_vectors_on_the_gpu(engine):
         assert (got[i]["err"] == 0) == (v is not None) and (v is not None or got[i]["err"] == abi.E_RATE), s
     links, want_err = [], []
     uid = 1
-    for ip, valid in GO_CIDRS:                          # MakeVeth parses a non-empty IP only (veth.go:21)
+    for ip, valid in GO_CIDRS + GO_PARSE_IP_CIDRS:      # MakeVeth parses a non-empty IP only (veth.go:21)
         links.append(Link("eth0", ip, "00:00:5e:00:53:01", "eth1", "", "", "b", uid))
         want_err.append(0 if valid or ip == "" else abi.E_VETH_CIDR)
         uid += 1
