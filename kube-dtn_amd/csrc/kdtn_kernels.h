@@ -154,11 +154,13 @@ constexpr int VAR_NT_LOAD = 1, VAR_NT_STORE = 2, VAR_NO_QSTORE = 4, VAR_NT_POD =
               VAR_SKIP_POD = 32, VAR_SKIP_PCT = 64, VAR_OCC5 = 128, VAR_OCC6 = 256,
               VAR_MASK_EMPTY = 512, VAR_NO_PREFIX = 1024, VAR_DIFF = 2048, VAR_DECODE_FIRST = 4096, VAR_PREFETCH = 16384,
               VAR_Q16 = 32768, VAR_GLDS = 65536,
-              VAR_PMAC_COLS = 131072,
-              VAR_AB = 262144,
-              VAR_SKIP_KB1 = 524288, VAR_SKIP_KB3 = 1048576,
-              VAR_HB = 2097152;   // CalcDiff window: both sides' key hashes first, one load round per old record   // (profiling, wrong results) skip the local-MAC /
-                                                               // all three key-string bitset gathers          // CalcDiff window: old + positional new records in one load phase   // (internal to VAR_GLDS) the entry's peer_mac id is in RecCols
+              VAR_PMAC_COLS = 131072,    // (internal to VAR_GLDS) the entry's peer_mac id is in RecCols
+              VAR_AB = 262144,           // CalcDiff window: old + positional new records in one load phase
+              VAR_SKIP_KB1 = 524288,     // (profiling, wrong results) skip the local-MAC bitset gather
+              VAR_SKIP_KB3 = 1048576,    // (profiling, wrong results) skip all three bitset gathers
+              VAR_HB = 2097152,          // CalcDiff window: both sides' key hashes first, one load round per old record
+              VAR_POD8 = 4194304;        // (profiling, wrong results) the pod-slot gather as an 8-B load from
+                                         // an 8-MB table: the footprint of a compact slot, timing only
 // VAR_GLDS: the tile column units an add entry reads, in LDS order: local_ip, local_mac (key 1, 2),
 // peer_ip, peer_mac, peer_pod (key 4..6), the 12 properties, gap, uid (2 units): every column of
 // the tile but local_intf and peer_intf. A delete reads units 0, 1 and the uid (at units 2, 3).
@@ -182,7 +184,7 @@ constexpr int DIFF_VARIANT = DEFAULT_VARIANT | VAR_DIFF | VAR_HB;   // 2116099
 #define KDTN_PROFILING_VARIANTS(X) X(0) X(1) X(2) X(3) X(4) X(5) X(9) X(11) X(17) X(33) X(65) X(97) \
     X(101) X(113) X(129) X(257) X(513) X(521) X(523) X(529) X(531) X(545) X(547) X(579) X(611) X(519) \
     X(641) X(643) X(771) X(1025) X(1537) X(2579) X(4611) X(515) X(16915) X(16963) X(16931) X(16995) X(16903) X(49667) \
-    X(66051) X(65539) X(281091) X(264723) X(541187) X(1065475) X(18947) X(2099731)
+    X(66051) X(65539) X(281091) X(264723) X(541187) X(1065475) X(18947) X(2099731) X(4211203)
 
 struct DevTopos {
     const uint32_t* ns;

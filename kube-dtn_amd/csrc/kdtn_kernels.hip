@@ -1225,7 +1225,12 @@ KD_INLINE void add_gather(const RecCols& c, const TopoCtx& tc, const DevTables& 
         else g.kb_mac = ldg(tb.kbits + (size_t)KB_MAC_BAD * tb.kb_words, c.lmac >> 5);
         g.kb_pip = ldg(tb.kbits + (size_t)KB_CIDR_BAD * tb.kb_words, c.pip >> 5);    // peer end (same / cross node)
     }
-    if constexpr ((V & VAR_SKIP_POD) == 0) g.slot = pod_slot<(V & VAR_NT_POD) != 0>(tb, c.pp);
+    if constexpr ((V & VAR_POD8) != 0) {              // profiling only: 8 B from the table's first half
+        const u32x2 w = ldg(reinterpret_cast<const u32x2*>(tb.pod_direct), c.pp);
+        g.slot = make_uint4(w.x, w.y, 0u, 0u);
+    } else if constexpr ((V & VAR_SKIP_POD) == 0) {
+        g.slot = pod_slot<(V & VAR_NT_POD) != 0>(tb, c.pp);
+    }
 }
 
 template <int V>
@@ -1246,6 +1251,10 @@ KD_INLINE uint4 add_calc(const RecCols& c, const AddGath& g, const DevLinks& N, 
         const bool lh = c.pp == tb.special[SPECIAL_LOCALHOST];
         uint2 p = make_uint2(0xFFFFFFFFu, 0u);
         if constexpr ((V & VAR_SKIP_POD) != 0) p = make_uint2(c.pp & POD_INDEX, g.lns);   // profiling only
+        else if constexpr ((V & VAR_POD8) != 0) {                                          // profiling only
+            asm volatile("" ::"v"(g.slot.x), "v"(g.slot.y));
+            p = make_uint2(c.pp & POD_INDEX, g.lns);
+        }
         else if (!lh) p = pod_resolve(tb, g.lns, c.pp, g.slot);
         const bool miss = p.x == 0xFFFFFFFFu;
         if (lh) {
