@@ -1499,13 +1499,20 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
         w.n_cap = c->des.n;
         uint32_t* wbase = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(w.wcount) + align_up((size_t)c->nwg * 12, 16));
         bool placed = false;                                        // VAR_DIFF: k_place_scan + k_place
-        // several workgroups per chunk when the chunks would not fill the chip about four times
+        // several workgroups per chunk when the chunks would not fill the chip about six times
         // over (4 resident k_reconcile workgroups per CU): they share a bulk chunk's records,
-        // at least ~320 records per part (measured: 125k-pod config 2, 640 records per chunk:
-        // split 2 0.097 ms, 3 0.106, 4 0.115; 12.5k-site config 4, 1266 per chunk: 4 best)
+        // at least ~300 records per part (measured: 125k-pod config 2, 640 records per chunk:
+        // split 2 0.097 ms, 3 0.106, 4 0.115; 100k-site config 4, 1267 per chunk: split 2 / 3 /
+        // 4 / 6 / 8 0.156 / 0.158 / 0.150 / 0.174 / 0.166 ms, profiles/r06v_split_sweep.json)
+        // Only bulk chunks share their records; in a chunk with comparisons the other parts
+        // return at once, so an epoch whose realised lists are a large share of the records
+        // runs one workgroup per chunk (config 1, 1274 records per chunk: split 1 / 2 / 4
+        // 0.185 / 0.186 / 0.205 ms, the same record)
         const uint64_t per_chunk = ((uint64_t)c->real.n + c->des.n) / std::max<uint32_t>(c->nwg, 1);
-        w.split = std::max<uint32_t>(1, std::min<uint32_t>({4u, (4 * 4 * c->n_cus + c->nwg - 1) / c->nwg,
-                                                            (uint32_t)std::max<uint64_t>(1, per_chunk / 320)}));
+        const bool cmp_heavy = (uint64_t)c->real.n * 4 > c->des.n;
+        w.split = cmp_heavy ? 1u
+                            : std::max<uint32_t>(1, std::min<uint32_t>({4u, (6 * 4 * c->n_cus + c->nwg - 1) / c->nwg,
+                                                                        (uint32_t)std::max<uint64_t>(1, per_chunk / 300)}));
 #if KDTN_PROFILING
         if (const char* ev = std::getenv("KDTN_SPLIT")) if (std::atoi(ev) > 0) w.split = (uint32_t)std::atoi(ev);
 #endif
