@@ -311,3 +311,32 @@ def test_parse_rate_go_parse_uint_vectors(s, want):
         assert not ok, (s, v)
     else:
         assert ok and v == want, (s, v, want)
+
+
+# strings_test.go trimSpaceTests with the payload made numeric ("abc" -> "123", "x" -> "7",
+# "y" -> "8"): ParseRate (common/qdisc.go:163) trims with strings.TrimSpace (unicode.IsSpace:
+# "\t\v\r\f\n", U+0085, U+00A0, U+2000, U+3000 ...) after strings.ToLower, then ParseUint's
+# answer on what TrimSpace leaves: (input, rate or None for an error).
+_GO_SPACE = "\t\v\r\f\n\u0085\u00a0\u2000\u3000"
+GO_TRIMSPACE_RATES = [
+    ("", 0), ("123", 123), (_GO_SPACE + "123" + _GO_SPACE, 123), (" ", 0), (" \t\r\n \t\t\r\r\n\n ", 0),
+    (" \t\r\n 7\t\t\r\r\n\n ", 7), (" \u2000\t\r\n 7\t\t\r\r\n8\n \u3000", None), ("1 \t\r\n2", None),
+    (" 7\x80", None), (" 7\xc0", None), ("7 \xc0\xc0 ", None), ("7 \xc0", None), ("7 ☺ ", None),
+]
+
+
+def _latin1_or_utf8(s: str) -> bytes:
+    """The test strings' bytes: \x80 / \xc0 stand for single invalid UTF-8 bytes, as in Go."""
+    out = bytearray()
+    for ch in s:
+        out += bytes([ord(ch)]) if ch in "\x80\xc0" else ch.encode()
+    return bytes(out)
+
+
+@pytest.mark.parametrize("s,want", GO_TRIMSPACE_RATES)
+def test_parse_rate_go_trimspace_vectors(s, want):
+    ok, v = O.parse_rate(_latin1_or_utf8(s))
+    if want is None:
+        assert not ok, (s, v)
+    else:
+        assert ok and v == want, (s, v, want)

@@ -684,7 +684,8 @@ def test_go_stdlib_vectors_on_the_gpu(engine):
     E_VETH_CIDR iff invalid and non-empty), a MAC as local_mac (E_VETH_MAC iff invalid); every
     output also equals the oracle's."""
     from test_oracle_go_stdlib import (GO_CIDRS, GO_DURATION_ERRORS, GO_DURATIONS, GO_MACS, GO_PARSE_IP_CIDRS,
-                                       GO_PARSE_UINT64, GO_PCT_INPUTS, go_percentage)
+                                       GO_PARSE_UINT64, GO_PCT_INPUTS, GO_TRIMSPACE_RATES, _latin1_or_utf8,
+                                       go_percentage)
     strs = [s for s, _ in GO_DURATIONS] + GO_DURATION_ERRORS
     pd, prop, gap = _props_batch(strs, "latency")
     got = engine.make_qdiscs(pd, prop, gap)
@@ -700,10 +701,11 @@ def test_go_stdlib_vectors_on_the_gpu(engine):
         assert got[i].tobytes() == want.tobytes(), (s[:40], got[i], want)
         ok = go_percentage(s) is not None
         assert (got[i]["err"] == 0) == ok and (ok or got[i]["err"] == abi.E_LOSS), (s[:40], got[i]["err"])
-    strs = [s for s, _ in GO_PARSE_UINT64]
+    rates = GO_PARSE_UINT64 + [(_latin1_or_utf8(s), v) for s, v in GO_TRIMSPACE_RATES]
+    strs = [s for s, _ in rates]
     pd, prop, gap = _props_batch(strs, "rate")
     got = engine.make_qdiscs(pd, prop, gap)
-    for i, (s, v) in enumerate(GO_PARSE_UINT64):
+    for i, (s, v) in enumerate(rates):
         want = O.make_qdisc({"rate": s}, TICK)
         assert got[i].tobytes() == want.tobytes(), (s, got[i], want)
         assert (got[i]["err"] == 0) == (v is not None) and (v is not None or got[i]["err"] == abi.E_RATE), s
