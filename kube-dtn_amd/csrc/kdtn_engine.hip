@@ -1231,16 +1231,18 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
     uint32_t* sync = dp<uint32_t>(c->sync);
     // Epoch front: first launch (sync header, look-back area, pod-status rows) + RCCL
     // all-gather, the dictionary parses, the pod lookup tables, in sequence. The tables need
-    // nothing from the parses, but running them beside the parses did not shorten the epoch
-    // (config 2): on a side stream 0.791-0.796 vs 0.789 ms (profiles/r03u_side_ab.json), fused
-    // into the parse launches (k_epoch_front + k_pdict_verify, profiling build, KDTN_FUSE=1)
-    // 0.7895 vs 0.7882 ms (profiles/r03v_fuse_ab.json): the launch's blocks add up, they do not
-    // overlap.
+    // nothing from the parses, but running them beside a long key-string parse did not shorten
+    // the epoch (config 2): on a side stream 0.791-0.796 vs 0.789 ms (profiles/r03u_side_ab.json),
+    // fused into the parse launches 0.804 vs 0.793 ms (profiles/r06ae_fuse_ab.json). When the key
+    // strings to parse are few (a churn epoch's appended strings, configs 1 and 4) the five
+    // launches are the cost, and one local rank fuses them into two: k_epoch_front (sync header,
+    // pod rows and their lookup slots, key strings) and k_pdict_verify (slot verify, full-prefix
+    // scan, property strings): config-3 churn epochs 0.762 -> 0.741 ms, config 4 0.246 -> 0.240,
+    // config 1 0.223 -> 0.206 (profiles/r06ad_fuse_churn.json, r06ae_fuse_ab.json).
+    constexpr uint32_t FUSE_MAX_KSTRINGS = 4u << 20;
+    int fuse_mode = (c->D - std::min(c->D, c->kd_from & ~63u)) < FUSE_MAX_KSTRINGS ? 1 : 0;
 #if KDTN_PROFILING
-    int fuse_mode = 0;
     if (const char* ev = std::getenv("KDTN_FUSE")) fuse_mode = std::atoi(ev);
-#else
-    constexpr int fuse_mode = 0;
 #endif
     const bool fused = fuse_mode && resolve && !pods_cur && c->nranks == 1 && !c->comm && c->pod_total &&
                        c->pod_total == c->slice && !c->n_late;
@@ -1297,7 +1299,6 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
             dp<unsigned long long>(c->pod_ovf), c->ovf_mask, c->D, T, sync + SYNC_FIRST_PARTIAL_INV, nbv,
             c->pods_rank_major ? (uint32_t)c->nranks : 1u, c->pod_total);
     };
-#if KDTN_PROFILING
     if (fused) {
         if (++c->pod_stamp >= 0x7FFFFFFFu) {                             // stamp wrap: clear once
             HIP_TRY(hipMemsetAsync(c->pod_direct.p, 0, c->pod_direct.cap, s));
@@ -1325,9 +1326,7 @@ int kdtn_epoch_run(kdtn_ctx* c, uint32_t stages) {
             dp<uint32_t>(c->pd_offs), p0, c->P, nbd, c->cfg.tick_in_usec, dp<uint32_t>(c->pd_pct), dp<uint2>(c->pd_dur),
             dp<uint2>(c->pd_rate), dp<uint32_t>(c->pd_rerr));
         timer_mark(c, "pdict_verify", 2);
-    } else
-#endif
-    {
+    } else {
         // k_epoch_begin zeroes the sync header (SYNC_*) and look-back area and fills this rank's
         // pod-status rows. With RCCL it runs on the comm stream, followed there by the
         // all-gather, beside this stream's dictionary parses; otherwise it follows the parses on

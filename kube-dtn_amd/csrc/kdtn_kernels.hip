@@ -1996,12 +1996,12 @@ template __global__ void k_pod_verify_prefix<4>(const uint4*, uint32_t, uint4*, 
 template __global__ void k_pod_verify_prefix<2>(const uint4*, uint32_t, uint4*, uint32_t, unsigned long long*, uint32_t,
                                                 uint32_t, DevTopos, uint32_t*, uint32_t, uint32_t, uint32_t);
 #endif
-#if KDTN_PROFILING
-// ---- (A/B, KDTN_FUSE=1) fused epoch front (one local rank: no exchange) ------------------
-// Measured no faster than the launches in sequence (0.7895 vs 0.7882 ms per config-2 epoch,
-// profiles/r03v_fuse_ab.json), so only the profiling build has these kernels.
-// The pod tables' memory-bound work shares launches with the VALU-bound dictionary parses (a
-// side stream only got CUs as the parse's waves retired: profiles/r03u_side_ab.json).
+// ---- fused epoch front (one local rank: no exchange) -------------------------------------
+// Two launches instead of five when the key-string parse is short (kdtn_epoch_run's rule):
+// the pod tables' memory-bound work shares launches with the dictionary parses. With a long
+// VALU-bound key parse (config 2, 12M strings) the sequence is faster (0.793 vs 0.804 ms); with
+// a short one the launches were the cost (config-3 churn epochs 0.762 -> 0.741 ms, config 4
+// 0.246 -> 0.240, config 1 0.223 -> 0.206; profiles/r06ad_fuse_churn.json, r06ae_fuse_ab.json).
 // k_epoch_front: blocks [0, nbz) zero the sync header and look-back area; [nbz, nbz + nbs)
 // fill this rank's pod-status rows and scatter each into its direct lookup slot (the row is
 // computed from the topology table here, the "physical/" prefix of the name read from its
@@ -2064,7 +2064,6 @@ __global__ void __launch_bounds__(BLOCK) k_pdict_verify(const uint4* pods, uint3
     else if (y == 1) pdict_parse_block<PD_DUR>(pbytes, poffs, s0, np, tick, ppct, pdur, prate, rate_err, buf);
     else pdict_parse_block<PD_RATE>(pbytes, poffs, s0, np, tick, ppct, pdur, prate, rate_err, buf);
 }
-#endif
 
 // (VAR_TRACE) phase timestamp of this workgroup: 100 MHz chip-wide clock
 template <int V>

@@ -24,13 +24,47 @@ ap.add_argument("--cache", default="")
 ap.add_argument("--variants", default="", help="comma list of KDTN_VARIANT values, interleaved")
 ap.add_argument("--env", default="", help="NAME=v1,v2,...: interleaved A/B of an env knob, all stages timed")
 ap.add_argument("--wall", action="store_true", help="--env: also the wall time of run + sync at timing level 0")
-ap.add_argument("--churn", type=int, default=0, help="--variants over K epochs of the config-3 churn sequence "
+ap.add_argument("--churn", type=int, default=0, help="--variants (or --env, wall time) over K epochs of the config-3 churn sequence "
                 "(each epoch uploaded once, the variants interleaved on it; k_reconcile + placement)")
 a = ap.parse_args()
 if a.variants or a.env:                 # A/B variants live in the profiling build
     from kdtn import engine as _kdtn_engine
     _kdtn_engine.use_profiling_library()
 res = {}
+if a.churn and a.env:                    # churn epochs: wall time of run + sync per env value
+    import time
+    name, vals = a.env.split("=")
+    vs = vals.split(",")
+    cs = synth.ChurnSequence(pods_per_shard=a.pods)
+    eng = Engine(device=0)
+    eng.set_timing(0)
+    per = {v: [] for v in vs}
+    inp = cs.epoch_input()
+    for ep in range(a.churn):
+        if ep:
+            keep = (inp.kdict.n, inp.pdict.n)
+            cs.advance()
+            inp = cs.epoch_input()
+            eng.upload(inp, *keep)
+        else:
+            eng.upload(inp)
+        acc = {v: [] for v in vs}
+        for rep in range(a.reps + 2):
+            for v in vs:
+                os.environ[name] = v
+                t = time.perf_counter()
+                eng.run(abi.STAGE_ALL)
+                eng.sync()
+                if rep >= 2:
+                    acc[v].append((time.perf_counter() - t) * 1e3)
+        for v in vs:
+            per[v].append(sorted(acc[v])[len(acc[v]) // 2])
+    os.environ.pop(name)
+    print(json.dumps({"config": 3, "pods": a.pods, "epochs": a.churn, "reps": a.reps, "env": name,
+                      "epoch_wall_ms": {v: {"mean_of_epoch_medians": round(sum(x) / len(x), 4),
+                                            "per_epoch": [round(y, 4) for y in x]} for v, x in per.items()}},
+                     indent=1))
+    sys.exit(0)
 if a.churn:                              # config 3 as the bench runs it: the churn sequence
     cs = synth.ChurnSequence(pods_per_shard=a.pods)
     eng = Engine(device=0)
